@@ -1,0 +1,119 @@
+"""Benchmark: Gauss-Newton iterations/s of the device-resident calibration loop (BASELINE.json metric).
+
+One step = one full Optimizer2 pass with the Gauss-Newton policy: buildSystem (residuals, Jacobians,
+arrow normal equations) + solveSystem (frame Schur complement, camera-block Cholesky, back
+substitution) + applyStateUpdate + evaluateError, on synthetic AprilGrid data resident in HBM.
+
+Workload (N=1): configs[1] = 2-camera stereo pinhole-radtan rig, 500 frames, 6x5 AprilGrid (120 corners),
+all views visible.  N>1: weak scaling, every rank holds its own 500-frame shard of a 2-camera rig with
+500*N frames; the camera block [S | b] and the cost / step statistics are all-reduced over RCCL once per
+pass.  value = (config-sized shard iterations of all ranks) / max-over-ranks wall time.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+METRIC = "Gauss-Newton iterations/sec (full J build + solve), N-cam×M-frame AprilGrid"
+FRAMES_PER_RANK = 500
+HBM_PEAK_GBS = 8000.0
+
+
+def cpu_baseline(prob, seconds_budget=12.0, threads=None):
+    """Oracle (our C restatement of the reference CPU flow: threaded per-term evaluation into CCS J^T,
+    serial rhs SpMV, J^T J, frame-first sparse Cholesky) timed on host cores."""
+    from oracle import oracle as O
+    o = O.Oracle(prob)
+    threads = threads or min(16, os.cpu_count() or 1)
+    t1 = o.time_gn(prob.state_init, 1, threads)  # includes first-touch / warm-up
+    n = max(2, min(200, int(seconds_budget / max(t1, 1e-4))))
+    t = o.time_gn(prob.state_init, n, threads)
+    return {"value": n / t, "unit": "iterations/s", "cores": threads, "kind": "port",
+            "sample": f"{n} GN iterations of configs[1] (full 500-frame problem, {prob.n_corners} corners), "
+                      f"oracle/kb_oracle.c kbo_time_gn, {threads} threads"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus > 1 and world != args.gpus:
+        raise SystemExit("for --gpus N>1 launch with torch.distributed.run --nproc-per-node N")
+
+    from kalibr_amd import build as B
+    from kalibr_amd import capi, synth
+    if not os.path.exists(B.OUT):
+        B.build()
+
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        dist.init_process_group("gloo", init_method="env://")  # id exchange + host barrier only
+
+    full = synth.make_problem(synth.CONFIGS[2]["models"], FRAMES_PER_RANK * world, seed=20261015 + 2,
+                              name=synth.CONFIGS[2]["name"])
+    shard = full.frame_slice(rank * FRAMES_PER_RANK, (rank + 1) * FRAMES_PER_RANK) if world > 1 else full
+    g = capi.Solver(shard, device=local)
+    g.set_state(shard.state_init)
+    if world > 1:
+        obj = [capi.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        g.comm_init(obj[0], world, rank)
+
+    g.run_gn(args.warmup)
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    sec = g.run_gn(args.steps)  # stream-synchronised on both sides inside
+    wall = time.perf_counter() - t0
+    if dist:
+        import torch
+        tt = torch.tensor([wall], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        wall = float(tt.item())
+
+    # dominant kernel (k_build) timing with HIP events on the handle's stream
+    build_ms, bytes_per, flops_per = g.build_kernel_stats()
+    achieved = bytes_per / (build_ms * 1e-3) / 1e9
+
+    if rank == 0:
+        value = world * args.steps / wall
+        out = {
+            "metric": METRIC, "value": value, "unit": "iterations/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": 1e3 * wall / args.steps, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "config": {"workload": "configs[1]: 2-cam stereo pinhole-radtan, 500 frames/GPU, 6x5 AprilGrid, p_view=1",
+                       "frames_per_gpu": FRAMES_PER_RANK, "cameras": 2, "corners_per_gpu": shard.n_corners,
+                       "jacobian_cols": full.total_cols, "camera_block": full.cam_cols, "policy": "gauss_newton",
+                       "parallelism": f"frame-sharded x{world}"},
+            "roofline": {"bound": "hbm", "kernel": "k_build", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None, "avg_ms": build_ms,
+                         "algorithmic_bytes": bytes_per, "fp64_tflops": flops_per / (build_ms * 1e-3) / 1e12},
+        }
+        if not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(full if world == 1 else full.frame_slice(0, FRAMES_PER_RANK))
+            out["speedup_vs_cpu_baseline"] = value / out["cpu_baseline"]["value"]
+        print(json.dumps(out))
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

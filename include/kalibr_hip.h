@@ -1,0 +1,149 @@
+/*
+ * kalibr_hip.h -- C-ABI of the MI355X-native batch calibration backend.
+ *
+ * Drop-in boundary for aslam_backend's LinearSystemSolver plugin surface
+ * (aslam_optimizer/aslam_backend/include/aslam/backend/LinearSystemSolver.hpp:16-109,
+ * paths relative to the reference repository) specialised to the
+ * ReprojectionError<Geometry> terms Kalibr2 builds in CalibrateMultiCameraRig
+ * (aslam_offline_calibration/kalibr2/include/kalibr2/CalibrationTools.hpp:376-428).
+ *
+ * Plain pointers and sizes only; every entry point returns an int status
+ * (0 = OK, < 0 = error, message in kb_last_error()).  One handle per optimizer,
+ * one HIP stream per handle, calls are not re-entrant (LinearSystemSolver is
+ * single-threaded at the API level).
+ *
+ * State layout (flat doubles, also used by kb_set_state_flat / kb_get_state_flat):
+ *   intr  [n_cams][KB_MAX_INTR]   projection params then distortion params
+ *   base  [n_cams-1][7]           B_j = T_{c(j+1),c(j)}: JPL quaternion (x,y,z,w) + t
+ *   frame [n_frames][7]           target pose DV T_f, p_c0 = T_f^-1 * P_target
+ * Column order of dx / rhs (canonical): [intrinsics cam0..cam(N-1) | B_0..B_(N-2) | frame 0..F-1],
+ * each pose block ordered (dphi[3], dt[3]) -- the DV insertion order of
+ * CalibrateMultiCameraRig (q DV before t DV, CalibrationTools.hpp:32-45).
+ */
+#ifndef KALIBR_HIP_H
+#define KALIBR_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KB_MAX_INTR 10
+#define KB_MAX_CAMS 16
+
+/* camera models (kalibr2/include/kalibr2/CameraModels.hpp:25-133) */
+enum kb_camera_model {
+  KB_PINHOLE_RADTAN = 0, /* DistortedPinhole: fu fv cu cv | k1 k2 p1 p2 */
+  KB_OMNI_RADTAN = 1,    /* DistortedOmni:    xi fu fv cu cv | k1 k2 p1 p2 */
+  KB_EUCM = 2,           /* ExtendedUnified:  alpha beta fu fv cu cv */
+  KB_OMNI = 3            /* Omni:             xi fu fv cu cv */
+};
+
+typedef struct kb_handle kb_handle;
+
+typedef struct kb_layout {
+  int32_t n_cams;            /* N <= KB_MAX_CAMS */
+  int32_t n_frames;          /* F (frames held by this handle / rank) */
+  int32_t n_target;          /* target corners (120 for the 6x5 AprilGrid) */
+  const int32_t* cam_model;  /* [n_cams] kb_camera_model */
+  const double* target_points; /* [n_target][3] */
+  int32_t device;            /* HIP device ordinal */
+} kb_layout;
+
+/* Replaces SparseCholeskyLinearSystemSolver construction
+ * (aslam_backend/src/SparseCholeskyLinearSystemSolver.cpp:8-15). */
+kb_handle* kb_create(const kb_layout* layout);
+void kb_destroy(kb_handle* h);
+const char* kb_last_error(void);
+
+/* Replaces LinearSystemSolver::initMatrixStructure (LinearSystemSolver.cpp:117-138) for
+ * ReprojectionError terms: one term per observed corner, grouped in views.
+ * Views must be sorted by frame (then camera); one view per (frame, camera).
+ *   y            [n_corners][2]  measured keypoints (invR = I, CalibrationTools.hpp:391-393)
+ *   corner_id    [n_corners]     target corner index of each term
+ *   view_offsets [n_views+1]     corner range of each view
+ *   view_frame   [n_views], view_cam [n_views] */
+int kb_upload_observations(kb_handle* h, int32_t n_views, int32_t n_corners, const double* y,
+                           const uint16_t* corner_id, const uint32_t* view_offsets,
+                           const uint32_t* view_frame, const uint8_t* view_cam);
+
+/* Design-variable values (the device owns the state between calls). */
+int kb_set_state(kb_handle* h, const double* poses_q, const double* poses_t, const double* baselines,
+                 const double* intrinsics);
+int kb_set_state_flat(kb_handle* h, const double* state);
+int kb_get_state_flat(kb_handle* h, double* state);
+int kb_state_size(const kb_handle* h);
+int kb_num_cols(const kb_handle* h);     /* JCols = C + 6F */
+int kb_camera_cols(const kb_handle* h);  /* C = sum(intrinsics) + 6(N-1) */
+
+/* LinearSystemSolver::evaluateError (LinearSystemSolver.cpp:81-92): chi^2 = sum e^T invR e. */
+int kb_eval_cost(kb_handle* h, double* J_out);
+/* LinearSystemSolver::buildSystem (SparseCholeskyLinearSystemSolver.cpp:39-46): J, rhs = -J^T e,
+ * assembled as the arrow normal equations (no explicit J).  use_mestimator must be 0 or 1
+ * (Kalibr2 uses NoMEstimator, weight 1). */
+int kb_build(kb_handle* h, int use_mestimator);
+/* LinearSystemSolver::setConstantConditioner (LinearSystemSolver.cpp:111-114):
+ * "the square of this value will be added to the diagonal" (LinearSystemSolver.hpp:33-39). */
+int kb_set_constant_conditioner(kb_handle* h, double diag);
+/* LinearSystemSolver::solveSystem (SparseCholeskyLinearSystemSolver.cpp:48-89):
+ * solves (J^T J + diag^2 I) dx = rhs.  *ok = 0 on a non-positive-definite system
+ * (CHOLMOD failure semantics, Cholmod(impl).hpp:287-328); dx_out untouched then. */
+int kb_solve(kb_handle* h, double* dx_out, int* ok);
+/* LinearSystemSolver::rhs (LinearSystemSolver.hpp:47). */
+int kb_get_rhs(kb_handle* h, double* rhs_out);
+/* Optimizer2::applyStateUpdate / revertLastStateUpdate (Optimizer2.cpp:290-318).
+ * dx == NULL applies the device-resident dx of the last kb_solve. */
+int kb_apply_update(kb_handle* h, const double* dx, double* deltaX_out);
+int kb_revert(kb_handle* h);
+
+/* Normal-equation blocks of the last kb_build, for parity tests:
+ * Hff [F][6][6], Hfc [F][6][C], gf [F][6], Hcc [C][C], gc [C], cost (chi^2 at build state). */
+int kb_get_normal_blocks(kb_handle* h, double* Hff, double* Hfc, double* gf, double* Hcc, double* gc,
+                         double* cost);
+
+/* Device-resident Optimizer2::optimize (Optimizer2.cpp:183-273) with the
+ * LevenbergMarquardt (policy 0, LevenbergMarquardtTrustRegionPolicy.cpp:50-113) or
+ * GaussNewton (policy 1, GaussNewtonTrustRegionPolicy.cpp:18-39) trust-region policy.
+ * The whole loop (build, Schur solve, update, cost, policy) runs as one hipGraph per
+ * iteration; the host synchronises only every `sync_every` iterations. */
+typedef struct kb_optimizer_options {
+  int32_t policy;          /* 0 = levenberg_marquardt, 1 = gauss_newton */
+  double lambda_init;      /* LM lambdaInit (CalibrationTools.hpp:65: 10) */
+  int32_t max_iterations;  /* Optimizer2Options::maxIterations */
+  double convergence_dx;   /* convergenceDeltaX */
+  double convergence_dj;   /* convergenceDeltaJ */
+  int32_t sync_every;      /* host checks the done flag every n passes (0 = auto) */
+  int32_t use_graph;       /* capture the iteration in a hipGraph (1) or launch eagerly (0) */
+} kb_optimizer_options;
+
+typedef struct kb_solution {
+  double J_start, J_final, dx_final, dj_final; /* SolutionReturnValue (backend.hpp:11-24) */
+  int32_t iterations, failed_iterations, linear_solver_failure;
+  int32_t passes;
+} kb_solution;
+
+int kb_optimize(kb_handle* h, const kb_optimizer_options* opts, kb_solution* out);
+/* Per-pass trace of the last kb_optimize: [J, lambda, deltaX, accepted] x n (returns count). */
+int kb_get_trace(kb_handle* h, double* trace, int32_t cap);
+
+/* Benchmark entry: run exactly n_iter Gauss-Newton passes of the device loop (convergence
+ * tests disabled), no host sync inside; *seconds = wall time between stream syncs. */
+int kb_run_gn_iterations(kb_handle* h, int32_t n_iter, double* seconds);
+/* Average device duration (ms) of the build kernel over the last kb_run_gn_iterations,
+ * measured with HIP events on the handle's stream; algorithmic bytes per build launch. */
+int kb_build_kernel_stats(kb_handle* h, double* avg_ms, double* bytes_per_launch, double* flops_per_launch);
+
+/* Multi-GPU (frame sharding): each rank's handle holds its own frames;
+ * the camera-block [S | b] and the cost/step statistics are all-reduced over RCCL once
+ * per pass.  unique_id is the 128-byte ncclUniqueId. */
+int kb_comm_get_unique_id(void* unique_id_out128);
+int kb_comm_init(kb_handle* h, const void* unique_id128, int32_t nranks, int32_t rank);
+
+/* Self test of the f64 MFMA fragment layout used by the build kernel (A = I, asymmetric B). */
+int kb_selftest_mfma(double* max_err);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

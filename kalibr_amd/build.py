@@ -1,0 +1,30 @@
+"""In-tree build of libkalibr_hip.so for gfx950 (explicit hipcc, no JIT cache)."""
+import os
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SRC = os.path.join(HERE, "csrc", "kb_capi.hip")
+OUT = os.path.join(HERE, "libkalibr_hip.so")
+DEPS = ["kb_capi.hip", "kb_kernels.hip", "kb_device.h", "kb_math.h"]
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wno-unused-result", "-Wno-unused-value"]
+
+
+def needs_build():
+    if not os.path.exists(OUT):
+        return True
+    t = os.path.getmtime(OUT)
+    deps = [os.path.join(HERE, "csrc", f) for f in DEPS] + [os.path.join(HERE, "..", "include", "kalibr_hip.h")]
+    return any(os.path.getmtime(p) > t for p in deps)
+
+
+def build(force=False):
+    if force or needs_build():
+        cmd = [HIPCC] + FLAGS + ["-o", OUT + ".tmp", SRC, "-lrccl"]
+        subprocess.run(cmd, check=True)
+        os.replace(OUT + ".tmp", OUT)
+    return OUT
+
+
+if __name__ == "__main__":
+    print(build(force=True))

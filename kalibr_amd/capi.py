@@ -1,0 +1,222 @@
+"""ctypes binding of the C-ABI in include/kalibr_hip.h (libkalibr_hip.so, built in-tree).
+
+There is no CPU fallback: if the shared library or a HIP device is missing, every entry point
+raises.  The library is loaded from this package directory so the GPU box loads the in-tree build.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libkalibr_hip.so")
+_lib = None
+
+dp = C.POINTER(C.c_double)
+
+# every symbol declared in include/kalibr_hip.h
+EXPORTS = [
+    "kb_create", "kb_destroy", "kb_last_error", "kb_upload_observations", "kb_set_state", "kb_set_state_flat",
+    "kb_get_state_flat", "kb_state_size", "kb_num_cols", "kb_camera_cols", "kb_eval_cost", "kb_build",
+    "kb_set_constant_conditioner", "kb_solve", "kb_get_rhs", "kb_apply_update", "kb_revert", "kb_get_normal_blocks",
+    "kb_optimize", "kb_get_trace", "kb_run_gn_iterations", "kb_build_kernel_stats", "kb_comm_get_unique_id",
+    "kb_comm_init", "kb_selftest_mfma",
+]
+
+
+class KbError(RuntimeError):
+    pass
+
+
+class Layout(C.Structure):
+    _fields_ = [("n_cams", C.c_int32), ("n_frames", C.c_int32), ("n_target", C.c_int32),
+                ("cam_model", C.POINTER(C.c_int32)), ("target_points", dp), ("device", C.c_int32)]
+
+
+class OptimizerOptions(C.Structure):
+    _fields_ = [("policy", C.c_int32), ("lambda_init", C.c_double), ("max_iterations", C.c_int32),
+                ("convergence_dx", C.c_double), ("convergence_dj", C.c_double), ("sync_every", C.c_int32),
+                ("use_graph", C.c_int32)]
+
+
+class Solution(C.Structure):
+    _fields_ = [("J_start", C.c_double), ("J_final", C.c_double), ("dx_final", C.c_double), ("dj_final", C.c_double),
+                ("iterations", C.c_int32), ("failed_iterations", C.c_int32), ("linear_solver_failure", C.c_int32),
+                ("passes", C.c_int32)]
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise KbError(f"{LIB_PATH} missing: run __graft_entry__.build() (the HIP path has no fallback)")
+        L = C.CDLL(LIB_PATH)
+        L.kb_create.restype = C.c_void_p
+        L.kb_create.argtypes = [C.POINTER(Layout)]
+        L.kb_destroy.argtypes = [C.c_void_p]
+        L.kb_last_error.restype = C.c_char_p
+        for name in EXPORTS:
+            fn = getattr(L, name)
+            if name not in ("kb_create", "kb_destroy", "kb_last_error"):
+                fn.restype = C.c_int
+        L.kb_upload_observations.argtypes = [C.c_void_p, C.c_int32, C.c_int32, dp, C.c_void_p, C.c_void_p, C.c_void_p,
+                                             C.c_void_p]
+        L.kb_set_state_flat.argtypes = [C.c_void_p, dp]
+        L.kb_get_state_flat.argtypes = [C.c_void_p, dp]
+        L.kb_set_state.argtypes = [C.c_void_p, dp, dp, dp, dp]
+        for n in ("kb_state_size", "kb_num_cols", "kb_camera_cols", "kb_revert"):
+            getattr(L, n).argtypes = [C.c_void_p]
+        L.kb_eval_cost.argtypes = [C.c_void_p, dp]
+        L.kb_build.argtypes = [C.c_void_p, C.c_int]
+        L.kb_set_constant_conditioner.argtypes = [C.c_void_p, C.c_double]
+        L.kb_solve.argtypes = [C.c_void_p, dp, C.POINTER(C.c_int)]
+        L.kb_get_rhs.argtypes = [C.c_void_p, dp]
+        L.kb_apply_update.argtypes = [C.c_void_p, dp, dp]
+        L.kb_get_normal_blocks.argtypes = [C.c_void_p, dp, dp, dp, dp, dp, dp]
+        L.kb_optimize.argtypes = [C.c_void_p, C.POINTER(OptimizerOptions), C.POINTER(Solution)]
+        L.kb_get_trace.argtypes = [C.c_void_p, dp, C.c_int32]
+        L.kb_run_gn_iterations.argtypes = [C.c_void_p, C.c_int32, dp]
+        L.kb_build_kernel_stats.argtypes = [C.c_void_p, dp, dp, dp]
+        L.kb_comm_get_unique_id.argtypes = [C.c_void_p]
+        L.kb_comm_init.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32]
+        L.kb_selftest_mfma.argtypes = [dp]
+        _lib = L
+    return _lib
+
+
+def _check(rc):
+    if rc < 0:
+        raise KbError(lib().kb_last_error().decode())
+    return rc
+
+
+def _d(a):
+    return a.ctypes.data_as(dp)
+
+
+def selftest_mfma():
+    err = C.c_double(0.0)
+    _check(lib().kb_selftest_mfma(C.byref(err)))
+    return err.value
+
+
+def comm_unique_id() -> bytes:
+    buf = C.create_string_buffer(128)
+    _check(lib().kb_comm_get_unique_id(buf))
+    return buf.raw
+
+
+class Solver:
+    """One device handle = one LinearSystemSolver instance over a synthetic/real observation set."""
+
+    def __init__(self, prob, device=0):
+        self.prob = prob
+        self._cm = np.ascontiguousarray(prob.cam_model, dtype=np.int32)
+        self._tg = np.ascontiguousarray(prob.target, dtype=np.float64)
+        lay = Layout(prob.n_cams, prob.n_frames, self._tg.shape[0], self._cm.ctypes.data_as(C.POINTER(C.c_int32)),
+                     _d(self._tg), device)
+        h = lib().kb_create(C.byref(lay))
+        if not h:
+            raise KbError(lib().kb_last_error().decode())
+        self.h = C.c_void_p(h)
+        y = np.ascontiguousarray(prob.y, dtype=np.float64)
+        cid = np.ascontiguousarray(prob.corner_id, dtype=np.uint16)
+        vo = np.ascontiguousarray(prob.view_offset, dtype=np.uint32)
+        vf = np.ascontiguousarray(prob.view_frame, dtype=np.uint32)
+        vc = np.ascontiguousarray(prob.view_cam, dtype=np.uint8)
+        _check(lib().kb_upload_observations(self.h, prob.n_views, prob.n_corners, _d(y), cid.ctypes.data,
+                                            vo.ctypes.data, vf.ctypes.data, vc.ctypes.data))
+        self.S = lib().kb_state_size(self.h)
+        self.ncols = lib().kb_num_cols(self.h)
+        self.C = lib().kb_camera_cols(self.h)
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().kb_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- LinearSystemSolver-like surface --
+    def set_state(self, state):
+        st = np.ascontiguousarray(state, dtype=np.float64)
+        assert st.shape[0] == self.S
+        _check(lib().kb_set_state_flat(self.h, _d(st)))
+
+    def get_state(self):
+        st = np.zeros(self.S)
+        _check(lib().kb_get_state_flat(self.h, _d(st)))
+        return st
+
+    def eval_cost(self):
+        J = C.c_double()
+        _check(lib().kb_eval_cost(self.h, C.byref(J)))
+        return J.value
+
+    def build(self, use_mestimator=True):
+        _check(lib().kb_build(self.h, int(use_mestimator)))
+
+    def set_constant_conditioner(self, diag):
+        _check(lib().kb_set_constant_conditioner(self.h, float(diag)))
+
+    def solve(self):
+        dx = np.zeros(self.ncols)
+        ok = C.c_int(0)
+        _check(lib().kb_solve(self.h, _d(dx), C.byref(ok)))
+        return bool(ok.value), dx
+
+    def rhs(self):
+        r = np.zeros(self.ncols)
+        _check(lib().kb_get_rhs(self.h, _d(r)))
+        return r
+
+    def apply_update(self, dx):
+        dX = C.c_double()
+        _check(lib().kb_apply_update(self.h, _d(np.ascontiguousarray(dx, dtype=np.float64)), C.byref(dX)))
+        return dX.value
+
+    def revert(self):
+        _check(lib().kb_revert(self.h))
+
+    def normal_blocks(self):
+        F, Cc = self.prob.n_frames, self.C
+        out = dict(Hff=np.zeros((F, 6, 6)), Hfc=np.zeros((F, 6, Cc)), gf=np.zeros((F, 6)), Hcc=np.zeros((Cc, Cc)),
+                   gc=np.zeros(Cc), cost=np.zeros(1))
+        _check(lib().kb_get_normal_blocks(self.h, _d(out["Hff"]), _d(out["Hfc"]), _d(out["gf"]), _d(out["Hcc"]),
+                                          _d(out["gc"]), _d(out["cost"])))
+        out["cost"] = float(out["cost"][0])
+        return out
+
+    # -- device-resident Optimizer2 --
+    def optimize(self, policy="lm", lambda0=10.0, max_iterations=200, eps_x=1e-3, eps_j=1.0, sync_every=4,
+                 use_graph=True):
+        o = OptimizerOptions(0 if policy == "lm" else 1, lambda0, max_iterations, eps_x, eps_j, sync_every,
+                             int(use_graph))
+        s = Solution()
+        _check(lib().kb_optimize(self.h, C.byref(o), C.byref(s)))
+        res = {f: getattr(s, f) for f, _ in Solution._fields_}
+        cap = 2 * max_iterations + 2
+        tr = np.zeros((cap, 4))
+        n = _check(lib().kb_get_trace(self.h, _d(tr), cap))
+        res["trace"] = tr[:n].copy()
+        return res
+
+    def run_gn(self, n_iter):
+        sec = C.c_double()
+        _check(lib().kb_run_gn_iterations(self.h, int(n_iter), C.byref(sec)))
+        return sec.value
+
+    def build_kernel_stats(self):
+        ms, by, fl = C.c_double(), C.c_double(), C.c_double()
+        _check(lib().kb_build_kernel_stats(self.h, C.byref(ms), C.byref(by), C.byref(fl)))
+        return ms.value, by.value, fl.value
+
+    def comm_init(self, uid: bytes, nranks, rank):
+        buf = C.create_string_buffer(uid, 128)
+        _check(lib().kb_comm_init(self.h, buf, int(nranks), int(rank)))

@@ -1,0 +1,735 @@
+// kb_capi.hip -- host side of the C-ABI (include/kalibr_hip.h): buffer management, launch
+// sequencing, the hipGraph-captured device-resident optimizer loop and the RCCL exchange.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/kalibr_hip.h"
+#include "kb_kernels.hip"
+
+using namespace kb;
+
+namespace {
+thread_local std::string g_err;
+
+int fail(const std::string& m) {
+  g_err = m;
+  return -1;
+}
+
+#define KB_HIP(call)                                                                              \
+  do {                                                                                            \
+    hipError_t e_ = (call);                                                                       \
+    if (e_ != hipSuccess) return fail(std::string(#call) + ": " + hipGetErrorString(e_));        \
+  } while (0)
+
+#define KB_NCCL(call)                                                                             \
+  do {                                                                                            \
+    ncclResult_t r_ = (call);                                                                     \
+    if (r_ != ncclSuccess) return fail(std::string(#call) + ": " + ncclGetErrorString(r_));      \
+  } while (0)
+
+int nintr_host(int m) {
+  switch (m) {
+    case KB_PINHOLE_RADTAN: return 8;
+    case KB_OMNI_RADTAN: return 9;
+    case KB_EUCM: return 6;
+    case KB_OMNI: return 5;
+    default: return -1;
+  }
+}
+}  // namespace
+
+struct kb_handle {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  KbDev d{};
+  int N = 0, F = 0, K = 0, V = 0, NC = 0, C = 0, ncols = 0, S = 0, W = 0;
+  int WPB = 1;
+  size_t lds_build = 0, lds_camexp = 0, lds_schur = 0, lds_solve = 0;
+  int cur = 0;  // host mirror of ctrl->cur for the per-call path
+  bool uploaded = false;
+  std::vector<void*> allocs;
+  // loop
+  hipGraphExec_t graph = nullptr;
+  int graph_trace_cap = 0;
+  double* trace = nullptr;
+  int trace_cap = 0;
+  // sharding
+  ncclComm_t comm = nullptr;
+  int nranks = 1, rank = 0;
+  double* redA_local = nullptr;
+  double* redA = nullptr;
+  int redA_n = 0;
+  // build-kernel timing
+  double build_ms = 0.0;
+
+  template <class T>
+  int alloc(T** p, size_t n) {
+    void* q = nullptr;
+    if (n == 0) n = 1;
+    hipError_t e = hipMalloc(&q, n * sizeof(T));
+    if (e != hipSuccess) return fail(std::string("hipMalloc: ") + hipGetErrorString(e));
+    hipMemsetAsync(q, 0, n * sizeof(T), stream);
+    allocs.push_back(q);
+    *p = (T*)q;
+    return 0;
+  }
+};
+
+extern "C" {
+
+const char* kb_last_error(void) { return g_err.c_str(); }
+
+kb_handle* kb_create(const kb_layout* L) {
+  if (!L || !L->cam_model || !L->target_points) {
+    fail("kb_create: null layout");
+    return nullptr;
+  }
+  if (L->n_cams < 1 || L->n_cams > KB_MAX_CAMS) {
+    fail("kb_create: n_cams out of range");
+    return nullptr;
+  }
+  if (L->n_frames < 1 || L->n_target < 1 || L->n_target > 65535) {
+    fail("kb_create: bad n_frames / n_target");
+    return nullptr;
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+    fail("kb_create: no HIP device available (the product path has no CPU fallback)");
+    return nullptr;
+  }
+  kb_handle* h = new kb_handle();
+  h->device = L->device;
+  if (hipSetDevice(h->device) != hipSuccess || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+    fail("kb_create: cannot select device / create stream");
+    delete h;
+    return nullptr;
+  }
+  h->N = L->n_cams;
+  h->F = L->n_frames;
+  h->K = L->n_target;
+  KbDev& d = h->d;
+  d.N = h->N;
+  d.F = h->F;
+  int c = 0;
+  for (int i = 0; i < h->N; ++i) {
+    const int n = nintr_host(L->cam_model[i]);
+    if (n < 0) {
+      fail("kb_create: unknown camera model");
+      delete h;
+      return nullptr;
+    }
+    d.model[i] = L->cam_model[i];
+    d.nintr[i] = n;
+    d.col_intr[i] = c;
+    c += n;
+  }
+  for (int j = 0; j < h->N - 1; ++j) {
+    d.col_base[j] = c;
+    c += 6;
+  }
+  h->C = c;
+  if (h->C > 109) {
+    fail("kb_create: camera block C > 109 not supported by k_schur (kSchurM)");
+    delete h;
+    return nullptr;
+  }
+  h->ncols = h->C + 6 * h->F;
+  h->S = h->N * KB_MAX_INTR + 7 * (h->N - 1) + 7 * h->F;
+  h->W = h->C * (h->C + 1) / 2 + h->C;
+  d.C = h->C;
+  d.ncols = h->ncols;
+  d.S = h->S;
+  d.off_base = h->N * KB_MAX_INTR;
+  d.off_frame = h->N * KB_MAX_INTR + 7 * (h->N - 1);
+  d.gframes = (h->F + 511) / 512;
+  d.nblk = (h->F + d.gframes - 1) / d.gframes;
+  d.nblk_bs = (h->F + 3) / 4;
+  h->WPB = h->N < 4 ? h->N : 4;
+
+  int rc = 0;
+  double* tgt = nullptr;
+  rc |= h->alloc(&tgt, 3 * (size_t)h->K);
+  rc |= h->alloc(&d.state, 2 * (size_t)h->S);
+  rc |= h->alloc(&d.camL, 12 * (size_t)h->N);
+  rc |= h->alloc(&d.camK, 36 * (size_t)h->N * h->N);
+  rc |= h->alloc(&d.Hff, 36 * (size_t)h->F);
+  rc |= h->alloc(&d.Hfc, 6 * (size_t)h->C * h->F);
+  rc |= h->alloc(&d.gf, 6 * (size_t)h->F);
+  rc |= h->alloc(&d.campart, (size_t)d.nblk * h->N * 136);
+  h->redA_n = h->N * 136 + h->W + 1;
+  rc |= h->alloc(&h->redA_local, (size_t)h->redA_n);
+  h->redA = h->redA_local;
+  rc |= h->alloc(&d.Hcc, (size_t)h->C * h->C);
+  rc |= h->alloc(&d.gc, (size_t)h->C);
+  rc |= h->alloc(&d.cost_build, 2);
+  rc |= h->alloc(&d.Lf, 36 * (size_t)h->F);
+  rc |= h->alloc(&d.Yf, 6 * (size_t)h->C * h->F);
+  rc |= h->alloc(&d.zf, 6 * (size_t)h->F);
+  rc |= h->alloc(&d.schurpart, (size_t)d.nblk * (h->W + 1));
+  rc |= h->alloc(&d.dx, (size_t)h->ncols);
+  rc |= h->alloc(&d.rhs, (size_t)h->ncols);
+  rc |= h->alloc(&d.statpart, 3 * (size_t)d.nblk_bs);
+  rc |= h->alloc(&d.camstat, 4);
+  rc |= h->alloc(&d.red_local, 8);
+  d.red = d.red_local;
+  rc |= h->alloc(&d.ctrl, 1);
+  std::vector<int32_t> colinfo(h->C), tri(h->C * (h->C + 1) / 2);
+  for (int i = 0; i < h->N; ++i)
+    for (int x = 0; x < d.nintr[i]; ++x) colinfo[d.col_intr[i] + x] = (0 << 16) | (i << 8) | x;
+  for (int j = 0; j < h->N - 1; ++j)
+    for (int x = 0; x < 6; ++x) colinfo[d.col_base[j] + x] = (1 << 16) | (j << 8) | x;
+  int e = 0;
+  for (int a = 0; a < h->C; ++a)
+    for (int b = a; b < h->C; ++b) tri[e++] = (a << 16) | b;
+  int32_t *ci = nullptr, *tr = nullptr;
+  rc |= h->alloc(&ci, colinfo.size());
+  rc |= h->alloc(&tr, tri.size());
+  if (rc) {
+    kb_destroy(h);
+    return nullptr;
+  }
+  d.colinfo = ci;
+  d.tri = tr;
+  d.target = tgt;
+  d.camsum_local = h->redA_local;
+  d.schursum_local = h->redA_local + h->N * 136;
+  d.camsum = h->redA;
+  d.schursum = h->redA + h->N * 136;
+  hipMemcpyAsync(ci, colinfo.data(), colinfo.size() * sizeof(int32_t), hipMemcpyHostToDevice, h->stream);
+  hipMemcpyAsync(tr, tri.data(), tri.size() * sizeof(int32_t), hipMemcpyHostToDevice, h->stream);
+  hipMemcpyAsync(tgt, L->target_points, 3 * sizeof(double) * h->K, hipMemcpyHostToDevice, h->stream);
+  h->lds_build = sizeof(double) * (h->WPB * 64 * XS + h->WPB * 256 + h->WPB * 64 + h->N * 256 + h->N * 36 * 2 + h->N * 8);
+  h->lds_camexp = sizeof(double) * (h->N * 256 + h->N * h->N * 36);
+  h->lds_schur = sizeof(double) * (6 * h->C + 36 + 8);
+  h->lds_solve = sizeof(double) * (h->C * h->C);
+  hipFuncSetAttribute((const void*)k_build, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_build);
+  hipFuncSetAttribute((const void*)k_camexpand, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_camexp);
+  hipFuncSetAttribute((const void*)k_schur, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_schur);
+  hipFuncSetAttribute((const void*)k_solve, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_solve);
+  if (hipStreamSynchronize(h->stream) != hipSuccess) {
+    fail("kb_create: stream sync failed");
+    kb_destroy(h);
+    return nullptr;
+  }
+  return h;
+}
+
+void kb_destroy(kb_handle* h) {
+  if (!h) return;
+  hipSetDevice(h->device);
+  if (h->stream) hipStreamSynchronize(h->stream);
+  if (h->graph) hipGraphExecDestroy(h->graph);
+  if (h->comm) ncclCommDestroy(h->comm);
+  for (void* p : h->allocs) hipFree(p);
+  if (h->trace) hipFree(h->trace);
+  if (h->stream) hipStreamDestroy(h->stream);
+  delete h;
+}
+
+int kb_state_size(const kb_handle* h) { return h ? h->S : -1; }
+int kb_num_cols(const kb_handle* h) { return h ? h->ncols : -1; }
+int kb_camera_cols(const kb_handle* h) { return h ? h->C : -1; }
+
+int kb_upload_observations(kb_handle* h, int32_t n_views, int32_t n_corners, const double* y, const uint16_t* corner_id,
+                           const uint32_t* view_offsets, const uint32_t* view_frame, const uint8_t* view_cam) {
+  if (!h) return fail("null handle");
+  if (h->uploaded) return fail("kb_upload_observations: observations already uploaded for this handle");
+  if (n_views < 1 || n_corners < 1 || !y || !corner_id || !view_offsets || !view_frame || !view_cam)
+    return fail("kb_upload_observations: empty or null input");
+  KB_HIP(hipSetDevice(h->device));
+  // host-side validation: shapes the kernels and grids assume
+  if (view_offsets[0] != 0 || (int64_t)view_offsets[n_views] != n_corners)
+    return fail("kb_upload_observations: view_offsets must start at 0 and end at n_corners");
+  std::vector<int32_t> fvc((size_t)h->F * h->N, -1), vf(n_views), vc(n_views);
+  for (int v = 0; v < n_views; ++v) {
+    if (view_offsets[v + 1] < view_offsets[v]) return fail("kb_upload_observations: view_offsets not monotone");
+    if ((int)view_frame[v] >= h->F || view_cam[v] >= h->N) return fail("kb_upload_observations: view index out of range");
+    if (v > 0 && view_frame[v] < view_frame[v - 1]) return fail("kb_upload_observations: views must be sorted by frame");
+    int32_t& slot = fvc[(size_t)view_frame[v] * h->N + view_cam[v]];
+    if (slot >= 0) return fail("kb_upload_observations: two views for one (frame, camera)");
+    slot = v;
+    vf[v] = (int32_t)view_frame[v];
+    vc[v] = (int32_t)view_cam[v];
+  }
+  for (int k = 0; k < n_corners; ++k)
+    if ((int)corner_id[k] >= h->K) return fail("kb_upload_observations: corner_id out of range");
+  h->V = n_views;
+  h->NC = n_corners;
+  KbDev& d = h->d;
+  d.V = n_views;
+  d.NC = n_corners;
+  d.nblk_cost = (n_views + 3) / 4;
+  double2* yd = nullptr;
+  uint16_t* cd = nullptr;
+  uint32_t* vo = nullptr;
+  int32_t *vfd = nullptr, *vcd = nullptr, *fv = nullptr;
+  int rc = 0;
+  rc |= h->alloc(&yd, (size_t)n_corners);
+  rc |= h->alloc(&cd, (size_t)n_corners);
+  rc |= h->alloc(&vo, (size_t)n_views + 1);
+  rc |= h->alloc(&vfd, (size_t)n_views);
+  rc |= h->alloc(&vcd, (size_t)n_views);
+  rc |= h->alloc(&fv, fvc.size());
+  rc |= h->alloc(&d.costpart, (size_t)d.nblk_cost);
+  if (rc) return -1;
+  KB_HIP(hipMemcpyAsync(yd, y, sizeof(double2) * n_corners, hipMemcpyHostToDevice, h->stream));
+  KB_HIP(hipMemcpyAsync(cd, corner_id, sizeof(uint16_t) * n_corners, hipMemcpyHostToDevice, h->stream));
+  KB_HIP(hipMemcpyAsync(vo, view_offsets, sizeof(uint32_t) * (n_views + 1), hipMemcpyHostToDevice, h->stream));
+  KB_HIP(hipMemcpyAsync(vfd, vf.data(), sizeof(int32_t) * n_views, hipMemcpyHostToDevice, h->stream));
+  KB_HIP(hipMemcpyAsync(vcd, vc.data(), sizeof(int32_t) * n_views, hipMemcpyHostToDevice, h->stream));
+  KB_HIP(hipMemcpyAsync(fv, fvc.data(), sizeof(int32_t) * fvc.size(), hipMemcpyHostToDevice, h->stream));
+  KB_HIP(hipStreamSynchronize(h->stream));
+  d.y = yd;
+  d.cid = cd;
+  d.view_off = vo;
+  d.view_frame = vfd;
+  d.view_cam = vcd;
+  d.frame_vcam = fv;
+  h->uploaded = true;
+  return 0;
+}
+
+static int set_cur(kb_handle* h, int cur) {
+  h->cur = cur;
+  KB_HIP(hipMemcpyAsync(&h->d.ctrl->cur, &h->cur, sizeof(int), hipMemcpyHostToDevice, h->stream));
+  return 0;
+}
+
+int kb_set_state_flat(kb_handle* h, const double* state) {
+  if (!h || !state) return fail("kb_set_state_flat: null");
+  KB_HIP(hipSetDevice(h->device));
+  KB_HIP(hipMemcpyAsync(h->d.state + (size_t)h->cur * h->S, state, sizeof(double) * h->S, hipMemcpyHostToDevice, h->stream));
+  KB_HIP(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+int kb_set_state(kb_handle* h, const double* poses_q, const double* poses_t, const double* baselines,
+                 const double* intrinsics) {
+  if (!h || !poses_q || !poses_t || !intrinsics || (h->N > 1 && !baselines)) return fail("kb_set_state: null");
+  std::vector<double> s(h->S, 0.0);
+  for (int q = 0; q < h->N * KB_MAX_INTR; ++q) s[q] = intrinsics[q];
+  for (int q = 0; q < 7 * (h->N - 1); ++q) s[h->d.off_base + q] = baselines[q];
+  for (int f = 0; f < h->F; ++f) {
+    for (int q = 0; q < 4; ++q) s[h->d.off_frame + 7 * f + q] = poses_q[4 * f + q];
+    for (int q = 0; q < 3; ++q) s[h->d.off_frame + 7 * f + 4 + q] = poses_t[3 * f + q];
+  }
+  return kb_set_state_flat(h, s.data());
+}
+
+int kb_get_state_flat(kb_handle* h, double* state) {
+  if (!h || !state) return fail("kb_get_state_flat: null");
+  KB_HIP(hipSetDevice(h->device));
+  KB_HIP(hipMemcpyAsync(state, h->d.state + (size_t)h->cur * h->S, sizeof(double) * h->S, hipMemcpyDeviceToHost, h->stream));
+  KB_HIP(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+// ---------------------------------------------------------------- launch helpers
+static int launch_cost(kb_handle* h, int gate, int which) {
+  hipLaunchKernelGGL(k_cost, dim3(h->d.nblk_cost), dim3(256), 0, h->stream, h->d, gate, which);
+  KB_HIP(hipGetLastError());
+  return 0;
+}
+
+static int allreduce_red(kb_handle* h) {
+  if (!h->comm) return 0;
+  KB_NCCL(ncclAllReduce(h->d.red_local, h->d.red, 3, ncclDouble, ncclSum, h->comm, h->stream));
+  KB_NCCL(ncclAllReduce(h->d.red_local + 3, h->d.red + 3, 1, ncclDouble, ncclMax, h->comm, h->stream));
+  return 0;
+}
+
+static int allreduce_A(kb_handle* h) {
+  if (!h->comm) return 0;
+  KB_NCCL(ncclAllReduce(h->redA_local, h->redA, h->redA_n, ncclDouble, ncclSum, h->comm, h->stream));
+  return 0;
+}
+
+static int launch_build(kb_handle* h, int gate) {
+  KbDev& d = h->d;
+  hipLaunchKernelGGL(k_prep, dim3(1), dim3(256), 0, h->stream, d, gate);
+  hipLaunchKernelGGL(k_build, dim3(d.nblk), dim3(64 * h->WPB), h->lds_build, h->stream, d, gate);
+  hipLaunchKernelGGL(k_colsum, dim3((h->N * 136 + 63) / 64), dim3(256), 0, h->stream, d, (const double*)d.campart, d.nblk,
+                     h->N * 136, d.camsum_local, gate ? 1 : 0);
+  KB_HIP(hipGetLastError());
+  return 0;
+}
+
+static int launch_schur(kb_handle* h, int gate) {
+  KbDev& d = h->d;
+  hipLaunchKernelGGL(k_schur, dim3(d.nblk), dim3(256), h->lds_schur, h->stream, d, gate);
+  hipLaunchKernelGGL(k_colsum, dim3((h->W + 1 + 63) / 64), dim3(256), 0, h->stream, d, (const double*)d.schurpart, d.nblk,
+                     h->W + 1, d.schursum_local, gate ? 2 : 0);
+  KB_HIP(hipGetLastError());
+  return 0;
+}
+
+static int launch_camexpand(kb_handle* h, int gate) {
+  hipLaunchKernelGGL(k_camexpand, dim3(1), dim3(256), h->lds_camexp, h->stream, h->d, gate);
+  KB_HIP(hipGetLastError());
+  return 0;
+}
+
+static int launch_solve(kb_handle* h, int gate, int do_update) {
+  hipLaunchKernelGGL(k_solve, dim3(1), dim3(256), h->lds_solve, h->stream, h->d, gate, do_update);
+  KB_HIP(hipGetLastError());
+  return 0;
+}
+
+static int launch_backsub(kb_handle* h, int gate, int do_update) {
+  hipLaunchKernelGGL(k_backsub, dim3(h->d.nblk_bs), dim3(256), 0, h->stream, h->d, gate, do_update);
+  KB_HIP(hipGetLastError());
+  return 0;
+}
+
+// ---------------------------------------------------------------- per-call API
+int kb_eval_cost(kb_handle* h, double* J_out) {
+  if (!h || !J_out) return fail("kb_eval_cost: null");
+  if (!h->uploaded) return fail("kb_eval_cost: no observations");
+  KB_HIP(hipSetDevice(h->device));
+  if (launch_cost(h, 0, 0)) return -1;
+  hipLaunchKernelGGL(k_reduce, dim3(1), dim3(256), 0, h->stream, h->d, 0, 0);
+  if (allreduce_red(h)) return -1;
+  KB_HIP(hipMemcpyAsync(J_out, h->d.red, sizeof(double), hipMemcpyDeviceToHost, h->stream));
+  KB_HIP(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+int kb_build(kb_handle* h, int use_mestimator) {
+  if (!h) return fail("kb_build: null");
+  if (!h->uploaded) return fail("kb_build: no observations");
+  (void)use_mestimator;  // NoMEstimator: weight 1 either way (ErrorTerm.cpp:11)
+  KB_HIP(hipSetDevice(h->device));
+  if (launch_build(h, 0)) return -1;
+  // the camera block needs the (reduced) per-camera sums; on one GPU redA == redA_local
+  if (h->comm) {
+    KB_NCCL(ncclAllReduce(h->redA_local, h->redA, h->N * 136, ncclDouble, ncclSum, h->comm, h->stream));
+  }
+  if (launch_camexpand(h, 0)) return -1;
+  KB_HIP(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+int kb_set_constant_conditioner(kb_handle* h, double diag) {
+  if (!h) return fail("null handle");
+  h->d.host_lambda = diag;
+  return 0;
+}
+
+int kb_solve(kb_handle* h, double* dx_out, int* ok) {
+  if (!h || !ok) return fail("kb_solve: null");
+  KB_HIP(hipSetDevice(h->device));
+  const int one = 1;
+  KB_HIP(hipMemcpyAsync(&h->d.ctrl->solve_ok, &one, sizeof(int), hipMemcpyHostToDevice, h->stream));
+  if (launch_schur(h, 0)) return -1;
+  if (h->comm) {
+    KB_NCCL(ncclAllReduce(h->d.schursum_local, h->d.schursum, h->W + 1, ncclDouble, ncclSum, h->comm, h->stream));
+  }
+  // k_solve folds the Schur failure count (schursum[W]) and the Cholesky of S into ctrl->solve_ok
+  if (launch_solve(h, 0, 0)) return -1;
+  int okd = 0;
+  KB_HIP(hipMemcpyAsync(&okd, &h->d.ctrl->solve_ok, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+  KB_HIP(hipStreamSynchronize(h->stream));
+  *ok = okd;
+  if (!okd) return 0;
+  if (launch_backsub(h, 0, 0)) return -1;
+  if (dx_out) KB_HIP(hipMemcpyAsync(dx_out, h->d.dx, sizeof(double) * h->ncols, hipMemcpyDeviceToHost, h->stream));
+  KB_HIP(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+int kb_get_rhs(kb_handle* h, double* rhs_out) {
+  if (!h || !rhs_out) return fail("kb_get_rhs: null");
+  KB_HIP(hipSetDevice(h->device));
+  KB_HIP(hipMemcpyAsync(rhs_out, h->d.gc, sizeof(double) * h->C, hipMemcpyDeviceToHost, h->stream));
+  KB_HIP(hipMemcpyAsync(rhs_out + h->C, h->d.gf, sizeof(double) * 6 * h->F, hipMemcpyDeviceToHost, h->stream));
+  KB_HIP(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+int kb_apply_update(kb_handle* h, const double* dx, double* deltaX_out) {
+  if (!h) return fail("kb_apply_update: null");
+  KB_HIP(hipSetDevice(h->device));
+  std::vector<double> hx;
+  if (dx) {
+    KB_HIP(hipMemcpyAsync(h->d.dx, dx, sizeof(double) * h->ncols, hipMemcpyHostToDevice, h->stream));
+  } else {
+    hx.resize(h->ncols);
+    KB_HIP(hipMemcpyAsync(hx.data(), h->d.dx, sizeof(double) * h->ncols, hipMemcpyDeviceToHost, h->stream));
+  }
+  const int n = std::max(h->F, h->N * KB_MAX_INTR);
+  hipLaunchKernelGGL(k_update_all, dim3((n + 255) / 256), dim3(256), 0, h->stream, h->d);
+  KB_HIP(hipGetLastError());
+  if (set_cur(h, 1 - h->cur)) return -1;
+  KB_HIP(hipStreamSynchronize(h->stream));
+  if (deltaX_out) {
+    const double* p = dx ? dx : hx.data();
+    double m = 0.0;
+    for (int q = 0; q < h->ncols; ++q) m = std::max(m, std::fabs(p[q]));
+    *deltaX_out = m;
+  }
+  return 0;
+}
+
+int kb_revert(kb_handle* h) {
+  if (!h) return fail("kb_revert: null");
+  KB_HIP(hipSetDevice(h->device));
+  if (set_cur(h, 1 - h->cur)) return -1;
+  KB_HIP(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+int kb_get_normal_blocks(kb_handle* h, double* Hff, double* Hfc, double* gf, double* Hcc, double* gc, double* cost) {
+  if (!h) return fail("null handle");
+  KB_HIP(hipSetDevice(h->device));
+  if (Hff) KB_HIP(hipMemcpyAsync(Hff, h->d.Hff, sizeof(double) * 36 * h->F, hipMemcpyDeviceToHost, h->stream));
+  if (Hfc) KB_HIP(hipMemcpyAsync(Hfc, h->d.Hfc, sizeof(double) * 6 * h->C * h->F, hipMemcpyDeviceToHost, h->stream));
+  if (gf) KB_HIP(hipMemcpyAsync(gf, h->d.gf, sizeof(double) * 6 * h->F, hipMemcpyDeviceToHost, h->stream));
+  if (Hcc) KB_HIP(hipMemcpyAsync(Hcc, h->d.Hcc, sizeof(double) * h->C * h->C, hipMemcpyDeviceToHost, h->stream));
+  if (gc) KB_HIP(hipMemcpyAsync(gc, h->d.gc, sizeof(double) * h->C, hipMemcpyDeviceToHost, h->stream));
+  if (cost) KB_HIP(hipMemcpyAsync(cost, h->d.cost_build, sizeof(double), hipMemcpyDeviceToHost, h->stream));
+  KB_HIP(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+// ---------------------------------------------------------------- device-resident loop
+// One pass: pol_pre | prep build colsum (gated on do_build) | schur colsum [allreduce A] camexpand solve |
+// backsub cost reduce [allreduce stats] | pol_post.  Every kernel early-exits once ctrl->done is set.
+static int enqueue_pass(kb_handle* h) {
+  KbDev& d = h->d;
+  hipLaunchKernelGGL(k_pol_pre, dim3(1), dim3(1), 0, h->stream, d);
+  if (launch_build(h, 1)) return -1;
+  if (launch_schur(h, 1)) return -1;
+  if (allreduce_A(h)) return -1;
+  if (launch_camexpand(h, 1)) return -1;
+  if (launch_solve(h, 1, 1)) return -1;
+  if (launch_backsub(h, 1, 1)) return -1;
+  if (launch_cost(h, 1, 1)) return -1;
+  hipLaunchKernelGGL(k_reduce, dim3(1), dim3(256), 0, h->stream, d, 1, 1);
+  if (allreduce_red(h)) return -1;
+  hipLaunchKernelGGL(k_pol_post, dim3(1), dim3(1), 0, h->stream, d);
+  KB_HIP(hipGetLastError());
+  return 0;
+}
+
+static int ensure_trace(kb_handle* h, int cap) {
+  if (h->trace_cap >= cap) return 0;
+  if (h->trace) hipFree(h->trace);
+  h->trace = nullptr;
+  KB_HIP(hipMalloc(&h->trace, sizeof(double) * 4 * cap));
+  h->trace_cap = cap;
+  h->d.trace = h->trace;
+  h->d.trace_cap = cap;
+  if (h->graph) {  // captured kernel args hold the old pointer
+    hipGraphExecDestroy(h->graph);
+    h->graph = nullptr;
+  }
+  return 0;
+}
+
+static int ensure_graph(kb_handle* h) {
+  if (h->graph) return 0;
+  hipGraph_t g = nullptr;
+  KB_HIP(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
+  int rc = enqueue_pass(h);
+  hipError_t e = hipStreamEndCapture(h->stream, &g);
+  if (rc) return rc;
+  if (e != hipSuccess) return fail(std::string("hipStreamEndCapture: ") + hipGetErrorString(e));
+  KB_HIP(hipGraphInstantiate(&h->graph, g, nullptr, nullptr, 0));
+  KB_HIP(hipGraphDestroy(g));
+  return 0;
+}
+
+static int loop_start(kb_handle* h, const KbOpts& o) {
+  // evaluateError on the start state (Optimizer2.cpp:192-196), then optimizationStarting
+  if (launch_cost(h, 0, 0)) return -1;
+  hipLaunchKernelGGL(k_reduce, dim3(1), dim3(256), 0, h->stream, h->d, 0, 0);
+  if (allreduce_red(h)) return -1;
+  hipLaunchKernelGGL(k_pol_init, dim3(1), dim3(1), 0, h->stream, h->d, o);
+  KB_HIP(hipGetLastError());
+  return 0;
+}
+
+int kb_optimize(kb_handle* h, const kb_optimizer_options* opts, kb_solution* out) {
+  if (!h || !opts || !out) return fail("kb_optimize: null");
+  if (!h->uploaded) return fail("kb_optimize: no observations");
+  if (opts->policy != 0 && opts->policy != 1) return fail("kb_optimize: unknown policy");
+  KB_HIP(hipSetDevice(h->device));
+  const int max_passes = 2 * opts->max_iterations + 1;
+  if (ensure_trace(h, max_passes + 1)) return -1;
+  KbOpts o{opts->policy, opts->max_iterations, opts->lambda_init, opts->convergence_dx, opts->convergence_dj};
+  if (loop_start(h, o)) return -1;
+  const bool graph = opts->use_graph != 0 && !h->comm;  // RCCL calls stay eager
+  if (graph && ensure_graph(h)) return -1;
+  const int every = opts->sync_every > 0 ? opts->sync_every : 4;
+  KbCtrl ctrl{};
+  int passes = 0;
+  while (passes < max_passes) {
+    const int n = std::min(every, max_passes - passes);
+    for (int i = 0; i < n; ++i) {
+      if (graph) {
+        KB_HIP(hipGraphLaunch(h->graph, h->stream));
+      } else if (enqueue_pass(h)) {
+        return -1;
+      }
+    }
+    passes += n;
+    KB_HIP(hipMemcpyAsync(&ctrl, h->d.ctrl, sizeof(KbCtrl), hipMemcpyDeviceToHost, h->stream));
+    KB_HIP(hipStreamSynchronize(h->stream));
+    if (ctrl.done) break;
+  }
+  h->cur = ctrl.cur;
+  out->J_start = ctrl.J_start;
+  out->J_final = ctrl.p_J;
+  out->dx_final = ctrl.deltaX;
+  out->dj_final = ctrl.deltaJ;
+  out->iterations = ctrl.iterations;
+  out->failed_iterations = ctrl.failed_iterations;
+  out->linear_solver_failure = ctrl.lin_fail;
+  out->passes = ctrl.passes;
+  return 0;
+}
+
+int kb_get_trace(kb_handle* h, double* trace, int32_t cap) {
+  if (!h || !trace) return fail("kb_get_trace: null");
+  KB_HIP(hipSetDevice(h->device));
+  KbCtrl ctrl{};
+  KB_HIP(hipMemcpy(&ctrl, h->d.ctrl, sizeof(KbCtrl), hipMemcpyDeviceToHost));
+  const int n = std::min(cap, std::min(ctrl.n_trace, h->trace_cap));
+  if (n > 0) KB_HIP(hipMemcpy(trace, h->trace, sizeof(double) * 4 * n, hipMemcpyDeviceToHost));
+  return n;
+}
+
+int kb_run_gn_iterations(kb_handle* h, int32_t n_iter, double* seconds) {
+  if (!h || n_iter < 0) return fail("kb_run_gn_iterations: bad args");
+  if (!h->uploaded) return fail("kb_run_gn_iterations: no observations");
+  KB_HIP(hipSetDevice(h->device));
+  if (ensure_trace(h, 64)) return -1;
+  // GN, convergence tests disabled (thresholds -1 keep (dX > eps && |dJ| > eps) true)
+  KbOpts o{1, 0x3fffffff, 0.0, -1.0, -1.0};
+  if (loop_start(h, o)) return -1;
+  const bool graph = !h->comm;
+  if (graph && ensure_graph(h)) return -1;
+  KB_HIP(hipStreamSynchronize(h->stream));
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int i = 0; i < n_iter; ++i) {
+    if (graph) {
+      KB_HIP(hipGraphLaunch(h->graph, h->stream));
+    } else if (enqueue_pass(h)) {
+      return -1;
+    }
+  }
+  KB_HIP(hipStreamSynchronize(h->stream));
+  const auto t1 = std::chrono::steady_clock::now();
+  if (seconds) *seconds = std::chrono::duration<double>(t1 - t0).count();
+  KbCtrl ctrl{};
+  KB_HIP(hipMemcpy(&ctrl, h->d.ctrl, sizeof(KbCtrl), hipMemcpyDeviceToHost));
+  h->cur = ctrl.cur;
+  if (ctrl.iterations != n_iter) return fail("kb_run_gn_iterations: linear solver failures during the timed passes");
+  return 0;
+}
+
+int kb_build_kernel_stats(kb_handle* h, double* avg_ms, double* bytes_per_launch, double* flops_per_launch) {
+  if (!h) return fail("null handle");
+  KB_HIP(hipSetDevice(h->device));
+  const int reps = 20;
+  hipEvent_t e0, e1;
+  KB_HIP(hipEventCreate(&e0));
+  KB_HIP(hipEventCreate(&e1));
+  // warm
+  hipLaunchKernelGGL(k_prep, dim3(1), dim3(256), 0, h->stream, h->d, 0);
+  hipLaunchKernelGGL(k_build, dim3(h->d.nblk), dim3(64 * h->WPB), h->lds_build, h->stream, h->d, 0);
+  double tot = 0.0;
+  for (int r = 0; r < reps; ++r) {
+    KB_HIP(hipEventRecord(e0, h->stream));
+    hipLaunchKernelGGL(k_build, dim3(h->d.nblk), dim3(64 * h->WPB), h->lds_build, h->stream, h->d, 0);
+    KB_HIP(hipEventRecord(e1, h->stream));
+    KB_HIP(hipEventSynchronize(e1));
+    float ms = 0.f;
+    KB_HIP(hipEventElapsedTime(&ms, e0, e1));
+    tot += ms;
+  }
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  h->build_ms = tot / reps;
+  if (avg_ms) *avg_ms = h->build_ms;
+  // algorithmic bytes: observations (y 16 B + id 2 B per corner), view/frame index tables, state,
+  // written frame blocks (H_ff, g_f, H_fc) and per-block camera partials.
+  const double bytes = 18.0 * h->NC + 4.0 * (h->V + 1) + 4.0 * h->F * h->N + 8.0 * h->S +
+                       8.0 * h->F * (36 + 6 + 6.0 * h->C) + 8.0 * h->d.nblk * h->N * 136;
+  if (bytes_per_launch) *bytes_per_launch = bytes;
+  // executed MFMA flops (2 x 16 x 16 x rows, rows padded to 64 per 32-corner phase) + ~300 VALU flops/corner
+  double rows = 0.0;
+  std::vector<uint32_t> vo(h->V + 1);
+  KB_HIP(hipMemcpy(vo.data(), h->d.view_off, sizeof(uint32_t) * (h->V + 1), hipMemcpyDeviceToHost));
+  for (int v = 0; v < h->V; ++v) rows += 64.0 * ((vo[v + 1] - vo[v] + 31) / 32);
+  if (flops_per_launch) *flops_per_launch = rows * 16 * 16 * 2 + 300.0 * h->NC;
+  return 0;
+}
+
+int kb_comm_get_unique_id(void* out) {
+  if (!out) return fail("null");
+  ncclUniqueId id;
+  KB_NCCL(ncclGetUniqueId(&id));
+  std::memcpy(out, &id, sizeof(id));
+  return 0;
+}
+
+int kb_comm_init(kb_handle* h, const void* uid, int32_t nranks, int32_t rank) {
+  if (!h || !uid) return fail("kb_comm_init: null");
+  KB_HIP(hipSetDevice(h->device));
+  if (nranks <= 1) return 0;
+  ncclUniqueId id;
+  std::memcpy(&id, uid, sizeof(id));
+  KB_NCCL(ncclCommInitRank(&h->comm, nranks, id, rank));
+  h->nranks = nranks;
+  h->rank = rank;
+  // separate reduced buffers
+  double* ra = nullptr;
+  double* rr = nullptr;
+  if (h->alloc(&ra, (size_t)h->redA_n) || h->alloc(&rr, 8)) return -1;
+  h->redA = ra;
+  h->d.camsum = ra;
+  h->d.schursum = ra + h->N * 136;
+  h->d.red = rr;
+  if (h->graph) {
+    hipGraphExecDestroy(h->graph);
+    h->graph = nullptr;
+  }
+  KB_HIP(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+int kb_selftest_mfma(double* max_err) {
+  double* d = nullptr;
+  KB_HIP(hipMalloc(&d, sizeof(double) * 256));
+  double worst = 0.0;
+  for (int ident = 1; ident >= 0; --ident) {
+    hipLaunchKernelGGL(k_selftest_mfma, dim3(1), dim3(64), 0, 0, d, ident);
+    KB_HIP(hipGetLastError());
+    double hD[256];
+    KB_HIP(hipMemcpy(hD, d, sizeof(hD), hipMemcpyDeviceToHost));
+    for (int i = 0; i < 16; ++i)
+      for (int j = 0; j < 16; ++j) {
+        double s = 0.0;
+        for (int k = 0; k < 16; ++k) {
+          const double a = ident ? (i == k ? 1.0 : 0.0) : (i * 0.5 + k * 0.125 + ((i * 3 + k) % 5));
+          const double b = k * 16.0 + j + 0.25 * ((k * 5 + j * 3) % 7);
+          s += a * b;
+        }
+        worst = std::max(worst, std::fabs(s - hD[i * 16 + j]));
+      }
+  }
+  hipFree(d);
+  if (max_err) *max_err = worst;
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,341 @@
+"""Deterministic synthetic AprilGrid calibration problems.
+
+Generates the observation set that Kalibr2's CalibrateMultiCameraRig consumes
+(kalibr2/include/kalibr2/CalibrationTools.hpp:376-428): one target pose per
+synchronised frame, camera i observes p_ci = B_{i-1} ... B_0 T_f^-1 P.
+
+Target geometry follows GridCalibrationTargetAprilgrid::createGridPoints
+(aslam_cv/aslam_cameras_april/src/GridCalibrationTargetAprilgrid.cpp:83-95) with
+the board of kalibr2_ros/calibration_config.yaml:1-6 (6x5 tags, 0.088 m,
+spacing 0.2954) -> 120 corners.  Quaternions are JPL [x, y, z, w]
+(Schweizer-Messer/sm_kinematics/src/quaternion_algebra.cpp).
+
+The flat state layout and the column order are documented in DESIGN.md and in
+include/kalibr_hip.h.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+
+MAX_INTR = 10
+POSE = 7
+
+PINHOLE_RADTAN = 0
+OMNI_RADTAN = 1
+EUCM = 2
+OMNI = 3
+MODEL_NAMES = {PINHOLE_RADTAN: "pinhole-radtan", OMNI_RADTAN: "omni-radtan", EUCM: "eucm", OMNI: "omni"}
+NINTR = {PINHOLE_RADTAN: 8, OMNI_RADTAN: 9, EUCM: 6, OMNI: 5}
+
+
+def aprilgrid_points(tag_rows=5, tag_cols=6, tag_size=0.088, tag_spacing=0.2954):
+    rows, cols = 2 * tag_rows, 2 * tag_cols
+    pts = np.zeros((rows * cols, 3))
+    for r in range(rows):
+        for c in range(cols):
+            pts[r * cols + c, 0] = (c // 2) * (1 + tag_spacing) * tag_size + (c % 2) * tag_size
+            pts[r * cols + c, 1] = (r // 2) * (1 + tag_spacing) * tag_size + (r % 2) * tag_size
+    return pts
+
+
+# ---- JPL quaternion helpers (restated from quaternion_algebra.cpp) ----
+
+def quat2r(q):
+    x, y, z, w = q
+    return np.array([
+        [x * x - y * y - z * z + w * w, 2 * x * y + 2 * z * w, 2 * x * z - 2 * y * w],
+        [2 * x * y - 2 * z * w, -x * x + y * y - z * z + w * w, 2 * x * w + 2 * y * z],
+        [2 * x * z + 2 * y * w, -2 * x * w + 2 * y * z, -x * x - y * y + z * z + w * w],
+    ])
+
+
+def r2quat(R):
+    c1, c2, c3 = R[0, 0], R[1, 0], R[2, 0]
+    c4, c5, c6 = R[0, 1], R[1, 1], R[2, 1]
+    c7, c8, c9 = R[0, 2], R[1, 2], R[2, 2]
+    dc = np.abs([1 + c1 - c5 - c9, 1 - c1 + c5 - c9, 1 - c1 - c5 + c9, 1 + c1 + c5 + c9])
+    m = int(np.argmax(dc))
+    q = np.zeros(4)
+    if m == 0:
+        q[0] = 0.5 * np.sqrt(dc[0]); c = 0.25 / q[0]
+        q[1] = c * (c4 + c2); q[2] = c * (c7 + c3); q[3] = c * (c8 - c6)
+    elif m == 1:
+        q[1] = 0.5 * np.sqrt(dc[1]); c = 0.25 / q[1]
+        q[0] = c * (c4 + c2); q[2] = c * (c6 + c8); q[3] = c * (c3 - c7)
+    elif m == 2:
+        q[2] = 0.5 * np.sqrt(dc[2]); c = 0.25 / q[2]
+        q[0] = c * (c3 + c7); q[1] = c * (c6 + c8); q[3] = c * (c4 - c2)
+    else:
+        q[3] = 0.5 * np.sqrt(dc[3]); c = 0.25 / q[3]
+        q[0] = c * (c8 - c6); q[1] = c * (c3 - c7); q[2] = c * (c4 - c2)
+    if q[3] < 0:
+        q = -q
+    return q
+
+
+def rotvec(a):
+    """Standard (right-handed, active) rotation matrix exp([a]x)."""
+    th = np.linalg.norm(a)
+    if th < 1e-15:
+        return np.eye(3)
+    k = a / th
+    K = np.array([[0, -k[2], k[1]], [k[2], 0, -k[0]], [-k[1], k[0], 0]])
+    return np.eye(3) + np.sin(th) * K + (1 - np.cos(th)) * K @ K
+
+
+def pose_from_Rt(R, t):
+    return np.concatenate([r2quat(R), t])
+
+
+def pose_to_T(pose):
+    T = np.eye(4)
+    T[:3, :3] = quat2r(pose[:4])
+    T[:3, 3] = pose[4:7]
+    return T
+
+
+def inv_T(T):
+    Ti = np.eye(4)
+    Ti[:3, :3] = T[:3, :3].T
+    Ti[:3, 3] = -T[:3, :3].T @ T[:3, 3]
+    return Ti
+
+
+# ---- projection (vectorised, used only to synthesise observations) ----
+
+def project(model, intr, p):
+    """p: (n,3) camera-frame points -> (n,2) keypoints, valid mask."""
+    x, y, z = p[:, 0], p[:, 1], p[:, 2]
+    if model == PINHOLE_RADTAN:
+        fu, fv, cu, cv, k1, k2, p1, p2 = intr[:8]
+        mx, my = x / z, y / z
+        valid = z > 0
+        dist = True
+    elif model in (OMNI_RADTAN, OMNI):
+        xi, fu, fv, cu, cv = intr[:5]
+        d = np.sqrt(x * x + y * y + z * z)
+        fovp = xi if xi <= 1 else 1 / xi
+        valid = z > -(fovp * d)
+        mx, my = x / (z + xi * d), y / (z + xi * d)
+        dist = model == OMNI_RADTAN
+        if dist:
+            k1, k2, p1, p2 = intr[5:9]
+    elif model == EUCM:
+        al, be, fu, fv, cu, cv = intr[:6]
+        d = np.sqrt(be * (x * x + y * y) + z * z)
+        fovp = al / (1 - al) if al <= 0.5 else (1 - al) / al
+        valid = z > -(fovp * d)
+        n = al * d + (1 - al) * z
+        mx, my = x / n, y / n
+        dist = False
+    else:
+        raise ValueError(model)
+    if dist:
+        mx2, my2, mxy = mx * mx, my * my, mx * my
+        r2 = mx2 + my2
+        rad = k1 * r2 + k2 * r2 * r2
+        ux = mx + mx * rad + 2 * p1 * mxy + p2 * (r2 + 2 * mx2)
+        uy = my + my * rad + 2 * p2 * mxy + p1 * (r2 + 2 * my2)
+        mx, my = ux, uy
+    return np.stack([fu * mx + cu, fv * my + cv], axis=1), valid
+
+
+@dataclass
+class Problem:
+    """Observation set + state in the layout of include/kalibr_hip.h."""
+
+    cam_model: np.ndarray  # int32 [N]
+    target: np.ndarray  # float64 [K,3]
+    view_frame: np.ndarray  # int32 [V]  (sorted by frame, then camera)
+    view_cam: np.ndarray  # int32 [V]
+    view_offset: np.ndarray  # int32 [V+1]
+    corner_id: np.ndarray  # int32 [Nc]
+    y: np.ndarray  # float64 [Nc,2]
+    state_truth: np.ndarray
+    state_init: np.ndarray
+    resolution: tuple = (1280, 1024)
+    name: str = ""
+    meta: dict = field(default_factory=dict)
+
+    @property
+    def n_cams(self):
+        return int(self.cam_model.shape[0])
+
+    @property
+    def n_frames(self):
+        return int(self.view_frame.max()) + 1 if self.view_frame.size else 0
+
+    @property
+    def n_views(self):
+        return int(self.view_frame.shape[0])
+
+    @property
+    def n_corners(self):
+        return int(self.corner_id.shape[0])
+
+    @property
+    def cam_cols(self):
+        return int(sum(NINTR[int(m)] for m in self.cam_model) + 6 * (self.n_cams - 1))
+
+    @property
+    def total_cols(self):
+        return self.cam_cols + 6 * self.n_frames
+
+    def frame_slice(self, f0, f1):
+        """Sub-problem holding frames [f0, f1) (frames renumbered from 0), used for sharding."""
+        vm = (self.view_frame >= f0) & (self.view_frame < f1)
+        vidx = np.nonzero(vm)[0]
+        offs = self.view_offset
+        corners = np.concatenate([np.arange(offs[v], offs[v + 1]) for v in vidx]) if vidx.size else np.zeros(0, int)
+        counts = offs[vidx + 1] - offs[vidx]
+        N = self.n_cams
+        so = N * MAX_INTR + POSE * (N - 1)
+
+        def cut(st):
+            return np.concatenate([st[:so], st[so + POSE * f0: so + POSE * f1]])
+
+        return Problem(
+            cam_model=self.cam_model.copy(), target=self.target.copy(),
+            view_frame=(self.view_frame[vidx] - f0).astype(np.int32), view_cam=self.view_cam[vidx].copy(),
+            view_offset=np.concatenate([[0], np.cumsum(counts)]).astype(np.int32),
+            corner_id=self.corner_id[corners].astype(np.int32), y=self.y[corners].copy(),
+            state_truth=cut(self.state_truth), state_init=cut(self.state_init),
+            resolution=self.resolution, name=f"{self.name}[{f0}:{f1}]", meta=dict(self.meta))
+
+
+def state_size(n_cams, n_frames):
+    return n_cams * MAX_INTR + POSE * (n_cams - 1) + POSE * n_frames
+
+
+def make_problem(models, n_frames, seed, p_view=1.0, noise_px=0.3, min_corners=12,
+                 resolution=(1280, 1024), name="", init_noise=True):
+    """Synthesise an N-camera x F-frame AprilGrid problem."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    W, H = resolution
+    N = len(models)
+    target = aprilgrid_points()
+    tcen = target.mean(axis=0)
+    intr_truth = np.zeros((N, MAX_INTR))
+    for i, m in enumerate(models):
+        if m == PINHOLE_RADTAN:
+            intr_truth[i, :8] = [881.0, 881.0, 640.0, 512.0, -0.2, 0.13, 5e-4, 5e-4]
+        elif m == OMNI_RADTAN:
+            intr_truth[i, :9] = [0.9, 450.0, 450.0, 640.0, 512.0, -0.05, 0.01, 1e-4, 1e-4]
+        elif m == OMNI:
+            intr_truth[i, :5] = [0.9, 450.0, 450.0, 640.0, 512.0]
+        elif m == EUCM:
+            intr_truth[i, :6] = [0.6, 1.1, 450.0, 450.0, 640.0, 512.0]
+        else:
+            raise ValueError(m)
+    # rig: camera i+1 sits 0.12 m along -x from camera i, +-3 deg, +-5 mm
+    base_T = []
+    cam_T_c0 = [np.eye(4)]  # T_{ci, c0}
+    for j in range(N - 1):
+        R = rotvec(np.deg2rad(rng.uniform(-3, 3, 3)))
+        o = np.array([-0.12, 0.0, 0.0]) + rng.uniform(-0.005, 0.005, 3)
+        T_ci_cj1 = np.eye(4)
+        T_ci_cj1[:3, :3] = R
+        T_ci_cj1[:3, 3] = o
+        B = inv_T(T_ci_cj1)  # T_{c(j+1), c(j)}
+        base_T.append(B)
+        cam_T_c0.append(B @ cam_T_c0[-1])
+    rig_centre = np.array([-0.12 * (N - 1) / 2.0, 0.0, 0.0])
+
+    frames, views = [], []
+    attempts = 0
+    while len(frames) < n_frames:
+        attempts += 1
+        if attempts > 200 * n_frames + 1000:
+            raise RuntimeError("could not synthesise enough visible frames")
+        depth = rng.uniform(0.6, 1.5)
+        tilt_axis = rng.normal(size=2)
+        tilt_axis = np.array([tilt_axis[0], tilt_axis[1], 0.0]) / np.linalg.norm(tilt_axis)
+        tilt = np.deg2rad(rng.uniform(0, 35))
+        roll = np.deg2rad(rng.uniform(-180, 180))
+        R = rotvec(tilt_axis * tilt) @ rotvec(np.array([0, 0, roll]))
+        centre = rig_centre + np.array([rng.uniform(-0.15, 0.15), rng.uniform(-0.15, 0.15), depth])
+        T_c0_t = np.eye(4)
+        T_c0_t[:3, :3] = R
+        T_c0_t[:3, 3] = centre - R @ tcen
+        fviews = []
+        for i in range(N):
+            T = cam_T_c0[i] @ T_c0_t
+            pc = (T[:3, :3] @ target.T).T + T[:3, 3]
+            kp, valid = project(models[i], intr_truth[i], pc)
+            ok = valid & (pc[:, 2] > 0.05) & (kp[:, 0] >= 5) & (kp[:, 0] <= W - 5) & (kp[:, 1] >= 5) & (kp[:, 1] <= H - 5)
+            ids = np.nonzero(ok)[0]
+            if ids.size < min_corners or rng.uniform() > p_view:
+                continue
+            meas = kp[ids] + rng.normal(0.0, noise_px, (ids.size, 2))
+            fviews.append((i, ids, meas))
+        if not fviews:
+            continue
+        frames.append(inv_T(T_c0_t))  # T_f: p_c0 = T_f^-1 P
+        views.append(fviews)
+
+    vf, vc, counts, cid, ys = [], [], [], [], []
+    for f, fv in enumerate(views):
+        for (i, ids, meas) in fv:
+            vf.append(f)
+            vc.append(i)
+            counts.append(ids.size)
+            cid.append(ids)
+            ys.append(meas)
+    st_truth = np.zeros(state_size(N, n_frames))
+    st_truth[: N * MAX_INTR] = intr_truth.reshape(-1)
+    so = N * MAX_INTR
+    for j, B in enumerate(base_T):
+        st_truth[so + POSE * j: so + POSE * (j + 1)] = pose_from_Rt(B[:3, :3], B[:3, 3])
+    so += POSE * (N - 1)
+    for f, T in enumerate(frames):
+        st_truth[so + POSE * f: so + POSE * (f + 1)] = pose_from_Rt(T[:3, :3], T[:3, 3])
+
+    st_init = st_truth.copy()
+    if init_noise:
+        for i, m in enumerate(models):
+            base = i * MAX_INTR
+            if m == PINHOLE_RADTAN:
+                st_init[base + 0: base + 2] *= 1 + 0.02 * rng.normal(size=2)
+                st_init[base + 2: base + 4] += 5.0 * rng.normal(size=2)
+                st_init[base + 4: base + 8] = 0.0
+            elif m in (OMNI_RADTAN, OMNI):
+                st_init[base + 0] *= 1 + 0.02 * rng.normal()
+                st_init[base + 1: base + 3] *= 1 + 0.02 * rng.normal(size=2)
+                st_init[base + 3: base + 5] += 5.0 * rng.normal(size=2)
+                if m == OMNI_RADTAN:
+                    st_init[base + 5: base + 9] = 0.0
+            elif m == EUCM:
+                st_init[base + 0: base + 2] *= 1 + 0.02 * rng.normal(size=2)
+                st_init[base + 2: base + 4] *= 1 + 0.02 * rng.normal(size=2)
+                st_init[base + 4: base + 6] += 5.0 * rng.normal(size=2)
+        so = N * MAX_INTR
+        for k in range(N - 1 + n_frames):
+            o = so + POSE * k
+            T = pose_to_T(st_truth[o: o + POSE])
+            Rn = rotvec(np.deg2rad(1.0) * rng.normal(size=3) / np.sqrt(3)) @ T[:3, :3]
+            tn = T[:3, 3] + 0.01 * rng.normal(size=3) / np.sqrt(3)
+            st_init[o: o + POSE] = pose_from_Rt(Rn, tn)
+    return Problem(
+        cam_model=np.asarray(models, dtype=np.int32), target=target,
+        view_frame=np.asarray(vf, dtype=np.int32), view_cam=np.asarray(vc, dtype=np.int32),
+        view_offset=np.concatenate([[0], np.cumsum(counts)]).astype(np.int32),
+        corner_id=np.concatenate(cid).astype(np.int32), y=np.concatenate(ys, axis=0).astype(np.float64),
+        state_truth=st_truth, state_init=st_init, resolution=resolution, name=name,
+        meta={"seed": seed, "p_view": p_view, "noise_px": noise_px})
+
+
+# BASELINE.json configs; seeds PCG64(20261015 + config_index)
+CONFIGS = {
+    1: dict(models=[PINHOLE_RADTAN], n_frames=50, name="1x pinhole-radtan, 50-frame 6x5 AprilGrid"),
+    2: dict(models=[PINHOLE_RADTAN] * 2, n_frames=500, name="2-cam stereo pinhole-radtan, 500 frames"),
+    3: dict(models=[OMNI_RADTAN, OMNI_RADTAN, EUCM, EUCM], n_frames=1000, name="4-cam omni + EUCM mixed rig, 1000 frames"),
+    4: dict(models=[PINHOLE_RADTAN] * 8, n_frames=2000, name="8-cam pinhole rig, 2000 frames"),
+}
+
+
+def make_config(idx, p_view=1.0, n_frames=None, seed_offset=0, **kw):
+    c = CONFIGS[idx]
+    return make_problem(c["models"], n_frames or c["n_frames"], seed=20261015 + idx + seed_offset,
+                        p_view=p_view, name=c["name"], **kw)

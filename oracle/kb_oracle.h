@@ -1,0 +1,135 @@
+/*
+ * kb_oracle.h -- CPU restatement of the Kalibr2 / aslam_backend Gauss-Newton /
+ * Levenberg-Marquardt hot path over camera ReprojectionError terms.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in kalibr_amd/ (the product) may link,
+ * import or call this code; only tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py use it, as the checker / CPU baseline.
+ *
+ * Pinning: the reference (Eigen/Boost/SuiteSparse C++) cannot be built in this
+ * image.  The restatement is pinned by the reference's own
+ * known-answer table (sm_kinematics/test/QuaternionTests.cpp:44-59), by its
+ * finite-difference Jacobian harnesses (CameraGeometryTestHarness.hpp,
+ * ErrorTermTestHarness.hpp) and by its structural identities
+ * (H = J^T J, rhs = -J^T e: aslam_backend/test/TestOptimizer.cpp:101-120;
+ * solver agreement: LinearSolverTests.cpp:18-63).  See tests/golden/.
+ *
+ * All citations are relative to /root/reference.
+ */
+#ifndef KB_ORACLE_H
+#define KB_ORACLE_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KBO_MAX_INTR 10   /* per-camera intrinsic slot stride in the state */
+#define KBO_POSE 7        /* q (JPL x,y,z,w) + t */
+
+/* camera models (kalibr2/include/kalibr2/CameraModels.hpp:25-133) */
+enum {
+  KBO_PINHOLE_RADTAN = 0, /* PinholeProjection<RadialTangentialDistortion>: fu fv cu cv | k1 k2 p1 p2 */
+  KBO_OMNI_RADTAN = 1,    /* OmniProjection<RadialTangentialDistortion>: xi fu fv cu cv | k1 k2 p1 p2 */
+  KBO_EUCM = 2,           /* ExtendedUnifiedProjection<NoDistortion>: alpha beta fu fv cu cv */
+  KBO_OMNI = 3,           /* OmniProjection<NoDistortion>: xi fu fv cu cv */
+  KBO_NUM_MODELS = 4
+};
+
+typedef struct {
+  int n_cams, n_frames, n_views, n_corners, n_target;
+  const int* cam_model;   /* [n_cams] */
+  const double* target;   /* [n_target][3] target-frame corner coordinates */
+  const int* view_frame;  /* [n_views] */
+  const int* view_cam;    /* [n_views] */
+  const int* view_offset; /* [n_views+1] corner range of each view */
+  const int* corner_id;   /* [n_corners] index into target */
+  const double* y;        /* [n_corners][2] measured keypoints */
+} kbo_problem;
+
+/* Flat state layout (shared with the device path):
+ *   intr  [n_cams][KBO_MAX_INTR]   (projection params then distortion params)
+ *   base  [n_cams-1][7]            baseline B_j = T_{c(j+1), c(j)}  (q, t)
+ *   frame [n_frames][7]            target pose DV T_f (p_c0 = T_f^-1 * P)
+ * Canonical column order of dx / rhs / H:
+ *   [intr cam0 | intr cam1 | ... | B_0 (dphi,dt) | ... | frame 0 (dphi,dt) | ...]
+ * which is the DV insertion order of CalibrateMultiCameraRig
+ * (kalibr2/include/kalibr2/CalibrationTools.hpp:376-428; Optimizer2.cpp:110-124). */
+int kbo_model_nintr(int model);
+int kbo_state_size(int n_cams, int n_frames);
+int kbo_cam_cols(const kbo_problem* P);   /* C = sum nintr + 6 (N-1) */
+int kbo_total_cols(const kbo_problem* P); /* C + 6F */
+
+/* --- sm_kinematics restatements (known-answer tested) --- */
+void kbo_axis_angle2quat(const double a[3], double q[4]);
+void kbo_quat2axis_angle(const double q[4], double a[3]);
+void kbo_update_quat(const double q[4], const double dq[3], double out[4]);
+void kbo_quat2r(const double q[4], double R[9]);
+void kbo_r2quat(const double R[9], double q[4]);
+
+/* --- camera maths: keypoint, dy/dp (2x3), dy/dintrinsics (2 x nintr) --- */
+int kbo_project(int model, const double* intr, const double p[3], double y[2], double Jp[6], double Ji[2 * KBO_MAX_INTR]);
+
+/* --- one ReprojectionError term through the expression chain --- */
+/* J out: dense row block 2 x total_cols (caller zeroes), e out: y - yhat. returns chi2. */
+double kbo_term_dense(const kbo_problem* P, const double* state, int view, int k, double e[2], double* Jrow, int ncols);
+
+/* --- cost (LinearSystemSolver::evaluateError) --- */
+double kbo_eval_cost(const kbo_problem* P, const double* state, int nthreads);
+
+/* --- arrow normal equations --- */
+typedef struct {
+  int C, F;
+  double* Hff; /* [F][36] */
+  double* Hfc; /* [F][6*C] row-major 6 x C */
+  double* Hcc; /* [C*C] */
+  double* gf;  /* [F][6]  rhs = -J^T e */
+  double* gc;  /* [C] */
+  double cost;
+} kbo_arrow;
+
+/* CCS J^T (CompressedColumnJacobianTransposeBuilder restatement) */
+typedef struct kbo_jt kbo_jt;
+kbo_jt* kbo_jt_create(const kbo_problem* P);
+void kbo_jt_destroy(kbo_jt* jt);
+/* threaded per-term evaluation into J^T values + _e = -e (buildSystem) then rhs = J^T _e */
+void kbo_jt_build(kbo_jt* jt, const double* state, int nthreads, double* rhs);
+/* J^T J accumulated into the arrow blocks (what CHOLMOD's A A^T forms) */
+void kbo_jt_normal_arrow(kbo_jt* jt, int nthreads, kbo_arrow* A);
+long long kbo_jt_nnz(const kbo_jt* jt);
+
+/* Build straight into arrow blocks (same numbers, no CCS) */
+void kbo_build_arrow(const kbo_problem* P, const double* state, int nthreads, kbo_arrow* A);
+
+/* Solve (J^T J + lambda^2 I) dx = rhs  (LinearSystemSolver.hpp:33-39: square of the conditioner).
+ * Schur onto the camera block.  returns 1 on success, 0 on non-PD. */
+int kbo_arrow_solve(const kbo_arrow* A, double conditioner, int nthreads, double* dx);
+/* Dense reference solve on the full (small) system, for cross-checking the Schur path. */
+int kbo_dense_solve(const kbo_arrow* A, double conditioner, double* dx);
+/* Partial Schur quantities of a frame range (for sharding): S_part (C*C), b_part (C) */
+void kbo_arrow_schur_partial(const kbo_arrow* A, double conditioner, int f0, int f1, double* S_part, double* b_part, int* ok);
+
+/* Optimizer2::applyStateUpdate / revert */
+double kbo_apply_update(const kbo_problem* P, double* state, const double* dx);
+
+/* Optimizer2::optimize with LM (LevenbergMarquardtTrustRegionPolicy) or GN */
+typedef struct {
+  int policy;      /* 0 = levenberg_marquardt, 1 = gauss_newton */
+  double lambda0;  /* LM lambdaInit */
+  int max_iterations;
+  double eps_x, eps_j;
+  int nthreads;
+} kbo_options;
+typedef struct {
+  double J_start, J_final, dx_final, dj_final;
+  int iterations, failed_iterations, linear_solver_failure;
+} kbo_srv;
+/* trace (optional, may be NULL): per loop pass: [J_after, lambda, deltaX, accepted] */
+int kbo_optimize(const kbo_problem* P, double* state, const kbo_options* o, kbo_srv* srv, double* trace, int trace_cap);
+
+/* CPU baseline: time n_iter GN iterations (build + solve + update + cost), returns seconds. */
+double kbo_time_gn(const kbo_problem* P, double* state, int n_iter, int nthreads);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,214 @@
+"""ctypes wrapper of the CPU restatement (oracle/kb_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py -- never by the product package kalibr_amd/.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = os.path.join(_HERE, "_build", "libkb_oracle.so")
+_lib = None
+
+dp = C.POINTER(C.c_double)
+ip = C.POINTER(C.c_int)
+
+
+class _Problem(C.Structure):
+    _fields_ = [("n_cams", C.c_int), ("n_frames", C.c_int), ("n_views", C.c_int), ("n_corners", C.c_int),
+                ("n_target", C.c_int), ("cam_model", ip), ("target", dp), ("view_frame", ip), ("view_cam", ip),
+                ("view_offset", ip), ("corner_id", ip), ("y", dp)]
+
+
+class _Arrow(C.Structure):
+    _fields_ = [("C", C.c_int), ("F", C.c_int), ("Hff", dp), ("Hfc", dp), ("Hcc", dp), ("gf", dp), ("gc", dp),
+                ("cost", C.c_double)]
+
+
+class _Options(C.Structure):
+    _fields_ = [("policy", C.c_int), ("lambda0", C.c_double), ("max_iterations", C.c_int), ("eps_x", C.c_double),
+                ("eps_j", C.c_double), ("nthreads", C.c_int)]
+
+
+class _Srv(C.Structure):
+    _fields_ = [("J_start", C.c_double), ("J_final", C.c_double), ("dx_final", C.c_double), ("dj_final", C.c_double),
+                ("iterations", C.c_int), ("failed_iterations", C.c_int), ("linear_solver_failure", C.c_int)]
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB):
+            build()
+        L = C.CDLL(_LIB)
+        L.kbo_eval_cost.restype = C.c_double
+        L.kbo_term_dense.restype = C.c_double
+        L.kbo_apply_update.restype = C.c_double
+        L.kbo_time_gn.restype = C.c_double
+        L.kbo_jt_create.restype = C.c_void_p
+        L.kbo_jt_destroy.argtypes = [C.c_void_p]
+        L.kbo_jt_build.argtypes = [C.c_void_p, dp, C.c_int, dp]
+        L.kbo_jt_normal_arrow.argtypes = [C.c_void_p, C.c_int, C.POINTER(_Arrow)]
+        L.kbo_jt_nnz.argtypes = [C.c_void_p]
+        L.kbo_jt_nnz.restype = C.c_longlong
+        L.kbo_arrow_solve.argtypes = [C.POINTER(_Arrow), C.c_double, C.c_int, dp]
+        L.kbo_dense_solve.argtypes = [C.POINTER(_Arrow), C.c_double, dp]
+        L.kbo_arrow_schur_partial.argtypes = [C.POINTER(_Arrow), C.c_double, C.c_int, C.c_int, dp, dp, ip]
+        _lib = L
+    return _lib
+
+
+def _d(a):
+    return a.ctypes.data_as(dp)
+
+
+def _i(a):
+    return a.ctypes.data_as(ip)
+
+
+class Oracle:
+    """Holds one problem (arrays kept alive) and exposes the restated reference path."""
+
+    def __init__(self, prob):
+        self.prob = prob
+        self._keep = dict(
+            cam_model=np.ascontiguousarray(prob.cam_model, dtype=np.int32),
+            target=np.ascontiguousarray(prob.target, dtype=np.float64),
+            view_frame=np.ascontiguousarray(prob.view_frame, dtype=np.int32),
+            view_cam=np.ascontiguousarray(prob.view_cam, dtype=np.int32),
+            view_offset=np.ascontiguousarray(prob.view_offset, dtype=np.int32),
+            corner_id=np.ascontiguousarray(prob.corner_id, dtype=np.int32),
+            y=np.ascontiguousarray(prob.y, dtype=np.float64))
+        k = self._keep
+        self.P = _Problem(prob.n_cams, prob.n_frames, prob.n_views, prob.n_corners, k["target"].shape[0],
+                          _i(k["cam_model"]), _d(k["target"]), _i(k["view_frame"]), _i(k["view_cam"]),
+                          _i(k["view_offset"]), _i(k["corner_id"]), _d(k["y"]))
+        self.C = prob.cam_cols
+        self.ncols = prob.total_cols
+
+    # -- primitives --
+    def cost(self, state, nthreads=1):
+        st = np.ascontiguousarray(state, dtype=np.float64)
+        return lib().kbo_eval_cost(C.byref(self.P), _d(st), nthreads)
+
+    def term_dense(self, state, view, k):
+        st = np.ascontiguousarray(state, dtype=np.float64)
+        J = np.zeros((2, self.ncols))
+        e = np.zeros(2)
+        chi2 = lib().kbo_term_dense(C.byref(self.P), _d(st), view, k, _d(e), _d(J), self.ncols)
+        return chi2, e, J
+
+    def dense_jacobian(self, state):
+        """Full J (2Nc x ncols) and e for small problems (test use)."""
+        rows = []
+        es = []
+        for v in range(self.prob.n_views):
+            nk = self.prob.view_offset[v + 1] - self.prob.view_offset[v]
+            for k in range(nk):
+                _, e, J = self.term_dense(state, v, k)
+                rows.append(J)
+                es.append(e)
+        return np.concatenate(rows, axis=0), np.concatenate(es)
+
+    def arrow(self, state, nthreads=1, via_ccs=True):
+        """Normal-equation blocks (J^T J, rhs = -J^T e) in canonical order."""
+        F, Cc = self.prob.n_frames, self.C
+        out = dict(Hff=np.zeros((F, 6, 6)), Hfc=np.zeros((F, 6, Cc)), Hcc=np.zeros((Cc, Cc)), gf=np.zeros((F, 6)),
+                   gc=np.zeros(Cc))
+        A = _Arrow(Cc, F, _d(out["Hff"]), _d(out["Hfc"]), _d(out["Hcc"]), _d(out["gf"]), _d(out["gc"]), 0.0)
+        st = np.ascontiguousarray(state, dtype=np.float64)
+        rhs = np.zeros(self.ncols)
+        jt = lib().kbo_jt_create(C.byref(self.P))
+        lib().kbo_jt_build(jt, _d(st), nthreads, _d(rhs))
+        lib().kbo_jt_normal_arrow(jt, nthreads, C.byref(A))
+        out["nnz"] = lib().kbo_jt_nnz(jt)
+        lib().kbo_jt_destroy(jt)
+        out["cost"] = A.cost
+        out["rhs"] = rhs
+        out["_A"] = A
+        return out
+
+    def solve(self, arrow, conditioner=0.0, nthreads=1, dense=False):
+        dx = np.zeros(self.ncols)
+        if dense:
+            ok = lib().kbo_dense_solve(C.byref(arrow["_A"]), conditioner, _d(dx))
+        else:
+            ok = lib().kbo_arrow_solve(C.byref(arrow["_A"]), conditioner, nthreads, _d(dx))
+        return bool(ok), dx
+
+    def schur_partial(self, arrow, conditioner, f0, f1):
+        S = np.zeros((self.C, self.C))
+        b = np.zeros(self.C)
+        ok = C.c_int(1)
+        lib().kbo_arrow_schur_partial(C.byref(arrow["_A"]), conditioner, f0, f1, _d(S), _d(b), C.byref(ok))
+        return bool(ok.value), S, b
+
+    def apply_update(self, state, dx):
+        st = np.array(state, dtype=np.float64, copy=True)
+        dX = lib().kbo_apply_update(C.byref(self.P), _d(st), _d(np.ascontiguousarray(dx, dtype=np.float64)))
+        return st, dX
+
+    def optimize(self, state, policy="lm", lambda0=10.0, max_iterations=200, eps_x=1e-3, eps_j=1.0, nthreads=1,
+                 trace_cap=1000):
+        st = np.array(state, dtype=np.float64, copy=True)
+        o = _Options(0 if policy == "lm" else 1, lambda0, max_iterations, eps_x, eps_j, nthreads)
+        srv = _Srv()
+        tr = np.zeros((trace_cap, 4))
+        n = lib().kbo_optimize(C.byref(self.P), _d(st), C.byref(o), C.byref(srv), _d(tr), trace_cap)
+        res = {f: getattr(srv, f) for f, _ in _Srv._fields_}
+        res["trace"] = tr[:n].copy()
+        return st, res
+
+    def time_gn(self, state, n_iter, nthreads):
+        st = np.array(state, dtype=np.float64, copy=True)
+        return lib().kbo_time_gn(C.byref(self.P), _d(st), n_iter, nthreads)
+
+
+def axis_angle2quat(a):
+    q = np.zeros(4)
+    lib().kbo_axis_angle2quat(_d(np.ascontiguousarray(a, dtype=np.float64)), _d(q))
+    return q
+
+
+def quat2axis_angle(q):
+    a = np.zeros(3)
+    lib().kbo_quat2axis_angle(_d(np.ascontiguousarray(q, dtype=np.float64)), _d(a))
+    return a
+
+
+def update_quat(q, dq):
+    out = np.zeros(4)
+    lib().kbo_update_quat(_d(np.ascontiguousarray(q, dtype=np.float64)), _d(np.ascontiguousarray(dq, dtype=np.float64)),
+                          _d(out))
+    return out
+
+
+def quat2r(q):
+    R = np.zeros(9)
+    lib().kbo_quat2r(_d(np.ascontiguousarray(q, dtype=np.float64)), _d(R))
+    return R.reshape(3, 3)
+
+
+def r2quat(R):
+    q = np.zeros(4)
+    lib().kbo_r2quat(_d(np.ascontiguousarray(R, dtype=np.float64).reshape(-1)), _d(q))
+    return q
+
+
+def project(model, intr, p):
+    """returns (valid, y[2], Jp[2,3], Ji[2,MAX_INTR])."""
+    y = np.zeros(2)
+    Jp = np.zeros(6)
+    Ji = np.zeros(20)
+    ok = lib().kbo_project(int(model), _d(np.ascontiguousarray(intr, dtype=np.float64)),
+                           _d(np.ascontiguousarray(p, dtype=np.float64)), _d(y), _d(Jp), _d(Ji))
+    return bool(ok), y, Jp.reshape(2, 3), Ji.reshape(2, 10)
