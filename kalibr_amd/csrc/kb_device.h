@@ -6,10 +6,11 @@
 //   view_off uint32  [V+1]; view_frame int32 [V]; view_cam int32 [V]; frame_vcam int32 [F][N] (-1 = none)
 //   state    [2][S]                ping-pong design-variable buffers, ctrl->cur = accepted one
 //   Hff [F][36], Hfc [F][6][C], gf [F][6]     arrow blocks written by k_build
-//   campart [nblk][N][136]         per-block per-camera partial sums (16x16 upper)
-//   Lf [F][36], Yf [F][6][C], zf [F][6]       Schur factors written by k_schur
-//   schurpart [nblk][W]            per-block sum Y^T Y (upper packed) | Y^T z, W = C(C+1)/2 + C
-//   redA_local = [camsum N*136 | schursum W] (all-reduced into redA when sharded)
+//   Lf [F][36], Yf [F][6][C], zf [F][6]       frame Schur factors (k_build fused / k_schur)
+//   part [nblk][Wtot]              per-block partials: per-camera 16x16 upper sums (N*136) |
+//                                  sum Y^T Y upper (C(C+1)/2) | sum Y^T z (C) | #non-PD frames (1)
+//   part8 [8][Wtot]                stage-1 column sums of part (k_colsum), finished by the consumer
+//   bpart [nblk_bs][4]             k_backsub_cost: cost, max|dx|, dx.dx, dx.rhs per block
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -31,10 +32,15 @@ struct KbOpts {
   double lambda_init, eps_x, eps_j;
 };
 
+constexpr int kColsumRows = 8;  // stage-1 row splits of the block partial reduction
+
 struct KbDev {
   int N, F, V, NC, C, ncols, S;
   int off_base, off_frame;
   int gframes, nblk, nblk_bs, nblk_cost;
+  int nsplit, wpb;   // k_build: waves per block = N * nsplit
+  int W, Wtot;       // W = C(C+1)/2 + C ; Wtot = N*136 + W + 1
+  int npart;         // rows of psum the consumers add up (8 locally, 1 after an all-reduce)
   int trace_cap;
   double host_lambda;  // conditioner for the per-call (non-gated) path
   int model[KB_MAX_CAMS], nintr[KB_MAX_CAMS], col_intr[KB_MAX_CAMS], col_base[KB_MAX_CAMS];
@@ -51,41 +57,32 @@ struct KbDev {
   double* camL;  // [N][12]
   double* camK;  // [N][N][36]
   double *Hff, *Hfc, *gf;
-  double* campart;
-  double* camsum_local;  // colsum output (this rank)
-  double* camsum;        // reduced over ranks (aliases camsum_local on one GPU)
-  double *Hcc, *gc, *cost_build;
   double *Lf, *Yf, *zf;
-  double* schurpart;
-  double* schursum_local;
-  double* schursum;
+  double* part;   // [nblk][Wtot]
+  double* part8;  // [8][Wtot] (this rank)
+  double* psum;   // consumer view: part8 (npart 8) or the all-reduced [Wtot] (npart 1)
+  double *Hcc, *gc, *cost_build;
   double *dx, *rhs;
-  double* statpart;
-  double* camstat;   // [3]
-  double* costpart;
-  double* red_local; // [4]
-  double* red;       // [4] (reduced)
+  double* bpart;     // [nblk_bs][4]
+  double* camstat;   // [4]
+  double* costpart;  // [nblk_cost]
+  double* red_local; // [4]: cost, dx.dx, dx.rhs, max|dx|
+  double* red;       // [4] (all-reduced; aliases red_local on one GPU)
   double* trace;
   KbCtrl* ctrl;
 };
 
 // 16x16 upper-packed helpers (row-major upper: a <= b)
 __host__ __device__ __forceinline__ int d16_index(int a, int b) { return a * 16 - a * (a - 1) / 2 + (b - a); }
-__device__ __forceinline__ int d16_row(int e) {
-  int a = 0;
-  while (e >= 16 - a) {
-    e -= 16 - a;
-    ++a;
+__device__ __forceinline__ void d16_rowcol(int e, int& a, int& b) {
+  int r = 0;
+  while (e >= 16 - r) {
+    e -= 16 - r;
+    ++r;
   }
-  return a;
+  a = r;
+  b = r + e;
 }
-__device__ __forceinline__ int d16_col(int e) {
-  int a = 0;
-  while (e >= 16 - a) {
-    e -= 16 - a;
-    ++a;
-  }
-  return a + e;
-}
+__host__ __device__ __forceinline__ int upper_index(int a, int b, int n) { return a * n - a * (a - 1) / 2 + (b - a); }
 
 }  // namespace kb

@@ -1,22 +1,25 @@
 // kb_kernels.hip -- CDNA4 (gfx950) kernels of one Gauss-Newton / Levenberg-Marquardt pass
 // over Kalibr2 ReprojectionError terms, FP64 throughout.
 //
-//   k_prep       camera-only chain quantities L_i = B_{i-1}..B_0 and K_{i,j} (frame independent)
-//   k_build      K1+K2+K3: per view, residual + 2x16 Jacobian rows staged in LDS, local
-//                16x16 [J|-e]^T[J|-e] by v_mfma_f64_16x16x4; per frame the 6-D adjoint expansion into
-//                H_ff, H_fc, g_f; per camera deterministic partial sums for the camera block
-//   k_colsum     deterministic column sums of per-block partials
-//   k_camexpand  camera block H_cc, g_c from the per-camera sums (K_{i,j} expansion)
-//   k_schur      K4a: per frame chol(H_ff + lambda^2 I), Y = L^-1 H_fc, z = L^-1 g_f, sum Y^T Y
-//   k_solve      K4b: dense Cholesky of S = H_cc + lambda^2 I - sum Y^T Y, camera dx, camera update
-//   k_backsub    K4c+K5: frame dx = L^-T (z - Y dx_c), frame pose update, step statistics
-//   k_cost       K1 (cost only) on either state buffer
-//   k_pol_*      the Optimizer2 / trust-region state machine, device resident
+// One optimizer pass (device-resident loop, every kernel gated on ctrl):
+//   k_pre        policy prelude (while-condition, lambda schedule) + camera chain L_i, K_{i,j}
+//   k_build      K1+K2+K3 (+K4a fused): per view residual + 2x16 Jacobian rows staged in LDS,
+//                local 16x16 [J|-e]^T[J|-e] on v_mfma_f64_16x16x4; per frame the 6-D adjoint expansion
+//                into H_ff, H_fc, g_f and, fused, chol(H_ff + lambda^2 I), Y = L^-1 H_fc, z = L^-1 g_f,
+//                block partials of sum Y^T Y, Y^T z and of the per-camera local sums
+//   k_schur      K4a alone (LM passes that do not rebuild: lambda changed only)
+//   k_colsum     stage-1 deterministic column sums of the block partials (8 row splits)
+//   k_solve      K4b: camera block H_cc / g_c expansion, S = H_cc + lambda^2 I - sum Y^T Y, LDL^T,
+//                camera dx, camera DV update
+//   k_backsub    K4c+K5(+K1): frame dx = L^-T (z - Y dx_c), pose update, cost of the frame's views at the
+//                new state, step statistics
+//   k_post       fixed-order reduction of the per-block cost / statistics + accept/revert policy
 //
 // Reference data flow replaced (paths relative to the reference repository):
 //   LinearSystemSolver.cpp:12-92, CompressedColumnJacobianTransposeBuilder(impl).hpp:19-101,
 //   SparseCholeskyLinearSystemSolver.cpp:39-89, Cholmod(impl).hpp:180-399, Optimizer2.cpp:183-318,
-//   LevenbergMarquardtTrustRegionPolicy.cpp:50-113, GaussNewtonTrustRegionPolicy.cpp:18-39.
+//   TrustRegionPolicy.cpp:39-57, LevenbergMarquardtTrustRegionPolicy.cpp:50-113,
+//   GaussNewtonTrustRegionPolicy.cpp:18-39.
 #include "kb_device.h"
 
 namespace kb {
@@ -25,9 +28,11 @@ typedef double v4d __attribute__((ext_vector_type(4)));
 
 #define KB_WAVE_SYNC() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
 
+constexpr int XS = 17;       // LDS row stride (doubles) of the 64 x 16 Jacobian-row tile
+constexpr int kMaxM = 24;    // largest Schur-sum entries per thread: (W + 1) <= M * blockDim
+
 // ---------------------------------------------------------------------------------------------
-// camera chain: L_i (R|t, 12 doubles) and K_{i,j} = boxTimes(B_{i-1}..B_{j+1}) * M(t_Bj)
-// (TransformationExpressionNode.cpp:61-72 chain of boxTimes; TransformationBasic.cpp:49-66 M(t))
+// rigid-transform helpers
 // ---------------------------------------------------------------------------------------------
 __device__ __forceinline__ void pose_rt(const double* pose, double* R, double* t) {
   quat2r(pose, R);
@@ -42,17 +47,46 @@ __device__ __forceinline__ void rt_mul(const double* R1, const double* t1, const
 #pragma unroll
   for (int r = 0; r < 3; ++r) {
 #pragma unroll
-    for (int c = 0; c < 3; ++c) R[r * 3 + c] = R1[r * 3 + 0] * R2[0 * 3 + c] + R1[r * 3 + 1] * R2[1 * 3 + c] + R1[r * 3 + 2] * R2[2 * 3 + c];
+    for (int c = 0; c < 3; ++c)
+      R[r * 3 + c] = R1[r * 3 + 0] * R2[0 * 3 + c] + R1[r * 3 + 1] * R2[1 * 3 + c] + R1[r * 3 + 2] * R2[2 * 3 + c];
     t[r] = R1[r * 3 + 0] * t2[0] + R1[r * 3 + 1] * t2[1] + R1[r * 3 + 2] * t2[2] + t1[r];
   }
 }
 
+// T_f^-1 of a pose DV
+__device__ __forceinline__ void pose_inverse(const double* fp, double* Ri, double* ti) {
+  double Rf[9];
+  quat2r(fp, Rf);
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+#pragma unroll
+    for (int cc = 0; cc < 3; ++cc) Ri[r * 3 + cc] = Rf[cc * 3 + r];
+    ti[r] = -(Ri[r * 3 + 0] * fp[4] + Ri[r * 3 + 1] * fp[5] + Ri[r * 3 + 2] * fp[6]);
+  }
+}
+
+// T_cam_w = B_{cam-1} .. B_0 T_f^-1 computed from a state vector (cost passes, where the chain is new)
+__device__ __forceinline__ void cam_from_state(const KbDev& d, const double* s, int cam, const double* fp, double* R,
+                                               double* t) {
+  pose_inverse(fp, R, t);
+  for (int j = 0; j < cam; ++j) {
+    double RB[9], tB[3], R2[9], t2[3];
+    pose_rt(s + d.off_base + 7 * j, RB, tB);
+    rt_mul(RB, tB, R, t, R2, t2);
+#pragma unroll
+    for (int q = 0; q < 9; ++q) R[q] = R2[q];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) t[q] = t2[q];
+  }
+}
+
 // G = -boxTimes(T_q) M(t_m) = [[R [t_m]x + [t_q]x R, -R], [-R, 0]]  (6x6, row-major), entry (a,b).
-// Used with T_q = T_cam_w, t_m = t_f for the frame DV and, negated, for K_{i,j}.
+// boxTimes: sm_kinematics/src/transformations.cpp:132-141; M(t): TransformationBasic.cpp:49-66
+// (rotation DV chain [-[t]x; I], translation DV chain [I; 0]); the inverse node contributes
+// -boxTimes(T^-1) (TransformationExpressionNode.cpp:92-101).  With T_q = T_cam_w this is the chain of the
+// frame DV; -G(Q, t_Bj) with Q = B_{i-1}..B_{j+1} is the chain of baseline B_j.
 __device__ __forceinline__ double chain_entry(const double* R, const double* tq, const double* tm, int a, int b) {
   if (a < 3 && b < 3) {
-    // (R [tm]x)[a][b] + ([tq]x R)[a][b]
-    // [x]x = [[0,-x2,x1],[x2,0,-x0],[-x1,x0,0]]
     double s;
     const double r0 = R[a * 3 + 0], r1 = R[a * 3 + 1], r2 = R[a * 3 + 2];
     if (b == 0) s = r1 * tm[2] - r2 * tm[1];
@@ -70,10 +104,113 @@ __device__ __forceinline__ double chain_entry(const double* R, const double* tq,
   return 0.0;
 }
 
-__global__ void k_prep(KbDev d, int gate) {
+// ---------------------------------------------------------------------------------------------
+// policy: while-condition (Optimizer2.cpp:215-219) + TrustRegionPolicy::solveSystem prelude
+// (TrustRegionPolicy.cpp:39-52) + LM lambda schedule (LevenbergMarquardtTrustRegionPolicy.cpp:50-84)
+// or GN (build every pass, no conditioner: GaussNewtonTrustRegionPolicy.cpp:25-29).
+// ---------------------------------------------------------------------------------------------
+__device__ void pol_pre(KbCtrl* c) {
+  const bool cont = c->iterations < c->max_iterations && c->failed_iterations < c->max_iterations &&
+                    ((c->deltaX > c->eps_x && fabs(c->deltaJ) > c->eps_j) || c->lin_fail);
+  if (!cont) {
+    c->done = 1;
+    return;
+  }
+  const double J = c->J;
+  if (c->prev_failed) {
+    c->pol_J = J;
+  } else {
+    c->pol_pJ = c->last_succ;
+    c->last_succ = J;
+    c->pol_J = J;
+  }
+  c->solve_ok = 1;
+  if (c->policy == 0) {
+    if (c->first) {
+      c->do_build = 1;
+    } else {
+      const double d2 = c->lambda * c->dxdx + c->dxrhs;  // dx^T (lambda dx + rhs), getLmRho (:107-113)
+      const double rho = (c->pol_pJ - c->pol_J) / d2;
+      if (c->prev_failed) {
+        c->mu *= 2;
+        c->lambda *= c->mu;
+        c->do_build = 0;
+      } else if (rho <= 0) {
+        c->mu *= 10;
+        c->lambda *= c->mu;
+        c->do_build = 0;
+      } else {
+        c->do_build = 1;
+        if (c->lambda > 1e-16) {
+          const double gamma = 3.0, beta = 2.0;
+          const double u1 = 1 / gamma;
+          const double u2 = 1 - (beta - 1) * pow((2 * rho - 1), 3.0);
+          if (u1 > u2)
+            c->lambda *= u1;
+          else
+            c->lambda *= u2;
+          c->mu = beta;
+        } else {
+          c->lambda = 1e-15;
+        }
+      }
+    }
+  } else {
+    c->do_build = 1;
+  }
+  c->first = 0;
+}
+
+// accept / revert (Optimizer2.cpp:221-259); red = [cost, dx.dx, dx.rhs, max|dx|] (all ranks)
+__device__ void pol_post(KbCtrl* c, const KbDev& d, const double* red) {
+  double J = 0.0, dX = c->deltaX;
+  int accepted = 0;
+  if (!c->solve_ok) {
+    c->prev_failed = 1;
+    c->lin_fail = 1;
+    c->failed_iterations++;
+    J = NAN;
+  } else {
+    J = red[0];
+    dX = red[3];
+    c->dxdx = red[1];
+    c->dxrhs = red[2];
+    c->deltaX = dX;
+    c->J = J;
+    c->deltaJ = c->p_J - J;
+    if (c->policy == 0 && c->deltaJ < 0.0) {  // regression: revertLastStateUpdate (state[cur] untouched)
+      c->failed_iterations++;
+      c->prev_failed = 1;
+    } else {
+      c->cur = 1 - c->cur;
+      c->p_J = J;
+      c->prev_failed = 0;
+      accepted = 1;
+    }
+    c->iterations++;
+  }
+  if (c->n_trace < d.trace_cap) {
+    double* tr = d.trace + 4 * c->n_trace;
+    tr[0] = J;
+    tr[1] = c->lambda;
+    tr[2] = dX;
+    tr[3] = accepted;
+    c->n_trace++;
+  }
+  c->passes++;
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_pre: [policy prelude] + camera chain L_i (R|t) and K_{i,j} (one block)
+// ---------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_pre(KbDev d, int gate) {
   KbCtrl* c = d.ctrl;
-  if (gate && (c->done || !c->do_build)) return;
-  // one block; thread t < N: L_t ; threads over (i,j,entry) for K
+  if (gate) {
+    if (c->done) return;
+    if (threadIdx.x == 0) pol_pre(c);
+    __syncthreads();
+    if (c->done || !c->do_build) return;
+  }
   __shared__ double sR[KB_MAX_CAMS][9], st[KB_MAX_CAMS][3];  // baseline B_j
   __shared__ double LR[KB_MAX_CAMS][9], Lt[KB_MAX_CAMS][3];
   const double* s = d.state + (size_t)c->cur * d.S;
@@ -89,8 +226,6 @@ __global__ void k_prep(KbDev d, int gate) {
       for (int q = 0; q < 3; ++q) d.camL[i * 12 + 9 + q] = Lt[i][q];
     }
   }
-  __syncthreads();
-  // K_{i,j} for j < i: Q = B_{i-1}..B_{j+1} (identity when j = i-1); K = -G(Q, t_Bj)
   for (int idx = threadIdx.x; idx < N * N * 36; idx += blockDim.x) {
     const int e = idx % 36, ij = idx / 36, i = ij / N, j = ij % N;
     double val = 0.0;
@@ -108,226 +243,394 @@ __global__ void k_prep(KbDev d, int gate) {
   }
 }
 
-// ---------------------------------------------------------------------------------------------
-// k_build: one block = a group of frames, one wave per camera slot (cameras w, w+WPB, ...).
-// ---------------------------------------------------------------------------------------------
-constexpr int XS = 17;  // LDS row stride (doubles) of the 64 x 16 Jacobian-row tile
+// in-place 6x6 Cholesky (lower) in LDS, by one thread; returns 0 if not PD
+__device__ __forceinline__ int chol6(double* L) {
+  int ok = 1;
+  for (int j = 0; j < 6; ++j) {
+    double dd = L[j * 6 + j];
+    for (int k = 0; k < j; ++k) dd -= L[j * 6 + k] * L[j * 6 + k];
+    if (!(dd > 0.0)) ok = 0;
+    dd = sqrt(dd);
+    L[j * 6 + j] = dd;
+    for (int i = j + 1; i < 6; ++i) {
+      double s2 = L[i * 6 + j];
+      for (int k = 0; k < j; ++k) s2 -= L[i * 6 + k] * L[j * 6 + k];
+      L[i * 6 + j] = s2 / dd;
+    }
+  }
+  return ok;
+}
 
-__global__ void __launch_bounds__(256) k_build(KbDev d, int gate) {
+// Schur-sum entries of this thread: sum Y^T Y (upper packed) and Y^T z
+template <int M>
+__device__ __forceinline__ void schur_accumulate(const int C, const int Wt, const int W, const double* Y,
+                                                 const double* z, const int* ab, double* acc) {
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    const int e = threadIdx.x + blockDim.x * m;
+    if (e < Wt) {
+      const int a = ab[m] >> 16, b = ab[m] & 0xffff;
+      double s2 = 0.0;
+#pragma unroll
+      for (int r = 0; r < 6; ++r) s2 += Y[r * C + a] * Y[r * C + b];
+      acc[m] += s2;
+    } else if (e < W) {
+      const int a = e - Wt;
+      double s2 = 0.0;
+#pragma unroll
+      for (int r = 0; r < 6; ++r) s2 += Y[r * C + a] * z[r];
+      acc[m] += s2;
+    }
+  }
+}
+
+// Y = L^-1 H_fc (thread per column), z = L^-1 g_f (last thread); stored to LDS and HBM
+__device__ __forceinline__ void schur_forward(const KbDev& d, int f, const double* L, const double* Hfc_lds,
+                                              const double* g_lds, double* Y, double* z) {
+  const int C = d.C, t = threadIdx.x;
+  if (t < C) {
+    double yv[6];
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+      double s2 = Hfc_lds ? Hfc_lds[r * C + t] : d.Hfc[((size_t)f * 6 + r) * C + t];
+#pragma unroll
+      for (int k = 0; k < r; ++k) s2 -= L[r * 6 + k] * yv[k];
+      yv[r] = s2 / L[r * 6 + r];
+      Y[r * C + t] = yv[r];
+      d.Yf[((size_t)f * 6 + r) * C + t] = yv[r];
+    }
+  } else if (t == (int)blockDim.x - 1) {
+    double zv[6];
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+      double s2 = g_lds ? g_lds[r] : d.gf[(size_t)f * 6 + r];
+#pragma unroll
+      for (int k = 0; k < r; ++k) s2 -= L[r * 6 + k] * zv[k];
+      zv[r] = s2 / L[r * 6 + r];
+      z[r] = zv[r];
+      d.zf[(size_t)f * 6 + r] = zv[r];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_build: one block = a group of frames; waves = N * nsplit, wave w -> camera w % N, corner split w / N.
+// ---------------------------------------------------------------------------------------------
+template <int M>
+__global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
   KbCtrl* c = d.ctrl;
   if (gate && (c->done || !c->do_build)) return;
   extern __shared__ __attribute__((aligned(16))) double sm[];
-  const int WPB = blockDim.x >> 6;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int N = d.N, C = d.C;
-  double* Xw = sm + wave * 64 * XS;                 // [64][XS]
-  double* Hw = sm + WPB * 64 * XS + wave * 256;     // per-wave local 16x16
-  double* Ww = sm + WPB * 64 * XS + WPB * 256 + wave * 64;  // wave scratch: R(9) t(3) tf(3) G(36)
-  double* camsum = sm + WPB * 64 * XS + WPB * 256 + WPB * 64;  // [N][256]
-  double* Pv = camsum + N * 256;                    // [N][36]
-  double* dH = Pv + N * 36;                         // [N][36]
-  double* dg = dH + N * 36;                         // [N][8]
+  const int N = d.N, C = d.C, WPB = d.wpb, NS = d.nsplit;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, nth = blockDim.x;
+  double* Xw = sm + wave * 64 * XS;
+  double* Hw = sm + WPB * 64 * XS;   // [WPB][256] per-wave partial local Hessians
+  double* Hv = Hw + WPB * 256;       // [N][256] per-view local Hessian of the current frame
+  double* camsum = Hv + N * 256;     // [N][256] per-camera sums over the block's frames
+  double* Wv = camsum + N * 256;     // [N][64]: R(9) t(3) tf(3) | G(36) at +16
+  double* Pv = Wv + N * 64;          // [N][36]  G^T H_dd
+  double* dH = Pv + N * 36;          // [N][36]  G^T H_dd G
+  double* dg = dH + N * 36;          // [N][8]   G^T g_d
+  double* Fh = dg + N * 8;           // frame H_ff [36]
+  double* Fg = Fh + 36;              // frame g_f [8]
+  double* Fc = Fg + 8;               // frame H_fc [6][C]
+  double* L = Fc + 6 * C;            // [36]
+  double* Y = L + 36;                // [6][C]
+  double* z = Y + 6 * C;             // [8]
+  __shared__ int okl;
   const double* s = d.state + (size_t)c->cur * d.S;
-
-  for (int q = threadIdx.x; q < N * 256; q += blockDim.x) camsum[q] = 0.0;
+  const double lam = gate ? c->lambda : d.host_lambda;
+  const double lam2 = lam * lam;
+  const int W = d.W, Wt = W - C;
+  double acc[M];
+  int ab[M];
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    acc[m] = 0.0;
+    const int e = threadIdx.x + nth * m;
+    ab[m] = (fuse && e < Wt) ? d.tri[e] : 0;
+  }
+  if (threadIdx.x == 0) okl = 1;
+  for (int q = threadIdx.x; q < N * 256; q += nth) camsum[q] = 0.0;
   __syncthreads();
 
-  const int f0 = blockIdx.x * d.gframes;
-  const int f1 = min(d.F, f0 + d.gframes);
+  const int f0 = blockIdx.x * d.gframes, f1 = min(d.F, f0 + d.gframes);
   const int mrow = lane >> 4, mcol = lane & 15;
+  const int cam = wave % N, sp = wave / N;
+  const int model = d.model[cam], nin = d.nintr[cam];
+  const double* intr = s + cam * KB_MAX_INTR;
   for (int f = f0; f < f1; ++f) {
     const double* fp = s + d.off_frame + 7 * f;
-    // T_f^-1 = (Rf^T | -Rf^T tf)
-    double Rf[9];
-    quat2r(fp, Rf);
-    const double tf[3] = {fp[4], fp[5], fp[6]};
-    double Ri[9], ti[3];
+    double Ri[9], ti[3], R[9], t[3];
+    pose_inverse(fp, Ri, ti);
+    rt_mul(d.camL + cam * 12, d.camL + cam * 12 + 9, Ri, ti, R, t);  // T_cam_w = L_cam T_f^-1
+    const int v = d.frame_vcam[f * N + cam];
+    v4d acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+    if (v >= 0) {
+      const int o0 = d.view_off[v], o1 = d.view_off[v + 1];
+      for (int base = o0 + sp * 64; base < o1; base += NS * 64) {
+        const int k = base + lane;
+        double xr[2][16];
 #pragma unroll
-    for (int r = 0; r < 3; ++r) {
+        for (int r = 0; r < 2; ++r)
 #pragma unroll
-      for (int cc = 0; cc < 3; ++cc) Ri[r * 3 + cc] = Rf[cc * 3 + r];
-      ti[r] = -(Ri[r * 3 + 0] * tf[0] + Ri[r * 3 + 1] * tf[1] + Ri[r * 3 + 2] * tf[2]);
-    }
-    for (int cam = wave; cam < N; cam += WPB) {
-      const int v = d.frame_vcam[f * N + cam];
-      const int model = d.model[cam], nin = d.nintr[cam];
-      const double* intr = s + cam * KB_MAX_INTR;
-      // T_cam_w = L_cam * T_f^-1
-      double R[9], t[3];
-      rt_mul(d.camL + cam * 12, d.camL + cam * 12 + 9, Ri, ti, R, t);
-      v4d acc = {0.0, 0.0, 0.0, 0.0};
-      if (v >= 0) {
-        const int o0 = d.view_off[v], o1 = d.view_off[v + 1];
-        for (int base = o0; base < o1; base += 64) {
-          const int k = base + lane;
-          double xr[2][16];
+          for (int q = 0; q < 16; ++q) xr[r][q] = 0.0;
+        if (k < o1) {
+          const int cid = d.cid[k];
+          const double X0 = d.target[3 * cid], X1 = d.target[3 * cid + 1], X2 = d.target[3 * cid + 2];
+          const double p0 = R[0] * X0 + R[1] * X1 + R[2] * X2 + t[0];
+          const double p1 = R[3] * X0 + R[4] * X1 + R[5] * X2 + t[1];
+          const double p2 = R[6] * X0 + R[7] * X1 + R[8] * X2 + t[2];
+          double u, w, Jp[6], Ji[2 * KB_MAX_INTR];
+          project_jac(model, intr, p0, p1, p2, u, w, Jp, Ji);
+          const double2 yv = d.y[k];
+          const double e0 = yv.x - u, e1 = yv.y - w;
 #pragma unroll
-          for (int r = 0; r < 2; ++r)
+          for (int r = 0; r < 2; ++r) {
+            const double j0 = Jp[3 * r], j1 = Jp[3 * r + 1], j2 = Jp[3 * r + 2];
+            // J_delta = -Jp [I | [p]x]   (HomogeneousExpressionNode.cpp:71-81, boxMinus)
+            xr[r][0] = -j0;
+            xr[r][1] = -j1;
+            xr[r][2] = -j2;
+            xr[r][3] = -(j1 * p2 - j2 * p1);
+            xr[r][4] = -(-j0 * p2 + j2 * p0);
+            xr[r][5] = -(j0 * p1 - j1 * p0);
+            // intrinsics: -Jp, -Jd (CameraDesignVariable.hpp(impl):38-54)
 #pragma unroll
-            for (int q = 0; q < 16; ++q) xr[r][q] = 0.0;
-          if (k < o1) {
-            const int cid = d.cid[k];
-            const double X0 = d.target[3 * cid], X1 = d.target[3 * cid + 1], X2 = d.target[3 * cid + 2];
-            const double p0 = R[0] * X0 + R[1] * X1 + R[2] * X2 + t[0];
-            const double p1 = R[3] * X0 + R[4] * X1 + R[5] * X2 + t[1];
-            const double p2 = R[6] * X0 + R[7] * X1 + R[8] * X2 + t[2];
-            double u, w, Jp[6], Ji[2 * KB_MAX_INTR];
-            project_jac(model, intr, p0, p1, p2, u, w, Jp, Ji);
-            const double2 yv = d.y[k];
-            const double e0 = yv.x - u, e1 = yv.y - w;
-#pragma unroll
-            for (int r = 0; r < 2; ++r) {
-              const double j0 = Jp[3 * r], j1 = Jp[3 * r + 1], j2 = Jp[3 * r + 2];
-              // J_delta = -Jp [I | [p]x]   (HomogeneousExpressionNode.cpp:71-81, boxMinus)
-              xr[r][0] = -j0;
-              xr[r][1] = -j1;
-              xr[r][2] = -j2;
-              xr[r][3] = -(j1 * p2 - j2 * p1);
-              xr[r][4] = -(-j0 * p2 + j2 * p0);
-              xr[r][5] = -(j0 * p1 - j1 * p0);
-              // intrinsics: -Jp, -Jd (CameraDesignVariable.hpp(impl):38-54)
-#pragma unroll
-              for (int q = 0; q < 9; ++q) xr[r][6 + q] = (q < nin) ? -Ji[r * KB_MAX_INTR + q] : 0.0;
-              xr[r][15] = -(r == 0 ? e0 : e1);  // column 15 carries -e: H[:,15] = rhs, H[15][15] = chi^2
-            }
-          }
-          // two phases of 32 corners (64 rows) through the LDS tile, 16 MFMA k-steps each
-#pragma unroll
-          for (int ph = 0; ph < 2; ++ph) {
-            if (ph == 1 && base + 32 >= o1) break;  // wave-uniform
-            if ((lane >> 5) == ph) {
-              const int rr = 2 * (lane & 31);
-#pragma unroll
-              for (int q = 0; q < 16; ++q) {
-                Xw[rr * XS + q] = xr[0][q];
-                Xw[(rr + 1) * XS + q] = xr[1][q];
-              }
-            }
-            KB_WAVE_SYNC();
-#pragma unroll
-            for (int ks = 0; ks < 16; ++ks) {
-              const double xv = Xw[(4 * ks + mrow) * XS + mcol];
-              acc = __builtin_amdgcn_mfma_f64_16x16x4f64(xv, xv, acc, 0, 0, 0);
-            }
-            KB_WAVE_SYNC();
+            for (int q = 0; q < 9; ++q) xr[r][6 + q] = (q < nin) ? -Ji[r * KB_MAX_INTR + q] : 0.0;
+            xr[r][15] = -(r == 0 ? e0 : e1);  // column 15 carries -e: H[:,15] = rhs part, H[15][15] = chi^2
           }
         }
-      }
-      // f64 MFMA C/D layout: lane l, reg r -> row (l>>4) + 4r, col l&15
+        // two phases of 32 corners (64 rows) through the LDS tile, 16 MFMA k-steps each
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int idx = (mrow + 4 * r) * 16 + mcol;
-        Hw[idx] = acc[r];
-        camsum[cam * 256 + idx] += acc[r];
-      }
-      if (lane == 0) {
+        for (int ph = 0; ph < 2; ++ph) {
+          if (ph == 1 && base + 32 >= o1) break;  // wave-uniform
+          if ((lane >> 5) == ph) {
+            const int rr = 2 * (lane & 31);
 #pragma unroll
-        for (int q = 0; q < 9; ++q) Ww[q] = R[q];
-        Ww[9] = t[0]; Ww[10] = t[1]; Ww[11] = t[2];
-        Ww[12] = tf[0]; Ww[13] = tf[1]; Ww[14] = tf[2];
+            for (int q = 0; q < 16; ++q) {
+              Xw[rr * XS + q] = xr[0][q];
+              Xw[(rr + 1) * XS + q] = xr[1][q];
+            }
+          }
+          KB_WAVE_SYNC();
+#pragma unroll
+          for (int ks = 0; ks < 16; ks += 2) {
+            const double xa = Xw[(4 * ks + mrow) * XS + mcol];
+            const double xb = Xw[(4 * ks + 4 + mrow) * XS + mcol];
+            acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(xa, xa, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(xb, xb, acc1, 0, 0, 0);
+          }
+          KB_WAVE_SYNC();
+        }
       }
+    }
+    // f64 MFMA C/D layout: lane l, reg r -> row (l>>4) + 4r, col l&15
+#pragma unroll
+    for (int r = 0; r < 4; ++r) Hw[wave * 256 + (mrow + 4 * r) * 16 + mcol] = acc0[r] + acc1[r];
+    if (sp == 0 && lane == 0) {
+      double* wv = Wv + cam * 64;
+#pragma unroll
+      for (int q = 0; q < 9; ++q) wv[q] = R[q];
+      wv[9] = t[0]; wv[10] = t[1]; wv[11] = t[2];
+      wv[12] = fp[4]; wv[13] = fp[5]; wv[14] = fp[6];
+    }
+    __syncthreads();
+    for (int q = threadIdx.x; q < N * 256; q += nth) {
+      const int qc = q >> 8, e = q & 255;
+      double sacc = 0.0;
+      for (int k = 0; k < NS; ++k) sacc += Hw[(k * N + qc) * 256 + e];
+      Hv[q] = sacc;
+      camsum[q] += sacc;
+    }
+    __syncthreads();
+    if (wave < N) {  // expansion of view (f, cam = wave) through the 6-D chains
+      const int vc = wave;
+      const bool has = d.frame_vcam[f * N + vc] >= 0;
+      const int nv = d.nintr[vc];
+      const double* H = Hv + vc * 256;
+      double* wv = Wv + vc * 64;
+      double* G = wv + 16;
+      if (lane < 36) G[lane] = chain_entry(wv, wv + 9, wv + 12, lane / 6, lane % 6);
       KB_WAVE_SYNC();
-      // frame-DV chain G_v = -boxTimes(T_cam_w) M(t_f) (6x6)
-      double* G = Ww + 16;
-      if (lane < 36) G[lane] = chain_entry(Ww, Ww + 9, Ww + 12, lane / 6, lane % 6);
-      KB_WAVE_SYNC();
-      const bool has = v >= 0;
       if (lane < 36) {
         const int a = lane / 6, b = lane % 6;
         double sacc = 0.0;
 #pragma unroll
-        for (int k = 0; k < 6; ++k) sacc += G[k * 6 + a] * Hw[k * 16 + b];
-        Pv[cam * 36 + lane] = has ? sacc : 0.0;  // P_v = G^T H_dd
+        for (int k = 0; k < 6; ++k) sacc += G[k * 6 + a] * H[k * 16 + b];
+        Pv[vc * 36 + lane] = has ? sacc : 0.0;  // P_v = G^T H_dd
       } else if (lane < 42) {
         const int a = lane - 36;
         double sacc = 0.0;
 #pragma unroll
-        for (int k = 0; k < 6; ++k) sacc += G[k * 6 + a] * Hw[k * 16 + 15];
-        dg[cam * 8 + a] = has ? sacc : 0.0;  // G^T g_d
+        for (int k = 0; k < 6; ++k) sacc += G[k * 6 + a] * H[k * 16 + 15];
+        dg[vc * 8 + a] = has ? sacc : 0.0;  // G^T g_d
       }
       KB_WAVE_SYNC();
       if (lane < 36) {
         const int a = lane / 6, b = lane % 6;
         double sacc = 0.0;
 #pragma unroll
-        for (int k = 0; k < 6; ++k) sacc += Pv[cam * 36 + a * 6 + k] * G[k * 6 + b];
-        dH[cam * 36 + lane] = sacc;  // P_v G_v
+        for (int k = 0; k < 6; ++k) sacc += Pv[vc * 36 + a * 6 + k] * G[k * 6 + b];
+        dH[vc * 36 + lane] = sacc;  // P_v G_v
       }
-      if (lane < 6 * nin) {
-        const int a = lane / nin, q = lane % nin;
+      if (lane < 6 * nv) {
+        const int a = lane / nv, q = lane % nv;
         double sacc = 0.0;
 #pragma unroll
-        for (int k = 0; k < 6; ++k) sacc += G[k * 6 + a] * Hw[k * 16 + 6 + q];
-        d.Hfc[((size_t)f * 6 + a) * C + d.col_intr[cam] + q] = has ? sacc : 0.0;  // G^T H_dI
+        for (int k = 0; k < 6; ++k) sacc += G[k * 6 + a] * H[k * 16 + 6 + q];
+        sacc = has ? sacc : 0.0;  // G^T H_dI
+        Fc[a * C + d.col_intr[vc] + q] = sacc;
+        d.Hfc[((size_t)f * 6 + a) * C + d.col_intr[vc] + q] = sacc;
       }
-      KB_WAVE_SYNC();
     }
     __syncthreads();
     // frame outputs: sums over the frame's views in camera order
-    for (int q = threadIdx.x; q < 42 + 36 * (N - 1); q += blockDim.x) {
+    for (int q = threadIdx.x; q < 42 + 36 * (N - 1); q += nth) {
       if (q < 36) {
         double sacc = 0.0;
-        for (int cam = 0; cam < N; ++cam) sacc += dH[cam * 36 + q];
+        for (int i = 0; i < N; ++i) sacc += dH[i * 36 + q];
+        Fh[q] = sacc;
         d.Hff[(size_t)f * 36 + q] = sacc;
       } else if (q < 42) {
         double sacc = 0.0;
-        for (int cam = 0; cam < N; ++cam) sacc += dg[cam * 8 + q - 36];
+        for (int i = 0; i < N; ++i) sacc += dg[i * 8 + q - 36];
+        Fg[q - 36] = sacc;
         d.gf[(size_t)f * 6 + q - 36] = sacc;
-      } else {
-        // H_f,B_j = sum_{i > j} P_i K_{i,j}
-        const int e = q - 42, j = e / 36, ab = e % 36, a = ab / 6, b = ab % 6;
+      } else {  // H_f,B_j = sum_{i > j} P_i K_{i,j}
+        const int e = q - 42, j = e / 36, ab2 = e % 36, a = ab2 / 6, b = ab2 % 6;
         double sacc = 0.0;
         for (int i = j + 1; i < N; ++i) {
           const double* K = d.camK + (size_t)(i * N + j) * 36;
 #pragma unroll
           for (int k = 0; k < 6; ++k) sacc += Pv[i * 36 + a * 6 + k] * K[k * 6 + b];
         }
+        Fc[a * C + d.col_base[j] + b] = sacc;
         d.Hfc[((size_t)f * 6 + a) * C + d.col_base[j] + b] = sacc;
       }
     }
+    if (fuse) {
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        for (int q = 0; q < 36; ++q) L[q] = Fh[q] + ((q % 7 == 0) ? lam2 : 0.0);
+        if (!chol6(L)) okl = 0;
+        for (int q = 0; q < 36; ++q) d.Lf[(size_t)f * 36 + q] = L[q];
+      }
+      __syncthreads();
+      schur_forward(d, f, L, Fc, Fg, Y, z);
+      __syncthreads();
+      schur_accumulate<M>(C, Wt, W, Y, z, ab, acc);
+    }
     __syncthreads();
   }
-  // per-camera partial sums (upper triangle of the 16x16) of this block
-  for (int q = threadIdx.x; q < N * 136; q += blockDim.x) {
-    const int cam = q / 136, e = q % 136;
-    const int a = d16_row(e), b = d16_col(e);
-    d.campart[(size_t)blockIdx.x * N * 136 + q] = camsum[cam * 256 + a * 16 + b];
+  double* prow = d.part + (size_t)blockIdx.x * d.Wtot;
+  for (int q = threadIdx.x; q < N * 136; q += nth) {
+    const int qc = q / 136;
+    int a, b;
+    d16_rowcol(q % 136, a, b);
+    prow[q] = camsum[qc * 256 + a * 16 + b];
+  }
+  if (fuse) {
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const int e = threadIdx.x + nth * m;
+      if (e < W) prow[N * 136 + e] = acc[m];
+    }
+    if (threadIdx.x == 0) prow[N * 136 + W] = okl ? 0.0 : 1.0;  // non-PD frame blocks (summed)
   }
 }
 
 // ---------------------------------------------------------------------------------------------
-// deterministic column sums: out[w] = sum_b in[b][w] (fixed order)
+// k_schur: Schur step from the stored arrow blocks (LM passes with a new lambda, per-call solve)
 // ---------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_colsum(KbDev d, const double* in, int B, int W, double* out, int gate) {
+template <int M>
+__global__ void __launch_bounds__(256) k_schur(KbDev d, int gate) {
   KbCtrl* c = d.ctrl;
-  if (gate == 1 && (c->done || !c->do_build)) return;
-  if (gate == 2 && c->done) return;
-  __shared__ double part[4][64];
-  const int l = threadIdx.x & 63, w4 = threadIdx.x >> 6;
-  const int e = blockIdx.x * 64 + l;
-  double s = 0.0;
-  if (e < W)
-    for (int b = w4; b < B; b += 4) s += in[(size_t)b * W + e];
-  part[w4][l] = s;
+  if (gate && (c->done || c->do_build)) return;  // rebuild passes ran it fused in k_build
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  const int C = d.C, W = d.W, Wt = W - C, N = d.N;
+  double* Y = sm;         // [6][C]
+  double* L = Y + 6 * C;  // [36]
+  double* z = L + 36;     // [8]
+  __shared__ int okl;
+  const double lam = gate ? c->lambda : d.host_lambda;
+  const double lam2 = lam * lam;
+  double acc[M];
+  int ab[M];
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    acc[m] = 0.0;
+    const int e = threadIdx.x + blockDim.x * m;
+    ab[m] = (e < Wt) ? d.tri[e] : 0;
+  }
+  if (threadIdx.x == 0) okl = 1;
+  const int f0 = blockIdx.x * d.gframes, f1 = min(d.F, f0 + d.gframes);
+  for (int f = f0; f < f1; ++f) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      for (int q = 0; q < 36; ++q) L[q] = d.Hff[(size_t)f * 36 + q] + ((q % 7 == 0) ? lam2 : 0.0);
+      if (!chol6(L)) okl = 0;
+      for (int q = 0; q < 36; ++q) d.Lf[(size_t)f * 36 + q] = L[q];
+    }
+    __syncthreads();
+    schur_forward(d, f, L, nullptr, nullptr, Y, z);
+    __syncthreads();
+    schur_accumulate<M>(C, Wt, W, Y, z, ab, acc);
+  }
+  double* prow = d.part + (size_t)blockIdx.x * d.Wtot + N * 136;
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    const int e = threadIdx.x + blockDim.x * m;
+    if (e < W) prow[e] = acc[m];
+  }
   __syncthreads();
-  if (w4 == 0 && e < W) out[e] = ((part[0][l] + part[1][l]) + part[2][l]) + part[3][l];
+  if (threadIdx.x == 0) prow[W] = okl ? 0.0 : 1.0;
 }
 
 // ---------------------------------------------------------------------------------------------
-// camera block H_cc, g_c from the per-camera local sums
+// k_colsum: part8[ry][e] = sum_{b = ry mod 8} part[b][e]  (fixed order), grid (ceil(Wtot/64), 8)
 // ---------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_camexpand(KbDev d, int gate) {
+__global__ void __launch_bounds__(256) k_colsum(KbDev d, int gate) {
   KbCtrl* c = d.ctrl;
-  if (gate && (c->done || !c->do_build)) return;
-  extern __shared__ __attribute__((aligned(16))) double sm[];
-  const int N = d.N, C = d.C;
-  double* Hs = sm;                    // [N][256] full per-camera 16x16 sums
-  double* T = Hs + N * 256;           // [N][N][36]: T_{i,k} = H_dd,i K_{i,k}
-  const double* cs = d.camsum;        // [N][136] upper packed
+  if (gate && c->done) return;
+  __shared__ double part[4][64];
+  const int l = threadIdx.x & 63, w4 = threadIdx.x >> 6;
+  const int e = blockIdx.x * 64 + l, ry = blockIdx.y;
+  double s = 0.0;
+  if (e < d.Wtot)
+    for (int b = ry + kColsumRows * w4; b < d.nblk; b += 4 * kColsumRows) s += d.part[(size_t)b * d.Wtot + e];
+  part[w4][l] = s;
+  __syncthreads();
+  if (w4 == 0 && e < d.Wtot) d.part8[(size_t)ry * d.Wtot + e] = ((part[0][l] + part[1][l]) + part[2][l]) + part[3][l];
+}
+
+// k_colsum_final: [8][Wtot] -> [Wtot] before the all-reduce (sharded runs)
+__global__ void __launch_bounds__(256) k_colsum_final(KbDev d, double* out, int gate) {
+  KbCtrl* c = d.ctrl;
+  if (gate && c->done) return;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= d.Wtot) return;
+  double s = 0.0;
+  for (int r = 0; r < kColsumRows; ++r) s += d.part8[(size_t)r * d.Wtot + e];
+  out[e] = s;
+}
+
+__device__ __forceinline__ double psum_at(const KbDev& d, int e) {
+  double s = 0.0;
+  for (int r = 0; r < d.npart; ++r) s += d.psum[(size_t)r * d.Wtot + e];
+  return s;
+}
+
+// ---------------------------------------------------------------------------------------------
+// camera block from the per-camera local sums (H_cc, g_c), shared by k_camexpand and k_solve
+// H_{I_i,I_i} = Hs_i[II]; H_{I_i,B_j} = Hs_i[Id] K_{i,j}; H_{B_j,B_k} = sum_{i>max} K_{i,j}^T Hs_i[dd] K_{i,k}
+// ---------------------------------------------------------------------------------------------
+__device__ void cam_load(const KbDev& d, double* Hs, double* T) {
+  const int N = d.N;
   for (int q = threadIdx.x; q < N * 256; q += blockDim.x) {
-    const int cam = q / 256, a = (q % 256) / 16, b = q % 16;
+    const int cam = q >> 8, a = (q & 255) >> 4, b = q & 15;
     const int lo = a < b ? a : b, hi = a < b ? b : a;
-    Hs[q] = cs[cam * 136 + d16_index(lo, hi)];
+    Hs[q] = psum_at(d, cam * 136 + d16_index(lo, hi));
   }
   __syncthreads();
   for (int q = threadIdx.x; q < N * N * 36; q += blockDim.x) {
@@ -339,198 +642,116 @@ __global__ void __launch_bounds__(256) k_camexpand(KbDev d, int gate) {
 #pragma unroll
       for (int m = 0; m < 6; ++m) s += Hs[i * 256 + a * 16 + m] * K[m * 6 + b];
     }
-    T[q] = s;
+    T[q] = s;  // T_{i,k} = Hs_i[dd] K_{i,k}
   }
   __syncthreads();
-  for (int q = threadIdx.x; q < C * C + C + 1; q += blockDim.x) {
-    if (q == C * C + C) {
-      double s = 0.0;
-      for (int i = 0; i < N; ++i) s += Hs[i * 256 + 255];
-      d.cost_build[0] = s;
-      continue;
-    }
-    const bool isg = q >= C * C;
-    const int p = isg ? q - C * C : q / C;
-    const int r = isg ? 15 : q % C;  // r == 15 marks the gradient column
-    const int kp = d.colinfo[p] >> 16, ip = (d.colinfo[p] >> 8) & 0xff, xp = d.colinfo[p] & 0xff;
-    double s = 0.0;
-    if (isg) {
-      if (kp == 0) {
-        s = Hs[ip * 256 + (6 + xp) * 16 + 15];
-      } else {
-        for (int i = ip + 1; i < N; ++i) {
-          const double* K = d.camK + (size_t)(i * N + ip) * 36;
-#pragma unroll
-          for (int a = 0; a < 6; ++a) s += K[a * 6 + xp] * Hs[i * 256 + a * 16 + 15];
-        }
-      }
-      d.gc[p] = s;
-      continue;
-    }
-    const int kq = d.colinfo[r] >> 16, iq = (d.colinfo[r] >> 8) & 0xff, xq = d.colinfo[r] & 0xff;
-    if (kp == 0 && kq == 0) {
-      if (ip == iq) s = Hs[ip * 256 + (6 + xp) * 16 + 6 + xq];
-    } else if (kp == 0 && kq == 1) {
-      if (iq < ip) {
-        const double* K = d.camK + (size_t)(ip * N + iq) * 36;
-#pragma unroll
-        for (int b = 0; b < 6; ++b) s += Hs[ip * 256 + (6 + xp) * 16 + b] * K[b * 6 + xq];
-      }
-    } else if (kp == 1 && kq == 0) {
-      if (ip < iq) {
-        const double* K = d.camK + (size_t)(iq * N + ip) * 36;
-#pragma unroll
-        for (int a = 0; a < 6; ++a) s += K[a * 6 + xp] * Hs[iq * 256 + a * 16 + 6 + xq];
-      }
-    } else {
-      const int m = ip > iq ? ip : iq;
-      for (int i = m + 1; i < N; ++i) {
-        const double* K = d.camK + (size_t)(i * N + ip) * 36;
-        const double* Tq = T + (size_t)(i * N + iq) * 36;
-#pragma unroll
-        for (int a = 0; a < 6; ++a) s += K[a * 6 + xp] * Tq[a * 6 + xq];
-      }
-    }
-    d.Hcc[q] = s;
-  }
 }
 
-// ---------------------------------------------------------------------------------------------
-// k_schur: per frame chol(H_ff + lambda^2 I), Y = L^-1 H_fc, z = L^-1 g_f; sum Y^T Y, Y^T z
-// ---------------------------------------------------------------------------------------------
-constexpr int kSchurM = 24;  // entries per thread (256 threads) -> W <= 6144, C <= 109
+__device__ double cam_entry(const KbDev& d, const double* Hs, const double* T, int p, int q) {
+  const int N = d.N;
+  const int kp = d.colinfo[p] >> 16, ip = (d.colinfo[p] >> 8) & 0xff, xp = d.colinfo[p] & 0xff;
+  const int kq = d.colinfo[q] >> 16, iq = (d.colinfo[q] >> 8) & 0xff, xq = d.colinfo[q] & 0xff;
+  double s = 0.0;
+  if (kp == 0 && kq == 0) {
+    if (ip == iq) s = Hs[ip * 256 + (6 + xp) * 16 + 6 + xq];
+  } else if (kp == 0 && kq == 1) {
+    if (iq < ip) {
+      const double* K = d.camK + (size_t)(ip * N + iq) * 36;
+#pragma unroll
+      for (int b = 0; b < 6; ++b) s += Hs[ip * 256 + (6 + xp) * 16 + b] * K[b * 6 + xq];
+    }
+  } else if (kp == 1 && kq == 0) {
+    if (ip < iq) {
+      const double* K = d.camK + (size_t)(iq * N + ip) * 36;
+#pragma unroll
+      for (int a = 0; a < 6; ++a) s += K[a * 6 + xp] * Hs[iq * 256 + a * 16 + 6 + xq];
+    }
+  } else {
+    const int m = ip > iq ? ip : iq;
+    for (int i = m + 1; i < N; ++i) {
+      const double* K = d.camK + (size_t)(i * N + ip) * 36;
+      const double* Tq = T + (size_t)(i * N + iq) * 36;
+#pragma unroll
+      for (int a = 0; a < 6; ++a) s += K[a * 6 + xp] * Tq[a * 6 + xq];
+    }
+  }
+  return s;
+}
 
-__global__ void __launch_bounds__(256) k_schur(KbDev d, int gate) {
-  KbCtrl* c = d.ctrl;
-  if (gate && c->done) return;
+__device__ double cam_grad(const KbDev& d, const double* Hs, int p) {
+  const int N = d.N;
+  const int kp = d.colinfo[p] >> 16, ip = (d.colinfo[p] >> 8) & 0xff, xp = d.colinfo[p] & 0xff;
+  if (kp == 0) return Hs[ip * 256 + (6 + xp) * 16 + 15];
+  double s = 0.0;
+  for (int i = ip + 1; i < N; ++i) {
+    const double* K = d.camK + (size_t)(i * N + ip) * 36;
+#pragma unroll
+    for (int a = 0; a < 6; ++a) s += K[a * 6 + xp] * Hs[i * 256 + a * 16 + 15];
+  }
+  return s;
+}
+
+// per-call path: H_cc, g_c, cost at the build state (kb_get_normal_blocks / kb_get_rhs)
+__global__ void __launch_bounds__(256) k_camexpand(KbDev d) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
-  const int C = d.C, Wt = C * (C + 1) / 2, W = Wt + C;
-  double* Y = sm;            // [6][C]
-  double* L = Y + 6 * C;     // [36]
-  double* z = L + 36;        // [8]
-  __shared__ int okl;
-  const double lam = gate ? c->lambda : d.host_lambda;
-  const double lam2 = lam * lam;
-  double acc[kSchurM];
-  int ab[kSchurM];
-#pragma unroll
-  for (int m = 0; m < kSchurM; ++m) {
-    acc[m] = 0.0;
-    const int e = threadIdx.x + 256 * m;
-    ab[m] = (e < Wt) ? d.tri[e] : -1;
+  const int N = d.N, C = d.C;
+  double* Hs = sm;
+  double* T = Hs + N * 256;
+  cam_load(d, Hs, T);
+  for (int q = threadIdx.x; q < C * C; q += blockDim.x) d.Hcc[q] = cam_entry(d, Hs, T, q / C, q % C);
+  for (int p = threadIdx.x; p < C; p += blockDim.x) d.gc[p] = cam_grad(d, Hs, p);
+  if (threadIdx.x == 0) {
+    double s = 0.0;
+    for (int i = 0; i < N; ++i) s += Hs[i * 256 + 255];
+    d.cost_build[0] = s;
   }
-  if (threadIdx.x == 0) okl = 1;
-  const int f0 = blockIdx.x * d.gframes, f1 = min(d.F, f0 + d.gframes);
-  for (int f = f0; f < f1; ++f) {
-    if (threadIdx.x < 36) L[threadIdx.x] = d.Hff[(size_t)f * 36 + threadIdx.x] + ((threadIdx.x % 7 == 0) ? lam2 : 0.0);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      // in-place Cholesky, lower
-      for (int j = 0; j < 6; ++j) {
-        double dd = L[j * 6 + j];
-        for (int k = 0; k < j; ++k) dd -= L[j * 6 + k] * L[j * 6 + k];
-        if (!(dd > 0.0)) okl = 0;
-        dd = sqrt(dd);
-        L[j * 6 + j] = dd;
-        for (int i = j + 1; i < 6; ++i) {
-          double s2 = L[i * 6 + j];
-          for (int k = 0; k < j; ++k) s2 -= L[i * 6 + k] * L[j * 6 + k];
-          L[i * 6 + j] = s2 / dd;
-        }
-      }
-      for (int q = 0; q < 36; ++q) d.Lf[(size_t)f * 36 + q] = L[q];
-    }
-    __syncthreads();
-    const int t = threadIdx.x;
-    if (t < C) {
-      double yv[6];
-#pragma unroll
-      for (int r = 0; r < 6; ++r) {
-        double s2 = d.Hfc[((size_t)f * 6 + r) * C + t];
-#pragma unroll
-        for (int k = 0; k < r; ++k) s2 -= L[r * 6 + k] * yv[k];
-        yv[r] = s2 / L[r * 6 + r];
-        Y[r * C + t] = yv[r];
-        d.Yf[((size_t)f * 6 + r) * C + t] = yv[r];
-      }
-    } else if (t == 255) {
-      double zv[6];
-#pragma unroll
-      for (int r = 0; r < 6; ++r) {
-        double s2 = d.gf[(size_t)f * 6 + r];
-#pragma unroll
-        for (int k = 0; k < r; ++k) s2 -= L[r * 6 + k] * zv[k];
-        zv[r] = s2 / L[r * 6 + r];
-        z[r] = zv[r];
-        d.zf[(size_t)f * 6 + r] = zv[r];
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int m = 0; m < kSchurM; ++m) {
-      const int e = threadIdx.x + 256 * m;
-      if (e < Wt) {
-        const int a = ab[m] >> 16, b = ab[m] & 0xffff;
-        double s2 = 0.0;
-#pragma unroll
-        for (int r = 0; r < 6; ++r) s2 += Y[r * C + a] * Y[r * C + b];
-        acc[m] += s2;
-      } else if (e < W) {
-        const int a = e - Wt;
-        double s2 = 0.0;
-#pragma unroll
-        for (int r = 0; r < 6; ++r) s2 += Y[r * C + a] * z[r];
-        acc[m] += s2;
-      }
-    }
-    __syncthreads();
-  }
-#pragma unroll
-  for (int m = 0; m < kSchurM; ++m) {
-    const int e = threadIdx.x + 256 * m;
-    if (e < W) d.schurpart[(size_t)blockIdx.x * (W + 1) + e] = acc[m];
-  }
-  // entry W counts blocks with a non-positive-definite H_ff + lambda^2 I (summed over blocks and ranks)
-  if (threadIdx.x == 0) d.schurpart[(size_t)blockIdx.x * (W + 1) + W] = okl ? 0.0 : 1.0;
 }
 
 // ---------------------------------------------------------------------------------------------
-// k_solve: S = H_cc + lambda^2 I - sum Y^T Y, b = g_c - sum Y^T z; chol; dx_c; camera update
+// k_solve: S = H_cc + lambda^2 I - sum Y^T Y, b = g_c - sum Y^T z; LDL^T (one barrier per column);
+// dx_c; camera DV update into state[1-cur]
 // ---------------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_solve(KbDev d, int gate, int do_update) {
   KbCtrl* c = d.ctrl;
   if (gate && c->done) return;
   extern __shared__ __attribute__((aligned(16))) double sm[];
-  const int C = d.C, Wt = C * (C + 1) / 2;
-  double* S = sm;  // [C][C]
+  const int N = d.N, C = d.C, W = d.W, Wt = W - C, nth = blockDim.x;
+  double* S = sm;               // [C][C] (lower part used)
+  double* Hs = S + C * C;       // [N][256]
+  double* T = Hs + N * 256;     // [N][N][36]
+  double* bv = T + N * N * 36;  // [C]
   __shared__ int okl;
   __shared__ double red[4][64];
   const double lam = gate ? c->lambda : d.host_lambda;
   const double lam2 = lam * lam;
-  const double* ss = d.schursum;
-  for (int q = threadIdx.x; q < C * C; q += blockDim.x) {
+  cam_load(d, Hs, T);
+  for (int q = threadIdx.x; q < C * C; q += nth) {
     const int a = q / C, b = q % C;
-    const int lo = a < b ? a : b, hi = a < b ? b : a;
-    const int e = lo * C - lo * (lo - 1) / 2 + (hi - lo);
-    S[q] = d.Hcc[q] + ((a == b) ? lam2 : 0.0) - ss[e];
+    if (b > a) continue;
+    S[q] = cam_entry(d, Hs, T, a, b) + ((a == b) ? lam2 : 0.0) - psum_at(d, N * 136 + upper_index(b, a, C));
   }
-  if (threadIdx.x == 0) okl = (c->solve_ok != 0) && !(ss[Wt + C] > 0.0);
+  for (int p = threadIdx.x; p < C; p += nth) {
+    const double g = cam_grad(d, Hs, p);
+    bv[p] = g - psum_at(d, N * 136 + Wt + p);
+    d.gc[p] = g;
+    d.rhs[p] = g;
+  }
+  if (threadIdx.x == 0) {
+    okl = (c->solve_ok != 0) && !(psum_at(d, N * 136 + W) > 0.0);
+    double s = 0.0;
+    for (int i = 0; i < N; ++i) s += Hs[i * 256 + 255];
+    d.cost_build[0] = s;
+  }
   __syncthreads();
-  // right-looking Cholesky (lower), 3 barriers per column
+  // LDL^T in place: after step k, S[i][k] = Ltilde[i][k] * D_k for i > k, S[k][k] = D_k
   for (int k = 0; k < C; ++k) {
-    if (threadIdx.x == 0) {
-      const double dd = S[k * C + k];
-      if (!(dd > 0.0)) okl = 0;
-      S[k * C + k] = sqrt(dd);
-    }
-    __syncthreads();
     const double dk = S[k * C + k];
-    for (int i = k + 1 + threadIdx.x; i < C; i += blockDim.x) S[i * C + k] /= dk;
-    __syncthreads();
+    if (threadIdx.x == 0 && !(dk > 0.0)) okl = 0;
     const int n = C - k - 1;
-    for (int q = threadIdx.x; q < n * n; q += blockDim.x) {
+    const double rdk = 1.0 / dk;
+    for (int q = threadIdx.x; q < n * n; q += nth) {
       const int i = k + 1 + q / n, j = k + 1 + q % n;
-      if (j <= i) S[i * C + j] -= S[i * C + k] * S[j * C + k];
+      if (j <= i) S[i * C + j] -= S[i * C + k] * S[j * C + k] * rdk;
     }
     __syncthreads();
   }
@@ -539,31 +760,36 @@ __global__ void __launch_bounds__(256) k_solve(KbDev d, int gate, int do_update)
     if (threadIdx.x == 0) c->solve_ok = 0;
     return;
   }
-  // triangular solves by wave 0; row i held by lane i & 63 (slot i >> 6)
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
-    double bv[2];
+    double x[2];
 #pragma unroll
     for (int sl = 0; sl < 2; ++sl) {
       const int i = lane + 64 * sl;
-      bv[sl] = (i < C) ? d.gc[i] - ss[Wt + i] : 0.0;
+      x[sl] = (i < C) ? bv[i] : 0.0;
     }
+    // forward Ltilde y = b (column oriented), then z = D^-1 y
     for (int k = 0; k < C; ++k) {
-      const double bk = __shfl(bv[k >> 6], k & 63) / S[k * C + k];
+      const double yk = __shfl(x[k >> 6], k & 63);
+      const double rdk = 1.0 / S[k * C + k];
 #pragma unroll
       for (int sl = 0; sl < 2; ++sl) {
         const int i = lane + 64 * sl;
-        if (i == k) bv[sl] = bk;
-        else if (i > k && i < C) bv[sl] -= S[i * C + k] * bk;
+        if (i > k && i < C) x[sl] -= S[i * C + k] * rdk * yk;
       }
     }
+#pragma unroll
+    for (int sl = 0; sl < 2; ++sl) {
+      const int i = lane + 64 * sl;
+      if (i < C) x[sl] /= S[i * C + i];
+    }
+    // backward Ltilde^T x = z
     for (int k = C - 1; k >= 0; --k) {
-      const double xk = __shfl(bv[k >> 6], k & 63) / S[k * C + k];
+      const double xk = __shfl(x[k >> 6], k & 63);
 #pragma unroll
       for (int sl = 0; sl < 2; ++sl) {
         const int i = lane + 64 * sl;
-        if (i == k) bv[sl] = xk;
-        else if (i < k) bv[sl] -= S[k * C + i] * xk;
+        if (i < k) x[sl] -= S[k * C + i] / S[i * C + i] * xk;
       }
     }
     double mx = 0.0, dd = 0.0, dr = 0.0;
@@ -572,11 +798,10 @@ __global__ void __launch_bounds__(256) k_solve(KbDev d, int gate, int do_update)
       const int i = lane + 64 * sl;
       if (i < C) {
         const double g = d.gc[i];
-        d.dx[i] = bv[sl];
-        d.rhs[i] = g;
-        mx = fmax(mx, fabs(bv[sl]));
-        dd += bv[sl] * bv[sl];
-        dr += bv[sl] * g;
+        d.dx[i] = x[sl];
+        mx = fmax(mx, fabs(x[sl]));
+        dd += x[sl] * x[sl];
+        dr += x[sl] * g;
       }
     }
     red[0][lane] = mx;
@@ -599,10 +824,9 @@ __global__ void __launch_bounds__(256) k_solve(KbDev d, int gate, int do_update)
     __syncthreads();
     const double* in = d.state + (size_t)c->cur * d.S;
     double* out = d.state + (size_t)(1 - c->cur) * d.S;
-    const int N = d.N;
-    for (int q = threadIdx.x; q < N * KB_MAX_INTR; q += blockDim.x) {
-      const int cam = q / KB_MAX_INTR, x = q % KB_MAX_INTR;
-      out[q] = in[q] + ((x < d.nintr[cam]) ? d.dx[d.col_intr[cam] + x] : 0.0);
+    for (int q = threadIdx.x; q < N * KB_MAX_INTR; q += nth) {
+      const int cm = q / KB_MAX_INTR, x = q % KB_MAX_INTR;
+      out[q] = in[q] + ((x < d.nintr[cm]) ? d.dx[d.col_intr[cm] + x] : 0.0);
     }
     if (threadIdx.x < N - 1) {
       const int j = threadIdx.x;
@@ -612,16 +836,17 @@ __global__ void __launch_bounds__(256) k_solve(KbDev d, int gate, int do_update)
 }
 
 // ---------------------------------------------------------------------------------------------
-// k_backsub: one wave per frame: dx_f = L^-T (z - Y dx_c); optional pose update; statistics
+// k_backsub: one wave per frame: dx_f = L^-T (z - Y dx_c); pose update; cost of the frame's views at the
+// new state (evaluateError fused); per-block [cost, max|dx|, dx.dx, dx.rhs]
 // ---------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_backsub(KbDev d, int gate, int do_update) {
+__global__ void __launch_bounds__(256) k_backsub(KbDev d, int gate, int do_update, int with_cost) {
   KbCtrl* c = d.ctrl;
   if (gate && (c->done || !c->solve_ok)) return;
-  __shared__ double st4[4][3];
+  __shared__ double st4[4][4];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int f = blockIdx.x * 4 + wave;
-  const int C = d.C;
-  double mx = 0.0, dd = 0.0, dr = 0.0;
+  const int C = d.C, N = d.N;
+  double mx = 0.0, dd = 0.0, dr = 0.0, cost = 0.0;
   if (f < d.F) {
     double w[6];
 #pragma unroll
@@ -644,50 +869,78 @@ __global__ void __launch_bounds__(256) k_backsub(KbDev d, int gate, int do_updat
       double xv = w[0];
 #pragma unroll
       for (int r = 1; r < 6; ++r) xv = (lane == r) ? w[r] : xv;
-      const double g = d.gf[(size_t)f * 6 + lane];
       d.dx[C + 6 * f + lane] = xv;
-      d.rhs[C + 6 * f + lane] = g;
+      d.rhs[C + 6 * f + lane] = d.gf[(size_t)f * 6 + lane];
     }
-    if (lane == 0) {
 #pragma unroll
-      for (int r = 0; r < 6; ++r) {
-        const double g = d.gf[(size_t)f * 6 + r];
-        mx = fmax(mx, fabs(w[r]));
-        dd += w[r] * w[r];
-        dr += w[r] * g;
-      }
-      if (do_update) {
-        const double* in = d.state + (size_t)c->cur * d.S + d.off_frame + 7 * f;
-        double* out = d.state + (size_t)(1 - c->cur) * d.S + d.off_frame + 7 * f;
-        update_pose(in, w, out);
+    for (int r = 0; r < 6; ++r) {
+      const double g = d.gf[(size_t)f * 6 + r];
+      mx = fmax(mx, fabs(w[r]));
+      dd += w[r] * w[r];
+      dr += w[r] * g;
+    }
+    if (do_update) {
+      const double* s0 = d.state + (size_t)c->cur * d.S;
+      double* s1 = d.state + (size_t)(1 - c->cur) * d.S;
+      double np[7];
+      update_pose(s0 + d.off_frame + 7 * f, w, np);  // every lane: the new pose stays in registers
+      if (lane == 0)
+        for (int q = 0; q < 7; ++q) s1[d.off_frame + 7 * f + q] = np[q];
+      if (with_cost) {
+        for (int cm = 0; cm < N; ++cm) {
+          const int v = d.frame_vcam[f * N + cm];
+          if (v < 0) continue;
+          double R[9], t[3];
+          cam_from_state(d, s1, cm, np, R, t);
+          const int model = d.model[cm];
+          const double* intr = s1 + cm * KB_MAX_INTR;
+          const int o0 = d.view_off[v], o1 = d.view_off[v + 1];
+          for (int k = o0 + lane; k < o1; k += 64) {
+            const int cid = d.cid[k];
+            const double X0 = d.target[3 * cid], X1 = d.target[3 * cid + 1], X2 = d.target[3 * cid + 2];
+            const double p0 = R[0] * X0 + R[1] * X1 + R[2] * X2 + t[0];
+            const double p1 = R[3] * X0 + R[4] * X1 + R[5] * X2 + t[1];
+            const double p2 = R[6] * X0 + R[7] * X1 + R[8] * X2 + t[2];
+            double u, vv;
+            project(model, intr, p0, p1, p2, u, vv);
+            const double2 yv = d.y[k];
+            const double e0 = yv.x - u, e1 = yv.y - vv;
+            cost += e0 * e0 + e1 * e1;
+          }
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) cost += __shfl_xor(cost, o);
       }
     }
   }
   if (lane == 0) {
-    st4[wave][0] = mx;
-    st4[wave][1] = dd;
-    st4[wave][2] = dr;
+    st4[wave][0] = cost;
+    st4[wave][1] = mx;
+    st4[wave][2] = dd;
+    st4[wave][3] = dr;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
     for (int q = 0; q < (int)(blockDim.x >> 6); ++q) {
-      a0 = fmax(a0, st4[q][0]);
-      a1 += st4[q][1];
+      a0 += st4[q][0];
+      a1 = fmax(a1, st4[q][1]);
       a2 += st4[q][2];
+      a3 += st4[q][3];
     }
-    d.statpart[(size_t)blockIdx.x * 3 + 0] = a0;
-    d.statpart[(size_t)blockIdx.x * 3 + 1] = a1;
-    d.statpart[(size_t)blockIdx.x * 3 + 2] = a2;
+    double* bp = d.bpart + (size_t)blockIdx.x * 4;
+    bp[0] = a0;
+    bp[1] = a1;
+    bp[2] = a2;
+    bp[3] = a3;
   }
 }
 
 // ---------------------------------------------------------------------------------------------
-// k_cost: one wave per view on state buffer (cur ^ which); per-block partial sums
+// k_cost: one wave per view on state buffer (cur ^ which); per-block partial sums (kb_eval_cost, loop start)
 // ---------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_cost(KbDev d, int gate, int which) {
+__global__ void __launch_bounds__(256) k_cost(KbDev d, int which) {
   KbCtrl* c = d.ctrl;
-  if (gate && (c->done || !c->solve_ok)) return;
   __shared__ double part[4];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int v = blockIdx.x * 4 + wave;
@@ -695,25 +948,8 @@ __global__ void __launch_bounds__(256) k_cost(KbDev d, int gate, int which) {
   double acc = 0.0;
   if (v < d.V) {
     const int f = d.view_frame[v], cam = d.view_cam[v];
-    // T_cam_w = B_{cam-1} .. B_0 T_f^-1 on this state
-    double R[9], t[3], Rf[9];
-    const double* fp = s + d.off_frame + 7 * f;
-    quat2r(fp, Rf);
-#pragma unroll
-    for (int r = 0; r < 3; ++r) {
-#pragma unroll
-      for (int cc = 0; cc < 3; ++cc) R[r * 3 + cc] = Rf[cc * 3 + r];
-      t[r] = -(Rf[0 * 3 + r] * fp[4] + Rf[1 * 3 + r] * fp[5] + Rf[2 * 3 + r] * fp[6]);
-    }
-    for (int j = 0; j < cam; ++j) {
-      double RB[9], tB[3], R2[9], t2[3];
-      pose_rt(s + d.off_base + 7 * j, RB, tB);
-      rt_mul(RB, tB, R, t, R2, t2);
-#pragma unroll
-      for (int q = 0; q < 9; ++q) R[q] = R2[q];
-#pragma unroll
-      for (int q = 0; q < 3; ++q) t[q] = t2[q];
-    }
+    double R[9], t[3];
+    cam_from_state(d, s, cam, s + d.off_frame + 7 * f, R, t);
     const int model = d.model[cam];
     const double* intr = s + cam * KB_MAX_INTR;
     const int o0 = d.view_off[v], o1 = d.view_off[v + 1];
@@ -737,40 +973,13 @@ __global__ void __launch_bounds__(256) k_cost(KbDev d, int gate, int which) {
   if (threadIdx.x == 0) d.costpart[blockIdx.x] = ((part[0] + part[1]) + part[2]) + part[3];
 }
 
-// fixed-order block reduction helper (one block of 256)
-__device__ double block_sum(const double* in, int n, double* sh) {
-  double s = 0.0;
-  for (int q = threadIdx.x; q < n; q += blockDim.x) s += in[q];
+// fixed-order block reduction (one block of 256)
+__device__ double block_reduce(double s, double* sh, bool is_max) {
   sh[threadIdx.x] = s;
   __syncthreads();
   for (int o = blockDim.x / 2; o > 0; o >>= 1) {
-    if ((int)threadIdx.x < o) sh[threadIdx.x] += sh[threadIdx.x + o];
-    __syncthreads();
-  }
-  const double r = sh[0];
-  __syncthreads();
-  return r;
-}
-__device__ double block_max(const double* in, int n, int stride, double* sh) {
-  double s = 0.0;
-  for (int q = threadIdx.x; q < n; q += blockDim.x) s = fmax(s, in[(size_t)q * stride]);
-  sh[threadIdx.x] = s;
-  __syncthreads();
-  for (int o = blockDim.x / 2; o > 0; o >>= 1) {
-    if ((int)threadIdx.x < o) sh[threadIdx.x] = fmax(sh[threadIdx.x], sh[threadIdx.x + o]);
-    __syncthreads();
-  }
-  const double r = sh[0];
-  __syncthreads();
-  return r;
-}
-__device__ double block_sum_strided(const double* in, int n, int stride, double* sh) {
-  double s = 0.0;
-  for (int q = threadIdx.x; q < n; q += blockDim.x) s += in[(size_t)q * stride];
-  sh[threadIdx.x] = s;
-  __syncthreads();
-  for (int o = blockDim.x / 2; o > 0; o >>= 1) {
-    if ((int)threadIdx.x < o) sh[threadIdx.x] += sh[threadIdx.x + o];
+    if ((int)threadIdx.x < o)
+      sh[threadIdx.x] = is_max ? fmax(sh[threadIdx.x], sh[threadIdx.x + o]) : sh[threadIdx.x] + sh[threadIdx.x + o];
     __syncthreads();
   }
   const double r = sh[0];
@@ -778,29 +987,51 @@ __device__ double block_sum_strided(const double* in, int n, int stride, double*
   return r;
 }
 
-// red[0] = cost (sum of costpart); with stats: red[1] = dx.dx, red[2] = dx.rhs, red[3] = max|dx|
-__global__ void __launch_bounds__(256) k_reduce(KbDev d, int gate, int with_stats) {
-  KbCtrl* c = d.ctrl;
-  if (gate && (c->done || !c->solve_ok)) return;
+__global__ void __launch_bounds__(256) k_reduce_cost(KbDev d) {
   __shared__ double sh[256];
-  const double cost = block_sum(d.costpart, d.nblk_cost, sh);
-  double dd = 0.0, dr = 0.0, mx = 0.0;
-  if (with_stats) {
-    mx = block_max(d.statpart, d.nblk_bs, 3, sh);
-    dd = block_sum_strided(d.statpart + 1, d.nblk_bs, 3, sh);
-    dr = block_sum_strided(d.statpart + 2, d.nblk_bs, 3, sh);
-  }
+  double s = 0.0;
+  for (int q = threadIdx.x; q < d.nblk_cost; q += blockDim.x) s += d.costpart[q];
+  s = block_reduce(s, sh, false);
   if (threadIdx.x == 0) {
-    d.red_local[0] = cost;
-    d.red_local[1] = dd + (with_stats ? d.camstat[1] : 0.0);
-    d.red_local[2] = dr + (with_stats ? d.camstat[2] : 0.0);
-    d.red_local[3] = with_stats ? fmax(mx, d.camstat[0]) : 0.0;
+    d.red_local[0] = s;
+    d.red_local[1] = d.red_local[2] = d.red_local[3] = 0.0;
   }
 }
 
-// ---------------------------------------------------------------------------------------------
-// Optimizer2 + trust-region state machine
-// ---------------------------------------------------------------------------------------------
+// k_post: per-block [cost, max, dd, dr] of k_backsub (+ camera part) -> red_local; then the policy
+__global__ void __launch_bounds__(256) k_post(KbDev d, int with_policy) {
+  KbCtrl* c = d.ctrl;
+  if (c->done) return;
+  __shared__ double sh[256];
+  if (c->solve_ok) {
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+    for (int q = threadIdx.x; q < d.nblk_bs; q += blockDim.x) {
+      const double* bp = d.bpart + (size_t)q * 4;
+      s0 += bp[0];
+      s1 = fmax(s1, bp[1]);
+      s2 += bp[2];
+      s3 += bp[3];
+    }
+    s0 = block_reduce(s0, sh, false);
+    s1 = block_reduce(s1, sh, true);
+    s2 = block_reduce(s2, sh, false);
+    s3 = block_reduce(s3, sh, false);
+    if (threadIdx.x == 0) {
+      d.red_local[0] = s0;
+      d.red_local[1] = s2 + d.camstat[1];
+      d.red_local[2] = s3 + d.camstat[2];
+      d.red_local[3] = fmax(s1, d.camstat[0]);
+    }
+  }
+  if (with_policy && threadIdx.x == 0) pol_post(c, d, d.red_local);
+}
+
+__global__ void k_pol_post(KbDev d) {
+  KbCtrl* c = d.ctrl;
+  if (c->done) return;
+  pol_post(c, d, d.red);
+}
+
 __global__ void k_pol_init(KbDev d, KbOpts o) {
   KbCtrl* c = d.ctrl;
   const double J = d.red[0];
@@ -833,109 +1064,6 @@ __global__ void k_pol_init(KbDev d, KbOpts o) {
   c->passes = 0;
 }
 
-// while-condition (Optimizer2.cpp:215-219) + TrustRegionPolicy::solveSystem prelude (:39-52)
-// + LM lambda schedule (LevenbergMarquardtTrustRegionPolicy.cpp:50-84) or GN (always build).
-__global__ void k_pol_pre(KbDev d) {
-  KbCtrl* c = d.ctrl;
-  if (c->done) return;
-  const bool cont = c->iterations < c->max_iterations && c->failed_iterations < c->max_iterations &&
-                    ((c->deltaX > c->eps_x && fabs(c->deltaJ) > c->eps_j) || c->lin_fail);
-  if (!cont) {
-    c->done = 1;
-    return;
-  }
-  const double J = c->J;
-  if (c->prev_failed) {
-    c->pol_J = J;
-  } else {
-    c->pol_pJ = c->last_succ;
-    c->last_succ = J;
-    c->pol_J = J;
-  }
-  c->solve_ok = 1;
-  if (c->policy == 0) {
-    if (c->first) {
-      c->do_build = 1;
-    } else {
-      const double d2 = c->lambda * c->dxdx + c->dxrhs;  // dx^T (lambda dx + rhs)
-      const double rho = (c->pol_pJ - c->pol_J) / d2;
-      if (c->prev_failed) {
-        c->mu *= 2;
-        c->lambda *= c->mu;
-        c->do_build = 0;
-      } else if (rho <= 0) {
-        c->mu *= 10;
-        c->lambda *= c->mu;
-        c->do_build = 0;
-      } else {
-        c->do_build = 1;
-        if (c->lambda > 1e-16) {
-          const double gamma = 3.0, beta = 2.0;
-          const double u1 = 1 / gamma;
-          const double u2 = 1 - (beta - 1) * pow((2 * rho - 1), 3.0);
-          if (u1 > u2)
-            c->lambda *= u1;
-          else
-            c->lambda *= u2;
-          c->mu = beta;
-        } else {
-          c->lambda = 1e-15;
-        }
-      }
-    }
-  } else {
-    c->do_build = 1;
-  }
-  c->first = 0;
-}
-
-// accept / revert (Optimizer2.cpp:221-259)
-__global__ void k_pol_post(KbDev d) {
-  KbCtrl* c = d.ctrl;
-  if (c->done) return;
-  double J = 0.0, dX = c->deltaX;
-  int accepted = 0;
-  if (!c->solve_ok) {
-    c->prev_failed = 1;
-    c->lin_fail = 1;
-    c->failed_iterations++;
-    J = NAN;
-  } else {
-    J = d.red[0];
-    dX = d.red[3];
-    c->dxdx = d.red[1];
-    c->dxrhs = d.red[2];
-    c->deltaX = dX;
-    c->J = J;
-    c->deltaJ = c->p_J - J;
-    if (c->policy == 0) {
-      if (c->deltaJ < 0.0) {
-        c->failed_iterations++;
-        c->prev_failed = 1;
-      } else {
-        c->cur = 1 - c->cur;
-        c->p_J = J;
-        c->prev_failed = 0;
-        accepted = 1;
-      }
-    } else {
-      c->cur = 1 - c->cur;
-      c->p_J = J;
-      accepted = 1;
-    }
-    c->iterations++;
-  }
-  if (c->n_trace < d.trace_cap) {
-    double* tr = d.trace + 4 * c->n_trace;
-    tr[0] = J;
-    tr[1] = c->lambda;
-    tr[2] = dX;
-    tr[3] = accepted;
-    c->n_trace++;
-  }
-  c->passes++;
-}
-
 // per-call update (kb_apply_update): all DVs from state[cur] -> state[1-cur]
 __global__ void __launch_bounds__(256) k_update_all(KbDev d) {
   KbCtrl* c = d.ctrl;
@@ -949,10 +1077,6 @@ __global__ void __launch_bounds__(256) k_update_all(KbDev d) {
   }
   if (t < N - 1) update_pose(in + d.off_base + 7 * t, d.dx + d.col_base[t], out + d.off_base + 7 * t);
   if (t < d.F) update_pose(in + d.off_frame + 7 * t, d.dx + d.C + 6 * t, out + d.off_frame + 7 * t);
-}
-
-__global__ void k_set_cur(KbDev d, int flip) {
-  if (flip) d.ctrl->cur = 1 - d.ctrl->cur;
 }
 
 // f64 MFMA fragment-layout self test: D = A * B (16x16x16 in 4 k-steps) with asymmetric A and B;

@@ -158,3 +158,25 @@ def test_run_gn_full_size_properties(capi):
     g2.run_gn(5)
     assert np.array_equal(s1, g2.get_state())
     assert np.isfinite(J1) and J1 < 2.0 * p.n_corners * 2 * 0.09
+
+
+def test_comm_path_single_rank_is_bitwise_identical(capi):
+    """The sharded code path (stage-2 column sum, RCCL all-reduce of [camera sums | Schur sums] and of the
+    cost/step statistics, separate policy kernel) run over a 1-rank communicator must reproduce the
+    single-GPU path bit for bit (same fixed reduction order)."""
+    p = PROBLEMS["c4_small"]()
+    a = capi.Solver(p)
+    a.set_state(p.state_init)
+    ra = a.optimize()
+    b = capi.Solver(p)
+    b.comm_init(capi.comm_unique_id(), 1, 0)
+    b.set_state(p.state_init)
+    rb = b.optimize()
+    assert np.array_equal(a.get_state(), b.get_state())
+    assert ra["iterations"] == rb["iterations"] and ra["J_final"] == rb["J_final"]
+    b.set_state(p.state_init)
+    b.build()
+    a.set_state(p.state_init)
+    a.build()
+    for k in ("Hcc", "gc", "Hff", "Hfc"):
+        assert np.array_equal(a.normal_blocks()[k], b.normal_blocks()[k])
