@@ -62,15 +62,15 @@ struct kb_handle {
   bool uploaded = false;
   std::vector<void*> allocs;
   // loop
-  hipGraphExec_t graph = nullptr;
+  hipGraphExec_t graph = nullptr;  // captured pass of graph_policy
+  int graph_policy = -1;
   int graph_trace_cap = 0;
   double* trace = nullptr;
   int trace_cap = 0;
   // sharding
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
-  double* psum_local = nullptr;  // [Wtot] finished column sums of this rank (sharded runs)
-  double* psum_red = nullptr;    // [Wtot] all-reduced
+  double* psum_red = nullptr;  // [Wtot] all-reduced column sums (sharded runs)
   // build-kernel timing
   double build_ms = 0.0;
 
@@ -122,6 +122,7 @@ kb_handle* kb_create(const kb_layout* L) {
   KbDev& d = h->d;
   d.N = h->N;
   d.F = h->F;
+  d.K = h->K;
   int c = 0;
   for (int i = 0; i < h->N; ++i) {
     const int n = nintr_host(L->cam_model[i]);
@@ -155,13 +156,12 @@ kb_handle* kb_create(const kb_layout* L) {
   d.off_frame = h->N * KB_MAX_INTR + 7 * (h->N - 1);
   d.gframes = (h->F + 511) / 512;
   d.nblk = (h->F + d.gframes - 1) / d.gframes;
-  d.nblk_bs = (h->F + 3) / 4;
+  d.nblk_bs = h->F;  // k_backsub: one block per frame
   d.nsplit = std::max(1, (4 + h->N - 1) / h->N);  // >= 4 waves per build block
   d.wpb = h->N * d.nsplit;
   h->WPB = d.wpb;
   d.W = h->W;
   d.Wtot = h->N * 136 + h->W + 1;
-  d.npart = kColsumRows;
   if (h->W + 1 > kMaxM * 256 || 64 * d.wpb > 512) {
     fail("kb_create: camera block / rig too large for the build kernel");
     delete h;
@@ -182,7 +182,9 @@ kb_handle* kb_create(const kb_layout* L) {
   rc |= h->alloc(&d.zf, 6 * (size_t)h->F);
   rc |= h->alloc(&d.part, (size_t)d.nblk * d.Wtot);
   rc |= h->alloc(&d.part8, (size_t)kColsumRows * d.Wtot);
-  d.psum = d.part8;
+  rc |= h->alloc(&d.psum_local, (size_t)d.Wtot);
+  d.psum = d.psum_local;
+  rc |= h->alloc(&d.ticket, 16);
   rc |= h->alloc(&d.Hcc, (size_t)h->C * h->C);
   rc |= h->alloc(&d.gc, (size_t)h->C);
   rc |= h->alloc(&d.cost_build, 2);
@@ -217,10 +219,10 @@ kb_handle* kb_create(const kb_layout* L) {
   {
     const int N = h->N, C = h->C, WPB = d.wpb;
     h->lds_build = sizeof(double) * (WPB * 64 * XS + WPB * 256 + N * (256 + 256 + 64 + 36 + 36 + 8) + 36 + 8 + 6 * C +
-                                     36 + 6 * C + 8);
+                                     36 + 6 * C + 8 + 18 * N * (N - 1) + (3 * h->K <= kTargetLds ? 3 * h->K : 0));
     h->lds_camexp = sizeof(double) * (N * 256 + N * N * 36);
     h->lds_schur = sizeof(double) * (6 * C + 36 + 8);
-    h->lds_solve = sizeof(double) * (C * C + N * 256 + N * N * 36 + C);
+    h->lds_solve = sizeof(double) * (C * (C + 1) / 2 + 2 * C + N * 256 + 2 * N * N * 36) + sizeof(int) * (C + C * (C - 1) / 2);
     h->solve_threads = C <= 64 ? 64 : 256;
     if (h->lds_build > 160 * 1024 || h->lds_solve > 160 * 1024 || h->lds_camexp > 160 * 1024) {
       fail("kb_create: LDS budget exceeded for this rig");
@@ -372,25 +374,21 @@ static int allreduce_red(kb_handle* h) {
   return 0;
 }
 
-// stage-1 column sums of the block partials (+ finish and all-reduce when sharded)
+// column sums of the block partials (finished in-kernel) + all-reduce over ranks when sharded
 static int launch_colsum(kb_handle* h, int gate) {
   KbDev& d = h->d;
   hipLaunchKernelGGL(k_colsum, dim3((d.Wtot + 63) / 64, kColsumRows), dim3(256), 0, h->stream, d, gate);
   KB_HIP(hipGetLastError());
-  if (h->comm) {
-    hipLaunchKernelGGL(k_colsum_final, dim3((d.Wtot + 255) / 256), dim3(256), 0, h->stream, d, h->psum_local, gate);
-    KB_HIP(hipGetLastError());
-    KB_NCCL(ncclAllReduce(h->psum_local, h->psum_red, d.Wtot, ncclDouble, ncclSum, h->comm, h->stream));
-  }
+  if (h->comm) KB_NCCL(ncclAllReduce(d.psum_local, h->psum_red, d.Wtot, ncclDouble, ncclSum, h->comm, h->stream));
   return 0;
 }
 
 static int launch_build(kb_handle* h, int gate, int fuse) {
   KbDev& d = h->d;
-  hipLaunchKernelGGL(k_pre, dim3(1), dim3(256), 0, h->stream, d, gate);
+  // per-call path: camera chain first; in the loop the previous k_post (or loop start) computed it
+  if (!gate) hipLaunchKernelGGL(k_pre, dim3(1), dim3(256), 0, h->stream, d, 0);
   void* args[] = {&d, &gate, &fuse};
   KB_HIP(hipLaunchKernel(h->fn_build, dim3(d.nblk), dim3(64 * d.wpb), args, h->lds_build, h->stream));
-  KB_HIP(hipGetLastError());
   return 0;
 }
 
@@ -408,7 +406,8 @@ static int launch_solve(kb_handle* h, int gate, int do_update) {
 }
 
 static int launch_backsub(kb_handle* h, int gate, int do_update, int with_cost) {
-  hipLaunchKernelGGL(k_backsub, dim3(h->d.nblk_bs), dim3(256), 0, h->stream, h->d, gate, do_update, with_cost);
+  hipLaunchKernelGGL(k_backsub, dim3(h->d.nblk_bs), dim3(64 * std::min(h->N, 8)), 0, h->stream, h->d, gate, do_update,
+                     with_cost);
   KB_HIP(hipGetLastError());
   return 0;
 }
@@ -521,10 +520,12 @@ int kb_get_normal_blocks(kb_handle* h, double* Hff, double* Hfc, double* gf, dou
 // ---------------------------------------------------------------- device-resident loop
 // One pass: pol_pre | prep build colsum (gated on do_build) | schur colsum [allreduce A] camexpand solve |
 // backsub cost reduce [allreduce stats] | pol_post.  Every kernel early-exits once ctrl->done is set.
-static int enqueue_pass(kb_handle* h) {
+// One optimizer pass: build (+ fused Schur) | [schur, LM only] | colsum [all-reduce] | solve |
+// backsub + cost | post (reduce, accept/revert, next pass prelude + camera chain).
+static int enqueue_pass(kb_handle* h, int policy) {
   KbDev& d = h->d;
-  if (launch_build(h, 1, 1)) return -1;  // k_pre (policy prelude + chain) + k_build fused with the Schur step
-  if (launch_schur(h, 1)) return -1;     // only for LM passes that keep the system (lambda change)
+  if (launch_build(h, 1, 1)) return -1;
+  if (policy == 0 && launch_schur(h, 1)) return -1;  // LM passes that keep the system (lambda change)
   if (launch_colsum(h, 1)) return -1;
   if (launch_solve(h, 1, 1)) return -1;
   if (launch_backsub(h, 1, 1, 1)) return -1;
@@ -532,7 +533,7 @@ static int enqueue_pass(kb_handle* h) {
   KB_HIP(hipGetLastError());
   if (h->comm) {
     if (allreduce_red(h)) return -1;
-    hipLaunchKernelGGL(k_pol_post, dim3(1), dim3(1), 0, h->stream, d);
+    hipLaunchKernelGGL(k_policy, dim3(1), dim3(256), 0, h->stream, d);
     KB_HIP(hipGetLastError());
   }
   return 0;
@@ -553,24 +554,30 @@ static int ensure_trace(kb_handle* h, int cap) {
   return 0;
 }
 
-static int ensure_graph(kb_handle* h) {
-  if (h->graph) return 0;
+static int ensure_graph(kb_handle* h, int policy) {
+  if (h->graph && h->graph_policy == policy) return 0;
+  if (h->graph) {
+    KB_HIP(hipGraphExecDestroy(h->graph));
+    h->graph = nullptr;
+  }
   hipGraph_t g = nullptr;
   KB_HIP(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
-  int rc = enqueue_pass(h);
+  int rc = enqueue_pass(h, policy);
   hipError_t e = hipStreamEndCapture(h->stream, &g);
   if (rc) return rc;
   if (e != hipSuccess) return fail(std::string("hipStreamEndCapture: ") + hipGetErrorString(e));
   KB_HIP(hipGraphInstantiate(&h->graph, g, nullptr, nullptr, 0));
   KB_HIP(hipGraphDestroy(g));
+  h->graph_policy = policy;
   return 0;
 }
 
 static int loop_start(kb_handle* h, const KbOpts& o) {
-  // evaluateError on the start state (Optimizer2.cpp:192-196), then optimizationStarting
+  // evaluateError on the start state (Optimizer2.cpp:192-196), optimizationStarting, first prelude
   if (launch_cost(h, 0)) return -1;
   if (allreduce_red(h)) return -1;
   hipLaunchKernelGGL(k_pol_init, dim3(1), dim3(1), 0, h->stream, h->d, o);
+  hipLaunchKernelGGL(k_pre, dim3(1), dim3(256), 0, h->stream, h->d, 1);
   KB_HIP(hipGetLastError());
   return 0;
 }
@@ -585,7 +592,7 @@ int kb_optimize(kb_handle* h, const kb_optimizer_options* opts, kb_solution* out
   KbOpts o{opts->policy, opts->max_iterations, opts->lambda_init, opts->convergence_dx, opts->convergence_dj};
   if (loop_start(h, o)) return -1;
   const bool graph = opts->use_graph != 0 && !h->comm;  // RCCL calls stay eager
-  if (graph && ensure_graph(h)) return -1;
+  if (graph && ensure_graph(h, opts->policy)) return -1;
   const int every = opts->sync_every > 0 ? opts->sync_every : 4;
   KbCtrl ctrl{};
   int passes = 0;
@@ -594,7 +601,7 @@ int kb_optimize(kb_handle* h, const kb_optimizer_options* opts, kb_solution* out
     for (int i = 0; i < n; ++i) {
       if (graph) {
         KB_HIP(hipGraphLaunch(h->graph, h->stream));
-      } else if (enqueue_pass(h)) {
+      } else if (enqueue_pass(h, opts->policy)) {
         return -1;
       }
     }
@@ -634,13 +641,13 @@ int kb_run_gn_iterations(kb_handle* h, int32_t n_iter, double* seconds) {
   KbOpts o{1, 0x3fffffff, 0.0, -1.0, -1.0};
   if (loop_start(h, o)) return -1;
   const bool graph = !h->comm;
-  if (graph && ensure_graph(h)) return -1;
+  if (graph && ensure_graph(h, 1)) return -1;
   KB_HIP(hipStreamSynchronize(h->stream));
   const auto t0 = std::chrono::steady_clock::now();
   for (int i = 0; i < n_iter; ++i) {
     if (graph) {
       KB_HIP(hipGraphLaunch(h->graph, h->stream));
-    } else if (enqueue_pass(h)) {
+    } else if (enqueue_pass(h, 1)) {
       return -1;
     }
   }
@@ -663,8 +670,10 @@ int kb_build_kernel_stats(kb_handle* h, double* avg_ms, double* bytes_per_launch
   KB_HIP(hipEventCreate(&e1));
   // warm; the timed launches are the fused build + Schur step exactly as one GN pass runs it
   hipLaunchKernelGGL(k_pre, dim3(1), dim3(256), 0, h->stream, h->d, 0);
+  KbDev dd = h->d;
+  dd.host_lambda = 0.0;  // GN pass: no conditioner
   int g0 = 0, f1 = 1;
-  void* args[] = {&h->d, &g0, &f1};
+  void* args[] = {&dd, &g0, &f1};
   KB_HIP(hipLaunchKernel(h->fn_build, dim3(h->d.nblk), dim3(64 * h->d.wpb), args, h->lds_build, h->stream));
   double tot = 0.0;
   for (int r = 0; r < reps; ++r) {
@@ -715,11 +724,10 @@ int kb_comm_init(kb_handle* h, const void* uid, int32_t nranks, int32_t rank) {
   KB_NCCL(ncclCommInitRank(&h->comm, nranks, id, rank));
   h->nranks = nranks;
   h->rank = rank;
-  if (h->alloc(&h->psum_local, (size_t)h->d.Wtot) || h->alloc(&h->psum_red, (size_t)h->d.Wtot)) return -1;
+  if (h->alloc(&h->psum_red, (size_t)h->d.Wtot)) return -1;
   double* rr = nullptr;
   if (h->alloc(&rr, 8)) return -1;
   h->d.psum = h->psum_red;
-  h->d.npart = 1;
   h->d.red = rr;
   if (h->graph) {
     hipGraphExecDestroy(h->graph);
@@ -728,6 +736,26 @@ int kb_comm_init(kb_handle* h, const void* uid, int32_t nranks, int32_t rank) {
   KB_HIP(hipStreamSynchronize(h->stream));
   return 0;
 }
+
+#ifdef KB_STAMPS
+// diagnostic build only: run n GN passes eagerly and return the last pass's phase stamps (100 MHz ticks)
+int kb_diag_stamps(kb_handle* h, int n, unsigned long long* out, int cap) {
+  KB_HIP(hipSetDevice(h->device));
+  unsigned long long* st = nullptr;
+  KB_HIP(hipMalloc(&st, sizeof(unsigned long long) * 64));
+  KB_HIP(hipMemset(st, 0, sizeof(unsigned long long) * 64));
+  h->d.stamps = st;
+  KbOpts o{1, 0x3fffffff, 0.0, -1.0, -1.0};
+  if (ensure_trace(h, 64) || loop_start(h, o)) return -1;
+  for (int i = 0; i < n; ++i)
+    if (enqueue_pass(h, 1)) return -1;
+  KB_HIP(hipStreamSynchronize(h->stream));
+  KB_HIP(hipMemcpy(out, st, sizeof(unsigned long long) * std::min(cap, 64), hipMemcpyDeviceToHost));
+  h->d.stamps = nullptr;
+  hipFree(st);
+  return 0;
+}
+#endif
 
 int kb_selftest_mfma(double* max_err) {
   double* d = nullptr;

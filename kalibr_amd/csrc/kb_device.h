@@ -9,7 +9,7 @@
 //   Lf [F][36], Yf [F][6][C], zf [F][6]       frame Schur factors (k_build fused / k_schur)
 //   part [nblk][Wtot]              per-block partials: per-camera 16x16 upper sums (N*136) |
 //                                  sum Y^T Y upper (C(C+1)/2) | sum Y^T z (C) | #non-PD frames (1)
-//   part8 [8][Wtot]                stage-1 column sums of part (k_colsum), finished by the consumer
+//   part8 [8][Wtot]                stage-1 column sums of part (k_colsum); psum_local [Wtot] the finished sums
 //   bpart [nblk_bs][4]             k_backsub_cost: cost, max|dx|, dx.dx, dx.rhs per block
 #pragma once
 #include <hip/hip_runtime.h>
@@ -35,12 +35,11 @@ struct KbOpts {
 constexpr int kColsumRows = 8;  // stage-1 row splits of the block partial reduction
 
 struct KbDev {
-  int N, F, V, NC, C, ncols, S;
+  int N, F, V, NC, C, ncols, S, K;  // K = target corners
   int off_base, off_frame;
   int gframes, nblk, nblk_bs, nblk_cost;
   int nsplit, wpb;   // k_build: waves per block = N * nsplit
   int W, Wtot;       // W = C(C+1)/2 + C ; Wtot = N*136 + W + 1
-  int npart;         // rows of psum the consumers add up (8 locally, 1 after an all-reduce)
   int trace_cap;
   double host_lambda;  // conditioner for the per-call (non-gated) path
   int model[KB_MAX_CAMS], nintr[KB_MAX_CAMS], col_intr[KB_MAX_CAMS], col_base[KB_MAX_CAMS];
@@ -59,8 +58,10 @@ struct KbDev {
   double *Hff, *Hfc, *gf;
   double *Lf, *Yf, *zf;
   double* part;   // [nblk][Wtot]
-  double* part8;  // [8][Wtot] (this rank)
-  double* psum;   // consumer view: part8 (npart 8) or the all-reduced [Wtot] (npart 1)
+  double* part8;       // [8][Wtot] stage-1 column sums
+  double* psum_local;  // [Wtot] finished column sums of this rank (last k_colsum block)
+  double* psum;        // consumer view: psum_local, or its all-reduce over ranks
+  unsigned* ticket;    // k_colsum arrival counter (re-armed by the last block)
   double *Hcc, *gc, *cost_build;
   double *dx, *rhs;
   double* bpart;     // [nblk_bs][4]
@@ -70,7 +71,20 @@ struct KbDev {
   double* red;       // [4] (all-reduced; aliases red_local on one GPU)
   double* trace;
   KbCtrl* ctrl;
+  unsigned long long* stamps;  // diagnostic build only (KB_STAMPS): s_memrealtime per phase
 };
+
+#ifdef KB_STAMPS
+#define KB_STAMP(d, i)                                                              \
+  do {                                                                              \
+    if (threadIdx.x == 0 && blockIdx.x == 0 && (d).stamps)                          \
+      (d).stamps[i] = __builtin_amdgcn_s_memrealtime();                             \
+  } while (0)
+#else
+#define KB_STAMP(d, i) \
+  do {                 \
+  } while (0)
+#endif
 
 // 16x16 upper-packed helpers (row-major upper: a <= b)
 __host__ __device__ __forceinline__ int d16_index(int a, int b) { return a * 16 - a * (a - 1) / 2 + (b - a); }

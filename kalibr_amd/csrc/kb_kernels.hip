@@ -28,8 +28,17 @@ typedef double v4d __attribute__((ext_vector_type(4)));
 
 #define KB_WAVE_SYNC() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
 
+// broadcast of a double from a wave-uniform lane (v_readlane_b32 x2, no LDS round trip)
+__device__ __forceinline__ double readlane_d(double v, int lane) {
+  const unsigned long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffull), lane);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+  return __longlong_as_double(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+
 constexpr int XS = 17;       // LDS row stride (doubles) of the 64 x 16 Jacobian-row tile
 constexpr int kMaxM = 24;    // largest Schur-sum entries per thread: (W + 1) <= M * blockDim
+constexpr int kTargetLds = 1536;  // target corners staged in k_build's LDS when 3 * n_target <= this
 
 // ---------------------------------------------------------------------------------------------
 // rigid-transform helpers
@@ -201,19 +210,12 @@ __device__ void pol_post(KbCtrl* c, const KbDev& d, const double* red) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// k_pre: [policy prelude] + camera chain L_i (R|t) and K_{i,j} (one block)
+// camera chain of the accepted state: L_i (R|t) = B_{i-1}..B_0 and K_{i,j} (one block)
 // ---------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_pre(KbDev d, int gate) {
-  KbCtrl* c = d.ctrl;
-  if (gate) {
-    if (c->done) return;
-    if (threadIdx.x == 0) pol_pre(c);
-    __syncthreads();
-    if (c->done || !c->do_build) return;
-  }
+__device__ void prep_block(const KbDev& d) {
   __shared__ double sR[KB_MAX_CAMS][9], st[KB_MAX_CAMS][3];  // baseline B_j
   __shared__ double LR[KB_MAX_CAMS][9], Lt[KB_MAX_CAMS][3];
-  const double* s = d.state + (size_t)c->cur * d.S;
+  const double* s = d.state + (size_t)d.ctrl->cur * d.S;
   const int N = d.N;
   if (threadIdx.x < N - 1) pose_rt(s + d.off_base + 7 * threadIdx.x, sR[threadIdx.x], st[threadIdx.x]);
   __syncthreads();
@@ -241,6 +243,23 @@ __global__ void __launch_bounds__(256) k_pre(KbDev d, int gate) {
     }
     d.camK[idx] = val;
   }
+}
+
+// policy prelude of the next pass + its camera chain (one block)
+__device__ void next_pass_block(const KbDev& d) {
+  KbCtrl* c = d.ctrl;
+  if (threadIdx.x == 0 && !c->done) pol_pre(c);
+  __syncthreads();
+  if (c->done || !c->do_build) return;
+  prep_block(d);
+}
+
+// k_pre: gate 0 -> camera chain only (per-call build); gate 1 -> prelude of the first pass + its chain
+__global__ void __launch_bounds__(256) k_pre(KbDev d, int gate) {
+  if (gate)
+    next_pass_block(d);
+  else
+    prep_block(d);
 }
 
 // in-place 6x6 Cholesky (lower) in LDS, by one thread; returns 0 if not PD
@@ -337,8 +356,21 @@ __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
   double* L = Fc + 6 * C;            // [36]
   double* Y = L + 36;                // [6][C]
   double* z = Y + 6 * C;             // [8]
+  double* Kl = z + 8;                // [N(N-1)/2][36] K_{i,j}, j < i, at (i(i-1)/2 + j)
+  double* tg = Kl + 18 * N * (N - 1);  // [n_target][3] target corners (when staged)
   __shared__ int okl;
   const double* s = d.state + (size_t)c->cur * d.S;
+  const bool tg_lds = d.K * 3 <= kTargetLds;
+  if (tg_lds)
+    for (int q = threadIdx.x; q < 3 * d.K; q += nth) tg[q] = d.target[q];
+  for (int q = threadIdx.x; q < 18 * N * (N - 1); q += nth) {
+    const int e = q % 36, ij = q / 36;
+    int i = 1;
+    while (i * (i + 1) / 2 <= ij) ++i;
+    const int j = ij - i * (i - 1) / 2;
+    Kl[q] = d.camK[(size_t)(i * N + j) * 36 + e];
+  }
+  const double* tgt = tg_lds ? tg : d.target;
   const double lam = gate ? c->lambda : d.host_lambda;
   const double lam2 = lam * lam;
   const int W = d.W, Wt = W - C;
@@ -351,6 +383,7 @@ __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
     ab[m] = (fuse && e < Wt) ? d.tri[e] : 0;
   }
   if (threadIdx.x == 0) okl = 1;
+  KB_STAMP(d, 16);
   for (int q = threadIdx.x; q < N * 256; q += nth) camsum[q] = 0.0;
   __syncthreads();
 
@@ -377,7 +410,7 @@ __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
           for (int q = 0; q < 16; ++q) xr[r][q] = 0.0;
         if (k < o1) {
           const int cid = d.cid[k];
-          const double X0 = d.target[3 * cid], X1 = d.target[3 * cid + 1], X2 = d.target[3 * cid + 2];
+          const double X0 = tgt[3 * cid], X1 = tgt[3 * cid + 1], X2 = tgt[3 * cid + 2];
           const double p0 = R[0] * X0 + R[1] * X1 + R[2] * X2 + t[0];
           const double p1 = R[3] * X0 + R[4] * X1 + R[5] * X2 + t[1];
           const double p2 = R[6] * X0 + R[7] * X1 + R[8] * X2 + t[2];
@@ -435,15 +468,24 @@ __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
       wv[9] = t[0]; wv[10] = t[1]; wv[11] = t[2];
       wv[12] = fp[4]; wv[13] = fp[5]; wv[14] = fp[6];
     }
+    KB_STAMP(d, 17);
     __syncthreads();
+    KB_STAMP(d, 18);
     for (int q = threadIdx.x; q < N * 256; q += nth) {
       const int qc = q >> 8, e = q & 255;
-      double sacc = 0.0;
-      for (int k = 0; k < NS; ++k) sacc += Hw[(k * N + qc) * 256 + e];
+      double hv[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const double h = Hw[((k < NS ? k : 0) * N + qc) * 256 + e];
+        hv[k] = (k < NS) ? h : 0.0;
+      }
+      const double cs = camsum[q];
+      const double sacc = ((hv[0] + hv[1]) + hv[2]) + hv[3];
       Hv[q] = sacc;
-      camsum[q] += sacc;
+      camsum[q] = cs + sacc;
     }
     __syncthreads();
+    KB_STAMP(d, 19);
     if (wave < N) {  // expansion of view (f, cam = wave) through the 6-D chains
       const int vc = wave;
       const bool has = d.frame_vcam[f * N + vc] >= 0;
@@ -501,7 +543,7 @@ __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
         const int e = q - 42, j = e / 36, ab2 = e % 36, a = ab2 / 6, b = ab2 % 6;
         double sacc = 0.0;
         for (int i = j + 1; i < N; ++i) {
-          const double* K = d.camK + (size_t)(i * N + j) * 36;
+          const double* K = Kl + (i * (i - 1) / 2 + j) * 36;
 #pragma unroll
           for (int k = 0; k < 6; ++k) sacc += Pv[i * 36 + a * 6 + k] * K[k * 6 + b];
         }
@@ -509,19 +551,24 @@ __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
         d.Hfc[((size_t)f * 6 + a) * C + d.col_base[j] + b] = sacc;
       }
     }
+    KB_STAMP(d, 20);
     if (fuse) {
       __syncthreads();
+      KB_STAMP(d, 21);
       if (threadIdx.x == 0) {
         for (int q = 0; q < 36; ++q) L[q] = Fh[q] + ((q % 7 == 0) ? lam2 : 0.0);
         if (!chol6(L)) okl = 0;
         for (int q = 0; q < 36; ++q) d.Lf[(size_t)f * 36 + q] = L[q];
       }
       __syncthreads();
+      KB_STAMP(d, 22);
       schur_forward(d, f, L, Fc, Fg, Y, z);
       __syncthreads();
+      KB_STAMP(d, 23);
       schur_accumulate<M>(C, Wt, W, Y, z, ab, acc);
     }
     __syncthreads();
+    KB_STAMP(d, 24);
   }
   double* prow = d.part + (size_t)blockIdx.x * d.Wtot;
   for (int q = threadIdx.x; q < N * 136; q += nth) {
@@ -538,6 +585,7 @@ __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
     }
     if (threadIdx.x == 0) prow[N * 136 + W] = okl ? 0.0 : 1.0;  // non-PD frame blocks (summed)
   }
+  KB_STAMP(d, 25);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -588,12 +636,15 @@ __global__ void __launch_bounds__(256) k_schur(KbDev d, int gate) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// k_colsum: part8[ry][e] = sum_{b = ry mod 8} part[b][e]  (fixed order), grid (ceil(Wtot/64), 8)
+// k_colsum: column sums of the block partials in fixed order: block (bx, ry) sums rows b = ry (mod 8) of
+// 64 columns into part8[ry]; the last-arriving block (agent-scope release/acquire ticket, guide G16 recipe)
+// finishes psum_local[e] = sum_r part8[r][e].  Grid (ceil(Wtot/64), 8).
 // ---------------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_colsum(KbDev d, int gate) {
   KbCtrl* c = d.ctrl;
   if (gate && c->done) return;
   __shared__ double part[4][64];
+  __shared__ int last;
   const int l = threadIdx.x & 63, w4 = threadIdx.x >> 6;
   const int e = blockIdx.x * 64 + l, ry = blockIdx.y;
   double s = 0.0;
@@ -602,24 +653,35 @@ __global__ void __launch_bounds__(256) k_colsum(KbDev d, int gate) {
   part[w4][l] = s;
   __syncthreads();
   if (w4 == 0 && e < d.Wtot) d.part8[(size_t)ry * d.Wtot + e] = ((part[0][l] + part[1][l]) + part[2][l]) + part[3][l];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned total = gridDim.x * gridDim.y;
+    const unsigned t = __hip_atomic_fetch_add(d.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = (t == total - 1);
+  }
+  __syncthreads();
+  if (!last) return;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  for (int q = threadIdx.x; q < d.Wtot; q += blockDim.x) {
+    double v[kColsumRows];
+#pragma unroll
+    for (int r = 0; r < kColsumRows; ++r) v[r] = d.part8[(size_t)r * d.Wtot + q];
+    double acc = 0.0;
+#pragma unroll
+    for (int r = 0; r < kColsumRows; ++r) acc += v[r];
+    d.psum_local[q] = acc;
+  }
+  if (threadIdx.x == 0) *d.ticket = 0u;  // re-armed for the next launch (ordered by the kernel boundary)
 }
 
-// k_colsum_final: [8][Wtot] -> [Wtot] before the all-reduce (sharded runs)
-__global__ void __launch_bounds__(256) k_colsum_final(KbDev d, double* out, int gate) {
-  KbCtrl* c = d.ctrl;
-  if (gate && c->done) return;
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= d.Wtot) return;
-  double s = 0.0;
-  for (int r = 0; r < kColsumRows; ++r) s += d.part8[(size_t)r * d.Wtot + e];
-  out[e] = s;
-}
-
-__device__ __forceinline__ double psum_at(const KbDev& d, int e) {
-  double s = 0.0;
-  for (int r = 0; r < d.npart; ++r) s += d.psum[(size_t)r * d.Wtot + e];
-  return s;
-}
+__device__ __forceinline__ double psum_at(const KbDev& d, int e) { return d.psum[e]; }
 
 // ---------------------------------------------------------------------------------------------
 // camera block from the per-camera local sums (H_cc, g_c), shared by k_camexpand and k_solve
@@ -708,227 +770,363 @@ __global__ void __launch_bounds__(256) k_camexpand(KbDev d) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// k_solve: S = H_cc + lambda^2 I - sum Y^T Y, b = g_c - sum Y^T z; LDL^T (one barrier per column);
-// dx_c; camera DV update into state[1-cur]
+// k_solve: S = H_cc + lambda^2 I - sum Y^T Y, b = g_c - sum Y^T z (packed lower, staged in LDS);
+// LDL^T (one wave when C <= 64, else the block with one barrier per column); dx_c; camera DV update
 // ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ int tri_row(int q) {  // row of packed-lower index q
+  int r = (int)((sqrtf(8.0f * (float)q + 1.0f) - 1.0f) * 0.5f);
+  while (r * (r + 1) / 2 > q) --r;
+  while ((r + 1) * (r + 2) / 2 <= q) ++r;
+  return r;
+}
+
+__device__ double cam_entry_l(const int N, const int* ci, const double* Hs, const double* T, const double* K, int p,
+                              int q) {
+  const int kp = ci[p] >> 16, ip = (ci[p] >> 8) & 0xff, xp = ci[p] & 0xff;
+  const int kq = ci[q] >> 16, iq = (ci[q] >> 8) & 0xff, xq = ci[q] & 0xff;
+  double s = 0.0;
+  if (kp == 0 && kq == 0) {
+    if (ip == iq) s = Hs[ip * 256 + (6 + xp) * 16 + 6 + xq];
+  } else if (kp == 0 && kq == 1) {
+    if (iq < ip) {
+      const double* Kk = K + (size_t)(ip * N + iq) * 36;
+#pragma unroll
+      for (int b = 0; b < 6; ++b) s += Hs[ip * 256 + (6 + xp) * 16 + b] * Kk[b * 6 + xq];
+    }
+  } else if (kp == 1 && kq == 0) {
+    if (ip < iq) {
+      const double* Kk = K + (size_t)(iq * N + ip) * 36;
+#pragma unroll
+      for (int a = 0; a < 6; ++a) s += Kk[a * 6 + xp] * Hs[iq * 256 + a * 16 + 6 + xq];
+    }
+  } else {
+    const int m = ip > iq ? ip : iq;
+    for (int i = m + 1; i < N; ++i) {
+      const double* Kk = K + (size_t)(i * N + ip) * 36;
+      const double* Tq = T + (size_t)(i * N + iq) * 36;
+#pragma unroll
+      for (int a = 0; a < 6; ++a) s += Kk[a * 6 + xp] * Tq[a * 6 + xq];
+    }
+  }
+  return s;
+}
+
+__device__ double cam_grad_l(const int N, const int* ci, const double* Hs, const double* K, int p) {
+  const int kp = ci[p] >> 16, ip = (ci[p] >> 8) & 0xff, xp = ci[p] & 0xff;
+  if (kp == 0) return Hs[ip * 256 + (6 + xp) * 16 + 15];
+  double s = 0.0;
+  for (int i = ip + 1; i < N; ++i) {
+    const double* Kk = K + (size_t)(i * N + ip) * 36;
+#pragma unroll
+    for (int a = 0; a < 6; ++a) s += Kk[a * 6 + xp] * Hs[i * 256 + a * 16 + 15];
+  }
+  return s;
+}
+
+// column-major packed lower index of (i, j), i >= j (== row-major packed upper index of (j, i))
+__device__ __forceinline__ int cidx(int i, int j, int C) { return j * (2 * C - j - 1) / 2 + i; }
+
 __global__ void __launch_bounds__(256) k_solve(KbDev d, int gate, int do_update) {
   KbCtrl* c = d.ctrl;
   if (gate && c->done) return;
   extern __shared__ __attribute__((aligned(16))) double sm[];
-  const int N = d.N, C = d.C, W = d.W, Wt = W - C, nth = blockDim.x;
-  double* S = sm;               // [C][C] (lower part used)
-  double* Hs = S + C * C;       // [N][256]
-  double* T = Hs + N * 256;     // [N][N][36]
-  double* bv = T + N * N * 36;  // [C]
+  const int N = d.N, C = d.C, W = d.W, Wt = W - C, nth = blockDim.x, tid = threadIdx.x;
+  const int Cp = C * (C + 1) / 2;
+  double* S = sm;                    // column-major packed lower [Cp]
+  double* bv = S + Cp;               // [C]
+  double* gl = bv + C;               // [C]
+  double* Hs = gl + C;               // [N][256]
+  double* T = Hs + N * 256;          // [N][N][36]
+  double* K = T + N * N * 36;        // [N][N][36]
+  int* ci = (int*)(K + N * N * 36);  // [C]
+  int* ptab = ci + C;                // [(C-1)C/2] pair table of the trailing triangle: ii<<16 | jj
   __shared__ int okl;
-  __shared__ double red[4][64];
   const double lam = gate ? c->lambda : d.host_lambda;
   const double lam2 = lam * lam;
-  cam_load(d, Hs, T);
-  for (int q = threadIdx.x; q < C * C; q += nth) {
-    const int a = q / C, b = q % C;
-    if (b > a) continue;
-    S[q] = cam_entry(d, Hs, T, a, b) + ((a == b) ? lam2 : 0.0) - psum_at(d, N * 136 + upper_index(b, a, C));
+  KB_STAMP(d, 0);
+#ifdef KB_STAMPS
+  if (tid == 0 && d.stamps) d.stamps[40] = __builtin_amdgcn_s_memtime();
+#endif
+  // phase A: stage K, column info, per-camera sums and the Schur sums in LDS (one row: psum)
+  for (int q = tid; q < N * N * 36; q += nth) K[q] = d.camK[q];
+  for (int q = tid; q < C; q += nth) ci[q] = d.colinfo[q];
+  for (int q = tid; q < (C - 1) * C / 2; q += nth) {
+    const int ii = tri_row(q);
+    ptab[q] = (ii << 16) | (q - ii * (ii + 1) / 2);
   }
-  for (int p = threadIdx.x; p < C; p += nth) {
-    const double g = cam_grad(d, Hs, p);
-    bv[p] = g - psum_at(d, N * 136 + Wt + p);
-    d.gc[p] = g;
-    d.rhs[p] = g;
+  for (int q = tid; q < N * 256; q += nth) {
+    const int cam = q >> 8, a = (q & 255) >> 4, b = q & 15;
+    const int lo = a < b ? a : b, hi = a < b ? b : a;
+    Hs[q] = d.psum[cam * 136 + d16_index(lo, hi)];
   }
-  if (threadIdx.x == 0) {
-    okl = (c->solve_ok != 0) && !(psum_at(d, N * 136 + W) > 0.0);
+  for (int e = tid; e < Wt; e += nth) S[e] = -d.psum[N * 136 + e];  // upper (a,b) row-major == lower (b,a) col-major
+  for (int p = tid; p < C; p += nth) bv[p] = -d.psum[N * 136 + Wt + p];
+  if (tid == 0) okl = (c->solve_ok != 0) && !(d.psum[N * 136 + W] > 0.0);
+  __syncthreads();
+  KB_STAMP(d, 1);
+  // phase B: camera block expansion
+  for (int q = tid; q < N * N * 36; q += nth) {
+    const int e = q % 36, ik = q / 36, i = ik / N, k = ik % N;
+    double s = 0.0;
+    if (k < i) {
+      const int a = e / 6, b = e % 6;
+#pragma unroll
+      for (int m = 0; m < 6; ++m) s += Hs[i * 256 + a * 16 + m] * K[(i * N + k) * 36 + m * 6 + b];
+    }
+    T[q] = s;
+  }
+  if (tid == 0) {
     double s = 0.0;
     for (int i = 0; i < N; ++i) s += Hs[i * 256 + 255];
     d.cost_build[0] = s;
   }
   __syncthreads();
-  // LDL^T in place: after step k, S[i][k] = Ltilde[i][k] * D_k for i > k, S[k][k] = D_k
-  for (int k = 0; k < C; ++k) {
-    const double dk = S[k * C + k];
-    if (threadIdx.x == 0 && !(dk > 0.0)) okl = 0;
-    const int n = C - k - 1;
-    const double rdk = 1.0 / dk;
-    for (int q = threadIdx.x; q < n * n; q += nth) {
-      const int i = k + 1 + q / n, j = k + 1 + q % n;
-      if (j <= i) S[i * C + j] -= S[i * C + k] * S[j * C + k] * rdk;
-    }
-    __syncthreads();
+  for (int e = tid; e < Cp; e += nth) {
+    const int ab = d.tri[e], j = ab >> 16, i = ab & 0xffff;  // lower (i, j), i >= j
+    S[e] += cam_entry_l(N, ci, Hs, T, K, i, j) + ((i == j) ? lam2 : 0.0);
   }
-  const bool ok = okl != 0;
-  if (!ok) {
-    if (threadIdx.x == 0) c->solve_ok = 0;
+  for (int p = tid; p < C; p += nth) {
+    const double g = cam_grad_l(N, ci, Hs, K, p);
+    bv[p] += g;
+    gl[p] = g;
+    d.gc[p] = g;
+    d.rhs[p] = g;
+  }
+  __syncthreads();
+  KB_STAMP(d, 2);
+  // phase C: right-looking LDL^T on (i, j) pairs, k < j <= i: S[i][j] -= S[i][k] S[j][k] / D_k.
+  // Column k is final during step k and every pair is written by one thread: each thread gathers its pairs'
+  // operands first (8 per batch), then writes, so one step costs ~2 LDS round trips.
+  const bool one_wave = C <= 64;
+  if (!one_wave || tid < 64) {
+    const int nt = one_wave ? 64 : nth;
+    for (int k = 0; k < C; ++k) {
+      const double Dk = S[cidx(k, k, C)];
+      if (tid == 0 && !(Dk > 0.0)) okl = 0;
+      const double rdk = 1.0 / Dk;
+      const int n = C - k - 1, np = n * (n + 1) / 2;
+      for (int q0 = tid; q0 < np; q0 += 8 * nt) {
+        double a[8], b[8], v[8];
+        int ix[8];
+        bool ok[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {  // unconditional (clamped) loads: no per-element branch
+          const int q = q0 + u * nt;
+          ok[u] = q < np;
+          const int pt = ptab[ok[u] ? q : 0], i = k + 1 + (pt >> 16), j = k + 1 + (pt & 0xffff);
+          ix[u] = cidx(i, j, C);
+          a[u] = S[cidx(i, k, C)];
+          b[u] = S[cidx(j, k, C)];
+          v[u] = S[ix[u]];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (ok[u]) S[ix[u]] = v[u] - a[u] * b[u] * rdk;
+      }
+      if (one_wave)
+        KB_WAVE_SYNC();
+      else
+        __syncthreads();
+    }
+  }
+  if (tid >= 64) return;
+  const int lane = tid;
+  KB_WAVE_SYNC();
+  KB_STAMP(d, 3);
+  if (!okl) {
+    if (lane == 0) c->solve_ok = 0;
     return;
   }
-  if (threadIdx.x < 64) {
-    const int lane = threadIdx.x;
-    double x[2];
+  // phase D: Ltilde y = b, z = D^-1 y, Ltilde^T x = z; row i held by lane i & 63 (slot i >> 6).
+  // Each 16-step chunk first preloads the lane's matrix entries into registers.
+  double x[2], rD[2];
+#pragma unroll
+  for (int sl = 0; sl < 2; ++sl) {
+    const int i = lane + 64 * sl;
+    x[sl] = (i < C) ? bv[i] : 0.0;
+    rD[sl] = (i < C) ? 1.0 / S[cidx(i, i, C)] : 0.0;
+  }
+  for (int k0 = 0; k0 < C; k0 += 16) {
+    double Lr[2][16];
 #pragma unroll
     for (int sl = 0; sl < 2; ++sl) {
       const int i = lane + 64 * sl;
-      x[sl] = (i < C) ? bv[i] : 0.0;
-    }
-    // forward Ltilde y = b (column oriented), then z = D^-1 y
-    for (int k = 0; k < C; ++k) {
-      const double yk = __shfl(x[k >> 6], k & 63);
-      const double rdk = 1.0 / S[k * C + k];
 #pragma unroll
-      for (int sl = 0; sl < 2; ++sl) {
-        const int i = lane + 64 * sl;
-        if (i > k && i < C) x[sl] -= S[i * C + k] * rdk * yk;
+      for (int u = 0; u < 16; ++u) {
+        const bool use = i < C && k0 + u < i;
+        const double val = S[use ? cidx(i, k0 + u, C) : 0];
+        Lr[sl][u] = use ? val : 0.0;
       }
     }
 #pragma unroll
-    for (int sl = 0; sl < 2; ++sl) {
-      const int i = lane + 64 * sl;
-      if (i < C) x[sl] /= S[i * C + i];
-    }
-    // backward Ltilde^T x = z
-    for (int k = C - 1; k >= 0; --k) {
-      const double xk = __shfl(x[k >> 6], k & 63);
+    for (int u = 0; u < 16; ++u) {
+      const int k = k0 + u;
+      if (k < C) {
+        const double yk = readlane_d(x[k >> 6], k & 63) * readlane_d(rD[k >> 6], k & 63);
 #pragma unroll
-      for (int sl = 0; sl < 2; ++sl) {
-        const int i = lane + 64 * sl;
-        if (i < k) x[sl] -= S[k * C + i] / S[i * C + i] * xk;
+        for (int sl = 0; sl < 2; ++sl) x[sl] -= Lr[sl][u] * yk;  // Lr = 0 unless i > k
       }
     }
-    double mx = 0.0, dd = 0.0, dr = 0.0;
+  }
+#pragma unroll
+  for (int sl = 0; sl < 2; ++sl) x[sl] *= rD[sl];
+  for (int k1 = C - 1; k1 >= 0; k1 -= 16) {
+    double Lc[2][16];
 #pragma unroll
     for (int sl = 0; sl < 2; ++sl) {
       const int i = lane + 64 * sl;
-      if (i < C) {
-        const double g = d.gc[i];
-        d.dx[i] = x[sl];
-        mx = fmax(mx, fabs(x[sl]));
-        dd += x[sl] * x[sl];
-        dr += x[sl] * g;
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int k = k1 - u;
+        const bool use = k >= 0 && i < k;
+        const double val = S[use ? cidx(k, i, C) : 0];
+        Lc[sl][u] = use ? val * rD[sl] : 0.0;
       }
     }
-    red[0][lane] = mx;
-    red[1][lane] = dd;
-    red[2][lane] = dr;
-    KB_WAVE_SYNC();
-    if (lane == 0) {
-      double a0 = 0.0, a1 = 0.0, a2 = 0.0;
-      for (int q = 0; q < 64; ++q) {
-        a0 = fmax(a0, red[0][q]);
-        a1 += red[1][q];
-        a2 += red[2][q];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int k = k1 - u;
+      if (k >= 0) {
+        const double xk = readlane_d(x[k >> 6], k & 63);
+#pragma unroll
+        for (int sl = 0; sl < 2; ++sl) x[sl] -= Lc[sl][u] * xk;  // Lc = 0 unless i < k
       }
-      d.camstat[0] = a0;
-      d.camstat[1] = a1;
-      d.camstat[2] = a2;
     }
+  }
+  KB_STAMP(d, 4);
+  double mx = 0.0, dd = 0.0, dr = 0.0;
+#pragma unroll
+  for (int sl = 0; sl < 2; ++sl) {
+    const int i = lane + 64 * sl;
+    if (i < C) {
+      const double g = gl[i];
+      d.dx[i] = x[sl];
+      mx = fmax(mx, fabs(x[sl]));
+      dd += x[sl] * x[sl];
+      dr += x[sl] * g;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    mx = fmax(mx, __shfl_xor(mx, o));
+    dd += __shfl_xor(dd, o);
+    dr += __shfl_xor(dr, o);
+  }
+  if (lane == 0) {
+    d.camstat[0] = mx;
+    d.camstat[1] = dd;
+    d.camstat[2] = dr;
   }
   if (do_update) {
-    __syncthreads();
     const double* in = d.state + (size_t)c->cur * d.S;
     double* out = d.state + (size_t)(1 - c->cur) * d.S;
-    for (int q = threadIdx.x; q < N * KB_MAX_INTR; q += nth) {
-      const int cm = q / KB_MAX_INTR, x = q % KB_MAX_INTR;
-      out[q] = in[q] + ((x < d.nintr[cm]) ? d.dx[d.col_intr[cm] + x] : 0.0);
+    for (int q0 = 0; q0 < N * KB_MAX_INTR; q0 += 64) {  // wave-uniform trip count (shuffles inside)
+      const int q = q0 + lane;
+      const int cm = q / KB_MAX_INTR, xi = q % KB_MAX_INTR;
+      const int col = (q < N * KB_MAX_INTR && xi < d.nintr[cm]) ? d.col_intr[cm] + xi : 0;
+      const double v0 = __shfl(x[0], col & 63), v1 = __shfl(x[1], col & 63);
+      const double dv = (col >> 6) ? v1 : v0;
+      if (q < N * KB_MAX_INTR) out[q] = in[q] + ((xi < d.nintr[cm]) ? dv : 0.0);
     }
-    if (threadIdx.x < N - 1) {
-      const int j = threadIdx.x;
-      update_pose(in + d.off_base + 7 * j, d.dx + d.col_base[j], out + d.off_base + 7 * j);
+    for (int j = 0; j < N - 1; ++j) {
+      double d6[6];
+#pragma unroll
+      for (int q = 0; q < 6; ++q) {
+        const int col = d.col_base[j] + q;  // wave-uniform
+        d6[q] = __shfl(x[col >> 6], col & 63);
+      }
+      if (lane == 0) update_pose(in + d.off_base + 7 * j, d6, out + d.off_base + 7 * j);
     }
   }
+  KB_STAMP(d, 5);
+#ifdef KB_STAMPS
+  if (tid == 0 && d.stamps) d.stamps[41] = __builtin_amdgcn_s_memtime();
+#endif
 }
 
 // ---------------------------------------------------------------------------------------------
-// k_backsub: one wave per frame: dx_f = L^-T (z - Y dx_c); pose update; cost of the frame's views at the
-// new state (evaluateError fused); per-block [cost, max|dx|, dx.dx, dx.rhs]
+// k_backsub: one block per frame, one wave per camera view: every wave forms dx_f = L^-T (z - Y dx_c)
+// (6 wave dot products), wave 0 stores dx / pose, each wave then evaluates the cost of its view at the new
+// state (evaluateError fused); per-frame [cost, max|dx|, dx.dx, dx.rhs]
 // ---------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_backsub(KbDev d, int gate, int do_update, int with_cost) {
+__global__ void __launch_bounds__(512) k_backsub(KbDev d, int gate, int do_update, int with_cost) {
   KbCtrl* c = d.ctrl;
   if (gate && (c->done || !c->solve_ok)) return;
-  __shared__ double st4[4][4];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int f = blockIdx.x * 4 + wave;
+  __shared__ double sc[8];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+  const int f = blockIdx.x;
   const int C = d.C, N = d.N;
-  double mx = 0.0, dd = 0.0, dr = 0.0, cost = 0.0;
-  if (f < d.F) {
-    double w[6];
+  double w[6];
 #pragma unroll
-    for (int r = 0; r < 6; ++r) {
-      double s = 0.0;
-      for (int q = lane; q < C; q += 64) s += d.Yf[((size_t)f * 6 + r) * C + q] * d.dx[q];
+  for (int r = 0; r < 6; ++r) {
+    double s = 0.0;
+    for (int q = lane; q < C; q += 64) s += d.Yf[((size_t)f * 6 + r) * C + q] * d.dx[q];
 #pragma unroll
-      for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-      w[r] = d.zf[(size_t)f * 6 + r] - s;
-    }
-    const double* L = d.Lf + (size_t)f * 36;
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    w[r] = d.zf[(size_t)f * 6 + r] - s;
+  }
+  const double* L = d.Lf + (size_t)f * 36;
 #pragma unroll
-    for (int r = 5; r >= 0; --r) {
-      double s = w[r];
+  for (int r = 5; r >= 0; --r) {
+    double s = w[r];
 #pragma unroll
-      for (int k = r + 1; k < 6; ++k) s -= L[k * 6 + r] * w[k];
-      w[r] = s / L[r * 6 + r];
-    }
-    if (lane < 6) {
-      double xv = w[0];
+    for (int k = r + 1; k < 6; ++k) s -= L[k * 6 + r] * w[k];
+    w[r] = s / L[r * 6 + r];
+  }
+  if (wave == 0 && lane < 6) {
+    double xv = w[0];
 #pragma unroll
-      for (int r = 1; r < 6; ++r) xv = (lane == r) ? w[r] : xv;
-      d.dx[C + 6 * f + lane] = xv;
-      d.rhs[C + 6 * f + lane] = d.gf[(size_t)f * 6 + lane];
-    }
-#pragma unroll
-    for (int r = 0; r < 6; ++r) {
-      const double g = d.gf[(size_t)f * 6 + r];
-      mx = fmax(mx, fabs(w[r]));
-      dd += w[r] * w[r];
-      dr += w[r] * g;
-    }
-    if (do_update) {
-      const double* s0 = d.state + (size_t)c->cur * d.S;
-      double* s1 = d.state + (size_t)(1 - c->cur) * d.S;
-      double np[7];
-      update_pose(s0 + d.off_frame + 7 * f, w, np);  // every lane: the new pose stays in registers
-      if (lane == 0)
-        for (int q = 0; q < 7; ++q) s1[d.off_frame + 7 * f + q] = np[q];
-      if (with_cost) {
-        for (int cm = 0; cm < N; ++cm) {
-          const int v = d.frame_vcam[f * N + cm];
-          if (v < 0) continue;
-          double R[9], t[3];
-          cam_from_state(d, s1, cm, np, R, t);
-          const int model = d.model[cm];
-          const double* intr = s1 + cm * KB_MAX_INTR;
-          const int o0 = d.view_off[v], o1 = d.view_off[v + 1];
-          for (int k = o0 + lane; k < o1; k += 64) {
-            const int cid = d.cid[k];
-            const double X0 = d.target[3 * cid], X1 = d.target[3 * cid + 1], X2 = d.target[3 * cid + 2];
-            const double p0 = R[0] * X0 + R[1] * X1 + R[2] * X2 + t[0];
-            const double p1 = R[3] * X0 + R[4] * X1 + R[5] * X2 + t[1];
-            const double p2 = R[6] * X0 + R[7] * X1 + R[8] * X2 + t[2];
-            double u, vv;
-            project(model, intr, p0, p1, p2, u, vv);
-            const double2 yv = d.y[k];
-            const double e0 = yv.x - u, e1 = yv.y - vv;
-            cost += e0 * e0 + e1 * e1;
-          }
+    for (int r = 1; r < 6; ++r) xv = (lane == r) ? w[r] : xv;
+    d.dx[C + 6 * f + lane] = xv;
+    d.rhs[C + 6 * f + lane] = d.gf[(size_t)f * 6 + lane];
+  }
+  double cost = 0.0;
+  if (do_update) {
+    const double* s0 = d.state + (size_t)c->cur * d.S;
+    double* s1 = d.state + (size_t)(1 - c->cur) * d.S;
+    double np[7];
+    update_pose(s0 + d.off_frame + 7 * f, w, np);  // every lane: the new pose stays in registers
+    if (wave == 0 && lane == 0)
+      for (int q = 0; q < 7; ++q) s1[d.off_frame + 7 * f + q] = np[q];
+    if (with_cost) {
+      for (int cm = wave; cm < N; cm += nw) {
+        const int v = d.frame_vcam[f * N + cm];
+        if (v < 0) continue;
+        double R[9], t[3];
+        cam_from_state(d, s1, cm, np, R, t);
+        const int model = d.model[cm];
+        const double* intr = s1 + cm * KB_MAX_INTR;
+        const int o0 = d.view_off[v], o1 = d.view_off[v + 1];
+        for (int k = o0 + lane; k < o1; k += 64) {
+          const int cid = d.cid[k];
+          const double X0 = d.target[3 * cid], X1 = d.target[3 * cid + 1], X2 = d.target[3 * cid + 2];
+          const double p0 = R[0] * X0 + R[1] * X1 + R[2] * X2 + t[0];
+          const double p1 = R[3] * X0 + R[4] * X1 + R[5] * X2 + t[1];
+          const double p2 = R[6] * X0 + R[7] * X1 + R[8] * X2 + t[2];
+          double u, vv;
+          project(model, intr, p0, p1, p2, u, vv);
+          const double2 yv = d.y[k];
+          const double e0 = yv.x - u, e1 = yv.y - vv;
+          cost += e0 * e0 + e1 * e1;
         }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) cost += __shfl_xor(cost, o);
       }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) cost += __shfl_xor(cost, o);
     }
   }
-  if (lane == 0) {
-    st4[wave][0] = cost;
-    st4[wave][1] = mx;
-    st4[wave][2] = dd;
-    st4[wave][3] = dr;
-  }
+  if (lane == 0) sc[wave] = cost;
   __syncthreads();
   if (threadIdx.x == 0) {
     double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-    for (int q = 0; q < (int)(blockDim.x >> 6); ++q) {
-      a0 += st4[q][0];
-      a1 = fmax(a1, st4[q][1]);
-      a2 += st4[q][2];
-      a3 += st4[q][3];
+    for (int q = 0; q < nw; ++q) a0 += sc[q];
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+      const double g = d.gf[(size_t)f * 6 + r];
+      a1 = fmax(a1, fabs(w[r]));
+      a2 += w[r] * w[r];
+      a3 += w[r] * g;
     }
-    double* bp = d.bpart + (size_t)blockIdx.x * 4;
+    double* bp = d.bpart + (size_t)f * 4;
     bp[0] = a0;
     bp[1] = a1;
     bp[2] = a2;
@@ -998,38 +1196,67 @@ __global__ void __launch_bounds__(256) k_reduce_cost(KbDev d) {
   }
 }
 
-// k_post: per-block [cost, max, dd, dr] of k_backsub (+ camera part) -> red_local; then the policy
+// k_post: per-frame [cost, max, dd, dr] of k_backsub (+ camera part) -> red_local; then (one GPU) the
+// accept/revert policy, the next pass's prelude and its camera chain
 __global__ void __launch_bounds__(256) k_post(KbDev d, int with_policy) {
   KbCtrl* c = d.ctrl;
   if (c->done) return;
-  __shared__ double sh[256];
+  __shared__ double sh[4][4];
+  KB_STAMP(d, 8);
   if (c->solve_ok) {
     double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
     for (int q = threadIdx.x; q < d.nblk_bs; q += blockDim.x) {
-      const double* bp = d.bpart + (size_t)q * 4;
-      s0 += bp[0];
-      s1 = fmax(s1, bp[1]);
-      s2 += bp[2];
-      s3 += bp[3];
+      const double4 bp = reinterpret_cast<const double4*>(d.bpart)[q];
+      s0 += bp.x;
+      s1 = fmax(s1, bp.y);
+      s2 += bp.z;
+      s3 += bp.w;
     }
-    s0 = block_reduce(s0, sh, false);
-    s1 = block_reduce(s1, sh, true);
-    s2 = block_reduce(s2, sh, false);
-    s3 = block_reduce(s3, sh, false);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      s0 += __shfl_xor(s0, o);
+      s1 = fmax(s1, __shfl_xor(s1, o));
+      s2 += __shfl_xor(s2, o);
+      s3 += __shfl_xor(s3, o);
+    }
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+      sh[w][0] = s0;
+      sh[w][1] = s1;
+      sh[w][2] = s2;
+      sh[w][3] = s3;
+    }
+    __syncthreads();
     if (threadIdx.x == 0) {
-      d.red_local[0] = s0;
-      d.red_local[1] = s2 + d.camstat[1];
-      d.red_local[2] = s3 + d.camstat[2];
-      d.red_local[3] = fmax(s1, d.camstat[0]);
+      double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+      for (int q = 0; q < (int)(blockDim.x >> 6); ++q) {
+        a0 += sh[q][0];
+        a1 = fmax(a1, sh[q][1]);
+        a2 += sh[q][2];
+        a3 += sh[q][3];
+      }
+      d.red_local[0] = a0;
+      d.red_local[1] = a2 + d.camstat[1];
+      d.red_local[2] = a3 + d.camstat[2];
+      d.red_local[3] = fmax(a1, d.camstat[0]);
     }
   }
-  if (with_policy && threadIdx.x == 0) pol_post(c, d, d.red_local);
+  KB_STAMP(d, 9);
+  if (!with_policy) return;
+  if (threadIdx.x == 0) pol_post(c, d, d.red_local);
+  __syncthreads();
+  KB_STAMP(d, 10);
+  next_pass_block(d);
+  KB_STAMP(d, 11);
 }
 
-__global__ void k_pol_post(KbDev d) {
+// sharded runs: the policy after the all-reduce of red
+__global__ void __launch_bounds__(256) k_policy(KbDev d) {
   KbCtrl* c = d.ctrl;
   if (c->done) return;
-  pol_post(c, d, d.red);
+  if (threadIdx.x == 0) pol_post(c, d, d.red);
+  __syncthreads();
+  next_pass_block(d);
 }
 
 __global__ void k_pol_init(KbDev d, KbOpts o) {
