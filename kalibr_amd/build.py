@@ -26,5 +26,13 @@ def build(force=False):
     return OUT
 
 
+def build_stamps():
+    """Diagnostic variant with per-phase s_memrealtime stamps (tools/diag_stamps.py only)."""
+    out = os.path.join(HERE, "libkalibr_hip_stamps.so")
+    subprocess.run([HIPCC] + FLAGS + ["-DKB_STAMPS", "-o", out + ".tmp", SRC, "-lrccl"], check=True)
+    os.replace(out + ".tmp", out)
+    return out
+
+
 if __name__ == "__main__":
     print(build(force=True))

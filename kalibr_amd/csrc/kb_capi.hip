@@ -58,6 +58,7 @@ struct kb_handle {
   int mb = 24, ms = 24;  // Schur entries per thread of k_build / k_schur (template bucket)
   const void* fn_build = nullptr;
   const void* fn_schur = nullptr;
+  const void* fn_solve = nullptr;
   int cur = 0;  // host mirror of ctrl->cur for the per-call path
   bool uploaded = false;
   std::vector<void*> allocs;
@@ -223,7 +224,13 @@ kb_handle* kb_create(const kb_layout* L) {
     h->lds_camexp = sizeof(double) * (N * 256 + N * N * 36);
     h->lds_schur = sizeof(double) * (6 * C + 36 + 8);
     h->lds_solve = sizeof(double) * (C * (C + 1) / 2 + 2 * C + N * 256 + 2 * N * N * 36) + sizeof(int) * (C + C * (C - 1) / 2);
-    h->solve_threads = C <= 64 ? 64 : 256;
+    h->solve_threads = 256;
+    h->fn_solve = C <= 16   ? (const void*)k_solve<16>
+                  : C <= 24 ? (const void*)k_solve<24>
+                  : C <= 32 ? (const void*)k_solve<32>
+                  : C <= 48 ? (const void*)k_solve<48>
+                  : C <= 64 ? (const void*)k_solve<64>
+                            : (const void*)k_solve<0>;
     if (h->lds_build > 160 * 1024 || h->lds_solve > 160 * 1024 || h->lds_camexp > 160 * 1024) {
       fail("kb_create: LDS budget exceeded for this rig");
       kb_destroy(h);
@@ -240,7 +247,7 @@ kb_handle* kb_create(const kb_layout* L) {
   hipFuncSetAttribute(h->fn_build, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_build);
   hipFuncSetAttribute((const void*)k_camexpand, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_camexp);
   hipFuncSetAttribute(h->fn_schur, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_schur);
-  hipFuncSetAttribute((const void*)k_solve, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_solve);
+  hipFuncSetAttribute(h->fn_solve, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_solve);
   if (hipStreamSynchronize(h->stream) != hipSuccess) {
     fail("kb_create: stream sync failed");
     kb_destroy(h);
@@ -400,7 +407,8 @@ static int launch_schur(kb_handle* h, int gate) {
 }
 
 static int launch_solve(kb_handle* h, int gate, int do_update) {
-  hipLaunchKernelGGL(k_solve, dim3(1), dim3(h->solve_threads), h->lds_solve, h->stream, h->d, gate, do_update);
+  void* args[] = {(void*)&h->d, (void*)&gate, (void*)&do_update};
+  KB_HIP(hipLaunchKernel(h->fn_solve, dim3(1), dim3(h->solve_threads), args, h->lds_solve, h->stream));
   KB_HIP(hipGetLastError());
   return 0;
 }

@@ -826,11 +826,106 @@ __device__ double cam_grad_l(const int N, const int* ci, const double* Hs, const
 // column-major packed lower index of (i, j), i >= j (== row-major packed upper index of (j, i))
 __device__ __forceinline__ int cidx(int i, int j, int C) { return j * (2 * C - j - 1) / 2 + i; }
 
+// batched global -> LDS staging of the k_solve inputs: every thread keeps U independent loads in flight
+// (a runtime-bounded copy loop would otherwise wait for each load before the next).  Items are laid out as
+// [camK N*N*36 | per-camera sums N*256 | Schur sums Wt | Schur rhs C | colinfo C] over one index space.
+template <int U>
+__device__ __forceinline__ void solve_stage(const KbDev& d, double* K, double* Hs, double* S, double* bv, int* ci,
+                                            int tid, int nth) {
+  const int N = d.N, C = d.C, Wt = d.W - C;
+  const int n0 = N * N * 36, n1 = n0 + N * 256, n2 = n1 + Wt, n3 = n2 + C, n4 = n3 + C;
+  for (int q0 = tid; q0 < n4; q0 += U * nth) {
+    double v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int q = min(q0 + u * nth, n4 - 1);
+      if (q < n0) {
+        v[u] = d.camK[q];
+      } else if (q < n1) {
+        const int r = q - n0, cam = r >> 8, a = (r & 255) >> 4, b = r & 15;
+        v[u] = d.psum[cam * 136 + (a < b ? d16_index(a, b) : d16_index(b, a))];
+      } else if (q < n3) {
+        v[u] = -d.psum[N * 136 + (q - n1)];  // Schur sums, then rhs (contiguous in psum)
+      } else {
+        v[u] = (double)d.colinfo[q - n3];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int q = q0 + u * nth;
+      if (q < n0)
+        K[q] = v[u];
+      else if (q < n1)
+        Hs[q - n0] = v[u];
+      else if (q < n2)
+        S[q - n1] = v[u];  // upper (a,b) row-major == lower (b,a) col-major
+      else if (q < n3)
+        bv[q - n2] = v[u];
+      else if (q < n4)
+        ci[q - n3] = (int)v[u];
+    }
+  }
+}
+
+// column of col-major packed lower index e (C columns)
+__device__ __forceinline__ int cidx_col(int e, int C) {
+  int j = (int)((2.0f * C + 1.0f - sqrtf((2.0f * C + 1.0f) * (2.0f * C + 1.0f) - 8.0f * (float)e)) * 0.5f);
+  j = max(0, min(j, C - 1));
+  while (j > 0 && j * (2 * C - j + 1) / 2 > e) --j;
+  while ((j + 1) * (2 * C - j) / 2 <= e) ++j;
+  return j;
+}
+
+// LDL^T + the three triangular solves of one wave, matrix rows in registers (lane i holds row i of the
+// trailing matrix, CM >= C padded with the identity).  Step k broadcasts row k with v_readlane (no LDS), and
+// lanes i > k apply S[i][j] -= (S[i][k] / D_k) S[k][j].  Row i freezes at step i, so lane i ends holding
+// Ltilde[i][k] D_k (k < i), D_i, and by symmetry of the trailing matrix Ltilde[k][i] D_i (k > i).
+template <int CM>
+__device__ __forceinline__ bool ldl_solve_reg(const double* S, const double* bv, int C, int lane, double& xo) {
+  double row[CM];
+#pragma unroll
+  for (int j = 0; j < CM; ++j) {
+    const bool in = lane < C && j < C;
+    const int a = lane > j ? lane : j, b = lane > j ? j : lane;
+    const double v = S[in ? cidx(a, b, C) : 0];
+    row[j] = in ? v : (lane == j ? 1.0 : 0.0);
+  }
+  double x = lane < C ? bv[lane] : 0.0;
+  bool ok = true;
+  double rD = 1.0;
+#pragma unroll
+  for (int k = 0; k < CM; ++k) {
+    const double Dk = readlane_d(row[k], k);
+    ok = ok && (Dk > 0.0);
+    const double rdk = 1.0 / Dk;
+    rD = (lane == k) ? rdk : rD;
+    const double f = (lane > k) ? row[k] * rdk : 0.0;
+#pragma unroll
+    for (int j = k + 1; j < CM; ++j) row[j] -= f * readlane_d(row[j], k);
+  }
+  // Ltilde y = b ; z = D^-1 y ; Ltilde^T x = z
+#pragma unroll
+  for (int k = 0; k < CM; ++k) {
+    const double yk = readlane_d(x, k) * readlane_d(rD, k);
+    x -= ((lane > k) ? row[k] : 0.0) * yk;
+  }
+  x *= rD;
+#pragma unroll
+  for (int k = CM - 1; k > 0; --k) {
+    const double wk = readlane_d(x, k);
+    x -= ((lane < k) ? row[k] * rD : 0.0) * wk;
+  }
+  xo = x;
+  return ok;
+}
+
+// CM > 0: one-wave register LDL^T for C <= CM (<= 64); CM == 0: block LDL^T in LDS for C > 64
+template <int CM>
 __global__ void __launch_bounds__(256) k_solve(KbDev d, int gate, int do_update) {
   KbCtrl* c = d.ctrl;
   if (gate && c->done) return;
   extern __shared__ __attribute__((aligned(16))) double sm[];
-  const int N = d.N, C = d.C, W = d.W, Wt = W - C, nth = blockDim.x, tid = threadIdx.x;
+  const int N = d.N, C = d.C, W = d.W, nth = blockDim.x, tid = threadIdx.x;
   const int Cp = C * (C + 1) / 2;
   double* S = sm;                    // column-major packed lower [Cp]
   double* bv = S + Cp;               // [C]
@@ -839,7 +934,7 @@ __global__ void __launch_bounds__(256) k_solve(KbDev d, int gate, int do_update)
   double* T = Hs + N * 256;          // [N][N][36]
   double* K = T + N * N * 36;        // [N][N][36]
   int* ci = (int*)(K + N * N * 36);  // [C]
-  int* ptab = ci + C;                // [(C-1)C/2] pair table of the trailing triangle: ii<<16 | jj
+  int* ptab = ci + C;                // [(C-1)C/2] pair table of the trailing triangle: ii<<16 | jj (CM == 0)
   __shared__ int okl;
   const double lam = gate ? c->lambda : d.host_lambda;
   const double lam2 = lam * lam;
@@ -848,19 +943,12 @@ __global__ void __launch_bounds__(256) k_solve(KbDev d, int gate, int do_update)
   if (tid == 0 && d.stamps) d.stamps[40] = __builtin_amdgcn_s_memtime();
 #endif
   // phase A: stage K, column info, per-camera sums and the Schur sums in LDS (one row: psum)
-  for (int q = tid; q < N * N * 36; q += nth) K[q] = d.camK[q];
-  for (int q = tid; q < C; q += nth) ci[q] = d.colinfo[q];
-  for (int q = tid; q < (C - 1) * C / 2; q += nth) {
-    const int ii = tri_row(q);
-    ptab[q] = (ii << 16) | (q - ii * (ii + 1) / 2);
-  }
-  for (int q = tid; q < N * 256; q += nth) {
-    const int cam = q >> 8, a = (q & 255) >> 4, b = q & 15;
-    const int lo = a < b ? a : b, hi = a < b ? b : a;
-    Hs[q] = d.psum[cam * 136 + d16_index(lo, hi)];
-  }
-  for (int e = tid; e < Wt; e += nth) S[e] = -d.psum[N * 136 + e];  // upper (a,b) row-major == lower (b,a) col-major
-  for (int p = tid; p < C; p += nth) bv[p] = -d.psum[N * 136 + Wt + p];
+  solve_stage<8>(d, K, Hs, S, bv, ci, tid, nth);
+  if (CM == 0)
+    for (int q = tid; q < (C - 1) * C / 2; q += nth) {
+      const int ii = tri_row(q);
+      ptab[q] = (ii << 16) | (q - ii * (ii + 1) / 2);
+    }
   if (tid == 0) okl = (c->solve_ok != 0) && !(d.psum[N * 136 + W] > 0.0);
   __syncthreads();
   KB_STAMP(d, 1);
@@ -882,7 +970,7 @@ __global__ void __launch_bounds__(256) k_solve(KbDev d, int gate, int do_update)
   }
   __syncthreads();
   for (int e = tid; e < Cp; e += nth) {
-    const int ab = d.tri[e], j = ab >> 16, i = ab & 0xffff;  // lower (i, j), i >= j
+    const int j = cidx_col(e, C), i = e - j * (2 * C - j - 1) / 2;  // lower (i, j), i >= j
     S[e] += cam_entry_l(N, ci, Hs, T, K, i, j) + ((i == j) ? lam2 : 0.0);
   }
   for (int p = tid; p < C; p += nth) {
@@ -894,24 +982,31 @@ __global__ void __launch_bounds__(256) k_solve(KbDev d, int gate, int do_update)
   }
   __syncthreads();
   KB_STAMP(d, 2);
-  // phase C: right-looking LDL^T on (i, j) pairs, k < j <= i: S[i][j] -= S[i][k] S[j][k] / D_k.
-  // Column k is final during step k and every pair is written by one thread: each thread gathers its pairs'
-  // operands first (8 per batch), then writes, so one step costs ~2 LDS round trips.
-  const bool one_wave = C <= 64;
-  if (!one_wave || tid < 64) {
-    const int nt = one_wave ? 64 : nth;
+  double x[2];
+  if constexpr (CM > 0) {
+    if (tid >= 64) return;
+    const bool ok = ldl_solve_reg<CM>(S, bv, C, tid, x[0]);
+    x[1] = 0.0;
+    if (!ok) okl = 0;
+    KB_WAVE_SYNC();
+    KB_STAMP(d, 3);
+    KB_STAMP(d, 4);
+  } else {
+    // phase C: right-looking LDL^T on (i, j) pairs, k < j <= i: S[i][j] -= S[i][k] S[j][k] / D_k.
+    // Column k is final during step k and every pair is written by one thread: each thread gathers its pairs'
+    // operands first (8 per batch), then writes, so one step costs ~2 LDS round trips.
     for (int k = 0; k < C; ++k) {
       const double Dk = S[cidx(k, k, C)];
       if (tid == 0 && !(Dk > 0.0)) okl = 0;
       const double rdk = 1.0 / Dk;
       const int n = C - k - 1, np = n * (n + 1) / 2;
-      for (int q0 = tid; q0 < np; q0 += 8 * nt) {
+      for (int q0 = tid; q0 < np; q0 += 8 * nth) {
         double a[8], b[8], v[8];
         int ix[8];
         bool ok[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {  // unconditional (clamped) loads: no per-element branch
-          const int q = q0 + u * nt;
+          const int q = q0 + u * nth;
           ok[u] = q < np;
           const int pt = ptab[ok[u] ? q : 0], i = k + 1 + (pt >> 16), j = k + 1 + (pt & 0xffff);
           ix[u] = cidx(i, j, C);
@@ -923,77 +1018,74 @@ __global__ void __launch_bounds__(256) k_solve(KbDev d, int gate, int do_update)
         for (int u = 0; u < 8; ++u)
           if (ok[u]) S[ix[u]] = v[u] - a[u] * b[u] * rdk;
       }
-      if (one_wave)
-        KB_WAVE_SYNC();
-      else
-        __syncthreads();
+      __syncthreads();
     }
+    if (tid >= 64) return;
+    KB_STAMP(d, 3);
+    // phase D: Ltilde y = b, z = D^-1 y, Ltilde^T x = z; row i held by lane i & 63 (slot i >> 6).
+    // Each 16-step chunk first preloads the lane's matrix entries into registers.
+    const int lane = tid;
+    double rD[2];
+#pragma unroll
+    for (int sl = 0; sl < 2; ++sl) {
+      const int i = lane + 64 * sl;
+      x[sl] = (i < C) ? bv[i] : 0.0;
+      rD[sl] = (i < C) ? 1.0 / S[cidx(i, i, C)] : 0.0;
+    }
+    for (int k0 = 0; k0 < C; k0 += 16) {
+      double Lr[2][16];
+#pragma unroll
+      for (int sl = 0; sl < 2; ++sl) {
+        const int i = lane + 64 * sl;
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          const bool use = i < C && k0 + u < i;
+          const double val = S[use ? cidx(i, k0 + u, C) : 0];
+          Lr[sl][u] = use ? val : 0.0;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int k = k0 + u;
+        if (k < C) {
+          const double yk = readlane_d(x[k >> 6], k & 63) * readlane_d(rD[k >> 6], k & 63);
+#pragma unroll
+          for (int sl = 0; sl < 2; ++sl) x[sl] -= Lr[sl][u] * yk;  // Lr = 0 unless i > k
+        }
+      }
+    }
+#pragma unroll
+    for (int sl = 0; sl < 2; ++sl) x[sl] *= rD[sl];
+    for (int k1 = C - 1; k1 >= 0; k1 -= 16) {
+      double Lc[2][16];
+#pragma unroll
+      for (int sl = 0; sl < 2; ++sl) {
+        const int i = lane + 64 * sl;
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          const int k = k1 - u;
+          const bool use = k >= 0 && i < k;
+          const double val = S[use ? cidx(k, i, C) : 0];
+          Lc[sl][u] = use ? val * rD[sl] : 0.0;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int k = k1 - u;
+        if (k >= 0) {
+          const double xk = readlane_d(x[k >> 6], k & 63);
+#pragma unroll
+          for (int sl = 0; sl < 2; ++sl) x[sl] -= Lc[sl][u] * xk;  // Lc = 0 unless i < k
+        }
+      }
+    }
+    KB_STAMP(d, 4);
   }
-  if (tid >= 64) return;
   const int lane = tid;
-  KB_WAVE_SYNC();
-  KB_STAMP(d, 3);
   if (!okl) {
     if (lane == 0) c->solve_ok = 0;
     return;
   }
-  // phase D: Ltilde y = b, z = D^-1 y, Ltilde^T x = z; row i held by lane i & 63 (slot i >> 6).
-  // Each 16-step chunk first preloads the lane's matrix entries into registers.
-  double x[2], rD[2];
-#pragma unroll
-  for (int sl = 0; sl < 2; ++sl) {
-    const int i = lane + 64 * sl;
-    x[sl] = (i < C) ? bv[i] : 0.0;
-    rD[sl] = (i < C) ? 1.0 / S[cidx(i, i, C)] : 0.0;
-  }
-  for (int k0 = 0; k0 < C; k0 += 16) {
-    double Lr[2][16];
-#pragma unroll
-    for (int sl = 0; sl < 2; ++sl) {
-      const int i = lane + 64 * sl;
-#pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        const bool use = i < C && k0 + u < i;
-        const double val = S[use ? cidx(i, k0 + u, C) : 0];
-        Lr[sl][u] = use ? val : 0.0;
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const int k = k0 + u;
-      if (k < C) {
-        const double yk = readlane_d(x[k >> 6], k & 63) * readlane_d(rD[k >> 6], k & 63);
-#pragma unroll
-        for (int sl = 0; sl < 2; ++sl) x[sl] -= Lr[sl][u] * yk;  // Lr = 0 unless i > k
-      }
-    }
-  }
-#pragma unroll
-  for (int sl = 0; sl < 2; ++sl) x[sl] *= rD[sl];
-  for (int k1 = C - 1; k1 >= 0; k1 -= 16) {
-    double Lc[2][16];
-#pragma unroll
-    for (int sl = 0; sl < 2; ++sl) {
-      const int i = lane + 64 * sl;
-#pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        const int k = k1 - u;
-        const bool use = k >= 0 && i < k;
-        const double val = S[use ? cidx(k, i, C) : 0];
-        Lc[sl][u] = use ? val * rD[sl] : 0.0;
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const int k = k1 - u;
-      if (k >= 0) {
-        const double xk = readlane_d(x[k >> 6], k & 63);
-#pragma unroll
-        for (int sl = 0; sl < 2; ++sl) x[sl] -= Lc[sl][u] * xk;  // Lc = 0 unless i < k
-      }
-    }
-  }
-  KB_STAMP(d, 4);
   double mx = 0.0, dd = 0.0, dr = 0.0;
 #pragma unroll
   for (int sl = 0; sl < 2; ++sl) {
@@ -1018,24 +1110,41 @@ __global__ void __launch_bounds__(256) k_solve(KbDev d, int gate, int do_update)
     d.camstat[2] = dr;
   }
   if (do_update) {
+    // camera design variables: intrinsics (additive, one lane per slot) and baselines (one lane per pose)
     const double* in = d.state + (size_t)c->cur * d.S;
     double* out = d.state + (size_t)(1 - c->cur) * d.S;
-    for (int q0 = 0; q0 < N * KB_MAX_INTR; q0 += 64) {  // wave-uniform trip count (shuffles inside)
-      const int q = q0 + lane;
-      const int cm = q / KB_MAX_INTR, xi = q % KB_MAX_INTR;
-      const int col = (q < N * KB_MAX_INTR && xi < d.nintr[cm]) ? d.col_intr[cm] + xi : 0;
+    constexpr int kIntrSlots = (KB_MAX_CAMS * KB_MAX_INTR + 63) / 64;
+    double vin[kIntrSlots];
+#pragma unroll
+    for (int r = 0; r < kIntrSlots; ++r) {
+      const int q = lane + 64 * r;
+      vin[r] = (q < N * KB_MAX_INTR) ? in[q] : 0.0;
+    }
+    double bq[7];
+    const int jb = lane < N - 1 ? lane : 0;
+#pragma unroll
+    for (int q = 0; q < 7; ++q) bq[q] = in[d.off_base + 7 * jb + q];
+#pragma unroll
+    for (int r = 0; r < kIntrSlots; ++r) {
+      if (64 * r >= N * KB_MAX_INTR) break;  // wave-uniform
+      const int q = lane + 64 * r;
+      const int cm = min(q / KB_MAX_INTR, N - 1), xi = q % KB_MAX_INTR;
+      const bool act = q < N * KB_MAX_INTR && xi < d.nintr[cm];
+      const int col = act ? d.col_intr[cm] + xi : 0;
       const double v0 = __shfl(x[0], col & 63), v1 = __shfl(x[1], col & 63);
       const double dv = (col >> 6) ? v1 : v0;
-      if (q < N * KB_MAX_INTR) out[q] = in[q] + ((xi < d.nintr[cm]) ? dv : 0.0);
+      if (q < N * KB_MAX_INTR) out[q] = vin[r] + (act ? dv : 0.0);
     }
-    for (int j = 0; j < N - 1; ++j) {
+    if (N > 1) {
       double d6[6];
+      const int cb = d.col_base[jb];
 #pragma unroll
       for (int q = 0; q < 6; ++q) {
-        const int col = d.col_base[j] + q;  // wave-uniform
-        d6[q] = __shfl(x[col >> 6], col & 63);
+        const int col = cb + q;
+        const double v0 = __shfl(x[0], col & 63), v1 = __shfl(x[1], col & 63);
+        d6[q] = (col >> 6) ? v1 : v0;
       }
-      if (lane == 0) update_pose(in + d.off_base + 7 * j, d6, out + d.off_base + 7 * j);
+      if (lane < N - 1) update_pose(bq, d6, out + d.off_base + 7 * lane);
     }
   }
   KB_STAMP(d, 5);
