@@ -47,6 +47,8 @@ int nintr_host(int m) {
 }
 }  // namespace
 
+constexpr int kGraphPasses = 8;  // optimizer passes per captured multi-pass graph
+
 struct kb_handle {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -63,7 +65,8 @@ struct kb_handle {
   bool uploaded = false;
   std::vector<void*> allocs;
   // loop
-  hipGraphExec_t graph = nullptr;  // captured pass of graph_policy
+  hipGraphExec_t graph = nullptr;   // one captured pass of graph_policy
+  hipGraphExec_t graphP = nullptr;  // kGraphPasses captured passes (no inter-launch gap between them)
   int graph_policy = -1;
   int graph_trace_cap = 0;
   double* trace = nullptr;
@@ -87,6 +90,14 @@ struct kb_handle {
     return 0;
   }
 };
+
+static void drop_graphs(kb_handle* h) {
+  if (h->graph) hipGraphExecDestroy(h->graph);
+  if (h->graphP) hipGraphExecDestroy(h->graphP);
+  h->graph = h->graphP = nullptr;
+  h->graph_policy = -1;
+}
+
 
 extern "C" {
 
@@ -260,7 +271,7 @@ void kb_destroy(kb_handle* h) {
   if (!h) return;
   hipSetDevice(h->device);
   if (h->stream) hipStreamSynchronize(h->stream);
-  if (h->graph) hipGraphExecDestroy(h->graph);
+  drop_graphs(h);
   if (h->comm) ncclCommDestroy(h->comm);
   for (void* p : h->allocs) hipFree(p);
   if (h->trace) hipFree(h->trace);
@@ -555,28 +566,43 @@ static int ensure_trace(kb_handle* h, int cap) {
   h->trace_cap = cap;
   h->d.trace = h->trace;
   h->d.trace_cap = cap;
-  if (h->graph) {  // captured kernel args hold the old pointer
-    hipGraphExecDestroy(h->graph);
-    h->graph = nullptr;
-  }
+  drop_graphs(h);  // captured kernel args hold the old pointer
+  return 0;
+}
+
+static int capture(kb_handle* h, int policy, int passes, hipGraphExec_t* out) {
+  hipGraph_t g = nullptr;
+  KB_HIP(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
+  int rc = 0;
+  for (int i = 0; i < passes && !rc; ++i) rc = enqueue_pass(h, policy);
+  hipError_t e = hipStreamEndCapture(h->stream, &g);
+  if (rc) return rc;
+  if (e != hipSuccess) return fail(std::string("hipStreamEndCapture: ") + hipGetErrorString(e));
+  KB_HIP(hipGraphInstantiate(out, g, nullptr, nullptr, 0));
+  KB_HIP(hipGraphDestroy(g));
   return 0;
 }
 
 static int ensure_graph(kb_handle* h, int policy) {
-  if (h->graph && h->graph_policy == policy) return 0;
-  if (h->graph) {
-    KB_HIP(hipGraphExecDestroy(h->graph));
-    h->graph = nullptr;
-  }
-  hipGraph_t g = nullptr;
-  KB_HIP(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
-  int rc = enqueue_pass(h, policy);
-  hipError_t e = hipStreamEndCapture(h->stream, &g);
-  if (rc) return rc;
-  if (e != hipSuccess) return fail(std::string("hipStreamEndCapture: ") + hipGetErrorString(e));
-  KB_HIP(hipGraphInstantiate(&h->graph, g, nullptr, nullptr, 0));
-  KB_HIP(hipGraphDestroy(g));
+  if (h->graph && h->graphP && h->graph_policy == policy) return 0;
+  drop_graphs(h);
+  if (capture(h, policy, 1, &h->graph) || capture(h, policy, kGraphPasses, &h->graphP)) return -1;
   h->graph_policy = policy;
+  return 0;
+}
+
+// launch n passes: whole kGraphPasses graphs, then single-pass graphs (or eager passes when not graphed)
+static int launch_passes(kb_handle* h, int policy, int n, bool graph) {
+  int i = 0;
+  if (graph)
+    for (; i + kGraphPasses <= n; i += kGraphPasses) KB_HIP(hipGraphLaunch(h->graphP, h->stream));
+  for (; i < n; ++i) {
+    if (graph) {
+      KB_HIP(hipGraphLaunch(h->graph, h->stream));
+    } else if (enqueue_pass(h, policy)) {
+      return -1;
+    }
+  }
   return 0;
 }
 
@@ -601,18 +627,12 @@ int kb_optimize(kb_handle* h, const kb_optimizer_options* opts, kb_solution* out
   if (loop_start(h, o)) return -1;
   const bool graph = opts->use_graph != 0 && !h->comm;  // RCCL calls stay eager
   if (graph && ensure_graph(h, opts->policy)) return -1;
-  const int every = opts->sync_every > 0 ? opts->sync_every : 4;
+  const int every = opts->sync_every > 0 ? opts->sync_every : 2 * kGraphPasses;
   KbCtrl ctrl{};
   int passes = 0;
   while (passes < max_passes) {
     const int n = std::min(every, max_passes - passes);
-    for (int i = 0; i < n; ++i) {
-      if (graph) {
-        KB_HIP(hipGraphLaunch(h->graph, h->stream));
-      } else if (enqueue_pass(h, opts->policy)) {
-        return -1;
-      }
-    }
+    if (launch_passes(h, opts->policy, n, graph)) return -1;
     passes += n;
     KB_HIP(hipMemcpyAsync(&ctrl, h->d.ctrl, sizeof(KbCtrl), hipMemcpyDeviceToHost, h->stream));
     KB_HIP(hipStreamSynchronize(h->stream));
@@ -652,13 +672,7 @@ int kb_run_gn_iterations(kb_handle* h, int32_t n_iter, double* seconds) {
   if (graph && ensure_graph(h, 1)) return -1;
   KB_HIP(hipStreamSynchronize(h->stream));
   const auto t0 = std::chrono::steady_clock::now();
-  for (int i = 0; i < n_iter; ++i) {
-    if (graph) {
-      KB_HIP(hipGraphLaunch(h->graph, h->stream));
-    } else if (enqueue_pass(h, 1)) {
-      return -1;
-    }
-  }
+  if (launch_passes(h, 1, n_iter, graph)) return -1;
   KB_HIP(hipStreamSynchronize(h->stream));
   const auto t1 = std::chrono::steady_clock::now();
   if (seconds) *seconds = std::chrono::duration<double>(t1 - t0).count();
@@ -737,10 +751,7 @@ int kb_comm_init(kb_handle* h, const void* uid, int32_t nranks, int32_t rank) {
   if (h->alloc(&rr, 8)) return -1;
   h->d.psum = h->psum_red;
   h->d.red = rr;
-  if (h->graph) {
-    hipGraphExecDestroy(h->graph);
-    h->graph = nullptr;
-  }
+  drop_graphs(h);
   KB_HIP(hipStreamSynchronize(h->stream));
   return 0;
 }
