@@ -184,8 +184,8 @@ kb_handle* kb_create(const kb_layout* L) {
   double* tgt = nullptr;
   rc |= h->alloc(&tgt, 3 * (size_t)h->K);
   rc |= h->alloc(&d.state, 2 * (size_t)h->S);
-  rc |= h->alloc(&d.camL, 12 * (size_t)h->N);
-  rc |= h->alloc(&d.camK, 36 * (size_t)h->N * h->N);
+  rc |= h->alloc(&d.camL, 2 * 12 * (size_t)h->N);  // [2] slots: ping-pong with the state buffers
+  rc |= h->alloc(&d.camK, 2 * 36 * (size_t)h->N * h->N);
   rc |= h->alloc(&d.Hff, 36 * (size_t)h->F);
   rc |= h->alloc(&d.Hfc, 6 * (size_t)h->C * h->F);
   rc |= h->alloc(&d.gf, 6 * (size_t)h->F);
@@ -196,6 +196,7 @@ kb_handle* kb_create(const kb_layout* L) {
   rc |= h->alloc(&d.part8, (size_t)kColsumRows * d.Wtot);
   rc |= h->alloc(&d.psum_local, (size_t)d.Wtot);
   d.psum = d.psum_local;
+  d.psum_rows = 1;
   rc |= h->alloc(&d.ticket, 16);
   rc |= h->alloc(&d.Hcc, (size_t)h->C * h->C);
   rc |= h->alloc(&d.gc, (size_t)h->C);
@@ -234,7 +235,7 @@ kb_handle* kb_create(const kb_layout* L) {
                                      36 + 6 * C + 8 + 18 * N * (N - 1) + (3 * h->K <= kTargetLds ? 3 * h->K : 0));
     h->lds_camexp = sizeof(double) * (N * 256 + N * N * 36);
     h->lds_schur = sizeof(double) * (6 * C + 36 + 8);
-    h->lds_solve = sizeof(double) * (C * (C + 1) / 2 + 2 * C + N * 256 + 2 * N * N * 36) + sizeof(int) * (C + C * (C - 1) / 2);
+    h->lds_solve = sizeof(double) * (C * (C + 1) / 2 + 2 * C + 1 + N * 256 + 2 * N * N * 36) + sizeof(int) * (C + C * (C - 1) / 2);
     h->solve_threads = 256;
     h->fn_solve = C <= 16   ? (const void*)k_solve<16>
                   : C <= 24 ? (const void*)k_solve<24>
@@ -323,6 +324,8 @@ int kb_upload_observations(kb_handle* h, int32_t n_views, int32_t n_corners, con
   rc |= h->alloc(&vfd, (size_t)n_views);
   rc |= h->alloc(&vcd, (size_t)n_views);
   rc |= h->alloc(&fv, fvc.size());
+  int2* fvo = nullptr;
+  rc |= h->alloc(&fvo, fvc.size());
   rc |= h->alloc(&d.costpart, (size_t)d.nblk_cost);
   if (rc) return -1;
   KB_HIP(hipMemcpyAsync(yd, y, sizeof(double2) * n_corners, hipMemcpyHostToDevice, h->stream));
@@ -331,6 +334,11 @@ int kb_upload_observations(kb_handle* h, int32_t n_views, int32_t n_corners, con
   KB_HIP(hipMemcpyAsync(vfd, vf.data(), sizeof(int32_t) * n_views, hipMemcpyHostToDevice, h->stream));
   KB_HIP(hipMemcpyAsync(vcd, vc.data(), sizeof(int32_t) * n_views, hipMemcpyHostToDevice, h->stream));
   KB_HIP(hipMemcpyAsync(fv, fvc.data(), sizeof(int32_t) * fvc.size(), hipMemcpyHostToDevice, h->stream));
+  std::vector<int2> fvr(fvc.size());
+  for (size_t q = 0; q < fvc.size(); ++q)
+    fvr[q] = fvc[q] < 0 ? make_int2(0, 0)
+                        : make_int2((int)view_offsets[fvc[q]], (int)view_offsets[fvc[q] + 1]);
+  KB_HIP(hipMemcpyAsync(fvo, fvr.data(), sizeof(int2) * fvr.size(), hipMemcpyHostToDevice, h->stream));
   KB_HIP(hipStreamSynchronize(h->stream));
   d.y = yd;
   d.cid = cd;
@@ -338,6 +346,7 @@ int kb_upload_observations(kb_handle* h, int32_t n_views, int32_t n_corners, con
   d.view_frame = vfd;
   d.view_cam = vcd;
   d.frame_vcam = fv;
+  d.fview = fvo;
   h->uploaded = true;
   return 0;
 }
@@ -393,9 +402,11 @@ static int allreduce_red(kb_handle* h) {
 }
 
 // column sums of the block partials (finished in-kernel) + all-reduce over ranks when sharded
-static int launch_colsum(kb_handle* h, int gate) {
+// finish = 0 (one GPU, optimizer loop): k_solve sums the kColsumRows stage-1 rows itself
+static int launch_colsum(kb_handle* h, int gate, bool finish = true) {
   KbDev& d = h->d;
   hipLaunchKernelGGL(k_colsum, dim3((d.Wtot + 63) / 64, kColsumRows), dim3(256), 0, h->stream, d, gate);
+  if (finish) hipLaunchKernelGGL(k_colfin, dim3((d.Wtot + 255) / 256), dim3(256), 0, h->stream, d, gate);
   KB_HIP(hipGetLastError());
   if (h->comm) KB_NCCL(ncclAllReduce(d.psum_local, h->psum_red, d.Wtot, ncclDouble, ncclSum, h->comm, h->stream));
   return 0;
@@ -403,7 +414,7 @@ static int launch_colsum(kb_handle* h, int gate) {
 
 static int launch_build(kb_handle* h, int gate, int fuse) {
   KbDev& d = h->d;
-  // per-call path: camera chain first; in the loop the previous k_post (or loop start) computed it
+  // per-call path: camera chains first; in the loop k_solve (or the loop start) computed them
   if (!gate) hipLaunchKernelGGL(k_pre, dim3(1), dim3(256), 0, h->stream, d, 0);
   void* args[] = {&d, &gate, &fuse};
   KB_HIP(hipLaunchKernel(h->fn_build, dim3(d.nblk), dim3(64 * d.wpb), args, h->lds_build, h->stream));
@@ -417,8 +428,13 @@ static int launch_schur(kb_handle* h, int gate) {
   return 0;
 }
 
-static int launch_solve(kb_handle* h, int gate, int do_update) {
-  void* args[] = {(void*)&h->d, (void*)&gate, (void*)&do_update};
+static int launch_solve(kb_handle* h, int gate, int do_update, bool from_rows = false) {
+  KbDev d = h->d;
+  if (from_rows) {  // column sums still split in kColsumRows stage-1 rows
+    d.psum = d.part8;
+    d.psum_rows = kColsumRows;
+  }
+  void* args[] = {(void*)&d, (void*)&gate, (void*)&do_update};
   KB_HIP(hipLaunchKernel(h->fn_solve, dim3(1), dim3(h->solve_threads), args, h->lds_solve, h->stream));
   KB_HIP(hipGetLastError());
   return 0;
@@ -537,22 +553,22 @@ int kb_get_normal_blocks(kb_handle* h, double* Hff, double* Hfc, double* gf, dou
 }
 
 // ---------------------------------------------------------------- device-resident loop
-// One pass: pol_pre | prep build colsum (gated on do_build) | schur colsum [allreduce A] camexpand solve |
-// backsub cost reduce [allreduce stats] | pol_post.  Every kernel early-exits once ctrl->done is set.
-// One optimizer pass: build (+ fused Schur) | [schur, LM only] | colsum [all-reduce] | solve |
-// backsub + cost | post (reduce, accept/revert, next pass prelude + camera chain).
+// One optimizer pass: build (+ fused Schur) | [schur, LM passes that keep the system] | colsum [all-reduce] |
+// solve (+ candidate camera chains) | backsub + cost, its last block: reduce, accept/revert, next prelude
+// ([all-reduce + k_policy] when sharded).  Every kernel early-exits once ctrl->done is set.
 static int enqueue_pass(kb_handle* h, int policy) {
   KbDev& d = h->d;
   if (launch_build(h, 1, 1)) return -1;
   if (policy == 0 && launch_schur(h, 1)) return -1;  // LM passes that keep the system (lambda change)
-  if (launch_colsum(h, 1)) return -1;
-  if (launch_solve(h, 1, 1)) return -1;
+  const bool one_gpu = !h->comm;
+  if (launch_colsum(h, 1, !one_gpu)) return -1;
+  if (launch_solve(h, 1, 1, one_gpu)) return -1;
   if (launch_backsub(h, 1, 1, 1)) return -1;
-  hipLaunchKernelGGL(k_post, dim3(1), dim3(256), 0, h->stream, d, h->comm ? 0 : 1);
+  hipLaunchKernelGGL(k_post, dim3(1), dim3(256), 0, h->stream, d, one_gpu ? 1 : 0);
   KB_HIP(hipGetLastError());
   if (h->comm) {
     if (allreduce_red(h)) return -1;
-    hipLaunchKernelGGL(k_policy, dim3(1), dim3(256), 0, h->stream, d);
+    hipLaunchKernelGGL(k_policy, dim3(1), dim3(1), 0, h->stream, d);
     KB_HIP(hipGetLastError());
   }
   return 0;
@@ -750,6 +766,7 @@ int kb_comm_init(kb_handle* h, const void* uid, int32_t nranks, int32_t rank) {
   double* rr = nullptr;
   if (h->alloc(&rr, 8)) return -1;
   h->d.psum = h->psum_red;
+  h->d.psum_rows = 1;
   h->d.red = rr;
   drop_graphs(h);
   KB_HIP(hipStreamSynchronize(h->stream));

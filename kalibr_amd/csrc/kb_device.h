@@ -50,18 +50,20 @@ struct KbDev {
   const int32_t* view_frame;
   const int32_t* view_cam;
   const int32_t* frame_vcam;
+  const int2* fview;       // [F][N]: corner range (o0, o1) of view (f, cam); o0 == o1 when absent
   const int32_t* colinfo;  // [C]: kind<<16 | cam_or_baseline<<8 | index
   const int32_t* tri;      // [C(C+1)/2]: a<<16 | b
   double* state;
-  double* camL;  // [N][12]
-  double* camK;  // [N][N][36]
+  double* camL;  // [2][N][12]    camera chains L_i of state buffer `slot` (ping-pong with ctrl->cur)
+  double* camK;  // [2][N][N][36] baseline chains K_{i,j} of state buffer `slot`
   double *Hff, *Hfc, *gf;
   double *Lf, *Yf, *zf;
   double* part;   // [nblk][Wtot]
   double* part8;       // [8][Wtot] stage-1 column sums
   double* psum_local;  // [Wtot] finished column sums of this rank (last k_colsum block)
-  double* psum;        // consumer view: psum_local, or its all-reduce over ranks
-  unsigned* ticket;    // k_colsum arrival counter (re-armed by the last block)
+  const double* psum;  // consumer view of the column sums: psum_rows rows of Wtot summed in fixed order
+  int psum_rows;       // 1 (psum_local or its all-reduce over ranks) or kColsumRows (part8, one GPU loop)
+  unsigned* ticket;    // [2] arrival counters: k_colsum, k_backsub (re-armed by the last block)
   double *Hcc, *gc, *cost_build;
   double *dx, *rhs;
   double* bpart;     // [nblk_bs][4]
@@ -85,6 +87,9 @@ struct KbDev {
   do {                 \
   } while (0)
 #endif
+
+__device__ __forceinline__ double* cam_L(const KbDev& d, int slot) { return d.camL + (size_t)slot * d.N * 12; }
+__device__ __forceinline__ double* cam_K(const KbDev& d, int slot) { return d.camK + (size_t)slot * d.N * d.N * 36; }
 
 // 16x16 upper-packed helpers (row-major upper: a <= b)
 __host__ __device__ __forceinline__ int d16_index(int a, int b) { return a * 16 - a * (a - 1) / 2 + (b - a); }

@@ -2,7 +2,7 @@
 // over Kalibr2 ReprojectionError terms, FP64 throughout.
 //
 // One optimizer pass (device-resident loop, every kernel gated on ctrl):
-//   k_pre        policy prelude (while-condition, lambda schedule) + camera chain L_i, K_{i,j}
+//   k_pre        (loop start / per-call) policy prelude + camera chains L_i, K_{i,j} of the current state
 //   k_build      K1+K2+K3 (+K4a fused): per view residual + 2x16 Jacobian rows staged in LDS,
 //                local 16x16 [J|-e]^T[J|-e] on v_mfma_f64_16x16x4; per frame the 6-D adjoint expansion
 //                into H_ff, H_fc, g_f and, fused, chol(H_ff + lambda^2 I), Y = L^-1 H_fc, z = L^-1 g_f,
@@ -10,10 +10,10 @@
 //   k_schur      K4a alone (LM passes that do not rebuild: lambda changed only)
 //   k_colsum     stage-1 deterministic column sums of the block partials (8 row splits)
 //   k_solve      K4b: camera block H_cc / g_c expansion, S = H_cc + lambda^2 I - sum Y^T Y, LDL^T,
-//                camera dx, camera DV update
+//                camera dx, camera DV update, camera chains of the candidate state
 //   k_backsub    K4c+K5(+K1): frame dx = L^-T (z - Y dx_c), pose update, cost of the frame's views at the
-//                new state, step statistics
-//   k_post       fixed-order reduction of the per-block cost / statistics + accept/revert policy
+//                new state, step statistics; its last block reduces them and runs the accept/revert policy
+//                and the next pass's prelude (k_policy after an all-reduce when sharded)
 //
 // Reference data flow replaced (paths relative to the reference repository):
 //   LinearSystemSolver.cpp:12-92, CompressedColumnJacobianTransposeBuilder(impl).hpp:19-101,
@@ -27,6 +27,9 @@ namespace kb {
 typedef double v4d __attribute__((ext_vector_type(4)));
 
 #define KB_WAVE_SYNC() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
+// materialise a loaded value at this point (an empty asm use): loads issued above cannot sink below it
+#define KB_KEEP(x) asm volatile("" ::"v"(x))
+#define KB_KEEPS(x) asm volatile("" ::"s"(x))
 
 // broadcast of a double from a wave-uniform lane (v_readlane_b32 x2, no LDS round trip)
 __device__ __forceinline__ double readlane_d(double v, int lane) {
@@ -39,6 +42,31 @@ __device__ __forceinline__ double readlane_d(double v, int lane) {
 constexpr int XS = 17;       // LDS row stride (doubles) of the 64 x 16 Jacobian-row tile
 constexpr int kMaxM = 24;    // largest Schur-sum entries per thread: (W + 1) <= M * blockDim
 constexpr int kTargetLds = 1536;  // target corners staged in k_build's LDS when 3 * n_target <= this
+
+// 64-bit DPP move within rows of 16 lanes (VALU, no LDS round trip); CTRL = DPP control (0x121.. = row_ror:1..)
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+  const unsigned long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffull), CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xf, 0xf, false);
+  return __longlong_as_double(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+
+// wave-wide sum / max, fixed order, result uniform: row butterflies by rotation, then the 4 row values
+__device__ __forceinline__ double wave_sum_d(double v) {
+  v += dpp_d<0x128>(v);
+  v += dpp_d<0x124>(v);
+  v += dpp_d<0x122>(v);
+  v += dpp_d<0x121>(v);
+  return (readlane_d(v, 0) + readlane_d(v, 16)) + (readlane_d(v, 32) + readlane_d(v, 48));
+}
+__device__ __forceinline__ double wave_max_d(double v) {
+  v = fmax(v, dpp_d<0x128>(v));
+  v = fmax(v, dpp_d<0x124>(v));
+  v = fmax(v, dpp_d<0x122>(v));
+  v = fmax(v, dpp_d<0x121>(v));
+  return fmax(fmax(readlane_d(v, 0), readlane_d(v, 16)), fmax(readlane_d(v, 32), readlane_d(v, 48)));
+}
 
 // ---------------------------------------------------------------------------------------------
 // rigid-transform helpers
@@ -210,23 +238,26 @@ __device__ void pol_post(KbCtrl* c, const KbDev& d, const double* red) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// camera chain of the accepted state: L_i (R|t) = B_{i-1}..B_0 and K_{i,j} (one block)
+// camera chains of a state: L_i (R|t) = B_{i-1}..B_0 and K_{i,j} (one block) -> slot `slot` of camL / camK.
+// `base` points at the N-1 baseline poses (7-stride, HBM or LDS).
 // ---------------------------------------------------------------------------------------------
-__device__ void prep_block(const KbDev& d) {
+__device__ void chain_block(const KbDev& d, const double* base, int slot) {
   __shared__ double sR[KB_MAX_CAMS][9], st[KB_MAX_CAMS][3];  // baseline B_j
   __shared__ double LR[KB_MAX_CAMS][9], Lt[KB_MAX_CAMS][3];
-  const double* s = d.state + (size_t)d.ctrl->cur * d.S;
   const int N = d.N;
-  if (threadIdx.x < N - 1) pose_rt(s + d.off_base + 7 * threadIdx.x, sR[threadIdx.x], st[threadIdx.x]);
+  double* Lo = cam_L(d, slot);
+  double* Ko = cam_K(d, slot);
+  if (threadIdx.x < N - 1) pose_rt(base + 7 * threadIdx.x, sR[threadIdx.x], st[threadIdx.x]);
   __syncthreads();
   if (threadIdx.x == 0) {
     for (int q = 0; q < 9; ++q) LR[0][q] = (q % 4 == 0) ? 1.0 : 0.0;
     Lt[0][0] = Lt[0][1] = Lt[0][2] = 0.0;
     for (int i = 1; i < N; ++i) rt_mul(sR[i - 1], st[i - 1], LR[i - 1], Lt[i - 1], LR[i], Lt[i]);
-    for (int i = 0; i < N; ++i) {
-      for (int q = 0; q < 9; ++q) d.camL[i * 12 + q] = LR[i][q];
-      for (int q = 0; q < 3; ++q) d.camL[i * 12 + 9 + q] = Lt[i][q];
-    }
+  }
+  __syncthreads();
+  for (int q = threadIdx.x; q < N * 12; q += blockDim.x) {
+    const int i = q / 12, e = q % 12;
+    Lo[q] = e < 9 ? LR[i][e] : Lt[i][e - 9];
   }
   for (int idx = threadIdx.x; idx < N * N * 36; idx += blockDim.x) {
     const int e = idx % 36, ij = idx / 36, i = ij / N, j = ij % N;
@@ -241,25 +272,18 @@ __device__ void prep_block(const KbDev& d) {
       }
       val = -chain_entry(QR, Qt, st[j], e / 6, e % 6);
     }
-    d.camK[idx] = val;
+    Ko[idx] = val;
   }
 }
 
-// policy prelude of the next pass + its camera chain (one block)
-__device__ void next_pass_block(const KbDev& d) {
-  KbCtrl* c = d.ctrl;
-  if (threadIdx.x == 0 && !c->done) pol_pre(c);
-  __syncthreads();
-  if (c->done || !c->do_build) return;
-  prep_block(d);
-}
-
-// k_pre: gate 0 -> camera chain only (per-call build); gate 1 -> prelude of the first pass + its chain
+// k_pre: camera chains of the current state (slot cur); gate 1 also runs the policy prelude of the first pass.
+// Inside the optimizer loop k_solve computes the chains of each candidate state, so the accepted state's are
+// always in slot cur.
 __global__ void __launch_bounds__(256) k_pre(KbDev d, int gate) {
-  if (gate)
-    next_pass_block(d);
-  else
-    prep_block(d);
+  KbCtrl* c = d.ctrl;
+  if (gate && threadIdx.x == 0 && !c->done) pol_pre(c);
+  const int cur = c->cur;
+  chain_block(d, d.state + (size_t)cur * d.S + d.off_base, cur);
 }
 
 // in-place 6x6 Cholesky (lower) in LDS, by one thread; returns 0 if not PD
@@ -368,7 +392,7 @@ __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
     int i = 1;
     while (i * (i + 1) / 2 <= ij) ++i;
     const int j = ij - i * (i - 1) / 2;
-    Kl[q] = d.camK[(size_t)(i * N + j) * 36 + e];
+    Kl[q] = cam_K(d, c->cur)[(size_t)(i * N + j) * 36 + e];
   }
   const double* tgt = tg_lds ? tg : d.target;
   const double lam = gate ? c->lambda : d.host_lambda;
@@ -396,7 +420,8 @@ __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
     const double* fp = s + d.off_frame + 7 * f;
     double Ri[9], ti[3], R[9], t[3];
     pose_inverse(fp, Ri, ti);
-    rt_mul(d.camL + cam * 12, d.camL + cam * 12 + 9, Ri, ti, R, t);  // T_cam_w = L_cam T_f^-1
+    const double* Lc = cam_L(d, c->cur) + cam * 12;
+    rt_mul(Lc, Lc + 9, Ri, ti, R, t);  // T_cam_w = L_cam T_f^-1
     const int v = d.frame_vcam[f * N + cam];
     v4d acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
     if (v >= 0) {
@@ -637,51 +662,55 @@ __global__ void __launch_bounds__(256) k_schur(KbDev d, int gate) {
 
 // ---------------------------------------------------------------------------------------------
 // k_colsum: column sums of the block partials in fixed order: block (bx, ry) sums rows b = ry (mod 8) of
-// 64 columns into part8[ry]; the last-arriving block (agent-scope release/acquire ticket, guide G16 recipe)
-// finishes psum_local[e] = sum_r part8[r][e].  Grid (ceil(Wtot/64), 8).
+// 64 columns into part8[ry] (8 loads in flight per thread).  Grid (ceil(Wtot/64), 8).  The 8 rows are
+// finished by the consumer: k_solve's staging (one GPU) or k_colfin (per-call path, all-reduce input).
 // ---------------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_colsum(KbDev d, int gate) {
   KbCtrl* c = d.ctrl;
   if (gate && c->done) return;
   __shared__ double part[4][64];
-  __shared__ int last;
   const int l = threadIdx.x & 63, w4 = threadIdx.x >> 6;
   const int e = blockIdx.x * 64 + l, ry = blockIdx.y;
+  const int ec = min(e, d.Wtot - 1);
   double s = 0.0;
-  if (e < d.Wtot)
-    for (int b = ry + kColsumRows * w4; b < d.nblk; b += 4 * kColsumRows) s += d.part[(size_t)b * d.Wtot + e];
+  constexpr int U = 8, step = 4 * kColsumRows;
+  for (int b0 = ry + kColsumRows * w4; b0 < d.nblk; b0 += U * step) {
+    double v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = d.part[(size_t)min(b0 + u * step, d.nblk - 1) * d.Wtot + ec];
+#pragma unroll
+    for (int u = 0; u < U; ++u) s += (b0 + u * step < d.nblk) ? v[u] : 0.0;
+  }
   part[w4][l] = s;
   __syncthreads();
   if (w4 == 0 && e < d.Wtot) d.part8[(size_t)ry * d.Wtot + e] = ((part[0][l] + part[1][l]) + part[2][l]) + part[3][l];
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned total = gridDim.x * gridDim.y;
-    const unsigned t = __hip_atomic_fetch_add(d.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = (t == total - 1);
-  }
-  __syncthreads();
-  if (!last) return;
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-  for (int q = threadIdx.x; q < d.Wtot; q += blockDim.x) {
-    double v[kColsumRows];
-#pragma unroll
-    for (int r = 0; r < kColsumRows; ++r) v[r] = d.part8[(size_t)r * d.Wtot + q];
-    double acc = 0.0;
-#pragma unroll
-    for (int r = 0; r < kColsumRows; ++r) acc += v[r];
-    d.psum_local[q] = acc;
-  }
-  if (threadIdx.x == 0) *d.ticket = 0u;  // re-armed for the next launch (ordered by the kernel boundary)
 }
 
-__device__ __forceinline__ double psum_at(const KbDev& d, int e) { return d.psum[e]; }
+// psum_local[e] = sum_r part8[r][e] (fixed order)
+__global__ void __launch_bounds__(256) k_colfin(KbDev d, int gate) {
+  if (gate && d.ctrl->done) return;
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= d.Wtot) return;
+  double v[kColsumRows];
+#pragma unroll
+  for (int r = 0; r < kColsumRows; ++r) v[r] = d.part8[(size_t)r * d.Wtot + q];
+  double acc = 0.0;
+#pragma unroll
+  for (int r = 0; r < kColsumRows; ++r) acc += v[r];
+  d.psum_local[q] = acc;
+}
+
+// entry e of the column sums: psum_rows rows (stride Wtot) summed in fixed order
+__device__ __forceinline__ double psum_at(const KbDev& d, int e) {
+  double v[kColsumRows];
+#pragma unroll
+  for (int r = 0; r < kColsumRows; ++r) v[r] = d.psum[(size_t)(r < d.psum_rows ? r : 0) * d.Wtot + e];
+  double acc = 0.0;
+#pragma unroll
+  for (int r = 0; r < kColsumRows; ++r) acc += (r < d.psum_rows) ? v[r] : 0.0;
+  return acc;
+}
+
 
 // ---------------------------------------------------------------------------------------------
 // camera block from the per-camera local sums (H_cc, g_c), shared by k_camexpand and k_solve
@@ -700,7 +729,7 @@ __device__ void cam_load(const KbDev& d, double* Hs, double* T) {
     double s = 0.0;
     if (k < i) {
       const int a = e / 6, b = e % 6;
-      const double* K = d.camK + (size_t)(i * N + k) * 36;
+      const double* K = cam_K(d, d.ctrl->cur) + (size_t)(i * N + k) * 36;
 #pragma unroll
       for (int m = 0; m < 6; ++m) s += Hs[i * 256 + a * 16 + m] * K[m * 6 + b];
     }
@@ -718,20 +747,20 @@ __device__ double cam_entry(const KbDev& d, const double* Hs, const double* T, i
     if (ip == iq) s = Hs[ip * 256 + (6 + xp) * 16 + 6 + xq];
   } else if (kp == 0 && kq == 1) {
     if (iq < ip) {
-      const double* K = d.camK + (size_t)(ip * N + iq) * 36;
+      const double* K = cam_K(d, d.ctrl->cur) + (size_t)(ip * N + iq) * 36;
 #pragma unroll
       for (int b = 0; b < 6; ++b) s += Hs[ip * 256 + (6 + xp) * 16 + b] * K[b * 6 + xq];
     }
   } else if (kp == 1 && kq == 0) {
     if (ip < iq) {
-      const double* K = d.camK + (size_t)(iq * N + ip) * 36;
+      const double* K = cam_K(d, d.ctrl->cur) + (size_t)(iq * N + ip) * 36;
 #pragma unroll
       for (int a = 0; a < 6; ++a) s += K[a * 6 + xp] * Hs[iq * 256 + a * 16 + 6 + xq];
     }
   } else {
     const int m = ip > iq ? ip : iq;
     for (int i = m + 1; i < N; ++i) {
-      const double* K = d.camK + (size_t)(i * N + ip) * 36;
+      const double* K = cam_K(d, d.ctrl->cur) + (size_t)(i * N + ip) * 36;
       const double* Tq = T + (size_t)(i * N + iq) * 36;
 #pragma unroll
       for (int a = 0; a < 6; ++a) s += K[a * 6 + xp] * Tq[a * 6 + xq];
@@ -746,7 +775,7 @@ __device__ double cam_grad(const KbDev& d, const double* Hs, int p) {
   if (kp == 0) return Hs[ip * 256 + (6 + xp) * 16 + 15];
   double s = 0.0;
   for (int i = ip + 1; i < N; ++i) {
-    const double* K = d.camK + (size_t)(i * N + ip) * 36;
+    const double* K = cam_K(d, d.ctrl->cur) + (size_t)(i * N + ip) * 36;
 #pragma unroll
     for (int a = 0; a < 6; ++a) s += K[a * 6 + xp] * Hs[i * 256 + a * 16 + 15];
   }
@@ -833,36 +862,41 @@ template <int U>
 __device__ __forceinline__ void solve_stage(const KbDev& d, double* K, double* Hs, double* S, double* bv, int* ci,
                                             int tid, int nth) {
   const int N = d.N, C = d.C, Wt = d.W - C;
-  const int n0 = N * N * 36, n1 = n0 + N * 256, n2 = n1 + Wt, n3 = n2 + C, n4 = n3 + C;
+  // [camK N*N*36 | per-camera upper sums N*136 | Schur sums Wt + rhs C + non-PD count 1 | colinfo C]
+  const int n0 = N * N * 36, n1 = n0 + N * 136, n2 = n1 + Wt, n3 = n2 + C + 1, n4 = n3 + C;
+  const double* Kc = cam_K(d, d.ctrl->cur);
   for (int q0 = tid; q0 < n4; q0 += U * nth) {
     double v[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int q = min(q0 + u * nth, n4 - 1);
-      if (q < n0) {
-        v[u] = d.camK[q];
-      } else if (q < n1) {
-        const int r = q - n0, cam = r >> 8, a = (r & 255) >> 4, b = r & 15;
-        v[u] = d.psum[cam * 136 + (a < b ? d16_index(a, b) : d16_index(b, a))];
-      } else if (q < n3) {
-        v[u] = -d.psum[N * 136 + (q - n1)];  // Schur sums, then rhs (contiguous in psum)
-      } else {
+      if (q < n0)
+        v[u] = Kc[q];
+      else if (q < n3)
+        v[u] = psum_at(d, q - n0);  // camera sums, Schur sums, rhs, count: contiguous in the partial rows
+      else
         v[u] = (double)d.colinfo[q - n3];
-      }
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int q = q0 + u * nth;
-      if (q < n0)
+      if (q < n0) {
         K[q] = v[u];
-      else if (q < n1)
-        Hs[q - n0] = v[u];
-      else if (q < n2)
-        S[q - n1] = v[u];  // upper (a,b) row-major == lower (b,a) col-major
-      else if (q < n3)
-        bv[q - n2] = v[u];
-      else if (q < n4)
+      } else if (q < n1) {
+        const int r = q - n0, cam = r / 136;
+        int a, b;
+        d16_rowcol(r % 136, a, b);
+        Hs[cam * 256 + a * 16 + b] = v[u];
+        Hs[cam * 256 + b * 16 + a] = v[u];
+      } else if (q < n2) {
+        S[q - n1] = -v[u];  // upper (a,b) row-major == lower (b,a) col-major
+      } else if (q < n2 + C) {
+        bv[q - n2] = -v[u];
+      } else if (q < n3) {
+        bv[C] = v[u];  // non-PD frame-block count (bv has C + 1 slots)
+      } else if (q < n4) {
         ci[q - n3] = (int)v[u];
+      }
     }
   }
 }
@@ -919,38 +953,42 @@ __device__ __forceinline__ bool ldl_solve_reg(const double* S, const double* bv,
   return ok;
 }
 
-// CM > 0: one-wave register LDL^T for C <= CM (<= 64); CM == 0: block LDL^T in LDS for C > 64
+// Camera solve of one pass (one block): S = H_cc + lambda^2 I - sum Y^T Y, b = g_c - sum Y^T z staged in LDS,
+// LDL^T + solves (CM > 0: one-wave register LDL^T for C <= CM <= 64; CM == 0: block LDL^T in LDS), camera DV
+// update into state[1 - cur] and the camera chains of that candidate state into slot 1 - cur.
+// Every thread of the block must call it (barriers inside).
 template <int CM>
-__global__ void __launch_bounds__(256) k_solve(KbDev d, int gate, int do_update) {
+__device__ void solve_body(const KbDev& d, int gate, int do_update) {
   KbCtrl* c = d.ctrl;
-  if (gate && c->done) return;
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const int N = d.N, C = d.C, W = d.W, nth = blockDim.x, tid = threadIdx.x;
   const int Cp = C * (C + 1) / 2;
   double* S = sm;                    // column-major packed lower [Cp]
-  double* bv = S + Cp;               // [C]
-  double* gl = bv + C;               // [C]
+  double* bv = S + Cp;               // [C] (+1: non-PD frame-block count while staging)
+  double* gl = bv + C + 1;           // [C]
   double* Hs = gl + C;               // [N][256]
   double* T = Hs + N * 256;          // [N][N][36]
   double* K = T + N * N * 36;        // [N][N][36]
   int* ci = (int*)(K + N * N * 36);  // [C]
   int* ptab = ci + C;                // [(C-1)C/2] pair table of the trailing triangle: ii<<16 | jj (CM == 0)
   __shared__ int okl;
+  __shared__ double nbase[KB_MAX_CAMS * 7];  // candidate baselines
   const double lam = gate ? c->lambda : d.host_lambda;
   const double lam2 = lam * lam;
+  const int cur = c->cur;
   KB_STAMP(d, 0);
 #ifdef KB_STAMPS
   if (tid == 0 && d.stamps) d.stamps[40] = __builtin_amdgcn_s_memtime();
 #endif
   // phase A: stage K, column info, per-camera sums and the Schur sums in LDS (one row: psum)
-  solve_stage<8>(d, K, Hs, S, bv, ci, tid, nth);
+  solve_stage<4>(d, K, Hs, S, bv, ci, tid, nth);
   if (CM == 0)
     for (int q = tid; q < (C - 1) * C / 2; q += nth) {
       const int ii = tri_row(q);
       ptab[q] = (ii << 16) | (q - ii * (ii + 1) / 2);
     }
-  if (tid == 0) okl = (c->solve_ok != 0) && !(d.psum[N * 136 + W] > 0.0);
   __syncthreads();
+  if (tid == 0) okl = (c->solve_ok != 0) && !(bv[C] > 0.0);
   KB_STAMP(d, 1);
   // phase B: camera block expansion
   for (int q = tid; q < N * N * 36; q += nth) {
@@ -982,13 +1020,12 @@ __global__ void __launch_bounds__(256) k_solve(KbDev d, int gate, int do_update)
   }
   __syncthreads();
   KB_STAMP(d, 2);
-  double x[2];
+  double x[2] = {0.0, 0.0};
   if constexpr (CM > 0) {
-    if (tid >= 64) return;
-    const bool ok = ldl_solve_reg<CM>(S, bv, C, tid, x[0]);
-    x[1] = 0.0;
-    if (!ok) okl = 0;
-    KB_WAVE_SYNC();
+    if (tid < 64) {
+      const bool ok = ldl_solve_reg<CM>(S, bv, C, tid, x[0]);
+      if (!ok) okl = 0;
+    }
     KB_STAMP(d, 3);
     KB_STAMP(d, 4);
   } else {
@@ -1020,212 +1057,387 @@ __global__ void __launch_bounds__(256) k_solve(KbDev d, int gate, int do_update)
       }
       __syncthreads();
     }
-    if (tid >= 64) return;
     KB_STAMP(d, 3);
     // phase D: Ltilde y = b, z = D^-1 y, Ltilde^T x = z; row i held by lane i & 63 (slot i >> 6).
     // Each 16-step chunk first preloads the lane's matrix entries into registers.
-    const int lane = tid;
-    double rD[2];
-#pragma unroll
-    for (int sl = 0; sl < 2; ++sl) {
-      const int i = lane + 64 * sl;
-      x[sl] = (i < C) ? bv[i] : 0.0;
-      rD[sl] = (i < C) ? 1.0 / S[cidx(i, i, C)] : 0.0;
-    }
-    for (int k0 = 0; k0 < C; k0 += 16) {
-      double Lr[2][16];
+    if (tid < 64) {
+      const int lane = tid;
+      double rD[2];
 #pragma unroll
       for (int sl = 0; sl < 2; ++sl) {
         const int i = lane + 64 * sl;
+        x[sl] = (i < C) ? bv[i] : 0.0;
+        rD[sl] = (i < C) ? 1.0 / S[cidx(i, i, C)] : 0.0;
+      }
+      for (int k0 = 0; k0 < C; k0 += 16) {
+        double Lr[2][16];
+#pragma unroll
+        for (int sl = 0; sl < 2; ++sl) {
+          const int i = lane + 64 * sl;
+#pragma unroll
+          for (int u = 0; u < 16; ++u) {
+            const bool use = i < C && k0 + u < i;
+            const double val = S[use ? cidx(i, k0 + u, C) : 0];
+            Lr[sl][u] = use ? val : 0.0;
+          }
+        }
 #pragma unroll
         for (int u = 0; u < 16; ++u) {
-          const bool use = i < C && k0 + u < i;
-          const double val = S[use ? cidx(i, k0 + u, C) : 0];
-          Lr[sl][u] = use ? val : 0.0;
+          const int k = k0 + u;
+          if (k < C) {
+            const double yk = readlane_d(x[k >> 6], k & 63) * readlane_d(rD[k >> 6], k & 63);
+#pragma unroll
+            for (int sl = 0; sl < 2; ++sl) x[sl] -= Lr[sl][u] * yk;  // Lr = 0 unless i > k
+          }
         }
       }
 #pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        const int k = k0 + u;
-        if (k < C) {
-          const double yk = readlane_d(x[k >> 6], k & 63) * readlane_d(rD[k >> 6], k & 63);
+      for (int sl = 0; sl < 2; ++sl) x[sl] *= rD[sl];
+      for (int k1 = C - 1; k1 >= 0; k1 -= 16) {
+        double Lc[2][16];
 #pragma unroll
-          for (int sl = 0; sl < 2; ++sl) x[sl] -= Lr[sl][u] * yk;  // Lr = 0 unless i > k
+        for (int sl = 0; sl < 2; ++sl) {
+          const int i = lane + 64 * sl;
+#pragma unroll
+          for (int u = 0; u < 16; ++u) {
+            const int k = k1 - u;
+            const bool use = k >= 0 && i < k;
+            const double val = S[use ? cidx(k, i, C) : 0];
+            Lc[sl][u] = use ? val * rD[sl] : 0.0;
+          }
         }
-      }
-    }
-#pragma unroll
-    for (int sl = 0; sl < 2; ++sl) x[sl] *= rD[sl];
-    for (int k1 = C - 1; k1 >= 0; k1 -= 16) {
-      double Lc[2][16];
-#pragma unroll
-      for (int sl = 0; sl < 2; ++sl) {
-        const int i = lane + 64 * sl;
 #pragma unroll
         for (int u = 0; u < 16; ++u) {
           const int k = k1 - u;
-          const bool use = k >= 0 && i < k;
-          const double val = S[use ? cidx(k, i, C) : 0];
-          Lc[sl][u] = use ? val * rD[sl] : 0.0;
-        }
-      }
+          if (k >= 0) {
+            const double xk = readlane_d(x[k >> 6], k & 63);
 #pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        const int k = k1 - u;
-        if (k >= 0) {
-          const double xk = readlane_d(x[k >> 6], k & 63);
-#pragma unroll
-          for (int sl = 0; sl < 2; ++sl) x[sl] -= Lc[sl][u] * xk;  // Lc = 0 unless i < k
+            for (int sl = 0; sl < 2; ++sl) x[sl] -= Lc[sl][u] * xk;  // Lc = 0 unless i < k
+          }
         }
       }
     }
     KB_STAMP(d, 4);
   }
-  const int lane = tid;
+  __syncthreads();  // okl final
   if (!okl) {
-    if (lane == 0) c->solve_ok = 0;
+    if (tid == 0) c->solve_ok = 0;
     return;
   }
-  double mx = 0.0, dd = 0.0, dr = 0.0;
+  if (tid < 64) {
+    const int lane = tid;
+    double mx = 0.0, dd = 0.0, dr = 0.0;
 #pragma unroll
-  for (int sl = 0; sl < 2; ++sl) {
-    const int i = lane + 64 * sl;
-    if (i < C) {
-      const double g = gl[i];
-      d.dx[i] = x[sl];
-      mx = fmax(mx, fabs(x[sl]));
-      dd += x[sl] * x[sl];
-      dr += x[sl] * g;
-    }
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    mx = fmax(mx, __shfl_xor(mx, o));
-    dd += __shfl_xor(dd, o);
-    dr += __shfl_xor(dr, o);
-  }
-  if (lane == 0) {
-    d.camstat[0] = mx;
-    d.camstat[1] = dd;
-    d.camstat[2] = dr;
-  }
-  if (do_update) {
-    // camera design variables: intrinsics (additive, one lane per slot) and baselines (one lane per pose)
-    const double* in = d.state + (size_t)c->cur * d.S;
-    double* out = d.state + (size_t)(1 - c->cur) * d.S;
-    constexpr int kIntrSlots = (KB_MAX_CAMS * KB_MAX_INTR + 63) / 64;
-    double vin[kIntrSlots];
-#pragma unroll
-    for (int r = 0; r < kIntrSlots; ++r) {
-      const int q = lane + 64 * r;
-      vin[r] = (q < N * KB_MAX_INTR) ? in[q] : 0.0;
-    }
-    double bq[7];
-    const int jb = lane < N - 1 ? lane : 0;
-#pragma unroll
-    for (int q = 0; q < 7; ++q) bq[q] = in[d.off_base + 7 * jb + q];
-#pragma unroll
-    for (int r = 0; r < kIntrSlots; ++r) {
-      if (64 * r >= N * KB_MAX_INTR) break;  // wave-uniform
-      const int q = lane + 64 * r;
-      const int cm = min(q / KB_MAX_INTR, N - 1), xi = q % KB_MAX_INTR;
-      const bool act = q < N * KB_MAX_INTR && xi < d.nintr[cm];
-      const int col = act ? d.col_intr[cm] + xi : 0;
-      const double v0 = __shfl(x[0], col & 63), v1 = __shfl(x[1], col & 63);
-      const double dv = (col >> 6) ? v1 : v0;
-      if (q < N * KB_MAX_INTR) out[q] = vin[r] + (act ? dv : 0.0);
-    }
-    if (N > 1) {
-      double d6[6];
-      const int cb = d.col_base[jb];
-#pragma unroll
-      for (int q = 0; q < 6; ++q) {
-        const int col = cb + q;
-        const double v0 = __shfl(x[0], col & 63), v1 = __shfl(x[1], col & 63);
-        d6[q] = (col >> 6) ? v1 : v0;
+    for (int sl = 0; sl < 2; ++sl) {
+      const int i = lane + 64 * sl;
+      if (i < C) {
+        const double g = gl[i];
+        d.dx[i] = x[sl];
+        mx = fmax(mx, fabs(x[sl]));
+        dd += x[sl] * x[sl];
+        dr += x[sl] * g;
       }
-      if (lane < N - 1) update_pose(bq, d6, out + d.off_base + 7 * lane);
+    }
+    mx = wave_max_d(mx);
+    dd = wave_sum_d(dd);
+    dr = wave_sum_d(dr);
+    if (lane == 0) {
+      d.camstat[0] = mx;
+      d.camstat[1] = dd;
+      d.camstat[2] = dr;
+    }
+    if (do_update) {
+      // camera design variables: intrinsics (additive, one lane per slot) and baselines (one lane per pose)
+      const double* in = d.state + (size_t)cur * d.S;
+      double* out = d.state + (size_t)(1 - cur) * d.S;
+      constexpr int kIntrSlots = (KB_MAX_CAMS * KB_MAX_INTR + 63) / 64;
+      double vin[kIntrSlots];
+#pragma unroll
+      for (int r = 0; r < kIntrSlots; ++r) {
+        const int q = lane + 64 * r;
+        vin[r] = (q < N * KB_MAX_INTR) ? in[q] : 0.0;
+      }
+      double bq[7];
+      const int jb = lane < N - 1 ? lane : 0;
+#pragma unroll
+      for (int q = 0; q < 7; ++q) bq[q] = in[d.off_base + 7 * jb + q];
+#pragma unroll
+      for (int r = 0; r < kIntrSlots; ++r) {
+        if (64 * r >= N * KB_MAX_INTR) break;  // wave-uniform
+        const int q = lane + 64 * r;
+        const int cm = min(q / KB_MAX_INTR, N - 1), xi = q % KB_MAX_INTR;
+        const bool act = q < N * KB_MAX_INTR && xi < d.nintr[cm];
+        const int col = act ? d.col_intr[cm] + xi : 0;
+        const double v0 = __shfl(x[0], col & 63), v1 = __shfl(x[1], col & 63);
+        const double dv = (col >> 6) ? v1 : v0;
+        if (q < N * KB_MAX_INTR) out[q] = vin[r] + (act ? dv : 0.0);
+      }
+      if (N > 1) {
+        double d6[6], nb[7];
+        const int cb = d.col_base[jb];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) {
+          const int col = cb + q;
+          const double v0 = __shfl(x[0], col & 63), v1 = __shfl(x[1], col & 63);
+          d6[q] = (col >> 6) ? v1 : v0;
+        }
+        update_pose(bq, d6, nb);
+        if (lane < N - 1)
+#pragma unroll
+          for (int q = 0; q < 7; ++q) {
+            out[d.off_base + 7 * lane + q] = nb[q];
+            nbase[7 * lane + q] = nb[q];
+          }
+      }
     }
   }
   KB_STAMP(d, 5);
 #ifdef KB_STAMPS
   if (tid == 0 && d.stamps) d.stamps[41] = __builtin_amdgcn_s_memtime();
 #endif
+  if (do_update) {
+    __syncthreads();
+    chain_block(d, nbase, 1 - cur);  // chains of the candidate state (k_backsub's cost, next build if accepted)
+  }
+}
+
+template <int CM>
+__global__ void __launch_bounds__(256) k_solve(KbDev d, int gate, int do_update) {
+  if (gate && d.ctrl->done) return;
+  solve_body<CM>(d, gate, do_update);
 }
 
 // ---------------------------------------------------------------------------------------------
-// k_backsub: one block per frame, one wave per camera view: every wave forms dx_f = L^-T (z - Y dx_c)
-// (6 wave dot products), wave 0 stores dx / pose, each wave then evaluates the cost of its view at the new
-// state (evaluateError fused); per-frame [cost, max|dx|, dx.dx, dx.rhs]
+// k_backsub: one block per frame, one wave per camera view (waves = min(N, 8)).  Every wave forms
+// dx_f = L^-T (z - Y dx_c) (6 wave dot products), wave 0 stores dx / the new pose, each wave then evaluates
+// the cost of its views at the candidate state (evaluateError fused): per-frame [cost, max|dx|, dx.dx, dx.rhs].
+// All loads are issued in two dependent rounds (launch-independent ones, then those indexed by them).
+// k_post (one block) reduces the per-frame rows (+ camera stats) into red_local and, on one GPU, runs the
+// policy (accept / revert, next pass prelude); sharded runs all-reduce red first and run k_policy.
 // ---------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_post(KbDev d, int policy) {
+  __shared__ double sh[8][4];
+  KbCtrl* c = d.ctrl;
+  if (c->done) return;
+  const int tid = threadIdx.x, nth = blockDim.x;
+  const int sok = c->solve_ok;
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+  if (sok) {
+    const double4* bp = reinterpret_cast<const double4*>(d.bpart);
+    for (int q0 = tid; q0 < d.nblk_bs; q0 += 4 * nth) {
+      double4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = bp[min(q0 + u * nth, d.nblk_bs - 1)];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (q0 + u * nth < d.nblk_bs) {
+          s0 += v[u].x;
+          s1 = fmax(s1, v[u].y);
+          s2 += v[u].z;
+          s3 += v[u].w;
+        }
+    }
+    s0 = wave_sum_d(s0);
+    s1 = wave_max_d(s1);
+    s2 = wave_sum_d(s2);
+    s3 = wave_sum_d(s3);
+    if ((tid & 63) == 0) {
+      sh[tid >> 6][0] = s0;
+      sh[tid >> 6][1] = s1;
+      sh[tid >> 6][2] = s2;
+      sh[tid >> 6][3] = s3;
+    }
+  }
+  __syncthreads();
+  if (tid != 0) return;
+  double red[4] = {0.0, 0.0, 0.0, 0.0};
+  if (sok) {
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    for (int q = 0; q < (nth >> 6); ++q) {
+      a0 += sh[q][0];
+      a1 = fmax(a1, sh[q][1]);
+      a2 += sh[q][2];
+      a3 += sh[q][3];
+    }
+    red[0] = a0;
+    red[1] = a2 + d.camstat[1];
+    red[2] = a3 + d.camstat[2];
+    red[3] = fmax(a1, d.camstat[0]);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) d.red_local[q] = red[q];
+  }
+  if (policy) {
+    KbCtrl cl = *c;
+    pol_post(&cl, d, red);
+    if (!cl.done) pol_pre(&cl);
+    *c = cl;
+  }
+}
+
 __global__ void __launch_bounds__(512) k_backsub(KbDev d, int gate, int do_update, int with_cost) {
   KbCtrl* c = d.ctrl;
-  if (gate && (c->done || !c->solve_ok)) return;
+  __shared__ double tg[kTargetLds];
   __shared__ double sc[8];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, nw = blockDim.x >> 6, nth = blockDim.x;
   const int f = blockIdx.x;
   const int C = d.C, N = d.N;
-  double w[6];
+  const bool cost_pass = do_update && with_cost;
+  // ---- round 1: launch-independent loads, straight-line and unconditional (clamped) so that they are all in
+  // flight together; the gate and the LDS stores come after
+  const int done = c->done, sok = c->solve_ok, cur = c->cur;
+  const bool tg_lds = 3 * d.K <= kTargetLds;
+  const int nt3 = 3 * d.K;
+  constexpr int kTgU = 6;  // 6 x 64 >= 3 x 120 AprilGrid corners even for a one-wave block
+  double tv[kTgU];
 #pragma unroll
-  for (int r = 0; r < 6; ++r) {
-    double s = 0.0;
-    for (int q = lane; q < C; q += 64) s += d.Yf[((size_t)f * 6 + r) * C + q] * d.dx[q];
+  for (int u = 0; u < kTgU; ++u) tv[u] = d.target[min(tid + u * nth, nt3 - 1)];
+  double yr[6][2], dxv[2];
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-    w[r] = d.zf[(size_t)f * 6 + r] - s;
+  for (int sl = 0; sl < 2; ++sl) {
+    const int q = lane + 64 * sl, qc = min(q, C - 1);
+    const double v = d.dx[qc];
+    dxv[sl] = q < C ? v : 0.0;
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+      const double yv = d.Yf[((size_t)f * 6 + r) * C + qc];
+      yr[r][sl] = q < C ? yv : 0.0;
+    }
   }
-  const double* L = d.Lf + (size_t)f * 36;
+  const int cm0 = __builtin_amdgcn_readfirstlane(min(wave, N - 1));  // wave-uniform: scalar loads below
+  const int2 fv0 = d.fview[(size_t)f * N + cm0];
+  // pin the round-1 values here: keeps the compiler from sinking the loads below the gate (one round trip)
+  KB_KEEPS(fv0.x);
+  KB_KEEPS(fv0.y);
 #pragma unroll
-  for (int r = 5; r >= 0; --r) {
-    double s = w[r];
+  for (int u = 0; u < kTgU; ++u) KB_KEEP(tv[u]);
 #pragma unroll
-    for (int k = r + 1; k < 6; ++k) s -= L[k * 6 + r] * w[k];
-    w[r] = s / L[r * 6 + r];
+  for (int sl = 0; sl < 2; ++sl) {
+    KB_KEEP(dxv[sl]);
+#pragma unroll
+    for (int r = 0; r < 6; ++r) KB_KEEP(yr[r][sl]);
   }
-  if (wave == 0 && lane < 6) {
-    double xv = w[0];
+  if (gate && done) return;
+  if (tg_lds && cost_pass) {
 #pragma unroll
-    for (int r = 1; r < 6; ++r) xv = (lane == r) ? w[r] : xv;
-    d.dx[C + 6 * f + lane] = xv;
-    d.rhs[C + 6 * f + lane] = d.gf[(size_t)f * 6 + lane];
+    for (int u = 0; u < kTgU; ++u)
+      if (tid + u * nth < nt3) tg[tid + u * nth] = tv[u];
+    for (int q = tid + kTgU * nth; q < nt3; q += nth) tg[q] = d.target[q];
   }
+  const bool work = !gate || sok;
+  double w[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
   double cost = 0.0;
-  if (do_update) {
-    const double* s0 = d.state + (size_t)c->cur * d.S;
-    double* s1 = d.state + (size_t)(1 - c->cur) * d.S;
-    double np[7];
-    update_pose(s0 + d.off_frame + 7 * f, w, np);  // every lane: the new pose stays in registers
-    if (wave == 0 && lane == 0)
-      for (int q = 0; q < 7; ++q) s1[d.off_frame + 7 * f + q] = np[q];
-    if (with_cost) {
-      for (int cm = wave; cm < N; cm += nw) {
-        const int v = d.frame_vcam[f * N + cm];
-        if (v < 0) continue;
-        double R[9], t[3];
-        cam_from_state(d, s1, cm, np, R, t);
-        const int model = d.model[cm];
-        const double* intr = s1 + cm * KB_MAX_INTR;
-        const int o0 = d.view_off[v], o1 = d.view_off[v + 1];
-        for (int k = o0 + lane; k < o1; k += 64) {
-          const int cid = d.cid[k];
-          const double X0 = d.target[3 * cid], X1 = d.target[3 * cid + 1], X2 = d.target[3 * cid + 2];
-          const double p0 = R[0] * X0 + R[1] * X1 + R[2] * X2 + t[0];
-          const double p1 = R[3] * X0 + R[4] * X1 + R[5] * X2 + t[1];
-          const double p2 = R[6] * X0 + R[7] * X1 + R[8] * X2 + t[2];
-          double u, vv;
-          project(model, intr, p0, p1, p2, u, vv);
-          const double2 yv = d.y[k];
-          const double e0 = yv.x - u, e1 = yv.y - vv;
-          cost += e0 * e0 + e1 * e1;
-        }
-      }
+  if (work) {
+    // ---- round 2: loads indexed by round 1 (state buffer, corner ids of the view)
+    double pose[7], Lc[12], intr[KB_MAX_INTR];
+    const double* s0 = d.state + (size_t)cur * d.S;
+    double* s1 = d.state + (size_t)(1 - cur) * d.S;
+    if (do_update) {
 #pragma unroll
-      for (int o = 32; o > 0; o >>= 1) cost += __shfl_xor(cost, o);
+      for (int q = 0; q < 7; ++q) pose[q] = s0[d.off_frame + 7 * f + q];
+    }
+    int cid0[2] = {0, 0};
+    double2 y0[2];
+    if (cost_pass) {
+      const double* Lp = cam_L(d, 1 - cur) + cm0 * 12;
+#pragma unroll
+      for (int q = 0; q < 12; ++q) Lc[q] = Lp[q];
+#pragma unroll
+      for (int q = 0; q < KB_MAX_INTR; ++q) intr[q] = s1[cm0 * KB_MAX_INTR + q];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int k = min(fv0.x + lane + 64 * u, max(fv0.y - 1, 0));
+        cid0[u] = d.cid[k];
+        y0[u] = d.y[k];
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+      double s = yr[r][0] * dxv[0] + yr[r][1] * dxv[1];
+      s = wave_sum_d(s);
+      w[r] = d.zf[(size_t)f * 6 + r] - s;
+    }
+    const double* L = d.Lf + (size_t)f * 36;
+#pragma unroll
+    for (int r = 5; r >= 0; --r) {
+      double s = w[r];
+#pragma unroll
+      for (int k = r + 1; k < 6; ++k) s -= L[k * 6 + r] * w[k];
+      w[r] = s / L[r * 6 + r];
+    }
+    if (wave == 0 && lane < 6) {
+      double xv = w[0];
+#pragma unroll
+      for (int r = 1; r < 6; ++r) xv = (lane == r) ? w[r] : xv;
+      d.dx[C + 6 * f + lane] = xv;
+      d.rhs[C + 6 * f + lane] = d.gf[(size_t)f * 6 + lane];
+    }
+    if (do_update) {
+      double np[7];
+      update_pose(pose, w, np);  // every lane: the new pose stays in registers
+      if (wave == 0 && lane < 7) {
+        double pv = np[0];
+#pragma unroll
+        for (int q = 1; q < 7; ++q) pv = (lane == q) ? np[q] : pv;
+        s1[d.off_frame + 7 * f + lane] = pv;
+      }
+      if (with_cost) {
+        const double* tgt = tg_lds ? tg : d.target;
+        if (tg_lds) __syncthreads();  // target staged
+        double Ri[9], ti[3];
+        pose_inverse(np, Ri, ti);
+        for (int cm = wave; cm < N; cm += nw) {
+          int2 fv = fv0;
+          if (cm != wave) {  // rigs with more than 8 cameras: second view of this wave (unbatched loads)
+            fv = d.fview[(size_t)f * N + cm];
+            const double* Lp = cam_L(d, 1 - cur) + cm * 12;
+#pragma unroll
+            for (int q = 0; q < 12; ++q) Lc[q] = Lp[q];
+#pragma unroll
+            for (int q = 0; q < KB_MAX_INTR; ++q) intr[q] = s1[cm * KB_MAX_INTR + q];
+          }
+          if (fv.y <= fv.x) continue;
+          double R[9], t[3];
+          rt_mul(Lc, Lc + 9, Ri, ti, R, t);  // T_cam_w = L_cam(candidate) T_f^-1
+          const int model = d.model[cm];
+          for (int k0 = fv.x; k0 < fv.y; k0 += 128) {
+            int cid[2];
+            double2 yv[2];
+            if (k0 == fv0.x && cm == wave) {
+#pragma unroll
+              for (int u = 0; u < 2; ++u) {
+                cid[u] = cid0[u];
+                yv[u] = y0[u];
+              }
+            } else {
+#pragma unroll
+              for (int u = 0; u < 2; ++u) {
+                const int k = min(k0 + lane + 64 * u, fv.y - 1);
+                cid[u] = d.cid[k];
+                yv[u] = d.y[k];
+              }
+            }
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+              if (k0 + lane + 64 * u < fv.y) {
+                const double X0 = tgt[3 * cid[u]], X1 = tgt[3 * cid[u] + 1], X2 = tgt[3 * cid[u] + 2];
+                const double p0 = R[0] * X0 + R[1] * X1 + R[2] * X2 + t[0];
+                const double p1 = R[3] * X0 + R[4] * X1 + R[5] * X2 + t[1];
+                const double p2 = R[6] * X0 + R[7] * X1 + R[8] * X2 + t[2];
+                double u0, u1;
+                project(model, intr, p0, p1, p2, u0, u1);
+                const double e0 = yv[u].x - u0, e1 = yv[u].y - u1;
+                cost += e0 * e0 + e1 * e1;
+              }
+            }
+          }
+        }
+        cost = wave_sum_d(cost);
+      }
     }
   }
   if (lane == 0) sc[wave] = cost;
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (tid == 0 && work) {
     double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
     for (int q = 0; q < nw; ++q) a0 += sc[q];
 #pragma unroll
@@ -1235,11 +1447,7 @@ __global__ void __launch_bounds__(512) k_backsub(KbDev d, int gate, int do_updat
       a2 += w[r] * w[r];
       a3 += w[r] * g;
     }
-    double* bp = d.bpart + (size_t)f * 4;
-    bp[0] = a0;
-    bp[1] = a1;
-    bp[2] = a2;
-    bp[3] = a3;
+    reinterpret_cast<double4*>(d.bpart)[f] = make_double4(a0, a1, a2, a3);
   }
 }
 
@@ -1272,8 +1480,7 @@ __global__ void __launch_bounds__(256) k_cost(KbDev d, int which) {
       const double e0 = yv.x - u, e1 = yv.y - w;
       acc += e0 * e0 + e1 * e1;
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+    acc = wave_sum_d(acc);
   }
   if (lane == 0) part[wave] = acc;
   __syncthreads();
@@ -1305,67 +1512,14 @@ __global__ void __launch_bounds__(256) k_reduce_cost(KbDev d) {
   }
 }
 
-// k_post: per-frame [cost, max, dd, dr] of k_backsub (+ camera part) -> red_local; then (one GPU) the
-// accept/revert policy, the next pass's prelude and its camera chain
-__global__ void __launch_bounds__(256) k_post(KbDev d, int with_policy) {
+// sharded runs: the policy after the all-reduce of red (accept / revert, next pass prelude)
+__global__ void k_policy(KbDev d) {
   KbCtrl* c = d.ctrl;
   if (c->done) return;
-  __shared__ double sh[4][4];
-  KB_STAMP(d, 8);
-  if (c->solve_ok) {
-    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
-    for (int q = threadIdx.x; q < d.nblk_bs; q += blockDim.x) {
-      const double4 bp = reinterpret_cast<const double4*>(d.bpart)[q];
-      s0 += bp.x;
-      s1 = fmax(s1, bp.y);
-      s2 += bp.z;
-      s3 += bp.w;
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      s0 += __shfl_xor(s0, o);
-      s1 = fmax(s1, __shfl_xor(s1, o));
-      s2 += __shfl_xor(s2, o);
-      s3 += __shfl_xor(s3, o);
-    }
-    const int w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) {
-      sh[w][0] = s0;
-      sh[w][1] = s1;
-      sh[w][2] = s2;
-      sh[w][3] = s3;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-      for (int q = 0; q < (int)(blockDim.x >> 6); ++q) {
-        a0 += sh[q][0];
-        a1 = fmax(a1, sh[q][1]);
-        a2 += sh[q][2];
-        a3 += sh[q][3];
-      }
-      d.red_local[0] = a0;
-      d.red_local[1] = a2 + d.camstat[1];
-      d.red_local[2] = a3 + d.camstat[2];
-      d.red_local[3] = fmax(a1, d.camstat[0]);
-    }
-  }
-  KB_STAMP(d, 9);
-  if (!with_policy) return;
-  if (threadIdx.x == 0) pol_post(c, d, d.red_local);
-  __syncthreads();
-  KB_STAMP(d, 10);
-  next_pass_block(d);
-  KB_STAMP(d, 11);
-}
-
-// sharded runs: the policy after the all-reduce of red
-__global__ void __launch_bounds__(256) k_policy(KbDev d) {
-  KbCtrl* c = d.ctrl;
-  if (c->done) return;
-  if (threadIdx.x == 0) pol_post(c, d, d.red);
-  __syncthreads();
-  next_pass_block(d);
+  KbCtrl cl = *c;
+  pol_post(&cl, d, d.red);
+  if (!cl.done) pol_pre(&cl);
+  *c = cl;
 }
 
 __global__ void k_pol_init(KbDev d, KbOpts o) {

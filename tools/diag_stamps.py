@@ -31,4 +31,3 @@ for rep in range(3):
     print("  k_solve  stageA %.2f  camexp %.2f  ldl %.2f  solves %.2f  stats+update %.2f" % (
         us(0, 1), us(1, 2), us(2, 3), us(3, 4), us(4, 5)))
     print("  clock in k_solve: %.0f MHz" % ((t[41] - t[40]) / max(1, t[5] - t[0]) * 100.0))
-    print("  k_post   reduce %.2f  policy %.2f  next(prep) %.2f" % (us(8, 9), us(9, 10), us(10, 11)))
