@@ -197,6 +197,7 @@ kb_handle* kb_create(const kb_layout* L) {
   rc |= h->alloc(&d.psum_local, (size_t)d.Wtot);
   d.psum = d.psum_local;
   d.psum_rows = 1;
+  d.dbg_stop = -1;
   rc |= h->alloc(&d.ticket, 16);
   rc |= h->alloc(&d.Hcc, (size_t)h->C * h->C);
   rc |= h->alloc(&d.gc, (size_t)h->C);
@@ -774,21 +775,42 @@ int kb_comm_init(kb_handle* h, const void* uid, int32_t nranks, int32_t rank) {
 }
 
 #ifdef KB_STAMPS
-// diagnostic build only: run n GN passes eagerly and return the last pass's phase stamps (100 MHz ticks)
-int kb_diag_stamps(kb_handle* h, int n, unsigned long long* out, int cap) {
+// diagnostic build only: average duration (us, HIP events over `reps` launches) of one kernel of the GN pass run
+// up to stop point `stop` (KB_STAMP): which = 0 fused build, 1 camera solve, 2 back-substitution.
+int kb_diag_phase_time(kb_handle* h, int which, int stop, int reps, double* us) {
   KB_HIP(hipSetDevice(h->device));
-  unsigned long long* st = nullptr;
-  KB_HIP(hipMalloc(&st, sizeof(unsigned long long) * 64));
-  KB_HIP(hipMemset(st, 0, sizeof(unsigned long long) * 64));
-  h->d.stamps = st;
   KbOpts o{1, 0x3fffffff, 0.0, -1.0, -1.0};
   if (ensure_trace(h, 64) || loop_start(h, o)) return -1;
-  for (int i = 0; i < n; ++i)
+  for (int i = 0; i < 2; ++i)
     if (enqueue_pass(h, 1)) return -1;
-  KB_HIP(hipStreamSynchronize(h->stream));
-  KB_HIP(hipMemcpy(out, st, sizeof(unsigned long long) * std::min(cap, 64), hipMemcpyDeviceToHost));
-  h->d.stamps = nullptr;
-  hipFree(st);
+  if (launch_build(h, 0, 1) || launch_colsum(h, 0, false)) return -1;
+  KbDev d = h->d;
+  d.dbg_stop = stop;
+  d.psum = d.part8;
+  d.psum_rows = kColsumRows;
+  hipEvent_t e0, e1;
+  KB_HIP(hipEventCreate(&e0));
+  KB_HIP(hipEventCreate(&e1));
+  int g = 0, one = 1, zero = 0;
+  for (int r = -2; r < reps; ++r) {
+    if (r == 0) KB_HIP(hipEventRecord(e0, h->stream));
+    if (which == 0) {
+      void* args[] = {&d, &g, &one};
+      KB_HIP(hipLaunchKernel(h->fn_build, dim3(d.nblk), dim3(64 * d.wpb), args, h->lds_build, h->stream));
+    } else if (which == 1) {
+      void* args[] = {&d, &g, &zero};
+      KB_HIP(hipLaunchKernel(h->fn_solve, dim3(1), dim3(h->solve_threads), args, h->lds_solve, h->stream));
+    } else {
+      hipLaunchKernelGGL(k_backsub, dim3(d.nblk_bs), dim3(64 * std::min(h->N, 8)), 0, h->stream, d, 0, 1, 1);
+    }
+  }
+  KB_HIP(hipEventRecord(e1, h->stream));
+  KB_HIP(hipEventSynchronize(e1));
+  float ms = 0.f;
+  KB_HIP(hipEventElapsedTime(&ms, e0, e1));
+  *us = 1e3 * ms / reps;
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
   return 0;
 }
 #endif

@@ -73,14 +73,16 @@ struct KbDev {
   double* red;       // [4] (all-reduced; aliases red_local on one GPU)
   double* trace;
   KbCtrl* ctrl;
-  unsigned long long* stamps;  // diagnostic build only (KB_STAMPS): s_memrealtime per phase
+  int dbg_stop;  // diagnostic build only (KB_STAMPS): stop point of the timed kernel (-1: run to the end)
 };
 
 #ifdef KB_STAMPS
-#define KB_STAMP(d, i)                                                              \
-  do {                                                                              \
-    if (threadIdx.x == 0 && blockIdx.x == 0 && (d).stamps)                          \
-      (d).stamps[i] = __builtin_amdgcn_s_memrealtime();                             \
+// diagnostic build only: every thread leaves the kernel at stop point i when d.dbg_stop == i, so the kernel's
+// duration up to that point can be timed from the host (tools/diag_stamps.py); stop points sit where the
+// whole block is converged
+#define KB_STAMP(d, i)          \
+  do {                          \
+    if ((d).dbg_stop == (i)) return; \
   } while (0)
 #else
 #define KB_STAMP(d, i) \
@@ -101,6 +103,15 @@ __device__ __forceinline__ void d16_rowcol(int e, int& a, int& b) {
   }
   a = r;
   b = r + e;
+}
+// closed form of d16_rowcol: row a = largest with a(33 - a)/2 <= e
+__device__ __forceinline__ void d16_rowcol_fast(int e, int& a, int& b) {
+  int r = (int)((33.0f - sqrtf(1089.0f - 8.0f * (float)e)) * 0.5f);
+  r = r < 0 ? 0 : (r > 15 ? 15 : r);
+  if (r * (33 - r) / 2 > e) --r;
+  else if (r < 15 && (r + 1) * (32 - r) / 2 <= e) ++r;
+  a = r;
+  b = r + e - r * (33 - r) / 2;
 }
 __host__ __device__ __forceinline__ int upper_index(int a, int b, int n) { return a * n - a * (a - 1) / 2 + (b - a); }
 

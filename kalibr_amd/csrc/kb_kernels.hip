@@ -286,21 +286,33 @@ __global__ void __launch_bounds__(256) k_pre(KbDev d, int gate) {
   chain_block(d, d.state + (size_t)cur * d.S + d.off_base, cur);
 }
 
-// in-place 6x6 Cholesky (lower) in LDS, by one thread; returns 0 if not PD
-__device__ __forceinline__ int chol6(double* L) {
-  int ok = 1;
-  for (int j = 0; j < 6; ++j) {
-    double dd = L[j * 6 + j];
-    for (int k = 0; k < j; ++k) dd -= L[j * 6 + k] * L[j * 6 + k];
-    if (!(dd > 0.0)) ok = 0;
-    dd = sqrt(dd);
-    L[j * 6 + j] = dd;
-    for (int i = j + 1; i < 6; ++i) {
-      double s2 = L[i * 6 + j];
-      for (int k = 0; k < j; ++k) s2 -= L[i * 6 + k] * L[j * 6 + k];
-      L[i * 6 + j] = s2 / dd;
-    }
+// 6x6 Cholesky of A + lam2 I by one wave (lanes 0..5 hold rows; column k broadcast with v_readlane):
+// L (row-major lower, upper zero) and 1/diag(L) to LDS, L also to HBM.  Returns false if not PD.
+__device__ __forceinline__ bool chol6_wave(const double* A, double lam2, double* L, double* rdiag, double* Lg,
+                                           int lane) {
+  double row[6];
+  const int i = lane < 6 ? lane : 5;
+#pragma unroll
+  for (int j = 0; j < 6; ++j) row[j] = A[i * 6 + j] + ((i == j) ? lam2 : 0.0);
+  bool ok = true;
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    const double dkk = readlane_d(row[k], k);
+    ok = ok && (dkk > 0.0);
+    const double sk = sqrt(dkk), rk = 1.0 / sk;
+    row[k] = (lane == k) ? sk : ((lane > k) ? row[k] * rk : row[k]);
+    if (lane == k) rdiag[k] = rk;
+    const double lik = (lane > k) ? row[k] : 0.0;
+#pragma unroll
+    for (int j = k + 1; j < 6; ++j) row[j] -= lik * readlane_d(row[k], j);
   }
+  if (lane < 6)
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      const double v = (j <= lane) ? row[j] : 0.0;
+      L[lane * 6 + j] = v;
+      Lg[lane * 6 + j] = v;
+    }
   return ok;
 }
 
@@ -328,8 +340,8 @@ __device__ __forceinline__ void schur_accumulate(const int C, const int Wt, cons
 }
 
 // Y = L^-1 H_fc (thread per column), z = L^-1 g_f (last thread); stored to LDS and HBM
-__device__ __forceinline__ void schur_forward(const KbDev& d, int f, const double* L, const double* Hfc_lds,
-                                              const double* g_lds, double* Y, double* z) {
+__device__ __forceinline__ void schur_forward(const KbDev& d, int f, const double* L, const double* rdiag,
+                                              const double* Hfc_lds, const double* g_lds, double* Y, double* z) {
   const int C = d.C, t = threadIdx.x;
   if (t < C) {
     double yv[6];
@@ -338,7 +350,7 @@ __device__ __forceinline__ void schur_forward(const KbDev& d, int f, const doubl
       double s2 = Hfc_lds ? Hfc_lds[r * C + t] : d.Hfc[((size_t)f * 6 + r) * C + t];
 #pragma unroll
       for (int k = 0; k < r; ++k) s2 -= L[r * 6 + k] * yv[k];
-      yv[r] = s2 / L[r * 6 + r];
+      yv[r] = s2 * rdiag[r];
       Y[r * C + t] = yv[r];
       d.Yf[((size_t)f * 6 + r) * C + t] = yv[r];
     }
@@ -349,7 +361,7 @@ __device__ __forceinline__ void schur_forward(const KbDev& d, int f, const doubl
       double s2 = g_lds ? g_lds[r] : d.gf[(size_t)f * 6 + r];
 #pragma unroll
       for (int k = 0; k < r; ++k) s2 -= L[r * 6 + k] * zv[k];
-      zv[r] = s2 / L[r * 6 + r];
+      zv[r] = s2 * rdiag[r];
       z[r] = zv[r];
       d.zf[(size_t)f * 6 + r] = zv[r];
     }
@@ -362,10 +374,9 @@ __device__ __forceinline__ void schur_forward(const KbDev& d, int f, const doubl
 template <int M>
 __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
   KbCtrl* c = d.ctrl;
-  if (gate && (c->done || !c->do_build)) return;
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const int N = d.N, C = d.C, WPB = d.wpb, NS = d.nsplit;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, nth = blockDim.x;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, nth = blockDim.x, tid = threadIdx.x;
   double* Xw = sm + wave * 64 * XS;
   double* Hw = sm + WPB * 64 * XS;   // [WPB][256] per-wave partial local Hessians
   double* Hv = Hw + WPB * 256;       // [N][256] per-view local Hessian of the current frame
@@ -383,65 +394,119 @@ __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
   double* Kl = z + 8;                // [N(N-1)/2][36] K_{i,j}, j < i, at (i(i-1)/2 + j)
   double* tg = Kl + 18 * N * (N - 1);  // [n_target][3] target corners (when staged)
   __shared__ int okl;
-  const double* s = d.state + (size_t)c->cur * d.S;
+  __shared__ double cst[KB_MAX_CAMS][24];  // per camera: chain L (12) | intrinsics (10)
+  __shared__ int ctab[2][KB_MAX_CAMS];      // per camera: first intrinsic column | baseline column
+  __shared__ double rdg[6];
+  const int W = d.W, Wt = W - C;
+  const int f0 = blockIdx.x * d.gframes, f1 = min(d.F, f0 + d.gframes);
+  const int cam = __builtin_amdgcn_readfirstlane(wave % N), sp = __builtin_amdgcn_readfirstlane(wave / N);
+  // ---- round 1: launch-independent loads, unconditional (clamped) and pinned before the gate
+  const int done = c->done, dob = c->do_build, cur = c->cur;
   const bool tg_lds = d.K * 3 <= kTargetLds;
-  if (tg_lds)
-    for (int q = threadIdx.x; q < 3 * d.K; q += nth) tg[q] = d.target[q];
-  for (int q = threadIdx.x; q < 18 * N * (N - 1); q += nth) {
+  const int nt3 = 3 * d.K;
+  constexpr int kTgU = 2;  // 2 x 256 threads >= 3 x 120 AprilGrid corners
+  double tv[kTgU];
+#pragma unroll
+  for (int u = 0; u < kTgU; ++u) tv[u] = d.target[min(tid + u * nth, nt3 - 1)];
+  int ab[M];
+#pragma unroll
+  for (int m = 0; m < M; ++m) ab[m] = d.tri[min(tid + nth * m, Wt - 1)];
+  int2 fv = d.fview[(size_t)f0 * N + cam];
+#pragma unroll
+  for (int u = 0; u < kTgU; ++u) KB_KEEP(tv[u]);
+#pragma unroll
+  for (int m = 0; m < M; ++m) KB_KEEP(ab[m]);
+  KB_KEEPS(fv.x);
+  KB_KEEPS(fv.y);
+  if (gate && (done || !dob)) return;
+  // ---- round 2: loads indexed by round 1 (accepted state buffer, chains of slot cur, corners of the view)
+  const double* s = d.state + (size_t)cur * d.S;
+  if (tid < N * 22) {
+    const int cm = tid / 22, e = tid % 22;
+    cst[cm][e] = e < 12 ? cam_L(d, cur)[cm * 12 + e] : s[cm * KB_MAX_INTR + e - 12];
+  }
+  if (tid < 2 * N) ctab[tid / N][tid % N] = (tid < N) ? d.col_intr[tid] : d.col_base[tid - N];
+  double fp0[7];  // pose of the block's first frame
+#pragma unroll
+  for (int q = 0; q < 7; ++q) fp0[q] = s[d.off_frame + 7 * f0 + q];
+  int cidn;
+  double2 yn;
+  {
+    const int k = min(fv.x + sp * 64 + lane, max(fv.y - 1, 0));
+    cidn = d.cid[k];
+    yn = d.y[k];
+  }
+  const double* Kc = cam_K(d, cur);
+  for (int q = tid; q < 18 * N * (N - 1); q += nth) {
     const int e = q % 36, ij = q / 36;
     int i = 1;
     while (i * (i + 1) / 2 <= ij) ++i;
     const int j = ij - i * (i - 1) / 2;
-    Kl[q] = cam_K(d, c->cur)[(size_t)(i * N + j) * 36 + e];
+    Kl[q] = Kc[(size_t)(i * N + j) * 36 + e];
+  }
+  if (tg_lds) {
+#pragma unroll
+    for (int u = 0; u < kTgU; ++u)
+      if (tid + u * nth < nt3) tg[tid + u * nth] = tv[u];
+    for (int q = tid + kTgU * nth; q < nt3; q += nth) tg[q] = d.target[q];
   }
   const double* tgt = tg_lds ? tg : d.target;
   const double lam = gate ? c->lambda : d.host_lambda;
   const double lam2 = lam * lam;
-  const int W = d.W, Wt = W - C;
   double acc[M];
-  int ab[M];
 #pragma unroll
   for (int m = 0; m < M; ++m) {
     acc[m] = 0.0;
-    const int e = threadIdx.x + nth * m;
-    ab[m] = (fuse && e < Wt) ? d.tri[e] : 0;
+    const int e = tid + nth * m;
+    ab[m] = (fuse && e < Wt) ? ab[m] : 0;
   }
-  if (threadIdx.x == 0) okl = 1;
+  if (tid == 0) okl = 1;
   KB_STAMP(d, 16);
-  for (int q = threadIdx.x; q < N * 256; q += nth) camsum[q] = 0.0;
+  for (int q = tid; q < N * 256; q += nth) camsum[q] = 0.0;
   __syncthreads();
 
-  const int f0 = blockIdx.x * d.gframes, f1 = min(d.F, f0 + d.gframes);
   const int mrow = lane >> 4, mcol = lane & 15;
-  const int cam = wave % N, sp = wave / N;
   const int model = d.model[cam], nin = d.nintr[cam];
-  const double* intr = s + cam * KB_MAX_INTR;
+  const double* Lc = cst[cam];
+  const double* intr = cst[cam] + 12;
   for (int f = f0; f < f1; ++f) {
-    const double* fp = s + d.off_frame + 7 * f;
+    double fp[7];
+#pragma unroll
+    for (int q = 0; q < 7; ++q) fp[q] = (f == f0) ? fp0[q] : s[d.off_frame + 7 * f + q];
     double Ri[9], ti[3], R[9], t[3];
     pose_inverse(fp, Ri, ti);
-    const double* Lc = cam_L(d, c->cur) + cam * 12;
-    rt_mul(Lc, Lc + 9, Ri, ti, R, t);  // T_cam_w = L_cam T_f^-1
-    const int v = d.frame_vcam[f * N + cam];
+    rt_mul(Lc, Lc + 9, Ri, ti, R, t);  // T_cam_w = L_cam T_f^-1 (chain of the accepted state)
+    KB_STAMP(d, 26);
+    if (f > f0) {  // next frame of a multi-frame block
+      fv = d.fview[(size_t)f * N + cam];
+      const int k = min(fv.x + sp * 64 + lane, max(fv.y - 1, 0));
+      cidn = d.cid[k];
+      yn = d.y[k];
+    }
     v4d acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
-    if (v >= 0) {
-      const int o0 = d.view_off[v], o1 = d.view_off[v + 1];
+    {
+      const int o0 = fv.x, o1 = fv.y;
       for (int base = o0 + sp * 64; base < o1; base += NS * 64) {
         const int k = base + lane;
+        const int cid = cidn;
+        const double2 yv = yn;
+        if (base + NS * 64 < o1) {  // software-pipelined: next chunk's corner ids and keypoints
+          const int kn = min(k + NS * 64, o1 - 1);
+          cidn = d.cid[kn];
+          yn = d.y[kn];
+        }
         double xr[2][16];
 #pragma unroll
         for (int r = 0; r < 2; ++r)
 #pragma unroll
           for (int q = 0; q < 16; ++q) xr[r][q] = 0.0;
         if (k < o1) {
-          const int cid = d.cid[k];
           const double X0 = tgt[3 * cid], X1 = tgt[3 * cid + 1], X2 = tgt[3 * cid + 2];
           const double p0 = R[0] * X0 + R[1] * X1 + R[2] * X2 + t[0];
           const double p1 = R[3] * X0 + R[4] * X1 + R[5] * X2 + t[1];
           const double p2 = R[6] * X0 + R[7] * X1 + R[8] * X2 + t[2];
           double u, w, Jp[6], Ji[2 * KB_MAX_INTR];
           project_jac(model, intr, p0, p1, p2, u, w, Jp, Ji);
-          const double2 yv = d.y[k];
           const double e0 = yv.x - u, e1 = yv.y - w;
 #pragma unroll
           for (int r = 0; r < 2; ++r) {
@@ -459,6 +524,7 @@ __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
             xr[r][15] = -(r == 0 ? e0 : e1);  // column 15 carries -e: H[:,15] = rhs part, H[15][15] = chi^2
           }
         }
+        KB_STAMP(d, 27);
         // two phases of 32 corners (64 rows) through the LDS tile, 16 MFMA k-steps each
 #pragma unroll
         for (int ph = 0; ph < 2; ++ph) {
@@ -512,14 +578,15 @@ __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
     __syncthreads();
     KB_STAMP(d, 19);
     if (wave < N) {  // expansion of view (f, cam = wave) through the 6-D chains
-      const int vc = wave;
-      const bool has = d.frame_vcam[f * N + vc] >= 0;
+      const int vc = __builtin_amdgcn_readfirstlane(wave);
+      const bool has = fv.y > fv.x;  // this wave's camera == vc
       const int nv = d.nintr[vc];
       const double* H = Hv + vc * 256;
       double* wv = Wv + vc * 64;
       double* G = wv + 16;
       if (lane < 36) G[lane] = chain_entry(wv, wv + 9, wv + 12, lane / 6, lane % 6);
       KB_WAVE_SYNC();
+      KB_STAMP(d, 28);
       if (lane < 36) {
         const int a = lane / 6, b = lane % 6;
         double sacc = 0.0;
@@ -541,14 +608,15 @@ __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
         for (int k = 0; k < 6; ++k) sacc += Pv[vc * 36 + a * 6 + k] * G[k * 6 + b];
         dH[vc * 36 + lane] = sacc;  // P_v G_v
       }
+      KB_STAMP(d, 29);
       if (lane < 6 * nv) {
         const int a = lane / nv, q = lane % nv;
         double sacc = 0.0;
 #pragma unroll
         for (int k = 0; k < 6; ++k) sacc += G[k * 6 + a] * H[k * 16 + 6 + q];
         sacc = has ? sacc : 0.0;  // G^T H_dI
-        Fc[a * C + d.col_intr[vc] + q] = sacc;
-        d.Hfc[((size_t)f * 6 + a) * C + d.col_intr[vc] + q] = sacc;
+        Fc[a * C + ctab[0][vc] + q] = sacc;
+        d.Hfc[((size_t)f * 6 + a) * C + ctab[0][vc] + q] = sacc;
       }
     }
     __syncthreads();
@@ -572,22 +640,21 @@ __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
 #pragma unroll
           for (int k = 0; k < 6; ++k) sacc += Pv[i * 36 + a * 6 + k] * K[k * 6 + b];
         }
-        Fc[a * C + d.col_base[j] + b] = sacc;
-        d.Hfc[((size_t)f * 6 + a) * C + d.col_base[j] + b] = sacc;
+        Fc[a * C + ctab[1][j] + b] = sacc;
+        d.Hfc[((size_t)f * 6 + a) * C + ctab[1][j] + b] = sacc;
       }
     }
     KB_STAMP(d, 20);
     if (fuse) {
       __syncthreads();
       KB_STAMP(d, 21);
-      if (threadIdx.x == 0) {
-        for (int q = 0; q < 36; ++q) L[q] = Fh[q] + ((q % 7 == 0) ? lam2 : 0.0);
-        if (!chol6(L)) okl = 0;
-        for (int q = 0; q < 36; ++q) d.Lf[(size_t)f * 36 + q] = L[q];
+      if (wave == 0) {
+        const bool ok = chol6_wave(Fh, lam2, L, rdg, d.Lf + (size_t)f * 36, lane);
+        if (!ok && lane == 0) okl = 0;
       }
       __syncthreads();
       KB_STAMP(d, 22);
-      schur_forward(d, f, L, Fc, Fg, Y, z);
+      schur_forward(d, f, L, rdg, Fc, Fg, Y, z);
       __syncthreads();
       KB_STAMP(d, 23);
       schur_accumulate<M>(C, Wt, W, Y, z, ab, acc);
@@ -599,7 +666,7 @@ __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
   for (int q = threadIdx.x; q < N * 136; q += nth) {
     const int qc = q / 136;
     int a, b;
-    d16_rowcol(q % 136, a, b);
+    d16_rowcol_fast(q % 136, a, b);
     prow[q] = camsum[qc * 256 + a * 16 + b];
   }
   if (fuse) {
@@ -626,6 +693,7 @@ __global__ void __launch_bounds__(256) k_schur(KbDev d, int gate) {
   double* L = Y + 6 * C;  // [36]
   double* z = L + 36;     // [8]
   __shared__ int okl;
+  __shared__ double rdg[6];
   const double lam = gate ? c->lambda : d.host_lambda;
   const double lam2 = lam * lam;
   double acc[M];
@@ -640,13 +708,12 @@ __global__ void __launch_bounds__(256) k_schur(KbDev d, int gate) {
   const int f0 = blockIdx.x * d.gframes, f1 = min(d.F, f0 + d.gframes);
   for (int f = f0; f < f1; ++f) {
     __syncthreads();
-    if (threadIdx.x == 0) {
-      for (int q = 0; q < 36; ++q) L[q] = d.Hff[(size_t)f * 36 + q] + ((q % 7 == 0) ? lam2 : 0.0);
-      if (!chol6(L)) okl = 0;
-      for (int q = 0; q < 36; ++q) d.Lf[(size_t)f * 36 + q] = L[q];
+    if (threadIdx.x < 64) {
+      const bool ok = chol6_wave(d.Hff + (size_t)f * 36, lam2, L, rdg, d.Lf + (size_t)f * 36, threadIdx.x);
+      if (!ok && threadIdx.x == 0) okl = 0;
     }
     __syncthreads();
-    schur_forward(d, f, L, nullptr, nullptr, Y, z);
+    schur_forward(d, f, L, rdg, nullptr, nullptr, Y, z);
     __syncthreads();
     schur_accumulate<M>(C, Wt, W, Y, z, ab, acc);
   }
@@ -673,7 +740,7 @@ __global__ void __launch_bounds__(256) k_colsum(KbDev d, int gate) {
   const int e = blockIdx.x * 64 + l, ry = blockIdx.y;
   const int ec = min(e, d.Wtot - 1);
   double s = 0.0;
-  constexpr int U = 8, step = 4 * kColsumRows;
+  constexpr int U = 16, step = 4 * kColsumRows;
   for (int b0 = ry + kColsumRows * w4; b0 < d.nblk; b0 += U * step) {
     double v[U];
 #pragma unroll
@@ -885,7 +952,7 @@ __device__ __forceinline__ void solve_stage(const KbDev& d, double* K, double* H
       } else if (q < n1) {
         const int r = q - n0, cam = r / 136;
         int a, b;
-        d16_rowcol(r % 136, a, b);
+        d16_rowcol_fast(r % 136, a, b);
         Hs[cam * 256 + a * 16 + b] = v[u];
         Hs[cam * 256 + b * 16 + a] = v[u];
       } else if (q < n2) {
@@ -910,6 +977,15 @@ __device__ __forceinline__ int cidx_col(int e, int C) {
   return j;
 }
 
+// 1/x by v_rcp_f64 + two Newton steps (a short dependent chain; within an ulp of the IEEE quotient)
+__device__ __forceinline__ double recip_d(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  double e = fma(-x, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-x, r, 1.0);
+  return fma(r, e, r);
+}
+
 // LDL^T + the three triangular solves of one wave, matrix rows in registers (lane i holds row i of the
 // trailing matrix, CM >= C padded with the identity).  Step k broadcasts row k with v_readlane (no LDS), and
 // lanes i > k apply S[i][j] -= (S[i][k] / D_k) S[k][j].  Row i freezes at step i, so lane i ends holding
@@ -931,7 +1007,7 @@ __device__ __forceinline__ bool ldl_solve_reg(const double* S, const double* bv,
   for (int k = 0; k < CM; ++k) {
     const double Dk = readlane_d(row[k], k);
     ok = ok && (Dk > 0.0);
-    const double rdk = 1.0 / Dk;
+    const double rdk = recip_d(Dk);
     rD = (lane == k) ? rdk : rD;
     const double f = (lane > k) ? row[k] * rdk : 0.0;
 #pragma unroll
@@ -973,15 +1049,14 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update) {
   int* ptab = ci + C;                // [(C-1)C/2] pair table of the trailing triangle: ii<<16 | jj (CM == 0)
   __shared__ int okl;
   __shared__ double nbase[KB_MAX_CAMS * 7];  // candidate baselines
+  __shared__ int ctab[3][KB_MAX_CAMS];       // per camera: #intrinsics | first intrinsic column | baseline column
   const double lam = gate ? c->lambda : d.host_lambda;
   const double lam2 = lam * lam;
   const int cur = c->cur;
   KB_STAMP(d, 0);
-#ifdef KB_STAMPS
-  if (tid == 0 && d.stamps) d.stamps[40] = __builtin_amdgcn_s_memtime();
-#endif
   // phase A: stage K, column info, per-camera sums and the Schur sums in LDS (one row: psum)
   solve_stage<4>(d, K, Hs, S, bv, ci, tid, nth);
+  if (tid < 3 * N) ctab[tid / N][tid % N] = tid < N ? d.nintr[tid] : (tid < 2 * N ? d.col_intr[tid - N] : d.col_base[tid - 2 * N]);
   if (CM == 0)
     for (int q = tid; q < (C - 1) * C / 2; q += nth) {
       const int ii = tri_row(q);
@@ -1166,15 +1241,15 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update) {
         if (64 * r >= N * KB_MAX_INTR) break;  // wave-uniform
         const int q = lane + 64 * r;
         const int cm = min(q / KB_MAX_INTR, N - 1), xi = q % KB_MAX_INTR;
-        const bool act = q < N * KB_MAX_INTR && xi < d.nintr[cm];
-        const int col = act ? d.col_intr[cm] + xi : 0;
+        const bool act = q < N * KB_MAX_INTR && xi < ctab[0][cm];
+        const int col = act ? ctab[1][cm] + xi : 0;
         const double v0 = __shfl(x[0], col & 63), v1 = __shfl(x[1], col & 63);
         const double dv = (col >> 6) ? v1 : v0;
         if (q < N * KB_MAX_INTR) out[q] = vin[r] + (act ? dv : 0.0);
       }
       if (N > 1) {
         double d6[6], nb[7];
-        const int cb = d.col_base[jb];
+        const int cb = ctab[2][jb];
 #pragma unroll
         for (int q = 0; q < 6; ++q) {
           const int col = cb + q;
@@ -1192,9 +1267,6 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update) {
     }
   }
   KB_STAMP(d, 5);
-#ifdef KB_STAMPS
-  if (tid == 0 && d.stamps) d.stamps[41] = __builtin_amdgcn_s_memtime();
-#endif
   if (do_update) {
     __syncthreads();
     chain_block(d, nbase, 1 - cur);  // chains of the candidate state (k_backsub's cost, next build if accepted)
@@ -1317,6 +1389,7 @@ __global__ void __launch_bounds__(512) k_backsub(KbDev d, int gate, int do_updat
     for (int r = 0; r < 6; ++r) KB_KEEP(yr[r][sl]);
   }
   if (gate && done) return;
+  KB_STAMP(d, 30);
   if (tg_lds && cost_pass) {
 #pragma unroll
     for (int u = 0; u < kTgU; ++u)
@@ -1364,6 +1437,7 @@ __global__ void __launch_bounds__(512) k_backsub(KbDev d, int gate, int do_updat
       for (int k = r + 1; k < 6; ++k) s -= L[k * 6 + r] * w[k];
       w[r] = s / L[r * 6 + r];
     }
+    KB_STAMP(d, 31);
     if (wave == 0 && lane < 6) {
       double xv = w[0];
 #pragma unroll
@@ -1380,6 +1454,7 @@ __global__ void __launch_bounds__(512) k_backsub(KbDev d, int gate, int do_updat
         for (int q = 1; q < 7; ++q) pv = (lane == q) ? np[q] : pv;
         s1[d.off_frame + 7 * f + lane] = pv;
       }
+      KB_STAMP(d, 32);
       if (with_cost) {
         const double* tgt = tg_lds ? tg : d.target;
         if (tg_lds) __syncthreads();  // target staged
@@ -1435,6 +1510,7 @@ __global__ void __launch_bounds__(512) k_backsub(KbDev d, int gate, int do_updat
       }
     }
   }
+  KB_STAMP(d, 33);
   if (lane == 0) sc[wave] = cost;
   __syncthreads();
   if (tid == 0 && work) {
