@@ -1,4 +1,5 @@
-"""In-tree build of libkalibr_hip.so for gfx950 (explicit hipcc, no JIT cache)."""
+"""In-tree builds: libkalibr_hip.so (HIP kernels + C-ABI, gfx950, explicit hipcc, no JIT cache) and
+libkalibr_backend.so (the C++ host layer over the C-ABI, host/kalibr_backend.*, plain g++)."""
 import os
 import subprocess
 
@@ -26,6 +27,23 @@ def build(force=False):
     return OUT
 
 
+HOST_SRC = os.path.join(HERE, "host", "kalibr_backend.cpp")
+HOST_OUT = os.path.join(HERE, "libkalibr_backend.so")
+INCLUDE = os.path.join(HERE, "..", "include")
+CXX = os.environ.get("CXX", "g++")
+
+
+def build_host(force=False):
+    """C++ host layer (LinearSystemSolver / TrustRegionPolicy / Optimizer2 mirror) linked to libkalibr_hip.so."""
+    deps = [HOST_SRC, os.path.join(HERE, "host", "kalibr_backend.hpp"), OUT]
+    if force or not os.path.exists(HOST_OUT) or any(os.path.getmtime(p) > os.path.getmtime(HOST_OUT) for p in deps):
+        cmd = [CXX, "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-I", INCLUDE, "-o", HOST_OUT + ".tmp", HOST_SRC,
+               "-L", HERE, "-lkalibr_hip", "-Wl,-rpath,$ORIGIN"]
+        subprocess.run(cmd, check=True)
+        os.replace(HOST_OUT + ".tmp", HOST_OUT)
+    return HOST_OUT
+
+
 def build_stamps():
     """Diagnostic variant with per-phase s_memrealtime stamps (tools/diag_stamps.py only)."""
     out = os.path.join(HERE, "libkalibr_hip_stamps.so")
@@ -36,3 +54,4 @@ def build_stamps():
 
 if __name__ == "__main__":
     print(build(force=True))
+    print(build_host(force=True))

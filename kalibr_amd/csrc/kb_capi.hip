@@ -728,11 +728,10 @@ int kb_build_kernel_stats(kb_handle* h, double* avg_ms, double* bytes_per_launch
   hipEventDestroy(e1);
   h->build_ms = tot / reps;
   if (avg_ms) *avg_ms = h->build_ms;
-  // algorithmic bytes: observations (y 16 B + id 2 B per corner), view/frame index tables, state,
-  // written frame blocks (H_ff, g_f, H_fc) and per-block camera partials.
-  // observations (y 16 B + id 2 B per corner), view/frame tables, state; written frame blocks
-  // (H_ff, g_f, H_fc), Schur factors (L, Y, z) and the per-block partial rows.
-  const double bytes = 18.0 * h->NC + 4.0 * (h->V + 1) + 4.0 * h->F * h->N + 8.0 * h->S +
+  // algorithmic bytes of one launch: observations (y 16 B + corner id 2 B per corner), view ranges (8 B per
+  // frame x camera), state and camera chains read; frame blocks (H_ff, g_f, H_fc), Schur factors (L, Y, z)
+  // and the per-block partial rows written.
+  const double bytes = 18.0 * h->NC + 8.0 * h->F * h->N + 8.0 * h->S + 8.0 * (12.0 * h->N + 36.0 * h->N * h->N) +
                        8.0 * h->F * (36 + 6 + 6.0 * h->C) + 8.0 * h->F * (36 + 6 + 6.0 * h->C) +
                        8.0 * h->d.nblk * h->d.Wtot;
   if (bytes_per_launch) *bytes_per_launch = bytes;

@@ -1,0 +1,339 @@
+// kalibr_backend.cpp -- host layer over the kalibr_hip C-ABI (see kalibr_backend.hpp for the reference map).
+#include "kalibr_backend.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <iostream>
+
+#include "kalibr_hip.h"
+
+namespace kalibr_amd {
+namespace backend {
+
+// ---------------------------------------------------------------- LinearSystemSolver defaults
+void LinearSystemSolver::setConditioner(const std::vector<double>& diag) {
+  if (diag.size() != _JCols)  // LinearSystemSolver.cpp:98-102
+    throw Exception("The diagonal conditioner must have the same number of rows as the Hessian matrix");
+  _diagonalConditioner = diag;
+}
+
+void LinearSystemSolver::setConstantConditioner(double diag) {
+  _diagonalConditioner.assign(_JCols, diag);  // LinearSystemSolver.cpp:104-107
+}
+
+// ---------------------------------------------------------------- GpuLinearSystemSolver
+GpuLinearSystemSolver::GpuLinearSystemSolver(const GpuOptions& o) : _opt(o) {}
+
+GpuLinearSystemSolver::~GpuLinearSystemSolver() {
+  if (_h) kb_destroy(static_cast<kb_handle*>(_h));
+}
+
+void GpuLinearSystemSolver::check(int rc, const char* what) const {
+  if (rc < 0) throw Exception(std::string(what) + ": " + kb_last_error());
+}
+
+void GpuLinearSystemSolver::initMatrixStructure(const CalibrationProblem& p, bool /*useDiagonalConditioner*/) {
+  if (p.view_offset.size() != p.view_frame.size() + 1 || p.view_cam.size() != p.view_frame.size() ||
+      p.y.size() != 2 * p.corner_id.size() || p.target.size() % 3 != 0)
+    throw Exception("initMatrixStructure: inconsistent problem arrays");
+  if (_h) {
+    kb_destroy(static_cast<kb_handle*>(_h));
+    _h = nullptr;
+  }
+  kb_layout L{};
+  L.n_cams = p.n_cams();
+  L.n_frames = p.n_frames;
+  L.n_target = p.n_target();
+  L.cam_model = p.cam_model.data();
+  L.target_points = p.target.data();
+  L.device = _opt.device;
+  kb_handle* h = kb_create(&L);
+  if (!h) throw Exception(std::string("kb_create: ") + kb_last_error());
+  _h = h;
+  check(kb_upload_observations(h, p.n_views(), p.n_corners(), p.y.data(), p.corner_id.data(), p.view_offset.data(),
+                               p.view_frame.data(), p.view_cam.data()),
+        "kb_upload_observations");
+  if ((int)p.state.size() != kb_state_size(h)) throw Exception("initMatrixStructure: state size mismatch");
+  check(kb_set_state_flat(h, p.state.data()), "kb_set_state_flat");
+  _JRows = 2 * (size_t)p.n_corners();
+  _JCols = (size_t)kb_num_cols(h);
+  _C = (size_t)kb_camera_cols(h);
+  _rhs.assign(_JCols, 0.0);
+  _diagonalConditioner.assign(_JCols, 0.0);
+  _conditioner = 0.0;
+  _built = false;
+  _rhs_valid = false;
+}
+
+double GpuLinearSystemSolver::evaluateError(size_t, bool) {
+  if (!_h) throw Exception("evaluateError: initMatrixStructure first");
+  double J = 0.0;
+  check(kb_eval_cost(static_cast<kb_handle*>(_h), &J), "kb_eval_cost");
+  return J;
+}
+
+void GpuLinearSystemSolver::buildSystem(size_t, bool useMEstimator) {
+  if (!_h) throw Exception("buildSystem: initMatrixStructure first");
+  check(kb_build(static_cast<kb_handle*>(_h), useMEstimator ? 1 : 0), "kb_build");
+  _built = true;
+  _rhs_valid = false;
+}
+
+void GpuLinearSystemSolver::setConstantConditioner(double diag) {
+  LinearSystemSolver::setConstantConditioner(diag);
+  _conditioner = diag;
+  if (_h) check(kb_set_constant_conditioner(static_cast<kb_handle*>(_h), diag), "kb_set_constant_conditioner");
+}
+
+void GpuLinearSystemSolver::setConditioner(const std::vector<double>& diag) {
+  LinearSystemSolver::setConditioner(diag);
+  // the device path conditions with one value (the LM policies only ever set a constant, :86-88)
+  for (double v : diag)
+    if (v != diag.front()) throw Exception("setConditioner: only constant conditioners are supported on the device");
+  setConstantConditioner(diag.empty() ? 0.0 : diag.front());
+}
+
+bool GpuLinearSystemSolver::solveSystem(std::vector<double>& outDx) {
+  if (!_built) throw Exception("solveSystem: buildSystem first");
+  outDx.resize(_JCols);
+  int ok = 0;
+  check(kb_solve(static_cast<kb_handle*>(_h), outDx.data(), &ok), "kb_solve");
+  return ok != 0;
+}
+
+const std::vector<double>& GpuLinearSystemSolver::rhs() const {
+  if (!_rhs_valid && _h && _built) {
+    auto* self = const_cast<GpuLinearSystemSolver*>(this);
+    check(kb_get_rhs(static_cast<kb_handle*>(_h), self->_rhs.data()), "kb_get_rhs");
+    _rhs_valid = true;
+  }
+  return _rhs;
+}
+
+double GpuLinearSystemSolver::rhsJtJrhs() {
+  // rhs^T (J^T J) rhs from the arrow blocks of the last build
+  if (!_built) throw Exception("rhsJtJrhs: buildSystem first");
+  const size_t C = _C, F = (_JCols - _C) / 6;
+  std::vector<double> Hff(36 * F), Hfc(6 * C * F), gf(6 * F), Hcc(C * C), gc(C);
+  double cost = 0.0;
+  check(kb_get_normal_blocks(static_cast<kb_handle*>(_h), Hff.data(), Hfc.data(), gf.data(), Hcc.data(), gc.data(),
+                             &cost),
+        "kb_get_normal_blocks");
+  const std::vector<double>& r = rhs();
+  double s = 0.0;
+  for (size_t a = 0; a < C; ++a)
+    for (size_t b = 0; b < C; ++b) s += r[a] * Hcc[a * C + b] * r[b];
+  for (size_t f = 0; f < F; ++f) {
+    const double* rf = &r[C + 6 * f];
+    for (int a = 0; a < 6; ++a) {
+      for (int b = 0; b < 6; ++b) s += rf[a] * Hff[36 * f + 6 * a + b] * rf[b];
+      for (size_t b = 0; b < C; ++b) s += 2.0 * rf[a] * Hfc[(6 * f + a) * C + b] * r[b];
+    }
+  }
+  return s;
+}
+
+double GpuLinearSystemSolver::applyStateUpdate(const std::vector<double>& dx) {
+  if (dx.size() != _JCols) throw Exception("applyStateUpdate: dx has the wrong size");
+  double deltaX = 0.0;
+  check(kb_apply_update(static_cast<kb_handle*>(_h), dx.data(), &deltaX), "kb_apply_update");
+  return deltaX;
+}
+
+void GpuLinearSystemSolver::revertLastStateUpdate() { check(kb_revert(static_cast<kb_handle*>(_h)), "kb_revert"); }
+
+std::vector<double> GpuLinearSystemSolver::state() const {
+  std::vector<double> s((size_t)kb_state_size(static_cast<kb_handle*>(_h)));
+  check(kb_get_state_flat(static_cast<kb_handle*>(_h), s.data()), "kb_get_state_flat");
+  return s;
+}
+
+void GpuLinearSystemSolver::setState(const std::vector<double>& s) {
+  if ((int)s.size() != kb_state_size(static_cast<kb_handle*>(_h))) throw Exception("setState: size mismatch");
+  check(kb_set_state_flat(static_cast<kb_handle*>(_h), s.data()), "kb_set_state_flat");
+  _built = false;
+}
+
+// ---------------------------------------------------------------- TrustRegionPolicy (TrustRegionPolicy.cpp)
+void TrustRegionPolicy::optimizationStarting(double J) {
+  _J = J;
+  _p_J = J;
+  _last_successful_J = J;
+  _isFirstIteration = true;
+  optimizationStartingImplementation(J);
+}
+
+bool TrustRegionPolicy::solveSystem(double J, bool previousIterationFailed, int nThreads, std::vector<double>& outDx) {
+  if (previousIterationFailed) {
+    _J = J;
+  } else {
+    _p_J = _last_successful_J;
+    _last_successful_J = J;
+    _J = J;
+  }
+  const bool success = solveSystemImplementation(J, previousIterationFailed, nThreads, outDx);
+  _isFirstIteration = false;
+  return success;
+}
+
+// ---------------------------------------------------------------- LM (LevenbergMarquardtTrustRegionPolicy.cpp)
+void LevenbergMarquardtTrustRegionPolicy::optimizationStartingImplementation(double) {
+  _lambda = _lambdaInit;
+  _gamma = _gammaInit;
+  _beta = _betaInit;
+  _p = _pInit;
+  _mu = _muInit;
+}
+
+bool LevenbergMarquardtTrustRegionPolicy::solveSystemImplementation(double, bool previousIterationFailed, int nThreads,
+                                                                    std::vector<double>& outDx) {
+  if (!_solver) throw LinearSystemSolver::Exception("The solver is null");
+  if (isFirstIteration()) {
+    _solver->buildSystem(nThreads, true);
+  } else {
+    const double rho = getLmRho();
+    if (previousIterationFailed) {  // the last step was a regression
+      _mu *= 2;
+      _lambda *= _mu;
+    } else if (rho <= 0) {  // no rebuild, only a new conditioner
+      _mu *= 10;
+      _lambda *= _mu;
+    } else {  // success: rebuild
+      _solver->buildSystem(nThreads, true);
+      if (_lambda > 1e-16) {
+        const double u1 = 1 / _gamma;
+        const double u2 = 1 - (_beta - 1) * std::pow((2 * rho - 1), _p);
+        if (u1 > u2)
+          _lambda *= u1;
+        else
+          _lambda *= u2;
+        _mu = _beta;
+      } else {
+        _lambda = 1e-15;
+      }
+    }
+  }
+  _solver->setConstantConditioner(_lambda);
+  const bool success = _solver->solveSystem(_dx);
+  outDx = _dx;
+  return success;
+}
+
+double LevenbergMarquardtTrustRegionPolicy::getLmRho() {
+  const double d1 = get_dJ();
+  // L(0) - L(h) = dx^T (lambda dx + rhs)   (:107-113: lambda, not lambda^2)
+  const std::vector<double>& r = _solver->rhs();
+  double d2 = 0.0;
+  for (size_t i = 0; i < _dx.size(); ++i) d2 += _dx[i] * (_lambda * _dx[i] + r[i]);
+  return d1 / d2;
+}
+
+std::ostream& LevenbergMarquardtTrustRegionPolicy::printState(std::ostream& out) const {
+  return out << "LM - lambda:" << _lambda << " mu:" << _mu;
+}
+
+// ---------------------------------------------------------------- GN (GaussNewtonTrustRegionPolicy.cpp:18-24)
+bool GaussNewtonTrustRegionPolicy::solveSystemImplementation(double, bool, int nThreads, std::vector<double>& outDx) {
+  _solver->buildSystem(nThreads, true);
+  return _solver->solveSystem(outDx);
+}
+
+// ---------------------------------------------------------------- Optimizer2 (Optimizer2.cpp:183-273)
+Optimizer2::Optimizer2(const Optimizer2Options& options) : _options(options) {}
+
+SolutionReturnValue Optimizer2::optimize() {
+  auto solver = _options.linearSystemSolver;
+  auto policy = _options.trustRegionPolicy;
+  if (!solver) throw Exception("The solver is null");
+  if (!policy) throw Exception("The trust region policy is null");
+  SolutionReturnValue srv;
+  double J = solver->evaluateError(_options.nThreads, true);
+  double p_J = J;
+  srv.JStart = p_J;
+  double deltaX = _options.convergenceDeltaX + 1.0;
+  double deltaJ = _options.convergenceDeltaJ + 1.0;
+  bool previousIterationFailed = false;
+  bool linearSolverFailure = false;
+  policy->setSolver(solver);
+  policy->optimizationStarting(J);
+  while (srv.iterations < _options.maxIterations && srv.failedIterations < _options.maxIterations &&
+         ((deltaX > _options.convergenceDeltaX && std::fabs(deltaJ) > _options.convergenceDeltaJ) ||
+          linearSolverFailure)) {
+    const bool solutionSuccess = policy->solveSystem(J, previousIterationFailed, _options.nThreads, _dx);
+    if (!solutionSuccess) {
+      if (_options.verbose) std::cout << "[WARNING] System solution failed\n";
+      previousIterationFailed = true;
+      linearSolverFailure = true;
+      srv.failedIterations++;
+    } else {
+      deltaX = solver->applyStateUpdate(_dx);
+      J = solver->evaluateError(_options.nThreads, true);
+      deltaJ = p_J - J;
+      if (policy->revertOnFailure()) {
+        if (deltaJ < 0.0) {
+          if (_options.verbose) std::cout << "Last step was a regression. Reverting\n";
+          solver->revertLastStateUpdate();
+          srv.failedIterations++;
+          previousIterationFailed = true;
+        } else {
+          p_J = J;
+          previousIterationFailed = false;
+        }
+      } else {
+        p_J = J;
+      }
+      srv.iterations++;
+      if (_options.verbose) {
+        std::cout << "[" << srv.iterations << "]: J: " << J << ", dJ: " << deltaJ << ", deltaX: " << deltaX << ", ";
+        policy->printState(std::cout);
+        std::cout << std::endl;
+      }
+    }
+  }
+  srv.JFinal = p_J;
+  srv.dXFinal = deltaX;
+  srv.dJFinal = deltaJ;
+  srv.linearSolverFailure = linearSolverFailure;
+  return srv;
+}
+
+SolutionReturnValue Optimizer2::optimizeOnDevice(int syncEvery) {
+  auto gpu = std::dynamic_pointer_cast<GpuLinearSystemSolver>(_options.linearSystemSolver);
+  if (!gpu) throw Exception("optimizeOnDevice: the linear system solver is not a GpuLinearSystemSolver");
+  auto policy = _options.trustRegionPolicy;
+  if (!policy) throw Exception("The trust region policy is null");
+  kb_optimizer_options o{};
+  if (auto lm = std::dynamic_pointer_cast<LevenbergMarquardtTrustRegionPolicy>(policy)) {
+    o.policy = 0;
+    o.lambda_init = lm->lambdaInit();
+  } else if (std::dynamic_pointer_cast<GaussNewtonTrustRegionPolicy>(policy)) {
+    o.policy = 1;
+  } else {
+    throw Exception("optimizeOnDevice: only the LM and GN policies run device-resident");
+  }
+  o.max_iterations = _options.maxIterations;
+  o.convergence_dx = _options.convergenceDeltaX;
+  o.convergence_dj = _options.convergenceDeltaJ;
+  o.sync_every = syncEvery;
+  o.use_graph = 1;
+  kb_solution s{};
+  auto* h = static_cast<kb_handle*>(gpu->handle());
+  if (kb_optimize(h, &o, &s) < 0) throw Exception(std::string("kb_optimize: ") + kb_last_error());
+  const int cap = 2 * _options.maxIterations + 2;
+  _trace.assign(4 * (size_t)cap, 0.0);
+  const int n = kb_get_trace(h, _trace.data(), cap);
+  if (n < 0) throw Exception(std::string("kb_get_trace: ") + kb_last_error());
+  _trace.resize(4 * (size_t)n);
+  SolutionReturnValue srv;
+  srv.JStart = s.J_start;
+  srv.JFinal = s.J_final;
+  srv.dXFinal = s.dx_final;
+  srv.dJFinal = s.dj_final;
+  srv.iterations = s.iterations;
+  srv.failedIterations = s.failed_iterations;
+  srv.linearSolverFailure = s.linear_solver_failure != 0;
+  return srv;
+}
+
+}  // namespace backend
+}  // namespace kalibr_amd

@@ -1,0 +1,230 @@
+// kalibr_backend.hpp -- C++ host layer over the kalibr_hip C-ABI, mirroring the aslam_backend plugin surface
+// that Kalibr2's batch calibration drives (paths relative to the reference repository):
+//   LinearSystemSolver      aslam_optimizer/aslam_backend/include/aslam/backend/LinearSystemSolver.hpp:16-109
+//   TrustRegionPolicy       aslam_optimizer/aslam_backend/include/aslam/backend/TrustRegionPolicy.hpp:13-57
+//   LevenbergMarquardt...   aslam_optimizer/aslam_backend/src/LevenbergMarquardtTrustRegionPolicy.cpp:7-117
+//   GaussNewton...          aslam_optimizer/aslam_backend/src/GaussNewtonTrustRegionPolicy.cpp:7-39
+//   Optimizer2Options       aslam_optimizer/aslam_backend/include/aslam/backend/Optimizer2Options.hpp:9-42
+//   Optimizer2::optimize    aslam_optimizer/aslam_backend/src/Optimizer2.cpp:183-273
+//   SolutionReturnValue     aslam_optimizer/aslam_backend/include/aslam/backend/backend.hpp:11-24
+// Same names, argument meaning and error behaviour (contract violations and device errors throw
+// LinearSystemSolver::Exception, a std::runtime_error; a numerically failed solve returns false).
+// Deviations, all because the device owns the design variables:
+//   * evaluateError is virtual (the GPU solver owns the cost pass);
+//   * applyStateUpdate / revertLastStateUpdate go through the solver, which holds the device state;
+//   * vectors are std::vector<double> instead of Eigen::VectorXd (Eigen is not a dependency here).
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <memory>
+#include <ostream>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+namespace kalibr_amd {
+namespace backend {
+
+// ---------------------------------------------------------------- problem description
+// What CalibrateMultiCameraRig / CreateBatchProblem hand to the optimizer (CalibrationTools.hpp:376-521):
+// the camera models, the target corners, one ReprojectionError term per observed corner grouped in
+// (frame, camera) views, and the design-variable values (flat state, include/kalibr_hip.h).
+struct CalibrationProblem {
+  std::vector<int32_t> cam_model;    // kb_camera_model per camera
+  std::vector<double> target;        // [n_target][3]
+  std::vector<uint32_t> view_frame;  // [n_views], sorted by frame
+  std::vector<uint8_t> view_cam;     // [n_views]
+  std::vector<uint32_t> view_offset; // [n_views + 1]
+  std::vector<uint16_t> corner_id;   // [n_corners]
+  std::vector<double> y;             // [n_corners][2]
+  std::vector<double> state;         // flat design-variable values
+  int n_frames = 0;
+  int n_cams() const { return (int)cam_model.size(); }
+  int n_views() const { return (int)view_frame.size(); }
+  int n_corners() const { return (int)corner_id.size(); }
+  int n_target() const { return (int)target.size() / 3; }
+};
+
+struct SolutionReturnValue {  // backend.hpp:11-24
+  double JStart = 0.0, JFinal = 0.0, dXFinal = 0.0, dJFinal = 0.0;
+  int iterations = 0, failedIterations = 0;
+  bool linearSolverFailure = false;
+};
+
+// ---------------------------------------------------------------- LinearSystemSolver
+class LinearSystemSolver {
+ public:
+  struct Exception : std::runtime_error {
+    explicit Exception(const std::string& m) : std::runtime_error(m) {}
+  };
+  virtual ~LinearSystemSolver() = default;
+
+  /// chi^2 = sum_i e_i^T invR e_i of the current state (LinearSystemSolver.cpp:81-92)
+  virtual double evaluateError(size_t nThreads, bool useMEstimator) = 0;
+  /// build J and rhs = -J^T e at the current state
+  virtual void buildSystem(size_t nThreads, bool useMEstimator) = 0;
+  /// "The square of these values will be added to the diagonal of the Hessian matrix" (:33-35)
+  virtual void setConditioner(const std::vector<double>& diag);
+  virtual void setConstantConditioner(double diag);
+  /// solve (J^T J + diag^2) dx = rhs; false on a numerically failed factorisation
+  virtual bool solveSystem(std::vector<double>& outDx) = 0;
+  virtual std::string name() const = 0;
+  virtual const std::vector<double>& rhs() const { return _rhs; }
+  virtual double rhsJtJrhs() = 0;
+  /// design-variable update x <- x [+] dx, returns max|dx| (Optimizer2.cpp:290-310)
+  virtual double applyStateUpdate(const std::vector<double>& dx) = 0;
+  virtual void revertLastStateUpdate() = 0;
+
+  size_t JRows() const { return _JRows; }
+  size_t JCols() const { return _JCols; }
+
+ protected:
+  std::vector<double> _rhs;
+  std::vector<double> _diagonalConditioner;
+  size_t _JRows = 0, _JCols = 0;
+};
+
+// ---------------------------------------------------------------- GPU solver over the C-ABI
+struct GpuOptions {
+  int device = 0;
+};
+
+/// LinearSystemSolver whose build / solve / update / cost run on one MI355X (kalibr_hip.h).  The
+/// per-call methods mirror the reference solver one call at a time; optimizeOnDevice() runs the whole
+/// Optimizer2 loop device-resident (one captured graph per pass).
+class GpuLinearSystemSolver : public LinearSystemSolver {
+ public:
+  explicit GpuLinearSystemSolver(const GpuOptions& o = GpuOptions());
+  ~GpuLinearSystemSolver() override;
+  GpuLinearSystemSolver(const GpuLinearSystemSolver&) = delete;
+  GpuLinearSystemSolver& operator=(const GpuLinearSystemSolver&) = delete;
+
+  /// LinearSystemSolver::initMatrixStructure (LinearSystemSolver.cpp:117-138): uploads the terms and state
+  void initMatrixStructure(const CalibrationProblem& problem, bool useDiagonalConditioner);
+
+  double evaluateError(size_t nThreads, bool useMEstimator) override;
+  void buildSystem(size_t nThreads, bool useMEstimator) override;
+  void setConstantConditioner(double diag) override;
+  void setConditioner(const std::vector<double>& diag) override;
+  bool solveSystem(std::vector<double>& outDx) override;
+  std::string name() const override { return "kalibr_hip_schur_cholesky"; }
+  const std::vector<double>& rhs() const override;
+  double rhsJtJrhs() override;
+  double applyStateUpdate(const std::vector<double>& dx) override;
+  void revertLastStateUpdate() override;
+
+  std::vector<double> state() const;
+  void setState(const std::vector<double>& s);
+  size_t cameraCols() const { return _C; }
+  void* handle() const { return _h; }
+
+ private:
+  void check(int rc, const char* what) const;
+  void* _h = nullptr;
+  GpuOptions _opt;
+  size_t _C = 0;
+  double _conditioner = 0.0;
+  bool _built = false;
+  mutable bool _rhs_valid = false;
+};
+
+// ---------------------------------------------------------------- trust-region policies
+class TrustRegionPolicy {
+ public:
+  virtual ~TrustRegionPolicy() = default;
+  /// called by the optimizer when an optimization is starting (TrustRegionPolicy.cpp:29-37)
+  void optimizationStarting(double J);
+  /// TrustRegionPolicy::solveSystem (TrustRegionPolicy.cpp:39-52): true if the solution was successful
+  bool solveSystem(double J, bool previousIterationFailed, int nThreads, std::vector<double>& outDx);
+  std::shared_ptr<LinearSystemSolver> getSolver() { return _solver; }
+  virtual void setSolver(std::shared_ptr<LinearSystemSolver> solver) { _solver = std::move(solver); }
+  virtual bool revertOnFailure() { return true; }
+  virtual std::ostream& printState(std::ostream& out) const = 0;
+  virtual std::string name() const = 0;
+  virtual bool requiresAugmentedDiagonal() const = 0;
+
+ protected:
+  double get_dJ() const { return _p_J - _J; }
+  bool isFirstIteration() const { return _isFirstIteration; }
+  virtual void optimizationStartingImplementation(double J) = 0;
+  virtual bool solveSystemImplementation(double J, bool previousIterationFailed, int nThreads,
+                                         std::vector<double>& outDx) = 0;
+  std::shared_ptr<LinearSystemSolver> _solver;
+
+ private:
+  double _J = 0.0, _p_J = 0.0, _last_successful_J = 0.0;
+  bool _isFirstIteration = true;
+};
+
+class LevenbergMarquardtTrustRegionPolicy : public TrustRegionPolicy {
+ public:
+  LevenbergMarquardtTrustRegionPolicy() : _lambdaInit(1e-3) {}
+  explicit LevenbergMarquardtTrustRegionPolicy(double lambdaInit) : _lambdaInit(lambdaInit) {}
+  bool revertOnFailure() override { return true; }
+  std::ostream& printState(std::ostream& out) const override;
+  std::string name() const override { return "levenberg_marquardt"; }
+  bool requiresAugmentedDiagonal() const override { return true; }
+  double lambdaInit() const { return _lambdaInit; }
+  double lambda() const { return _lambda; }
+
+ protected:
+  void optimizationStartingImplementation(double J) override;
+  bool solveSystemImplementation(double J, bool previousIterationFailed, int nThreads,
+                                 std::vector<double>& outDx) override;
+
+ private:
+  double getLmRho();
+  std::vector<double> _dx;
+  double _lambdaInit, _gammaInit = 3, _betaInit = 2, _muInit = 2;
+  int _pInit = 3;
+  double _lambda = 0, _gamma = 0, _beta = 0, _mu = 0;
+  int _p = 0;
+};
+
+class GaussNewtonTrustRegionPolicy : public TrustRegionPolicy {
+ public:
+  bool revertOnFailure() override { return false; }
+  std::ostream& printState(std::ostream& out) const override { return out << "GN"; }
+  std::string name() const override { return "gauss_newton"; }
+  bool requiresAugmentedDiagonal() const override { return false; }
+
+ protected:
+  void optimizationStartingImplementation(double) override {}
+  bool solveSystemImplementation(double J, bool previousIterationFailed, int nThreads,
+                                 std::vector<double>& outDx) override;
+};
+
+// ---------------------------------------------------------------- optimizer
+struct Optimizer2Options {  // Optimizer2Options.hpp:9-42 (defaults kept)
+  double convergenceDeltaJ = 1e-3;
+  double convergenceDeltaX = 1e-3;
+  int maxIterations = 20;
+  bool verbose = false;
+  int linearSolverMaximumFails = 0;
+  int nThreads = 4;
+  std::shared_ptr<LinearSystemSolver> linearSystemSolver;
+  std::shared_ptr<TrustRegionPolicy> trustRegionPolicy;
+};
+
+class Optimizer2 {
+ public:
+  using Exception = LinearSystemSolver::Exception;
+  explicit Optimizer2(const Optimizer2Options& options);
+  /// host-driven loop, Optimizer2.cpp:183-273 statement by statement (any LinearSystemSolver)
+  SolutionReturnValue optimize();
+  /// the same loop device-resident (GpuLinearSystemSolver with an LM or GN policy): one captured graph per
+  /// pass, the host only polls the done flag every `syncEvery` passes
+  SolutionReturnValue optimizeOnDevice(int syncEvery = 0);
+  const Optimizer2Options& options() const { return _options; }
+  /// per-pass [J, lambda, deltaX, accepted] of the last optimizeOnDevice()
+  const std::vector<double>& trace() const { return _trace; }
+
+ private:
+  Optimizer2Options _options;
+  std::vector<double> _dx;
+  std::vector<double> _trace;
+};
+
+}  // namespace backend
+}  // namespace kalibr_amd

@@ -1,0 +1,213 @@
+// Test driver for the C++ host layer (kalibr_amd/host/kalibr_backend.*), run by tests/test_host_cpp.py.
+//   test_host cpu <problem.bin> <lm|gn> <maxIt> : Optimizer2 + policy over an oracle-backed LinearSystemSolver
+//                                                 vs the oracle's own loop (kbo_optimize): must agree bitwise
+//   test_host gpu <problem.bin> <lm|gn> <maxIt> : host-driven Optimizer2 over GpuLinearSystemSolver, the
+//                                                 device-resident loop (optimizeOnDevice) and kbo_optimize
+// Prints one JSON line.  The oracle is test infrastructure only (oracle/kb_oracle.h).
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "kalibr_backend.hpp"
+#include "kb_oracle.h"
+
+using namespace kalibr_amd::backend;
+
+// binary problem file written by tests/host_problem.py
+static CalibrationProblem load(const char* path) {
+  std::ifstream f(path, std::ios::binary);
+  if (!f) throw std::runtime_error(std::string("cannot open ") + path);
+  int32_t hdr[7];
+  f.read(reinterpret_cast<char*>(hdr), sizeof(hdr));
+  if (hdr[0] != 0x4b424850) throw std::runtime_error("bad magic");
+  const int N = hdr[1], F = hdr[2], V = hdr[3], NC = hdr[4], K = hdr[5], S = hdr[6];
+  CalibrationProblem p;
+  p.n_frames = F;
+  auto rd = [&](void* dst, size_t bytes) { f.read(reinterpret_cast<char*>(dst), (std::streamsize)bytes); };
+  std::vector<int32_t> tmp;
+  p.cam_model.resize(N);
+  rd(p.cam_model.data(), 4 * N);
+  p.target.resize(3 * (size_t)K);
+  rd(p.target.data(), 8 * 3 * (size_t)K);
+  tmp.resize(V);
+  rd(tmp.data(), 4 * (size_t)V);
+  p.view_frame.assign(tmp.begin(), tmp.end());
+  rd(tmp.data(), 4 * (size_t)V);
+  p.view_cam.assign(tmp.begin(), tmp.end());
+  tmp.resize(V + 1);
+  rd(tmp.data(), 4 * (size_t)(V + 1));
+  p.view_offset.assign(tmp.begin(), tmp.end());
+  tmp.resize(NC);
+  rd(tmp.data(), 4 * (size_t)NC);
+  p.corner_id.assign(tmp.begin(), tmp.end());
+  p.y.resize(2 * (size_t)NC);
+  rd(p.y.data(), 8 * 2 * (size_t)NC);
+  p.state.resize(S);
+  rd(p.state.data(), 8 * (size_t)S);
+  if (!f) throw std::runtime_error("truncated problem file");
+  return p;
+}
+
+// oracle view of a problem (int arrays kept alive by the holder)
+struct OracleProblem {
+  std::vector<int> cam_model, view_frame, view_cam, view_offset, corner_id;
+  kbo_problem P{};
+  explicit OracleProblem(const CalibrationProblem& p)
+      : cam_model(p.cam_model.begin(), p.cam_model.end()),
+        view_frame(p.view_frame.begin(), p.view_frame.end()),
+        view_cam(p.view_cam.begin(), p.view_cam.end()),
+        view_offset(p.view_offset.begin(), p.view_offset.end()),
+        corner_id(p.corner_id.begin(), p.corner_id.end()) {
+    P.n_cams = p.n_cams();
+    P.n_frames = p.n_frames;
+    P.n_views = p.n_views();
+    P.n_corners = p.n_corners();
+    P.n_target = p.n_target();
+    P.cam_model = cam_model.data();
+    P.target = p.target.data();
+    P.view_frame = view_frame.data();
+    P.view_cam = view_cam.data();
+    P.view_offset = view_offset.data();
+    P.corner_id = corner_id.data();
+    P.y = p.y.data();
+  }
+};
+
+// LinearSystemSolver over the oracle's arrow build / Schur solve (the CPU reference data flow)
+class OracleLinearSystemSolver : public LinearSystemSolver {
+ public:
+  OracleLinearSystemSolver(const CalibrationProblem& p, int nthreads)
+      : _op(p), _state(p.state), _nt(nthreads) {
+    _C = kbo_cam_cols(&_op.P);
+    _F = p.n_frames;
+    _JCols = (size_t)kbo_total_cols(&_op.P);
+    _JRows = 2 * (size_t)p.n_corners();
+    _Hff.resize(36 * (size_t)_F);
+    _Hfc.resize(6 * (size_t)_C * _F);
+    _Hcc.resize((size_t)_C * _C);
+    _gf.resize(6 * (size_t)_F);
+    _gc.resize(_C);
+    _A.C = _C;
+    _A.F = _F;
+    _A.Hff = _Hff.data();
+    _A.Hfc = _Hfc.data();
+    _A.Hcc = _Hcc.data();
+    _A.gf = _gf.data();
+    _A.gc = _gc.data();
+    _rhs.assign(_JCols, 0.0);
+    _jt = kbo_jt_create(&_op.P);
+  }
+  ~OracleLinearSystemSolver() override { kbo_jt_destroy(_jt); }
+  double evaluateError(size_t, bool) override { return kbo_eval_cost(&_op.P, _state.data(), _nt); }
+  void buildSystem(size_t, bool) override {  // the reference data flow: CCS J^T, rhs = J^T (-e), J^T J
+    kbo_jt_build(_jt, _state.data(), _nt, _rhs.data());
+    kbo_jt_normal_arrow(_jt, _nt, &_A);
+  }
+  void setConstantConditioner(double d) override {
+    LinearSystemSolver::setConstantConditioner(d);
+    _cond = d;
+  }
+  bool solveSystem(std::vector<double>& dx) override {  // outDx untouched on failure
+    std::vector<double> tmp(_JCols, 0.0);
+    const bool ok = kbo_arrow_solve(&_A, _cond, _nt, tmp.data()) != 0;
+    if (ok) dx = tmp;
+    return ok;
+  }
+  std::string name() const override { return "oracle_arrow_schur"; }
+  double rhsJtJrhs() override { return 0.0; }
+  double applyStateUpdate(const std::vector<double>& dx) override {
+    _backup = _state;
+    return kbo_apply_update(&_op.P, _state.data(), dx.data());
+  }
+  void revertLastStateUpdate() override { _state = _backup; }
+  const std::vector<double>& state() const { return _state; }
+
+ private:
+  OracleProblem _op;
+  std::vector<double> _state, _backup;
+  std::vector<double> _Hff, _Hfc, _Hcc, _gf, _gc;
+  kbo_arrow _A{};
+  kbo_jt* _jt = nullptr;
+  int _C = 0, _F = 0, _nt = 1;
+  double _cond = 0.0;
+};
+
+static std::shared_ptr<TrustRegionPolicy> make_policy(const std::string& p) {
+  if (p == "lm") return std::make_shared<LevenbergMarquardtTrustRegionPolicy>(10.0);  // CalibrationTools.hpp:65
+  return std::make_shared<GaussNewtonTrustRegionPolicy>();
+}
+
+static double maxdiff(const std::vector<double>& a, const std::vector<double>& b, size_t n0, size_t n1) {
+  double m = 0.0;
+  for (size_t i = n0; i < n1 && i < a.size(); ++i) m = std::max(m, std::fabs(a[i] - b[i]));
+  return m;
+}
+
+int main(int argc, char** argv) {
+  if (argc < 5) {
+    std::fprintf(stderr, "usage: test_host cpu|gpu problem.bin lm|gn maxIt\n");
+    return 2;
+  }
+  const std::string mode = argv[1], pol = argv[3];
+  const int maxIt = std::atoi(argv[4]);
+  try {
+    CalibrationProblem p = load(argv[2]);
+    Optimizer2Options opt;
+    opt.maxIterations = maxIt;
+    opt.convergenceDeltaX = 1e-3;  // CalibrationTools.hpp:57-66
+    opt.convergenceDeltaJ = 1.0;
+    opt.nThreads = 4;
+    // oracle's own loop
+    OracleProblem op(p);
+    std::vector<double> s_ref = p.state;
+    kbo_options ko{pol == "lm" ? 0 : 1, 10.0, maxIt, opt.convergenceDeltaX, opt.convergenceDeltaJ, 4};
+    kbo_srv ksrv{};
+    kbo_optimize(&op.P, s_ref.data(), &ko, &ksrv, nullptr, 0);
+    const size_t ncam = (size_t)p.n_cams() * KBO_MAX_INTR + 7 * (size_t)(p.n_cams() - 1);
+    if (mode == "cpu") {
+      auto solver = std::make_shared<OracleLinearSystemSolver>(p, 4);
+      opt.linearSystemSolver = solver;
+      opt.trustRegionPolicy = make_policy(pol);
+      Optimizer2 o(opt);
+      SolutionReturnValue srv = o.optimize();
+      std::printf(
+          "{\"iterations\": %d, \"ref_iterations\": %d, \"failed\": %d, \"ref_failed\": %d, \"J_final\": %.17g, "
+          "\"ref_J_final\": %.17g, \"cam_diff\": %.3e, \"frame_diff\": %.3e}\n",
+          srv.iterations, ksrv.iterations, srv.failedIterations, ksrv.failed_iterations, srv.JFinal, ksrv.J_final,
+          maxdiff(solver->state(), s_ref, 0, ncam), maxdiff(solver->state(), s_ref, ncam, s_ref.size()));
+      return 0;
+    }
+    // gpu: host-driven loop over the per-call C-ABI
+    auto gh = std::make_shared<GpuLinearSystemSolver>();
+    gh->initMatrixStructure(p, false);
+    opt.linearSystemSolver = gh;
+    opt.trustRegionPolicy = make_policy(pol);
+    SolutionReturnValue sh = Optimizer2(opt).optimize();
+    const std::vector<double> st_h = gh->state();
+    // device-resident loop
+    auto gd = std::make_shared<GpuLinearSystemSolver>();
+    gd->initMatrixStructure(p, false);
+    opt.linearSystemSolver = gd;
+    opt.trustRegionPolicy = make_policy(pol);
+    Optimizer2 od(opt);
+    SolutionReturnValue sd = od.optimizeOnDevice();
+    const std::vector<double> st_d = gd->state();
+    std::printf(
+        "{\"host_iterations\": %d, \"dev_iterations\": %d, \"ref_iterations\": %d, \"host_failed\": %d, "
+        "\"dev_failed\": %d, \"ref_failed\": %d, \"host_J\": %.17g, \"dev_J\": %.17g, \"ref_J\": %.17g, "
+        "\"host_vs_ref_cam\": %.3e, \"host_vs_ref_frame\": %.3e, \"dev_vs_ref_cam\": %.3e, \"dev_vs_ref_frame\": "
+        "%.3e, \"host_vs_dev\": %.3e, \"trace_len\": %zu}\n",
+        sh.iterations, sd.iterations, ksrv.iterations, sh.failedIterations, sd.failedIterations,
+        ksrv.failed_iterations, sh.JFinal, sd.JFinal, ksrv.J_final, maxdiff(st_h, s_ref, 0, ncam),
+        maxdiff(st_h, s_ref, ncam, s_ref.size()), maxdiff(st_d, s_ref, 0, ncam), maxdiff(st_d, s_ref, ncam, s_ref.size()),
+        maxdiff(st_h, st_d, 0, s_ref.size()), od.trace().size() / 4);
+    return 0;
+  } catch (const std::exception& e) {
+    std::printf("{\"error\": \"%s\"}\n", e.what());
+    return 1;
+  }
+}
