@@ -23,8 +23,25 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 
 METRIC = "Gauss-Newton iterations/sec (full J build + solve), N-cam×M-frame AprilGrid"
+BUILD_KERNEL = "void kb::k_build<2>(kb::KbDev, int, int)"
 FRAMES_PER_RANK = 500
 HBM_PEAK_GBS = 8000.0
+
+
+def pmc_traffic_bytes(kernel):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary (profiles/*/pmc_traffic.json,
+    written by tools/pmc_traffic.py from two separate rocprofv3 --pmc passes of this bench workload, gfx950
+    FETCH_SIZE correction applied), or None."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_traffic.json")), reverse=True):
+        try:
+            with open(path) as f:
+                k = json.load(f)["kernels"].get(kernel)
+        except (OSError, ValueError, KeyError):
+            continue
+        if k:
+            return k["hbm_bytes_per_launch"], os.path.relpath(path, ROOT)
+    return None
 
 
 def cpu_baseline(prob, seconds_budget=12.0, threads=None):
@@ -91,6 +108,7 @@ def main():
     # dominant kernel (k_build) timing with HIP events on the handle's stream
     build_ms, bytes_per, flops_per = g.build_kernel_stats()
     achieved = bytes_per / (build_ms * 1e-3) / 1e9
+    pmc = pmc_traffic_bytes(BUILD_KERNEL) if world == 1 else None
 
     if rank == 0:
         value = world * args.steps / wall
@@ -103,8 +121,12 @@ def main():
                        "jacobian_cols": full.total_cols, "camera_block": full.cam_cols, "policy": "gauss_newton",
                        "parallelism": f"frame-sharded x{world}"},
             "roofline": {"bound": "hbm", "kernel": "k_build", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None, "avg_ms": build_ms,
-                         "algorithmic_bytes": bytes_per, "fp64_tflops": flops_per / (build_ms * 1e-3) / 1e12},
+                         "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": (pmc[0] / (build_ms * 1e-3) / 1e9) if pmc else None,
+                         "traffic_bytes_per_launch": pmc[0] if pmc else None,
+                         "traffic_source": pmc[1] if pmc else None,
+                         "avg_ms": build_ms, "algorithmic_bytes": bytes_per,
+                         "fp64_tflops": flops_per / (build_ms * 1e-3) / 1e12},
         }
         if not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(full if world == 1 else full.frame_slice(0, FRAMES_PER_RANK))

@@ -1,4 +1,7 @@
 """Print the rocprofv3 kernel stats + one pass of the kernel trace (tools helper)."""
+import signal
+
+signal.signal(signal.SIGPIPE, signal.SIG_DFL)
 import csv
 import sys
 
