@@ -57,7 +57,7 @@ struct kb_handle {
   int WPB = 1;
   size_t lds_build = 0, lds_camexp = 0, lds_schur = 0, lds_solve = 0;
   int solve_threads = 64;
-  int mb = 24, ms = 24;  // Schur entries per thread of k_build / k_schur (template bucket)
+  int mb = 7, ms = 7;  // Schur-sum tiles per wave of k_build / k_schur (template bucket)
   const void* fn_build = nullptr;
   const void* fn_schur = nullptr;
   const void* fn_solve = nullptr;
@@ -153,8 +153,8 @@ kb_handle* kb_create(const kb_layout* L) {
     c += 6;
   }
   h->C = c;
-  if (h->C > 109) {
-    fail("kb_create: camera block C > 109 not supported by k_schur (kSchurM)");
+  if (h->C > 111) {  // [Y | z] Schur tiles: ceil((C + 1) / 16) <= 7 (7 tiles per wave of 4)
+    fail("kb_create: camera block C > 111 not supported");
     delete h;
     return nullptr;
   }
@@ -174,7 +174,7 @@ kb_handle* kb_create(const kb_layout* L) {
   h->WPB = d.wpb;
   d.W = h->W;
   d.Wtot = h->N * 136 + h->W + 1;
-  if (h->W + 1 > kMaxM * 256 || 64 * d.wpb > 512) {
+  if (64 * d.wpb > 512) {
     fail("kb_create: camera block / rig too large for the build kernel");
     delete h;
     return nullptr;
@@ -232,11 +232,19 @@ kb_handle* kb_create(const kb_layout* L) {
   hipMemcpyAsync(tgt, L->target_points, 3 * sizeof(double) * h->K, hipMemcpyHostToDevice, h->stream);
   {
     const int N = h->N, C = h->C, WPB = d.wpb;
+    const int CZ = 16 * ((C + 16) / 16);  // [Y | z] row stride of the Schur tiles
     h->lds_build = sizeof(double) * (WPB * 64 * XS + WPB * 256 + N * (256 + 256 + 64 + 36 + 36 + 8) + 36 + 8 + 6 * C +
-                                     36 + 6 * C + 8 + 18 * N * (N - 1) + (3 * h->K <= kTargetLds ? 3 * h->K : 0));
+                                     36 + 8 * CZ + 18 * N * (N - 1) + (3 * h->K <= kTargetLds ? 3 * h->K : 0));
     h->lds_camexp = sizeof(double) * (N * 256 + N * N * 36);
-    h->lds_schur = sizeof(double) * (6 * C + 36 + 8);
-    h->lds_solve = sizeof(double) * (C * (C + 1) / 2 + 2 * C + 1 + N * 256 + 2 * N * N * 36) + sizeof(int) * (C + C * (C - 1) / 2);
+    h->lds_schur = sizeof(double) * (8 * CZ + 36);
+    if (C <= 64) {
+      h->lds_solve = sizeof(double) * (C * (C + 1) / 2 + 2 * C + 1 + N * 256 + 2 * N * N * 36) + sizeof(int) * C;
+    } else {  // 16 x 16 lower tiles + panel scratch + 1/D + solution vector
+      const int nb = (C + 15) / 16, n16 = 16 * nb;
+      h->lds_solve = sizeof(double) * (128 * nb * (nb + 1) + 2 * C + 1 + N * 256 + 2 * N * N * 36 + 16 * (n16 - 16) +
+                                       2 * n16) +
+                     sizeof(int) * C;
+    }
     h->solve_threads = 256;
     h->fn_solve = C <= 16   ? (const void*)k_solve<16>
                   : C <= 24 ? (const void*)k_solve<24>
@@ -251,11 +259,13 @@ kb_handle* kb_create(const kb_layout* L) {
     }
   }
   {
-    const int bt = 64 * d.wpb;
-    h->mb = (h->W + 1 <= 2 * bt) ? 2 : (h->W + 1 <= 8 * bt) ? 8 : 24;
-    h->ms = (h->W + 1 <= 2 * 256) ? 2 : (h->W + 1 <= 8 * 256) ? 8 : 24;
-    h->fn_build = h->mb == 2 ? (const void*)k_build<2> : h->mb == 8 ? (const void*)k_build<8> : (const void*)k_build<24>;
-    h->fn_schur = h->ms == 2 ? (const void*)k_schur<2> : h->ms == 8 ? (const void*)k_schur<8> : (const void*)k_schur<24>;
+    // Schur-sum tiles per wave (template bucket): ceil(lower tiles of [Y|z]^T [Y|z] / waves)
+    const int nbz = (h->C + 16) / 16, ntiles = nbz * (nbz + 1) / 2;
+    const int tb = (ntiles + d.wpb - 1) / d.wpb, ts = (ntiles + 3) / 4;
+    h->mb = tb <= 1 ? 1 : tb <= 4 ? 4 : 7;
+    h->ms = ts <= 1 ? 1 : ts <= 4 ? 4 : 7;
+    h->fn_build = h->mb == 1 ? (const void*)k_build<1> : h->mb == 4 ? (const void*)k_build<4> : (const void*)k_build<7>;
+    h->fn_schur = h->ms == 1 ? (const void*)k_schur<1> : h->ms == 4 ? (const void*)k_schur<4> : (const void*)k_schur<7>;
   }
   hipFuncSetAttribute(h->fn_build, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_build);
   hipFuncSetAttribute((const void*)k_camexpand, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_camexp);

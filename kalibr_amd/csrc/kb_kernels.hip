@@ -40,8 +40,16 @@ __device__ __forceinline__ double readlane_d(double v, int lane) {
 }
 
 constexpr int XS = 17;       // LDS row stride (doubles) of the 64 x 16 Jacobian-row tile
-constexpr int kMaxM = 24;    // largest Schur-sum entries per thread: (W + 1) <= M * blockDim
 constexpr int kTargetLds = 1536;  // target corners staged in k_build's LDS when 3 * n_target <= this
+
+// 1/x by v_rcp_f64 + two Newton steps (a short dependent chain; within an ulp of the IEEE quotient)
+__device__ __forceinline__ double recip_d(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  double e = fma(-x, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-x, r, 1.0);
+  return fma(r, e, r);
+}
 
 // 64-bit DPP move within rows of 16 lanes (VALU, no LDS round trip); CTRL = DPP control (0x121.. = row_ror:1..)
 template <int CTRL>
@@ -66,6 +74,13 @@ __device__ __forceinline__ double wave_max_d(double v) {
   v = fmax(v, dpp_d<0x122>(v));
   v = fmax(v, dpp_d<0x121>(v));
   return fmax(fmax(readlane_d(v, 0), readlane_d(v, 16)), fmax(readlane_d(v, 32), readlane_d(v, 48)));
+}
+
+__device__ __forceinline__ int tri_row(int q) {  // row of packed-lower index q
+  int r = (int)((sqrtf(8.0f * (float)q + 1.0f) - 1.0f) * 0.5f);
+  while (r * (r + 1) / 2 > q) --r;
+  while ((r + 1) * (r + 2) / 2 <= q) ++r;
+  return r;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -316,32 +331,62 @@ __device__ __forceinline__ bool chol6_wave(const double* A, double lam2, double*
   return ok;
 }
 
-// Schur-sum entries of this thread: sum Y^T Y (upper packed) and Y^T z
-template <int M>
-__device__ __forceinline__ void schur_accumulate(const int C, const int Wt, const int W, const double* Y,
-                                                 const double* z, const int* ab, double* acc) {
+// Schur sums of a block on MFMA: [Y | z] (8 x CZ in LDS, rows 6..7 and columns > C zero, CZ = 16 nbz,
+// nbz = ceil((C + 1) / 16)); wave w owns lower tiles q = w, w + nw, ... (at most TW) and accumulates
+// acc[t] += Y_ii^T Y_jj over the block's frames (two 16x16x4 steps per frame).  Tile entry (r, c) is
+// sum_k [Y|z][k][r] [Y|z][k][c]: r, c < C -> sum Y^T Y, r == C -> sum Y^T z.
+template <int TW>
+__device__ __forceinline__ void schur_tiles_accumulate(const double* Y, int CZ, const int* tii, const int* tjj,
+                                                       v4d* acc) {
+  const int lane = threadIdx.x & 63;
 #pragma unroll
-  for (int m = 0; m < M; ++m) {
-    const int e = threadIdx.x + blockDim.x * m;
-    if (e < Wt) {
-      const int a = ab[m] >> 16, b = ab[m] & 0xffff;
-      double s2 = 0.0;
+  for (int t = 0; t < TW; ++t) {
+    if (tii[t] < 0) break;  // wave-uniform
+    const double* ya = Y + 16 * tii[t] + (lane & 15);
+    const double* yb = Y + 16 * tjj[t] + (lane & 15);
 #pragma unroll
-      for (int r = 0; r < 6; ++r) s2 += Y[r * C + a] * Y[r * C + b];
-      acc[m] += s2;
-    } else if (e < W) {
-      const int a = e - Wt;
-      double s2 = 0.0;
-#pragma unroll
-      for (int r = 0; r < 6; ++r) s2 += Y[r * C + a] * z[r];
-      acc[m] += s2;
+    for (int s = 0; s < 2; ++s) {
+      const int k = 4 * s + (lane >> 4);
+      acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(ya[k * CZ], yb[k * CZ], acc[t], 0, 0, 0);
     }
   }
 }
 
-// Y = L^-1 H_fc (thread per column), z = L^-1 g_f (last thread); stored to LDS and HBM
+// this wave's tiles (-1 terminated)
+template <int TW>
+__device__ __forceinline__ void schur_tiles_assign(int nbz, int* tii, int* tjj) {
+  const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6, ntiles = nbz * (nbz + 1) / 2;
+#pragma unroll
+  for (int t = 0; t < TW; ++t) {
+    const int q = wave + t * nw;
+    const int ii = q < ntiles ? tri_row(q) : -1;
+    tii[t] = ii;
+    tjj[t] = q < ntiles ? q - ii * (ii + 1) / 2 : -1;
+  }
+}
+
+// the tiles' entries into the block's partial row: sum Y^T Y upper packed (a <= b) | sum Y^T z
+template <int TW>
+__device__ __forceinline__ void schur_tiles_store(double* prow_schur, int C, const int* tii, const int* tjj,
+                                                  const v4d* acc) {
+  const int lane = threadIdx.x & 63, Wt = C * (C + 1) / 2;
+#pragma unroll
+  for (int t = 0; t < TW; ++t) {
+    if (tii[t] < 0) break;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int rg = 16 * tii[t] + (lane >> 4) + 4 * r, cg = 16 * tjj[t] + (lane & 15);
+      if (rg < C && cg <= rg)
+        prow_schur[upper_index(cg, rg, C)] = acc[t][r];
+      else if (rg == C && cg < C)
+        prow_schur[Wt + cg] = acc[t][r];
+    }
+  }
+}
+
+// Y = L^-1 H_fc (thread per column), z = L^-1 g_f (last thread) into [Y | z] (row stride CZ) and HBM
 __device__ __forceinline__ void schur_forward(const KbDev& d, int f, const double* L, const double* rdiag,
-                                              const double* Hfc_lds, const double* g_lds, double* Y, double* z) {
+                                              const double* Hfc_lds, const double* g_lds, double* Y, int CZ) {
   const int C = d.C, t = threadIdx.x;
   if (t < C) {
     double yv[6];
@@ -351,7 +396,7 @@ __device__ __forceinline__ void schur_forward(const KbDev& d, int f, const doubl
 #pragma unroll
       for (int k = 0; k < r; ++k) s2 -= L[r * 6 + k] * yv[k];
       yv[r] = s2 * rdiag[r];
-      Y[r * C + t] = yv[r];
+      Y[r * CZ + t] = yv[r];
       d.Yf[((size_t)f * 6 + r) * C + t] = yv[r];
     }
   } else if (t == (int)blockDim.x - 1) {
@@ -362,7 +407,7 @@ __device__ __forceinline__ void schur_forward(const KbDev& d, int f, const doubl
 #pragma unroll
       for (int k = 0; k < r; ++k) s2 -= L[r * 6 + k] * zv[k];
       zv[r] = s2 * rdiag[r];
-      z[r] = zv[r];
+      Y[r * CZ + C] = zv[r];
       d.zf[(size_t)f * 6 + r] = zv[r];
     }
   }
@@ -371,7 +416,7 @@ __device__ __forceinline__ void schur_forward(const KbDev& d, int f, const doubl
 // ---------------------------------------------------------------------------------------------
 // k_build: one block = a group of frames; waves = N * nsplit, wave w -> camera w % N, corner split w / N.
 // ---------------------------------------------------------------------------------------------
-template <int M>
+template <int TW>
 __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
   KbCtrl* c = d.ctrl;
   extern __shared__ __attribute__((aligned(16))) double sm[];
@@ -389,9 +434,9 @@ __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
   double* Fg = Fh + 36;              // frame g_f [8]
   double* Fc = Fg + 8;               // frame H_fc [6][C]
   double* L = Fc + 6 * C;            // [36]
-  double* Y = L + 36;                // [6][C]
-  double* z = Y + 6 * C;             // [8]
-  double* Kl = z + 8;                // [N(N-1)/2][36] K_{i,j}, j < i, at (i(i-1)/2 + j)
+  const int nbz = (C + 16) >> 4, CZ = 16 * nbz;
+  double* Y = L + 36;                // [8][CZ]: [Y | z] of the current frame, zero-padded
+  double* Kl = Y + 8 * CZ;           // [N(N-1)/2][36] K_{i,j}, j < i, at (i(i-1)/2 + j)
   double* tg = Kl + 18 * N * (N - 1);  // [n_target][3] target corners (when staged)
   __shared__ int okl;
   __shared__ double cst[KB_MAX_CAMS][24];  // per camera: chain L (12) | intrinsics (10)
@@ -408,14 +453,9 @@ __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
   double tv[kTgU];
 #pragma unroll
   for (int u = 0; u < kTgU; ++u) tv[u] = d.target[min(tid + u * nth, nt3 - 1)];
-  int ab[M];
-#pragma unroll
-  for (int m = 0; m < M; ++m) ab[m] = d.tri[min(tid + nth * m, Wt - 1)];
   int2 fv = d.fview[(size_t)f0 * N + cam];
 #pragma unroll
   for (int u = 0; u < kTgU; ++u) KB_KEEP(tv[u]);
-#pragma unroll
-  for (int m = 0; m < M; ++m) KB_KEEP(ab[m]);
   KB_KEEPS(fv.x);
   KB_KEEPS(fv.y);
   if (gate && (done || !dob)) return;
@@ -453,13 +493,13 @@ __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
   const double* tgt = tg_lds ? tg : d.target;
   const double lam = gate ? c->lambda : d.host_lambda;
   const double lam2 = lam * lam;
-  double acc[M];
+  v4d acc[TW];
+  int tii[TW], tjj[TW];
 #pragma unroll
-  for (int m = 0; m < M; ++m) {
-    acc[m] = 0.0;
-    const int e = tid + nth * m;
-    ab[m] = (fuse && e < Wt) ? ab[m] : 0;
-  }
+  for (int t = 0; t < TW; ++t) acc[t] = v4d{0.0, 0.0, 0.0, 0.0};
+  schur_tiles_assign<TW>(fuse ? nbz : 0, tii, tjj);
+  for (int q = tid; q < 8 * CZ; q += nth)  // [Y | z] padding (rows 6, 7 and columns > C stay zero)
+    if (q >= 6 * CZ || (q % CZ) > C) Y[q] = 0.0;
   if (tid == 0) okl = 1;
   KB_STAMP(d, 16);
   for (int q = tid; q < N * 256; q += nth) camsum[q] = 0.0;
@@ -654,10 +694,10 @@ __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
       }
       __syncthreads();
       KB_STAMP(d, 22);
-      schur_forward(d, f, L, rdg, Fc, Fg, Y, z);
+      schur_forward(d, f, L, rdg, Fc, Fg, Y, CZ);
       __syncthreads();
       KB_STAMP(d, 23);
-      schur_accumulate<M>(C, Wt, W, Y, z, ab, acc);
+      schur_tiles_accumulate<TW>(Y, CZ, tii, tjj, acc);
     }
     __syncthreads();
     KB_STAMP(d, 24);
@@ -670,11 +710,7 @@ __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
     prow[q] = camsum[qc * 256 + a * 16 + b];
   }
   if (fuse) {
-#pragma unroll
-    for (int m = 0; m < M; ++m) {
-      const int e = threadIdx.x + nth * m;
-      if (e < W) prow[N * 136 + e] = acc[m];
-    }
+    schur_tiles_store<TW>(prow + N * 136, C, tii, tjj, acc);
     if (threadIdx.x == 0) prow[N * 136 + W] = okl ? 0.0 : 1.0;  // non-PD frame blocks (summed)
   }
   KB_STAMP(d, 25);
@@ -683,27 +719,26 @@ __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
 // ---------------------------------------------------------------------------------------------
 // k_schur: Schur step from the stored arrow blocks (LM passes with a new lambda, per-call solve)
 // ---------------------------------------------------------------------------------------------
-template <int M>
+template <int TW>
 __global__ void __launch_bounds__(256) k_schur(KbDev d, int gate) {
   KbCtrl* c = d.ctrl;
   if (gate && (c->done || c->do_build)) return;  // rebuild passes ran it fused in k_build
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const int C = d.C, W = d.W, Wt = W - C, N = d.N;
-  double* Y = sm;         // [6][C]
-  double* L = Y + 6 * C;  // [36]
-  double* z = L + 36;     // [8]
+  const int nbz = (C + 16) >> 4, CZ = 16 * nbz;
+  double* Y = sm;          // [8][CZ]: [Y | z], zero-padded
+  double* L = Y + 8 * CZ;  // [36]
   __shared__ int okl;
   __shared__ double rdg[6];
   const double lam = gate ? c->lambda : d.host_lambda;
   const double lam2 = lam * lam;
-  double acc[M];
-  int ab[M];
+  v4d acc[TW];
+  int tii[TW], tjj[TW];
 #pragma unroll
-  for (int m = 0; m < M; ++m) {
-    acc[m] = 0.0;
-    const int e = threadIdx.x + blockDim.x * m;
-    ab[m] = (e < Wt) ? d.tri[e] : 0;
-  }
+  for (int t = 0; t < TW; ++t) acc[t] = v4d{0.0, 0.0, 0.0, 0.0};
+  schur_tiles_assign<TW>(nbz, tii, tjj);
+  for (int q = threadIdx.x; q < 8 * CZ; q += blockDim.x)
+    if (q >= 6 * CZ || (q % CZ) > C) Y[q] = 0.0;
   if (threadIdx.x == 0) okl = 1;
   const int f0 = blockIdx.x * d.gframes, f1 = min(d.F, f0 + d.gframes);
   for (int f = f0; f < f1; ++f) {
@@ -713,16 +748,12 @@ __global__ void __launch_bounds__(256) k_schur(KbDev d, int gate) {
       if (!ok && threadIdx.x == 0) okl = 0;
     }
     __syncthreads();
-    schur_forward(d, f, L, rdg, nullptr, nullptr, Y, z);
+    schur_forward(d, f, L, rdg, nullptr, nullptr, Y, CZ);
     __syncthreads();
-    schur_accumulate<M>(C, Wt, W, Y, z, ab, acc);
+    schur_tiles_accumulate<TW>(Y, CZ, tii, tjj, acc);
   }
   double* prow = d.part + (size_t)blockIdx.x * d.Wtot + N * 136;
-#pragma unroll
-  for (int m = 0; m < M; ++m) {
-    const int e = threadIdx.x + blockDim.x * m;
-    if (e < W) prow[e] = acc[m];
-  }
+  schur_tiles_store<TW>(prow, C, tii, tjj, acc);
   __syncthreads();
   if (threadIdx.x == 0) prow[W] = okl ? 0.0 : 1.0;
 }
@@ -869,12 +900,6 @@ __global__ void __launch_bounds__(256) k_camexpand(KbDev d) {
 // k_solve: S = H_cc + lambda^2 I - sum Y^T Y, b = g_c - sum Y^T z (packed lower, staged in LDS);
 // LDL^T (one wave when C <= 64, else the block with one barrier per column); dx_c; camera DV update
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ int tri_row(int q) {  // row of packed-lower index q
-  int r = (int)((sqrtf(8.0f * (float)q + 1.0f) - 1.0f) * 0.5f);
-  while (r * (r + 1) / 2 > q) --r;
-  while ((r + 1) * (r + 2) / 2 <= q) ++r;
-  return r;
-}
 
 __device__ double cam_entry_l(const int N, const int* ci, const double* Hs, const double* T, const double* K, int p,
                               int q) {
@@ -922,10 +947,169 @@ __device__ double cam_grad_l(const int N, const int* ci, const double* Hs, const
 // column-major packed lower index of (i, j), i >= j (== row-major packed upper index of (j, i))
 __device__ __forceinline__ int cidx(int i, int j, int C) { return j * (2 * C - j - 1) / 2 + i; }
 
+// column of col-major packed lower index e (C columns)
+__device__ __forceinline__ int cidx_col(int e, int C) {
+  int j = (int)((2.0f * C + 1.0f - sqrtf((2.0f * C + 1.0f) * (2.0f * C + 1.0f) - 8.0f * (float)e)) * 0.5f);
+  j = max(0, min(j, C - 1));
+  while (j > 0 && j * (2 * C - j + 1) / 2 > e) --j;
+  while ((j + 1) * (2 * C - j) / 2 <= e) ++j;
+  return j;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Blocked LDL^T for camera blocks C > 64 (config 4: C = 106): 16 x 16 lower tiles in LDS, tile (it, jt) at
+// (it(it+1)/2 + jt) * 256, rows/cols in [C, 16 nb) padded with the identity.  Per 16-column panel: the
+// diagonal tile is factored in one wave's registers (v_readlane broadcasts), the rows below are solved
+// against it (one row per thread), and the trailing tiles are updated with v_mfma_f64_16x16x4f64
+// (S_ij -= W_i Ltilde_j^T, W = L D), one tile per wave at a time: 3 barriers per panel instead of one per column.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ int tile_base(int it, int jt) { return (it * (it + 1) / 2 + jt) * 256; }
+__device__ __forceinline__ int tidx(int i, int j) { return tile_base(i >> 4, j >> 4) + (i & 15) * 16 + (j & 15); }
+
+// LDS index of lower entry (i, j), i >= j, of the staged camera block: packed column-major (CM > 0) or tiles
+template <int CM>
+__device__ __forceinline__ int sidx(int i, int j, int C) {
+  if constexpr (CM > 0)
+    return cidx(i, j, C);
+  else
+    return tidx(i, j);
+}
+
+__device__ void ldl_tiles(double* S, double* rD, double* Wsc, int C, int nb, int* okl) {
+  const int tid = threadIdx.x, nth = blockDim.x, wave = tid >> 6, lane = tid & 63, nw = nth >> 6;
+  for (int p = 0; p < nb; ++p) {
+    const int b0 = tile_base(p, p);
+    if (wave == 0) {  // diagonal tile: lanes 0..15 hold its rows
+      const int r = lane < 16 ? lane : 15;
+      double row[16];
+#pragma unroll
+      for (int c = 0; c < 16; ++c) row[c] = S[b0 + (r > c ? r : c) * 16 + (r > c ? c : r)];
+      bool ok = true;
+      double rd = 1.0;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const double Dk = readlane_d(row[k], k);
+        ok = ok && (Dk > 0.0);
+        const double rdk = recip_d(Dk);
+        rd = (lane == k) ? rdk : rd;
+        const double f = (lane > k) ? row[k] * rdk : 0.0;
+#pragma unroll
+        for (int j = k + 1; j < 16; ++j) row[j] -= f * readlane_d(row[j], k);
+      }
+      double lrow[16];
+#pragma unroll
+      for (int c = 0; c < 16; ++c) lrow[c] = row[c] * readlane_d(rd, c);  // Ltilde[r][c] = (L D)[r][c] / D_c
+      if (lane < 16) {
+#pragma unroll
+        for (int c = 0; c < 16; ++c)
+          if (c <= lane) S[b0 + lane * 16 + c] = (c < lane) ? lrow[c] : row[c];  // strictly lower Ltilde, diag D
+        rD[16 * p + lane] = rd;
+      }
+      if (!ok && lane == 0) *okl = 0;  // padding rows have D = 1: only real pivots can fail
+    }
+    __syncthreads();
+    if (p == nb - 1) break;
+    // rows below the panel: W = S_ip Ltilde_pp^-T (stored in Wsc), Ltilde_ip = W D^-1 (in place)
+    const int nr = 16 * (nb - p - 1);
+    for (int g = tid; g < nr; g += nth) {
+      double* srow = S + tile_base(p + 1 + (g >> 4), p) + (g & 15) * 16;
+      double w[16];
+#pragma unroll
+      for (int c = 0; c < 16; ++c) w[c] = srow[c];
+#pragma unroll
+      for (int c = 1; c < 16; ++c)
+#pragma unroll
+        for (int c2 = 0; c2 < c; ++c2) w[c] -= w[c2] * S[b0 + c * 16 + c2];
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        Wsc[g * 16 + c] = w[c];
+        srow[c] = w[c] * rD[16 * p + c];
+      }
+    }
+    __syncthreads();
+    // trailing tiles (i, j), p < j <= i < nb: S_ij -= W_i Ltilde_j^T on MFMA (lane l: A[l&15][k], B[k][l&15])
+    const int m = nb - p - 1, ntiles = m * (m + 1) / 2;
+    for (int q = wave; q < ntiles; q += nw) {
+      const int ii = tri_row(q), jj = q - ii * (ii + 1) / 2;
+      const double* A = Wsc + ii * 256;
+      const double* B = S + tile_base(p + 1 + jj, p);
+      v4d acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int k = 4 * s + (lane >> 4);
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(A[(lane & 15) * 16 + k], B[(lane & 15) * 16 + k], acc, 0, 0, 0);
+      }
+      double* Ct = S + tile_base(p + 1 + ii, p + 1 + jj);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Ct[((lane >> 4) + 4 * r) * 16 + (lane & 15)] -= acc[r];
+    }
+    __syncthreads();
+  }
+}
+
+// xv (n = 16 nb entries, b on entry, zero-padded) <- (Ltilde D Ltilde^T)^-1 b
+__device__ void ldl_tiles_solve(const double* S, const double* rD, double* xv, int nb) {
+  const int tid = threadIdx.x, nth = blockDim.x, wave = tid >> 6, lane = tid & 63;
+  const int n = 16 * nb;
+  for (int p = 0; p < nb; ++p) {  // forward: Ltilde y = b
+    const int b0 = tile_base(p, p);
+    if (wave == 0) {
+      const int r = lane < 16 ? lane : 15;
+      double Lr[16];
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        const double v = S[b0 + r * 16 + c];
+        Lr[c] = (c < r) ? v : 0.0;
+      }
+      double xr = xv[16 * p + r];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) xr -= Lr[k] * readlane_d(xr, k);
+      if (lane < 16) xv[16 * p + lane] = xr;
+    }
+    __syncthreads();
+    for (int g = 16 * (p + 1) + tid; g < n; g += nth) {
+      const double* lr = S + tile_base(g >> 4, p) + (g & 15) * 16;
+      double s = 0.0;
+#pragma unroll
+      for (int c = 0; c < 16; ++c) s += lr[c] * xv[16 * p + c];
+      xv[g] -= s;
+    }
+    __syncthreads();
+  }
+  for (int g = tid; g < n; g += nth) xv[g] *= rD[g];  // z = D^-1 y
+  __syncthreads();
+  for (int p = nb - 1; p >= 0; --p) {  // backward: Ltilde^T x = z
+    const int b0 = tile_base(p, p);
+    if (wave == 0) {
+      const int r = lane < 16 ? lane : 15;
+      double Lc[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const double v = S[b0 + k * 16 + r];
+        Lc[k] = (k > r) ? v : 0.0;
+      }
+      double xr = xv[16 * p + r];
+#pragma unroll
+      for (int k = 15; k >= 0; --k) xr -= Lc[k] * readlane_d(xr, k);
+      if (lane < 16) xv[16 * p + lane] = xr;
+    }
+    __syncthreads();
+    if (p == 0) break;
+    for (int g = tid; g < 16 * p; g += nth) {  // rows of earlier panels: z_g -= sum_r Ltilde_{p,q}[r][g] x_p[r]
+      const double* lc = S + tile_base(p, g >> 4) + (g & 15);
+      double s = 0.0;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s += lc[r * 16] * xv[16 * p + r];
+      xv[g] -= s;
+    }
+    __syncthreads();
+  }
+}
+
 // batched global -> LDS staging of the k_solve inputs: every thread keeps U independent loads in flight
 // (a runtime-bounded copy loop would otherwise wait for each load before the next).  Items are laid out as
 // [camK N*N*36 | per-camera sums N*256 | Schur sums Wt | Schur rhs C | colinfo C] over one index space.
-template <int U>
+template <int U, int CM>
 __device__ __forceinline__ void solve_stage(const KbDev& d, double* K, double* Hs, double* S, double* bv, int* ci,
                                             int tid, int nth) {
   const int N = d.N, C = d.C, Wt = d.W - C;
@@ -956,7 +1140,13 @@ __device__ __forceinline__ void solve_stage(const KbDev& d, double* K, double* H
         Hs[cam * 256 + a * 16 + b] = v[u];
         Hs[cam * 256 + b * 16 + a] = v[u];
       } else if (q < n2) {
-        S[q - n1] = -v[u];  // upper (a,b) row-major == lower (b,a) col-major
+        const int e = q - n1;  // upper (a,b) row-major == lower (b,a) col-major packed index e
+        if constexpr (CM > 0) {
+          S[e] = -v[u];
+        } else {
+          const int a = cidx_col(e, C), b = e - a * (2 * C - a - 1) / 2;
+          S[tidx(b, a)] = -v[u];
+        }
       } else if (q < n2 + C) {
         bv[q - n2] = -v[u];
       } else if (q < n3) {
@@ -968,23 +1158,7 @@ __device__ __forceinline__ void solve_stage(const KbDev& d, double* K, double* H
   }
 }
 
-// column of col-major packed lower index e (C columns)
-__device__ __forceinline__ int cidx_col(int e, int C) {
-  int j = (int)((2.0f * C + 1.0f - sqrtf((2.0f * C + 1.0f) * (2.0f * C + 1.0f) - 8.0f * (float)e)) * 0.5f);
-  j = max(0, min(j, C - 1));
-  while (j > 0 && j * (2 * C - j + 1) / 2 > e) --j;
-  while ((j + 1) * (2 * C - j) / 2 <= e) ++j;
-  return j;
-}
 
-// 1/x by v_rcp_f64 + two Newton steps (a short dependent chain; within an ulp of the IEEE quotient)
-__device__ __forceinline__ double recip_d(double x) {
-  double r = __builtin_amdgcn_rcp(x);
-  double e = fma(-x, r, 1.0);
-  r = fma(r, e, r);
-  e = fma(-x, r, 1.0);
-  return fma(r, e, r);
-}
 
 // LDL^T + the three triangular solves of one wave, matrix rows in registers (lane i holds row i of the
 // trailing matrix, CM >= C padded with the identity).  Step k broadcasts row k with v_readlane (no LDS), and
@@ -1039,14 +1213,17 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const int N = d.N, C = d.C, W = d.W, nth = blockDim.x, tid = threadIdx.x;
   const int Cp = C * (C + 1) / 2;
-  double* S = sm;                    // column-major packed lower [Cp]
-  double* bv = S + Cp;               // [C] (+1: non-PD frame-block count while staging)
+  const int nb = (C + 15) >> 4, n16 = 16 * nb;  // CM == 0: 16 x 16 tiles
+  double* S = sm;                    // CM > 0: column-major packed lower [Cp]; CM == 0: lower tiles
+  double* bv = S + (CM > 0 ? Cp : 128 * nb * (nb + 1));  // [C] (+1: non-PD frame-block count while staging)
   double* gl = bv + C + 1;           // [C]
   double* Hs = gl + C;               // [N][256]
   double* T = Hs + N * 256;          // [N][N][36]
   double* K = T + N * N * 36;        // [N][N][36]
-  int* ci = (int*)(K + N * N * 36);  // [C]
-  int* ptab = ci + C;                // [(C-1)C/2] pair table of the trailing triangle: ii<<16 | jj (CM == 0)
+  double* Wsc = K + N * N * 36;      // CM == 0: [n16 - 16][16] panel scratch
+  double* rDv = Wsc + (CM > 0 ? 0 : 16 * (n16 - 16));  // CM == 0: [n16] 1/D
+  double* xv = rDv + (CM > 0 ? 0 : n16);               // CM == 0: [n16] right-hand side / solution
+  int* ci = (int*)(xv + (CM > 0 ? 0 : n16));           // [C]
   __shared__ int okl;
   __shared__ double nbase[KB_MAX_CAMS * 7];  // candidate baselines
   __shared__ int ctab[3][KB_MAX_CAMS];       // per camera: #intrinsics | first intrinsic column | baseline column
@@ -1055,13 +1232,11 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update) {
   const int cur = c->cur;
   KB_STAMP(d, 0);
   // phase A: stage K, column info, per-camera sums and the Schur sums in LDS (one row: psum)
-  solve_stage<4>(d, K, Hs, S, bv, ci, tid, nth);
+  solve_stage<4, CM>(d, K, Hs, S, bv, ci, tid, nth);
   if (tid < 3 * N) ctab[tid / N][tid % N] = tid < N ? d.nintr[tid] : (tid < 2 * N ? d.col_intr[tid - N] : d.col_base[tid - 2 * N]);
-  if (CM == 0)
-    for (int q = tid; q < (C - 1) * C / 2; q += nth) {
-      const int ii = tri_row(q);
-      ptab[q] = (ii << 16) | (q - ii * (ii + 1) / 2);
-    }
+  if (CM == 0)  // identity padding of the tiles beyond C (disjoint from the staged entries)
+    for (int i = C; i < n16; ++i)
+      for (int j = tid; j <= i; j += nth) S[tidx(i, j)] = (i == j) ? 1.0 : 0.0;
   __syncthreads();
   if (tid == 0) okl = (c->solve_ok != 0) && !(bv[C] > 0.0);
   KB_STAMP(d, 1);
@@ -1084,7 +1259,7 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update) {
   __syncthreads();
   for (int e = tid; e < Cp; e += nth) {
     const int j = cidx_col(e, C), i = e - j * (2 * C - j - 1) / 2;  // lower (i, j), i >= j
-    S[e] += cam_entry_l(N, ci, Hs, T, K, i, j) + ((i == j) ? lam2 : 0.0);
+    S[sidx<CM>(i, j, C)] += cam_entry_l(N, ci, Hs, T, K, i, j) + ((i == j) ? lam2 : 0.0);
   }
   for (int p = tid; p < C; p += nth) {
     const double g = cam_grad_l(N, ci, Hs, K, p);
@@ -1104,93 +1279,15 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update) {
     KB_STAMP(d, 3);
     KB_STAMP(d, 4);
   } else {
-    // phase C: right-looking LDL^T on (i, j) pairs, k < j <= i: S[i][j] -= S[i][k] S[j][k] / D_k.
-    // Column k is final during step k and every pair is written by one thread: each thread gathers its pairs'
-    // operands first (8 per batch), then writes, so one step costs ~2 LDS round trips.
-    for (int k = 0; k < C; ++k) {
-      const double Dk = S[cidx(k, k, C)];
-      if (tid == 0 && !(Dk > 0.0)) okl = 0;
-      const double rdk = 1.0 / Dk;
-      const int n = C - k - 1, np = n * (n + 1) / 2;
-      for (int q0 = tid; q0 < np; q0 += 8 * nth) {
-        double a[8], b[8], v[8];
-        int ix[8];
-        bool ok[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {  // unconditional (clamped) loads: no per-element branch
-          const int q = q0 + u * nth;
-          ok[u] = q < np;
-          const int pt = ptab[ok[u] ? q : 0], i = k + 1 + (pt >> 16), j = k + 1 + (pt & 0xffff);
-          ix[u] = cidx(i, j, C);
-          a[u] = S[cidx(i, k, C)];
-          b[u] = S[cidx(j, k, C)];
-          v[u] = S[ix[u]];
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-          if (ok[u]) S[ix[u]] = v[u] - a[u] * b[u] * rdk;
-      }
-      __syncthreads();
-    }
+    // phase C: blocked LDL^T on 16 x 16 tiles (MFMA trailing updates); phase D: blocked solves
+    ldl_tiles(S, rDv, Wsc, C, nb, &okl);
     KB_STAMP(d, 3);
-    // phase D: Ltilde y = b, z = D^-1 y, Ltilde^T x = z; row i held by lane i & 63 (slot i >> 6).
-    // Each 16-step chunk first preloads the lane's matrix entries into registers.
+    for (int g = tid; g < n16; g += nth) xv[g] = g < C ? bv[g] : 0.0;
+    __syncthreads();
+    ldl_tiles_solve(S, rDv, xv, nb);
     if (tid < 64) {
-      const int lane = tid;
-      double rD[2];
 #pragma unroll
-      for (int sl = 0; sl < 2; ++sl) {
-        const int i = lane + 64 * sl;
-        x[sl] = (i < C) ? bv[i] : 0.0;
-        rD[sl] = (i < C) ? 1.0 / S[cidx(i, i, C)] : 0.0;
-      }
-      for (int k0 = 0; k0 < C; k0 += 16) {
-        double Lr[2][16];
-#pragma unroll
-        for (int sl = 0; sl < 2; ++sl) {
-          const int i = lane + 64 * sl;
-#pragma unroll
-          for (int u = 0; u < 16; ++u) {
-            const bool use = i < C && k0 + u < i;
-            const double val = S[use ? cidx(i, k0 + u, C) : 0];
-            Lr[sl][u] = use ? val : 0.0;
-          }
-        }
-#pragma unroll
-        for (int u = 0; u < 16; ++u) {
-          const int k = k0 + u;
-          if (k < C) {
-            const double yk = readlane_d(x[k >> 6], k & 63) * readlane_d(rD[k >> 6], k & 63);
-#pragma unroll
-            for (int sl = 0; sl < 2; ++sl) x[sl] -= Lr[sl][u] * yk;  // Lr = 0 unless i > k
-          }
-        }
-      }
-#pragma unroll
-      for (int sl = 0; sl < 2; ++sl) x[sl] *= rD[sl];
-      for (int k1 = C - 1; k1 >= 0; k1 -= 16) {
-        double Lc[2][16];
-#pragma unroll
-        for (int sl = 0; sl < 2; ++sl) {
-          const int i = lane + 64 * sl;
-#pragma unroll
-          for (int u = 0; u < 16; ++u) {
-            const int k = k1 - u;
-            const bool use = k >= 0 && i < k;
-            const double val = S[use ? cidx(k, i, C) : 0];
-            Lc[sl][u] = use ? val * rD[sl] : 0.0;
-          }
-        }
-#pragma unroll
-        for (int u = 0; u < 16; ++u) {
-          const int k = k1 - u;
-          if (k >= 0) {
-            const double xk = readlane_d(x[k >> 6], k & 63);
-#pragma unroll
-            for (int sl = 0; sl < 2; ++sl) x[sl] -= Lc[sl][u] * xk;  // Lc = 0 unless i < k
-          }
-        }
-      }
+      for (int sl = 0; sl < 2; ++sl) x[sl] = (tid + 64 * sl < C) ? xv[tid + 64 * sl] : 0.0;
     }
     KB_STAMP(d, 4);
   }

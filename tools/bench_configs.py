@@ -11,8 +11,10 @@ sys.path.insert(0, ROOT)
 from kalibr_amd import capi, synth  # noqa: E402
 
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 200
-for cfg in (1, 2, 3, 4):
-    p = synth.make_config(cfg)
+cfgs = [int(c) for c in sys.argv[2].split(",")] if len(sys.argv) > 2 else [1, 2, 3, 4]
+frames = int(sys.argv[3]) if len(sys.argv) > 3 else None
+for cfg in cfgs:
+    p = synth.make_config(cfg, n_frames=frames) if frames else synth.make_config(cfg)
     g = capi.Solver(p)
     g.set_state(p.state_init)
     g.optimize(policy="lm", lambda0=10.0, max_iterations=100, eps_x=1e-3, eps_j=1.0)  # GN from a converged state
