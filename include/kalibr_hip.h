@@ -121,6 +121,7 @@ typedef struct kb_solution {
   double J_start, J_final, dx_final, dj_final; /* SolutionReturnValue (backend.hpp:11-24) */
   int32_t iterations, failed_iterations, linear_solver_failure;
   int32_t passes;
+  int32_t graphed;         /* 1 if the passes ran as captured hipGraphs (RCCL calls included when sharded) */
 } kb_solution;
 
 int kb_optimize(kb_handle* h, const kb_optimizer_options* opts, kb_solution* out);

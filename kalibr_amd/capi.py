@@ -44,7 +44,7 @@ class OptimizerOptions(C.Structure):
 class Solution(C.Structure):
     _fields_ = [("J_start", C.c_double), ("J_final", C.c_double), ("dx_final", C.c_double), ("dj_final", C.c_double),
                 ("iterations", C.c_int32), ("failed_iterations", C.c_int32), ("linear_solver_failure", C.c_int32),
-                ("passes", C.c_int32)]
+                ("passes", C.c_int32), ("graphed", C.c_int32)]
 
 
 def lib():

@@ -68,6 +68,7 @@ struct kb_handle {
   hipGraphExec_t graph = nullptr;   // one captured pass of graph_policy
   hipGraphExec_t graphP = nullptr;  // kGraphPasses captured passes (no inter-launch gap between them)
   int graph_policy = -1;
+  bool graph_failed = false;  // capture of the RCCL calls failed once: eager passes from then on
   int graph_trace_cap = 0;
   double* trace = nullptr;
   int trace_cap = 0;
@@ -198,6 +199,7 @@ kb_handle* kb_create(const kb_layout* L) {
   d.psum = d.psum_local;
   d.psum_rows = 1;
   d.dbg_stop = -1;
+  d.dbg_flags = 0;
   rc |= h->alloc(&d.ticket, 16);
   rc |= h->alloc(&d.Hcc, (size_t)h->C * h->C);
   rc |= h->alloc(&d.gc, (size_t)h->C);
@@ -241,11 +243,11 @@ kb_handle* kb_create(const kb_layout* L) {
       h->lds_solve = sizeof(double) * (C * (C + 1) / 2 + 2 * C + 1 + N * 256 + 2 * N * N * 36) + sizeof(int) * C;
     } else {  // 16 x 16 lower tiles + panel scratch + 1/D + solution vector
       const int nb = (C + 15) / 16, n16 = 16 * nb;
-      h->lds_solve = sizeof(double) * (128 * nb * (nb + 1) + 2 * C + 1 + N * 256 + 2 * N * N * 36 + 16 * (n16 - 16) +
+      h->lds_solve = sizeof(double) * (8 * 17 * nb * (nb + 1) + 2 * C + 1 + N * 256 + 2 * N * N * 36 + 17 * (n16 - 16) +
                                        2 * n16) +
                      sizeof(int) * C;
     }
-    h->solve_threads = 256;
+    h->solve_threads = C <= 64 ? 256 : 512;
     h->fn_solve = C <= 16   ? (const void*)k_solve<16>
                   : C <= 24 ? (const void*)k_solve<24>
                   : C <= 32 ? (const void*)k_solve<32>
@@ -405,10 +407,15 @@ static int launch_cost(kb_handle* h, int which) {
   return 0;
 }
 
-static int allreduce_red(kb_handle* h) {
+// one all-gather of every rank's [cost, dx.dx, dx.rhs, max|dx|]; reduced in rank order on every rank (by
+// k_red_gather, or inline by k_policy) so that all ranks hold bitwise-identical sums
+static int allreduce_red(kb_handle* h, bool reduce = true) {
   if (!h->comm) return 0;
-  KB_NCCL(ncclAllReduce(h->d.red_local, h->d.red, 3, ncclDouble, ncclSum, h->comm, h->stream));
-  KB_NCCL(ncclAllReduce(h->d.red_local + 3, h->d.red + 3, 1, ncclDouble, ncclMax, h->comm, h->stream));
+  KB_NCCL(ncclAllGather(h->d.red_local, const_cast<double*>(h->d.red_all), 4, ncclDouble, h->comm, h->stream));
+  if (reduce) {
+    hipLaunchKernelGGL(k_red_gather, dim3(1), dim3(1), 0, h->stream, h->d);
+    KB_HIP(hipGetLastError());
+  }
   return 0;
 }
 
@@ -571,14 +578,16 @@ static int enqueue_pass(kb_handle* h, int policy) {
   KbDev& d = h->d;
   if (launch_build(h, 1, 1)) return -1;
   if (policy == 0 && launch_schur(h, 1)) return -1;  // LM passes that keep the system (lambda change)
-  const bool one_gpu = !h->comm;
-  if (launch_colsum(h, 1, !one_gpu)) return -1;
-  if (launch_solve(h, 1, 1, one_gpu)) return -1;
+  // one GPU and a small partial row: k_solve sums the stage-1 rows while staging (one launch less); otherwise
+  // k_colfin finishes the rows in parallel (and feeds the all-reduce when sharded)
+  const bool from_rows = !h->comm && h->d.Wtot <= 2048;
+  if (launch_colsum(h, 1, !from_rows)) return -1;
+  if (launch_solve(h, 1, 1, from_rows)) return -1;
   if (launch_backsub(h, 1, 1, 1)) return -1;
-  hipLaunchKernelGGL(k_post, dim3(1), dim3(256), 0, h->stream, d, one_gpu ? 1 : 0);
+  hipLaunchKernelGGL(k_post, dim3(1), dim3(256), 0, h->stream, d, h->comm ? 0 : 1);
   KB_HIP(hipGetLastError());
   if (h->comm) {
-    if (allreduce_red(h)) return -1;
+    if (allreduce_red(h, false)) return -1;
     hipLaunchKernelGGL(k_policy, dim3(1), dim3(1), 0, h->stream, d);
     KB_HIP(hipGetLastError());
   }
@@ -618,6 +627,18 @@ static int ensure_graph(kb_handle* h, int policy) {
   return 0;
 }
 
+// captured graphs for this policy; RCCL calls are captured too when sharded.  If capturing them fails on this
+// stack, the handle falls back to eager passes for good (same kernels, same results).
+static bool graph_ok(kb_handle* h, int policy) {
+  if (h->graph_failed) return false;
+  if (ensure_graph(h, policy) == 0) return true;
+  if (!h->comm) return false;  // caller reports the error through kb_last_error on the eager path as well
+  hipGetLastError();
+  drop_graphs(h);
+  h->graph_failed = true;
+  return false;
+}
+
 // launch n passes: whole kGraphPasses graphs, then single-pass graphs (or eager passes when not graphed)
 static int launch_passes(kb_handle* h, int policy, int n, bool graph) {
   int i = 0;
@@ -652,8 +673,7 @@ int kb_optimize(kb_handle* h, const kb_optimizer_options* opts, kb_solution* out
   if (ensure_trace(h, max_passes + 1)) return -1;
   KbOpts o{opts->policy, opts->max_iterations, opts->lambda_init, opts->convergence_dx, opts->convergence_dj};
   if (loop_start(h, o)) return -1;
-  const bool graph = opts->use_graph != 0 && !h->comm;  // RCCL calls stay eager
-  if (graph && ensure_graph(h, opts->policy)) return -1;
+  const bool graph = opts->use_graph != 0 && graph_ok(h, opts->policy);
   const int every = opts->sync_every > 0 ? opts->sync_every : 2 * kGraphPasses;
   KbCtrl ctrl{};
   int passes = 0;
@@ -674,6 +694,7 @@ int kb_optimize(kb_handle* h, const kb_optimizer_options* opts, kb_solution* out
   out->failed_iterations = ctrl.failed_iterations;
   out->linear_solver_failure = ctrl.lin_fail;
   out->passes = ctrl.passes;
+  out->graphed = graph ? 1 : 0;
   return 0;
 }
 
@@ -695,8 +716,7 @@ int kb_run_gn_iterations(kb_handle* h, int32_t n_iter, double* seconds) {
   // GN, convergence tests disabled (thresholds -1 keep (dX > eps && |dJ| > eps) true)
   KbOpts o{1, 0x3fffffff, 0.0, -1.0, -1.0};
   if (loop_start(h, o)) return -1;
-  const bool graph = !h->comm;
-  if (graph && ensure_graph(h, 1)) return -1;
+  const bool graph = graph_ok(h, 1);
   KB_HIP(hipStreamSynchronize(h->stream));
   const auto t0 = std::chrono::steady_clock::now();
   if (launch_passes(h, 1, n_iter, graph)) return -1;
@@ -778,6 +798,10 @@ int kb_comm_init(kb_handle* h, const void* uid, int32_t nranks, int32_t rank) {
   h->d.psum = h->psum_red;
   h->d.psum_rows = 1;
   h->d.red = rr;
+  double* ra = nullptr;
+  if (h->alloc(&ra, 4 * (size_t)nranks)) return -1;
+  h->d.red_all = ra;
+  h->d.nranks = nranks;
   drop_graphs(h);
   KB_HIP(hipStreamSynchronize(h->stream));
   return 0;
@@ -786,7 +810,7 @@ int kb_comm_init(kb_handle* h, const void* uid, int32_t nranks, int32_t rank) {
 #ifdef KB_STAMPS
 // diagnostic build only: average duration (us, HIP events over `reps` launches) of one kernel of the GN pass run
 // up to stop point `stop` (KB_STAMP): which = 0 fused build, 1 camera solve, 2 back-substitution.
-int kb_diag_phase_time(kb_handle* h, int which, int stop, int reps, double* us) {
+int kb_diag_phase_time(kb_handle* h, int which, int stop, int reps, int flags, double* us) {
   KB_HIP(hipSetDevice(h->device));
   KbOpts o{1, 0x3fffffff, 0.0, -1.0, -1.0};
   if (ensure_trace(h, 64) || loop_start(h, o)) return -1;
@@ -795,6 +819,7 @@ int kb_diag_phase_time(kb_handle* h, int which, int stop, int reps, double* us) 
   if (launch_build(h, 0, 1) || launch_colsum(h, 0, false)) return -1;
   KbDev d = h->d;
   d.dbg_stop = stop;
+  d.dbg_flags = flags;
   d.psum = d.part8;
   d.psum_rows = kColsumRows;
   hipEvent_t e0, e1;

@@ -70,10 +70,13 @@ struct KbDev {
   double* camstat;   // [4]
   double* costpart;  // [nblk_cost]
   double* red_local; // [4]: cost, dx.dx, dx.rhs, max|dx|
-  double* red;       // [4] (all-reduced; aliases red_local on one GPU)
+  double* red;       // [4] (reduced over ranks; aliases red_local on one GPU)
+  const double* red_all;  // [nranks][4] all-gathered red_local (sharded runs)
+  int nranks;
   double* trace;
   KbCtrl* ctrl;
-  int dbg_stop;  // diagnostic build only (KB_STAMPS): stop point of the timed kernel (-1: run to the end)
+  int dbg_stop;   // diagnostic build only (KB_STAMPS): stop point of the timed kernel (-1: run to the end)
+  int dbg_flags;  // diagnostic build only: bit 0 run the camera LDL^T twice (rolled)
 };
 
 #ifdef KB_STAMPS

@@ -256,7 +256,7 @@ __device__ void pol_post(KbCtrl* c, const KbDev& d, const double* red) {
 // camera chains of a state: L_i (R|t) = B_{i-1}..B_0 and K_{i,j} (one block) -> slot `slot` of camL / camK.
 // `base` points at the N-1 baseline poses (7-stride, HBM or LDS).
 // ---------------------------------------------------------------------------------------------
-__device__ void chain_block(const KbDev& d, const double* base, int slot) {
+__device__ void chain_block(const KbDev& d, const double* base, int slot, int nth) {
   __shared__ double sR[KB_MAX_CAMS][9], st[KB_MAX_CAMS][3];  // baseline B_j
   __shared__ double LR[KB_MAX_CAMS][9], Lt[KB_MAX_CAMS][3];
   const int N = d.N;
@@ -270,11 +270,11 @@ __device__ void chain_block(const KbDev& d, const double* base, int slot) {
     for (int i = 1; i < N; ++i) rt_mul(sR[i - 1], st[i - 1], LR[i - 1], Lt[i - 1], LR[i], Lt[i]);
   }
   __syncthreads();
-  for (int q = threadIdx.x; q < N * 12; q += blockDim.x) {
+  for (int q = threadIdx.x; q < N * 12; q += nth) {
     const int i = q / 12, e = q % 12;
     Lo[q] = e < 9 ? LR[i][e] : Lt[i][e - 9];
   }
-  for (int idx = threadIdx.x; idx < N * N * 36; idx += blockDim.x) {
+  for (int idx = threadIdx.x; idx < N * N * 36; idx += nth) {
     const int e = idx % 36, ij = idx / 36, i = ij / N, j = ij % N;
     double val = 0.0;
     if (j < i) {
@@ -298,7 +298,7 @@ __global__ void __launch_bounds__(256) k_pre(KbDev d, int gate) {
   KbCtrl* c = d.ctrl;
   if (gate && threadIdx.x == 0 && !c->done) pol_pre(c);
   const int cur = c->cur;
-  chain_block(d, d.state + (size_t)cur * d.S + d.off_base, cur);
+  chain_block(d, d.state + (size_t)cur * d.S + d.off_base, cur, blockDim.x);
 }
 
 // 6x6 Cholesky of A + lam2 I by one wave (lanes 0..5 hold rows; column k broadcast with v_readlane):
@@ -963,8 +963,10 @@ __device__ __forceinline__ int cidx_col(int e, int C) {
 // against it (one row per thread), and the trailing tiles are updated with v_mfma_f64_16x16x4f64
 // (S_ij -= W_i Ltilde_j^T, W = L D), one tile per wave at a time: 3 barriers per panel instead of one per column.
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ int tile_base(int it, int jt) { return (it * (it + 1) / 2 + jt) * 256; }
-__device__ __forceinline__ int tidx(int i, int j) { return tile_base(i >> 4, j >> 4) + (i & 15) * 16 + (j & 15); }
+constexpr int kTS = 17;             // tile row stride (doubles): 16 + 1 keeps row-parallel LDS accesses conflict-free
+constexpr int kTileSz = 16 * kTS;
+__device__ __forceinline__ int tile_base(int it, int jt) { return (it * (it + 1) / 2 + jt) * kTileSz; }
+__device__ __forceinline__ int tidx(int i, int j) { return tile_base(i >> 4, j >> 4) + (i & 15) * kTS + (j & 15); }
 
 // LDS index of lower entry (i, j), i >= j, of the staged camera block: packed column-major (CM > 0) or tiles
 template <int CM>
@@ -975,15 +977,19 @@ __device__ __forceinline__ int sidx(int i, int j, int C) {
     return tidx(i, j);
 }
 
-__device__ void ldl_tiles(double* S, double* rD, double* Wsc, int C, int nb, int* okl) {
+__device__ void ldl_tiles(const KbDev& d, double* S, double* rD, double* Wsc, int C, int nb, int* okl) {
   const int tid = threadIdx.x, nth = blockDim.x, wave = tid >> 6, lane = tid & 63, nw = nth >> 6;
   for (int p = 0; p < nb; ++p) {
     const int b0 = tile_base(p, p);
+#ifdef KB_STAMPS
+    const int reps = (p == 0 && d.dbg_stop == 43) ? 2 : 1;  // diagnostic: second (I-cache warm) execution
+    for (int rep = 0; rep < reps; ++rep)
+#endif
     if (wave == 0) {  // diagonal tile: lanes 0..15 hold its rows
       const int r = lane < 16 ? lane : 15;
       double row[16];
 #pragma unroll
-      for (int c = 0; c < 16; ++c) row[c] = S[b0 + (r > c ? r : c) * 16 + (r > c ? c : r)];
+      for (int c = 0; c < 16; ++c) row[c] = S[b0 + (r > c ? r : c) * kTS + (r > c ? c : r)];
       bool ok = true;
       double rd = 1.0;
 #pragma unroll
@@ -1002,48 +1008,52 @@ __device__ void ldl_tiles(double* S, double* rD, double* Wsc, int C, int nb, int
       if (lane < 16) {
 #pragma unroll
         for (int c = 0; c < 16; ++c)
-          if (c <= lane) S[b0 + lane * 16 + c] = (c < lane) ? lrow[c] : row[c];  // strictly lower Ltilde, diag D
+          if (c <= lane) S[b0 + lane * kTS + c] = (c < lane) ? lrow[c] : row[c];  // strictly lower Ltilde, diag D
         rD[16 * p + lane] = rd;
       }
       if (!ok && lane == 0) *okl = 0;  // padding rows have D = 1: only real pivots can fail
     }
     __syncthreads();
+    if (p == 0) KB_STAMP(d, 40);
+    if (p == 0) KB_STAMP(d, 43);
     if (p == nb - 1) break;
     // rows below the panel: W = S_ip Ltilde_pp^-T (stored in Wsc), Ltilde_ip = W D^-1 (in place)
     const int nr = 16 * (nb - p - 1);
     for (int g = tid; g < nr; g += nth) {
-      double* srow = S + tile_base(p + 1 + (g >> 4), p) + (g & 15) * 16;
+      double* srow = S + tile_base(p + 1 + (g >> 4), p) + (g & 15) * kTS;
       double w[16];
 #pragma unroll
       for (int c = 0; c < 16; ++c) w[c] = srow[c];
 #pragma unroll
       for (int c = 1; c < 16; ++c)
 #pragma unroll
-        for (int c2 = 0; c2 < c; ++c2) w[c] -= w[c2] * S[b0 + c * 16 + c2];
+        for (int c2 = 0; c2 < c; ++c2) w[c] -= w[c2] * S[b0 + c * kTS + c2];
 #pragma unroll
       for (int c = 0; c < 16; ++c) {
-        Wsc[g * 16 + c] = w[c];
+        Wsc[g * kTS + c] = w[c];
         srow[c] = w[c] * rD[16 * p + c];
       }
     }
     __syncthreads();
+    if (p == 0) KB_STAMP(d, 41);
     // trailing tiles (i, j), p < j <= i < nb: S_ij -= W_i Ltilde_j^T on MFMA (lane l: A[l&15][k], B[k][l&15])
     const int m = nb - p - 1, ntiles = m * (m + 1) / 2;
     for (int q = wave; q < ntiles; q += nw) {
       const int ii = tri_row(q), jj = q - ii * (ii + 1) / 2;
-      const double* A = Wsc + ii * 256;
+      const double* A = Wsc + ii * kTileSz;
       const double* B = S + tile_base(p + 1 + jj, p);
       v4d acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         const int k = 4 * s + (lane >> 4);
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(A[(lane & 15) * 16 + k], B[(lane & 15) * 16 + k], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(A[(lane & 15) * kTS + k], B[(lane & 15) * kTS + k], acc, 0, 0, 0);
       }
       double* Ct = S + tile_base(p + 1 + ii, p + 1 + jj);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) Ct[((lane >> 4) + 4 * r) * 16 + (lane & 15)] -= acc[r];
+      for (int r = 0; r < 4; ++r) Ct[((lane >> 4) + 4 * r) * kTS + (lane & 15)] -= acc[r];
     }
     __syncthreads();
+    if (p == 0) KB_STAMP(d, 42);
   }
 }
 
@@ -1058,7 +1068,7 @@ __device__ void ldl_tiles_solve(const double* S, const double* rD, double* xv, i
       double Lr[16];
 #pragma unroll
       for (int c = 0; c < 16; ++c) {
-        const double v = S[b0 + r * 16 + c];
+        const double v = S[b0 + r * kTS + c];
         Lr[c] = (c < r) ? v : 0.0;
       }
       double xr = xv[16 * p + r];
@@ -1068,7 +1078,7 @@ __device__ void ldl_tiles_solve(const double* S, const double* rD, double* xv, i
     }
     __syncthreads();
     for (int g = 16 * (p + 1) + tid; g < n; g += nth) {
-      const double* lr = S + tile_base(g >> 4, p) + (g & 15) * 16;
+      const double* lr = S + tile_base(g >> 4, p) + (g & 15) * kTS;
       double s = 0.0;
 #pragma unroll
       for (int c = 0; c < 16; ++c) s += lr[c] * xv[16 * p + c];
@@ -1085,7 +1095,7 @@ __device__ void ldl_tiles_solve(const double* S, const double* rD, double* xv, i
       double Lc[16];
 #pragma unroll
       for (int k = 0; k < 16; ++k) {
-        const double v = S[b0 + k * 16 + r];
+        const double v = S[b0 + k * kTS + r];
         Lc[k] = (k > r) ? v : 0.0;
       }
       double xr = xv[16 * p + r];
@@ -1099,7 +1109,7 @@ __device__ void ldl_tiles_solve(const double* S, const double* rD, double* xv, i
       const double* lc = S + tile_base(p, g >> 4) + (g & 15);
       double s = 0.0;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) s += lc[r * 16] * xv[16 * p + r];
+      for (int r = 0; r < 16; ++r) s += lc[r * kTS] * xv[16 * p + r];
       xv[g] -= s;
     }
     __syncthreads();
@@ -1164,21 +1174,10 @@ __device__ __forceinline__ void solve_stage(const KbDev& d, double* K, double* H
 // trailing matrix, CM >= C padded with the identity).  Step k broadcasts row k with v_readlane (no LDS), and
 // lanes i > k apply S[i][j] -= (S[i][k] / D_k) S[k][j].  Row i freezes at step i, so lane i ends holding
 // Ltilde[i][k] D_k (k < i), D_i, and by symmetry of the trailing matrix Ltilde[k][i] D_i (k > i).
-template <int CM>
-__device__ __forceinline__ bool ldl_solve_reg(const double* S, const double* bv, int C, int lane, double& xo) {
-  double row[CM];
+template <int CM, int K0, int K1>
+__device__ __forceinline__ void ldl_steps(double (&row)[CM], int lane, bool& ok, double& rD) {
 #pragma unroll
-  for (int j = 0; j < CM; ++j) {
-    const bool in = lane < C && j < C;
-    const int a = lane > j ? lane : j, b = lane > j ? j : lane;
-    const double v = S[in ? cidx(a, b, C) : 0];
-    row[j] = in ? v : (lane == j ? 1.0 : 0.0);
-  }
-  double x = lane < C ? bv[lane] : 0.0;
-  bool ok = true;
-  double rD = 1.0;
-#pragma unroll
-  for (int k = 0; k < CM; ++k) {
+  for (int k = K0; k < K1; ++k) {
     const double Dk = readlane_d(row[k], k);
     ok = ok && (Dk > 0.0);
     const double rdk = recip_d(Dk);
@@ -1187,6 +1186,71 @@ __device__ __forceinline__ bool ldl_solve_reg(const double* S, const double* bv,
 #pragma unroll
     for (int j = k + 1; j < CM; ++j) row[j] -= f * readlane_d(row[j], k);
   }
+}
+
+struct LdlOut {
+  double x;
+  int ok;
+};
+
+// One factorisation step set with the column broadcast through LDS instead of v_readlane: at step k every lane j
+// publishes its S[j][k] (column k of the trailing matrix, D_k at j = k) and lanes i > k read the column back as
+// broadcasts (ds_read_b128 pairs): ~1.5 instructions per updated entry instead of ~3.5.
+template <int CM, int K0, int K1>
+__device__ __forceinline__ void ldl_steps_lds(double (&row)[CM], int lane, bool& ok, double& rD, double* pub) {
+#pragma unroll
+  for (int k = K0; k < K1; ++k) {
+    if (lane < CM) pub[lane] = row[k];
+    KB_WAVE_SYNC();  // the other lanes' column entries: no reuse of an earlier read across this point
+    const double Dk = pub[k];
+    ok = ok && (Dk > 0.0);
+    const double rdk = recip_d(Dk);
+    rD = (lane == k) ? rdk : rD;
+    const double f = (lane > k) ? row[k] * rdk : 0.0;
+#pragma unroll
+    for (int j = k + 1; j < CM; ++j) row[j] -= f * pub[j];
+  }
+}
+
+template <int CM>
+__device__ __forceinline__ LdlOut ldl_solve_reg(const KbDev& d, const double* S, const double* bv, int C, int lane,
+                                                double* pub) {
+  // all CM + 1 loads unconditional (clamped) and materialised together: a select on a loaded value otherwise
+  // becomes one exec-masked branch (and one wait) per load
+  double row[CM];
+  const int li = lane < C ? lane : 0;
+  const int cs_i = li * (2 * C - li - 1) / 2;  // start of packed column li
+#pragma unroll
+  for (int j = 0; j < CM; ++j) {
+    const int jc = j < C ? j : 0;
+    const int cs_j = jc * (2 * C - jc - 1) / 2;  // wave-uniform
+    row[j] = S[(li >= jc) ? cs_j + li : cs_i + jc];  // lower (max, min) of (lane, j); clamped outside C
+  }
+  double x = bv[li];
+#pragma unroll
+  for (int j = 0; j < CM; ++j) KB_KEEP(row[j]);
+  KB_KEEP(x);
+#pragma unroll
+  for (int j = 0; j < CM; ++j) {
+    const bool in = lane < C && j < C;
+    row[j] = in ? row[j] : (lane == j ? 1.0 : 0.0);
+  }
+  x = lane < C ? x : 0.0;
+  bool ok = true;
+  double rD = 1.0;
+#ifdef KB_STAMPS
+  KB_KEEP(x);
+#pragma unroll
+  for (int j = 0; j < CM; ++j) KB_KEEP(row[j]);
+  if (d.dbg_stop == 45) return LdlOut{x, 1};
+#endif
+  ldl_steps_lds<CM, 0, CM>(row, lane, ok, rD, pub);
+#ifdef KB_STAMPS
+  KB_KEEP(rD);
+#pragma unroll
+  for (int j = 0; j < CM; ++j) KB_KEEP(row[j]);
+  if (d.dbg_stop == 46) return LdlOut{x, 1};
+#endif
   // Ltilde y = b ; z = D^-1 y ; Ltilde^T x = z
 #pragma unroll
   for (int k = 0; k < CM; ++k) {
@@ -1199,8 +1263,51 @@ __device__ __forceinline__ bool ldl_solve_reg(const double* S, const double* bv,
     const double wk = readlane_d(x, k);
     x -= ((lane < k) ? row[k] * rD : 0.0) * wk;
   }
-  xo = x;
-  return ok;
+  return LdlOut{x, ok ? 1 : 0};
+}
+
+// Camera block H_cc from the per-camera local sums, added to the staged S (lower entries), one wave per block
+// of H_cc (lanes = the block's entries):  intrinsics_i x intrinsics_i = Hs_i[II];
+// intrinsics_i x B_j = Hs_i[Id] K_{i,j} (j < i);  B_j x B_k = sum_{i > max(j,k)} K_{i,j}^T T_{i,k}, T = Hs_i[dd] K
+template <int CM>
+__device__ void cam_expand_blocks(double* S, int C, int N, const int (*ctab)[KB_MAX_CAMS], const double* Hs,
+                                  const double* T, const double* K, double lam2, int nw) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int nA = N, nB = N * (N - 1) / 2, nC = (N - 1) * N / 2;
+  for (int it = wave; it < nA + nB + nC; it += nw) {
+    if (it < nA) {
+      const int i = it, nin = ctab[0][i], c0 = ctab[1][i];
+      for (int e = lane; e < nin * nin; e += 64) {
+        const int x = e / nin, y = e % nin;
+        if (y <= x) S[sidx<CM>(c0 + x, c0 + y, C)] += Hs[i * 256 + (6 + x) * 16 + 6 + y] + ((x == y) ? lam2 : 0.0);
+      }
+    } else if (it < nA + nB) {
+      const int q = it - nA, i = tri_row(q) + 1, j = q - (i - 1) * i / 2;  // j < i
+      const int nin = ctab[0][i], x = lane / 6, a = lane % 6;
+      if (x < nin) {
+        const double* Kk = K + (size_t)(i * N + j) * 36;
+        double v = 0.0;
+#pragma unroll
+        for (int b = 0; b < 6; ++b) v += Hs[i * 256 + (6 + x) * 16 + b] * Kk[b * 6 + a];
+        S[sidx<CM>(ctab[2][j] + a, ctab[1][i] + x, C)] += v;  // baseline columns follow all intrinsics
+      }
+    } else {
+      const int q = it - nA - nB, k = tri_row(q), j = q - k * (k + 1) / 2;  // j <= k < N - 1
+      const int a = lane / 6, b = lane % 6;
+      if (lane < 36 && (j < k || a >= b)) {
+        double v = 0.0;
+        for (int i = k + 1; i < N; ++i) {
+          const double* Kj = K + (size_t)(i * N + j) * 36;
+          const double* Tk = T + (size_t)(i * N + k) * 36;
+#pragma unroll
+          for (int m = 0; m < 6; ++m) v += Kj[m * 6 + a] * Tk[m * 6 + b];
+        }
+        // entry (B_j a, B_k b) -> lower (B_k b, B_j a) when j < k
+        const int r = (j < k) ? ctab[2][k] + b : ctab[2][j] + a, cc = (j < k) ? ctab[2][j] + a : ctab[2][j] + b;
+        S[sidx<CM>(r, cc, C)] += v + ((j == k && a == b) ? lam2 : 0.0);
+      }
+    }
+  }
 }
 
 // Camera solve of one pass (one block): S = H_cc + lambda^2 I - sum Y^T Y, b = g_c - sum Y^T z staged in LDS,
@@ -1208,28 +1315,30 @@ __device__ __forceinline__ bool ldl_solve_reg(const double* S, const double* bv,
 // update into state[1 - cur] and the camera chains of that candidate state into slot 1 - cur.
 // Every thread of the block must call it (barriers inside).
 template <int CM>
-__device__ void solve_body(const KbDev& d, int gate, int do_update) {
+__device__ void solve_body(const KbDev& d, int gate, int do_update, int nth) {
   KbCtrl* c = d.ctrl;
   extern __shared__ __attribute__((aligned(16))) double sm[];
-  const int N = d.N, C = d.C, W = d.W, nth = blockDim.x, tid = threadIdx.x;
+  const int N = d.N, C = d.C, W = d.W, tid = threadIdx.x;
   const int Cp = C * (C + 1) / 2;
   const int nb = (C + 15) >> 4, n16 = 16 * nb;  // CM == 0: 16 x 16 tiles
   double* S = sm;                    // CM > 0: column-major packed lower [Cp]; CM == 0: lower tiles
-  double* bv = S + (CM > 0 ? Cp : 128 * nb * (nb + 1));  // [C] (+1: non-PD frame-block count while staging)
+  double* bv = S + (CM > 0 ? Cp : kTileSz * nb * (nb + 1) / 2);  // [C] (+1: non-PD frame-block count while staging)
   double* gl = bv + C + 1;           // [C]
   double* Hs = gl + C;               // [N][256]
   double* T = Hs + N * 256;          // [N][N][36]
   double* K = T + N * N * 36;        // [N][N][36]
-  double* Wsc = K + N * N * 36;      // CM == 0: [n16 - 16][16] panel scratch
-  double* rDv = Wsc + (CM > 0 ? 0 : 16 * (n16 - 16));  // CM == 0: [n16] 1/D
+  double* Wsc = K + N * N * 36;      // CM == 0: [n16 - 16][kTS] panel scratch
+  double* rDv = Wsc + (CM > 0 ? 0 : kTS * (n16 - 16));  // CM == 0: [n16] 1/D
   double* xv = rDv + (CM > 0 ? 0 : n16);               // CM == 0: [n16] right-hand side / solution
   int* ci = (int*)(xv + (CM > 0 ? 0 : n16));           // [C]
   __shared__ int okl;
   __shared__ double nbase[KB_MAX_CAMS * 7];  // candidate baselines
   __shared__ int ctab[3][KB_MAX_CAMS];       // per camera: #intrinsics | first intrinsic column | baseline column
+  __shared__ __attribute__((aligned(16))) double pubcol[CM > 0 ? CM : 1];  // LDL^T column broadcast
   const double lam = gate ? c->lambda : d.host_lambda;
   const double lam2 = lam * lam;
   const int cur = c->cur;
+  double x[2] = {0.0, 0.0};
   KB_STAMP(d, 0);
   // phase A: stage K, column info, per-camera sums and the Schur sums in LDS (one row: psum)
   solve_stage<4, CM>(d, K, Hs, S, bv, ci, tid, nth);
@@ -1257,10 +1366,7 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update) {
     d.cost_build[0] = s;
   }
   __syncthreads();
-  for (int e = tid; e < Cp; e += nth) {
-    const int j = cidx_col(e, C), i = e - j * (2 * C - j - 1) / 2;  // lower (i, j), i >= j
-    S[sidx<CM>(i, j, C)] += cam_entry_l(N, ci, Hs, T, K, i, j) + ((i == j) ? lam2 : 0.0);
-  }
+  cam_expand_blocks<CM>(S, C, N, ctab, Hs, T, K, lam2, nth >> 6);
   for (int p = tid; p < C; p += nth) {
     const double g = cam_grad_l(N, ci, Hs, K, p);
     bv[p] += g;
@@ -1270,17 +1376,22 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update) {
   }
   __syncthreads();
   KB_STAMP(d, 2);
-  double x[2] = {0.0, 0.0};
   if constexpr (CM > 0) {
+#ifdef KB_STAMPS
+    const int reps = (d.dbg_flags & 1) ? 2 : 1;  // diagnostic: factor twice (rolled: same code, warm)
+#pragma unroll 1
+    for (int rep = 0; rep < reps; ++rep)
+#endif
     if (tid < 64) {
-      const bool ok = ldl_solve_reg<CM>(S, bv, C, tid, x[0]);
-      if (!ok) okl = 0;
+      const LdlOut r = ldl_solve_reg<CM>(d, S, bv, C, tid, pubcol);
+      x[0] = r.x;
+      if (!r.ok) okl = 0;
     }
     KB_STAMP(d, 3);
     KB_STAMP(d, 4);
   } else {
     // phase C: blocked LDL^T on 16 x 16 tiles (MFMA trailing updates); phase D: blocked solves
-    ldl_tiles(S, rDv, Wsc, C, nb, &okl);
+    ldl_tiles(d, S, rDv, Wsc, C, nb, &okl);
     KB_STAMP(d, 3);
     for (int g = tid; g < n16; g += nth) xv[g] = g < C ? bv[g] : 0.0;
     __syncthreads();
@@ -1366,14 +1477,15 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update) {
   KB_STAMP(d, 5);
   if (do_update) {
     __syncthreads();
-    chain_block(d, nbase, 1 - cur);  // chains of the candidate state (k_backsub's cost, next build if accepted)
+    chain_block(d, nbase, 1 - cur, nth);  // chains of the candidate state (k_backsub's cost, next build if accepted)
   }
 }
 
+// CM > 0: 4 waves (one factors); CM == 0: 8 waves
 template <int CM>
-__global__ void __launch_bounds__(256) k_solve(KbDev d, int gate, int do_update) {
+__global__ void __launch_bounds__(CM == 0 ? 512 : 256) k_solve(KbDev d, int gate, int do_update) {
   if (gate && d.ctrl->done) return;
-  solve_body<CM>(d, gate, do_update);
+  solve_body<CM>(d, gate, do_update, blockDim.x);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1685,12 +1797,32 @@ __global__ void __launch_bounds__(256) k_reduce_cost(KbDev d) {
   }
 }
 
-// sharded runs: the policy after the all-reduce of red (accept / revert, next pass prelude)
+// red = fixed-order reduction of the all-gathered per-rank [cost, dx.dx, dx.rhs] (sum) and max|dx| (max)
+__device__ __forceinline__ void red_gather(const KbDev& d, double* red) {
+  red[0] = red[1] = red[2] = red[3] = 0.0;
+  for (int r = 0; r < d.nranks; ++r) {
+    const double* q = d.red_all + 4 * r;
+    red[0] += q[0];
+    red[1] += q[1];
+    red[2] += q[2];
+    red[3] = fmax(red[3], q[3]);
+  }
+}
+
+__global__ void k_red_gather(KbDev d) {
+  double red[4];
+  red_gather(d, red);
+  for (int q = 0; q < 4; ++q) d.red[q] = red[q];
+}
+
+// sharded runs: the policy after the all-gather of red (accept / revert, next pass prelude)
 __global__ void k_policy(KbDev d) {
   KbCtrl* c = d.ctrl;
   if (c->done) return;
+  double red[4];
+  red_gather(d, red);
   KbCtrl cl = *c;
-  pol_post(&cl, d, d.red);
+  pol_post(&cl, d, red);
   if (!cl.done) pol_pre(&cl);
   *c = cl;
 }

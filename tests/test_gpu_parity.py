@@ -174,6 +174,16 @@ def test_comm_path_single_rank_is_bitwise_identical(capi):
     rb = b.optimize()
     assert np.array_equal(a.get_state(), b.get_state())
     assert ra["iterations"] == rb["iterations"] and ra["J_final"] == rb["J_final"]
+    print("sharded path graphed:", rb["graphed"])
+    b.set_state(p.state_init)
+    rc = b.optimize(use_graph=False)  # eager RCCL path
+    assert np.array_equal(a.get_state(), b.get_state()) and rc["iterations"] == ra["iterations"]
+    # fixed-count GN passes through the sharded path == unsharded
+    a.set_state(p.state_init)
+    b.set_state(p.state_init)
+    a.run_gn(6)
+    b.run_gn(6)
+    assert np.array_equal(a.get_state(), b.get_state())
     b.set_state(p.state_init)
     b.build()
     a.set_state(p.state_init)
