@@ -198,6 +198,7 @@ kb_handle* kb_create(const kb_layout* L) {
   rc |= h->alloc(&d.psum_local, (size_t)d.Wtot);
   d.psum = d.psum_local;
   d.psum_rows = 1;
+  d.fold = 1;
   d.dbg_stop = -1;
   d.dbg_flags = 0;
   rc |= h->alloc(&d.ticket, 16);
@@ -584,9 +585,11 @@ static int enqueue_pass(kb_handle* h, int policy) {
   if (launch_colsum(h, 1, !from_rows)) return -1;
   if (launch_solve(h, 1, 1, from_rows)) return -1;
   if (launch_backsub(h, 1, 1, 1)) return -1;
-  hipLaunchKernelGGL(k_post, dim3(1), dim3(256), 0, h->stream, d, h->comm ? 0 : 1);
-  KB_HIP(hipGetLastError());
+  // one GPU: the pass end (accept / revert, next prelude) is folded into the next pass's k_build (d.fold);
+  // sharded: k_post reduces this rank's statistics, all ranks all-gather them, k_policy applies the policy
   if (h->comm) {
+    hipLaunchKernelGGL(k_post, dim3(1), dim3(256), 0, h->stream, d, 0);
+    KB_HIP(hipGetLastError());
     if (allreduce_red(h, false)) return -1;
     hipLaunchKernelGGL(k_policy, dim3(1), dim3(1), 0, h->stream, d);
     KB_HIP(hipGetLastError());
@@ -654,6 +657,13 @@ static int launch_passes(kb_handle* h, int policy, int n, bool graph) {
   return 0;
 }
 
+// the last pass's pending end (accept / revert) when the loop stops: no-op if nothing is pending
+static int finish_pass(kb_handle* h) {
+  hipLaunchKernelGGL(k_post, dim3(1), dim3(256), 0, h->stream, h->d, 1);
+  KB_HIP(hipGetLastError());
+  return 0;
+}
+
 static int loop_start(kb_handle* h, const KbOpts& o) {
   // evaluateError on the start state (Optimizer2.cpp:192-196), optimizationStarting, first prelude
   if (launch_cost(h, 0)) return -1;
@@ -685,6 +695,8 @@ int kb_optimize(kb_handle* h, const kb_optimizer_options* opts, kb_solution* out
     KB_HIP(hipStreamSynchronize(h->stream));
     if (ctrl.done) break;
   }
+  if (finish_pass(h)) return -1;
+  KB_HIP(hipMemcpy(&ctrl, h->d.ctrl, sizeof(KbCtrl), hipMemcpyDeviceToHost));
   h->cur = ctrl.cur;
   out->J_start = ctrl.J_start;
   out->J_final = ctrl.p_J;
@@ -720,6 +732,7 @@ int kb_run_gn_iterations(kb_handle* h, int32_t n_iter, double* seconds) {
   KB_HIP(hipStreamSynchronize(h->stream));
   const auto t0 = std::chrono::steady_clock::now();
   if (launch_passes(h, 1, n_iter, graph)) return -1;
+  if (finish_pass(h)) return -1;
   KB_HIP(hipStreamSynchronize(h->stream));
   const auto t1 = std::chrono::steady_clock::now();
   if (seconds) *seconds = std::chrono::duration<double>(t1 - t0).count();
@@ -802,6 +815,7 @@ int kb_comm_init(kb_handle* h, const void* uid, int32_t nranks, int32_t rank) {
   if (h->alloc(&ra, 4 * (size_t)nranks)) return -1;
   h->d.red_all = ra;
   h->d.nranks = nranks;
+  h->d.fold = 0;  // the pass end needs every rank's statistics: k_post + all-gather + k_policy
   drop_graphs(h);
   KB_HIP(hipStreamSynchronize(h->stream));
   return 0;

@@ -21,7 +21,8 @@ namespace kb {
 
 struct KbCtrl {
   int cur, done, do_build, solve_ok, first, prev_failed, lin_fail;
-  int iterations, failed_iterations, max_iterations, policy, n_trace, passes, pad_;
+  int iterations, failed_iterations, max_iterations, policy, n_trace, passes;
+  int pending;  // a pass ran its solve: its accept/revert + the next prelude are still to apply
   double J, p_J, J_start, deltaX, deltaJ, eps_x, eps_j;
   double pol_J, pol_pJ, last_succ, lambda, mu;
   double dxdx, dxrhs;
@@ -41,6 +42,7 @@ struct KbDev {
   int nsplit, wpb;   // k_build: waves per block = N * nsplit
   int W, Wtot;       // W = C(C+1)/2 + C ; Wtot = N*136 + W + 1
   int trace_cap;
+  int fold;          // 1: the next pass's k_build applies the pending policy (one GPU); 0: k_post / k_policy
   double host_lambda;  // conditioner for the per-call (non-gated) path
   int model[KB_MAX_CAMS], nintr[KB_MAX_CAMS], col_intr[KB_MAX_CAMS], col_base[KB_MAX_CAMS];
   const double* target;

@@ -214,7 +214,7 @@ __device__ void pol_pre(KbCtrl* c) {
 }
 
 // accept / revert (Optimizer2.cpp:221-259); red = [cost, dx.dx, dx.rhs, max|dx|] (all ranks)
-__device__ void pol_post(KbCtrl* c, const KbDev& d, const double* red) {
+__device__ void pol_post(KbCtrl* c, const KbDev& d, const double* red, bool write_trace = true) {
   double J = 0.0, dX = c->deltaX;
   int accepted = 0;
   if (!c->solve_ok) {
@@ -243,13 +243,99 @@ __device__ void pol_post(KbCtrl* c, const KbDev& d, const double* red) {
   }
   if (c->n_trace < d.trace_cap) {
     double* tr = d.trace + 4 * c->n_trace;
+    if (write_trace) {
     tr[0] = J;
     tr[1] = c->lambda;
     tr[2] = dX;
     tr[3] = accepted;
+    }
     c->n_trace++;
   }
   c->passes++;
+}
+
+constexpr int kPassPre = 2;  // per-frame rows per thread prefetched by k_build's first load round
+
+// ---------------------------------------------------------------------------------------------
+// the pending pass end on one GPU: fixed-order reduction of the per-frame rows [cost, max|dx|, dx.dx, dx.rhs]
+// (+ camera statistics) -> red; pol_post (accept / revert) + pol_pre (next prelude) on a register copy of ctrl.
+// Every thread of the block calls it; every block that calls it computes the same bits.  Returns the updated
+// control block in *out (LDS); block `writer` stores it (and the trace entry) to HBM.
+// ---------------------------------------------------------------------------------------------
+__device__ void pass_end_block(const KbDev& d, const KbCtrl& cin, KbCtrl* out, bool writer, int nth,
+                               bool apply_policy = true, const double4* pre = nullptr) {
+  __shared__ double sh[8][4];
+  const int tid = threadIdx.x;
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+  if (cin.solve_ok) {
+    const double4* bp = reinterpret_cast<const double4*>(d.bpart);
+    int q0 = tid;
+    if (pre) {  // the caller's first kPassPre rows of this thread, already loaded
+#pragma unroll
+      for (int u = 0; u < kPassPre; ++u)
+        if (q0 + u * nth < d.nblk_bs) {
+          s0 += pre[u].x;
+          s1 = fmax(s1, pre[u].y);
+          s2 += pre[u].z;
+          s3 += pre[u].w;
+        }
+      q0 += kPassPre * nth;
+    }
+    for (; q0 < d.nblk_bs; q0 += 4 * nth) {
+      double4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = bp[min(q0 + u * nth, d.nblk_bs - 1)];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (q0 + u * nth < d.nblk_bs) {
+          s0 += v[u].x;
+          s1 = fmax(s1, v[u].y);
+          s2 += v[u].z;
+          s3 += v[u].w;
+        }
+    }
+    s0 = wave_sum_d(s0);
+    s1 = wave_max_d(s1);
+    s2 = wave_sum_d(s2);
+    s3 = wave_sum_d(s3);
+    if ((tid & 63) == 0 && tid < nth) {
+      sh[tid >> 6][0] = s0;
+      sh[tid >> 6][1] = s1;
+      sh[tid >> 6][2] = s2;
+      sh[tid >> 6][3] = s3;
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    double red[4] = {0.0, 0.0, 0.0, 0.0};
+    if (cin.solve_ok) {
+      double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+      for (int q = 0; q < (nth >> 6); ++q) {
+        a0 += sh[q][0];
+        a1 = fmax(a1, sh[q][1]);
+        a2 += sh[q][2];
+        a3 += sh[q][3];
+      }
+      red[0] = a0;
+      red[1] = a2 + d.camstat[1];
+      red[2] = a3 + d.camstat[2];
+      red[3] = fmax(a1, d.camstat[0]);
+      if (writer)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) d.red_local[q] = red[q];
+    }
+    if (!apply_policy) goto done_tid0;
+    {
+    KbCtrl cl = cin;
+    pol_post(&cl, d, red, writer);
+    if (!cl.done) pol_pre(&cl);
+    cl.pending = 0;
+    *out = cl;
+    if (writer) *d.ctrl = cl;
+    }
+  done_tid0:;
+  }
+  __syncthreads();
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -446,7 +532,10 @@ __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
   const int f0 = blockIdx.x * d.gframes, f1 = min(d.F, f0 + d.gframes);
   const int cam = __builtin_amdgcn_readfirstlane(wave % N), sp = __builtin_amdgcn_readfirstlane(wave / N);
   // ---- round 1: launch-independent loads, unconditional (clamped) and pinned before the gate
-  const int done = c->done, dob = c->do_build, cur = c->cur;
+  __shared__ KbCtrl cnew;
+  const KbCtrl cin = *c;
+  int done = cin.done, dob = cin.do_build, cur = cin.cur;
+  double lam = gate ? cin.lambda : d.host_lambda;
   const bool tg_lds = d.K * 3 <= kTargetLds;
   const int nt3 = 3 * d.K;
   constexpr int kTgU = 2;  // 2 x 256 threads >= 3 x 120 AprilGrid corners
@@ -454,10 +543,23 @@ __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
 #pragma unroll
   for (int u = 0; u < kTgU; ++u) tv[u] = d.target[min(tid + u * nth, nt3 - 1)];
   int2 fv = d.fview[(size_t)f0 * N + cam];
+  const bool fold = gate && d.fold;
+  double4 pre[kPassPre];  // previous pass's per-frame rows (fold): loaded with this round
+#pragma unroll
+  for (int u = 0; u < kPassPre; ++u)
+    pre[u] = fold ? reinterpret_cast<const double4*>(d.bpart)[min(tid + u * nth, d.nblk_bs - 1)]
+                  : make_double4(0.0, 0.0, 0.0, 0.0);
 #pragma unroll
   for (int u = 0; u < kTgU; ++u) KB_KEEP(tv[u]);
   KB_KEEPS(fv.x);
   KB_KEEPS(fv.y);
+  if (fold && cin.pending && !cin.done) {  // previous pass's end (accept / revert, next prelude)
+    pass_end_block(d, cin, &cnew, blockIdx.x == 0, nth, true, pre);
+    done = cnew.done;
+    dob = cnew.do_build;
+    cur = cnew.cur;
+    lam = cnew.lambda;
+  }
   if (gate && (done || !dob)) return;
   // ---- round 2: loads indexed by round 1 (accepted state buffer, chains of slot cur, corners of the view)
   const double* s = d.state + (size_t)cur * d.S;
@@ -491,7 +593,6 @@ __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
     for (int q = tid + kTgU * nth; q < nt3; q += nth) tg[q] = d.target[q];
   }
   const double* tgt = tg_lds ? tg : d.target;
-  const double lam = gate ? c->lambda : d.host_lambda;
   const double lam2 = lam * lam;
   v4d acc[TW];
   int tii[TW], tjj[TW];
@@ -1485,6 +1586,7 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update, int nth) {
 template <int CM>
 __global__ void __launch_bounds__(CM == 0 ? 512 : 256) k_solve(KbDev d, int gate, int do_update) {
   if (gate && d.ctrl->done) return;
+  if (gate && threadIdx.x == 0) d.ctrl->pending = 1;
   solve_body<CM>(d, gate, do_update, blockDim.x);
 }
 
@@ -1497,62 +1599,11 @@ __global__ void __launch_bounds__(CM == 0 ? 512 : 256) k_solve(KbDev d, int gate
 // policy (accept / revert, next pass prelude); sharded runs all-reduce red first and run k_policy.
 // ---------------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_post(KbDev d, int policy) {
-  __shared__ double sh[8][4];
-  KbCtrl* c = d.ctrl;
-  if (c->done) return;
-  const int tid = threadIdx.x, nth = blockDim.x;
-  const int sok = c->solve_ok;
-  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
-  if (sok) {
-    const double4* bp = reinterpret_cast<const double4*>(d.bpart);
-    for (int q0 = tid; q0 < d.nblk_bs; q0 += 4 * nth) {
-      double4 v[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] = bp[min(q0 + u * nth, d.nblk_bs - 1)];
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-        if (q0 + u * nth < d.nblk_bs) {
-          s0 += v[u].x;
-          s1 = fmax(s1, v[u].y);
-          s2 += v[u].z;
-          s3 += v[u].w;
-        }
-    }
-    s0 = wave_sum_d(s0);
-    s1 = wave_max_d(s1);
-    s2 = wave_sum_d(s2);
-    s3 = wave_sum_d(s3);
-    if ((tid & 63) == 0) {
-      sh[tid >> 6][0] = s0;
-      sh[tid >> 6][1] = s1;
-      sh[tid >> 6][2] = s2;
-      sh[tid >> 6][3] = s3;
-    }
-  }
-  __syncthreads();
-  if (tid != 0) return;
-  double red[4] = {0.0, 0.0, 0.0, 0.0};
-  if (sok) {
-    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-    for (int q = 0; q < (nth >> 6); ++q) {
-      a0 += sh[q][0];
-      a1 = fmax(a1, sh[q][1]);
-      a2 += sh[q][2];
-      a3 += sh[q][3];
-    }
-    red[0] = a0;
-    red[1] = a2 + d.camstat[1];
-    red[2] = a3 + d.camstat[2];
-    red[3] = fmax(a1, d.camstat[0]);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) d.red_local[q] = red[q];
-  }
-  if (policy) {
-    KbCtrl cl = *c;
-    pol_post(&cl, d, red);
-    if (!cl.done) pol_pre(&cl);
-    *c = cl;
-  }
+  __shared__ KbCtrl cnew;
+  const KbCtrl cin = *d.ctrl;
+  if (cin.done) return;
+  if (policy && !cin.pending) return;  // nothing pending (already applied by a folding k_build)
+  pass_end_block(d, cin, &cnew, true, blockDim.x, policy != 0);
 }
 
 __global__ void __launch_bounds__(512) k_backsub(KbDev d, int gate, int do_update, int with_cost) {
@@ -1824,6 +1875,7 @@ __global__ void k_policy(KbDev d) {
   KbCtrl cl = *c;
   pol_post(&cl, d, red);
   if (!cl.done) pol_pre(&cl);
+  cl.pending = 0;
   *c = cl;
 }
 
@@ -1857,6 +1909,7 @@ __global__ void k_pol_init(KbDev d, KbOpts o) {
   c->solve_ok = 1;
   c->n_trace = 0;
   c->passes = 0;
+  c->pending = 0;
 }
 
 // per-call update (kb_apply_update): all DVs from state[cur] -> state[1-cur]
