@@ -75,7 +75,10 @@ struct kb_handle {
   // sharding
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
-  double* psum_red = nullptr;  // [Wtot] all-reduced column sums (sharded runs)
+  double* psum_red = nullptr;   // [Wtot] all-reduced finished column sums (sharded, per-call path)
+  double* psum_red8 = nullptr;  // [8][Wtot] all-reduced stage-1 rows (sharded optimizer loop)
+  double* bpart_all = nullptr;  // [nranks][F_max][4] all-gathered per-frame step rows (sharded)
+  int F_max = 0;
   // build-kernel timing
   double build_ms = 0.0;
 
@@ -208,6 +211,8 @@ kb_handle* kb_create(const kb_layout* L) {
   rc |= h->alloc(&d.dx, (size_t)h->ncols);
   rc |= h->alloc(&d.rhs, (size_t)h->ncols);
   rc |= h->alloc(&d.bpart, 4 * (size_t)d.nblk_bs);
+  d.bsrc = d.bpart;
+  d.bsrc_rows = d.nblk_bs;
   rc |= h->alloc(&d.camstat, 4);
   rc |= h->alloc(&d.red_local, 8);
   d.red = d.red_local;
@@ -422,12 +427,20 @@ static int allreduce_red(kb_handle* h, bool reduce = true) {
 
 // column sums of the block partials (finished in-kernel) + all-reduce over ranks when sharded
 // finish = 0 (one GPU, optimizer loop): k_solve sums the kColsumRows stage-1 rows itself
+// finish = 0 (optimizer loop): the consumer (k_solve) sums the kColsumRows stage-1 rows; sharded, those rows are
+// all-reduced as they are (one collective, no finishing kernel)
 static int launch_colsum(kb_handle* h, int gate, bool finish = true) {
   KbDev& d = h->d;
   hipLaunchKernelGGL(k_colsum, dim3((d.Wtot + 63) / 64, kColsumRows), dim3(256), 0, h->stream, d, gate);
   if (finish) hipLaunchKernelGGL(k_colfin, dim3((d.Wtot + 255) / 256), dim3(256), 0, h->stream, d, gate);
   KB_HIP(hipGetLastError());
-  if (h->comm) KB_NCCL(ncclAllReduce(d.psum_local, h->psum_red, d.Wtot, ncclDouble, ncclSum, h->comm, h->stream));
+  if (h->comm) {
+    if (finish)
+      KB_NCCL(ncclAllReduce(d.psum_local, h->psum_red, d.Wtot, ncclDouble, ncclSum, h->comm, h->stream));
+    else
+      KB_NCCL(ncclAllReduce(d.part8, h->psum_red8, (size_t)kColsumRows * d.Wtot, ncclDouble, ncclSum, h->comm,
+                            h->stream));
+  }
   return 0;
 }
 
@@ -449,8 +462,8 @@ static int launch_schur(kb_handle* h, int gate) {
 
 static int launch_solve(kb_handle* h, int gate, int do_update, bool from_rows = false) {
   KbDev d = h->d;
-  if (from_rows) {  // column sums still split in kColsumRows stage-1 rows
-    d.psum = d.part8;
+  if (from_rows) {  // column sums still split in kColsumRows stage-1 rows (all-reduced ones when sharded)
+    d.psum = h->comm ? h->psum_red8 : d.part8;
     d.psum_rows = kColsumRows;
   }
   void* args[] = {(void*)&d, (void*)&gate, (void*)&do_update};
@@ -579,21 +592,16 @@ static int enqueue_pass(kb_handle* h, int policy) {
   KbDev& d = h->d;
   if (launch_build(h, 1, 1)) return -1;
   if (policy == 0 && launch_schur(h, 1)) return -1;  // LM passes that keep the system (lambda change)
-  // one GPU and a small partial row: k_solve sums the stage-1 rows while staging (one launch less); otherwise
-  // k_colfin finishes the rows in parallel (and feeds the all-reduce when sharded)
-  const bool from_rows = !h->comm && h->d.Wtot <= 2048;
+  // small partial row (or sharded): k_solve sums the stage-1 rows while staging (one launch less); otherwise
+  // k_colfin finishes the rows in parallel
+  const bool from_rows = h->comm || h->d.Wtot <= 2048;
   if (launch_colsum(h, 1, !from_rows)) return -1;
   if (launch_solve(h, 1, 1, from_rows)) return -1;
   if (launch_backsub(h, 1, 1, 1)) return -1;
-  // one GPU: the pass end (accept / revert, next prelude) is folded into the next pass's k_build (d.fold);
-  // sharded: k_post reduces this rank's statistics, all ranks all-gather them, k_policy applies the policy
-  if (h->comm) {
-    hipLaunchKernelGGL(k_post, dim3(1), dim3(256), 0, h->stream, d, 0);
-    KB_HIP(hipGetLastError());
-    if (allreduce_red(h, false)) return -1;
-    hipLaunchKernelGGL(k_policy, dim3(1), dim3(1), 0, h->stream, d);
-    KB_HIP(hipGetLastError());
-  }
+  // the pass end (accept / revert, next prelude) is folded into the next pass's k_build; sharded, the
+  // per-frame step rows of every rank are all-gathered first and every rank reduces all of them in rank order
+  if (h->comm)
+    KB_NCCL(ncclAllGather(d.bpart, h->bpart_all, 4 * (size_t)h->F_max, ncclDouble, h->comm, h->stream));
   return 0;
 }
 
@@ -815,7 +823,20 @@ int kb_comm_init(kb_handle* h, const void* uid, int32_t nranks, int32_t rank) {
   if (h->alloc(&ra, 4 * (size_t)nranks)) return -1;
   h->d.red_all = ra;
   h->d.nranks = nranks;
-  h->d.fold = 0;  // the pass end needs every rank's statistics: k_post + all-gather + k_policy
+  // per-frame step rows: padded to the largest rank's frame count (zero rows are neutral for the sums and the
+  // max), all-gathered once per pass and reduced by every rank in rank order
+  int* fm = nullptr;
+  if (h->alloc(&fm, 1)) return -1;
+  KB_HIP(hipMemcpyAsync(fm, &h->F, sizeof(int), hipMemcpyHostToDevice, h->stream));
+  KB_NCCL(ncclAllReduce(fm, fm, 1, ncclInt32, ncclMax, h->comm, h->stream));
+  KB_HIP(hipMemcpyAsync(&h->F_max, fm, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+  KB_HIP(hipStreamSynchronize(h->stream));
+  double* bp = nullptr;
+  if (h->alloc(&bp, 4 * (size_t)h->F_max) || h->alloc(&h->bpart_all, 4 * (size_t)h->F_max * nranks)) return -1;
+  h->d.bpart = bp;
+  h->d.bsrc = h->bpart_all;
+  h->d.bsrc_rows = h->F_max * nranks;
+  if (h->alloc(&h->psum_red8, (size_t)kColsumRows * h->d.Wtot)) return -1;
   drop_graphs(h);
   KB_HIP(hipStreamSynchronize(h->stream));
   return 0;

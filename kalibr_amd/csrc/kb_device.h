@@ -68,7 +68,9 @@ struct KbDev {
   unsigned* ticket;    // [2] arrival counters: k_colsum, k_backsub (re-armed by the last block)
   double *Hcc, *gc, *cost_build;
   double *dx, *rhs;
-  double* bpart;     // [nblk_bs][4]
+  double* bpart;     // [nblk_bs][4] (sharded: padded to the largest rank's frame count, zero rows beyond F)
+  const double* bsrc;  // rows the pass end reduces: bpart (one GPU) or the all-gathered [nranks][F_max][4]
+  int bsrc_rows;
   double* camstat;   // [4]
   double* costpart;  // [nblk_cost]
   double* red_local; // [4]: cost, dx.dx, dx.rhs, max|dx|

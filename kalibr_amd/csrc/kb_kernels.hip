@@ -268,12 +268,13 @@ __device__ void pass_end_block(const KbDev& d, const KbCtrl& cin, KbCtrl* out, b
   const int tid = threadIdx.x;
   double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
   if (cin.solve_ok) {
-    const double4* bp = reinterpret_cast<const double4*>(d.bpart);
+    const double4* bp = reinterpret_cast<const double4*>(d.bsrc);
+    const int nrows = d.bsrc_rows;
     int q0 = tid;
     if (pre) {  // the caller's first kPassPre rows of this thread, already loaded
 #pragma unroll
       for (int u = 0; u < kPassPre; ++u)
-        if (q0 + u * nth < d.nblk_bs) {
+        if (q0 + u * nth < nrows) {
           s0 += pre[u].x;
           s1 = fmax(s1, pre[u].y);
           s2 += pre[u].z;
@@ -281,13 +282,13 @@ __device__ void pass_end_block(const KbDev& d, const KbCtrl& cin, KbCtrl* out, b
         }
       q0 += kPassPre * nth;
     }
-    for (; q0 < d.nblk_bs; q0 += 4 * nth) {
+    for (; q0 < nrows; q0 += 4 * nth) {
       double4 v[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] = bp[min(q0 + u * nth, d.nblk_bs - 1)];
+      for (int u = 0; u < 4; ++u) v[u] = bp[min(q0 + u * nth, nrows - 1)];
 #pragma unroll
       for (int u = 0; u < 4; ++u)
-        if (q0 + u * nth < d.nblk_bs) {
+        if (q0 + u * nth < nrows) {
           s0 += v[u].x;
           s1 = fmax(s1, v[u].y);
           s2 += v[u].z;
@@ -547,7 +548,7 @@ __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
   double4 pre[kPassPre];  // previous pass's per-frame rows (fold): loaded with this round
 #pragma unroll
   for (int u = 0; u < kPassPre; ++u)
-    pre[u] = fold ? reinterpret_cast<const double4*>(d.bpart)[min(tid + u * nth, d.nblk_bs - 1)]
+    pre[u] = fold ? reinterpret_cast<const double4*>(d.bsrc)[min(tid + u * nth, d.bsrc_rows - 1)]
                   : make_double4(0.0, 0.0, 0.0, 0.0);
 #pragma unroll
   for (int u = 0; u < kTgU; ++u) KB_KEEP(tv[u]);
@@ -1117,6 +1118,7 @@ __device__ void ldl_tiles(const KbDev& d, double* S, double* rD, double* Wsc, in
     __syncthreads();
     if (p == 0) KB_STAMP(d, 40);
     if (p == 0) KB_STAMP(d, 43);
+    if (p < 3) KB_STAMP(d, 50 + 3 * p);
     if (p == nb - 1) break;
     // rows below the panel: W = S_ip Ltilde_pp^-T (stored in Wsc), Ltilde_ip = W D^-1 (in place)
     const int nr = 16 * (nb - p - 1);
@@ -1137,6 +1139,7 @@ __device__ void ldl_tiles(const KbDev& d, double* S, double* rD, double* Wsc, in
     }
     __syncthreads();
     if (p == 0) KB_STAMP(d, 41);
+    if (p < 3) KB_STAMP(d, 51 + 3 * p);
     // trailing tiles (i, j), p < j <= i < nb: S_ij -= W_i Ltilde_j^T on MFMA (lane l: A[l&15][k], B[k][l&15])
     const int m = nb - p - 1, ntiles = m * (m + 1) / 2;
     for (int q = wave; q < ntiles; q += nw) {
@@ -1155,6 +1158,7 @@ __device__ void ldl_tiles(const KbDev& d, double* S, double* rD, double* Wsc, in
     }
     __syncthreads();
     if (p == 0) KB_STAMP(d, 42);
+    if (p < 3) KB_STAMP(d, 52 + 3 * p);
   }
 }
 
