@@ -592,9 +592,9 @@ static int enqueue_pass(kb_handle* h, int policy) {
   KbDev& d = h->d;
   if (launch_build(h, 1, 1)) return -1;
   if (policy == 0 && launch_schur(h, 1)) return -1;  // LM passes that keep the system (lambda change)
-  // small partial row (or sharded): k_solve sums the stage-1 rows while staging (one launch less); otherwise
-  // k_colfin finishes the rows in parallel
-  const bool from_rows = h->comm || h->d.Wtot <= 2048;
+  // small partial row: k_solve sums the stage-1 rows while staging (one launch less; sharded, the rows are
+  // all-reduced as they are); otherwise k_colfin finishes the rows in parallel (then one row is all-reduced)
+  const bool from_rows = h->d.Wtot <= 2048;
   if (launch_colsum(h, 1, !from_rows)) return -1;
   if (launch_solve(h, 1, 1, from_rows)) return -1;
   if (launch_backsub(h, 1, 1, 1)) return -1;

@@ -1349,7 +1349,7 @@ __device__ __forceinline__ LdlOut ldl_solve_reg(const KbDev& d, const double* S,
   for (int j = 0; j < CM; ++j) KB_KEEP(row[j]);
   if (d.dbg_stop == 45) return LdlOut{x, 1};
 #endif
-  ldl_steps_lds<CM, 0, CM>(row, lane, ok, rD, pub);
+  ldl_steps<CM, 0, CM>(row, lane, ok, rD);  // (ldl_steps_lds: same speed at CM = 24, spills at CM >= 32)
 #ifdef KB_STAMPS
   KB_KEEP(rD);
 #pragma unroll
@@ -1446,7 +1446,7 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update, int nth) {
   double x[2] = {0.0, 0.0};
   KB_STAMP(d, 0);
   // phase A: stage K, column info, per-camera sums and the Schur sums in LDS (one row: psum)
-  solve_stage<4, CM>(d, K, Hs, S, bv, ci, tid, nth);
+  solve_stage<CM == 0 ? 8 : 4, CM>(d, K, Hs, S, bv, ci, tid, nth);
   if (tid < 3 * N) ctab[tid / N][tid % N] = tid < N ? d.nintr[tid] : (tid < 2 * N ? d.col_intr[tid - N] : d.col_base[tid - 2 * N]);
   if (CM == 0)  // identity padding of the tiles beyond C (disjoint from the staged entries)
     for (int i = C; i < n16; ++i)
@@ -1496,6 +1496,12 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update, int nth) {
     KB_STAMP(d, 4);
   } else {
     // phase C: blocked LDL^T on 16 x 16 tiles (MFMA trailing updates); phase D: blocked solves
+#ifdef KB_STAMPS
+    if (d.dbg_flags & 1) {  // diagnostic: a first (throw-away) factorisation, then the timed one below
+      ldl_tiles(d, S, rDv, Wsc, C, nb, &okl);
+      KB_STAMP(d, 47);
+    }
+#endif
     ldl_tiles(d, S, rDv, Wsc, C, nb, &okl);
     KB_STAMP(d, 3);
     for (int g = tid; g < n16; g += nth) xv[g] = g < C ? bv[g] : 0.0;
