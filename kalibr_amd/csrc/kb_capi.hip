@@ -7,6 +7,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -59,6 +60,7 @@ struct kb_handle {
   int solve_threads = 64;
   int mb = 7, ms = 7;  // Schur-sum tiles per wave of k_build / k_schur (template bucket)
   const void* fn_build = nullptr;
+  const void* fn_build_gn = nullptr;  // GN fused passes
   const void* fn_schur = nullptr;
   const void* fn_solve = nullptr;
   int cur = 0;  // host mirror of ctrl->cur for the per-call path
@@ -78,6 +80,7 @@ struct kb_handle {
   double* psum_red = nullptr;   // [Wtot] all-reduced finished column sums (sharded, per-call path)
   double* psum_red8 = nullptr;  // [8][Wtot] all-reduced stage-1 rows (sharded optimizer loop)
   double* bpart_all = nullptr;  // [nranks][F_max][4] all-gathered per-frame step rows (sharded)
+  bool gn_fuse = true;          // GN passes fused (KB_GN_FUSED=0: the general pass, for comparison)
   int F_max = 0;
   // build-kernel timing
   double build_ms = 0.0;
@@ -177,7 +180,10 @@ kb_handle* kb_create(const kb_layout* L) {
   d.wpb = h->N * d.nsplit;
   h->WPB = d.wpb;
   d.W = h->W;
-  d.Wtot = h->N * 136 + h->W + 1;
+  d.Wp = h->N * 136 + h->W + 1;
+  d.Wtot = d.Wp + 1;  // + per-rank max|dx_f| column(s); kb_comm_init widens it to nranks
+  d.nranks = 1;
+  d.rank = 0;
   if (64 * d.wpb > 512) {
     fail("kb_create: camera block / rig too large for the build kernel");
     delete h;
@@ -196,15 +202,17 @@ kb_handle* kb_create(const kb_layout* L) {
   rc |= h->alloc(&d.Lf, 36 * (size_t)h->F);
   rc |= h->alloc(&d.Yf, 6 * (size_t)h->C * h->F);
   rc |= h->alloc(&d.zf, 6 * (size_t)h->F);
-  rc |= h->alloc(&d.part, (size_t)d.nblk * d.Wtot);
+  rc |= h->alloc(&d.part, (size_t)d.nblk * d.Wp);
   rc |= h->alloc(&d.part8, (size_t)kColsumRows * d.Wtot);
   rc |= h->alloc(&d.psum_local, (size_t)d.Wtot);
   d.psum = d.psum_local;
   d.psum_rows = 1;
   d.fold = 1;
+  if (const char* e = std::getenv("KB_GN_FUSED")) h->gn_fuse = std::atoi(e) != 0;
   d.dbg_stop = -1;
   d.dbg_flags = 0;
   rc |= h->alloc(&d.ticket, 16);
+  rc |= h->alloc(&d.dxmax, (size_t)kDxSlots * kDxStride);
   rc |= h->alloc(&d.Hcc, (size_t)h->C * h->C);
   rc |= h->alloc(&d.gc, (size_t)h->C);
   rc |= h->alloc(&d.cost_build, 2);
@@ -272,10 +280,14 @@ kb_handle* kb_create(const kb_layout* L) {
     const int tb = (ntiles + d.wpb - 1) / d.wpb, ts = (ntiles + 3) / 4;
     h->mb = tb <= 1 ? 1 : tb <= 4 ? 4 : 7;
     h->ms = ts <= 1 ? 1 : ts <= 4 ? 4 : 7;
-    h->fn_build = h->mb == 1 ? (const void*)k_build<1> : h->mb == 4 ? (const void*)k_build<4> : (const void*)k_build<7>;
+    h->fn_build = h->mb == 1 ? (const void*)k_build<1, false> : h->mb == 4 ? (const void*)k_build<4, false>
+                                                                       : (const void*)k_build<7, false>;
+    h->fn_build_gn = h->mb == 1 ? (const void*)k_build<1, true> : h->mb == 4 ? (const void*)k_build<4, true>
+                                                                          : (const void*)k_build<7, true>;
     h->fn_schur = h->ms == 1 ? (const void*)k_schur<1> : h->ms == 4 ? (const void*)k_schur<4> : (const void*)k_schur<7>;
   }
   hipFuncSetAttribute(h->fn_build, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_build);
+  hipFuncSetAttribute(h->fn_build_gn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_build);
   hipFuncSetAttribute((const void*)k_camexpand, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_camexp);
   hipFuncSetAttribute(h->fn_schur, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_schur);
   hipFuncSetAttribute(h->fn_solve, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_solve);
@@ -449,7 +461,8 @@ static int launch_build(kb_handle* h, int gate, int fuse) {
   // per-call path: camera chains first; in the loop k_solve (or the loop start) computed them
   if (!gate) hipLaunchKernelGGL(k_pre, dim3(1), dim3(256), 0, h->stream, d, 0);
   void* args[] = {&d, &gate, &fuse};
-  KB_HIP(hipLaunchKernel(h->fn_build, dim3(d.nblk), dim3(64 * d.wpb), args, h->lds_build, h->stream));
+  KB_HIP(hipLaunchKernel(d.gn_fused ? h->fn_build_gn : h->fn_build, dim3(d.nblk), dim3(64 * d.wpb), args,
+                         h->lds_build, h->stream));
   return 0;
 }
 
@@ -588,13 +601,36 @@ int kb_get_normal_blocks(kb_handle* h, double* Hff, double* Hfc, double* gf, dou
 // One optimizer pass: build (+ fused Schur) | [schur, LM passes that keep the system] | colsum [all-reduce] |
 // solve (+ candidate camera chains) | backsub + cost, its last block: reduce, accept/revert, next prelude
 // ([all-reduce + k_policy] when sharded).  Every kernel early-exits once ctrl->done is set.
+// GN fused passes: [frame steps of the previous solve + build at that candidate] | colsum | [previous pass's
+// end + solve]; the back-substitution and cost kernels drop out (the build's chi^2 is the candidate's cost).
+// The launches see a KbDev with gn_fused set for the scope.
+struct GnFusedScope {
+  kb_handle* h;
+  KbDev saved;
+  GnFusedScope(kb_handle* hh, bool on) : h(hh), saved(hh->d) {
+    if (on) {
+      h->d.gn_fused = 1;
+      h->d.fold = 0;
+    }
+  }
+  ~GnFusedScope() { h->d = saved; }
+};
+
+static bool gn_fused(const kb_handle* h, int policy) { return policy == 1 && h->gn_fuse; }
+
 static int enqueue_pass(kb_handle* h, int policy) {
   KbDev& d = h->d;
+  if (gn_fused(h, policy)) {
+    GnFusedScope scope(h, true);
+    const bool from_rows = h->d.Wp <= 2048;
+    if (launch_build(h, 1, 1) || launch_colsum(h, 1, !from_rows) || launch_solve(h, 1, 1, from_rows)) return -1;
+    return 0;
+  }
   if (launch_build(h, 1, 1)) return -1;
   if (policy == 0 && launch_schur(h, 1)) return -1;  // LM passes that keep the system (lambda change)
   // small partial row: k_solve sums the stage-1 rows while staging (one launch less; sharded, the rows are
   // all-reduced as they are); otherwise k_colfin finishes the rows in parallel (then one row is all-reduced)
-  const bool from_rows = h->d.Wtot <= 2048;
+  const bool from_rows = h->d.Wp <= 2048;
   if (launch_colsum(h, 1, !from_rows)) return -1;
   if (launch_solve(h, 1, 1, from_rows)) return -1;
   if (launch_backsub(h, 1, 1, 1)) return -1;
@@ -666,7 +702,13 @@ static int launch_passes(kb_handle* h, int policy, int n, bool graph) {
 }
 
 // the last pass's pending end (accept / revert) when the loop stops: no-op if nothing is pending
-static int finish_pass(kb_handle* h) {
+static int finish_pass(kb_handle* h, int policy) {
+  if (gn_fused(h, policy)) {  // the last solve's step: back-substitution + cost, then its end as usual
+    GnFusedScope scope(h, true);
+    if (launch_backsub(h, 1, 1, 1)) return -1;
+    if (h->comm)
+      KB_NCCL(ncclAllGather(h->d.bpart, h->bpart_all, 4 * (size_t)h->F_max, ncclDouble, h->comm, h->stream));
+  }
   hipLaunchKernelGGL(k_post, dim3(1), dim3(256), 0, h->stream, h->d, 1);
   KB_HIP(hipGetLastError());
   return 0;
@@ -703,7 +745,7 @@ int kb_optimize(kb_handle* h, const kb_optimizer_options* opts, kb_solution* out
     KB_HIP(hipStreamSynchronize(h->stream));
     if (ctrl.done) break;
   }
-  if (finish_pass(h)) return -1;
+  if (finish_pass(h, opts->policy)) return -1;
   KB_HIP(hipMemcpy(&ctrl, h->d.ctrl, sizeof(KbCtrl), hipMemcpyDeviceToHost));
   h->cur = ctrl.cur;
   out->J_start = ctrl.J_start;
@@ -740,7 +782,7 @@ int kb_run_gn_iterations(kb_handle* h, int32_t n_iter, double* seconds) {
   KB_HIP(hipStreamSynchronize(h->stream));
   const auto t0 = std::chrono::steady_clock::now();
   if (launch_passes(h, 1, n_iter, graph)) return -1;
-  if (finish_pass(h)) return -1;
+  if (finish_pass(h, 1)) return -1;
   KB_HIP(hipStreamSynchronize(h->stream));
   const auto t1 = std::chrono::steady_clock::now();
   if (seconds) *seconds = std::chrono::duration<double>(t1 - t0).count();
@@ -784,7 +826,7 @@ int kb_build_kernel_stats(kb_handle* h, double* avg_ms, double* bytes_per_launch
   // and the per-block partial rows written.
   const double bytes = 18.0 * h->NC + 8.0 * h->F * h->N + 8.0 * h->S + 8.0 * (12.0 * h->N + 36.0 * h->N * h->N) +
                        8.0 * h->F * (36 + 6 + 6.0 * h->C) + 8.0 * h->F * (36 + 6 + 6.0 * h->C) +
-                       8.0 * h->d.nblk * h->d.Wtot;
+                       8.0 * h->d.nblk * h->d.Wp;
   if (bytes_per_launch) *bytes_per_launch = bytes;
   // executed MFMA flops (2 x 16 x 16 x rows, rows padded to 64 per 32-corner phase) + ~300 VALU flops/corner
   double rows = 0.0;
@@ -813,6 +855,12 @@ int kb_comm_init(kb_handle* h, const void* uid, int32_t nranks, int32_t rank) {
   KB_NCCL(ncclCommInitRank(&h->comm, nranks, id, rank));
   h->nranks = nranks;
   h->rank = rank;
+  h->d.rank = rank;
+  // column sums widened by one max|dx_f| column per rank (GN fused passes); the one-rank buffers stay allocated
+  // until kb_destroy
+  h->d.Wtot = h->d.Wp + nranks;
+  if (h->alloc(&h->d.part8, (size_t)kColsumRows * h->d.Wtot) || h->alloc(&h->d.psum_local, (size_t)h->d.Wtot))
+    return -1;
   if (h->alloc(&h->psum_red, (size_t)h->d.Wtot)) return -1;
   double* rr = nullptr;
   if (h->alloc(&rr, 8)) return -1;
@@ -844,7 +892,7 @@ int kb_comm_init(kb_handle* h, const void* uid, int32_t nranks, int32_t rank) {
 
 #ifdef KB_STAMPS
 // diagnostic build only: average duration (us, HIP events over `reps` launches) of one kernel of the GN pass run
-// up to stop point `stop` (KB_STAMP): which = 0 fused build, 1 camera solve, 2 back-substitution.
+// up to stop point `stop` (KB_STAMP): which = 0 fused build, 1 camera solve, 2 back-substitution, 3 GN fused build.
 int kb_diag_phase_time(kb_handle* h, int which, int stop, int reps, int flags, double* us) {
   KB_HIP(hipSetDevice(h->device));
   KbOpts o{1, 0x3fffffff, 0.0, -1.0, -1.0};
@@ -866,6 +914,12 @@ int kb_diag_phase_time(kb_handle* h, int which, int stop, int reps, int flags, d
     if (which == 0) {
       void* args[] = {&d, &g, &one};
       KB_HIP(hipLaunchKernel(h->fn_build, dim3(d.nblk), dim3(64 * d.wpb), args, h->lds_build, h->stream));
+    } else if (which == 3) {  // GN fused build (gated: applies the pending frame steps each launch)
+      KbDev dg = d;
+      dg.gn_fused = 1;
+      dg.fold = 0;
+      void* args[] = {&dg, &one, &one};
+      KB_HIP(hipLaunchKernel(h->fn_build_gn, dim3(d.nblk), dim3(64 * d.wpb), args, h->lds_build, h->stream));
     } else if (which == 1) {
       void* args[] = {&d, &g, &zero};
       KB_HIP(hipLaunchKernel(h->fn_solve, dim3(1), dim3(h->solve_threads), args, h->lds_solve, h->stream));

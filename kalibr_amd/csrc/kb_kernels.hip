@@ -32,6 +32,15 @@ typedef double v4d __attribute__((ext_vector_type(4)));
 #define KB_KEEPS(x) asm volatile("" ::"s"(x))
 
 // broadcast of a double from a wave-uniform lane (v_readlane_b32 x2, no LDS round trip)
+// per-camera kernel-argument arrays read at a run-time index by selects: a dynamically indexed kernel argument
+// would make the compiler copy the whole KbDev into scratch (private memory), which costs every launch
+__device__ __forceinline__ int cam_arg(const int (&a)[KB_MAX_CAMS], int i) {
+  int v = a[0];
+#pragma unroll
+  for (int k = 1; k < KB_MAX_CAMS; ++k) v = (i == k) ? a[k] : v;
+  return v;
+}
+
 __device__ __forceinline__ double readlane_d(double v, int lane) {
   const unsigned long long b = __double_as_longlong(v);
   const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffull), lane);
@@ -161,7 +170,8 @@ __device__ __forceinline__ double chain_entry(const double* R, const double* tq,
 // (TrustRegionPolicy.cpp:39-52) + LM lambda schedule (LevenbergMarquardtTrustRegionPolicy.cpp:50-84)
 // or GN (build every pass, no conditioner: GaussNewtonTrustRegionPolicy.cpp:25-29).
 // ---------------------------------------------------------------------------------------------
-__device__ void pol_pre(KbCtrl* c) {
+template <bool GN_ONLY = false>
+__device__ __forceinline__ void pol_pre(KbCtrl* c) {
   const bool cont = c->iterations < c->max_iterations && c->failed_iterations < c->max_iterations &&
                     ((c->deltaX > c->eps_x && fabs(c->deltaJ) > c->eps_j) || c->lin_fail);
   if (!cont) {
@@ -177,7 +187,7 @@ __device__ void pol_pre(KbCtrl* c) {
     c->pol_J = J;
   }
   c->solve_ok = 1;
-  if (c->policy == 0) {
+  if (!GN_ONLY && c->policy == 0) {
     if (c->first) {
       c->do_build = 1;
     } else {
@@ -214,7 +224,7 @@ __device__ void pol_pre(KbCtrl* c) {
 }
 
 // accept / revert (Optimizer2.cpp:221-259); red = [cost, dx.dx, dx.rhs, max|dx|] (all ranks)
-__device__ void pol_post(KbCtrl* c, const KbDev& d, const double* red, bool write_trace = true) {
+__device__ __forceinline__ void pol_post(KbCtrl* c, const KbDev& d, const double* red, bool write_trace = true) {
   double J = 0.0, dX = c->deltaX;
   int accepted = 0;
   if (!c->solve_ok) {
@@ -331,6 +341,7 @@ __device__ void pass_end_block(const KbDev& d, const KbCtrl& cin, KbCtrl* out, b
     pol_post(&cl, d, red, writer);
     if (!cl.done) pol_pre(&cl);
     cl.pending = 0;
+    cl.have_dx = 0;
     *out = cl;
     if (writer) *d.ctrl = cl;
     }
@@ -500,10 +511,66 @@ __device__ __forceinline__ void schur_forward(const KbDev& d, int f, const doubl
   }
 }
 
+// GN fused passes: dx_f = L_f^-T (z_f - Y_f dx_c) of the previous solve, computed by every wave of the frame's
+// build block (k_backsub's arithmetic in the same order).  Loads: lane slot sl holds column lane + 64 sl of Y_f;
+// lanes 0..5 / 0..35 hold z_f / L_f (broadcast with v_readlane).
+__device__ __forceinline__ void fdx_load(const KbDev& d, int f, int lane, double (&yr)[6][2], double& zq,
+                                         double& lq) {
+  const int C = d.C;
+#pragma unroll
+  for (int sl = 0; sl < 2; ++sl) {
+    const int q = lane + 64 * sl, qc = min(q, C - 1);
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+      const double v = d.Yf[((size_t)f * 6 + r) * C + qc];
+      yr[r][sl] = q < C ? v : 0.0;
+    }
+  }
+  zq = d.zf[(size_t)f * 6 + min(lane, 5)];
+  lq = d.Lf[(size_t)f * 36 + min(lane, 35)];
+}
+
+__device__ __forceinline__ void fdx_solve(const double (&yr)[6][2], const double* dxv, double zq, double lq,
+                                          double* w) {
+#pragma unroll
+  for (int r = 0; r < 6; ++r) {
+    double s = yr[r][0] * dxv[0] + yr[r][1] * dxv[1];
+    s = wave_sum_d(s);
+    w[r] = readlane_d(zq, r) - s;
+  }
+#pragma unroll
+  for (int r = 5; r >= 0; --r) {
+    double s = w[r];
+#pragma unroll
+    for (int k = r + 1; k < 6; ++k) s -= readlane_d(lq, k * 6 + r) * w[k];
+    w[r] = s / readlane_d(lq, r * 6 + r);
+  }
+}
+
+// pose of frame f moved by its step (in place), stored to the candidate buffer by wave 0; wmax = max |dx_f|
+__device__ __forceinline__ void frame_step(const KbDev& d, int f, int wave, int lane, const double (&yr)[6][2],
+                                           const double* dxv, double zq, double lq, double* fp, double* snew,
+                                           double& wmax) {
+  double w[6], np[7];
+  fdx_solve(yr, dxv, zq, lq, w);
+  update_pose(fp, w, np);
+#pragma unroll
+  for (int q = 0; q < 7; ++q) fp[q] = np[q];
+#pragma unroll
+  for (int r = 0; r < 6; ++r) wmax = fmax(wmax, fabs(w[r]));
+  if (wave == 0 && lane < 7) {
+    double pv = np[0];
+#pragma unroll
+    for (int q = 1; q < 7; ++q) pv = (lane == q) ? np[q] : pv;
+    snew[d.off_frame + 7 * f + lane] = pv;
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // k_build: one block = a group of frames; waves = N * nsplit, wave w -> camera w % N, corner split w / N.
 // ---------------------------------------------------------------------------------------------
-template <int TW>
+// GNF: Gauss-Newton fused variant (applies the previous solve's frame steps; no folded pass end)
+template <int TW, bool GNF>
 __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
   KbCtrl* c = d.ctrl;
   extern __shared__ __attribute__((aligned(16))) double sm[];
@@ -544,7 +611,7 @@ __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
 #pragma unroll
   for (int u = 0; u < kTgU; ++u) tv[u] = d.target[min(tid + u * nth, nt3 - 1)];
   int2 fv = d.fview[(size_t)f0 * N + cam];
-  const bool fold = gate && d.fold;
+  const bool fold = !GNF && gate && d.fold;
   double4 pre[kPassPre];  // previous pass's per-frame rows (fold): loaded with this round
 #pragma unroll
   for (int u = 0; u < kPassPre; ++u)
@@ -554,6 +621,26 @@ __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
   for (int u = 0; u < kTgU; ++u) KB_KEEP(tv[u]);
   KB_KEEPS(fv.x);
   KB_KEEPS(fv.y);
+  // GN fused passes: the previous solve's frame steps are applied here (back-substitution of frame f0)
+  const bool gfu = GNF && gate;
+  double yr[6][2], dxv[2] = {0.0, 0.0}, zq = 0.0, lq = 0.0;
+  if (gfu) {
+#pragma unroll
+    for (int sl = 0; sl < 2; ++sl) {
+      const int q = lane + 64 * sl;
+      const double v = d.dx[min(q, C - 1)];
+      dxv[sl] = q < C ? v : 0.0;
+    }
+    fdx_load(d, f0, lane, yr, zq, lq);
+#pragma unroll
+    for (int sl = 0; sl < 2; ++sl) {
+      KB_KEEP(dxv[sl]);
+#pragma unroll
+      for (int r = 0; r < 6; ++r) KB_KEEP(yr[r][sl]);
+    }
+    KB_KEEP(zq);
+    KB_KEEP(lq);
+  }
   if (fold && cin.pending && !cin.done) {  // previous pass's end (accept / revert, next prelude)
     pass_end_block(d, cin, &cnew, blockIdx.x == 0, nth, true, pre);
     done = cnew.done;
@@ -562,16 +649,25 @@ __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
     lam = cnew.lambda;
   }
   if (gate && (done || !dob)) return;
-  // ---- round 2: loads indexed by round 1 (accepted state buffer, chains of slot cur, corners of the view)
-  const double* s = d.state + (size_t)cur * d.S;
+  // GN fused with a pending step: build at the candidate state (buffer / chain slot 1 - cur: cameras updated by
+  // the previous k_solve, frames updated below from the accepted poses of buffer cur)
+  const bool upd = gfu && cin.have_dx;
+  const int bs = upd ? 1 - cur : cur;
+  // ---- round 2: loads indexed by round 1 (state buffer, chains of slot bs, corners of the view)
+  const double* s = d.state + (size_t)bs * d.S;
+  const double* sf = d.state + (size_t)cur * d.S;  // frame poses (the step is applied on top when upd)
+  double* snew = d.state + (size_t)(1 - cur) * d.S;
   if (tid < N * 22) {
     const int cm = tid / 22, e = tid % 22;
-    cst[cm][e] = e < 12 ? cam_L(d, cur)[cm * 12 + e] : s[cm * KB_MAX_INTR + e - 12];
+    cst[cm][e] = e < 12 ? cam_L(d, bs)[cm * 12 + e] : s[cm * KB_MAX_INTR + e - 12];
   }
-  if (tid < 2 * N) ctab[tid / N][tid % N] = (tid < N) ? d.col_intr[tid] : d.col_base[tid - N];
+  if (tid < 2 * N) ctab[tid / N][tid % N] = (tid < N) ? cam_arg(d.col_intr, tid) : cam_arg(d.col_base, tid - N);
   double fp0[7];  // pose of the block's first frame
 #pragma unroll
-  for (int q = 0; q < 7; ++q) fp0[q] = s[d.off_frame + 7 * f0 + q];
+  for (int q = 0; q < 7; ++q) fp0[q] = sf[d.off_frame + 7 * f0 + q];
+  double wmax = 0.0;  // GN fused: max |dx_f| over the block's frames
+  if (upd) frame_step(d, f0, wave, lane, yr, dxv, zq, lq, fp0, snew, wmax);  // frame f0 (its loads in round 1)
+  KB_STAMP(d, 14);
   int cidn;
   double2 yn;
   {
@@ -579,7 +675,7 @@ __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
     cidn = d.cid[k];
     yn = d.y[k];
   }
-  const double* Kc = cam_K(d, cur);
+  const double* Kc = cam_K(d, bs);
   for (int q = tid; q < 18 * N * (N - 1); q += nth) {
     const int e = q % 36, ij = q / 36;
     int i = 1;
@@ -608,13 +704,18 @@ __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
   __syncthreads();
 
   const int mrow = lane >> 4, mcol = lane & 15;
-  const int model = d.model[cam], nin = d.nintr[cam];
+  const int model = cam_arg(d.model, cam), nin = cam_arg(d.nintr, cam);
   const double* Lc = cst[cam];
   const double* intr = cst[cam] + 12;
   for (int f = f0; f < f1; ++f) {
     double fp[7];
 #pragma unroll
-    for (int q = 0; q < 7; ++q) fp[q] = (f == f0) ? fp0[q] : s[d.off_frame + 7 * f + q];
+    for (int q = 0; q < 7; ++q) fp[q] = (f == f0) ? fp0[q] : sf[d.off_frame + 7 * f + q];
+    if (upd && f > f0) {  // wave-uniform: next frame of a multi-frame block
+      double yf[6][2], zf, lf;
+      fdx_load(d, f, lane, yf, zf, lf);
+      frame_step(d, f, wave, lane, yf, dxv, zf, lf, fp, snew, wmax);
+    }
     double Ri[9], ti[3], R[9], t[3];
     pose_inverse(fp, Ri, ti);
     rt_mul(Lc, Lc + 9, Ri, ti, R, t);  // T_cam_w = L_cam T_f^-1 (chain of the accepted state)
@@ -722,7 +823,7 @@ __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
     if (wave < N) {  // expansion of view (f, cam = wave) through the 6-D chains
       const int vc = __builtin_amdgcn_readfirstlane(wave);
       const bool has = fv.y > fv.x;  // this wave's camera == vc
-      const int nv = d.nintr[vc];
+      const int nv = cam_arg(d.nintr, vc);
       const double* H = Hv + vc * 256;
       double* wv = Wv + vc * 64;
       double* G = wv + 16;
@@ -804,7 +905,7 @@ __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
     __syncthreads();
     KB_STAMP(d, 24);
   }
-  double* prow = d.part + (size_t)blockIdx.x * d.Wtot;
+  double* prow = d.part + (size_t)blockIdx.x * d.Wp;
   for (int q = threadIdx.x; q < N * 136; q += nth) {
     const int qc = q / 136;
     int a, b;
@@ -815,6 +916,8 @@ __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
     schur_tiles_store<TW>(prow + N * 136, C, tii, tjj, acc);
     if (threadIdx.x == 0) prow[N * 136 + W] = okl ? 0.0 : 1.0;  // non-PD frame blocks (summed)
   }
+  if (upd && threadIdx.x == 0)
+    atomicMax(d.dxmax + (blockIdx.x % kDxSlots) * kDxStride, (unsigned long long)__double_as_longlong(wmax));
   KB_STAMP(d, 25);
 }
 
@@ -854,7 +957,7 @@ __global__ void __launch_bounds__(256) k_schur(KbDev d, int gate) {
     __syncthreads();
     schur_tiles_accumulate<TW>(Y, CZ, tii, tjj, acc);
   }
-  double* prow = d.part + (size_t)blockIdx.x * d.Wtot + N * 136;
+  double* prow = d.part + (size_t)blockIdx.x * d.Wp + N * 136;
   schur_tiles_store<TW>(prow, C, tii, tjj, acc);
   __syncthreads();
   if (threadIdx.x == 0) prow[W] = okl ? 0.0 : 1.0;
@@ -871,19 +974,29 @@ __global__ void __launch_bounds__(256) k_colsum(KbDev d, int gate) {
   __shared__ double part[4][64];
   const int l = threadIdx.x & 63, w4 = threadIdx.x >> 6;
   const int e = blockIdx.x * 64 + l, ry = blockIdx.y;
-  const int ec = min(e, d.Wtot - 1);
+  const int ec = min(e, d.Wp - 1);
   double s = 0.0;
   constexpr int U = 16, step = 4 * kColsumRows;
   for (int b0 = ry + kColsumRows * w4; b0 < d.nblk; b0 += U * step) {
     double v[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) v[u] = d.part[(size_t)min(b0 + u * step, d.nblk - 1) * d.Wtot + ec];
+    for (int u = 0; u < U; ++u) v[u] = d.part[(size_t)min(b0 + u * step, d.nblk - 1) * d.Wp + ec];
 #pragma unroll
     for (int u = 0; u < U; ++u) s += (b0 + u * step < d.nblk) ? v[u] : 0.0;
   }
   part[w4][l] = s;
+  double dm = 0.0;  // max|dx_f| of this rank (GN fused passes): max over the atomic slots, by wave 0
+  if (d.gn_fused && ry == 0 && w4 == 0 && blockIdx.x == (d.Wp + d.rank) / 64) {  // wave-uniform
+    dm = __longlong_as_double((long long)d.dxmax[l * kDxStride]);
+    dm = wave_max_d(dm);
+  }
   __syncthreads();
-  if (w4 == 0 && e < d.Wtot) d.part8[(size_t)ry * d.Wtot + e] = ((part[0][l] + part[1][l]) + part[2][l]) + part[3][l];
+  if (w4 == 0 && e < d.Wtot) {
+    double v = ((part[0][l] + part[1][l]) + part[2][l]) + part[3][l];
+    if (e >= d.Wp)  // max|dx_f| column of each rank: this rank's value in row 0 (GN fused passes), zero elsewhere
+      v = (ry == 0 && d.gn_fused && e - d.Wp == d.rank) ? dm : 0.0;
+    d.part8[(size_t)ry * d.Wtot + e] = v;
+  }
 }
 
 // psum_local[e] = sum_r part8[r][e] (fixed order)
@@ -1225,12 +1338,12 @@ __device__ void ldl_tiles_solve(const double* S, const double* rD, double* xv, i
 // (a runtime-bounded copy loop would otherwise wait for each load before the next).  Items are laid out as
 // [camK N*N*36 | per-camera sums N*256 | Schur sums Wt | Schur rhs C | colinfo C] over one index space.
 template <int U, int CM>
-__device__ __forceinline__ void solve_stage(const KbDev& d, double* K, double* Hs, double* S, double* bv, int* ci,
-                                            int tid, int nth) {
+__device__ __forceinline__ void solve_stage(const KbDev& d, int bslot, double* K, double* Hs, double* S, double* bv,
+                                            int* ci, int tid, int nth) {
   const int N = d.N, C = d.C, Wt = d.W - C;
   // [camK N*N*36 | per-camera upper sums N*136 | Schur sums Wt + rhs C + non-PD count 1 | colinfo C]
   const int n0 = N * N * 36, n1 = n0 + N * 136, n2 = n1 + Wt, n3 = n2 + C + 1, n4 = n3 + C;
-  const double* Kc = cam_K(d, d.ctrl->cur);
+  const double* Kc = cam_K(d, bslot);  // chains of the state the system was built at
   for (int q0 = tid; q0 < n4; q0 += U * nth) {
     double v[U];
 #pragma unroll
@@ -1440,14 +1553,27 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update, int nth) {
   __shared__ double nbase[KB_MAX_CAMS * 7];  // candidate baselines
   __shared__ int ctab[3][KB_MAX_CAMS];       // per camera: #intrinsics | first intrinsic column | baseline column
   __shared__ __attribute__((aligned(16))) double pubcol[CM > 0 ? CM : 1];  // LDL^T column broadcast
+  __shared__ int fin[2];  // GN fused: done, cur after the previous pass's end
+  __shared__ KbCtrl cls;
+  __shared__ double cl_red[4];
   const double lam = gate ? c->lambda : d.host_lambda;
   const double lam2 = lam * lam;
-  const int cur = c->cur;
+  int cur = c->cur;
+  const bool gfu = gate && d.gn_fused;
+  // GN fused: a pending step means the system was built at the candidate state (slot 1 - cur)
+  const int bslot = (gfu && c->have_dx) ? 1 - cur : cur;
   double x[2] = {0.0, 0.0};
+  double dxr = 0.0;  // GN fused: max|dx_f| of the previous step, one column per rank
+  if (gfu && tid < 64) {
+    d.dxmax[tid * kDxStride] = 0ull;  // read by k_colsum already; armed for the next build
+    const int nr = d.Wtot - d.Wp;
+    dxr = psum_at(d, d.Wp + min(tid, nr - 1));
+    for (int r = tid + 64; r < nr; r += 64) dxr = fmax(dxr, psum_at(d, d.Wp + r));
+  }
   KB_STAMP(d, 0);
   // phase A: stage K, column info, per-camera sums and the Schur sums in LDS (one row: psum)
-  solve_stage<CM == 0 ? 8 : 4, CM>(d, K, Hs, S, bv, ci, tid, nth);
-  if (tid < 3 * N) ctab[tid / N][tid % N] = tid < N ? d.nintr[tid] : (tid < 2 * N ? d.col_intr[tid - N] : d.col_base[tid - 2 * N]);
+  solve_stage<CM == 0 ? 8 : 4, CM>(d, bslot, K, Hs, S, bv, ci, tid, nth);
+  if (tid < 3 * N) ctab[tid / N][tid % N] = tid < N ? cam_arg(d.nintr, tid) : (tid < 2 * N ? cam_arg(d.col_intr, tid - N) : cam_arg(d.col_base, tid - 2 * N));
   if (CM == 0)  // identity padding of the tiles beyond C (disjoint from the staged entries)
     for (int i = C; i < n16; ++i)
       for (int j = tid; j <= i; j += nth) S[tidx(i, j)] = (i == j) ? 1.0 : 0.0;
@@ -1465,12 +1591,35 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update, int nth) {
     }
     T[q] = s;
   }
+  if (gfu && tid < 64) dxr = wave_max_d(dxr);
   if (tid == 0) {
     double s = 0.0;
     for (int i = 0; i < N; ++i) s += Hs[i * 256 + 255];
     d.cost_build[0] = s;
+    if (gfu) {
+      // GN fused: the previous pass's end.  Its cost is this build's (the system was built at its candidate):
+      // accept (GN always does) and the next prelude (Optimizer2.cpp:221-259, TrustRegionPolicy.cpp:39-52)
+      KbCtrl& cl = cls;  // LDS copy (a private one would put the kernel arguments in scratch)
+      cl = *c;
+      if (cl.have_dx) {
+        cl_red[0] = s;
+        cl_red[1] = cl_red[2] = 0.0;
+        cl_red[3] = fmax(dxr, d.camstat[0]);
+        pol_post(&cl, d, cl_red);
+        if (!cl.done) pol_pre<true>(&cl);
+        cl.have_dx = 0;
+        cl.pending = 0;
+        *c = cl;
+      }
+      fin[0] = cl.done;
+      fin[1] = cl.cur;
+    }
   }
   __syncthreads();
+  if (gfu) {
+    if (fin[0]) return;
+    cur = fin[1];
+  }
   cam_expand_blocks<CM>(S, C, N, ctab, Hs, T, K, lam2, nth >> 6);
   for (int p = tid; p < C; p += nth) {
     const double g = cam_grad_l(N, ci, Hs, K, p);
@@ -1515,7 +1664,19 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update, int nth) {
   }
   __syncthreads();  // okl final
   if (!okl) {
-    if (tid == 0) c->solve_ok = 0;
+    if (tid == 0) {
+      c->solve_ok = 0;
+      if (gfu) {  // GN fused: the failed pass ends here (nothing to apply)
+        KbCtrl& cl = cls;
+        cl = *c;
+        cl_red[0] = cl_red[1] = cl_red[2] = cl_red[3] = 0.0;
+        pol_post(&cl, d, cl_red);
+        if (!cl.done) pol_pre<true>(&cl);
+        cl.pending = 0;
+        cl.have_dx = 0;
+        *c = cl;
+      }
+    }
     return;
   }
   if (tid < 64) {
@@ -1539,6 +1700,10 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update, int nth) {
       d.camstat[0] = mx;
       d.camstat[1] = dd;
       d.camstat[2] = dr;
+      if (gfu) {  // the step is applied by the next pass's build (or the finishing back-substitution)
+        c->have_dx = 1;
+        c->pending = 1;
+      }
     }
     if (do_update) {
       // camera design variables: intrinsics (additive, one lane per slot) and baselines (one lane per pose)
@@ -1596,7 +1761,7 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update, int nth) {
 template <int CM>
 __global__ void __launch_bounds__(CM == 0 ? 512 : 256) k_solve(KbDev d, int gate, int do_update) {
   if (gate && d.ctrl->done) return;
-  if (gate && threadIdx.x == 0) d.ctrl->pending = 1;
+  if (gate && !d.gn_fused && threadIdx.x == 0) d.ctrl->pending = 1;
   solve_body<CM>(d, gate, do_update, blockDim.x);
 }
 
@@ -1626,7 +1791,7 @@ __global__ void __launch_bounds__(512) k_backsub(KbDev d, int gate, int do_updat
   const bool cost_pass = do_update && with_cost;
   // ---- round 1: launch-independent loads, straight-line and unconditional (clamped) so that they are all in
   // flight together; the gate and the LDS stores come after
-  const int done = c->done, sok = c->solve_ok, cur = c->cur;
+  const int done = c->done || (gate && d.gn_fused && !c->have_dx), sok = c->solve_ok, cur = c->cur;
   const bool tg_lds = 3 * d.K <= kTargetLds;
   const int nt3 = 3 * d.K;
   constexpr int kTgU = 6;  // 6 x 64 >= 3 x 120 AprilGrid corners even for a one-wave block
@@ -1743,7 +1908,7 @@ __global__ void __launch_bounds__(512) k_backsub(KbDev d, int gate, int do_updat
           if (fv.y <= fv.x) continue;
           double R[9], t[3];
           rt_mul(Lc, Lc + 9, Ri, ti, R, t);  // T_cam_w = L_cam(candidate) T_f^-1
-          const int model = d.model[cm];
+          const int model = cam_arg(d.model, cm);
           for (int k0 = fv.x; k0 < fv.y; k0 += 128) {
             int cid[2];
             double2 yv[2];
@@ -1811,7 +1976,7 @@ __global__ void __launch_bounds__(256) k_cost(KbDev d, int which) {
     const int f = d.view_frame[v], cam = d.view_cam[v];
     double R[9], t[3];
     cam_from_state(d, s, cam, s + d.off_frame + 7 * f, R, t);
-    const int model = d.model[cam];
+    const int model = cam_arg(d.model, cam);
     const double* intr = s + cam * KB_MAX_INTR;
     const int o0 = d.view_off[v], o1 = d.view_off[v + 1];
     for (int k = o0 + lane; k < o1; k += 64) {
@@ -1886,6 +2051,7 @@ __global__ void k_policy(KbDev d) {
   pol_post(&cl, d, red);
   if (!cl.done) pol_pre(&cl);
   cl.pending = 0;
+  cl.have_dx = 0;
   *c = cl;
 }
 
@@ -1920,6 +2086,8 @@ __global__ void k_pol_init(KbDev d, KbOpts o) {
   c->n_trace = 0;
   c->passes = 0;
   c->pending = 0;
+  c->have_dx = 0;
+  for (int q = 0; q < kDxSlots; ++q) d.dxmax[q * kDxStride] = 0ull;
 }
 
 // per-call update (kb_apply_update): all DVs from state[cur] -> state[1-cur]
@@ -1931,9 +2099,9 @@ __global__ void __launch_bounds__(256) k_update_all(KbDev d) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t < N * KB_MAX_INTR) {
     const int cam = t / KB_MAX_INTR, x = t % KB_MAX_INTR;
-    out[t] = in[t] + ((x < d.nintr[cam]) ? d.dx[d.col_intr[cam] + x] : 0.0);
+    out[t] = in[t] + ((x < cam_arg(d.nintr, cam)) ? d.dx[cam_arg(d.col_intr, cam) + x] : 0.0);
   }
-  if (t < N - 1) update_pose(in + d.off_base + 7 * t, d.dx + d.col_base[t], out + d.off_base + 7 * t);
+  if (t < N - 1) update_pose(in + d.off_base + 7 * t, d.dx + cam_arg(d.col_base, t), out + d.off_base + 7 * t);
   if (t < d.F) update_pose(in + d.off_frame + 7 * t, d.dx + d.C + 6 * t, out + d.off_frame + 7 * t);
 }
 
