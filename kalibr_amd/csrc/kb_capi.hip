@@ -181,6 +181,7 @@ kb_handle* kb_create(const kb_layout* L) {
   h->WPB = d.wpb;
   d.W = h->W;
   d.Wp = h->N * 136 + h->W + 1;
+  d.Wr = d.Wp + 1;
   d.Wtot = d.Wp + 1;  // + per-rank max|dx_f| column(s); kb_comm_init widens it to nranks
   d.nranks = 1;
   d.rank = 0;
@@ -199,10 +200,9 @@ kb_handle* kb_create(const kb_layout* L) {
   rc |= h->alloc(&d.Hff, 36 * (size_t)h->F);
   rc |= h->alloc(&d.Hfc, 6 * (size_t)h->C * h->F);
   rc |= h->alloc(&d.gf, 6 * (size_t)h->F);
-  rc |= h->alloc(&d.Lf, 36 * (size_t)h->F);
-  rc |= h->alloc(&d.Yf, 6 * (size_t)h->C * h->F);
-  rc |= h->alloc(&d.zf, 6 * (size_t)h->F);
-  rc |= h->alloc(&d.part, (size_t)d.nblk * d.Wp);
+  rc |= h->alloc(&d.Af, 6 * (size_t)h->C * h->F);
+  rc |= h->alloc(&d.bf, 6 * (size_t)h->F);
+  rc |= h->alloc(&d.part, (size_t)d.nblk * d.Wr);
   rc |= h->alloc(&d.part8, (size_t)kColsumRows * d.Wtot);
   rc |= h->alloc(&d.psum_local, (size_t)d.Wtot);
   d.psum = d.psum_local;
@@ -212,7 +212,6 @@ kb_handle* kb_create(const kb_layout* L) {
   d.dbg_stop = -1;
   d.dbg_flags = 0;
   rc |= h->alloc(&d.ticket, 16);
-  rc |= h->alloc(&d.dxmax, (size_t)kDxSlots * kDxStride);
   rc |= h->alloc(&d.Hcc, (size_t)h->C * h->C);
   rc |= h->alloc(&d.gc, (size_t)h->C);
   rc |= h->alloc(&d.cost_build, 2);
@@ -250,7 +249,8 @@ kb_handle* kb_create(const kb_layout* L) {
     const int N = h->N, C = h->C, WPB = d.wpb;
     const int CZ = 16 * ((C + 16) / 16);  // [Y | z] row stride of the Schur tiles
     h->lds_build = sizeof(double) * (WPB * 64 * XS + WPB * 256 + N * (256 + 256 + 64 + 36 + 36 + 8) + 36 + 8 + 6 * C +
-                                     36 + 8 * CZ + 18 * N * (N - 1) + (3 * h->K <= kTargetLds ? 3 * h->K : 0));
+                                     36 + 8 * CZ + 18 * N * (N - 1) + (3 * h->K <= kTargetLds ? 3 * h->K : 0) +
+                                     8 * d.gframes);
     h->lds_camexp = sizeof(double) * (N * 256 + N * N * 36);
     h->lds_schur = sizeof(double) * (8 * CZ + 36);
     if (C <= 64) {
@@ -826,7 +826,7 @@ int kb_build_kernel_stats(kb_handle* h, double* avg_ms, double* bytes_per_launch
   // and the per-block partial rows written.
   const double bytes = 18.0 * h->NC + 8.0 * h->F * h->N + 8.0 * h->S + 8.0 * (12.0 * h->N + 36.0 * h->N * h->N) +
                        8.0 * h->F * (36 + 6 + 6.0 * h->C) + 8.0 * h->F * (36 + 6 + 6.0 * h->C) +
-                       8.0 * h->d.nblk * h->d.Wp;
+                       8.0 * h->d.nblk * h->d.Wr;
   if (bytes_per_launch) *bytes_per_launch = bytes;
   // executed MFMA flops (2 x 16 x 16 x rows, rows padded to 64 per 32-corner phase) + ~300 VALU flops/corner
   double rows = 0.0;

@@ -6,9 +6,9 @@
 //   view_off uint32  [V+1]; view_frame int32 [V]; view_cam int32 [V]; frame_vcam int32 [F][N] (-1 = none)
 //   state    [2][S]                ping-pong design-variable buffers, ctrl->cur = accepted one
 //   Hff [F][36], Hfc [F][6][C], gf [F][6]     arrow blocks written by k_build
-//   Lf [F][36], Yf [F][6][C], zf [F][6]       frame Schur factors (k_build fused / k_schur)
-//   part [nblk][Wp]                per-block partials: per-camera 16x16 upper sums (N*136) |
-//                                  sum Y^T Y upper (C(C+1)/2) | sum Y^T z (C) | #non-PD frames (1)
+//   Af [F][6][C], bf [F][6]                   dx_f = b_f - A_f dx_c (k_build fused / k_schur)
+//   part [nblk][Wr]                per-block partials: per-camera 16x16 upper sums (N*136) |
+//                                  sum Y^T Y upper (C(C+1)/2) | sum Y^T z (C) | #non-PD frames (1) | max|dx_f| (1)
 //   part8 [8][Wtot]                stage-1 column sums of part (k_colsum) | per-rank max|dx_f| (GN fused);
 //                                  psum_local [Wtot] the finished sums
 //   bpart [nblk_bs][4]             k_backsub_cost: cost, max|dx|, dx.dx, dx.rhs per block
@@ -36,21 +36,17 @@ struct KbOpts {
 };
 
 constexpr int kColsumRows = 8;  // stage-1 row splits of the block partial reduction
-constexpr int kDxSlots = 64, kDxStride = 16;  // spread atomics: contention on one address serialises them
-static_assert(kDxSlots == 64, "k_colsum reduces the slots with one wave");
 
 struct KbDev {
   int N, F, V, NC, C, ncols, S, K;  // K = target corners
   int off_base, off_frame;
   int gframes, nblk, nblk_bs, nblk_cost;
   int nsplit, wpb;   // k_build: waves per block = N * nsplit
-  int W, Wp, Wtot;   // W = C(C+1)/2 + C ; Wp = N*136 + W + 1 (block partial row) ; Wtot = Wp + max(nranks, 1)
+  int W, Wp, Wr, Wtot;  // W = C(C+1)/2 + C ; Wp = N*136 + W + 1 summed entries of a block partial row ;
+                       // Wr = Wp + 1 (+ the block's max|dx_f|, GN fused) ; Wtot = Wp + max(nranks, 1)
   int trace_cap;
   int fold;          // 1: the next pass's k_build applies the pending policy (non-fused passes)
   int gn_fused;      // 1: Gauss-Newton passes fused as [update + build] -> colsum -> [GN policy + solve]
-  unsigned long long* dxmax;  // GN fused: [kDxSlots] (stride kDxStride, one cache line each) max|dx_f| of this
-                              // rank's frames, block b -> slot b % kDxSlots (bits of a non-negative double,
-                              // atomicMax); k_colsum puts their max in column Wp + rank of the column sums
   int rank;
   double host_lambda;  // conditioner for the per-call (non-gated) path
   int model[KB_MAX_CAMS], nintr[KB_MAX_CAMS], col_intr[KB_MAX_CAMS], col_base[KB_MAX_CAMS];
@@ -68,8 +64,8 @@ struct KbDev {
   double* camL;  // [2][N][12]    camera chains L_i of state buffer `slot` (ping-pong with ctrl->cur)
   double* camK;  // [2][N][N][36] baseline chains K_{i,j} of state buffer `slot`
   double *Hff, *Hfc, *gf;
-  double *Lf, *Yf, *zf;
-  double* part;   // [nblk][Wp]
+  double *Af, *bf;  // [F][6][C], [F][6]: frame back-substitution rows L_f^-T Y_f, L_f^-T z_f
+  double* part;   // [nblk][Wr]
   double* part8;       // [8][Wtot] stage-1 column sums
   double* psum_local;  // [Wtot] finished column sums of this rank (last k_colsum block)
   const double* psum;  // consumer view of the column sums: psum_rows rows of Wtot summed in fixed order

@@ -400,9 +400,8 @@ __global__ void __launch_bounds__(256) k_pre(KbDev d, int gate) {
 }
 
 // 6x6 Cholesky of A + lam2 I by one wave (lanes 0..5 hold rows; column k broadcast with v_readlane):
-// L (row-major lower, upper zero) and 1/diag(L) to LDS, L also to HBM.  Returns false if not PD.
-__device__ __forceinline__ bool chol6_wave(const double* A, double lam2, double* L, double* rdiag, double* Lg,
-                                           int lane) {
+// L (row-major lower, upper zero) and 1/diag(L) to LDS.  Returns false if not PD.
+__device__ __forceinline__ bool chol6_wave(const double* A, double lam2, double* L, double* rdiag, int lane) {
   double row[6];
   const int i = lane < 6 ? lane : 5;
 #pragma unroll
@@ -422,9 +421,7 @@ __device__ __forceinline__ bool chol6_wave(const double* A, double lam2, double*
   if (lane < 6)
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
-      const double v = (j <= lane) ? row[j] : 0.0;
-      L[lane * 6 + j] = v;
-      Lg[lane * 6 + j] = v;
+      L[lane * 6 + j] = (j <= lane) ? row[j] : 0.0;
     }
   return ok;
 }
@@ -482,83 +479,83 @@ __device__ __forceinline__ void schur_tiles_store(double* prow_schur, int C, con
   }
 }
 
-// Y = L^-1 H_fc (thread per column), z = L^-1 g_f (last thread) into [Y | z] (row stride CZ) and HBM
+// Y = L^-1 H_fc (thread per column), z = L^-1 g_f (last thread) into [Y | z] (row stride CZ); to HBM the frame
+// back-substitution rows A_f = L^-T Y and b_f = L^-T z, so that dx_f = L^-T (z - Y dx_c) = b_f - A_f dx_c
+// (solveSystem's frame block of the Schur solve) is one row-times-vector per frame in the next kernel
 __device__ __forceinline__ void schur_forward(const KbDev& d, int f, const double* L, const double* rdiag,
                                               const double* Hfc_lds, const double* g_lds, double* Y, int CZ) {
   const int C = d.C, t = threadIdx.x;
-  if (t < C) {
-    double yv[6];
+  const bool col = t < C;
+  if (col || t == (int)blockDim.x - 1) {
+    double yv[6], av[6];
 #pragma unroll
     for (int r = 0; r < 6; ++r) {
-      double s2 = Hfc_lds ? Hfc_lds[r * C + t] : d.Hfc[((size_t)f * 6 + r) * C + t];
+      double s2 = col ? (Hfc_lds ? Hfc_lds[r * C + t] : d.Hfc[((size_t)f * 6 + r) * C + t])
+                      : (g_lds ? g_lds[r] : d.gf[(size_t)f * 6 + r]);
 #pragma unroll
       for (int k = 0; k < r; ++k) s2 -= L[r * 6 + k] * yv[k];
       yv[r] = s2 * rdiag[r];
-      Y[r * CZ + t] = yv[r];
-      d.Yf[((size_t)f * 6 + r) * C + t] = yv[r];
+      Y[r * CZ + (col ? t : C)] = yv[r];
     }
-  } else if (t == (int)blockDim.x - 1) {
-    double zv[6];
 #pragma unroll
-    for (int r = 0; r < 6; ++r) {
-      double s2 = g_lds ? g_lds[r] : d.gf[(size_t)f * 6 + r];
+    for (int r = 5; r >= 0; --r) {
+      double s2 = yv[r];
 #pragma unroll
-      for (int k = 0; k < r; ++k) s2 -= L[r * 6 + k] * zv[k];
-      zv[r] = s2 * rdiag[r];
-      Y[r * CZ + C] = zv[r];
-      d.zf[(size_t)f * 6 + r] = zv[r];
+      for (int k = r + 1; k < 6; ++k) s2 -= L[k * 6 + r] * av[k];
+      av[r] = s2 * rdiag[r];
+      if (col)
+        d.Af[((size_t)f * 6 + r) * C + t] = av[r];
+      else
+        d.bf[(size_t)f * 6 + r] = av[r];
     }
   }
 }
 
-// GN fused passes: dx_f = L_f^-T (z_f - Y_f dx_c) of the previous solve, computed by every wave of the frame's
-// build block (k_backsub's arithmetic in the same order).  Loads: lane slot sl holds column lane + 64 sl of Y_f;
-// lanes 0..5 / 0..35 hold z_f / L_f (broadcast with v_readlane).
-__device__ __forceinline__ void fdx_load(const KbDev& d, int f, int lane, double (&yr)[6][2], double& zq,
-                                         double& lq) {
+// dx_f = b_f - A_f dx_c.  Lane slot sl holds column lane + 64 sl of A_f (zero beyond C); lanes 0..5 hold b_f.
+__device__ __forceinline__ void fdx_load(const KbDev& d, int f, int lane, double (&ar)[6][2], double& bq) {
   const int C = d.C;
 #pragma unroll
   for (int sl = 0; sl < 2; ++sl) {
     const int q = lane + 64 * sl, qc = min(q, C - 1);
 #pragma unroll
     for (int r = 0; r < 6; ++r) {
-      const double v = d.Yf[((size_t)f * 6 + r) * C + qc];
-      yr[r][sl] = q < C ? v : 0.0;
+      const double v = d.Af[((size_t)f * 6 + r) * C + qc];
+      ar[r][sl] = q < C ? v : 0.0;
     }
   }
-  zq = d.zf[(size_t)f * 6 + min(lane, 5)];
-  lq = d.Lf[(size_t)f * 36 + min(lane, 35)];
+  bq = d.bf[(size_t)f * 6 + min(lane, 5)];
 }
 
-__device__ __forceinline__ void fdx_solve(const double (&yr)[6][2], const double* dxv, double zq, double lq,
-                                          double* w) {
+// every lane ends with all six entries of dx_f
+__device__ __forceinline__ void fdx_solve(const double (&ar)[6][2], const double* dxv, double bq, double* w) {
 #pragma unroll
   for (int r = 0; r < 6; ++r) {
-    double s = yr[r][0] * dxv[0] + yr[r][1] * dxv[1];
+    double s = ar[r][0] * dxv[0] + ar[r][1] * dxv[1];
     s = wave_sum_d(s);
-    w[r] = readlane_d(zq, r) - s;
-  }
-#pragma unroll
-  for (int r = 5; r >= 0; --r) {
-    double s = w[r];
-#pragma unroll
-    for (int k = r + 1; k < 6; ++k) s -= readlane_d(lq, k * 6 + r) * w[k];
-    w[r] = s / readlane_d(lq, r * 6 + r);
+    w[r] = readlane_d(bq, r) - s;
   }
 }
 
-// pose of frame f moved by its step (in place), stored to the candidate buffer by wave 0; wmax = max |dx_f|
-__device__ __forceinline__ void frame_step(const KbDev& d, int f, int wave, int lane, const double (&yr)[6][2],
-                                           const double* dxv, double zq, double lq, double* fp, double* snew,
-                                           double& wmax) {
+// pose of frame f moved by its step (in place), stored to the candidate buffer if `store`; wmax = max |dx_f|
+__device__ __forceinline__ void frame_step(const KbDev& d, int f, bool store, int lane, const double (&ar)[6][2],
+                                           const double* dxv, double bq, double* fp, double* snew, double& wmax) {
   double w[6], np[7];
-  fdx_solve(yr, dxv, zq, lq, w);
+  fdx_solve(ar, dxv, bq, w);
+#ifdef KB_STAMPS
+  if (d.dbg_flags & 4) {  // diagnostic: additive pose update
+#pragma unroll
+    for (int q = 0; q < 7; ++q) np[q] = fp[q] + w[q % 6];
+  } else
+#endif
   update_pose(fp, w, np);
 #pragma unroll
   for (int q = 0; q < 7; ++q) fp[q] = np[q];
 #pragma unroll
   for (int r = 0; r < 6; ++r) wmax = fmax(wmax, fabs(w[r]));
-  if (wave == 0 && lane < 7) {
+#ifdef KB_STAMPS
+  if (d.dbg_flags & 8) return;  // diagnostic: no pose store
+#endif
+  if (store && lane < 7) {
     double pv = np[0];
 #pragma unroll
     for (int q = 1; q < 7; ++q) pv = (lane == q) ? np[q] : pv;
@@ -592,6 +589,7 @@ __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
   double* Y = L + 36;                // [8][CZ]: [Y | z] of the current frame, zero-padded
   double* Kl = Y + 8 * CZ;           // [N(N-1)/2][36] K_{i,j}, j < i, at (i(i-1)/2 + j)
   double* tg = Kl + 18 * N * (N - 1);  // [n_target][3] target corners (when staged)
+  __shared__ double wmx[8];            // GN fused: per-wave max |dx_f|
   __shared__ int okl;
   __shared__ double cst[KB_MAX_CAMS][24];  // per camera: chain L (12) | intrinsics (10)
   __shared__ int ctab[2][KB_MAX_CAMS];      // per camera: first intrinsic column | baseline column
@@ -623,7 +621,7 @@ __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
   KB_KEEPS(fv.y);
   // GN fused passes: the previous solve's frame steps are applied here (back-substitution of frame f0)
   const bool gfu = GNF && gate;
-  double yr[6][2], dxv[2] = {0.0, 0.0}, zq = 0.0, lq = 0.0;
+  double yr[6][2], dxv[2] = {0.0, 0.0}, bq = 0.0;
   if (gfu) {
 #pragma unroll
     for (int sl = 0; sl < 2; ++sl) {
@@ -631,15 +629,21 @@ __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
       const double v = d.dx[min(q, C - 1)];
       dxv[sl] = q < C ? v : 0.0;
     }
-    fdx_load(d, f0, lane, yr, zq, lq);
+#ifdef KB_STAMPS
+    if (d.dbg_flags & 2) {  // diagnostic: no A_f / b_f loads
+#pragma unroll
+      for (int r = 0; r < 6; ++r) yr[r][0] = yr[r][1] = 1e-3 * r;
+      bq = 1e-3 * lane;
+    } else
+#endif
+    fdx_load(d, f0, lane, yr, bq);
 #pragma unroll
     for (int sl = 0; sl < 2; ++sl) {
       KB_KEEP(dxv[sl]);
 #pragma unroll
       for (int r = 0; r < 6; ++r) KB_KEEP(yr[r][sl]);
     }
-    KB_KEEP(zq);
-    KB_KEEP(lq);
+    KB_KEEP(bq);
   }
   if (fold && cin.pending && !cin.done) {  // previous pass's end (accept / revert, next prelude)
     pass_end_block(d, cin, &cnew, blockIdx.x == 0, nth, true, pre);
@@ -662,11 +666,36 @@ __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
     cst[cm][e] = e < 12 ? cam_L(d, bs)[cm * 12 + e] : s[cm * KB_MAX_INTR + e - 12];
   }
   if (tid < 2 * N) ctab[tid / N][tid % N] = (tid < N) ? cam_arg(d.col_intr, tid) : cam_arg(d.col_base, tid - N);
+  double* fpl = tg + (tg_lds ? nt3 : 0);  // [gframes][8] the block's frame poses (after their steps)
   double fp0[7];  // pose of the block's first frame
 #pragma unroll
   for (int q = 0; q < 7; ++q) fp0[q] = sf[d.off_frame + 7 * f0 + q];
-  double wmax = 0.0;  // GN fused: max |dx_f| over the block's frames
-  if (upd) frame_step(d, f0, wave, lane, yr, dxv, zq, lq, fp0, snew, wmax);  // frame f0 (its loads in round 1)
+  double wmax = 0.0;  // GN fused: max |dx_f| over this wave's frames
+  if (upd) frame_step(d, f0, wave == 0, lane, yr, dxv, bq, fp0, snew, wmax);  // frame f0 (its loads in round 1)
+  if (wave == 0 && lane < 7) {
+    double pv = fp0[0];
+#pragma unroll
+    for (int q = 1; q < 7; ++q) pv = (lane == q) ? fp0[q] : pv;
+    fpl[lane] = pv;
+  }
+  // further frames of a multi-frame block: one wave each
+  for (int j = 1 + wave; j < f1 - f0; j += WPB) {
+    double fp[7];
+#pragma unroll
+    for (int q = 0; q < 7; ++q) fp[q] = sf[d.off_frame + 7 * (f0 + j) + q];
+    if (upd) {
+      double af[6][2], bfq;
+      fdx_load(d, f0 + j, lane, af, bfq);
+      frame_step(d, f0 + j, true, lane, af, dxv, bfq, fp, snew, wmax);
+    }
+    if (lane < 7) {
+      double pv = fp[0];
+#pragma unroll
+      for (int q = 1; q < 7; ++q) pv = (lane == q) ? fp[q] : pv;
+      fpl[8 * j + lane] = pv;
+    }
+  }
+  if (lane == 0) wmx[wave] = wmax;
   KB_STAMP(d, 14);
   int cidn;
   double2 yn;
@@ -710,12 +739,7 @@ __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
   for (int f = f0; f < f1; ++f) {
     double fp[7];
 #pragma unroll
-    for (int q = 0; q < 7; ++q) fp[q] = (f == f0) ? fp0[q] : sf[d.off_frame + 7 * f + q];
-    if (upd && f > f0) {  // wave-uniform: next frame of a multi-frame block
-      double yf[6][2], zf, lf;
-      fdx_load(d, f, lane, yf, zf, lf);
-      frame_step(d, f, wave, lane, yf, dxv, zf, lf, fp, snew, wmax);
-    }
+    for (int q = 0; q < 7; ++q) fp[q] = fpl[8 * (f - f0) + q];
     double Ri[9], ti[3], R[9], t[3];
     pose_inverse(fp, Ri, ti);
     rt_mul(Lc, Lc + 9, Ri, ti, R, t);  // T_cam_w = L_cam T_f^-1 (chain of the accepted state)
@@ -892,7 +916,7 @@ __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
       __syncthreads();
       KB_STAMP(d, 21);
       if (wave == 0) {
-        const bool ok = chol6_wave(Fh, lam2, L, rdg, d.Lf + (size_t)f * 36, lane);
+        const bool ok = chol6_wave(Fh, lam2, L, rdg, lane);
         if (!ok && lane == 0) okl = 0;
       }
       __syncthreads();
@@ -905,7 +929,7 @@ __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
     __syncthreads();
     KB_STAMP(d, 24);
   }
-  double* prow = d.part + (size_t)blockIdx.x * d.Wp;
+  double* prow = d.part + (size_t)blockIdx.x * d.Wr;
   for (int q = threadIdx.x; q < N * 136; q += nth) {
     const int qc = q / 136;
     int a, b;
@@ -916,8 +940,11 @@ __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
     schur_tiles_store<TW>(prow + N * 136, C, tii, tjj, acc);
     if (threadIdx.x == 0) prow[N * 136 + W] = okl ? 0.0 : 1.0;  // non-PD frame blocks (summed)
   }
-  if (upd && threadIdx.x == 0)
-    atomicMax(d.dxmax + (blockIdx.x % kDxSlots) * kDxStride, (unsigned long long)__double_as_longlong(wmax));
+  if (GNF && threadIdx.x == 0) {  // the block's max |dx_f| (reduced with max by k_colsum)
+    double m = 0.0;
+    for (int q = 0; q < WPB; ++q) m = fmax(m, wmx[q]);
+    prow[d.Wp] = m;
+  }
   KB_STAMP(d, 25);
 }
 
@@ -949,7 +976,7 @@ __global__ void __launch_bounds__(256) k_schur(KbDev d, int gate) {
   for (int f = f0; f < f1; ++f) {
     __syncthreads();
     if (threadIdx.x < 64) {
-      const bool ok = chol6_wave(d.Hff + (size_t)f * 36, lam2, L, rdg, d.Lf + (size_t)f * 36, threadIdx.x);
+      const bool ok = chol6_wave(d.Hff + (size_t)f * 36, lam2, L, rdg, threadIdx.x);
       if (!ok && threadIdx.x == 0) okl = 0;
     }
     __syncthreads();
@@ -957,7 +984,7 @@ __global__ void __launch_bounds__(256) k_schur(KbDev d, int gate) {
     __syncthreads();
     schur_tiles_accumulate<TW>(Y, CZ, tii, tjj, acc);
   }
-  double* prow = d.part + (size_t)blockIdx.x * d.Wp + N * 136;
+  double* prow = d.part + (size_t)blockIdx.x * d.Wr + N * 136;
   schur_tiles_store<TW>(prow, C, tii, tjj, acc);
   __syncthreads();
   if (threadIdx.x == 0) prow[W] = okl ? 0.0 : 1.0;
@@ -974,27 +1001,27 @@ __global__ void __launch_bounds__(256) k_colsum(KbDev d, int gate) {
   __shared__ double part[4][64];
   const int l = threadIdx.x & 63, w4 = threadIdx.x >> 6;
   const int e = blockIdx.x * 64 + l, ry = blockIdx.y;
-  const int ec = min(e, d.Wp - 1);
+  const bool mx = e >= d.Wp;  // max|dx_f| column(s): reduced with max (non-negative values)
+  const int ec = min(e, d.Wp);
   double s = 0.0;
   constexpr int U = 16, step = 4 * kColsumRows;
   for (int b0 = ry + kColsumRows * w4; b0 < d.nblk; b0 += U * step) {
     double v[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) v[u] = d.part[(size_t)min(b0 + u * step, d.nblk - 1) * d.Wp + ec];
+    for (int u = 0; u < U; ++u) v[u] = d.part[(size_t)min(b0 + u * step, d.nblk - 1) * d.Wr + ec];
 #pragma unroll
-    for (int u = 0; u < U; ++u) s += (b0 + u * step < d.nblk) ? v[u] : 0.0;
+    for (int u = 0; u < U; ++u) {
+      const double x = (b0 + u * step < d.nblk) ? v[u] : 0.0;
+      s = mx ? fmax(s, x) : s + x;
+    }
   }
   part[w4][l] = s;
-  double dm = 0.0;  // max|dx_f| of this rank (GN fused passes): max over the atomic slots, by wave 0
-  if (d.gn_fused && ry == 0 && w4 == 0 && blockIdx.x == (d.Wp + d.rank) / 64) {  // wave-uniform
-    dm = __longlong_as_double((long long)d.dxmax[l * kDxStride]);
-    dm = wave_max_d(dm);
-  }
   __syncthreads();
   if (w4 == 0 && e < d.Wtot) {
     double v = ((part[0][l] + part[1][l]) + part[2][l]) + part[3][l];
-    if (e >= d.Wp)  // max|dx_f| column of each rank: this rank's value in row 0 (GN fused passes), zero elsewhere
-      v = (ry == 0 && d.gn_fused && e - d.Wp == d.rank) ? dm : 0.0;
+    if (mx)  // one column per rank: this rank's max in its own column (GN fused passes), zero elsewhere
+      v = (d.gn_fused && e - d.Wp == d.rank) ? fmax(fmax(part[0][l], part[1][l]), fmax(part[2][l], part[3][l]))
+                                             : 0.0;
     d.part8[(size_t)ry * d.Wtot + e] = v;
   }
 }
@@ -1009,7 +1036,7 @@ __global__ void __launch_bounds__(256) k_colfin(KbDev d, int gate) {
   for (int r = 0; r < kColsumRows; ++r) v[r] = d.part8[(size_t)r * d.Wtot + q];
   double acc = 0.0;
 #pragma unroll
-  for (int r = 0; r < kColsumRows; ++r) acc += v[r];
+  for (int r = 0; r < kColsumRows; ++r) acc = (q >= d.Wp) ? fmax(acc, v[r]) : acc + v[r];
   d.psum_local[q] = acc;
 }
 
@@ -1022,6 +1049,17 @@ __device__ __forceinline__ double psum_at(const KbDev& d, int e) {
 #pragma unroll
   for (int r = 0; r < kColsumRows; ++r) acc += (r < d.psum_rows) ? v[r] : 0.0;
   return acc;
+}
+
+// max over the psum_rows rows (the max|dx_f| columns)
+__device__ __forceinline__ double psum_max_at(const KbDev& d, int e) {
+  double v[kColsumRows];
+#pragma unroll
+  for (int r = 0; r < kColsumRows; ++r) v[r] = d.psum[(size_t)(r < d.psum_rows ? r : 0) * d.Wtot + e];
+  double m = v[0];
+#pragma unroll
+  for (int r = 1; r < kColsumRows; ++r) m = fmax(m, v[r]);
+  return m;
 }
 
 
@@ -1565,10 +1603,9 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update, int nth) {
   double x[2] = {0.0, 0.0};
   double dxr = 0.0;  // GN fused: max|dx_f| of the previous step, one column per rank
   if (gfu && tid < 64) {
-    d.dxmax[tid * kDxStride] = 0ull;  // read by k_colsum already; armed for the next build
     const int nr = d.Wtot - d.Wp;
-    dxr = psum_at(d, d.Wp + min(tid, nr - 1));
-    for (int r = tid + 64; r < nr; r += 64) dxr = fmax(dxr, psum_at(d, d.Wp + r));
+    dxr = psum_max_at(d, d.Wp + min(tid, nr - 1));
+    for (int r = tid + 64; r < nr; r += 64) dxr = fmax(dxr, psum_max_at(d, d.Wp + r));
   }
   KB_STAMP(d, 0);
   // phase A: stage K, column info, per-camera sums and the Schur sums in LDS (one row: psum)
@@ -1806,7 +1843,7 @@ __global__ void __launch_bounds__(512) k_backsub(KbDev d, int gate, int do_updat
     dxv[sl] = q < C ? v : 0.0;
 #pragma unroll
     for (int r = 0; r < 6; ++r) {
-      const double yv = d.Yf[((size_t)f * 6 + r) * C + qc];
+      const double yv = d.Af[((size_t)f * 6 + r) * C + qc];
       yr[r][sl] = q < C ? yv : 0.0;
     }
   }
@@ -1862,15 +1899,7 @@ __global__ void __launch_bounds__(512) k_backsub(KbDev d, int gate, int do_updat
     for (int r = 0; r < 6; ++r) {
       double s = yr[r][0] * dxv[0] + yr[r][1] * dxv[1];
       s = wave_sum_d(s);
-      w[r] = d.zf[(size_t)f * 6 + r] - s;
-    }
-    const double* L = d.Lf + (size_t)f * 36;
-#pragma unroll
-    for (int r = 5; r >= 0; --r) {
-      double s = w[r];
-#pragma unroll
-      for (int k = r + 1; k < 6; ++k) s -= L[k * 6 + r] * w[k];
-      w[r] = s / L[r * 6 + r];
+      w[r] = d.bf[(size_t)f * 6 + r] - s;
     }
     KB_STAMP(d, 31);
     if (wave == 0 && lane < 6) {
@@ -2087,7 +2116,6 @@ __global__ void k_pol_init(KbDev d, KbOpts o) {
   c->passes = 0;
   c->pending = 0;
   c->have_dx = 0;
-  for (int q = 0; q < kDxSlots; ++q) d.dxmax[q * kDxStride] = 0ull;
 }
 
 // per-call update (kb_apply_update): all DVs from state[cur] -> state[1-cur]

@@ -33,8 +33,10 @@ __device__ __forceinline__ void quat2r(const double* q, double* R) {
 __device__ __forceinline__ void update_pose(const double* in, const double* d6, double* out) {
   const double a0 = d6[0], a1 = d6[1], a2 = d6[2];
   const double th = sqrt(a0 * a0 + a1 * a1 + a2 * a2);
-  const double na = (th < kEps4thRoot) ? 0.5 + (th * th) * (1.0 / 48.0) : sin(th * 0.5) / th;
-  const double d0 = a0 * na, d1 = a1 * na, d2 = a2 * na, ca = cos(th * 0.5);
+  double sh, ca;
+  sincos(th * 0.5, &sh, &ca);  // one argument reduction for both
+  const double na = (th < kEps4thRoot) ? 0.5 + (th * th) * (1.0 / 48.0) : sh / th;
+  const double d0 = a0 * na, d1 = a1 * na, d2 = a2 * na;
   const double q0 = in[0], q1 = in[1], q2 = in[2], q3 = in[3];
   out[0] = q0 * ca + d0 * q3 - d1 * q2 + d2 * q1;
   out[1] = q1 * ca + d0 * q2 + d1 * q3 - d2 * q0;
