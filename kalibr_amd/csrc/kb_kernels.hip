@@ -31,7 +31,6 @@ typedef double v4d __attribute__((ext_vector_type(4)));
 #define KB_KEEP(x) asm volatile("" ::"v"(x))
 #define KB_KEEPS(x) asm volatile("" ::"s"(x))
 
-// broadcast of a double from a wave-uniform lane (v_readlane_b32 x2, no LDS round trip)
 // per-camera kernel-argument arrays read at a run-time index by selects: a dynamically indexed kernel argument
 // would make the compiler copy the whole KbDev into scratch (private memory), which costs every launch
 __device__ __forceinline__ int cam_arg(const int (&a)[KB_MAX_CAMS], int i) {
@@ -41,6 +40,7 @@ __device__ __forceinline__ int cam_arg(const int (&a)[KB_MAX_CAMS], int i) {
   return v;
 }
 
+// broadcast of a double from a wave-uniform lane (v_readlane_b32 x2, no LDS round trip)
 __device__ __forceinline__ double readlane_d(double v, int lane) {
   const unsigned long long b = __double_as_longlong(v);
   const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffull), lane);
@@ -540,6 +540,12 @@ __device__ __forceinline__ void fdx_solve(const double (&ar)[6][2], const double
 __device__ __forceinline__ void frame_step(const KbDev& d, int f, bool store, int lane, const double (&ar)[6][2],
                                            const double* dxv, double bq, double* fp, double* snew, double& wmax) {
   double w[6], np[7];
+#ifdef KB_STAMPS
+  if (d.dbg_flags & 32) {  // diagnostic: no wave sums
+#pragma unroll
+    for (int r = 0; r < 6; ++r) w[r] = ar[r][0] * dxv[0] + bq;
+  } else
+#endif
   fdx_solve(ar, dxv, bq, w);
 #ifdef KB_STAMPS
   if (d.dbg_flags & 4) {  // diagnostic: additive pose update
@@ -670,6 +676,22 @@ __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
   double fp0[7];  // pose of the block's first frame
 #pragma unroll
   for (int q = 0; q < 7; ++q) fp0[q] = sf[d.off_frame + 7 * f0 + q];
+  int cidn;
+  double2 yn;
+  {
+    const int k = min(fv.x + sp * 64 + lane, max(fv.y - 1, 0));
+    cidn = d.cid[k];
+    yn = d.y[k];
+  }
+  const double* Kc = cam_K(d, bs);
+  for (int q = tid; q < 18 * N * (N - 1); q += nth) {
+    const int e = q % 36, ij = q / 36;
+    int i = 1;
+    while (i * (i + 1) / 2 <= ij) ++i;
+    const int j = ij - i * (i - 1) / 2;
+    Kl[q] = Kc[(size_t)(i * N + j) * 36 + e];
+  }
+  KB_KEEPS(cidn);  // issued before the frame step's arithmetic (their latency overlaps it)
   double wmax = 0.0;  // GN fused: max |dx_f| over this wave's frames
   if (upd) frame_step(d, f0, wave == 0, lane, yr, dxv, bq, fp0, snew, wmax);  // frame f0 (its loads in round 1)
   if (wave == 0 && lane < 7) {
@@ -697,21 +719,6 @@ __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
   }
   if (lane == 0) wmx[wave] = wmax;
   KB_STAMP(d, 14);
-  int cidn;
-  double2 yn;
-  {
-    const int k = min(fv.x + sp * 64 + lane, max(fv.y - 1, 0));
-    cidn = d.cid[k];
-    yn = d.y[k];
-  }
-  const double* Kc = cam_K(d, bs);
-  for (int q = tid; q < 18 * N * (N - 1); q += nth) {
-    const int e = q % 36, ij = q / 36;
-    int i = 1;
-    while (i * (i + 1) / 2 <= ij) ++i;
-    const int j = ij - i * (i - 1) / 2;
-    Kl[q] = Kc[(size_t)(i * N + j) * 36 + e];
-  }
   if (tg_lds) {
 #pragma unroll
     for (int u = 0; u < kTgU; ++u)
@@ -1601,8 +1608,13 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update, int nth) {
   // GN fused: a pending step means the system was built at the candidate state (slot 1 - cur)
   const int bslot = (gfu && c->have_dx) ? 1 - cur : cur;
   double x[2] = {0.0, 0.0};
+  // GN fused: the previous pass's end runs in wave kFinWave: while wave 0 factors (CM > 0), else before the
+  // camera expansion
+  constexpr int kFinWave = CM > 0 ? 1 : 0;
+  const bool fwave = (tid >> 6) == kFinWave;
   double dxr = 0.0;  // GN fused: max|dx_f| of the previous step, one column per rank
-  if (gfu && tid < 64) {
+  if (gfu && fwave) {
+    const int tid = threadIdx.x & 63;
     const int nr = d.Wtot - d.Wp;
     dxr = psum_max_at(d, d.Wp + min(tid, nr - 1));
     for (int r = tid + 64; r < nr; r += 64) dxr = fmax(dxr, psum_max_at(d, d.Wp + r));
@@ -1628,18 +1640,20 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update, int nth) {
     }
     T[q] = s;
   }
-  if (gfu && tid < 64) dxr = wave_max_d(dxr);
   if (tid == 0) {
     double s = 0.0;
     for (int i = 0; i < N; ++i) s += Hs[i * 256 + 255];
     d.cost_build[0] = s;
-    if (gfu) {
-      // GN fused: the previous pass's end.  Its cost is this build's (the system was built at its candidate):
-      // accept (GN always does) and the next prelude (Optimizer2.cpp:221-259, TrustRegionPolicy.cpp:39-52)
+    cl_red[0] = s;
+  }
+  // GN fused: the previous pass's end.  Its cost is this build's (the system was built at its candidate):
+  // accept (GN always does) and the next prelude (Optimizer2.cpp:221-259, TrustRegionPolicy.cpp:39-52)
+  auto finish_prev = [&]() {
+    dxr = wave_max_d(dxr);
+    if ((tid & 63) == 0) {
       KbCtrl& cl = cls;  // LDS copy (a private one would put the kernel arguments in scratch)
       cl = *c;
       if (cl.have_dx) {
-        cl_red[0] = s;
         cl_red[1] = cl_red[2] = 0.0;
         cl_red[3] = fmax(dxr, d.camstat[0]);
         pol_post(&cl, d, cl_red);
@@ -1651,11 +1665,12 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update, int nth) {
       fin[0] = cl.done;
       fin[1] = cl.cur;
     }
-  }
+  };
   __syncthreads();
-  if (gfu) {
+  if (CM == 0 && gfu) {
+    if (fwave) finish_prev();
+    __syncthreads();
     if (fin[0]) return;
-    cur = fin[1];
   }
   cam_expand_blocks<CM>(S, C, N, ctab, Hs, T, K, lam2, nth >> 6);
   for (int p = tid; p < C; p += nth) {
@@ -1677,6 +1692,8 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update, int nth) {
       const LdlOut r = ldl_solve_reg<CM>(d, S, bv, C, tid, pubcol);
       x[0] = r.x;
       if (!r.ok) okl = 0;
+    } else if (gfu && fwave) {
+      finish_prev();
     }
     KB_STAMP(d, 3);
     KB_STAMP(d, 4);
@@ -1700,6 +1717,10 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update, int nth) {
     KB_STAMP(d, 4);
   }
   __syncthreads();  // okl final
+  if (gfu) {
+    if (fin[0]) return;  // the loop ended at the previous pass: this solve is discarded
+    cur = fin[1];
+  }
   if (!okl) {
     if (tid == 0) {
       c->solve_ok = 0;

@@ -16,7 +16,7 @@ r = subprocess.run([B.HIPCC] + B.FLAGS + extra + ["-Rpass-analysis=kernel-resour
 cur = None
 rows = {}
 for line in r.stderr.splitlines():
-    m = re.search(r"remark: (?:\s*)([^:\[]+): (.*?) \[-Rpass", line)
+    m = re.search(r"remark:\s+(.*?): (.*?) \[-Rpass", line)
     if not m:
         continue
     k, v = m.group(1).strip(), m.group(2).strip()
