@@ -23,24 +23,31 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 
 METRIC = "Gauss-Newton iterations/sec (full J build + solve), N-cam×M-frame AprilGrid"
-BUILD_KERNEL = "void kb::k_build<2>(kb::KbDev, int, int)"
+GN_FUSED = os.environ.get("KB_GN_FUSED", "1") != "0"  # the library's pass variant (kb_create reads the same)
+
+
+def is_build_kernel(name):
+    """The pass's build kernel as rocprofv3 names it: k_build<TW, GNF> with GNF = the GN fused variant."""
+    return name.startswith("void kb::k_build<") and name.endswith(
+        (", true>(kb::KbDev, int, int)" if GN_FUSED else ", false>(kb::KbDev, int, int)"))
 FRAMES_PER_RANK = 500
 HBM_PEAK_GBS = 8000.0
 
 
-def pmc_traffic_bytes(kernel):
-    """HBM bytes per launch of `kernel` from the newest committed PMC summary (profiles/*/pmc_traffic.json,
-    written by tools/pmc_traffic.py from two separate rocprofv3 --pmc passes of this bench workload, gfx950
-    FETCH_SIZE correction applied), or None."""
+def pmc_traffic_bytes(match):
+    """HBM bytes per launch of the kernel `match(name)` selects, from the newest committed PMC summary
+    (profiles/*/pmc_traffic.json, written by tools/pmc_traffic.py from two separate rocprofv3 --pmc passes of this
+    bench workload, gfx950 FETCH_SIZE correction applied), or None."""
     import glob
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_traffic.json")), reverse=True):
         try:
             with open(path) as f:
-                k = json.load(f)["kernels"].get(kernel)
+                ks = json.load(f)["kernels"]
         except (OSError, ValueError, KeyError):
             continue
-        if k:
-            return k["hbm_bytes_per_launch"], os.path.relpath(path, ROOT)
+        for name, k in ks.items():
+            if match(name):
+                return k["hbm_bytes_per_launch"], os.path.relpath(path, ROOT)
     return None
 
 
@@ -105,10 +112,10 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         wall = float(tt.item())
 
-    # dominant kernel (k_build) timing with HIP events on the handle's stream
+    # dominant kernel (k_build) timing with HIP events on the handle's stream, inside GN passes
     build_ms, bytes_per, flops_per = g.build_kernel_stats()
     achieved = bytes_per / (build_ms * 1e-3) / 1e9
-    pmc = pmc_traffic_bytes(BUILD_KERNEL) if world == 1 else None
+    pmc = pmc_traffic_bytes(is_build_kernel) if world == 1 else None
 
     if rank == 0:
         value = world * args.steps / wall

@@ -131,8 +131,9 @@ int kb_get_trace(kb_handle* h, double* trace, int32_t cap);
 /* Benchmark entry: run exactly n_iter Gauss-Newton passes of the device loop (convergence
  * tests disabled), no host sync inside; *seconds = wall time between stream syncs. */
 int kb_run_gn_iterations(kb_handle* h, int32_t n_iter, double* seconds);
-/* Average device duration (ms) of the build kernel over the last kb_run_gn_iterations,
- * measured with HIP events on the handle's stream; algorithmic bytes per build launch. */
+/* Average device duration (ms) of the build kernel inside Gauss-Newton passes (runs 22 passes from the
+ * current state, HIP events around each build launch on the handle's stream); algorithmic bytes and
+ * flops per build launch. */
 int kb_build_kernel_stats(kb_handle* h, double* avg_ms, double* bytes_per_launch, double* flops_per_launch);
 
 /* Multi-GPU (frame sharding): each rank's handle holds its own frames;

@@ -248,11 +248,11 @@ kb_handle* kb_create(const kb_layout* L) {
   {
     const int N = h->N, C = h->C, WPB = d.wpb;
     const int CZ = 16 * ((C + 16) / 16);  // [Y | z] row stride of the Schur tiles
-    h->lds_build = sizeof(double) * (WPB * 64 * XS + WPB * 256 + N * (256 + 256 + 64 + 36 + 36 + 8) + 36 + 8 + 6 * C +
-                                     36 + 8 * CZ + 18 * N * (N - 1) + (3 * h->K <= kTargetLds ? 3 * h->K : 0) +
+    h->lds_build = sizeof(double) * (WPB * 64 * XS + WPB * 256 + N * (256 + 256 + 64 + 36 + 36 + 8) + 36 +
+                                     16 * CZ + 18 * N * (N - 1) + (3 * h->K <= kTargetLds ? 3 * h->K : 0) +
                                      8 * d.gframes);
     h->lds_camexp = sizeof(double) * (N * 256 + N * N * 36);
-    h->lds_schur = sizeof(double) * (8 * CZ + 36);
+    h->lds_schur = sizeof(double) * 16 * CZ;
     if (C <= 64) {
       h->lds_solve = sizeof(double) * (C * (C + 1) / 2 + 2 * C + 1 + N * 256 + 2 * N * N * 36) + sizeof(int) * C;
     } else {  // 16 x 16 lower tiles + panel scratch + 1/D + solution vector
@@ -618,15 +618,22 @@ struct GnFusedScope {
 
 static bool gn_fused(const kb_handle* h, int policy) { return policy == 1 && h->gn_fuse; }
 
-static int enqueue_pass(kb_handle* h, int policy) {
+// ev0 / ev1 (optional): HIP events recorded around the build kernel (kb_build_kernel_stats)
+static int enqueue_pass(kb_handle* h, int policy, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr) {
   KbDev& d = h->d;
+  auto build = [&]() -> int {
+    if (ev0) KB_HIP(hipEventRecord(ev0, h->stream));
+    if (launch_build(h, 1, 1)) return -1;
+    if (ev1) KB_HIP(hipEventRecord(ev1, h->stream));
+    return 0;
+  };
   if (gn_fused(h, policy)) {
     GnFusedScope scope(h, true);
     const bool from_rows = h->d.Wp <= 2048;
-    if (launch_build(h, 1, 1) || launch_colsum(h, 1, !from_rows) || launch_solve(h, 1, 1, from_rows)) return -1;
+    if (build() || launch_colsum(h, 1, !from_rows) || launch_solve(h, 1, 1, from_rows)) return -1;
     return 0;
   }
-  if (launch_build(h, 1, 1)) return -1;
+  if (build()) return -1;
   if (policy == 0 && launch_schur(h, 1)) return -1;  // LM passes that keep the system (lambda change)
   // small partial row: k_solve sums the stage-1 rows while staging (one launch less; sharded, the rows are
   // all-reduced as they are); otherwise k_colfin finishes the rows in parallel (then one row is all-reduced)
@@ -795,37 +802,38 @@ int kb_run_gn_iterations(kb_handle* h, int32_t n_iter, double* seconds) {
 
 int kb_build_kernel_stats(kb_handle* h, double* avg_ms, double* bytes_per_launch, double* flops_per_launch) {
   if (!h) return fail("null handle");
+  if (!h->uploaded) return fail("kb_build_kernel_stats: no observations");
   KB_HIP(hipSetDevice(h->device));
-  const int reps = 20;
-  hipEvent_t e0, e1;
-  KB_HIP(hipEventCreate(&e0));
-  KB_HIP(hipEventCreate(&e1));
-  // warm; the timed launches are the fused build + Schur step exactly as one GN pass runs it
-  hipLaunchKernelGGL(k_pre, dim3(1), dim3(256), 0, h->stream, h->d, 0);
-  KbDev dd = h->d;
-  dd.host_lambda = 0.0;  // GN pass: no conditioner
-  int g0 = 0, f1 = 1;
-  void* args[] = {&dd, &g0, &f1};
-  KB_HIP(hipLaunchKernel(h->fn_build, dim3(h->d.nblk), dim3(64 * h->d.wpb), args, h->lds_build, h->stream));
+  // Gauss-Newton passes from the current state, launched eagerly with HIP events around each build kernel: the
+  // timed launches are the build exactly as it runs inside the pass (frame steps of the previous solve applied)
+  const int reps = 20, warm = 2;
+  if (ensure_trace(h, 64)) return -1;
+  KbOpts o{1, 0x3fffffff, 0.0, -1.0, -1.0};
+  if (loop_start(h, o)) return -1;
+  std::vector<hipEvent_t> ev(2 * (reps + warm));
+  for (auto& e : ev) KB_HIP(hipEventCreate(&e));
+  for (int r = 0; r < reps + warm; ++r)
+    if (enqueue_pass(h, 1, ev[2 * r], ev[2 * r + 1])) return -1;
+  if (finish_pass(h, 1)) return -1;
+  KB_HIP(hipStreamSynchronize(h->stream));
   double tot = 0.0;
-  for (int r = 0; r < reps; ++r) {
-    KB_HIP(hipEventRecord(e0, h->stream));
-    KB_HIP(hipLaunchKernel(h->fn_build, dim3(h->d.nblk), dim3(64 * h->d.wpb), args, h->lds_build, h->stream));
-    KB_HIP(hipEventRecord(e1, h->stream));
-    KB_HIP(hipEventSynchronize(e1));
+  for (int r = warm; r < reps + warm; ++r) {
     float ms = 0.f;
-    KB_HIP(hipEventElapsedTime(&ms, e0, e1));
+    KB_HIP(hipEventElapsedTime(&ms, ev[2 * r], ev[2 * r + 1]));
     tot += ms;
   }
-  hipEventDestroy(e0);
-  hipEventDestroy(e1);
+  for (auto& e : ev) hipEventDestroy(e);
+  KbCtrl ctrl{};
+  KB_HIP(hipMemcpy(&ctrl, h->d.ctrl, sizeof(KbCtrl), hipMemcpyDeviceToHost));
+  h->cur = ctrl.cur;
   h->build_ms = tot / reps;
   if (avg_ms) *avg_ms = h->build_ms;
   // algorithmic bytes of one launch: observations (y 16 B + corner id 2 B per corner), view ranges (8 B per
-  // frame x camera), state and camera chains read; frame blocks (H_ff, g_f, H_fc), Schur factors (L, Y, z)
-  // and the per-block partial rows written.
-  const double bytes = 18.0 * h->NC + 8.0 * h->F * h->N + 8.0 * h->S + 8.0 * (12.0 * h->N + 36.0 * h->N * h->N) +
-                       8.0 * h->F * (36 + 6 + 6.0 * h->C) + 8.0 * h->F * (36 + 6 + 6.0 * h->C) +
+  // frame x camera), state and camera chains read; the previous step (dx_c, A_f, b_f) read; frame blocks
+  // (H_ff, g_f, H_fc), back-substitution rows (A_f, b_f), candidate poses and the per-block partial rows written.
+  const double C = h->C, F = h->F;
+  const double bytes = 18.0 * h->NC + 8.0 * F * h->N + 8.0 * h->S + 8.0 * (12.0 * h->N + 36.0 * h->N * h->N) +
+                       8.0 * (C + F * (6 * C + 6)) + 8.0 * F * (36 + 6 + 6 * C) + 8.0 * F * (6 * C + 6 + 7) +
                        8.0 * h->d.nblk * h->d.Wr;
   if (bytes_per_launch) *bytes_per_launch = bytes;
   // executed MFMA flops (2 x 16 x 16 x rows, rows padded to 64 per 32-corner phase) + ~300 VALU flops/corner

@@ -399,46 +399,19 @@ __global__ void __launch_bounds__(256) k_pre(KbDev d, int gate) {
   chain_block(d, d.state + (size_t)cur * d.S + d.off_base, cur, blockDim.x);
 }
 
-// 6x6 Cholesky of A + lam2 I by one wave (lanes 0..5 hold rows; column k broadcast with v_readlane):
-// L (row-major lower, upper zero) and 1/diag(L) to LDS.  Returns false if not PD.
-__device__ __forceinline__ bool chol6_wave(const double* A, double lam2, double* L, double* rdiag, int lane) {
-  double row[6];
-  const int i = lane < 6 ? lane : 5;
-#pragma unroll
-  for (int j = 0; j < 6; ++j) row[j] = A[i * 6 + j] + ((i == j) ? lam2 : 0.0);
-  bool ok = true;
-#pragma unroll
-  for (int k = 0; k < 6; ++k) {
-    const double dkk = readlane_d(row[k], k);
-    ok = ok && (dkk > 0.0);
-    const double sk = sqrt(dkk), rk = 1.0 / sk;
-    row[k] = (lane == k) ? sk : ((lane > k) ? row[k] * rk : row[k]);
-    if (lane == k) rdiag[k] = rk;
-    const double lik = (lane > k) ? row[k] : 0.0;
-#pragma unroll
-    for (int j = k + 1; j < 6; ++j) row[j] -= lik * readlane_d(row[k], j);
-  }
-  if (lane < 6)
-#pragma unroll
-    for (int j = 0; j < 6; ++j) {
-      L[lane * 6 + j] = (j <= lane) ? row[j] : 0.0;
-    }
-  return ok;
-}
-
-// Schur sums of a block on MFMA: [Y | z] (8 x CZ in LDS, rows 6..7 and columns > C zero, CZ = 16 nbz,
-// nbz = ceil((C + 1) / 16)); wave w owns lower tiles q = w, w + nw, ... (at most TW) and accumulates
-// acc[t] += Y_ii^T Y_jj over the block's frames (two 16x16x4 steps per frame).  Tile entry (r, c) is
-// sum_k [Y|z][k][r] [Y|z][k][c]: r, c < C -> sum Y^T Y, r == C -> sum Y^T z.
+// Schur sums of a block on MFMA: P = [H_fc | g_f] and Q = [A | b] (8 x CZ in LDS, rows 6..7 and columns > C
+// zero, CZ = 16 nbz, nbz = ceil((C + 1) / 16)); wave w owns lower tiles q = w, w + nw, ... (at most TW) and
+// accumulates acc[t] += P_ii^T Q_jj over the block's frames (two 16x16x4 steps per frame).  Tile entry (r, c)
+// is sum_k P[k][r] Q[k][c]: r, c < C -> H_fc^T H_ff^-1 H_fc, r == C -> g_f^T H_ff^-1 H_fc = (H_fc^T b)^T.
 template <int TW>
-__device__ __forceinline__ void schur_tiles_accumulate(const double* Y, int CZ, const int* tii, const int* tjj,
-                                                       v4d* acc) {
+__device__ __forceinline__ void schur_tiles_accumulate(const double* P, const double* Q, int CZ, const int* tii,
+                                                       const int* tjj, v4d* acc) {
   const int lane = threadIdx.x & 63;
 #pragma unroll
   for (int t = 0; t < TW; ++t) {
     if (tii[t] < 0) break;  // wave-uniform
-    const double* ya = Y + 16 * tii[t] + (lane & 15);
-    const double* yb = Y + 16 * tjj[t] + (lane & 15);
+    const double* ya = P + 16 * tii[t] + (lane & 15);
+    const double* yb = Q + 16 * tjj[t] + (lane & 15);
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int k = 4 * s + (lane >> 4);
@@ -479,36 +452,56 @@ __device__ __forceinline__ void schur_tiles_store(double* prow_schur, int C, con
   }
 }
 
-// Y = L^-1 H_fc (thread per column), z = L^-1 g_f (last thread) into [Y | z] (row stride CZ); to HBM the frame
-// back-substitution rows A_f = L^-T Y and b_f = L^-T z, so that dx_f = L^-T (z - Y dx_c) = b_f - A_f dx_c
-// (solveSystem's frame block of the Schur solve) is one row-times-vector per frame in the next kernel
-__device__ __forceinline__ void schur_forward(const KbDev& d, int f, const double* L, const double* rdiag,
-                                              const double* Hfc_lds, const double* g_lds, double* Y, int CZ) {
-  const int C = d.C, t = threadIdx.x;
-  const bool col = t < C;
-  if (col || t == (int)blockDim.x - 1) {
-    double yv[6], av[6];
+// Gauss-Jordan elimination of [H_ff + lam2 I | H_fc | g_f] by one wave, lanes = columns (slot s: column
+// lane + 64 s), rows 0..5 in registers; pivot column k broadcast with v_readlane.  No pivoting: H_ff is SPD,
+// the pivots are the squared Cholesky diagonal (all > 0 iff positive definite).  Ends with [I | A | b]:
+// A = (H_ff + lam2 I)^-1 H_fc, b = (H_ff + lam2 I)^-1 g_f (solveSystem's frame blocks of the Schur solve)
+// into Q (row stride CZ) and HBM.  P holds rows 0..5 of [H_fc | g_f] (stride CZ).  Returns false if not PD.
+__device__ __forceinline__ bool frame_gj(const KbDev& d, int f, const double* Hff, double lam2, const double* P,
+                                         double* Q, int CZ, int lane) {
+  const int C = d.C;
+  double col[2][6];
 #pragma unroll
-    for (int r = 0; r < 6; ++r) {
-      double s2 = col ? (Hfc_lds ? Hfc_lds[r * C + t] : d.Hfc[((size_t)f * 6 + r) * C + t])
-                      : (g_lds ? g_lds[r] : d.gf[(size_t)f * 6 + r]);
+  for (int sl = 0; sl < 2; ++sl) {
+    const int q = lane + 64 * sl, qh = min(q, 5), qp = min(max(q - 6, 0), C);
 #pragma unroll
-      for (int k = 0; k < r; ++k) s2 -= L[r * 6 + k] * yv[k];
-      yv[r] = s2 * rdiag[r];
-      Y[r * CZ + (col ? t : C)] = yv[r];
-    }
-#pragma unroll
-    for (int r = 5; r >= 0; --r) {
-      double s2 = yv[r];
-#pragma unroll
-      for (int k = r + 1; k < 6; ++k) s2 -= L[k * 6 + r] * av[k];
-      av[r] = s2 * rdiag[r];
-      if (col)
-        d.Af[((size_t)f * 6 + r) * C + t] = av[r];
-      else
-        d.bf[(size_t)f * 6 + r] = av[r];
+    for (int i = 0; i < 6; ++i) {
+      const double h = Hff[i * 6 + qh] + (i == qh ? lam2 : 0.0), pv = P[i * CZ + qp];
+      col[sl][i] = q < 6 ? h : (q - 6 <= C ? pv : 0.0);
     }
   }
+  bool ok = true;
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    double a[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) a[i] = readlane_d(col[0][i], k);  // column k (lane k, slot 0)
+    ok = ok && (a[k] > 0.0);
+    const double r = 1.0 / a[k];
+#pragma unroll
+    for (int sl = 0; sl < 2; ++sl) {
+      const double ck = col[sl][k] * r;
+#pragma unroll
+      for (int i = 0; i < 6; ++i)
+        if (i != k) col[sl][i] -= a[i] * ck;
+      col[sl][k] = ck;
+    }
+  }
+#pragma unroll
+  for (int sl = 0; sl < 2; ++sl) {
+    const int c = lane + 64 * sl - 6;
+    if (c >= 0 && c <= C) {
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        Q[i * CZ + c] = col[sl][i];
+        if (c < C)
+          d.Af[((size_t)f * 6 + i) * C + c] = col[sl][i];
+        else
+          d.bf[(size_t)f * 6 + i] = col[sl][i];
+      }
+    }
+  }
+  return ok;
 }
 
 // dx_f = b_f - A_f dx_c.  Lane slot sl holds column lane + 64 sl of A_f (zero beyond C); lanes 0..5 hold b_f.
@@ -588,18 +581,15 @@ __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
   double* dH = Pv + N * 36;          // [N][36]  G^T H_dd G
   double* dg = dH + N * 36;          // [N][8]   G^T g_d
   double* Fh = dg + N * 8;           // frame H_ff [36]
-  double* Fg = Fh + 36;              // frame g_f [8]
-  double* Fc = Fg + 8;               // frame H_fc [6][C]
-  double* L = Fc + 6 * C;            // [36]
   const int nbz = (C + 16) >> 4, CZ = 16 * nbz;
-  double* Y = L + 36;                // [8][CZ]: [Y | z] of the current frame, zero-padded
-  double* Kl = Y + 8 * CZ;           // [N(N-1)/2][36] K_{i,j}, j < i, at (i(i-1)/2 + j)
+  double* P = Fh + 36;               // [8][CZ]: [H_fc | g_f] of the current frame, zero-padded
+  double* Q = P + 8 * CZ;            // [8][CZ]: [A | b] (frame_gj), zero-padded
+  double* Kl = Q + 8 * CZ;           // [N(N-1)/2][36] K_{i,j}, j < i, at (i(i-1)/2 + j)
   double* tg = Kl + 18 * N * (N - 1);  // [n_target][3] target corners (when staged)
   __shared__ double wmx[8];            // GN fused: per-wave max |dx_f|
   __shared__ int okl;
   __shared__ double cst[KB_MAX_CAMS][24];  // per camera: chain L (12) | intrinsics (10)
   __shared__ int ctab[2][KB_MAX_CAMS];      // per camera: first intrinsic column | baseline column
-  __shared__ double rdg[6];
   const int W = d.W, Wt = W - C;
   const int f0 = blockIdx.x * d.gframes, f1 = min(d.F, f0 + d.gframes);
   const int cam = __builtin_amdgcn_readfirstlane(wave % N), sp = __builtin_amdgcn_readfirstlane(wave / N);
@@ -732,8 +722,8 @@ __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
 #pragma unroll
   for (int t = 0; t < TW; ++t) acc[t] = v4d{0.0, 0.0, 0.0, 0.0};
   schur_tiles_assign<TW>(fuse ? nbz : 0, tii, tjj);
-  for (int q = tid; q < 8 * CZ; q += nth)  // [Y | z] padding (rows 6, 7 and columns > C stay zero)
-    if (q >= 6 * CZ || (q % CZ) > C) Y[q] = 0.0;
+  for (int q = tid; q < 8 * CZ; q += nth)  // P, Q padding (rows 6, 7 and columns > C stay zero)
+    if (q >= 6 * CZ || (q % CZ) > C) P[q] = Q[q] = 0.0;
   if (tid == 0) okl = 1;
   KB_STAMP(d, 16);
   for (int q = tid; q < N * 256; q += nth) camsum[q] = 0.0;
@@ -889,7 +879,7 @@ __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
 #pragma unroll
         for (int k = 0; k < 6; ++k) sacc += G[k * 6 + a] * H[k * 16 + 6 + q];
         sacc = has ? sacc : 0.0;  // G^T H_dI
-        Fc[a * C + ctab[0][vc] + q] = sacc;
+        P[a * CZ + ctab[0][vc] + q] = sacc;
         d.Hfc[((size_t)f * 6 + a) * C + ctab[0][vc] + q] = sacc;
       }
     }
@@ -904,7 +894,7 @@ __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
       } else if (q < 42) {
         double sacc = 0.0;
         for (int i = 0; i < N; ++i) sacc += dg[i * 8 + q - 36];
-        Fg[q - 36] = sacc;
+        P[(q - 36) * CZ + C] = sacc;
         d.gf[(size_t)f * 6 + q - 36] = sacc;
       } else {  // H_f,B_j = sum_{i > j} P_i K_{i,j}
         const int e = q - 42, j = e / 36, ab2 = e % 36, a = ab2 / 6, b = ab2 % 6;
@@ -914,7 +904,7 @@ __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
 #pragma unroll
           for (int k = 0; k < 6; ++k) sacc += Pv[i * 36 + a * 6 + k] * K[k * 6 + b];
         }
-        Fc[a * C + ctab[1][j] + b] = sacc;
+        P[a * CZ + ctab[1][j] + b] = sacc;
         d.Hfc[((size_t)f * 6 + a) * C + ctab[1][j] + b] = sacc;
       }
     }
@@ -923,15 +913,12 @@ __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
       __syncthreads();
       KB_STAMP(d, 21);
       if (wave == 0) {
-        const bool ok = chol6_wave(Fh, lam2, L, rdg, lane);
+        const bool ok = frame_gj(d, f, Fh, lam2, P, Q, CZ, lane);
         if (!ok && lane == 0) okl = 0;
       }
       __syncthreads();
-      KB_STAMP(d, 22);
-      schur_forward(d, f, L, rdg, Fc, Fg, Y, CZ);
-      __syncthreads();
       KB_STAMP(d, 23);
-      schur_tiles_accumulate<TW>(Y, CZ, tii, tjj, acc);
+      schur_tiles_accumulate<TW>(P, Q, CZ, tii, tjj, acc);
     }
     __syncthreads();
     KB_STAMP(d, 24);
@@ -963,12 +950,11 @@ __global__ void __launch_bounds__(256) k_schur(KbDev d, int gate) {
   KbCtrl* c = d.ctrl;
   if (gate && (c->done || c->do_build)) return;  // rebuild passes ran it fused in k_build
   extern __shared__ __attribute__((aligned(16))) double sm[];
-  const int C = d.C, W = d.W, Wt = W - C, N = d.N;
+  const int C = d.C, W = d.W, N = d.N;
   const int nbz = (C + 16) >> 4, CZ = 16 * nbz;
-  double* Y = sm;          // [8][CZ]: [Y | z], zero-padded
-  double* L = Y + 8 * CZ;  // [36]
+  double* P = sm;           // [8][CZ]: [H_fc | g_f], zero-padded
+  double* Q = P + 8 * CZ;   // [8][CZ]: [A | b], zero-padded
   __shared__ int okl;
-  __shared__ double rdg[6];
   const double lam = gate ? c->lambda : d.host_lambda;
   const double lam2 = lam * lam;
   v4d acc[TW];
@@ -977,19 +963,22 @@ __global__ void __launch_bounds__(256) k_schur(KbDev d, int gate) {
   for (int t = 0; t < TW; ++t) acc[t] = v4d{0.0, 0.0, 0.0, 0.0};
   schur_tiles_assign<TW>(nbz, tii, tjj);
   for (int q = threadIdx.x; q < 8 * CZ; q += blockDim.x)
-    if (q >= 6 * CZ || (q % CZ) > C) Y[q] = 0.0;
+    if (q >= 6 * CZ || (q % CZ) > C) P[q] = Q[q] = 0.0;
   if (threadIdx.x == 0) okl = 1;
   const int f0 = blockIdx.x * d.gframes, f1 = min(d.F, f0 + d.gframes);
   for (int f = f0; f < f1; ++f) {
     __syncthreads();
+    for (int q = threadIdx.x; q < 6 * (C + 1); q += blockDim.x) {  // [H_fc | g_f] of frame f
+      const int i = q / (C + 1), cc = q % (C + 1);
+      P[i * CZ + cc] = cc < C ? d.Hfc[((size_t)f * 6 + i) * C + cc] : d.gf[(size_t)f * 6 + i];
+    }
+    __syncthreads();
     if (threadIdx.x < 64) {
-      const bool ok = chol6_wave(d.Hff + (size_t)f * 36, lam2, L, rdg, threadIdx.x);
+      const bool ok = frame_gj(d, f, d.Hff + (size_t)f * 36, lam2, P, Q, CZ, threadIdx.x);
       if (!ok && threadIdx.x == 0) okl = 0;
     }
     __syncthreads();
-    schur_forward(d, f, L, rdg, nullptr, nullptr, Y, CZ);
-    __syncthreads();
-    schur_tiles_accumulate<TW>(Y, CZ, tii, tjj, acc);
+    schur_tiles_accumulate<TW>(P, Q, CZ, tii, tjj, acc);
   }
   double* prow = d.part + (size_t)blockIdx.x * d.Wr + N * 136;
   schur_tiles_store<TW>(prow, C, tii, tjj, acc);
