@@ -11,5 +11,5 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $R/gpurun_ou
 echo "fetch ok"
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $R/gpurun_out/pmc_write -o pmc -- python3 bench.py --steps 20 --warmup 2 --no-cpu-baseline > gpurun_out/pmc_write.log 2>&1 || exit $?
 echo "write ok"
-find gpurun_out/pmc_fetch gpurun_out/pmc_write -name "*.csv" | head
-python3 tools/prof_summary.py gpurun_out/prof | head -12
+find gpurun_out/pmc_fetch gpurun_out/pmc_write -name "*.csv"
+python3 tools/prof_summary.py gpurun_out/prof

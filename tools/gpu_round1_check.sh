@@ -12,5 +12,5 @@ timeout -k 10 300 python bench.py --steps 200 --warmup 20 > gpurun_out/bench.log
 if [ $rc -ne 0 ]; then exit $rc; fi
 export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof -o bench -- python3 bench.py --steps 200 --warmup 20 --no-cpu-baseline > gpurun_out/prof.log 2>&1; rc=$?; echo "rocprof rc=$rc"
-find gpurun_out/prof -name "*stats*" | head
+find gpurun_out/prof -name "*stats*"
 exit $rc
