@@ -37,7 +37,10 @@ enum kb_camera_model {
   KB_PINHOLE_RADTAN = 0, /* DistortedPinhole: fu fv cu cv | k1 k2 p1 p2 */
   KB_OMNI_RADTAN = 1,    /* DistortedOmni:    xi fu fv cu cv | k1 k2 p1 p2 */
   KB_EUCM = 2,           /* ExtendedUnified:  alpha beta fu fv cu cv */
-  KB_OMNI = 3            /* Omni:             xi fu fv cu cv */
+  KB_OMNI = 3,           /* Omni:             xi fu fv cu cv */
+  KB_DS = 4,             /* DoubleSphere:     xi alpha fu fv cu cv */
+  KB_PINHOLE_EQUI = 5,   /* EquidistantPinhole: fu fv cu cv | k1 k2 k3 k4 */
+  KB_PINHOLE_FOV = 6     /* FovPinhole:       fu fv cu cv | w */
 };
 
 typedef struct kb_handle kb_handle;

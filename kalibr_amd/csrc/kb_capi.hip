@@ -43,6 +43,9 @@ int nintr_host(int m) {
     case KB_OMNI_RADTAN: return 9;
     case KB_EUCM: return 6;
     case KB_OMNI: return 5;
+    case KB_DS: return 6;
+    case KB_PINHOLE_EQUI: return 8;
+    case KB_PINHOLE_FOV: return 5;
     default: return -1;
   }
 }

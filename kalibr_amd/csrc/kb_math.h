@@ -4,7 +4,9 @@
 //   quaternion algebra  Schweizer-Messer/sm_kinematics/src/quaternion_algebra.cpp:77-101,200-220,302-315
 //   camera projections  aslam_cv/aslam_cameras/include/aslam/cameras/implementation/
 //                        PinholeProjection.hpp:99-145,310-378; RadialTangentialDistortion.hpp:28-65,152-182;
-//                        OmniProjection.hpp:117-183,383-445; ExtendedUnifiedProjection.hpp:131-198,399-457
+//                        OmniProjection.hpp:117-183,383-445; ExtendedUnifiedProjection.hpp:131-198,399-457;
+//                        DoubleSphereProjection.hpp:140-221,443-505; EquidistantDistortion.hpp:31-200,244-273;
+//                        FovDistortion.hpp:19-83,130-168
 // (paths relative to the reference repository).  Written once for the device; the CPU
 // oracle under oracle/ is an independent restatement used only as the checker.
 #pragma once
@@ -48,7 +50,64 @@ __device__ __forceinline__ void update_pose(const double* in, const double* d6, 
 }
 
 __device__ __forceinline__ int model_nintr(int m) {
-  return m == KB_PINHOLE_RADTAN ? 8 : m == KB_OMNI_RADTAN ? 9 : m == KB_EUCM ? 6 : 5;
+  return (m == KB_PINHOLE_RADTAN || m == KB_PINHOLE_EQUI) ? 8 : m == KB_OMNI_RADTAN ? 9
+         : (m == KB_EUCM || m == KB_DS)                   ? 6 : 5;
+}
+
+// Equidistant: y *= thetad / r, theta = atan r (scaling 1 for r <= 1e-8).  Jd = d(y')/dy (2x2, row-major),
+// Jk = d(y')/dk (2x4, row-major), both evaluated at the undistorted y, as the reference does.
+__device__ __forceinline__ void equi(const double* k, double& x, double& y, double* Jd, double* Jk) {
+  const double r2 = x * x + y * y, r = sqrt(r2), th = atan(r), t2 = th * th;
+  const double P = 1.0 + t2 * (k[0] + t2 * (k[1] + t2 * (k[2] + t2 * k[3])));
+  const double thd = th * P;
+  if (Jd) {
+    const double dP = 1.0 + t2 * (3.0 * k[0] + t2 * (5.0 * k[1] + t2 * (7.0 * k[2] + t2 * 9.0 * k[3])));
+    const double s = thd / r, g = (dP / (1.0 + r2) - s) / r2;
+    Jd[0] = s + x * x * g;
+    Jd[1] = x * y * g;
+    Jd[2] = Jd[1];
+    Jd[3] = s + y * y * g;
+    const double a = th * t2 / r, b = a * t2, c = b * t2, e = c * t2;
+    Jk[0] = x * a; Jk[1] = x * b; Jk[2] = x * c; Jk[3] = x * e;
+    Jk[4] = y * a; Jk[5] = y * b; Jk[6] = y * c; Jk[7] = y * e;
+  }
+  const double sc = (r > 1e-8) ? thd / r : 1.0;
+  x *= sc;
+  y *= sc;
+}
+
+// FOV: y *= atan(2 tan(w/2) r) / (w r), with the reference's limits (w^2 < 1e-5: identity; r^2 < 1e-5: constant
+// scale 2 tan(w/2)/w, constant w column (w - sin w)/(w^2 cos^2(w/2)) in both rows).  Jw = d(y')/dw (2).
+__device__ __forceinline__ void fov(double w, double& x, double& y, double* Jd, double* Jw) {
+  const double u = x, v = y, r2 = u * u + v * v, r = sqrt(r2);
+  const double tw = tan(0.5 * w), tw2 = tw * tw;
+  double s;
+  if (w * w < 1e-5) {
+    s = 1.0;
+    if (Jd) { Jd[0] = 1.0; Jd[1] = 0.0; Jd[2] = 0.0; Jd[3] = 1.0; Jw[0] = 0.0; Jw[1] = 0.0; }
+  } else if (r2 < 1e-5) {
+    s = 2.0 * tw / w;
+    if (Jd) {
+      const double c = cos(0.5 * w);
+      Jd[0] = s; Jd[1] = 0.0; Jd[2] = 0.0; Jd[3] = s;
+      Jw[0] = Jw[1] = (w - sin(w)) / (w * w * c * c);
+    }
+  } else {
+    const double den = 1.0 / (w * (1.0 + 4.0 * tw2 * r2));
+    s = atan(2.0 * tw * r) / (r * w);
+    if (Jd) {
+      const double q = (2.0 * tw * den - s) / r2;
+      Jd[0] = s + u * u * q;
+      Jd[1] = u * v * q;
+      Jd[2] = Jd[1];
+      Jd[3] = s + v * v * q;
+      const double ds = (1.0 + tw2) * den - s / w;
+      Jw[0] = u * ds;
+      Jw[1] = v * ds;
+    }
+  }
+  x = u * s;
+  y = v * s;
 }
 
 __device__ __forceinline__ void radtan(const double* d, double& x, double& y, double* Jd) {
@@ -92,12 +151,27 @@ __device__ __forceinline__ void project(int model, const double* in, double px, 
     if (model == KB_OMNI_RADTAN) radtan_only(in + 5, x, y);
     u = in[1] * x + in[3];
     v = in[2] * y + in[4];
-  } else {  // EUCM
+  } else if (model == KB_EUCM) {
     const double al = in[0], be = in[1];
     const double d = sqrt(be * (px * px + py * py) + pz * pz);
     const double ninv = 1.0 / (al * d + (1 - al) * pz);
     u = in[2] * (px * ninv) + in[4];
     v = in[3] * (py * ninv) + in[5];
+  } else if (model == KB_DS) {
+    const double xi = in[0], al = in[1], r2 = px * px + py * py;
+    const double k = xi * sqrt(r2 + pz * pz) + pz;
+    const double ninv = 1.0 / (al * sqrt(r2 + k * k) + (1 - al) * k);
+    u = in[2] * (px * ninv) + in[4];
+    v = in[3] * (py * ninv) + in[5];
+  } else {  // pinhole + equidistant / FOV
+    const double rz = 1.0 / pz;
+    double x = px * rz, y = py * rz;
+    if (model == KB_PINHOLE_EQUI)
+      equi(in + 4, x, y, nullptr, nullptr);
+    else
+      fov(in[4], x, y, nullptr, nullptr);
+    u = in[0] * x + in[2];
+    v = in[1] * y + in[3];
   }
 }
 
@@ -160,7 +234,7 @@ __device__ __forceinline__ void project_jac(int model, const double* in, double 
     }
     u = fu * x + in[3];
     v = fv * y + in[4];
-  } else {  // EUCM
+  } else if (model == KB_EUCM) {
     const double al = in[0], be = in[1], fu = in[2], fv = in[3];
     const double xx = px * px, yy = py * py, r2 = xx + yy;
     const double d = sqrt(be * r2 + pz * pz), d_inv = 1.0 / d;
@@ -184,6 +258,55 @@ __device__ __forceinline__ void project_jac(int model, const double* in, double 
     Ji[KB_MAX_INTR + 3] = my; Ji[KB_MAX_INTR + 4] = 0.0; Ji[KB_MAX_INTR + 5] = 1.0;
     u = fu * mx + in[4];
     v = fv * my + in[5];
+  } else if (model == KB_DS) {
+    const double xi = in[0], al = in[1], fu = in[2], fv = in[3];
+    const double r2 = px * px + py * py, d1 = sqrt(r2 + pz * pz), d1_inv = 1.0 / d1;
+    const double k = xi * d1 + pz, d2 = sqrt(r2 + k * k), d2_inv = 1.0 / d2;
+    const double ninv = 1.0 / (al * d2 + (1 - al) * k), ninv2 = ninv * ninv;
+    const double mx = px * ninv, my = py * ninv;
+    const double tt2 = xi * pz * d1_inv + 1;
+    const double dn = (xi * (1 - al) * d1_inv + al * (xi * k * d1_inv + 1) * d2_inv) * ninv2;
+    const double t2 = ((1 - al) * tt2 + al * k * tt2 * d2_inv) * ninv2;
+    Jp[0] = fu * (ninv - px * px * dn);
+    Jp[1] = -fu * px * py * dn;
+    Jp[2] = -fu * px * t2;
+    Jp[3] = -fv * px * py * dn;
+    Jp[4] = fv * (ninv - py * py * dn);
+    Jp[5] = -fv * py * t2;
+    const double t4 = (al - 1 - al * k * d2_inv) * d1 * ninv2, t5 = (k - d2) * ninv2;
+    Ji[0] = fu * px * t4; Ji[1] = fu * px * t5; Ji[2] = mx; Ji[3] = 0.0; Ji[4] = 1.0; Ji[5] = 0.0;
+    Ji[KB_MAX_INTR + 0] = fv * py * t4; Ji[KB_MAX_INTR + 1] = fv * py * t5; Ji[KB_MAX_INTR + 2] = 0.0;
+    Ji[KB_MAX_INTR + 3] = my; Ji[KB_MAX_INTR + 4] = 0.0; Ji[KB_MAX_INTR + 5] = 1.0;
+    u = fu * mx + in[4];
+    v = fv * my + in[5];
+  } else {  // pinhole + equidistant (4 distortion columns) / FOV (1)
+    const double fu = in[0], fv = in[1];
+    const double rz = 1.0 / pz, rz2 = rz * rz;
+    double x = px * rz, y = py * rz, Jd[4], Jk[8];
+    if (model == KB_PINHOLE_EQUI)
+      equi(in + 4, x, y, Jd, Jk);
+    else
+      fov(in[4], x, y, Jd, Jk);
+    Jp[0] = fu * Jd[0] * rz;
+    Jp[1] = fu * Jd[1] * rz;
+    Jp[2] = -fu * (px * Jd[0] + py * Jd[1]) * rz2;
+    Jp[3] = fv * Jd[2] * rz;
+    Jp[4] = fv * Jd[3] * rz;
+    Jp[5] = -fv * (px * Jd[2] + py * Jd[3]) * rz2;
+    Ji[0] = x; Ji[1] = 0.0; Ji[2] = 1.0; Ji[3] = 0.0;
+    Ji[KB_MAX_INTR + 0] = 0.0; Ji[KB_MAX_INTR + 1] = y; Ji[KB_MAX_INTR + 2] = 0.0; Ji[KB_MAX_INTR + 3] = 1.0;
+    if (model == KB_PINHOLE_EQUI) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        Ji[4 + c] = Jk[c] * fu;
+        Ji[KB_MAX_INTR + 4 + c] = Jk[4 + c] * fv;
+      }
+    } else {
+      Ji[4] = Jk[0] * fu;
+      Ji[KB_MAX_INTR + 4] = Jk[1] * fv;
+    }
+    u = fu * x + in[2];
+    v = fv * y + in[3];
   }
 }
 

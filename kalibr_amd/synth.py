@@ -26,8 +26,12 @@ PINHOLE_RADTAN = 0
 OMNI_RADTAN = 1
 EUCM = 2
 OMNI = 3
-MODEL_NAMES = {PINHOLE_RADTAN: "pinhole-radtan", OMNI_RADTAN: "omni-radtan", EUCM: "eucm", OMNI: "omni"}
-NINTR = {PINHOLE_RADTAN: 8, OMNI_RADTAN: 9, EUCM: 6, OMNI: 5}
+DS = 4
+PINHOLE_EQUI = 5
+PINHOLE_FOV = 6
+MODEL_NAMES = {PINHOLE_RADTAN: "pinhole-radtan", OMNI_RADTAN: "omni-radtan", EUCM: "eucm", OMNI: "omni",
+               DS: "ds", PINHOLE_EQUI: "pinhole-equi", PINHOLE_FOV: "pinhole-fov"}
+NINTR = {PINHOLE_RADTAN: 8, OMNI_RADTAN: 9, EUCM: 6, OMNI: 5, DS: 6, PINHOLE_EQUI: 8, PINHOLE_FOV: 5}
 
 
 def aprilgrid_points(tag_rows=5, tag_cols=6, tag_size=0.088, tag_spacing=0.2954):
@@ -130,6 +134,34 @@ def project(model, intr, p):
         n = al * d + (1 - al) * z
         mx, my = x / n, y / n
         dist = False
+    elif model == DS:
+        xi, al, fu, fv, cu, cv = intr[:6]
+        r2 = x * x + y * y
+        d1 = np.sqrt(r2 + z * z)
+        t = al / (1 - al) if al <= 0.5 else (1 - al) / al
+        fovp = (t + xi) / np.sqrt(2 * t * xi + xi * xi + 1)
+        valid = z > -(fovp * d1)
+        k = xi * d1 + z
+        n = al * np.sqrt(r2 + k * k) + (1 - al) * k
+        mx, my = x / n, y / n
+        dist = False
+    elif model in (PINHOLE_EQUI, PINHOLE_FOV):
+        fu, fv, cu, cv = intr[:4]
+        mx, my = x / z, y / z
+        valid = z > 0
+        r = np.sqrt(mx * mx + my * my)
+        if model == PINHOLE_EQUI:
+            k1, k2, k3, k4 = intr[4:8]
+            th = np.arctan(r)
+            t2 = th * th
+            thd = th * (1 + t2 * (k1 + t2 * (k2 + t2 * (k3 + t2 * k4))))
+            sc = np.where(r > 1e-8, thd / np.maximum(r, 1e-300), 1.0)
+        else:
+            w = intr[4]
+            tw = np.tan(w / 2)
+            sc = np.where(r * r < 1e-5, 2 * tw / w, np.arctan(2 * tw * r) / (np.maximum(r, 1e-300) * w))
+        mx, my = mx * sc, my * sc
+        dist = False
     else:
         raise ValueError(model)
     if dist:
@@ -227,6 +259,12 @@ def make_problem(models, n_frames, seed, p_view=1.0, noise_px=0.3, min_corners=1
             intr_truth[i, :5] = [0.9, 450.0, 450.0, 640.0, 512.0]
         elif m == EUCM:
             intr_truth[i, :6] = [0.6, 1.1, 450.0, 450.0, 640.0, 512.0]
+        elif m == DS:
+            intr_truth[i, :6] = [-0.2, 0.6, 400.0, 400.0, 640.0, 512.0]
+        elif m == PINHOLE_EQUI:
+            intr_truth[i, :8] = [600.0, 600.0, 640.0, 512.0, -0.01, 0.02, -0.01, 0.003]
+        elif m == PINHOLE_FOV:
+            intr_truth[i, :5] = [700.0, 700.0, 640.0, 512.0, 0.9]
         else:
             raise ValueError(m)
     # rig: camera i+1 sits 0.12 m along -x from camera i, +-3 deg, +-5 mm
@@ -306,6 +344,18 @@ def make_problem(models, n_frames, seed, p_view=1.0, noise_px=0.3, min_corners=1
                 st_init[base + 3: base + 5] += 5.0 * rng.normal(size=2)
                 if m == OMNI_RADTAN:
                     st_init[base + 5: base + 9] = 0.0
+            elif m == DS:
+                st_init[base + 0] += 0.02 * rng.normal()
+                st_init[base + 1] *= 1 + 0.02 * rng.normal()
+                st_init[base + 2: base + 4] *= 1 + 0.02 * rng.normal(size=2)
+                st_init[base + 4: base + 6] += 5.0 * rng.normal(size=2)
+            elif m in (PINHOLE_EQUI, PINHOLE_FOV):
+                st_init[base + 0: base + 2] *= 1 + 0.02 * rng.normal(size=2)
+                st_init[base + 2: base + 4] += 5.0 * rng.normal(size=2)
+                if m == PINHOLE_EQUI:
+                    st_init[base + 4: base + 8] = 0.0
+                else:
+                    st_init[base + 4] *= 1 + 0.05 * rng.normal()
             elif m == EUCM:
                 st_init[base + 0: base + 2] *= 1 + 0.02 * rng.normal(size=2)
                 st_init[base + 2: base + 4] *= 1 + 0.02 * rng.normal(size=2)
@@ -332,6 +382,10 @@ CONFIGS = {
     2: dict(models=[PINHOLE_RADTAN] * 2, n_frames=500, name="2-cam stereo pinhole-radtan, 500 frames"),
     3: dict(models=[OMNI_RADTAN, OMNI_RADTAN, EUCM, EUCM], n_frames=1000, name="4-cam omni + EUCM mixed rig, 1000 frames"),
     4: dict(models=[PINHOLE_RADTAN] * 8, n_frames=2000, name="8-cam pinhole rig, 2000 frames"),
+    # not a BASELINE.json config: the remaining Kalibr2 camera models (CameraModels.hpp:25-133) in one rig,
+    # for parity tests only
+    6: dict(models=[DS, PINHOLE_EQUI, PINHOLE_FOV, OMNI], n_frames=200,
+            name="4-cam double-sphere + equidistant + FOV + omni rig, 200 frames (parity only)"),
 }
 
 

@@ -191,6 +191,9 @@ int kbo_model_nintr(int model) {
     case KBO_OMNI_RADTAN: return 9;
     case KBO_EUCM: return 6;
     case KBO_OMNI: return 5;
+    case KBO_DS: return 6;
+    case KBO_PINHOLE_EQUI: return 8;
+    case KBO_PINHOLE_FOV: return 5;
     default: return -1;
   }
 }
@@ -216,6 +219,81 @@ static void radtan_param_jac(const double y[2], double J[8]) {
   double y0 = y[0], y1 = y[1], r2 = y0 * y0 + y1 * y1, r4 = r2 * r2;
   J[0] = y0 * r2; J[1] = y0 * r4; J[2] = 2.0 * y0 * y1; J[3] = r2 + 2.0 * y0 * y0;
   J[4] = y1 * r2; J[5] = y1 * r4; J[6] = r2 + 2.0 * y1 * y1; J[7] = 2.0 * y0 * y1;
+}
+
+/* EquidistantDistortion::distort(y, J) and distortParameterJacobian (aslam_cameras/include/aslam/cameras/
+ * implementation/EquidistantDistortion.hpp:31-200, :244-273): y <- y * thetad(theta)/r, theta = atan r,
+ * thetad = theta (1 + k1 theta^2 + k2 theta^4 + k3 theta^6 + k4 theta^8); scaling 1 for r <= 1e-8.
+ * The Jacobians are the reference's closed forms, written as the chain rule through r (they are not
+ * guarded at r = 0, as in the reference). */
+static void equi_distort(const double* k, double y[2], double Jd[4], double Jk[8]) {
+  const double x0 = y[0], x1 = y[1];
+  const double r2 = x0 * x0 + x1 * x1, r = sqrt(r2), th = atan(r), t2 = th * th;
+  const double P = 1.0 + t2 * (k[0] + t2 * (k[1] + t2 * (k[2] + t2 * k[3])));
+  const double thd = th * P;
+  if (Jd) {
+    /* d(thetad)/d(theta) */
+    const double dP = 1.0 + t2 * (3.0 * k[0] + t2 * (5.0 * k[1] + t2 * (7.0 * k[2] + t2 * 9.0 * k[3])));
+    const double s = thd / r;
+    const double g = (dP / (1.0 + r2) - s) / r2; /* (ds/dr) / r */
+    Jd[0] = s + x0 * x0 * g;
+    Jd[1] = x0 * x1 * g;
+    Jd[2] = Jd[1];
+    Jd[3] = s + x1 * x1 * g;
+  }
+  if (Jk) {
+    const double t3r = th * t2 / r;
+    const double pw[4] = {t3r, t3r * t2, t3r * t2 * t2, t3r * t2 * t2 * t2};
+    for (int j = 0; j < 4; ++j) {
+      Jk[j] = x0 * pw[j];
+      Jk[4 + j] = x1 * pw[j];
+    }
+  }
+  const double sc = (r > 1e-8) ? thd / r : 1.0;
+  y[0] *= sc;
+  y[1] *= sc;
+}
+
+/* FovDistortion::distort(y, J) and distortParameterJacobian (aslam_cameras/include/aslam/cameras/
+ * implementation/FovDistortion.hpp:19-83, :130-168), including the reference's limits: w^2 < 1e-5 -> identity;
+ * r_u^2 < 1e-5 -> scale 2 tan(w/2)/w with J = that scale times I and the parameter column set to
+ * (w - sin w) / (w^2 cos^2(w/2)) in both rows (not multiplied by u, v). */
+static void fov_distort(double w, double y[2], double Jd[4], double Jw[2]) {
+  const double u = y[0], v = y[1];
+  const double ru2 = u * u + v * v, ru = sqrt(ru2);
+  const double tw = tan(w / 2.0), tw2 = tw * tw;
+  const double at = atan(2.0 * tw * ru);
+  double s;
+  if (w * w < 1e-5) {
+    s = 1.0;
+    if (Jd) { Jd[0] = 1.0; Jd[1] = 0.0; Jd[2] = 0.0; Jd[3] = 1.0; }
+    if (Jw) { Jw[0] = 0.0; Jw[1] = 0.0; }
+  } else if (ru2 < 1e-5) {
+    s = 2.0 * tw / w;
+    if (Jd) { Jd[0] = s; Jd[1] = 0.0; Jd[2] = 0.0; Jd[3] = s; }
+    if (Jw) {
+      const double c = cos(w / 2.0);
+      Jw[0] = Jw[1] = (w - sin(w)) / (w * w * c * c);
+    }
+  } else {
+    s = at / (ru * w);
+    if (Jd) {
+      /* d(u s)/du = s + u^2 (ds/dr)/r, ds/dr = (2 tw / (1 + 4 tw^2 r^2)) / (w r) - s / r */
+      const double q = (2.0 * tw / (w * (1.0 + 4.0 * tw2 * ru2)) - s) / ru2;
+      Jd[0] = s + u * u * q;
+      Jd[1] = u * v * q;
+      Jd[2] = Jd[1];
+      Jd[3] = s + v * v * q;
+    }
+    if (Jw) {
+      /* d s / dw = (1 + tw^2) / (w (1 + 4 tw^2 r^2)) - s / w */
+      const double ds = (1.0 + tw2) / (w * (1.0 + 4.0 * tw2 * ru2)) - s / w;
+      Jw[0] = u * ds;
+      Jw[1] = v * ds;
+    }
+  }
+  y[0] = u * s;
+  y[1] = v * s;
 }
 
 /* Returns 1 if the keypoint is defined.  Ji is 2 x nintr row-major with stride KBO_MAX_INTR.
@@ -334,6 +412,71 @@ int kbo_project(int model, const double* in, const double p[3], double y[2], dou
     y[0] = fu * mx + cu;
     y[1] = fv * my + cv;
     return 1;
+  }
+  if (model == KBO_DS) {
+    /* DoubleSphereProjection.hpp(impl):140-221 (keypoint + Jp), :443-505 (intrinsics) */
+    const double xi = in[0], al = in[1], fu = in[2], fv = in[3], cu = in[4], cv = in[5];
+    const double x = p[0], yv = p[1], z = p[2];
+    const double r2 = x * x + yv * yv, d1 = sqrt(r2 + z * z), d1_inv = 1.0 / d1;
+    const double tmp = (al <= 0.5) ? al / (1 - al) : (1 - al) / al;
+    const double fovp = (tmp + xi) / sqrt(2 * tmp * xi + xi * xi + 1);
+    if (z <= -(fovp * d1)) return 0;
+    const double k = xi * d1 + z, d2 = sqrt(r2 + k * k), d2_inv = 1.0 / d2;
+    const double norm = al * d2 + (1 - al) * k, ninv = 1.0 / norm, ninv2 = ninv * ninv;
+    const double mx = x * ninv, my = yv * ninv;
+    if (Jp) {
+      const double tt2 = xi * z * d1_inv + 1;
+      const double dn = (xi * (1 - al) * d1_inv + al * (xi * k * d1_inv + 1) * d2_inv) * ninv2;
+      const double t2 = ((1 - al) * tt2 + al * k * tt2 * d2_inv) * ninv2;
+      Jp[0] = fu * (ninv - x * x * dn);
+      Jp[1] = -fu * x * yv * dn;
+      Jp[2] = -fu * x * t2;
+      Jp[3] = -fv * x * yv * dn;
+      Jp[4] = fv * (ninv - yv * yv * dn);
+      Jp[5] = -fv * yv * t2;
+    }
+    if (Ji) {
+      const double t4 = (al - 1 - al * k * d2_inv) * d1 * ninv2;
+      const double t5 = (k - d2) * ninv2;
+      Ji[0] = fu * x * t4; Ji[KBO_MAX_INTR + 0] = fv * yv * t4;
+      Ji[1] = fu * x * t5; Ji[KBO_MAX_INTR + 1] = fv * yv * t5;
+      Ji[2] = mx; Ji[4] = 1.0;
+      Ji[KBO_MAX_INTR + 3] = my; Ji[KBO_MAX_INTR + 5] = 1.0;
+    }
+    y[0] = fu * mx + cu;
+    y[1] = fv * my + cv;
+    return 1;
+  }
+  if (model == KBO_PINHOLE_EQUI || model == KBO_PINHOLE_FOV) {
+    /* PinholeProjection.hpp(impl):99-145, :324-378 with the Equidistant / FOV distortion */
+    const double fu = in[0], fv = in[1], cu = in[2], cv = in[3];
+    const double rz = 1.0 / p[2], rz2 = rz * rz;
+    double kp[2] = {p[0] * rz, p[1] * rz};
+    double Jd[4], Jk[8];
+    const int nd = (model == KBO_PINHOLE_EQUI) ? 4 : 1;
+    if (model == KBO_PINHOLE_EQUI)
+      equi_distort(in + 4, kp, Jd, Jk);
+    else
+      fov_distort(in[4], kp, Jd, Jk);
+    if (Jp) {
+      Jp[0] = fu * Jd[0] * rz;
+      Jp[1] = fu * Jd[1] * rz;
+      Jp[2] = -fu * (p[0] * Jd[0] + p[1] * Jd[1]) * rz2;
+      Jp[3] = fv * Jd[2] * rz;
+      Jp[4] = fv * Jd[3] * rz;
+      Jp[5] = -fv * (p[0] * Jd[2] + p[1] * Jd[3]) * rz2;
+    }
+    if (Ji) {
+      Ji[0] = kp[0]; Ji[2] = 1.0;
+      Ji[KBO_MAX_INTR + 1] = kp[1]; Ji[KBO_MAX_INTR + 3] = 1.0;
+      for (int c = 0; c < nd; ++c) {
+        Ji[4 + c] = Jk[c] * fu;
+        Ji[KBO_MAX_INTR + 4 + c] = Jk[nd + c] * fv;
+      }
+    }
+    y[0] = fu * kp[0] + cu;
+    y[1] = fv * kp[1] + cv;
+    return p[2] > 0;
   }
   return 0;
 }

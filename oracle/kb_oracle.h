@@ -32,7 +32,10 @@ enum {
   KBO_OMNI_RADTAN = 1,    /* OmniProjection<RadialTangentialDistortion>: xi fu fv cu cv | k1 k2 p1 p2 */
   KBO_EUCM = 2,           /* ExtendedUnifiedProjection<NoDistortion>: alpha beta fu fv cu cv */
   KBO_OMNI = 3,           /* OmniProjection<NoDistortion>: xi fu fv cu cv */
-  KBO_NUM_MODELS = 4
+  KBO_DS = 4,             /* DoubleSphereProjection<NoDistortion>: xi alpha fu fv cu cv */
+  KBO_PINHOLE_EQUI = 5,   /* PinholeProjection<EquidistantDistortion>: fu fv cu cv | k1 k2 k3 k4 */
+  KBO_PINHOLE_FOV = 6,    /* PinholeProjection<FovDistortion>: fu fv cu cv | w */
+  KBO_NUM_MODELS = 7
 };
 
 typedef struct {

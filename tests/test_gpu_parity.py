@@ -47,6 +47,7 @@ PROBLEMS = {
     "c2_ragged": lambda: synth.make_config(2, n_frames=60, p_view=0.5, seed_offset=7),
     "c3_small": lambda: synth.make_config(3, n_frames=40),
     "c4_small": lambda: synth.make_config(4, n_frames=24, p_view=0.7),
+    "c6_small": lambda: synth.make_config(6, n_frames=40, p_view=0.8),  # DS + equidistant + FOV + omni
 }
 
 
@@ -69,7 +70,7 @@ def test_cost_and_blocks(capi, oracle_mod, name):
         assert _rel(g.rhs(), A["rhs"]) < 1e-10
 
 
-@pytest.mark.parametrize("name", ["c1", "c2_small", "c3_small", "c4_small"])
+@pytest.mark.parametrize("name", ["c1", "c2_small", "c3_small", "c4_small", "c6_small"])
 @pytest.mark.parametrize("lam", [0.0, 10.0, 1e3])
 def test_solve(capi, oracle_mod, name, lam):
     p = PROBLEMS[name]()
@@ -105,7 +106,7 @@ def test_update_revert(capi, oracle_mod):
     assert np.abs(g.get_state() - p.state_init).max() == 0.0
 
 
-@pytest.mark.parametrize("name", ["c1", "c2_small", "c2_ragged", "c3_small", "c4_small"])
+@pytest.mark.parametrize("name", ["c1", "c2_small", "c2_ragged", "c3_small", "c4_small", "c6_small"])
 def test_lm_optimize_parity(capi, oracle_mod, name):
     """Full Kalibr2 default optimizer (LM lambda0=10, epsX 1e-3, epsJ 1, maxIt 200) end to end."""
     p = PROBLEMS[name]()

@@ -63,6 +63,11 @@ TEST_INTR = {
     synth.OMNI_RADTAN: [0.9, 400, 400, 320, 240, -0.2, 0.13, 0.0005, 0.0005],
     synth.OMNI: [0.9, 400, 400, 320, 240],
     synth.EUCM: [0.6, 1.1, 400, 400, 320, 240],
+    # DoubleSphereProjection / EquidistantDistortion / FovDistortion test values
+    # (DoubleSphereProjection.hpp(impl) getTestProjection; EquidistantDistortion.cpp / FovDistortion.cpp:54-56)
+    synth.DS: [-0.2, 0.6, 400, 400, 320, 240],
+    synth.PINHOLE_EQUI: [400, 400, 320, 240, -0.01, 0.02, -0.01, 0.003],
+    synth.PINHOLE_FOV: [400, 400, 320, 240, 1.0],
 }
 
 
@@ -92,6 +97,32 @@ def test_projection_jacobians_fd(oracle_mod, model):
             _, y1, _, _ = oracle_mod.project(model, intr + di, p)
             _, y2, _, _ = oracle_mod.project(model, intr - di, p)
             assert np.abs((y1 - y2) / (2 * hh) - Ji[:, c]).max() < 1e-5 * max(1.0, np.abs(Ji[:, c]).max()), c
+
+
+def test_fov_small_radius_limit(oracle_mod):
+    """FovDistortion inside r_u^2 < 1e-5 (FovDistortion.hpp(impl):40-62, :150-153): the keypoint is scaled by
+    2 tan(w/2)/w, dy/dp uses that constant scale, and the w column is (w - sin w)/(w^2 cos^2(w/2)) times fu/fv
+    in both rows, independent of (u, v) -- reproduced as the reference has it."""
+    w = 0.9
+    intr = np.zeros(10)
+    intr[:5] = [400, 300, 320, 240, w]
+    p = np.array([1e-3, -2e-3, 1.5])
+    ok, y, Jp, Ji = oracle_mod.project(synth.PINHOLE_FOV, intr, p)
+    s = 2 * np.tan(w / 2) / w
+    assert abs(y[0] - (400 * s * p[0] / p[2] + 320)) < 1e-12
+    lim = (w - np.sin(w)) / (w * w * np.cos(w / 2) ** 2)
+    assert abs(Ji[0, 4] - 400 * lim) < 1e-9 and abs(Ji[1, 4] - 300 * lim) < 1e-9
+    assert abs(Jp[0, 0] - 400 * s / p[2]) < 1e-12 and Jp[0, 1] == 0.0
+
+
+def test_equidistant_identity_at_zero_coefficients(oracle_mod):
+    """k = 0: the equidistant model is y * atan(r)/r (EquidistantDistortion.hpp(impl):13-28)."""
+    intr = np.zeros(10)
+    intr[:4] = [400, 400, 320, 240]
+    p = np.array([0.4, -0.3, 1.0])
+    _, y, _, _ = oracle_mod.project(synth.PINHOLE_EQUI, intr, p)
+    r = np.hypot(0.4, 0.3)
+    assert np.abs(y - [320 + 400 * 0.4 * np.arctan(r) / r, 240 - 400 * 0.3 * np.arctan(r) / r]).max() < 1e-12
 
 
 def test_eucm_alpha_beta_quirk(oracle_mod):
@@ -203,3 +234,19 @@ def test_golden_config1(oracle_mod):
     st, r = o.optimize(p.state_init)
     assert r["iterations"] == int(z["lm_iterations"])
     assert np.abs(st - z["state_lm"]).max() < 1e-9
+
+
+def test_lm_all_camera_models(oracle_mod):
+    """DS + equidistant + FOV + omni rig (synth config 6): the default LM run converges to the noise floor
+    and recovers the well-observed intrinsics (focal lengths within 1.5 %, principal points within 3 px)."""
+    p = synth.make_config(6, n_frames=30, p_view=0.8)
+    o = oracle_mod.Oracle(p)
+    st, r = o.optimize(p.state_init, policy="lm", lambda0=10.0, max_iterations=200, eps_x=1e-3, eps_j=1.0)
+    assert r["linear_solver_failure"] == 0
+    assert r["J_final"] < 1.2 * p.n_corners * 2 * 0.09  # chi^2 ~ 2 N_c sigma^2 (sigma = 0.3 px)
+    intr, tru = st[:40].reshape(4, 10), p.state_truth[:40].reshape(4, 10)
+    fcol = {synth.DS: (2, 4), synth.PINHOLE_EQUI: (0, 2), synth.PINHOLE_FOV: (0, 2), synth.OMNI: (1, 3)}
+    for i, m in enumerate(p.cam_model):
+        a, b = fcol[int(m)]
+        assert np.abs(intr[i, a:b] / tru[i, a:b] - 1).max() < 0.015, (m, intr[i], tru[i])
+        assert np.abs(intr[i, b:b + 2] - tru[i, b:b + 2]).max() < 3.0, (m, intr[i], tru[i])
