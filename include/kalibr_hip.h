@@ -100,6 +100,35 @@ int kb_get_rhs(kb_handle* h, double* rhs_out);
 int kb_apply_update(kb_handle* h, const double* dx, double* deltaX_out);
 int kb_revert(kb_handle* h);
 
+/* aslam_incremental_calibration's LinearSolver (incremental_calibration/src/core/LinearSolver.cpp), the
+ * linear solver of IncrementalEstimator's optimizer (IncrementalEstimator.cpp:46-66) and so of the CLI's final
+ * calibration (CalibrateCameras.cpp:258-272).  Options: LinearSolverOptions (LinearSolverOptions.cpp:30-38). */
+typedef struct kb_marginal_options {
+  int32_t column_scaling; /* columnScaling (Kalibr2: 1) */
+  double eps_norm;        /* epsNorm: column-norm tolerance sqrt(rows * epsNorm) (default DBL_EPSILON) */
+  double eps_svd;         /* epsSVD: rankTol = sv_0 * epsSVD * C (Kalibr2: 1e-6) */
+  double svd_tol;         /* svdTol: fixed tolerance, -1 = rankTol */
+} kb_marginal_options;
+typedef struct kb_marginal_info {
+  int32_t rank;       /* getSVDRank (C - rank = getSVDRankDeficiency) */
+  int32_t sweeps;     /* Jacobi sweeps used */
+  double tolerance;   /* getSVDTolerance */
+  double sv_gap;      /* getSvGap: sv[rank-1] / sv[rank], +inf at full rank */
+  double sv_log2_sum; /* getSingularValuesLog2Sum over the first rank singular values */
+} kb_marginal_info;
+/* LinearSolver::solveSystem -> solve (LinearSolver.cpp:247-280, 299-466) after kb_build: the frame blocks are
+ * eliminated (lambda = 0; the conditioner is ignored, as LinearSolver ignores it), the camera block Omega is
+ * column-scaled and solved by truncated SVD, the frame steps back-substituted.  sv_out [C] (descending) and
+ * V_out [C][C] (row-major, singular vector j in column j) are the scaled SVD (getSingularValues /
+ * getMatrixV); either may be NULL.  *ok = 0 if a frame block is not positive definite.  C <= 112. */
+int kb_solve_marginal(kb_handle* h, const kb_marginal_options* opts, double* dx_out, int* ok,
+                      kb_marginal_info* info, double* sv_out, double* V_out);
+/* LinearSolver::analyzeMarginal (LinearSolver.cpp:468-528): SVD of the unscaled Omega of the last kb_build.
+ * info->rank / tolerance / sv_gap / sv_log2_sum are those of this SVD; the reference keeps the rank of the last
+ * solve (the C++ host layer's MarginalLinearSolver does the same). */
+int kb_analyze_marginal(kb_handle* h, const kb_marginal_options* opts, kb_marginal_info* info, double* sv_out,
+                        double* V_out);
+
 /* Normal-equation blocks of the last kb_build, for parity tests:
  * Hff [F][6][6], Hfc [F][6][C], gf [F][6], Hcc [C][C], gc [C], cost (chi^2 at build state). */
 int kb_get_normal_blocks(kb_handle* h, double* Hff, double* Hfc, double* gf, double* Hcc, double* gc,

@@ -22,7 +22,7 @@ EXPORTS = [
     "kb_get_state_flat", "kb_state_size", "kb_num_cols", "kb_camera_cols", "kb_eval_cost", "kb_build",
     "kb_set_constant_conditioner", "kb_solve", "kb_get_rhs", "kb_apply_update", "kb_revert", "kb_get_normal_blocks",
     "kb_optimize", "kb_get_trace", "kb_run_gn_iterations", "kb_build_kernel_stats", "kb_comm_get_unique_id",
-    "kb_comm_init", "kb_selftest_mfma",
+    "kb_comm_init", "kb_selftest_mfma", "kb_solve_marginal", "kb_analyze_marginal",
 ]
 
 
@@ -45,6 +45,24 @@ class Solution(C.Structure):
     _fields_ = [("J_start", C.c_double), ("J_final", C.c_double), ("dx_final", C.c_double), ("dj_final", C.c_double),
                 ("iterations", C.c_int32), ("failed_iterations", C.c_int32), ("linear_solver_failure", C.c_int32),
                 ("passes", C.c_int32), ("graphed", C.c_int32)]
+
+
+class MarginalOptions(C.Structure):
+    _fields_ = [("column_scaling", C.c_int32), ("eps_norm", C.c_double), ("eps_svd", C.c_double),
+                ("svd_tol", C.c_double)]
+
+
+class MarginalInfo(C.Structure):
+    _fields_ = [("rank", C.c_int32), ("sweeps", C.c_int32), ("tolerance", C.c_double), ("sv_gap", C.c_double),
+                ("sv_log2_sum", C.c_double)]
+
+
+DBL_EPS = float(np.finfo(float).eps)
+
+
+def marginal_options(column_scaling=True, eps_norm=DBL_EPS, eps_svd=1e-6, svd_tol=-1.0):
+    """LinearSolverOptions as CalibrateCameras sets them (CalibrateCameras.cpp:263-267)."""
+    return MarginalOptions(int(column_scaling), eps_norm, eps_svd, svd_tol)
 
 
 def lib():
@@ -82,6 +100,9 @@ def lib():
         L.kb_comm_get_unique_id.argtypes = [C.c_void_p]
         L.kb_comm_init.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32]
         L.kb_selftest_mfma.argtypes = [dp]
+        L.kb_solve_marginal.argtypes = [C.c_void_p, C.POINTER(MarginalOptions), dp, C.POINTER(C.c_int),
+                                        C.POINTER(MarginalInfo), dp, dp]
+        L.kb_analyze_marginal.argtypes = [C.c_void_p, C.POINTER(MarginalOptions), C.POINTER(MarginalInfo), dp, dp]
         _lib = L
     return _lib
 
@@ -170,6 +191,28 @@ class Solver:
         ok = C.c_int(0)
         _check(lib().kb_solve(self.h, _d(dx), C.byref(ok)))
         return bool(ok.value), dx
+
+    def _minfo(self, inf, sv, V):
+        return dict(rank=inf.rank, sweeps=inf.sweeps, tol=inf.tolerance, gap=inf.sv_gap, log2sum=inf.sv_log2_sum,
+                    sv=sv, V=V)
+
+    def solve_marginal(self, opts=None):
+        """calibration::LinearSolver::solveSystem after build(): (ok, dx, info with the scaled SVD)."""
+        opts = opts or marginal_options()
+        dx = np.zeros(self.ncols)
+        sv, V = np.zeros(self.C), np.zeros((self.C, self.C))
+        ok = C.c_int(0)
+        inf = MarginalInfo()
+        _check(lib().kb_solve_marginal(self.h, C.byref(opts), _d(dx), C.byref(ok), C.byref(inf), _d(sv), _d(V)))
+        return bool(ok.value), dx, self._minfo(inf, sv, V)
+
+    def analyze_marginal(self, opts=None):
+        """LinearSolver::analyzeMarginal: unscaled SVD of the last built system."""
+        opts = opts or marginal_options()
+        sv, V = np.zeros(self.C), np.zeros((self.C, self.C))
+        inf = MarginalInfo()
+        _check(lib().kb_analyze_marginal(self.h, C.byref(opts), C.byref(inf), _d(sv), _d(V)))
+        return self._minfo(inf, sv, V)
 
     def rhs(self):
         r = np.zeros(self.ncols)

@@ -87,6 +87,7 @@ struct kb_handle {
   int F_max = 0;
   // build-kernel timing
   double build_ms = 0.0;
+  double* marg_buf = nullptr;  // marginal solver outputs: V [C][C] | sv [C] | info [8]
 
   template <class T>
   int alloc(T** p, size_t n) {
@@ -585,6 +586,75 @@ int kb_revert(kb_handle* h) {
   if (set_cur(h, 1 - h->cur)) return -1;
   KB_HIP(hipStreamSynchronize(h->stream));
   return 0;
+}
+
+// ---------------------------------------------------------------- marginal SVD solver (calibration::LinearSolver)
+static int run_marginal(kb_handle* h, const kb_marginal_options* o, int write_dx, kb_marginal_info* info,
+                        double* sv_out, double* V_out) {
+  if (h->C > kMargMaxC) return fail("marginal solver: camera block C > 112 is not supported");
+  if (h->comm) return fail("marginal solver: not available on a sharded handle");
+  const int C = h->C;
+  if (!h->marg_buf && h->alloc(&h->marg_buf, (size_t)C * C + C + 8)) return -1;
+  KbMarg m;
+  m.scaling = o->column_scaling ? 1 : 0;
+  m.write_dx = write_dx;
+  m.norm_tol = std::sqrt(2.0 * (double)h->NC * o->eps_norm);  // rows of J: 2 per corner
+  m.eps_svd = o->eps_svd;
+  m.svd_tol = o->svd_tol;
+  m.V = h->marg_buf;
+  m.sv = m.V + (size_t)C * C;
+  m.info = m.sv + C;
+  // the frame blocks eliminated at lambda = 0 (stored H_ff, H_fc, g_f of the last build), column sums finished
+  const double lam_saved = h->d.host_lambda;
+  h->d.host_lambda = 0.0;
+  int rc = launch_schur(h, 0);
+  if (!rc) rc = launch_colsum(h, 0);
+  h->d.host_lambda = lam_saved;
+  if (rc) return rc;
+  const size_t lds = sizeof(double) * ((size_t)C * (C + 1) / 2 + (size_t)C * C + 2 * C);
+  KB_HIP(hipFuncSetAttribute((const void*)k_marg, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL(k_marg, dim3(1), dim3(kMargThreads), lds, h->stream, h->d, m);
+  KB_HIP(hipGetLastError());
+  double inf[8];
+  KB_HIP(hipMemcpyAsync(inf, m.info, sizeof(inf), hipMemcpyDeviceToHost, h->stream));
+  if (sv_out) KB_HIP(hipMemcpyAsync(sv_out, m.sv, sizeof(double) * C, hipMemcpyDeviceToHost, h->stream));
+  if (V_out) KB_HIP(hipMemcpyAsync(V_out, m.V, sizeof(double) * C * C, hipMemcpyDeviceToHost, h->stream));
+  KB_HIP(hipStreamSynchronize(h->stream));
+  if (info) {
+    info->rank = (int32_t)inf[0];
+    info->sweeps = (int32_t)inf[1];
+    info->tolerance = inf[2];
+    info->sv_gap = inf[3];
+    info->sv_log2_sum = inf[4];
+  }
+  return 0;
+}
+
+int kb_solve_marginal(kb_handle* h, const kb_marginal_options* opts, double* dx_out, int* ok, kb_marginal_info* info,
+                      double* sv_out, double* V_out) {
+  if (!h || !opts || !ok) return fail("kb_solve_marginal: null");
+  KB_HIP(hipSetDevice(h->device));
+  const int one = 1;
+  KB_HIP(hipMemcpyAsync(&h->d.ctrl->solve_ok, &one, sizeof(int), hipMemcpyHostToDevice, h->stream));
+  if (run_marginal(h, opts, 1, info, sv_out, V_out)) return -1;
+  int okd = 0;
+  KB_HIP(hipMemcpyAsync(&okd, &h->d.ctrl->solve_ok, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+  KB_HIP(hipStreamSynchronize(h->stream));
+  *ok = okd;
+  if (!okd) return 0;
+  if (launch_backsub(h, 0, 0, 0)) return -1;  // frame steps from the lambda = 0 blocks k_schur left
+  if (dx_out) KB_HIP(hipMemcpyAsync(dx_out, h->d.dx, sizeof(double) * h->ncols, hipMemcpyDeviceToHost, h->stream));
+  KB_HIP(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+int kb_analyze_marginal(kb_handle* h, const kb_marginal_options* opts, kb_marginal_info* info, double* sv_out,
+                        double* V_out) {
+  if (!h || !opts) return fail("kb_analyze_marginal: null");
+  KB_HIP(hipSetDevice(h->device));
+  kb_marginal_options un = *opts;
+  un.column_scaling = 0;
+  return run_marginal(h, &un, 0, info, sv_out, V_out);
 }
 
 int kb_get_normal_blocks(kb_handle* h, double* Hff, double* Hfc, double* gf, double* Hcc, double* gc, double* cost) {

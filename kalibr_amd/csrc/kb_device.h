@@ -37,6 +37,21 @@ struct KbOpts {
 
 constexpr int kColsumRows = 8;  // stage-1 row splits of the block partial reduction
 
+// k_marg (marginal truncated-SVD camera solve, aslam_incremental_calibration LinearSolver)
+constexpr int kMargThreads = 1024;
+constexpr int kMargMaxC = 112;         // packed Omega + V in LDS: C(C+1)/2 + C^2 + 2C doubles <= 160 KB
+constexpr int kMargMaxSweeps = 40;
+constexpr double kMargJacobiTol = 1.1102230246251565e-16;  // skip |a_pq| <= 2^-53 sqrt|a_pp a_qq|
+struct KbMarg {
+  int scaling;      // LinearSolverOptions::columnScaling
+  int write_dx;     // 1: solve (dx_c into d.dx); 0: analyzeMarginal (SVD only)
+  double norm_tol;  // sqrt(rows * epsNorm)
+  double eps_svd, svd_tol;
+  double* sv;    // [C] singular values, descending
+  double* V;     // [C][C] row-major, right singular vector j in column j
+  double* info;  // [8]: rank, sweeps, tolerance, sv gap, log2 sum of the first rank singular values
+};
+
 struct KbDev {
   int N, F, V, NC, C, ncols, S, K;  // K = target corners
   int off_base, off_frame;

@@ -1146,6 +1146,198 @@ __global__ void __launch_bounds__(256) k_camexpand(KbDev d) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// k_marg: the camera-block solve of aslam_incremental_calibration's LinearSolver (LinearSolver.cpp:299-466,
+// analyzeMarginal :468-528) on the Schur-reduced system the build + k_schur (lambda = 0) + k_colsum produced:
+//   S = H_cc - sum H_fc^T A_f,  b = g_c - sum H_fc^T b_f   (= Omega, b_r of reduceLeft/RightHandSide)
+//   column scaling G_j = 1/sqrt(H_cc[j][j]) (0 below sqrt(rows * epsNorm), linalg.cpp:128-152)
+//   SVD of G S G (Eigen::JacobiSVD, linalg.cpp:412-424) by cyclic two-sided Jacobi: the symmetric matrix packed
+//   upper in LDS, V in LDS; the round-robin parallel ordering applies C/2 disjoint rotations per round, each
+//   2x2 block (pair k, pair l) rotated in place by one thread (rows by k, then columns by l); 2 barriers/round
+//   truncation at rankTol = sv_0 epsSVD C, x_r = G V_r diag(1/w) V_r^T G b (solveSVD, linalg.cpp:426-443)
+// One block of kMargThreads.  LDS: C(C+1)/2 + C^2 + 2C doubles (C <= kMargMaxC).
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ int pk_up(int i, int j, int n) {  // packed upper index, any order
+  const int a = min(i, j), b = max(i, j);
+  return a * n - a * (a - 1) / 2 + (b - a);
+}
+
+__device__ __forceinline__ void rr_pair(int m, int r, int k, int& p, int& q) {  // round-robin pairing
+  int a, b;
+  if (k == 0) {
+    a = r;
+    b = m - 1;
+  } else {
+    a = (r + k) % (m - 1);
+    b = (r - k + (m - 1)) % (m - 1);
+  }
+  p = min(a, b);
+  q = max(a, b);
+}
+
+__global__ void __launch_bounds__(kMargThreads) k_marg(KbDev d, KbMarg mo) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  const int C = d.C, n = C, m = C + (C & 1), h = m / 2, tid = threadIdx.x, nth = blockDim.x;
+  const int np = n * (n + 1) / 2, Wt = d.W - C, o0 = d.N * 136;
+  double* A = sm;       // [np] packed upper
+  double* V = A + np;   // [n][n]
+  double* G = V + n * n;  // [n]
+  double* bs = G + n;     // [n]
+  __shared__ double cs[2 * (kMargMaxC / 2 + 1)];
+  __shared__ int pq[2 * (kMargMaxC / 2 + 1)];
+  __shared__ int nrot, okl;
+  __shared__ double wsort[kMargMaxC];
+  __shared__ int perm[kMargMaxC];
+  __shared__ double tco[kMargMaxC];
+  __shared__ double stat[4];
+  __shared__ int srank;
+  // ---- load: scaling, Omega = G S G, b_s = G b, V = I
+  for (int i = tid; i < n; i += nth) {
+    const double nrm = sqrt(d.Hcc[(size_t)i * C + i]);
+    G[i] = mo.scaling ? (nrm < mo.norm_tol ? 0.0 : 1.0 / nrm) : 1.0;
+  }
+  if (tid == 0) okl = !(psum_at(d, o0 + Wt + C) > 0.0);  // non-PD frame blocks
+  __syncthreads();
+  for (int e = tid; e < n * n; e += nth) {
+    const int i = e / n, j = e % n;
+    V[e] = (i == j) ? 1.0 : 0.0;
+    if (j >= i) A[pk_up(i, j, n)] = G[i] * (d.Hcc[(size_t)i * C + j] - psum_at(d, o0 + upper_index(i, j, C))) * G[j];
+  }
+  for (int i = tid; i < n; i += nth) bs[i] = G[i] * (d.gc[i] - psum_at(d, o0 + Wt + i));
+  // ---- Jacobi sweeps
+  int sweeps = 0;
+  const int nblk = h * (h + 1) / 2;
+  for (; sweeps < kMargMaxSweeps; ++sweeps) {
+    if (tid == 0) nrot = 0;
+    __syncthreads();
+    for (int r = 0; r < m - 1; ++r) {
+      for (int k = tid; k < h; k += nth) {
+        int p, q;
+        rr_pair(m, r, k, p, q);
+        double c = 1.0, sn = 0.0;
+        if (q < n) {
+          const double apq = A[pk_up(p, q, n)], app = A[pk_up(p, p, n)], aqq = A[pk_up(q, q, n)];
+          if (apq != 0.0 && fabs(apq) > kMargJacobiTol * sqrt(fabs(app * aqq))) {
+            const double th = (aqq - app) / (2.0 * apq);
+            const double t = (th >= 0.0 ? 1.0 : -1.0) / (fabs(th) + sqrt(th * th + 1.0));
+            c = 1.0 / sqrt(t * t + 1.0);
+            sn = t * c;
+            atomicAdd(&nrot, 1);
+          }
+        }
+        pq[2 * k] = p;
+        pq[2 * k + 1] = q;
+        cs[2 * k] = c;
+        cs[2 * k + 1] = sn;
+      }
+      __syncthreads();
+      for (int bI = tid; bI < nblk + n * h; bI += nth) {
+        if (bI < nblk) {  // 2x2 block (k, l), l >= k, of the upper triangle of pairs
+          int k = (int)((2.0f * h + 1.0f - sqrtf((2.0f * h + 1.0f) * (2.0f * h + 1.0f) - 8.0f * bI)) * 0.5f);
+          k = max(0, min(k, h - 1));
+          while (k > 0 && k * (2 * h - k + 1) / 2 > bI) --k;
+          while (k + 1 < h && (k + 1) * (2 * h - k) / 2 <= bI) ++k;
+          const int l = k + (bI - k * (2 * h - k + 1) / 2);
+          const int p = pq[2 * k], q = pq[2 * k + 1];
+          const double ck = cs[2 * k], sk = cs[2 * k + 1];
+          if (l == k) {
+            if (q < n && sk != 0.0) {
+              const int ipq = pk_up(p, q, n);
+              const double apq = A[ipq], t = sk / ck;
+              A[pk_up(p, p, n)] -= t * apq;
+              A[pk_up(q, q, n)] += t * apq;
+              A[ipq] = 0.0;
+            }
+          } else {
+            const int r2 = pq[2 * l], s2 = pq[2 * l + 1];
+            const double cl = cs[2 * l], sl = cs[2 * l + 1];
+            if (sk != 0.0 || sl != 0.0) {
+              const bool rv = r2 < n, sv = s2 < n, qv = q < n;
+              const double apr = rv ? A[pk_up(p, r2, n)] : 0.0, aps = sv ? A[pk_up(p, s2, n)] : 0.0;
+              const double aqr = (qv && rv) ? A[pk_up(q, r2, n)] : 0.0, aqs = (qv && sv) ? A[pk_up(q, s2, n)] : 0.0;
+              const double tpr = ck * apr - sk * aqr, tps = ck * aps - sk * aqs;
+              const double tqr = sk * apr + ck * aqr, tqs = sk * aps + ck * aqs;
+              if (rv) A[pk_up(p, r2, n)] = cl * tpr - sl * tps;
+              if (sv) A[pk_up(p, s2, n)] = sl * tpr + cl * tps;
+              if (qv && rv) A[pk_up(q, r2, n)] = cl * tqr - sl * tqs;
+              if (qv && sv) A[pk_up(q, s2, n)] = sl * tqr + cl * tqs;
+            }
+          }
+        } else {  // V <- V J: row i, pair k
+          const int e = bI - nblk, i = e / h, k = e % h;
+          const int p = pq[2 * k], q = pq[2 * k + 1];
+          const double c = cs[2 * k], sn = cs[2 * k + 1];
+          if (q < n && sn != 0.0) {
+            const double vp = V[i * n + p], vq = V[i * n + q];
+            V[i * n + p] = c * vp - sn * vq;
+            V[i * n + q] = sn * vp + c * vq;
+          }
+        }
+      }
+      __syncthreads();
+    }
+    const int nr = nrot;
+    __syncthreads();
+    if (nr == 0) break;
+  }
+  // ---- sort by |w| descending (ties: lower index first); singular values |w|
+  for (int i = tid; i < n; i += nth) {
+    const double wi = A[pk_up(i, i, n)], ai = fabs(wi);
+    int pos = 0;
+    for (int j = 0; j < n; ++j) {
+      const double aj = fabs(A[pk_up(j, j, n)]);
+      pos += (aj > ai || (aj == ai && j < i)) ? 1 : 0;
+    }
+    wsort[pos] = wi;
+    perm[pos] = i;
+  }
+  __syncthreads();
+  for (int e = tid; e < n * n; e += nth) {
+    const int r = e / n, j = e % n;
+    mo.V[e] = V[r * n + perm[j]];
+  }
+  for (int j = tid; j < n; j += nth) mo.sv[j] = fabs(wsort[j]);
+  if (tid == 0) {  // rankTol, estimateNumericalRank, svGap, log2 sum (linalg.cpp:243-282; LinearSolver.cpp:197-201)
+    const double tol = (mo.svd_tol != -1.0) ? mo.svd_tol : fabs(wsort[0]) * mo.eps_svd * n;
+    int rank = n;
+    for (int i = n - 1; i > 0; --i) {
+      if (fabs(wsort[i]) > tol) break;
+      --rank;
+    }
+    double l2 = 0.0;
+    for (int i = 0; i < rank; ++i) l2 += log(fabs(wsort[i]));
+    srank = rank;
+    stat[0] = tol;
+    stat[1] = rank < n ? fabs(wsort[rank - 1]) / fabs(wsort[rank]) : __builtin_inf();
+    stat[2] = l2 / log(2.0);
+  }
+  __syncthreads();
+  const int rank = srank;
+  // ---- truncated solve: t_j = (v_j . b_s) / w_j, x = G V_r t
+  for (int j = tid; j < rank; j += nth) {
+    const int pj = perm[j];
+    double s = 0.0;
+    for (int i = 0; i < n; ++i) s += V[i * n + pj] * bs[i];
+    tco[j] = s / wsort[j];
+  }
+  __syncthreads();
+  if (mo.write_dx) {
+    for (int i = tid; i < n; i += nth) {
+      double s = 0.0;
+      for (int j = 0; j < rank; ++j) s += V[i * n + perm[j]] * tco[j];
+      d.dx[i] = G[i] * s;
+    }
+  }
+  if (tid == 0) {
+    mo.info[0] = rank;
+    mo.info[1] = sweeps;
+    mo.info[2] = stat[0];
+    mo.info[3] = stat[1];
+    mo.info[4] = stat[2];
+    if (!okl) d.ctrl->solve_ok = 0;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // k_solve: S = H_cc + lambda^2 I - sum Y^T Y, b = g_c - sum Y^T z (packed lower, staged in LDS);
 // LDL^T (one wave when C <= 64, else the block with one barrier per column); dx_c; camera DV update
 // ---------------------------------------------------------------------------------------------

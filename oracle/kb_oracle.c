@@ -997,8 +997,184 @@ void kbo_arrow_schur_partial(const kbo_arrow* A, double conditioner, int f0, int
   free(c.z);
 }
 
+/* ------------------------------------------------------------------ */
+/* marginal SVD solve (aslam_incremental_calibration LinearSolver)     */
+/* ------------------------------------------------------------------ */
+
+/* Symmetric eigen-decomposition by cyclic Jacobi with the round-robin ("circle") parallel ordering the GPU kernel
+ * uses: m = n rounded up to even, m - 1 rounds per sweep, round r pairs (r, m-1) and ((r+k) mod (m-1),
+ * (r-k) mod (m-1)), k = 1 .. m/2-1; an index >= n is a bye.  Per round all rotations are computed first, then
+ * every 2x2 block (pair k, pair l) is rotated as rows-then-columns (the GPU's per-block formula).  Stops after a
+ * sweep without rotations.  Out: w[n] sorted by |w| descending, V[n*n] row-major with eigenvector j in column j.
+ * Replaces Eigen::JacobiSVD of the symmetric Omega (linalg.cpp:412-424): for a symmetric matrix the singular
+ * values are |w| and U = V up to the signs of negative eigenvalues. */
+static void jacobi_pair(int m, int r, int k, int* p, int* q) {
+  int a, b;
+  if (k == 0) {
+    a = r;
+    b = m - 1;
+  } else {
+    a = (r + k) % (m - 1);
+    b = (r - k + (m - 1)) % (m - 1);
+  }
+  *p = a < b ? a : b;
+  *q = a < b ? b : a;
+}
+
+int kbo_sym_eig(int n, const double* Ain, double* w, double* V) {
+  const int m = n + (n & 1), h = m / 2;
+  double* A = (double*)malloc(sizeof(double) * (size_t)n * n);
+  double* Vw = (double*)malloc(sizeof(double) * (size_t)n * n);
+  double* cs = (double*)malloc(sizeof(double) * 2 * h);
+  int* pp = (int*)malloc(sizeof(int) * 2 * h);
+  memcpy(A, Ain, sizeof(double) * (size_t)n * n);
+  for (int i = 0; i < n * n; ++i) Vw[i] = 0.0;
+  for (int i = 0; i < n; ++i) Vw[i * n + i] = 1.0;
+  int sweeps = 0;
+  for (; sweeps < KBO_JACOBI_MAX_SWEEPS; ++sweeps) {
+    int nrot = 0;
+    for (int r = 0; r < m - 1; ++r) {
+      for (int k = 0; k < h; ++k) {
+        int p, q;
+        jacobi_pair(m, r, k, &p, &q);
+        pp[2 * k] = p;
+        pp[2 * k + 1] = q;
+        double c = 1.0, s = 0.0;
+        if (q < n) {
+          const double apq = A[p * n + q], app = A[p * n + p], aqq = A[q * n + q];
+          if (apq != 0.0 && fabs(apq) > KBO_JACOBI_TOL * sqrt(fabs(app * aqq))) {
+            const double th = (aqq - app) / (2.0 * apq);
+            const double t = (th >= 0.0 ? 1.0 : -1.0) / (fabs(th) + sqrt(th * th + 1.0));
+            c = 1.0 / sqrt(t * t + 1.0);
+            s = t * c;
+            ++nrot;
+          }
+        }
+        cs[2 * k] = c;
+        cs[2 * k + 1] = s;
+      }
+      /* 2x2 blocks (k, l), l >= k: rows by rotation k, columns by rotation l; mirrored below the diagonal */
+      for (int k = 0; k < h; ++k) {
+        const int p = pp[2 * k], q = pp[2 * k + 1];
+        const double ck = cs[2 * k], sk = cs[2 * k + 1];
+        for (int l = k; l < h; ++l) {
+          const int r2 = pp[2 * l], s2 = pp[2 * l + 1];
+          const double cl = cs[2 * l], sl = cs[2 * l + 1];
+          if (l == k) {
+            if (q >= n || sk == 0.0) continue;
+            const double apq = A[p * n + q], t = sk / ck;
+            A[p * n + p] -= t * apq;
+            A[q * n + q] += t * apq;
+            A[p * n + q] = A[q * n + p] = 0.0;
+            continue;
+          }
+          const int rv = r2 < n, sv = s2 < n, qv = q < n;
+          const double apr = rv ? A[p * n + r2] : 0.0, aps = sv ? A[p * n + s2] : 0.0;
+          const double aqr = (qv && rv) ? A[q * n + r2] : 0.0, aqs = (qv && sv) ? A[q * n + s2] : 0.0;
+          const double tpr = ck * apr - sk * aqr, tps = ck * aps - sk * aqs;
+          const double tqr = sk * apr + ck * aqr, tqs = sk * aps + ck * aqs;
+          const double npr = cl * tpr - sl * tps, nps = sl * tpr + cl * tps;
+          const double nqr = cl * tqr - sl * tqs, nqs = sl * tqr + cl * tqs;
+          if (rv) A[p * n + r2] = A[r2 * n + p] = npr;
+          if (sv) A[p * n + s2] = A[s2 * n + p] = nps;
+          if (qv && rv) A[q * n + r2] = A[r2 * n + q] = nqr;
+          if (qv && sv) A[q * n + s2] = A[s2 * n + q] = nqs;
+        }
+      }
+      for (int k = 0; k < h; ++k) { /* V <- V J: columns p, q */
+        const int p = pp[2 * k], q = pp[2 * k + 1];
+        const double c = cs[2 * k], s = cs[2 * k + 1];
+        if (q >= n || s == 0.0) continue;
+        for (int i = 0; i < n; ++i) {
+          const double vp = Vw[i * n + p], vq = Vw[i * n + q];
+          Vw[i * n + p] = c * vp - s * vq;
+          Vw[i * n + q] = s * vp + c * vq;
+        }
+      }
+    }
+    if (nrot == 0) break;
+  }
+  /* sort by |w| descending (ties: lower index first) */
+  for (int i = 0; i < n; ++i) {
+    const double ai = fabs(A[i * n + i]);
+    int pos = 0;
+    for (int j = 0; j < n; ++j) {
+      const double aj = fabs(A[j * n + j]);
+      if (aj > ai || (aj == ai && j < i)) ++pos;
+    }
+    w[pos] = A[i * n + i];
+    for (int r = 0; r < n; ++r) V[r * n + pos] = Vw[r * n + i];
+  }
+  free(A);
+  free(Vw);
+  free(cs);
+  free(pp);
+  return sweeps;
+}
+
+/* LinearSolver::solve's camera-block part (LinearSolver.cpp:299-466) on the Schur-reduced system: column scaling
+ * G_j = 1/||A_r col j|| = 1/sqrt(Hcc_jj), 0 below sqrt(nrows * epsNorm) (linalg.cpp:128-152); Omega = G S G,
+ * b_r = G b (the SPQR route forms the same Schur complement, reduceLeftHandSide / reduceRightHandSide,
+ * linalg.cpp:284-410); SVD (analyzeSVD :412-424); tolerance rankTol = sv_0 * epsSVD * n (:256-261) unless svdTol
+ * != -1; rank by estimateNumericalRank (:243-254); svGap (:273-282); x_r = G V_r diag(1/sv) U_r^T b_r (solveSVD
+ * :426-443).  scaling = 0 gives analyzeMarginal's unscaled SVD (LinearSolver.cpp:468-528). */
+void kbo_marginal_solve(int C, const double* S, const double* b, const double* hdiag, const kbo_marg_opts* o,
+                        double* x, kbo_marg_info* info) {
+  double* G = (double*)malloc(sizeof(double) * C);
+  double* Om = (double*)malloc(sizeof(double) * (size_t)C * C);
+  double* w = (double*)malloc(sizeof(double) * C);
+  double* V = info->V ? info->V : (double*)malloc(sizeof(double) * (size_t)C * C);
+  const double normTol = sqrt(o->n_rows * o->eps_norm);
+  for (int j = 0; j < C; ++j) {
+    if (!o->column_scaling) {
+      G[j] = 1.0;
+      continue;
+    }
+    const double nrm = sqrt(hdiag[j]);
+    G[j] = (nrm < normTol) ? 0.0 : 1.0 / nrm;
+  }
+  for (int i = 0; i < C; ++i)
+    for (int j = 0; j < C; ++j) Om[i * C + j] = G[i] * S[i * C + j] * G[j];
+  info->sweeps = kbo_sym_eig(C, Om, w, V);
+  for (int i = 0; i < C; ++i) info->sv[i] = fabs(w[i]);
+  info->tol = (o->svd_tol != -1.0) ? o->svd_tol : info->sv[0] * o->eps_svd * C;
+  int rank = C;
+  for (int i = C - 1; i > 0; --i) {
+    if (info->sv[i] > info->tol) break;
+    --rank;
+  }
+  info->rank = rank;
+  info->gap = rank < C ? info->sv[rank - 1] / info->sv[rank] : INFINITY;
+  double l2 = 0.0;
+  for (int i = 0; i < rank; ++i) l2 += log(info->sv[i]);
+  info->log2sum = l2 / log(2.0);
+  if (x) {
+    for (int i = 0; i < C; ++i) x[i] = 0.0;
+    for (int j = 0; j < rank; ++j) {
+      double vb = 0.0;
+      for (int i = 0; i < C; ++i) vb += V[i * C + j] * G[i] * b[i];
+      const double a = vb / w[j];
+      for (int i = 0; i < C; ++i) x[i] += V[i * C + j] * a;
+    }
+    for (int i = 0; i < C; ++i) x[i] *= G[i];
+  }
+  if (!info->V) free(V);
+  free(G);
+  free(Om);
+  free(w);
+}
+
 int kbo_arrow_solve(const kbo_arrow* A, double conditioner, int nthreads, double* dx) {
+  return kbo_arrow_solve_ex(A, conditioner, nthreads, dx, NULL, NULL);
+}
+
+/* marg != NULL: the calibration::LinearSolver (QR + marginal SVD) in place of CHOLMOD: the conditioner is
+ * ignored (LinearSolver does not use it), the camera block is solved by kbo_marginal_solve and the frame blocks
+ * by back-substitution (solveQR, linalg.cpp:445-501: least squares of A_l x_l = b - A_r x_r). */
+int kbo_arrow_solve_ex(const kbo_arrow* A, double conditioner, int nthreads, double* dx, const kbo_marg_opts* marg,
+                       kbo_marg_info* info) {
   const int C = A->C, F = A->F;
+  if (marg) conditioner = 0.0;
   if (nthreads < 1) nthreads = 1;
   if (nthreads > F) nthreads = F > 0 ? F : 1;
   if (nthreads > 256) nthreads = 256;
@@ -1031,10 +1207,20 @@ int kbo_arrow_solve(const kbo_arrow* A, double conditioner, int nthreads, double
       for (int t = 0; t < nthreads; ++t) s += c.b_part[(size_t)t * C + q];
       b[q] = A->gc[q] - s;
     }
-    ok = chol_inplace(S, C);
+    if (marg) {
+      double* hd = (double*)malloc(sizeof(double) * C);
+      double* xr = (double*)malloc(sizeof(double) * C);
+      for (int q = 0; q < C; ++q) hd[q] = A->Hcc[q * C + q];
+      kbo_marginal_solve(C, S, b, hd, marg, xr, info);
+      memcpy(b, xr, sizeof(double) * C);
+      free(hd);
+      free(xr);
+    } else {
+      ok = chol_inplace(S, C);
+    }
   }
   if (ok) {
-    chol_solve(S, C, b);
+    if (!marg) chol_solve(S, C, b);
     for (int q = 0; q < C; ++q) dx[q] = b[q];
     c.dxc = b;
     c.dx = dx;
@@ -1202,13 +1388,13 @@ int kbo_optimize(const kbo_problem* P, double* st, const kbo_options* o, kbo_srv
         }
       }
       double* tmp = (double*)malloc(sizeof(double) * ncols);
-      success = kbo_arrow_solve(&A, lambda, nt, tmp);
+      success = kbo_arrow_solve_ex(&A, lambda, nt, tmp, o->marg, o->solve_info);
       if (success) memcpy(dx, tmp, sizeof(double) * ncols);
       free(tmp);
     } else {
       kbo_jt_build(jt, st, nt, rhs);
       kbo_jt_normal_arrow(jt, nt, &A);
-      success = kbo_arrow_solve(&A, 0.0, nt, dx);
+      success = kbo_arrow_solve_ex(&A, 0.0, nt, dx, o->marg, o->solve_info);
     }
     first = 0;
     int accepted = 0;
@@ -1244,6 +1430,29 @@ int kbo_optimize(const kbo_problem* P, double* st, const kbo_options* o, kbo_srv
       trace[4 * ntrace + 3] = accepted;
       ntrace++;
     }
+  }
+  if (o->marg && o->analyze_info) {
+    /* LinearSolver::analyzeMarginal (LinearSolver.cpp:468-528): unscaled Omega of the last built system; the
+     * rank, tolerance and gap stay those of the last solve when there was one (_svdRank != -1) */
+    kbo_marg_opts un = *o->marg;
+    un.column_scaling = 0;
+    double* S = (double*)malloc(sizeof(double) * C * C);
+    double* b = (double*)malloc(sizeof(double) * C);
+    int okp = 1;
+    kbo_arrow_schur_partial(&A, 0.0, 0, A.F, S, b, &okp);
+    for (int q = 0; q < C * C; ++q) S[q] = A.Hcc[q] - S[q];
+    kbo_marginal_solve(C, S, b, NULL, &un, NULL, o->analyze_info);
+    if (o->solve_info && srv->iterations + srv->failed_iterations > 0) {
+      kbo_marg_info* ai = o->analyze_info;
+      ai->rank = o->solve_info->rank;
+      ai->tol = o->solve_info->tol;
+      ai->gap = o->solve_info->gap;
+      double l2 = 0.0;
+      for (int i = 0; i < ai->rank; ++i) l2 += log(ai->sv[i]);
+      ai->log2sum = l2 / log(2.0);
+    }
+    free(S);
+    free(b);
   }
   srv->J_final = p_J;
   srv->dx_final = deltaX;

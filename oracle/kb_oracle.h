@@ -111,6 +111,28 @@ int kbo_dense_solve(const kbo_arrow* A, double conditioner, double* dx);
 /* Partial Schur quantities of a frame range (for sharding): S_part (C*C), b_part (C) */
 void kbo_arrow_schur_partial(const kbo_arrow* A, double conditioner, int f0, int f1, double* S_part, double* b_part, int* ok);
 
+/* --- aslam_incremental_calibration LinearSolver: marginal (camera-block) truncated-SVD solve --- */
+#define KBO_JACOBI_MAX_SWEEPS 40
+#define KBO_JACOBI_TOL 1.1102230246251565e-16 /* skip |a_pq| <= 2^-53 sqrt|a_pp a_qq| */
+typedef struct kbo_marg_opts_s {
+  int column_scaling; /* LinearSolverOptions::columnScaling */
+  double eps_norm;    /* epsNorm (default DBL_EPSILON) */
+  double eps_svd;     /* epsSVD (Kalibr2: 1e-6) */
+  double svd_tol;     /* svdTol (-1: rankTol from epsSVD) */
+  double n_rows;      /* rows of J (2 x corners): the column-norm tolerance sqrt(n_rows * epsNorm) */
+} kbo_marg_opts;
+typedef struct kbo_marg_info_s {
+  double* sv;  /* [C] singular values, descending */
+  double* V;   /* [C*C] row-major, right singular vector j in column j (may be NULL) */
+  int rank, sweeps;
+  double tol, gap, log2sum; /* svdTolerance, svGap, getSingularValuesLog2Sum */
+} kbo_marg_info;
+int kbo_sym_eig(int n, const double* A, double* w, double* V);
+void kbo_marginal_solve(int C, const double* S, const double* b, const double* hdiag, const kbo_marg_opts* o,
+                        double* x, kbo_marg_info* info);
+int kbo_arrow_solve_ex(const kbo_arrow* A, double conditioner, int nthreads, double* dx, const kbo_marg_opts* marg,
+                       kbo_marg_info* info);
+
 /* Optimizer2::applyStateUpdate / revert */
 double kbo_apply_update(const kbo_problem* P, double* state, const double* dx);
 
@@ -121,6 +143,12 @@ typedef struct {
   int max_iterations;
   double eps_x, eps_j;
   int nthreads;
+  /* calibration::LinearSolver in place of CHOLMOD when marg != NULL (IncrementalEstimator's optimizer);
+   * solve_info (optional): the last solve's scaled SVD; analyze_info (optional): LinearSolver::analyzeMarginal
+   * after the loop -- unscaled SVD of the last built system, rank kept from the last solve */
+  const struct kbo_marg_opts_s* marg;
+  struct kbo_marg_info_s* solve_info;
+  struct kbo_marg_info_s* analyze_info;
 } kbo_options;
 typedef struct {
   double J_start, J_final, dx_final, dj_final;

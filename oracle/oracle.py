@@ -30,9 +30,40 @@ class _Arrow(C.Structure):
                 ("cost", C.c_double)]
 
 
+class _MargOpts(C.Structure):
+    _fields_ = [("column_scaling", C.c_int), ("eps_norm", C.c_double), ("eps_svd", C.c_double),
+                ("svd_tol", C.c_double), ("n_rows", C.c_double)]
+
+
+class _MargInfo(C.Structure):
+    _fields_ = [("sv", dp), ("V", dp), ("rank", C.c_int), ("sweeps", C.c_int), ("tol", C.c_double),
+                ("gap", C.c_double), ("log2sum", C.c_double)]
+
+
 class _Options(C.Structure):
     _fields_ = [("policy", C.c_int), ("lambda0", C.c_double), ("max_iterations", C.c_int), ("eps_x", C.c_double),
-                ("eps_j", C.c_double), ("nthreads", C.c_int)]
+                ("eps_j", C.c_double), ("nthreads", C.c_int), ("marg", C.POINTER(_MargOpts)),
+                ("solve_info", C.POINTER(_MargInfo)), ("analyze_info", C.POINTER(_MargInfo))]
+
+
+EPS = float(np.finfo(float).eps)
+
+
+def marg_opts(n_rows, column_scaling=True, eps_norm=EPS, eps_svd=1e-6, svd_tol=-1.0):
+    """LinearSolverOptions as Kalibr2's CalibrateCameras sets them (CalibrateCameras.cpp:263-267): column scaling,
+    epsSVD 1e-6, the rest default (LinearSolverOptions.cpp:30-38)."""
+    return _MargOpts(int(column_scaling), eps_norm, eps_svd, svd_tol, float(n_rows))
+
+
+class _InfoBuf:
+    def __init__(self, Cc):
+        self.sv = np.zeros(Cc)
+        self.V = np.zeros((Cc, Cc))
+        self.s = _MargInfo(_d(self.sv), _d(self.V), 0, 0, 0.0, 0.0, 0.0)
+
+    def result(self):
+        return dict(sv=self.sv.copy(), V=self.V.copy(), rank=self.s.rank, sweeps=self.s.sweeps, tol=self.s.tol,
+                    gap=self.s.gap, log2sum=self.s.log2sum)
 
 
 class _Srv(C.Structure):
@@ -63,6 +94,10 @@ def lib():
         L.kbo_arrow_solve.argtypes = [C.POINTER(_Arrow), C.c_double, C.c_int, dp]
         L.kbo_dense_solve.argtypes = [C.POINTER(_Arrow), C.c_double, dp]
         L.kbo_arrow_schur_partial.argtypes = [C.POINTER(_Arrow), C.c_double, C.c_int, C.c_int, dp, dp, ip]
+        L.kbo_arrow_solve_ex.argtypes = [C.POINTER(_Arrow), C.c_double, C.c_int, dp, C.POINTER(_MargOpts),
+                                         C.POINTER(_MargInfo)]
+        L.kbo_marginal_solve.argtypes = [C.c_int, dp, dp, dp, C.POINTER(_MargOpts), dp, C.POINTER(_MargInfo)]
+        L.kbo_sym_eig.argtypes = [C.c_int, dp, dp, dp]
         _lib = L
     return _lib
 
@@ -145,6 +180,14 @@ class Oracle:
             ok = lib().kbo_arrow_solve(C.byref(arrow["_A"]), conditioner, nthreads, _d(dx))
         return bool(ok), dx
 
+    def solve_marginal(self, arrow, opts=None):
+        """calibration::LinearSolver::solve on the arrow system: (ok, dx, info) with the scaled SVD of Omega."""
+        opts = opts or marg_opts(2 * self.prob.n_corners)
+        dx = np.zeros(self.ncols)
+        buf = _InfoBuf(self.C)
+        ok = lib().kbo_arrow_solve_ex(C.byref(arrow["_A"]), 0.0, 1, _d(dx), C.byref(opts), C.byref(buf.s))
+        return bool(ok), dx, buf.result()
+
     def schur_partial(self, arrow, conditioner, f0, f1):
         S = np.zeros((self.C, self.C))
         b = np.zeros(self.C)
@@ -158,19 +201,50 @@ class Oracle:
         return st, dX
 
     def optimize(self, state, policy="lm", lambda0=10.0, max_iterations=200, eps_x=1e-3, eps_j=1.0, nthreads=1,
-                 trace_cap=1000):
+                 trace_cap=1000, marg=None):
+        """Optimizer2::optimize; marg (a marg_opts()) selects calibration::LinearSolver, then res["solve_info"] is
+        the last solve's scaled SVD and res["analyze_info"] LinearSolver::analyzeMarginal's."""
         st = np.array(state, dtype=np.float64, copy=True)
         o = _Options(0 if policy == "lm" else 1, lambda0, max_iterations, eps_x, eps_j, nthreads)
+        if marg is not None:
+            si, ai = _InfoBuf(self.C), _InfoBuf(self.C)
+            o.marg = C.pointer(marg)
+            o.solve_info = C.pointer(si.s)
+            o.analyze_info = C.pointer(ai.s)
         srv = _Srv()
         tr = np.zeros((trace_cap, 4))
         n = lib().kbo_optimize(C.byref(self.P), _d(st), C.byref(o), C.byref(srv), _d(tr), trace_cap)
         res = {f: getattr(srv, f) for f, _ in _Srv._fields_}
         res["trace"] = tr[:n].copy()
+        if marg is not None:
+            res["solve_info"] = si.result()
+            res["analyze_info"] = ai.result()
         return st, res
 
     def time_gn(self, state, n_iter, nthreads):
         st = np.array(state, dtype=np.float64, copy=True)
         return lib().kbo_time_gn(C.byref(self.P), _d(st), n_iter, nthreads)
+
+
+def sym_eig(A):
+    """kbo_sym_eig: (w sorted by |w| descending, V with eigenvectors in columns, sweeps)."""
+    A = np.ascontiguousarray(A, dtype=np.float64)
+    n = A.shape[0]
+    w, V = np.zeros(n), np.zeros((n, n))
+    sw = lib().kbo_sym_eig(n, _d(A), _d(w), _d(V))
+    return w, V, sw
+
+
+def marginal_solve(S, b, hdiag, opts):
+    """kbo_marginal_solve on a reduced system: (x, info)."""
+    Cc = S.shape[0]
+    x = np.zeros(Cc)
+    buf = _InfoBuf(Cc)
+    hd = np.ascontiguousarray(hdiag if hdiag is not None else np.ones(Cc), dtype=np.float64)
+    lib().kbo_marginal_solve(Cc, _d(np.ascontiguousarray(S, dtype=np.float64)),
+                             _d(np.ascontiguousarray(b, dtype=np.float64)), _d(hd), C.byref(opts), _d(x),
+                             C.byref(buf.s))
+    return x, buf.result()
 
 
 def axis_angle2quat(a):
