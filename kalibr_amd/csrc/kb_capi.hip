@@ -102,6 +102,28 @@ struct kb_handle {
   }
 };
 
+template <bool GN, unsigned MM>
+static const void* build_fn(int mb) {
+  return mb == 1 ? (const void*)k_build<1, GN, MM> : mb == 4 ? (const void*)k_build<4, GN, MM>
+                                                             : (const void*)k_build<7, GN, MM>;
+}
+
+// Build kernel for the rig's camera-model set `mm` (bit m = model m present).
+template <bool GN>
+static const void* pick_build(int mb, unsigned mm) {
+  switch (mm) {
+    case 1u << KB_PINHOLE_RADTAN: return build_fn<GN, 1u << KB_PINHOLE_RADTAN>(mb);
+    case 1u << KB_OMNI_RADTAN: return build_fn<GN, 1u << KB_OMNI_RADTAN>(mb);
+    case 1u << KB_EUCM: return build_fn<GN, 1u << KB_EUCM>(mb);
+    case 1u << KB_OMNI: return build_fn<GN, 1u << KB_OMNI>(mb);
+    case 1u << KB_DS: return build_fn<GN, 1u << KB_DS>(mb);
+    case 1u << KB_PINHOLE_EQUI: return build_fn<GN, 1u << KB_PINHOLE_EQUI>(mb);
+    case 1u << KB_PINHOLE_FOV: return build_fn<GN, 1u << KB_PINHOLE_FOV>(mb);
+    case (1u << KB_OMNI_RADTAN) | (1u << KB_EUCM): return build_fn<GN, (1u << KB_OMNI_RADTAN) | (1u << KB_EUCM)>(mb);
+    default: return build_fn<GN, kMmAll>(mb);
+  }
+}
+
 static void drop_graphs(kb_handle* h) {
   if (h->graph) hipGraphExecDestroy(h->graph);
   if (h->graphP) hipGraphExecDestroy(h->graphP);
@@ -284,10 +306,12 @@ kb_handle* kb_create(const kb_layout* L) {
     const int tb = (ntiles + d.wpb - 1) / d.wpb, ts = (ntiles + 3) / 4;
     h->mb = tb <= 1 ? 1 : tb <= 4 ? 4 : 7;
     h->ms = ts <= 1 ? 1 : ts <= 4 ? 4 : 7;
-    h->fn_build = h->mb == 1 ? (const void*)k_build<1, false> : h->mb == 4 ? (const void*)k_build<4, false>
-                                                                       : (const void*)k_build<7, false>;
-    h->fn_build_gn = h->mb == 1 ? (const void*)k_build<1, true> : h->mb == 4 ? (const void*)k_build<4, true>
-                                                                          : (const void*)k_build<7, true>;
+    // camera-model set: one-model rigs (and the omni-radtan + EUCM rig of configs[2]) get their own build
+    // kernels; any other mix uses the all-models instantiation
+    unsigned mm = 0;
+    for (int i = 0; i < h->N; ++i) mm |= 1u << d.model[i];
+    h->fn_build = pick_build<false>(h->mb, mm);
+    h->fn_build_gn = pick_build<true>(h->mb, mm);
     h->fn_schur = h->ms == 1 ? (const void*)k_schur<1> : h->ms == 4 ? (const void*)k_schur<4> : (const void*)k_schur<7>;
   }
   hipFuncSetAttribute(h->fn_build, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_build);

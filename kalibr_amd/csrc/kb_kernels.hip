@@ -566,7 +566,8 @@ __device__ __forceinline__ void frame_step(const KbDev& d, int f, bool store, in
 // k_build: one block = a group of frames; waves = N * nsplit, wave w -> camera w % N, corner split w / N.
 // ---------------------------------------------------------------------------------------------
 // GNF: Gauss-Newton fused variant (applies the previous solve's frame steps; no folded pass end)
-template <int TW, bool GNF>
+// MM: camera-model set of the rig (kMmAll = any model; a single-model set compiles one projection)
+template <int TW, bool GNF, unsigned MM>
 __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
   KbCtrl* c = d.ctrl;
   extern __shared__ __attribute__((aligned(16))) double sm[];
@@ -770,7 +771,7 @@ __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
           const double p1 = R[3] * X0 + R[4] * X1 + R[5] * X2 + t[1];
           const double p2 = R[6] * X0 + R[7] * X1 + R[8] * X2 + t[2];
           double u, w, Jp[6], Ji[2 * KB_MAX_INTR];
-          project_jac(model, intr, p0, p1, p2, u, w, Jp, Ji);
+          project_jac<MM>(model, intr, p0, p1, p2, u, w, Jp, Ji);
           const double e0 = yv.x - u, e1 = yv.y - w;
 #pragma unroll
           for (int r = 0; r < 2; ++r) {

@@ -134,39 +134,52 @@ __device__ __forceinline__ void radtan_only(const double* d, double& x, double& 
   y = ny;
 }
 
+// Camera-model sets: kernels are instantiated per set of models present in the rig, so a one-model rig
+// compiles only its own projection (the all-models union costs the build kernel ~40 spilled VGPRs).
+constexpr unsigned kMmAll = 0x7Fu;
+#define KB_MM(m) ((MM >> (m)) & 1u)
+
 // Keypoint only (cost pass).
+template <unsigned MM = kMmAll>
 __device__ __forceinline__ void project(int model, const double* in, double px, double py, double pz, double& u,
                                         double& v) {
-  if (model == KB_PINHOLE_RADTAN) {
+  if (MM == (1u << KB_PINHOLE_RADTAN)) model = KB_PINHOLE_RADTAN;  // single-model sets: constant model
+  else if (MM == (1u << KB_OMNI_RADTAN)) model = KB_OMNI_RADTAN;
+  else if (MM == (1u << KB_EUCM)) model = KB_EUCM;
+  else if (MM == (1u << KB_OMNI)) model = KB_OMNI;
+  else if (MM == (1u << KB_DS)) model = KB_DS;
+  else if (MM == (1u << KB_PINHOLE_EQUI)) model = KB_PINHOLE_EQUI;
+  else if (MM == (1u << KB_PINHOLE_FOV)) model = KB_PINHOLE_FOV;
+  if (KB_MM(KB_PINHOLE_RADTAN) && model == KB_PINHOLE_RADTAN) {
     const double rz = 1.0 / pz;
     double x = px * rz, y = py * rz;
     radtan_only(in + 4, x, y);
     u = in[0] * x + in[2];
     v = in[1] * y + in[3];
-  } else if (model == KB_OMNI_RADTAN || model == KB_OMNI) {
+  } else if ((KB_MM(KB_OMNI_RADTAN) && model == KB_OMNI_RADTAN) || (KB_MM(KB_OMNI) && model == KB_OMNI)) {
     const double xi = in[0];
     const double d = sqrt(px * px + py * py + pz * pz);
     const double rz = 1.0 / (pz + xi * d);
     double x = px * rz, y = py * rz;
-    if (model == KB_OMNI_RADTAN) radtan_only(in + 5, x, y);
+    if (KB_MM(KB_OMNI_RADTAN) && model == KB_OMNI_RADTAN) radtan_only(in + 5, x, y);
     u = in[1] * x + in[3];
     v = in[2] * y + in[4];
-  } else if (model == KB_EUCM) {
+  } else if (KB_MM(KB_EUCM) && model == KB_EUCM) {
     const double al = in[0], be = in[1];
     const double d = sqrt(be * (px * px + py * py) + pz * pz);
     const double ninv = 1.0 / (al * d + (1 - al) * pz);
     u = in[2] * (px * ninv) + in[4];
     v = in[3] * (py * ninv) + in[5];
-  } else if (model == KB_DS) {
+  } else if (KB_MM(KB_DS) && model == KB_DS) {
     const double xi = in[0], al = in[1], r2 = px * px + py * py;
     const double k = xi * sqrt(r2 + pz * pz) + pz;
     const double ninv = 1.0 / (al * sqrt(r2 + k * k) + (1 - al) * k);
     u = in[2] * (px * ninv) + in[4];
     v = in[3] * (py * ninv) + in[5];
-  } else {  // pinhole + equidistant / FOV
+  } else if (KB_MM(KB_PINHOLE_EQUI) || KB_MM(KB_PINHOLE_FOV)) {  // pinhole + equidistant / FOV
     const double rz = 1.0 / pz;
     double x = px * rz, y = py * rz;
-    if (model == KB_PINHOLE_EQUI)
+    if (KB_MM(KB_PINHOLE_EQUI) && (!KB_MM(KB_PINHOLE_FOV) || model == KB_PINHOLE_EQUI))
       equi(in + 4, x, y, nullptr, nullptr);
     else
       fov(in[4], x, y, nullptr, nullptr);
@@ -178,9 +191,17 @@ __device__ __forceinline__ void project(int model, const double* in, double px, 
 // Keypoint, dy/dp (2x3, row-major Jp[6]) and dy/dintrinsics (Ji[2][KB_MAX_INTR] row-major, only the
 // first nintr columns written).  Mirrors the reference per model, including its quirks (EUCM alpha/beta
 // rows both scaled by fu, ExtendedUnifiedProjection.hpp(impl):440-441).
+template <unsigned MM = kMmAll>
 __device__ __forceinline__ void project_jac(int model, const double* in, double px, double py, double pz, double& u,
                                             double& v, double* Jp, double* Ji) {
-  if (model == KB_PINHOLE_RADTAN) {
+  if (MM == (1u << KB_PINHOLE_RADTAN)) model = KB_PINHOLE_RADTAN;
+  else if (MM == (1u << KB_OMNI_RADTAN)) model = KB_OMNI_RADTAN;
+  else if (MM == (1u << KB_EUCM)) model = KB_EUCM;
+  else if (MM == (1u << KB_OMNI)) model = KB_OMNI;
+  else if (MM == (1u << KB_DS)) model = KB_DS;
+  else if (MM == (1u << KB_PINHOLE_EQUI)) model = KB_PINHOLE_EQUI;
+  else if (MM == (1u << KB_PINHOLE_FOV)) model = KB_PINHOLE_FOV;
+  if (KB_MM(KB_PINHOLE_RADTAN) && model == KB_PINHOLE_RADTAN) {
     const double fu = in[0], fv = in[1];
     const double rz = 1.0 / pz, rz2 = rz * rz;
     const double ux = px * rz, uy = py * rz;
@@ -200,7 +221,7 @@ __device__ __forceinline__ void project_jac(int model, const double* in, double 
     Ji[KB_MAX_INTR + 6] = (r2 + 2.0 * uy * uy) * fv; Ji[KB_MAX_INTR + 7] = 2.0 * ux * uy * fv;
     u = fu * x + in[2];
     v = fv * y + in[3];
-  } else if (model == KB_OMNI_RADTAN || model == KB_OMNI) {
+  } else if ((KB_MM(KB_OMNI_RADTAN) && model == KB_OMNI_RADTAN) || (KB_MM(KB_OMNI) && model == KB_OMNI)) {
     const double xi = in[0], fu = in[1], fv = in[2];
     const double d = sqrt(px * px + py * py + pz * pz);
     const double rz = 1.0 / (pz + xi * d);
@@ -215,7 +236,7 @@ __device__ __forceinline__ void project_jac(int model, const double* in, double 
     J[2] = px * rzj;
     J[5] = py * rzj;
     double x = ux, y = uy, Jd[4] = {1.0, 0.0, 0.0, 1.0};
-    if (model == KB_OMNI_RADTAN) radtan(in + 5, x, y, Jd);
+    if (KB_MM(KB_OMNI_RADTAN) && model == KB_OMNI_RADTAN) radtan(in + 5, x, y, Jd);
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
       Jp[c] = fu * (J[c] * Jd[0] + J[3 + c] * Jd[1]);
@@ -226,7 +247,7 @@ __device__ __forceinline__ void project_jac(int model, const double* in, double 
     Ji[1] = x; Ji[2] = 0.0; Ji[3] = 1.0; Ji[4] = 0.0;
     Ji[KB_MAX_INTR + 0] = fv * (Jd[2] * jx0 + Jd[3] * jx1);
     Ji[KB_MAX_INTR + 1] = 0.0; Ji[KB_MAX_INTR + 2] = y; Ji[KB_MAX_INTR + 3] = 0.0; Ji[KB_MAX_INTR + 4] = 1.0;
-    if (model == KB_OMNI_RADTAN) {
+    if (KB_MM(KB_OMNI_RADTAN) && model == KB_OMNI_RADTAN) {
       const double r2 = ux * ux + uy * uy, r4 = r2 * r2;
       Ji[5] = ux * r2 * fu; Ji[6] = ux * r4 * fu; Ji[7] = 2.0 * ux * uy * fu; Ji[8] = (r2 + 2.0 * ux * ux) * fu;
       Ji[KB_MAX_INTR + 5] = uy * r2 * fv; Ji[KB_MAX_INTR + 6] = uy * r4 * fv;
@@ -234,7 +255,7 @@ __device__ __forceinline__ void project_jac(int model, const double* in, double 
     }
     u = fu * x + in[3];
     v = fv * y + in[4];
-  } else if (model == KB_EUCM) {
+  } else if (KB_MM(KB_EUCM) && model == KB_EUCM) {
     const double al = in[0], be = in[1], fu = in[2], fv = in[3];
     const double xx = px * px, yy = py * py, r2 = xx + yy;
     const double d = sqrt(be * r2 + pz * pz), d_inv = 1.0 / d;
@@ -258,7 +279,7 @@ __device__ __forceinline__ void project_jac(int model, const double* in, double 
     Ji[KB_MAX_INTR + 3] = my; Ji[KB_MAX_INTR + 4] = 0.0; Ji[KB_MAX_INTR + 5] = 1.0;
     u = fu * mx + in[4];
     v = fv * my + in[5];
-  } else if (model == KB_DS) {
+  } else if (KB_MM(KB_DS) && model == KB_DS) {
     const double xi = in[0], al = in[1], fu = in[2], fv = in[3];
     const double r2 = px * px + py * py, d1 = sqrt(r2 + pz * pz), d1_inv = 1.0 / d1;
     const double k = xi * d1 + pz, d2 = sqrt(r2 + k * k), d2_inv = 1.0 / d2;
@@ -279,11 +300,12 @@ __device__ __forceinline__ void project_jac(int model, const double* in, double 
     Ji[KB_MAX_INTR + 3] = my; Ji[KB_MAX_INTR + 4] = 0.0; Ji[KB_MAX_INTR + 5] = 1.0;
     u = fu * mx + in[4];
     v = fv * my + in[5];
-  } else {  // pinhole + equidistant (4 distortion columns) / FOV (1)
+  } else if (KB_MM(KB_PINHOLE_EQUI) || KB_MM(KB_PINHOLE_FOV)) {  // pinhole + equidistant (4) / FOV (1)
+    const bool eq = KB_MM(KB_PINHOLE_EQUI) && (!KB_MM(KB_PINHOLE_FOV) || model == KB_PINHOLE_EQUI);
     const double fu = in[0], fv = in[1];
     const double rz = 1.0 / pz, rz2 = rz * rz;
     double x = px * rz, y = py * rz, Jd[4], Jk[8];
-    if (model == KB_PINHOLE_EQUI)
+    if (eq)
       equi(in + 4, x, y, Jd, Jk);
     else
       fov(in[4], x, y, Jd, Jk);
@@ -295,7 +317,7 @@ __device__ __forceinline__ void project_jac(int model, const double* in, double 
     Jp[5] = -fv * (px * Jd[2] + py * Jd[3]) * rz2;
     Ji[0] = x; Ji[1] = 0.0; Ji[2] = 1.0; Ji[3] = 0.0;
     Ji[KB_MAX_INTR + 0] = 0.0; Ji[KB_MAX_INTR + 1] = y; Ji[KB_MAX_INTR + 2] = 0.0; Ji[KB_MAX_INTR + 3] = 1.0;
-    if (model == KB_PINHOLE_EQUI) {
+    if (eq) {
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         Ji[4 + c] = Jk[c] * fu;
