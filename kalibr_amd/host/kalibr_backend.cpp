@@ -2,6 +2,7 @@
 #include "kalibr_backend.hpp"
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <iostream>
 
@@ -333,6 +334,203 @@ SolutionReturnValue Optimizer2::optimizeOnDevice(int syncEvery) {
   srv.failedIterations = s.failed_iterations;
   srv.linearSolverFailure = s.linear_solver_failure != 0;
   return srv;
+}
+
+// ---------------------------------------------------------------- marginal solver (LinearSolver.cpp)
+double MarginalLinearSystemSolver::getSingularValuesLog2Sum() const {
+  if (_svdRank == -1) return 0.0;
+  double s = 0.0;
+  for (std::ptrdiff_t i = 0; i < _svdRank; ++i) s += std::log(_sv[(size_t)i]);
+  return s / std::log(2);
+}
+
+std::vector<double> MarginalLinearSystemSolver::getNullSpace() const {
+  const size_t C = _sv.size();
+  if (_svdRank == -1 || (size_t)_svdRank > C) return {};
+  const size_t r = (size_t)_svdRank, k = C - r;
+  std::vector<double> out(C * k);
+  for (size_t i = 0; i < C; ++i)
+    for (size_t j = 0; j < k; ++j) out[i * k + j] = _V[i * C + r + j];
+  return out;
+}
+
+std::vector<double> MarginalLinearSystemSolver::getRowSpace() const {
+  const size_t C = _sv.size();
+  if (_svdRank == -1 || (size_t)_svdRank > C) return {};
+  const size_t r = (size_t)_svdRank;
+  std::vector<double> out(C * r);
+  for (size_t i = 0; i < C; ++i)
+    for (size_t j = 0; j < r; ++j) out[i * r + j] = _V[i * C + j];
+  return out;
+}
+
+std::vector<double> MarginalLinearSystemSolver::getCovariance() const {
+  const size_t C = _sv.size();
+  if (_svdRank == -1 || (size_t)_svdRank > C) return {};
+  std::vector<double> out(C * C, 0.0);
+  for (size_t k = 0; k < (size_t)_svdRank; ++k) {
+    const double w = 1.0 / _sv[k];
+    for (size_t i = 0; i < C; ++i)
+      for (size_t j = 0; j < C; ++j) out[i * C + j] += _V[i * C + k] * w * _V[j * C + k];
+  }
+  return out;
+}
+
+GpuMarginalLinearSolver::GpuMarginalLinearSolver(const LinearSolverOptions& o, const GpuOptions& g) : _g(g) {
+  _lopt = o;
+}
+
+void GpuMarginalLinearSolver::initMatrixStructure(const CalibrationProblem& p, bool useDiagonalConditioner) {
+  _g.initMatrixStructure(p, useDiagonalConditioner);
+  _JRows = _g.JRows();
+  _JCols = _g.JCols();
+  _diagonalConditioner.assign(_JCols, 0.0);
+  _svdRank = -1;
+  _svdTolerance = _svGap = -1.0;
+  _sv.clear();
+  _V.clear();
+}
+
+static kb_marginal_options marg_opts(const LinearSolverOptions& o) {
+  kb_marginal_options m{};
+  m.column_scaling = o.columnScaling ? 1 : 0;
+  m.eps_norm = o.epsNorm;
+  m.eps_svd = o.epsSVD;
+  m.svd_tol = o.svdTol;
+  return m;
+}
+
+bool GpuMarginalLinearSolver::solveSystem(std::vector<double>& outDx) {
+  const size_t C = _g.cameraCols();
+  std::vector<double> dx(_JCols);
+  _sv.resize(C);
+  _V.resize(C * C);
+  kb_marginal_options m = marg_opts(_lopt);
+  kb_marginal_info inf{};
+  int ok = 0;
+  const int rc = kb_solve_marginal(static_cast<kb_handle*>(_g.handle()), &m, dx.data(), &ok, &inf, _sv.data(),
+                                   _V.data());
+  if (rc < 0) throw Exception(std::string("kb_solve_marginal: ") + kb_last_error());
+  _svdRank = inf.rank;
+  _svdTolerance = inf.tolerance;
+  _svGap = inf.sv_gap;
+  if (ok) outDx = dx;
+  return ok != 0;
+}
+
+void GpuMarginalLinearSolver::analyzeMarginal() {
+  const size_t C = _g.cameraCols();
+  _sv.resize(C);
+  _V.resize(C * C);
+  kb_marginal_options m = marg_opts(_lopt);
+  kb_marginal_info inf{};
+  if (kb_analyze_marginal(static_cast<kb_handle*>(_g.handle()), &m, &inf, _sv.data(), _V.data()) < 0)
+    throw Exception(std::string("kb_analyze_marginal: ") + kb_last_error());
+  // rank, tolerance and gap stay those of the last solve when there was one (LinearSolver.cpp:518-524)
+  if (_svdRank == -1) {
+    _svdRank = inf.rank;
+    _svdTolerance = inf.tolerance;
+    _svGap = inf.sv_gap;
+  }
+}
+
+// ---------------------------------------------------------------- IncrementalEstimator
+IncrementalEstimator::IncrementalEstimator(const CalibrationProblem& base,
+                                           std::shared_ptr<MarginalLinearSystemSolver> solver, const Options& options,
+                                           const Optimizer2Options& optimizerOptions)
+    : _options(options), _optOptions(optimizerOptions), _solver(std::move(solver)), _problem(base) {
+  if (!_solver) throw LinearSystemSolver::Exception("IncrementalEstimator: the linear solver is null");
+  if (base.n_frames != 0 || !base.view_frame.empty())
+    throw LinearSystemSolver::Exception("IncrementalEstimator: the base problem must not hold frames");
+  _problem.view_offset.assign(1, 0u);
+  // IncrementalEstimator.cpp:66-71: the optimizer runs the GN policy over the marginal linear solver
+  _optOptions.linearSystemSolver = _solver;
+  _optOptions.trustRegionPolicy = std::make_shared<GaussNewtonTrustRegionPolicy>();
+}
+
+void IncrementalEstimator::appendBatch(const CalibrationBatch& b) {
+  if (b.frame_pose.size() != 7 || b.view_offset.size() != b.view_cam.size() + 1 ||
+      b.y.size() != 2 * b.corner_id.size() || (b.view_offset.empty() ? 0 : b.view_offset.back()) != b.corner_id.size())
+    throw LinearSystemSolver::Exception("addBatch: inconsistent batch arrays");
+  const uint32_t f = (uint32_t)_problem.n_frames, c0 = (uint32_t)_problem.corner_id.size();
+  for (size_t v = 0; v < b.view_cam.size(); ++v) {
+    if (b.view_cam[v] >= _problem.n_cams()) throw LinearSystemSolver::Exception("addBatch: camera index out of range");
+    _problem.view_frame.push_back(f);
+    _problem.view_cam.push_back(b.view_cam[v]);
+    _problem.view_offset.push_back(c0 + b.view_offset[v + 1]);
+  }
+  _problem.corner_id.insert(_problem.corner_id.end(), b.corner_id.begin(), b.corner_id.end());
+  _problem.y.insert(_problem.y.end(), b.y.begin(), b.y.end());
+  _problem.state.insert(_problem.state.end(), b.frame_pose.begin(), b.frame_pose.end());
+  _problem.n_frames++;
+}
+
+void IncrementalEstimator::removeLastBatch(size_t n_views, size_t n_corners) {
+  _problem.view_frame.resize(_problem.view_frame.size() - n_views);
+  _problem.view_cam.resize(_problem.view_cam.size() - n_views);
+  _problem.view_offset.resize(_problem.view_offset.size() - n_views);
+  _problem.corner_id.resize(_problem.corner_id.size() - n_corners);
+  _problem.y.resize(_problem.y.size() - 2 * n_corners);
+  _problem.state.resize(_problem.state.size() - 7);
+  _problem.n_frames--;
+}
+
+IncrementalEstimator::ReturnValue IncrementalEstimator::addBatch(const CalibrationBatch& batch, bool force) {
+  const auto t0 = std::chrono::steady_clock::now();
+  // insert the new batch; save the design variables in case it is rejected (:343-351)
+  const std::vector<double> saved = _problem.state;
+  appendBatch(batch);
+  // Optimizer2::initialize -> initMatrixStructure over the grown problem, then optimize (:373)
+  _solver->initMatrixStructure(_problem, false);
+  Optimizer2 optimizer(_optOptions);
+  const SolutionReturnValue srv = optimizer.optimize();
+  ReturnValue ret;
+  ret.numIterations = (size_t)srv.iterations;
+  ret.JStart = srv.JStart;
+  ret.JFinal = srv.JFinal;
+  if (_solver->getOptions().columnScaling) ret.singularValuesScaled = _solver->getSingularValues();  // :384-397
+  const std::vector<double> state = _solver->state();
+  // analyze the unscaled marginal system (:400)
+  _solver->analyzeMarginal();
+  ret.rankTheta = _solver->getSVDRank();
+  ret.rankThetaDeficiency = _solver->getSVDRankDeficiency();
+  ret.svdTolerance = _solver->getSVDTolerance();
+  ret.nobsBasis = _solver->getNullSpace();
+  ret.obsBasis = _solver->getRowSpace();
+  ret.sigma2Theta = _solver->getCovariance();
+  ret.singularValues = _solver->getSingularValues();
+  // validity (:419-422) and information gain (:425-426)
+  bool solutionValid = true;
+  if (_options.checkValidity && (srv.iterations == _optOptions.maxIterations || srv.JFinal >= srv.JStart))
+    solutionValid = false;
+  const double svLog2Sum = _solver->getSingularValuesLog2Sum();
+  ret.informationGain = 0.5 * (svLog2Sum - _svLog2Sum);
+  // keep the batch on an information gain or a rank increase of a valid solution, or when forced (:463-494)
+  bool keep = false;
+  if (((ret.informationGain > _options.infoGainDelta || ret.rankTheta > _rankTheta) && solutionValid) || force) {
+    if (ret.rankTheta < _rankTheta && _options.verbose)
+      std::cerr << "IncrementalEstimator::addBatch(): WARNING: RANK GOING DOWN!" << std::endl;
+    keep = true;
+    _informationGain = ret.informationGain;
+    _svLog2Sum = svLog2Sum;
+    _svdTolerance = ret.svdTolerance;
+    _rankTheta = ret.rankTheta;
+    _rankThetaDeficiency = ret.rankThetaDeficiency;
+    _initialCost = srv.JStart;
+    _finalCost = srv.JFinal;
+    _problem.state = state;
+  }
+  ret.batchAccepted = keep;
+  if (_options.verbose)
+    std::cout << "[IncrementalEstimator::addBatch] Batch #" << _problem.n_frames << " information gain "
+              << ret.informationGain << " rank " << ret.rankTheta << " cost " << ret.JStart << " -> " << ret.JFinal
+              << (keep ? " ACCEPTED" : " REJECTED") << std::endl;
+  if (!keep) {  // restore the design variables and drop the batch (:517-527)
+    removeLastBatch(batch.view_cam.size(), batch.corner_id.size());
+    _problem.state = saved;
+  }
+  ret.elapsedTime = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  return ret;
 }
 
 }  // namespace backend

@@ -7,6 +7,10 @@
 //   Optimizer2Options       aslam_optimizer/aslam_backend/include/aslam/backend/Optimizer2Options.hpp:9-42
 //   Optimizer2::optimize    aslam_optimizer/aslam_backend/src/Optimizer2.cpp:183-273
 //   SolutionReturnValue     aslam_optimizer/aslam_backend/include/aslam/backend/backend.hpp:11-24
+//   MarginalLinearSolver    aslam_incremental_calibration/incremental_calibration/src/core/LinearSolver.cpp:113-528
+//                           (calibration::LinearSolver; options LinearSolverOptions.cpp:30-38)
+//   IncrementalEstimator    aslam_incremental_calibration/incremental_calibration/src/core/IncrementalEstimator.cpp
+//                           :44-77, 337-530 (addBatch: GN optimize, marginal analysis, information-gain acceptance)
 // Same names, argument meaning and error behaviour (contract violations and device errors throw
 // LinearSystemSolver::Exception, a std::runtime_error; a numerically failed solve returns false).
 // Deviations, all because the device owns the design variables:
@@ -15,6 +19,7 @@
 //   * vectors are std::vector<double> instead of Eigen::VectorXd (Eigen is not a dependency here).
 #pragma once
 
+#include <cfloat>
 #include <cstddef>
 #include <cstdint>
 #include <memory>
@@ -129,6 +134,72 @@ class GpuLinearSystemSolver : public LinearSystemSolver {
   mutable bool _rhs_valid = false;
 };
 
+// ---------------------------------------------------------------- marginal (camera-block) solver
+/// LinearSolverOptions (LinearSolverOptions.cpp:30-38); Kalibr2 sets columnScaling = true, epsSVD = 1e-6
+/// (CalibrateCameras.cpp:263-267).  The QR part of the reference (epsQR, SPQR) is the frame-block
+/// elimination here; its options have no counterpart.
+struct LinearSolverOptions {
+  bool columnScaling = false;
+  double epsNorm = DBL_EPSILON;
+  double epsSVD = DBL_EPSILON;
+  double svdTol = -1.0;
+  bool verbose = false;
+};
+
+/// The calibration::LinearSolver surface the IncrementalEstimator drives (LinearSolver.h:60-236): the
+/// Schur complement onto the marginalized (camera) block solved by truncated SVD, plus the SVD statistics
+/// of the last solve (scaled when columnScaling) and of analyzeMarginal (unscaled).
+class MarginalLinearSystemSolver : public LinearSystemSolver {
+ public:
+  /// LinearSystemSolver::initMatrixStructure over a (re)assembled problem (IncrementalEstimator.cpp:593-596)
+  virtual void initMatrixStructure(const CalibrationProblem& problem, bool useDiagonalConditioner) = 0;
+  virtual std::vector<double> state() const = 0;
+  /// LinearSolver::analyzeMarginal (LinearSolver.cpp:468-528): SVD of the unscaled marginal system of the
+  /// last build.  As in the reference the rank is the one of the last solve.
+  virtual void analyzeMarginal() = 0;
+  const LinearSolverOptions& getOptions() const { return _lopt; }
+  std::ptrdiff_t getSVDRank() const { return _svdRank; }
+  std::ptrdiff_t getSVDRankDeficiency() const { return _svdRank == -1 ? -1 : (std::ptrdiff_t)_sv.size() - _svdRank; }
+  double getSVDTolerance() const { return _svdTolerance; }
+  double getSvGap() const { return _svGap; }
+  const std::vector<double>& getSingularValues() const { return _sv; }
+  /// V [C][C] row-major, right singular vector j in column j
+  const std::vector<double>& getMatrixV() const { return _V; }
+  double getSingularValuesLog2Sum() const;  // LinearSolver.cpp:196-201
+  std::vector<double> getNullSpace() const;  // [C][C - rank] (LinearSolver.cpp:166-171)
+  std::vector<double> getRowSpace() const;   // [C][rank] (:173-178)
+  std::vector<double> getCovariance() const; // [C][C] = V_r diag(1/sv_r) V_r^T (:180-187)
+
+ protected:
+  LinearSolverOptions _lopt;
+  std::ptrdiff_t _svdRank = -1;
+  double _svdTolerance = -1.0, _svGap = -1.0;
+  std::vector<double> _sv, _V;
+};
+
+/// MarginalLinearSystemSolver on one MI355X: build / cost / update through GpuLinearSystemSolver, the
+/// solve through kb_solve_marginal (k_marg: Jacobi SVD of the column-scaled Omega in LDS).
+class GpuMarginalLinearSolver : public MarginalLinearSystemSolver {
+ public:
+  explicit GpuMarginalLinearSolver(const LinearSolverOptions& o = LinearSolverOptions(),
+                                   const GpuOptions& g = GpuOptions());
+  void initMatrixStructure(const CalibrationProblem& problem, bool useDiagonalConditioner) override;
+  double evaluateError(size_t nThreads, bool useMEstimator) override { return _g.evaluateError(nThreads, useMEstimator); }
+  void buildSystem(size_t nThreads, bool useMEstimator) override { _g.buildSystem(nThreads, useMEstimator); }
+  void setConstantConditioner(double d) override { LinearSystemSolver::setConstantConditioner(d); }  // ignored (:247-280)
+  bool solveSystem(std::vector<double>& outDx) override;
+  std::string name() const override { return "kalibr_hip_marginal_svd"; }
+  const std::vector<double>& rhs() const override { return _g.rhs(); }
+  double rhsJtJrhs() override { return _g.rhsJtJrhs(); }
+  double applyStateUpdate(const std::vector<double>& dx) override { return _g.applyStateUpdate(dx); }
+  void revertLastStateUpdate() override { _g.revertLastStateUpdate(); }
+  std::vector<double> state() const override { return _g.state(); }
+  void analyzeMarginal() override;
+
+ private:
+  GpuLinearSystemSolver _g;
+};
+
 // ---------------------------------------------------------------- trust-region policies
 class TrustRegionPolicy {
  public:
@@ -224,6 +295,67 @@ class Optimizer2 {
   Optimizer2Options _options;
   std::vector<double> _dx;
   std::vector<double> _trace;
+};
+
+// ---------------------------------------------------------------- incremental estimator
+/// One batch = one synchronized set of views: a new target pose (frame) and its observations
+/// (CreateBatchProblem, CalibrationTools.hpp:440-521; CalibrateCameras.cpp:302-307).
+struct CalibrationBatch {
+  std::vector<double> frame_pose;    // 7: initial T_t_c guess of the frame (q xyzw | t), state layout
+  std::vector<uint8_t> view_cam;     // [n_views]
+  std::vector<uint32_t> view_offset; // [n_views + 1]
+  std::vector<uint16_t> corner_id;   // [n_corners]
+  std::vector<double> y;             // [n_corners][2]
+};
+
+/// IncrementalEstimator (IncrementalEstimator.cpp:44-77, 337-530): adds batches one at a time, optimizes the
+/// accumulated problem with Optimizer2 + GaussNewtonTrustRegionPolicy over the marginal linear solver, and
+/// keeps a batch only if it raises the information of the camera block (0.5 * delta sum log2 sv >
+/// infoGainDelta) or its SVD rank, on a valid solution.  A rejected batch is removed and the design
+/// variables restored.  The calibration group (cameras + baselines) takes the role of _margGroupId.
+struct IncrementalEstimatorOptions {  // IncrementalEstimator.h:83-95
+  double infoGainDelta = 0.2;
+  bool checkValidity = false;
+  bool verbose = false;
+};
+
+class IncrementalEstimator {
+ public:
+  using Options = IncrementalEstimatorOptions;
+  struct ReturnValue {  // IncrementalEstimator.h:97-142 (the QR fields have no counterpart)
+    bool batchAccepted = false;
+    double informationGain = 0.0;
+    std::ptrdiff_t rankTheta = -1, rankThetaDeficiency = -1;
+    double svdTolerance = 0.0;
+    std::vector<double> singularValues, singularValuesScaled;
+    std::vector<double> nobsBasis, obsBasis, sigma2Theta;  // unscaled (analyzeMarginal), row-major [C][.]
+    size_t numIterations = 0;
+    double JStart = 0.0, JFinal = 0.0, elapsedTime = 0.0;
+  };
+
+  /// `base` holds the cameras, the target and the initial calibration state (intrinsics + baselines) and no
+  /// frames; `solver` is the marginal solver the optimizer uses (GpuMarginalLinearSolver on the device).
+  IncrementalEstimator(const CalibrationProblem& base, std::shared_ptr<MarginalLinearSystemSolver> solver,
+                       const Options& options = Options(), const Optimizer2Options& optimizerOptions = Optimizer2Options());
+  ReturnValue addBatch(const CalibrationBatch& batch, bool force = false);
+  /// the accumulated problem of the accepted batches with the current design-variable values
+  const CalibrationProblem& getProblem() const { return _problem; }
+  size_t getNumBatches() const { return (size_t)_problem.n_frames; }
+  double getInformationGain() const { return _informationGain; }
+  std::ptrdiff_t getRankTheta() const { return _rankTheta; }
+  double getSvLog2Sum() const { return _svLog2Sum; }
+  const Options& getOptions() const { return _options; }
+
+ private:
+  void appendBatch(const CalibrationBatch& b);
+  void removeLastBatch(size_t n_views, size_t n_corners);
+  Options _options;
+  Optimizer2Options _optOptions;
+  std::shared_ptr<MarginalLinearSystemSolver> _solver;
+  CalibrationProblem _problem;
+  double _informationGain = 0.0, _svLog2Sum = 0.0, _svdTolerance = 0.0;
+  std::ptrdiff_t _rankTheta = -1, _rankThetaDeficiency = -1;
+  double _initialCost = 0.0, _finalCost = 0.0;
 };
 
 }  // namespace backend

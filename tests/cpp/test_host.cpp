@@ -3,7 +3,13 @@
 //                                                 vs the oracle's own loop (kbo_optimize): must agree bitwise
 //   test_host gpu <problem.bin> <lm|gn> <maxIt> : host-driven Optimizer2 over GpuLinearSystemSolver, the
 //                                                 device-resident loop (optimizeOnDevice) and kbo_optimize
+//   test_host incr-cpu <problem.bin> <delta> <maxIt> : IncrementalEstimator (one batch per frame) over an
+//                                                 oracle-backed marginal solver vs the oracle's own GN loop
+//                                                 (kbo_optimize with the marginal solve) + the addBatch rule
+//   test_host incr-gpu <problem.bin> <delta> <maxIt> : IncrementalEstimator over GpuMarginalLinearSolver vs
+//                                                 over the oracle-backed marginal solver
 // Prints one JSON line.  The oracle is test infrastructure only (oracle/kb_oracle.h).
+#include <cfloat>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -136,6 +142,222 @@ class OracleLinearSystemSolver : public LinearSystemSolver {
   double _cond = 0.0;
 };
 
+
+// calibration::LinearSolver over the oracle (arrow build, Schur onto the camera block, Jacobi SVD)
+class OracleMarginalSolver : public MarginalLinearSystemSolver {
+ public:
+  OracleMarginalSolver(const LinearSolverOptions& o, int nthreads) : _nt(nthreads) { _lopt = o; }
+  void initMatrixStructure(const CalibrationProblem& p, bool) override {
+    _p = p;
+    _op.reset(new OracleProblem(_p));
+    _state = p.state;
+    _C = kbo_cam_cols(&_op->P);
+    _F = p.n_frames;
+    _JCols = (size_t)kbo_total_cols(&_op->P);
+    _JRows = 2 * (size_t)p.n_corners();
+    _Hff.assign(36 * (size_t)_F, 0.0);
+    _Hfc.assign(6 * (size_t)_C * _F, 0.0);
+    _Hcc.assign((size_t)_C * _C, 0.0);
+    _gf.assign(6 * (size_t)_F, 0.0);
+    _gc.assign(_C, 0.0);
+    _A = kbo_arrow{};
+    _A.C = _C;
+    _A.F = _F;
+    _A.Hff = _Hff.data();
+    _A.Hfc = _Hfc.data();
+    _A.Hcc = _Hcc.data();
+    _A.gf = _gf.data();
+    _A.gc = _gc.data();
+    _rhs.assign(_JCols, 0.0);
+    _svdRank = -1;
+    _sv.clear();
+    _V.clear();
+  }
+  double evaluateError(size_t, bool) override { return kbo_eval_cost(&_op->P, _state.data(), _nt); }
+  void buildSystem(size_t, bool) override { kbo_build_arrow(&_op->P, _state.data(), _nt, &_A); }
+  bool solveSystem(std::vector<double>& dx) override {
+    std::vector<double> tmp(_JCols, 0.0);
+    kbo_marg_opts m = opts();
+    _sv.assign(_C, 0.0);
+    _V.assign((size_t)_C * _C, 0.0);
+    kbo_marg_info inf{};
+    inf.sv = _sv.data();
+    inf.V = _V.data();
+    const bool ok = kbo_arrow_solve_ex(&_A, 0.0, _nt, tmp.data(), &m, &inf) != 0;
+    _svdRank = inf.rank;
+    _svdTolerance = inf.tol;
+    _svGap = inf.gap;
+    if (ok) dx = tmp;
+    return ok;
+  }
+  void analyzeMarginal() override {
+    kbo_marg_opts un = opts();
+    un.column_scaling = 0;
+    std::vector<double> S((size_t)_C * _C), b(_C);
+    int okp = 1;
+    kbo_arrow_schur_partial(&_A, 0.0, 0, _F, S.data(), b.data(), &okp);
+    for (size_t q = 0; q < S.size(); ++q) S[q] = _Hcc[q] - S[q];
+    _sv.assign(_C, 0.0);
+    _V.assign((size_t)_C * _C, 0.0);
+    kbo_marg_info inf{};
+    inf.sv = _sv.data();
+    inf.V = _V.data();
+    kbo_marginal_solve(_C, S.data(), b.data(), nullptr, &un, nullptr, &inf);
+    if (_svdRank == -1) {
+      _svdRank = inf.rank;
+      _svdTolerance = inf.tol;
+      _svGap = inf.gap;
+    }
+  }
+  std::string name() const override { return "oracle_marginal_svd"; }
+  double rhsJtJrhs() override { return 0.0; }
+  double applyStateUpdate(const std::vector<double>& dx) override {
+    _backup = _state;
+    return kbo_apply_update(&_op->P, _state.data(), dx.data());
+  }
+  void revertLastStateUpdate() override { _state = _backup; }
+  std::vector<double> state() const override { return _state; }
+
+ private:
+  kbo_marg_opts opts() const {
+    kbo_marg_opts m{};
+    m.column_scaling = _lopt.columnScaling ? 1 : 0;
+    m.eps_norm = _lopt.epsNorm;
+    m.eps_svd = _lopt.epsSVD;
+    m.svd_tol = _lopt.svdTol;
+    m.n_rows = (double)_JRows;
+    return m;
+  }
+  CalibrationProblem _p;
+  std::unique_ptr<OracleProblem> _op;
+  std::vector<double> _state, _backup, _Hff, _Hfc, _Hcc, _gf, _gc;
+  kbo_arrow _A{};
+  int _C = 0, _F = 0, _nt = 1;
+};
+
+// the problem's frames as batches: base (no frames) + one CalibrationBatch per frame
+static CalibrationProblem base_of(const CalibrationProblem& p) {
+  CalibrationProblem b;
+  b.cam_model = p.cam_model;
+  b.target = p.target;
+  const size_t ncam = (size_t)p.n_cams() * KBO_MAX_INTR + 7 * (size_t)(p.n_cams() - 1);
+  b.state.assign(p.state.begin(), p.state.begin() + (long)ncam);
+  return b;
+}
+
+static std::vector<CalibrationBatch> batches_of(const CalibrationProblem& p) {
+  const size_t ncam = (size_t)p.n_cams() * KBO_MAX_INTR + 7 * (size_t)(p.n_cams() - 1);
+  std::vector<CalibrationBatch> out((size_t)p.n_frames);
+  for (int f = 0; f < p.n_frames; ++f) {
+    auto& b = out[(size_t)f];
+    b.frame_pose.assign(p.state.begin() + (long)(ncam + 7 * (size_t)f), p.state.begin() + (long)(ncam + 7 * (size_t)f + 7));
+    b.view_offset.push_back(0);
+  }
+  for (int v = 0; v < p.n_views(); ++v) {
+    auto& b = out[p.view_frame[(size_t)v]];
+    b.view_cam.push_back(p.view_cam[(size_t)v]);
+    for (uint32_t k = p.view_offset[(size_t)v]; k < p.view_offset[(size_t)v + 1]; ++k) {
+      b.corner_id.push_back(p.corner_id[k]);
+      b.y.push_back(p.y[2 * (size_t)k]);
+      b.y.push_back(p.y[2 * (size_t)k + 1]);
+    }
+    b.view_offset.push_back((uint32_t)b.corner_id.size());
+  }
+  return out;
+}
+
+struct IncrRun {
+  std::vector<int> accepted;
+  std::vector<double> gain, state;
+  std::vector<long> rank, iters;
+};
+
+static IncrRun run_estimator(const CalibrationProblem& p, std::shared_ptr<MarginalLinearSystemSolver> solver,
+                             double delta, int maxIt) {
+  IncrementalEstimator::Options eo;
+  eo.infoGainDelta = delta;
+  eo.checkValidity = true;  // CalibrateCameras.cpp:258-261
+  Optimizer2Options oo;
+  oo.maxIterations = maxIt;
+  oo.nThreads = 4;
+  IncrementalEstimator est(base_of(p), solver, eo, oo);
+  IncrRun r;
+  for (const auto& b : batches_of(p)) {
+    auto rv = est.addBatch(b);
+    r.accepted.push_back(rv.batchAccepted ? 1 : 0);
+    r.gain.push_back(rv.informationGain);
+    r.rank.push_back((long)rv.rankTheta);
+    r.iters.push_back((long)rv.numIterations);
+  }
+  r.state = est.getProblem().state;
+  return r;
+}
+
+// the addBatch rule (IncrementalEstimator.cpp:337-530) over the oracle's own loop (kbo_optimize + marginal)
+static IncrRun run_oracle_incremental(const CalibrationProblem& p, double delta, int maxIt) {
+  const auto batches = batches_of(p);
+  CalibrationProblem acc = base_of(p);
+  acc.view_offset.assign(1, 0u);
+  IncrRun r;
+  double svl = 0.0;
+  long rank_prev = -1;
+  for (const auto& b : batches) {
+    CalibrationProblem trial = acc;
+    const uint32_t c0 = (uint32_t)trial.corner_id.size();
+    for (size_t v = 0; v < b.view_cam.size(); ++v) {
+      trial.view_frame.push_back((uint32_t)trial.n_frames);
+      trial.view_cam.push_back(b.view_cam[v]);
+      trial.view_offset.push_back(c0 + b.view_offset[v + 1]);
+    }
+    trial.corner_id.insert(trial.corner_id.end(), b.corner_id.begin(), b.corner_id.end());
+    trial.y.insert(trial.y.end(), b.y.begin(), b.y.end());
+    trial.state.insert(trial.state.end(), b.frame_pose.begin(), b.frame_pose.end());
+    trial.n_frames++;
+    OracleProblem op(trial);
+    const int C = kbo_cam_cols(&op.P);
+    std::vector<double> st = trial.state, sv1(C), sv2(C);
+    kbo_marg_opts m{1, DBL_EPSILON, 1e-6, -1.0, 2.0 * trial.n_corners()};
+    kbo_marg_info si{}, ai{};
+    si.sv = sv1.data();
+    ai.sv = sv2.data();
+    kbo_options ko{1, 0.0, maxIt, 1e-3, 1e-3, 4, &m, &si, &ai};
+    kbo_srv srv{};
+    kbo_optimize(&op.P, st.data(), &ko, &srv, nullptr, 0);
+    const bool valid = !(srv.iterations == maxIt || srv.J_final >= srv.J_start);
+    const double gain = 0.5 * (ai.log2sum - svl);
+    const bool keep = (gain > delta || ai.rank > rank_prev) && valid;
+    r.accepted.push_back(keep ? 1 : 0);
+    r.gain.push_back(gain);
+    r.rank.push_back(ai.rank);
+    r.iters.push_back(srv.iterations);
+    if (keep) {
+      svl = ai.log2sum;
+      rank_prev = ai.rank;
+      trial.state = st;
+      acc = trial;
+    }
+  }
+  r.state = acc.state;
+  return r;
+}
+
+static std::string ints(const std::vector<int>& v) {
+  std::string s = "[";
+  for (size_t i = 0; i < v.size(); ++i) s += (i ? "," : "") + std::to_string(v[i]);
+  return s + "]";
+}
+static std::string longs(const std::vector<long>& v) {
+  std::string s = "[";
+  for (size_t i = 0; i < v.size(); ++i) s += (i ? "," : "") + std::to_string(v[i]);
+  return s + "]";
+}
+static double maxrel(const std::vector<double>& a, const std::vector<double>& b) {
+  double m = 0.0;
+  for (size_t i = 0; i < a.size() && i < b.size(); ++i)
+    m = std::max(m, std::fabs(a[i] - b[i]) / std::max(1.0, std::fabs(b[i])));
+  return m;
+}
+
 static std::shared_ptr<TrustRegionPolicy> make_policy(const std::string& p) {
   if (p == "lm") return std::make_shared<LevenbergMarquardtTrustRegionPolicy>(10.0);  // CalibrationTools.hpp:65
   return std::make_shared<GaussNewtonTrustRegionPolicy>();
@@ -156,6 +378,25 @@ int main(int argc, char** argv) {
   const int maxIt = std::atoi(argv[4]);
   try {
     CalibrationProblem p = load(argv[2]);
+    if (mode == "incr-cpu" || mode == "incr-gpu") {
+      const double delta = std::atof(argv[3]);
+      LinearSolverOptions lo;
+      lo.columnScaling = true;  // CalibrateCameras.cpp:263-267
+      lo.epsSVD = 1e-6;
+      const IncrRun a = run_estimator(p, std::make_shared<OracleMarginalSolver>(lo, 4), delta, maxIt);
+      const IncrRun b = mode == "incr-cpu" ? run_oracle_incremental(p, delta, maxIt)
+                                           : run_estimator(p, std::make_shared<GpuMarginalLinearSolver>(lo), delta, maxIt);
+      const size_t ncam = (size_t)p.n_cams() * KBO_MAX_INTR + 7 * (size_t)(p.n_cams() - 1);
+      std::printf(
+          "{\"accepted\": %s, \"ref_accepted\": %s, \"rank\": %s, \"ref_rank\": %s, \"iters\": %s, "
+          "\"ref_iters\": %s, \"gain_rel\": %.3e, \"gain0\": %.17g, \"state_len\": %zu, \"ref_state_len\": %zu, "
+          "\"cam_diff\": %.3e, \"frame_diff\": %.3e}\n",
+          ints(a.accepted).c_str(), ints(b.accepted).c_str(), longs(a.rank).c_str(), longs(b.rank).c_str(),
+          longs(a.iters).c_str(), longs(b.iters).c_str(), maxrel(a.gain, b.gain), a.gain.empty() ? 0.0 : a.gain[0],
+          a.state.size(), b.state.size(), maxdiff(a.state, b.state, 0, ncam),
+          maxdiff(a.state, b.state, ncam, b.state.size()));
+      return 0;
+    }
     Optimizer2Options opt;
     opt.maxIterations = maxIt;
     opt.convergenceDeltaX = 1e-3;  // CalibrationTools.hpp:57-66

@@ -67,3 +67,37 @@ def test_host_gpu_loops_match_oracle(driver, tmp_path, cfg, frames, policy):
         assert r[k] < 1e-6, r  # north_star tolerance on intrinsics / extrinsics
     for k in ("host_vs_ref_frame", "dev_vs_ref_frame", "host_vs_dev"):
         assert r[k] < 1e-6, r
+
+
+def run_incr(driver, tmp_path, mode, prob, delta, max_it):
+    path = str(tmp_path / "p.bin")
+    write_problem(path, prob)
+    r = subprocess.run([driver, mode, path, str(delta), str(max_it)], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+@pytest.mark.parametrize("cfg,frames,delta", [(1, 10, 0.2), (2, 8, 0.2), (2, 8, 5.0)])
+def test_incremental_estimator_matches_oracle(driver, tmp_path, cfg, frames, delta):
+    """IncrementalEstimator::addBatch (IncrementalEstimator.cpp:337-530): one batch per frame, GN over the
+    marginal solver, information-gain / rank acceptance.  The host estimator over an oracle-backed marginal
+    solver takes the same decisions as the addBatch rule over the oracle's own loop, bitwise."""
+    p = synth.make_config(cfg, n_frames=frames)
+    r = run_incr(driver, tmp_path, "incr-cpu", p, delta, 20)
+    assert r["accepted"] == r["ref_accepted"] and r["rank"] == r["ref_rank"], r
+    assert r["iters"] == r["ref_iters"], r
+    assert r["accepted"][0] == 1, r  # the first batch always raises the rank
+    if delta > 1.0:
+        assert 0 in r["accepted"], r  # a large threshold rejects some batches
+    assert r["gain_rel"] == 0.0 and r["cam_diff"] == 0.0 and r["frame_diff"] == 0.0, r
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg,frames,delta", [(1, 10, 0.2), (2, 8, 5.0)])
+def test_incremental_estimator_gpu_matches_oracle(driver, tmp_path, cfg, frames, delta):
+    p = synth.make_config(cfg, n_frames=frames)
+    r = run_incr(driver, tmp_path, "incr-gpu", p, delta, 20)
+    assert r["accepted"] == r["ref_accepted"] and r["rank"] == r["ref_rank"], r
+    assert r["iters"] == r["ref_iters"], r
+    assert r["gain_rel"] < 1e-6, r
+    assert r["cam_diff"] < 1e-6 and r["frame_diff"] < 1e-6, r
