@@ -393,3 +393,299 @@ def make_config(idx, p_view=1.0, n_frames=None, seed_offset=0, **kw):
     c = CONFIGS[idx]
     return make_problem(c["models"], n_frames or c["n_frames"], seed=20261015 + idx + seed_offset,
                         p_view=p_view, name=c["name"], **kw)
+
+
+# ---------------------------------------------------------------------------------------------
+# configs[4]: 2-cam + IMU continuous-time calibration on a B-spline pose trajectory.
+# The rig (IMU body b) moves in front of the fixed target (world = target frame) along a cubic
+# BSplinePose with a RotationVector rotation (bsplines/src/BSplinePose.cpp; RotationVector.cpp).
+# Truth = the spline with the coefficients below; camera and IMU measurements are generated from it.
+# ---------------------------------------------------------------------------------------------
+
+def bspline_basis(order, knots, seg):
+    """Basis matrix of valid segment `seg`: the M(k, i) recursion of BSpline.cpp:70-152."""
+    def d0(k, i, j):
+        den = knots[j + k - 1] - knots[j]
+        return 0.0 if den <= 0 else (knots[i] - knots[j]) / den
+
+    def d1(k, i, j):
+        den = knots[j + k - 1] - knots[j]
+        return 0.0 if den <= 0 else (knots[i + 1] - knots[i]) / den
+
+    def M(k, i):
+        if k == 1:
+            return np.ones((1, 1))
+        Mp = M(k - 1, i)
+        M1 = np.vstack([Mp, np.zeros((1, k - 1))])
+        M2 = np.vstack([np.zeros((1, k - 1)), Mp])
+        A = np.zeros((k - 1, k))
+        B = np.zeros((k - 1, k))
+        for idx in range(k - 1):
+            j = i - k + 2 + idx
+            A[idx, idx], A[idx, idx + 1] = 1 - d0(k, i, j), d0(k, i, j)
+            B[idx, idx], B[idx, idx + 1] = -d1(k, i, j), d1(k, i, j)
+        return M1 @ A + M2 @ B
+
+    return M(order, seg + order - 1)
+
+
+def bspline_weights(order, knots, t, deriv):
+    """(bidx, w[order]) of BSpline::evalDAndJacobian at t (BSpline.cpp:237-387)."""
+    knots = np.asarray(knots)
+    n = knots.size
+    tmin, tmax = knots[order - 1], knots[n - order]
+    if t < tmin or t > tmax + 1e-10:
+        raise ValueError("time outside the spline interval")
+    if abs(tmax - t) < 1e-10:
+        t = tmax
+    idx = n - order - 1 if t == tmax else int(np.searchsorted(knots, t, side="right")) - 1
+    dt = knots[idx + 1] - knots[idx]
+    u = 0.0 if dt <= 0 else (t - knots[idx]) / dt
+    mult = 0.0 if dt <= 0 else 1.0 / dt ** deriv
+    uv = np.zeros(order)
+    uu = 1.0
+    for i in range(deriv, order):
+        dm = 1
+        for q in range(deriv):
+            dm *= i - q
+        uv[i] = mult * uu * dm
+        uu *= u
+    bidx = idx - order + 1
+    return bidx, bspline_basis(order, knots, bidx).T @ uv
+
+
+def rv_to_C(a):
+    """RotationVector::parametersToRotationMatrix (RotationVector.cpp:10-52) = standard exp(-[a]x)."""
+    return rotvec(-np.asarray(a, dtype=float))
+
+
+def rv_from_C(C):
+    """RotationVector::rotationMatrixToParameters (RotationVector.cpp:54-78)."""
+    tr = max(-1.0, min((C[0, 0] + C[1, 1] + C[2, 2] - 1.0) * 0.5, 1.0))
+    a = np.arccos(tr)
+    if abs(a) < 1e-14:
+        return np.zeros(3)
+    p = np.array([C[2, 1] - C[1, 2], C[0, 2] - C[2, 0], C[1, 0] - C[0, 1]])
+    n2 = np.linalg.norm(p)
+    if abs(n2) < 1e-14:
+        return np.zeros(3)
+    return (-a / n2) * p
+
+
+def rv_S(a):
+    """RotationVector::parametersToSMatrix (RotationVector.cpp:80-103)."""
+    a = np.asarray(a, dtype=float)
+    ang = np.linalg.norm(a)
+    if ang < 1e-14:
+        return np.eye(3)
+    ax = a / ang
+    c1 = -2.0 * np.sin(ang / 2) ** 2 / ang
+    c2 = (ang - np.sin(ang)) / ang
+    X = np.array([[0, -ax[2], ax[1]], [ax[2], 0, -ax[0]], [-ax[1], ax[0], 0]])
+    return np.eye(3) + c1 * X + c2 * X @ X
+
+
+@dataclass
+class SplineProblem:
+    order: int
+    knots: np.ndarray
+    cam_model: np.ndarray
+    target: np.ndarray
+    frame_time: np.ndarray
+    view_frame: np.ndarray
+    view_cam: np.ndarray
+    view_offset: np.ndarray
+    corner_id: np.ndarray
+    y: np.ndarray
+    imu_time: np.ndarray
+    imu_gyro: np.ndarray
+    imu_acc: np.ndarray
+    sigma_gyro: float
+    sigma_acc: float
+    state_truth: np.ndarray
+    state_init: np.ndarray
+    name: str = ""
+    meta: dict = field(default_factory=dict)
+
+    @property
+    def n_cams(self):
+        return int(self.cam_model.size)
+
+    @property
+    def n_frames(self):
+        return int(self.frame_time.size)
+
+    @property
+    def n_views(self):
+        return int(self.view_frame.size)
+
+    @property
+    def n_corners(self):
+        return int(self.corner_id.size)
+
+    @property
+    def n_imu(self):
+        return int(self.imu_time.size)
+
+    @property
+    def n_coeffs(self):
+        return int(self.knots.size - self.order)
+
+    @property
+    def cam_cols(self):
+        return int(sum(NINTR[int(m)] for m in self.cam_model)) + 6 * (self.n_cams - 1) + 6 + 9
+
+    @property
+    def total_cols(self):
+        return self.cam_cols + 6 * self.n_coeffs
+
+    @property
+    def off_coeff(self):
+        return self.n_cams * MAX_INTR + POSE * (self.n_cams - 1) + POSE + 9
+
+
+def spline_state_size(n_cams, n_coeffs):
+    return n_cams * MAX_INTR + POSE * (n_cams - 1) + POSE + 9 + 6 * n_coeffs
+
+
+def spline_eval(order, knots, coeffs, t, deriv):
+    b, w = bspline_weights(order, knots, t, deriv)
+    return w @ coeffs[b: b + order]
+
+
+def make_spline_problem(models, n_frames, seed, cam_rate=20.0, imu_rate=200.0, knots_per_second=50.0,
+                        order=4, noise_px=0.3, sigma_gyro=0.005, sigma_acc=0.05, min_corners=12,
+                        resolution=(1280, 1024), name="", init_noise=True):
+    """Synthesise configs[4]: an N-camera rig + IMU on a B-spline trajectory in front of the AprilGrid."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    W, H = resolution
+    N = len(models)
+    target = aprilgrid_points()
+    tcen = target.mean(axis=0)
+    base = make_problem(models, 1, seed, init_noise=False)  # camera truth (intrinsics, baselines)
+    intr_truth = base.state_truth[: N * MAX_INTR].reshape(N, MAX_INTR)
+    cam_T_c0 = [np.eye(4)]
+    base_T = []
+    for j in range(N - 1):
+        o = N * MAX_INTR + POSE * j
+        B = pose_to_T(base.state_truth[o: o + POSE])
+        base_T.append(B)
+        cam_T_c0.append(B @ cam_T_c0[-1])
+    # IMU -> cam0
+    T_c0_b = np.eye(4)
+    T_c0_b[:3, :3] = rotvec(np.deg2rad(np.array([2.0, -3.0, 1.5])))
+    T_c0_b[:3, 3] = [0.03, -0.02, 0.01]
+    t0 = 0.0
+    span = (n_frames - 1) / cam_rate  # frames at t0 .. t0 + span
+    dtk = 1.0 / knots_per_second
+    nseg = max(1, int(np.ceil(span / dtk - 1e-9)))
+    n_knots = nseg + 2 * order - 1  # uniform knots, [t_min, t_max] = [t0, t0 + nseg dtk]
+    knots = t0 + dtk * (np.arange(n_knots) - (order - 1))
+    K = n_knots - order
+    # smooth excitation (rotation about all axes, translation) of cam0 in the target frame
+    ph = rng.uniform(0, 2 * np.pi, 6)
+    fr = np.array([0.23, 0.31, 0.17, 0.13, 0.19, 0.11])
+    amp_r = np.deg2rad(np.array([14.0, 12.0, 18.0]))
+    rig_centre = np.array([-0.12 * (N - 1) / 2.0, 0.0, 0.0])
+
+    def T_w_c0(t):
+        R = rotvec(amp_r * np.sin(2 * np.pi * fr[:3] * t + ph[:3]))
+        c = tcen - rig_centre + np.array([0.12 * np.sin(2 * np.pi * fr[3] * t + ph[3]),
+                                          0.10 * np.sin(2 * np.pi * fr[4] * t + ph[4]),
+                                          -1.0 + 0.2 * np.sin(2 * np.pi * fr[5] * t + ph[5])])
+        T = np.eye(4)
+        T[:3, :3] = R
+        T[:3, 3] = c
+        return T
+
+    # Greville abscissae -> coefficients [p | rotation vector] of T_w_b = T_w_c0 T_c0_b
+    coeffs = np.zeros((K, 6))
+    for k in range(K):
+        tau = knots[k + 1: k + order].mean()
+        Twb = T_w_c0(tau) @ T_c0_b
+        coeffs[k, :3] = Twb[:3, 3]
+        coeffs[k, 3:] = rv_from_C(Twb[:3, :3])
+    frame_time = t0 + np.arange(n_frames) / cam_rate
+    vf, vc, counts, cid, ys = [], [], [], [], []
+    T_b_c0 = inv_T(T_c0_b)
+    for f, t in enumerate(frame_time):
+        v = spline_eval(order, knots, coeffs, t, 0)
+        Twb = np.eye(4)
+        Twb[:3, :3] = rv_to_C(v[3:])
+        Twb[:3, 3] = v[:3]
+        T_c0_w = inv_T(Twb @ T_b_c0)
+        for i in range(N):
+            T = cam_T_c0[i] @ T_c0_w
+            pc = (T[:3, :3] @ target.T).T + T[:3, 3]
+            kp, valid = project(models[i], intr_truth[i], pc)
+            ok = valid & (pc[:, 2] > 0.05) & (kp[:, 0] >= 5) & (kp[:, 0] <= W - 5) & (kp[:, 1] >= 5) & (kp[:, 1] <= H - 5)
+            ids = np.nonzero(ok)[0]
+            if ids.size < min_corners:
+                continue
+            vf.append(f)
+            vc.append(i)
+            counts.append(ids.size)
+            cid.append(ids)
+            ys.append(kp[ids] + rng.normal(0.0, noise_px, (ids.size, 2)))
+    g_w = 9.81 * np.array([0.08, -0.99, 0.06]) / np.linalg.norm([0.08, -0.99, 0.06])
+    b_g = np.array([0.002, -0.001, 0.003])
+    b_a = np.array([0.05, -0.03, 0.02])
+    t_max = knots[n_knots - order]
+    imu_time = t0 + np.arange(int(np.floor((t_max - t0) * imu_rate + 1e-9)) + 1) / imu_rate
+    gyro = np.zeros((imu_time.size, 3))
+    acc = np.zeros((imu_time.size, 3))
+    for m, t in enumerate(imu_time):
+        v0 = spline_eval(order, knots, coeffs, t, 0)
+        v1 = spline_eval(order, knots, coeffs, t, 1)
+        v2 = spline_eval(order, knots, coeffs, t, 2)
+        Cwb = rv_to_C(v0[3:])
+        om = -Cwb.T @ rv_S(v0[3:]) @ v1[3:]   # BSplinePose::angularVelocityBodyFrame
+        fb = Cwb.T @ (v2[:3] - g_w)
+        gyro[m] = om + b_g + rng.normal(0.0, sigma_gyro, 3)
+        acc[m] = fb + b_a + rng.normal(0.0, sigma_acc, 3)
+    st = np.zeros(spline_state_size(N, K))
+    st[: N * MAX_INTR] = intr_truth.reshape(-1)
+    so = N * MAX_INTR
+    for j, B in enumerate(base_T):
+        st[so + POSE * j: so + POSE * (j + 1)] = pose_from_Rt(B[:3, :3], B[:3, 3])
+    so += POSE * (N - 1)
+    st[so: so + POSE] = pose_from_Rt(T_c0_b[:3, :3], T_c0_b[:3, 3])
+    so += POSE
+    st[so: so + 3] = b_g
+    st[so + 3: so + 6] = b_a
+    st[so + 6: so + 9] = g_w
+    so += 9
+    st[so:] = coeffs.reshape(-1)
+    st_init = st.copy()
+    if init_noise:
+        pinit = make_problem(models, 1, seed, init_noise=True)
+        st_init[: N * MAX_INTR] = pinit.state_init[: N * MAX_INTR]
+        so = N * MAX_INTR
+        for k in range(N):  # baselines + T_c0_b: 1 deg / 1 cm
+            o = so + POSE * k
+            T = pose_to_T(st[o: o + POSE])
+            Rn = rotvec(np.deg2rad(1.0) * rng.normal(size=3) / np.sqrt(3)) @ T[:3, :3]
+            tn = T[:3, 3] + 0.01 * rng.normal(size=3) / np.sqrt(3)
+            st_init[o: o + POSE] = pose_from_Rt(Rn, tn)
+        so += POSE * N
+        st_init[so: so + 6] = 0.0  # biases
+        st_init[so + 6: so + 9] = rotvec(np.deg2rad(3.0) * rng.normal(size=3) / np.sqrt(3)) @ g_w
+        so += 9
+        c = st_init[so:].reshape(K, 6)
+        c[:, :3] += 0.005 * rng.normal(size=(K, 3))
+        c[:, 3:] += np.deg2rad(0.5) * rng.normal(size=(K, 3))
+    return SplineProblem(
+        order=order, knots=knots, cam_model=np.asarray(models, dtype=np.int32), target=target,
+        frame_time=frame_time, view_frame=np.asarray(vf, dtype=np.int32), view_cam=np.asarray(vc, dtype=np.int32),
+        view_offset=np.concatenate([[0], np.cumsum(counts)]).astype(np.int32),
+        corner_id=np.concatenate(cid).astype(np.int32), y=np.concatenate(ys, axis=0).astype(np.float64),
+        imu_time=imu_time, imu_gyro=gyro, imu_acc=acc, sigma_gyro=sigma_gyro, sigma_acc=sigma_acc,
+        state_truth=st, state_init=st_init, name=name,
+        meta={"seed": seed, "cam_rate": cam_rate, "imu_rate": imu_rate, "knots_per_second": knots_per_second,
+              "noise_px": noise_px})
+
+
+def make_spline_config(n_frames=None, seed_offset=0, **kw):
+    """configs[4]: '2-cam + IMU continuous-time B-spline (aslam_splines) calibration, 1200 frames'."""
+    return make_spline_problem([PINHOLE_RADTAN] * 2, n_frames or 1200, seed=20261015 + 5 + seed_offset,
+                               name="2-cam + IMU continuous-time B-spline calibration, 1200 frames", **kw)

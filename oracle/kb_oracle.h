@@ -160,6 +160,71 @@ int kbo_optimize(const kbo_problem* P, double* state, const kbo_options* o, kbo_
 /* CPU baseline: time n_iter GN iterations (build + solve + update + cost), returns seconds. */
 double kbo_time_gn(const kbo_problem* P, double* state, int n_iter, int nthreads);
 
+/* ------------------------------------------------------------------------------------------------
+ * configs[4]: continuous-time calibration on a B-spline pose trajectory (kb_oracle_spline.c).
+ * Camera i at frame time t_f:  T_ci_w = B_{i-1} ... B_0 * T_c0_b * T_wb(t_f)^-1
+ * IMU sample m at t_m:          gyro w_m = w_b(t_m) + b_g,  accel a_m = C_wb^T (p_ddot - g_w) + b_a
+ * State:  intr [n_cams][KBO_MAX_INTR] | base [n_cams-1][7] | T_c0_b [7] | b_g [3] | b_a [3] | g_w [3] |
+ *         coefficients [K][6] (BSplinePose curve value [p | rotation vector])
+ * Columns: [intr | B_j (dphi, dt) | T_c0_b (dphi, dt) | b_g | b_a | g_w | coefficients 6K]
+ * ------------------------------------------------------------------------------------------------ */
+typedef struct {
+  int order;             /* spline order (4 = cubic) */
+  int n_knots;
+  const double* knots;   /* non-decreasing */
+  int n_cams, n_target;
+  const int* cam_model;
+  const double* target;
+  int n_frames;
+  const double* frame_time;
+  int n_views, n_corners;
+  const int* view_frame;  /* views sorted by frame */
+  const int* view_cam;
+  const int* view_offset;
+  const int* corner_id;
+  const double* y;
+  int n_imu;
+  const double* imu_time;
+  const double* imu_gyro; /* [n_imu][3] */
+  const double* imu_acc;  /* [n_imu][3] */
+  double sigma_gyro, sigma_acc;
+} kbo_sp_problem;
+
+typedef struct {
+  int C, K, order;
+  double* Hcc;   /* [C][C] */
+  double* Hsc;   /* [6K][C] */
+  double* Hband; /* [K][order][6][6]: block (k, k+d) */
+  double* gc;    /* [C]  = -J_c^T e */
+  double* gs;    /* [6K] */
+  double cost;
+} kbo_sp_system;
+
+int kbo_bspline_num_coeffs(int order, int n_knots);
+void kbo_bspline_basis(int order, const double* knots, int segment, double* M);
+/* basis weights of derivative `deriv` at t (BSpline::evalDAndJacobian's B^T u); returns the first
+ * coefficient index (bidx) or -1 outside [t_min, t_max] */
+int kbo_bspline_weights(int order, const double* knots, int n_knots, double t, int deriv, double* w);
+void kbo_rv_to_C(const double a[3], double Cm[9]);
+void kbo_rv_S(const double a[3], double S[9]);
+void kbo_rv_dSv(const double a[3], const double v[3], double D[9]);
+int kbo_sp_state_size(const kbo_sp_problem* P);
+int kbo_sp_num_coeffs(const kbo_sp_problem* P);
+int kbo_sp_cam_cols(const kbo_sp_problem* P);
+int kbo_sp_total_cols(const kbo_sp_problem* P);
+double kbo_sp_reproj_dense(const kbo_sp_problem* P, const double* st, int v, int k, double e[2], double* J, int ncols);
+double kbo_sp_imu_dense(const kbo_sp_problem* P, const double* st, int m, double e[6], double* J, int ncols);
+double kbo_sp_eval_cost(const kbo_sp_problem* P, const double* st, int nthreads);
+int kbo_sp_system_alloc(const kbo_sp_problem* P, kbo_sp_system* A);
+void kbo_sp_system_free(kbo_sp_system* A);
+void kbo_sp_build(const kbo_sp_problem* P, const double* st, int nthreads, kbo_sp_system* A);
+int kbo_sp_solve(const kbo_sp_system* A, double lambda, double* dx);
+int kbo_sp_dense_solve(const kbo_sp_system* A, double lambda, double* dx);
+double kbo_sp_apply_update(const kbo_sp_problem* P, double* st, const double* dx);
+int kbo_sp_optimize(const kbo_sp_problem* P, double* st, const kbo_options* o, kbo_srv* srv, double* trace,
+                    int trace_cap);
+double kbo_sp_time_gn(const kbo_sp_problem* P, double* st, int n_iter, int nthreads);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,207 @@
+"""configs[4] oracle (oracle/kb_oracle_spline.c): B-spline basis, RotationVector kinematics, term Jacobians,
+normal equations and the banded Schur solve.  CPU only.
+
+Pinning: the reference holds no numeric spline fixture; its own tests are identities
+and finite-difference checks, restated here:
+  * SplineTests.cpp:133-175 (testGetBi): basis weights sum to 1, successive local coefficient indices;
+  * SplineTests.cpp:54-94 (testBSplineJacobian) / TestBSplineExpressions.cpp:111-288: finite-difference
+    Jacobians of the spline value and of the pose expressions;
+  * RotationalKinematicsTests.cpp: parametersToRotationMatrix / rotationMatrixToParameters round trip and the
+    S-matrix identity.
+The IMU terms have no reference counterpart: their parity is "unpinned" beyond the finite differences below.
+"""
+import numpy as np
+import pytest
+
+from kalibr_amd import synth
+from oracle import oracle as O
+
+
+@pytest.fixture(scope="module")
+def small():
+    p = synth.make_spline_config(n_frames=16)
+    return p, O.SplineOracle(p)
+
+
+def test_uniform_cubic_basis_known_answer():
+    # uniform knots: M(4, i) is the textbook uniform cubic B-spline matrix (rows = powers of u)
+    knots = np.arange(12, dtype=float)
+    M = np.zeros(16)
+    O._sp_lib().kbo_bspline_basis(4, O._d(knots), 2, O._d(M))
+    ref = np.array([[1, 4, 1, 0], [-3, 0, 3, 0], [3, -6, 3, 0], [-1, 3, -3, 1]]) / 6.0
+    assert np.allclose(M.reshape(4, 4), ref, atol=1e-15)
+    assert np.allclose(synth.bspline_basis(4, knots, 2), ref, atol=1e-15)
+
+
+@pytest.mark.parametrize("order", [2, 3, 4, 5, 6])
+def test_basis_weights_partition_of_unity(order):
+    """SplineTests.cpp:133-175: the local basis values sum to 1; derivatives of a constant vanish."""
+    rng = np.random.default_rng(order)
+    knots = np.cumsum(rng.uniform(0.1, 1.0, 4 * order + 6))  # non-uniform, strictly increasing
+    tmin, tmax = knots[order - 1], knots[knots.size - order]
+    for t in np.concatenate([rng.uniform(tmin, tmax, 25), [tmin, tmax]]):
+        b, w = O.bspline_weights(order, knots, t, 0)
+        assert 0 <= b <= knots.size - 2 * order + 1
+        assert abs(w.sum() - 1.0) < 1e-12
+        for d in range(1, order):
+            _, wd = O.bspline_weights(order, knots, t, d)
+            assert abs(wd.sum()) < 1e-9 * max(1.0, np.abs(wd).max())
+        b2, w2 = synth.bspline_weights(order, knots, t, 0)
+        assert b2 == b and np.allclose(w2, w, atol=1e-14)
+    assert O.bspline_weights(order, knots, tmin - 1e-3, 0)[0] == -1
+
+
+@pytest.mark.parametrize("order", [3, 4, 6])
+def test_basis_derivative_finite_difference(order):
+    """evalD(t, d) is the d-th time derivative of eval(t) (SplineTests.cpp:54-94 style)."""
+    rng = np.random.default_rng(10 + order)
+    knots = np.cumsum(rng.uniform(0.2, 1.0, 4 * order + 6))
+    c = rng.normal(size=knots.size - order)
+    tmin, tmax = knots[order - 1], knots[knots.size - order]
+
+    def val(t, d):
+        b, w = O.bspline_weights(order, knots, t, d)
+        return w @ c[b: b + order]
+
+    h = 1e-6
+    for t in rng.uniform(tmin + 0.01, tmax - 0.01, 10):
+        for d in range(1, order - 1):
+            num = (val(t + h, d - 1) - val(t - h, d - 1)) / (2 * h)
+            if abs(knots[np.searchsorted(knots, t)] - t) < 2 * h or abs(knots[np.searchsorted(knots, t) - 1] - t) < 2 * h:
+                continue
+            assert abs(num - val(t, d)) < 1e-6 * max(1.0, abs(num)), (t, d)
+
+
+def test_rotation_vector_kinematics():
+    rng = np.random.default_rng(3)
+    h = 1e-7
+    for _ in range(20):
+        a = rng.normal(size=3)
+        a *= rng.uniform(0.05, 3.0) / np.linalg.norm(a)  # angle < pi: the parameterisation's domain
+        C = O.rv_to_C(a)
+        assert np.allclose(C @ C.T, np.eye(3), atol=1e-14)
+        assert np.allclose(C, synth.rv_to_C(a), atol=1e-14)
+        assert np.allclose(synth.rv_from_C(C), a, atol=1e-10)
+        S = O.rv_S(a)
+        assert np.allclose(S, synth.rv_S(a), atol=1e-14)
+        # C(a + da) = (I - [S da]x) C(a) to first order (the rotation-perturbation convention of JT)
+        for j in range(3):
+            da = np.zeros(3)
+            da[j] = h
+            dC = (O.rv_to_C(a + da) - O.rv_to_C(a - da)) / (2 * h)
+            phi = S[:, j]
+            phix = np.array([[0, -phi[2], phi[1]], [phi[2], 0, -phi[0]], [-phi[1], phi[0], 0]])
+            assert np.allclose(dC, -phix @ C, atol=1e-7)
+        # d(S(a) v)/da
+        v = rng.normal(size=3)
+        D = O.rv_dSv(a, v)
+        Dn = np.zeros((3, 3))
+        for j in range(3):
+            da = np.zeros(3)
+            da[j] = h
+            Dn[:, j] = (O.rv_S(a + da) @ v - O.rv_S(a - da) @ v) / (2 * h)
+        assert np.allclose(D, Dn, atol=1e-7)
+    # small-angle branch of dSv is continuous with the closed form
+    a = np.array([3e-5, -2e-5, 1e-5])
+    v = np.array([0.3, 0.2, -0.1])
+    Dn = np.zeros((3, 3))
+    for j in range(3):
+        da = np.zeros(3)
+        da[j] = 1e-7
+        Dn[:, j] = (O.rv_S(a + da) @ v - O.rv_S(a - da) @ v) / 2e-7
+    assert np.allclose(O.rv_dSv(a, v), Dn, atol=1e-6)
+
+
+def _fd_jac(o, fn, st, h=1e-6):
+    e0 = fn(st)[0]
+    J = np.zeros((e0.size, o.ncols))
+    for j in range(o.ncols):
+        d = np.zeros(o.ncols)
+        d[j] = h
+        sp, _ = o.apply_update(st, d)
+        sm, _ = o.apply_update(st, -d)
+        J[:, j] = (fn(sp)[0] - fn(sm)[0]) / (2 * h)
+    return J
+
+
+def test_reprojection_jacobian_finite_difference(small):
+    """TestBSplineExpressions.cpp:111-288 / ErrorTermTestHarness: every column of the reprojection term
+    (intrinsics, baseline, T_c0_b, the order active spline coefficients) against central differences under
+    the DV update rules."""
+    p, o = small
+    st = p.state_init
+    for v, k in [(0, 3), (1, 10), (p.n_views - 1, 7)]:
+        e, J = o.reproj_dense(st, v, k)
+        Jn = _fd_jac(o, lambda s: o.reproj_dense(s, v, k), st)
+        assert np.abs(J - Jn).max() < 1e-6 * np.abs(J).max(), (v, k)
+        nz = np.count_nonzero(J[:, o.C:].any(axis=0))  # at a knot the last basis weight is exactly 0
+        assert 6 * (p.order - 1) <= nz <= 6 * p.order
+
+
+def test_imu_jacobian_finite_difference(small):
+    p, o = small
+    st = p.state_init
+    for m in [0, p.n_imu // 2, p.n_imu - 1]:
+        e, J = o.imu_dense(st, m)
+        Jn = _fd_jac(o, lambda s: o.imu_dense(s, m), st)
+        assert np.abs(J - Jn).max() < 1e-6 * np.abs(J).max(), m
+
+
+def test_cost_at_truth_is_noise(small):
+    p, o = small
+    c = o.cost(p.state_truth)
+    expect = 2 * p.n_corners * p.meta["noise_px"] ** 2 + 6 * p.n_imu
+    assert 0.7 * expect < c < 1.3 * expect
+    assert o.cost(p.state_init) > 100 * c
+
+
+def test_normal_equations_and_banded_solve(small):
+    """H = J^T J, g = -J^T e (TestOptimizer.cpp:101-120) over the dense term rows; the banded Schur solve agrees
+    with a dense Cholesky of the same system (solver_tests.cpp:110-111 style, 1e-10)."""
+    p, o = small
+    st = p.state_init
+    rows, es = [], []
+    for v in range(p.n_views):
+        for k in range(p.view_offset[v + 1] - p.view_offset[v]):
+            e, J = o.reproj_dense(st, v, k)
+            rows.append(J)
+            es.append(e)
+    for m in range(p.n_imu):
+        e, J = o.imu_dense(st, m)
+        rows.append(J)
+        es.append(e)
+    J = np.vstack(rows)
+    e = np.concatenate(es)
+    s = o.system(st, nthreads=3)
+    Cc, K = o.C, o.K
+    H = np.zeros((o.ncols, o.ncols))
+    H[:Cc, :Cc] = s["Hcc"]
+    H[Cc:, :Cc] = s["Hsc"]
+    H[:Cc, Cc:] = s["Hsc"].T
+    for k in range(K):
+        for d in range(p.order):
+            if k + d < K:
+                H[Cc + 6 * k: Cc + 6 * k + 6, Cc + 6 * (k + d): Cc + 6 * (k + d) + 6] = s["Hband"][k, d]
+                H[Cc + 6 * (k + d): Cc + 6 * (k + d) + 6, Cc + 6 * k: Cc + 6 * k + 6] = s["Hband"][k, d].T
+    Href = J.T @ J
+    assert np.abs(H - Href).max() <= 1e-12 * np.abs(Href).max()
+    assert np.abs(np.concatenate([s["gc"], s["gs"]]) + J.T @ e).max() <= 1e-12 * np.abs(J.T @ e).max()
+    assert abs(s["cost"] - e @ e) <= 1e-12 * (e @ e)
+    for lam in (0.0, 10.0):
+        ok, dx = o.solve(s, lam)
+        ok2, dx2 = o.solve(s, lam, dense=True)
+        assert ok and ok2
+        assert np.abs(dx - dx2).max() <= 1e-8 * np.abs(dx2).max()
+
+
+def test_gauss_newton_recovers_calibration():
+    p = synth.make_spline_config(n_frames=200)
+    o = O.SplineOracle(p)
+    st, res = o.optimize(p.state_init, policy="gn", max_iterations=20, eps_j=1e-3, nthreads=8)
+    assert res["iterations"] < 20 and res["J_final"] < 1e-4 * res["J_start"]
+    N = p.n_cams
+    intr = (st - p.state_truth)[: N * synth.MAX_INTR].reshape(N, synth.MAX_INTR)
+    assert np.abs(intr[:, :4]).max() < 1.0  # fu fv cu cv within 1 px
+    imu = slice(p.off_coeff - 9, p.off_coeff)
+    assert np.abs(st[imu][:3] - p.state_truth[imu][:3]).max() < 1e-3  # gyro bias
+    assert np.abs(st[imu][6:] - p.state_truth[imu][6:]).max() < 0.05  # gravity
