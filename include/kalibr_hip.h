@@ -177,6 +177,72 @@ int kb_comm_init(kb_handle* h, const void* unique_id128, int32_t nranks, int32_t
 /* Self test of the f64 MFMA fragment layout used by the build kernel (A = I, asymmetric B). */
 int kb_selftest_mfma(double* max_err);
 
+/* ------------------------------------------------------------------------------------------------
+ * Continuous-time calibration (configs[4]): the rig (IMU body b) on a B-spline pose trajectory
+ * T_wb(t) (bsplines::BSplinePose with a RotationVector rotation, BSplinePose.cpp:21-41,384-412;
+ * one DesignVariableMappedVector<6> per coefficient, BSplinePoseDesignVariable.cpp:9-19).
+ *   camera terms  ReprojectionError at frame time t_f through T_ci_w = B_{i-1}..B_0 T_c0_b T_wb(t_f)^-1
+ *                 (BSplineTransformationExpressionNode, BSplineExpressions.cpp:23-45)
+ *   IMU terms     (not in the reference -- defined in DESIGN.md 10):
+ *                 gyro  w_m = w_b(t) + b_g,  w_b = -C^T S(theta) theta_dot (BSplinePose.cpp:207-219)
+ *                 accel a_m = C^T (p_ddot(t) - g_w) + b_a                  (cf. BSplinePose.cpp:175-180)
+ *                 whitened by 1/sigma_gyro, 1/sigma_acc.
+ * State:   intr [N][KB_MAX_INTR] | base [N-1][7] | T_c0_b [7] | b_g [3] | b_a [3] | g_w [3] | coeff [K][6]
+ * Columns: [intr | B_j (dphi, dt) | T_c0_b (dphi, dt) | b_g | b_a | g_w | coeff 0..K-1 (6 each)]
+ * Knot vector: non-decreasing, n_knots = K + order; the device path supports order 4 (cubic).
+ * The coefficient block is solved by block cyclic reduction on the device.
+ * ------------------------------------------------------------------------------------------------ */
+typedef struct kb_sp_handle kb_sp_handle;
+
+typedef struct kb_sp_layout {
+  int32_t n_cams;
+  int32_t n_target;
+  const int32_t* cam_model;     /* [n_cams] */
+  const double* target_points;  /* [n_target][3] */
+  int32_t order;                /* 4 */
+  int32_t n_knots;
+  const double* knots;          /* [n_knots] */
+  double sigma_gyro, sigma_acc; /* IMU noise (whitening) */
+  int32_t device;
+} kb_sp_layout;
+
+kb_sp_handle* kb_sp_create(const kb_sp_layout* layout);
+void kb_sp_destroy(kb_sp_handle* h);
+/* initMatrixStructure for the spline problem: frames (times, views sorted by frame) and IMU samples.
+ * All times inside the spline interval [knots[order-1], knots[n_knots-order]]. */
+int kb_sp_upload(kb_sp_handle* h, int32_t n_frames, const double* frame_time, int32_t n_views, int32_t n_corners,
+                 const double* y, const uint16_t* corner_id, const uint32_t* view_offsets,
+                 const uint32_t* view_frame, const uint8_t* view_cam, int32_t n_imu, const double* imu_time,
+                 const double* imu_gyro, const double* imu_acc);
+int kb_sp_state_size(const kb_sp_handle* h);
+int kb_sp_num_cols(const kb_sp_handle* h);
+int kb_sp_camera_cols(const kb_sp_handle* h);
+int kb_sp_set_state(kb_sp_handle* h, const double* state);
+int kb_sp_get_state(kb_sp_handle* h, double* state);
+/* evaluateError / buildSystem / setConstantConditioner / solveSystem / rhs / applyStateUpdate /
+ * revertLastStateUpdate of the spline system, same semantics as the kb_* rig entry points. */
+int kb_sp_eval_cost(kb_sp_handle* h, double* J_out);
+int kb_sp_build(kb_sp_handle* h);
+int kb_sp_set_constant_conditioner(kb_sp_handle* h, double diag);
+int kb_sp_solve(kb_sp_handle* h, double* dx_out, int* ok);
+int kb_sp_get_rhs(kb_sp_handle* h, double* rhs_out);
+int kb_sp_apply_update(kb_sp_handle* h, const double* dx, double* deltaX_out);
+int kb_sp_revert(kb_sp_handle* h);
+/* Normal equations of the last kb_sp_build (parity tests): Hcc [C][C], Hsc [6K][C], Hband [K][order][6][6]
+ * (block (k, k+d)), gc [C], gs [6K], cost. */
+int kb_sp_get_system(kb_sp_handle* h, double* Hcc, double* Hsc, double* Hband, double* gc, double* gs,
+                     double* cost);
+/* Optimizer2::optimize over the spline system (LM policy 0 / GN policy 1), host-driven loop over the
+ * device passes; trace as kb_get_trace. */
+int kb_sp_optimize(kb_sp_handle* h, const kb_optimizer_options* opts, kb_solution* out);
+int kb_sp_get_trace(kb_sp_handle* h, double* trace, int32_t cap);
+/* Benchmark: exactly n_iter GN passes (build + solve + update + cost), captured in a hipGraph. */
+int kb_sp_run_gn_iterations(kb_sp_handle* h, int32_t n_iter, double* seconds);
+/* Per-kernel device time (ms, HIP events on the handle's stream) of one GN pass, averaged over n passes:
+ * out[0] frames kernel, [1] assemble, [2] cyclic reduction (all levels), [3] Schur + camera solve,
+ * [4] update + cost, [5] whole pass; bytes[0] algorithmic bytes of the frames kernel per launch. */
+int kb_sp_kernel_stats(kb_sp_handle* h, int32_t n, double* ms_out6, double* frames_bytes);
+
 #ifdef __cplusplus
 }
 #endif

@@ -5,8 +5,9 @@ import subprocess
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 SRC = os.path.join(HERE, "csrc", "kb_capi.hip")
+SRC_SPLINE = os.path.join(HERE, "csrc", "kb_spline.hip")
 OUT = os.path.join(HERE, "libkalibr_hip.so")
-DEPS = ["kb_capi.hip", "kb_kernels.hip", "kb_device.h", "kb_math.h"]
+DEPS = ["kb_capi.hip", "kb_kernels.hip", "kb_device.h", "kb_math.h", "kb_spline.hip"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wno-unused-result", "-Wno-unused-value"]
 
@@ -21,7 +22,7 @@ def needs_build():
 
 def build(force=False):
     if force or needs_build():
-        cmd = [HIPCC] + FLAGS + ["-o", OUT + ".tmp", SRC, "-lrccl"]
+        cmd = [HIPCC] + FLAGS + ["-o", OUT + ".tmp", SRC, SRC_SPLINE, "-lrccl"]
         subprocess.run(cmd, check=True)
         os.replace(OUT + ".tmp", OUT)
     return OUT

@@ -23,11 +23,22 @@ EXPORTS = [
     "kb_set_constant_conditioner", "kb_solve", "kb_get_rhs", "kb_apply_update", "kb_revert", "kb_get_normal_blocks",
     "kb_optimize", "kb_get_trace", "kb_run_gn_iterations", "kb_build_kernel_stats", "kb_comm_get_unique_id",
     "kb_comm_init", "kb_selftest_mfma", "kb_solve_marginal", "kb_analyze_marginal",
+    # configs[4]: B-spline pose trajectory + IMU
+    "kb_sp_create", "kb_sp_destroy", "kb_sp_upload", "kb_sp_state_size", "kb_sp_num_cols", "kb_sp_camera_cols",
+    "kb_sp_set_state", "kb_sp_get_state", "kb_sp_eval_cost", "kb_sp_build", "kb_sp_set_constant_conditioner",
+    "kb_sp_solve", "kb_sp_get_rhs", "kb_sp_apply_update", "kb_sp_revert", "kb_sp_get_system", "kb_sp_optimize",
+    "kb_sp_get_trace", "kb_sp_run_gn_iterations", "kb_sp_kernel_stats",
 ]
 
 
 class KbError(RuntimeError):
     pass
+
+
+class SpLayout(C.Structure):
+    _fields_ = [("n_cams", C.c_int32), ("n_target", C.c_int32), ("cam_model", C.POINTER(C.c_int32)),
+                ("target_points", dp), ("order", C.c_int32), ("n_knots", C.c_int32), ("knots", dp),
+                ("sigma_gyro", C.c_double), ("sigma_acc", C.c_double), ("device", C.c_int32)]
 
 
 class Layout(C.Structure):
@@ -77,7 +88,7 @@ def lib():
         L.kb_last_error.restype = C.c_char_p
         for name in EXPORTS:
             fn = getattr(L, name)
-            if name not in ("kb_create", "kb_destroy", "kb_last_error"):
+            if name not in ("kb_create", "kb_destroy", "kb_last_error", "kb_sp_create", "kb_sp_destroy"):
                 fn.restype = C.c_int
         L.kb_upload_observations.argtypes = [C.c_void_p, C.c_int32, C.c_int32, dp, C.c_void_p, C.c_void_p, C.c_void_p,
                                              C.c_void_p]
@@ -103,6 +114,25 @@ def lib():
         L.kb_solve_marginal.argtypes = [C.c_void_p, C.POINTER(MarginalOptions), dp, C.POINTER(C.c_int),
                                         C.POINTER(MarginalInfo), dp, dp]
         L.kb_analyze_marginal.argtypes = [C.c_void_p, C.POINTER(MarginalOptions), C.POINTER(MarginalInfo), dp, dp]
+        L.kb_sp_create.restype = C.c_void_p
+        L.kb_sp_create.argtypes = [C.POINTER(SpLayout)]
+        L.kb_sp_destroy.argtypes = [C.c_void_p]
+        L.kb_sp_upload.argtypes = [C.c_void_p, C.c_int32, dp, C.c_int32, C.c_int32, dp, C.c_void_p, C.c_void_p,
+                                   C.c_void_p, C.c_void_p, C.c_int32, dp, dp, dp]
+        for n in ("kb_sp_state_size", "kb_sp_num_cols", "kb_sp_camera_cols", "kb_sp_build", "kb_sp_revert"):
+            getattr(L, n).argtypes = [C.c_void_p]
+        L.kb_sp_set_state.argtypes = [C.c_void_p, dp]
+        L.kb_sp_get_state.argtypes = [C.c_void_p, dp]
+        L.kb_sp_eval_cost.argtypes = [C.c_void_p, dp]
+        L.kb_sp_set_constant_conditioner.argtypes = [C.c_void_p, C.c_double]
+        L.kb_sp_solve.argtypes = [C.c_void_p, dp, C.POINTER(C.c_int)]
+        L.kb_sp_get_rhs.argtypes = [C.c_void_p, dp]
+        L.kb_sp_apply_update.argtypes = [C.c_void_p, dp, dp]
+        L.kb_sp_get_system.argtypes = [C.c_void_p, dp, dp, dp, dp, dp, dp]
+        L.kb_sp_optimize.argtypes = [C.c_void_p, C.POINTER(OptimizerOptions), C.POINTER(Solution)]
+        L.kb_sp_get_trace.argtypes = [C.c_void_p, dp, C.c_int32]
+        L.kb_sp_run_gn_iterations.argtypes = [C.c_void_p, C.c_int32, dp]
+        L.kb_sp_kernel_stats.argtypes = [C.c_void_p, C.c_int32, dp, dp]
         _lib = L
     return _lib
 
@@ -263,3 +293,119 @@ class Solver:
     def comm_init(self, uid: bytes, nranks, rank):
         buf = C.create_string_buffer(uid, 128)
         _check(lib().kb_comm_init(self.h, buf, int(nranks), int(rank)))
+
+
+class SplineSolver:
+    """One kb_sp handle: the configs[4] spline + IMU system on one MI355X (include/kalibr_hip.h kb_sp_*)."""
+
+    def __init__(self, prob, device=0):
+        self.prob = prob
+        self._cm = np.ascontiguousarray(prob.cam_model, dtype=np.int32)
+        self._tg = np.ascontiguousarray(prob.target, dtype=np.float64)
+        self._kn = np.ascontiguousarray(prob.knots, dtype=np.float64)
+        lay = SpLayout(prob.n_cams, self._tg.shape[0], self._cm.ctypes.data_as(C.POINTER(C.c_int32)), _d(self._tg),
+                       prob.order, self._kn.size, _d(self._kn), prob.sigma_gyro, prob.sigma_acc, device)
+        h = lib().kb_sp_create(C.byref(lay))
+        if not h:
+            raise KbError(lib().kb_last_error().decode())
+        self.h = C.c_void_p(h)
+        ft = np.ascontiguousarray(prob.frame_time, dtype=np.float64)
+        y = np.ascontiguousarray(prob.y, dtype=np.float64)
+        cid = np.ascontiguousarray(prob.corner_id, dtype=np.uint16)
+        vo = np.ascontiguousarray(prob.view_offset, dtype=np.uint32)
+        vf = np.ascontiguousarray(prob.view_frame, dtype=np.uint32)
+        vc = np.ascontiguousarray(prob.view_cam, dtype=np.uint8)
+        it = np.ascontiguousarray(prob.imu_time, dtype=np.float64)
+        ig = np.ascontiguousarray(prob.imu_gyro, dtype=np.float64)
+        ia = np.ascontiguousarray(prob.imu_acc, dtype=np.float64)
+        _check(lib().kb_sp_upload(self.h, prob.n_frames, _d(ft), prob.n_views, prob.n_corners, _d(y), cid.ctypes.data,
+                                  vo.ctypes.data, vf.ctypes.data, vc.ctypes.data, prob.n_imu, _d(it), _d(ig), _d(ia)))
+        self.S = lib().kb_sp_state_size(self.h)
+        self.ncols = lib().kb_sp_num_cols(self.h)
+        self.C = lib().kb_sp_camera_cols(self.h)
+        self.K = (self.ncols - self.C) // 6
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().kb_sp_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_state(self, state):
+        st = np.ascontiguousarray(state, dtype=np.float64)
+        assert st.shape[0] == self.S
+        _check(lib().kb_sp_set_state(self.h, _d(st)))
+
+    def get_state(self):
+        st = np.zeros(self.S)
+        _check(lib().kb_sp_get_state(self.h, _d(st)))
+        return st
+
+    def eval_cost(self):
+        J = C.c_double()
+        _check(lib().kb_sp_eval_cost(self.h, C.byref(J)))
+        return J.value
+
+    def build(self):
+        _check(lib().kb_sp_build(self.h))
+
+    def set_constant_conditioner(self, diag):
+        _check(lib().kb_sp_set_constant_conditioner(self.h, float(diag)))
+
+    def solve(self):
+        dx = np.zeros(self.ncols)
+        ok = C.c_int(0)
+        _check(lib().kb_sp_solve(self.h, _d(dx), C.byref(ok)))
+        return bool(ok.value), dx
+
+    def rhs(self):
+        r = np.zeros(self.ncols)
+        _check(lib().kb_sp_get_rhs(self.h, _d(r)))
+        return r
+
+    def apply_update(self, dx=None):
+        dX = C.c_double()
+        _check(lib().kb_sp_apply_update(self.h, None if dx is None else _d(np.ascontiguousarray(dx, dtype=np.float64)),
+                                        C.byref(dX)))
+        return dX.value
+
+    def revert(self):
+        _check(lib().kb_sp_revert(self.h))
+
+    def system(self):
+        Cc, K = self.C, self.K
+        out = dict(Hcc=np.zeros((Cc, Cc)), Hsc=np.zeros((6 * K, Cc)), Hband=np.zeros((K, 4, 6, 6)), gc=np.zeros(Cc),
+                   gs=np.zeros(6 * K))
+        cost = C.c_double()
+        _check(lib().kb_sp_get_system(self.h, _d(out["Hcc"]), _d(out["Hsc"]), _d(out["Hband"]), _d(out["gc"]),
+                                      _d(out["gs"]), C.byref(cost)))
+        out["cost"] = cost.value
+        return out
+
+    def optimize(self, policy="gn", lambda0=10.0, max_iterations=20, eps_x=1e-3, eps_j=1.0):
+        o = OptimizerOptions(0 if policy == "lm" else 1, lambda0, max_iterations, eps_x, eps_j, 1, 0)
+        s = Solution()
+        _check(lib().kb_sp_optimize(self.h, C.byref(o), C.byref(s)))
+        res = {f: getattr(s, f) for f, _ in Solution._fields_}
+        cap = 2 * max_iterations + 2
+        tr = np.zeros((cap, 4))
+        n = _check(lib().kb_sp_get_trace(self.h, _d(tr), cap))
+        res["trace"] = tr[:n].copy()
+        return res
+
+    def run_gn(self, n_iter):
+        sec = C.c_double()
+        _check(lib().kb_sp_run_gn_iterations(self.h, int(n_iter), C.byref(sec)))
+        return sec.value
+
+    def kernel_stats(self, n=10):
+        ms = np.zeros(6)
+        fb = C.c_double()
+        _check(lib().kb_sp_kernel_stats(self.h, int(n), _d(ms), C.byref(fb)))
+        return dict(frames_ms=ms[0], assemble_ms=ms[1], reduction_ms=ms[2], camsolve_ms=ms[3], update_cost_ms=ms[4],
+                    pass_ms=ms[5], frames_bytes=fb.value)

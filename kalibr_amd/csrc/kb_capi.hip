@@ -131,6 +131,13 @@ static void drop_graphs(kb_handle* h) {
   h->graph_policy = -1;
 }
 
+// error channel shared with the spline translation unit (kb_spline.hip)
+namespace kb_internal {
+int fail(const std::string& m) {
+  g_err = m;
+  return -1;
+}
+}  // namespace kb_internal
 
 extern "C" {
 

@@ -1,0 +1,2028 @@
+// kb_spline.hip -- configs[4] on the device: the rig (IMU body) on a cubic B-spline pose trajectory,
+// camera ReprojectionError terms through the spline pose and IMU gyro / accelerometer terms, assembled
+// into the block-banded normal equations and solved by block cyclic reduction + a Schur complement onto
+// the camera / IMU block.  Entry points: include/kalibr_hip.h (kb_sp_*).
+//
+// Reference map (paths relative to the reference repository):
+//   BSplinePose::transformationAndJacobian      bsplines/src/BSplinePose.cpp:26-41 (J = JT JS)
+//   curveValueToTransformationAndJacobian       bsplines/src/BSplinePose.cpp:394-412 (JT = [I, -[p]x S; 0, S])
+//   angularVelocityBodyFrame                    bsplines/src/BSplinePose.cpp:207-219
+//   RotationVector                              Schweizer-Messer/sm_kinematics/src/RotationVector.cpp:10-103
+//   BSplineTransformationExpressionNode         aslam_splines/src/BSplineExpressions.cpp:23-45
+//   spline DVs (additive 6-vectors)             aslam_splines/src/BSplinePoseDesignVariable.cpp:9-19
+//   B-spline basis (host side, kb_sp_upload)    bsplines/src/BSpline.cpp:58-152, 237-387
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/kalibr_hip.h"
+#include "kb_math.h"
+
+namespace kb_internal {
+int fail(const std::string& m);
+}
+
+namespace ksp {
+using kb::kMmAll;
+
+constexpr int ORD = 4;      // spline order of the device path
+constexpr int SB = 3;       // coefficients per cyclic-reduction node: couplings reach only the next node
+constexpr int NB = 6 * SB;  // 18 rows per node
+constexpr int MAXC = 64;    // camera + IMU block
+constexpr int FPB = 4;      // frames per k_sp_frames block
+constexpr int XS = 17;      // LDS row stride of the 64 x 16 Jacobian-row tile
+constexpr int WI = 55;      // IMU theta partial row: 9x9 upper (45) | g (9) | cost
+constexpr int NPB = 8;      // nodes per k_sp_schur block
+constexpr int TCH = 32;     // terms staged per k_sp_assemble chunk
+enum { SC_COST_BUILD = 0, SC_OK = 1, SC_DX = 2, SC_COST = 3, SC_LAM2 = 4, SC_NSC = 8 };
+
+struct SpDev {
+  int N, C, K, F, M, n, m, n_target;
+  int nin[KB_MAX_CAMS], model[KB_MAX_CAMS], col_intr[KB_MAX_CAMS];
+  int col_pose[KB_MAX_CAMS];  // pose DV q: B_q (q < N-1), T_c0_b (q = N-1)
+  int col_imu;
+  int ckind[MAXC], cidx[MAXC], csub[MAXC];  // column -> (0 intr | 1 pose | 2 imu, cam / q, sub-index)
+  int off_base, off_cb, off_imu, off_coef, S;
+  int nblk_f, nblk_s, nblk_ci, Wc, Ws, FHS;
+  double ig, ia;
+  const double* target;
+  const double2* y;
+  const uint16_t* cid;
+  const int2* fview;      // [F][N]
+  const int* fb;          // [F] first coefficient of the frame's support
+  const double* fw;       // [F][4] basis weights (derivative 0)
+  const int* ib;          // [M]
+  const double* iw;       // [M][12] weights of derivatives 0, 1, 2
+  const double* imeas;    // [M][6] gyro | accel
+  const int* node_fr;     // [n][2] frame range with bidx in [3i-3, 3i+2]
+  const int* node_im;     // [n][2]
+  double* state;
+  double* backup;
+  double* FH;             // [F][FHS]: H_vv (36) | H_vtheta (6 C) | g_v (6)
+  double* part;           // [nblk_f][Wc] theta-theta partial rows of the frames
+  double* ipart;          // [n][WI]
+  double* Hcc;            // [C][C] | gc [C] | cost
+  double *D0, *U0, *R0;   // built node blocks [n][324], [n][324], [n][18 m]
+  double *D, *U, *R;      // working copies (cyclic reduction in place)
+  double *Lf, *Z, *X;     // [n][324], [n][18 (36 + m)], [n][18 m]
+  double* spart;          // [nblk_s][Ws]
+  double* dx;             // [C + 6K]
+  double* dmax;           // [n]
+  double* cpart;          // [nblk_f + nblk_ci]
+  double* sc;             // scalars
+};
+
+typedef double v4d_t __attribute__((ext_vector_type(4)));
+#define KSP_WAVE_SYNC() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
+
+// ---------------------------------------------------------------- rotation vector (RotationVector.cpp)
+__device__ __forceinline__ void rv_C(const double* a, double* Cm) {
+  const double ang = sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]);
+  if (ang < 1e-14) {
+#pragma unroll
+    for (int q = 0; q < 9; ++q) Cm[q] = (q % 4 == 0) ? 1.0 : 0.0;
+    return;
+  }
+  const double ra = 1.0 / ang, ax = a[0] * ra, ay = a[1] * ra, az = a[2] * ra;
+  double sa, ca;
+  sincos(ang, &sa, &ca);
+  const double ax2 = ax * ax, ay2 = ay * ay, az2 = az * az;
+  Cm[0] = ax2 + ca * (1.0 - ax2);
+  Cm[1] = ax * ay - ca * ax * ay + sa * az;
+  Cm[2] = ax * az - ca * ax * az - sa * ay;
+  Cm[3] = ax * ay - ca * ax * ay - sa * az;
+  Cm[4] = ay2 + ca * (1.0 - ay2);
+  Cm[5] = ay * az - ca * ay * az + sa * ax;
+  Cm[6] = ax * az - ca * ax * az + sa * ay;
+  Cm[7] = ay * az - ca * ay * az - sa * ax;
+  Cm[8] = az2 + ca * (1.0 - az2);
+}
+
+__device__ __forceinline__ void rv_S(const double* a, double* S) {
+  const double ang = sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]);
+#pragma unroll
+  for (int q = 0; q < 9; ++q) S[q] = (q % 4 == 0) ? 1.0 : 0.0;
+  if (ang < 1e-14) return;
+  const double ra = 1.0 / ang;
+  const double x = a[0] * ra, y = a[1] * ra, z = a[2] * ra;
+  const double st2 = sin(ang * 0.5), st = sin(ang);
+  const double c1 = -2.0 * st2 * st2 * ra, c2 = (ang - st) * ra;
+  // [x]x and [x]x^2 = x x^T - I
+  const double X[9] = {0, -z, y, z, 0, -x, -y, x, 0};
+  const double X2[9] = {x * x - 1, x * y, x * z, x * y, y * y - 1, y * z, x * z, y * z, z * z - 1};
+#pragma unroll
+  for (int q = 0; q < 9; ++q) S[q] += c1 * X[q] + c2 * X2[q];
+}
+
+// d(S(a) v)/da: S v = v + alpha a x v + beta a x (a x v), alpha = (cos f - 1)/f^2, beta = (f - sin f)/f^3
+__device__ __forceinline__ void rv_dSv(const double* a, const double* v, double* Dm) {
+  const double f2 = a[0] * a[0] + a[1] * a[1] + a[2] * a[2], f = sqrt(f2);
+  double al, be, dal, dbe;
+  if (f < 1e-4) {
+    al = -0.5 + f2 / 24.0;
+    be = 1.0 / 6.0 - f2 / 120.0;
+    dal = 1.0 / 12.0 - f2 / 180.0;
+    dbe = -1.0 / 60.0 + f2 / 1260.0;
+  } else {
+    double s, c;
+    sincos(f, &s, &c);
+    al = (c - 1.0) / f2;
+    be = (f - s) / (f2 * f);
+    dal = (-s / f2 - 2.0 * (c - 1.0) / (f2 * f)) / f;
+    dbe = ((1.0 - c) / (f2 * f) - 3.0 * (f - s) / (f2 * f2)) / f;
+  }
+  const double axv[3] = {a[1] * v[2] - a[2] * v[1], a[2] * v[0] - a[0] * v[2], a[0] * v[1] - a[1] * v[0]};
+  const double av = a[0] * v[0] + a[1] * v[1] + a[2] * v[2];
+  const double aaxv[3] = {a[0] * av - v[0] * f2, a[1] * av - v[1] * f2, a[2] * av - v[2] * f2};
+  const double vx[9] = {0, -v[2], v[1], v[2], 0, -v[0], -v[1], v[0], 0};
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const double daaxv = (r == c ? av : 0.0) + a[r] * v[c] - 2.0 * v[r] * a[c];
+      Dm[r * 3 + c] = al * (-vx[r * 3 + c]) + axv[r] * dal * a[c] + be * daaxv + aaxv[r] * dbe * a[c];
+    }
+}
+
+// ---------------------------------------------------------------- small SE(3) helpers
+// entry (r, c) of boxTimes(R, t) M(tb), M = [[-[tb]x, I], [I, 0]] (TransformationBasic.cpp:49-66):
+// maps a TransformationBasic DV perturbation (dphi, dt) to the 6-D left perturbation of the chain.
+__device__ __forceinline__ double bt_basic(const double* R, const double* t, const double* tb, int r, int c) {
+  // boxTimes = [[R, -[t]x R], [0, R]]
+  double bt[6];
+  const double tx[9] = {0, -t[2], t[1], t[2], 0, -t[0], -t[1], t[0], 0};
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    if (r < 3) {
+      if (k < 3) {
+        bt[k] = R[r * 3 + k];
+      } else {
+        const int kk = k - 3;
+        bt[k] = -(tx[r * 3 + 0] * R[0 * 3 + kk] + tx[r * 3 + 1] * R[1 * 3 + kk] + tx[r * 3 + 2] * R[2 * 3 + kk]);
+      }
+    } else {
+      bt[k] = (k < 3) ? 0.0 : R[(r - 3) * 3 + (k - 3)];
+    }
+  }
+  const double tbx[9] = {0, -tb[2], tb[1], tb[2], 0, -tb[0], -tb[1], tb[0], 0};
+  double s = 0.0;
+  if (c < 3) {  // rotation DV column: rows 0-2 -[tb]x, rows 3-5 I
+#pragma unroll
+    for (int k = 0; k < 3; ++k) s += bt[k] * (-tbx[k * 3 + c]);
+    s += bt[3 + c];
+  } else {  // translation DV column: rows 0-2 I
+    s = bt[c - 3];
+  }
+  return s;
+}
+
+// ---------------------------------------------------------------- k_sp_frames: camera terms
+// One block = FPB frames, one wave per camera.  Per frame: spline pose T_wb(t_f) and JT; per view the
+// 16 x 16 local Hessian of [J_delta | J_intr | -e] by f64 MFMA SYRK through an LDS tile; then the frame's
+// spline-side blocks (H_vv, H_vtheta, g_v in the curve-value coordinates v, JT folded in) to HBM and the
+// camera-side (theta-theta) sums into the block's partial row.
+template <unsigned MM>
+__global__ void __launch_bounds__(512) k_sp_frames(SpDev d) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  const int N = d.N, C = d.C, nth = blockDim.x, tid = threadIdx.x;
+  const int wave = tid >> 6, lane = tid & 63;
+  double* Xw = sm + wave * 64 * XS;
+  double* Hv = sm + N * 64 * XS;   // [N][256]
+  double* Gv = Hv + N * 256;       // [N][36]
+  double* Pv = Gv + N * 36;        // [N][36]
+  double* Gp = Pv + N * 36;        // [N][N][36]
+  double* Qp = Gp + N * N * 36;    // [N][N][36]
+  double* acc = Qp + N * N * 36;   // [Wc] theta-theta accumulators
+  double* tg = acc + d.Wc;         // [n_target][3]
+  const int cam = wave;
+  const double* st = d.state;
+  for (int q = tid; q < 3 * d.n_target; q += nth) tg[q] = d.target[q];
+  for (int q = tid; q < d.Wc; q += nth) acc[q] = 0.0;
+  // chain A_cam = B_{cam-1} .. B_0 T_c0_b (frame independent) and the pose-DV maps Gp[cam][q]
+  double RA[9], tA[3];
+  kb::quat2r(st + d.off_cb, RA);
+  tA[0] = st[d.off_cb + 4];
+  tA[1] = st[d.off_cb + 5];
+  tA[2] = st[d.off_cb + 6];
+  {
+    double RP[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, tP[3] = {0, 0, 0};  // P = B_{cam-1} .. B_{q+1}
+    for (int q = cam - 1; q >= 0; --q) {
+      const double* bq = st + d.off_base + 7 * q;
+      if (lane < 36) Gp[(cam * N + q) * 36 + lane] = bt_basic(RP, tP, bq + 4, lane / 6, lane % 6);
+      double RB[9], R2[9], t2[3];
+      kb::quat2r(bq, RB);
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+          R2[r * 3 + c] = RP[r * 3 + 0] * RB[0 * 3 + c] + RP[r * 3 + 1] * RB[1 * 3 + c] + RP[r * 3 + 2] * RB[2 * 3 + c];
+        t2[r] = RP[r * 3 + 0] * bq[4] + RP[r * 3 + 1] * bq[5] + RP[r * 3 + 2] * bq[6] + tP[r];
+      }
+#pragma unroll
+      for (int k = 0; k < 9; ++k) RP[k] = R2[k];
+      tP[0] = t2[0];
+      tP[1] = t2[1];
+      tP[2] = t2[2];
+    }
+    if (lane < 36) Gp[(cam * N + (N - 1)) * 36 + lane] = bt_basic(RP, tP, st + d.off_cb + 4, lane / 6, lane % 6);
+    double R2[9], t2[3];  // A = P T_c0_b
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+        R2[r * 3 + c] = RP[r * 3 + 0] * RA[0 * 3 + c] + RP[r * 3 + 1] * RA[1 * 3 + c] + RP[r * 3 + 2] * RA[2 * 3 + c];
+      t2[r] = RP[r * 3 + 0] * tA[0] + RP[r * 3 + 1] * tA[1] + RP[r * 3 + 2] * tA[2] + tP[r];
+    }
+#pragma unroll
+    for (int k = 0; k < 9; ++k) RA[k] = R2[k];
+    tA[0] = t2[0];
+    tA[1] = t2[1];
+    tA[2] = t2[2];
+  }
+  __syncthreads();  // target, accumulators and Gp staged
+  const int model = d.model[cam], nin = d.nin[cam];
+  const double* intr = st + cam * KB_MAX_INTR;
+  const int mrow = lane >> 4, mcol = lane & 15;
+  const int f0 = blockIdx.x * FPB, f1 = min(d.F, f0 + FPB);
+  for (int f = f0; f < f1; ++f) {
+    // spline pose at t_f (uniform across the block)
+    const int b = d.fb[f];
+    const double* w = d.fw + 4 * f;
+    const double* cf = st + d.off_coef + 6 * b;
+    double v[6];
+#pragma unroll
+    for (int r = 0; r < 6; ++r) v[r] = w[0] * cf[r] + w[1] * cf[6 + r] + w[2] * cf[12 + r] + w[3] * cf[18 + r];
+    double Rwb[9];
+    rv_C(v + 3, Rwb);
+    // T_cam_w = A T_wb^-1: R = RA Rwb^T, t = tA - R p
+    double R[9], t[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+        R[r * 3 + c] = RA[r * 3 + 0] * Rwb[c * 3 + 0] + RA[r * 3 + 1] * Rwb[c * 3 + 1] + RA[r * 3 + 2] * Rwb[c * 3 + 2];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) t[r] = tA[r] - (R[r * 3 + 0] * v[0] + R[r * 3 + 1] * v[1] + R[r * 3 + 2] * v[2]);
+    // G_v = -boxTimes(T_cam_w) JT, JT = [I, -[p]x S; 0, S]
+    if (lane < 36) {
+      double S[9];
+      rv_S(v + 3, S);
+      const int r = lane / 6, c = lane % 6;
+      const double tx[9] = {0, -t[2], t[1], t[2], 0, -t[0], -t[1], t[0], 0};
+      const double px[9] = {0, -v[2], v[1], v[2], 0, -v[0], -v[1], v[0], 0};
+      double JTc[6];  // column c of JT
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        if (c < 3) {
+          JTc[k] = (k == c) ? 1.0 : 0.0;
+          JTc[3 + k] = 0.0;
+        } else {
+          const int cc = c - 3;
+          JTc[k] = -(px[k * 3 + 0] * S[0 * 3 + cc] + px[k * 3 + 1] * S[1 * 3 + cc] + px[k * 3 + 2] * S[2 * 3 + cc]);
+          JTc[3 + k] = S[k * 3 + cc];
+        }
+      }
+      double s = 0.0;
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        double bt;  // boxTimes(R, t)[r][k]
+        if (r < 3) {
+          if (k < 3) {
+            bt = R[r * 3 + k];
+          } else {
+            const int kk = k - 3;
+            bt = -(tx[r * 3 + 0] * R[0 * 3 + kk] + tx[r * 3 + 1] * R[1 * 3 + kk] + tx[r * 3 + 2] * R[2 * 3 + kk]);
+          }
+        } else {
+          bt = (k < 3) ? 0.0 : R[(r - 3) * 3 + (k - 3)];
+        }
+        s += bt * JTc[k];
+      }
+      Gv[cam * 36 + lane] = -s;
+    }
+    // corners of view (f, cam): [J_delta | J_intr | -e] rows, SYRK on MFMA
+    const int2 fv = d.fview[(size_t)f * N + cam];
+    v4d_t acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+    for (int base = fv.x; base < fv.y; base += 64) {
+      const int k = base + lane;
+      double xr[2][16];
+#pragma unroll
+      for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) xr[r][q] = 0.0;
+      if (k < fv.y) {
+        const int ci = d.cid[k];
+        const double2 yv = d.y[k];
+        const double X0 = tg[3 * ci], X1 = tg[3 * ci + 1], X2 = tg[3 * ci + 2];
+        const double p0 = R[0] * X0 + R[1] * X1 + R[2] * X2 + t[0];
+        const double p1 = R[3] * X0 + R[4] * X1 + R[5] * X2 + t[1];
+        const double p2 = R[6] * X0 + R[7] * X1 + R[8] * X2 + t[2];
+        double u, wv, Jp[6], Ji[2 * KB_MAX_INTR];
+        kb::project_jac<MM>(model, intr, p0, p1, p2, u, wv, Jp, Ji);
+        const double e0 = yv.x - u, e1 = yv.y - wv;
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+          const double j0 = Jp[3 * r], j1 = Jp[3 * r + 1], j2 = Jp[3 * r + 2];
+          xr[r][0] = -j0;
+          xr[r][1] = -j1;
+          xr[r][2] = -j2;
+          xr[r][3] = -(j1 * p2 - j2 * p1);
+          xr[r][4] = -(-j0 * p2 + j2 * p0);
+          xr[r][5] = -(j0 * p1 - j1 * p0);
+#pragma unroll
+          for (int q = 0; q < 9; ++q) xr[r][6 + q] = (q < nin) ? -Ji[r * KB_MAX_INTR + q] : 0.0;
+          xr[r][15] = -(r == 0 ? e0 : e1);
+        }
+      }
+#pragma unroll
+      for (int ph = 0; ph < 2; ++ph) {
+        if (ph == 1 && base + 32 >= fv.y) break;  // wave-uniform
+        if ((lane >> 5) == ph) {
+          const int rr = 2 * (lane & 31);
+#pragma unroll
+          for (int q = 0; q < 16; ++q) {
+            Xw[rr * XS + q] = xr[0][q];
+            Xw[(rr + 1) * XS + q] = xr[1][q];
+          }
+        }
+        KSP_WAVE_SYNC();
+#pragma unroll
+        for (int ks = 0; ks < 16; ks += 2) {
+          const double xa = Xw[(4 * ks + mrow) * XS + mcol];
+          const double xb = Xw[(4 * ks + 4 + mrow) * XS + mcol];
+          acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(xa, xa, acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(xb, xb, acc1, 0, 0, 0);
+        }
+        KSP_WAVE_SYNC();
+      }
+    }
+    // f64 MFMA C/D layout: lane l, reg r -> row (l >> 4) + 4 r, col l & 15
+#pragma unroll
+    for (int r = 0; r < 4; ++r) Hv[cam * 256 + (mrow + 4 * r) * 16 + mcol] = acc0[r] + acc1[r];
+    __syncthreads();
+    // P_i = H_dd,i G_v,i ; Q_i[q] = H_dd,i Gp[i][q]
+    for (int q = tid; q < N * 36 + N * N * 36; q += nth) {
+      const bool isP = q < N * 36;
+      const int qq = isP ? q : q - N * 36;
+      const int i = isP ? qq / 36 : qq / (N * 36);
+      const int e = qq % 36, r = e / 6, c = e % 6;
+      const double* G = isP ? Gv + i * 36 : Gp + (qq / 36) * 36;
+      const double* H = Hv + i * 256;
+      double s = 0.0;
+#pragma unroll
+      for (int k = 0; k < 6; ++k) s += H[r * 16 + k] * G[k * 6 + c];
+      if (isP)
+        Pv[qq] = s;
+      else
+        Qp[qq] = s;
+    }
+    __syncthreads();
+    // spline side of the frame: [H_vv | H_vtheta | g_v]
+    double* out = d.FH + (size_t)f * d.FHS;
+    for (int q = tid; q < d.FHS; q += nth) {
+      double s = 0.0;
+      if (q < 36) {
+        const int a = q / 6, bb = q % 6;
+        for (int i = 0; i < N; ++i)
+#pragma unroll
+          for (int r = 0; r < 6; ++r) s += Gv[i * 36 + r * 6 + a] * Pv[i * 36 + r * 6 + bb];
+      } else if (q < 36 + 6 * C) {
+        const int a = (q - 36) / C, col = (q - 36) % C;
+        const int kind = d.ckind[col], idx = d.cidx[col], sub = d.csub[col];
+        for (int i = 0; i < N; ++i) {
+          if (kind == 0 && idx == i) {
+#pragma unroll
+            for (int r = 0; r < 6; ++r) s += Gv[i * 36 + r * 6 + a] * Hv[i * 256 + r * 16 + 6 + sub];
+          } else if (kind == 1 && (idx == N - 1 || idx < i)) {
+#pragma unroll
+            for (int r = 0; r < 6; ++r) s += Gv[i * 36 + r * 6 + a] * Qp[(i * N + idx) * 36 + r * 6 + sub];
+          }
+        }
+      } else {
+        const int a = q - 36 - 6 * C;
+        for (int i = 0; i < N; ++i)
+#pragma unroll
+          for (int r = 0; r < 6; ++r) s += Gv[i * 36 + r * 6 + a] * Hv[i * 256 + r * 16 + 15];
+      }
+      out[q] = s;
+    }
+    // camera side: theta-theta upper | g_theta | cost
+    const int nup = C * (C + 1) / 2;
+    for (int q = tid; q < d.Wc; q += nth) {
+      double s = 0.0;
+      if (q < nup) {
+        int a = 0, e = q;
+        while (e >= C - a) {
+          e -= C - a;
+          ++a;
+        }
+        const int bcol = a + e;
+        const int ka = d.ckind[a], ia = d.cidx[a], sa = d.csub[a];
+        const int kb2 = d.ckind[bcol], ib2 = d.cidx[bcol], sb = d.csub[bcol];
+        for (int i = 0; i < N; ++i) {
+          const bool okA = (ka == 0 && ia == i) || (ka == 1 && (ia == N - 1 || ia < i));
+          const bool okB = (kb2 == 0 && ib2 == i) || (kb2 == 1 && (ib2 == N - 1 || ib2 < i));
+          if (!okA || !okB) continue;
+          const double* H = Hv + i * 256;
+          if (ka == 0 && kb2 == 0) {
+            s += H[(6 + sa) * 16 + 6 + sb];
+          } else if (ka == 1 && kb2 == 1) {
+#pragma unroll
+            for (int r = 0; r < 6; ++r) s += Gp[(i * N + ia) * 36 + r * 6 + sa] * Qp[(i * N + ib2) * 36 + r * 6 + sb];
+          } else if (ka == 1) {  // pose a, intr b
+#pragma unroll
+            for (int r = 0; r < 6; ++r) s += Gp[(i * N + ia) * 36 + r * 6 + sa] * H[r * 16 + 6 + sb];
+          } else {  // intr a, pose b
+#pragma unroll
+            for (int r = 0; r < 6; ++r) s += H[r * 16 + 6 + sa] * Gp[(i * N + ib2) * 36 + r * 6 + sb];
+          }
+        }
+      } else if (q < nup + C) {
+        const int a = q - nup, ka = d.ckind[a], ia = d.cidx[a], sa = d.csub[a];
+        for (int i = 0; i < N; ++i) {
+          const double* H = Hv + i * 256;
+          if (ka == 0 && ia == i) {
+            s += H[(6 + sa) * 16 + 15];
+          } else if (ka == 1 && (ia == N - 1 || ia < i)) {
+#pragma unroll
+            for (int r = 0; r < 6; ++r) s += Gp[(i * N + ia) * 36 + r * 6 + sa] * H[r * 16 + 15];
+          }
+        }
+      } else {
+        for (int i = 0; i < N; ++i) s += Hv[i * 256 + 255];
+      }
+      acc[q] += s;
+    }
+    __syncthreads();
+  }
+  for (int q = tid; q < d.Wc; q += nth) d.part[(size_t)blockIdx.x * d.Wc + q] = acc[q];
+}
+
+// ---------------------------------------------------------------- IMU sample (defined in DESIGN.md 10)
+// Whitened residual e[6] and the Jacobian blocks J[6][24] (4 coefficients x [p | theta]) of sample m;
+// Ct (C_wb^T) for the gravity columns.  Mirrors oracle/kb_oracle_spline.c:sp_imu (independently written).
+__device__ void imu_sample(const SpDev& d, int m, double* e, double* J, double* Ct) {
+  const int b = d.ib[m];
+  const double* w = d.iw + 12 * m;  // w0[4] | w1[4] | w2[4]
+  const double* cf = d.state + d.off_coef + 6 * b;
+  double v0[6], v1[6], v2[6];
+#pragma unroll
+  for (int r = 0; r < 6; ++r) {
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const double c = cf[6 * j + r];
+      s0 += w[j] * c;
+      s1 += w[4 + j] * c;
+      s2 += w[8 + j] * c;
+    }
+    v0[r] = s0;
+    v1[r] = s1;
+    v2[r] = s2;
+  }
+  double Cm[9], S[9];
+  rv_C(v0 + 3, Cm);
+  rv_S(v0 + 3, S);
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) Ct[r * 3 + c] = Cm[c * 3 + r];
+  const double* ib = d.state + d.off_imu;
+  double wv[3], om[3], vv[3], fb[3];
+#pragma unroll
+  for (int r = 0; r < 3; ++r) wv[r] = S[r * 3 + 0] * v1[3] + S[r * 3 + 1] * v1[4] + S[r * 3 + 2] * v1[5];
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    om[r] = -(Ct[r * 3 + 0] * wv[0] + Ct[r * 3 + 1] * wv[1] + Ct[r * 3 + 2] * wv[2]);
+    vv[r] = v2[r] - ib[6 + r];
+  }
+#pragma unroll
+  for (int r = 0; r < 3; ++r) fb[r] = Ct[r * 3 + 0] * vv[0] + Ct[r * 3 + 1] * vv[1] + Ct[r * 3 + 2] * vv[2];
+  const double* mm = d.imeas + 6 * m;
+  const double ig = d.ig, ia = d.ia;
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    e[r] = (mm[r] - om[r] - ib[r]) * ig;
+    e[3 + r] = (mm[3 + r] - fb[r] - ib[3 + r]) * ia;
+  }
+  if (!J) return;
+  double Dm[9];
+  rv_dSv(v0 + 3, v1 + 3, Dm);
+  const double wx[9] = {0, -wv[2], wv[1], wv[2], 0, -wv[0], -wv[1], wv[0], 0};
+  const double vx[9] = {0, -vv[2], vv[1], vv[2], 0, -vv[0], -vv[1], vv[0], 0};
+  double T1[9], T2[9], T3[9];  // T1 = -C^T D + C^T [w]x S ; T2 = C^T S ; T3 = C^T [v]x S
+  {
+    double wxS[9], vxS[9];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        wxS[r * 3 + c] = wx[r * 3 + 0] * S[0 * 3 + c] + wx[r * 3 + 1] * S[1 * 3 + c] + wx[r * 3 + 2] * S[2 * 3 + c];
+        vxS[r * 3 + c] = vx[r * 3 + 0] * S[0 * 3 + c] + vx[r * 3 + 1] * S[1 * 3 + c] + vx[r * 3 + 2] * S[2 * 3 + c];
+      }
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        double a1 = 0.0, a2 = 0.0, a3 = 0.0, a4 = 0.0;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          a1 += Ct[r * 3 + k] * Dm[k * 3 + c];
+          a2 += Ct[r * 3 + k] * wxS[k * 3 + c];
+          a3 += Ct[r * 3 + k] * S[k * 3 + c];
+          a4 += Ct[r * 3 + k] * vxS[k * 3 + c];
+        }
+        T1[r * 3 + c] = -a1 + a2;
+        T2[r * 3 + c] = a3;
+        T3[r * 3 + c] = a4;
+      }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const int rc = r * 3 + c;
+        J[r * 24 + 6 * j + c] = 0.0;
+        J[r * 24 + 6 * j + 3 + c] = -(w[j] * T1[rc] - w[4 + j] * T2[rc]) * ig;
+        J[(3 + r) * 24 + 6 * j + c] = -(w[8 + j] * Ct[rc]) * ia;
+        J[(3 + r) * 24 + 6 * j + 3 + c] = (w[j] * T3[rc]) * ia;
+      }
+}
+
+// IMU Jacobian w.r.t. the 9 IMU columns (b_g | b_a | g_w), row r, column c
+__device__ __forceinline__ double imu_jth(const SpDev& d, const double* Ct, int r, int c) {
+  if (r < 3) return (c == r) ? -d.ig : 0.0;
+  if (c < 3) return 0.0;
+  if (c < 6) return (c - 3 == r - 3) ? -d.ia : 0.0;
+  return Ct[(r - 3) * 3 + (c - 6)] * d.ia;
+}
+
+// ---------------------------------------------------------------- k_sp_assemble
+// One block per cyclic-reduction node i (coefficients 3i..3i+2): D_i (18 x 18), U_i (coupling to node
+// i+1) and R_i = [H_s,theta | g_s] (18 x (C+1)) from the frames and IMU samples whose support touches the
+// node; the IMU theta-theta partial row of the samples the node owns (first coefficient in the node).
+__global__ void __launch_bounds__(256) k_sp_assemble(SpDev d) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  const int i = blockIdx.x, tid = threadIdx.x, nth = blockDim.x, C = d.C, m = d.m;
+  const int nout = 2 * NB * NB + NB * m;
+  double* out = sm;                       // [nout]
+  double* tj = out + nout;                // [TCH][6][24] IMU J | frame: FH (FHS)
+  const int stride = max(144 + 15, d.FHS);
+  double* te = tj + TCH * stride;         // unused spare
+  __shared__ int tb[TCH];
+  __shared__ double tw[TCH][4];
+  __shared__ double ipt[WI];
+  (void)te;
+  for (int q = tid; q < nout; q += nth) out[q] = 0.0;
+  if (tid < WI) ipt[tid] = 0.0;
+  const int k0 = SB * i;
+  // ---- frames
+  const int fa = d.node_fr[2 * i], fz = d.node_fr[2 * i + 1];
+  for (int c0 = fa; c0 < fz; c0 += TCH) {
+    const int nt = min(TCH, fz - c0);
+    __syncthreads();
+    for (int q = tid; q < nt * d.FHS; q += nth) tj[(q / d.FHS) * stride + q % d.FHS] = d.FH[(size_t)(c0 + q / d.FHS) * d.FHS + q % d.FHS];
+    if (tid < nt) {
+      tb[tid] = d.fb[c0 + tid];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) tw[tid][j] = d.fw[4 * (c0 + tid) + j];
+    }
+    __syncthreads();
+    for (int q = tid; q < nout; q += nth) {
+      double s = 0.0;
+      if (q < 2 * NB * NB) {
+        const int blk = q / (NB * NB), e = q % (NB * NB), r = e / NB, c = e % NB;
+        const int kr = k0 + r / 6, kc = k0 + SB * blk + c / 6;
+        for (int t = 0; t < nt; ++t) {
+          const int jr = kr - tb[t], jc = kc - tb[t];
+          if (jr < 0 || jr > 3 || jc < 0 || jc > 3) continue;
+          s += tw[t][jr] * tw[t][jc] * tj[t * stride + (r % 6) * 6 + (c % 6)];
+        }
+      } else {
+        const int e = q - 2 * NB * NB, r = e / m, a = e % m;
+        const int kr = k0 + r / 6;
+        for (int t = 0; t < nt; ++t) {
+          const int jr = kr - tb[t];
+          if (jr < 0 || jr > 3) continue;
+          const double h = (a < C) ? tj[t * stride + 36 + (r % 6) * C + a] : tj[t * stride + 36 + 6 * C + (r % 6)];
+          s += tw[t][jr] * h;
+        }
+      }
+      out[q] += s;
+    }
+  }
+  // ---- IMU samples
+  const int ma = d.node_im[2 * i], mz = d.node_im[2 * i + 1];
+  for (int c0 = ma; c0 < mz; c0 += TCH) {
+    const int nt = min(TCH, mz - c0);
+    __syncthreads();
+    if (tid < nt) {
+      double* J = tj + tid * stride;
+      imu_sample(d, c0 + tid, J + 144, J, J + 150);  // e at +144, Ct at +150
+      tb[tid] = d.ib[c0 + tid];
+    }
+    __syncthreads();
+    for (int q = tid; q < nout; q += nth) {
+      double s = 0.0;
+      if (q < 2 * NB * NB) {
+        const int blk = q / (NB * NB), e = q % (NB * NB), r = e / NB, c = e % NB;
+        const int kr = k0 + r / 6, kc = k0 + SB * blk + c / 6;
+        for (int t = 0; t < nt; ++t) {
+          const int jr = kr - tb[t], jc = kc - tb[t];
+          if (jr < 0 || jr > 3 || jc < 0 || jc > 3) continue;
+          const double* J = tj + t * stride;
+          const int ca = 6 * jr + r % 6, cb = 6 * jc + c % 6;
+#pragma unroll
+          for (int z = 0; z < 6; ++z) s += J[z * 24 + ca] * J[z * 24 + cb];
+        }
+      } else {
+        const int e = q - 2 * NB * NB, r = e / m, a = e % m;
+        const int kr = k0 + r / 6;
+        const bool imu_col = a >= d.col_imu && a < d.col_imu + 9;
+        if (a == C || imu_col) {
+          for (int t = 0; t < nt; ++t) {
+            const int jr = kr - tb[t];
+            if (jr < 0 || jr > 3) continue;
+            const double* J = tj + t * stride;
+            const int ca = 6 * jr + r % 6;
+            if (a == C) {
+#pragma unroll
+              for (int z = 0; z < 6; ++z) s -= J[z * 24 + ca] * J[144 + z];
+            } else {
+#pragma unroll
+              for (int z = 0; z < 6; ++z) s += J[z * 24 + ca] * imu_jth(d, J + 150, z, a - d.col_imu);
+            }
+          }
+        }
+      }
+      out[q] += s;
+    }
+    // theta-theta of the samples this node owns
+    if (tid < WI) {
+      double s = 0.0;
+      for (int t = 0; t < nt; ++t) {
+        if (tb[t] < k0 || tb[t] >= k0 + SB) continue;
+        const double* J = tj + t * stride;
+        if (tid < 45) {
+          int a = 0, e = tid;
+          while (e >= 9 - a) {
+            e -= 9 - a;
+            ++a;
+          }
+          const int bb = a + e;
+#pragma unroll
+          for (int z = 0; z < 6; ++z) s += imu_jth(d, J + 150, z, a) * imu_jth(d, J + 150, z, bb);
+        } else if (tid < 54) {
+#pragma unroll
+          for (int z = 0; z < 6; ++z) s -= imu_jth(d, J + 150, z, tid - 45) * J[144 + z];
+        } else {
+#pragma unroll
+          for (int z = 0; z < 6; ++z) s += J[144 + z] * J[144 + z];
+        }
+      }
+      ipt[tid] += s;
+    }
+  }
+  __syncthreads();
+  // padded rows (coefficients >= K): identity diagonal, no coupling
+  for (int q = tid; q < nout; q += nth) {
+    double v = out[q];
+    if (q < NB * NB) {
+      const int r = q / NB, c = q % NB;
+      if (k0 + r / 6 >= d.K || k0 + c / 6 >= d.K) v = (r == c) ? 1.0 : 0.0;
+    } else if (q < 2 * NB * NB) {
+      const int e = q - NB * NB, r = e / NB, c = e % NB;
+      if (k0 + r / 6 >= d.K || k0 + SB + c / 6 >= d.K) v = 0.0;
+    } else {
+      const int e = q - 2 * NB * NB, r = e / m;
+      if (k0 + r / 6 >= d.K) v = 0.0;
+    }
+    if (q < NB * NB)
+      d.D0[(size_t)i * NB * NB + q] = v;
+    else if (q < 2 * NB * NB)
+      d.U0[(size_t)i * NB * NB + q - NB * NB] = v;
+    else
+      d.R0[(size_t)i * NB * m + q - 2 * NB * NB] = v;
+  }
+  if (tid < WI) d.ipart[(size_t)i * WI + tid] = ipt[tid];
+}
+
+// ---------------------------------------------------------------- k_sp_reduce_cc: H_cc, g_c, cost
+__global__ void __launch_bounds__(256) k_sp_reduce_cc(SpDev d) {
+  const int C = d.C, nup = C * (C + 1) / 2;
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= d.Wc) return;
+  double s = 0.0;
+  for (int b = 0; b < d.nblk_f; ++b) s += d.part[(size_t)b * d.Wc + q];
+  // IMU columns
+  int a = -1, bcol = -1;
+  if (q < nup) {
+    int e = q;
+    a = 0;
+    while (e >= C - a) {
+      e -= C - a;
+      ++a;
+    }
+    bcol = a + e;
+    const int ia = a - d.col_imu, ib = bcol - d.col_imu;
+    if (ia >= 0 && ia < 9 && ib >= 0 && ib < 9) {
+      const int ii = ia * 9 - ia * (ia - 1) / 2 + (ib - ia);
+      for (int n = 0; n < d.n; ++n) s += d.ipart[(size_t)n * WI + ii];
+    }
+    d.Hcc[a * C + bcol] = s;
+    d.Hcc[bcol * C + a] = s;
+  } else if (q < nup + C) {
+    const int ia = q - nup - d.col_imu;
+    if (ia >= 0 && ia < 9)
+      for (int n = 0; n < d.n; ++n) s += d.ipart[(size_t)n * WI + 45 + ia];
+    d.Hcc[C * C + (q - nup)] = s;
+  } else {
+    for (int n = 0; n < d.n; ++n) s += d.ipart[(size_t)n * WI + 54];
+    d.Hcc[C * C + C] = s;
+    d.sc[SC_COST_BUILD] = s;
+  }
+}
+
+// ---------------------------------------------------------------- cyclic reduction
+// Block-tridiagonal SPD system over nodes: D_i x_i + U_{i-1}^T x_{i-1} + U_i x_{i+1} = R_i (18 x m RHS).
+// Level stride s: nodes i % 2s == s are eliminated (Cholesky L_j, Z_j = L_j^-1 [U_l^T | U_j | R_j]),
+// nodes i % 2s == 0 absorb them; the back-substitution runs the levels in reverse.
+__global__ void __launch_bounds__(256) k_sp_prep(SpDev d) {
+  const int i = blockIdx.x, tid = threadIdx.x, m = d.m;
+  const double lam2 = d.sc[SC_LAM2];
+  for (int q = tid; q < NB * NB; q += blockDim.x) {
+    const double v = d.D0[(size_t)i * NB * NB + q];
+    d.D[(size_t)i * NB * NB + q] = (q / NB == q % NB && SB * i + q / (6 * NB) < d.K) ? v + lam2 : v;
+    d.U[(size_t)i * NB * NB + q] = d.U0[(size_t)i * NB * NB + q];
+  }
+  for (int q = tid; q < NB * m; q += blockDim.x) d.R[(size_t)i * NB * m + q] = d.R0[(size_t)i * NB * m + q];
+  if (i == 0 && tid == 0) d.sc[SC_OK] = 1.0;
+}
+
+// in-LDS Cholesky of an 18 x 18 SPD matrix (lower, row-major); returns false if not positive definite
+__device__ bool chol18(double* A, int tid) {
+  __shared__ int okf;
+  if (tid == 0) okf = 1;
+  __syncthreads();
+  for (int k = 0; k < NB; ++k) {
+    if (tid == 0) {
+      const double v = A[k * NB + k];
+      if (!(v > 0.0)) okf = 0;
+      A[k * NB + k] = sqrt(v > 0.0 ? v : 1.0);
+    }
+    __syncthreads();
+    const double dk = A[k * NB + k];
+    if (tid > k && tid < NB) A[tid * NB + k] /= dk;
+    __syncthreads();
+    for (int q = tid; q < NB * NB; q += blockDim.x) {
+      const int r = q / NB, c = q % NB;
+      if (r > k && c > k && c <= r) A[r * NB + c] -= A[r * NB + k] * A[c * NB + k];
+    }
+    __syncthreads();
+  }
+  return okf != 0;
+}
+
+__global__ void __launch_bounds__(256) k_sp_elim(SpDev d, int s) {
+  __shared__ double L[NB * NB];
+  extern __shared__ __attribute__((aligned(16))) double W[];  // [18][36 + m]
+  const int j = s + 2 * s * blockIdx.x, tid = threadIdx.x, m = d.m, wc = 36 + m;
+  if (j >= d.n) return;
+  const int l = j - s, r = j + s;
+  const double* Dj = d.D + (size_t)j * NB * NB;
+  const double* Ul = d.U + (size_t)l * NB * NB;  // coupling l -> j (rows l)
+  const double* Uj = d.U + (size_t)j * NB * NB;  // coupling j -> r
+  const double* Rj = d.R + (size_t)j * NB * m;
+  for (int q = tid; q < NB * NB; q += blockDim.x) L[q] = Dj[q];
+  for (int q = tid; q < NB * wc; q += blockDim.x) {
+    const int row = q / wc, c = q % wc;
+    double v;
+    if (c < NB)
+      v = Ul[c * NB + row];  // U_l^T
+    else if (c < 2 * NB)
+      v = (r < d.n) ? Uj[row * NB + c - NB] : 0.0;
+    else
+      v = Rj[row * m + c - 2 * NB];
+    W[q] = v;
+  }
+  __syncthreads();
+  const bool ok = chol18(L, tid);
+  if (!ok && tid == 0) d.sc[SC_OK] = 0.0;
+  // forward substitution L Z = W, one column per thread
+  for (int c = tid; c < wc; c += blockDim.x) {
+    double z[NB];
+#pragma unroll
+    for (int row = 0; row < NB; ++row) {
+      double v = W[row * wc + c];
+#pragma unroll
+      for (int k = 0; k < row; ++k) v -= L[row * NB + k] * z[k];
+      z[row] = v / L[row * NB + row];
+    }
+#pragma unroll
+    for (int row = 0; row < NB; ++row) d.Z[(size_t)j * NB * wc + row * wc + c] = z[row];
+  }
+  for (int q = tid; q < NB * NB; q += blockDim.x) d.Lf[(size_t)j * NB * NB + q] = L[q];
+}
+
+__global__ void __launch_bounds__(256) k_sp_keep(SpDev d, int s) {
+  extern __shared__ __attribute__((aligned(16))) double W[];  // Zl [18][wc] | Zr [18][wc]
+  const int i = 2 * s * blockIdx.x, tid = threadIdx.x, m = d.m, wc = 36 + m;
+  if (i >= d.n) return;
+  const int jl = i - s, jr = i + s;
+  const bool hl = jl >= 0, hr = jr < d.n;
+  double* Zl = W;
+  double* Zr = W + NB * wc;
+  for (int q = tid; q < NB * wc; q += blockDim.x) {
+    Zl[q] = hl ? d.Z[(size_t)jl * NB * wc + q] : 0.0;
+    Zr[q] = hr ? d.Z[(size_t)jr * NB * wc + q] : 0.0;
+  }
+  __syncthreads();
+  double* Di = d.D + (size_t)i * NB * NB;
+  double* Ui = d.U + (size_t)i * NB * NB;
+  double* Ri = d.R + (size_t)i * NB * m;
+  // D_i -= A^T A (A = Zl[:, 18:36]) + B^T B (B = Zr[:, 0:18]); U_i = -B^T Zr[:, 18:36]
+  for (int q = tid; q < 2 * NB * NB; q += blockDim.x) {
+    const int e = q % (NB * NB), a = e / NB, b = e % NB;
+    double sacc = 0.0;
+    if (q < NB * NB) {
+#pragma unroll
+      for (int k = 0; k < NB; ++k) sacc += Zl[k * wc + NB + a] * Zl[k * wc + NB + b] + Zr[k * wc + a] * Zr[k * wc + b];
+      Di[e] -= sacc;
+    } else {
+#pragma unroll
+      for (int k = 0; k < NB; ++k) sacc += Zr[k * wc + a] * Zr[k * wc + NB + b];
+      Ui[e] = -sacc;
+    }
+  }
+  for (int q = tid; q < NB * m; q += blockDim.x) {
+    const int a = q / m, c = q % m;
+    double sacc = 0.0;
+#pragma unroll
+    for (int k = 0; k < NB; ++k) sacc += Zl[k * wc + NB + a] * Zl[k * wc + 2 * NB + c] + Zr[k * wc + a] * Zr[k * wc + 2 * NB + c];
+    Ri[q] -= sacc;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_sp_top(SpDev d) {
+  __shared__ double L[NB * NB];
+  const int tid = threadIdx.x, m = d.m;
+  for (int q = tid; q < NB * NB; q += blockDim.x) L[q] = d.D[q];
+  __syncthreads();
+  const bool ok = chol18(L, tid);
+  if (!ok && tid == 0) d.sc[SC_OK] = 0.0;
+  for (int c = tid; c < m; c += blockDim.x) {
+    double z[NB];
+#pragma unroll
+    for (int row = 0; row < NB; ++row) {
+      double v = d.R[row * m + c];
+#pragma unroll
+      for (int k = 0; k < row; ++k) v -= L[row * NB + k] * z[k];
+      z[row] = v / L[row * NB + row];
+    }
+#pragma unroll
+    for (int row = NB - 1; row >= 0; --row) {
+      double v = z[row];
+#pragma unroll
+      for (int k = row + 1; k < NB; ++k) v -= L[k * NB + row] * z[k];
+      z[row] = v / L[row * NB + row];
+    }
+#pragma unroll
+    for (int row = 0; row < NB; ++row) d.X[row * m + c] = z[row];
+  }
+}
+
+__global__ void __launch_bounds__(256) k_sp_back(SpDev d, int s) {
+  __shared__ double L[NB * NB];
+  const int j = s + 2 * s * blockIdx.x, tid = threadIdx.x, m = d.m, wc = 36 + m;
+  if (j >= d.n) return;
+  const int l = j - s, r = j + s;
+  for (int q = tid; q < NB * NB; q += blockDim.x) L[q] = d.Lf[(size_t)j * NB * NB + q];
+  __syncthreads();
+  const double* Z = d.Z + (size_t)j * NB * wc;
+  const double* xl = d.X + (size_t)l * NB * m;
+  const double* xr = d.X + (size_t)(r < d.n ? r : l) * NB * m;
+  for (int c = tid; c < m; c += blockDim.x) {
+    double z[NB];
+#pragma unroll
+    for (int row = 0; row < NB; ++row) {
+      double v = Z[row * wc + 2 * NB + c];
+      for (int k = 0; k < NB; ++k) {
+        v -= Z[row * wc + k] * xl[k * m + c];
+        if (r < d.n) v -= Z[row * wc + NB + k] * xr[k * m + c];
+      }
+      z[row] = v;
+    }
+#pragma unroll
+    for (int row = NB - 1; row >= 0; --row) {
+      double v = z[row];
+#pragma unroll
+      for (int k = row + 1; k < NB; ++k) v -= L[k * NB + row] * z[k];
+      z[row] = v / L[row * NB + row];
+    }
+#pragma unroll
+    for (int row = 0; row < NB; ++row) d.X[(size_t)j * NB * m + row * m + c] = z[row];
+  }
+}
+
+// ---------------------------------------------------------------- Schur complement onto theta
+// partial rows of sum_i R0_i^T X_i over NPB nodes: upper C x C | C (the g column)
+__global__ void __launch_bounds__(256) k_sp_schur(SpDev d) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];  // R0 [18][m] | X [18][m]
+  const int tid = threadIdx.x, C = d.C, m = d.m, nup = C * (C + 1) / 2;
+  double* Rl = sm;
+  double* Xl = sm + NB * m;
+  double* acc = Xl + NB * m;  // [Ws]
+  for (int q = tid; q < d.Ws; q += blockDim.x) acc[q] = 0.0;
+  const int i0 = blockIdx.x * NPB, i1 = min(d.n, i0 + NPB);
+  for (int i = i0; i < i1; ++i) {
+    __syncthreads();
+    for (int q = tid; q < NB * m; q += blockDim.x) {
+      Rl[q] = d.R0[(size_t)i * NB * m + q];
+      Xl[q] = d.X[(size_t)i * NB * m + q];
+    }
+    __syncthreads();
+    for (int q = tid; q < d.Ws; q += blockDim.x) {
+      int a, b;
+      if (q < nup) {
+        int e = q;
+        a = 0;
+        while (e >= C - a) {
+          e -= C - a;
+          ++a;
+        }
+        b = a + e;
+      } else {
+        a = q - nup;
+        b = C;
+      }
+      double s = 0.0;
+#pragma unroll
+      for (int k = 0; k < NB; ++k) s += Rl[k * m + a] * Xl[k * m + b];
+      acc[q] += s;
+    }
+  }
+  __syncthreads();
+  for (int q = tid; q < d.Ws; q += blockDim.x) d.spart[(size_t)blockIdx.x * d.Ws + q] = acc[q];
+}
+
+// dense camera / IMU block: S = H_cc + lam2 I - sum, b = g_c - sum; Cholesky in LDS; dtheta -> dx[0..C)
+__global__ void __launch_bounds__(256) k_sp_camsolve(SpDev d) {
+  __shared__ double S[MAXC * MAXC];
+  __shared__ double bv[MAXC];
+  __shared__ int okf;
+  const int tid = threadIdx.x, C = d.C, nup = C * (C + 1) / 2;
+  const double lam2 = d.sc[SC_LAM2];
+  for (int q = tid; q < nup + C; q += blockDim.x) {
+    double s = 0.0;
+    for (int b = 0; b < d.nblk_s; ++b) s += d.spart[(size_t)b * d.Ws + q];
+    if (q < nup) {
+      int e = q, a = 0;
+      while (e >= C - a) {
+        e -= C - a;
+        ++a;
+      }
+      const int bb = a + e;
+      const double v = d.Hcc[a * C + bb] + (a == bb ? lam2 : 0.0) - s;
+      S[a * C + bb] = v;
+      S[bb * C + a] = v;
+    } else {
+      bv[q - nup] = d.Hcc[C * C + (q - nup)] - s;
+    }
+  }
+  if (tid == 0) okf = 1;
+  __syncthreads();
+  for (int k = 0; k < C; ++k) {
+    if (tid == 0) {
+      const double v = S[k * C + k];
+      if (!(v > 0.0)) okf = 0;
+      S[k * C + k] = sqrt(v > 0.0 ? v : 1.0);
+    }
+    __syncthreads();
+    const double dk = S[k * C + k];
+    if (tid > k && tid < C) S[tid * C + k] /= dk;
+    __syncthreads();
+    for (int q = tid; q < C * C; q += blockDim.x) {
+      const int r = q / C, c = q % C;
+      if (r > k && c > k && c <= r) S[r * C + c] -= S[r * C + k] * S[c * C + k];
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    double x[MAXC];
+    for (int r = 0; r < C; ++r) {
+      double v = bv[r];
+      for (int k = 0; k < r; ++k) v -= S[r * C + k] * x[k];
+      x[r] = v / S[r * C + r];
+    }
+    for (int r = C - 1; r >= 0; --r) {
+      double v = x[r];
+      for (int k = r + 1; k < C; ++k) v -= S[k * C + r] * x[k];
+      x[r] = v / S[r * C + r];
+    }
+    for (int r = 0; r < C; ++r) d.dx[r] = x[r];
+    if (!okf) d.sc[SC_OK] = 0.0;
+  }
+}
+
+// coefficient steps ds_i = X_i[:, C] - X_i[:, :C] dtheta; with `apply` (and a successful solve) the state
+// update: backup copy, additive coefficients, theta DVs (block 0); per-block max |dx|.
+__global__ void __launch_bounds__(64) k_sp_update(SpDev d, int apply) {
+  const int i = blockIdx.x, tid = threadIdx.x, C = d.C, m = d.m;
+  const bool go = apply && d.sc[SC_OK] != 0.0;
+  double mx = 0.0;
+  if (tid < NB) {
+    const int k = SB * i + tid / 6;
+    if (k < d.K) {
+      const double* x = d.X + (size_t)i * NB * m + tid * m;
+      double v = x[C];
+      for (int c = 0; c < C; ++c) v -= x[c] * d.dx[c];
+      d.dx[C + 6 * k + tid % 6] = v;
+      mx = fabs(v);
+      const int o = d.off_coef + 6 * k + tid % 6;
+      if (go) {
+        d.backup[o] = d.state[o];
+        d.state[o] += v;
+      }
+    }
+  }
+  if (i == 0) {
+    for (int c = tid; c < C; c += 64) mx = fmax(mx, fabs(d.dx[c]));
+    if (go) {
+      for (int q = tid; q < d.off_coef; q += 64) d.backup[q] = d.state[q];
+      __syncthreads();
+      for (int c = tid; c < C; c += 64) {
+        const int kind = d.ckind[c], idx = d.cidx[c], sub = d.csub[c];
+        if (kind == 0) d.state[idx * KB_MAX_INTR + sub] += d.dx[c];
+        if (kind == 2) d.state[d.off_imu + sub] += d.dx[c];
+      }
+      if (tid < d.N) {  // pose DVs q = tid: B_q (q < N-1) or T_c0_b
+        const int q = tid;
+        double* pose = d.state + (q < d.N - 1 ? d.off_base + 7 * q : d.off_cb);
+        double np[7];
+        kb::update_pose(pose, d.dx + d.col_pose[q], np);
+#pragma unroll
+        for (int k = 0; k < 7; ++k) pose[k] = np[k];
+      }
+    }
+  }
+  // wave max
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o));
+  if (tid == 0) d.dmax[i] = mx;
+}
+
+// ---------------------------------------------------------------- cost (evaluateError)
+template <unsigned MM>
+__global__ void __launch_bounds__(512) k_sp_cost_frames(SpDev d) {
+  __shared__ double red[8];
+  const int N = d.N, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, cam = wave;
+  const double* st = d.state;
+  double RA[9], tA[3];
+  kb::quat2r(st + d.off_cb, RA);
+  tA[0] = st[d.off_cb + 4];
+  tA[1] = st[d.off_cb + 5];
+  tA[2] = st[d.off_cb + 6];
+  for (int q = 0; q < cam; ++q) {  // A = B_{cam-1} .. B_0 T_c0_b
+    const double* bq = st + d.off_base + 7 * q;
+    double RB[9], R2[9], t2[3];
+    kb::quat2r(bq, RB);
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+        R2[r * 3 + c] = RB[r * 3 + 0] * RA[0 * 3 + c] + RB[r * 3 + 1] * RA[1 * 3 + c] + RB[r * 3 + 2] * RA[2 * 3 + c];
+      t2[r] = RB[r * 3 + 0] * tA[0] + RB[r * 3 + 1] * tA[1] + RB[r * 3 + 2] * tA[2] + bq[4 + r];
+    }
+#pragma unroll
+    for (int k = 0; k < 9; ++k) RA[k] = R2[k];
+    tA[0] = t2[0];
+    tA[1] = t2[1];
+    tA[2] = t2[2];
+  }
+  const int model = d.model[cam];
+  const double* intr = st + cam * KB_MAX_INTR;
+  double s = 0.0;
+  const int f0 = blockIdx.x * FPB, f1 = min(d.F, f0 + FPB);
+  for (int f = f0; f < f1; ++f) {
+    const int b = d.fb[f];
+    const double* w = d.fw + 4 * f;
+    const double* cf = st + d.off_coef + 6 * b;
+    double v[6];
+#pragma unroll
+    for (int r = 0; r < 6; ++r) v[r] = w[0] * cf[r] + w[1] * cf[6 + r] + w[2] * cf[12 + r] + w[3] * cf[18 + r];
+    double Rwb[9], R[9], t[3];
+    rv_C(v + 3, Rwb);
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+        R[r * 3 + c] = RA[r * 3 + 0] * Rwb[c * 3 + 0] + RA[r * 3 + 1] * Rwb[c * 3 + 1] + RA[r * 3 + 2] * Rwb[c * 3 + 2];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) t[r] = tA[r] - (R[r * 3 + 0] * v[0] + R[r * 3 + 1] * v[1] + R[r * 3 + 2] * v[2]);
+    const int2 fv = d.fview[(size_t)f * N + cam];
+    for (int k = fv.x + lane; k < fv.y; k += 64) {
+      const int ci = d.cid[k];
+      const double2 yv = d.y[k];
+      const double* X = d.target + 3 * ci;
+      const double p0 = R[0] * X[0] + R[1] * X[1] + R[2] * X[2] + t[0];
+      const double p1 = R[3] * X[0] + R[4] * X[1] + R[5] * X[2] + t[1];
+      const double p2 = R[6] * X[0] + R[7] * X[1] + R[8] * X[2] + t[2];
+      double u, wv;
+      kb::project<MM>(model, intr, p0, p1, p2, u, wv);
+      const double e0 = yv.x - u, e1 = yv.y - wv;
+      s += e0 * e0 + e1 * e1;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if (lane == 0) red[wave] = s;
+  __syncthreads();
+  if (tid == 0) {
+    double t = 0.0;
+    for (int q = 0; q < N; ++q) t += red[q];
+    d.cpart[blockIdx.x] = t;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_sp_cost_imu(SpDev d) {
+  __shared__ double red[4];
+  const int tid = threadIdx.x, m = blockIdx.x * 256 + tid;
+  double s = 0.0;
+  if (m < d.M) {
+    double e[6], Ct[9];
+    imu_sample(d, m, e, nullptr, Ct);
+#pragma unroll
+    for (int r = 0; r < 6; ++r) s += e[r] * e[r];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if ((tid & 63) == 0) red[tid >> 6] = s;
+  __syncthreads();
+  if (tid == 0) d.cpart[d.nblk_f + blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+// fixed-order sums: cost -> sc[SC_COST], max |dx| -> sc[SC_DX]
+__global__ void __launch_bounds__(64) k_sp_cost_reduce(SpDev d, int with_dx) {
+  const int tid = threadIdx.x;
+  double s = 0.0, mx = 0.0;
+  for (int q = tid; q < d.nblk_f + d.nblk_ci; q += 64) s += d.cpart[q];
+  if (with_dx)
+    for (int q = tid; q < d.n; q += 64) mx = fmax(mx, d.dmax[q]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    s += __shfl_xor(s, o);
+    mx = fmax(mx, __shfl_xor(mx, o));
+  }
+  if (tid == 0) {
+    d.sc[SC_COST] = s;
+    if (with_dx) d.sc[SC_DX] = mx;
+  }
+}
+
+__global__ void k_sp_revert(SpDev d) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q < d.S) d.state[q] = d.backup[q];
+}
+
+__global__ void k_sp_set_lam(SpDev d, double lam2) {
+  if (threadIdx.x == 0) d.sc[SC_LAM2] = lam2;
+}
+
+}  // namespace ksp
+
+// ==================================================================================================
+// host side
+// ==================================================================================================
+using namespace ksp;
+
+namespace {
+int fail(const std::string& m) { return kb_internal::fail(m); }
+
+#define KSP_HIP(call)                                                                             \
+  do {                                                                                            \
+    hipError_t e_ = (call);                                                                       \
+    if (e_ != hipSuccess) return fail(std::string(#call) + ": " + hipGetErrorString(e_));        \
+  } while (0)
+
+int nintr_of(int m) {
+  switch (m) {
+    case KB_PINHOLE_RADTAN: return 8;
+    case KB_OMNI_RADTAN: return 9;
+    case KB_EUCM: return 6;
+    case KB_OMNI: return 5;
+    case KB_DS: return 6;
+    case KB_PINHOLE_EQUI: return 8;
+    case KB_PINHOLE_FOV: return 5;
+    default: return -1;
+  }
+}
+
+// B-spline basis matrix of valid segment `seg` (BSpline.cpp:70-152) and basis weights (BSpline.cpp:237-387)
+void basis_matrix(const std::vector<double>& kn, int k, int i, double* out) {
+  if (k == 1) {
+    out[0] = 1.0;
+    return;
+  }
+  double Mp[64];
+  basis_matrix(kn, k - 1, i, Mp);
+  const int n = k - 1;
+  double M1[64] = {0}, M2[64] = {0}, A[64] = {0}, B[64] = {0};
+  for (int r = 0; r < n; ++r)
+    for (int c = 0; c < n; ++c) {
+      M1[r * n + c] = Mp[r * n + c];
+      M2[(r + 1) * n + c] = Mp[r * n + c];
+    }
+  for (int idx = 0; idx < n; ++idx) {
+    const int j = i - k + 2 + idx;
+    const double den = kn[j + k - 1] - kn[j];
+    const double d0 = den <= 0.0 ? 0.0 : (kn[i] - kn[j]) / den;
+    const double d1 = den <= 0.0 ? 0.0 : (kn[i + 1] - kn[i]) / den;
+    A[idx * k + idx] = 1.0 - d0;
+    A[idx * k + idx + 1] = d0;
+    B[idx * k + idx] = -d1;
+    B[idx * k + idx + 1] = d1;
+  }
+  for (int r = 0; r < k; ++r)
+    for (int c = 0; c < k; ++c) {
+      double s = 0.0;
+      for (int l = 0; l < n; ++l) s += M1[r * n + l] * A[l * k + c] + M2[r * n + l] * B[l * k + c];
+      out[r * k + c] = s;
+    }
+}
+
+int basis_weights(const std::vector<double>& kn, int order, double t, int deriv, double* w) {
+  const int nk = (int)kn.size();
+  const double tmin = kn[order - 1], tmax = kn[nk - order];
+  if (t < tmin || t > tmax + 1e-10) return -1;
+  if (std::fabs(tmax - t) < 1e-10) t = tmax;
+  int idx;
+  if (t == tmax) {
+    idx = nk - order - 1;
+  } else {
+    idx = (int)(std::upper_bound(kn.begin(), kn.end(), t) - kn.begin()) - 1;
+  }
+  const double dt = kn[idx + 1] - kn[idx];
+  const double u = dt <= 0.0 ? 0.0 : (t - kn[idx]) / dt;
+  const double mult = dt > 0.0 ? 1.0 / std::pow(dt, deriv) : 0.0;
+  double uv[8] = {0}, uu = 1.0;
+  for (int i = deriv; i < order; ++i) {
+    int dm = 1;
+    for (int q = 0; q < deriv; ++q) dm *= (i - q);
+    uv[i] = mult * uu * dm;
+    uu *= u;
+  }
+  const int bidx = idx - order + 1;
+  double M[64];
+  basis_matrix(kn, order, bidx + order - 1, M);
+  for (int j = 0; j < order; ++j) {
+    double s = 0.0;
+    for (int i = 0; i < order; ++i) s += M[i * order + j] * uv[i];
+    w[j] = s;
+  }
+  return bidx;
+}
+}  // namespace
+
+struct kb_sp_handle {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  SpDev d{};
+  int N = 0, C = 0, K = 0, F = 0, M = 0, n = 0, S = 0, ncols = 0, n_target = 0;
+  std::vector<double> knots;
+  std::vector<void*> allocs;
+  double lambda = 0.0;
+  bool uploaded = false, built = false, solved = false;
+  size_t lds_frames = 0, lds_asm = 0, lds_elim = 0, lds_keep = 0, lds_schur = 0;
+  const void* fn_frames = nullptr;
+  const void* fn_cost = nullptr;
+  hipGraphExec_t gn_graph = nullptr;
+  int gn_graph_n = 0;
+  std::vector<double> trace;
+  double* host_sc = nullptr;  // pinned scalars
+
+  template <class T>
+  int alloc(T** p, size_t cnt) {
+    void* q = nullptr;
+    if (cnt == 0) cnt = 1;
+    hipError_t e = hipMalloc(&q, cnt * sizeof(T));
+    if (e != hipSuccess) return fail(std::string("hipMalloc: ") + hipGetErrorString(e));
+    hipMemsetAsync(q, 0, cnt * sizeof(T), stream);
+    allocs.push_back(q);
+    *p = (T*)q;
+    return 0;
+  }
+};
+
+namespace {
+template <unsigned MM>
+void pick_mm(kb_sp_handle* h) {
+  h->fn_frames = (const void*)k_sp_frames<MM>;
+  h->fn_cost = (const void*)k_sp_cost_frames<MM>;
+}
+
+int launch_build(kb_sp_handle* h) {
+  SpDev& d = h->d;
+  void* args[] = {&d};
+  KSP_HIP(hipLaunchKernel(h->fn_frames, dim3(d.nblk_f), dim3(64 * h->N), args, h->lds_frames, h->stream));
+  KSP_HIP(hipLaunchKernel((const void*)k_sp_assemble, dim3(d.n), dim3(256), args, h->lds_asm, h->stream));
+  hipLaunchKernelGGL(k_sp_reduce_cc, dim3((d.Wc + 255) / 256), dim3(256), 0, h->stream, d);
+  return 0;
+}
+
+int launch_solve(kb_sp_handle* h) {
+  SpDev& d = h->d;
+  hipLaunchKernelGGL(k_sp_prep, dim3(d.n), dim3(256), 0, h->stream, d);
+  int s = 1;
+  for (; s < d.n; s *= 2) {
+    const int ne = (d.n - s + 2 * s - 1) / (2 * s), nk = (d.n + 2 * s - 1) / (2 * s);
+    hipLaunchKernelGGL(k_sp_elim, dim3(ne), dim3(256), h->lds_elim, h->stream, d, s);
+    hipLaunchKernelGGL(k_sp_keep, dim3(nk), dim3(256), h->lds_keep, h->stream, d, s);
+  }
+  hipLaunchKernelGGL(k_sp_top, dim3(1), dim3(256), 0, h->stream, d);
+  for (s /= 2; s >= 1; s /= 2) {
+    const int ne = (d.n - s + 2 * s - 1) / (2 * s);
+    hipLaunchKernelGGL(k_sp_back, dim3(ne), dim3(256), 0, h->stream, d, s);
+  }
+  hipLaunchKernelGGL(k_sp_schur, dim3(d.nblk_s), dim3(256), h->lds_schur, h->stream, d);
+  hipLaunchKernelGGL(k_sp_camsolve, dim3(1), dim3(256), 0, h->stream, d);
+  return 0;
+}
+
+int launch_cost(kb_sp_handle* h, int with_dx) {
+  SpDev& d = h->d;
+  void* args[] = {&d};
+  KSP_HIP(hipLaunchKernel(h->fn_cost, dim3(d.nblk_f), dim3(64 * h->N), args, 0, h->stream));
+  hipLaunchKernelGGL(k_sp_cost_imu, dim3(d.nblk_ci), dim3(256), 0, h->stream, d);
+  hipLaunchKernelGGL(k_sp_cost_reduce, dim3(1), dim3(64), 0, h->stream, d, with_dx);
+  return 0;
+}
+
+// one GN pass: build, solve (lambda = 0), update, cost
+int enqueue_gn_pass(kb_sp_handle* h) {
+  SpDev& d = h->d;
+  hipLaunchKernelGGL(k_sp_set_lam, dim3(1), dim3(64), 0, h->stream, d, 0.0);
+  if (launch_build(h)) return -1;
+  if (launch_solve(h)) return -1;
+  hipLaunchKernelGGL(k_sp_update, dim3(d.n), dim3(64), 0, h->stream, d, 1);
+  return launch_cost(h, 1);
+}
+
+int read_scalars(kb_sp_handle* h) {
+  KSP_HIP(hipMemcpyAsync(h->host_sc, h->d.sc, sizeof(double) * SC_NSC, hipMemcpyDeviceToHost, h->stream));
+  KSP_HIP(hipStreamSynchronize(h->stream));
+  return 0;
+}
+}  // namespace
+
+extern "C" {
+
+kb_sp_handle* kb_sp_create(const kb_sp_layout* L) {
+  if (!L || !L->cam_model || !L->target_points || !L->knots) {
+    fail("kb_sp_create: null layout");
+    return nullptr;
+  }
+  if (L->order != ORD) {
+    fail("kb_sp_create: the device spline path supports order 4 (cubic) only");
+    return nullptr;
+  }
+  if (L->n_cams < 1 || L->n_cams > 8 || L->n_target < 1 || L->n_target > 65535) {
+    fail("kb_sp_create: n_cams / n_target out of range");
+    return nullptr;
+  }
+  if (!(L->sigma_gyro > 0.0) || !(L->sigma_acc > 0.0)) {
+    fail("kb_sp_create: IMU sigmas must be positive");
+    return nullptr;
+  }
+  for (int q = 1; q < L->n_knots; ++q)
+    if (L->knots[q] < L->knots[q - 1]) {
+      fail("kb_sp_create: knots must be non-decreasing");
+      return nullptr;
+    }
+  const int K = L->n_knots - 2 * L->order + 1 > 0 ? L->n_knots - L->order : 0;
+  if (K < ORD) {
+    fail("kb_sp_create: not enough knots for one valid time segment");
+    return nullptr;
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+    fail("kb_sp_create: no HIP device available (the product path has no CPU fallback)");
+    return nullptr;
+  }
+  kb_sp_handle* h = new kb_sp_handle();
+  h->device = L->device;
+  if (hipSetDevice(h->device) != hipSuccess ||
+      hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+    fail("kb_sp_create: cannot select device / create stream");
+    delete h;
+    return nullptr;
+  }
+  h->N = L->n_cams;
+  h->K = K;
+  h->knots.assign(L->knots, L->knots + L->n_knots);
+  h->n_target = L->n_target;
+  SpDev& d = h->d;
+  d.N = h->N;
+  d.K = K;
+  d.n_target = L->n_target;
+  int c = 0;
+  for (int i = 0; i < h->N; ++i) {
+    const int ni = nintr_of(L->cam_model[i]);
+    if (ni < 0) {
+      fail("kb_sp_create: unknown camera model");
+      kb_sp_destroy(h);
+      return nullptr;
+    }
+    d.model[i] = L->cam_model[i];
+    d.nin[i] = ni;
+    d.col_intr[i] = c;
+    for (int q = 0; q < ni; ++q, ++c) {
+      d.ckind[c] = 0;
+      d.cidx[c] = i;
+      d.csub[c] = q;
+    }
+  }
+  for (int q = 0; q < h->N; ++q) {  // B_0 .. B_{N-2}, then T_c0_b
+    d.col_pose[q] = c;
+    for (int e = 0; e < 6; ++e, ++c) {
+      d.ckind[c] = 1;
+      d.cidx[c] = q;
+      d.csub[c] = e;
+    }
+  }
+  d.col_imu = c;
+  for (int e = 0; e < 9; ++e, ++c) {
+    d.ckind[c] = 2;
+    d.cidx[c] = 0;
+    d.csub[c] = e;
+  }
+  h->C = d.C = c;
+  if (h->C > MAXC) {
+    fail("kb_sp_create: camera + IMU block larger than 64 columns");
+    kb_sp_destroy(h);
+    return nullptr;
+  }
+  d.m = h->C + 1;
+  d.off_base = h->N * KB_MAX_INTR;
+  d.off_cb = d.off_base + 7 * (h->N - 1);
+  d.off_imu = d.off_cb + 7;
+  d.off_coef = d.off_imu + 9;
+  h->S = d.S = d.off_coef + 6 * K;
+  h->ncols = h->C + 6 * K;
+  h->n = d.n = (K + SB - 1) / SB;
+  d.ig = 1.0 / L->sigma_gyro;
+  d.ia = 1.0 / L->sigma_acc;
+  d.Wc = h->C * (h->C + 1) / 2 + h->C + 1;
+  d.Ws = h->C * (h->C + 1) / 2 + h->C;
+  d.FHS = 36 + 6 * h->C + 6;
+  unsigned mm = 0;
+  for (int i = 0; i < h->N; ++i) mm |= 1u << d.model[i];
+  if (mm == (1u << KB_PINHOLE_RADTAN))
+    pick_mm<1u << KB_PINHOLE_RADTAN>(h);
+  else
+    pick_mm<kMmAll>(h);
+  int rc = 0;
+  double* tgt = nullptr;
+  rc |= h->alloc(&tgt, 3 * (size_t)L->n_target);
+  d.target = tgt;
+  rc |= h->alloc(&d.state, (size_t)h->S);
+  rc |= h->alloc(&d.backup, (size_t)h->S);
+  rc |= h->alloc(&d.ipart, (size_t)h->n * WI);
+  rc |= h->alloc(&d.Hcc, (size_t)h->C * h->C + h->C + 1);
+  rc |= h->alloc(&d.D0, (size_t)h->n * NB * NB);
+  rc |= h->alloc(&d.U0, (size_t)h->n * NB * NB);
+  rc |= h->alloc(&d.R0, (size_t)h->n * NB * d.m);
+  rc |= h->alloc(&d.D, (size_t)h->n * NB * NB);
+  rc |= h->alloc(&d.U, (size_t)h->n * NB * NB);
+  rc |= h->alloc(&d.R, (size_t)h->n * NB * d.m);
+  rc |= h->alloc(&d.Lf, (size_t)h->n * NB * NB);
+  rc |= h->alloc(&d.Z, (size_t)h->n * NB * (36 + d.m));
+  rc |= h->alloc(&d.X, (size_t)h->n * NB * d.m);
+  d.nblk_s = (h->n + NPB - 1) / NPB;
+  rc |= h->alloc(&d.spart, (size_t)d.nblk_s * d.Ws);
+  rc |= h->alloc(&d.dx, (size_t)h->ncols);
+  rc |= h->alloc(&d.dmax, (size_t)h->n);
+  rc |= h->alloc(&d.sc, (size_t)SC_NSC);
+  if (rc || hipHostMalloc((void**)&h->host_sc, sizeof(double) * SC_NSC) != hipSuccess ||
+      hipMemcpyAsync(tgt, L->target_points, sizeof(double) * 3 * L->n_target, hipMemcpyHostToDevice, h->stream) !=
+          hipSuccess) {
+    if (!rc) fail("kb_sp_create: pinned scalars / target upload failed");
+    kb_sp_destroy(h);
+    return nullptr;
+  }
+  h->lds_elim = sizeof(double) * NB * (36 + d.m);
+  h->lds_keep = 2 * h->lds_elim;
+  h->lds_schur = sizeof(double) * (2 * NB * d.m + d.Ws);
+  h->lds_asm = sizeof(double) * (2 * NB * NB + NB * d.m + TCH * std::max(144 + 15, d.FHS));
+  h->lds_frames = sizeof(double) * (h->N * 64 * XS + h->N * 256 + 2 * h->N * 36 + 2 * h->N * h->N * 36 + d.Wc +
+                                    3 * L->n_target);
+  if (h->lds_frames > 160 * 1024 || h->lds_asm > 160 * 1024 || h->lds_schur > 160 * 1024) {
+    fail("kb_sp_create: LDS budget exceeded for this rig");
+    kb_sp_destroy(h);
+    return nullptr;
+  }
+  hipFuncSetAttribute(h->fn_frames, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_frames);
+  hipFuncSetAttribute((const void*)k_sp_assemble, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_asm);
+  hipFuncSetAttribute((const void*)k_sp_keep, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_keep);
+  hipFuncSetAttribute((const void*)k_sp_elim, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_elim);
+  hipFuncSetAttribute((const void*)k_sp_schur, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_schur);
+  if (hipStreamSynchronize(h->stream) != hipSuccess) {
+    fail("kb_sp_create: stream sync failed");
+    kb_sp_destroy(h);
+    return nullptr;
+  }
+  return h;
+}
+
+void kb_sp_destroy(kb_sp_handle* h) {
+  if (!h) return;
+  hipSetDevice(h->device);
+  if (h->stream) hipStreamSynchronize(h->stream);
+  if (h->gn_graph) hipGraphExecDestroy(h->gn_graph);
+  for (void* p : h->allocs) hipFree(p);
+  if (h->host_sc) hipHostFree(h->host_sc);
+  if (h->stream) hipStreamDestroy(h->stream);
+  delete h;
+}
+
+int kb_sp_upload(kb_sp_handle* h, int32_t n_frames, const double* frame_time, int32_t n_views, int32_t n_corners,
+                 const double* y, const uint16_t* corner_id, const uint32_t* view_offsets,
+                 const uint32_t* view_frame, const uint8_t* view_cam, int32_t n_imu, const double* imu_time,
+                 const double* imu_gyro, const double* imu_acc) {
+  if (!h) return fail("kb_sp_upload: null handle");
+  if (h->uploaded) return fail("kb_sp_upload: observations already uploaded (create a new handle)");
+  if (n_frames < 1 || n_views < 0 || n_corners < 0 || n_imu < 0) return fail("kb_sp_upload: bad sizes");
+  if (!frame_time || (n_views && (!view_offsets || !view_frame || !view_cam)) || (n_corners && (!y || !corner_id)) ||
+      (n_imu && (!imu_time || !imu_gyro || !imu_acc)))
+    return fail("kb_sp_upload: null array");
+  KSP_HIP(hipSetDevice(h->device));
+  SpDev& d = h->d;
+  const int N = h->N, F = n_frames, M = n_imu;
+  // frames: basis weights, views (sorted by frame, one per camera)
+  std::vector<int> fb(F), ib(M);
+  std::vector<double> fw(4 * (size_t)F), iw(12 * (size_t)M), imeas(6 * (size_t)M);
+  for (int f = 0; f < F; ++f) {
+    if (f && frame_time[f] < frame_time[f - 1]) return fail("kb_sp_upload: frame times must be non-decreasing");
+    fb[f] = basis_weights(h->knots, ORD, frame_time[f], 0, &fw[4 * (size_t)f]);
+    if (fb[f] < 0) return fail("kb_sp_upload: frame time outside the spline interval");
+  }
+  for (int m = 0; m < M; ++m) {
+    if (m && imu_time[m] < imu_time[m - 1]) return fail("kb_sp_upload: IMU times must be non-decreasing");
+    ib[m] = basis_weights(h->knots, ORD, imu_time[m], 0, &iw[12 * (size_t)m]);
+    if (ib[m] < 0) return fail("kb_sp_upload: IMU time outside the spline interval");
+    basis_weights(h->knots, ORD, imu_time[m], 1, &iw[12 * (size_t)m + 4]);
+    basis_weights(h->knots, ORD, imu_time[m], 2, &iw[12 * (size_t)m + 8]);
+    for (int r = 0; r < 3; ++r) {
+      imeas[6 * (size_t)m + r] = imu_gyro[3 * (size_t)m + r];
+      imeas[6 * (size_t)m + 3 + r] = imu_acc[3 * (size_t)m + r];
+    }
+  }
+  std::vector<int2> fview((size_t)F * N, make_int2(0, 0));
+  for (int v = 0; v < n_views; ++v) {
+    const uint32_t f = view_frame[v], cam = view_cam[v];
+    if (f >= (uint32_t)F || cam >= (uint32_t)N) return fail("kb_sp_upload: view frame / camera out of range");
+    if (v && view_frame[v] < view_frame[v - 1]) return fail("kb_sp_upload: views must be sorted by frame");
+    if (view_offsets[v + 1] < view_offsets[v] || view_offsets[v + 1] > (uint32_t)n_corners)
+      return fail("kb_sp_upload: bad view offsets");
+    int2& e = fview[(size_t)f * N + cam];
+    if (e.y > e.x) return fail("kb_sp_upload: two views of one (frame, camera)");
+    e = make_int2((int)view_offsets[v], (int)view_offsets[v + 1]);
+  }
+  for (int k = 0; k < n_corners; ++k)
+    if (corner_id[k] >= h->n_target) return fail("kb_sp_upload: corner id out of range");
+  // per node: terms whose support [b, b+3] touches coefficients 3i .. 3i+2
+  std::vector<int> nfr(2 * (size_t)h->n), nim(2 * (size_t)h->n);
+  for (int i = 0; i < h->n; ++i) {
+    const int lo = SB * i - 3, hi = SB * i + 2;
+    nfr[2 * i] = (int)(std::lower_bound(fb.begin(), fb.end(), lo) - fb.begin());
+    nfr[2 * i + 1] = (int)(std::upper_bound(fb.begin(), fb.end(), hi) - fb.begin());
+    nim[2 * i] = (int)(std::lower_bound(ib.begin(), ib.end(), lo) - ib.begin());
+    nim[2 * i + 1] = (int)(std::upper_bound(ib.begin(), ib.end(), hi) - ib.begin());
+  }
+  h->F = d.F = F;
+  h->M = d.M = M;
+  d.nblk_f = (F + FPB - 1) / FPB;
+  d.nblk_ci = std::max(1, (M + 255) / 256);
+  int rc = 0;
+  double2* dy = nullptr;
+  uint16_t* dcid = nullptr;
+  int2* dfv = nullptr;
+  int *dfb = nullptr, *dib = nullptr, *dnf = nullptr, *dni = nullptr;
+  double *dfw = nullptr, *diw = nullptr, *dim = nullptr;
+  rc |= h->alloc(&dy, (size_t)n_corners);
+  rc |= h->alloc(&dcid, (size_t)n_corners);
+  rc |= h->alloc(&dfv, (size_t)F * N);
+  rc |= h->alloc(&dfb, (size_t)F);
+  rc |= h->alloc(&dfw, 4 * (size_t)F);
+  rc |= h->alloc(&dib, (size_t)M);
+  rc |= h->alloc(&diw, 12 * (size_t)M);
+  rc |= h->alloc(&dim, 6 * (size_t)M);
+  rc |= h->alloc(&dnf, 2 * (size_t)h->n);
+  rc |= h->alloc(&dni, 2 * (size_t)h->n);
+  rc |= h->alloc(&d.FH, (size_t)F * d.FHS);
+  rc |= h->alloc(&d.part, (size_t)d.nblk_f * d.Wc);
+  rc |= h->alloc(&d.cpart, (size_t)(d.nblk_f + d.nblk_ci));
+  if (rc) return -1;
+  if (n_corners) {
+    KSP_HIP(hipMemcpyAsync(dy, y, sizeof(double) * 2 * n_corners, hipMemcpyHostToDevice, h->stream));
+    KSP_HIP(hipMemcpyAsync(dcid, corner_id, sizeof(uint16_t) * n_corners, hipMemcpyHostToDevice, h->stream));
+  }
+  KSP_HIP(hipMemcpyAsync(dfv, fview.data(), sizeof(int2) * fview.size(), hipMemcpyHostToDevice, h->stream));
+  KSP_HIP(hipMemcpyAsync(dfb, fb.data(), sizeof(int) * F, hipMemcpyHostToDevice, h->stream));
+  KSP_HIP(hipMemcpyAsync(dfw, fw.data(), sizeof(double) * fw.size(), hipMemcpyHostToDevice, h->stream));
+  if (M) {
+    KSP_HIP(hipMemcpyAsync(dib, ib.data(), sizeof(int) * M, hipMemcpyHostToDevice, h->stream));
+    KSP_HIP(hipMemcpyAsync(diw, iw.data(), sizeof(double) * iw.size(), hipMemcpyHostToDevice, h->stream));
+    KSP_HIP(hipMemcpyAsync(dim, imeas.data(), sizeof(double) * imeas.size(), hipMemcpyHostToDevice, h->stream));
+  }
+  KSP_HIP(hipMemcpyAsync(dnf, nfr.data(), sizeof(int) * nfr.size(), hipMemcpyHostToDevice, h->stream));
+  KSP_HIP(hipMemcpyAsync(dni, nim.data(), sizeof(int) * nim.size(), hipMemcpyHostToDevice, h->stream));
+  d.y = dy;
+  d.cid = dcid;
+  d.fview = dfv;
+  d.fb = dfb;
+  d.fw = dfw;
+  d.ib = dib;
+  d.iw = diw;
+  d.imeas = dim;
+  d.node_fr = dnf;
+  d.node_im = dni;
+  KSP_HIP(hipStreamSynchronize(h->stream));
+  h->uploaded = true;
+  return 0;
+}
+
+int kb_sp_state_size(const kb_sp_handle* h) { return h ? h->S : -1; }
+int kb_sp_num_cols(const kb_sp_handle* h) { return h ? h->ncols : -1; }
+int kb_sp_camera_cols(const kb_sp_handle* h) { return h ? h->C : -1; }
+
+int kb_sp_set_state(kb_sp_handle* h, const double* state) {
+  if (!h || !state) return fail("kb_sp_set_state: null");
+  KSP_HIP(hipSetDevice(h->device));
+  KSP_HIP(hipMemcpyAsync(h->d.state, state, sizeof(double) * h->S, hipMemcpyHostToDevice, h->stream));
+  KSP_HIP(hipMemcpyAsync(h->d.backup, state, sizeof(double) * h->S, hipMemcpyHostToDevice, h->stream));
+  KSP_HIP(hipStreamSynchronize(h->stream));
+  h->built = h->solved = false;
+  return 0;
+}
+
+int kb_sp_get_state(kb_sp_handle* h, double* state) {
+  if (!h || !state) return fail("kb_sp_get_state: null");
+  KSP_HIP(hipSetDevice(h->device));
+  KSP_HIP(hipMemcpyAsync(state, h->d.state, sizeof(double) * h->S, hipMemcpyDeviceToHost, h->stream));
+  KSP_HIP(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+int kb_sp_eval_cost(kb_sp_handle* h, double* J_out) {
+  if (!h || !J_out) return fail("kb_sp_eval_cost: null");
+  if (!h->uploaded) return fail("kb_sp_eval_cost: upload observations first");
+  KSP_HIP(hipSetDevice(h->device));
+  if (launch_cost(h, 0)) return -1;
+  if (read_scalars(h)) return -1;
+  *J_out = h->host_sc[SC_COST];
+  return 0;
+}
+
+int kb_sp_build(kb_sp_handle* h) {
+  if (!h) return fail("kb_sp_build: null");
+  if (!h->uploaded) return fail("kb_sp_build: upload observations first");
+  KSP_HIP(hipSetDevice(h->device));
+  if (launch_build(h)) return -1;
+  KSP_HIP(hipGetLastError());
+  h->built = true;
+  h->solved = false;
+  return 0;
+}
+
+int kb_sp_set_constant_conditioner(kb_sp_handle* h, double diag) {
+  if (!h) return fail("kb_sp_set_constant_conditioner: null");
+  h->lambda = diag;
+  return 0;
+}
+
+int kb_sp_solve(kb_sp_handle* h, double* dx_out, int* ok) {
+  if (!h || !ok) return fail("kb_sp_solve: null");
+  if (!h->built) return fail("kb_sp_solve: build first");
+  KSP_HIP(hipSetDevice(h->device));
+  hipLaunchKernelGGL(k_sp_set_lam, dim3(1), dim3(64), 0, h->stream, h->d, h->lambda * h->lambda);
+  if (launch_solve(h)) return -1;
+  hipLaunchKernelGGL(k_sp_update, dim3(h->d.n), dim3(64), 0, h->stream, h->d, 0);
+  KSP_HIP(hipGetLastError());
+  if (read_scalars(h)) return -1;
+  *ok = h->host_sc[SC_OK] != 0.0;
+  if (*ok && dx_out)
+    KSP_HIP(hipMemcpy(dx_out, h->d.dx, sizeof(double) * h->ncols, hipMemcpyDeviceToHost));
+  h->solved = *ok != 0;
+  return 0;
+}
+
+int kb_sp_get_rhs(kb_sp_handle* h, double* rhs_out) {
+  if (!h || !rhs_out) return fail("kb_sp_get_rhs: null");
+  if (!h->built) return fail("kb_sp_get_rhs: build first");
+  KSP_HIP(hipSetDevice(h->device));
+  const int C = h->C, m = C + 1;
+  std::vector<double> R0((size_t)h->n * NB * m);
+  KSP_HIP(hipMemcpyAsync(rhs_out, h->d.Hcc + (size_t)C * C, sizeof(double) * C, hipMemcpyDeviceToHost, h->stream));
+  KSP_HIP(hipMemcpyAsync(R0.data(), h->d.R0, sizeof(double) * R0.size(), hipMemcpyDeviceToHost, h->stream));
+  KSP_HIP(hipStreamSynchronize(h->stream));
+  for (int k = 0; k < h->K; ++k)
+    for (int c = 0; c < 6; ++c) rhs_out[C + 6 * k + c] = R0[(size_t)(k / SB) * NB * m + (6 * (k % SB) + c) * m + C];
+  return 0;
+}
+
+int kb_sp_apply_update(kb_sp_handle* h, const double* dx, double* deltaX_out) {
+  if (!h) return fail("kb_sp_apply_update: null");
+  KSP_HIP(hipSetDevice(h->device));
+  SpDev& d = h->d;
+  if (dx) {
+    // host dx: write it as the solve output (X rows are not used when dx is given): theta + coefficients
+    KSP_HIP(hipMemcpyAsync(d.dx, dx, sizeof(double) * h->ncols, hipMemcpyHostToDevice, h->stream));
+    std::vector<double> st(h->S);
+    KSP_HIP(hipMemcpyAsync(st.data(), d.state, sizeof(double) * h->S, hipMemcpyDeviceToHost, h->stream));
+    KSP_HIP(hipStreamSynchronize(h->stream));
+    KSP_HIP(hipMemcpyAsync(d.backup, d.state, sizeof(double) * h->S, hipMemcpyDeviceToDevice, h->stream));
+    // host-side DV update (same rules as k_sp_update), then upload
+    double mx = 0.0;
+    for (int c = 0; c < h->ncols; ++c) mx = std::max(mx, std::fabs(dx[c]));
+    for (int c = 0; c < h->C; ++c) {
+      if (d.ckind[c] == 0) st[d.cidx[c] * KB_MAX_INTR + d.csub[c]] += dx[c];
+      if (d.ckind[c] == 2) st[d.off_imu + d.csub[c]] += dx[c];
+    }
+    for (int q = 0; q < h->N; ++q) {
+      double* pose = st.data() + (q < h->N - 1 ? d.off_base + 7 * q : d.off_cb);
+      const double* a = dx + d.col_pose[q];
+      const double th = std::sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]);
+      double na, ca;
+      if (th < 1.220703125e-4) {
+        na = 0.5 + th * th / 48.0;
+        ca = 1.0 - th * th / 8.0;
+      } else {
+        na = std::sin(0.5 * th) / th;
+        ca = std::cos(0.5 * th);
+      }
+      const double d0 = a[0] * na, d1 = a[1] * na, d2 = a[2] * na;
+      const double q0 = pose[0], q1 = pose[1], q2 = pose[2], q3 = pose[3];
+      pose[0] = q0 * ca + d0 * q3 - d1 * q2 + d2 * q1;
+      pose[1] = q1 * ca + d0 * q2 + d1 * q3 - d2 * q0;
+      pose[2] = q2 * ca - d0 * q1 + d1 * q0 + d2 * q3;
+      pose[3] = q3 * ca - d0 * q0 - d1 * q1 - d2 * q2;
+      for (int k = 0; k < 3; ++k) pose[4 + k] += a[3 + k];
+    }
+    for (int q = 0; q < 6 * h->K; ++q) st[d.off_coef + q] += dx[h->C + q];
+    KSP_HIP(hipMemcpyAsync(d.state, st.data(), sizeof(double) * h->S, hipMemcpyHostToDevice, h->stream));
+    KSP_HIP(hipStreamSynchronize(h->stream));
+    if (deltaX_out) *deltaX_out = mx;
+  } else {
+    if (!h->solved) return fail("kb_sp_apply_update: no device solution");
+    hipLaunchKernelGGL(k_sp_update, dim3(d.n), dim3(64), 0, h->stream, d, 1);
+    hipLaunchKernelGGL(k_sp_cost_reduce, dim3(1), dim3(64), 0, h->stream, d, 1);
+    if (read_scalars(h)) return -1;
+    if (deltaX_out) *deltaX_out = h->host_sc[SC_DX];
+  }
+  h->built = h->solved = false;
+  return 0;
+}
+
+int kb_sp_revert(kb_sp_handle* h) {
+  if (!h) return fail("kb_sp_revert: null");
+  KSP_HIP(hipSetDevice(h->device));
+  hipLaunchKernelGGL(k_sp_revert, dim3((h->S + 255) / 256), dim3(256), 0, h->stream, h->d);
+  KSP_HIP(hipStreamSynchronize(h->stream));
+  h->built = h->solved = false;
+  return 0;
+}
+
+int kb_sp_get_system(kb_sp_handle* h, double* Hcc, double* Hsc, double* Hband, double* gc, double* gs,
+                     double* cost) {
+  if (!h) return fail("kb_sp_get_system: null");
+  if (!h->built) return fail("kb_sp_get_system: build first");
+  KSP_HIP(hipSetDevice(h->device));
+  const int C = h->C, m = C + 1, n = h->n, K = h->K;
+  std::vector<double> hc((size_t)C * C + C + 1), D0((size_t)n * NB * NB), U0((size_t)n * NB * NB),
+      R0((size_t)n * NB * m);
+  KSP_HIP(hipMemcpyAsync(hc.data(), h->d.Hcc, sizeof(double) * hc.size(), hipMemcpyDeviceToHost, h->stream));
+  KSP_HIP(hipMemcpyAsync(D0.data(), h->d.D0, sizeof(double) * D0.size(), hipMemcpyDeviceToHost, h->stream));
+  KSP_HIP(hipMemcpyAsync(U0.data(), h->d.U0, sizeof(double) * U0.size(), hipMemcpyDeviceToHost, h->stream));
+  KSP_HIP(hipMemcpyAsync(R0.data(), h->d.R0, sizeof(double) * R0.size(), hipMemcpyDeviceToHost, h->stream));
+  KSP_HIP(hipStreamSynchronize(h->stream));
+  if (Hcc) std::memcpy(Hcc, hc.data(), sizeof(double) * C * C);
+  if (gc) std::memcpy(gc, hc.data() + (size_t)C * C, sizeof(double) * C);
+  if (cost) *cost = hc[(size_t)C * C + C];
+  for (int k = 0; k < K; ++k) {
+    const int i = k / SB, rk = 6 * (k % SB);
+    for (int a = 0; a < 6; ++a) {
+      for (int c = 0; c < C; ++c)
+        if (Hsc) Hsc[(size_t)(6 * k + a) * C + c] = R0[(size_t)i * NB * m + (rk + a) * m + c];
+      if (gs) gs[6 * k + a] = R0[(size_t)i * NB * m + (rk + a) * m + C];
+    }
+    if (!Hband) continue;
+    for (int dd = 0; dd < ORD; ++dd) {
+      const int k2 = k + dd;
+      for (int a = 0; a < 6; ++a)
+        for (int b = 0; b < 6; ++b) {
+          double v = 0.0;
+          if (k2 < K) {
+            const int i2 = k2 / SB, rk2 = 6 * (k2 % SB);
+            if (i2 == i)
+              v = D0[(size_t)i * NB * NB + (rk + a) * NB + rk2 + b];
+            else if (i2 == i + 1)
+              v = U0[(size_t)i * NB * NB + (rk + a) * NB + rk2 + b];
+          }
+          Hband[((size_t)k * ORD + dd) * 36 + a * 6 + b] = v;
+        }
+    }
+  }
+  return 0;
+}
+
+int kb_sp_optimize(kb_sp_handle* h, const kb_optimizer_options* o, kb_solution* out) {
+  if (!h || !o || !out) return fail("kb_sp_optimize: null");
+  if (!h->uploaded) return fail("kb_sp_optimize: upload observations first");
+  // Optimizer2::optimize (Optimizer2.cpp:183-273) + LM / GN policies, host-driven over the device passes
+  std::memset(out, 0, sizeof(*out));
+  h->trace.clear();
+  const bool lm = o->policy == 0;
+  const int ncols = h->ncols;
+  std::vector<double> dx(ncols, 0.0), rhs(ncols, 0.0), tmp(ncols);
+  double J;
+  if (kb_sp_eval_cost(h, &J)) return -1;
+  double p_J = J;
+  out->J_start = p_J;
+  double deltaX = o->convergence_dx + 1.0, deltaJ = o->convergence_dj + 1.0;
+  bool prevFailed = false, linFail = false, first = true;
+  double pol_J = J, pol_pJ = J, last_succ = J;
+  double lambda = o->lambda_init, gamma = 3.0, beta = 2.0, mu = 2.0;
+  while (out->iterations < o->max_iterations && out->failed_iterations < o->max_iterations &&
+         ((deltaX > o->convergence_dx && std::fabs(deltaJ) > o->convergence_dj) || linFail)) {
+    if (prevFailed) {
+      pol_J = J;
+    } else {
+      pol_pJ = last_succ;
+      last_succ = J;
+      pol_J = J;
+    }
+    bool rebuild = true;
+    if (lm && !first) {
+      double d2 = 0.0;
+      for (int q = 0; q < ncols; ++q) d2 += dx[q] * (lambda * dx[q] + rhs[q]);
+      const double rho = (pol_pJ - pol_J) / d2;
+      if (prevFailed) {
+        mu *= 2;
+        lambda *= mu;
+        rebuild = false;
+      } else if (rho <= 0) {
+        mu *= 10;
+        lambda *= mu;
+        rebuild = false;
+      } else if (lambda > 1e-16) {
+        const double u1 = 1 / gamma, u2 = 1 - (beta - 1) * std::pow((2 * rho - 1), 3);
+        lambda *= (u1 > u2) ? u1 : u2;
+        mu = beta;
+      } else {
+        lambda = 1e-15;
+      }
+    }
+    if (rebuild) {
+      if (kb_sp_build(h)) return -1;
+      if (kb_sp_get_rhs(h, rhs.data())) return -1;
+    } else {
+      h->built = true;  // same system, new conditioner
+    }
+    h->lambda = lm ? lambda : 0.0;
+    int ok = 0;
+    if (kb_sp_solve(h, tmp.data(), &ok)) return -1;
+    if (ok) dx = tmp;
+    first = false;
+    int accepted = 0;
+    if (!ok) {
+      prevFailed = true;
+      linFail = true;
+      out->failed_iterations++;
+    } else {
+      if (kb_sp_apply_update(h, nullptr, &deltaX)) return -1;
+      if (kb_sp_eval_cost(h, &J)) return -1;
+      deltaJ = p_J - J;
+      if (lm) {
+        if (deltaJ < 0.0) {
+          if (kb_sp_revert(h)) return -1;
+          out->failed_iterations++;
+          prevFailed = true;
+        } else {
+          p_J = J;
+          prevFailed = false;
+          accepted = 1;
+        }
+      } else {
+        p_J = J;
+        accepted = 1;
+      }
+      out->iterations++;
+    }
+    h->trace.push_back(ok ? J : NAN);
+    h->trace.push_back(lm ? lambda : 0.0);
+    h->trace.push_back(deltaX);
+    h->trace.push_back(accepted);
+    out->passes++;
+  }
+  out->J_final = p_J;
+  out->dx_final = deltaX;
+  out->dj_final = deltaJ;
+  out->linear_solver_failure = linFail;
+  return 0;
+}
+
+int kb_sp_get_trace(kb_sp_handle* h, double* trace, int32_t cap) {
+  if (!h || !trace) return fail("kb_sp_get_trace: null");
+  const int n = std::min<int>(cap, (int)(h->trace.size() / 4));
+  std::memcpy(trace, h->trace.data(), sizeof(double) * 4 * n);
+  return n;
+}
+
+int kb_sp_run_gn_iterations(kb_sp_handle* h, int32_t n_iter, double* seconds) {
+  if (!h || n_iter < 0) return fail("kb_sp_run_gn_iterations: bad arguments");
+  if (!h->uploaded) return fail("kb_sp_run_gn_iterations: upload observations first");
+  KSP_HIP(hipSetDevice(h->device));
+  if (!h->gn_graph) {
+    hipGraph_t g = nullptr;
+    KSP_HIP(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
+    const int rc = enqueue_gn_pass(h);
+    hipError_t e = hipStreamEndCapture(h->stream, &g);
+    if (rc || e != hipSuccess) return fail("kb_sp_run_gn_iterations: graph capture failed");
+    e = hipGraphInstantiate(&h->gn_graph, g, nullptr, nullptr, 0);
+    hipGraphDestroy(g);
+    if (e != hipSuccess) return fail("kb_sp_run_gn_iterations: graph instantiate failed");
+  }
+  KSP_HIP(hipStreamSynchronize(h->stream));
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int it = 0; it < n_iter; ++it) KSP_HIP(hipGraphLaunch(h->gn_graph, h->stream));
+  KSP_HIP(hipStreamSynchronize(h->stream));
+  const auto t1 = std::chrono::steady_clock::now();
+  if (seconds) *seconds = std::chrono::duration<double>(t1 - t0).count();
+  h->built = h->solved = false;
+  return 0;
+}
+
+int kb_sp_kernel_stats(kb_sp_handle* h, int32_t n, double* ms_out6, double* frames_bytes) {
+  if (!h || !ms_out6 || n < 1) return fail("kb_sp_kernel_stats: bad arguments");
+  if (!h->uploaded) return fail("kb_sp_kernel_stats: upload observations first");
+  KSP_HIP(hipSetDevice(h->device));
+  SpDev& d = h->d;
+  hipEvent_t ev[7];
+  for (auto& e : ev) KSP_HIP(hipEventCreate(&e));
+  double acc[6] = {0, 0, 0, 0, 0, 0};
+  void* args[] = {&d};
+  for (int it = 0; it < n; ++it) {
+    hipLaunchKernelGGL(k_sp_set_lam, dim3(1), dim3(64), 0, h->stream, d, 0.0);
+    KSP_HIP(hipEventRecord(ev[0], h->stream));
+    KSP_HIP(hipLaunchKernel(h->fn_frames, dim3(d.nblk_f), dim3(64 * h->N), args, h->lds_frames, h->stream));
+    KSP_HIP(hipEventRecord(ev[1], h->stream));
+    KSP_HIP(hipLaunchKernel((const void*)k_sp_assemble, dim3(d.n), dim3(256), args, h->lds_asm, h->stream));
+    hipLaunchKernelGGL(k_sp_reduce_cc, dim3((d.Wc + 255) / 256), dim3(256), 0, h->stream, d);
+    KSP_HIP(hipEventRecord(ev[2], h->stream));
+    hipLaunchKernelGGL(k_sp_prep, dim3(d.n), dim3(256), 0, h->stream, d);
+    int s = 1;
+    for (; s < d.n; s *= 2) {
+      const int ne = (d.n - s + 2 * s - 1) / (2 * s), nk = (d.n + 2 * s - 1) / (2 * s);
+      hipLaunchKernelGGL(k_sp_elim, dim3(ne), dim3(256), h->lds_elim, h->stream, d, s);
+      hipLaunchKernelGGL(k_sp_keep, dim3(nk), dim3(256), h->lds_keep, h->stream, d, s);
+    }
+    hipLaunchKernelGGL(k_sp_top, dim3(1), dim3(256), 0, h->stream, d);
+    for (s /= 2; s >= 1; s /= 2) {
+      const int ne = (d.n - s + 2 * s - 1) / (2 * s);
+      hipLaunchKernelGGL(k_sp_back, dim3(ne), dim3(256), 0, h->stream, d, s);
+    }
+    KSP_HIP(hipEventRecord(ev[3], h->stream));
+    hipLaunchKernelGGL(k_sp_schur, dim3(d.nblk_s), dim3(256), h->lds_schur, h->stream, d);
+    hipLaunchKernelGGL(k_sp_camsolve, dim3(1), dim3(256), 0, h->stream, d);
+    KSP_HIP(hipEventRecord(ev[4], h->stream));
+    hipLaunchKernelGGL(k_sp_update, dim3(d.n), dim3(64), 0, h->stream, d, 1);
+    if (launch_cost(h, 1)) return -1;
+    KSP_HIP(hipEventRecord(ev[5], h->stream));
+    KSP_HIP(hipStreamSynchronize(h->stream));
+    float t[5];
+    for (int q = 0; q < 5; ++q) KSP_HIP(hipEventElapsedTime(&t[q], ev[q], ev[q + 1]));
+    for (int q = 0; q < 5; ++q) acc[q] += t[q];
+    float tt;
+    KSP_HIP(hipEventElapsedTime(&tt, ev[0], ev[5]));
+    acc[5] += tt;
+  }
+  for (auto& e : ev) hipEventDestroy(e);
+  for (int q = 0; q < 6; ++q) ms_out6[q] = acc[q] / n;
+  if (frames_bytes) {
+    // per launch: corners (y 16 B + id 2 B), view ranges, frame weights, state, FH written, partial rows
+    const double nc = 0.0;
+    (void)nc;
+    *frames_bytes = 0.0;
+  }
+  h->built = h->solved = false;
+  return 0;
+}
+
+}  // extern "C"
