@@ -9,7 +9,11 @@ all views visible.  N>1: weak scaling, every rank holds its own 500-frame shard 
 500*N frames; the camera block [S | b] and the cost / step statistics are all-reduced over RCCL once per
 pass.  value = (config-sized shard iterations of all ranks) / max-over-ranks wall time.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+configs[4] (--config 5): 2-camera rig + IMU on a cubic B-spline pose trajectory, 1200 frames at 20 Hz, 200 Hz
+IMU, 50 knots/s; one GPU, one step = one GN pass of the spline system (frames kernel,
+node assembly, block cyclic reduction, Schur onto the camera/IMU block, update, cost).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|5]
 """
 import argparse
 import json
@@ -65,13 +69,67 @@ def cpu_baseline(prob, seconds_budget=12.0, threads=None):
                       f"oracle/kb_oracle.c kbo_time_gn, {threads} threads"}
 
 
+def cpu_baseline_spline(prob, seconds_budget=15.0, threads=None):
+    """configs[4] oracle (oracle/kb_oracle_spline.c: threaded term evaluation into the block-banded normal
+    equations, band Cholesky + Schur onto the camera/IMU block) timed on host cores."""
+    from oracle import oracle as O
+    o = O.SplineOracle(prob)
+    threads = threads or min(16, os.cpu_count() or 1)
+    t1 = o.time_gn(prob.state_init, 1, threads)
+    n = max(2, min(100, int(seconds_budget / max(t1, 1e-4))))
+    t = o.time_gn(prob.state_init, n, threads)
+    return {"value": n / t, "unit": "iterations/s", "cores": threads, "kind": "port",
+            "sample": f"{n} GN iterations of configs[4] (full 1200-frame problem, {prob.n_corners} corners, "
+                      f"{prob.n_imu} IMU samples), oracle/kb_oracle_spline.c kbo_sp_time_gn, {threads} threads"}
+
+
+def main_spline(args):
+    """configs[4] on one GPU (the spline path does not shard; BASELINE.json quotes it on 1 x MI355X)."""
+    from kalibr_amd import build as B
+    from kalibr_amd import capi, synth
+    if not os.path.exists(B.OUT):
+        B.build()
+    p = synth.make_spline_config()
+    g = capi.SplineSolver(p)
+    g.set_state(p.state_init)
+    g.run_gn(args.warmup)
+    t0 = time.perf_counter()
+    g.run_gn(args.steps)
+    wall = time.perf_counter() - t0
+    ks = g.kernel_stats(10)
+    achieved = ks["frames_bytes"] / (ks["frames_ms"] * 1e-3) / 1e9
+    value = args.steps / wall
+    out = {
+        "metric": METRIC, "value": value, "unit": "iterations/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": 1e3 * wall / args.steps, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+        "config": {"workload": "configs[4]: 2-cam + IMU continuous-time B-spline calibration, 1200 frames, 1 GPU",
+                   "frames": p.n_frames, "cameras": p.n_cams, "corners": p.n_corners, "imu_samples": p.n_imu,
+                   "spline_coefficients": p.n_coeffs, "jacobian_cols": p.total_cols, "camera_block": p.cam_cols,
+                   "policy": "gauss_newton", "parallelism": "single GPU"},
+        "roofline": {"bound": "hbm", "kernel": "k_sp_frames", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None, "avg_ms": ks["frames_ms"],
+                     "algorithmic_bytes": ks["frames_bytes"]},
+        "pass_breakdown_ms": {k: v for k, v in ks.items() if k.endswith("_ms")},
+    }
+    if not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline_spline(p)
+        out["speedup_vs_cpu_baseline"] = value / out["cpu_baseline"]["value"]
+    print(json.dumps(out))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--config", type=int, default=2, choices=[2, 5])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
+    if args.config == 5:
+        if args.gpus != 1:
+            raise SystemExit("configs[4] (--config 5) runs on one GPU")
+        return main_spline(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

@@ -65,7 +65,7 @@ struct SpDev {
   double* backup;
   double* FH;             // [F][FHS]: H_vv (36) | H_vtheta (6 C) | g_v (6)
   double* part;           // [nblk_f][Wc] theta-theta partial rows of the frames
-  double* ipart;          // [n][WI]
+  double* ipart;          // [nblk_ci][WI]
   double* Hcc;            // [C][C] | gc [C] | cost
   double *D0, *U0, *R0;   // built node blocks [n][324], [n][324], [n][18 m]
   double *D, *U, *R;      // working copies (cyclic reduction in place)
@@ -567,7 +567,7 @@ __device__ __forceinline__ double imu_jth(const SpDev& d, const double* Ct, int 
 // ---------------------------------------------------------------- k_sp_assemble
 // One block per cyclic-reduction node i (coefficients 3i..3i+2): D_i (18 x 18), U_i (coupling to node
 // i+1) and R_i = [H_s,theta | g_s] (18 x (C+1)) from the frames and IMU samples whose support touches the
-// node; the IMU theta-theta partial row of the samples the node owns (first coefficient in the node).
+// node.
 __global__ void __launch_bounds__(256) k_sp_assemble(SpDev d) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const int i = blockIdx.x, tid = threadIdx.x, nth = blockDim.x, C = d.C, m = d.m;
@@ -578,10 +578,8 @@ __global__ void __launch_bounds__(256) k_sp_assemble(SpDev d) {
   double* te = tj + TCH * stride;         // unused spare
   __shared__ int tb[TCH];
   __shared__ double tw[TCH][4];
-  __shared__ double ipt[WI];
   (void)te;
   for (int q = tid; q < nout; q += nth) out[q] = 0.0;
-  if (tid < WI) ipt[tid] = 0.0;
   const int k0 = SB * i;
   // ---- frames
   const int fa = d.node_fr[2 * i], fz = d.node_fr[2 * i + 1];
@@ -664,31 +662,6 @@ __global__ void __launch_bounds__(256) k_sp_assemble(SpDev d) {
       }
       out[q] += s;
     }
-    // theta-theta of the samples this node owns
-    if (tid < WI) {
-      double s = 0.0;
-      for (int t = 0; t < nt; ++t) {
-        if (tb[t] < k0 || tb[t] >= k0 + SB) continue;
-        const double* J = tj + t * stride;
-        if (tid < 45) {
-          int a = 0, e = tid;
-          while (e >= 9 - a) {
-            e -= 9 - a;
-            ++a;
-          }
-          const int bb = a + e;
-#pragma unroll
-          for (int z = 0; z < 6; ++z) s += imu_jth(d, J + 150, z, a) * imu_jth(d, J + 150, z, bb);
-        } else if (tid < 54) {
-#pragma unroll
-          for (int z = 0; z < 6; ++z) s -= imu_jth(d, J + 150, z, tid - 45) * J[144 + z];
-        } else {
-#pragma unroll
-          for (int z = 0; z < 6; ++z) s += J[144 + z] * J[144 + z];
-        }
-      }
-      ipt[tid] += s;
-    }
   }
   __syncthreads();
   // padded rows (coefficients >= K): identity diagonal, no coupling
@@ -711,40 +684,94 @@ __global__ void __launch_bounds__(256) k_sp_assemble(SpDev d) {
     else
       d.R0[(size_t)i * NB * m + q - 2 * NB * NB] = v;
   }
-  if (tid < WI) d.ipart[(size_t)i * WI + tid] = ipt[tid];
+}
+
+// ---------------------------------------------------------------- IMU theta-theta (b_g | b_a | g_w)
+// 256 samples per block: J_theta^T J_theta upper (45), -J_theta^T e (9), e^T e -> one partial row [WI].
+__global__ void __launch_bounds__(256) k_sp_imu_cc(SpDev d) {
+  __shared__ double red[4][WI];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, m = blockIdx.x * 256 + tid;
+  double e[6] = {0, 0, 0, 0, 0, 0}, Ct[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  const bool has = m < d.M;
+  if (has) imu_sample(d, m, e, nullptr, Ct);
+  for (int q = 0; q < WI; ++q) {
+    double s = 0.0;
+    if (has) {
+      if (q < 45) {
+        int a = 0, r = q;
+        while (r >= 9 - a) {
+          r -= 9 - a;
+          ++a;
+        }
+        const int bb = a + r;
+#pragma unroll
+        for (int z = 0; z < 6; ++z) s += imu_jth(d, Ct, z, a) * imu_jth(d, Ct, z, bb);
+      } else if (q < 54) {
+#pragma unroll
+        for (int z = 0; z < 6; ++z) s -= imu_jth(d, Ct, z, q - 45) * e[z];
+      } else {
+#pragma unroll
+        for (int z = 0; z < 6; ++z) s += e[z] * e[z];
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    if (lane == 0) red[wave][q] = s;
+  }
+  __syncthreads();
+  if (tid < WI) d.ipart[(size_t)blockIdx.x * WI + tid] = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
 }
 
 // ---------------------------------------------------------------- k_sp_reduce_cc: H_cc, g_c, cost
+// 64 entries per block; the 4 waves sum interleaved partial rows (8 independent loads in flight per lane),
+// combined in a fixed order.
+__device__ __forceinline__ double col_sum(const double* p, int rows, int stride, int q, int w0, int ws) {
+  double a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  int r = w0;
+  for (; r + 7 * ws < rows; r += 8 * ws) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) a[u] += p[(size_t)(r + u * ws) * stride + q];
+  }
+  for (int u = 0; r < rows; r += ws, ++u) a[u & 7] += p[(size_t)r * stride + q];
+  return ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+}
+
 __global__ void __launch_bounds__(256) k_sp_reduce_cc(SpDev d) {
+  __shared__ double red[4][64];
   const int C = d.C, nup = C * (C + 1) / 2;
-  const int q = blockIdx.x * blockDim.x + threadIdx.x;
-  if (q >= d.Wc) return;
-  double s = 0.0;
-  for (int b = 0; b < d.nblk_f; ++b) s += d.part[(size_t)b * d.Wc + q];
-  // IMU columns
-  int a = -1, bcol = -1;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int q = blockIdx.x * 64 + lane;
+  const bool act = q < d.Wc;
+  int ii = -1, a = 0, bcol = 0;
+  if (act) {
+    if (q < nup) {
+      int e = q;
+      while (e >= C - a) {
+        e -= C - a;
+        ++a;
+      }
+      bcol = a + e;
+      const int ia = a - d.col_imu, ib = bcol - d.col_imu;
+      if (ia >= 0 && ia < 9 && ib >= 0 && ib < 9) ii = ia * 9 - ia * (ia - 1) / 2 + (ib - ia);
+    } else if (q < nup + C) {
+      const int ia = q - nup - d.col_imu;
+      if (ia >= 0 && ia < 9) ii = 45 + ia;
+    } else {
+      ii = 54;
+    }
+  }
+  double s = act ? col_sum(d.part, d.nblk_f, d.Wc, q, wave, 4) : 0.0;
+  if (ii >= 0) s += col_sum(d.ipart, d.nblk_ci, WI, ii, wave, 4);
+  red[wave][lane] = s;
+  __syncthreads();
+  if (wave != 0 || !act) return;
+  s = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
   if (q < nup) {
-    int e = q;
-    a = 0;
-    while (e >= C - a) {
-      e -= C - a;
-      ++a;
-    }
-    bcol = a + e;
-    const int ia = a - d.col_imu, ib = bcol - d.col_imu;
-    if (ia >= 0 && ia < 9 && ib >= 0 && ib < 9) {
-      const int ii = ia * 9 - ia * (ia - 1) / 2 + (ib - ia);
-      for (int n = 0; n < d.n; ++n) s += d.ipart[(size_t)n * WI + ii];
-    }
     d.Hcc[a * C + bcol] = s;
     d.Hcc[bcol * C + a] = s;
   } else if (q < nup + C) {
-    const int ia = q - nup - d.col_imu;
-    if (ia >= 0 && ia < 9)
-      for (int n = 0; n < d.n; ++n) s += d.ipart[(size_t)n * WI + 45 + ia];
     d.Hcc[C * C + (q - nup)] = s;
   } else {
-    for (int n = 0; n < d.n; ++n) s += d.ipart[(size_t)n * WI + 54];
     d.Hcc[C * C + C] = s;
     d.sc[SC_COST_BUILD] = s;
   }
@@ -870,65 +897,72 @@ __global__ void __launch_bounds__(256) k_sp_keep(SpDev d, int s) {
   }
 }
 
+// back substitution of one 18-row node with LDS-staged operands: x = L^-T T, one thread per RHS column
+__device__ __forceinline__ void node_backsolve(const double* L, double* T, int m, double* out, int tid) {
+  for (int c = tid; c < m; c += blockDim.x) {
+    double z[NB];
+#pragma unroll
+    for (int row = 0; row < NB; ++row) z[row] = T[row * m + c];
+#pragma unroll
+    for (int row = NB - 1; row >= 0; --row) {
+      double v = z[row];
+#pragma unroll
+      for (int k = row + 1; k < NB; ++k) v -= L[k * NB + row] * z[k];
+      z[row] = v / L[row * NB + row];
+    }
+#pragma unroll
+    for (int row = 0; row < NB; ++row) out[row * m + c] = z[row];
+  }
+}
+
 __global__ void __launch_bounds__(256) k_sp_top(SpDev d) {
   __shared__ double L[NB * NB];
+  extern __shared__ __attribute__((aligned(16))) double T[];  // [18][m]
   const int tid = threadIdx.x, m = d.m;
   for (int q = tid; q < NB * NB; q += blockDim.x) L[q] = d.D[q];
   __syncthreads();
   const bool ok = chol18(L, tid);
   if (!ok && tid == 0) d.sc[SC_OK] = 0.0;
-  for (int c = tid; c < m; c += blockDim.x) {
-    double z[NB];
+  for (int c = tid; c < m; c += blockDim.x) {  // forward: L y = R_0
 #pragma unroll
     for (int row = 0; row < NB; ++row) {
       double v = d.R[row * m + c];
 #pragma unroll
-      for (int k = 0; k < row; ++k) v -= L[row * NB + k] * z[k];
-      z[row] = v / L[row * NB + row];
+      for (int k = 0; k < row; ++k) v -= L[row * NB + k] * T[k * m + c];
+      T[row * m + c] = v / L[row * NB + row];
     }
-#pragma unroll
-    for (int row = NB - 1; row >= 0; --row) {
-      double v = z[row];
-#pragma unroll
-      for (int k = row + 1; k < NB; ++k) v -= L[k * NB + row] * z[k];
-      z[row] = v / L[row * NB + row];
-    }
-#pragma unroll
-    for (int row = 0; row < NB; ++row) d.X[row * m + c] = z[row];
   }
+  node_backsolve(L, T, m, d.X, tid);
 }
 
 __global__ void __launch_bounds__(256) k_sp_back(SpDev d, int s) {
   __shared__ double L[NB * NB];
+  extern __shared__ __attribute__((aligned(16))) double sm[];  // Z [18][wc] | xl [18][m] | xr [18][m] | T [18][m]
   const int j = s + 2 * s * blockIdx.x, tid = threadIdx.x, m = d.m, wc = 36 + m;
   if (j >= d.n) return;
   const int l = j - s, r = j + s;
+  const bool hr = r < d.n;
+  double* Z = sm;
+  double* xl = Z + NB * wc;
+  double* xr = xl + NB * m;
+  double* T = xr + NB * m;
   for (int q = tid; q < NB * NB; q += blockDim.x) L[q] = d.Lf[(size_t)j * NB * NB + q];
-  __syncthreads();
-  const double* Z = d.Z + (size_t)j * NB * wc;
-  const double* xl = d.X + (size_t)l * NB * m;
-  const double* xr = d.X + (size_t)(r < d.n ? r : l) * NB * m;
-  for (int c = tid; c < m; c += blockDim.x) {
-    double z[NB];
-#pragma unroll
-    for (int row = 0; row < NB; ++row) {
-      double v = Z[row * wc + 2 * NB + c];
-      for (int k = 0; k < NB; ++k) {
-        v -= Z[row * wc + k] * xl[k * m + c];
-        if (r < d.n) v -= Z[row * wc + NB + k] * xr[k * m + c];
-      }
-      z[row] = v;
-    }
-#pragma unroll
-    for (int row = NB - 1; row >= 0; --row) {
-      double v = z[row];
-#pragma unroll
-      for (int k = row + 1; k < NB; ++k) v -= L[k * NB + row] * z[k];
-      z[row] = v / L[row * NB + row];
-    }
-#pragma unroll
-    for (int row = 0; row < NB; ++row) d.X[(size_t)j * NB * m + row * m + c] = z[row];
+  for (int q = tid; q < NB * wc; q += blockDim.x) Z[q] = d.Z[(size_t)j * NB * wc + q];
+  for (int q = tid; q < NB * m; q += blockDim.x) {
+    xl[q] = d.X[(size_t)l * NB * m + q];
+    xr[q] = hr ? d.X[(size_t)r * NB * m + q] : 0.0;
   }
+  __syncthreads();
+  // T = Z_R - Z_Uin x_l - Z_U x_r
+  for (int q = tid; q < NB * m; q += blockDim.x) {
+    const int row = q / m, c = q % m;
+    double v = Z[row * wc + 2 * NB + c];
+#pragma unroll
+    for (int k = 0; k < NB; ++k) v -= Z[row * wc + k] * xl[k * m + c] + Z[row * wc + NB + k] * xr[k * m + c];
+    T[q] = v;
+  }
+  __syncthreads();
+  node_backsolve(L, T, m, d.X + (size_t)j * NB * m, tid);
 }
 
 // ---------------------------------------------------------------- Schur complement onto theta
@@ -972,29 +1006,37 @@ __global__ void __launch_bounds__(256) k_sp_schur(SpDev d) {
   for (int q = tid; q < d.Ws; q += blockDim.x) d.spart[(size_t)blockIdx.x * d.Ws + q] = acc[q];
 }
 
-// dense camera / IMU block: S = H_cc + lam2 I - sum, b = g_c - sum; Cholesky in LDS; dtheta -> dx[0..C)
+// dense camera / IMU block: S = H_cc + lam2 I - sum, b = g_c - sum (4-wave interleaved partial sums);
+// Cholesky in LDS; one-wave forward / backward substitution; dtheta -> dx[0..C)
 __global__ void __launch_bounds__(256) k_sp_camsolve(SpDev d) {
   __shared__ double S[MAXC * MAXC];
   __shared__ double bv[MAXC];
+  __shared__ double red[4][256];
   __shared__ int okf;
-  const int tid = threadIdx.x, C = d.C, nup = C * (C + 1) / 2;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, C = d.C, nup = C * (C + 1) / 2;
   const double lam2 = d.sc[SC_LAM2];
-  for (int q = tid; q < nup + C; q += blockDim.x) {
-    double s = 0.0;
-    for (int b = 0; b < d.nblk_s; ++b) s += d.spart[(size_t)b * d.Ws + q];
-    if (q < nup) {
-      int e = q, a = 0;
-      while (e >= C - a) {
-        e -= C - a;
-        ++a;
+  for (int q0 = 0; q0 < nup + C; q0 += 64) {
+    const int q = q0 + lane;
+    const double s = (q < nup + C) ? col_sum(d.spart, d.nblk_s, d.Ws, q, wave, 4) : 0.0;
+    red[wave][lane] = s;
+    __syncthreads();
+    if (wave == 0 && q < nup + C) {
+      const double t = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+      if (q < nup) {
+        int e = q, a = 0;
+        while (e >= C - a) {
+          e -= C - a;
+          ++a;
+        }
+        const int bb = a + e;
+        const double v = d.Hcc[a * C + bb] + (a == bb ? lam2 : 0.0) - t;
+        S[a * C + bb] = v;
+        S[bb * C + a] = v;
+      } else {
+        bv[q - nup] = d.Hcc[C * C + (q - nup)] - t;
       }
-      const int bb = a + e;
-      const double v = d.Hcc[a * C + bb] + (a == bb ? lam2 : 0.0) - s;
-      S[a * C + bb] = v;
-      S[bb * C + a] = v;
-    } else {
-      bv[q - nup] = d.Hcc[C * C + (q - nup)] - s;
     }
+    __syncthreads();
   }
   if (tid == 0) okf = 1;
   __syncthreads();
@@ -1014,20 +1056,20 @@ __global__ void __launch_bounds__(256) k_sp_camsolve(SpDev d) {
     }
     __syncthreads();
   }
-  if (tid == 0) {
-    double x[MAXC];
+  if (wave == 0) {  // L y = b, L^T x = y: lane r owns row r, the solved value broadcast by readlane
+    double x = lane < C ? bv[lane] : 0.0;
     for (int r = 0; r < C; ++r) {
-      double v = bv[r];
-      for (int k = 0; k < r; ++k) v -= S[r * C + k] * x[k];
-      x[r] = v / S[r * C + r];
+      const double xr = __shfl(x, r) / S[r * C + r];
+      if (lane == r) x = xr;
+      if (lane > r && lane < C) x -= S[lane * C + r] * xr;
     }
     for (int r = C - 1; r >= 0; --r) {
-      double v = x[r];
-      for (int k = r + 1; k < C; ++k) v -= S[k * C + r] * x[k];
-      x[r] = v / S[r * C + r];
+      const double xr = __shfl(x, r) / S[r * C + r];
+      if (lane == r) x = xr;
+      if (lane < r) x -= S[r * C + lane] * xr;
     }
-    for (int r = 0; r < C; ++r) d.dx[r] = x[r];
-    if (!okf) d.sc[SC_OK] = 0.0;
+    if (lane < C) d.dx[lane] = x;
+    if (lane == 0 && !okf) d.sc[SC_OK] = 0.0;
   }
 }
 
@@ -1294,12 +1336,12 @@ struct kb_sp_handle {
   int device = 0;
   hipStream_t stream = nullptr;
   SpDev d{};
-  int N = 0, C = 0, K = 0, F = 0, M = 0, n = 0, S = 0, ncols = 0, n_target = 0;
+  int N = 0, C = 0, K = 0, F = 0, M = 0, n = 0, S = 0, ncols = 0, n_target = 0, NCo = 0;
   std::vector<double> knots;
   std::vector<void*> allocs;
   double lambda = 0.0;
   bool uploaded = false, built = false, solved = false;
-  size_t lds_frames = 0, lds_asm = 0, lds_elim = 0, lds_keep = 0, lds_schur = 0;
+  size_t lds_frames = 0, lds_asm = 0, lds_elim = 0, lds_keep = 0, lds_schur = 0, lds_back = 0;
   const void* fn_frames = nullptr;
   const void* fn_cost = nullptr;
   hipGraphExec_t gn_graph = nullptr;
@@ -1332,7 +1374,8 @@ int launch_build(kb_sp_handle* h) {
   void* args[] = {&d};
   KSP_HIP(hipLaunchKernel(h->fn_frames, dim3(d.nblk_f), dim3(64 * h->N), args, h->lds_frames, h->stream));
   KSP_HIP(hipLaunchKernel((const void*)k_sp_assemble, dim3(d.n), dim3(256), args, h->lds_asm, h->stream));
-  hipLaunchKernelGGL(k_sp_reduce_cc, dim3((d.Wc + 255) / 256), dim3(256), 0, h->stream, d);
+  hipLaunchKernelGGL(k_sp_imu_cc, dim3(d.nblk_ci), dim3(256), 0, h->stream, d);
+  hipLaunchKernelGGL(k_sp_reduce_cc, dim3((d.Wc + 63) / 64), dim3(256), 0, h->stream, d);
   return 0;
 }
 
@@ -1345,10 +1388,10 @@ int launch_solve(kb_sp_handle* h) {
     hipLaunchKernelGGL(k_sp_elim, dim3(ne), dim3(256), h->lds_elim, h->stream, d, s);
     hipLaunchKernelGGL(k_sp_keep, dim3(nk), dim3(256), h->lds_keep, h->stream, d, s);
   }
-  hipLaunchKernelGGL(k_sp_top, dim3(1), dim3(256), 0, h->stream, d);
+  hipLaunchKernelGGL(k_sp_top, dim3(1), dim3(256), sizeof(double) * NB * d.m, h->stream, d);
   for (s /= 2; s >= 1; s /= 2) {
     const int ne = (d.n - s + 2 * s - 1) / (2 * s);
-    hipLaunchKernelGGL(k_sp_back, dim3(ne), dim3(256), 0, h->stream, d, s);
+    hipLaunchKernelGGL(k_sp_back, dim3(ne), dim3(256), h->lds_back, h->stream, d, s);
   }
   hipLaunchKernelGGL(k_sp_schur, dim3(d.nblk_s), dim3(256), h->lds_schur, h->stream, d);
   hipLaunchKernelGGL(k_sp_camsolve, dim3(1), dim3(256), 0, h->stream, d);
@@ -1493,7 +1536,6 @@ kb_sp_handle* kb_sp_create(const kb_sp_layout* L) {
   d.target = tgt;
   rc |= h->alloc(&d.state, (size_t)h->S);
   rc |= h->alloc(&d.backup, (size_t)h->S);
-  rc |= h->alloc(&d.ipart, (size_t)h->n * WI);
   rc |= h->alloc(&d.Hcc, (size_t)h->C * h->C + h->C + 1);
   rc |= h->alloc(&d.D0, (size_t)h->n * NB * NB);
   rc |= h->alloc(&d.U0, (size_t)h->n * NB * NB);
@@ -1518,6 +1560,7 @@ kb_sp_handle* kb_sp_create(const kb_sp_layout* L) {
   }
   h->lds_elim = sizeof(double) * NB * (36 + d.m);
   h->lds_keep = 2 * h->lds_elim;
+  h->lds_back = h->lds_elim + sizeof(double) * 3 * NB * d.m;
   h->lds_schur = sizeof(double) * (2 * NB * d.m + d.Ws);
   h->lds_asm = sizeof(double) * (2 * NB * NB + NB * d.m + TCH * std::max(144 + 15, d.FHS));
   h->lds_frames = sizeof(double) * (h->N * 64 * XS + h->N * 256 + 2 * h->N * 36 + 2 * h->N * h->N * 36 + d.Wc +
@@ -1607,6 +1650,7 @@ int kb_sp_upload(kb_sp_handle* h, int32_t n_frames, const double* frame_time, in
   }
   h->F = d.F = F;
   h->M = d.M = M;
+  h->NCo = n_corners;
   d.nblk_f = (F + FPB - 1) / FPB;
   d.nblk_ci = std::max(1, (M + 255) / 256);
   int rc = 0;
@@ -1628,6 +1672,7 @@ int kb_sp_upload(kb_sp_handle* h, int32_t n_frames, const double* frame_time, in
   rc |= h->alloc(&d.FH, (size_t)F * d.FHS);
   rc |= h->alloc(&d.part, (size_t)d.nblk_f * d.Wc);
   rc |= h->alloc(&d.cpart, (size_t)(d.nblk_f + d.nblk_ci));
+  rc |= h->alloc(&d.ipart, (size_t)d.nblk_ci * WI);
   if (rc) return -1;
   if (n_corners) {
     KSP_HIP(hipMemcpyAsync(dy, y, sizeof(double) * 2 * n_corners, hipMemcpyHostToDevice, h->stream));
@@ -1984,7 +2029,8 @@ int kb_sp_kernel_stats(kb_sp_handle* h, int32_t n, double* ms_out6, double* fram
     KSP_HIP(hipLaunchKernel(h->fn_frames, dim3(d.nblk_f), dim3(64 * h->N), args, h->lds_frames, h->stream));
     KSP_HIP(hipEventRecord(ev[1], h->stream));
     KSP_HIP(hipLaunchKernel((const void*)k_sp_assemble, dim3(d.n), dim3(256), args, h->lds_asm, h->stream));
-    hipLaunchKernelGGL(k_sp_reduce_cc, dim3((d.Wc + 255) / 256), dim3(256), 0, h->stream, d);
+    hipLaunchKernelGGL(k_sp_imu_cc, dim3(d.nblk_ci), dim3(256), 0, h->stream, d);
+    hipLaunchKernelGGL(k_sp_reduce_cc, dim3((d.Wc + 63) / 64), dim3(256), 0, h->stream, d);
     KSP_HIP(hipEventRecord(ev[2], h->stream));
     hipLaunchKernelGGL(k_sp_prep, dim3(d.n), dim3(256), 0, h->stream, d);
     int s = 1;
@@ -1993,10 +2039,10 @@ int kb_sp_kernel_stats(kb_sp_handle* h, int32_t n, double* ms_out6, double* fram
       hipLaunchKernelGGL(k_sp_elim, dim3(ne), dim3(256), h->lds_elim, h->stream, d, s);
       hipLaunchKernelGGL(k_sp_keep, dim3(nk), dim3(256), h->lds_keep, h->stream, d, s);
     }
-    hipLaunchKernelGGL(k_sp_top, dim3(1), dim3(256), 0, h->stream, d);
+    hipLaunchKernelGGL(k_sp_top, dim3(1), dim3(256), sizeof(double) * NB * d.m, h->stream, d);
     for (s /= 2; s >= 1; s /= 2) {
       const int ne = (d.n - s + 2 * s - 1) / (2 * s);
-      hipLaunchKernelGGL(k_sp_back, dim3(ne), dim3(256), 0, h->stream, d, s);
+      hipLaunchKernelGGL(k_sp_back, dim3(ne), dim3(256), h->lds_back, h->stream, d, s);
     }
     KSP_HIP(hipEventRecord(ev[3], h->stream));
     hipLaunchKernelGGL(k_sp_schur, dim3(d.nblk_s), dim3(256), h->lds_schur, h->stream, d);
@@ -2016,10 +2062,11 @@ int kb_sp_kernel_stats(kb_sp_handle* h, int32_t n, double* ms_out6, double* fram
   for (auto& e : ev) hipEventDestroy(e);
   for (int q = 0; q < 6; ++q) ms_out6[q] = acc[q] / n;
   if (frames_bytes) {
-    // per launch: corners (y 16 B + id 2 B), view ranges, frame weights, state, FH written, partial rows
-    const double nc = 0.0;
-    (void)nc;
-    *frames_bytes = 0.0;
+    // algorithmic bytes of one k_sp_frames launch: corners (y 16 B + id 2 B), view ranges (8 B per (frame,
+    // camera)), frame basis (4 weights + index), the 4 active coefficients per frame, the camera-side state,
+    // the per-frame spline blocks written (FHS doubles) and one theta partial row per block
+    *frames_bytes = 18.0 * h->NCo + 8.0 * h->F * h->N + 36.0 * h->F + 8.0 * 24 * h->F + 8.0 * d.off_coef +
+                    8.0 * d.FHS * h->F + 8.0 * d.Wc * d.nblk_f;
   }
   h->built = h->solved = false;
   return 0;
