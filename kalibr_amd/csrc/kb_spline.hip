@@ -48,7 +48,7 @@ struct SpDev {
   int col_imu;
   int ckind[MAXC], cidx[MAXC], csub[MAXC];  // column -> (0 intr | 1 pose | 2 imu, cam / q, sub-index)
   int off_base, off_cb, off_imu, off_coef, S;
-  int nblk_f, nblk_s, nblk_ci, Wc, Ws, FHS;
+  int nblk_f, nblk_s, nblk_ci, nblk_ic, Wc, Ws, FHS;
   double ig, ia;
   const double* target;
   const double2* y;
@@ -70,11 +70,14 @@ struct SpDev {
   double *D0, *U0, *R0;   // built node blocks [n][324], [n][324], [n][18 m]
   double *D, *U, *R;      // working copies (cyclic reduction in place)
   double *Lf, *Z, *X;     // [n][324], [n][18 (36 + m)], [n][18 m]
+  double* Lid;            // [n][18] inverse diagonal of Lf
   double* spart;          // [nblk_s][Ws]
   double* dx;             // [C + 6K]
   double* dmax;           // [n]
   double* cpart;          // [nblk_f + nblk_ci]
   double* sc;             // scalars
+  double* Sf;             // [C][C] Schur complement (+ lam2 I) | b [C]
+  const short2* uab;      // [Wc] (a, b) of upper-triangle entry q; (a, C) for g_a; (C, C) for the cost
 };
 
 typedef double v4d_t __attribute__((ext_vector_type(4)));
@@ -416,12 +419,8 @@ __global__ void __launch_bounds__(512) k_sp_frames(SpDev d) {
     for (int q = tid; q < d.Wc; q += nth) {
       double s = 0.0;
       if (q < nup) {
-        int a = 0, e = q;
-        while (e >= C - a) {
-          e -= C - a;
-          ++a;
-        }
-        const int bcol = a + e;
+        const short2 ab = d.uab[q];
+        const int a = ab.x, bcol = ab.y;
         const int ka = d.ckind[a], ia = d.cidx[a], sa = d.csub[a];
         const int kb2 = d.ckind[bcol], ib2 = d.cidx[bcol], sb = d.csub[bcol];
         for (int i = 0; i < N; ++i) {
@@ -687,39 +686,49 @@ __global__ void __launch_bounds__(256) k_sp_assemble(SpDev d) {
 }
 
 // ---------------------------------------------------------------- IMU theta-theta (b_g | b_a | g_w)
-// 256 samples per block: J_theta^T J_theta upper (45), -J_theta^T e (9), e^T e -> one partial row [WI].
-__global__ void __launch_bounds__(256) k_sp_imu_cc(SpDev d) {
-  __shared__ double red[4][WI];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, m = blockIdx.x * 256 + tid;
+// 64 samples per block (one wave): each lane's J_theta^T J_theta upper (45), -J_theta^T e (9), e^T e staged in
+// LDS, summed per entry in sample order -> one partial row [WI].
+__global__ void __launch_bounds__(64) k_sp_imu_cc(SpDev d) {
+  __shared__ double v[64][WI + 1];
+  const int lane = threadIdx.x, m = blockIdx.x * 64 + lane;
   double e[6] = {0, 0, 0, 0, 0, 0}, Ct[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
   const bool has = m < d.M;
   if (has) imu_sample(d, m, e, nullptr, Ct);
-  for (int q = 0; q < WI; ++q) {
-    double s = 0.0;
-    if (has) {
-      if (q < 45) {
-        int a = 0, r = q;
-        while (r >= 9 - a) {
-          r -= 9 - a;
-          ++a;
-        }
-        const int bb = a + r;
+  // J_theta = [-ig I, 0, 0; 0, -ia I, ia C^T] (rows gyro | accel; columns b_g | b_a | g_w)
+  const double ig2 = d.ig * d.ig, ia2 = d.ia * d.ia;
+  int q = 0;
 #pragma unroll
-        for (int z = 0; z < 6; ++z) s += imu_jth(d, Ct, z, a) * imu_jth(d, Ct, z, bb);
-      } else if (q < 54) {
+  for (int a = 0; a < 9; ++a)
 #pragma unroll
-        for (int z = 0; z < 6; ++z) s -= imu_jth(d, Ct, z, q - 45) * e[z];
-      } else {
-#pragma unroll
-        for (int z = 0; z < 6; ++z) s += e[z] * e[z];
-      }
+    for (int b = a; b < 9; ++b, ++q) {
+      double t;
+      if (a < 3)
+        t = (b == a) ? ig2 : 0.0;
+      else if (a < 6)
+        t = (b == a) ? ia2 : (b >= 6 ? -ia2 * Ct[(a - 3) * 3 + (b - 6)] : 0.0);
+      else
+        t = (b == a) ? ia2 : 0.0;  // (C^T)^T C^T = I
+      v[lane][q] = has ? t : 0.0;
     }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-    if (lane == 0) red[wave][q] = s;
+  for (int a = 0; a < 9; ++a) {
+    double t;
+    if (a < 3) {
+      t = d.ig * e[a];
+    } else if (a < 6) {
+      t = d.ia * e[a];
+    } else {
+      t = -d.ia * (Ct[0 * 3 + (a - 6)] * e[3] + Ct[1 * 3 + (a - 6)] * e[4] + Ct[2 * 3 + (a - 6)] * e[5]);
+    }
+    v[lane][45 + a] = has ? t : 0.0;
   }
+  v[lane][54] = has ? ((e[0] * e[0] + e[1] * e[1]) + (e[2] * e[2] + e[3] * e[3])) + (e[4] * e[4] + e[5] * e[5]) : 0.0;
   __syncthreads();
-  if (tid < WI) d.ipart[(size_t)blockIdx.x * WI + tid] = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
+  if (lane < WI) {
+    double s = 0.0;
+    for (int k = 0; k < 64; ++k) s += v[k][lane];
+    d.ipart[(size_t)blockIdx.x * WI + lane] = s;
+  }
 }
 
 // ---------------------------------------------------------------- k_sp_reduce_cc: H_cc, g_c, cost
@@ -745,12 +754,9 @@ __global__ void __launch_bounds__(256) k_sp_reduce_cc(SpDev d) {
   int ii = -1, a = 0, bcol = 0;
   if (act) {
     if (q < nup) {
-      int e = q;
-      while (e >= C - a) {
-        e -= C - a;
-        ++a;
-      }
-      bcol = a + e;
+      const short2 ab = d.uab[q];
+      a = ab.x;
+      bcol = ab.y;
       const int ia = a - d.col_imu, ib = bcol - d.col_imu;
       if (ia >= 0 && ia < 9 && ib >= 0 && ib < 9) ii = ia * 9 - ia * (ia - 1) / 2 + (ib - ia);
     } else if (q < nup + C) {
@@ -761,7 +767,7 @@ __global__ void __launch_bounds__(256) k_sp_reduce_cc(SpDev d) {
     }
   }
   double s = act ? col_sum(d.part, d.nblk_f, d.Wc, q, wave, 4) : 0.0;
-  if (ii >= 0) s += col_sum(d.ipart, d.nblk_ci, WI, ii, wave, 4);
+  if (ii >= 0) s += col_sum(d.ipart, d.nblk_ic, WI, ii, wave, 4);
   red[wave][lane] = s;
   __syncthreads();
   if (wave != 0 || !act) return;
@@ -793,150 +799,211 @@ __global__ void __launch_bounds__(256) k_sp_prep(SpDev d) {
   if (i == 0 && tid == 0) d.sc[SC_OK] = 1.0;
 }
 
-// in-LDS Cholesky of an 18 x 18 SPD matrix (lower, row-major); returns false if not positive definite
-__device__ bool chol18(double* A, int tid) {
-  __shared__ int okf;
-  if (tid == 0) okf = 1;
-  __syncthreads();
-  for (int k = 0; k < NB; ++k) {
-    if (tid == 0) {
-      const double v = A[k * NB + k];
-      if (!(v > 0.0)) okf = 0;
-      A[k * NB + k] = sqrt(v > 0.0 ? v : 1.0);
-    }
-    __syncthreads();
-    const double dk = A[k * NB + k];
-    if (tid > k && tid < NB) A[tid * NB + k] /= dk;
-    __syncthreads();
-    for (int q = tid; q < NB * NB; q += blockDim.x) {
-      const int r = q / NB, c = q % NB;
-      if (r > k && c > k && c <= r) A[r * NB + c] -= A[r * NB + k] * A[c * NB + k];
-    }
-    __syncthreads();
-  }
-  return okf != 0;
+// broadcast of lane l's double (l wave-uniform)
+__device__ __forceinline__ double rdlane(double v, int l) {
+  const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(u & 0xffffffffull), l);
+  const int hi = __builtin_amdgcn_readlane((int)(u >> 32), l);
+  return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
 }
 
-__global__ void __launch_bounds__(256) k_sp_elim(SpDev d, int s) {
-  __shared__ double L[NB * NB];
-  extern __shared__ __attribute__((aligned(16))) double W[];  // [18][36 + m]
-  const int j = s + 2 * s * blockIdx.x, tid = threadIdx.x, m = d.m, wc = 36 + m;
-  if (j >= d.n) return;
-  const int l = j - s, r = j + s;
-  const double* Dj = d.D + (size_t)j * NB * NB;
-  const double* Ul = d.U + (size_t)l * NB * NB;  // coupling l -> j (rows l)
-  const double* Uj = d.U + (size_t)j * NB * NB;  // coupling j -> r
-  const double* Rj = d.R + (size_t)j * NB * m;
-  for (int q = tid; q < NB * NB; q += blockDim.x) L[q] = Dj[q];
-  for (int q = tid; q < NB * wc; q += blockDim.x) {
-    const int row = q / wc, c = q % wc;
-    double v;
-    if (c < NB)
-      v = Ul[c * NB + row];  // U_l^T
-    else if (c < 2 * NB)
-      v = (r < d.n) ? Uj[row * NB + c - NB] : 0.0;
-    else
-      v = Rj[row * m + c - 2 * NB];
-    W[q] = v;
+// one-wave register Cholesky of an 18 x 18 SPD matrix held in LDS (lower, row-major): lane r keeps row r in
+// registers, column k broadcast by v_readlane; the factor is written back.  Returns false if not positive
+// definite.  Call from one whole wave.
+__device__ bool chol18_wave(double* A, double* id, int lane) {
+  double a[NB];
+#pragma unroll
+  for (int c = 0; c < NB; ++c) a[c] = lane < NB ? A[lane * NB + c] : 0.0;
+  bool ok = true;
+#pragma unroll
+  for (int k = 0; k < NB; ++k) {
+    const double dkk = rdlane(a[k], k);
+    ok = ok && (dkk > 0.0);
+    const double dk = sqrt(dkk > 0.0 ? dkk : 1.0);
+    if (lane == k) a[k] = dk;
+    if (lane > k) a[k] = a[k] / dk;
+#pragma unroll
+    for (int c = k + 1; c < NB; ++c) {
+      const double lck = rdlane(a[k], c);
+      if (lane >= c) a[c] -= a[k] * lck;
+    }
   }
-  __syncthreads();
-  const bool ok = chol18(L, tid);
-  if (!ok && tid == 0) d.sc[SC_OK] = 0.0;
-  // forward substitution L Z = W, one column per thread
-  for (int c = tid; c < wc; c += blockDim.x) {
+  KSP_WAVE_SYNC();
+  if (lane < NB) {
+#pragma unroll
+    for (int c = 0; c < NB; ++c) A[lane * NB + c] = c <= lane ? a[c] : 0.0;
+    double dg = a[0];
+#pragma unroll
+    for (int c = 1; c < NB; ++c) dg = (c == lane) ? a[c] : dg;
+    id[lane] = 1.0 / dg;
+  }
+  KSP_WAVE_SYNC();
+  return ok;
+}
+
+// L Z = W (lower L in LDS, inverse diagonal id), one thread per column of the [18][ws] LDS tile W, written to
+// dst (row stride ds)
+__device__ __forceinline__ void node_forward(const double* L, const double* id, const double* W, int ws, int ncol,
+                                             double* dst, int ds, int tid) {
+  for (int c = tid; c < ncol; c += blockDim.x) {
     double z[NB];
 #pragma unroll
     for (int row = 0; row < NB; ++row) {
-      double v = W[row * wc + c];
+      double v = W[row * ws + c];
 #pragma unroll
       for (int k = 0; k < row; ++k) v -= L[row * NB + k] * z[k];
-      z[row] = v / L[row * NB + row];
+      z[row] = v * id[row];
     }
 #pragma unroll
-    for (int row = 0; row < NB; ++row) d.Z[(size_t)j * NB * wc + row * wc + c] = z[row];
-  }
-  for (int q = tid; q < NB * NB; q += blockDim.x) d.Lf[(size_t)j * NB * NB + q] = L[q];
-}
-
-__global__ void __launch_bounds__(256) k_sp_keep(SpDev d, int s) {
-  extern __shared__ __attribute__((aligned(16))) double W[];  // Zl [18][wc] | Zr [18][wc]
-  const int i = 2 * s * blockIdx.x, tid = threadIdx.x, m = d.m, wc = 36 + m;
-  if (i >= d.n) return;
-  const int jl = i - s, jr = i + s;
-  const bool hl = jl >= 0, hr = jr < d.n;
-  double* Zl = W;
-  double* Zr = W + NB * wc;
-  for (int q = tid; q < NB * wc; q += blockDim.x) {
-    Zl[q] = hl ? d.Z[(size_t)jl * NB * wc + q] : 0.0;
-    Zr[q] = hr ? d.Z[(size_t)jr * NB * wc + q] : 0.0;
-  }
-  __syncthreads();
-  double* Di = d.D + (size_t)i * NB * NB;
-  double* Ui = d.U + (size_t)i * NB * NB;
-  double* Ri = d.R + (size_t)i * NB * m;
-  // D_i -= A^T A (A = Zl[:, 18:36]) + B^T B (B = Zr[:, 0:18]); U_i = -B^T Zr[:, 18:36]
-  for (int q = tid; q < 2 * NB * NB; q += blockDim.x) {
-    const int e = q % (NB * NB), a = e / NB, b = e % NB;
-    double sacc = 0.0;
-    if (q < NB * NB) {
-#pragma unroll
-      for (int k = 0; k < NB; ++k) sacc += Zl[k * wc + NB + a] * Zl[k * wc + NB + b] + Zr[k * wc + a] * Zr[k * wc + b];
-      Di[e] -= sacc;
-    } else {
-#pragma unroll
-      for (int k = 0; k < NB; ++k) sacc += Zr[k * wc + a] * Zr[k * wc + NB + b];
-      Ui[e] = -sacc;
-    }
-  }
-  for (int q = tid; q < NB * m; q += blockDim.x) {
-    const int a = q / m, c = q % m;
-    double sacc = 0.0;
-#pragma unroll
-    for (int k = 0; k < NB; ++k) sacc += Zl[k * wc + NB + a] * Zl[k * wc + 2 * NB + c] + Zr[k * wc + a] * Zr[k * wc + 2 * NB + c];
-    Ri[q] -= sacc;
+    for (int row = 0; row < NB; ++row) dst[row * ds + c] = z[row];
   }
 }
 
-// back substitution of one 18-row node with LDS-staged operands: x = L^-T T, one thread per RHS column
-__device__ __forceinline__ void node_backsolve(const double* L, double* T, int m, double* out, int tid) {
+// back substitution of one 18-row node with LDS-staged operands: x = L^-T T (T row stride ts), one thread per
+// RHS column, written to out (row stride m)
+__device__ __forceinline__ void node_backsolve(const double* L, const double* id, const double* T, int ts, int m,
+                                               double* out, int tid) {
   for (int c = tid; c < m; c += blockDim.x) {
     double z[NB];
 #pragma unroll
-    for (int row = 0; row < NB; ++row) z[row] = T[row * m + c];
+    for (int row = 0; row < NB; ++row) z[row] = T[row * ts + c];
 #pragma unroll
     for (int row = NB - 1; row >= 0; --row) {
       double v = z[row];
 #pragma unroll
       for (int k = row + 1; k < NB; ++k) v -= L[k * NB + row] * z[k];
-      z[row] = v / L[row * NB + row];
+      z[row] = v * id[row];
     }
 #pragma unroll
     for (int row = 0; row < NB; ++row) out[row * m + c] = z[row];
   }
 }
 
+// first level (stride 1): odd nodes j eliminated, Z_j = L_j^-1 [U_{j-1}^T | U_j | R_j]
+__global__ void __launch_bounds__(256) k_sp_elim1(SpDev d) {
+  __shared__ double L[NB * NB];
+  __shared__ double id[NB];
+  extern __shared__ __attribute__((aligned(16))) double W[];  // [18][36 + m]
+  const int j = 1 + 2 * blockIdx.x, tid = threadIdx.x, m = d.m, wc = 36 + m;
+  if (j >= d.n) return;
+  const int l = j - 1, r = j + 1;
+  const double* Ul = d.U + (size_t)l * NB * NB;
+  const double* Uj = d.U + (size_t)j * NB * NB;
+  const double* Rj = d.R + (size_t)j * NB * m;
+  for (int q = tid; q < NB * NB; q += blockDim.x) L[q] = d.D[(size_t)j * NB * NB + q];
+  for (int q = tid; q < NB * wc; q += blockDim.x) {
+    const int row = q / wc, c = q % wc;
+    W[q] = c < NB ? Ul[c * NB + row] : c < 2 * NB ? (r < d.n ? Uj[row * NB + c - NB] : 0.0) : Rj[row * m + c - 2 * NB];
+  }
+  __syncthreads();
+  if (tid < 64) {
+    const bool ok = chol18_wave(L, id, tid);
+    if (!ok && tid == 0) d.sc[SC_OK] = 0.0;
+  }
+  __syncthreads();
+  node_forward(L, id, W, wc, wc, d.Z + (size_t)j * NB * wc, wc, tid);
+  for (int q = tid; q < NB * NB; q += blockDim.x) d.Lf[(size_t)j * NB * NB + q] = L[q];
+  if (tid < NB) d.Lid[(size_t)j * NB + tid] = id[tid];
+}
+
+// fused level: node i (i % 2s == 0) absorbs its level-s eliminated neighbours i -+ s, then either is
+// eliminated at level 2s (Cholesky + Z_i with the couplings to i -+ 2s it computes itself), stays for the next
+// level, or -- node 0 once no partner is left -- solves X_0 = D_0^-1 R_0.
+__global__ void __launch_bounds__(256) k_sp_level(SpDev d, int s) {
+  __shared__ double L[NB * NB];
+  __shared__ double id[NB];
+  __shared__ double Ui[NB * NB];  // coupling (i - 2s) -> i
+  __shared__ double Uo[NB * NB];  // coupling i -> (i + 2s)
+  extern __shared__ __attribute__((aligned(16))) double sm[];  // Zl [18][wc] | Zr [18][wc] | W [18][wc]
+  const int i = 2 * s * blockIdx.x, tid = threadIdx.x, m = d.m, wc = 36 + m;
+  if (i >= d.n) return;
+  const int jl = i - s, jr = i + s;
+  const bool hl = jl >= 0, hr = jr < d.n;
+  const bool elim = (i % (4 * s)) == 2 * s;  // eliminated at level 2s
+  const bool top = (i == 0) && (2 * s >= d.n);
+  double* Zl = sm;
+  double* Zr = Zl + NB * wc;
+  double* W = Zr + NB * wc;  // [Ui^T | Uo | R']
+  for (int q = tid; q < NB * wc; q += blockDim.x) {
+    Zl[q] = hl ? d.Z[(size_t)jl * NB * wc + q] : 0.0;
+    Zr[q] = hr ? d.Z[(size_t)jr * NB * wc + q] : 0.0;
+  }
+  __syncthreads();
+  const double* Di = d.D + (size_t)i * NB * NB;
+  const double* Ri = d.R + (size_t)i * NB * m;
+  for (int q = tid; q < 3 * NB * NB; q += blockDim.x) {
+    const int part = q / (NB * NB), e = q % (NB * NB), a = e / NB, b = e % NB;
+    double acc = 0.0;
+    if (part == 0) {  // D' = D - Zl_U^T Zl_U - Zr_Uin^T Zr_Uin
+#pragma unroll
+      for (int k = 0; k < NB; ++k) acc += Zl[k * wc + NB + a] * Zl[k * wc + NB + b] + Zr[k * wc + a] * Zr[k * wc + b];
+      L[e] = Di[e] - acc;
+    } else if (part == 1) {  // Uo = -Zr_Uin^T Zr_U
+#pragma unroll
+      for (int k = 0; k < NB; ++k) acc += Zr[k * wc + a] * Zr[k * wc + NB + b];
+      Uo[e] = -acc;
+    } else {  // Ui = -Zl_Uin^T Zl_U  (rows i - 2s, cols i)
+#pragma unroll
+      for (int k = 0; k < NB; ++k) acc += Zl[k * wc + a] * Zl[k * wc + NB + b];
+      Ui[e] = -acc;
+    }
+  }
+  for (int q = tid; q < NB * m; q += blockDim.x) {  // R' = R - Zl_U^T Zl_R - Zr_Uin^T Zr_R
+    const int a = q / m, c = q % m;
+    double acc = 0.0;
+#pragma unroll
+    for (int k = 0; k < NB; ++k) acc += Zl[k * wc + NB + a] * Zl[k * wc + 2 * NB + c] + Zr[k * wc + a] * Zr[k * wc + 2 * NB + c];
+    W[a * wc + 2 * NB + c] = Ri[q] - acc;
+  }
+  __syncthreads();
+  if (!elim && !top) {  // stays active: D', U (to i + 2s), R' for the next level
+    for (int q = tid; q < NB * NB; q += blockDim.x) {
+      d.D[(size_t)i * NB * NB + q] = L[q];
+      d.U[(size_t)i * NB * NB + q] = Uo[q];
+    }
+    for (int q = tid; q < NB * m; q += blockDim.x) d.R[(size_t)i * NB * m + q] = W[(q / m) * wc + 2 * NB + q % m];
+    return;
+  }
+  for (int q = tid; q < NB * NB; q += blockDim.x) {
+    const int a = q / NB, b = q % NB;
+    W[a * wc + b] = Ui[b * NB + a];  // Ui^T
+    W[a * wc + NB + b] = Uo[q];
+  }
+  if (tid < 64) {
+    const bool ok = chol18_wave(L, id, tid);
+    if (!ok && tid == 0) d.sc[SC_OK] = 0.0;
+  }
+  __syncthreads();
+  if (top) {  // X_0 = L^-T L^-1 R' (forward in place in W, then backward into X_0)
+    node_forward(L, id, W + 2 * NB, wc, m, W + 2 * NB, wc, tid);
+    node_backsolve(L, id, W + 2 * NB, wc, m, d.X, tid);
+    return;
+  }
+  node_forward(L, id, W, wc, wc, d.Z + (size_t)i * NB * wc, wc, tid);
+  for (int q = tid; q < NB * NB; q += blockDim.x) d.Lf[(size_t)i * NB * NB + q] = L[q];
+  if (tid < NB) d.Lid[(size_t)i * NB + tid] = id[tid];
+}
+
 __global__ void __launch_bounds__(256) k_sp_top(SpDev d) {
   __shared__ double L[NB * NB];
+  __shared__ double id[NB];
   extern __shared__ __attribute__((aligned(16))) double T[];  // [18][m]
   const int tid = threadIdx.x, m = d.m;
   for (int q = tid; q < NB * NB; q += blockDim.x) L[q] = d.D[q];
+  for (int q = tid; q < NB * m; q += blockDim.x) T[q] = d.R[q];
   __syncthreads();
-  const bool ok = chol18(L, tid);
-  if (!ok && tid == 0) d.sc[SC_OK] = 0.0;
-  for (int c = tid; c < m; c += blockDim.x) {  // forward: L y = R_0
-#pragma unroll
-    for (int row = 0; row < NB; ++row) {
-      double v = d.R[row * m + c];
-#pragma unroll
-      for (int k = 0; k < row; ++k) v -= L[row * NB + k] * T[k * m + c];
-      T[row * m + c] = v / L[row * NB + row];
-    }
+  if (tid < 64) {
+    const bool ok = chol18_wave(L, id, tid);
+    if (!ok && tid == 0) d.sc[SC_OK] = 0.0;
   }
-  node_backsolve(L, T, m, d.X, tid);
+  __syncthreads();
+  node_forward(L, id, T, m, m, T, m, tid);
+  node_backsolve(L, id, T, m, m, d.X, tid);
 }
 
 __global__ void __launch_bounds__(256) k_sp_back(SpDev d, int s) {
   __shared__ double L[NB * NB];
+  __shared__ double id[NB];
   extern __shared__ __attribute__((aligned(16))) double sm[];  // Z [18][wc] | xl [18][m] | xr [18][m] | T [18][m]
   const int j = s + 2 * s * blockIdx.x, tid = threadIdx.x, m = d.m, wc = 36 + m;
   if (j >= d.n) return;
@@ -947,6 +1014,7 @@ __global__ void __launch_bounds__(256) k_sp_back(SpDev d, int s) {
   double* xr = xl + NB * m;
   double* T = xr + NB * m;
   for (int q = tid; q < NB * NB; q += blockDim.x) L[q] = d.Lf[(size_t)j * NB * NB + q];
+  if (tid < NB) id[tid] = d.Lid[(size_t)j * NB + tid];
   for (int q = tid; q < NB * wc; q += blockDim.x) Z[q] = d.Z[(size_t)j * NB * wc + q];
   for (int q = tid; q < NB * m; q += blockDim.x) {
     xl[q] = d.X[(size_t)l * NB * m + q];
@@ -962,14 +1030,14 @@ __global__ void __launch_bounds__(256) k_sp_back(SpDev d, int s) {
     T[q] = v;
   }
   __syncthreads();
-  node_backsolve(L, T, m, d.X + (size_t)j * NB * m, tid);
+  node_backsolve(L, id, T, m, m, d.X + (size_t)j * NB * m, tid);
 }
 
 // ---------------------------------------------------------------- Schur complement onto theta
 // partial rows of sum_i R0_i^T X_i over NPB nodes: upper C x C | C (the g column)
 __global__ void __launch_bounds__(256) k_sp_schur(SpDev d) {
   extern __shared__ __attribute__((aligned(16))) double sm[];  // R0 [18][m] | X [18][m]
-  const int tid = threadIdx.x, C = d.C, m = d.m, nup = C * (C + 1) / 2;
+  const int tid = threadIdx.x, m = d.m;
   double* Rl = sm;
   double* Xl = sm + NB * m;
   double* acc = Xl + NB * m;  // [Ws]
@@ -983,19 +1051,8 @@ __global__ void __launch_bounds__(256) k_sp_schur(SpDev d) {
     }
     __syncthreads();
     for (int q = tid; q < d.Ws; q += blockDim.x) {
-      int a, b;
-      if (q < nup) {
-        int e = q;
-        a = 0;
-        while (e >= C - a) {
-          e -= C - a;
-          ++a;
-        }
-        b = a + e;
-      } else {
-        a = q - nup;
-        b = C;
-      }
+      const short2 ab = d.uab[q];
+      const int a = ab.x, b = ab.y;
       double s = 0.0;
 #pragma unroll
       for (int k = 0; k < NB; ++k) s += Rl[k * m + a] * Xl[k * m + b];
@@ -1006,71 +1063,78 @@ __global__ void __launch_bounds__(256) k_sp_schur(SpDev d) {
   for (int q = tid; q < d.Ws; q += blockDim.x) d.spart[(size_t)blockIdx.x * d.Ws + q] = acc[q];
 }
 
-// dense camera / IMU block: S = H_cc + lam2 I - sum, b = g_c - sum (4-wave interleaved partial sums);
-// Cholesky in LDS; one-wave forward / backward substitution; dtheta -> dx[0..C)
-__global__ void __launch_bounds__(256) k_sp_camsolve(SpDev d) {
-  __shared__ double S[MAXC * MAXC];
-  __shared__ double bv[MAXC];
-  __shared__ double red[4][256];
-  __shared__ int okf;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, C = d.C, nup = C * (C + 1) / 2;
-  const double lam2 = d.sc[SC_LAM2];
-  for (int q0 = 0; q0 < nup + C; q0 += 64) {
-    const int q = q0 + lane;
-    const double s = (q < nup + C) ? col_sum(d.spart, d.nblk_s, d.Ws, q, wave, 4) : 0.0;
-    red[wave][lane] = s;
-    __syncthreads();
-    if (wave == 0 && q < nup + C) {
-      const double t = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
-      if (q < nup) {
-        int e = q, a = 0;
-        while (e >= C - a) {
-          e -= C - a;
-          ++a;
+// S = H_cc + lam2 I - sum_i R0_i^T X_i, b = g_c - sum (4-wave interleaved partial sums), written full
+__global__ void __launch_bounds__(256) k_sp_schur_red(SpDev d) {
+  __shared__ double red[4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, C = d.C, nup = C * (C + 1) / 2;
+  const int q = blockIdx.x * 64 + lane;
+  const bool act = q < d.Ws;
+  red[wave][lane] = act ? col_sum(d.spart, d.nblk_s, d.Ws, q, wave, 4) : 0.0;
+  __syncthreads();
+  if (wave != 0 || !act) return;
+  const double t = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+  const short2 ab = d.uab[q];
+  const int a = ab.x, b = ab.y;
+  if (q < nup) {
+    const double v = d.Hcc[a * C + b] + (a == b ? d.sc[SC_LAM2] : 0.0) - t;
+    d.Sf[a * C + b] = v;
+    d.Sf[b * C + a] = v;
+  } else {
+    d.Sf[C * C + a] = d.Hcc[C * C + a] - t;
+  }
+}
+
+// dense camera / IMU block solve on one wave: lane r holds row r of S in registers, Cholesky and both
+// triangular solves with v_readlane broadcasts (CM >= C); dtheta -> dx[0..C)
+template <int CM>
+__global__ void __launch_bounds__(64) k_sp_camsolve(SpDev d) {
+  __shared__ double Lt[CM * CM];  // L[r][c] at r * CM + c
+  const int lane = threadIdx.x, C = d.C;
+  double a[CM];
+#pragma unroll
+  for (int c = 0; c < CM; ++c) a[c] = (lane < C && c < C) ? d.Sf[lane * C + c] : 0.0;
+  double x = lane < C ? d.Sf[C * C + lane] : 0.0;
+  bool ok = true;
+#pragma unroll
+  for (int k = 0; k < CM; ++k) {
+    if (k < C) {
+      const double dkk = rdlane(a[k], k);
+      ok = ok && (dkk > 0.0);
+      const double dk = sqrt(dkk > 0.0 ? dkk : 1.0);
+      if (lane == k) a[k] = dk;
+      if (lane > k) a[k] = a[k] / dk;
+#pragma unroll
+      for (int c = k + 1; c < CM; ++c) {
+        if (c < C) {
+          const double lck = rdlane(a[k], c);
+          if (lane >= c) a[c] -= a[k] * lck;
         }
-        const int bb = a + e;
-        const double v = d.Hcc[a * C + bb] + (a == bb ? lam2 : 0.0) - t;
-        S[a * C + bb] = v;
-        S[bb * C + a] = v;
-      } else {
-        bv[q - nup] = d.Hcc[C * C + (q - nup)] - t;
       }
     }
-    __syncthreads();
   }
-  if (tid == 0) okf = 1;
-  __syncthreads();
-  for (int k = 0; k < C; ++k) {
-    if (tid == 0) {
-      const double v = S[k * C + k];
-      if (!(v > 0.0)) okf = 0;
-      S[k * C + k] = sqrt(v > 0.0 ? v : 1.0);
-    }
-    __syncthreads();
-    const double dk = S[k * C + k];
-    if (tid > k && tid < C) S[tid * C + k] /= dk;
-    __syncthreads();
-    for (int q = tid; q < C * C; q += blockDim.x) {
-      const int r = q / C, c = q % C;
-      if (r > k && c > k && c <= r) S[r * C + c] -= S[r * C + k] * S[c * C + k];
-    }
-    __syncthreads();
+  if (lane < C) {
+#pragma unroll
+    for (int c = 0; c < CM; ++c) Lt[lane * CM + c] = a[c];
   }
-  if (wave == 0) {  // L y = b, L^T x = y: lane r owns row r, the solved value broadcast by readlane
-    double x = lane < C ? bv[lane] : 0.0;
-    for (int r = 0; r < C; ++r) {
-      const double xr = __shfl(x, r) / S[r * C + r];
-      if (lane == r) x = xr;
-      if (lane > r && lane < C) x -= S[lane * C + r] * xr;
+  // L y = b : lane r keeps y_r; column k of L is a[k] of lanes > k
+#pragma unroll
+  for (int k = 0; k < CM; ++k) {
+    if (k < C) {
+      const double yk = rdlane(x, k) / rdlane(a[k], k);
+      if (lane == k) x = yk;
+      if (lane > k) x -= a[k] * yk;
     }
-    for (int r = C - 1; r >= 0; --r) {
-      const double xr = __shfl(x, r) / S[r * C + r];
-      if (lane == r) x = xr;
-      if (lane < r) x -= S[r * C + lane] * xr;
-    }
-    if (lane < C) d.dx[lane] = x;
-    if (lane == 0 && !okf) d.sc[SC_OK] = 0.0;
   }
+  KSP_WAVE_SYNC();
+  // L^T x = y : right-looking, row k of L from LDS (lane j reads L[k][j])
+  for (int k = C - 1; k >= 0; --k) {
+    const double lkj = lane < k ? Lt[k * CM + lane] : 0.0;
+    const double xk = __shfl(x, k) / Lt[k * CM + k];
+    if (lane == k) x = xk;
+    x -= lkj * xk;
+  }
+  if (lane < C) d.dx[lane] = x;
+  if (lane == 0 && !ok) d.sc[SC_OK] = 0.0;
 }
 
 // coefficient steps ds_i = X_i[:, C] - X_i[:, :C] dtheta; with `apply` (and a successful solve) the state
@@ -1341,9 +1405,10 @@ struct kb_sp_handle {
   std::vector<void*> allocs;
   double lambda = 0.0;
   bool uploaded = false, built = false, solved = false;
-  size_t lds_frames = 0, lds_asm = 0, lds_elim = 0, lds_keep = 0, lds_schur = 0, lds_back = 0;
+  size_t lds_frames = 0, lds_asm = 0, lds_elim = 0, lds_level = 0, lds_schur = 0, lds_back = 0;
   const void* fn_frames = nullptr;
   const void* fn_cost = nullptr;
+  const void* fn_camsolve = nullptr;
   hipGraphExec_t gn_graph = nullptr;
   int gn_graph_n = 0;
   std::vector<double> trace;
@@ -1374,27 +1439,36 @@ int launch_build(kb_sp_handle* h) {
   void* args[] = {&d};
   KSP_HIP(hipLaunchKernel(h->fn_frames, dim3(d.nblk_f), dim3(64 * h->N), args, h->lds_frames, h->stream));
   KSP_HIP(hipLaunchKernel((const void*)k_sp_assemble, dim3(d.n), dim3(256), args, h->lds_asm, h->stream));
-  hipLaunchKernelGGL(k_sp_imu_cc, dim3(d.nblk_ci), dim3(256), 0, h->stream, d);
+  hipLaunchKernelGGL(k_sp_imu_cc, dim3(d.nblk_ic), dim3(64), 0, h->stream, d);
   hipLaunchKernelGGL(k_sp_reduce_cc, dim3((d.Wc + 63) / 64), dim3(256), 0, h->stream, d);
+  return 0;
+}
+
+int launch_reduction(kb_sp_handle* h) {
+  SpDev& d = h->d;
+  hipLaunchKernelGGL(k_sp_prep, dim3(d.n), dim3(256), 0, h->stream, d);
+  if (d.n == 1) {
+    hipLaunchKernelGGL(k_sp_top, dim3(1), dim3(256), sizeof(double) * NB * d.m, h->stream, d);
+    return 0;
+  }
+  hipLaunchKernelGGL(k_sp_elim1, dim3(d.n / 2), dim3(256), h->lds_elim, h->stream, d);
+  int s = 1;
+  for (; s < d.n; s *= 2)
+    hipLaunchKernelGGL(k_sp_level, dim3((d.n + 2 * s - 1) / (2 * s)), dim3(256), h->lds_level, h->stream, d, s);
+  for (s /= 2; s >= 1; s /= 2) {
+    const int ne = (d.n - s + 2 * s - 1) / (2 * s);
+    hipLaunchKernelGGL(k_sp_back, dim3(ne), dim3(256), h->lds_back, h->stream, d, s);
+  }
   return 0;
 }
 
 int launch_solve(kb_sp_handle* h) {
   SpDev& d = h->d;
-  hipLaunchKernelGGL(k_sp_prep, dim3(d.n), dim3(256), 0, h->stream, d);
-  int s = 1;
-  for (; s < d.n; s *= 2) {
-    const int ne = (d.n - s + 2 * s - 1) / (2 * s), nk = (d.n + 2 * s - 1) / (2 * s);
-    hipLaunchKernelGGL(k_sp_elim, dim3(ne), dim3(256), h->lds_elim, h->stream, d, s);
-    hipLaunchKernelGGL(k_sp_keep, dim3(nk), dim3(256), h->lds_keep, h->stream, d, s);
-  }
-  hipLaunchKernelGGL(k_sp_top, dim3(1), dim3(256), sizeof(double) * NB * d.m, h->stream, d);
-  for (s /= 2; s >= 1; s /= 2) {
-    const int ne = (d.n - s + 2 * s - 1) / (2 * s);
-    hipLaunchKernelGGL(k_sp_back, dim3(ne), dim3(256), h->lds_back, h->stream, d, s);
-  }
+  void* args[] = {&d};
+  launch_reduction(h);
   hipLaunchKernelGGL(k_sp_schur, dim3(d.nblk_s), dim3(256), h->lds_schur, h->stream, d);
-  hipLaunchKernelGGL(k_sp_camsolve, dim3(1), dim3(256), 0, h->stream, d);
+  hipLaunchKernelGGL(k_sp_schur_red, dim3((d.Ws + 63) / 64), dim3(256), 0, h->stream, d);
+  KSP_HIP(hipLaunchKernel(h->fn_camsolve, dim3(1), dim3(64), args, 0, h->stream));
   return 0;
 }
 
@@ -1544,6 +1618,7 @@ kb_sp_handle* kb_sp_create(const kb_sp_layout* L) {
   rc |= h->alloc(&d.U, (size_t)h->n * NB * NB);
   rc |= h->alloc(&d.R, (size_t)h->n * NB * d.m);
   rc |= h->alloc(&d.Lf, (size_t)h->n * NB * NB);
+  rc |= h->alloc(&d.Lid, (size_t)h->n * NB);
   rc |= h->alloc(&d.Z, (size_t)h->n * NB * (36 + d.m));
   rc |= h->alloc(&d.X, (size_t)h->n * NB * d.m);
   d.nblk_s = (h->n + NPB - 1) / NPB;
@@ -1551,6 +1626,23 @@ kb_sp_handle* kb_sp_create(const kb_sp_layout* L) {
   rc |= h->alloc(&d.dx, (size_t)h->ncols);
   rc |= h->alloc(&d.dmax, (size_t)h->n);
   rc |= h->alloc(&d.sc, (size_t)SC_NSC);
+  rc |= h->alloc(&d.Sf, (size_t)h->C * h->C + h->C);
+  {
+    std::vector<short2> tab((size_t)d.Wc);
+    int q = 0;
+    for (int a = 0; a < h->C; ++a)
+      for (int b = a; b < h->C; ++b) tab[q++] = make_short2((short)a, (short)b);
+    for (int a = 0; a < h->C; ++a) tab[q++] = make_short2((short)a, (short)h->C);
+    tab[q++] = make_short2((short)h->C, (short)h->C);
+    short2* dt = nullptr;
+    rc |= h->alloc(&dt, tab.size());
+    if (!rc) rc |= hipMemcpyAsync(dt, tab.data(), sizeof(short2) * tab.size(), hipMemcpyHostToDevice, h->stream) != hipSuccess;
+    d.uab = dt;
+  }
+  h->fn_camsolve = h->C <= 16 ? (const void*)k_sp_camsolve<16>
+                   : h->C <= 32 ? (const void*)k_sp_camsolve<32>
+                   : h->C <= 48 ? (const void*)k_sp_camsolve<48>
+                                : (const void*)k_sp_camsolve<64>;
   if (rc || hipHostMalloc((void**)&h->host_sc, sizeof(double) * SC_NSC) != hipSuccess ||
       hipMemcpyAsync(tgt, L->target_points, sizeof(double) * 3 * L->n_target, hipMemcpyHostToDevice, h->stream) !=
           hipSuccess) {
@@ -1559,7 +1651,7 @@ kb_sp_handle* kb_sp_create(const kb_sp_layout* L) {
     return nullptr;
   }
   h->lds_elim = sizeof(double) * NB * (36 + d.m);
-  h->lds_keep = 2 * h->lds_elim;
+  h->lds_level = 3 * h->lds_elim;
   h->lds_back = h->lds_elim + sizeof(double) * 3 * NB * d.m;
   h->lds_schur = sizeof(double) * (2 * NB * d.m + d.Ws);
   h->lds_asm = sizeof(double) * (2 * NB * NB + NB * d.m + TCH * std::max(144 + 15, d.FHS));
@@ -1572,8 +1664,9 @@ kb_sp_handle* kb_sp_create(const kb_sp_layout* L) {
   }
   hipFuncSetAttribute(h->fn_frames, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_frames);
   hipFuncSetAttribute((const void*)k_sp_assemble, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_asm);
-  hipFuncSetAttribute((const void*)k_sp_keep, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_keep);
-  hipFuncSetAttribute((const void*)k_sp_elim, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_elim);
+  hipFuncSetAttribute((const void*)k_sp_level, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_level);
+  hipFuncSetAttribute((const void*)k_sp_elim1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_elim);
+  hipFuncSetAttribute((const void*)k_sp_back, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_back);
   hipFuncSetAttribute((const void*)k_sp_schur, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_schur);
   if (hipStreamSynchronize(h->stream) != hipSuccess) {
     fail("kb_sp_create: stream sync failed");
@@ -1653,6 +1746,7 @@ int kb_sp_upload(kb_sp_handle* h, int32_t n_frames, const double* frame_time, in
   h->NCo = n_corners;
   d.nblk_f = (F + FPB - 1) / FPB;
   d.nblk_ci = std::max(1, (M + 255) / 256);
+  d.nblk_ic = std::max(1, (M + 63) / 64);
   int rc = 0;
   double2* dy = nullptr;
   uint16_t* dcid = nullptr;
@@ -1672,7 +1766,7 @@ int kb_sp_upload(kb_sp_handle* h, int32_t n_frames, const double* frame_time, in
   rc |= h->alloc(&d.FH, (size_t)F * d.FHS);
   rc |= h->alloc(&d.part, (size_t)d.nblk_f * d.Wc);
   rc |= h->alloc(&d.cpart, (size_t)(d.nblk_f + d.nblk_ci));
-  rc |= h->alloc(&d.ipart, (size_t)d.nblk_ci * WI);
+  rc |= h->alloc(&d.ipart, (size_t)d.nblk_ic * WI);
   if (rc) return -1;
   if (n_corners) {
     KSP_HIP(hipMemcpyAsync(dy, y, sizeof(double) * 2 * n_corners, hipMemcpyHostToDevice, h->stream));
@@ -2029,24 +2123,14 @@ int kb_sp_kernel_stats(kb_sp_handle* h, int32_t n, double* ms_out6, double* fram
     KSP_HIP(hipLaunchKernel(h->fn_frames, dim3(d.nblk_f), dim3(64 * h->N), args, h->lds_frames, h->stream));
     KSP_HIP(hipEventRecord(ev[1], h->stream));
     KSP_HIP(hipLaunchKernel((const void*)k_sp_assemble, dim3(d.n), dim3(256), args, h->lds_asm, h->stream));
-    hipLaunchKernelGGL(k_sp_imu_cc, dim3(d.nblk_ci), dim3(256), 0, h->stream, d);
+    hipLaunchKernelGGL(k_sp_imu_cc, dim3(d.nblk_ic), dim3(64), 0, h->stream, d);
     hipLaunchKernelGGL(k_sp_reduce_cc, dim3((d.Wc + 63) / 64), dim3(256), 0, h->stream, d);
     KSP_HIP(hipEventRecord(ev[2], h->stream));
-    hipLaunchKernelGGL(k_sp_prep, dim3(d.n), dim3(256), 0, h->stream, d);
-    int s = 1;
-    for (; s < d.n; s *= 2) {
-      const int ne = (d.n - s + 2 * s - 1) / (2 * s), nk = (d.n + 2 * s - 1) / (2 * s);
-      hipLaunchKernelGGL(k_sp_elim, dim3(ne), dim3(256), h->lds_elim, h->stream, d, s);
-      hipLaunchKernelGGL(k_sp_keep, dim3(nk), dim3(256), h->lds_keep, h->stream, d, s);
-    }
-    hipLaunchKernelGGL(k_sp_top, dim3(1), dim3(256), sizeof(double) * NB * d.m, h->stream, d);
-    for (s /= 2; s >= 1; s /= 2) {
-      const int ne = (d.n - s + 2 * s - 1) / (2 * s);
-      hipLaunchKernelGGL(k_sp_back, dim3(ne), dim3(256), h->lds_back, h->stream, d, s);
-    }
+    launch_reduction(h);
     KSP_HIP(hipEventRecord(ev[3], h->stream));
     hipLaunchKernelGGL(k_sp_schur, dim3(d.nblk_s), dim3(256), h->lds_schur, h->stream, d);
-    hipLaunchKernelGGL(k_sp_camsolve, dim3(1), dim3(256), 0, h->stream, d);
+    hipLaunchKernelGGL(k_sp_schur_red, dim3((d.Ws + 63) / 64), dim3(256), 0, h->stream, d);
+    KSP_HIP(hipLaunchKernel(h->fn_camsolve, dim3(1), dim3(64), args, 0, h->stream));
     KSP_HIP(hipEventRecord(ev[4], h->stream));
     hipLaunchKernelGGL(k_sp_update, dim3(d.n), dim3(64), 0, h->stream, d, 1);
     if (launch_cost(h, 1)) return -1;
