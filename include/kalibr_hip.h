@@ -93,6 +93,35 @@ int kb_set_constant_conditioner(kb_handle* h, double diag);
  * solves (J^T J + diag^2 I) dx = rhs.  *ok = 0 on a non-positive-definite system
  * (CHOLMOD failure semantics, Cholmod(impl).hpp:287-328); dx_out untouched then. */
 int kb_solve(kb_handle* h, double* dx_out, int* ok);
+/* Linear solver behind kb_solve ("direct or PCG by mode").
+ *   KB_SOLVER_SCHUR  (default) frame-block Schur complement + dense camera-block LDL^T: the exact solve that
+ *                    replaces CHOLMOD (SparseCholeskyLinearSystemSolver.cpp:48-89); parity mode.
+ *   KB_SOLVER_PCG    block-Jacobi preconditioned conjugate gradients on the full arrow system, as
+ *                    sparse_block_matrix's LinearSolverPCG::solve
+ *                    (sparse_block_matrix/include/sparse_block_matrix/implementation/linear_solver_pcg.hpp:58-130):
+ *                    preconditioner = inverses of the diagonal design-variable blocks; stops when
+ *                    r^T M^-1 r <= tolerance * r0^T M^-1 r0 (absolute mode: or <= the previous solve's _residual).
+ *                    The reference always returns true; here *ok = 0 on a singular DV block or non-positive
+ *                    curvature d^T A d.  One-GPU handles only (a sharded handle returns an error).
+ * kb_optimize always uses the direct solve (its passes are captured graphs); the per-call path
+ * (kb_build / kb_solve / kb_apply_update, driven by the host Optimizer2) uses the selected solver. */
+enum kb_linear_solver { KB_SOLVER_SCHUR = 0, KB_SOLVER_PCG = 1 };
+typedef struct kb_pcg_options {
+  double tolerance;           /* _tolerance (LinearSolverPCG default 1e-6) */
+  int32_t max_iterations;     /* _maxIter (-1: number of rows, the default) */
+  int32_t absolute_tolerance; /* _absoluteTolerance (default 1) */
+} kb_pcg_options;
+typedef struct kb_pcg_info {
+  int32_t iterations; /* PCG iterations of the last solve */
+  double residual;    /* _residual = 0.5 r^T M^-1 r at exit */
+  double d0;          /* stopping threshold used */
+} kb_pcg_info;
+/* selects the solver (pcg may be NULL: defaults); resets the PCG state as LinearSolverPCG::init() does */
+int kb_set_linear_solver(kb_handle* h, int32_t kind, const kb_pcg_options* pcg);
+/* LinearSolverPCG::init() (linear_solver_pcg.h:53-59): _residual = -1 */
+int kb_pcg_init(kb_handle* h);
+int kb_get_pcg_info(kb_handle* h, kb_pcg_info* info);
+
 /* LinearSystemSolver::rhs (LinearSystemSolver.hpp:47). */
 int kb_get_rhs(kb_handle* h, double* rhs_out);
 /* Optimizer2::applyStateUpdate / revertLastStateUpdate (Optimizer2.cpp:290-318).

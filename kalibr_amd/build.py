@@ -7,7 +7,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 SRC = os.path.join(HERE, "csrc", "kb_capi.hip")
 SRC_SPLINE = os.path.join(HERE, "csrc", "kb_spline.hip")
 OUT = os.path.join(HERE, "libkalibr_hip.so")
-DEPS = ["kb_capi.hip", "kb_kernels.hip", "kb_device.h", "kb_math.h", "kb_spline.hip"]
+DEPS = ["kb_capi.hip", "kb_kernels.hip", "kb_pcg.hip", "kb_device.h", "kb_math.h", "kb_spline.hip"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wno-unused-result", "-Wno-unused-value"]
 

@@ -68,6 +68,16 @@ class MarginalInfo(C.Structure):
                 ("sv_log2_sum", C.c_double)]
 
 
+class PcgOptions(C.Structure):
+    _fields_ = [("tolerance", C.c_double), ("max_iterations", C.c_int32), ("absolute_tolerance", C.c_int32)]
+
+
+class PcgInfo(C.Structure):
+    _fields_ = [("iterations", C.c_int32), ("residual", C.c_double), ("d0", C.c_double)]
+
+
+SOLVER_SCHUR, SOLVER_PCG = 0, 1
+
 DBL_EPS = float(np.finfo(float).eps)
 
 
@@ -111,6 +121,9 @@ def lib():
         L.kb_comm_get_unique_id.argtypes = [C.c_void_p]
         L.kb_comm_init.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32]
         L.kb_selftest_mfma.argtypes = [dp]
+        L.kb_set_linear_solver.argtypes = [C.c_void_p, C.c_int32, C.POINTER(PcgOptions)]
+        L.kb_pcg_init.argtypes = [C.c_void_p]
+        L.kb_get_pcg_info.argtypes = [C.c_void_p, C.POINTER(PcgInfo)]
         L.kb_solve_marginal.argtypes = [C.c_void_p, C.POINTER(MarginalOptions), dp, C.POINTER(C.c_int),
                                         C.POINTER(MarginalInfo), dp, dp]
         L.kb_analyze_marginal.argtypes = [C.c_void_p, C.POINTER(MarginalOptions), C.POINTER(MarginalInfo), dp, dp]
@@ -221,6 +234,20 @@ class Solver:
         ok = C.c_int(0)
         _check(lib().kb_solve(self.h, _d(dx), C.byref(ok)))
         return bool(ok.value), dx
+
+    def set_linear_solver(self, kind="schur", tolerance=1e-6, max_iterations=-1, absolute_tolerance=True):
+        """kind "schur" (direct, default) or "pcg" (LinearSolverPCG: block-Jacobi PCG) for solve()."""
+        k = {"schur": SOLVER_SCHUR, "pcg": SOLVER_PCG}[kind]
+        o = PcgOptions(float(tolerance), int(max_iterations), int(absolute_tolerance))
+        _check(lib().kb_set_linear_solver(self.h, k, C.byref(o)))
+
+    def pcg_init(self):
+        _check(lib().kb_pcg_init(self.h))
+
+    def pcg_info(self):
+        i = PcgInfo()
+        _check(lib().kb_get_pcg_info(self.h, C.byref(i)))
+        return dict(iterations=i.iterations, residual=i.residual, d0=i.d0)
 
     def _minfo(self, inf, sv, V):
         return dict(rank=inf.rank, sweeps=inf.sweeps, tol=inf.tolerance, gap=inf.sv_gap, log2sum=inf.sv_log2_sum,

@@ -14,6 +14,7 @@
 
 #include "../../include/kalibr_hip.h"
 #include "kb_kernels.hip"
+#include "kb_pcg.hip"
 
 using namespace kb;
 
@@ -88,6 +89,14 @@ struct kb_handle {
   // build-kernel timing
   double build_ms = 0.0;
   double* marg_buf = nullptr;  // marginal solver outputs: V [C][C] | sv [C] | info [8]
+  // linear solver of kb_solve: KB_SOLVER_SCHUR (direct) or KB_SOLVER_PCG (LinearSolverPCG)
+  int solver_kind = KB_SOLVER_SCHUR;
+  kb_pcg_options pcg{1e-6, -1, 1};
+  double pcg_residual = -1.0;  // LinearSolverPCG::_residual (init(): -1)
+  kb_pcg_info pcg_info{0, 0.0, 0.0};
+  double* pcg_buf = nullptr;   // part [F][C+1] | part2 [F] | info [8]
+  int* pcg_cb = nullptr;       // [2][C] camera DV block start / size per column
+  unsigned* pcg_bar = nullptr;
 
   template <class T>
   int alloc(T** p, size_t n) {
@@ -558,9 +567,127 @@ int kb_set_constant_conditioner(kb_handle* h, double diag) {
   return 0;
 }
 
+// ---------------------------------------------------------------- block-Jacobi PCG (LinearSolverPCG)
+// projection / distortion DV sizes of a camera model (CameraDesignVariable: projection, distortion DVs)
+static void dv_split(int model, int* a, int* b) {
+  switch (model) {
+    case KB_OMNI_RADTAN: *a = 5, *b = 4; break;
+    case KB_EUCM: *a = 6, *b = 0; break;
+    case KB_OMNI: *a = 5, *b = 0; break;
+    case KB_DS: *a = 6, *b = 0; break;
+    case KB_PINHOLE_FOV: *a = 4, *b = 1; break;
+    default: *a = 4, *b = 4; break;  // pinhole-radtan, pinhole-equidistant
+  }
+}
+
+static size_t pcg_lds(int fpb, int C, int F) {
+  const size_t R = 6 * (size_t)fpb, nblk = (F + fpb - 1) / fpb, nrow = (C + nblk - 1) / nblk;
+  return sizeof(double) * (R * C + 54 * (size_t)fpb + 5 * R + 11 * (size_t)C + nrow * C) + sizeof(int) * 2 * (size_t)C;
+}
+
+static int run_pcg(kb_handle* h, int* ok) {
+  if (h->comm) return fail("kb_solve (PCG): not available on a sharded handle");
+  const int C = h->C, F = h->F;
+  if (!h->pcg_buf) {
+    if (h->alloc(&h->pcg_buf, (size_t)F * (C + 1) + F + 8) || h->alloc(&h->pcg_cb, 2 * (size_t)C) ||
+        h->alloc(&h->pcg_bar, 4))
+      return -1;
+    std::vector<int> cb(2 * C);
+    int c = 0;
+    auto block = [&](int m) {
+      for (int k = 0; k < m; ++k) {
+        cb[c + k] = c;
+        cb[C + c + k] = m;
+      }
+      c += m;
+    };
+    for (int i = 0; i < h->N; ++i) {
+      int a, b;
+      dv_split(h->d.model[i], &a, &b);
+      block(a);
+      if (b) block(b);
+    }
+    for (int j = 0; j < h->N - 1; ++j) {
+      block(3);
+      block(3);
+    }
+    if (c != C) return fail("kb_solve (PCG): camera DV blocks do not cover the camera columns");
+    KB_HIP(hipMemcpyAsync(h->pcg_cb, cb.data(), sizeof(int) * 2 * C, hipMemcpyHostToDevice, h->stream));
+  }
+  // frames per block: >= 64 blocks when there are enough frames, H_fc rows of the block within ~120 KB of LDS
+  int fpb = std::max(1, std::min(kPcgMaxFpb, (F + 63) / 64));
+  while (fpb > 1 && pcg_lds(fpb, C, F) > 120 * 1024) --fpb;
+  const size_t lds = pcg_lds(fpb, C, F);
+  const int nblk = (F + fpb - 1) / fpb;
+  int per_cu = 0, ncu = 0;
+  KB_HIP(hipFuncSetAttribute((const void*)k_pcg, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  KB_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)k_pcg, kPcgThreads, lds));
+  KB_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, h->device));
+  if (lds > 160 * 1024 || per_cu < 1 || nblk > per_cu * ncu)
+    return fail("kb_solve (PCG): problem too large for one co-resident grid");
+  KbPcg P;
+  P.lam2 = h->d.host_lambda * h->d.host_lambda;
+  P.tol = h->pcg.tolerance;
+  P.prev_residual = h->pcg_residual;
+  P.max_it = h->pcg.max_iterations < 0 ? h->ncols : h->pcg.max_iterations;
+  P.abs_tol = h->pcg.absolute_tolerance ? 1 : 0;
+  P.fpb = fpb;
+  P.nblk = nblk;
+  P.cb_start = h->pcg_cb;
+  P.cb_size = h->pcg_cb + C;
+  P.part = h->pcg_buf;
+  P.part2 = P.part + (size_t)F * (C + 1);
+  P.info = P.part2 + F;
+  P.bar = h->pcg_bar;
+  KB_HIP(hipMemsetAsync(h->pcg_bar, 0, sizeof(unsigned) * 4, h->stream));
+  KB_HIP(hipMemsetAsync(P.info, 0, sizeof(double) * 8, h->stream));
+  void* args[] = {(void*)&h->d, (void*)&P};
+  KB_HIP(hipLaunchCooperativeKernel((const void*)k_pcg, dim3(nblk), dim3(kPcgThreads), args, (unsigned)lds,
+                                    h->stream));
+  double info[8];
+  KB_HIP(hipMemcpyAsync(info, P.info, sizeof(info), hipMemcpyDeviceToHost, h->stream));
+  KB_HIP(hipStreamSynchronize(h->stream));
+  if (info[4] != 0.0) return fail("kb_solve (PCG): grid barrier timed out");
+  h->pcg_info.iterations = (int32_t)info[0];
+  h->pcg_info.residual = info[1];
+  h->pcg_info.d0 = info[2];
+  h->pcg_residual = info[1];  // _residual = 0.5 dn (linear_solver_pcg.hpp:127)
+  *ok = info[3] != 0.0 ? 1 : 0;
+  return 0;
+}
+
+int kb_set_linear_solver(kb_handle* h, int32_t kind, const kb_pcg_options* pcg) {
+  if (!h) return fail("kb_set_linear_solver: null");
+  if (kind != KB_SOLVER_SCHUR && kind != KB_SOLVER_PCG) return fail("kb_set_linear_solver: unknown solver");
+  if (kind == KB_SOLVER_PCG && h->comm) return fail("kb_set_linear_solver: PCG is not available on a sharded handle");
+  h->solver_kind = kind;
+  h->pcg = pcg ? *pcg : kb_pcg_options{1e-6, -1, 1};
+  h->pcg_residual = -1.0;
+  return 0;
+}
+
+int kb_pcg_init(kb_handle* h) {
+  if (!h) return fail("kb_pcg_init: null");
+  h->pcg_residual = -1.0;
+  return 0;
+}
+
+int kb_get_pcg_info(kb_handle* h, kb_pcg_info* info) {
+  if (!h || !info) return fail("kb_get_pcg_info: null");
+  *info = h->pcg_info;
+  return 0;
+}
+
 int kb_solve(kb_handle* h, double* dx_out, int* ok) {
   if (!h || !ok) return fail("kb_solve: null");
   KB_HIP(hipSetDevice(h->device));
+  if (h->solver_kind == KB_SOLVER_PCG) {
+    if (run_pcg(h, ok)) return -1;
+    if (*ok && dx_out)
+      KB_HIP(hipMemcpyAsync(dx_out, h->d.dx, sizeof(double) * h->ncols, hipMemcpyDeviceToHost, h->stream));
+    KB_HIP(hipStreamSynchronize(h->stream));
+    return 0;
+  }
   const int one = 1;
   KB_HIP(hipMemcpyAsync(&h->d.ctrl->solve_ok, &one, sizeof(int), hipMemcpyHostToDevice, h->stream));
   if (launch_schur(h, 0)) return -1;

@@ -56,6 +56,12 @@ void GpuLinearSystemSolver::initMatrixStructure(const CalibrationProblem& p, boo
         "kb_upload_observations");
   if ((int)p.state.size() != kb_state_size(h)) throw Exception("initMatrixStructure: state size mismatch");
   check(kb_set_state_flat(h, p.state.data()), "kb_set_state_flat");
+  if (_opt.linearSolver == "pcg") {
+    kb_pcg_options po{_opt.pcgTolerance, _opt.pcgMaxIterations, _opt.pcgAbsoluteTolerance ? 1 : 0};
+    check(kb_set_linear_solver(h, KB_SOLVER_PCG, &po), "kb_set_linear_solver");
+  } else if (_opt.linearSolver != "schur") {
+    throw Exception("GpuLinearSystemSolver: unknown linearSolver " + _opt.linearSolver);
+  }
   _JRows = 2 * (size_t)p.n_corners();
   _JCols = (size_t)kb_num_cols(h);
   _C = (size_t)kb_camera_cols(h);
@@ -142,6 +148,13 @@ double GpuLinearSystemSolver::applyStateUpdate(const std::vector<double>& dx) {
 }
 
 void GpuLinearSystemSolver::revertLastStateUpdate() { check(kb_revert(static_cast<kb_handle*>(_h)), "kb_revert"); }
+
+int GpuLinearSystemSolver::lastPcgIterations() const {
+  if (!_h || _opt.linearSolver != "pcg") return 0;
+  kb_pcg_info info{};
+  check(kb_get_pcg_info(static_cast<kb_handle*>(_h), &info), "kb_get_pcg_info");
+  return info.iterations;
+}
 
 std::vector<double> GpuLinearSystemSolver::state() const {
   std::vector<double> s((size_t)kb_state_size(static_cast<kb_handle*>(_h)));

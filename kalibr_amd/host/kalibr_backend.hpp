@@ -91,8 +91,15 @@ class LinearSystemSolver {
 };
 
 // ---------------------------------------------------------------- GPU solver over the C-ABI
+/// linearSolver: "schur" (frame-block Schur + camera-block LDL^T, the exact CHOLMOD replacement, default) or
+/// "pcg" (sparse_block_matrix LinearSolverPCG: block-Jacobi PCG, linear_solver_pcg.hpp:58-130, with its
+/// defaults tolerance 1e-6 / maxIter = rows / absoluteTolerance, linear_solver_pcg.h:39-47).
 struct GpuOptions {
   int device = 0;
+  std::string linearSolver = "schur";
+  double pcgTolerance = 1e-6;
+  int pcgMaxIterations = -1;
+  bool pcgAbsoluteTolerance = true;
 };
 
 /// LinearSystemSolver whose build / solve / update / cost run on one MI355X (kalibr_hip.h).  The
@@ -113,7 +120,9 @@ class GpuLinearSystemSolver : public LinearSystemSolver {
   void setConstantConditioner(double diag) override;
   void setConditioner(const std::vector<double>& diag) override;
   bool solveSystem(std::vector<double>& outDx) override;
-  std::string name() const override { return "kalibr_hip_schur_cholesky"; }
+  std::string name() const override {
+    return _opt.linearSolver == "pcg" ? "kalibr_hip_block_jacobi_pcg" : "kalibr_hip_schur_cholesky";
+  }
   const std::vector<double>& rhs() const override;
   double rhsJtJrhs() override;
   double applyStateUpdate(const std::vector<double>& dx) override;
@@ -123,6 +132,8 @@ class GpuLinearSystemSolver : public LinearSystemSolver {
   void setState(const std::vector<double>& s);
   size_t cameraCols() const { return _C; }
   void* handle() const { return _h; }
+  /// PCG iterations of the last solveSystem (0 with the direct solver)
+  int lastPcgIterations() const;
 
  private:
   void check(int rc, const char* what) const;

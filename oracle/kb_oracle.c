@@ -1265,6 +1265,183 @@ int kbo_dense_solve(const kbo_arrow* A, double conditioner, double* dx) {
 }
 
 /* ------------------------------------------------------------------ */
+/* block-Jacobi PCG on the arrow system (H + c^2 I) dx = g:              */
+/* sparse_block_matrix LinearSolverPCG::solve                            */
+/* (sparse_block_matrix/include/sparse_block_matrix/implementation/     */
+/*  linear_solver_pcg.hpp:58-130; defaults linear_solver_pcg.h:39-47).   */
+/* Preconditioner blocks are the design-variable blocks of the diagonal  */
+/* (_J = diag block inverse, :72-75): the camera DV blocks given by the  */
+/* caller, then per frame the rotation DV (3) and translation DV (3).    */
+/* ------------------------------------------------------------------ */
+
+/* y = (H + lam2 I) x on the arrow (the reference's mult(): diagonal blocks + upper blocks and their
+ * transposes, linear_solver_pcg.hpp:153-171 -- the same product) */
+static void arrow_mult(const kbo_arrow* A, double lam2, const double* x, double* y) {
+  const int C = A->C, F = A->F;
+  for (int p = 0; p < C; ++p) {
+    double s = lam2 * x[p];
+    for (int q = 0; q < C; ++q) s += A->Hcc[(size_t)p * C + q] * x[q];
+    y[p] = s;
+  }
+  for (int f = 0; f < F; ++f) {
+    const double* Hf = A->Hff + 36 * (size_t)f;
+    const double* Bf = A->Hfc + (size_t)6 * C * f;
+    const double* xf = x + C + 6 * f;
+    for (int a = 0; a < 6; ++a) {
+      double s = lam2 * xf[a];
+      for (int b = 0; b < 6; ++b) s += Hf[a * 6 + b] * xf[b];
+      for (int q = 0; q < C; ++q) s += Bf[a * C + q] * x[q];
+      y[C + 6 * f + a] = s;
+    }
+    for (int q = 0; q < C; ++q) {
+      double s = 0.0;
+      for (int a = 0; a < 6; ++a) s += Bf[a * C + q] * xf[a];
+      y[q] += s;
+    }
+  }
+}
+
+/* in-place inverse of an n x n block by Gauss-Jordan with partial pivoting; 0 if singular */
+static int block_inverse(double* M, int n) {
+  double Aug[6 * 12];
+  for (int r = 0; r < n; ++r)
+    for (int c = 0; c < 2 * n; ++c) Aug[r * 12 + c] = c < n ? M[r * n + c] : (c - n == r ? 1.0 : 0.0);
+  for (int k = 0; k < n; ++k) {
+    int piv = k;
+    for (int r = k + 1; r < n; ++r)
+      if (fabs(Aug[r * 12 + k]) > fabs(Aug[piv * 12 + k])) piv = r;
+    if (!(fabs(Aug[piv * 12 + k]) > 0.0)) return 0;
+    if (piv != k)
+      for (int c = 0; c < 2 * n; ++c) {
+        const double t = Aug[k * 12 + c];
+        Aug[k * 12 + c] = Aug[piv * 12 + c];
+        Aug[piv * 12 + c] = t;
+      }
+    const double inv = 1.0 / Aug[k * 12 + k];
+    for (int c = 0; c < 2 * n; ++c) Aug[k * 12 + c] *= inv;
+    for (int r = 0; r < n; ++r) {
+      if (r == k) continue;
+      const double m = Aug[r * 12 + k];
+      if (m != 0.0)
+        for (int c = 0; c < 2 * n; ++c) Aug[r * 12 + c] -= m * Aug[k * 12 + c];
+    }
+  }
+  for (int r = 0; r < n; ++r)
+    for (int c = 0; c < n; ++c) M[r * n + c] = Aug[r * 12 + n + c];
+  return 1;
+}
+
+int kbo_arrow_pcg(const kbo_arrow* A, double conditioner, int n_cam_blocks, const int* cam_block_size,
+                  const kbo_pcg_opts* o, double* x, kbo_pcg_info* info) {
+  const int C = A->C, F = A->F, n = C + 6 * F;
+  const double lam2 = conditioner * conditioner;
+  const int nb = n_cam_blocks + 2 * F;
+  int* bstart = (int*)malloc(sizeof(int) * (nb + 1));
+  int* bsize = (int*)malloc(sizeof(int) * nb);
+  int c = 0;
+  for (int b = 0; b < n_cam_blocks; ++b) {
+    bstart[b] = c;
+    bsize[b] = cam_block_size[b];
+    c += cam_block_size[b];
+  }
+  for (int b = n_cam_blocks; b < nb; ++b) {
+    bstart[b] = c;
+    bsize[b] = 3;
+    c += 3;
+  }
+  bstart[nb] = c;
+  int ok = (c == n);
+  /* _J: inverses of the diagonal DV blocks of H + lam2 I */
+  double* Jinv = (double*)malloc(sizeof(double) * 36 * (size_t)nb);
+  for (int b = 0; ok && b < nb; ++b) {
+    const int s = bstart[b], m = bsize[b];
+    double* M = Jinv + 36 * (size_t)b;
+    if (m < 1 || m > 6) {
+      ok = 0;
+      break;
+    }
+    for (int r = 0; r < m; ++r)
+      for (int q = 0; q < m; ++q) {
+        double v;
+        const int gr = s + r, gq = s + q;
+        if (gr < C)
+          v = A->Hcc[(size_t)gr * C + gq];
+        else {
+          const int f = (gr - C) / 6;
+          v = A->Hff[36 * (size_t)f + ((gr - C) % 6) * 6 + (gq - C) % 6];
+        }
+        M[r * m + q] = v + (r == q ? lam2 : 0.0);
+      }
+    ok = block_inverse(M, m);
+  }
+  double *r = (double*)malloc(sizeof(double) * n), *d = (double*)malloc(sizeof(double) * n);
+  double *q = (double*)malloc(sizeof(double) * n), *s = (double*)malloc(sizeof(double) * n);
+  int it = 0;
+  double dn = 0.0, d0 = 0.0;
+  if (ok) {
+    for (int p = 0; p < C; ++p) r[p] = A->gc[p];
+    for (int p = 0; p < 6 * F; ++p) r[C + p] = A->gf[p];
+    for (int p = 0; p < n; ++p) x[p] = 0.0;
+    /* multDiag(_J, r, d) */
+    for (int b = 0; b < nb; ++b) {
+      const int s0 = bstart[b], m = bsize[b];
+      const double* M = Jinv + 36 * (size_t)b;
+      for (int a = 0; a < m; ++a) {
+        double v = 0.0;
+        for (int k = 0; k < m; ++k) v += M[a * m + k] * r[s0 + k];
+        d[s0 + a] = v;
+      }
+    }
+    for (int p = 0; p < n; ++p) dn += r[p] * d[p];
+    d0 = o->tolerance * dn;
+    if (o->absolute_tolerance && o->prev_residual > 0.0 && o->prev_residual > d0) d0 = o->prev_residual;
+    const int max_it = o->max_iterations < 0 ? n : o->max_iterations;
+    for (it = 0; it < max_it; ++it) {
+      if (dn <= d0) break;
+      arrow_mult(A, lam2, d, q);
+      double dq = 0.0;
+      for (int p = 0; p < n; ++p) dq += d[p] * q[p];
+      if (!(dq > 0.0) || !isfinite(dq)) { /* breakdown: not positive definite (reported, the reference has no check) */
+        ok = 0;
+        break;
+      }
+      const double a = dn / dq;
+      for (int p = 0; p < n; ++p) {
+        x[p] += a * d[p];
+        r[p] -= a * q[p];
+      }
+      for (int b = 0; b < nb; ++b) {
+        const int s0 = bstart[b], m = bsize[b];
+        const double* M = Jinv + 36 * (size_t)b;
+        for (int e = 0; e < m; ++e) {
+          double v = 0.0;
+          for (int k = 0; k < m; ++k) v += M[e * m + k] * r[s0 + k];
+          s[s0 + e] = v;
+        }
+      }
+      const double dold = dn;
+      dn = 0.0;
+      for (int p = 0; p < n; ++p) dn += r[p] * s[p];
+      const double ba = dn / dold;
+      for (int p = 0; p < n; ++p) d[p] = s[p] + ba * d[p];
+    }
+  }
+  if (info) {
+    info->iterations = it;
+    info->residual = 0.5 * dn; /* _residual (:127) */
+    info->d0 = d0;
+  }
+  free(bstart);
+  free(bsize);
+  free(Jinv);
+  free(r);
+  free(d);
+  free(q);
+  free(s);
+  return ok;
+}
+
+/* ------------------------------------------------------------------ */
 /* state update: Optimizer2::applyStateUpdate (Optimizer2.cpp:290-307)  */
 /* ------------------------------------------------------------------ */
 

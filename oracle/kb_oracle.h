@@ -133,6 +133,24 @@ void kbo_marginal_solve(int C, const double* S, const double* b, const double* h
 int kbo_arrow_solve_ex(const kbo_arrow* A, double conditioner, int nthreads, double* dx, const kbo_marg_opts* marg,
                        kbo_marg_info* info);
 
+/* --- sparse_block_matrix LinearSolverPCG (block-Jacobi preconditioned CG, linear_solver_pcg.hpp:58-130) --- */
+typedef struct kbo_pcg_opts_s {
+  double tolerance;       /* _tolerance (default 1e-6): stop when r^T M^-1 r <= tolerance * (r0^T M^-1 r0) */
+  int max_iterations;     /* _maxIter (-1: number of rows) */
+  int absolute_tolerance; /* _absoluteTolerance (default true): d0 = max(d0, previous _residual) */
+  double prev_residual;   /* _residual of the previous solve (-1 after init()) */
+} kbo_pcg_opts;
+typedef struct kbo_pcg_info_s {
+  int iterations;
+  double residual; /* _residual = 0.5 r^T M^-1 r at exit */
+  double d0;       /* the stopping threshold used */
+} kbo_pcg_info;
+/* (H + conditioner^2 I) dx = g by PCG with the diagonal design-variable blocks as preconditioner:
+ * cam_block_size[n_cam_blocks] partitions the C camera columns; each frame contributes its rotation (3) and
+ * translation (3) DV blocks.  Returns 1, or 0 on a singular block / non-positive curvature. */
+int kbo_arrow_pcg(const kbo_arrow* A, double conditioner, int n_cam_blocks, const int* cam_block_size,
+                  const kbo_pcg_opts* o, double* dx, kbo_pcg_info* info);
+
 /* Optimizer2::applyStateUpdate / revert */
 double kbo_apply_update(const kbo_problem* P, double* state, const double* dx);
 

@@ -66,6 +66,27 @@ class _InfoBuf:
                     gap=self.s.gap, log2sum=self.s.log2sum)
 
 
+class _PcgOpts(C.Structure):
+    _fields_ = [("tolerance", C.c_double), ("max_iterations", C.c_int), ("absolute_tolerance", C.c_int),
+                ("prev_residual", C.c_double)]
+
+
+class _PcgInfo(C.Structure):
+    _fields_ = [("iterations", C.c_int), ("residual", C.c_double), ("d0", C.c_double)]
+
+
+# projection / distortion DV sizes per camera model (CameraDesignVariable's projection and distortion DVs,
+# CameraDesignVariable.hpp(impl):4-81; PinholeProjection.hpp:28, OmniProjection.hpp:26, ...)
+_DV_SPLIT = {0: (4, 4), 1: (5, 4), 2: (6,), 3: (5,), 4: (6,), 5: (4, 4), 6: (4, 1)}
+
+
+def pcg_camera_blocks(cam_model):
+    """Design-variable blocks of the camera columns: per camera projection (+ distortion), then per baseline the
+    rotation and translation DVs."""
+    sizes = [s for m in cam_model for s in _DV_SPLIT[int(m)]]
+    return sizes + [3, 3] * (len(cam_model) - 1)
+
+
 class _Srv(C.Structure):
     _fields_ = [("J_start", C.c_double), ("J_final", C.c_double), ("dx_final", C.c_double), ("dj_final", C.c_double),
                 ("iterations", C.c_int), ("failed_iterations", C.c_int), ("linear_solver_failure", C.c_int)]
@@ -98,6 +119,8 @@ def lib():
                                          C.POINTER(_MargInfo)]
         L.kbo_marginal_solve.argtypes = [C.c_int, dp, dp, dp, C.POINTER(_MargOpts), dp, C.POINTER(_MargInfo)]
         L.kbo_sym_eig.argtypes = [C.c_int, dp, dp, dp]
+        L.kbo_arrow_pcg.argtypes = [C.POINTER(_Arrow), C.c_double, C.c_int, ip, C.POINTER(_PcgOpts), dp,
+                                    C.POINTER(_PcgInfo)]
         _lib = L
     return _lib
 
@@ -187,6 +210,17 @@ class Oracle:
         buf = _InfoBuf(self.C)
         ok = lib().kbo_arrow_solve_ex(C.byref(arrow["_A"]), 0.0, 1, _d(dx), C.byref(opts), C.byref(buf.s))
         return bool(ok), dx, buf.result()
+
+    def solve_pcg(self, arrow, conditioner=0.0, tolerance=1e-6, max_iterations=-1, absolute_tolerance=True,
+                  prev_residual=-1.0):
+        """sparse_block_matrix LinearSolverPCG::solve on the arrow system: (ok, dx, info)."""
+        sizes = np.ascontiguousarray(pcg_camera_blocks(self.prob.cam_model), dtype=np.int32)
+        dx = np.zeros(self.ncols)
+        o = _PcgOpts(tolerance, max_iterations, int(absolute_tolerance), prev_residual)
+        info = _PcgInfo()
+        ok = lib().kbo_arrow_pcg(C.byref(arrow["_A"]), conditioner, sizes.size, _i(sizes), C.byref(o), _d(dx),
+                                 C.byref(info))
+        return bool(ok), dx, dict(iterations=info.iterations, residual=info.residual, d0=info.d0)
 
     def schur_partial(self, arrow, conditioner, f0, f1):
         S = np.zeros((self.C, self.C))

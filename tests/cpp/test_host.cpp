@@ -3,6 +3,9 @@
 //                                                 vs the oracle's own loop (kbo_optimize): must agree bitwise
 //   test_host gpu <problem.bin> <lm|gn> <maxIt> : host-driven Optimizer2 over GpuLinearSystemSolver, the
 //                                                 device-resident loop (optimizeOnDevice) and kbo_optimize
+//   test_host gpu-pcg <problem.bin> <lm|gn> <maxIt> : host-driven Optimizer2 over GpuLinearSystemSolver with the
+//                                                 block-Jacobi PCG solver (tight tolerance, then the
+//                                                 LinearSolverPCG defaults) vs kbo_optimize
 //   test_host incr-cpu <problem.bin> <delta> <maxIt> : IncrementalEstimator (one batch per frame) over an
 //                                                 oracle-backed marginal solver vs the oracle's own GN loop
 //                                                 (kbo_optimize with the marginal solve) + the addBatch rule
@@ -420,6 +423,33 @@ int main(int argc, char** argv) {
           "\"ref_J_final\": %.17g, \"cam_diff\": %.3e, \"frame_diff\": %.3e}\n",
           srv.iterations, ksrv.iterations, srv.failedIterations, ksrv.failed_iterations, srv.JFinal, ksrv.J_final,
           maxdiff(solver->state(), s_ref, 0, ncam), maxdiff(solver->state(), s_ref, ncam, s_ref.size()));
+      return 0;
+    }
+    if (mode == "gpu-pcg") {
+      GpuOptions go;
+      go.linearSolver = "pcg";
+      go.pcgTolerance = 1e-24;
+      go.pcgMaxIterations = 50000;
+      go.pcgAbsoluteTolerance = false;
+      auto gt = std::make_shared<GpuLinearSystemSolver>(go);
+      gt->initMatrixStructure(p, false);
+      opt.linearSystemSolver = gt;
+      opt.trustRegionPolicy = make_policy(pol);
+      SolutionReturnValue st = Optimizer2(opt).optimize();
+      const std::vector<double> s_t = gt->state();
+      auto gr = std::make_shared<GpuLinearSystemSolver>(GpuOptions{0, "pcg"});  // LinearSolverPCG defaults
+      gr->initMatrixStructure(p, false);
+      opt.linearSystemSolver = gr;
+      opt.trustRegionPolicy = make_policy(pol);
+      SolutionReturnValue sr = Optimizer2(opt).optimize();
+      std::printf(
+          "{\"name\": \"%s\", \"tight_iterations\": %d, \"ref_iterations\": %d, \"tight_failed\": %d, "
+          "\"ref_failed\": %d, \"tight_J\": %.17g, \"ref_J\": %.17g, \"tight_vs_ref_cam\": %.3e, "
+          "\"tight_vs_ref_frame\": %.3e, \"default_iterations\": %d, \"default_J\": %.17g, "
+          "\"default_lin_fail\": %d, \"default_vs_ref_cam\": %.3e}\n",
+          gt->name().c_str(), st.iterations, ksrv.iterations, st.failedIterations, ksrv.failed_iterations, st.JFinal,
+          ksrv.J_final, maxdiff(s_t, s_ref, 0, ncam), maxdiff(s_t, s_ref, ncam, s_ref.size()), sr.iterations, sr.JFinal,
+          sr.linearSolverFailure ? 1 : 0, maxdiff(gr->state(), s_ref, 0, ncam));
       return 0;
     }
     // gpu: host-driven loop over the per-call C-ABI

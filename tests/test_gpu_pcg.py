@@ -1,0 +1,149 @@
+"""GPU parity of the block-Jacobi PCG solver (kb_set_linear_solver(KB_SOLVER_PCG); sparse_block_matrix
+LinearSolverPCG::solve, linear_solver_pcg.hpp:58-130) against the oracle's restatement (kbo_arrow_pcg).
+
+Tolerances (FP64; the two sides sum dot products in different orders, so the CG iterates drift apart by a
+few ulps per iteration):
+  first 1 and 3 iterations                      dx rel 1e-9 of max|dx| against the oracle's PCG dx
+  reference tolerance (1e-6)                    same d0 (1e-9), iterations within 2 + 25%, error vs the direct
+                                                solve <= 3x the oracle's (CG rounding sensitivity, see test)
+  dx with a tight tolerance                     rel 1e-8 of max|dx| against the direct Schur solve
+"""
+import numpy as np
+import pytest
+
+from kalibr_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def capi():
+    from kalibr_amd import capi as K
+    return K
+
+
+def _rel(a, b):
+    return float(np.abs(np.asarray(a) - np.asarray(b)).max() / max(1e-300, np.abs(np.asarray(b)).max()))
+
+
+PROBLEMS = {
+    "c1": lambda: synth.make_config(1),
+    "c2_small": lambda: synth.make_config(2, n_frames=60),
+    "c2_ragged": lambda: synth.make_config(2, n_frames=90, p_view=0.5, seed_offset=7),
+    "c3_small": lambda: synth.make_config(3, n_frames=40),
+    "c4_mid": lambda: synth.make_config(4, n_frames=300, p_view=0.7),  # C = 106, several frames per block
+    "c6_small": lambda: synth.make_config(6, n_frames=40, p_view=0.8),
+}
+
+
+@pytest.mark.parametrize("name", list(PROBLEMS))
+@pytest.mark.parametrize("lam", [0.0, 10.0])
+def test_pcg_first_iterations_match_oracle(capi, oracle_mod, name, lam):
+    """The first CG iterates (matvec on the arrow, DV-block preconditioner, dots, updates) agree to rounding."""
+    p = PROBLEMS[name]()
+    o = oracle_mod.Oracle(p)
+    A = o.arrow(p.state_init)
+    g = capi.Solver(p)
+    g.set_state(p.state_init)
+    g.build()
+    g.set_constant_conditioner(lam)
+    for k in (1, 3):
+        g.set_linear_solver("pcg", tolerance=1e-30, max_iterations=k)
+        ok, dx = g.solve()
+        ok_o, dx_o, info_o = o.solve_pcg(A, lam, tolerance=1e-30, max_iterations=k)
+        assert ok and ok_o and g.pcg_info()["iterations"] == info_o["iterations"] == k
+        assert _rel(dx, dx_o) < 1e-9, k
+        assert abs(g.pcg_info()["residual"] - info_o["residual"]) <= 1e-8 * abs(info_o["residual"])
+
+
+@pytest.mark.parametrize("name", list(PROBLEMS))
+@pytest.mark.parametrize("lam", [0.0, 10.0])
+def test_pcg_reference_tolerance_matches_oracle(capi, oracle_mod, name, lam):
+    """At LinearSolverPCG's defaults (tol 1e-6, absolute mode, maxIter = rows) CG's loss of conjugacy makes two
+    correct implementations with different summation orders end at iterates up to ~1e-3 apart on these
+    ill-conditioned systems (measured: numpy vs the C oracle, same algorithm).  The bar is therefore the
+    solver's contract: same threshold d0, iteration count within 2 + 25 %, stopping test met, and an error against the
+    exact (direct) solution no worse than 3x the oracle's."""
+    p = PROBLEMS[name]()
+    o = oracle_mod.Oracle(p)
+    A = o.arrow(p.state_init)
+    g = capi.Solver(p)
+    g.set_state(p.state_init)
+    g.build()
+    g.set_linear_solver("pcg")
+    g.set_constant_conditioner(lam)
+    ok, dx = g.solve()
+    info = g.pcg_info()
+    ok_o, dx_o, info_o = o.solve_pcg(A, lam)
+    ok_x, dx_x = o.solve(A, lam)
+    assert ok and ok_o and ok_x
+    assert abs(info["d0"] - info_o["d0"]) <= 1e-9 * abs(info_o["d0"])
+    assert abs(info["iterations"] - info_o["iterations"]) <= 2 + 0.25 * info_o["iterations"], (info, info_o)
+    assert 2.0 * info["residual"] <= info["d0"] or info["iterations"] == g.ncols
+    err, err_o = _rel(dx, dx_x), _rel(dx_o, dx_x)
+    assert err <= 3.0 * err_o + 1e-12, (err, err_o)
+
+
+@pytest.mark.parametrize("name", ["c1", "c2_small", "c4_mid"])
+def test_pcg_tight_equals_direct(capi, name):
+    p = PROBLEMS[name]()
+    g = capi.Solver(p)
+    g.set_state(p.state_init)
+    g.build()
+    g.set_constant_conditioner(10.0)
+    ok_d, dx_d = g.solve()  # direct Schur (default)
+    g.set_linear_solver("pcg", tolerance=1e-26, max_iterations=20000, absolute_tolerance=False)
+    ok_p, dx_p = g.solve()
+    assert ok_d and ok_p
+    assert _rel(dx_p, dx_d) < 1e-8, g.pcg_info()
+
+
+def test_pcg_absolute_tolerance_carries_residual(capi, oracle_mod):
+    """_absoluteTolerance: the second solve stops at max(tol dn0, previous _residual); init() resets it."""
+    p = PROBLEMS["c2_small"]()
+    o = oracle_mod.Oracle(p)
+    A = o.arrow(p.state_init)
+    g = capi.Solver(p)
+    g.set_state(p.state_init)
+    g.build()
+    g.set_linear_solver("pcg", tolerance=1e-6)
+    g.set_constant_conditioner(1.0)
+    g.solve()
+    r1 = g.pcg_info()["residual"]
+    g.set_constant_conditioner(10.0)
+    ok, dx = g.solve()
+    info = g.pcg_info()
+    ok_o, dx_o, info_o = o.solve_pcg(A, 10.0, prev_residual=r1)
+    assert ok and ok_o
+    assert abs(info["d0"] - info_o["d0"]) <= 1e-9 * abs(info_o["d0"])
+    assert abs(info["iterations"] - info_o["iterations"]) <= 2
+    g.pcg_init()
+    g.solve()
+    _, _, fresh = o.solve_pcg(A, 10.0)
+    assert abs(g.pcg_info()["d0"] - fresh["d0"]) <= 1e-9 * abs(fresh["d0"])
+
+
+def test_pcg_host_loop_reaches_direct_optimum(capi, oracle_mod):
+    """LM driven through the per-call API with the PCG solver (the host Optimizer2 path): with a tight PCG
+    tolerance the iterates follow the direct solve and the optimum agrees within 1e-6."""
+    p = synth.make_config(1, n_frames=30)
+    o = oracle_mod.Oracle(p)
+    g = capi.Solver(p)
+    g.set_state(p.state_init)
+    g.set_linear_solver("pcg", tolerance=1e-24, max_iterations=20000, absolute_tolerance=False)
+    J = g.eval_cost()
+    lam = 1e-3
+    for _ in range(30):
+        g.build()
+        g.set_constant_conditioner(lam)
+        ok, dx = g.solve()
+        assert ok
+        g.apply_update(dx)
+        J1 = g.eval_cost()
+        if J1 < J:
+            J, lam = J1, lam / 3
+        else:
+            g.revert()
+            lam *= 10
+    st_o, _ = o.optimize(p.state_init, policy="lm", lambda0=10.0, max_iterations=200, eps_x=1e-12, eps_j=1e-12)
+    assert np.abs(g.get_state() - st_o).max() < 1e-6

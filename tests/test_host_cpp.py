@@ -101,3 +101,17 @@ def test_incremental_estimator_gpu_matches_oracle(driver, tmp_path, cfg, frames,
     assert r["iters"] == r["ref_iters"], r
     assert r["gain_rel"] < 1e-6, r
     assert r["cam_diff"] < 1e-6 and r["frame_diff"] < 1e-6, r
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg,frames,policy", [(1, 20, "lm"), (2, 24, "lm")])
+def test_host_gpu_pcg_loop(driver, tmp_path, cfg, frames, policy):
+    """Optimizer2 over GpuLinearSystemSolver with the block-Jacobi PCG solver: converged tightly it reproduces
+    the oracle's (direct-solve) iteration sequence; at LinearSolverPCG's defaults (tol 1e-6) the inexact steps
+    still drive LM to the same optimum region without a linear-solver failure."""
+    p = synth.make_config(cfg, n_frames=frames)
+    r = run(driver, tmp_path, "gpu-pcg", p, policy, 30)
+    assert r["name"] == "kalibr_hip_block_jacobi_pcg", r
+    assert r["tight_iterations"] == r["ref_iterations"] and r["tight_failed"] == r["ref_failed"], r
+    assert r["tight_vs_ref_cam"] < 1e-6 and r["tight_vs_ref_frame"] < 1e-6, r
+    assert r["default_lin_fail"] == 0 and r["default_J"] <= 1.05 * r["ref_J"], r

@@ -250,3 +250,40 @@ def test_lm_all_camera_models(oracle_mod):
         a, b = fcol[int(m)]
         assert np.abs(intr[i, a:b] / tru[i, a:b] - 1).max() < 0.015, (m, intr[i], tru[i])
         assert np.abs(intr[i, b:b + 2] - tru[i, b:b + 2]).max() < 3.0, (m, intr[i], tru[i])
+
+
+# ---- sparse_block_matrix LinearSolverPCG restatement (linear_solver_pcg.hpp:58-130) ----
+@pytest.mark.parametrize("lam", [0.0, 10.0])
+def test_pcg_tight_tolerance_equals_dense(oracle_mod, small, lam):
+    o = oracle_mod.Oracle(small)
+    A = o.arrow(small.state_init)
+    ok_d, dx_d = o.solve(A, lam, dense=True)
+    ok_p, dx_p, info = o.solve_pcg(A, lam, tolerance=1e-26, absolute_tolerance=False, max_iterations=20000)
+    assert ok_d and ok_p
+    assert np.abs(dx_p - dx_d).max() <= 1e-8 * np.abs(dx_d).max()
+    assert 0 < info["iterations"] <= 20000
+
+
+def test_pcg_reference_stopping_rule(oracle_mod, small):
+    """dn <= tol * dn0, and with _absoluteTolerance the previous solve's _residual raises the threshold."""
+    o = oracle_mod.Oracle(small)
+    A = o.arrow(small.state_init)
+    ok, dx, i1 = o.solve_pcg(A, 10.0, tolerance=1e-6)
+    assert ok and i1["residual"] <= 0.5 * i1["d0"] + 1e-300
+    # a previous residual above tol * dn0 becomes the threshold and stops the solve earlier
+    _, _, i2 = o.solve_pcg(A, 10.0, tolerance=1e-6, prev_residual=1e3 * i1["d0"])
+    assert i2["d0"] == 1e3 * i1["d0"] and i2["iterations"] <= i1["iterations"]
+    # not in absolute mode: ignored
+    _, _, i3 = o.solve_pcg(A, 10.0, tolerance=1e-6, prev_residual=1e3 * i1["d0"], absolute_tolerance=False)
+    assert i3["d0"] == i1["d0"] and i3["iterations"] == i1["iterations"]
+    # maxIter caps the loop
+    _, _, i4 = o.solve_pcg(A, 10.0, tolerance=1e-30, max_iterations=3)
+    assert i4["iterations"] == 3
+
+
+def test_pcg_preconditioner_blocks(oracle_mod):
+    """camera DV blocks: projection (+ distortion) per camera model, then rotation / translation per baseline"""
+    assert oracle_mod.pcg_camera_blocks([synth.PINHOLE_RADTAN, synth.PINHOLE_RADTAN]) == [4, 4, 4, 4, 3, 3]
+    assert oracle_mod.pcg_camera_blocks([synth.OMNI_RADTAN, synth.EUCM, synth.PINHOLE_FOV]) == [5, 4, 6, 4, 1, 3, 3, 3, 3]
+    p = synth.make_config(3, n_frames=4)
+    assert sum(oracle_mod.pcg_camera_blocks(p.cam_model)) == p.cam_cols
