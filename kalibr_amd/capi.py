@@ -23,6 +23,8 @@ EXPORTS = [
     "kb_set_constant_conditioner", "kb_solve", "kb_get_rhs", "kb_apply_update", "kb_revert", "kb_get_normal_blocks",
     "kb_optimize", "kb_get_trace", "kb_run_gn_iterations", "kb_build_kernel_stats", "kb_comm_get_unique_id",
     "kb_comm_init", "kb_selftest_mfma", "kb_solve_marginal", "kb_analyze_marginal",
+    # block-Jacobi PCG (LinearSolverPCG)
+    "kb_set_linear_solver", "kb_pcg_init", "kb_get_pcg_info",
     # configs[4]: B-spline pose trajectory + IMU
     "kb_sp_create", "kb_sp_destroy", "kb_sp_upload", "kb_sp_state_size", "kb_sp_num_cols", "kb_sp_camera_cols",
     "kb_sp_set_state", "kb_sp_get_state", "kb_sp_eval_cost", "kb_sp_build", "kb_sp_set_constant_conditioner",
