@@ -1,0 +1,124 @@
+// calibration_io.hpp -- the data formats either side of the hot path:
+//   in:  AprilGrid target geometry + GridCalibrationTargetObservation records grouped in synchronized sets,
+//        packed into the device problem exactly as CalibrateMultiCameraRig creates its terms;
+//   out: the calibration as ROS CameraInfo / TransformStamped / TFMessage YAML, as kalibr_calibrate_cameras
+//        exports it.
+// Paths are relative to the reference repository.  Target detection (AprilTags, OpenCV), the intrinsics
+// initialisers and PnP (estimateTransformation) are not rebuilt: an observation carries its T_t_c when the
+// caller has one, as the reference's observation does after estimateTransformation.
+#pragma once
+
+#include <array>
+#include <cstddef>
+#include <cstdint>
+#include <optional>
+#include <string>
+#include <vector>
+
+#include "kalibr_backend.hpp"
+
+namespace kalibr_amd {
+namespace io {
+
+/// sm::kinematics::Transformation: JPL quaternion q = (x, y, z, w) of C_a_b and t_a_b_a
+/// (Schweizer-Messer/sm_kinematics/src/Transformation.cpp).
+struct Transformation {
+  std::array<double, 4> q{0.0, 0.0, 0.0, 1.0};
+  std::array<double, 3> t{0.0, 0.0, 0.0};
+  /// operator* (Transformation.cpp:95-98): q = qplus(q_a, q_b), t = C(q_a) t_b + t_a
+  Transformation operator*(const Transformation& rhs) const;
+  /// the rotation matrix (quat2r, quaternion_algebra.cpp:77-101), row-major
+  std::array<double, 9> C() const;
+  /// Transformation(T) (Transformation.cpp:24-29): q = r2quat(C) (canonical sign, w >= 0)
+  static Transformation fromMatrix(const std::array<double, 9>& C, const std::array<double, 3>& t);
+};
+
+/// GridCalibrationTargetAprilgrid geometry (aslam_cv/aslam_cameras_april/src/GridCalibrationTargetAprilgrid.cpp:
+/// 29-32, 83-95): 2 tagRows x 2 tagCols corners, row-major index r * cols + c, z = 0.
+struct AprilgridTarget {
+  size_t tagRows = 5, tagCols = 6;  // kalibr2_ros/calibration_config.yaml:1-6 (6 x 5 tags)
+  double tagSize = 0.088, tagSpacing = 0.2954;
+  size_t rows() const { return 2 * tagRows; }
+  size_t cols() const { return 2 * tagCols; }
+  size_t size() const { return rows() * cols(); }
+  std::vector<double> points() const;  // [size][3]
+};
+
+/// GridCalibrationTargetObservation (aslam_cv/aslam_cameras/include/aslam/cameras/
+/// GridCalibrationTargetObservation.hpp:46-150): row-major image points of every target corner, a success
+/// flag per corner, the image size and (once estimateTransformation ran) T_t_c.
+struct GridObservation {
+  std::vector<double> points;    // [target size][2]
+  std::vector<uint8_t> success;  // [target size]
+  size_t imRows = 0, imCols = 0;
+  std::optional<Transformation> T_t_c;
+  double time = 0.0;
+
+  explicit GridObservation(size_t targetSize = 0) : points(2 * targetSize, 0.0), success(targetSize, 0) {}
+  /// imagePoint(i, out): false if corner i was not seen
+  bool imagePoint(size_t i, double out[2]) const;
+  /// updateImagePoint(i, p): sets the point and marks it seen
+  void updateImagePoint(size_t i, double u, double v);
+  /// removeImagePoint(i)
+  void removeImagePoint(size_t i);
+  /// getCornersIdx: indices of the seen corners; returns their count
+  unsigned getCornersIdx(std::vector<unsigned>& idx) const;
+  bool hasSuccessfulObservation() const;
+};
+
+/// one synchronized set: an optional observation per camera (CalibrationTools.hpp:28)
+using SyncedSet = std::vector<std::optional<GridObservation>>;
+
+/// getTargetPoseGuess (CalibrationTools.hpp:315-355): T_t_c of the camera with the most corners, carried to
+/// camera 0 as std::accumulate(baselines[0 .. max), T_t_cN, *) -- i.e. T_t_cN * B_0 * ... * B_{max-1}, the
+/// reference's multiplication order.  Throws if that observation has no T_t_c.
+Transformation targetPoseGuess(const SyncedSet& set, const std::vector<Transformation>& baselineGuesses);
+
+/// CalibrateMultiCameraRig's problem (CalibrationTools.hpp:376-414): intrinsics DVs, baseline DVs, one target
+/// pose DV per synchronized set (initialised by targetPoseGuess, stored as T_f = T_t_c0), one ReprojectionError
+/// per seen corner of every present observation (CameraCalibrator.hpp:203-265 loops over the target corners in
+/// index order).  intrinsics: [n_cams][KB_MAX_INTR] in the state layout of include/kalibr_hip.h.
+backend::CalibrationProblem buildRigProblem(const std::vector<int32_t>& camModels,
+                                            const std::vector<double>& intrinsics, const AprilgridTarget& target,
+                                            const std::vector<SyncedSet>& sets,
+                                            const std::vector<Transformation>& baselineGuesses);
+
+// ---------------------------------------------------------------- export (kalibr2_ros)
+/// CameraCalibratorBase::CameraInfoParams (kalibr2/include/kalibr2/CameraCalibrator.hpp:156-191)
+struct CameraInfoParams {
+  double fx = 0, fy = 0, cx = 0, cy = 0;
+  std::vector<double> d;
+};
+CameraInfoParams cameraInfoParams(int32_t camModel, const double* intr);
+/// Kalibr2 model name of a kb_camera_model ("pinhole-radtan", "omni-radtan", "eucm-none", "omni-none",
+/// "ds-none", "pinhole-equi", "pinhole-fov"; kalibr2_ros Config.cpp model strings)
+std::string kalibrModelName(int32_t camModel);
+/// ToROSDistortionModel (KalibrToROSConverter.hpp:26-44, KalibrToROSConverter.cpp:5-13); "unknown" fallback
+std::string toRosDistortionModel(const std::string& kalibrModel);
+
+/// geometry_msgs TransformStamped as TransformationToROS fills it (KalibrToROSConverter.cpp:15-37)
+struct TransformStamped {
+  std::string frame_id, child_frame_id;
+  std::array<double, 3> translation{};
+  std::array<double, 4> rotation{};  // x, y, z, w = the JPL quaternion fields, as the reference copies them
+};
+TransformStamped transformationToRos(const Transformation& T, const std::string& parent, const std::string& child);
+
+/// CalibratorToYAML (ROSToYAMLConverter.cpp:32-75): CameraInfo in rosidl block style
+std::string cameraInfoYaml(const CameraInfoParams& p, const std::string& kalibrModel, const std::string& frameId,
+                           size_t width, size_t height);
+/// transformStampedToYAML / tfMessageToYAML (ROSToYAMLConverter.cpp:14-30)
+std::string transformStampedYaml(const TransformStamped& tf);
+std::string tfMessageYaml(const std::vector<TransformStamped>& tfs);
+
+/// The export step of kalibr_calibrate_cameras (CalibrateCameras.cpp:313-356) from a solved flat state:
+/// calibration_<camera>.yaml per camera, then transform_<cam0>_to_<cam1>.yaml (one baseline) or
+/// camera_chain_transforms.yaml (several); each baseline re-read through Transformation(T) as the reference
+/// does.  Returns the written paths.
+std::vector<std::string> exportCalibration(const std::string& outputDir, const std::vector<std::string>& cameraNames,
+                                           const std::vector<int32_t>& camModels,
+                                           const std::vector<std::pair<size_t, size_t>>& imageSizes,
+                                           const std::vector<double>& state);
+
+}  // namespace io
+}  // namespace kalibr_amd

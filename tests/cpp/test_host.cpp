@@ -11,6 +11,8 @@
 //                                                 (kbo_optimize with the marginal solve) + the addBatch rule
 //   test_host incr-gpu <problem.bin> <delta> <maxIt> : IncrementalEstimator over GpuMarginalLinearSolver vs
 //                                                 over the oracle-backed marginal solver
+//   test_host io <problem.bin> <outdir> 0       : observation records -> buildRigProblem (must rebuild the packed
+//                                                 problem), targetPoseGuess per frame, exportCalibration YAML
 // Prints one JSON line.  The oracle is test infrastructure only (oracle/kb_oracle.h).
 #include <cfloat>
 #include <cmath>
@@ -21,6 +23,7 @@
 #include <string>
 #include <vector>
 
+#include "calibration_io.hpp"
 #include "kalibr_backend.hpp"
 #include "kb_oracle.h"
 
@@ -372,6 +375,70 @@ static double maxdiff(const std::vector<double>& a, const std::vector<double>& b
   return m;
 }
 
+// io: per-frame synchronized sets of GridObservation records re-created from the packed problem, each observation
+// carrying its camera's T_t_c of the problem's state (T_t_ci = T_f (B_{i-1}..B_0)^-1); buildRigProblem must give
+// back the same term arrays; the target pose guesses and the exported YAML are checked by the Python side.
+static int run_io(const CalibrationProblem& p, const std::string& outdir) {
+  namespace io = kalibr_amd::io;
+  const size_t N = p.n_cams(), K = p.n_target();
+  io::AprilgridTarget tgt;
+  const std::vector<double> pts = tgt.points();
+  double tdiff = pts.size() == p.target.size() ? 0.0 : 1e300;
+  for (size_t q = 0; q < pts.size() && q < p.target.size(); ++q) tdiff = std::max(tdiff, std::fabs(pts[q] - p.target[q]));
+  auto pose = [&](size_t off) {
+    io::Transformation T;
+    for (int k = 0; k < 4; ++k) T.q[k] = p.state[off + k];
+    for (int k = 0; k < 3; ++k) T.t[k] = p.state[off + 4 + k];
+    return T;
+  };
+  auto inverse = [](const io::Transformation& T) {
+    io::Transformation I;
+    I.q = {-T.q[0], -T.q[1], -T.q[2], T.q[3]};
+    const auto R = T.C();
+    for (int r = 0; r < 3; ++r) I.t[r] = -(R[r] * T.t[0] + R[3 + r] * T.t[1] + R[6 + r] * T.t[2]);
+    return I;
+  };
+  const size_t offb = N * KBO_MAX_INTR, offf = offb + 7 * (N - 1);
+  std::vector<io::Transformation> base;
+  for (size_t j = 0; j + 1 < N; ++j) base.push_back(pose(offb + 7 * j));
+  std::vector<io::SyncedSet> sets(p.n_frames, io::SyncedSet(N));
+  for (int v = 0; v < p.n_views(); ++v) {
+    const size_t f = p.view_frame[v], i = p.view_cam[v];
+    io::GridObservation o(K);
+    for (uint32_t k = p.view_offset[v]; k < p.view_offset[v + 1]; ++k)
+      o.updateImagePoint(p.corner_id[k], p.y[2 * k], p.y[2 * k + 1]);
+    io::Transformation chain;  // B_{i-1} .. B_0
+    for (size_t j = 0; j < i; ++j) chain = base[j] * chain;
+    o.T_t_c = pose(offf + 7 * f) * inverse(chain);
+    sets[f][i] = o;
+  }
+  std::vector<double> intr(p.state.begin(), p.state.begin() + offb);
+  const CalibrationProblem q = io::buildRigProblem(p.cam_model, intr, tgt, sets, base);
+  std::string guess = "[";
+  for (int f = 0; f < q.n_frames; ++f) {
+    char buf[512];
+    const double* g = q.state.data() + offf + 7 * f;
+    std::snprintf(buf, sizeof buf, "%s[%.17g, %.17g, %.17g, %.17g, %.17g, %.17g, %.17g]", f ? ", " : "", g[0], g[1], g[2],
+                  g[3], g[4], g[5], g[6]);
+    guess += buf;
+  }
+  guess += "]";
+  std::vector<std::string> names;
+  std::vector<std::pair<size_t, size_t>> sizes;
+  for (size_t i = 0; i < N; ++i) {
+    names.push_back("cam" + std::to_string(i));
+    sizes.emplace_back(1280, 1024);
+  }
+  const auto files = io::exportCalibration(outdir, names, p.cam_model, sizes, p.state);
+  std::printf(
+      "{\"target_diff\": %.3e, \"same_views\": %d, \"same_corners\": %d, \"same_y\": %d, \"same_intr_base\": %d, "
+      "\"n_frames\": %d, \"n_files\": %zu, \"guess\": %s}\n",
+      tdiff, q.view_frame == p.view_frame && q.view_cam == p.view_cam && q.view_offset == p.view_offset,
+      q.corner_id == p.corner_id, q.y == p.y, std::equal(p.state.begin(), p.state.begin() + offf, q.state.begin()),
+      q.n_frames, files.size(), guess.c_str());
+  return 0;
+}
+
 int main(int argc, char** argv) {
   if (argc < 5) {
     std::fprintf(stderr, "usage: test_host cpu|gpu problem.bin lm|gn maxIt\n");
@@ -381,6 +448,7 @@ int main(int argc, char** argv) {
   const int maxIt = std::atoi(argv[4]);
   try {
     CalibrationProblem p = load(argv[2]);
+    if (mode == "io") return run_io(p, argv[3]);
     if (mode == "incr-cpu" || mode == "incr-gpu") {
       const double delta = std::atof(argv[3]);
       LinearSolverOptions lo;
