@@ -51,7 +51,7 @@ def build_host(force=False):
 def build_stamps():
     """Diagnostic variant with per-phase s_memrealtime stamps (tools/diag_stamps.py only)."""
     out = os.path.join(HERE, "libkalibr_hip_stamps.so")
-    subprocess.run([HIPCC] + FLAGS + ["-DKB_STAMPS", "-o", out + ".tmp", SRC, "-lrccl"], check=True)
+    subprocess.run([HIPCC] + FLAGS + ["-DKB_STAMPS", "-o", out + ".tmp", SRC, SRC_SPLINE, "-lrccl"], check=True)
     os.replace(out + ".tmp", out)
     return out
 
