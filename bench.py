@@ -13,7 +13,10 @@ configs[4] (--config 5): 2-camera rig + IMU on a cubic B-spline pose trajectory,
 IMU, 50 knots/s; one GPU, one step = one GN pass of the spline system (frames kernel,
 node assembly, block cyclic reduction, Schur onto the camera/IMU block, update, cost).
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|5]
+configs[3] (--config 4): the north-star problem, 8-camera pinhole-radtan rig x 2000 frames; N>1 shards its frames
+over the ranks (strong scaling: 2000 / N frames per rank, "scaling": "strong").
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|4|5]
 """
 import argparse
 import json
@@ -55,7 +58,7 @@ def pmc_traffic_bytes(match):
     return None
 
 
-def cpu_baseline(prob, seconds_budget=12.0, threads=None):
+def cpu_baseline(prob, seconds_budget=12.0, threads=None, label="configs[1] (full 500-frame problem"):
     """Oracle (our C restatement of the reference CPU flow: threaded per-term evaluation into CCS J^T,
     serial rhs SpMV, J^T J, frame-first sparse Cholesky) timed on host cores."""
     from oracle import oracle as O
@@ -65,7 +68,7 @@ def cpu_baseline(prob, seconds_budget=12.0, threads=None):
     n = max(2, min(200, int(seconds_budget / max(t1, 1e-4))))
     t = o.time_gn(prob.state_init, n, threads)
     return {"value": n / t, "unit": "iterations/s", "cores": threads, "kind": "port",
-            "sample": f"{n} GN iterations of configs[1] (full 500-frame problem, {prob.n_corners} corners), "
+            "sample": f"{n} GN iterations of {label}, {prob.n_corners} corners), "
                       f"oracle/kb_oracle.c kbo_time_gn, {threads} threads"}
 
 
@@ -123,7 +126,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", type=int, default=2, choices=[2, 5])
+    ap.add_argument("--config", type=int, default=2, choices=[2, 4, 5])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
     if args.config == 5:
@@ -148,9 +151,15 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("gloo", init_method="env://")  # id exchange + host barrier only
 
-    full = synth.make_problem(synth.CONFIGS[2]["models"], FRAMES_PER_RANK * world, seed=20261015 + 2,
-                              name=synth.CONFIGS[2]["name"])
-    shard = full.frame_slice(rank * FRAMES_PER_RANK, (rank + 1) * FRAMES_PER_RANK) if world > 1 else full
+    strong = args.config == 4
+    if strong:  # configs[3]: one 2000-frame problem, frames split over the ranks
+        full = synth.make_config(4)
+        fpr = (full.n_frames + world - 1) // world
+    else:  # configs[1] per rank: a 2-camera rig of 500 * world frames, 500 per rank
+        full = synth.make_problem(synth.CONFIGS[2]["models"], FRAMES_PER_RANK * world, seed=20261015 + 2,
+                                  name=synth.CONFIGS[2]["name"])
+        fpr = FRAMES_PER_RANK
+    shard = full.frame_slice(rank * fpr, min(full.n_frames, (rank + 1) * fpr)) if world > 1 else full
     g = capi.Solver(shard, device=local)
     g.set_state(shard.state_init)
     if world > 1:
@@ -173,16 +182,19 @@ def main():
     # dominant kernel (k_build) timing with HIP events on the handle's stream, inside GN passes
     build_ms, bytes_per, flops_per = g.build_kernel_stats()
     achieved = bytes_per / (build_ms * 1e-3) / 1e9
-    pmc = pmc_traffic_bytes(is_build_kernel) if world == 1 else None
+    pmc = pmc_traffic_bytes(is_build_kernel) if world == 1 and not strong else None  # PMC summary is of configs[1]
 
     if rank == 0:
-        value = world * args.steps / wall
+        # weak: every rank iterates its own configs[1]-sized problem; strong: all ranks iterate one problem
+        value = (1 if strong else world) * args.steps / wall
+        workload = ("configs[3]: 8-cam pinhole-radtan rig, 2000 frames sharded over the GPUs, 6x5 AprilGrid"
+                    if strong else "configs[1]: 2-cam stereo pinhole-radtan, 500 frames/GPU, 6x5 AprilGrid, p_view=1")
         out = {
             "metric": METRIC, "value": value, "unit": "iterations/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": 1e3 * wall / args.steps, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-            "config": {"workload": "configs[1]: 2-cam stereo pinhole-radtan, 500 frames/GPU, 6x5 AprilGrid, p_view=1",
-                       "frames_per_gpu": FRAMES_PER_RANK, "cameras": 2, "corners_per_gpu": shard.n_corners,
+            "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "config": {"workload": workload,
+                       "frames_per_gpu": shard.n_frames, "cameras": full.n_cams, "corners_per_gpu": shard.n_corners,
                        "jacobian_cols": full.total_cols, "camera_block": full.cam_cols, "policy": "gauss_newton",
                        "parallelism": f"frame-sharded x{world}"},
             "roofline": {"bound": "hbm", "kernel": "k_build", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -194,7 +206,11 @@ def main():
                          "fp64_tflops": flops_per / (build_ms * 1e-3) / 1e12},
         }
         if not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(full if world == 1 else full.frame_slice(0, FRAMES_PER_RANK))
+            if strong:  # the whole north-star problem on the host cores (a few iterations: ~10 s each at 16 threads)
+                out["cpu_baseline"] = cpu_baseline(full, seconds_budget=20.0,
+                                                   label="configs[3] (full 8-cam 2000-frame problem")
+            else:
+                out["cpu_baseline"] = cpu_baseline(full if world == 1 else full.frame_slice(0, FRAMES_PER_RANK))
             out["speedup_vs_cpu_baseline"] = value / out["cpu_baseline"]["value"]
         print(json.dumps(out))
     if dist:
