@@ -161,11 +161,13 @@ def test_run_gn_full_size_properties(capi):
     assert np.isfinite(J1) and J1 < 2.0 * p.n_corners * 2 * 0.09
 
 
-def test_comm_path_single_rank_is_bitwise_identical(capi):
+@pytest.mark.parametrize("name", ["c4_small", "c2_small"])
+def test_comm_path_single_rank_is_bitwise_identical(capi, name):
     """The sharded code path (stage-2 column sum, RCCL all-reduce of [camera sums | Schur sums] and of the
     cost/step statistics, separate policy kernel) run over a 1-rank communicator must reproduce the
-    single-GPU path bit for bit (same fixed reduction order)."""
-    p = PROBLEMS["c4_small"]()
+    single-GPU path bit for bit (same fixed reduction order).  c4_small (C = 106) all-reduces the finished
+    column sums; c2_small (C = 22, the bench's per-rank rig) all-reduces the 8 stage-1 rows."""
+    p = PROBLEMS[name]()
     a = capi.Solver(p)
     a.set_state(p.state_init)
     ra = a.optimize()
