@@ -206,6 +206,10 @@ typedef struct {
   const double* imu_gyro; /* [n_imu][3] */
   const double* imu_acc;  /* [n_imu][3] */
   double sigma_gyro, sigma_acc;
+  /* optional BSplineMotionError (aslam_splines BSplineMotionError.hpp:29-160): cost c^T Q c with
+   * Q = curveQuadraticIntegralSparse(W, order) (BSpline.cpp:1585-1622); NULL = no motion term */
+  const double* motion_W; /* [6][6] symmetric */
+  int motion_order;       /* errorTermOrder (BSplineMotionError default 2: acceleration) */
 } kbo_sp_problem;
 
 typedef struct {
@@ -241,6 +245,10 @@ int kbo_sp_dense_solve(const kbo_sp_system* A, double lambda, double* dx);
 double kbo_sp_apply_update(const kbo_sp_problem* P, double* st, const double* dx);
 int kbo_sp_optimize(const kbo_sp_problem* P, double* st, const kbo_options* o, kbo_srv* srv, double* trace,
                     int trace_cap);
+/* scalar band of the motion quadratic form: q[k][d] = int b_k^(m) b_(k+d)^(m) dt (d = 0..order-1), so that
+ * Q_(k,k+d) = q[k][d] W; returns 0 if P has no motion term */
+int kbo_sp_motion_band(const kbo_sp_problem* P, double* q);
+double kbo_sp_motion_cost(const kbo_sp_problem* P, const double* st);
 double kbo_sp_time_gn(const kbo_sp_problem* P, double* st, int n_iter, int nthreads);
 
 #ifdef __cplusplus

@@ -552,6 +552,73 @@ static void sp_cost_job(void* a, int tid, int nt) {
   for (int m = tid; m < P->n_imu; m += nt) s += sp_imu(P, c->st, m, e, NULL, NULL, NULL);
   c->part[tid] = s;
 }
+/* ------------------------------------------------------------------ BSplineMotionError */
+/* Q = curveQuadraticIntegralSparse(W, m) (BSpline.cpp:1585-1622; segmentQuadraticIntegral :1512-1548) is
+ * sum over the valid segments of int (d^m f/dt^m)^T W (d^m f/dt^m) dt as a quadratic form in the coefficients:
+ * Q_(k,l) = W * int b_k^(m)(t) b_l^(m)(t) dt.  Restated by 4-point Gauss-Legendre quadrature per segment of the
+ * basis-weight products (exact: the integrand is a polynomial of degree <= 2 (order - 1 - m) <= 6), an
+ * independent route from the reference's moment matrices V (Vi :1276-1300) and derivative matrices Dii. */
+int kbo_sp_motion_band(const kbo_sp_problem* P, double* q) {
+  if (!P->motion_W) return 0;
+  const int o = P->order, K = sp_ncoef(P), m = P->motion_order;
+  static const double gx[4] = {-0.86113631159405257522, -0.33998104358485626480, 0.33998104358485626480,
+                               0.86113631159405257522};
+  static const double gw[4] = {0.34785484513745385737, 0.65214515486254614263, 0.65214515486254614263,
+                               0.34785484513745385737};
+  memset(q, 0, sizeof(double) * (size_t)K * o);
+  for (int sgi = 0; sgi + o <= K; ++sgi) {
+    const double t0 = P->knots[sgi + o - 1], t1 = P->knots[sgi + o];
+    if (!(t1 > t0)) continue;
+    for (int g = 0; g < 4; ++g) {
+      const double t = t0 + 0.5 * (t1 - t0) * (1.0 + gx[g]), wt = 0.5 * (t1 - t0) * gw[g];
+      double w[8];
+      const int b = kbo_bspline_weights(o, P->knots, P->n_knots, t, m, w);
+      if (b < 0) continue;
+      for (int j = 0; j < o; ++j)
+        for (int l = j; l < o; ++l) q[(size_t)(b + j) * o + (l - j)] += wt * w[j] * w[l];
+    }
+  }
+  return 1;
+}
+
+static double sp_motion_terms(const kbo_sp_problem* P, const double* st, double* Hband, double* gs) {
+  const int o = P->order, K = sp_ncoef(P);
+  double* q = (double*)malloc(sizeof(double) * (size_t)K * o);
+  if (!kbo_sp_motion_band(P, q)) {
+    free(q);
+    return 0.0;
+  }
+  const double* c = st + sp_off_coef(P);
+  const double* W = P->motion_W;
+  double cost = 0.0;
+  for (int k = 0; k < K; ++k)
+    for (int d = 0; d < o && k + d < K; ++d) {
+      const double qk = q[(size_t)k * o + d];
+      double Wc[6], Wc2[6];  /* W c_(k+d), W c_k */
+      for (int a = 0; a < 6; ++a) {
+        Wc[a] = Wc2[a] = 0.0;
+        for (int bb = 0; bb < 6; ++bb) {
+          Wc[a] += W[a * 6 + bb] * c[6 * (k + d) + bb];
+          Wc2[a] += W[a * 6 + bb] * c[6 * k + bb];
+        }
+      }
+      double e = 0.0;
+      for (int a = 0; a < 6; ++a) e += c[6 * k + a] * Wc[a];
+      cost += (d == 0 ? 1.0 : 2.0) * qk * e;
+      if (Hband)
+        for (int a = 0; a < 36; ++a) Hband[((size_t)k * o + d) * 36 + a] += qk * W[a];
+      if (gs)
+        for (int a = 0; a < 6; ++a) {  /* buildHessianImplementation: rhs -= Q c (BSplineMotionError.hpp:154) */
+          gs[6 * k + a] -= qk * Wc[a];
+          if (d > 0) gs[6 * (k + d) + a] -= qk * Wc2[a];
+        }
+    }
+  free(q);
+  return cost;
+}
+
+double kbo_sp_motion_cost(const kbo_sp_problem* P, const double* st) { return sp_motion_terms(P, st, NULL, NULL); }
+
 double kbo_sp_eval_cost(const kbo_sp_problem* P, const double* st, int nthreads) {
   if (nthreads < 1) nthreads = 1;
   if (nthreads > 256) nthreads = 256;
@@ -561,7 +628,7 @@ double kbo_sp_eval_cost(const kbo_sp_problem* P, const double* st, int nthreads)
   sp_parallel(nthreads, sp_cost_job, &c);
   double s = 0.0;
   for (int t = 0; t < nthreads; ++t) s += c.part[t];
-  return s;
+  return s + sp_motion_terms(P, st, NULL, NULL);  /* evaluateErrorImplementation: c^T Q c */
 }
 
 /* ------------------------------------------------------------------ normal equations */
@@ -700,6 +767,7 @@ void kbo_sp_build(const kbo_sp_problem* P, const double* st, int nthreads, kbo_s
   /* symmetrise Hcc (full) */
   for (int a = 0; a < C; ++a)
     for (int b = 0; b < a; ++b) A->Hcc[a * C + b] = A->Hcc[b * C + a];
+  A->cost += sp_motion_terms(P, st, A->Hband, A->gs);  /* BSplineMotionError::buildHessianImplementation */
 }
 
 /* ------------------------------------------------------------------ solve */

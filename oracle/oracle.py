@@ -330,7 +330,8 @@ class _SpProblem(C.Structure):
                 ("cam_model", ip), ("target", dp), ("n_frames", C.c_int), ("frame_time", dp), ("n_views", C.c_int),
                 ("n_corners", C.c_int), ("view_frame", ip), ("view_cam", ip), ("view_offset", ip),
                 ("corner_id", ip), ("y", dp), ("n_imu", C.c_int), ("imu_time", dp), ("imu_gyro", dp),
-                ("imu_acc", dp), ("sigma_gyro", C.c_double), ("sigma_acc", C.c_double)]
+                ("imu_acc", dp), ("sigma_gyro", C.c_double), ("sigma_acc", C.c_double), ("motion_W", dp),
+                ("motion_order", C.c_int)]
 
 
 class _SpSystem(C.Structure):
@@ -342,7 +343,7 @@ def _sp_lib():
     L = lib()
     if not getattr(L, "_sp_ready", False):
         for f in ("kbo_sp_eval_cost", "kbo_sp_reproj_dense", "kbo_sp_imu_dense", "kbo_sp_apply_update",
-                  "kbo_sp_time_gn"):
+                  "kbo_sp_time_gn", "kbo_sp_motion_cost"):
             getattr(L, f).restype = C.c_double
         L.kbo_bspline_weights.argtypes = [C.c_int, dp, C.c_int, C.c_double, C.c_int, dp]
         L.kbo_bspline_basis.argtypes = [C.c_int, dp, C.c_int, dp]
@@ -379,7 +380,8 @@ def rv_dSv(a, v):
 class SplineOracle:
     """configs[4] restatement over one SplineProblem (kalibr_amd/synth.py)."""
 
-    def __init__(self, prob):
+    def __init__(self, prob, motion_W=None, motion_order=2):
+        """motion_W (6 x 6, optional): add a BSplineMotionError of that weight and derivative order."""
         self.prob = prob
         k = self._keep = dict(
             knots=np.ascontiguousarray(prob.knots, dtype=np.float64),
@@ -398,7 +400,10 @@ class SplineOracle:
                             _i(k["cam_model"]), _d(k["target"]), prob.n_frames, _d(k["frame_time"]), prob.n_views,
                             prob.n_corners, _i(k["view_frame"]), _i(k["view_cam"]), _i(k["view_offset"]),
                             _i(k["corner_id"]), _d(k["y"]), prob.n_imu, _d(k["imu_time"]), _d(k["imu_gyro"]),
-                            _d(k["imu_acc"]), prob.sigma_gyro, prob.sigma_acc)
+                            _d(k["imu_acc"]), prob.sigma_gyro, prob.sigma_acc, None, int(motion_order))
+        if motion_W is not None:
+            k["motion_W"] = np.ascontiguousarray(motion_W, dtype=np.float64).reshape(6, 6)
+            self.P.motion_W = _d(k["motion_W"])
         L = _sp_lib()
         self.C = L.kbo_sp_cam_cols(C.byref(self.P))
         self.K = L.kbo_sp_num_coeffs(C.byref(self.P))
@@ -458,3 +463,12 @@ class SplineOracle:
     def time_gn(self, state, n_iter, nthreads):
         st = np.array(state, dtype=np.float64, copy=True)
         return _sp_lib().kbo_sp_time_gn(C.byref(self.P), _d(st), n_iter, nthreads)
+
+    def motion_band(self):
+        """q[k][d] = int b_k^(m) b_(k+d)^(m) dt (None without a motion term)"""
+        q = np.zeros((self.K, self.prob.order))
+        return q if _sp_lib().kbo_sp_motion_band(C.byref(self.P), _d(q)) else None
+
+    def motion_cost(self, state):
+        st = np.ascontiguousarray(state, dtype=np.float64)
+        return _sp_lib().kbo_sp_motion_cost(C.byref(self.P), _d(st))

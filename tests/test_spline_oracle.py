@@ -205,3 +205,63 @@ def test_gauss_newton_recovers_calibration():
     imu = slice(p.off_coeff - 9, p.off_coeff)
     assert np.abs(st[imu][:3] - p.state_truth[imu][:3]).max() < 1e-3  # gyro bias
     assert np.abs(st[imu][6:] - p.state_truth[imu][6:]).max() < 0.05  # gravity
+
+
+# ---- BSplineMotionError (aslam_splines BSplineMotionError.hpp:29-160) ----
+W_MOTION = np.diag([4.0, 4.0, 4.0, 1.0, 1.0, 1.0]) + 0.1 * (np.ones((6, 6)) - np.eye(6))
+
+
+@pytest.mark.parametrize("m", [1, 2, 3])
+def test_motion_cost_is_the_curve_quadratic_integral(small, m):
+    """c^T Q c == int (d^m f / dt^m)^T W (d^m f / dt^m) dt over the valid time range (curveQuadraticIntegral,
+    BSpline.cpp:1669-1686), checked against 8-point Gauss-Legendre quadrature of the curve itself (synth's numpy
+    spline evaluation, segment by segment)."""
+    p, _ = small
+    o = O.SplineOracle(p, motion_W=W_MOTION, motion_order=m)
+    st = p.state_init
+    c = st[o.nstate - 6 * o.K:].reshape(o.K, 6)
+    kn = p.knots
+    t0, t1 = kn[p.order - 1], kn[len(kn) - p.order]
+    total = 0.0
+    for s in range(p.order - 1, len(kn) - p.order):  # segment by segment (the derivative is smooth inside)
+        a, b = kn[s], kn[s + 1]
+        x, w = np.polynomial.legendre.leggauss(8)
+        ts = a + 0.5 * (b - a) * (x + 1.0)
+        vals = np.array([(lambda v: v @ W_MOTION @ v)(synth.spline_eval(p.order, kn, c, t, m)) for t in ts])
+        total += 0.5 * (b - a) * (w @ vals)
+    assert t1 > t0
+    assert abs(o.motion_cost(st) - total) <= 1e-11 * abs(total)
+
+
+def test_motion_error_hessian_and_rhs(small):
+    """buildHessianImplementation: H += Q, rhs -= Q c; cost += c^T Q c.  Q is the Hessian of the cost / 2 and
+    -Q c the half-gradient: checked by finite differences of the cost along the coefficient columns."""
+    p, _ = small
+    o0 = O.SplineOracle(p)
+    o = O.SplineOracle(p, motion_W=W_MOTION, motion_order=2)
+    st = p.state_init
+    s0, s1 = o0.system(st), o.system(st)
+    q = o.motion_band()
+    assert q is not None and o0.motion_band() is None
+    assert abs((s1["cost"] - s0["cost"]) - o.motion_cost(st)) <= 1e-12 * s1["cost"]
+    for k in (0, 5, o.K - 1):
+        for d in range(p.order):
+            if k + d < o.K:
+                assert np.abs(s1["Hband"][k, d] - s0["Hband"][k, d] - q[k, d] * W_MOTION).max() <= 1e-12 * max(
+                    1.0, np.abs(s1["Hband"][k, d]).max())
+    gq = s1["gs"] - s0["gs"]
+    rng = np.random.default_rng(3)
+    for col in rng.choice(6 * o.K, 8, replace=False):
+        h = 1e-4
+        dx = np.zeros(o.ncols)
+        dx[o.C + col] = h
+        sp, _ = o.apply_update(st, dx)
+        dx[o.C + col] = -h
+        sm, _ = o.apply_update(st, dx)
+        fd = (o.motion_cost(sp) - o.motion_cost(sm)) / (2 * h)  # = 2 (Q c)_col
+        assert abs(fd + 2 * gq[col]) <= 1e-6 * max(1.0, abs(fd)), col
+    # the solve still agrees with the dense one
+    for lam in (0.0, 10.0):
+        ok, dx = o.solve(s1, lam)
+        ok2, dx2 = o.solve(s1, lam, dense=True)
+        assert ok and ok2 and np.abs(dx - dx2).max() <= 1e-8 * np.abs(dx2).max()
