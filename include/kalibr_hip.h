@@ -253,6 +253,12 @@ int kb_sp_get_state(kb_sp_handle* h, double* state);
 int kb_sp_eval_cost(kb_sp_handle* h, double* J_out);
 int kb_sp_build(kb_sp_handle* h);
 int kb_sp_set_constant_conditioner(kb_sp_handle* h, double diag);
+/* BSplineMotionError (aslam_splines/include/aslam/backend/implementation/BSplineMotionError.hpp:29-160) on the pose
+ * spline: cost c^T Q c with Q = curveQuadraticIntegralSparse(W, derivative_order) (bsplines/src/BSpline.cpp:
+ * 1585-1622), added to evaluateError; buildSystem adds Q to the coefficient band and -Q c to the rhs (the
+ * reference's buildHessianImplementation).  W [6][6] symmetric (row-major); derivative_order >= order is reduced to
+ * order - 1 as the reference does; W == NULL removes the term. */
+int kb_sp_set_motion_error(kb_sp_handle* h, const double* W, int32_t derivative_order);
 int kb_sp_solve(kb_sp_handle* h, double* dx_out, int* ok);
 int kb_sp_get_rhs(kb_sp_handle* h, double* rhs_out);
 int kb_sp_apply_update(kb_sp_handle* h, const double* dx, double* deltaX_out);

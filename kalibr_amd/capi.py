@@ -29,7 +29,7 @@ EXPORTS = [
     "kb_sp_create", "kb_sp_destroy", "kb_sp_upload", "kb_sp_state_size", "kb_sp_num_cols", "kb_sp_camera_cols",
     "kb_sp_set_state", "kb_sp_get_state", "kb_sp_eval_cost", "kb_sp_build", "kb_sp_set_constant_conditioner",
     "kb_sp_solve", "kb_sp_get_rhs", "kb_sp_apply_update", "kb_sp_revert", "kb_sp_get_system", "kb_sp_optimize",
-    "kb_sp_get_trace", "kb_sp_run_gn_iterations", "kb_sp_kernel_stats",
+    "kb_sp_get_trace", "kb_sp_run_gn_iterations", "kb_sp_kernel_stats", "kb_sp_set_motion_error",
 ]
 
 
@@ -148,6 +148,7 @@ def lib():
         L.kb_sp_get_trace.argtypes = [C.c_void_p, dp, C.c_int32]
         L.kb_sp_run_gn_iterations.argtypes = [C.c_void_p, C.c_int32, dp]
         L.kb_sp_kernel_stats.argtypes = [C.c_void_p, C.c_int32, dp, dp]
+        L.kb_sp_set_motion_error.argtypes = [C.c_void_p, dp, C.c_int32]
         _lib = L
     return _lib
 
@@ -364,6 +365,14 @@ class SplineSolver:
             self.close()
         except Exception:
             pass
+
+    def set_motion_error(self, W, derivative_order=2):
+        """BSplineMotionError on the pose spline (W 6 x 6 symmetric; None removes it)."""
+        if W is None:
+            _check(lib().kb_sp_set_motion_error(self.h, None, 0))
+            return
+        self._motion_W = np.ascontiguousarray(W, dtype=np.float64).reshape(6, 6)
+        _check(lib().kb_sp_set_motion_error(self.h, _d(self._motion_W), int(derivative_order)))
 
     def set_state(self, state):
         st = np.ascontiguousarray(state, dtype=np.float64)

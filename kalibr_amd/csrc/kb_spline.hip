@@ -74,10 +74,16 @@ struct SpDev {
   double* spart;          // [nblk_s][Ws]
   double* dx;             // [C + 6K]
   double* dmax;           // [n]
-  double* cpart;          // [nblk_f + nblk_ci]
+  double* cpart;          // [nblk_f + nblk_ci + nblk_q]
   double* sc;             // scalars
   double* Sf;             // [C][C] Schur complement (+ lam2 I) | b [C]
   const short2* uab;      // [Wc] (a, b) of upper-triangle entry q; (a, C) for g_a; (C, C) for the cost
+  // BSplineMotionError (kb_sp_set_motion_error): cost c^T Q c, H += Q, g -= Q c on the coefficient band
+  int mot;                // 1: active
+  int nblk_q;             // k_sp_cost_motion blocks (64 nodes each)
+  const double* QD;       // [n][324] Q blocks within node i
+  const double* QU;       // [n][324] Q block node i (rows) -> node i + 1 (columns)
+  double* mcost;          // [n] per-node motion cost at the build state
 };
 
 typedef double v4d_t __attribute__((ext_vector_type(4)));
@@ -663,6 +669,36 @@ __global__ void __launch_bounds__(256) k_sp_assemble(SpDev d) {
     }
   }
   __syncthreads();
+  if (d.mot) {  // BSplineMotionError::buildHessianImplementation (BSplineMotionError.hpp:96-160): H += Q, g -= Q c
+    __shared__ double cn[3 * NB];  // coefficients of nodes i - 1, i, i + 1 (0 outside [0, K))
+    for (int q = tid; q < 3 * NB; q += nth) {
+      const int k = SB * (i - 1) + q / 6;
+      cn[q] = (k >= 0 && k < d.K) ? d.state[d.off_coef + 6 * k + q % 6] : 0.0;
+    }
+    const double* QDi = d.QD + (size_t)i * NB * NB;
+    const double* QUi = d.QU + (size_t)i * NB * NB;
+    const double* QUl = d.QU + (size_t)(i > 0 ? i - 1 : 0) * NB * NB;
+    for (int q = tid; q < 2 * NB * NB; q += nth) out[q] += q < NB * NB ? QDi[q] : QUi[q - NB * NB];
+    __syncthreads();
+    double nc = 0.0;
+    if (tid < 64) {
+      if (tid < NB) {
+        const int r = tid;
+        double a = 0.0, w = 0.0, l = 0.0;
+        for (int c = 0; c < NB; ++c) {
+          a += QDi[r * NB + c] * cn[NB + c];
+          w += QUi[r * NB + c] * cn[2 * NB + c];
+          l += (i > 0) ? QUl[c * NB + r] * cn[c] : 0.0;
+        }
+        out[2 * NB * NB + r * m + C] -= (a + w) + l;  // rows of node i of Q c
+        nc = cn[NB + r] * (a + 2.0 * w);           // c_i^T QD_i c_i + 2 c_i^T QU_i c_(i+1)
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) nc += __shfl_xor(nc, o);
+      if (tid == 0) d.mcost[i] = nc;
+    }
+    __syncthreads();
+  }
   // padded rows (coefficients >= K): identity diagonal, no coupling
   for (int q = tid; q < nout; q += nth) {
     double v = out[q];
@@ -1274,11 +1310,58 @@ __global__ void __launch_bounds__(256) k_sp_cost_imu(SpDev d) {
   if (tid == 0) d.cpart[d.nblk_f + blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
+// BSplineMotionError::evaluateErrorImplementation (BSplineMotionError.hpp:62-78): c^T Q c of the current state,
+// one node per lane (c_i^T QD_i c_i + 2 c_i^T QU_i c_(i+1)) -> cpart[nblk_f + nblk_ci + block]
+__global__ void __launch_bounds__(64) k_sp_cost_motion(SpDev d) {
+  const int i = blockIdx.x * 64 + threadIdx.x;
+  double s = 0.0;
+  if (i < d.n) {
+    double ci[NB], cj[NB];
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
+      const int k = SB * i + q / 6, k1 = k + SB;
+      ci[q] = k < d.K ? d.state[d.off_coef + 6 * k + q % 6] : 0.0;
+      cj[q] = k1 < d.K ? d.state[d.off_coef + 6 * k1 + q % 6] : 0.0;
+    }
+    const double* QDi = d.QD + (size_t)i * NB * NB;
+    const double* QUi = d.QU + (size_t)i * NB * NB;
+#pragma unroll
+    for (int r = 0; r < NB; ++r) {
+      double a = 0.0, w = 0.0;
+#pragma unroll
+      for (int c = 0; c < NB; ++c) {
+        a += QDi[r * NB + c] * ci[c];
+        w += QUi[r * NB + c] * cj[c];
+      }
+      s += ci[r] * (a + 2.0 * w);
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if (threadIdx.x == 0) d.cpart[d.nblk_f + d.nblk_ci + blockIdx.x] = s;
+}
+
+// motion cost of the build state: fixed-order sum of k_sp_assemble's per-node values, added to the build cost
+__global__ void __launch_bounds__(256) k_sp_mcost_build(SpDev d) {
+  __shared__ double red[4];
+  double s = 0.0;
+  for (int q = threadIdx.x; q < d.n; q += 256) s += d.mcost[q];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const double t = (red[0] + red[1]) + (red[2] + red[3]);
+    d.Hcc[d.C * d.C + d.C] += t;
+    d.sc[SC_COST_BUILD] += t;
+  }
+}
+
 // fixed-order sums: cost -> sc[SC_COST], max |dx| -> sc[SC_DX]
 __global__ void __launch_bounds__(64) k_sp_cost_reduce(SpDev d, int with_dx) {
   const int tid = threadIdx.x;
   double s = 0.0, mx = 0.0;
-  for (int q = tid; q < d.nblk_f + d.nblk_ci; q += 64) s += d.cpart[q];
+  for (int q = tid; q < d.nblk_f + d.nblk_ci + (d.mot ? d.nblk_q : 0); q += 64) s += d.cpart[q];
   if (with_dx)
     for (int q = tid; q < d.n; q += 64) mx = fmax(mx, d.dmax[q]);
 #pragma unroll
@@ -1394,6 +1477,40 @@ int basis_weights(const std::vector<double>& kn, int order, double t, int deriv,
   }
   return bidx;
 }
+
+// segmentQuadraticIntegral (BSpline.cpp:1512-1548) of valid segment s without the W factor:
+// Q_s = M^T (Dm^T)^m V Dm^m M with V(r, c) = dt / (r + c + 1) (Vi, :1276-1300), Dm(i, i + 1) = (i + 1) / dt
+// (Dii, :1483-1500) and M the segment's basis matrix (Mi, :1391-1403); Q_s[j][l] couples coefficients s + j, s + l.
+void segment_quadratic(const std::vector<double>& kn, int s, int m, double* Q) {
+  double M[64], V[16], Dm[16] = {0}, T[16];
+  basis_matrix(kn, ORD, s + ORD - 1, M);
+  const double dt = kn[s + ORD] - kn[s + ORD - 1];
+  const double rdt = dt > 0.0 ? 1.0 / dt : 0.0;
+  for (int r = 0; r < ORD; ++r)
+    for (int c = 0; c < ORD; ++c) V[r * ORD + c] = dt / (r + c + 1.0);
+  for (int i = 0; i + 1 < ORD; ++i) Dm[i * ORD + i + 1] = (i + 1.0) * rdt;
+  for (int it = 0; it < m; ++it) {  // V <- Dm^T V Dm
+    for (int r = 0; r < ORD; ++r)
+      for (int c = 0; c < ORD; ++c) {
+        double a = 0.0;
+        for (int k = 0; k < ORD; ++k) a += V[r * ORD + k] * Dm[k * ORD + c];
+        T[r * ORD + c] = a;
+      }
+    for (int r = 0; r < ORD; ++r)
+      for (int c = 0; c < ORD; ++c) {
+        double a = 0.0;
+        for (int k = 0; k < ORD; ++k) a += Dm[k * ORD + r] * T[k * ORD + c];
+        V[r * ORD + c] = a;
+      }
+  }
+  for (int j = 0; j < ORD; ++j)
+    for (int l = 0; l < ORD; ++l) {
+      double a = 0.0;
+      for (int r = 0; r < ORD; ++r)
+        for (int c = 0; c < ORD; ++c) a += M[r * ORD + j] * V[r * ORD + c] * M[c * ORD + l];
+      Q[j * ORD + l] = a;
+    }
+}
 }  // namespace
 
 struct kb_sp_handle {
@@ -1441,6 +1558,7 @@ int launch_build(kb_sp_handle* h) {
   KSP_HIP(hipLaunchKernel((const void*)k_sp_assemble, dim3(d.n), dim3(256), args, h->lds_asm, h->stream));
   hipLaunchKernelGGL(k_sp_imu_cc, dim3(d.nblk_ic), dim3(64), 0, h->stream, d);
   hipLaunchKernelGGL(k_sp_reduce_cc, dim3((d.Wc + 63) / 64), dim3(256), 0, h->stream, d);
+  if (d.mot) hipLaunchKernelGGL(k_sp_mcost_build, dim3(1), dim3(256), 0, h->stream, d);
   return 0;
 }
 
@@ -1477,6 +1595,7 @@ int launch_cost(kb_sp_handle* h, int with_dx) {
   void* args[] = {&d};
   KSP_HIP(hipLaunchKernel(h->fn_cost, dim3(d.nblk_f), dim3(64 * h->N), args, 0, h->stream));
   hipLaunchKernelGGL(k_sp_cost_imu, dim3(d.nblk_ci), dim3(256), 0, h->stream, d);
+  if (d.mot) hipLaunchKernelGGL(k_sp_cost_motion, dim3(d.nblk_q), dim3(64), 0, h->stream, d);
   hipLaunchKernelGGL(k_sp_cost_reduce, dim3(1), dim3(64), 0, h->stream, d, with_dx);
   return 0;
 }
@@ -1765,7 +1884,9 @@ int kb_sp_upload(kb_sp_handle* h, int32_t n_frames, const double* frame_time, in
   rc |= h->alloc(&dni, 2 * (size_t)h->n);
   rc |= h->alloc(&d.FH, (size_t)F * d.FHS);
   rc |= h->alloc(&d.part, (size_t)d.nblk_f * d.Wc);
-  rc |= h->alloc(&d.cpart, (size_t)(d.nblk_f + d.nblk_ci));
+  d.nblk_q = (h->n + 63) / 64;
+  rc |= h->alloc(&d.cpart, (size_t)(d.nblk_f + d.nblk_ci + d.nblk_q));
+  rc |= h->alloc(&d.mcost, (size_t)h->n);
   rc |= h->alloc(&d.ipart, (size_t)d.nblk_ic * WI);
   if (rc) return -1;
   if (n_corners) {
@@ -1837,6 +1958,64 @@ int kb_sp_build(kb_sp_handle* h) {
   KSP_HIP(hipGetLastError());
   h->built = true;
   h->solved = false;
+  return 0;
+}
+
+// BSplineMotionError (aslam_splines BSplineMotionError.hpp:29-160) over the pose spline: Q =
+// curveQuadraticIntegralSparse(W, order) (BSpline.cpp:1585-1622) split into the node blocks of the cyclic reduction
+// (nodes of SB coefficients; Q's band reaches order - 1 = 3 coefficients, i.e. the next node only).
+int kb_sp_set_motion_error(kb_sp_handle* h, const double* W, int32_t derivative_order) {
+  if (!h) return fail("kb_sp_set_motion_error: null handle");
+  KSP_HIP(hipSetDevice(h->device));
+  if (h->gn_graph) {  // captured passes hold the old SpDev
+    hipGraphExecDestroy(h->gn_graph);
+    h->gn_graph = nullptr;
+  }
+  if (!W) {
+    h->d.mot = 0;
+    return 0;
+  }
+  int m = derivative_order;
+  if (m < 0) return fail("kb_sp_set_motion_error: negative derivative order");
+  if (m >= ORD) m = ORD - 1;  // BSplineMotionError::initialize: "Invalid ErrorTermOrder reduced" (:33-36)
+  for (int r = 0; r < 6; ++r)
+    for (int c = 0; c < 6; ++c)
+      if (std::fabs(W[r * 6 + c] - W[c * 6 + r]) > 1e-14)  // segmentQuadraticIntegral: "W must be symmetric"
+        return fail("kb_sp_set_motion_error: W must be symmetric");
+  const int K = h->K, n = h->n;
+  std::vector<double> q((size_t)K * ORD, 0.0);  // q[k][d]: scalar Q of coefficients (k, k + d)
+  double Qs[ORD * ORD];
+  for (int sg = 0; sg + ORD <= K; ++sg) {
+    if (!(h->knots[sg + ORD] > h->knots[sg + ORD - 1])) continue;
+    segment_quadratic(h->knots, sg, m, Qs);
+    for (int j = 0; j < ORD; ++j)
+      for (int l = j; l < ORD; ++l) q[(size_t)(sg + j) * ORD + (l - j)] += Qs[j * ORD + l];
+  }
+  std::vector<double> QD((size_t)n * NB * NB, 0.0), QU((size_t)n * NB * NB, 0.0);
+  auto qv = [&](int k, int l) {  // scalar Q(k, l), symmetric, 0 outside the band / beyond K
+    if (k > l) std::swap(k, l);
+    return (k < 0 || l >= K || l - k >= ORD) ? 0.0 : q[(size_t)k * ORD + (l - k)];
+  };
+  for (int i = 0; i < n; ++i)
+    for (int r = 0; r < NB; ++r)
+      for (int c = 0; c < NB; ++c) {
+        const int k = SB * i + r / 6, w = (r % 6) * 6 + c % 6;
+        QD[((size_t)i * NB + r) * NB + c] = qv(k, SB * i + c / 6) * W[w];
+        QU[((size_t)i * NB + r) * NB + c] = qv(k, SB * (i + 1) + c / 6) * W[w];
+      }
+  SpDev& d = h->d;
+  if (!d.QD) {
+    double *qd = nullptr, *qu = nullptr;
+    if (h->alloc(&qd, (size_t)n * NB * NB) || h->alloc(&qu, (size_t)n * NB * NB)) return -1;
+    d.QD = qd;
+    d.QU = qu;
+  }
+  KSP_HIP(hipMemcpyAsync(const_cast<double*>(d.QD), QD.data(), sizeof(double) * QD.size(), hipMemcpyHostToDevice,
+                         h->stream));
+  KSP_HIP(hipMemcpyAsync(const_cast<double*>(d.QU), QU.data(), sizeof(double) * QU.size(), hipMemcpyHostToDevice,
+                         h->stream));
+  KSP_HIP(hipStreamSynchronize(h->stream));
+  d.mot = 1;
   return 0;
 }
 
@@ -2125,6 +2304,7 @@ int kb_sp_kernel_stats(kb_sp_handle* h, int32_t n, double* ms_out6, double* fram
     KSP_HIP(hipLaunchKernel((const void*)k_sp_assemble, dim3(d.n), dim3(256), args, h->lds_asm, h->stream));
     hipLaunchKernelGGL(k_sp_imu_cc, dim3(d.nblk_ic), dim3(64), 0, h->stream, d);
     hipLaunchKernelGGL(k_sp_reduce_cc, dim3((d.Wc + 63) / 64), dim3(256), 0, h->stream, d);
+    if (d.mot) hipLaunchKernelGGL(k_sp_mcost_build, dim3(1), dim3(256), 0, h->stream, d);
     KSP_HIP(hipEventRecord(ev[2], h->stream));
     launch_reduction(h);
     KSP_HIP(hipEventRecord(ev[3], h->stream));

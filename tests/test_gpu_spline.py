@@ -109,3 +109,59 @@ def test_full_size_gn_properties():
     g.set_state(p.state_init)
     g.run_gn(8)
     assert np.array_equal(g.get_state(), st)
+
+
+# ---- BSplineMotionError (kb_sp_set_motion_error) against the oracle's restatement ----
+W_MOTION = np.diag([4.0, 4.0, 4.0, 1.0, 1.0, 1.0]) + 0.1 * (np.ones((6, 6)) - np.eye(6))
+
+
+@pytest.fixture(scope="module")
+def motion_case():
+    p = synth.make_spline_config(n_frames=40)
+    g = capi.SplineSolver(p)
+    g.set_motion_error(W_MOTION, 2)
+    return p, O.SplineOracle(p, motion_W=W_MOTION, motion_order=2), g
+
+
+def test_motion_error_cost_system_solve(motion_case):
+    """Q is formed two independent ways -- the reference's moment matrices M^T D^T V D M on the device side's host
+    (segmentQuadraticIntegral) and Gauss-Legendre quadrature of the basis products in the oracle -- which agree
+    entry-wise to ~1e-15 relative; c^T Q c cancels against Q's ~1/dt^3 entries, so the cost bar is 1e-10."""
+    p, o, g = motion_case
+    for st in (p.state_init, p.state_truth):
+        g.set_state(st)
+        J, Jo = g.eval_cost(), o.cost(st)
+        assert abs(J - Jo) <= 1e-10 * Jo, (J, Jo)
+    g.set_state(p.state_init)
+    g.build()
+    s = g.system()
+    so = o.system(p.state_init, nthreads=4)
+    assert abs(s["cost"] - so["cost"]) <= 1e-10 * so["cost"]
+    for k in ("Hcc", "Hsc", "gc", "gs", "Hband"):
+        assert _rel(s[k], so[k]) < 1e-10, k
+    for lam in (0.0, 10.0):
+        g.set_constant_conditioner(lam)
+        ok, dx = g.solve()
+        ok_o, dx_o = o.solve(so, lam)
+        assert ok and ok_o and _rel(dx, dx_o) < 1e-8
+
+
+@pytest.mark.parametrize("policy", ["gn", "lm"])
+def test_motion_error_optimize_parity(motion_case, policy):
+    p, o, g = motion_case
+    g.set_state(p.state_init)
+    res = g.optimize(policy=policy, lambda0=10.0, max_iterations=20, eps_x=1e-3, eps_j=1e-3)
+    st_o, res_o = o.optimize(p.state_init, policy=policy, lambda0=10.0, max_iterations=20, eps_x=1e-3, eps_j=1e-3,
+                             nthreads=4)
+    assert res["iterations"] == res_o["iterations"] and res["failed_iterations"] == res_o["failed_iterations"]
+    assert abs(res["J_final"] - res_o["J_final"]) <= 1e-9 * res_o["J_final"]
+    assert np.abs(g.get_state() - st_o).max() < 1e-6
+
+
+def test_motion_error_removed_restores_the_plain_system(motion_case):
+    p, o, g = motion_case
+    g.set_motion_error(None)
+    g.set_state(p.state_init)
+    o0 = O.SplineOracle(p)
+    assert abs(g.eval_cost() - o0.cost(p.state_init)) <= 1e-12 * o0.cost(p.state_init)
+    g.set_motion_error(W_MOTION, 2)
