@@ -34,9 +34,12 @@ GN_FUSED = os.environ.get("KB_GN_FUSED", "1") != "0"  # the library's pass varia
 
 
 def is_build_kernel(name):
-    """The pass's build kernel as rocprofv3 names it: k_build<TW, GNF> with GNF = the GN fused variant."""
-    return name.startswith("void kb::k_build<") and name.endswith(
-        (", true>(kb::KbDev, int, int)" if GN_FUSED else ", false>(kb::KbDev, int, int)"))
+    """The pass's build kernel as rocprofv3 names it: k_build<TW, GNF, MM> with GNF = the GN fused variant (MM = the
+    rig's camera-model set)."""
+    if not (name.startswith("void kb::k_build<") and name.endswith(">(kb::KbDev, int, int)")):
+        return False
+    args = name[len("void kb::k_build<"):-len(">(kb::KbDev, int, int)")].split(", ")
+    return len(args) >= 2 and args[1] == ("true" if GN_FUSED else "false")
 FRAMES_PER_RANK = 500
 HBM_PEAK_GBS = 8000.0
 
