@@ -994,7 +994,6 @@ __global__ void __launch_bounds__(256) k_schur(KbDev d, int gate) {
 // ---------------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_colsum(KbDev d, int gate) {
   KbCtrl* c = d.ctrl;
-  if (gate && c->done) return;
   __shared__ double part[4][64];
   const int l = threadIdx.x & 63, w4 = threadIdx.x >> 6;
   const int e = blockIdx.x * 64 + l, ry = blockIdx.y;
@@ -1002,10 +1001,21 @@ __global__ void __launch_bounds__(256) k_colsum(KbDev d, int gate) {
   const int ec = min(e, d.Wp);
   double s = 0.0;
   constexpr int U = 16, step = 4 * kColsumRows;
-  for (int b0 = ry + kColsumRows * w4; b0 < d.nblk; b0 += U * step) {
-    double v[U];
+  // the first batch of partial-row loads is issued with the gate's ctrl load (one round trip, not two): the
+  // rows are always valid addresses, the values are only used once the pass is known to be live
+  const int b00 = ry + kColsumRows * w4;
+  const int done = c->done;
+  double v[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) v[u] = d.part[(size_t)min(b0 + u * step, d.nblk - 1) * d.Wr + ec];
+  for (int u = 0; u < U; ++u) v[u] = d.part[(size_t)min(b00 + u * step, d.nblk - 1) * d.Wr + ec];
+#pragma unroll
+  for (int u = 0; u < U; ++u) KB_KEEP(v[u]);
+  if (gate && done) return;
+  for (int b0 = b00; b0 < d.nblk; b0 += U * step) {
+    if (b0 != b00) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = d.part[(size_t)min(b0 + u * step, d.nblk - 1) * d.Wr + ec];
+    }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const double x = (b0 + u * step < d.nblk) ? v[u] : 0.0;
