@@ -1820,6 +1820,10 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update, int nth) {
       for (int j = tid; j <= i; j += nth) S[tidx(i, j)] = (i == j) ? 1.0 : 0.0;
   __syncthreads();
   if (tid == 0) okl = (c->solve_ok != 0) && !(bv[C] > 0.0);
+  // the loop's done flag is tested only here: the ctrl and staging loads above went out in one round trip, and
+  // nothing global has been written yet
+  if (gate && c->done) return;
+  if (gate && !d.gn_fused && tid == 0) c->pending = 1;
   KB_STAMP(d, 1);
   // phase B: camera block expansion
   for (int q = tid; q < N * N * 36; q += nth) {
@@ -2010,9 +2014,7 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update, int nth) {
 // CM > 0: 4 waves (one factors); CM == 0: 8 waves
 template <int CM>
 __global__ void __launch_bounds__(CM == 0 ? 512 : 256) k_solve(KbDev d, int gate, int do_update) {
-  if (gate && d.ctrl->done) return;
-  if (gate && !d.gn_fused && threadIdx.x == 0) d.ctrl->pending = 1;
-  solve_body<CM>(d, gate, do_update, blockDim.x);
+  solve_body<CM>(d, gate, do_update, blockDim.x);  // returns early once ctrl->done (after its staging loads)
 }
 
 // ---------------------------------------------------------------------------------------------
