@@ -4,19 +4,19 @@ One step = one full Optimizer2 pass with the Gauss-Newton policy: buildSystem (r
 arrow normal equations) + solveSystem (frame Schur complement, camera-block Cholesky, back
 substitution) + applyStateUpdate + evaluateError, on synthetic AprilGrid data resident in HBM.
 
-Workload (N=1): configs[1] = 2-camera stereo pinhole-radtan rig, 500 frames, 6x5 AprilGrid (120 corners),
-all views visible.  N>1: weak scaling, every rank holds its own 500-frame shard of a 2-camera rig with
-500*N frames; the camera block [S | b] and the cost / step statistics are all-reduced over RCCL once per
-pass.  value = (config-sized shard iterations of all ranks) / max-over-ranks wall time.
+Default workload: configs[3], the north-star problem: 8-camera pinhole-radtan rig x 2000 frames, 6x5 AprilGrid
+(120 corners), all views visible (1.83 M corners, C = 106 camera-block columns).  It fits one MI355X, so N=1 runs
+the whole problem; N>1 shards its frames over the ranks (strong scaling: ceil(2000 / N) frames per rank,
+"scaling": "strong"); the stage-1 camera-block rows are all-reduced and the per-frame step rows all-gathered over
+RCCL once per pass.  value = GN iterations of the one problem / max-over-ranks wall time.
 
-configs[4] (--config 5): 2-camera rig + IMU on a cubic B-spline pose trajectory, 1200 frames at 20 Hz, 200 Hz
-IMU, 50 knots/s; one GPU, one step = one GN pass of the spline system (frames kernel,
-node assembly, block cyclic reduction, Schur onto the camera/IMU block, update, cost).
+Other configs behind --config (BASELINE.json configs[i] is --config i+1):
+  --config 2: configs[1], 2-camera stereo pinhole-radtan, 500 frames; N>1 is weak scaling (500 frames per rank).
+  --config 3: configs[2], 4-camera 2x omni-radtan + 2x EUCM rig, 1000 frames, one GPU.
+  --config 5: configs[4], 2-camera rig + IMU on a cubic B-spline pose trajectory, 1200 frames at 20 Hz, 200 Hz
+              IMU, 50 knots/s; one step = one GN pass of the spline system.
 
-configs[3] (--config 4): the north-star problem, 8-camera pinhole-radtan rig x 2000 frames; N>1 shards its frames
-over the ranks (strong scaling: 2000 / N frames per rank, "scaling": "strong").
-
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|4|5]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5]
 """
 import argparse
 import json
@@ -44,21 +44,43 @@ FRAMES_PER_RANK = 500
 HBM_PEAK_GBS = 8000.0
 
 
-def pmc_traffic_bytes(match):
-    """HBM bytes per launch of the kernel `match(name)` selects, from the newest committed PMC summary
-    (profiles/*/pmc_traffic.json, written by tools/pmc_traffic.py from two separate rocprofv3 --pmc passes of this
-    bench workload, gfx950 FETCH_SIZE correction applied), or None."""
+def pmc_traffic_bytes(match, config):
+    """HBM bytes per launch of the kernel `match(name)` selects, from the newest committed PMC summary of the same
+    bench workload (profiles/*/pmc_traffic*.json, written by tools/pmc_traffic.py from two separate rocprofv3 --pmc
+    passes of `bench.py --config <config>`, gfx950 FETCH_SIZE correction applied), or None."""
     import glob
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_traffic.json")), reverse=True):
+    paths = glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_traffic*.json"))
+    for path in sorted(paths, key=lambda p: (os.path.basename(os.path.dirname(p)), p), reverse=True):
         try:
             with open(path) as f:
-                ks = json.load(f)["kernels"]
+                doc = json.load(f)
+            ks = doc["kernels"]
         except (OSError, ValueError, KeyError):
+            continue
+        if doc.get("bench_config", 2) != config:  # round-1 summaries predate the field: configs[1] (--config 2)
             continue
         for name, k in ks.items():
             if match(name):
                 return k["hbm_bytes_per_launch"], os.path.relpath(path, ROOT)
     return None
+
+
+def host_cpu():
+    """CPU model and core counts of the host the CPU baseline runs on."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count()
+    return {"cpu_model": model, "nproc": avail, "os_cpu_count": os.cpu_count()}
 
 
 def cpu_baseline(prob, seconds_budget=12.0, threads=None, label="configs[1] (full 500-frame problem"):
@@ -70,9 +92,9 @@ def cpu_baseline(prob, seconds_budget=12.0, threads=None, label="configs[1] (ful
     t1 = o.time_gn(prob.state_init, 1, threads)  # includes first-touch / warm-up
     n = max(2, min(200, int(seconds_budget / max(t1, 1e-4))))
     t = o.time_gn(prob.state_init, n, threads)
-    return {"value": n / t, "unit": "iterations/s", "cores": threads, "kind": "port",
+    return {"value": n / t, "unit": "iterations/s", "cores": threads, "kind": "port", **host_cpu(),
             "sample": f"{n} GN iterations of {label}, {prob.n_corners} corners), "
-                      f"oracle/kb_oracle.c kbo_time_gn, {threads} threads"}
+                      f"oracle/kb_oracle.c kbo_time_gn (restatement, not CHOLMOD), {threads} threads"}
 
 
 def cpu_baseline_spline(prob, seconds_budget=15.0, threads=None):
@@ -84,7 +106,7 @@ def cpu_baseline_spline(prob, seconds_budget=15.0, threads=None):
     t1 = o.time_gn(prob.state_init, 1, threads)
     n = max(2, min(100, int(seconds_budget / max(t1, 1e-4))))
     t = o.time_gn(prob.state_init, n, threads)
-    return {"value": n / t, "unit": "iterations/s", "cores": threads, "kind": "port",
+    return {"value": n / t, "unit": "iterations/s", "cores": threads, "kind": "port", **host_cpu(),
             "sample": f"{n} GN iterations of configs[4] (full 1200-frame problem, {prob.n_corners} corners, "
                       f"{prob.n_imu} IMU samples), oracle/kb_oracle_spline.c kbo_sp_time_gn, {threads} threads"}
 
@@ -129,7 +151,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", type=int, default=2, choices=[2, 4, 5])
+    ap.add_argument("--config", type=int, default=4, choices=[2, 3, 4, 5],
+                    help="BASELINE.json configs[i] is --config i+1 (default 4: the north-star 8-cam x 2000-frame rig)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
     if args.config == 5:
@@ -154,9 +177,9 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("gloo", init_method="env://")  # id exchange + host barrier only
 
-    strong = args.config == 4
-    if strong:  # configs[3]: one 2000-frame problem, frames split over the ranks
-        full = synth.make_config(4)
+    strong = args.config in (3, 4)
+    if strong:  # configs[3] (configs[2]): one problem, frames split over the ranks
+        full = synth.make_config(args.config)
         fpr = (full.n_frames + world - 1) // world
     else:  # configs[1] per rank: a 2-camera rig of 500 * world frames, 500 per rank
         full = synth.make_problem(synth.CONFIGS[2]["models"], FRAMES_PER_RANK * world, seed=20261015 + 2,
@@ -185,13 +208,16 @@ def main():
     # dominant kernel (k_build) timing with HIP events on the handle's stream, inside GN passes
     build_ms, bytes_per, flops_per = g.build_kernel_stats()
     achieved = bytes_per / (build_ms * 1e-3) / 1e9
-    pmc = pmc_traffic_bytes(is_build_kernel) if world == 1 and not strong else None  # PMC summary is of configs[1]
+    pmc = pmc_traffic_bytes(is_build_kernel, args.config) if world == 1 else None  # summaries are of N=1 runs
 
     if rank == 0:
         # weak: every rank iterates its own configs[1]-sized problem; strong: all ranks iterate one problem
         value = (1 if strong else world) * args.steps / wall
-        workload = ("configs[3]: 8-cam pinhole-radtan rig, 2000 frames sharded over the GPUs, 6x5 AprilGrid"
-                    if strong else "configs[1]: 2-cam stereo pinhole-radtan, 500 frames/GPU, 6x5 AprilGrid, p_view=1")
+        workload = {4: "configs[3]: 8-cam pinhole-radtan rig, 2000 frames (sharded over the GPUs when N>1), 6x5 "
+                       "AprilGrid, p_view=1",
+                    3: "configs[2]: 4-cam 2x omni-radtan + 2x EUCM rig, 1000 frames (sharded over the GPUs when N>1), "
+                       "6x5 AprilGrid, p_view=1",
+                    2: "configs[1]: 2-cam stereo pinhole-radtan, 500 frames/GPU, 6x5 AprilGrid, p_view=1"}[args.config]
         out = {
             "metric": METRIC, "value": value, "unit": "iterations/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": 1e3 * wall / args.steps, "higher_is_better": True,
@@ -209,9 +235,9 @@ def main():
                          "fp64_tflops": flops_per / (build_ms * 1e-3) / 1e12},
         }
         if not args.no_cpu_baseline:
-            if strong:  # the whole north-star problem on the host cores (a few iterations: ~10 s each at 16 threads)
-                out["cpu_baseline"] = cpu_baseline(full, seconds_budget=20.0,
-                                                   label="configs[3] (full 8-cam 2000-frame problem")
+            if strong:  # the whole problem on the host cores (configs[3]: ~0.2 s per iteration at 16 threads)
+                lab = {4: "configs[3] (full 8-cam 2000-frame problem", 3: "configs[2] (full 4-cam 1000-frame problem"}
+                out["cpu_baseline"] = cpu_baseline(full, seconds_budget=20.0, label=lab[args.config])
             else:
                 out["cpu_baseline"] = cpu_baseline(full if world == 1 else full.frame_slice(0, FRAMES_PER_RANK))
             out["speedup_vs_cpu_baseline"] = value / out["cpu_baseline"]["value"]

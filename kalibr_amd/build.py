@@ -20,11 +20,24 @@ def needs_build():
     return any(os.path.getmtime(p) > t for p in deps)
 
 
+def _compile_link(out, extra=()):
+    """The two translation units compiled in parallel (hipcc -c, relocatable device code not needed: each TU owns
+    its kernels), then linked into one shared library."""
+    objs = [out + ".capi.o", out + ".spline.o"]
+    cflags = [f for f in FLAGS if f != "-shared"] + list(extra)
+    procs = [subprocess.Popen([HIPCC] + cflags + ["-c", "-o", o, s]) for o, s in zip(objs, [SRC, SRC_SPLINE])]
+    rcs = [p.wait() for p in procs]
+    if any(rcs):
+        raise subprocess.CalledProcessError(max(rcs), "hipcc -c")
+    subprocess.run([HIPCC] + FLAGS + list(extra) + ["-o", out + ".tmp"] + objs + ["-lrccl"], check=True)
+    os.replace(out + ".tmp", out)
+    for o in objs:
+        os.remove(o)
+
+
 def build(force=False):
     if force or needs_build():
-        cmd = [HIPCC] + FLAGS + ["-o", OUT + ".tmp", SRC, SRC_SPLINE, "-lrccl"]
-        subprocess.run(cmd, check=True)
-        os.replace(OUT + ".tmp", OUT)
+        _compile_link(OUT)
     return OUT
 
 
@@ -51,8 +64,7 @@ def build_host(force=False):
 def build_stamps():
     """Diagnostic variant with per-phase s_memrealtime stamps (tools/diag_stamps.py only)."""
     out = os.path.join(HERE, "libkalibr_hip_stamps.so")
-    subprocess.run([HIPCC] + FLAGS + ["-DKB_STAMPS", "-o", out + ".tmp", SRC, SRC_SPLINE, "-lrccl"], check=True)
-    os.replace(out + ".tmp", out)
+    _compile_link(out, ["-DKB_STAMPS"])
     return out
 
 
