@@ -251,7 +251,10 @@ kb_handle* kb_create(const kb_layout* L) {
   rc |= h->alloc(&d.psum_local, (size_t)d.Wtot);
   d.psum = d.psum_local;
   d.psum_rows = 1;
-  d.fold = 1;
+  // the pass end runs in its own one-block kernel (k_post), not folded into the next k_build: a folded end has block 0
+  // store the new control block while the other blocks load it, and under k_build's L2 pressure a block on another
+  // XCD can read it torn across cache lines (seen once as a diverged LM run on configs[3])
+  d.fold = 0;
   if (const char* e = std::getenv("KB_GN_FUSED")) h->gn_fuse = std::atoi(e) != 0;
   d.dbg_stop = -1;
   d.dbg_flags = 0;
@@ -268,6 +271,10 @@ kb_handle* kb_create(const kb_layout* L) {
   rc |= h->alloc(&d.red_local, 8);
   d.red = d.red_local;
   rc |= h->alloc(&d.ctrl, 1);
+  if (h->C > 64) {  // k_solve's staged camera block (k_colimg), sized as in the LDS budget below
+    const int nb = (h->C + 15) / 16;
+    rc |= h->alloc(&d.simg, (size_t)kTileSz * nb * (nb + 1) / 2 + 16 * nb + 2 + 256 * (size_t)h->N);
+  }
   std::vector<int32_t> colinfo(h->C), tri(h->C * (h->C + 1) / 2);
   for (int i = 0; i < h->N; ++i)
     for (int x = 0; x < d.nintr[i]; ++x) colinfo[d.col_intr[i] + x] = (0 << 16) | (i << 8) | x;
@@ -300,9 +307,10 @@ kb_handle* kb_create(const kb_layout* L) {
     if (C <= 64) {
       h->lds_solve = sizeof(double) * (C * (C + 1) / 2 + 2 * C + 1 + N * 256 + 2 * N * N * 36) + sizeof(int) * C;
     } else {  // 16 x 16 lower tiles + panel scratch + 1/D + solution vector
+      // k_colimg image [lower tiles | rhs (n16 + 2) | per-camera sums] + gl + T + K + panel scratch + 1/D + x
       const int nb = (C + 15) / 16, n16 = 16 * nb;
-      h->lds_solve = sizeof(double) * (8 * 17 * nb * (nb + 1) + 2 * C + 1 + N * 256 + 2 * N * N * 36 + 17 * (n16 - 16) +
-                                       2 * n16) +
+      d.img_n = kTileSz * nb * (nb + 1) / 2 + n16 + 2 + N * 256;
+      h->lds_solve = sizeof(double) * (d.img_n + ((C + 1) & ~1) + 2 * N * N * 36 + 17 * (n16 - 16) + 2 * n16) +
                      sizeof(int) * C;
     }
     h->solve_threads = C <= 64 ? 256 : 512;
@@ -490,6 +498,20 @@ static int allreduce_red(kb_handle* h, bool reduce = true) {
 static int launch_colsum(kb_handle* h, int gate, bool finish = true) {
   KbDev& d = h->d;
   hipLaunchKernelGGL(k_colsum, dim3((d.Wtot + 63) / 64, kColsumRows), dim3(256), 0, h->stream, d, gate);
+  if (finish && h->C > 64) {
+    // camera blocks for the tiled solve: the stage-1 rows are all-reduced as they are (sharded), then k_colimg
+    // finishes the sums (into the consumer's row) and writes k_solve's LDS image from the same rows
+    const double* rows = d.part8;
+    if (h->comm) {
+      KB_NCCL(ncclAllReduce(d.part8, h->psum_red8, (size_t)kColsumRows * d.Wtot, ncclDouble, ncclSum, h->comm,
+                            h->stream));
+      rows = h->psum_red8;
+    }
+    double* out = h->comm ? h->psum_red : d.psum_local;
+    hipLaunchKernelGGL(k_colimg, dim3((d.Wtot + d.img_n + 255) / 256), dim3(256), 0, h->stream, d, rows, out, gate);
+    KB_HIP(hipGetLastError());
+    return 0;
+  }
   if (finish) hipLaunchKernelGGL(k_colfin, dim3((d.Wtot + 255) / 256), dim3(256), 0, h->stream, d, gate);
   KB_HIP(hipGetLastError());
   if (h->comm) {
@@ -874,10 +896,14 @@ static int enqueue_pass(kb_handle* h, int policy, hipEvent_t ev0 = nullptr, hipE
   if (launch_colsum(h, 1, !from_rows)) return -1;
   if (launch_solve(h, 1, 1, from_rows)) return -1;
   if (launch_backsub(h, 1, 1, 1)) return -1;
-  // the pass end (accept / revert, next prelude) is folded into the next pass's k_build; sharded, the
-  // per-frame step rows of every rank are all-gathered first and every rank reduces all of them in rank order
+  // the pass end (accept / revert, next prelude): one block (k_post); sharded, the per-frame step rows of every
+  // rank are all-gathered first and every rank reduces all of them in rank order
   if (h->comm)
     KB_NCCL(ncclAllGather(d.bpart, h->bpart_all, 4 * (size_t)h->F_max, ncclDouble, h->comm, h->stream));
+  if (!d.fold) {
+    hipLaunchKernelGGL(k_post, dim3(1), dim3(256), 0, h->stream, d, 1);
+    KB_HIP(hipGetLastError());
+  }
   return 0;
 }
 

@@ -98,6 +98,8 @@ struct KbDev {
   const double* red_all;  // [nranks][4] all-gathered red_local (sharded runs)
   int nranks;
   double* trace;
+  double* simg;  // C > 64: k_solve's LDS image of the camera block (k_colimg) [img_n]
+  int img_n;
   KbCtrl* ctrl;
   int dbg_stop;   // diagnostic build only (KB_STAMPS): stop point of the timed kernel (-1: run to the end)
   int dbg_flags;  // diagnostic build only: bit 0 run the camera LDL^T twice (rolled)

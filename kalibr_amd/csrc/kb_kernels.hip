@@ -1353,7 +1353,7 @@ __global__ void __launch_bounds__(kMargThreads) k_marg(KbDev d, KbMarg mo) {
 // LDL^T (one wave when C <= 64, else the block with one barrier per column); dx_c; camera DV update
 // ---------------------------------------------------------------------------------------------
 
-__device__ double cam_entry_l(const int N, const int* ci, const double* Hs, const double* T, const double* K, int p,
+__device__ __forceinline__ double cam_entry_l(const int N, const int* ci, const double* Hs, const double* T, const double* K, int p,
                               int q) {
   const int kp = ci[p] >> 16, ip = (ci[p] >> 8) & 0xff, xp = ci[p] & 0xff;
   const int kq = ci[q] >> 16, iq = (ci[q] >> 8) & 0xff, xq = ci[q] & 0xff;
@@ -1384,7 +1384,7 @@ __device__ double cam_entry_l(const int N, const int* ci, const double* Hs, cons
   return s;
 }
 
-__device__ double cam_grad_l(const int N, const int* ci, const double* Hs, const double* K, int p) {
+__device__ __forceinline__ double cam_grad_l(const int N, const int* ci, const double* Hs, const double* K, int p) {
   const int kp = ci[p] >> 16, ip = (ci[p] >> 8) & 0xff, xp = ci[p] & 0xff;
   if (kp == 0) return Hs[ip * 256 + (6 + xp) * 16 + 15];
   double s = 0.0;
@@ -1429,152 +1429,240 @@ __device__ __forceinline__ int sidx(int i, int j, int C) {
     return tidx(i, j);
 }
 
-__device__ void ldl_tiles(const KbDev& d, double* S, double* rD, double* Wsc, int C, int nb, int* okl) {
-  const int tid = threadIdx.x, nth = blockDim.x, wave = tid >> 6, lane = tid & 63, nw = nth >> 6;
-  for (int p = 0; p < nb; ++p) {
-    const int b0 = tile_base(p, p);
-#ifdef KB_STAMPS
-    const int reps = (p == 0 && d.dbg_stop == 43) ? 2 : 1;  // diagnostic: second (I-cache warm) execution
-    for (int rep = 0; rep < reps; ++rep)
-#endif
-    if (wave == 0) {  // diagonal tile: lanes 0..15 hold its rows
-      const int r = lane < 16 ? lane : 15;
-      double row[16];
+// diagonal tile p factored in place by one wave (lanes 0..15 hold its rows, row k broadcast by v_readlane):
+// strictly lower Ltilde, D on the diagonal, rD[16 p + r] = 1 / D_r.  Returns false on a non-positive pivot (padding
+// rows have D = 1: only real pivots can fail).
+__device__ __forceinline__ bool diag_ldl16(double* S, double* rD, int p, int lane) {
+  const int b0 = tile_base(p, p);
+  const int r = lane < 16 ? lane : 15;
+  double row[16];
 #pragma unroll
-      for (int c = 0; c < 16; ++c) row[c] = S[b0 + (r > c ? r : c) * kTS + (r > c ? c : r)];
-      bool ok = true;
-      double rd = 1.0;
+  for (int c = 0; c < 16; ++c) row[c] = S[b0 + (r > c ? r : c) * kTS + (r > c ? c : r)];
+  bool ok = true;
+  double rd = 1.0;
 #pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        const double Dk = readlane_d(row[k], k);
-        ok = ok && (Dk > 0.0);
-        const double rdk = recip_d(Dk);
-        rd = (lane == k) ? rdk : rd;
-        const double f = (lane > k) ? row[k] * rdk : 0.0;
+  for (int k = 0; k < 16; ++k) {
+    const double Dk = readlane_d(row[k], k);
+    ok = ok && (Dk > 0.0);
+    const double rdk = recip_d(Dk);
+    rd = (lane == k) ? rdk : rd;
+    const double f = (lane > k) ? row[k] * rdk : 0.0;
 #pragma unroll
-        for (int j = k + 1; j < 16; ++j) row[j] -= f * readlane_d(row[j], k);
-      }
-      double lrow[16];
+    for (int j = k + 1; j < 16; ++j) row[j] -= f * readlane_d(row[j], k);
+  }
+  double lrow[16];
 #pragma unroll
-      for (int c = 0; c < 16; ++c) lrow[c] = row[c] * readlane_d(rd, c);  // Ltilde[r][c] = (L D)[r][c] / D_c
-      if (lane < 16) {
+  for (int c = 0; c < 16; ++c) lrow[c] = row[c] * readlane_d(rd, c);  // Ltilde[r][c] = (L D)[r][c] / D_c
+  if (lane < 16) {
 #pragma unroll
-        for (int c = 0; c < 16; ++c)
-          if (c <= lane) S[b0 + lane * kTS + c] = (c < lane) ? lrow[c] : row[c];  // strictly lower Ltilde, diag D
-        rD[16 * p + lane] = rd;
-      }
-      if (!ok && lane == 0) *okl = 0;  // padding rows have D = 1: only real pivots can fail
+    for (int c = 0; c < 16; ++c)
+      if (c <= lane) S[b0 + lane * kTS + c] = (c < lane) ? lrow[c] : row[c];  // strictly lower Ltilde, diag D
+    rD[16 * p + lane] = rd;
+  }
+  return ok;
+}
+
+// rows of panel tile (i, p) by one wave (lanes 0..15, one row each): W = S_ip Ltilde_pp^-T into Wsc (row
+// 16 (i - p - 1) + r), Ltilde_ip = W D_p^-1 in place.  Column-oriented substitution: every step updates all later
+// columns at once (a 15-deep dependency chain), each w[c] accumulated in the order c2 = 0, 1, ..., c - 1.
+__device__ __forceinline__ void panel_trsm16(double* S, const double* rD, double* Wsc, int p, int i, int lane) {
+  const int b0 = tile_base(p, p);
+  const int r = lane & 15;
+  double* srow = S + tile_base(i, p) + r * kTS;
+  double w[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) w[c] = srow[c];
+#pragma unroll
+  for (int c2 = 0; c2 < 15; ++c2)
+#pragma unroll
+    for (int c = c2 + 1; c < 16; ++c) w[c] -= w[c2] * S[b0 + c * kTS + c2];
+  if (lane < 16) {
+    double* wrow = Wsc + (16 * (i - p - 1) + r) * kTS;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      wrow[c] = w[c];
+      srow[c] = w[c] * rD[16 * p + c];
     }
-    __syncthreads();
-    if (p == 0) KB_STAMP(d, 40);
-    if (p == 0) KB_STAMP(d, 43);
-    if (p < 3) KB_STAMP(d, 50 + 3 * p);
-    if (p == nb - 1) break;
-    // rows below the panel: W = S_ip Ltilde_pp^-T (stored in Wsc), Ltilde_ip = W D^-1 (in place)
-    const int nr = 16 * (nb - p - 1);
-    for (int g = tid; g < nr; g += nth) {
-      double* srow = S + tile_base(p + 1 + (g >> 4), p) + (g & 15) * kTS;
-      double w[16];
-#pragma unroll
-      for (int c = 0; c < 16; ++c) w[c] = srow[c];
-#pragma unroll
-      for (int c = 1; c < 16; ++c)
-#pragma unroll
-        for (int c2 = 0; c2 < c; ++c2) w[c] -= w[c2] * S[b0 + c * kTS + c2];
-#pragma unroll
-      for (int c = 0; c < 16; ++c) {
-        Wsc[g * kTS + c] = w[c];
-        srow[c] = w[c] * rD[16 * p + c];
-      }
-    }
-    __syncthreads();
-    if (p == 0) KB_STAMP(d, 41);
-    if (p < 3) KB_STAMP(d, 51 + 3 * p);
-    // trailing tiles (i, j), p < j <= i < nb: S_ij -= W_i Ltilde_j^T on MFMA (lane l: A[l&15][k], B[k][l&15])
-    const int m = nb - p - 1, ntiles = m * (m + 1) / 2;
-    for (int q = wave; q < ntiles; q += nw) {
-      const int ii = tri_row(q), jj = q - ii * (ii + 1) / 2;
-      const double* A = Wsc + ii * kTileSz;
-      const double* B = S + tile_base(p + 1 + jj, p);
-      v4d acc = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const int k = 4 * s + (lane >> 4);
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(A[(lane & 15) * kTS + k], B[(lane & 15) * kTS + k], acc, 0, 0, 0);
-      }
-      double* Ct = S + tile_base(p + 1 + ii, p + 1 + jj);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) Ct[((lane >> 4) + 4 * r) * kTS + (lane & 15)] -= acc[r];
-    }
-    __syncthreads();
-    if (p == 0) KB_STAMP(d, 42);
-    if (p < 3) KB_STAMP(d, 52 + 3 * p);
   }
 }
 
-// xv (n = 16 nb entries, b on entry, zero-padded) <- (Ltilde D Ltilde^T)^-1 b
-__device__ void ldl_tiles_solve(const double* S, const double* rD, double* xv, int nb) {
-  const int tid = threadIdx.x, nth = blockDim.x, wave = tid >> 6, lane = tid & 63;
+// trailing tile (i, j), p < j <= i: S_ij -= W_ip Ltilde_jp^T on MFMA (lane l: A[l&15][k], B[k][l&15])
+__device__ __forceinline__ void trail_update16(double* S, const double* Wsc, int p, int i, int j, int lane) {
+  const double* A = Wsc + 16 * (i - p - 1) * kTS;
+  const double* B = S + tile_base(j, p);
+  v4d acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int k = 4 * s + (lane >> 4);
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(A[(lane & 15) * kTS + k], B[(lane & 15) * kTS + k], acc, 0, 0, 0);
+  }
+  double* Ct = S + tile_base(i, j);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) Ct[((lane >> 4) + 4 * r) * kTS + (lane & 15)] -= acc[r];
+}
+
+// Right-looking blocked LDL^T with a one-panel lookahead, two barriers per panel (8 waves):
+//   phase 1 of panel p: wave w solves the rows of panel tile i = p + 1 + w against Ltilde_pp (panel_trsm16); wave 0
+//            (i = p + 1) then applies panel p to the next diagonal tile (p + 1, p + 1) at once (it owns both operands);
+//   phase 2 of panel p: wave 0 factors diagonal tile p + 1 while the other waves apply panel p to the remaining
+//            trailing tiles.
+// The chain factor(p) -> trsm(p + 1, p) -> update(p + 1, p + 1) -> factor(p + 1) is the critical path; the bulk
+// trailing updates run beside the factorization.  Same arithmetic (and accumulation orders) as a panel-at-a-time
+// blocked factorization with the scalar right-looking LDL^T per diagonal tile.  One call site per helper: the
+// kernel runs on one CU whose instruction cache is cold at every launch, so code size is time.
+__device__ __forceinline__ void ldl_tiles(const KbDev& d, double* S, double* rD, double* Wsc, int C, int nb, int* okl) {
+  const int tid = threadIdx.x, nth = blockDim.x, wave = tid >> 6, lane = tid & 63, nw = nth >> 6;
+#pragma unroll 1
+  for (int p = 0; p < nb; ++p) {
+    // phase 2 of panel p - 1: diagonal tile p (wave 0) | trailing tiles of panel p - 1 except (p, p)
+    if (wave == 0) {
+      KB_WAVE_SYNC();
+      const bool ok = diag_ldl16(S, rD, p, lane);
+      if (!ok && lane == 0) *okl = 0;
+    } else if (p > 0) {
+      const int m = nb - p;  // trailing tiles (p + ii, p + jj), 0 <= jj <= ii < m; q = 0 is (p, p)
+      const int ntiles = m * (m + 1) / 2;
+#pragma unroll 1
+      for (int q = wave; q < ntiles; q += nw - 1) {
+        const int ii = tri_row(q), jj = q - ii * (ii + 1) / 2;
+        trail_update16(S, Wsc, p - 1, p + ii, p + jj, lane);
+      }
+    }
+    __syncthreads();
+    if (p == 0) KB_STAMP(d, 40);
+    if (p == nb - 1) break;
+    // phase 1 of panel p
+#pragma unroll 1
+    for (int ii = wave; ii < nb - p - 1; ii += nw) panel_trsm16(S, rD, Wsc, p, p + 1 + ii, lane);
+    if (wave == 0) {
+      KB_WAVE_SYNC();  // this wave's W and Ltilde rows of tile (p + 1, p) are in LDS
+      trail_update16(S, Wsc, p, p + 1, p + 1, lane);
+    }
+    __syncthreads();
+    if (p == 0) KB_STAMP(d, 41);
+  }
+}
+
+// xv (n = 16 nb entries, b on entry, zero-padded) <- (Ltilde D Ltilde^T)^-1 b, by one wave (no block barriers:
+// the wave's own LDS writes are waited for before the lanes read each other's entries)
+__device__ __forceinline__ void ldl_tiles_solve(const double* S, const double* rD, double* xv, int nb) {
+  const int lane = threadIdx.x & 63;
   const int n = 16 * nb;
   for (int p = 0; p < nb; ++p) {  // forward: Ltilde y = b
     const int b0 = tile_base(p, p);
-    if (wave == 0) {
-      const int r = lane < 16 ? lane : 15;
-      double Lr[16];
+    const int r = lane < 16 ? lane : 15;
+    double Lr[16];
 #pragma unroll
-      for (int c = 0; c < 16; ++c) {
-        const double v = S[b0 + r * kTS + c];
-        Lr[c] = (c < r) ? v : 0.0;
-      }
-      double xr = xv[16 * p + r];
-#pragma unroll
-      for (int k = 0; k < 16; ++k) xr -= Lr[k] * readlane_d(xr, k);
-      if (lane < 16) xv[16 * p + lane] = xr;
+    for (int c = 0; c < 16; ++c) {
+      const double v = S[b0 + r * kTS + c];
+      Lr[c] = (c < r) ? v : 0.0;
     }
-    __syncthreads();
-    for (int g = 16 * (p + 1) + tid; g < n; g += nth) {
+    double xr = xv[16 * p + r];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) xr -= Lr[k] * readlane_d(xr, k);
+    if (lane < 16) xv[16 * p + lane] = xr;
+    KB_WAVE_SYNC();
+    for (int g = 16 * (p + 1) + lane; g < n; g += 64) {
       const double* lr = S + tile_base(g >> 4, p) + (g & 15) * kTS;
       double s = 0.0;
 #pragma unroll
       for (int c = 0; c < 16; ++c) s += lr[c] * xv[16 * p + c];
       xv[g] -= s;
     }
-    __syncthreads();
+    KB_WAVE_SYNC();
   }
-  for (int g = tid; g < n; g += nth) xv[g] *= rD[g];  // z = D^-1 y
-  __syncthreads();
+  for (int g = lane; g < n; g += 64) xv[g] *= rD[g];  // z = D^-1 y
+  KB_WAVE_SYNC();
   for (int p = nb - 1; p >= 0; --p) {  // backward: Ltilde^T x = z
     const int b0 = tile_base(p, p);
-    if (wave == 0) {
-      const int r = lane < 16 ? lane : 15;
-      double Lc[16];
+    const int r = lane < 16 ? lane : 15;
+    double Lc[16];
 #pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        const double v = S[b0 + k * kTS + r];
-        Lc[k] = (k > r) ? v : 0.0;
-      }
-      double xr = xv[16 * p + r];
-#pragma unroll
-      for (int k = 15; k >= 0; --k) xr -= Lc[k] * readlane_d(xr, k);
-      if (lane < 16) xv[16 * p + lane] = xr;
+    for (int k = 0; k < 16; ++k) {
+      const double v = S[b0 + k * kTS + r];
+      Lc[k] = (k > r) ? v : 0.0;
     }
-    __syncthreads();
+    double xr = xv[16 * p + r];
+#pragma unroll
+    for (int k = 15; k >= 0; --k) xr -= Lc[k] * readlane_d(xr, k);
+    if (lane < 16) xv[16 * p + lane] = xr;
+    KB_WAVE_SYNC();
     if (p == 0) break;
-    for (int g = tid; g < 16 * p; g += nth) {  // rows of earlier panels: z_g -= sum_r Ltilde_{p,q}[r][g] x_p[r]
+    for (int g = lane; g < 16 * p; g += 64) {  // rows of earlier panels: z_g -= sum_r Ltilde_{p,q}[r][g] x_p[r]
       const double* lc = S + tile_base(p, g >> 4) + (g & 15);
       double s = 0.0;
 #pragma unroll
       for (int r = 0; r < 16; ++r) s += lc[r * kTS] * xv[16 * p + r];
       xv[g] -= s;
     }
-    __syncthreads();
+    KB_WAVE_SYNC();
   }
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_colimg (C > 64): finishes the column sums as k_colfin does (out[e] = sum_r rows[r][e], fixed order; max for
+// the max|dx_f| columns) and writes k_solve's LDS image of the camera block from the same rows:
+//   [S lower 16 x 16 tiles, stride kTS: -sum Y^T Y (diagonal tiles: lower half), identity padding beyond C |
+//    rhs (n16 + 2 slots): -sum Y^T z, slot C: the non-PD frame-block count | per-camera 16 x 16 sums, mirrored].
+// One thread per entry (the index arithmetic runs wide here, not in the one-block solve, which stages the image
+// with one contiguous copy).
+// ---------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_colimg(KbDev d, const double* rows, double* out, int gate) {
+  if (gate && d.ctrl->done) return;
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  const int N = d.N, C = d.C, Wt = d.W - d.C;
+  int src = -1;  // -1: zero, -2: one (identity padding)
+  double sg = 1.0;
+  double* dst;
+  if (q < d.Wtot) {
+    src = q;
+    dst = out + q;
+  } else {
+    const int e = q - d.Wtot;
+    if (e >= d.img_n) return;
+    dst = d.simg + e;
+    const int nb = (C + 15) >> 4, n16 = 16 * nb, ntz = kTileSz * nb * (nb + 1) / 2;
+    if (e < ntz) {
+      const int t = e / kTileSz, w = e - t * kTileSz, r = w / kTS, cc = w - r * kTS;
+      const int it = tri_row(t), jt = t - it * (it + 1) / 2;
+      const int i = 16 * it + r, j = 16 * jt + cc;
+      if (cc < 16 && (it > jt || cc <= r)) {
+        if (i < C) {
+          src = N * 136 + upper_index(j, i, C);
+          sg = -1.0;
+        } else if (i == j) {
+          src = -2;
+        }
+      }
+    } else if (e < ntz + n16 + 2) {
+      const int k = e - ntz;
+      if (k < C) {
+        src = N * 136 + Wt + k;
+        sg = -1.0;
+      } else if (k == C) {
+        src = N * 136 + Wt + C;
+      }
+    } else {
+      const int hq = e - ntz - n16 - 2, cam = hq >> 8, a = (hq >> 4) & 15, b = hq & 15;
+      src = cam * 136 + d16_index(min(a, b), max(a, b));
+    }
+  }
+  double acc = src == -2 ? 1.0 : 0.0;
+  if (src >= 0) {
+    double v[kColsumRows];
+#pragma unroll
+    for (int r = 0; r < kColsumRows; ++r) v[r] = rows[(size_t)r * d.Wtot + src];
+    const bool mx = src >= d.Wp;
+#pragma unroll
+    for (int r = 0; r < kColsumRows; ++r) acc = mx ? fmax(acc, v[r]) : acc + v[r];
+  }
+  *dst = sg * acc;
 }
 
 // batched global -> LDS staging of the k_solve inputs: every thread keeps U independent loads in flight
 // (a runtime-bounded copy loop would otherwise wait for each load before the next).  Items are laid out as
 // [camK N*N*36 | per-camera sums N*256 | Schur sums Wt | Schur rhs C | colinfo C] over one index space.
-template <int U, int CM>
+template <int U, int CM, bool ONE_ROW>
 __device__ __forceinline__ void solve_stage(const KbDev& d, int bslot, double* K, double* Hs, double* S, double* bv,
                                             int* ci, int tid, int nth) {
   const int N = d.N, C = d.C, Wt = d.W - C;
@@ -1589,7 +1677,7 @@ __device__ __forceinline__ void solve_stage(const KbDev& d, int bslot, double* K
       if (q < n0)
         v[u] = Kc[q];
       else if (q < n3)
-        v[u] = psum_at(d, q - n0);  // camera sums, Schur sums, rhs, count: contiguous in the partial rows
+        v[u] = ONE_ROW ? d.psum[q - n0] : psum_at(d, q - n0);  // camera sums, Schur sums, rhs, count: contiguous
       else
         v[u] = (double)d.colinfo[q - n3];
     }
@@ -1725,7 +1813,7 @@ __device__ __forceinline__ LdlOut ldl_solve_reg(const KbDev& d, const double* S,
 // of H_cc (lanes = the block's entries):  intrinsics_i x intrinsics_i = Hs_i[II];
 // intrinsics_i x B_j = Hs_i[Id] K_{i,j} (j < i);  B_j x B_k = sum_{i > max(j,k)} K_{i,j}^T T_{i,k}, T = Hs_i[dd] K
 template <int CM>
-__device__ void cam_expand_blocks(double* S, int C, int N, const int (*ctab)[KB_MAX_CAMS], const double* Hs,
+__device__ __forceinline__ void cam_expand_blocks(double* S, int C, int N, const int (*ctab)[KB_MAX_CAMS], const double* Hs,
                                   const double* T, const double* K, double lam2, int nw) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int nA = N, nB = N * (N - 1) / 2, nC = (N - 1) * N / 2;
@@ -1776,11 +1864,13 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update, int nth) {
   const int N = d.N, C = d.C, W = d.W, tid = threadIdx.x;
   const int Cp = C * (C + 1) / 2;
   const int nb = (C + 15) >> 4, n16 = 16 * nb;  // CM == 0: 16 x 16 tiles
-  double* S = sm;                    // CM > 0: column-major packed lower [Cp]; CM == 0: lower tiles
-  double* bv = S + (CM > 0 ? Cp : kTileSz * nb * (nb + 1) / 2);  // [C] (+1: non-PD frame-block count while staging)
-  double* gl = bv + C + 1;           // [C]
-  double* Hs = gl + C;               // [N][256]
-  double* T = Hs + N * 256;          // [N][N][36]
+  // CM > 0: S column-major packed lower [Cp] | bv [C + 1] (slot C: non-PD frame-block count) | gl [C] | Hs [N][256]
+  // CM == 0: the k_colimg image [S lower tiles | bv (n16 + 2) | Hs [N][256]] | gl (C, even-padded)
+  double* S = sm;
+  double* bv = S + (CM > 0 ? Cp : kTileSz * nb * (nb + 1) / 2);
+  double* Hs = CM > 0 ? bv + 2 * C + 1 : bv + n16 + 2;
+  double* gl = CM > 0 ? bv + C + 1 : Hs + N * 256;
+  double* T = CM > 0 ? Hs + N * 256 : gl + ((C + 1) & ~1);  // [N][N][36]
   double* K = T + N * N * 36;        // [N][N][36]
   double* Wsc = K + N * N * 36;      // CM == 0: [n16 - 16][kTS] panel scratch
   double* rDv = Wsc + (CM > 0 ? 0 : kTS * (n16 - 16));  // CM == 0: [n16] 1/D
@@ -1813,11 +1903,34 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update, int nth) {
   }
   KB_STAMP(d, 0);
   // phase A: stage K, column info, per-camera sums and the Schur sums in LDS (one row: psum)
-  solve_stage<CM == 0 ? 8 : 4, CM>(d, bslot, K, Hs, S, bv, ci, tid, nth);
+  if constexpr (CM == 0) {
+    // the k_colimg image and the chains K of the build state: one contiguous 16-byte copy, 12 loads in flight per
+    // thread (one round trip for an 8-camera rig)
+    const int n2i = d.img_n >> 1, n2 = n2i + N * N * 18;
+    const double2* gi = reinterpret_cast<const double2*>(d.simg);
+    const double2* gk = reinterpret_cast<const double2*>(cam_K(d, bslot)) - n2i;
+    double2* li = reinterpret_cast<double2*>(S);
+    double2* lk = reinterpret_cast<double2*>(K) - n2i;
+    constexpr int U = 12;
+#pragma unroll 1
+    for (int q0 = tid; q0 < n2; q0 += U * nth) {
+      double2 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int q = min(q0 + u * nth, n2 - 1);
+        v[u] = *(q < n2i ? gi + q : gk + q);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int q = q0 + u * nth;
+        if (q < n2) *(q < n2i ? li + q : lk + q) = v[u];
+      }
+    }
+    for (int p = tid; p < C; p += nth) ci[p] = d.colinfo[p];
+  } else {
+    solve_stage<4, CM, false>(d, bslot, K, Hs, S, bv, ci, tid, nth);
+  }
   if (tid < 3 * N) ctab[tid / N][tid % N] = tid < N ? cam_arg(d.nintr, tid) : (tid < 2 * N ? cam_arg(d.col_intr, tid - N) : cam_arg(d.col_base, tid - 2 * N));
-  if (CM == 0)  // identity padding of the tiles beyond C (disjoint from the staged entries)
-    for (int i = C; i < n16; ++i)
-      for (int j = tid; j <= i; j += nth) S[tidx(i, j)] = (i == j) ? 1.0 : 0.0;
   __syncthreads();
   if (tid == 0) okl = (c->solve_ok != 0) && !(bv[C] > 0.0);
   // the loop's done flag is tested only here: the ctrl and staging loads above went out in one round trip, and
@@ -1903,10 +2016,10 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update, int nth) {
 #endif
     ldl_tiles(d, S, rDv, Wsc, C, nb, &okl);
     KB_STAMP(d, 3);
-    for (int g = tid; g < n16; g += nth) xv[g] = g < C ? bv[g] : 0.0;
-    __syncthreads();
-    ldl_tiles_solve(S, rDv, xv, nb);
-    if (tid < 64) {
+    if (tid < 64) {  // the solves run in one wave
+      for (int g = tid; g < n16; g += 64) xv[g] = g < C ? bv[g] : 0.0;
+      KB_WAVE_SYNC();
+      ldl_tiles_solve(S, rDv, xv, nb);
 #pragma unroll
       for (int sl = 0; sl < 2; ++sl) x[sl] = (tid + 64 * sl < C) ? xv[tid + 64 * sl] : 0.0;
     }

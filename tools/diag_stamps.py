@@ -22,7 +22,7 @@ KERNELS = {
                     (21, "bar"), (23, "gauss-jordan"), (24, "acc"), (25, "part row"), (-1, "end")]),
     "k_build_gn": (3, [(14, "round2+step f0"), (16, "staged"), (26, "pose"), (27, "proj"), (17, "corners+mfma"), (18, "bar"), (19, "viewsum"), (28, "G"), (29, "P,dH"), (20, "expand+frame"),
                     (21, "bar"), (23, "gauss-jordan"), (24, "acc"), (25, "part row"), (-1, "end")]),
-    "k_solve": (1, [(0, "entry"), (1, "stage"), (2, "cam expand"), (47, "ldl#1 (flag 1)"), (50, "p0 diag"), (51, "p0 trsm"), (52, "p0 upd"), (53, "p1 diag"), (54, "p1 trsm"), (55, "p1 upd"), (56, "p2 diag"), (57, "p2 trsm"), (58, "p2 upd"), (45, "ldl rows"), (46, "ldl factor"), (3, "ldl+solves"), (4, "solves"), (5, "stats+update"),
+    "k_solve": (1, [(0, "entry"), (1, "stage"), (2, "cam expand"), (40, "diag 0"), (41, "p0 trsm+tile"), (42, "p0 diag 1 | trailing"), (45, "ldl rows"), (46, "ldl factor"), (3, "ldl"), (4, "solves"), (5, "stats+update"),
                     (-1, "end (chains)")]),
     "k_backsub": (2, [(30, "round1"), (31, "dx_f"), (32, "pose"), (33, "cost"), (-1, "end")]),
 }
