@@ -1199,6 +1199,18 @@ int kb_comm_init(kb_handle* h, const void* uid, int32_t nranks, int32_t rank) {
 }
 
 #ifdef KB_STAMPS
+// diagnostic build only: the KB_TS timeline of the last k_solve launch (100 MHz ticks)
+int kb_diag_read_ts(kb_handle* h, long long* out, int n) {
+  if (!h->d.dbg_ts) {
+    KB_HIP(hipMalloc(&h->d.dbg_ts, 64 * sizeof(long long)));
+    KB_HIP(hipMemset(h->d.dbg_ts, 0, 64 * sizeof(long long)));
+    drop_graphs(h);
+    return 0;
+  }
+  KB_HIP(hipMemcpy(out, h->d.dbg_ts, sizeof(long long) * std::min(n, 64), hipMemcpyDeviceToHost));
+  return 0;
+}
+
 // diagnostic build only: average duration (us, HIP events over `reps` launches) of one kernel of the GN pass run
 // up to stop point `stop` (KB_STAMP): which = 0 fused build, 1 camera solve, 2 back-substitution, 3 GN fused build.
 int kb_diag_phase_time(kb_handle* h, int which, int stop, int reps, int flags, double* us) {

@@ -103,6 +103,7 @@ struct KbDev {
   KbCtrl* ctrl;
   int dbg_stop;   // diagnostic build only (KB_STAMPS): stop point of the timed kernel (-1: run to the end)
   int dbg_flags;  // diagnostic build only: bit 0 run the camera LDL^T twice (rolled)
+  long long* dbg_ts;  // diagnostic build only: [64] s_memrealtime stamps of the last k_solve (KB_TS)
 };
 
 #ifdef KB_STAMPS
@@ -113,9 +114,17 @@ struct KbDev {
   do {                          \
     if ((d).dbg_stop == (i)) return; \
   } while (0)
+// timeline stamp (100 MHz s_memrealtime) of thread 0 at point i of the last launch, without leaving the kernel
+#define KB_TS(d, i)                                                                      \
+  do {                                                                                   \
+    if (threadIdx.x == 0 && (d).dbg_ts) (d).dbg_ts[i] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
 #else
 #define KB_STAMP(d, i) \
   do {                 \
+  } while (0)
+#define KB_TS(d, i) \
+  do {              \
   } while (0)
 #endif
 

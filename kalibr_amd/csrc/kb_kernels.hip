@@ -354,36 +354,46 @@ __device__ void pass_end_block(const KbDev& d, const KbCtrl& cin, KbCtrl* out, b
 // camera chains of a state: L_i (R|t) = B_{i-1}..B_0 and K_{i,j} (one block) -> slot `slot` of camL / camK.
 // `base` points at the N-1 baseline poses (7-stride, HBM or LDS).
 // ---------------------------------------------------------------------------------------------
-__device__ void chain_block(const KbDev& d, const double* base, int slot, int nth) {
+__device__ __forceinline__ void chain_block(const KbDev& d, const double* base, int slot, int nth) {
+  // P(i, j) = B_{i-1} ... B_{j+1} for -1 <= j < i (P(i, i-1) = I): L_i = P(i, -1), K_{i,j} from P(i, j) and B_j.
+  // One thread per pair builds its product in the reference association order (Q <- B_k Q, k = j+1 .. i-1), so
+  // every chain equals the former per-entry recomputation bit for bit; the 36 entries of K_{i,j} then read it.
   __shared__ double sR[KB_MAX_CAMS][9], st[KB_MAX_CAMS][3];  // baseline B_j
-  __shared__ double LR[KB_MAX_CAMS][9], Lt[KB_MAX_CAMS][3];
-  const int N = d.N;
+  // pair (i, j) at i(i+1)/2 + j + 1: R (9) | t (3); C <= 111 bounds the rig to N <= 10 cameras (55 pairs)
+  __shared__ double PR[64][12];
+  const int N = d.N, np = N * (N + 1) / 2;
   double* Lo = cam_L(d, slot);
   double* Ko = cam_K(d, slot);
   if (threadIdx.x < N - 1) pose_rt(base + 7 * threadIdx.x, sR[threadIdx.x], st[threadIdx.x]);
   __syncthreads();
-  if (threadIdx.x == 0) {
-    for (int q = 0; q < 9; ++q) LR[0][q] = (q % 4 == 0) ? 1.0 : 0.0;
-    Lt[0][0] = Lt[0][1] = Lt[0][2] = 0.0;
-    for (int i = 1; i < N; ++i) rt_mul(sR[i - 1], st[i - 1], LR[i - 1], Lt[i - 1], LR[i], Lt[i]);
+  if (threadIdx.x < np) {
+    const int q = threadIdx.x, i = tri_row(q), j = q - i * (i + 1) / 2 - 1;
+    double QR[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, Qt[3] = {0, 0, 0};
+#pragma unroll 1
+    for (int k = j + 1; k < i; ++k) {
+      double R2[9], t2[3];
+      rt_mul(sR[k], st[k], QR, Qt, R2, t2);
+#pragma unroll
+      for (int e = 0; e < 9; ++e) QR[e] = R2[e];
+#pragma unroll
+      for (int e = 0; e < 3; ++e) Qt[e] = t2[e];
+    }
+#pragma unroll
+    for (int e = 0; e < 9; ++e) PR[q][e] = QR[e];
+#pragma unroll
+    for (int e = 0; e < 3; ++e) PR[q][9 + e] = Qt[e];
   }
   __syncthreads();
-  for (int q = threadIdx.x; q < N * 12; q += nth) {
+  for (int q = threadIdx.x; q < N * 12; q += nth) {  // L_i = P(i, -1)
     const int i = q / 12, e = q % 12;
-    Lo[q] = e < 9 ? LR[i][e] : Lt[i][e - 9];
+    Lo[q] = PR[i * (i + 1) / 2][e];
   }
   for (int idx = threadIdx.x; idx < N * N * 36; idx += nth) {
     const int e = idx % 36, ij = idx / 36, i = ij / N, j = ij % N;
     double val = 0.0;
     if (j < i) {
-      double QR[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, Qt[3] = {0, 0, 0};
-      for (int k = j + 1; k < i; ++k) {
-        double R2[9], t2[3];
-        rt_mul(sR[k], st[k], QR, Qt, R2, t2);
-        for (int q = 0; q < 9; ++q) QR[q] = R2[q];
-        for (int q = 0; q < 3; ++q) Qt[q] = t2[q];
-      }
-      val = -chain_entry(QR, Qt, st[j], e / 6, e % 6);
+      const double* P = PR[i * (i + 1) / 2 + j + 1];
+      val = -chain_entry(P, P + 9, st[j], e / 6, e % 6);
     }
     Ko[idx] = val;
   }
@@ -1517,8 +1527,10 @@ __device__ __forceinline__ void ldl_tiles(const KbDev& d, double* S, double* rD,
     // phase 2 of panel p - 1: diagonal tile p (wave 0) | trailing tiles of panel p - 1 except (p, p)
     if (wave == 0) {
       KB_WAVE_SYNC();
+      KB_TS(d, 20 + 4 * p);
       const bool ok = diag_ldl16(S, rD, p, lane);
       if (!ok && lane == 0) *okl = 0;
+      KB_TS(d, 21 + 4 * p);
     } else if (p > 0) {
       const int m = nb - p;  // trailing tiles (p + ii, p + jj), 0 <= jj <= ii < m; q = 0 is (p, p)
       const int ntiles = m * (m + 1) / 2;
@@ -1536,9 +1548,13 @@ __device__ __forceinline__ void ldl_tiles(const KbDev& d, double* S, double* rD,
     for (int ii = wave; ii < nb - p - 1; ii += nw) panel_trsm16(S, rD, Wsc, p, p + 1 + ii, lane);
     if (wave == 0) {
       KB_WAVE_SYNC();  // this wave's W and Ltilde rows of tile (p + 1, p) are in LDS
+      KB_TS(d, 22 + 4 * p);
       trail_update16(S, Wsc, p, p + 1, p + 1, lane);
+      KB_WAVE_SYNC();
+      KB_TS(d, 23 + 4 * p);
     }
     __syncthreads();
+    KB_TS(d, 10 + p);
     if (p == 0) KB_STAMP(d, 41);
   }
 }
@@ -1901,6 +1917,7 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update, int nth) {
     dxr = psum_max_at(d, d.Wp + min(tid, nr - 1));
     for (int r = tid + 64; r < nr; r += 64) dxr = fmax(dxr, psum_max_at(d, d.Wp + r));
   }
+  KB_TS(d, 0);
   KB_STAMP(d, 0);
   // phase A: stage K, column info, per-camera sums and the Schur sums in LDS (one row: psum)
   if constexpr (CM == 0) {
@@ -1937,6 +1954,7 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update, int nth) {
   // nothing global has been written yet
   if (gate && c->done) return;
   if (gate && !d.gn_fused && tid == 0) c->pending = 1;
+  KB_TS(d, 1);
   KB_STAMP(d, 1);
   // phase B: camera block expansion
   for (int q = tid; q < N * N * 36; q += nth) {
@@ -1981,6 +1999,7 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update, int nth) {
     __syncthreads();
     if (fin[0]) return;
   }
+  KB_TS(d, 2);
   cam_expand_blocks<CM>(S, C, N, ctab, Hs, T, K, lam2, nth >> 6);
   for (int p = tid; p < C; p += nth) {
     const double g = cam_grad_l(N, ci, Hs, K, p);
@@ -1990,6 +2009,7 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update, int nth) {
     d.rhs[p] = g;
   }
   __syncthreads();
+  KB_TS(d, 3);
   KB_STAMP(d, 2);
   if constexpr (CM > 0) {
 #ifdef KB_STAMPS
@@ -2015,6 +2035,7 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update, int nth) {
     }
 #endif
     ldl_tiles(d, S, rDv, Wsc, C, nb, &okl);
+    KB_TS(d, 4);
     KB_STAMP(d, 3);
     if (tid < 64) {  // the solves run in one wave
       for (int g = tid; g < n16; g += 64) xv[g] = g < C ? bv[g] : 0.0;
@@ -2026,6 +2047,7 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update, int nth) {
     KB_STAMP(d, 4);
   }
   __syncthreads();  // okl final
+  KB_TS(d, 5);
   if (gfu) {
     if (fin[0]) return;  // the loop ended at the previous pass: this solve is discarded
     cur = fin[1];
@@ -2117,11 +2139,13 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update, int nth) {
       }
     }
   }
+  KB_TS(d, 6);
   KB_STAMP(d, 5);
   if (do_update) {
     __syncthreads();
     chain_block(d, nbase, 1 - cur, nth);  // chains of the candidate state (k_backsub's cost, next build if accepted)
   }
+  KB_TS(d, 7);
 }
 
 // CM > 0: 4 waves (one factors); CM == 0: 8 waves

@@ -1,0 +1,36 @@
+"""Diagnostic: timeline of one k_solve launch inside the captured GN passes (KB_TS stamps, s_memrealtime 100 MHz),
+diagnostic library only: python tools/diag_tstamps.py [config]"""
+import ctypes as C
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from kalibr_amd import capi, synth  # noqa: E402
+
+capi.LIB_PATH = os.path.join(ROOT, "kalibr_amd", "libkalibr_hip_stamps.so")
+L = capi.lib()
+L.kb_diag_read_ts.argtypes = [C.c_void_p, C.POINTER(C.c_longlong), C.c_int]
+cfg = int(sys.argv[1]) if len(sys.argv) > 1 else 4
+p = synth.make_config(cfg)
+g = capi.Solver(p)
+g.set_state(p.state_init)
+buf = (C.c_longlong * 64)()
+assert L.kb_diag_read_ts(g.h, buf, 64) == 0  # allocates the stamp buffer
+names = {0: "entry", 1: "staged", 2: "T (+pass end)", 3: "H_cc blocks + grad", 4: "LDL^T", 5: "solves",
+         6: "stats + DV update", 7: "chains"}
+for i in range(10, 20):
+    names[i] = f"  panel {i - 10}"
+for q in range(7):
+    names[20 + 4 * q] = f"    p{q} diag start"
+    names[21 + 4 * q] = f"    p{q} diag end"
+    names[22 + 4 * q] = f"    p{q} trsm end"
+    names[23 + 4 * q] = f"    p{q} tile upd end"
+for rep in range(3):
+    g.set_state(p.state_init)
+    g.run_gn(16)
+    assert L.kb_diag_read_ts(g.h, buf, 64) == 0
+    t0 = buf[0]
+    order = sorted((buf[i] - t0, i) for i in names if buf[i] >= t0 and buf[i] - t0 < 10_000_000)
+    print(f"k_solve timeline (rep {rep}, us from entry):\n" +
+          "\n".join(f"{names[i]:24s} {dt / 100:8.2f}" for dt, i in order))
