@@ -194,7 +194,7 @@ int kb_get_trace(kb_handle* h, double* trace, int32_t cap);
 int kb_run_gn_iterations(kb_handle* h, int32_t n_iter, double* seconds);
 /* Average device duration (ms) of the build kernel inside Gauss-Newton passes (runs 22 passes from the
  * current state, HIP events around each build launch on the handle's stream); algorithmic bytes and
- * flops per build launch. */
+ * flops per build launch.  The state, camera chains and control block are restored afterwards. */
 int kb_build_kernel_stats(kb_handle* h, double* avg_ms, double* bytes_per_launch, double* flops_per_launch);
 
 /* Multi-GPU (frame sharding): each rank's handle holds its own frames;
@@ -202,6 +202,11 @@ int kb_build_kernel_stats(kb_handle* h, double* avg_ms, double* bytes_per_launch
  * per pass.  unique_id is the 128-byte ncclUniqueId. */
 int kb_comm_get_unique_id(void* unique_id_out128);
 int kb_comm_init(kb_handle* h, const void* unique_id128, int32_t nranks, int32_t rank);
+/* In-process group: n handles of this process (any devices, one device included) become ranks 0..n-1 of one
+ * sharded problem and exchange through device copies instead of RCCL (sums in rank order).  Each handle must
+ * then be driven from its own host thread: the collectives of a pass meet in a host barrier (60 s timeout ->
+ * error).  Passes run eagerly, not graph-captured.  Used to test the sharded path with several ranks on one GPU. */
+int kb_comm_init_local(kb_handle* const* handles, int32_t n);
 
 /* Self test of the f64 MFMA fragment layout used by the build kernel (A = I, asymmetric B). */
 int kb_selftest_mfma(double* max_err);

@@ -22,7 +22,7 @@ EXPORTS = [
     "kb_get_state_flat", "kb_state_size", "kb_num_cols", "kb_camera_cols", "kb_eval_cost", "kb_build",
     "kb_set_constant_conditioner", "kb_solve", "kb_get_rhs", "kb_apply_update", "kb_revert", "kb_get_normal_blocks",
     "kb_optimize", "kb_get_trace", "kb_run_gn_iterations", "kb_build_kernel_stats", "kb_comm_get_unique_id",
-    "kb_comm_init", "kb_selftest_mfma", "kb_solve_marginal", "kb_analyze_marginal",
+    "kb_comm_init", "kb_comm_init_local", "kb_selftest_mfma", "kb_solve_marginal", "kb_analyze_marginal",
     # block-Jacobi PCG (LinearSolverPCG)
     "kb_set_linear_solver", "kb_pcg_init", "kb_get_pcg_info",
     # configs[4]: B-spline pose trajectory + IMU
@@ -122,6 +122,7 @@ def lib():
         L.kb_build_kernel_stats.argtypes = [C.c_void_p, dp, dp, dp]
         L.kb_comm_get_unique_id.argtypes = [C.c_void_p]
         L.kb_comm_init.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32]
+        L.kb_comm_init_local.argtypes = [C.POINTER(C.c_void_p), C.c_int32]
         L.kb_selftest_mfma.argtypes = [dp]
         L.kb_set_linear_solver.argtypes = [C.c_void_p, C.c_int32, C.POINTER(PcgOptions)]
         L.kb_pcg_init.argtypes = [C.c_void_p]
@@ -323,6 +324,13 @@ class Solver:
     def comm_init(self, uid: bytes, nranks, rank):
         buf = C.create_string_buffer(uid, 128)
         _check(lib().kb_comm_init(self.h, buf, int(nranks), int(rank)))
+
+
+def comm_init_local(solvers):
+    """kb_comm_init_local: the solvers (frame shards of one problem, in rank order) exchange in-process; drive each
+    one from its own thread afterwards."""
+    arr = (C.c_void_p * len(solvers))(*[s.h.value for s in solvers])
+    _check(lib().kb_comm_init_local(arr, len(solvers)))
 
 
 class SplineSolver:

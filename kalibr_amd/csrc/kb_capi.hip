@@ -6,6 +6,8 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <condition_variable>
+#include <mutex>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -53,6 +55,56 @@ int nintr_host(int m) {
 }  // namespace
 
 constexpr int kGraphPasses = 8;  // optimizer passes per captured multi-pass graph
+constexpr int kLocalMaxRanks = 16;  // kb_comm_init_local group size
+
+// In-process group of sharded handles (kb_comm_init_local): the collectives become device copies between the
+// members' buffers, ordered by HIP events and a host barrier (one host thread per member).
+struct kb_local_group {
+  int n = 0;
+  int refs = 0;
+  std::mutex m;
+  std::condition_variable cv;
+  int arrived = 0;
+  long gen = 0;
+  bool broken = false;  // a member timed out: every later barrier fails at once
+  std::vector<hipEvent_t> ready, done;
+  std::vector<const double*> src;
+  // false on timeout (a member never arrived)
+  bool barrier() {
+    std::unique_lock<std::mutex> lk(m);
+    if (broken) return false;
+    const long g = gen;
+    if (++arrived == n) {
+      arrived = 0;
+      ++gen;
+      cv.notify_all();
+      return true;
+    }
+    if (!cv.wait_for(lk, std::chrono::seconds(60), [&] { return gen != g || broken; }) || broken) {
+      broken = true;
+      cv.notify_all();
+      return false;
+    }
+    return true;
+  }
+};
+
+struct LocalSrc {
+  const double* p[kLocalMaxRanks];
+};
+
+// out[i] = sum_r src_r[i] in rank order (sum) or out[r * count + i] = src_r[i] (gather)
+__global__ void __launch_bounds__(256) k_local_coll(LocalSrc s, int n, size_t count, double* out, int gather) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (size_t)gridDim.x * blockDim.x) {
+    if (gather) {
+      for (int r = 0; r < n; ++r) out[(size_t)r * count + i] = s.p[r][i];
+    } else {
+      double a = s.p[0][i];
+      for (int r = 1; r < n; ++r) a += s.p[r][i];
+      out[i] = a;
+    }
+  }
+}
 
 struct kb_handle {
   int device = 0;
@@ -81,6 +133,7 @@ struct kb_handle {
   int trace_cap = 0;
   // sharding
   ncclComm_t comm = nullptr;
+  kb_local_group* lg = nullptr;  // in-process group (kb_comm_init_local) instead of RCCL
   int nranks = 1, rank = 0;
   double* psum_red = nullptr;   // [Wtot] all-reduced finished column sums (sharded, per-call path)
   double* psum_red8 = nullptr;  // [8][Wtot] all-reduced stage-1 rows (sharded optimizer loop)
@@ -142,6 +195,48 @@ static void drop_graphs(kb_handle* h) {
   h->graph_policy = -1;
 }
 
+static bool sharded(const kb_handle* h) { return h->comm || h->lg; }
+
+// one collective of the in-process group: every member publishes its send buffer and an event, waits for all
+// members' events, copies / sums on its own stream, then waits until every member has read its buffer
+static int local_coll(kb_handle* h, const double* send, double* recv, size_t count, bool gather) {
+  kb_local_group* G = h->lg;
+  const int r = h->rank;
+  if (send == recv) return fail("kb_comm_init_local: in-place collective");
+  G->src[r] = send;
+  KB_HIP(hipEventRecord(G->ready[r], h->stream));
+  if (!G->barrier()) return fail("kb_comm_init_local: a member of the group did not reach the collective (60 s)");
+  LocalSrc ls{};
+  for (int j = 0; j < G->n; ++j) {
+    KB_HIP(hipStreamWaitEvent(h->stream, G->ready[j], 0));
+    ls.p[j] = G->src[j];
+  }
+  const int blocks = (int)std::min<size_t>((count + 255) / 256, 1024);
+  hipLaunchKernelGGL(k_local_coll, dim3(std::max(blocks, 1)), dim3(256), 0, h->stream, ls, G->n, count, recv,
+                     gather ? 1 : 0);
+  KB_HIP(hipGetLastError());
+  KB_HIP(hipEventRecord(G->done[r], h->stream));
+  if (!G->barrier()) return fail("kb_comm_init_local: a member of the group did not reach the collective (60 s)");
+  for (int j = 0; j < G->n; ++j) KB_HIP(hipStreamWaitEvent(h->stream, G->done[j], 0));
+  // nobody re-records ready / done (next collective) before every member has enqueued its waits on them
+  if (!G->barrier()) return fail("kb_comm_init_local: a member of the group did not reach the collective (60 s)");
+  return 0;
+}
+
+// sum over ranks (RCCL or the in-process group); all ranks receive identical bits
+static int coll_allreduce(kb_handle* h, const double* send, double* recv, size_t count) {
+  if (h->lg) return local_coll(h, send, recv, count, false);
+  KB_NCCL(ncclAllReduce(send, recv, count, ncclDouble, ncclSum, h->comm, h->stream));
+  return 0;
+}
+
+// recv = [rank 0's count values | rank 1's | ...]
+static int coll_allgather(kb_handle* h, const double* send, double* recv, size_t count) {
+  if (h->lg) return local_coll(h, send, recv, count, true);
+  KB_NCCL(ncclAllGather(send, recv, count, ncclDouble, h->comm, h->stream));
+  return 0;
+}
+
 // error channel shared with the spline translation unit (kb_spline.hip)
 namespace kb_internal {
 int fail(const std::string& m) {
@@ -163,6 +258,8 @@ kb_handle* kb_create(const kb_layout* L) {
     fail("kb_create: n_cams out of range");
     return nullptr;
   }
+  // n_frames >= 1 keeps nblk >= 1: k_colsum (and k_solve's staging) clamp their ungated row loads to nblk - 1, so
+  // an empty shard would read part[-Wr]; a strong-scaling rank must own at least one frame
   if (L->n_frames < 1 || L->n_target < 1 || L->n_target > 65535) {
     fail("kb_create: bad n_frames / n_target");
     return nullptr;
@@ -359,6 +456,11 @@ void kb_destroy(kb_handle* h) {
   if (h->stream) hipStreamSynchronize(h->stream);
   drop_graphs(h);
   if (h->comm) ncclCommDestroy(h->comm);
+  if (h->lg && --h->lg->refs == 0) {
+    for (auto e : h->lg->ready) hipEventDestroy(e);
+    for (auto e : h->lg->done) hipEventDestroy(e);
+    delete h->lg;
+  }
   for (void* p : h->allocs) hipFree(p);
   if (h->trace) hipFree(h->trace);
   if (h->stream) hipStreamDestroy(h->stream);
@@ -482,8 +584,8 @@ static int launch_cost(kb_handle* h, int which) {
 // one all-gather of every rank's [cost, dx.dx, dx.rhs, max|dx|]; reduced in rank order on every rank (by
 // k_red_gather, or inline by k_policy) so that all ranks hold bitwise-identical sums
 static int allreduce_red(kb_handle* h, bool reduce = true) {
-  if (!h->comm) return 0;
-  KB_NCCL(ncclAllGather(h->d.red_local, const_cast<double*>(h->d.red_all), 4, ncclDouble, h->comm, h->stream));
+  if (!sharded(h)) return 0;
+  if (coll_allgather(h, h->d.red_local, const_cast<double*>(h->d.red_all), 4)) return -1;
   if (reduce) {
     hipLaunchKernelGGL(k_red_gather, dim3(1), dim3(1), 0, h->stream, h->d);
     KB_HIP(hipGetLastError());
@@ -502,24 +604,21 @@ static int launch_colsum(kb_handle* h, int gate, bool finish = true) {
     // camera blocks for the tiled solve: the stage-1 rows are all-reduced as they are (sharded), then k_colimg
     // finishes the sums (into the consumer's row) and writes k_solve's LDS image from the same rows
     const double* rows = d.part8;
-    if (h->comm) {
-      KB_NCCL(ncclAllReduce(d.part8, h->psum_red8, (size_t)kColsumRows * d.Wtot, ncclDouble, ncclSum, h->comm,
-                            h->stream));
+    if (sharded(h)) {
+      if (coll_allreduce(h, d.part8, h->psum_red8, (size_t)kColsumRows * d.Wtot)) return -1;
       rows = h->psum_red8;
     }
-    double* out = h->comm ? h->psum_red : d.psum_local;
+    double* out = sharded(h) ? h->psum_red : d.psum_local;
     hipLaunchKernelGGL(k_colimg, dim3((d.Wtot + d.img_n + 255) / 256), dim3(256), 0, h->stream, d, rows, out, gate);
     KB_HIP(hipGetLastError());
     return 0;
   }
   if (finish) hipLaunchKernelGGL(k_colfin, dim3((d.Wtot + 255) / 256), dim3(256), 0, h->stream, d, gate);
   KB_HIP(hipGetLastError());
-  if (h->comm) {
-    if (finish)
-      KB_NCCL(ncclAllReduce(d.psum_local, h->psum_red, d.Wtot, ncclDouble, ncclSum, h->comm, h->stream));
-    else
-      KB_NCCL(ncclAllReduce(d.part8, h->psum_red8, (size_t)kColsumRows * d.Wtot, ncclDouble, ncclSum, h->comm,
-                            h->stream));
+  if (sharded(h)) {
+    if (finish ? coll_allreduce(h, d.psum_local, h->psum_red, d.Wtot)
+               : coll_allreduce(h, d.part8, h->psum_red8, (size_t)kColsumRows * d.Wtot))
+      return -1;
   }
   return 0;
 }
@@ -544,7 +643,7 @@ static int launch_schur(kb_handle* h, int gate) {
 static int launch_solve(kb_handle* h, int gate, int do_update, bool from_rows = false) {
   KbDev d = h->d;
   if (from_rows) {  // column sums still split in kColsumRows stage-1 rows (all-reduced ones when sharded)
-    d.psum = h->comm ? h->psum_red8 : d.part8;
+    d.psum = sharded(h) ? h->psum_red8 : d.part8;
     d.psum_rows = kColsumRows;
   }
   void* args[] = {(void*)&d, (void*)&gate, (void*)&do_update};
@@ -610,7 +709,7 @@ static size_t pcg_lds(int fpb, int C, int F) {
 }
 
 static int run_pcg(kb_handle* h, int* ok) {
-  if (h->comm) return fail("kb_solve (PCG): not available on a sharded handle");
+  if (sharded(h)) return fail("kb_solve (PCG): not available on a sharded handle");
   const int C = h->C, F = h->F;
   if (!h->pcg_buf) {
     if (h->alloc(&h->pcg_buf, (size_t)F * (C + 1) + F + 8) || h->alloc(&h->pcg_cb, 2 * (size_t)C) ||
@@ -683,7 +782,7 @@ static int run_pcg(kb_handle* h, int* ok) {
 int kb_set_linear_solver(kb_handle* h, int32_t kind, const kb_pcg_options* pcg) {
   if (!h) return fail("kb_set_linear_solver: null");
   if (kind != KB_SOLVER_SCHUR && kind != KB_SOLVER_PCG) return fail("kb_set_linear_solver: unknown solver");
-  if (kind == KB_SOLVER_PCG && h->comm) return fail("kb_set_linear_solver: PCG is not available on a sharded handle");
+  if (kind == KB_SOLVER_PCG && sharded(h)) return fail("kb_set_linear_solver: PCG is not available on a sharded handle");
   h->solver_kind = kind;
   h->pcg = pcg ? *pcg : kb_pcg_options{1e-6, -1, 1};
   h->pcg_residual = -1.0;
@@ -774,7 +873,7 @@ int kb_revert(kb_handle* h) {
 static int run_marginal(kb_handle* h, const kb_marginal_options* o, int write_dx, kb_marginal_info* info,
                         double* sv_out, double* V_out) {
   if (h->C > kMargMaxC) return fail("marginal solver: camera block C > 112 is not supported");
-  if (h->comm) return fail("marginal solver: not available on a sharded handle");
+  if (sharded(h)) return fail("marginal solver: not available on a sharded handle");
   const int C = h->C;
   if (!h->marg_buf && h->alloc(&h->marg_buf, (size_t)C * C + C + 8)) return -1;
   KbMarg m;
@@ -898,8 +997,7 @@ static int enqueue_pass(kb_handle* h, int policy, hipEvent_t ev0 = nullptr, hipE
   if (launch_backsub(h, 1, 1, 1)) return -1;
   // the pass end (accept / revert, next prelude): one block (k_post); sharded, the per-frame step rows of every
   // rank are all-gathered first and every rank reduces all of them in rank order
-  if (h->comm)
-    KB_NCCL(ncclAllGather(d.bpart, h->bpart_all, 4 * (size_t)h->F_max, ncclDouble, h->comm, h->stream));
+  if (sharded(h) && coll_allgather(h, d.bpart, h->bpart_all, 4 * (size_t)h->F_max)) return -1;
   if (!d.fold) {
     hipLaunchKernelGGL(k_post, dim3(1), dim3(256), 0, h->stream, d, 1);
     KB_HIP(hipGetLastError());
@@ -950,7 +1048,7 @@ static int graph_of(kb_handle* h, int k, hipGraphExec_t* out) {
 // captured graphs for this policy; RCCL calls are captured too when sharded.  If capturing them fails on this
 // stack, the handle falls back to eager passes for good (same kernels, same results).
 static bool graph_ok(kb_handle* h, int policy) {
-  if (h->graph_failed) return false;
+  if (h->graph_failed || h->lg) return false;  // the in-process group's collectives meet on the host: eager
   if (ensure_graph(h, policy) == 0) return true;
   if (!h->comm) return false;  // caller reports the error through kb_last_error on the eager path as well
   hipGetLastError();
@@ -980,8 +1078,7 @@ static int finish_pass(kb_handle* h, int policy) {
   if (gn_fused(h, policy)) {  // the last solve's step: back-substitution + cost, then its end as usual
     GnFusedScope scope(h, true);
     if (launch_backsub(h, 1, 1, 1)) return -1;
-    if (h->comm)
-      KB_NCCL(ncclAllGather(h->d.bpart, h->bpart_all, 4 * (size_t)h->F_max, ncclDouble, h->comm, h->stream));
+    if (sharded(h) && coll_allgather(h, h->d.bpart, h->bpart_all, 4 * (size_t)h->F_max)) return -1;
   }
   hipLaunchKernelGGL(k_post, dim3(1), dim3(256), 0, h->stream, h->d, 1);
   KB_HIP(hipGetLastError());
@@ -1077,6 +1174,24 @@ int kb_build_kernel_stats(kb_handle* h, double* avg_ms, double* bytes_per_launch
   // timed launches are the build exactly as it runs inside the pass (frame steps of the previous solve applied)
   const int reps = 20, warm = 2;
   if (ensure_trace(h, 64)) return -1;
+  // a query: the state buffers, camera chains and control block are saved here and restored at the end
+  KbDev& dv = h->d;
+  const size_t n_state = 2 * (size_t)h->S, n_L = 2 * 12 * (size_t)h->N, n_K = 2 * 36 * (size_t)h->N * h->N;
+  const size_t n_ctrl = (sizeof(KbCtrl) + sizeof(double) - 1) / sizeof(double);
+  double* save = nullptr;
+  KB_HIP(hipMalloc(&save, sizeof(double) * (n_state + n_L + n_K + n_ctrl)));
+  auto snap = [&](bool restore) -> int {
+    char* c = (char*)save;
+    void* bufs[4] = {dv.state, dv.camL, dv.camK, dv.ctrl};
+    const size_t sz[4] = {n_state * 8, n_L * 8, n_K * 8, sizeof(KbCtrl)};
+    for (int q = 0; q < 4; ++q) {
+      KB_HIP(hipMemcpyAsync(restore ? bufs[q] : c, restore ? c : bufs[q], sz[q], hipMemcpyDeviceToDevice, h->stream));
+      c += (sz[q] + 7) & ~size_t(7);
+    }
+    return 0;
+  };
+  const int cur0 = h->cur;
+  if (snap(false)) return -1;
   KbOpts o{1, 0x3fffffff, 0.0, -1.0, -1.0};
   if (loop_start(h, o)) return -1;
   std::vector<hipEvent_t> ev(2 * (reps + warm));
@@ -1084,7 +1199,7 @@ int kb_build_kernel_stats(kb_handle* h, double* avg_ms, double* bytes_per_launch
   // the passes are captured in one graph, event records included, so the timed builds run exactly as in the
   // benchmarked graphs (no eager launch gaps around them); eager launches if this stack cannot capture events
   bool graphed = false;
-  if (!h->comm && hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal) == hipSuccess) {
+  if (!sharded(h) && hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal) == hipSuccess) {
     int rc = 0;
     for (int r = 0; r < reps + warm && !rc; ++r) rc = enqueue_pass(h, 1, ev[2 * r], ev[2 * r + 1]);
     hipGraph_t g = nullptr;
@@ -1121,11 +1236,11 @@ int kb_build_kernel_stats(kb_handle* h, double* avg_ms, double* bytes_per_launch
     }
   }
   if (finish_pass(h, 1)) return -1;
+  if (snap(true)) return -1;
   KB_HIP(hipStreamSynchronize(h->stream));
+  hipFree(save);
   for (auto& e : ev) hipEventDestroy(e);
-  KbCtrl ctrl{};
-  KB_HIP(hipMemcpy(&ctrl, h->d.ctrl, sizeof(KbCtrl), hipMemcpyDeviceToHost));
-  h->cur = ctrl.cur;
+  h->cur = cur0;
   h->build_ms = tot / reps;
   if (avg_ms) *avg_ms = h->build_ms;
   // algorithmic bytes of one launch: observations (y 16 B + corner id 2 B per corner), view ranges (8 B per
@@ -1153,14 +1268,8 @@ int kb_comm_get_unique_id(void* out) {
   return 0;
 }
 
-int kb_comm_init(kb_handle* h, const void* uid, int32_t nranks, int32_t rank) {
-  if (!h || !uid) return fail("kb_comm_init: null");
-  KB_HIP(hipSetDevice(h->device));
-  if (nranks < 1 || rank < 0 || rank >= nranks) return fail("kb_comm_init: bad rank / nranks");
-  if (h->comm) return fail("kb_comm_init: communicator already initialised");
-  ncclUniqueId id;
-  std::memcpy(&id, uid, sizeof(id));
-  KB_NCCL(ncclCommInitRank(&h->comm, nranks, id, rank));
+// buffers of a sharded handle (rank `rank` of `nranks`; F_max = the largest rank's frame count)
+static int shard_setup(kb_handle* h, int nranks, int rank, int F_max) {
   h->nranks = nranks;
   h->rank = rank;
   h->d.rank = rank;
@@ -1181,12 +1290,7 @@ int kb_comm_init(kb_handle* h, const void* uid, int32_t nranks, int32_t rank) {
   h->d.nranks = nranks;
   // per-frame step rows: padded to the largest rank's frame count (zero rows are neutral for the sums and the
   // max), all-gathered once per pass and reduced by every rank in rank order
-  int* fm = nullptr;
-  if (h->alloc(&fm, 1)) return -1;
-  KB_HIP(hipMemcpyAsync(fm, &h->F, sizeof(int), hipMemcpyHostToDevice, h->stream));
-  KB_NCCL(ncclAllReduce(fm, fm, 1, ncclInt32, ncclMax, h->comm, h->stream));
-  KB_HIP(hipMemcpyAsync(&h->F_max, fm, sizeof(int), hipMemcpyDeviceToHost, h->stream));
-  KB_HIP(hipStreamSynchronize(h->stream));
+  h->F_max = F_max;
   double* bp = nullptr;
   if (h->alloc(&bp, 4 * (size_t)h->F_max) || h->alloc(&h->bpart_all, 4 * (size_t)h->F_max * nranks)) return -1;
   h->d.bpart = bp;
@@ -1195,6 +1299,54 @@ int kb_comm_init(kb_handle* h, const void* uid, int32_t nranks, int32_t rank) {
   if (h->alloc(&h->psum_red8, (size_t)kColsumRows * h->d.Wtot)) return -1;
   drop_graphs(h);
   KB_HIP(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+int kb_comm_init(kb_handle* h, const void* uid, int32_t nranks, int32_t rank) {
+  if (!h || !uid) return fail("kb_comm_init: null");
+  KB_HIP(hipSetDevice(h->device));
+  if (nranks < 1 || rank < 0 || rank >= nranks) return fail("kb_comm_init: bad rank / nranks");
+  if (sharded(h)) return fail("kb_comm_init: communicator already initialised");
+  ncclUniqueId id;
+  std::memcpy(&id, uid, sizeof(id));
+  KB_NCCL(ncclCommInitRank(&h->comm, nranks, id, rank));
+  int* fm = nullptr;
+  if (h->alloc(&fm, 1)) return -1;
+  KB_HIP(hipMemcpyAsync(fm, &h->F, sizeof(int), hipMemcpyHostToDevice, h->stream));
+  KB_NCCL(ncclAllReduce(fm, fm, 1, ncclInt32, ncclMax, h->comm, h->stream));
+  int F_max = 0;
+  KB_HIP(hipMemcpyAsync(&F_max, fm, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+  KB_HIP(hipStreamSynchronize(h->stream));
+  return shard_setup(h, nranks, rank, F_max);
+}
+
+int kb_comm_init_local(kb_handle* const* hs, int32_t n) {
+  if (!hs || n < 1 || n > kLocalMaxRanks) return fail("kb_comm_init_local: bad handle list");
+  int F_max = 0;
+  for (int r = 0; r < n; ++r) {
+    if (!hs[r]) return fail("kb_comm_init_local: null handle");
+    if (sharded(hs[r])) return fail("kb_comm_init_local: handle already sharded");
+    for (int q = 0; q < r; ++q)
+      if (hs[q] == hs[r]) return fail("kb_comm_init_local: handle listed twice");
+    if (hs[r]->N != hs[0]->N || hs[r]->C != hs[0]->C) return fail("kb_comm_init_local: handles of different rigs");
+    F_max = std::max(F_max, hs[r]->F);
+  }
+  kb_local_group* G = new kb_local_group();
+  G->n = n;
+  G->ready.assign(n, nullptr);
+  G->done.assign(n, nullptr);
+  G->src.assign(n, nullptr);
+  for (int r = 0; r < n; ++r) {
+    KB_HIP(hipSetDevice(hs[r]->device));
+    KB_HIP(hipEventCreateWithFlags(&G->ready[r], hipEventDisableTiming));
+    KB_HIP(hipEventCreateWithFlags(&G->done[r], hipEventDisableTiming));
+  }
+  for (int r = 0; r < n; ++r) {
+    KB_HIP(hipSetDevice(hs[r]->device));
+    hs[r]->lg = G;
+    ++G->refs;
+    if (shard_setup(hs[r], n, r, F_max)) return -1;
+  }
   return 0;
 }
 
