@@ -34,12 +34,13 @@ GN_FUSED = os.environ.get("KB_GN_FUSED", "1") != "0"  # the library's pass varia
 
 
 def is_build_kernel(name):
-    """The pass's build kernel as rocprofv3 names it: k_build<TW, GNF, MM> with GNF = the GN fused variant (MM = the
-    rig's camera-model set)."""
-    if not (name.startswith("void kb::k_build<") and name.endswith(">(kb::KbDev, int, int)")):
-        return False
-    args = name[len("void kb::k_build<"):-len(">(kb::KbDev, int, int)")].split(", ")
-    return len(args) >= 2 and args[1] == ("true" if GN_FUSED else "false")
+    """The pass's build kernel as rocprofv3 names it: k_build<TW, GNF, MM> or the pipelined k_buildp<TT, GNF, MM>
+    (rigs with one wave per camera), with GNF = the GN fused variant (MM = the rig's camera-model set)."""
+    for pre in ("void kb::k_build<", "void kb::k_buildp<"):
+        if name.startswith(pre) and name.endswith(">(kb::KbDev, int, int)"):
+            args = name[len(pre):-len(">(kb::KbDev, int, int)")].split(", ")
+            return len(args) >= 2 and args[1] == ("true" if GN_FUSED else "false")
+    return False
 FRAMES_PER_RANK = 500
 HBM_PEAK_GBS = 8000.0
 

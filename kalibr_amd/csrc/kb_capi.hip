@@ -112,6 +112,8 @@ struct kb_handle {
   KbDev d{};
   int N = 0, F = 0, K = 0, V = 0, NC = 0, C = 0, ncols = 0, S = 0, W = 0;
   int WPB = 1;
+  bool build_pipe = false;  // k_buildp (one wave per camera, N + 2 waves) instead of k_build
+  int build_threads = 64;
   size_t lds_build = 0, lds_camexp = 0, lds_schur = 0, lds_solve = 0;
   int solve_threads = 64;
   int mb = 7, ms = 7;  // Schur-sum tiles per wave of k_build / k_schur (template bucket)
@@ -165,25 +167,28 @@ struct kb_handle {
   }
 };
 
+// mb: Schur tiles per wave of k_build (1 | 4 | 7), or per frame wave of k_buildp (5: 2 frame waves | 10: 3) when pipe
 template <bool GN, unsigned MM>
-static const void* build_fn(int mb) {
+static const void* build_fn(int mb, bool pipe) {
+  if (pipe) return mb == 5 ? (const void*)k_buildp<5, GN, MM> : (const void*)k_buildp<10, GN, MM>;
   return mb == 1 ? (const void*)k_build<1, GN, MM> : mb == 4 ? (const void*)k_build<4, GN, MM>
                                                              : (const void*)k_build<7, GN, MM>;
 }
 
 // Build kernel for the rig's camera-model set `mm` (bit m = model m present).
 template <bool GN>
-static const void* pick_build(int mb, unsigned mm) {
+static const void* pick_build(int mb, unsigned mm, bool pipe) {
   switch (mm) {
-    case 1u << KB_PINHOLE_RADTAN: return build_fn<GN, 1u << KB_PINHOLE_RADTAN>(mb);
-    case 1u << KB_OMNI_RADTAN: return build_fn<GN, 1u << KB_OMNI_RADTAN>(mb);
-    case 1u << KB_EUCM: return build_fn<GN, 1u << KB_EUCM>(mb);
-    case 1u << KB_OMNI: return build_fn<GN, 1u << KB_OMNI>(mb);
-    case 1u << KB_DS: return build_fn<GN, 1u << KB_DS>(mb);
-    case 1u << KB_PINHOLE_EQUI: return build_fn<GN, 1u << KB_PINHOLE_EQUI>(mb);
-    case 1u << KB_PINHOLE_FOV: return build_fn<GN, 1u << KB_PINHOLE_FOV>(mb);
-    case (1u << KB_OMNI_RADTAN) | (1u << KB_EUCM): return build_fn<GN, (1u << KB_OMNI_RADTAN) | (1u << KB_EUCM)>(mb);
-    default: return build_fn<GN, kMmAll>(mb);
+    case 1u << KB_PINHOLE_RADTAN: return build_fn<GN, 1u << KB_PINHOLE_RADTAN>(mb, pipe);
+    case 1u << KB_OMNI_RADTAN: return build_fn<GN, 1u << KB_OMNI_RADTAN>(mb, pipe);
+    case 1u << KB_EUCM: return build_fn<GN, 1u << KB_EUCM>(mb, pipe);
+    case 1u << KB_OMNI: return build_fn<GN, 1u << KB_OMNI>(mb, pipe);
+    case 1u << KB_DS: return build_fn<GN, 1u << KB_DS>(mb, pipe);
+    case 1u << KB_PINHOLE_EQUI: return build_fn<GN, 1u << KB_PINHOLE_EQUI>(mb, pipe);
+    case 1u << KB_PINHOLE_FOV: return build_fn<GN, 1u << KB_PINHOLE_FOV>(mb, pipe);
+    case (1u << KB_OMNI_RADTAN) | (1u << KB_EUCM):
+      return build_fn<GN, (1u << KB_OMNI_RADTAN) | (1u << KB_EUCM)>(mb, pipe);
+    default: return build_fn<GN, kMmAll>(mb, pipe);
   }
 }
 
@@ -314,12 +319,25 @@ kb_handle* kb_create(const kb_layout* L) {
   d.S = h->S;
   d.off_base = h->N * KB_MAX_INTR;
   d.off_frame = h->N * KB_MAX_INTR + 7 * (h->N - 1);
-  d.gframes = (h->F + 511) / 512;
-  d.nblk = (h->F + d.gframes - 1) / d.gframes;
-  d.nblk_bs = h->F;  // k_backsub: one block per frame
   d.nsplit = std::max(1, (4 + h->N - 1) / h->N);  // >= 4 waves per build block
   d.wpb = h->N * d.nsplit;
   h->WPB = d.wpb;
+  // one wave per camera and at most kBuildpMaxCams cameras: the pipelined build (N view waves + 2 frame waves);
+  // KB_BUILD_PIPE=0 keeps k_build for comparison
+  h->build_pipe = d.nsplit == 1 && h->N <= kBuildpMaxCams;
+  if (const char* e = std::getenv("KB_BUILD_PIPE")) h->build_pipe = h->build_pipe && std::atoi(e) != 0;
+  const int nbz0 = (h->C + 16) / 16, nf = (nbz0 * (nbz0 + 1) / 2 + 1) / 2 <= 5 ? 2 : 3;  // k_buildp frame waves
+  h->build_threads = 64 * (h->build_pipe ? h->N + nf : d.wpb);
+  if (h->build_pipe) {
+    // all blocks resident at once: one block per CU (two for rigs whose block fits twice: 12 waves per CU at the
+    // kernel's <= 168 VGPRs, half the LDS), each running its frames through the pipeline
+    const int bpc = (h->N + nf <= 6) ? 2 : 1;
+    d.gframes = (h->F + 256 * bpc - 1) / (256 * bpc);
+  } else {
+    d.gframes = (h->F + 511) / 512;
+  }
+  d.nblk = (h->F + d.gframes - 1) / d.gframes;
+  d.nblk_bs = h->F;  // k_backsub: one block per frame
   d.W = h->W;
   d.Wp = h->N * 136 + h->W + 1;
   d.Wr = d.Wp + 1;
@@ -396,9 +414,15 @@ kb_handle* kb_create(const kb_layout* L) {
   {
     const int N = h->N, C = h->C, WPB = d.wpb;
     const int CZ = 16 * ((C + 16) / 16);  // [Y | z] row stride of the Schur tiles
-    h->lds_build = sizeof(double) * (WPB * 64 * XS + WPB * 256 + N * (256 + 256 + 64 + 36 + 36 + 8) + 36 +
-                                     16 * CZ + 18 * N * (N - 1) + (3 * h->K <= kTargetLds ? 3 * h->K : 0) +
-                                     8 * d.gframes);
+    const int tgl = (3 * h->K <= kTargetLds ? 3 * h->K : 0) + 8 * d.gframes;
+    if (h->build_pipe) {  // k_buildp: tiles | H | chains | 2 view buffers | frame-wave buffers | K | target, poses
+      const int np = N * (N - 1) / 2, nf = (C + 16) / 16 <= 4 ? 2 : 3;  // as build_threads
+      h->lds_build = sizeof(double) * (N * 32 * XS + N * 256 + N * 64 + (36 * np + 44 * N + 6 * CZ) +
+                                       (40 + 6 * CZ) + nf * 6 * CZ + 36 * np + tgl);
+    } else {
+      h->lds_build = sizeof(double) * (WPB * 64 * XS + WPB * 256 + N * (256 + 256 + 64 + 36 + 36 + 8) + 36 +
+                                       16 * CZ + 18 * N * (N - 1) + tgl);
+    }
     h->lds_camexp = sizeof(double) * (N * 256 + N * N * 36);
     h->lds_schur = sizeof(double) * 16 * CZ;
     if (C <= 64) {
@@ -427,14 +451,14 @@ kb_handle* kb_create(const kb_layout* L) {
     // Schur-sum tiles per wave (template bucket): ceil(lower tiles of [Y|z]^T [Y|z] / waves)
     const int nbz = (h->C + 16) / 16, ntiles = nbz * (nbz + 1) / 2;
     const int tb = (ntiles + d.wpb - 1) / d.wpb, ts = (ntiles + 3) / 4;
-    h->mb = tb <= 1 ? 1 : tb <= 4 ? 4 : 7;
+    h->mb = h->build_pipe ? ((ntiles + 1) / 2 <= 5 ? 5 : 10) : tb <= 1 ? 1 : tb <= 4 ? 4 : 7;
     h->ms = ts <= 1 ? 1 : ts <= 4 ? 4 : 7;
     // camera-model set: one-model rigs (and the omni-radtan + EUCM rig of configs[2]) get their own build
     // kernels; any other mix uses the all-models instantiation
     unsigned mm = 0;
     for (int i = 0; i < h->N; ++i) mm |= 1u << d.model[i];
-    h->fn_build = pick_build<false>(h->mb, mm);
-    h->fn_build_gn = pick_build<true>(h->mb, mm);
+    h->fn_build = pick_build<false>(h->mb, mm, h->build_pipe);
+    h->fn_build_gn = pick_build<true>(h->mb, mm, h->build_pipe);
     h->fn_schur = h->ms == 1 ? (const void*)k_schur<1> : h->ms == 4 ? (const void*)k_schur<4> : (const void*)k_schur<7>;
   }
   hipFuncSetAttribute(h->fn_build, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_build);
@@ -628,7 +652,7 @@ static int launch_build(kb_handle* h, int gate, int fuse) {
   // per-call path: camera chains first; in the loop k_solve (or the loop start) computed them
   if (!gate) hipLaunchKernelGGL(k_pre, dim3(1), dim3(256), 0, h->stream, d, 0);
   void* args[] = {&d, &gate, &fuse};
-  KB_HIP(hipLaunchKernel(d.gn_fused ? h->fn_build_gn : h->fn_build, dim3(d.nblk), dim3(64 * d.wpb), args,
+  KB_HIP(hipLaunchKernel(d.gn_fused ? h->fn_build_gn : h->fn_build, dim3(d.nblk), dim3(h->build_threads), args,
                          h->lds_build, h->stream));
   return 0;
 }
@@ -1354,12 +1378,12 @@ int kb_comm_init_local(kb_handle* const* hs, int32_t n) {
 // diagnostic build only: the KB_TS timeline of the last k_solve launch (100 MHz ticks)
 int kb_diag_read_ts(kb_handle* h, long long* out, int n) {
   if (!h->d.dbg_ts) {
-    KB_HIP(hipMalloc(&h->d.dbg_ts, 64 * sizeof(long long)));
-    KB_HIP(hipMemset(h->d.dbg_ts, 0, 64 * sizeof(long long)));
+    KB_HIP(hipMalloc(&h->d.dbg_ts, 128 * sizeof(long long)));
+    KB_HIP(hipMemset(h->d.dbg_ts, 0, 128 * sizeof(long long)));
     drop_graphs(h);
     return 0;
   }
-  KB_HIP(hipMemcpy(out, h->d.dbg_ts, sizeof(long long) * std::min(n, 64), hipMemcpyDeviceToHost));
+  KB_HIP(hipMemcpy(out, h->d.dbg_ts, sizeof(long long) * std::min(n, 128), hipMemcpyDeviceToHost));
   return 0;
 }
 
@@ -1385,13 +1409,13 @@ int kb_diag_phase_time(kb_handle* h, int which, int stop, int reps, int flags, d
     if (r == 0) KB_HIP(hipEventRecord(e0, h->stream));
     if (which == 0) {
       void* args[] = {&d, &g, &one};
-      KB_HIP(hipLaunchKernel(h->fn_build, dim3(d.nblk), dim3(64 * d.wpb), args, h->lds_build, h->stream));
+      KB_HIP(hipLaunchKernel(h->fn_build, dim3(d.nblk), dim3(h->build_threads), args, h->lds_build, h->stream));
     } else if (which == 3) {  // GN fused build (gated: applies the pending frame steps each launch)
       KbDev dg = d;
       dg.gn_fused = 1;
       dg.fold = 0;
       void* args[] = {&dg, &one, &one};
-      KB_HIP(hipLaunchKernel(h->fn_build_gn, dim3(d.nblk), dim3(64 * d.wpb), args, h->lds_build, h->stream));
+      KB_HIP(hipLaunchKernel(h->fn_build_gn, dim3(d.nblk), dim3(h->build_threads), args, h->lds_build, h->stream));
     } else if (which == 1) {
       void* args[] = {&d, &g, &zero};
       KB_HIP(hipLaunchKernel(h->fn_solve, dim3(1), dim3(h->solve_threads), args, h->lds_solve, h->stream));

@@ -103,7 +103,7 @@ struct KbDev {
   KbCtrl* ctrl;
   int dbg_stop;   // diagnostic build only (KB_STAMPS): stop point of the timed kernel (-1: run to the end)
   int dbg_flags;  // diagnostic build only: bit 0 run the camera LDL^T twice (rolled)
-  long long* dbg_ts;  // diagnostic build only: [64] s_memrealtime stamps of the last k_solve (KB_TS)
+  long long* dbg_ts;  // diagnostic build only: [128] s_memrealtime stamps: k_solve (KB_TS) | k_buildp (KB_TSB, +64)
 };
 
 #ifdef KB_STAMPS
@@ -119,7 +119,15 @@ struct KbDev {
   do {                                                                                   \
     if (threadIdx.x == 0 && (d).dbg_ts) (d).dbg_ts[i] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
+// build-kernel timeline (k_buildp): lane 0 of the calling wave of block 0 stamps slot 64 + i
+#define KB_TSB(d, i)                                                                                        \
+  do {                                                                                                      \
+    if (blockIdx.x == 0 && (threadIdx.x & 63) == 0 && (d).dbg_ts) (d).dbg_ts[64 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
 #else
+#define KB_TSB(d, i) \
+  do {               \
+  } while (0)
 #define KB_STAMP(d, i) \
   do {                 \
   } while (0)

@@ -468,7 +468,7 @@ __device__ __forceinline__ void schur_tiles_store(double* prow_schur, int C, con
 // A = (H_ff + lam2 I)^-1 H_fc, b = (H_ff + lam2 I)^-1 g_f (solveSystem's frame blocks of the Schur solve)
 // into Q (row stride CZ) and HBM.  P holds rows 0..5 of [H_fc | g_f] (stride CZ).  Returns false if not PD.
 __device__ __forceinline__ bool frame_gj(const KbDev& d, int f, const double* Hff, double lam2, const double* P,
-                                         double* Q, int CZ, int lane) {
+                                         double* Q, int CZ, int lane, bool store = true) {
   const int C = d.C;
   double col[2][6];
 #pragma unroll
@@ -504,10 +504,78 @@ __device__ __forceinline__ bool frame_gj(const KbDev& d, int f, const double* Hf
 #pragma unroll
       for (int i = 0; i < 6; ++i) {
         Q[i * CZ + c] = col[sl][i];
+        if (!store) continue;
         if (c < C)
           d.Af[((size_t)f * 6 + i) * C + c] = col[sl][i];
         else
           d.bf[(size_t)f * 6 + i] = col[sl][i];
+      }
+    }
+  }
+  return ok;
+}
+
+// [A | b] = (H_ff + lam2 I)^-1 [H_fc | g_f] by LDL^T of the 6 x 6 block, factored redundantly in every lane's
+// registers (no cross-lane broadcast: a short dependent chain, which matters when the wave shares its SIMD with
+// MFMA-heavy waves), then each lane solves its columns lane and lane + 64 of [H_fc | g_f] (P, rows of 6).
+// Writes Q (rows of 6, columns 0..C) and, if `store`, A_f / b_f to HBM.  Returns false if not positive definite.
+__device__ __forceinline__ bool frame_ldl(const KbDev& d, int f, const double* Hff, double lam2, const double* P,
+                                          double* Q, int CZ, int lane, bool store) {
+  const int C = d.C;
+  double L[6][6], Di[6];
+  bool ok = true;
+#pragma unroll
+  for (int i = 0; i < 6; ++i)
+#pragma unroll
+    for (int j = 0; j <= i; ++j) L[i][j] = Hff[i * 6 + j] + (i == j ? lam2 : 0.0);
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    double v[6];
+#pragma unroll
+    for (int j = 0; j < k; ++j) v[j] = L[k][j] * L[j][j];  // L_kj D_j (D_j kept on the diagonal)
+    double dk = L[k][k];
+#pragma unroll
+    for (int j = 0; j < k; ++j) dk -= L[k][j] * v[j];
+    ok = ok && (dk > 0.0);
+    L[k][k] = dk;
+    Di[k] = recip_d(dk);
+#pragma unroll
+    for (int i = k + 1; i < 6; ++i) {
+      double s = L[i][k];
+#pragma unroll
+      for (int j = 0; j < k; ++j) s -= L[i][j] * v[j];
+      L[i][k] = s * Di[k];
+    }
+  }
+#pragma unroll
+  for (int sl = 0; sl < 2; ++sl) {
+    const int c = lane + 64 * sl, cc = min(c, C);
+    double x[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {  // L y = b
+      double s = P[i * CZ + cc];
+#pragma unroll
+      for (int j = 0; j < i; ++j) s -= L[i][j] * x[j];
+      x[i] = s;
+    }
+#pragma unroll
+    for (int i = 0; i < 6; ++i) x[i] *= Di[i];
+#pragma unroll
+    for (int i = 5; i >= 0; --i) {  // L^T x = D^-1 y
+      double s = x[i];
+#pragma unroll
+      for (int j = i + 1; j < 6; ++j) s -= L[j][i] * x[j];
+      x[i] = s;
+    }
+    if (c <= C) {
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        Q[i * CZ + c] = x[i];
+        if (!store) continue;
+        if (c < C)
+          d.Af[((size_t)f * 6 + i) * C + c] = x[i];
+        else
+          d.bf[(size_t)f * 6 + i] = x[i];
       }
     }
   }
@@ -951,6 +1019,457 @@ __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
     prow[d.Wp] = m;
   }
   KB_STAMP(d, 25);
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_buildp: k_build for rigs with one wave per camera (nsplit == 1, 4 <= N <= kBuildpMaxCams), pipelined over
+// the block's frames.  Waves 0..N-1 (view waves) own camera w: per frame the view's corners (projection, one
+// Jacobian row per lane, 32-row LDS tiles, v_mfma_f64_16x16x4 SYRK), the camera's running local sums (registers)
+// and the view's 6-D chain expansion (G, P_v = G^T H_dd, G^T g_d, P_v G, G^T H_dI: the camera's intrinsic
+// columns of [H_fc | g_f], and P_v K_{v,j}: its share of the baseline columns), all wave-local; the next frame's
+// first loads are issued before the expansion.  NF frame waves run one frame behind on the view outputs
+// (double-buffered by frame parity): the frame sums H_ff, g_f and sum_{i>j} P_i K_{i,j}, the Gauss-Jordan
+// elimination into [A_f | b_f] (every frame wave, identical bits; frame wave 0 stores) and the Schur tiles
+// [H_fc | g_f]^T [A_f | b_f], split over the frame waves.  One block barrier per frame: the SYRK of frame f (MFMA)
+// overlaps the elimination and Schur sums of frame f - 1 on the same CU.  The sums follow k_build's order except
+// the baseline columns (per-camera products summed over cameras).
+// ---------------------------------------------------------------------------------------------
+constexpr int kBuildpMaxCams = 8;
+// frame waves of k_buildp: the Schur tiles per frame wave TT picks them (<= 5 tiles: 2 waves, else 3)
+template <int TT>
+constexpr int buildp_nf() { return TT > 5 ? 3 : 2; }
+
+// intrinsics count of a one-model set (0 for a mix): a constant count lets the compiler drop the unused columns
+template <unsigned MM>
+constexpr int mm_nintr() {
+  if (MM == 0u || (MM & (MM - 1u))) return 0;
+  int m = 0;
+  while (!((MM >> m) & 1u)) ++m;
+  return (m == KB_PINHOLE_RADTAN || m == KB_PINHOLE_EQUI) ? 8 : m == KB_OMNI_RADTAN ? 9
+         : (m == KB_EUCM || m == KB_DS)                   ? 6 : 5;
+}
+
+// lower tiles of [P | .]^T [Q | .] owned by frame wave fw of NF (q = fw, fw + NF, ...), -1 terminated
+template <int TT>
+__device__ __forceinline__ void schur_tiles_assign_fw(int nbz, int fw, int* tii, int* tjj) {
+  const int ntiles = nbz * (nbz + 1) / 2;
+#pragma unroll
+  for (int t = 0; t < TT; ++t) {
+    const int q = fw + buildp_nf<TT>() * t;
+    const int ii = (fw >= 0 && q < ntiles) ? tri_row(q) : -1;
+    tii[t] = __builtin_amdgcn_readfirstlane(ii);  // wave-uniform: scalar registers, not 2 x TT VGPRs
+    tjj[t] = __builtin_amdgcn_readfirstlane(ii >= 0 ? q - ii * (ii + 1) / 2 : -1);
+  }
+}
+
+// schur_tiles_accumulate over 6-row P, Q (the MFMA k rows 6, 7 are zero operands, not LDS rows)
+template <int TT>
+__device__ __forceinline__ void schur_tiles_accumulate6(const double* P, const double* Q, int CZ, const int* tii,
+                                                        const int* tjj, v4d* acc, int lane) {
+#pragma unroll
+  for (int t = 0; t < TT; ++t) {
+    if (tii[t] < 0) break;  // wave-uniform
+    const double* ya = P + 16 * tii[t] + (lane & 15);
+    const double* yb = Q + 16 * tjj[t] + (lane & 15);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int k = 4 * s + (lane >> 4);
+      const int kc = min(k, 5);
+      const double a = ya[kc * CZ], b = yb[kc * CZ];
+      acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(k < 6 ? a : 0.0, k < 6 ? b : 0.0, acc[t], 0, 0, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);  // one tile's operands at a time (hoisting all of them spills)
+  }
+}
+
+template <int TT, bool GNF, unsigned MM>
+__global__ void __launch_bounds__(64 * (kBuildpMaxCams + 3)) k_buildp(KbDev d, int gate, int fuse) {
+  KbCtrl* c = d.ctrl;
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  constexpr int NF = buildp_nf<TT>();
+  const int N = d.N, C = d.C, NW = N + NF, NP = N * (N - 1) / 2;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, nth = blockDim.x;
+  const int tid = threadIdx.x;
+  const int nbz = (C + 16) >> 4, CZ = 16 * nbz;
+  const int VBS = 36 * NP + 44 * N + 6 * CZ, FBS = 6 * CZ;
+  double* Xw = sm + wave * 32 * XS;     // [N][32][XS] view waves' Jacobian-row tiles (P_v after the SYRK)
+  double* Hw = sm + N * 32 * XS;        // [N][256] view local Hessians
+  double* Wv = Hw + N * 256;            // [N][64]: R(9) t(3) tf(3) | G(36) at +16
+  double* VB = Wv + N * 64;             // [VBS] view outputs: P_i K_{i,j} [NP][36] | dH [N][36] | dg [N][8] |
+                                        //   intrinsic columns [6][CZ]
+  double* FI = VB + VBS;                // [40 + 6 CZ] frame sums: H_ff | [H_fc | g_f] (rows of 6)
+  double* FB = FI + 40 + 6 * CZ;        // [NF][FBS] frame wave's [A_f | b_f]
+  double* Kl = FB + NF * FBS;           // [NP][36] K_{i,j}, j < i, at (i(i-1)/2 + j)
+  double* tg = Kl + 36 * NP;            // [n_target][3] target corners (when staged) | frame poses [gframes][8]
+  __shared__ double wmx[kBuildpMaxCams + 3];
+  __shared__ int okl;
+  __shared__ double cst[KB_MAX_CAMS][24];  // per camera: chain L (12) | intrinsics (10)
+  __shared__ int ctab[2][KB_MAX_CAMS];      // per camera: first intrinsic column | baseline column
+  const int W = d.W;
+  const int f0 = blockIdx.x * d.gframes, f1 = min(d.F, f0 + d.gframes), G = f1 - f0;
+  const bool vw = wave < N;  // view wave (camera = wave) | frame wave fw = wave - N
+  const int cam = __builtin_amdgcn_readfirstlane(vw ? wave : 0), fw = __builtin_amdgcn_readfirstlane(wave - N);
+  if (wave == 0) KB_TSB(d, 0);
+  // ---- round 1: launch-independent loads, unconditional (clamped) and pinned before the gate
+  const KbCtrl cin = *c;
+  const int done = cin.done, dob = cin.do_build, cur = cin.cur;
+  const double lam = gate ? cin.lambda : d.host_lambda;
+  const bool tg_lds = d.K * 3 <= kTargetLds;
+  const int nt3 = 3 * d.K;
+  constexpr int kTgU = 2;
+  double tv[kTgU];
+#pragma unroll
+  for (int u = 0; u < kTgU; ++u) tv[u] = d.target[min(tid + u * nth, nt3 - 1)];
+  int2 fv = d.fview[(size_t)f0 * N + cam];
+#pragma unroll
+  for (int u = 0; u < kTgU; ++u) KB_KEEP(tv[u]);
+  KB_KEEPS(fv.x);
+  KB_KEEPS(fv.y);
+  const bool gfu = GNF && gate;  // GN fused: the previous solve's frame steps are applied here
+  double yr[6][2], dxv[2] = {0.0, 0.0}, bq = 0.0;
+  if (gfu) {
+#pragma unroll
+    for (int sl = 0; sl < 2; ++sl) {
+      const int q = lane + 64 * sl;
+      const double v = d.dx[min(q, C - 1)];
+      dxv[sl] = q < C ? v : 0.0;
+    }
+    fdx_load(d, f0, lane, yr, bq);
+#pragma unroll
+    for (int sl = 0; sl < 2; ++sl) {
+      KB_KEEP(dxv[sl]);
+#pragma unroll
+      for (int r = 0; r < 6; ++r) KB_KEEP(yr[r][sl]);
+    }
+    KB_KEEP(bq);
+  }
+  if (gate && (done || !dob)) return;
+  const bool upd = gfu && cin.have_dx;
+  const int bs = upd ? 1 - cur : cur;
+  // ---- round 2: loads indexed by round 1
+  const double* s = d.state + (size_t)bs * d.S;
+  const double* sf = d.state + (size_t)cur * d.S;
+  double* snew = d.state + (size_t)(1 - cur) * d.S;
+  if (tid < N * 22) {
+    const int cm = tid / 22, e = tid % 22;
+    cst[cm][e] = e < 12 ? cam_L(d, bs)[cm * 12 + e] : s[cm * KB_MAX_INTR + e - 12];
+  }
+  if (tid < 2 * N) ctab[tid / N][tid % N] = (tid < N) ? cam_arg(d.col_intr, tid) : cam_arg(d.col_base, tid - N);
+  double* fpl = tg + (tg_lds ? nt3 : 0);
+  double fp0[7];
+#pragma unroll
+  for (int q = 0; q < 7; ++q) fp0[q] = sf[d.off_frame + 7 * f0 + q];
+  int cidn;  // view waves: lane = corner (lane & 31) of a 32-corner tile, Jacobian row lane >> 5 (0: u, 1: v)
+  double2 yn;
+  {
+    const int k = min(fv.x + (lane & 31), max(fv.y - 1, 0));
+    cidn = d.cid[k];
+    yn = d.y[k];
+  }
+  const double* Kc = cam_K(d, bs);
+  for (int q = tid; q < 18 * N * (N - 1); q += nth) {
+    const int e = q % 36, ij = q / 36;
+    int i = 1;
+    while (i * (i + 1) / 2 <= ij) ++i;
+    const int j = ij - i * (i - 1) / 2;
+    Kl[q] = Kc[(size_t)(i * N + j) * 36 + e];
+  }
+  KB_KEEPS(cidn);
+  double wmax = 0.0;
+  if (upd) frame_step(d, f0, wave == 0, lane, yr, dxv, bq, fp0, snew, wmax);
+  if (wave == 0 && lane < 7) {
+    double pv = fp0[0];
+#pragma unroll
+    for (int q = 1; q < 7; ++q) pv = (lane == q) ? fp0[q] : pv;
+    fpl[lane] = pv;
+  }
+  for (int j = 1 + wave; j < G; j += NW) {
+    double fp[7];
+#pragma unroll
+    for (int q = 0; q < 7; ++q) fp[q] = sf[d.off_frame + 7 * (f0 + j) + q];
+    if (upd) {
+      double af[6][2], bfq;
+      fdx_load(d, f0 + j, lane, af, bfq);
+      frame_step(d, f0 + j, true, lane, af, dxv, bfq, fp, snew, wmax);
+    }
+    if (lane < 7) {
+      double pv = fp[0];
+#pragma unroll
+      for (int q = 1; q < 7; ++q) pv = (lane == q) ? fp[q] : pv;
+      fpl[8 * j + lane] = pv;
+    }
+  }
+  if (lane == 0) wmx[wave] = wmax;
+  if (tg_lds) {
+#pragma unroll
+    for (int u = 0; u < kTgU; ++u)
+      if (tid + u * nth < nt3) tg[tid + u * nth] = tv[u];
+    for (int q = tid + kTgU * nth; q < nt3; q += nth) tg[q] = d.target[q];
+  }
+  const double* tgt = tg_lds ? tg : d.target;
+  const double lam2 = lam * lam;
+  if (tid == 0) okl = 1;
+  __syncthreads();
+  if (wave == 0) KB_TSB(d, 1);
+
+  const int mrow = lane >> 4, mcol = lane & 15;
+  double* prow = d.part + (size_t)blockIdx.x * d.Wr;
+  double* Fh = FI;      // frame inputs of the frame being eliminated: H_ff (40) | [H_fc | g_f] [6][CZ]
+  double* P = FI + 40;
+  // iteration it: phase A (view waves) the frame sums of frame it - 1 -> FI; barrier; phase B: view waves run the
+  // views of frame it -> VB, frame waves eliminate frame it - 1 from FI; barrier.  The roles run separate loops
+  // with the same barrier count (2 (G + 1)), so neither holds the other's registers.
+  if (vw) {
+    const int model = cam_arg(d.model, cam), nin = mm_nintr<MM>() ? mm_nintr<MM>() : cam_arg(d.nintr, cam);
+    const double* Lc = cst[cam];
+    const double* intr = cst[cam] + 12;
+    v4d creg = {0.0, 0.0, 0.0, 0.0};  // the camera's local sums over the block's frames
+    for (int it = 0; it <= G; ++it) {
+      if (it > 0) {
+        // ---------------- phase A: sums of frame f - 1 over its views (camera order), all view waves
+        const int f = f0 + it - 1;
+        const double* Cb = VB;
+        const double* dHv = VB + 36 * NP;
+        const double* dgv = VB + 36 * NP + N * 36;
+        const double* Pi = VB + 36 * NP + N * 44;
+        const int CI = C - 6 * (N - 1);  // intrinsic columns [0, CI)
+        const int nsum = 42 + 36 * (N - 1);
+        for (int q = tid; q < nsum + 6 * CI; q += 64 * N) {
+          if (q >= nsum) {  // the views' intrinsic columns
+            const int e = q - nsum, a = e / CI, cc = e - a * CI;
+            P[a * CZ + cc] = Pi[a * CZ + cc];
+            continue;
+          }
+          // every term of an output is loaded at once (clamped addresses), then summed in camera order
+          double v[kBuildpMaxCams];
+          if (q < 42) {
+            const double* src = q < 36 ? dHv + q : dgv + q - 36;
+            const int stride = q < 36 ? 36 : 8;
+#pragma unroll
+            for (int i = 0; i < kBuildpMaxCams; ++i) v[i] = src[min(i, N - 1) * stride];
+          } else {  // H_f,B_j = sum_{i > j} P_i K_{i,j} (the views' products)
+            const int e = q - 42, j = e / 36, ab2 = e % 36;
+#pragma unroll
+            for (int i = 0; i < kBuildpMaxCams; ++i) {
+              const int ii = min(max(i, j + 1), N - 1);
+              v[i] = Cb[(ii * (ii - 1) / 2 + j) * 36 + ab2];
+            }
+          }
+          const int e = q - 42, j = q < 42 ? -1 : e / 36, ab2 = e - 36 * j;
+          double sacc = 0.0;
+#pragma unroll
+          for (int i = 0; i < kBuildpMaxCams; ++i)
+            if (i > j && i < N) sacc += v[i];
+          if (q < 36) {
+            Fh[q] = sacc;
+            d.Hff[(size_t)f * 36 + q] = sacc;
+          } else if (q < 42) {
+            P[(q - 36) * CZ + C] = sacc;
+            d.gf[(size_t)f * 6 + q - 36] = sacc;
+          } else {
+            const int a = ab2 / 6, b = ab2 % 6;
+            P[a * CZ + ctab[1][j] + b] = sacc;
+            d.Hfc[((size_t)f * 6 + a) * C + ctab[1][j] + b] = sacc;
+          }
+        }
+      }
+      __syncthreads();
+      if (it < G) {
+        // ---------------- phase B: view (f, cam)
+        const int f = f0 + it;
+        int lane = threadIdx.x & 63;  // opaque per frame (see the frame waves)
+        asm volatile("" : "+v"(lane));
+        const int r = lane >> 5, row = 2 * (lane & 31) + r, mrow = lane >> 4, mcol = lane & 15;
+        if (wave == 0 && it < 8) KB_TSB(d, 2 + 2 * it);
+        double* vb = VB;
+        const int2 fvn = d.fview[(size_t)min(f + 1, f1 - 1) * N + cam];  // the next frame's view (first loads below)
+        double fp[7];
+#pragma unroll
+        for (int q = 0; q < 7; ++q) fp[q] = fpl[8 * it + q];
+        double Ri[9], ti[3], R[9], t[3];
+        pose_inverse(fp, Ri, ti);
+        rt_mul(Lc, Lc + 9, Ri, ti, R, t);  // T_cam_w = L_cam T_f^-1
+        v4d acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+        const int o0 = fv.x, o1 = fv.y;
+        for (int base = o0; base < o1; base += 32) {  // 32 corners = 64 rows, through the 32-row tile in two halves
+          const int k = base + (lane & 31);
+          const int cid = cidn;
+          const double2 yv = yn;
+          if (base + 32 < o1) {  // software-pipelined: next tile's corner ids and keypoints
+            const int kn = min(k + 32, o1 - 1);
+            cidn = d.cid[kn];
+            yn = d.y[kn];
+          }
+          double xr[16];
+#pragma unroll
+          for (int q = 0; q < 16; ++q) xr[q] = 0.0;
+          if (k < o1) {
+            const double X0 = tgt[3 * cid], X1 = tgt[3 * cid + 1], X2 = tgt[3 * cid + 2];
+            const double p0 = R[0] * X0 + R[1] * X1 + R[2] * X2 + t[0];
+            const double p1 = R[3] * X0 + R[4] * X1 + R[5] * X2 + t[1];
+            const double p2 = R[6] * X0 + R[7] * X1 + R[8] * X2 + t[2];
+            double u, w, Jp[6], Ji[2 * KB_MAX_INTR];
+            project_jac<MM>(model, intr, p0, p1, p2, u, w, Jp, Ji);
+            const double e = r ? yv.y - w : yv.x - u;
+            const double j0 = r ? Jp[3] : Jp[0], j1 = r ? Jp[4] : Jp[1], j2 = r ? Jp[5] : Jp[2];
+            // J_delta = -Jp [I | [p]x]   (HomogeneousExpressionNode.cpp:71-81, boxMinus)
+            xr[0] = -j0;
+            xr[1] = -j1;
+            xr[2] = -j2;
+            xr[3] = -(j1 * p2 - j2 * p1);
+            xr[4] = -(-j0 * p2 + j2 * p0);
+            xr[5] = -(j0 * p1 - j1 * p0);
+            // intrinsics: -Jp, -Jd (CameraDesignVariable.hpp(impl):38-54)
+#pragma unroll
+            for (int q = 0; q < 9; ++q) xr[6 + q] = (q < nin) ? -(r ? Ji[KB_MAX_INTR + q] : Ji[q]) : 0.0;
+            xr[15] = -e;  // column 15 carries -e: H[:,15] = rhs part, H[15][15] = chi^2
+          }
+          // rows 2n .. 63 of a partial pass are zero: only the k-steps holding valid rows are issued (k-step ks = rows
+          // 4ks .. 4ks + 3 of the pass, even ks into acc0, odd into acc1)
+          const int nks = (2 * min(32, o1 - base) + 3) >> 2;
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            if (8 * h >= nks) break;  // wave-uniform
+            if ((row >> 5) == h) {
+#pragma unroll
+              for (int q = 0; q < 16; ++q) Xw[(row & 31) * XS + q] = xr[q];
+            }
+            KB_WAVE_SYNC();
+#pragma unroll
+            for (int kk = 0; kk < 8; kk += 2) {
+              const int ks = 8 * h + kk;
+              if (ks < nks) {
+                const double xa = Xw[(4 * kk + mrow) * XS + mcol];
+                acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(xa, xa, acc0, 0, 0, 0);
+              }
+              if (ks + 1 < nks) {
+                const double xb = Xw[(4 * kk + 4 + mrow) * XS + mcol];
+                acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(xb, xb, acc1, 0, 0, 0);
+              }
+            }
+            KB_WAVE_SYNC();
+          }
+        }
+        {  // the next frame's first corner ids and keypoints, in flight during the expansion and the barrier
+          fv = fvn;
+          const int k = min(fvn.x + (lane & 31), max(fvn.y - 1, 0));
+          cidn = d.cid[k];
+          yn = d.y[k];
+        }
+        if (wave == 0 && it < 8) KB_TSB(d, 3 + 2 * it);
+        // f64 MFMA C/D layout: lane l, reg r -> row (l>>4) + 4r, col l&15
+        double* H = Hw + cam * 256;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const double h = acc0[q] + acc1[q];
+          creg[q] = creg[q] + h;
+          H[(mrow + 4 * q) * 16 + mcol] = h;
+        }
+        double* wv = Wv + cam * 64;
+        if (lane == 0) {
+#pragma unroll
+          for (int q = 0; q < 9; ++q) wv[q] = R[q];
+          wv[9] = t[0];
+          wv[10] = t[1];
+          wv[11] = t[2];
+          wv[12] = fp[4];
+          wv[13] = fp[5];
+          wv[14] = fp[6];
+        }
+        KB_WAVE_SYNC();
+        // expansion of view (f, cam) through the 6-D chains
+        const bool has = o1 > o0;
+        double* Gm = wv + 16;
+        if (lane < 36) Gm[lane] = chain_entry(wv, wv + 9, wv + 12, lane / 6, lane % 6);
+        KB_WAVE_SYNC();
+        double* Pv = Xw;  // wave-local
+        double* Cb = vb;  // P_v K_{v,j} at pair (v(v-1)/2 + j)
+        double* dHv = vb + 36 * NP + cam * 36;
+        double* dgv = vb + 36 * NP + N * 36 + cam * 8;
+        double* Pi = vb + 36 * NP + N * 44;
+        if (lane < 36) {
+          const int a = lane / 6, b = lane % 6;
+          double sacc = 0.0;
+#pragma unroll
+          for (int k = 0; k < 6; ++k) sacc += Gm[k * 6 + a] * H[k * 16 + b];
+          Pv[lane] = has ? sacc : 0.0;  // P_v = G^T H_dd
+        } else if (lane < 42) {
+          const int a = lane - 36;
+          double sacc = 0.0;
+#pragma unroll
+          for (int k = 0; k < 6; ++k) sacc += Gm[k * 6 + a] * H[k * 16 + 15];
+          dgv[a] = has ? sacc : 0.0;  // G^T g_d
+        }
+        KB_WAVE_SYNC();
+        if (lane < 36) {
+          const int a = lane / 6, b = lane % 6;
+          double sacc = 0.0;
+#pragma unroll
+          for (int k = 0; k < 6; ++k) sacc += Pv[a * 6 + k] * Gm[k * 6 + b];
+          dHv[lane] = sacc;  // P_v G_v
+        }
+        if (lane < 6 * nin) {
+          const int a = lane / nin, q = lane % nin;
+          double sacc = 0.0;
+#pragma unroll
+          for (int k = 0; k < 6; ++k) sacc += Gm[k * 6 + a] * H[k * 16 + 6 + q];
+          sacc = has ? sacc : 0.0;  // G^T H_dI
+          Pi[a * CZ + ctab[0][cam] + q] = sacc;
+          d.Hfc[((size_t)f * 6 + a) * C + ctab[0][cam] + q] = sacc;
+        }
+        // this camera's share of the baseline columns: P_v K_{v,j}, j < v
+        for (int q = lane; q < 36 * cam; q += 64) {
+          const int j = q / 36, ab2 = q - 36 * j, a = ab2 / 6, b = ab2 % 6;
+          const double* K = Kl + (cam * (cam - 1) / 2 + j) * 36;
+          double sacc = 0.0;
+#pragma unroll
+          for (int k = 0; k < 6; ++k) sacc += Pv[a * 6 + k] * K[k * 6 + b];
+          Cb[(cam * (cam - 1) / 2) * 36 + q] = sacc;
+        }
+      }
+      __syncthreads();
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {  // the camera's local sums, upper packed
+      const int a = mrow + 4 * q, b = mcol;
+      if (a <= b) prow[cam * 136 + d16_index(a, b)] = creg[q];
+    }
+  } else {
+    v4d acc[TT];
+    int tii[TT], tjj[TT];
+#pragma unroll
+    for (int t = 0; t < TT; ++t) acc[t] = v4d{0.0, 0.0, 0.0, 0.0};
+    schur_tiles_assign_fw<TT>(fuse ? nbz : 0, fw, tii, tjj);
+    double* Q = FB + fw * FBS;  // this frame wave's [A_f | b_f] [6][CZ]
+    for (int it = 0; it <= G; ++it) {
+      __syncthreads();  // phase A: the view waves sum frame it - 1 into FI
+      if (it > 0 && fuse) {
+        // ---------------- phase B: frame f = it - 1 (one behind the views): elimination + Schur tiles
+        const int f = f0 + it - 1;
+        // an opaque lane id per frame: the lane-dependent addresses and selects of the elimination are recomputed
+        // here instead of being hoisted out of the loop (which spills at this kernel's register budget)
+        int lane = threadIdx.x & 63;
+        asm volatile("" : "+v"(lane));
+        if (fw == 0 && it <= 8) KB_TSB(d, 20 + 4 * (it - 1));
+        const bool ok = frame_ldl(d, f, Fh, lam2, P, Q, CZ, lane, fw == 0);
+        if (!ok && lane == 0) okl = 0;
+        KB_WAVE_SYNC();
+        if (fw == 0 && it <= 8) KB_TSB(d, 22 + 4 * (it - 1));
+        schur_tiles_accumulate6<TT>(P, Q, CZ, tii, tjj, acc, lane);
+        if (fw == 0 && it <= 8) KB_TSB(d, 23 + 4 * (it - 1));
+      }
+      __syncthreads();
+    }
+    if (fuse) schur_tiles_store<TT>(prow + N * 136, C, tii, tjj, acc);
+  }
+  __syncthreads();  // okl final
+  if (wave == 0) KB_TSB(d, 60);
+  if (fuse && tid == 0) prow[N * 136 + W] = okl ? 0.0 : 1.0;  // non-PD frame blocks (summed)
+  if (GNF && tid == 0) {  // the block's max |dx_f| (reduced with max by k_colsum)
+    double m = 0.0;
+    for (int q = 0; q < NW; ++q) m = fmax(m, wmx[q]);
+    prow[d.Wp] = m;
+  }
 }
 
 // ---------------------------------------------------------------------------------------------

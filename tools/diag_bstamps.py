@@ -1,0 +1,35 @@
+"""Diagnostic: timeline of block 0 of the last pipelined build (k_buildp) inside GN passes (KB_TSB stamps,
+s_memrealtime 100 MHz), diagnostic library only: python tools/diag_bstamps.py [config]"""
+import ctypes as C
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from kalibr_amd import capi, synth  # noqa: E402
+
+capi.LIB_PATH = os.path.join(ROOT, "kalibr_amd", "libkalibr_hip_stamps.so")
+L = capi.lib()
+L.kb_diag_read_ts.argtypes = [C.c_void_p, C.POINTER(C.c_longlong), C.c_int]
+cfg = int(sys.argv[1]) if len(sys.argv) > 1 else 4
+p = synth.make_config(cfg)
+g = capi.Solver(p)
+g.set_state(p.state_init)
+buf = (C.c_longlong * 128)()
+assert L.kb_diag_read_ts(g.h, buf, 128) == 0  # allocates the stamp buffer
+names = {0: "entry", 1: "prologue barrier", 60: "end"}
+for it in range(8):
+    names[2 + 2 * it] = f"view it{it} start"
+    names[3 + 2 * it] = f"view it{it} SYRK done"
+    names[20 + 4 * it] = f"  frame f{it} start"
+    names[21 + 4 * it] = f"  frame f{it} sums done"
+    names[22 + 4 * it] = f"  frame f{it} GJ done"
+    names[23 + 4 * it] = f"  frame f{it} Schur done"
+for rep in range(2):
+    g.set_state(p.state_init)
+    g.run_gn(16)
+    assert L.kb_diag_read_ts(g.h, buf, 128) == 0
+    t0 = buf[64]
+    order = sorted((buf[64 + i] - t0, i) for i in names if buf[64 + i] >= t0 and buf[64 + i] - t0 < 10_000_000)
+    print(f"k_buildp block 0 timeline (rep {rep}, us from entry):\n" +
+          "\n".join(f"{names[i]:28s} {dt / 100:8.2f}" for dt, i in order))
