@@ -89,6 +89,10 @@ int kb_build(kb_handle* h, int use_mestimator);
 /* LinearSystemSolver::setConstantConditioner (LinearSystemSolver.cpp:111-114):
  * "the square of this value will be added to the diagonal" (LinearSystemSolver.hpp:33-39). */
 int kb_set_constant_conditioner(kb_handle* h, double diag);
+/* LinearSystemSolver::setConditioner (LinearSystemSolver.cpp:98-102): diag[ncols] in the canonical column order;
+ * its squares are added to the diagonal of the system kb_solve solves (until kb_set_constant_conditioner).
+ * The direct solver only; the device-resident loop conditions with the trust-region lambda as before. */
+int kb_set_conditioner(kb_handle* h, const double* diag);
 /* LinearSystemSolver::solveSystem (SparseCholeskyLinearSystemSolver.cpp:48-89):
  * solves (J^T J + diag^2 I) dx = rhs.  *ok = 0 on a non-positive-definite system
  * (CHOLMOD failure semantics, Cholmod(impl).hpp:287-328); dx_out untouched then. */

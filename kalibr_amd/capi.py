@@ -20,7 +20,7 @@ dp = C.POINTER(C.c_double)
 EXPORTS = [
     "kb_create", "kb_destroy", "kb_last_error", "kb_upload_observations", "kb_set_state", "kb_set_state_flat",
     "kb_get_state_flat", "kb_state_size", "kb_num_cols", "kb_camera_cols", "kb_eval_cost", "kb_build",
-    "kb_set_constant_conditioner", "kb_solve", "kb_get_rhs", "kb_apply_update", "kb_revert", "kb_get_normal_blocks",
+    "kb_set_constant_conditioner", "kb_set_conditioner", "kb_solve", "kb_get_rhs", "kb_apply_update", "kb_revert", "kb_get_normal_blocks",
     "kb_optimize", "kb_get_trace", "kb_run_gn_iterations", "kb_build_kernel_stats", "kb_comm_get_unique_id",
     "kb_comm_init", "kb_comm_init_local", "kb_selftest_mfma", "kb_solve_marginal", "kb_analyze_marginal",
     # block-Jacobi PCG (LinearSolverPCG)
@@ -112,6 +112,7 @@ def lib():
         L.kb_eval_cost.argtypes = [C.c_void_p, dp]
         L.kb_build.argtypes = [C.c_void_p, C.c_int]
         L.kb_set_constant_conditioner.argtypes = [C.c_void_p, C.c_double]
+        L.kb_set_conditioner.argtypes = [C.c_void_p, dp]
         L.kb_solve.argtypes = [C.c_void_p, dp, C.POINTER(C.c_int)]
         L.kb_get_rhs.argtypes = [C.c_void_p, dp]
         L.kb_apply_update.argtypes = [C.c_void_p, dp, dp]
@@ -232,6 +233,12 @@ class Solver:
 
     def set_constant_conditioner(self, diag):
         _check(lib().kb_set_constant_conditioner(self.h, float(diag)))
+
+    def set_conditioner(self, diag):
+        """setConditioner: diag (canonical column order), squares added to the diagonal of kb_solve's system."""
+        d = np.ascontiguousarray(diag, dtype=np.float64)
+        assert d.shape == (self.ncols,)
+        _check(lib().kb_set_conditioner(self.h, _d(d)))
 
     def solve(self):
         dx = np.zeros(self.ncols)

@@ -150,6 +150,8 @@ struct kb_handle {
   kb_pcg_options pcg{1e-6, -1, 1};
   double pcg_residual = -1.0;  // LinearSolverPCG::_residual (init(): -1)
   kb_pcg_info pcg_info{0, 0.0, 0.0};
+  double* cond2 = nullptr;     // setConditioner: squared diagonal [ncols] (canonical order)
+  bool use_cond = false;       // kb_set_conditioner active (kb_set_constant_conditioner clears it)
   double* pcg_buf = nullptr;   // part [F][C+1] | part2 [F] | info [8]
   int* pcg_cb = nullptr;       // [2][C] camera DV block start / size per column
   unsigned* pcg_bar = nullptr;
@@ -711,6 +713,19 @@ int kb_build(kb_handle* h, int use_mestimator) {
 int kb_set_constant_conditioner(kb_handle* h, double diag) {
   if (!h) return fail("null handle");
   h->d.host_lambda = diag;
+  h->use_cond = false;
+  return 0;
+}
+
+int kb_set_conditioner(kb_handle* h, const double* diag) {
+  if (!h || !diag) return fail("kb_set_conditioner: null");
+  KB_HIP(hipSetDevice(h->device));
+  if (!h->cond2 && h->alloc(&h->cond2, (size_t)h->ncols)) return -1;
+  std::vector<double> sq(h->ncols);
+  for (int k = 0; k < h->ncols; ++k) sq[k] = diag[k] * diag[k];  // "the square of these values" (:33-35)
+  KB_HIP(hipMemcpyAsync(h->cond2, sq.data(), sizeof(double) * h->ncols, hipMemcpyHostToDevice, h->stream));
+  KB_HIP(hipStreamSynchronize(h->stream));
+  h->use_cond = true;
   return 0;
 }
 
@@ -829,6 +844,7 @@ int kb_solve(kb_handle* h, double* dx_out, int* ok) {
   if (!h || !ok) return fail("kb_solve: null");
   KB_HIP(hipSetDevice(h->device));
   if (h->solver_kind == KB_SOLVER_PCG) {
+    if (h->use_cond) return fail("kb_solve (PCG): a diagonal conditioner is not supported, use a constant one");
     if (run_pcg(h, ok)) return -1;
     if (*ok && dx_out)
       KB_HIP(hipMemcpyAsync(dx_out, h->d.dx, sizeof(double) * h->ncols, hipMemcpyDeviceToHost, h->stream));
@@ -837,6 +853,11 @@ int kb_solve(kb_handle* h, double* dx_out, int* ok) {
   }
   const int one = 1;
   KB_HIP(hipMemcpyAsync(&h->d.ctrl->solve_ok, &one, sizeof(int), hipMemcpyHostToDevice, h->stream));
+  struct CondScope {  // the diagonal conditioner (kb_set_conditioner) enters this solve's frame and camera blocks
+    kb_handle* h;
+    CondScope(kb_handle* hh) : h(hh) { h->d.cond2 = h->use_cond ? h->cond2 : nullptr; }
+    ~CondScope() { h->d.cond2 = nullptr; }
+  } cs(h);
   if (launch_schur(h, 0)) return -1;
   if (launch_colsum(h, 0)) return -1;
   // k_solve folds the frame-block failure count and the LDL^T of S into ctrl->solve_ok

@@ -64,6 +64,7 @@ struct KbDev {
   int gn_fused;      // 1: Gauss-Newton passes fused as [update + build] -> colsum -> [GN policy + solve]
   int rank;
   double host_lambda;  // conditioner for the per-call (non-gated) path
+  const double* cond2;  // per-call solve with a diagonal conditioner: its squares [C + 6F] (canonical order), or null
   int model[KB_MAX_CAMS], nintr[KB_MAX_CAMS], col_intr[KB_MAX_CAMS], col_base[KB_MAX_CAMS];
   const double* target;
   const double2* y;

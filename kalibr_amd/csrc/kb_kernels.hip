@@ -476,7 +476,8 @@ __device__ __forceinline__ bool frame_gj(const KbDev& d, int f, const double* Hf
     const int q = lane + 64 * sl, qh = min(q, 5), qp = min(max(q - 6, 0), C);
 #pragma unroll
     for (int i = 0; i < 6; ++i) {
-      const double h = Hff[i * 6 + qh] + (i == qh ? lam2 : 0.0), pv = P[i * CZ + qp];
+      const double dg = d.cond2 ? d.cond2[C + 6 * f + i] : lam2;  // setConditioner's squares, or lambda^2
+      const double h = Hff[i * 6 + qh] + (i == qh ? dg : 0.0), pv = P[i * CZ + qp];
       col[sl][i] = q < 6 ? h : (q - 6 <= C ? pv : 0.0);
     }
   }
@@ -2349,7 +2350,7 @@ __device__ __forceinline__ LdlOut ldl_solve_reg(const KbDev& d, const double* S,
 // intrinsics_i x B_j = Hs_i[Id] K_{i,j} (j < i);  B_j x B_k = sum_{i > max(j,k)} K_{i,j}^T T_{i,k}, T = Hs_i[dd] K
 template <int CM>
 __device__ __forceinline__ void cam_expand_blocks(double* S, int C, int N, const int (*ctab)[KB_MAX_CAMS], const double* Hs,
-                                  const double* T, const double* K, double lam2, int nw) {
+                                  const double* T, const double* K, double lam2, int nw, const double* cond2) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int nA = N, nB = N * (N - 1) / 2, nC = (N - 1) * N / 2;
   for (int it = wave; it < nA + nB + nC; it += nw) {
@@ -2357,7 +2358,9 @@ __device__ __forceinline__ void cam_expand_blocks(double* S, int C, int N, const
       const int i = it, nin = ctab[0][i], c0 = ctab[1][i];
       for (int e = lane; e < nin * nin; e += 64) {
         const int x = e / nin, y = e % nin;
-        if (y <= x) S[sidx<CM>(c0 + x, c0 + y, C)] += Hs[i * 256 + (6 + x) * 16 + 6 + y] + ((x == y) ? lam2 : 0.0);
+        if (y <= x)
+          S[sidx<CM>(c0 + x, c0 + y, C)] +=
+              Hs[i * 256 + (6 + x) * 16 + 6 + y] + ((x == y) ? (cond2 ? cond2[c0 + x] : lam2) : 0.0);
       }
     } else if (it < nA + nB) {
       const int q = it - nA, i = tri_row(q) + 1, j = q - (i - 1) * i / 2;  // j < i
@@ -2382,7 +2385,7 @@ __device__ __forceinline__ void cam_expand_blocks(double* S, int C, int N, const
         }
         // entry (B_j a, B_k b) -> lower (B_k b, B_j a) when j < k
         const int r = (j < k) ? ctab[2][k] + b : ctab[2][j] + a, cc = (j < k) ? ctab[2][j] + a : ctab[2][j] + b;
-        S[sidx<CM>(r, cc, C)] += v + ((j == k && a == b) ? lam2 : 0.0);
+        S[sidx<CM>(r, cc, C)] += v + ((j == k && a == b) ? (cond2 ? cond2[r] : lam2) : 0.0);
       }
     }
   }
@@ -2519,7 +2522,7 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update, int nth) {
     if (fin[0]) return;
   }
   KB_TS(d, 2);
-  cam_expand_blocks<CM>(S, C, N, ctab, Hs, T, K, lam2, nth >> 6);
+  cam_expand_blocks<CM>(S, C, N, ctab, Hs, T, K, lam2, nth >> 6, gate ? nullptr : d.cond2);
   for (int p = tid; p < C; p += nth) {
     const double g = cam_grad_l(N, ci, Hs, K, p);
     bv[p] += g;

@@ -22,6 +22,273 @@ void LinearSystemSolver::setConstantConditioner(double diag) {
   _diagonalConditioner.assign(_JCols, diag);  // LinearSystemSolver.cpp:104-107
 }
 
+// ---------------------------------------------------------------- design variables and error terms
+namespace {
+using Kind = DesignVariable::Kind;
+
+// projection | distortion DV sizes of a camera model (CameraDesignVariable)
+void dv_split(int model, int* a, int* b) {
+  switch (model) {
+    case KB_OMNI_RADTAN: *a = 5, *b = 4; break;
+    case KB_EUCM: *a = 6, *b = 0; break;
+    case KB_OMNI: *a = 5, *b = 0; break;
+    case KB_DS: *a = 6, *b = 0; break;
+    case KB_PINHOLE_FOV: *a = 4, *b = 1; break;
+    case KB_PINHOLE_RADTAN:
+    case KB_PINHOLE_EQUI: *a = 4, *b = 4; break;
+    default: throw LinearSystemSolver::Exception("unknown camera model");
+  }
+}
+
+void need(bool c, const std::string& m) {
+  if (!c) throw LinearSystemSolver::Exception("initMatrixStructure: " + m);
+}
+}  // namespace
+
+int DesignVariable::minimalDimensions() const {
+  switch (kind) {
+    case Kind::Projection:
+    case Kind::Distortion: return (int)value.size();
+    case Kind::RotationQuaternion:
+    case Kind::EuclideanPoint:
+    case Kind::HomogeneousPoint: return 3;
+  }
+  return 0;
+}
+
+std::vector<DesignVariable*> assignColumnBases(const std::vector<DesignVariable*>& dvs) {
+  std::vector<DesignVariable*> act;
+  for (DesignVariable* dv : dvs)
+    if (dv && dv->isActive()) act.push_back(dv);
+  int columnBase = 0;
+  for (size_t i = 0; i < act.size(); ++i) {
+    act[i]->blockIndex = (int)i;
+    act[i]->columnBase = columnBase;
+    columnBase += act[i]->minimalDimensions();
+  }
+  return act;
+}
+
+TermAssembly assembleTerms(const std::vector<DesignVariable*>& dvs, const std::vector<ReprojectionErrorTerm*>& errors,
+                           const std::vector<double>& target) {
+  need(!errors.empty(), "no error terms");
+  need(target.size() % 3 == 0 && !target.empty(), "target must be [n][3]");
+  TermAssembly a;
+  // the rig: cameras, baselines and frames the terms read
+  int N = 0;
+  for (const ReprojectionErrorTerm* e : errors) {
+    need(e && e->projection && e->targetRotation && e->targetTranslation, "term without its design variables");
+    need(e->camera >= 0 && e->camera < KB_MAX_CAMS, "camera index out of range");
+    N = std::max(N, e->camera + 1);
+  }
+  a.projection.assign(N, nullptr);
+  a.distortion.assign(N, nullptr);
+  a.baseRotation.assign(std::max(N - 1, 0), nullptr);
+  a.baseTranslation.assign(std::max(N - 1, 0), nullptr);
+  std::vector<DesignVariable*> rots;  // frames, by first appearance
+  for (const ReprojectionErrorTerm* e : errors) {
+    const int c = e->camera;
+    need(e->projection->kind == Kind::Projection && e->projection->camera == c, "projection DV of another camera");
+    need(!a.projection[c] || a.projection[c] == e->projection, "two projection DVs for one camera");
+    a.projection[c] = e->projection;
+    need(!e->distortion || (e->distortion->kind == Kind::Distortion && e->distortion->camera == c),
+         "distortion DV of another camera");
+    need(!a.distortion[c] || a.distortion[c] == e->distortion, "two distortion DVs for one camera");
+    a.distortion[c] = e->distortion;
+    need(e->baselines.size() == 2 * (size_t)c, "pose chain is not B_{c-1} .. B_0 T^-1");
+    for (int j = 0; j < c; ++j) {
+      DesignVariable *r = e->baselines[2 * j], *t = e->baselines[2 * j + 1];
+      need(r && t && r->kind == Kind::RotationQuaternion && t->kind == Kind::EuclideanPoint, "baseline DV kinds");
+      need(!a.baseRotation[j] || (a.baseRotation[j] == r && a.baseTranslation[j] == t), "inconsistent baselines");
+      a.baseRotation[j] = r;
+      a.baseTranslation[j] = t;
+    }
+    need(e->targetRotation->kind == Kind::RotationQuaternion && e->targetTranslation->kind == Kind::EuclideanPoint,
+         "target pose DV kinds");
+    need(e->cornerId >= 0 && 3 * (size_t)e->cornerId < target.size(), "corner id outside the target");
+    if (std::find(rots.begin(), rots.end(), e->targetRotation) == rots.end()) rots.push_back(e->targetRotation);
+  }
+  for (int c = 0; c < N; ++c) need(a.projection[c] != nullptr, "a camera without terms");
+  for (int j = 0; j + 1 < N; ++j) need(a.baseRotation[j] != nullptr, "a baseline no term reads");
+  // frames in the order of their rotation DVs' columns; every active DV must be one the terms read
+  std::vector<DesignVariable*> act;
+  for (DesignVariable* dv : dvs)
+    if (dv && dv->isActive()) act.push_back(dv);
+  std::sort(rots.begin(), rots.end(),
+            [](const DesignVariable* x, const DesignVariable* y) { return x->columnBase < y->columnBase; });
+  const int F = (int)rots.size();
+  std::vector<int> frame_of_rot;  // by rots index
+  a.frameRotation = rots;
+  a.frameTranslation.assign(F, nullptr);
+  for (const ReprojectionErrorTerm* e : errors) {
+    const int f = (int)(std::lower_bound(rots.begin(), rots.end(), e->targetRotation,
+                                         [](const DesignVariable* x, const DesignVariable* y) {
+                                           return x->columnBase < y->columnBase;
+                                         }) - rots.begin());
+    need(!a.frameTranslation[f] || a.frameTranslation[f] == e->targetTranslation, "inconsistent target pose");
+    a.frameTranslation[f] = e->targetTranslation;
+  }
+  // canonical columns -> caller columns
+  CalibrationProblem& p = a.problem;
+  p.n_frames = F;
+  p.target = target;
+  std::vector<const DesignVariable*> order;  // canonical DV sequence
+  for (int c = 0; c < N; ++c) {
+    int na = 0, nb = 0;
+    dv_split(a.projection[c]->cameraModel, &na, &nb);
+    need((int)a.projection[c]->value.size() == na, "projection DV size does not match the camera model");
+    need(nb == 0 ? a.distortion[c] == nullptr : (a.distortion[c] && (int)a.distortion[c]->value.size() == nb),
+         "distortion DV does not match the camera model");
+    p.cam_model.push_back(a.projection[c]->cameraModel);
+    order.push_back(a.projection[c]);
+    if (a.distortion[c]) order.push_back(a.distortion[c]);
+  }
+  for (int j = 0; j + 1 < N; ++j) {
+    order.push_back(a.baseRotation[j]);
+    order.push_back(a.baseTranslation[j]);
+  }
+  for (int f = 0; f < F; ++f) {
+    order.push_back(a.frameRotation[f]);
+    order.push_back(a.frameTranslation[f]);
+  }
+  size_t ncols_caller = 0;
+  for (const DesignVariable* dv : act) ncols_caller += dv->minimalDimensions();
+  for (const DesignVariable* dv : order) {
+    need(dv->isActive() && dv->columnBase >= 0, "a design variable the terms read is inactive or has no column base");
+    for (int k = 0; k < dv->minimalDimensions(); ++k) a.perm.push_back(dv->columnBase + k);
+  }
+  need(a.perm.size() == ncols_caller, "active design variables that no term reads (the device solves [intrinsics | "
+                                      "baselines | target poses] only)");
+  {
+    std::vector<char> seen(ncols_caller, 0);
+    for (int q : a.perm) {
+      need(q >= 0 && (size_t)q < ncols_caller && !seen[q], "overlapping column bases");
+      seen[q] = 1;
+    }
+  }
+  // views: the terms of (frame, camera) in their given order, views sorted by frame then camera
+  std::vector<std::vector<std::vector<const ReprojectionErrorTerm*>>> vt(F, std::vector<std::vector<const ReprojectionErrorTerm*>>(N));
+  for (const ReprojectionErrorTerm* e : errors) {
+    const int f = (int)(std::find(rots.begin(), rots.end(), e->targetRotation) - rots.begin());
+    vt[f][e->camera].push_back(e);
+  }
+  p.view_offset.push_back(0);
+  for (int f = 0; f < F; ++f)
+    for (int c = 0; c < N; ++c) {
+      if (vt[f][c].empty()) continue;
+      for (const ReprojectionErrorTerm* e : vt[f][c]) {
+        p.corner_id.push_back((uint16_t)e->cornerId);
+        p.y.push_back(e->y[0]);
+        p.y.push_back(e->y[1]);
+      }
+      p.view_frame.push_back((uint32_t)f);
+      p.view_cam.push_back((uint8_t)c);
+      p.view_offset.push_back((uint32_t)p.corner_id.size());
+    }
+  // state from the DV values
+  p.state.assign((size_t)N * KB_MAX_INTR + 7 * (size_t)(N - 1) + 7 * (size_t)F, 0.0);
+  for (int c = 0; c < N; ++c) {
+    const std::vector<double>& pv = a.projection[c]->value;
+    std::copy(pv.begin(), pv.end(), p.state.begin() + (size_t)c * KB_MAX_INTR);
+    if (a.distortion[c])
+      std::copy(a.distortion[c]->value.begin(), a.distortion[c]->value.end(),
+                p.state.begin() + (size_t)c * KB_MAX_INTR + pv.size());
+  }
+  auto put_pose = [&](size_t o, const DesignVariable* r, const DesignVariable* t) {
+    need(r->value.size() == 4 && t->value.size() == 3, "pose DV values must be a quaternion and a point");
+    std::copy(r->value.begin(), r->value.end(), p.state.begin() + o);
+    std::copy(t->value.begin(), t->value.end(), p.state.begin() + o + 4);
+  };
+  const size_t ob = (size_t)N * KB_MAX_INTR, of = ob + 7 * (size_t)(N - 1);
+  for (int j = 0; j + 1 < N; ++j) put_pose(ob + 7 * j, a.baseRotation[j], a.baseTranslation[j]);
+  for (int f = 0; f < F; ++f) put_pose(of + 7 * f, a.frameRotation[f], a.frameTranslation[f]);
+  return a;
+}
+
+void pullDesignVariables(const TermAssembly& a, const std::vector<double>& state) {
+  const size_t N = a.projection.size(), F = a.frameRotation.size();
+  if (state.size() != N * KB_MAX_INTR + 7 * (N - 1) + 7 * F)
+    throw LinearSystemSolver::Exception("pullDesignVariables: state size mismatch");
+  for (size_t c = 0; c < N; ++c) {
+    std::vector<double>& pv = a.projection[c]->value;
+    std::copy(state.begin() + c * KB_MAX_INTR, state.begin() + c * KB_MAX_INTR + pv.size(), pv.begin());
+    if (a.distortion[c]) {
+      std::vector<double>& dv = a.distortion[c]->value;
+      const size_t o = c * KB_MAX_INTR + pv.size();
+      std::copy(state.begin() + o, state.begin() + o + dv.size(), dv.begin());
+    }
+  }
+  auto get_pose = [&](size_t o, DesignVariable* r, DesignVariable* t) {
+    std::copy(state.begin() + o, state.begin() + o + 4, r->value.begin());
+    std::copy(state.begin() + o + 4, state.begin() + o + 7, t->value.begin());
+  };
+  const size_t ob = N * KB_MAX_INTR, of = ob + 7 * (N - 1);
+  for (size_t j = 0; j + 1 < N; ++j) get_pose(ob + 7 * j, a.baseRotation[j], a.baseTranslation[j]);
+  for (size_t f = 0; f < F; ++f) get_pose(of + 7 * f, a.frameRotation[f], a.frameTranslation[f]);
+}
+
+TermLinearSystemSolver::TermLinearSystemSolver(std::shared_ptr<ProblemLinearSystemSolver> inner,
+                                               std::vector<double> target)
+    : _inner(std::move(inner)), _target(std::move(target)) {
+  if (!_inner) throw Exception("TermLinearSystemSolver: null inner solver");
+}
+
+void TermLinearSystemSolver::initMatrixStructure(const std::vector<DesignVariable*>& dvs,
+                                                 const std::vector<ReprojectionErrorTerm*>& errors,
+                                                 bool useDiagonalConditioner) {
+  _a = assembleTerms(dvs, errors, _target);
+  _inner->initMatrixStructure(_a.problem, useDiagonalConditioner);
+  _JRows = _inner->JRows();
+  _JCols = _inner->JCols();
+  if (_JCols != _a.perm.size()) throw Exception("initMatrixStructure: column count mismatch");
+  _rhs.assign(_JCols, 0.0);
+  _diagonalConditioner.assign(_JCols, 0.0);
+}
+
+double TermLinearSystemSolver::evaluateError(size_t nThreads, bool useMEstimator) {
+  return _inner->evaluateError(nThreads, useMEstimator);
+}
+
+void TermLinearSystemSolver::buildSystem(size_t nThreads, bool useMEstimator) {
+  _inner->buildSystem(nThreads, useMEstimator);
+}
+
+void TermLinearSystemSolver::setConditioner(const std::vector<double>& diag) {
+  LinearSystemSolver::setConditioner(diag);
+  std::vector<double> dc(_JCols);
+  for (size_t k = 0; k < _JCols; ++k) dc[k] = diag[_a.perm[k]];
+  _inner->setConditioner(dc);
+}
+
+void TermLinearSystemSolver::setConstantConditioner(double diag) {
+  LinearSystemSolver::setConstantConditioner(diag);
+  _inner->setConstantConditioner(diag);
+}
+
+bool TermLinearSystemSolver::solveSystem(std::vector<double>& outDx) {
+  std::vector<double> dc;
+  if (!_inner->solveSystem(dc)) return false;
+  outDx.assign(_JCols, 0.0);
+  for (size_t k = 0; k < _JCols; ++k) outDx[_a.perm[k]] = dc[k];
+  return true;
+}
+
+const std::vector<double>& TermLinearSystemSolver::rhs() const {
+  const std::vector<double>& rc = _inner->rhs();
+  _rhs_caller.assign(_JCols, 0.0);
+  for (size_t k = 0; k < _JCols && k < rc.size(); ++k) _rhs_caller[_a.perm[k]] = rc[k];
+  return _rhs_caller;
+}
+
+double TermLinearSystemSolver::applyStateUpdate(const std::vector<double>& dx) {
+  if (dx.size() != _JCols) throw Exception("applyStateUpdate: dx has the wrong size");
+  std::vector<double> dc(_JCols);
+  for (size_t k = 0; k < _JCols; ++k) dc[k] = dx[_a.perm[k]];
+  return _inner->applyStateUpdate(dc);
+}
+
+void TermLinearSystemSolver::pullDesignVariables() const { backend::pullDesignVariables(_a, _inner->state()); }
+
 // ---------------------------------------------------------------- GpuLinearSystemSolver
 GpuLinearSystemSolver::GpuLinearSystemSolver(const GpuOptions& o) : _opt(o) {}
 
@@ -94,10 +361,13 @@ void GpuLinearSystemSolver::setConstantConditioner(double diag) {
 
 void GpuLinearSystemSolver::setConditioner(const std::vector<double>& diag) {
   LinearSystemSolver::setConditioner(diag);
-  // the device path conditions with one value (the LM policies only ever set a constant, :86-88)
-  for (double v : diag)
-    if (v != diag.front()) throw Exception("setConditioner: only constant conditioners are supported on the device");
-  setConstantConditioner(diag.empty() ? 0.0 : diag.front());
+  bool constant = true;
+  for (double v : diag) constant = constant && v == diag.front();
+  if (constant) {  // the device's constant path (what the LM policies set, :86-88)
+    setConstantConditioner(diag.empty() ? 0.0 : diag.front());
+    return;
+  }
+  if (_h) check(kb_set_conditioner(static_cast<kb_handle*>(_h), diag.data()), "kb_set_conditioner");
 }
 
 bool GpuLinearSystemSolver::solveSystem(std::vector<double>& outDx) {

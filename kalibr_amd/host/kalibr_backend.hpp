@@ -90,6 +90,104 @@ class LinearSystemSolver {
   size_t _JRows = 0, _JCols = 0;
 };
 
+/// A LinearSystemSolver that takes its terms as a packed CalibrationProblem in the canonical column order
+/// [intrinsics | baselines | frames] (the GPU solver; the tests' oracle-backed solver).
+class ProblemLinearSystemSolver : public LinearSystemSolver {
+ public:
+  virtual void initMatrixStructure(const CalibrationProblem& problem, bool useDiagonalConditioner) = 0;
+  /// flat design-variable values (include/kalibr_hip.h layout)
+  virtual std::vector<double> state() const = 0;
+};
+
+// ---------------------------------------------------------------- design variables and error terms
+/// aslam_backend::DesignVariable (DesignVariable.hpp) reduced to what the batch problem's terms read: the kind,
+/// minimal dimension and activity, the block index / column base Optimizer2::initialize assigns
+/// (Optimizer2.cpp:110-124), and the value.  Kinds: the camera's projection and distortion DVs
+/// (CameraDesignVariable: e.g. 4 | 4 for pinhole-radtan, 6 | none for EUCM), RotationQuaternion (value: JPL
+/// quaternion [x y z w], minimal dimension 3), EuclideanPoint (3), HomogeneousPoint (the target landmarks,
+/// inactive in the batch problems, CalibrationTools.hpp:470-473).
+struct DesignVariable {
+  enum class Kind { Projection, Distortion, RotationQuaternion, EuclideanPoint, HomogeneousPoint };
+  Kind kind = Kind::EuclideanPoint;
+  int camera = -1;       // Projection / Distortion: the camera's index in the rig
+  int cameraModel = -1;  // Projection: its kb_camera_model
+  std::vector<double> value;
+  bool active = true;
+  int blockIndex = -1, columnBase = -1;
+  bool isActive() const { return active; }
+  int minimalDimensions() const;
+};
+
+/// One ReprojectionError term (ReprojectionError.hpp(impl):49-77) of the rig problem: the corner `cornerId` of the
+/// target seen at `y` by camera `camera` through T_cam_w = B_{camera-1} .. B_0 T^-1, T = (targetRotation,
+/// targetTranslation), B_j = (baselines[2j], baselines[2j + 1]) -- the chain CalibrateMultiCameraRig and
+/// CreateBatchProblem build (CalibrationTools.hpp:401-410, 497-508); invR = I (corner uncertainty 1).
+struct ReprojectionErrorTerm {
+  int camera = 0;
+  int cornerId = 0;
+  double y[2] = {0.0, 0.0};
+  DesignVariable* targetRotation = nullptr;
+  DesignVariable* targetTranslation = nullptr;
+  std::vector<DesignVariable*> baselines;  // rotation, translation of B_0 .. B_{camera-1}
+  DesignVariable* projection = nullptr;
+  DesignVariable* distortion = nullptr;  // null for models without a distortion DV (EUCM, omni, double sphere)
+  int dimension() const { return 2; }
+};
+
+/// Optimizer2::initialize (Optimizer2.cpp:110-124): the active DVs in the given order get block index i and
+/// column base = the sum of the preceding minimal dimensions.  Returns the active list.
+std::vector<DesignVariable*> assignColumnBases(const std::vector<DesignVariable*>& dvs);
+
+/// The terms packed for a ProblemLinearSystemSolver: the canonical problem (frames in the order of their rotation
+/// DVs' column bases, views sorted by frame, terms of a view in the given order) and perm[k] = the caller's column
+/// of canonical column k.
+struct TermAssembly {
+  CalibrationProblem problem;
+  std::vector<int> perm;
+  std::vector<DesignVariable*> projection, distortion;  // per camera (distortion may be null)
+  std::vector<DesignVariable*> baseRotation, baseTranslation;  // per baseline
+  std::vector<DesignVariable*> frameRotation, frameTranslation;  // per frame, canonical order
+};
+
+/// Walks the terms (which must form the rig structure above) and packs them; `target` = [n_target][3] corners.
+/// Throws LinearSystemSolver::Exception on anything the device path cannot represent (an active DV no term
+/// reads, a chain that is not B_{c-1}..B_0 T^-1, missing column bases).
+TermAssembly assembleTerms(const std::vector<DesignVariable*>& dvs, const std::vector<ReprojectionErrorTerm*>& errors,
+                           const std::vector<double>& target);
+
+/// Design-variable values from a flat state (include/kalibr_hip.h layout) of the assembled problem.
+void pullDesignVariables(const TermAssembly& a, const std::vector<double>& state);
+
+/// LinearSystemSolver::initMatrixStructure(dvs, errors, useDiagonalConditioner) (LinearSystemSolver.hpp:28, 73)
+/// in front of a ProblemLinearSystemSolver: the terms are packed once, and rhs, dx and the conditioner are
+/// permuted between the caller's column order (the DVs' column bases) and the canonical one.
+class TermLinearSystemSolver : public LinearSystemSolver {
+ public:
+  TermLinearSystemSolver(std::shared_ptr<ProblemLinearSystemSolver> inner, std::vector<double> target);
+  void initMatrixStructure(const std::vector<DesignVariable*>& dvs, const std::vector<ReprojectionErrorTerm*>& errors,
+                           bool useDiagonalConditioner);
+  double evaluateError(size_t nThreads, bool useMEstimator) override;
+  void buildSystem(size_t nThreads, bool useMEstimator) override;
+  void setConditioner(const std::vector<double>& diag) override;
+  void setConstantConditioner(double diag) override;
+  bool solveSystem(std::vector<double>& outDx) override;
+  std::string name() const override { return _inner->name(); }
+  const std::vector<double>& rhs() const override;
+  double rhsJtJrhs() override { return _inner->rhsJtJrhs(); }  // invariant under the column permutation
+  double applyStateUpdate(const std::vector<double>& dx) override;
+  void revertLastStateUpdate() override { _inner->revertLastStateUpdate(); }
+  /// the solver's state into the design variables' values
+  void pullDesignVariables() const;
+  const TermAssembly& assembly() const { return _a; }
+  ProblemLinearSystemSolver& inner() { return *_inner; }
+
+ private:
+  std::shared_ptr<ProblemLinearSystemSolver> _inner;
+  std::vector<double> _target;
+  TermAssembly _a;
+  mutable std::vector<double> _rhs_caller;
+};
+
 // ---------------------------------------------------------------- GPU solver over the C-ABI
 /// linearSolver: "schur" (frame-block Schur + camera-block LDL^T, the exact CHOLMOD replacement, default) or
 /// "pcg" (sparse_block_matrix LinearSolverPCG: block-Jacobi PCG, linear_solver_pcg.hpp:58-130, with its
@@ -105,7 +203,7 @@ struct GpuOptions {
 /// LinearSystemSolver whose build / solve / update / cost run on one MI355X (kalibr_hip.h).  The
 /// per-call methods mirror the reference solver one call at a time; optimizeOnDevice() runs the whole
 /// Optimizer2 loop device-resident (one captured graph per pass).
-class GpuLinearSystemSolver : public LinearSystemSolver {
+class GpuLinearSystemSolver : public ProblemLinearSystemSolver {
  public:
   explicit GpuLinearSystemSolver(const GpuOptions& o = GpuOptions());
   ~GpuLinearSystemSolver() override;
@@ -113,7 +211,7 @@ class GpuLinearSystemSolver : public LinearSystemSolver {
   GpuLinearSystemSolver& operator=(const GpuLinearSystemSolver&) = delete;
 
   /// LinearSystemSolver::initMatrixStructure (LinearSystemSolver.cpp:117-138): uploads the terms and state
-  void initMatrixStructure(const CalibrationProblem& problem, bool useDiagonalConditioner);
+  void initMatrixStructure(const CalibrationProblem& problem, bool useDiagonalConditioner) override;
 
   double evaluateError(size_t nThreads, bool useMEstimator) override;
   void buildSystem(size_t nThreads, bool useMEstimator) override;
@@ -128,7 +226,7 @@ class GpuLinearSystemSolver : public LinearSystemSolver {
   double applyStateUpdate(const std::vector<double>& dx) override;
   void revertLastStateUpdate() override;
 
-  std::vector<double> state() const;
+  std::vector<double> state() const override;
   void setState(const std::vector<double>& s);
   size_t cameraCols() const { return _C; }
   void* handle() const { return _h; }

@@ -11,9 +11,16 @@
 //                                                 (kbo_optimize with the marginal solve) + the addBatch rule
 //   test_host incr-gpu <problem.bin> <delta> <maxIt> : IncrementalEstimator over GpuMarginalLinearSolver vs
 //                                                 over the oracle-backed marginal solver
+//   test_host terms-cpu|terms-gpu <problem.bin> <lm|gn> <maxIt> : the problem re-expressed as design variables +
+//                                                 ReprojectionError terms in CreateBatchProblem order, the DVs in
+//                                                 three column orders (insertion, groups reordered as the
+//                                                 IncrementalEstimator does, a seeded shuffle);
+//                                                 TermLinearSystemSolver over the oracle (cpu) or the GPU solver:
+//                                                 packing, dx / rhs permutation and Optimizer2 end to end
 //   test_host io <problem.bin> <outdir> 0       : observation records -> buildRigProblem (must rebuild the packed
 //                                                 problem), targetPoseGuess per frame, exportCalibration YAML
 // Prints one JSON line.  The oracle is test infrastructure only (oracle/kb_oracle.h).
+#include <algorithm>
 #include <cfloat>
 #include <cmath>
 #include <cstdio>
@@ -25,6 +32,7 @@
 
 #include "calibration_io.hpp"
 #include "kalibr_backend.hpp"
+#include "kalibr_hip.h"
 #include "kb_oracle.h"
 
 using namespace kalibr_amd::backend;
@@ -375,6 +383,277 @@ static double maxdiff(const std::vector<double>& a, const std::vector<double>& b
   return m;
 }
 
+// ProblemLinearSystemSolver over the oracle (for TermLinearSystemSolver on the CPU)
+class OracleProblemSolver : public ProblemLinearSystemSolver {
+ public:
+  void initMatrixStructure(const CalibrationProblem& p, bool) override {
+    _s = std::make_unique<OracleLinearSystemSolver>(p, 4);
+    _JRows = _s->JRows();
+    _JCols = _s->JCols();
+  }
+  std::vector<double> state() const override { return _s->state(); }
+  double evaluateError(size_t n, bool m) override { return _s->evaluateError(n, m); }
+  void buildSystem(size_t n, bool m) override { _s->buildSystem(n, m); }
+  void setConstantConditioner(double d) override { _s->setConstantConditioner(d); }
+  void setConditioner(const std::vector<double>& d) override {
+    for (double v : d)
+      if (v != d.front()) throw Exception("oracle: constant conditioners only");
+    _s->setConstantConditioner(d.front());
+  }
+  bool solveSystem(std::vector<double>& dx) override { return _s->solveSystem(dx); }
+  std::string name() const override { return _s->name(); }
+  const std::vector<double>& rhs() const override { return _s->rhs(); }
+  double rhsJtJrhs() override { return 0.0; }
+  double applyStateUpdate(const std::vector<double>& dx) override { return _s->applyStateUpdate(dx); }
+  void revertLastStateUpdate() override { _s->revertLastStateUpdate(); }
+
+ private:
+  std::unique_ptr<OracleLinearSystemSolver> _s;
+};
+
+// the packed problem as design variables and terms (CreateBatchProblem / CalibrateMultiCameraRig shape)
+struct TermProblem {
+  std::vector<std::unique_ptr<DesignVariable>> store;
+  std::vector<DesignVariable*> proj, dist, brot, btrans, frot, ftrans, landmarks;
+  std::vector<std::unique_ptr<ReprojectionErrorTerm>> terms;
+  std::vector<ReprojectionErrorTerm*> errors;
+  DesignVariable* make(DesignVariable::Kind k, std::vector<double> v, int cam = -1, int model = -1) {
+    store.push_back(std::make_unique<DesignVariable>());
+    DesignVariable* d = store.back().get();
+    d->kind = k;
+    d->value = std::move(v);
+    d->camera = cam;
+    d->cameraModel = model;
+    return d;
+  }
+};
+
+static void dv_sizes(int model, int* a, int* b) {
+  switch (model) {
+    case KB_OMNI_RADTAN: *a = 5, *b = 4; break;
+    case KB_EUCM: *a = 6, *b = 0; break;
+    case KB_OMNI: *a = 5, *b = 0; break;
+    case KB_DS: *a = 6, *b = 0; break;
+    case KB_PINHOLE_FOV: *a = 4, *b = 1; break;
+    default: *a = 4, *b = 4; break;
+  }
+}
+
+static TermProblem to_terms(const CalibrationProblem& p) {
+  using K = DesignVariable::Kind;
+  TermProblem t;
+  const int N = p.n_cams(), F = p.n_frames;
+  const size_t ob = (size_t)N * KB_MAX_INTR, of = ob + 7 * (size_t)(N - 1);
+  auto sl = [&](size_t o, size_t n) { return std::vector<double>(p.state.begin() + o, p.state.begin() + o + n); };
+  for (int c = 0; c < N; ++c) {
+    int a = 0, b = 0;
+    dv_sizes(p.cam_model[c], &a, &b);
+    t.proj.push_back(t.make(K::Projection, sl((size_t)c * KB_MAX_INTR, a), c, p.cam_model[c]));
+    t.dist.push_back(b ? t.make(K::Distortion, sl((size_t)c * KB_MAX_INTR + a, b), c) : nullptr);
+  }
+  for (int j = 0; j + 1 < N; ++j) {
+    t.brot.push_back(t.make(K::RotationQuaternion, sl(ob + 7 * j, 4)));
+    t.btrans.push_back(t.make(K::EuclideanPoint, sl(ob + 7 * j + 4, 3)));
+  }
+  for (int k = 0; k < p.n_target(); ++k) {
+    t.landmarks.push_back(t.make(K::HomogeneousPoint, {p.target[3 * k], p.target[3 * k + 1], p.target[3 * k + 2], 1.0}));
+    t.landmarks.back()->active = false;  // CalibrationTools.hpp:470-473
+  }
+  for (int f = 0; f < F; ++f) {
+    t.frot.push_back(t.make(K::RotationQuaternion, sl(of + 7 * f, 4)));
+    t.ftrans.push_back(t.make(K::EuclideanPoint, sl(of + 7 * f + 4, 3)));
+  }
+  for (int v = 0; v < p.n_views(); ++v) {  // per synced set, per camera, per corner (CalibrationTools.hpp:493-509)
+    const int f = (int)p.view_frame[v], c = p.view_cam[v];
+    for (uint32_t k = p.view_offset[v]; k < p.view_offset[v + 1]; ++k) {
+      t.terms.push_back(std::make_unique<ReprojectionErrorTerm>());
+      ReprojectionErrorTerm* e = t.terms.back().get();
+      e->camera = c;
+      e->cornerId = p.corner_id[k];
+      e->y[0] = p.y[2 * k];
+      e->y[1] = p.y[2 * k + 1];
+      e->targetRotation = t.frot[f];
+      e->targetTranslation = t.ftrans[f];
+      for (int j = 0; j < c; ++j) {
+        e->baselines.push_back(t.brot[j]);
+        e->baselines.push_back(t.btrans[j]);
+      }
+      e->projection = t.proj[c];
+      e->distortion = t.dist[c];
+      t.errors.push_back(e);
+    }
+  }
+  return t;
+}
+
+// DV orders: 0 = insertion (intrinsics, baselines, target poses: CalibrateMultiCameraRig), 1 = groups reordered as
+// the IncrementalEstimator's problem (target poses, landmarks, then the calibration group last), 2 = seeded shuffle
+static std::vector<DesignVariable*> dv_order(const TermProblem& t, int mode) {
+  std::vector<DesignVariable*> v;
+  auto cams = [&]() {
+    for (size_t c = 0; c < t.proj.size(); ++c) {
+      v.push_back(t.proj[c]);
+      if (t.dist[c]) v.push_back(t.dist[c]);
+    }
+  };
+  auto bases = [&]() {
+    for (size_t j = 0; j < t.brot.size(); ++j) {
+      v.push_back(t.brot[j]);
+      v.push_back(t.btrans[j]);
+    }
+  };
+  auto frames = [&]() {
+    for (size_t f = 0; f < t.frot.size(); ++f) {
+      v.push_back(t.frot[f]);
+      v.push_back(t.ftrans[f]);
+    }
+  };
+  if (mode == 0) {
+    cams();
+    bases();
+    frames();
+  } else {
+    frames();
+    for (DesignVariable* l : t.landmarks) v.push_back(l);
+    bases();
+    cams();
+  }
+  if (mode == 2) {  // Fisher-Yates with a fixed LCG
+    uint64_t r = 0x9e3779b97f4a7c15ull;
+    for (size_t i = v.size(); i > 1; --i) {
+      r = r * 6364136223846793005ull + 1442695040888963407ull;
+      std::swap(v[i - 1], v[(size_t)(r >> 33) % i]);
+    }
+  }
+  return v;
+}
+
+// terms: packing round trip, dx / rhs permutation against the canonical solver, Optimizer2 through the terms
+static int run_terms(const CalibrationProblem& p, bool gpu, const std::string& pol, int maxIt) {
+  double pack_diff = 0.0, dx_diff = 0.0, rhs_diff = 0.0, state_diff = 0.0, cost_diff = 0.0;
+  double shuf_dx = 0.0, shuf_rhs = 0.0, shuf_state = 0.0, shuf_cost = 0.0;  // mode 2: frames reordered
+  int frames_reordered = 0, it_terms[3] = {0, 0, 0}, it_ref = 0;
+  auto make_inner = [&]() -> std::shared_ptr<ProblemLinearSystemSolver> {
+    if (gpu) return std::make_shared<GpuLinearSystemSolver>();
+    return std::make_shared<OracleProblemSolver>();
+  };
+  // canonical reference: the packed problem straight into the inner solver
+  auto ref = make_inner();
+  ref->initMatrixStructure(p, false);
+  ref->buildSystem(4, true);
+  ref->setConstantConditioner(10.0);
+  std::vector<double> dx_ref;
+  if (!ref->solveSystem(dx_ref)) throw std::runtime_error("reference solve failed");
+  const std::vector<double> rhs_ref = ref->rhs();
+  const double J_ref = ref->evaluateError(4, true);
+  Optimizer2Options opt;
+  opt.maxIterations = maxIt;
+  opt.convergenceDeltaX = 1e-3;
+  opt.convergenceDeltaJ = 1.0;
+  opt.nThreads = 4;
+  auto refo = make_inner();
+  refo->initMatrixStructure(p, false);
+  opt.linearSystemSolver = refo;
+  opt.trustRegionPolicy = make_policy(pol);
+  it_ref = Optimizer2(opt).optimize().iterations;
+  const std::vector<double> st_ref = refo->state();
+  for (int mode = 0; mode < 3; ++mode) {
+    if (mode == 2) {  // a frame permutation changes the summation order: the shuffled run has its own maxima
+      std::swap(dx_diff, shuf_dx);
+      std::swap(rhs_diff, shuf_rhs);
+      std::swap(state_diff, shuf_state);
+      std::swap(cost_diff, shuf_cost);
+    }
+    TermProblem t = to_terms(p);
+    const std::vector<DesignVariable*> dvs = assignColumnBases(dv_order(t, mode));
+    auto ts = std::make_shared<TermLinearSystemSolver>(make_inner(), p.target);
+    ts->initMatrixStructure(dvs, t.errors, false);
+    const TermAssembly& a = ts->assembly();
+    // frames come out in column-base order: map them back to the problem's frames
+    std::vector<int> fmap(p.n_frames);
+    for (int f = 0; f < p.n_frames; ++f) {
+      fmap[f] = (int)(std::find(t.frot.begin(), t.frot.end(), a.frameRotation[f]) - t.frot.begin());
+      frames_reordered += fmap[f] != f;
+    }
+    if (mode < 2) {  // frames keep their order: the packed arrays are the problem's
+      pack_diff = std::max(pack_diff, maxdiff(a.problem.state, p.state, 0, p.state.size()));
+      pack_diff = std::max(pack_diff, a.problem.corner_id == p.corner_id && a.problem.view_frame == p.view_frame &&
+                                              a.problem.view_cam == p.view_cam && a.problem.view_offset == p.view_offset &&
+                                              a.problem.y == p.y
+                                          ? 0.0
+                                          : 1.0);
+    }
+    cost_diff = std::max(cost_diff, std::fabs(ts->evaluateError(4, true) - J_ref) / J_ref);
+    ts->buildSystem(4, true);
+    std::vector<double> cond(ts->JCols(), 10.0);
+    ts->setConditioner(cond);
+    std::vector<double> dx;
+    if (!ts->solveSystem(dx)) throw std::runtime_error("term solve failed");
+    const std::vector<double>& rhs = ts->rhs();
+    // every DV's block of the caller-order dx equals the canonical dx of the same DV
+    const size_t C = dx_ref.size() - 6 * (size_t)p.n_frames;
+    auto cmp_block = [&](const DesignVariable* dv, size_t canon) {
+      for (int k = 0; k < dv->minimalDimensions(); ++k) {
+        dx_diff = std::max(dx_diff, std::fabs(dx[dv->columnBase + k] - dx_ref[canon + k]) /
+                                        std::max(1e-300, std::fabs(dx_ref[canon + k]) + 1e-12));
+        rhs_diff = std::max(rhs_diff, std::fabs(rhs[dv->columnBase + k] - rhs_ref[canon + k]) /
+                                          std::max(1.0, std::fabs(rhs_ref[canon + k])));
+      }
+    };
+    size_t o = 0;
+    for (size_t c = 0; c < t.proj.size(); ++c) {
+      cmp_block(t.proj[c], o);
+      o += t.proj[c]->minimalDimensions();
+      if (t.dist[c]) {
+        cmp_block(t.dist[c], o);
+        o += t.dist[c]->minimalDimensions();
+      }
+    }
+    for (size_t j = 0; j < t.brot.size(); ++j, o += 6) {
+      cmp_block(t.brot[j], o);
+      cmp_block(t.btrans[j], o + 3);
+    }
+    for (int f = 0; f < p.n_frames; ++f) {
+      cmp_block(t.frot[f], C + 6 * (size_t)f);
+      cmp_block(t.ftrans[f], C + 6 * (size_t)f + 3);
+    }
+    // Optimizer2 through the terms; the DV values pulled back must be the canonical run's state
+    auto ts2 = std::make_shared<TermLinearSystemSolver>(make_inner(), p.target);
+    ts2->initMatrixStructure(dvs, t.errors, false);
+    opt.linearSystemSolver = ts2;
+    opt.trustRegionPolicy = make_policy(pol);
+    it_terms[mode] = Optimizer2(opt).optimize().iterations;
+    ts2->pullDesignVariables();
+    std::vector<double> st(p.state.size(), 0.0);
+    const int N = p.n_cams();
+    const size_t ob = (size_t)N * KB_MAX_INTR, of = ob + 7 * (size_t)(N - 1);
+    for (int c = 0; c < N; ++c) {
+      std::copy(t.proj[c]->value.begin(), t.proj[c]->value.end(), st.begin() + (size_t)c * KB_MAX_INTR);
+      if (t.dist[c])
+        std::copy(t.dist[c]->value.begin(), t.dist[c]->value.end(),
+                  st.begin() + (size_t)c * KB_MAX_INTR + t.proj[c]->value.size());
+    }
+    auto putp = [&](size_t q, const DesignVariable* r, const DesignVariable* tr) {
+      std::copy(r->value.begin(), r->value.end(), st.begin() + q);
+      std::copy(tr->value.begin(), tr->value.end(), st.begin() + q + 4);
+    };
+    for (int j = 0; j + 1 < N; ++j) putp(ob + 7 * j, t.brot[j], t.btrans[j]);
+    for (int f = 0; f < p.n_frames; ++f) putp(of + 7 * f, t.frot[f], t.ftrans[f]);
+    state_diff = std::max(state_diff, maxdiff(st, st_ref, 0, st.size()));
+  }
+  std::swap(dx_diff, shuf_dx);
+  std::swap(rhs_diff, shuf_rhs);
+  std::swap(state_diff, shuf_state);
+  std::swap(cost_diff, shuf_cost);
+  std::printf(
+      "{\"pack_diff\": %.3e, \"cost_rel\": %.3e, \"dx_rel\": %.3e, \"rhs_rel\": %.3e, \"state_diff\": %.3e, "
+      "\"shuf_cost_rel\": %.3e, \"shuf_dx_rel\": %.3e, \"shuf_rhs_rel\": %.3e, \"shuf_state_diff\": %.3e, "
+      "\"frames_reordered\": %d, \"iterations\": [%d, %d, %d], \"ref_iterations\": %d}\n",
+      pack_diff, cost_diff, dx_diff, rhs_diff, state_diff, shuf_cost, shuf_dx, shuf_rhs, shuf_state, frames_reordered,
+      it_terms[0], it_terms[1], it_terms[2], it_ref);
+  return 0;
+}
+
 // io: per-frame synchronized sets of GridObservation records re-created from the packed problem, each observation
 // carrying its camera's T_t_c of the problem's state (T_t_ci = T_f (B_{i-1}..B_0)^-1); buildRigProblem must give
 // back the same term arrays; the target pose guesses and the exported YAML are checked by the Python side.
@@ -449,6 +728,7 @@ int main(int argc, char** argv) {
   try {
     CalibrationProblem p = load(argv[2]);
     if (mode == "io") return run_io(p, argv[3]);
+    if (mode == "terms-cpu" || mode == "terms-gpu") return run_terms(p, mode == "terms-gpu", pol, maxIt);
     if (mode == "incr-cpu" || mode == "incr-gpu") {
       const double delta = std::atof(argv[3]);
       LinearSolverOptions lo;

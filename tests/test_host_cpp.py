@@ -115,3 +115,35 @@ def test_host_gpu_pcg_loop(driver, tmp_path, cfg, frames, policy):
     assert r["tight_iterations"] == r["ref_iterations"] and r["tight_failed"] == r["ref_failed"], r
     assert r["tight_vs_ref_cam"] < 1e-6 and r["tight_vs_ref_frame"] < 1e-6, r
     assert r["default_lin_fail"] == 0 and r["default_J"] <= 1.05 * r["ref_J"], r
+
+
+@pytest.mark.parametrize("cfg,frames,policy", [(2, 10, "lm"), (2, 10, "gn"), (3, 6, "lm"), (4, 5, "lm")])
+def test_term_solver_over_oracle(driver, tmp_path, cfg, frames, policy):
+    """initMatrixStructure(dvs, errors, useDiag) (LinearSystemSolver.hpp:28,73): the problem as DesignVariables and
+    ReprojectionError terms in CreateBatchProblem order (CalibrationTools.hpp:460-521), DVs in insertion order,
+    in the IncrementalEstimator's group order (target poses and landmarks first, the calibration group last,
+    IncrementalEstimator.cpp:550-565) and shuffled.  Packing gives back the problem; every DV's block of dx / rhs in
+    the caller's column order equals the canonical solve's; Optimizer2 through the terms ends at the canonical
+    run's state -- bitwise when the frames keep their order (the inner solver sees the same canonical problem),
+    to rounding when the shuffle reorders them (frame blocks summed in another order)."""
+    p = synth.make_config(cfg, n_frames=frames, p_view=0.8)
+    r = run(driver, tmp_path, "terms-cpu", p, policy, 20)
+    assert r["pack_diff"] == 0.0 and r["cost_rel"] == 0.0, r
+    assert r["dx_rel"] == 0.0 and r["rhs_rel"] == 0.0, r
+    assert r["state_diff"] == 0.0, r
+    assert r["shuf_cost_rel"] < 1e-12 and r["shuf_rhs_rel"] < 1e-10 and r["shuf_dx_rel"] < 1e-7, r
+    assert r["shuf_state_diff"] < 1e-8, r
+    assert r["iterations"] == [r["ref_iterations"]] * 3, r
+    assert r["frames_reordered"] > 0, r  # the shuffle exercised the frame permutation
+
+
+@pytest.mark.gpu
+def test_term_solver_over_gpu(driver, tmp_path):
+    p = synth.make_config(4, n_frames=12, p_view=0.8)
+    r = run(driver, tmp_path, "terms-gpu", p, "lm", 20)
+    assert r["pack_diff"] == 0.0 and r["cost_rel"] == 0.0, r
+    assert r["dx_rel"] == 0.0 and r["rhs_rel"] == 0.0, r
+    assert r["state_diff"] == 0.0, r
+    assert r["shuf_cost_rel"] < 1e-12 and r["shuf_rhs_rel"] < 1e-10 and r["shuf_dx_rel"] < 1e-7, r
+    assert r["shuf_state_diff"] < 1e-8, r
+    assert r["iterations"] == [r["ref_iterations"]] * 3, r
