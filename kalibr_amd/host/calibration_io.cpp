@@ -351,5 +351,397 @@ std::vector<std::string> exportCalibration(const std::string& dir, const std::ve
   return out;
 }
 
+// ---------------------------------------------------------------- initialisers (PinholeProjection.hpp(impl))
+namespace {
+// modified least squares circle fit (PinholeProjection.hpp(impl):642-691)
+void fit_circle(const std::vector<std::array<double, 2>>& pts, double& cx, double& cy, double& radius) {
+  double sx = 0, sy = 0, sxx = 0, sxy = 0, syy = 0, sxxx = 0, sxxy = 0, sxyy = 0, syyy = 0;
+  const int n = (int)pts.size();
+  for (const auto& p : pts) {
+    const double x = p[0], y = p[1];
+    sx += x;
+    sy += y;
+    sxx += x * x;
+    sxy += x * y;
+    syy += y * y;
+    sxxx += x * x * x;
+    sxxy += x * x * y;
+    sxyy += x * y * y;
+    syyy += y * y * y;
+  }
+  const double A = n * sxx - sx * sx, B = n * sxy - sx * sy, C = n * syy - sy * sy;
+  const double D = 0.5 * (n * sxyy - sx * syy + n * sxxx - sx * sxx);
+  const double E = 0.5 * (n * sxxy - sy * sxx + n * syyy - sy * syy);
+  cx = (D * C - B * E) / (A * C - B * B);
+  cy = (A * E - B * D) / (A * C - B * B);
+  double sr = 0.0;
+  for (const auto& p : pts) sr += std::hypot(p[0] - cx, p[1] - cy);
+  radius = sr / n;
+}
+
+// intersection points of two circles (:611-640)
+std::vector<std::array<double, 2>> intersect_circles(double x1, double y1, double r1, double x2, double y2, double r2) {
+  std::vector<std::array<double, 2>> out;
+  const double d = std::hypot(x1 - x2, y1 - y2);
+  if (d > r1 + r2 || d < std::fabs(r1 - r2)) return out;
+  const double a = (r1 * r1 - r2 * r2 + d * d) / (2.0 * d), h = std::sqrt(r1 * r1 - a * a);
+  const double x3 = x1 + a * (x2 - x1) / d, y3 = y1 + a * (y2 - y1) / d;
+  if (h < 1e-10) {
+    out.push_back({x3, y3});
+    return out;
+  }
+  out.push_back({x3 + h * (y2 - y1) / d, y3 - h * (x2 - x1) / d});
+  out.push_back({x3 - h * (y2 - y1) / d, y3 + h * (x2 - x1) / d});
+  return out;
+}
+
+double median_of(std::vector<double> v) {  // medianOfVectorElements (:693-703)
+  std::sort(v.begin(), v.end());
+  const size_t n = v.size();
+  return n % 2 == 0 ? (v[n / 2 - 1] + v[n / 2]) / 2 : v[n / 2];
+}
+
+int n_distortion(int32_t m) {
+  switch (m) {
+    case KB_PINHOLE_RADTAN:
+    case KB_PINHOLE_EQUI: return 4;
+    case KB_PINHOLE_FOV: return 1;
+    default: return -1;  // not a PinholeProjection model
+  }
+}
+
+// forward distortion of normalised coordinates (RadialTangential / Equidistant / Fov distort), Jacobian for radtan
+void distort(int32_t m, const double* d, double& x, double& y, double* J) {
+  if (m == KB_PINHOLE_RADTAN) {  // RadialTangentialDistortion.hpp(impl):20-60
+    const double k1 = d[0], k2 = d[1], p1 = d[2], p2 = d[3];
+    const double mx2 = x * x, my2 = y * y, mxy = x * y, rho2 = mx2 + my2, rad = k1 * rho2 + k2 * rho2 * rho2;
+    if (J) {
+      J[0] = 1 + rad + k1 * 2.0 * mx2 + k2 * rho2 * 4 * mx2 + 2.0 * p1 * y + 6 * p2 * x;
+      J[1] = k1 * 2.0 * x * y + k2 * 4 * rho2 * x * y + p1 * 2.0 * x + 2.0 * p2 * y;
+      J[2] = J[1];
+      J[3] = 1 + rad + k1 * 2.0 * my2 + k2 * rho2 * 4 * my2 + 6 * p1 * y + 2.0 * p2 * x;
+    }
+    const double nx = x + x * rad + 2.0 * p1 * mxy + p2 * (rho2 + 2.0 * mx2);
+    const double ny = y + y * rad + 2.0 * p2 * mxy + p1 * (rho2 + 2.0 * my2);
+    x = nx;
+    y = ny;
+    return;
+  }
+  double s = 1.0;
+  const double r = std::hypot(x, y);
+  if (m == KB_PINHOLE_EQUI) {  // EquidistantDistortion.hpp(impl):31-80
+    const double th = std::atan(r), t2 = th * th;
+    const double thd = th * (1.0 + t2 * (d[0] + t2 * (d[1] + t2 * (d[2] + t2 * d[3]))));
+    s = r > 1e-8 ? thd / r : 1.0;
+  } else if (m == KB_PINHOLE_FOV) {  // FovDistortion.hpp(impl):19-60
+    const double w = d[0];
+    if (w * w < 1e-5) s = 1.0;
+    else if (r * r < 1e-5) s = 2.0 * std::tan(0.5 * w) / w;
+    else s = std::atan(2.0 * std::tan(0.5 * w) * r) / (r * w);
+  }
+  x *= s;
+  y *= s;
+}
+
+// 9 x 9 symmetric eigenvector of the smallest eigenvalue (cyclic Jacobi)
+std::array<double, 9> smallest_eigvec9(std::array<double, 81> A) {
+  std::array<double, 81> V{};
+  for (int i = 0; i < 9; ++i) V[i * 9 + i] = 1.0;
+  for (int sweep = 0; sweep < 60; ++sweep) {
+    double off = 0.0;
+    for (int p = 0; p < 9; ++p)
+      for (int q = p + 1; q < 9; ++q) off += A[p * 9 + q] * A[p * 9 + q];
+    if (off < 1e-30) break;
+    for (int p = 0; p < 9; ++p)
+      for (int q = p + 1; q < 9; ++q) {
+        const double apq = A[p * 9 + q];
+        if (std::fabs(apq) < 1e-300) continue;
+        const double th = 0.5 * (A[q * 9 + q] - A[p * 9 + p]) / apq;
+        const double t = (th >= 0 ? 1.0 : -1.0) / (std::fabs(th) + std::sqrt(th * th + 1.0));
+        const double c = 1.0 / std::sqrt(t * t + 1.0), sn = t * c;
+        for (int k = 0; k < 9; ++k) {  // A <- J^T A J
+          const double akp = A[k * 9 + p], akq = A[k * 9 + q];
+          A[k * 9 + p] = c * akp - sn * akq;
+          A[k * 9 + q] = sn * akp + c * akq;
+        }
+        for (int k = 0; k < 9; ++k) {
+          const double apk = A[p * 9 + k], aqk = A[q * 9 + k];
+          A[p * 9 + k] = c * apk - sn * aqk;
+          A[q * 9 + k] = sn * apk + c * aqk;
+        }
+        for (int k = 0; k < 9; ++k) {
+          const double vkp = V[k * 9 + p], vkq = V[k * 9 + q];
+          V[k * 9 + p] = c * vkp - sn * vkq;
+          V[k * 9 + q] = sn * vkp + c * vkq;
+        }
+      }
+  }
+  int m = 0;
+  for (int i = 1; i < 9; ++i)
+    if (A[i * 9 + i] < A[m * 9 + m]) m = i;
+  std::array<double, 9> v{};
+  for (int k = 0; k < 9; ++k) v[k] = V[k * 9 + m];
+  return v;
+}
+
+// rotation vector -> matrix (Rodrigues), row-major
+std::array<double, 9> rodrigues(const double w[3]) {
+  const double th = std::sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+  std::array<double, 9> R{1, 0, 0, 0, 1, 0, 0, 0, 1};
+  if (th < 1e-300) return R;
+  const double k[3] = {w[0] / th, w[1] / th, w[2] / th}, c = std::cos(th), s = std::sin(th), v = 1.0 - c;
+  R = {c + k[0] * k[0] * v,        k[0] * k[1] * v - k[2] * s, k[0] * k[2] * v + k[1] * s,
+       k[1] * k[0] * v + k[2] * s, c + k[1] * k[1] * v,        k[1] * k[2] * v - k[0] * s,
+       k[2] * k[0] * v - k[1] * s, k[2] * k[1] * v + k[0] * s, c + k[2] * k[2] * v};
+  return R;
+}
+
+std::array<double, 9> matmul3(const std::array<double, 9>& A, const std::array<double, 9>& B) {
+  std::array<double, 9> C{};
+  for (int r = 0; r < 3; ++r)
+    for (int c = 0; c < 3; ++c)
+      for (int k = 0; k < 3; ++k) C[r * 3 + c] += A[r * 3 + k] * B[k * 3 + c];
+  return C;
+}
+}  // namespace
+
+bool initializeIntrinsics(const std::vector<GridObservation>& observations, const AprilgridTarget& target,
+                          std::optional<double> fallbackFocalLength, int32_t camModel, std::vector<double>& intr) {
+  if (observations.empty()) throw std::runtime_error("initializeIntrinsics: Need min. one observation");
+  const int nd = n_distortion(camModel);
+  if (nd < 0) throw std::runtime_error("initializeIntrinsics: not a pinhole camera model");
+  const double cu = (observations[0].imCols - 1.0) / 2.0, cv = (observations[0].imRows - 1.0) / 2.0;
+  const size_t R = target.rows(), Cn = target.cols();
+  std::vector<double> guesses;
+  for (const GridObservation& obs : observations) {
+    std::vector<std::array<double, 3>> circ(R);  // centre x, y, radius per corner row
+    bool skip = false;
+    for (size_t r = 0; r < R; ++r) {
+      std::vector<std::array<double, 2>> pts;
+      for (size_t c = 0; c < Cn; ++c) {
+        double p[2];
+        if (obs.imagePoint(r * Cn + c, p)) pts.push_back({p[0], p[1]});
+        else skip = true;  // the view is not complete
+      }
+      if (!pts.empty()) fit_circle(pts, circ[r][0], circ[r][1], circ[r][2]);
+    }
+    if (skip) continue;
+    for (size_t j = 0; j < R; ++j)
+      for (size_t k = j + 1; k < std::min(Cn, R); ++k) {
+        const auto ip = intersect_circles(circ[j][0], circ[j][1], circ[j][2], circ[k][0], circ[k][1], circ[k][2]);
+        if (ip.size() < 2) continue;
+        const double f = std::hypot(ip[0][0] - ip[1][0], ip[0][1] - ip[1][1]) / M_PI;
+        if (std::isfinite(f)) guesses.push_back(f);
+      }
+  }
+  if (guesses.empty()) {
+    if (!fallbackFocalLength) return false;
+    guesses.push_back(*fallbackFocalLength);
+  }
+  const double f0 = median_of(guesses);
+  intr.assign(4 + nd, 0.0);
+  intr[0] = f0;
+  intr[1] = f0;
+  intr[2] = cu;
+  intr[3] = cv;
+  return true;
+}
+
+bool keypointToEuclidean(int32_t camModel, const double* intr, size_t imCols, size_t imRows, const double kp[2],
+                         double out[3]) {
+  const int nd = n_distortion(camModel);
+  if (nd < 0) throw std::runtime_error("keypointToEuclidean: not a pinhole camera model");
+  const double yu = (kp[0] - intr[2]) / intr[0], yv = (kp[1] - intr[3]) / intr[1];
+  double bx = yu, by = yv;  // undistort: Gauss-Newton on distort(ybar) = y
+  const int n = camModel == KB_PINHOLE_RADTAN ? 5 : 20;
+  for (int i = 0; i < n; ++i) {
+    double tx = bx, ty = by, F[4];
+    if (camModel == KB_PINHOLE_RADTAN) {
+      distort(camModel, intr + 4, tx, ty, F);
+    } else {  // central differences of the forward map
+      const double h = 1e-7;
+      double a0 = bx + h, a1 = by, b0 = bx - h, b1 = by, c0 = bx, c1 = by + h, e0 = bx, e1 = by - h;
+      distort(camModel, intr + 4, a0, a1, nullptr);
+      distort(camModel, intr + 4, b0, b1, nullptr);
+      distort(camModel, intr + 4, c0, c1, nullptr);
+      distort(camModel, intr + 4, e0, e1, nullptr);
+      F[0] = (a0 - b0) / (2 * h);
+      F[2] = (a1 - b1) / (2 * h);
+      F[1] = (c0 - e0) / (2 * h);
+      F[3] = (c1 - e1) / (2 * h);
+      distort(camModel, intr + 4, tx, ty, nullptr);
+    }
+    const double ex = yu - tx, ey = yv - ty;
+    // du = (F^T F)^-1 F^T e = F^-1 e for a square F
+    const double det = F[0] * F[3] - F[1] * F[2];
+    bx += (F[3] * ex - F[1] * ey) / det;
+    by += (-F[2] * ex + F[0] * ey) / det;
+    if (ex * ex + ey * ey < 1e-15) break;
+  }
+  out[0] = bx;
+  out[1] = by;
+  out[2] = 1.0;
+  return kp[0] >= 0.0 && kp[1] >= 0.0 && kp[0] < (double)imCols && kp[1] < (double)imRows;  // isValid
+}
+
+bool estimateTransformation(const GridObservation& obs, const AprilgridTarget& target, int32_t camModel,
+                            const double* intr, Transformation& out_T_t_c) {
+  const std::vector<double> P = target.points();
+  std::vector<std::array<double, 2>> m;  // normalised image points
+  std::vector<std::array<double, 3>> X;  // target points
+  const double cos80 = std::cos(80.0 * M_PI / 180.0);
+  for (size_t i = 0; i < target.size(); ++i) {
+    double kp[2], b[3];
+    if (!obs.imagePoint(i, kp)) continue;
+    if (!keypointToEuclidean(camModel, intr, obs.imCols, obs.imRows, kp, b)) continue;
+    if (b[2] / std::sqrt(b[0] * b[0] + b[1] * b[1] + b[2] * b[2]) <= cos80) continue;
+    m.push_back({b[0] / b[2], b[1] / b[2]});
+    X.push_back({P[3 * i], P[3 * i + 1], P[3 * i + 2]});
+  }
+  if (m.size() < 4) return false;
+  for (const auto& x : X)
+    if (x[2] != 0.0) throw std::runtime_error("estimateTransformation: planar targets only");
+  // normalised DLT of the homography (X, Y, 1) -> (x, y, 1)
+  const size_t n = m.size();
+  double mx = 0, my = 0, Mx = 0, My = 0;
+  for (size_t i = 0; i < n; ++i) {
+    mx += m[i][0];
+    my += m[i][1];
+    Mx += X[i][0];
+    My += X[i][1];
+  }
+  mx /= n;
+  my /= n;
+  Mx /= n;
+  My /= n;
+  double sm = 0, sM = 0;
+  for (size_t i = 0; i < n; ++i) {
+    sm += std::hypot(m[i][0] - mx, m[i][1] - my);
+    sM += std::hypot(X[i][0] - Mx, X[i][1] - My);
+  }
+  sm = std::sqrt(2.0) * n / sm;
+  sM = std::sqrt(2.0) * n / sM;
+  std::array<double, 81> AtA{};
+  for (size_t i = 0; i < n; ++i) {
+    const double X0 = (X[i][0] - Mx) * sM, Y0 = (X[i][1] - My) * sM;
+    const double u = (m[i][0] - mx) * sm, v = (m[i][1] - my) * sm;
+    const double r1[9] = {-X0, -Y0, -1, 0, 0, 0, u * X0, u * Y0, u};
+    const double r2[9] = {0, 0, 0, -X0, -Y0, -1, v * X0, v * Y0, v};
+    for (int a = 0; a < 9; ++a)
+      for (int b = 0; b < 9; ++b) AtA[a * 9 + b] += r1[a] * r1[b] + r2[a] * r2[b];
+  }
+  const std::array<double, 9> hn = smallest_eigvec9(AtA);
+  // denormalise: H = Tm^-1 Hn TM
+  const std::array<double, 9> Tmi{1 / sm, 0, mx, 0, 1 / sm, my, 0, 0, 1}, TM{sM, 0, -sM * Mx, 0, sM, -sM * My, 0, 0, 1};
+  std::array<double, 9> H = matmul3(Tmi, matmul3(hn, TM));
+  // H ~ [r1 r2 t]
+  const double n1 = std::sqrt(H[0] * H[0] + H[3] * H[3] + H[6] * H[6]), n2 = std::sqrt(H[1] * H[1] + H[4] * H[4] + H[7] * H[7]);
+  double lam = 2.0 / (n1 + n2);
+  if (H[8] * lam < 0) lam = -lam;  // target in front of the camera
+  std::array<double, 9> Rm;
+  double t[3];
+  for (int r = 0; r < 3; ++r) {
+    Rm[r * 3 + 0] = lam * H[r * 3 + 0];
+    Rm[r * 3 + 1] = lam * H[r * 3 + 1];
+    t[r] = lam * H[r * 3 + 2];
+  }
+  Rm[2] = Rm[3] * Rm[7] - Rm[6] * Rm[4];  // r3 = r1 x r2
+  Rm[5] = Rm[6] * Rm[1] - Rm[0] * Rm[7];
+  Rm[8] = Rm[0] * Rm[4] - Rm[3] * Rm[1];
+  for (int it = 0; it < 30; ++it) {  // polar decomposition: R <- (R + R^-T) / 2
+    std::array<double, 9> cof{Rm[4] * Rm[8] - Rm[5] * Rm[7], Rm[5] * Rm[6] - Rm[3] * Rm[8], Rm[3] * Rm[7] - Rm[4] * Rm[6],
+                              Rm[2] * Rm[7] - Rm[1] * Rm[8], Rm[0] * Rm[8] - Rm[2] * Rm[6], Rm[1] * Rm[6] - Rm[0] * Rm[7],
+                              Rm[1] * Rm[5] - Rm[2] * Rm[4], Rm[2] * Rm[3] - Rm[0] * Rm[5], Rm[0] * Rm[4] - Rm[1] * Rm[3]};
+    const double det = Rm[0] * cof[0] + Rm[1] * cof[1] + Rm[2] * cof[2];
+    for (int k = 0; k < 9; ++k) Rm[k] = 0.5 * (Rm[k] + cof[k] / det);  // R^-T = cof / det
+  }
+  // Levenberg-Marquardt on the normalised reprojection error, parameters (rotation-vector increment, t)
+  auto residual = [&](const std::array<double, 9>& Rr, const double* tt, std::vector<double>& e) {
+    e.resize(2 * n);
+    double c = 0.0;
+    for (size_t i = 0; i < n; ++i) {
+      const double* x = X[i].data();
+      const double p0 = Rr[0] * x[0] + Rr[1] * x[1] + Rr[2] * x[2] + tt[0];
+      const double p1 = Rr[3] * x[0] + Rr[4] * x[1] + Rr[5] * x[2] + tt[1];
+      const double p2 = Rr[6] * x[0] + Rr[7] * x[1] + Rr[8] * x[2] + tt[2];
+      e[2 * i] = p0 / p2 - m[i][0];
+      e[2 * i + 1] = p1 / p2 - m[i][1];
+      c += e[2 * i] * e[2 * i] + e[2 * i + 1] * e[2 * i + 1];
+    }
+    return c;
+  };
+  std::vector<double> e, e2;
+  double cost = residual(Rm, t, e), mu = 1e-3;
+  for (int it = 0; it < 50; ++it) {
+    double JtJ[36] = {0}, Jte[6] = {0};
+    std::vector<double> J(2 * n * 6);
+    const double h = 1e-7;
+    for (int k = 0; k < 6; ++k) {  // forward differences of the 6 parameters
+      double w[3] = {0, 0, 0}, tt[3] = {t[0], t[1], t[2]};
+      if (k < 3) w[k] = h;
+      else tt[k - 3] += h;
+      const std::array<double, 9> Rk = matmul3(rodrigues(w), Rm);
+      residual(Rk, tt, e2);
+      for (size_t r = 0; r < 2 * n; ++r) J[r * 6 + k] = (e2[r] - e[r]) / h;
+    }
+    for (size_t r = 0; r < 2 * n; ++r)
+      for (int a = 0; a < 6; ++a) {
+        Jte[a] += J[r * 6 + a] * e[r];
+        for (int b = 0; b < 6; ++b) JtJ[a * 6 + b] += J[r * 6 + a] * J[r * 6 + b];
+      }
+    bool improved = false;
+    for (int tries = 0; tries < 10 && !improved; ++tries) {
+      double A[36], bvec[6];
+      for (int a = 0; a < 36; ++a) A[a] = JtJ[a];
+      for (int a = 0; a < 6; ++a) {
+        A[a * 6 + a] += mu * (1.0 + JtJ[a * 6 + a]);
+        bvec[a] = -Jte[a];
+      }
+      for (int k = 0; k < 6; ++k) {  // Gaussian elimination with partial pivoting
+        int piv = k;
+        for (int r = k + 1; r < 6; ++r)
+          if (std::fabs(A[r * 6 + k]) > std::fabs(A[piv * 6 + k])) piv = r;
+        for (int c = 0; c < 6; ++c) std::swap(A[k * 6 + c], A[piv * 6 + c]);
+        std::swap(bvec[k], bvec[piv]);
+        for (int r = k + 1; r < 6; ++r) {
+          const double fct = A[r * 6 + k] / A[k * 6 + k];
+          for (int c = k; c < 6; ++c) A[r * 6 + c] -= fct * A[k * 6 + c];
+          bvec[r] -= fct * bvec[k];
+        }
+      }
+      double dlt[6];
+      for (int k = 5; k >= 0; --k) {
+        double sacc = bvec[k];
+        for (int c = k + 1; c < 6; ++c) sacc -= A[k * 6 + c] * dlt[c];
+        dlt[k] = sacc / A[k * 6 + k];
+      }
+      const std::array<double, 9> Rn = matmul3(rodrigues(dlt), Rm);
+      const double tn[3] = {t[0] + dlt[3], t[1] + dlt[4], t[2] + dlt[5]};
+      const double cn = residual(Rn, tn, e2);
+      if (cn < cost) {
+        Rm = Rn;
+        t[0] = tn[0];
+        t[1] = tn[1];
+        t[2] = tn[2];
+        const double rel = (cost - cn) / std::max(cost, 1e-300);
+        cost = cn;
+        e = e2;
+        mu = std::max(mu * 0.3, 1e-12);
+        improved = true;
+        if (rel < 1e-14) it = 50;
+      } else {
+        mu *= 10.0;
+      }
+    }
+    if (!improved) break;
+  }
+  // T_c_t = (R, t); out = T_t_c = T_c_t^-1
+  std::array<double, 9> Rt{Rm[0], Rm[3], Rm[6], Rm[1], Rm[4], Rm[7], Rm[2], Rm[5], Rm[8]};
+  const std::array<double, 3> ti{-(Rt[0] * t[0] + Rt[1] * t[1] + Rt[2] * t[2]), -(Rt[3] * t[0] + Rt[4] * t[1] + Rt[5] * t[2]),
+                                 -(Rt[6] * t[0] + Rt[7] * t[1] + Rt[8] * t[2])};
+  out_T_t_c = Transformation::fromMatrix(Rt, ti);
+  return true;
+}
+
 }  // namespace io
 }  // namespace kalibr_amd

@@ -3,9 +3,8 @@
 //        packed into the device problem exactly as CalibrateMultiCameraRig creates its terms;
 //   out: the calibration as ROS CameraInfo / TransformStamped / TFMessage YAML, as kalibr_calibrate_cameras
 //        exports it.
-// Paths are relative to the reference repository.  Target detection (AprilTags, OpenCV), the intrinsics
-// initialisers and PnP (estimateTransformation) are not rebuilt: an observation carries its T_t_c when the
-// caller has one, as the reference's observation does after estimateTransformation.
+// Paths are relative to the reference repository.  Target detection (AprilTags, OpenCV) is not rebuilt; the
+// pinhole initialisers (initializeIntrinsics, estimateTransformation) are, without OpenCV.
 #pragma once
 
 #include <array>
@@ -82,6 +81,32 @@ backend::CalibrationProblem buildRigProblem(const std::vector<int32_t>& camModel
                                             const std::vector<double>& intrinsics, const AprilgridTarget& target,
                                             const std::vector<SyncedSet>& sets,
                                             const std::vector<Transformation>& baselineGuesses);
+
+// ---------------------------------------------------------------- initialisers (PinholeProjection)
+/// PinholeProjection::initializeIntrinsics (aslam_cv/aslam_cameras/include/aslam/cameras/implementation/
+/// PinholeProjection.hpp:713-803): image centre (cols - 1) / 2, (rows - 1) / 2; focal length = the median over the
+/// complete views of |v1 - v2| / pi for the intersections v1, v2 of the circles fitted to pairs of corner rows
+/// (Hughes et al., PAMI 2010; circle fit by modified least squares, Umbach & Jones 2000, :642-691); the fallback
+/// when no guess is finite.  intr = [fu fv cu cv | distortion cleared to 0] (4 + nDistortion values).
+/// Deviation: the reference pairs row j with rows j + 1 .. target.cols() - 1 and so reads past its row array when
+/// cols > rows; here the pairs stop at the last row.  Returns false (the reference's SM_ERROR path) when neither a
+/// guess nor a fallback exists.
+bool initializeIntrinsics(const std::vector<GridObservation>& observations, const AprilgridTarget& target,
+                          std::optional<double> fallbackFocalLength, int32_t camModel, std::vector<double>& intr);
+
+/// PinholeProjection::keypointToEuclidean (:202-227): normalised coordinates, the distortion inverted by 5
+/// Gauss-Newton steps for radtan (RadialTangentialDistortion.hpp(impl):68-98, the reference's loop) and up to 20
+/// for equidistant / FOV; false when the keypoint is outside the image (isValid).
+bool keypointToEuclidean(int32_t camModel, const double* intr, size_t imCols, size_t imRows, const double kp[2],
+                         double out[3]);
+
+/// PinholeProjection::estimateTransformation (:811-880): the seen corners back-projected (kept when the ray is
+/// within 80 degrees of the axis), then the pose of the planar target from those normalised points -- solvePnP
+/// with K = I there; here a normalised-DLT homography, its decomposition into (R, t) and a Levenberg-Marquardt
+/// refinement of the normalised reprojection error.  out_T_t_c takes camera points to the target frame.  False
+/// with fewer than 4 usable corners.
+bool estimateTransformation(const GridObservation& obs, const AprilgridTarget& target, int32_t camModel,
+                            const double* intr, Transformation& out_T_t_c);
 
 // ---------------------------------------------------------------- export (kalibr2_ros)
 /// CameraCalibratorBase::CameraInfoParams (kalibr2/include/kalibr2/CameraCalibrator.hpp:156-191)

@@ -17,6 +17,8 @@
 //                                                 IncrementalEstimator does, a seeded shuffle);
 //                                                 TermLinearSystemSolver over the oracle (cpu) or the GPU solver:
 //                                                 packing, dx / rhs permutation and Optimizer2 end to end
+//   test_host init <problem.bin> <imCols> <imRows> : per view estimateTransformation with the problem's (truth)
+//                                                 intrinsics vs the state's T_t_c; initializeIntrinsics of each camera
 //   test_host io <problem.bin> <outdir> 0       : observation records -> buildRigProblem (must rebuild the packed
 //                                                 problem), targetPoseGuess per frame, exportCalibration YAML
 // Prints one JSON line.  The oracle is test infrastructure only (oracle/kb_oracle.h).
@@ -657,6 +659,71 @@ static int run_terms(const CalibrationProblem& p, bool gpu, const std::string& p
 // io: per-frame synchronized sets of GridObservation records re-created from the packed problem, each observation
 // carrying its camera's T_t_c of the problem's state (T_t_ci = T_f (B_{i-1}..B_0)^-1); buildRigProblem must give
 // back the same term arrays; the target pose guesses and the exported YAML are checked by the Python side.
+// init: the pinhole initialisers on the problem's views (the state holds the truth)
+static int run_init(const CalibrationProblem& p, size_t imCols, size_t imRows) {
+  namespace io = kalibr_amd::io;
+  const size_t N = p.n_cams(), K = p.n_target();
+  io::AprilgridTarget tgt;
+  auto pose = [&](size_t off) {
+    io::Transformation T;
+    for (int k = 0; k < 4; ++k) T.q[k] = p.state[off + k];
+    for (int k = 0; k < 3; ++k) T.t[k] = p.state[off + 4 + k];
+    return T;
+  };
+  auto inverse = [](const io::Transformation& T) {
+    io::Transformation I;
+    I.q = {-T.q[0], -T.q[1], -T.q[2], T.q[3]};
+    const auto R = T.C();
+    for (int r = 0; r < 3; ++r) I.t[r] = -(R[r] * T.t[0] + R[3 + r] * T.t[1] + R[6 + r] * T.t[2]);
+    return I;
+  };
+  const size_t offb = N * KBO_MAX_INTR, offf = offb + 7 * (N - 1);
+  std::vector<io::Transformation> base;
+  for (size_t j = 0; j + 1 < N; ++j) base.push_back(pose(offb + 7 * j));
+  double max_rot = 0.0, max_trans = 0.0;
+  int n_ok = 0, n_views = 0;
+  std::vector<std::vector<io::GridObservation>> per_cam(N);
+  for (int v = 0; v < p.n_views(); ++v) {
+    const size_t f = p.view_frame[v], i = p.view_cam[v];
+    io::GridObservation o(K);
+    o.imCols = imCols;
+    o.imRows = imRows;
+    for (uint32_t k = p.view_offset[v]; k < p.view_offset[v + 1]; ++k)
+      o.updateImagePoint(p.corner_id[k], p.y[2 * k], p.y[2 * k + 1]);
+    io::Transformation chain;
+    for (size_t j = 0; j < i; ++j) chain = base[j] * chain;
+    const io::Transformation truth = pose(offf + 7 * f) * inverse(chain);
+    io::Transformation est;
+    ++n_views;
+    if (!io::estimateTransformation(o, tgt, p.cam_model[i], p.state.data() + i * KBO_MAX_INTR, est)) continue;
+    ++n_ok;
+    // rotation error: angle of q_est^-1 q_truth (|w| of the product), translation error in metres
+    const auto Re = est.C(), Rt = truth.C();
+    double tr = 0.0;
+    for (int a = 0; a < 3; ++a)
+      for (int b = 0; b < 3; ++b) tr += Re[a * 3 + b] * Rt[a * 3 + b];
+    max_rot = std::max(max_rot, std::acos(std::min(1.0, std::max(-1.0, (tr - 1.0) / 2.0))));
+    for (int a = 0; a < 3; ++a) max_trans = std::max(max_trans, std::fabs(est.t[a] - truth.t[a]));
+    per_cam[i].push_back(o);
+  }
+  std::string f0 = "[";
+  for (size_t i = 0; i < N; ++i) {
+    std::vector<double> intr;
+    const bool ok = io::initializeIntrinsics(per_cam[i], tgt, std::nullopt, p.cam_model[i], intr);
+    char buf[128];
+    std::snprintf(buf, sizeof buf, "%s[%d, %.17g, %.17g, %.17g]", i ? ", " : "", ok ? 1 : 0, ok ? intr[0] : 0.0,
+                  ok ? intr[2] : 0.0, ok ? intr[3] : 0.0);
+    f0 += buf;
+  }
+  f0 += "]";
+  std::vector<double> fb;
+  const bool fb_ok = io::initializeIntrinsics({io::GridObservation(K)}, tgt, 777.0, p.cam_model[0], fb);
+  std::printf("{\"views\": %d, \"estimated\": %d, \"max_rot\": %.3e, \"max_trans\": %.3e, \"init\": %s, "
+              "\"fallback_ok\": %d, \"fallback_f\": %.17g}\n",
+              n_views, n_ok, max_rot, max_trans, f0.c_str(), fb_ok ? 1 : 0, fb_ok ? fb[0] : 0.0);
+  return 0;
+}
+
 static int run_io(const CalibrationProblem& p, const std::string& outdir) {
   namespace io = kalibr_amd::io;
   const size_t N = p.n_cams(), K = p.n_target();
@@ -728,6 +795,7 @@ int main(int argc, char** argv) {
   try {
     CalibrationProblem p = load(argv[2]);
     if (mode == "io") return run_io(p, argv[3]);
+    if (mode == "init") return run_init(p, (size_t)std::atol(argv[3]), (size_t)std::atol(argv[4]));
     if (mode == "terms-cpu" || mode == "terms-gpu") return run_terms(p, mode == "terms-gpu", pol, maxIt);
     if (mode == "incr-cpu" || mode == "incr-gpu") {
       const double delta = std::atof(argv[3]);
