@@ -419,7 +419,7 @@ kb_handle* kb_create(const kb_layout* L) {
     const int tgl = (3 * h->K <= kTargetLds ? 3 * h->K : 0) + 8 * d.gframes;
     if (h->build_pipe) {  // k_buildp: tiles | H | chains | 2 view buffers | frame-wave buffers | K | target, poses
       const int np = N * (N - 1) / 2, nf = (C + 16) / 16 <= 4 ? 2 : 3;  // as build_threads
-      h->lds_build = sizeof(double) * (N * 32 * XS + N * 256 + N * 64 + (36 * np + 44 * N + 6 * CZ) +
+      h->lds_build = sizeof(double) * (N * 64 * XS + N * 256 + N * 64 + (36 * np + 44 * N + 6 * CZ) +
                                        (40 + 6 * CZ) + nf * 6 * CZ + 36 * np + tgl);
     } else {
       h->lds_build = sizeof(double) * (WPB * 64 * XS + WPB * 256 + N * (256 + 256 + 64 + 36 + 36 + 8) + 36 +

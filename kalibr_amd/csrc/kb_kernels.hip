@@ -1093,8 +1093,8 @@ __global__ void __launch_bounds__(64 * (kBuildpMaxCams + 3)) k_buildp(KbDev d, i
   const int tid = threadIdx.x;
   const int nbz = (C + 16) >> 4, CZ = 16 * nbz;
   const int VBS = 36 * NP + 44 * N + 6 * CZ, FBS = 6 * CZ;
-  double* Xw = sm + wave * 32 * XS;     // [N][32][XS] view waves' Jacobian-row tiles (P_v after the SYRK)
-  double* Hw = sm + N * 32 * XS;        // [N][256] view local Hessians
+  double* Xw = sm + wave * 64 * XS;     // [N][64][XS] view waves' Jacobian-row tiles (P_v after the SYRK)
+  double* Hw = sm + N * 64 * XS;        // [N][256] view local Hessians
   double* Wv = Hw + N * 256;            // [N][64]: R(9) t(3) tf(3) | G(36) at +16
   double* VB = Wv + N * 64;             // [VBS] view outputs: P_i K_{i,j} [NP][36] | dH [N][36] | dg [N][8] |
                                         //   intrinsic columns [6][CZ]
@@ -1292,7 +1292,7 @@ __global__ void __launch_bounds__(64 * (kBuildpMaxCams + 3)) k_buildp(KbDev d, i
         rt_mul(Lc, Lc + 9, Ri, ti, R, t);  // T_cam_w = L_cam T_f^-1
         v4d acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
         const int o0 = fv.x, o1 = fv.y;
-        for (int base = o0; base < o1; base += 32) {  // 32 corners = 64 rows, through the 32-row tile in two halves
+        for (int base = o0; base < o1; base += 32) {  // 32 corners = 64 rows per tile
           const int k = base + (lane & 31);
           const int cid = cidn;
           const double2 yv = yn;
@@ -1325,31 +1325,24 @@ __global__ void __launch_bounds__(64 * (kBuildpMaxCams + 3)) k_buildp(KbDev d, i
             for (int q = 0; q < 9; ++q) xr[6 + q] = (q < nin) ? -(r ? Ji[KB_MAX_INTR + q] : Ji[q]) : 0.0;
             xr[15] = -e;  // column 15 carries -e: H[:,15] = rhs part, H[15][15] = chi^2
           }
-          // rows 2n .. 63 of a partial pass are zero: only the k-steps holding valid rows are issued (k-step ks = rows
-          // 4ks .. 4ks + 3 of the pass, even ks into acc0, odd into acc1)
+          // the 64 rows of the pass in one tile write; rows 2n .. 63 of a partial pass are zero: only the k-steps
+          // holding valid rows are issued (k-step ks = rows 4ks .. 4ks + 3, even ks into acc0, odd into acc1)
+#pragma unroll
+          for (int q = 0; q < 16; ++q) Xw[row * XS + q] = xr[q];
+          KB_WAVE_SYNC();
           const int nks = (2 * min(32, o1 - base) + 3) >> 2;
 #pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            if (8 * h >= nks) break;  // wave-uniform
-            if ((row >> 5) == h) {
-#pragma unroll
-              for (int q = 0; q < 16; ++q) Xw[(row & 31) * XS + q] = xr[q];
+          for (int ks = 0; ks < 16; ks += 2) {
+            if (ks < nks) {
+              const double xa = Xw[(4 * ks + mrow) * XS + mcol];
+              acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(xa, xa, acc0, 0, 0, 0);
             }
-            KB_WAVE_SYNC();
-#pragma unroll
-            for (int kk = 0; kk < 8; kk += 2) {
-              const int ks = 8 * h + kk;
-              if (ks < nks) {
-                const double xa = Xw[(4 * kk + mrow) * XS + mcol];
-                acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(xa, xa, acc0, 0, 0, 0);
-              }
-              if (ks + 1 < nks) {
-                const double xb = Xw[(4 * kk + 4 + mrow) * XS + mcol];
-                acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(xb, xb, acc1, 0, 0, 0);
-              }
+            if (ks + 1 < nks) {
+              const double xb = Xw[(4 * ks + 4 + mrow) * XS + mcol];
+              acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(xb, xb, acc1, 0, 0, 0);
             }
-            KB_WAVE_SYNC();
           }
+          KB_WAVE_SYNC();
         }
         {  // the next frame's first corner ids and keypoints, in flight during the expansion and the barrier
           fv = fvn;
