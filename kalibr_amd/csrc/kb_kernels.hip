@@ -1280,7 +1280,9 @@ __global__ void __launch_bounds__(64 * (kBuildpMaxCams + 3)) k_buildp(KbDev d, i
         const int f = f0 + it;
         int lane = threadIdx.x & 63;  // opaque per frame (see the frame waves)
         asm volatile("" : "+v"(lane));
-        const int r = lane >> 5, row = 2 * (lane & 31) + r, mrow = lane >> 4, mcol = lane & 15;
+        // lane = corner (lane & 31) of the pass, Jacobian row r = lane >> 5; u rows 0..31, v rows 32..63 of the tile
+      // (row = lane: the 32 lanes of a write hit 16 distinct LDS bank pairs at the 17-double row stride)
+      const int r = lane >> 5, row = lane, mrow = lane >> 4, mcol = lane & 15;
         if (wave == 0 && it < 8) KB_TSB(d, 2 + 2 * it);
         double* vb = VB;
         const int2 fvn = d.fview[(size_t)min(f + 1, f1 - 1) * N + cam];  // the next frame's view (first loads below)
@@ -1325,19 +1327,19 @@ __global__ void __launch_bounds__(64 * (kBuildpMaxCams + 3)) k_buildp(KbDev d, i
             for (int q = 0; q < 9; ++q) xr[6 + q] = (q < nin) ? -(r ? Ji[KB_MAX_INTR + q] : Ji[q]) : 0.0;
             xr[15] = -e;  // column 15 carries -e: H[:,15] = rhs part, H[15][15] = chi^2
           }
-          // the 64 rows of the pass in one tile write; rows 2n .. 63 of a partial pass are zero: only the k-steps
-          // holding valid rows are issued (k-step ks = rows 4ks .. 4ks + 3, even ks into acc0, odd into acc1)
+          // the 64 rows of the pass in one tile write; rows n .. 31 and 32 + n .. 63 of a partial pass are zero: only
+          // the k-steps holding valid rows are issued (k-step ks = rows 4ks .. 4ks + 3, even ks into acc0, odd into acc1)
 #pragma unroll
           for (int q = 0; q < 16; ++q) Xw[row * XS + q] = xr[q];
           KB_WAVE_SYNC();
-          const int nks = (2 * min(32, o1 - base) + 3) >> 2;
+          const int nkh = (min(32, o1 - base) + 3) >> 2;  // valid k-steps per half
 #pragma unroll
           for (int ks = 0; ks < 16; ks += 2) {
-            if (ks < nks) {
+            if ((ks & 7) < nkh) {
               const double xa = Xw[(4 * ks + mrow) * XS + mcol];
               acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(xa, xa, acc0, 0, 0, 0);
             }
-            if (ks + 1 < nks) {
+            if (((ks + 1) & 7) < nkh) {
               const double xb = Xw[(4 * ks + 4 + mrow) * XS + mcol];
               acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(xb, xb, acc1, 0, 0, 0);
             }
