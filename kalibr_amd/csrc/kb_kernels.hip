@@ -1135,7 +1135,7 @@ __global__ void __launch_bounds__(64 * (kBuildpMaxCams + 3)) k_buildp(KbDev d, i
       const double v = d.dx[min(q, C - 1)];
       dxv[sl] = q < C ? v : 0.0;
     }
-    fdx_load(d, f0, lane, yr, bq);
+    fdx_load(d, f0 + min(wave, G - 1), lane, yr, bq);  // wave j steps frame f0 + j (its rows in this round)
 #pragma unroll
     for (int sl = 0; sl < 2; ++sl) {
       KB_KEEP(dxv[sl]);
@@ -1157,9 +1157,6 @@ __global__ void __launch_bounds__(64 * (kBuildpMaxCams + 3)) k_buildp(KbDev d, i
   }
   if (tid < 2 * N) ctab[tid / N][tid % N] = (tid < N) ? cam_arg(d.col_intr, tid) : cam_arg(d.col_base, tid - N);
   double* fpl = tg + (tg_lds ? nt3 : 0);
-  double fp0[7];
-#pragma unroll
-  for (int q = 0; q < 7; ++q) fp0[q] = sf[d.off_frame + 7 * f0 + q];
   int cidn;  // view waves: lane = corner (lane & 31) of a 32-corner tile, Jacobian row lane >> 5 (0: u, 1: v)
   double2 yn;
   {
@@ -1176,22 +1173,20 @@ __global__ void __launch_bounds__(64 * (kBuildpMaxCams + 3)) k_buildp(KbDev d, i
     Kl[q] = Kc[(size_t)(i * N + j) * 36 + e];
   }
   KB_KEEPS(cidn);
+  // the previous solve's frame steps: wave j moves frame f0 + j (then f0 + j + NW, ...) and stages its pose
   double wmax = 0.0;
-  if (upd) frame_step(d, f0, wave == 0, lane, yr, dxv, bq, fp0, snew, wmax);
-  if (wave == 0 && lane < 7) {
-    double pv = fp0[0];
-#pragma unroll
-    for (int q = 1; q < 7; ++q) pv = (lane == q) ? fp0[q] : pv;
-    fpl[lane] = pv;
-  }
-  for (int j = 1 + wave; j < G; j += NW) {
+  for (int j = wave; j < G; j += NW) {
     double fp[7];
 #pragma unroll
     for (int q = 0; q < 7; ++q) fp[q] = sf[d.off_frame + 7 * (f0 + j) + q];
     if (upd) {
-      double af[6][2], bfq;
-      fdx_load(d, f0 + j, lane, af, bfq);
-      frame_step(d, f0 + j, true, lane, af, dxv, bfq, fp, snew, wmax);
+      if (j == wave) {
+        frame_step(d, f0 + j, true, lane, yr, dxv, bq, fp, snew, wmax);
+      } else {
+        double af[6][2], bfq;
+        fdx_load(d, f0 + j, lane, af, bfq);
+        frame_step(d, f0 + j, true, lane, af, dxv, bfq, fp, snew, wmax);
+      }
     }
     if (lane < 7) {
       double pv = fp[0];
