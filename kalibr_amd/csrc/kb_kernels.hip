@@ -2126,14 +2126,15 @@ __device__ __forceinline__ void ldl_tiles_solve(const double* S, const double* r
 }
 
 // ---------------------------------------------------------------------------------------------
-// k_colimg (C > 64): finishes the column sums as k_colfin does (out[e] = sum_r rows[r][e], fixed order; max for
-// the max|dx_f| columns) and writes k_solve's LDS image of the camera block from the same rows:
+// k_colimg (C > 64): finishes the column sums as k_colfin does (out[e] = sum_r rows[r][e] over the nrows rows: the 8
+// stage-1 rows, or 1 all-reduced row when sharded; fixed order; max for the max|dx_f| columns) and writes k_solve's
+// LDS image of the camera block from the same rows:
 //   [S lower 16 x 16 tiles, stride kTS: -sum Y^T Y (diagonal tiles: lower half), identity padding beyond C |
 //    rhs (n16 + 2 slots): -sum Y^T z, slot C: the non-PD frame-block count | per-camera 16 x 16 sums, mirrored].
 // One thread per entry (the index arithmetic runs wide here, not in the one-block solve, which stages the image
 // with one contiguous copy).
 // ---------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_colimg(KbDev d, const double* rows, double* out, int gate) {
+__global__ void __launch_bounds__(256) k_colimg(KbDev d, const double* rows, double* out, int gate, int nrows) {
   if (gate && d.ctrl->done) return;
   const int q = blockIdx.x * blockDim.x + threadIdx.x;
   const int N = d.N, C = d.C, Wt = d.W - d.C;
@@ -2177,10 +2178,11 @@ __global__ void __launch_bounds__(256) k_colimg(KbDev d, const double* rows, dou
   if (src >= 0) {
     double v[kColsumRows];
 #pragma unroll
-    for (int r = 0; r < kColsumRows; ++r) v[r] = rows[(size_t)r * d.Wtot + src];
+    for (int r = 0; r < kColsumRows; ++r) v[r] = rows[(size_t)(r < nrows ? r : 0) * d.Wtot + src];
     const bool mx = src >= d.Wp;
 #pragma unroll
-    for (int r = 0; r < kColsumRows; ++r) acc = mx ? fmax(acc, v[r]) : acc + v[r];
+    for (int r = 0; r < kColsumRows; ++r)
+      if (r < nrows) acc = mx ? fmax(acc, v[r]) : acc + v[r];
   }
   *dst = sg * acc;
 }
