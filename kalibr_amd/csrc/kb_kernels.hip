@@ -1949,7 +1949,30 @@ __device__ __forceinline__ int sidx(int i, int j, int C) {
     return tidx(i, j);
 }
 
-// diagonal tile p factored in place by one wave (lanes 0..15 hold its rows, row k broadcast by v_readlane):
+// lane k's value to every lane of its 16-lane row (DPP row_newbcast, gfx90a+): a plain VALU move, without the
+// v_readlane -> SGPR -> VALU round trip and its wait states.  k must fold to a constant (unrolled loops).
+__device__ __forceinline__ double bcast16(double v, int k) {
+  switch (k) {
+    case 0: return dpp_d<0x150>(v);
+    case 1: return dpp_d<0x151>(v);
+    case 2: return dpp_d<0x152>(v);
+    case 3: return dpp_d<0x153>(v);
+    case 4: return dpp_d<0x154>(v);
+    case 5: return dpp_d<0x155>(v);
+    case 6: return dpp_d<0x156>(v);
+    case 7: return dpp_d<0x157>(v);
+    case 8: return dpp_d<0x158>(v);
+    case 9: return dpp_d<0x159>(v);
+    case 10: return dpp_d<0x15A>(v);
+    case 11: return dpp_d<0x15B>(v);
+    case 12: return dpp_d<0x15C>(v);
+    case 13: return dpp_d<0x15D>(v);
+    case 14: return dpp_d<0x15E>(v);
+    default: return dpp_d<0x15F>(v);
+  }
+}
+
+// diagonal tile p factored in place by one wave (lanes 0..15 hold its rows, row k broadcast by DPP row_newbcast):
 // strictly lower Ltilde, D on the diagonal, rD[16 p + r] = 1 / D_r.  Returns false on a non-positive pivot (padding
 // rows have D = 1: only real pivots can fail).
 __device__ __forceinline__ bool diag_ldl16(double* S, double* rD, int p, int lane) {
@@ -1962,17 +1985,17 @@ __device__ __forceinline__ bool diag_ldl16(double* S, double* rD, int p, int lan
   double rd = 1.0;
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
-    const double Dk = readlane_d(row[k], k);
+    const double Dk = bcast16(row[k], k);
     ok = ok && (Dk > 0.0);
     const double rdk = recip_d(Dk);
     rd = (lane == k) ? rdk : rd;
     const double f = (lane > k) ? row[k] * rdk : 0.0;
 #pragma unroll
-    for (int j = k + 1; j < 16; ++j) row[j] -= f * readlane_d(row[j], k);
+    for (int j = k + 1; j < 16; ++j) row[j] -= f * bcast16(row[j], k);
   }
   double lrow[16];
 #pragma unroll
-  for (int c = 0; c < 16; ++c) lrow[c] = row[c] * readlane_d(rd, c);  // Ltilde[r][c] = (L D)[r][c] / D_c
+  for (int c = 0; c < 16; ++c) lrow[c] = row[c] * bcast16(rd, c);  // Ltilde[r][c] = (L D)[r][c] / D_c
   if (lane < 16) {
 #pragma unroll
     for (int c = 0; c < 16; ++c)
@@ -2041,11 +2064,14 @@ __device__ __forceinline__ void ldl_tiles(const KbDev& d, double* S, double* rD,
       const bool ok = diag_ldl16(S, rD, p, lane);
       if (!ok && lane == 0) *okl = 0;
       KB_TS(d, 21 + 4 * p);
-    } else if (p > 0) {
+    } else if (p > 0 && wave != 4) {
+      // wave 4 shares wave 0's SIMD (waves map to SIMDs round robin): it stays idle, so the MFMA tiles do not
+      // slow the factorization on the critical path
       const int m = nb - p;  // trailing tiles (p + ii, p + jj), 0 <= jj <= ii < m; q = 0 is (p, p)
       const int ntiles = m * (m + 1) / 2;
+      const int wv = wave - (wave > 4);  // 1 .. nw - 2
 #pragma unroll 1
-      for (int q = wave; q < ntiles; q += nw - 1) {
+      for (int q = wv; q < ntiles; q += nw - 2) {
         const int ii = tri_row(q), jj = q - ii * (ii + 1) / 2;
         trail_update16(S, Wsc, p - 1, p + ii, p + jj, lane);
       }
@@ -2055,7 +2081,8 @@ __device__ __forceinline__ void ldl_tiles(const KbDev& d, double* S, double* rD,
     if (p == nb - 1) break;
     // phase 1 of panel p
 #pragma unroll 1
-    for (int ii = wave; ii < nb - p - 1; ii += nw) panel_trsm16(S, rD, Wsc, p, p + 1 + ii, lane);
+    for (int ii = wave - (wave > 4); ii < nb - p - 1 && wave != 4; ii += nw - 1)
+      panel_trsm16(S, rD, Wsc, p, p + 1 + ii, lane);
     if (wave == 0) {
       KB_WAVE_SYNC();  // this wave's W and Ltilde rows of tile (p + 1, p) are in LDS
       KB_TS(d, 22 + 4 * p);
@@ -2085,7 +2112,7 @@ __device__ __forceinline__ void ldl_tiles_solve(const double* S, const double* r
     }
     double xr = xv[16 * p + r];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) xr -= Lr[k] * readlane_d(xr, k);
+    for (int k = 0; k < 16; ++k) xr -= Lr[k] * bcast16(xr, k);
     if (lane < 16) xv[16 * p + lane] = xr;
     KB_WAVE_SYNC();
     for (int g = 16 * (p + 1) + lane; g < n; g += 64) {
@@ -2110,7 +2137,7 @@ __device__ __forceinline__ void ldl_tiles_solve(const double* S, const double* r
     }
     double xr = xv[16 * p + r];
 #pragma unroll
-    for (int k = 15; k >= 0; --k) xr -= Lc[k] * readlane_d(xr, k);
+    for (int k = 15; k >= 0; --k) xr -= Lc[k] * bcast16(xr, k);
     if (lane < 16) xv[16 * p + lane] = xr;
     KB_WAVE_SYNC();
     if (p == 0) break;
