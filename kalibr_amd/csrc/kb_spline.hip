@@ -1057,13 +1057,32 @@ __global__ void __launch_bounds__(256) k_sp_back(SpDev d, int s) {
     xr[q] = hr ? d.X[(size_t)r * NB * m + q] : 0.0;
   }
   __syncthreads();
-  // T = Z_R - Z_Uin x_l - Z_U x_r
-  for (int q = tid; q < NB * m; q += blockDim.x) {
-    const int row = q / m, c = q % m;
-    double v = Z[row * wc + 2 * NB + c];
+  // T = Z_R - Z_Uin x_l - Z_U x_r on MFMA tiles: T[row][c] = Z_R[row][c] - sum_k (Z[row][k] xl[k][c] + Z[row][NB + k]
+  // xr[k][c]); A = Z^T is read from the Z rows (stride 1 in k), B from xl / xr
+  {
+    const int wave = tid >> 6, lane = tid & 63, nw = blockDim.x >> 6, nct = (m + 15) >> 4;
+    for (int t = wave; t < 2 * nct; t += nw) {
+      const int ti = t / nct, tj = t % nct, i = lane & 15;
+      const int rc = min(16 * ti + i, NB - 1), cc = min(16 * tj + i, m - 1);
+      const bool rv = 16 * ti + i < NB, cv = 16 * tj + i < m;
+      v4d_t acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-    for (int k = 0; k < NB; ++k) v -= Z[row * wc + k] * xl[k * m + c] + Z[row * wc + NB + k] * xr[k * m + c];
-    T[q] = v;
+      for (int h = 0; h < 2; ++h) {
+        const double* B = h ? xr : xl;
+#pragma unroll
+        for (int st = 0; st < 5; ++st) {
+          const int k = 4 * st + (lane >> 4), kc = min(k, NB - 1);
+          const double a = Z[rc * wc + h * NB + kc], b = B[kc * m + cc];
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64((k < NB && rv) ? a : 0.0, (k < NB && cv) ? b : 0.0, acc, 0, 0, 0);
+        }
+      }
+      const int c = 16 * tj + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * ti + (lane >> 4) + 4 * r;
+        if (row < NB && c < m) T[row * m + c] = Z[row * wc + 2 * NB + c] - acc[r];
+      }
+    }
   }
   __syncthreads();
   node_backsolve(L, id, T, m, m, d.X + (size_t)j * NB * m, tid);
