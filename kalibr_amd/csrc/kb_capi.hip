@@ -169,10 +169,10 @@ struct kb_handle {
   }
 };
 
-// mb: Schur tiles per wave of k_build (1 | 4 | 7), or per frame wave of k_buildp (5: 2 frame waves | 10: 3) when pipe
+// mb: Schur tiles per wave of k_build (1 | 4 | 7), or per frame wave of k_buildp (5: 2 frame waves | 7: 4) when pipe
 template <bool GN, unsigned MM>
 static const void* build_fn(int mb, bool pipe) {
-  if (pipe) return mb == 5 ? (const void*)k_buildp<5, GN, MM> : (const void*)k_buildp<10, GN, MM>;
+  if (pipe) return mb == 5 ? (const void*)k_buildp<5, GN, MM> : (const void*)k_buildp<7, GN, MM>;
   return mb == 1 ? (const void*)k_build<1, GN, MM> : mb == 4 ? (const void*)k_build<4, GN, MM>
                                                              : (const void*)k_build<7, GN, MM>;
 }
@@ -328,7 +328,7 @@ kb_handle* kb_create(const kb_layout* L) {
   // KB_BUILD_PIPE=0 keeps k_build for comparison
   h->build_pipe = d.nsplit == 1 && h->N <= kBuildpMaxCams;
   if (const char* e = std::getenv("KB_BUILD_PIPE")) h->build_pipe = h->build_pipe && std::atoi(e) != 0;
-  const int nbz0 = (h->C + 16) / 16, nf = (nbz0 * (nbz0 + 1) / 2 + 1) / 2 <= 5 ? 2 : 3;  // k_buildp frame waves
+  const int nbz0 = (h->C + 16) / 16, nf = (nbz0 * (nbz0 + 1) / 2 + 1) / 2 <= 5 ? 2 : 4;  // k_buildp frame waves
   h->build_threads = 64 * (h->build_pipe ? h->N + nf : d.wpb);
   if (h->build_pipe) {
     // all blocks resident at once: one block per CU (two for rigs whose block fits twice: 12 waves per CU at the
@@ -418,7 +418,7 @@ kb_handle* kb_create(const kb_layout* L) {
     const int CZ = 16 * ((C + 16) / 16);  // [Y | z] row stride of the Schur tiles
     const int tgl = (3 * h->K <= kTargetLds ? 3 * h->K : 0) + 8 * d.gframes;
     if (h->build_pipe) {  // k_buildp: tiles | H | chains | 2 view buffers | frame-wave buffers | K | target, poses
-      const int np = N * (N - 1) / 2, nf = (C + 16) / 16 <= 4 ? 2 : 3;  // as build_threads
+      const int np = N * (N - 1) / 2, nf = (C + 16) / 16 <= 4 ? 2 : 4;  // as build_threads
       h->lds_build = sizeof(double) * (N * 64 * XS + N * 256 + N * 64 + (36 * np + 44 * N + 6 * CZ) +
                                        (40 + 6 * CZ) + nf * 6 * CZ + 36 * np + tgl);
     } else {
@@ -453,7 +453,7 @@ kb_handle* kb_create(const kb_layout* L) {
     // Schur-sum tiles per wave (template bucket): ceil(lower tiles of [Y|z]^T [Y|z] / waves)
     const int nbz = (h->C + 16) / 16, ntiles = nbz * (nbz + 1) / 2;
     const int tb = (ntiles + d.wpb - 1) / d.wpb, ts = (ntiles + 3) / 4;
-    h->mb = h->build_pipe ? ((ntiles + 1) / 2 <= 5 ? 5 : 10) : tb <= 1 ? 1 : tb <= 4 ? 4 : 7;
+    h->mb = h->build_pipe ? ((ntiles + 1) / 2 <= 5 ? 5 : 7) : tb <= 1 ? 1 : tb <= 4 ? 4 : 7;
     h->ms = ts <= 1 ? 1 : ts <= 4 ? 4 : 7;
     // camera-model set: one-model rigs (and the omni-radtan + EUCM rig of configs[2]) get their own build
     // kernels; any other mix uses the all-models instantiation

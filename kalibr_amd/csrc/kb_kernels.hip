@@ -1036,9 +1036,10 @@ __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
 // the baseline columns (per-camera products summed over cameras).
 // ---------------------------------------------------------------------------------------------
 constexpr int kBuildpMaxCams = 8;
-// frame waves of k_buildp: the Schur tiles per frame wave TT picks them (<= 5 tiles: 2 waves, else 3)
+// frame waves of k_buildp: the Schur tiles per frame wave TT picks them (<= 5 tiles: 2 waves, else 4: one frame wave
+// per SIMD beside its two view waves)
 template <int TT>
-constexpr int buildp_nf() { return TT > 5 ? 3 : 2; }
+constexpr int buildp_nf() { return TT > 5 ? 4 : 2; }
 
 // intrinsics count of a one-model set (0 for a mix): a constant count lets the compiler drop the unused columns
 template <unsigned MM>
@@ -1084,7 +1085,7 @@ __device__ __forceinline__ void schur_tiles_accumulate6(const double* P, const d
 }
 
 template <int TT, bool GNF, unsigned MM>
-__global__ void __launch_bounds__(64 * (kBuildpMaxCams + 3)) k_buildp(KbDev d, int gate, int fuse) {
+__global__ void __launch_bounds__(64 * (kBuildpMaxCams + 4)) k_buildp(KbDev d, int gate, int fuse) {
   KbCtrl* c = d.ctrl;
   extern __shared__ __attribute__((aligned(16))) double sm[];
   constexpr int NF = buildp_nf<TT>();
@@ -1102,7 +1103,7 @@ __global__ void __launch_bounds__(64 * (kBuildpMaxCams + 3)) k_buildp(KbDev d, i
   double* FB = FI + 40 + 6 * CZ;        // [NF][FBS] frame wave's [A_f | b_f]
   double* Kl = FB + NF * FBS;           // [NP][36] K_{i,j}, j < i, at (i(i-1)/2 + j)
   double* tg = Kl + 36 * NP;            // [n_target][3] target corners (when staged) | frame poses [gframes][8]
-  __shared__ double wmx[kBuildpMaxCams + 3];
+  __shared__ double wmx[kBuildpMaxCams + 4];
   __shared__ int okl;
   __shared__ double cst[KB_MAX_CAMS][24];  // per camera: chain L (12) | intrinsics (10)
   __shared__ int ctab[2][KB_MAX_CAMS];      // per camera: first intrinsic column | baseline column
