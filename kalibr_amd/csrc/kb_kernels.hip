@@ -1223,6 +1223,7 @@ __global__ void __launch_bounds__(64 * (kBuildpMaxCams + 4)) k_buildp(KbDev d, i
     v4d creg = {0.0, 0.0, 0.0, 0.0};  // the camera's local sums over the block's frames
     for (int it = 0; it <= G; ++it) {
       if (it > 0) {
+        if (wave == 0 && it <= 8) KB_TSB(d, 51 + it);
         // ---------------- phase A: sums of frame f - 1 over its views (camera order), all view waves
         const int f = f0 + it - 1;
         const double* Cb = VB;
@@ -1350,12 +1351,11 @@ __global__ void __launch_bounds__(64 * (kBuildpMaxCams + 4)) k_buildp(KbDev d, i
         }
         if (wave == 0 && it < 8) KB_TSB(d, 3 + 2 * it);
         // f64 MFMA C/D layout: lane l, reg r -> row (l>>4) + 4r, col l&15
-        double* H = Hw + cam * 256;
+        v4d hv;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const double h = acc0[q] + acc1[q];
-          creg[q] = creg[q] + h;
-          H[(mrow + 4 * q) * 16 + mcol] = h;
+          hv[q] = acc0[q] + acc1[q];
+          creg[q] = creg[q] + hv[q];
         }
         double* wv = Wv + cam * 64;
         if (lane == 0) {
@@ -1369,54 +1369,79 @@ __global__ void __launch_bounds__(64 * (kBuildpMaxCams + 4)) k_buildp(KbDev d, i
           wv[14] = fp[6];
         }
         KB_WAVE_SYNC();
-        // expansion of view (f, cam) through the 6-D chains
-        const bool has = o1 > o0;
+        // expansion of view (f, cam) through the 6-D chains on three MFMA steps (no LDS copy of H):
+        //   T1 = G^T [H_dd | H_dI | . | g_d]  (A = G from LDS, B = the lane's own H registers: MFMA C layout row r of a
+        //        lane is B row r of the next k-step), rows 0..5: P_v = G^T H_dd, G^T H_dI, G^T g_d;
+        //   dH = P_v G and this camera's share of the baseline columns P_v K_{v,j} (A = P_v^T through LDS)
         double* Gm = wv + 16;
         if (lane < 36) Gm[lane] = chain_entry(wv, wv + 9, wv + 12, lane / 6, lane % 6);
         KB_WAVE_SYNC();
-        double* Pv = Xw;  // wave-local
+        double* T1 = Xw;  // [16][17] wave-local: rows 0..5 of T1
         double* Cb = vb;  // P_v K_{v,j} at pair (v(v-1)/2 + j)
         double* dHv = vb + 36 * NP + cam * 36;
         double* dgv = vb + 36 * NP + N * 36 + cam * 8;
         double* Pi = vb + 36 * NP + N * 44;
-        if (lane < 36) {
-          const int a = lane / 6, b = lane % 6;
-          double sacc = 0.0;
+        const int i16 = lane & 15, k0 = lane >> 4;
+        v4d t1 = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-          for (int k = 0; k < 6; ++k) sacc += Gm[k * 6 + a] * H[k * 16 + b];
-          Pv[lane] = has ? sacc : 0.0;  // P_v = G^T H_dd
-        } else if (lane < 42) {
-          const int a = lane - 36;
-          double sacc = 0.0;
+        for (int st = 0; st < 2; ++st) {
+          const int k = k0 + 4 * st;
+          const double ga = Gm[min(k, 5) * 6 + min(i16, 5)];
+          t1 = __builtin_amdgcn_mfma_f64_16x16x4f64((k < 6 && i16 < 6) ? ga : 0.0, k < 6 ? hv[st] : 0.0, t1, 0, 0, 0);
+        }
+        // T1 entry (a, j): a = k0 + 4 r, j = i16
 #pragma unroll
-          for (int k = 0; k < 6; ++k) sacc += Gm[k * 6 + a] * H[k * 16 + 15];
-          dgv[a] = has ? sacc : 0.0;  // G^T g_d
+        for (int r = 0; r < 2; ++r) {
+          const int arow = k0 + 4 * r;
+          if (arow < 6) {
+            T1[arow * 17 + i16] = t1[r];
+            if (i16 >= 6 && i16 < 6 + nin) {  // G^T H_dI: the camera's intrinsic columns
+              Pi[arow * CZ + ctab[0][cam] + i16 - 6] = t1[r];
+              d.Hfc[((size_t)f * 6 + arow) * C + ctab[0][cam] + i16 - 6] = t1[r];
+            } else if (i16 == 15) {
+              dgv[arow] = t1[r];  // G^T g_d
+            }
+          }
         }
         KB_WAVE_SYNC();
-        if (lane < 36) {
-          const int a = lane / 6, b = lane % 6;
-          double sacc = 0.0;
+        // A = P_v^T: lane supplies P_v[i16][k] = T1[i16][k]
+        double pa[2];
 #pragma unroll
-          for (int k = 0; k < 6; ++k) sacc += Pv[a * 6 + k] * Gm[k * 6 + b];
-          dHv[lane] = sacc;  // P_v G_v
+        for (int st = 0; st < 2; ++st) {
+          const int k = k0 + 4 * st;
+          const double v = T1[min(i16, 5) * 17 + min(k, 5)];
+          pa[st] = (k < 6 && i16 < 6) ? v : 0.0;
         }
-        if (lane < 6 * nin) {
-          const int a = lane / nin, q = lane % nin;
-          double sacc = 0.0;
+        {  // dH = P_v G
+          v4d t2 = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-          for (int k = 0; k < 6; ++k) sacc += Gm[k * 6 + a] * H[k * 16 + 6 + q];
-          sacc = has ? sacc : 0.0;  // G^T H_dI
-          Pi[a * CZ + ctab[0][cam] + q] = sacc;
-          d.Hfc[((size_t)f * 6 + a) * C + ctab[0][cam] + q] = sacc;
+          for (int st = 0; st < 2; ++st) {
+            const int k = k0 + 4 * st;
+            const double gb = Gm[min(k, 5) * 6 + min(i16, 5)];
+            t2 = __builtin_amdgcn_mfma_f64_16x16x4f64(pa[st], (k < 6 && i16 < 6) ? gb : 0.0, t2, 0, 0, 0);
+          }
+#pragma unroll
+          for (int r = 0; r < 2; ++r) {
+            const int arow = k0 + 4 * r;
+            if (arow < 6 && i16 < 6) dHv[arow * 6 + i16] = t2[r];
+          }
         }
-        // this camera's share of the baseline columns: P_v K_{v,j}, j < v
-        for (int q = lane; q < 36 * cam; q += 64) {
-          const int j = q / 36, ab2 = q - 36 * j, a = ab2 / 6, b = ab2 % 6;
-          const double* K = Kl + (cam * (cam - 1) / 2 + j) * 36;
-          double sacc = 0.0;
+        // P_v K_{v,j}, j < cam: columns c = 6 j + b of [K_{v,0} | K_{v,1} | ...]
+        const double* Kv = Kl + (cam * (cam - 1) / 2) * 36;
+        for (int ct = 0; 16 * ct < 6 * cam; ++ct) {
+          const int c = 16 * ct + i16, cc = min(c, 6 * cam - 1), jj = cc / 6, bb = cc - 6 * jj;
+          v4d t3 = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-          for (int k = 0; k < 6; ++k) sacc += Pv[a * 6 + k] * K[k * 6 + b];
-          Cb[(cam * (cam - 1) / 2) * 36 + q] = sacc;
+          for (int st = 0; st < 2; ++st) {
+            const int k = k0 + 4 * st;
+            const double kb = Kv[jj * 36 + min(k, 5) * 6 + bb];
+            t3 = __builtin_amdgcn_mfma_f64_16x16x4f64(pa[st], (k < 6 && c < 6 * cam) ? kb : 0.0, t3, 0, 0, 0);
+          }
+#pragma unroll
+          for (int r = 0; r < 2; ++r) {
+            const int arow = k0 + 4 * r;
+            if (arow < 6 && c < 6 * cam) Cb[(cam * (cam - 1) / 2) * 36 + jj * 36 + arow * 6 + bb] = t3[r];
+          }
         }
       }
       __syncthreads();
@@ -1455,7 +1480,7 @@ __global__ void __launch_bounds__(64 * (kBuildpMaxCams + 4)) k_buildp(KbDev d, i
     if (fuse) schur_tiles_store<TT>(prow + N * 136, C, tii, tjj, acc);
   }
   __syncthreads();  // okl final
-  if (wave == 0) KB_TSB(d, 60);
+  if (wave == 0) KB_TSB(d, 63);
   if (fuse && tid == 0) prow[N * 136 + W] = okl ? 0.0 : 1.0;  // non-PD frame blocks (summed)
   if (GNF && tid == 0) {  // the block's max |dx_f| (reduced with max by k_colsum)
     double m = 0.0;

@@ -17,7 +17,7 @@ g = capi.Solver(p)
 g.set_state(p.state_init)
 buf = (C.c_longlong * 128)()
 assert L.kb_diag_read_ts(g.h, buf, 128) == 0  # allocates the stamp buffer
-names = {0: "entry", 1: "prologue barrier", 60: "end"}
+names = {0: "entry", 1: "prologue barrier", 63: "end"}
 for it in range(8):
     names[2 + 2 * it] = f"view it{it} start"
     names[3 + 2 * it] = f"view it{it} SYRK done"
@@ -25,6 +25,7 @@ for it in range(8):
     names[21 + 4 * it] = f"  frame f{it} sums done"
     names[22 + 4 * it] = f"  frame f{it} GJ done"
     names[23 + 4 * it] = f"  frame f{it} Schur done"
+    names[52 + it] = f"view phase A of f{it} start"
 for rep in range(2):
     g.set_state(p.state_init)
     g.run_gn(16)
