@@ -34,11 +34,14 @@ constexpr int ORD = 4;      // spline order of the device path
 constexpr int SB = 3;       // coefficients per cyclic-reduction node: couplings reach only the next node
 constexpr int NB = 6 * SB;  // 18 rows per node
 constexpr int MAXC = 64;    // camera + IMU block
-constexpr int FPB = 4;      // frames per k_sp_frames block
+constexpr int FPB = 2;      // frames per k_sp_frames block (600 blocks at configs[4]: every block resident at once)
+constexpr int RW = 16;      // waves of the column-sum kernels (k_sp_reduce_cc, k_sp_schur_red)
 constexpr int XS = 17;      // LDS row stride of the 64 x 16 Jacobian-row tile
 constexpr int WI = 55;      // IMU theta partial row: 9x9 upper (45) | g (9) | cost
 constexpr int NPB = 8;      // nodes per k_sp_schur block
-constexpr int TCH = 32;     // terms staged per k_sp_assemble chunk
+constexpr int TCH = 32;     // IMU samples staged per k_sp_assemble chunk
+constexpr int TCF = 8;      // frames staged per k_sp_assemble chunk
+constexpr int IST = 144 + 15;  // LDS stride of a staged IMU sample: J [6][24] | e [6] | C^T [9]
 enum { SC_COST_BUILD = 0, SC_OK = 1, SC_DX = 2, SC_COST = 3, SC_LAM2 = 4, SC_NSC = 8 };
 
 struct SpDev {
@@ -88,6 +91,23 @@ struct SpDev {
 
 typedef double v4d_t __attribute__((ext_vector_type(4)));
 #define KSP_WAVE_SYNC() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
+
+// ---------------------------------------------------------------- batched staging
+// Copies with U independent loads in flight per thread.  A runtime-bounded loop of load / store pairs waits for
+// each load before it issues the next one, i.e. one memory round trip per iteration: that latency chain, not
+// bytes or flops, was what the cyclic-reduction and Schur kernels spent their time on.  ld(q) is called for
+// clamped q in [0, n) only (n >= 1) and must not depend on a loaded value; st(q, v) stores item q.
+template <int U, class Ld, class St>
+__device__ __forceinline__ void ksp_batched(int n, int tid, int nth, Ld ld, St st) {
+  for (int q0 = tid; q0 < n; q0 += U * nth) {
+    double v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = ld(min(q0 + u * nth, n - 1));
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (q0 + u * nth < n) st(q0 + u * nth, v[u]);
+  }
+}
 
 // ---------------------------------------------------------------- rotation vector (RotationVector.cpp)
 __device__ __forceinline__ void rv_C(const double* a, double* Cm) {
@@ -208,10 +228,25 @@ __global__ void __launch_bounds__(512) k_sp_frames(SpDev d) {
   double* Qp = Gp + N * N * 36;    // [N][N][36]
   double* acc = Qp + N * N * 36;   // [Wc] theta-theta accumulators
   double* tg = acc + d.Wc;         // [n_target][3]
+  // frame-independent column tables, read per entry of every frame: (a, b) of the theta-theta entries and
+  // column -> (kind, index, sub) (a load per entry and frame otherwise puts a dependent round trip in each
+  // iteration of the per-frame loops)
+  short2* tuab = (short2*)(tg + 3 * d.n_target);  // [Wc]
+  int* tck = (int*)(tuab + d.Wc);                 // [C] kind | [C] index | [C] sub
+  int* tci = tck + C;
+  int* tcs = tci + C;
   const int cam = wave;
   const double* st = d.state;
   for (int q = tid; q < 3 * d.n_target; q += nth) tg[q] = d.target[q];
-  for (int q = tid; q < d.Wc; q += nth) acc[q] = 0.0;
+  for (int q = tid; q < d.Wc; q += nth) {
+    acc[q] = 0.0;
+    tuab[q] = d.uab[q];
+  }
+  for (int q = tid; q < C; q += nth) {
+    tck[q] = d.ckind[q];
+    tci[q] = d.cidx[q];
+    tcs[q] = d.csub[q];
+  }
   // chain A_cam = B_{cam-1} .. B_0 T_c0_b (frame independent) and the pose-DV maps Gp[cam][q]
   double RA[9], tA[3];
   kb::quat2r(st + d.off_cb, RA);
@@ -402,7 +437,7 @@ __global__ void __launch_bounds__(512) k_sp_frames(SpDev d) {
           for (int r = 0; r < 6; ++r) s += Gv[i * 36 + r * 6 + a] * Pv[i * 36 + r * 6 + bb];
       } else if (q < 36 + 6 * C) {
         const int a = (q - 36) / C, col = (q - 36) % C;
-        const int kind = d.ckind[col], idx = d.cidx[col], sub = d.csub[col];
+        const int kind = tck[col], idx = tci[col], sub = tcs[col];
         for (int i = 0; i < N; ++i) {
           if (kind == 0 && idx == i) {
 #pragma unroll
@@ -425,10 +460,10 @@ __global__ void __launch_bounds__(512) k_sp_frames(SpDev d) {
     for (int q = tid; q < d.Wc; q += nth) {
       double s = 0.0;
       if (q < nup) {
-        const short2 ab = d.uab[q];
+        const short2 ab = tuab[q];
         const int a = ab.x, bcol = ab.y;
-        const int ka = d.ckind[a], ia = d.cidx[a], sa = d.csub[a];
-        const int kb2 = d.ckind[bcol], ib2 = d.cidx[bcol], sb = d.csub[bcol];
+        const int ka = tck[a], ia = tci[a], sa = tcs[a];
+        const int kb2 = tck[bcol], ib2 = tci[bcol], sb = tcs[bcol];
         for (int i = 0; i < N; ++i) {
           const bool okA = (ka == 0 && ia == i) || (ka == 1 && (ia == N - 1 || ia < i));
           const bool okB = (kb2 == 0 && ib2 == i) || (kb2 == 1 && (ib2 == N - 1 || ib2 < i));
@@ -448,7 +483,7 @@ __global__ void __launch_bounds__(512) k_sp_frames(SpDev d) {
           }
         }
       } else if (q < nup + C) {
-        const int a = q - nup, ka = d.ckind[a], ia = d.cidx[a], sa = d.csub[a];
+        const int a = q - nup, ka = tck[a], ia = tci[a], sa = tcs[a];
         for (int i = 0; i < N; ++i) {
           const double* H = Hv + i * 256;
           if (ka == 0 && ia == i) {
@@ -578,25 +613,35 @@ __global__ void __launch_bounds__(256) k_sp_assemble(SpDev d) {
   const int i = blockIdx.x, tid = threadIdx.x, nth = blockDim.x, C = d.C, m = d.m;
   const int nout = 2 * NB * NB + NB * m;
   double* out = sm;                       // [nout]
-  double* tj = out + nout;                // [TCH][6][24] IMU J | frame: FH (FHS)
-  const int stride = max(144 + 15, d.FHS);
-  double* te = tj + TCH * stride;         // unused spare
+  // frame chunk [TCF][FHS] (FH rows) | IMU chunk [TCH][IST] (J 6 x 24 | e | C^T) share one region: a node has
+  // ~3 frames and ~25 IMU samples, so a 32-term region of FHS rows would cut the blocks per CU to one
+  double* tj = out + nout;
+  const int stride = d.FHS;
   __shared__ int tb[TCH];
   __shared__ double tw[TCH][4];
-  (void)te;
   for (int q = tid; q < nout; q += nth) out[q] = 0.0;
   const int k0 = SB * i;
   // ---- frames
   const int fa = d.node_fr[2 * i], fz = d.node_fr[2 * i + 1];
-  for (int c0 = fa; c0 < fz; c0 += TCH) {
-    const int nt = min(TCH, fz - c0);
+  for (int c0 = fa; c0 < fz; c0 += TCF) {
+    const int nt = min(TCF, fz - c0);
     __syncthreads();
-    for (int q = tid; q < nt * d.FHS; q += nth) tj[(q / d.FHS) * stride + q % d.FHS] = d.FH[(size_t)(c0 + q / d.FHS) * d.FHS + q % d.FHS];
-    if (tid < nt) {
-      tb[tid] = d.fb[c0 + tid];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) tw[tid][j] = d.fw[4 * (c0 + tid) + j];
-    }
+    const double* FHc = d.FH + (size_t)c0 * d.FHS;  // nt consecutive rows
+    ksp_batched<8>(
+        nt * d.FHS + 5 * nt, tid, nth,
+        [&](int q) {
+          const int e = q - nt * d.FHS;
+          return e < 0 ? FHc[q] : e < nt ? (double)d.fb[c0 + e] : d.fw[4 * c0 + e - nt];
+        },
+        [&](int q, double v) {
+          const int e = q - nt * d.FHS;
+          if (e < 0)
+            tj[q] = v;
+          else if (e < nt)
+            tb[e] = (int)v;
+          else
+            tw[(e - nt) / 4][(e - nt) % 4] = v;
+        });
     __syncthreads();
     for (int q = tid; q < nout; q += nth) {
       double s = 0.0;
@@ -627,7 +672,7 @@ __global__ void __launch_bounds__(256) k_sp_assemble(SpDev d) {
     const int nt = min(TCH, mz - c0);
     __syncthreads();
     if (tid < nt) {
-      double* J = tj + tid * stride;
+      double* J = tj + tid * IST;
       imu_sample(d, c0 + tid, J + 144, J, J + 150);  // e at +144, Ct at +150
       tb[tid] = d.ib[c0 + tid];
     }
@@ -640,7 +685,7 @@ __global__ void __launch_bounds__(256) k_sp_assemble(SpDev d) {
         for (int t = 0; t < nt; ++t) {
           const int jr = kr - tb[t], jc = kc - tb[t];
           if (jr < 0 || jr > 3 || jc < 0 || jc > 3) continue;
-          const double* J = tj + t * stride;
+          const double* J = tj + t * IST;
           const int ca = 6 * jr + r % 6, cb = 6 * jc + c % 6;
 #pragma unroll
           for (int z = 0; z < 6; ++z) s += J[z * 24 + ca] * J[z * 24 + cb];
@@ -653,7 +698,7 @@ __global__ void __launch_bounds__(256) k_sp_assemble(SpDev d) {
           for (int t = 0; t < nt; ++t) {
             const int jr = kr - tb[t];
             if (jr < 0 || jr > 3) continue;
-            const double* J = tj + t * stride;
+            const double* J = tj + t * IST;
             const int ca = 6 * jr + r % 6;
             if (a == C) {
 #pragma unroll
@@ -770,6 +815,18 @@ __global__ void __launch_bounds__(64) k_sp_imu_cc(SpDev d) {
 // ---------------------------------------------------------------- k_sp_reduce_cc: H_cc, g_c, cost
 // 64 entries per block; the 4 waves sum interleaved partial rows (8 independent loads in flight per lane),
 // combined in a fixed order.
+// the RW waves' partial sums of one column, combined as a fixed pairwise tree
+__device__ __forceinline__ double red_waves(const double (*red)[64], int lane) {
+  double t[RW];
+#pragma unroll
+  for (int w = 0; w < RW; ++w) t[w] = red[w][lane];
+#pragma unroll
+  for (int h = RW / 2; h > 0; h /= 2)
+#pragma unroll
+    for (int w = 0; w < h; ++w) t[w] += t[w + h];
+  return t[0];
+}
+
 __device__ __forceinline__ double col_sum(const double* p, int rows, int stride, int q, int w0, int ws) {
   double a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   int r = w0;
@@ -781,8 +838,8 @@ __device__ __forceinline__ double col_sum(const double* p, int rows, int stride,
   return ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
 }
 
-__global__ void __launch_bounds__(256) k_sp_reduce_cc(SpDev d) {
-  __shared__ double red[4][64];
+__global__ void __launch_bounds__(64 * RW) k_sp_reduce_cc(SpDev d) {
+  __shared__ double red[RW][64];
   const int C = d.C, nup = C * (C + 1) / 2;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int q = blockIdx.x * 64 + lane;
@@ -802,12 +859,12 @@ __global__ void __launch_bounds__(256) k_sp_reduce_cc(SpDev d) {
       ii = 54;
     }
   }
-  double s = act ? col_sum(d.part, d.nblk_f, d.Wc, q, wave, 4) : 0.0;
-  if (ii >= 0) s += col_sum(d.ipart, d.nblk_ic, WI, ii, wave, 4);
+  double s = act ? col_sum(d.part, d.nblk_f, d.Wc, q, wave, RW) : 0.0;
+  if (ii >= 0) s += col_sum(d.ipart, d.nblk_ic, WI, ii, wave, RW);
   red[wave][lane] = s;
   __syncthreads();
   if (wave != 0 || !act) return;
-  s = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+  s = red_waves(red, lane);
   if (q < nup) {
     d.Hcc[a * C + bcol] = s;
     d.Hcc[bcol * C + a] = s;
@@ -826,12 +883,24 @@ __global__ void __launch_bounds__(256) k_sp_reduce_cc(SpDev d) {
 __global__ void __launch_bounds__(256) k_sp_prep(SpDev d) {
   const int i = blockIdx.x, tid = threadIdx.x, m = d.m;
   const double lam2 = d.sc[SC_LAM2];
-  for (int q = tid; q < NB * NB; q += blockDim.x) {
-    const double v = d.D0[(size_t)i * NB * NB + q];
-    d.D[(size_t)i * NB * NB + q] = (q / NB == q % NB && SB * i + q / (6 * NB) < d.K) ? v + lam2 : v;
-    d.U[(size_t)i * NB * NB + q] = d.U0[(size_t)i * NB * NB + q];
-  }
-  for (int q = tid; q < NB * m; q += blockDim.x) d.R[(size_t)i * NB * m + q] = d.R0[(size_t)i * NB * m + q];
+  const int nd = NB * NB, nr = NB * m;
+  const double* D0 = d.D0 + (size_t)i * nd;
+  const double* U0 = d.U0 + (size_t)i * nd;
+  const double* R0 = d.R0 + (size_t)i * nr;
+  double* D = d.D + (size_t)i * nd;
+  double* Uw = d.U + (size_t)i * nd;
+  double* R = d.R + (size_t)i * nr;
+  ksp_batched<6>(
+      2 * nd + nr, tid, blockDim.x,
+      [&](int q) { return q < nd ? D0[q] : q < 2 * nd ? U0[q - nd] : R0[q - 2 * nd]; },
+      [&](int q, double v) {
+        if (q < nd)
+          D[q] = (q / NB == q % NB && SB * i + q / (6 * NB) < d.K) ? v + lam2 : v;
+        else if (q < 2 * nd)
+          Uw[q - nd] = v;
+        else
+          R[q - 2 * nd] = v;
+      });
   if (i == 0 && tid == 0) d.sc[SC_OK] = 1.0;
 }
 
@@ -843,6 +912,15 @@ __device__ __forceinline__ double rdlane(double v, int l) {
   return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
 }
 
+// 1/x by v_rcp_f64 + two Newton steps (within an ulp of the IEEE quotient)
+__device__ __forceinline__ double ksp_recip(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  double e = fma(-x, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-x, r, 1.0);
+  return fma(r, e, r);
+}
+
 // one-wave register Cholesky of an 18 x 18 SPD matrix held in LDS (lower, row-major): lane r keeps row r in
 // registers, column k broadcast by v_readlane; the factor is written back.  Returns false if not positive
 // definite.  Call from one whole wave.
@@ -851,13 +929,18 @@ __device__ bool chol18_wave(double* A, double* id, int lane) {
 #pragma unroll
   for (int c = 0; c < NB; ++c) a[c] = lane < NB ? A[lane * NB + c] : 0.0;
   bool ok = true;
+  double rid = 1.0;  // lane k: 1 / L_kk
 #pragma unroll
   for (int k = 0; k < NB; ++k) {
     const double dkk = rdlane(a[k], k);
     ok = ok && (dkk > 0.0);
     const double dk = sqrt(dkk > 0.0 ? dkk : 1.0);
-    if (lane == k) a[k] = dk;
-    if (lane > k) a[k] = a[k] / dk;
+    const double rdk = ksp_recip(dk);  // wave-uniform: one reciprocal per step instead of a division per lane
+    if (lane == k) {
+      a[k] = dk;
+      rid = rdk;
+    }
+    if (lane > k) a[k] = a[k] * rdk;
 #pragma unroll
     for (int c = k + 1; c < NB; ++c) {
       const double lck = rdlane(a[k], c);
@@ -868,10 +951,7 @@ __device__ bool chol18_wave(double* A, double* id, int lane) {
   if (lane < NB) {
 #pragma unroll
     for (int c = 0; c < NB; ++c) A[lane * NB + c] = c <= lane ? a[c] : 0.0;
-    double dg = a[0];
-#pragma unroll
-    for (int c = 1; c < NB; ++c) dg = (c == lane) ? a[c] : dg;
-    id[lane] = 1.0 / dg;
+    id[lane] = rid;
   }
   KSP_WAVE_SYNC();
   return ok;
@@ -926,11 +1006,23 @@ __global__ void __launch_bounds__(256) k_sp_elim1(SpDev d) {
   const double* Ul = d.U + (size_t)l * NB * NB;
   const double* Uj = d.U + (size_t)j * NB * NB;
   const double* Rj = d.R + (size_t)j * NB * m;
-  for (int q = tid; q < NB * NB; q += blockDim.x) L[q] = d.D[(size_t)j * NB * NB + q];
-  for (int q = tid; q < NB * wc; q += blockDim.x) {
-    const int row = q / wc, c = q % wc;
-    W[q] = c < NB ? Ul[c * NB + row] : c < 2 * NB ? (r < d.n ? Uj[row * NB + c - NB] : 0.0) : Rj[row * m + c - 2 * NB];
-  }
+  const double* Dj = d.D + (size_t)j * NB * NB;
+  const bool hr = r < d.n;
+  ksp_batched<7>(
+      NB * NB + NB * wc, tid, blockDim.x,
+      [&](int q) {
+        if (q < NB * NB) return Dj[q];
+        const int e = q - NB * NB, row = e / wc, c = e % wc;
+        return c < NB ? Ul[c * NB + row] : c < 2 * NB ? Uj[row * NB + c - NB] : Rj[row * m + c - 2 * NB];
+      },
+      [&](int q, double v) {
+        if (q < NB * NB) {
+          L[q] = v;
+        } else {
+          const int e = q - NB * NB, c = e % wc;
+          W[e] = (c >= NB && c < 2 * NB && !hr) ? 0.0 : v;
+        }
+      });
   __syncthreads();
   if (tid < 64) {
     const bool ok = chol18_wave(L, id, tid);
@@ -960,20 +1052,40 @@ __global__ void __launch_bounds__(256) k_sp_level(SpDev d, int s) {
   double* Zl = sm;
   double* Zr = Zl + NB * wc;
   double* W = Zr + NB * wc;  // [Ui^T | Uo | R']
-  for (int q = tid; q < NB * wc; q += blockDim.x) {
-    Zl[q] = hl ? d.Z[(size_t)jl * NB * wc + q] : 0.0;
-    Zr[q] = hr ? d.Z[(size_t)jr * NB * wc + q] : 0.0;
+  {
+    // Zl | Zr | D_i (into L) | R_i (into W's R columns) in one batch of loads; absent neighbours read node i's Z
+    // slot (any valid address) and store zeros
+    const double* Zsl = d.Z + (size_t)(hl ? jl : i) * NB * wc;
+    const double* Zsr = d.Z + (size_t)(hr ? jr : i) * NB * wc;
+    const double* Di = d.D + (size_t)i * NB * NB;
+    const double* Ri = d.R + (size_t)i * NB * m;
+    const int nz = NB * wc;
+    ksp_batched<15>(
+        2 * nz + NB * NB + NB * m, tid, blockDim.x,
+        [&](int q) {
+          return q < nz ? Zsl[q] : q < 2 * nz ? Zsr[q - nz] : q < 2 * nz + NB * NB ? Di[q - 2 * nz] : Ri[q - 2 * nz - NB * NB];
+        },
+        [&](int q, double v) {
+          if (q < nz) {
+            Zl[q] = hl ? v : 0.0;
+          } else if (q < 2 * nz) {
+            Zr[q - nz] = hr ? v : 0.0;
+          } else if (q < 2 * nz + NB * NB) {
+            L[q - 2 * nz] = v;
+          } else {
+            const int e = q - 2 * nz - NB * NB;
+            W[(e / m) * wc + 2 * NB + e % m] = v;
+          }
+        });
   }
   __syncthreads();
-  const double* Di = d.D + (size_t)i * NB * NB;
-  const double* Ri = d.R + (size_t)i * NB * m;
   for (int q = tid; q < 3 * NB * NB; q += blockDim.x) {
     const int part = q / (NB * NB), e = q % (NB * NB), a = e / NB, b = e % NB;
     double acc = 0.0;
     if (part == 0) {  // D' = D - Zl_U^T Zl_U - Zr_Uin^T Zr_Uin
 #pragma unroll
       for (int k = 0; k < NB; ++k) acc += Zl[k * wc + NB + a] * Zl[k * wc + NB + b] + Zr[k * wc + a] * Zr[k * wc + b];
-      L[e] = Di[e] - acc;
+      L[e] -= acc;
     } else if (part == 1) {  // Uo = -Zr_Uin^T Zr_U
 #pragma unroll
       for (int k = 0; k < NB; ++k) acc += Zr[k * wc + a] * Zr[k * wc + NB + b];
@@ -989,7 +1101,7 @@ __global__ void __launch_bounds__(256) k_sp_level(SpDev d, int s) {
     double acc = 0.0;
 #pragma unroll
     for (int k = 0; k < NB; ++k) acc += Zl[k * wc + NB + a] * Zl[k * wc + 2 * NB + c] + Zr[k * wc + a] * Zr[k * wc + 2 * NB + c];
-    W[a * wc + 2 * NB + c] = Ri[q] - acc;
+    W[a * wc + 2 * NB + c] -= acc;
   }
   __syncthreads();
   if (!elim && !top) {  // stays active: D', U (to i + 2s), R' for the next level
@@ -1049,12 +1161,29 @@ __global__ void __launch_bounds__(256) k_sp_back(SpDev d, int s) {
   double* xl = Z + NB * wc;
   double* xr = xl + NB * m;
   double* T = xr + NB * m;
-  for (int q = tid; q < NB * NB; q += blockDim.x) L[q] = d.Lf[(size_t)j * NB * NB + q];
-  if (tid < NB) id[tid] = d.Lid[(size_t)j * NB + tid];
-  for (int q = tid; q < NB * wc; q += blockDim.x) Z[q] = d.Z[(size_t)j * NB * wc + q];
-  for (int q = tid; q < NB * m; q += blockDim.x) {
-    xl[q] = d.X[(size_t)l * NB * m + q];
-    xr[q] = hr ? d.X[(size_t)r * NB * m + q] : 0.0;
+  {
+    // L_j | 1/diag | Z_j | x_l | x_r in one batch of loads (x_r of an absent neighbour: zeros)
+    const double* Ls = d.Lf + (size_t)j * NB * NB;
+    const double* Is = d.Lid + (size_t)j * NB;
+    const double* Zs = d.Z + (size_t)j * NB * wc;
+    const double* Xl = d.X + (size_t)l * NB * m;
+    const double* Xr = d.X + (size_t)(hr ? r : l) * NB * m;
+    const int n0 = NB * NB, n1 = n0 + NB, n2 = n1 + NB * wc, n3 = n2 + NB * m;
+    ksp_batched<13>(
+        n3 + NB * m, tid, blockDim.x,
+        [&](int q) { return q < n0 ? Ls[q] : q < n1 ? Is[q - n0] : q < n2 ? Zs[q - n1] : q < n3 ? Xl[q - n2] : Xr[q - n3]; },
+        [&](int q, double v) {
+          if (q < n0)
+            L[q] = v;
+          else if (q < n1)
+            id[q - n0] = v;
+          else if (q < n2)
+            Z[q - n1] = v;
+          else if (q < n3)
+            xl[q - n2] = v;
+          else
+            xr[q - n3] = hr ? v : 0.0;
+        });
   }
   __syncthreads();
   // T = Z_R - Z_Uin x_l - Z_U x_r on MFMA tiles: T[row][c] = Z_R[row][c] - sum_k (Z[row][k] xl[k][c] + Z[row][NB + k]
@@ -1098,13 +1227,33 @@ __global__ void __launch_bounds__(256) k_sp_schur(SpDev d) {
   double* acc = Xl + NB * m;  // [Ws]
   for (int q = tid; q < d.Ws; q += blockDim.x) acc[q] = 0.0;
   const int i0 = blockIdx.x * NPB, i1 = min(d.n, i0 + NPB);
+  // node i + 1's R0 | X rows are loaded into registers while node i's products run (2 * 18 * m <= SCH_U * 256 for
+  // m = C + 1 <= MAXC + 1; launched with 256 threads)
+  constexpr int SCH_U = (2 * NB * (MAXC + 1) + 255) / 256;
+  const int nq = 2 * NB * m;
+  double v[SCH_U];
+  auto load = [&](int i) {
+    const double* R0 = d.R0 + (size_t)i * NB * m;
+    const double* X = d.X + (size_t)i * NB * m;
+#pragma unroll
+    for (int u = 0; u < SCH_U; ++u) {
+      const int q = min(tid + u * 256, nq - 1);
+      v[u] = q < NB * m ? R0[q] : X[q - NB * m];
+    }
+  };
+  if (i0 < i1) load(i0);
   for (int i = i0; i < i1; ++i) {
     __syncthreads();
-    for (int q = tid; q < NB * m; q += blockDim.x) {
-      Rl[q] = d.R0[(size_t)i * NB * m + q];
-      Xl[q] = d.X[(size_t)i * NB * m + q];
+#pragma unroll
+    for (int u = 0; u < SCH_U; ++u) {
+      const int q = tid + u * 256;
+      if (q < NB * m)
+        Rl[q] = v[u];
+      else if (q < nq)
+        Xl[q - NB * m] = v[u];
     }
     __syncthreads();
+    if (i + 1 < i1) load(i + 1);
     for (int q = tid; q < d.Ws; q += blockDim.x) {
       const short2 ab = d.uab[q];
       const int a = ab.x, b = ab.y;
@@ -1119,15 +1268,15 @@ __global__ void __launch_bounds__(256) k_sp_schur(SpDev d) {
 }
 
 // S = H_cc + lam2 I - sum_i R0_i^T X_i, b = g_c - sum (4-wave interleaved partial sums), written full
-__global__ void __launch_bounds__(256) k_sp_schur_red(SpDev d) {
-  __shared__ double red[4][64];
+__global__ void __launch_bounds__(64 * RW) k_sp_schur_red(SpDev d) {
+  __shared__ double red[RW][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, C = d.C, nup = C * (C + 1) / 2;
   const int q = blockIdx.x * 64 + lane;
   const bool act = q < d.Ws;
-  red[wave][lane] = act ? col_sum(d.spart, d.nblk_s, d.Ws, q, wave, 4) : 0.0;
+  red[wave][lane] = act ? col_sum(d.spart, d.nblk_s, d.Ws, q, wave, RW) : 0.0;
   __syncthreads();
   if (wave != 0 || !act) return;
-  const double t = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+  const double t = red_waves(red, lane);
   const short2 ab = d.uab[q];
   const int a = ab.x, b = ab.y;
   if (q < nup) {
@@ -1139,54 +1288,44 @@ __global__ void __launch_bounds__(256) k_sp_schur_red(SpDev d) {
   }
 }
 
-// dense camera / IMU block solve on one wave: lane r holds row r of S in registers, Cholesky and both
-// triangular solves with v_readlane broadcasts (CM >= C); dtheta -> dx[0..C)
+// dense camera / IMU block solve on one wave: lane r holds row r of S in registers (CM >= C, padded with the
+// identity so that no step depends on the run-time C), LDL^T with row k broadcast by v_readlane and 1/D_k by
+// rcp + Newton (no square roots or IEEE divisions on the dependent chain), then L y = b, z = D^-1 y, L^T x = z.
+// Lanes i > k apply S[i][j] -= (S[i][k] / D_k) S[k][j]; row i freezes at step i, so lane i ends holding
+// Ltilde[i][k] D_k (k < i) and D_i.  dtheta -> dx[0..C)
 template <int CM>
 __global__ void __launch_bounds__(64) k_sp_camsolve(SpDev d) {
-  __shared__ double Lt[CM * CM];  // L[r][c] at r * CM + c
   const int lane = threadIdx.x, C = d.C;
+  const int li = lane < C ? lane : 0;
   double a[CM];
 #pragma unroll
-  for (int c = 0; c < CM; ++c) a[c] = (lane < C && c < C) ? d.Sf[lane * C + c] : 0.0;
-  double x = lane < C ? d.Sf[C * C + lane] : 0.0;
+  for (int c = 0; c < CM; ++c) a[c] = d.Sf[li * C + (c < C ? c : 0)];  // clamped: every load unconditional
+  double x = d.Sf[C * C + li];
+#pragma unroll
+  for (int c = 0; c < CM; ++c) a[c] = (lane < C && c < C) ? a[c] : (lane == c ? 1.0 : 0.0);
+  x = lane < C ? x : 0.0;
   bool ok = true;
+  double rD = 1.0;
 #pragma unroll
   for (int k = 0; k < CM; ++k) {
-    if (k < C) {
-      const double dkk = rdlane(a[k], k);
-      ok = ok && (dkk > 0.0);
-      const double dk = sqrt(dkk > 0.0 ? dkk : 1.0);
-      if (lane == k) a[k] = dk;
-      if (lane > k) a[k] = a[k] / dk;
+    const double Dk = rdlane(a[k], k);
+    ok = ok && (Dk > 0.0);
+    const double rdk = ksp_recip(Dk);
+    rD = (lane == k) ? rdk : rD;
+    const double f = (lane > k) ? a[k] * rdk : 0.0;
 #pragma unroll
-      for (int c = k + 1; c < CM; ++c) {
-        if (c < C) {
-          const double lck = rdlane(a[k], c);
-          if (lane >= c) a[c] -= a[k] * lck;
-        }
-      }
-    }
+    for (int j = k + 1; j < CM; ++j) a[j] -= f * rdlane(a[j], k);
   }
-  if (lane < C) {
-#pragma unroll
-    for (int c = 0; c < CM; ++c) Lt[lane * CM + c] = a[c];
-  }
-  // L y = b : lane r keeps y_r; column k of L is a[k] of lanes > k
 #pragma unroll
   for (int k = 0; k < CM; ++k) {
-    if (k < C) {
-      const double yk = rdlane(x, k) / rdlane(a[k], k);
-      if (lane == k) x = yk;
-      if (lane > k) x -= a[k] * yk;
-    }
+    const double yk = rdlane(x, k) * rdlane(rD, k);
+    x -= ((lane > k) ? a[k] : 0.0) * yk;
   }
-  KSP_WAVE_SYNC();
-  // L^T x = y : right-looking, row k of L from LDS (lane j reads L[k][j])
-  for (int k = C - 1; k >= 0; --k) {
-    const double lkj = lane < k ? Lt[k * CM + lane] : 0.0;
-    const double xk = __shfl(x, k) / Lt[k * CM + k];
-    if (lane == k) x = xk;
-    x -= lkj * xk;
+  x *= rD;
+#pragma unroll
+  for (int k = CM - 1; k > 0; --k) {
+    const double wk = rdlane(x, k);
+    x -= ((lane < k) ? a[k] * rD : 0.0) * wk;
   }
   if (lane < C) d.dx[lane] = x;
   if (lane == 0 && !ok) d.sc[SC_OK] = 0.0;
@@ -1203,6 +1342,7 @@ __global__ void __launch_bounds__(64) k_sp_update(SpDev d, int apply) {
     if (k < d.K) {
       const double* x = d.X + (size_t)i * NB * m + tid * m;
       double v = x[C];
+#pragma unroll 16
       for (int c = 0; c < C; ++c) v -= x[c] * d.dx[c];
       d.dx[C + 6 * k + tid % 6] = v;
       mx = fabs(v);
@@ -1380,9 +1520,12 @@ __global__ void __launch_bounds__(256) k_sp_mcost_build(SpDev d) {
 __global__ void __launch_bounds__(64) k_sp_cost_reduce(SpDev d, int with_dx) {
   const int tid = threadIdx.x;
   double s = 0.0, mx = 0.0;
+#pragma unroll 8
   for (int q = tid; q < d.nblk_f + d.nblk_ci + (d.mot ? d.nblk_q : 0); q += 64) s += d.cpart[q];
-  if (with_dx)
+  if (with_dx) {
+#pragma unroll 8
     for (int q = tid; q < d.n; q += 64) mx = fmax(mx, d.dmax[q]);
+  }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     s += __shfl_xor(s, o);
@@ -1576,7 +1719,7 @@ int launch_build(kb_sp_handle* h) {
   KSP_HIP(hipLaunchKernel(h->fn_frames, dim3(d.nblk_f), dim3(64 * h->N), args, h->lds_frames, h->stream));
   KSP_HIP(hipLaunchKernel((const void*)k_sp_assemble, dim3(d.n), dim3(256), args, h->lds_asm, h->stream));
   hipLaunchKernelGGL(k_sp_imu_cc, dim3(d.nblk_ic), dim3(64), 0, h->stream, d);
-  hipLaunchKernelGGL(k_sp_reduce_cc, dim3((d.Wc + 63) / 64), dim3(256), 0, h->stream, d);
+  hipLaunchKernelGGL(k_sp_reduce_cc, dim3((d.Wc + 63) / 64), dim3(64 * RW), 0, h->stream, d);
   if (d.mot) hipLaunchKernelGGL(k_sp_mcost_build, dim3(1), dim3(256), 0, h->stream, d);
   return 0;
 }
@@ -1604,7 +1747,7 @@ int launch_solve(kb_sp_handle* h) {
   void* args[] = {&d};
   launch_reduction(h);
   hipLaunchKernelGGL(k_sp_schur, dim3(d.nblk_s), dim3(256), h->lds_schur, h->stream, d);
-  hipLaunchKernelGGL(k_sp_schur_red, dim3((d.Ws + 63) / 64), dim3(256), 0, h->stream, d);
+  hipLaunchKernelGGL(k_sp_schur_red, dim3((d.Ws + 63) / 64), dim3(64 * RW), 0, h->stream, d);
   KSP_HIP(hipLaunchKernel(h->fn_camsolve, dim3(1), dim3(64), args, 0, h->stream));
   return 0;
 }
@@ -1792,9 +1935,10 @@ kb_sp_handle* kb_sp_create(const kb_sp_layout* L) {
   h->lds_level = 3 * h->lds_elim;
   h->lds_back = h->lds_elim + sizeof(double) * 3 * NB * d.m;
   h->lds_schur = sizeof(double) * (2 * NB * d.m + d.Ws);
-  h->lds_asm = sizeof(double) * (2 * NB * NB + NB * d.m + TCH * std::max(144 + 15, d.FHS));
+  h->lds_asm = sizeof(double) * (2 * NB * NB + NB * d.m + std::max(TCH * IST, TCF * d.FHS));
   h->lds_frames = sizeof(double) * (h->N * 64 * XS + h->N * 256 + 2 * h->N * 36 + 2 * h->N * h->N * 36 + d.Wc +
-                                    3 * L->n_target);
+                                    3 * L->n_target) +
+                  sizeof(short2) * d.Wc + sizeof(int) * 3 * d.C;
   if (h->lds_frames > 160 * 1024 || h->lds_asm > 160 * 1024 || h->lds_schur > 160 * 1024) {
     fail("kb_sp_create: LDS budget exceeded for this rig");
     kb_sp_destroy(h);
@@ -2322,13 +2466,13 @@ int kb_sp_kernel_stats(kb_sp_handle* h, int32_t n, double* ms_out6, double* fram
     KSP_HIP(hipEventRecord(ev[1], h->stream));
     KSP_HIP(hipLaunchKernel((const void*)k_sp_assemble, dim3(d.n), dim3(256), args, h->lds_asm, h->stream));
     hipLaunchKernelGGL(k_sp_imu_cc, dim3(d.nblk_ic), dim3(64), 0, h->stream, d);
-    hipLaunchKernelGGL(k_sp_reduce_cc, dim3((d.Wc + 63) / 64), dim3(256), 0, h->stream, d);
+    hipLaunchKernelGGL(k_sp_reduce_cc, dim3((d.Wc + 63) / 64), dim3(64 * RW), 0, h->stream, d);
     if (d.mot) hipLaunchKernelGGL(k_sp_mcost_build, dim3(1), dim3(256), 0, h->stream, d);
     KSP_HIP(hipEventRecord(ev[2], h->stream));
     launch_reduction(h);
     KSP_HIP(hipEventRecord(ev[3], h->stream));
     hipLaunchKernelGGL(k_sp_schur, dim3(d.nblk_s), dim3(256), h->lds_schur, h->stream, d);
-    hipLaunchKernelGGL(k_sp_schur_red, dim3((d.Ws + 63) / 64), dim3(256), 0, h->stream, d);
+    hipLaunchKernelGGL(k_sp_schur_red, dim3((d.Ws + 63) / 64), dim3(64 * RW), 0, h->stream, d);
     KSP_HIP(hipLaunchKernel(h->fn_camsolve, dim3(1), dim3(64), args, 0, h->stream));
     KSP_HIP(hipEventRecord(ev[4], h->stream));
     hipLaunchKernelGGL(k_sp_update, dim3(d.n), dim3(64), 0, h->stream, d, 1);

@@ -25,7 +25,7 @@ def main():
     write, nw = per_kernel(f"{d}/pmc_write/pmc_counter_collection.csv", "WRITE_SIZE")
     res = {}
     for k in sorted(set(fetch) | set(write)):
-        if not k.startswith(("kb::", "void kb::")):
+        if not k.startswith(("kb::", "void kb::", "ksp::", "void ksp::")):
             continue
         f_kib, w_kib = fetch.get(k, 0.0), write.get(k, 0.0)
         res[k] = {"dispatches": [nf.get(k, 0), nw.get(k, 0)], "FETCH_SIZE_KiB": f_kib, "WRITE_SIZE_KiB": w_kib,
