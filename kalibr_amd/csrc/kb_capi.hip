@@ -113,6 +113,7 @@ struct kb_handle {
   int N = 0, F = 0, K = 0, V = 0, NC = 0, C = 0, ncols = 0, S = 0, W = 0;
   int WPB = 1;
   bool build_pipe = false;  // k_buildp (one wave per camera, N + 2 waves) instead of k_build
+  bool buildp_wide = false;  // k_buildp<.., MW = 8> (multi-model rigs with <= 8 waves per block)
   int build_threads = 64;
   size_t lds_build = 0, lds_camexp = 0, lds_schur = 0, lds_solve = 0;
   int solve_threads = 64;
@@ -171,26 +172,30 @@ struct kb_handle {
 
 // mb: Schur tiles per wave of k_build (1 | 4 | 7), or per frame wave of k_buildp (5: 2 frame waves | 7: 4) when pipe
 template <bool GN, unsigned MM>
-static const void* build_fn(int mb, bool pipe) {
-  if (pipe) return mb == 5 ? (const void*)k_buildp<5, GN, MM> : (const void*)k_buildp<7, GN, MM>;
+static const void* build_fn(int mb, bool pipe, bool wide) {
+  constexpr int MWN = kBuildpMaxCams + 4;
+  if constexpr (__builtin_popcount(MM) >= 2) {  // multi-model view roles: the spill-free 8-wave variant
+    if (pipe && wide) return mb == 5 ? (const void*)k_buildp<5, GN, MM, 8> : (const void*)k_buildp<7, GN, MM, 8>;
+  }
+  if (pipe) return mb == 5 ? (const void*)k_buildp<5, GN, MM, MWN> : (const void*)k_buildp<7, GN, MM, MWN>;
   return mb == 1 ? (const void*)k_build<1, GN, MM> : mb == 4 ? (const void*)k_build<4, GN, MM>
                                                              : (const void*)k_build<7, GN, MM>;
 }
 
 // Build kernel for the rig's camera-model set `mm` (bit m = model m present).
 template <bool GN>
-static const void* pick_build(int mb, unsigned mm, bool pipe) {
+static const void* pick_build(int mb, unsigned mm, bool pipe, bool wide) {
   switch (mm) {
-    case 1u << KB_PINHOLE_RADTAN: return build_fn<GN, 1u << KB_PINHOLE_RADTAN>(mb, pipe);
-    case 1u << KB_OMNI_RADTAN: return build_fn<GN, 1u << KB_OMNI_RADTAN>(mb, pipe);
-    case 1u << KB_EUCM: return build_fn<GN, 1u << KB_EUCM>(mb, pipe);
-    case 1u << KB_OMNI: return build_fn<GN, 1u << KB_OMNI>(mb, pipe);
-    case 1u << KB_DS: return build_fn<GN, 1u << KB_DS>(mb, pipe);
-    case 1u << KB_PINHOLE_EQUI: return build_fn<GN, 1u << KB_PINHOLE_EQUI>(mb, pipe);
-    case 1u << KB_PINHOLE_FOV: return build_fn<GN, 1u << KB_PINHOLE_FOV>(mb, pipe);
+    case 1u << KB_PINHOLE_RADTAN: return build_fn<GN, 1u << KB_PINHOLE_RADTAN>(mb, pipe, wide);
+    case 1u << KB_OMNI_RADTAN: return build_fn<GN, 1u << KB_OMNI_RADTAN>(mb, pipe, wide);
+    case 1u << KB_EUCM: return build_fn<GN, 1u << KB_EUCM>(mb, pipe, wide);
+    case 1u << KB_OMNI: return build_fn<GN, 1u << KB_OMNI>(mb, pipe, wide);
+    case 1u << KB_DS: return build_fn<GN, 1u << KB_DS>(mb, pipe, wide);
+    case 1u << KB_PINHOLE_EQUI: return build_fn<GN, 1u << KB_PINHOLE_EQUI>(mb, pipe, wide);
+    case 1u << KB_PINHOLE_FOV: return build_fn<GN, 1u << KB_PINHOLE_FOV>(mb, pipe, wide);
     case (1u << KB_OMNI_RADTAN) | (1u << KB_EUCM):
-      return build_fn<GN, (1u << KB_OMNI_RADTAN) | (1u << KB_EUCM)>(mb, pipe);
-    default: return build_fn<GN, kMmAll>(mb, pipe);
+      return build_fn<GN, (1u << KB_OMNI_RADTAN) | (1u << KB_EUCM)>(mb, pipe, wide);
+    default: return build_fn<GN, kMmAll>(mb, pipe, wide);
   }
 }
 
@@ -333,7 +338,13 @@ kb_handle* kb_create(const kb_layout* L) {
   if (h->build_pipe) {
     // all blocks resident at once: one block per CU (two for rigs whose block fits twice: 12 waves per CU at the
     // kernel's <= 168 VGPRs, half the LDS), each running its frames through the pipeline
-    const int bpc = (h->N + nf <= 6) ? 2 : 1;
+    // rigs whose view role compiles several projection models and whose block has <= 8 waves use the 8-wave
+    // (256-VGPR, spill-free) build kernel, one block per CU; KB_BUILDP_WIDE=0 keeps the 12-wave variant
+    unsigned mm0 = 0;
+    for (int i = 0; i < h->N; ++i) mm0 |= 1u << d.model[i];
+    h->buildp_wide = __builtin_popcount(mm0) >= 2 && h->N + nf <= 8;
+    if (const char* e = std::getenv("KB_BUILDP_WIDE")) h->buildp_wide = h->buildp_wide && std::atoi(e) != 0;
+    const int bpc = (h->N + nf <= 6 && !h->buildp_wide) ? 2 : 1;
     d.gframes = (h->F + 256 * bpc - 1) / (256 * bpc);
   } else {
     d.gframes = (h->F + 511) / 512;
@@ -459,8 +470,8 @@ kb_handle* kb_create(const kb_layout* L) {
     // kernels; any other mix uses the all-models instantiation
     unsigned mm = 0;
     for (int i = 0; i < h->N; ++i) mm |= 1u << d.model[i];
-    h->fn_build = pick_build<false>(h->mb, mm, h->build_pipe);
-    h->fn_build_gn = pick_build<true>(h->mb, mm, h->build_pipe);
+    h->fn_build = pick_build<false>(h->mb, mm, h->build_pipe, h->buildp_wide);
+    h->fn_build_gn = pick_build<true>(h->mb, mm, h->build_pipe, h->buildp_wide);
     h->fn_schur = h->ms == 1 ? (const void*)k_schur<1> : h->ms == 4 ? (const void*)k_schur<4> : (const void*)k_schur<7>;
   }
   hipFuncSetAttribute(h->fn_build, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_build);

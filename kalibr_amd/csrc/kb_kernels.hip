@@ -1084,8 +1084,11 @@ __device__ __forceinline__ void schur_tiles_accumulate6(const double* P, const d
   }
 }
 
-template <int TT, bool GNF, unsigned MM>
-__global__ void __launch_bounds__(64 * (kBuildpMaxCams + 4)) k_buildp(KbDev d, int gate, int fuse) {
+// MW: the most waves a block may have.  12 (8 cameras + 4 frame waves) caps the kernel at 168 VGPRs, so that two
+// 6-wave blocks share a CU; rigs with N + frame waves <= 8 whose view role compiles two projection models
+// (configs[2]) take MW = 8 (256 VGPRs, no spills, one block per CU) -- kb_capi.hip `buildp_wide`.
+template <int TT, bool GNF, unsigned MM, int MW>
+__global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse) {
   KbCtrl* c = d.ctrl;
   extern __shared__ __attribute__((aligned(16))) double sm[];
   constexpr int NF = buildp_nf<TT>();

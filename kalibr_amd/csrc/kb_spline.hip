@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -38,7 +39,7 @@ constexpr int FPB = 2;      // frames per k_sp_frames block (600 blocks at confi
 constexpr int RW = 16;      // waves of the column-sum kernels (k_sp_reduce_cc, k_sp_schur_red)
 constexpr int XS = 17;      // LDS row stride of the 64 x 16 Jacobian-row tile
 constexpr int WI = 55;      // IMU theta partial row: 9x9 upper (45) | g (9) | cost
-constexpr int NPB = 8;      // nodes per k_sp_schur block
+constexpr int NPB = 4;      // nodes per k_sp_schur block
 constexpr int TCH = 32;     // IMU samples staged per k_sp_assemble chunk
 constexpr int TCF = 8;      // frames staged per k_sp_assemble chunk
 constexpr int IST = 144 + 15;  // LDS stride of a staged IMU sample: J [6][24] | e [6] | C^T [9]
@@ -87,6 +88,8 @@ struct SpDev {
   const double* QD;       // [n][324] Q blocks within node i
   const double* QU;       // [n][324] Q block node i (rows) -> node i + 1 (columns)
   double* mcost;          // [n] per-node motion cost at the build state
+  int dbg_stop;           // diagnostics only (KSP_DBG_STOP): 0, or the phase after which the timed kernels return
+  int zero_lam;           // GN pass: k_sp_imu_cc sets lambda^2 = 0 (no separate launch)
 };
 
 typedef double v4d_t __attribute__((ext_vector_type(4)));
@@ -666,8 +669,11 @@ __global__ void __launch_bounds__(256) k_sp_assemble(SpDev d) {
       out[q] += s;
     }
   }
+  if (d.dbg_stop == 1) return;
   // ---- IMU samples
   const int ma = d.node_im[2 * i], mz = d.node_im[2 * i + 1];
+  const int wave = tid >> 6, lane = tid & 63;
+  v4d_t iacc[2] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
   for (int c0 = ma; c0 < mz; c0 += TCH) {
     const int nt = min(TCH, mz - c0);
     __syncthreads();
@@ -677,40 +683,57 @@ __global__ void __launch_bounds__(256) k_sp_assemble(SpDev d) {
       tb[tid] = d.ib[c0 + tid];
     }
     __syncthreads();
-    for (int q = tid; q < nout; q += nth) {
-      double s = 0.0;
-      if (q < 2 * NB * NB) {
-        const int blk = q / (NB * NB), e = q % (NB * NB), r = e / NB, c = e % NB;
-        const int kr = k0 + r / 6, kc = k0 + SB * blk + c / 6;
-        for (int t = 0; t < nt; ++t) {
-          const int jr = kr - tb[t], jc = kc - tb[t];
-          if (jr < 0 || jr > 3 || jc < 0 || jc > 3) continue;
-          const double* J = tj + t * IST;
-          const int ca = 6 * jr + r % 6, cb = 6 * jc + c % 6;
+    if (d.dbg_stop == 2) return;
+    // Jn^T [Jw | J_theta | -e] over the chunk's 6 nt residual rows: Jn = the samples' Jacobian columns of this
+    // node's 18 rows, Jw those of nodes i and i + 1 (D_i | U_i), J_theta the 9 IMU columns, e the whitened
+    // residual.  A 2 x 3 grid of 16 x 16 tiles (rows 0..17, columns 0..35 D | U, 36..44 IMU, 45 g), tiles wave and
+    // wave + 4, k = 4 st + (lane >> 4) = 6 t + z
+    const int ks = (6 * nt + 3) / 4;
 #pragma unroll
-          for (int z = 0; z < 6; ++z) s += J[z * 24 + ca] * J[z * 24 + cb];
-        }
-      } else {
-        const int e = q - 2 * NB * NB, r = e / m, a = e % m;
-        const int kr = k0 + r / 6;
-        const bool imu_col = a >= d.col_imu && a < d.col_imu + 9;
-        if (a == C || imu_col) {
-          for (int t = 0; t < nt; ++t) {
-            const int jr = kr - tb[t];
-            if (jr < 0 || jr > 3) continue;
+    for (int u = 0; u < 2; ++u) {
+      const int tile = wave + 4 * u;
+      if (tile < 6) {  // wave-uniform
+        const int ir = 16 * (tile / 3) + (lane & 15), jc = 16 * (tile % 3) + (lane & 15);
+        for (int st = 0; st < ks; ++st) {
+          const int k = 4 * st + (lane >> 4), t = k / 6, z = k % 6;
+          double av = 0.0, bv = 0.0;
+          if (t < nt) {
             const double* J = tj + t * IST;
-            const int ca = 6 * jr + r % 6;
-            if (a == C) {
-#pragma unroll
-              for (int z = 0; z < 6; ++z) s -= J[z * 24 + ca] * J[144 + z];
-            } else {
-#pragma unroll
-              for (int z = 0; z < 6; ++z) s += J[z * 24 + ca] * imu_jth(d, J + 150, z, a - d.col_imu);
+            const int jr = k0 + ir / 6 - tb[t];
+            if (ir < NB && jr >= 0 && jr <= 3) av = J[z * 24 + 6 * jr + ir % 6];
+            if (jc < 2 * NB) {
+              const int jj = k0 + jc / 6 - tb[t];
+              if (jj >= 0 && jj <= 3) bv = J[z * 24 + 6 * jj + jc % 6];
+            } else if (jc < 2 * NB + 9) {
+              bv = imu_jth(d, J + 150, z, jc - 2 * NB);
+            } else if (jc == 2 * NB + 9) {
+              bv = -J[144 + z];
             }
           }
+          iacc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, iacc[u], 0, 0, 0);
         }
       }
-      out[q] += s;
+    }
+  }
+  __syncthreads();  // frame sums complete (they are owned per entry q, the tiles per lane)
+  // f64 MFMA C/D layout: lane l, reg r -> row (l >> 4) + 4 r, column l & 15
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int tile = wave + 4 * u;
+    if (tile < 6 && ma < mz) {
+      const int jc = 16 * (tile % 3) + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * (tile / 3) + (lane >> 4) + 4 * r;
+        if (row < NB) {
+          if (jc < 2 * NB)
+            out[(jc < NB ? 0 : NB * NB) + row * NB + jc % NB] += iacc[u][r];
+          else if (jc < 2 * NB + 9)
+            out[2 * NB * NB + row * m + d.col_imu + jc - 2 * NB] += iacc[u][r];
+          else if (jc == 2 * NB + 9)
+            out[2 * NB * NB + row * m + C] += iacc[u][r];
+        }
+      }
     }
   }
   __syncthreads();
@@ -774,6 +797,10 @@ __global__ void __launch_bounds__(64) k_sp_imu_cc(SpDev d) {
   const int lane = threadIdx.x, m = blockIdx.x * 64 + lane;
   double e[6] = {0, 0, 0, 0, 0, 0}, Ct[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
   const bool has = m < d.M;
+  if (d.zero_lam && m == 0) {  // k_sp_set_lam(0) of a GN pass, before the reduction reads it (same stream)
+    d.sc[SC_LAM2] = 0.0;
+    d.sc[SC_OK] = 1.0;
+  }
   if (has) imu_sample(d, m, e, nullptr, Ct);
   // J_theta = [-ig I, 0, 0; 0, -ia I, ia C^T] (rows gyro | accel; columns b_g | b_a | g_w)
   const double ig2 = d.ig * d.ig, ia2 = d.ia * d.ia;
@@ -877,33 +904,16 @@ __global__ void __launch_bounds__(64 * RW) k_sp_reduce_cc(SpDev d) {
 }
 
 // ---------------------------------------------------------------- cyclic reduction
+// The first elimination level and the first fused level read the built blocks D0 / U0 / R0 directly (the working
+// copies D / U / R are written from the second level on): D_i = D0_i + lambda^2 I on the rows of real
+// coefficients (padded rows keep their identity diagonal).
+__device__ __forceinline__ double lam_diag(const SpDev& d, int i, int q, double lam2) {
+  return (q / NB == q % NB && SB * i + q / (6 * NB) < d.K) ? lam2 : 0.0;
+}
+
 // Block-tridiagonal SPD system over nodes: D_i x_i + U_{i-1}^T x_{i-1} + U_i x_{i+1} = R_i (18 x m RHS).
 // Level stride s: nodes i % 2s == s are eliminated (Cholesky L_j, Z_j = L_j^-1 [U_l^T | U_j | R_j]),
 // nodes i % 2s == 0 absorb them; the back-substitution runs the levels in reverse.
-__global__ void __launch_bounds__(256) k_sp_prep(SpDev d) {
-  const int i = blockIdx.x, tid = threadIdx.x, m = d.m;
-  const double lam2 = d.sc[SC_LAM2];
-  const int nd = NB * NB, nr = NB * m;
-  const double* D0 = d.D0 + (size_t)i * nd;
-  const double* U0 = d.U0 + (size_t)i * nd;
-  const double* R0 = d.R0 + (size_t)i * nr;
-  double* D = d.D + (size_t)i * nd;
-  double* Uw = d.U + (size_t)i * nd;
-  double* R = d.R + (size_t)i * nr;
-  ksp_batched<6>(
-      2 * nd + nr, tid, blockDim.x,
-      [&](int q) { return q < nd ? D0[q] : q < 2 * nd ? U0[q - nd] : R0[q - 2 * nd]; },
-      [&](int q, double v) {
-        if (q < nd)
-          D[q] = (q / NB == q % NB && SB * i + q / (6 * NB) < d.K) ? v + lam2 : v;
-        else if (q < 2 * nd)
-          Uw[q - nd] = v;
-        else
-          R[q - 2 * nd] = v;
-      });
-  if (i == 0 && tid == 0) d.sc[SC_OK] = 1.0;
-}
-
 // broadcast of lane l's double (l wave-uniform)
 __device__ __forceinline__ double rdlane(double v, int l) {
   const unsigned long long u = (unsigned long long)__double_as_longlong(v);
@@ -936,15 +946,14 @@ __device__ bool chol18_wave(double* A, double* id, int lane) {
     ok = ok && (dkk > 0.0);
     const double dk = sqrt(dkk > 0.0 ? dkk : 1.0);
     const double rdk = ksp_recip(dk);  // wave-uniform: one reciprocal per step instead of a division per lane
-    if (lane == k) {
-      a[k] = dk;
-      rid = rdk;
-    }
-    if (lane > k) a[k] = a[k] * rdk;
+    // selects instead of lane-conditional blocks: no exec-mask save / restore around each update
+    rid = (lane == k) ? rdk : rid;
+    a[k] = (lane == k) ? dk : (lane > k) ? a[k] * rdk : a[k];
+    const double lk = (lane > k) ? a[k] : 0.0;  // rows above the pivot take no update
 #pragma unroll
     for (int c = k + 1; c < NB; ++c) {
       const double lck = rdlane(a[k], c);
-      if (lane >= c) a[c] -= a[k] * lck;
+      a[c] -= ((lane >= c) ? lk : 0.0) * lck;
     }
   }
   KSP_WAVE_SYNC();
@@ -1003,10 +1012,11 @@ __global__ void __launch_bounds__(256) k_sp_elim1(SpDev d) {
   const int j = 1 + 2 * blockIdx.x, tid = threadIdx.x, m = d.m, wc = 36 + m;
   if (j >= d.n) return;
   const int l = j - 1, r = j + 1;
-  const double* Ul = d.U + (size_t)l * NB * NB;
-  const double* Uj = d.U + (size_t)j * NB * NB;
-  const double* Rj = d.R + (size_t)j * NB * m;
-  const double* Dj = d.D + (size_t)j * NB * NB;
+  const double* Ul = d.U0 + (size_t)l * NB * NB;
+  const double* Uj = d.U0 + (size_t)j * NB * NB;
+  const double* Rj = d.R0 + (size_t)j * NB * m;
+  const double* Dj = d.D0 + (size_t)j * NB * NB;
+  const double lam2 = d.sc[SC_LAM2];
   const bool hr = r < d.n;
   ksp_batched<7>(
       NB * NB + NB * wc, tid, blockDim.x,
@@ -1017,7 +1027,7 @@ __global__ void __launch_bounds__(256) k_sp_elim1(SpDev d) {
       },
       [&](int q, double v) {
         if (q < NB * NB) {
-          L[q] = v;
+          L[q] = v + lam_diag(d, j, q, lam2);
         } else {
           const int e = q - NB * NB, c = e % wc;
           W[e] = (c >= NB && c < 2 * NB && !hr) ? 0.0 : v;
@@ -1057,8 +1067,9 @@ __global__ void __launch_bounds__(256) k_sp_level(SpDev d, int s) {
     // slot (any valid address) and store zeros
     const double* Zsl = d.Z + (size_t)(hl ? jl : i) * NB * wc;
     const double* Zsr = d.Z + (size_t)(hr ? jr : i) * NB * wc;
-    const double* Di = d.D + (size_t)i * NB * NB;
-    const double* Ri = d.R + (size_t)i * NB * m;
+    const double* Di = (s == 1 ? d.D0 : d.D) + (size_t)i * NB * NB;
+    const double* Ri = (s == 1 ? d.R0 : d.R) + (size_t)i * NB * m;
+    const double lam2 = s == 1 ? d.sc[SC_LAM2] : 0.0;
     const int nz = NB * wc;
     ksp_batched<15>(
         2 * nz + NB * NB + NB * m, tid, blockDim.x,
@@ -1071,7 +1082,7 @@ __global__ void __launch_bounds__(256) k_sp_level(SpDev d, int s) {
           } else if (q < 2 * nz) {
             Zr[q - nz] = hr ? v : 0.0;
           } else if (q < 2 * nz + NB * NB) {
-            L[q - 2 * nz] = v;
+            L[q - 2 * nz] = v + lam_diag(d, i, q - 2 * nz, lam2);
           } else {
             const int e = q - 2 * nz - NB * NB;
             W[(e / m) * wc + 2 * NB + e % m] = v;
@@ -1079,6 +1090,7 @@ __global__ void __launch_bounds__(256) k_sp_level(SpDev d, int s) {
         });
   }
   __syncthreads();
+  if (d.dbg_stop == 1) return;
   for (int q = tid; q < 3 * NB * NB; q += blockDim.x) {
     const int part = q / (NB * NB), e = q % (NB * NB), a = e / NB, b = e % NB;
     double acc = 0.0;
@@ -1104,6 +1116,7 @@ __global__ void __launch_bounds__(256) k_sp_level(SpDev d, int s) {
     W[a * wc + 2 * NB + c] -= acc;
   }
   __syncthreads();
+  if (d.dbg_stop == 2) return;
   if (!elim && !top) {  // stays active: D', U (to i + 2s), R' for the next level
     for (int q = tid; q < NB * NB; q += blockDim.x) {
       d.D[(size_t)i * NB * NB + q] = L[q];
@@ -1122,12 +1135,14 @@ __global__ void __launch_bounds__(256) k_sp_level(SpDev d, int s) {
     if (!ok && tid == 0) d.sc[SC_OK] = 0.0;
   }
   __syncthreads();
+  if (d.dbg_stop == 3) return;
   if (top) {  // X_0 = L^-T L^-1 R' (forward in place in W, then backward into X_0)
     node_forward(L, id, W + 2 * NB, wc, m, W + 2 * NB, wc, tid);
     node_backsolve(L, id, W + 2 * NB, wc, m, d.X, tid);
     return;
   }
   node_forward(L, id, W, wc, wc, d.Z + (size_t)i * NB * wc, wc, tid);
+  if (d.dbg_stop == 4) return;
   for (int q = tid; q < NB * NB; q += blockDim.x) d.Lf[(size_t)i * NB * NB + q] = L[q];
   if (tid < NB) d.Lid[(size_t)i * NB + tid] = id[tid];
 }
@@ -1137,8 +1152,9 @@ __global__ void __launch_bounds__(256) k_sp_top(SpDev d) {
   __shared__ double id[NB];
   extern __shared__ __attribute__((aligned(16))) double T[];  // [18][m]
   const int tid = threadIdx.x, m = d.m;
-  for (int q = tid; q < NB * NB; q += blockDim.x) L[q] = d.D[q];
-  for (int q = tid; q < NB * m; q += blockDim.x) T[q] = d.R[q];
+  const double lam2 = d.sc[SC_LAM2];
+  for (int q = tid; q < NB * NB; q += blockDim.x) L[q] = d.D0[q] + lam_diag(d, 0, q, lam2);
+  for (int q = tid; q < NB * m; q += blockDim.x) T[q] = d.R0[q];
   __syncthreads();
   if (tid < 64) {
     const bool ok = chol18_wave(L, id, tid);
@@ -1186,6 +1202,7 @@ __global__ void __launch_bounds__(256) k_sp_back(SpDev d, int s) {
         });
   }
   __syncthreads();
+  if (d.dbg_stop == 1) return;
   // T = Z_R - Z_Uin x_l - Z_U x_r on MFMA tiles: T[row][c] = Z_R[row][c] - sum_k (Z[row][k] xl[k][c] + Z[row][NB + k]
   // xr[k][c]); A = Z^T is read from the Z rows (stride 1 in k), B from xl / xr
   {
@@ -1214,6 +1231,7 @@ __global__ void __launch_bounds__(256) k_sp_back(SpDev d, int s) {
     }
   }
   __syncthreads();
+  if (d.dbg_stop == 2) return;
   node_backsolve(L, id, T, m, m, d.X + (size_t)j * NB * m, tid);
 }
 
@@ -1225,7 +1243,11 @@ __global__ void __launch_bounds__(256) k_sp_schur(SpDev d) {
   double* Rl = sm;
   double* Xl = sm + NB * m;
   double* acc = Xl + NB * m;  // [Ws]
-  for (int q = tid; q < d.Ws; q += blockDim.x) acc[q] = 0.0;
+  short2* tab = (short2*)(acc + d.Ws);  // [Ws] (a, b) of the entries, read for every node
+  for (int q = tid; q < d.Ws; q += blockDim.x) {
+    acc[q] = 0.0;
+    tab[q] = d.uab[q];
+  }
   const int i0 = blockIdx.x * NPB, i1 = min(d.n, i0 + NPB);
   // node i + 1's R0 | X rows are loaded into registers while node i's products run (2 * 18 * m <= SCH_U * 256 for
   // m = C + 1 <= MAXC + 1; launched with 256 threads)
@@ -1255,7 +1277,7 @@ __global__ void __launch_bounds__(256) k_sp_schur(SpDev d) {
     __syncthreads();
     if (i + 1 < i1) load(i + 1);
     for (int q = tid; q < d.Ws; q += blockDim.x) {
-      const short2 ab = d.uab[q];
+      const short2 ab = tab[q];
       const int a = ab.x, b = ab.y;
       double s = 0.0;
 #pragma unroll
@@ -1542,8 +1564,12 @@ __global__ void k_sp_revert(SpDev d) {
   if (q < d.S) d.state[q] = d.backup[q];
 }
 
+// lambda^2 of the next solve, and its success flag reset (the reduction kernels clear it on a failed factorisation)
 __global__ void k_sp_set_lam(SpDev d, double lam2) {
-  if (threadIdx.x == 0) d.sc[SC_LAM2] = lam2;
+  if (threadIdx.x == 0) {
+    d.sc[SC_LAM2] = lam2;
+    d.sc[SC_OK] = 1.0;
+  }
 }
 
 }  // namespace ksp
@@ -1717,8 +1743,8 @@ int launch_build(kb_sp_handle* h) {
   SpDev& d = h->d;
   void* args[] = {&d};
   KSP_HIP(hipLaunchKernel(h->fn_frames, dim3(d.nblk_f), dim3(64 * h->N), args, h->lds_frames, h->stream));
+  hipLaunchKernelGGL(k_sp_imu_cc, dim3(d.nblk_ic), dim3(64), 0, h->stream, d);  // sets lambda^2 = 0 in a GN pass
   KSP_HIP(hipLaunchKernel((const void*)k_sp_assemble, dim3(d.n), dim3(256), args, h->lds_asm, h->stream));
-  hipLaunchKernelGGL(k_sp_imu_cc, dim3(d.nblk_ic), dim3(64), 0, h->stream, d);
   hipLaunchKernelGGL(k_sp_reduce_cc, dim3((d.Wc + 63) / 64), dim3(64 * RW), 0, h->stream, d);
   if (d.mot) hipLaunchKernelGGL(k_sp_mcost_build, dim3(1), dim3(256), 0, h->stream, d);
   return 0;
@@ -1726,7 +1752,6 @@ int launch_build(kb_sp_handle* h) {
 
 int launch_reduction(kb_sp_handle* h) {
   SpDev& d = h->d;
-  hipLaunchKernelGGL(k_sp_prep, dim3(d.n), dim3(256), 0, h->stream, d);
   if (d.n == 1) {
     hipLaunchKernelGGL(k_sp_top, dim3(1), dim3(256), sizeof(double) * NB * d.m, h->stream, d);
     return 0;
@@ -1765,8 +1790,10 @@ int launch_cost(kb_sp_handle* h, int with_dx) {
 // one GN pass: build, solve (lambda = 0), update, cost
 int enqueue_gn_pass(kb_sp_handle* h) {
   SpDev& d = h->d;
-  hipLaunchKernelGGL(k_sp_set_lam, dim3(1), dim3(64), 0, h->stream, d, 0.0);
-  if (launch_build(h)) return -1;
+  d.zero_lam = 1;  // lambda = 0 written by the build's k_sp_imu_cc
+  const int rb = launch_build(h);
+  d.zero_lam = 0;
+  if (rb) return -1;
   if (launch_solve(h)) return -1;
   hipLaunchKernelGGL(k_sp_update, dim3(d.n), dim3(64), 0, h->stream, d, 1);
   return launch_cost(h, 1);
@@ -1934,7 +1961,7 @@ kb_sp_handle* kb_sp_create(const kb_sp_layout* L) {
   h->lds_elim = sizeof(double) * NB * (36 + d.m);
   h->lds_level = 3 * h->lds_elim;
   h->lds_back = h->lds_elim + sizeof(double) * 3 * NB * d.m;
-  h->lds_schur = sizeof(double) * (2 * NB * d.m + d.Ws);
+  h->lds_schur = sizeof(double) * (2 * NB * d.m + d.Ws) + sizeof(short2) * d.Ws;
   h->lds_asm = sizeof(double) * (2 * NB * NB + NB * d.m + std::max(TCH * IST, TCF * d.FHS));
   h->lds_frames = sizeof(double) * (h->N * 64 * XS + h->N * 256 + 2 * h->N * 36 + 2 * h->N * h->N * 36 + d.Wc +
                                     3 * L->n_target) +
@@ -2048,6 +2075,7 @@ int kb_sp_upload(kb_sp_handle* h, int32_t n_frames, const double* frame_time, in
   rc |= h->alloc(&d.FH, (size_t)F * d.FHS);
   rc |= h->alloc(&d.part, (size_t)d.nblk_f * d.Wc);
   d.nblk_q = (h->n + 63) / 64;
+  if (const char* e = std::getenv("KSP_DBG_STOP")) d.dbg_stop = std::atoi(e);
   rc |= h->alloc(&d.cpart, (size_t)(d.nblk_f + d.nblk_ci + d.nblk_q));
   rc |= h->alloc(&d.mcost, (size_t)h->n);
   rc |= h->alloc(&d.ipart, (size_t)d.nblk_ic * WI);
@@ -2464,8 +2492,8 @@ int kb_sp_kernel_stats(kb_sp_handle* h, int32_t n, double* ms_out6, double* fram
     KSP_HIP(hipEventRecord(ev[0], h->stream));
     KSP_HIP(hipLaunchKernel(h->fn_frames, dim3(d.nblk_f), dim3(64 * h->N), args, h->lds_frames, h->stream));
     KSP_HIP(hipEventRecord(ev[1], h->stream));
-    KSP_HIP(hipLaunchKernel((const void*)k_sp_assemble, dim3(d.n), dim3(256), args, h->lds_asm, h->stream));
     hipLaunchKernelGGL(k_sp_imu_cc, dim3(d.nblk_ic), dim3(64), 0, h->stream, d);
+    KSP_HIP(hipLaunchKernel((const void*)k_sp_assemble, dim3(d.n), dim3(256), args, h->lds_asm, h->stream));
     hipLaunchKernelGGL(k_sp_reduce_cc, dim3((d.Wc + 63) / 64), dim3(64 * RW), 0, h->stream, d);
     if (d.mot) hipLaunchKernelGGL(k_sp_mcost_build, dim3(1), dim3(256), 0, h->stream, d);
     KSP_HIP(hipEventRecord(ev[2], h->stream));
