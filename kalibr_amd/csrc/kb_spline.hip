@@ -694,9 +694,10 @@ __global__ void __launch_bounds__(256) k_sp_assemble(SpDev d) {
       const int tile = wave + 4 * u;
       if (tile < 6) {  // wave-uniform
         const int ir = 16 * (tile / 3) + (lane & 15), jc = 16 * (tile % 3) + (lane & 15);
-        for (int st = 0; st < ks; ++st) {
+        auto operands = [&](int st, double& av, double& bv) {
           const int k = 4 * st + (lane >> 4), t = k / 6, z = k % 6;
-          double av = 0.0, bv = 0.0;
+          av = 0.0;
+          bv = 0.0;
           if (t < nt) {
             const double* J = tj + t * IST;
             const int jr = k0 + ir / 6 - tb[t];
@@ -710,7 +711,13 @@ __global__ void __launch_bounds__(256) k_sp_assemble(SpDev d) {
               bv = -J[144 + z];
             }
           }
-          iacc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, iacc[u], 0, 0, 0);
+        };
+        for (int st = 0; st < ks; st += 2) {  // two steps' operands loaded before their MFMAs (t >= nt: zeros)
+          double a0, b0, a1, b1;
+          operands(st, a0, b0);
+          operands(st + 1, a1, b1);
+          iacc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, iacc[u], 0, 0, 0);
+          iacc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, iacc[u], 0, 0, 0);
         }
       }
     }
@@ -944,8 +951,13 @@ __device__ bool chol18_wave(double* A, double* id, int lane) {
   for (int k = 0; k < NB; ++k) {
     const double dkk = rdlane(a[k], k);
     ok = ok && (dkk > 0.0);
-    const double dk = sqrt(dkk > 0.0 ? dkk : 1.0);
-    const double rdk = ksp_recip(dk);  // wave-uniform: one reciprocal per step instead of a division per lane
+    // 1 / sqrt(d_kk) by v_rsq_f64 + two Newton steps and L_kk = d_kk / sqrt(d_kk): a shorter dependent chain than
+    // an IEEE square root followed by a reciprocal (wave-uniform, one per pivot)
+    const double dpos = dkk > 0.0 ? dkk : 1.0;
+    double rdk = __builtin_amdgcn_rsq(dpos);
+    rdk = rdk * fma(-0.5 * dpos * rdk, rdk, 1.5);
+    rdk = rdk * fma(-0.5 * dpos * rdk, rdk, 1.5);
+    const double dk = dpos * rdk;
     // selects instead of lane-conditional blocks: no exec-mask save / restore around each update
     rid = (lane == k) ? rdk : rid;
     a[k] = (lane == k) ? dk : (lane > k) ? a[k] * rdk : a[k];
