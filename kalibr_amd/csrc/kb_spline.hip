@@ -35,7 +35,7 @@ constexpr int ORD = 4;      // spline order of the device path
 constexpr int SB = 3;       // coefficients per cyclic-reduction node: couplings reach only the next node
 constexpr int NB = 6 * SB;  // 18 rows per node
 constexpr int MAXC = 64;    // camera + IMU block
-constexpr int FPB = 2;      // frames per k_sp_frames block (600 blocks at configs[4]: every block resident at once)
+constexpr int FPB = 2;      // frames per k_sp_frames block (600 blocks at configs[4]; 1 frame per block measured no faster: its 1,200 partial rows cost k_sp_reduce_cc 4 us)
 constexpr int RW = 16;      // waves of the column-sum kernels (k_sp_reduce_cc, k_sp_schur_red)
 constexpr int XS = 17;      // LDS row stride of the 64 x 16 Jacobian-row tile
 constexpr int WI = 55;      // IMU theta partial row: 9x9 upper (45) | g (9) | cost
@@ -1961,6 +1961,7 @@ kb_sp_handle* kb_sp_create(const kb_sp_layout* L) {
   }
   h->fn_camsolve = h->C <= 16 ? (const void*)k_sp_camsolve<16>
                    : h->C <= 32 ? (const void*)k_sp_camsolve<32>
+                   : h->C <= 40 ? (const void*)k_sp_camsolve<40>  // configs[4]: C = 37
                    : h->C <= 48 ? (const void*)k_sp_camsolve<48>
                                 : (const void*)k_sp_camsolve<64>;
   if (rc || hipHostMalloc((void**)&h->host_sc, sizeof(double) * SC_NSC) != hipSuccess ||
