@@ -84,18 +84,28 @@ def host_cpu():
     return {"cpu_model": model, "nproc": avail, "os_cpu_count": os.cpu_count()}
 
 
-def cpu_baseline(prob, seconds_budget=12.0, threads=None, label="configs[1] (full 500-frame problem"):
+def cpu_baseline(prob, seconds_budget=12.0, threads=None, label="configs[1] (full 500-frame problem", state=None):
     """Oracle (our C restatement of the reference CPU flow: threaded per-term evaluation into CCS J^T,
-    serial rhs SpMV, J^T J, frame-first sparse Cholesky) timed on host cores."""
+    serial rhs SpMV, J^T J, frame-first sparse Cholesky) timed on host cores, GN passes from `state` (default: the
+    problem's initial state)."""
     from oracle import oracle as O
     o = O.Oracle(prob)
     threads = threads or min(16, os.cpu_count() or 1)
-    t1 = o.time_gn(prob.state_init, 1, threads)  # includes first-touch / warm-up
+    st = prob.state_init if state is None else state
+    t1 = o.time_gn(st, 1, threads)  # includes first-touch / warm-up
     n = max(2, min(200, int(seconds_budget / max(t1, 1e-4))))
-    t = o.time_gn(prob.state_init, n, threads)
+    t = o.time_gn(st, n, threads)
     return {"value": n / t, "unit": "iterations/s", "cores": threads, "kind": "port", **host_cpu(),
             "sample": f"{n} GN iterations of {label}, {prob.n_corners} corners), "
                       f"oracle/kb_oracle.c kbo_time_gn (restatement, not CHOLMOD), {threads} threads"}
+
+
+def all_host_cores():
+    """every host CPU this process may run on (the strongest CPU configuration of the box)"""
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
 
 
 def cpu_baseline_spline(prob, seconds_budget=15.0, threads=None):
@@ -158,6 +168,8 @@ def main():
     ap.add_argument("--config", type=int, default=4, choices=[2, 3, 4, 5],
                     help="BASELINE.json configs[i] is --config i+1 (default 4: the north-star 8-cam x 2000-frame rig)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--comm", action="store_true",
+                    help="N=1 through the multi-GPU path: rendezvous, a one-rank RCCL communicator, captured RCCL")
     args = ap.parse_args()
     if args.config == 5:
         if args.gpus != 1:
@@ -171,15 +183,18 @@ def main():
         raise SystemExit("for --gpus N>1 launch with torch.distributed.run --nproc-per-node N")
 
     from kalibr_amd import build as B
-    from kalibr_amd import capi, synth
+    from kalibr_amd import capi, rdzv, synth
     if not os.path.exists(B.OUT):
         B.build()
 
-    dist = None
-    if world > 1:
-        import torch
-        import torch.distributed as dist
-        dist.init_process_group("gloo", init_method="env://")  # id exchange + host barrier only
+    # host rendezvous over stdlib TCP (RCCL id broadcast, barriers, max of the wall time): no torch in this process,
+    # so the library's /opt/rocm HIP runtime and RCCL are the only ones loaded
+    use_comm = world > 1 or args.comm
+    grp = rdzv.TcpGroup(rank, world) if use_comm else None
+    # the JSON line must be the only stdout output: native banners (RCCL prints its version at init) go to stderr
+    sys.stdout.flush()
+    stdout_fd = os.dup(1)
+    os.dup2(2, 1)
 
     strong = args.config in (3, 4)
     if strong:  # configs[3] (configs[2]): one problem, frames split over the ranks
@@ -192,32 +207,35 @@ def main():
     shard = full.frame_slice(rank * fpr, min(full.n_frames, (rank + 1) * fpr)) if world > 1 else full
     g = capi.Solver(shard, device=local)
     g.set_state(shard.state_init)
-    if world > 1:
-        obj = [capi.comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
-        g.comm_init(obj[0], world, rank)
+    if use_comm:  # --comm at N=1: the same launcher + RCCL path with a one-rank communicator
+        uid = grp.broadcast(capi.comm_unique_id() if rank == 0 else b"")
+        g.comm_init(uid, world, rank)
+    gn_start = None
     if args.config == 3:
         # undamped GN diverges from configs[2]'s initial state (the omni xi / focal-length coupling; the oracle does
         # the same): the timed GN passes start from the Kalibr2-default LM solution instead (same pass cost)
         g.optimize(policy="lm", lambda0=10.0, max_iterations=200, eps_x=1e-3, eps_j=1.0)
+        gn_start = g.get_state()
 
     g.run_gn(args.warmup)
-    if dist:
-        dist.barrier()
+    graphed = g.gn_prepare(args.steps)  # loop start + every graph the timed passes launch, captured and uploaded
+    if grp:
+        grp.barrier()
     t0 = time.perf_counter()
-    sec = g.run_gn(args.steps)  # stream-synchronised on both sides inside
+    sec = g.gn_launch(args.steps)  # stream-synchronised on both sides inside
     wall = time.perf_counter() - t0
-    if dist:
-        import torch
-        tt = torch.tensor([wall], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        wall = float(tt.item())
+    if grp:
+        wall = grp.max(wall)
 
-    # dominant kernel (k_build) timing with HIP events on the handle's stream, inside GN passes
+    # dominant kernel (the build) timing with HIP events on the handle's stream, inside GN passes
     build_ms, bytes_per, flops_per = g.build_kernel_stats()
+    kname = g.build_kernel_name()
     achieved = bytes_per / (build_ms * 1e-3) / 1e9
     pmc = pmc_traffic_bytes(is_build_kernel, args.config) if world == 1 else None  # summaries are of N=1 runs
 
+    sys.stdout.flush()
+    os.dup2(stdout_fd, 1)
+    os.close(stdout_fd)
     if rank == 0:
         # weak: every rank iterates its own configs[1]-sized problem; strong: all ranks iterate one problem
         value = (1 if strong else world) * args.steps / wall
@@ -234,25 +252,36 @@ def main():
                        "frames_per_gpu": shard.n_frames, "cameras": full.n_cams, "corners_per_gpu": shard.n_corners,
                        "jacobian_cols": full.total_cols, "camera_block": full.cam_cols, "policy": "gauss_newton",
                        "parallelism": f"frame-sharded x{world}"},
-            "roofline": {"bound": "hbm", "kernel": "k_build", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "roofline": {"bound": "hbm", "kernel": kname, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
                          "traffic": (pmc[0] / (build_ms * 1e-3) / 1e9) if pmc else None,
                          "traffic_bytes_per_launch": pmc[0] if pmc else None,
                          "traffic_source": pmc[1] if pmc else None,
                          "avg_ms": build_ms, "algorithmic_bytes": bytes_per,
                          "fp64_tflops": flops_per / (build_ms * 1e-3) / 1e12},
+            "library_seconds": sec,
+            "comm": {"rccl": bool(use_comm), "ranks": world, "rendezvous": "stdlib TCP" if use_comm else None,
+                     "graphed": int(graphed)},
         }
         if not args.no_cpu_baseline:
             if strong:  # the whole problem on the host cores (configs[3]: ~0.2 s per iteration at 16 threads)
                 lab = {4: "configs[3] (full 8-cam 2000-frame problem", 3: "configs[2] (full 4-cam 1000-frame problem"}
-                out["cpu_baseline"] = cpu_baseline(full, seconds_budget=20.0, label=lab[args.config])
+                # configs[2]: both sides time GN from the same (post-LM) state
+                st = gn_start if (gn_start is not None and world == 1) else None
+                out["cpu_baseline"] = cpu_baseline(full, seconds_budget=20.0, label=lab[args.config], state=st)
+                allc = all_host_cores()
+                if allc != out["cpu_baseline"]["cores"]:
+                    out["cpu_baseline_all_cores"] = cpu_baseline(full, seconds_budget=20.0, label=lab[args.config],
+                                                                 threads=allc, state=st)
             else:
                 out["cpu_baseline"] = cpu_baseline(full if world == 1 else full.frame_slice(0, FRAMES_PER_RANK))
             out["speedup_vs_cpu_baseline"] = value / out["cpu_baseline"]["value"]
+            if "cpu_baseline_all_cores" in out:
+                out["speedup_vs_cpu_baseline_all_cores"] = value / out["cpu_baseline_all_cores"]["value"]
         print(json.dumps(out))
-    if dist:
-        dist.barrier()
-        dist.destroy_process_group()
+    if grp:
+        grp.barrier()
+        grp.close()
 
 
 if __name__ == "__main__":

@@ -196,10 +196,20 @@ int kb_get_trace(kb_handle* h, double* trace, int32_t cap);
 /* Benchmark entry: run exactly n_iter Gauss-Newton passes of the device loop (convergence
  * tests disabled), no host sync inside; *seconds = wall time between stream syncs. */
 int kb_run_gn_iterations(kb_handle* h, int32_t n_iter, double* seconds);
+/* kb_run_gn_iterations in two calls, so that a multi-process run can put a host barrier between them:
+ * kb_gn_prepare = the loop start (evaluateError on the current state, first prelude) + capture and upload of
+ * every graph n_iter passes will launch, then a stream sync; kb_gn_launch = the n_iter passes and the last
+ * pass's end between two stream syncs (*seconds = that wall time).  Same passes, same results.
+ * kb_gn_prepare returns 1 when the passes will run as captured hipGraphs (RCCL calls included when sharded),
+ * 0 when they run eagerly, < 0 on error. */
+int kb_gn_prepare(kb_handle* h, int32_t n_iter);
+int kb_gn_launch(kb_handle* h, int32_t n_iter, double* seconds);
 /* Average device duration (ms) of the build kernel inside Gauss-Newton passes (runs 22 passes from the
  * current state, HIP events around each build launch on the handle's stream); algorithmic bytes and
  * flops per build launch.  The state, camera chains and control block are restored afterwards. */
 int kb_build_kernel_stats(kb_handle* h, double* avg_ms, double* bytes_per_launch, double* flops_per_launch);
+/* Name of the build kernel this handle launches ("k_buildp" or "k_build") into buf (NUL-terminated). */
+int kb_build_kernel_name(kb_handle* h, char* buf, int32_t cap);
 
 /* Multi-GPU (frame sharding): each rank's handle holds its own frames;
  * the camera-block [S | b] and the cost/step statistics are all-reduced over RCCL once

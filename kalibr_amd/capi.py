@@ -21,7 +21,8 @@ EXPORTS = [
     "kb_create", "kb_destroy", "kb_last_error", "kb_upload_observations", "kb_set_state", "kb_set_state_flat",
     "kb_get_state_flat", "kb_state_size", "kb_num_cols", "kb_camera_cols", "kb_eval_cost", "kb_build",
     "kb_set_constant_conditioner", "kb_set_conditioner", "kb_solve", "kb_get_rhs", "kb_apply_update", "kb_revert", "kb_get_normal_blocks",
-    "kb_optimize", "kb_get_trace", "kb_run_gn_iterations", "kb_build_kernel_stats", "kb_comm_get_unique_id",
+    "kb_optimize", "kb_get_trace", "kb_run_gn_iterations", "kb_gn_prepare", "kb_gn_launch", "kb_build_kernel_stats",
+    "kb_build_kernel_name", "kb_comm_get_unique_id",
     "kb_comm_init", "kb_comm_init_local", "kb_selftest_mfma", "kb_solve_marginal", "kb_analyze_marginal",
     # block-Jacobi PCG (LinearSolverPCG)
     "kb_set_linear_solver", "kb_pcg_init", "kb_get_pcg_info",
@@ -120,6 +121,9 @@ def lib():
         L.kb_optimize.argtypes = [C.c_void_p, C.POINTER(OptimizerOptions), C.POINTER(Solution)]
         L.kb_get_trace.argtypes = [C.c_void_p, dp, C.c_int32]
         L.kb_run_gn_iterations.argtypes = [C.c_void_p, C.c_int32, dp]
+        L.kb_gn_prepare.argtypes = [C.c_void_p, C.c_int32]
+        L.kb_gn_launch.argtypes = [C.c_void_p, C.c_int32, dp]
+        L.kb_build_kernel_name.argtypes = [C.c_void_p, C.c_char_p, C.c_int32]
         L.kb_build_kernel_stats.argtypes = [C.c_void_p, dp, dp, dp]
         L.kb_comm_get_unique_id.argtypes = [C.c_void_p]
         L.kb_comm_init.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32]
@@ -322,6 +326,21 @@ class Solver:
         sec = C.c_double()
         _check(lib().kb_run_gn_iterations(self.h, int(n_iter), C.byref(sec)))
         return sec.value
+
+    def gn_prepare(self, n_iter):
+        """loop start + every graph n_iter passes need, captured and uploaded (kb_gn_prepare); True if graphed"""
+        return bool(_check(lib().kb_gn_prepare(self.h, int(n_iter))))
+
+    def gn_launch(self, n_iter):
+        """the n_iter prepared passes between two stream syncs; returns their wall seconds (kb_gn_launch)"""
+        sec = C.c_double()
+        _check(lib().kb_gn_launch(self.h, int(n_iter), C.byref(sec)))
+        return sec.value
+
+    def build_kernel_name(self):
+        buf = C.create_string_buffer(32)
+        _check(lib().kb_build_kernel_name(self.h, buf, 32))
+        return buf.value.decode()
 
     def build_kernel_stats(self):
         ms, by, fl = C.c_double(), C.c_double(), C.c_double()

@@ -1958,11 +1958,21 @@ __device__ __forceinline__ int cidx_col(int e, int C) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Blocked LDL^T for camera blocks C > 64 (config 4: C = 106): 16 x 16 lower tiles in LDS, tile (it, jt) at
-// (it(it+1)/2 + jt) * 256, rows/cols in [C, 16 nb) padded with the identity.  Per 16-column panel: the
-// diagonal tile is factored in one wave's registers (v_readlane broadcasts), the rows below are solved
-// against it (one row per thread), and the trailing tiles are updated with v_mfma_f64_16x16x4f64
-// (S_ij -= W_i Ltilde_j^T, W = L D), one tile per wave at a time: 3 barriers per panel instead of one per column.
+// Blocked LDL^T of the camera block for C > 64 (configs[3]: C = 106), the right-hand side appended as row C.
+// LDS layout: lower 16 x 16 tiles, tile (it, jt) at (it(it+1)/2 + jt) * kTileSz, row stride kTS, nb = ceil((C+1)/16)
+// tile rows.  Row C holds b (diagonal 1), rows C+1 .. 16 nb - 1 the identity.  After the factorisation tile (i, q),
+// i > q, holds W = L D (the unscaled sub-diagonal rows), a diagonal tile W strictly below its diagonal and D on it,
+// rD = 1 / D.  Row C then holds y = Ltilde^-1 b: the forward solve comes out of the factorisation, z = y D^-1.
+//
+// Panel q (columns 16q .. 16q+15) is factored by nF(q) <= 2 "factor" waves with one matrix row per lane:
+//   lanes 0..15 the rows of the diagonal tile (symmetric, read from the lower storage), lanes 16..63 the rows of three
+//   tiles below (factor wave fw: tiles q+1+3fw .. q+3+3fw).  Step k broadcasts the current row k (lane k) with
+//   v_readlane, so the diagonal factor and the panel's triangular solve are one 16-step register loop.
+// Before that, each factor wave applies panel q-1 to its own tiles on v_mfma_f64_16x16x4f64 (the lookahead column;
+// the diagonal tile into a private scratch copy), while 4 "update" waves apply panel q-1 to the remaining trailing
+// tiles (i, j), j > q.  One block barrier per panel; the 106-pivot chain runs on the factor waves only.
+// Same algebra as the scalar right-looking LDL^T (SparseCholeskyLinearSystemSolver.cpp:48-89 / Cholmod(impl).hpp:
+// 387-399 factor the same matrix); only the accumulation order of the trailing updates differs.
 // ---------------------------------------------------------------------------------------------
 constexpr int kTS = 17;             // tile row stride (doubles): 16 + 1 keeps row-parallel LDS accesses conflict-free
 constexpr int kTileSz = 16 * kTS;
@@ -1978,8 +1988,201 @@ __device__ __forceinline__ int sidx(int i, int j, int C) {
     return tidx(i, j);
 }
 
+// W_a (W_b D_q^-1)^T of two 16 x 16 tiles on MFMA (lane l: A[l & 15][k], B[k][l & 15]; acc[r] = entry
+// ((l >> 4) + 4 r, l & 15))
+__device__ __forceinline__ v4d tile_prod(const double* Wa, const double* Wb, const double* rdq, int lane) {
+  v4d acc = {0.0, 0.0, 0.0, 0.0};
+  const int r = lane & 15;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int k = 4 * s + (lane >> 4);
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(Wa[r * kTS + k], Wb[r * kTS + k] * rdq[k], acc, 0, 0, 0);
+  }
+  return acc;
+}
+
+__device__ __forceinline__ void tile_sub(const double* src, double* dst, const v4d& acc, int lane) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int e = ((lane >> 4) + 4 * r) * kTS + (lane & 15);
+    dst[e] = src[e] - acc[r];
+  }
+}
+
+// panel q by factor wave fw (see above); Dsc: this wave's 16 x kTS scratch tile.  Returns false on a non-positive
+// pivot of a real row (< C); the b row's pivot and the identity padding are not tested.
+__device__ __forceinline__ bool panel_factor(double* S, double* rD, double* Dsc, int q, int nb, int C, int fw) {
+  const int lane = threadIdx.x & 63, r = lane & 15, t = lane >> 4;
+  if (q > 0) {
+    // lookahead: panel q-1 applied to the wave's tiles (all products first, then the stores)
+    const double* rdq = rD + 16 * (q - 1);
+    const double* Wq = S + tile_base(q, q - 1);
+    v4d acc[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int iu = u == 0 ? q : q + 3 * fw + u;
+      acc[u] = tile_prod(S + tile_base(iu < nb ? iu : q, q - 1), Wq, rdq, lane);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int iu = u == 0 ? q : q + 3 * fw + u;
+      if (iu < nb) tile_sub(S + tile_base(iu, q), u == 0 ? Dsc : S + tile_base(iu, q), acc[u], lane);
+    }
+    KB_WAVE_SYNC();  // the wave's own tile stores, read back below by other lanes
+  }
+  const int ti_raw = q + 3 * fw + t;
+  const bool live = t == 0 || ti_raw < nb;
+  const double* base = t == 0 ? (q > 0 ? Dsc : S + tile_base(q, q)) : S + tile_base(live ? ti_raw : q, q);
+  double row[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    const int e = t == 0 ? (r > c ? r * kTS + c : c * kTS + r) : r * kTS + c;
+    row[c] = base[e];
+  }
+  bool ok = true;
+  double rd = 1.0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const double Dk = readlane_d(row[k], k);
+    ok = ok & ((Dk > 0.0) | (16 * q + k >= C));  // bitwise: no branch per pivot
+    const double rdk = Dk > 0.0 ? recip_d(Dk) : 0.0;
+    rd = (lane == k) ? rdk : rd;
+    const double f = (lane > k) ? row[k] * rdk : 0.0;
+#pragma unroll
+    for (int j = k + 1; j < 16; ++j) row[j] -= f * readlane_d(row[j], k);
+  }
+  if (t == 0) {
+    if (fw == 0) {
+      double* dd = S + tile_base(q, q) + r * kTS;
+#pragma unroll
+      for (int c = 0; c < 16; ++c)
+        if (c <= r) dd[c] = row[c];
+      rD[16 * q + r] = rd;
+    }
+  } else if (live) {
+    double* dd = S + tile_base(ti_raw, q) + r * kTS;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) dd[c] = row[c];
+  }
+  return ok;
+}
+
+// the factorisation (every thread of the 8-wave block calls it).  Factor waves: 0 and 1 (while panel q has more
+// than three tiles below it); update waves: 2, 3, 6, 7 (waves 4 and 5 share the factor waves' SIMDs and stay idle,
+// so that the MFMA tiles do not slow the pivot chain).  okl is cleared on a non-positive real pivot.
+__device__ __forceinline__ void ldl_panels(const KbDev& d, double* S, double* rD, double* Dsc, int C, int nb, int* okl) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int ow = wave == 2 ? 0 : wave == 3 ? 1 : wave == 6 ? 2 : wave == 7 ? 3 : -1;
+#pragma unroll 1
+  for (int q = 0; q < nb; ++q) {
+    const int nf = (nb - 1 - q) > 3 ? 2 : 1;
+    if (wave < nf) {
+      if (wave == 0) KB_TS(d, 20 + 2 * q);
+      const bool ok = panel_factor(S, rD, Dsc + wave * kTileSz, q, nb, C, wave);
+      if (wave == 0) {
+        if (!ok && lane == 0) *okl = 0;
+        KB_WAVE_SYNC();
+        KB_TS(d, 21 + 2 * q);
+      }
+    } else if (ow >= 0 && q > 0) {
+      // panel q-1 on tiles (q+1+ii, q+1+jj), 0 <= jj <= ii < m
+      const int m = nb - 1 - q, ntiles = m * (m + 1) / 2;
+      const double* rdq = rD + 16 * (q - 1);
+#pragma unroll 1
+      for (int qq = ow; qq < ntiles; qq += 4) {
+        const int ii = tri_row(qq), jj = qq - ii * (ii + 1) / 2;
+        const int i = q + 1 + ii, j = q + 1 + jj;
+        const v4d acc = tile_prod(S + tile_base(i, q - 1), S + tile_base(j, q - 1), rdq, lane);
+        tile_sub(S + tile_base(i, j), S + tile_base(i, j), acc, lane);
+      }
+    }
+    __syncthreads();
+    KB_TS(d, 10 + q);
+  }
+}
+
+// Camera block expansion of the tiled solve (CM == 0) on MFMA.  The baseline rows of H_cc and g_c are one product
+//   Z = Kcat^T [U | D | g]      (6(N-1) x (6(N-1) + CI + 1), inner dimension 6N):
+//   Kcat[6i + m][6j + a] = K_{i,j}[m][a] (zero for j >= i), U[6i + m][6k + b] = T_{i,k}[m][b] = (H_i,dd K_{i,k})[m][b],
+//   D[6i + m][p] = H_i[m][6 + x] for intrinsic column p = (camera i, index x) and zero for the other cameras'
+//   columns, g[6i + m] = H_i[m][15].  Z's first 6(N-1) columns are the baseline x baseline block (sum over i > max(j, k)
+//   of K_{i,j}^T H_i,dd K_{i,k}), the next CI the baseline x intrinsic block, the last the baselines' gradient
+//   (CalibrationTools.hpp:404-408 chains; the same sums as cam_entry_l / cam_grad_l).  The intrinsic x intrinsic
+//   blocks and gradients are H_i[II] and H_i[I][15] (one thread per entry).  Every entry is written by one thread:
+//   S lower tiles += H_cc (+ lambda^2 or the conditioner on the diagonal), row C of S = b + g (the right-hand side of
+//   the factorisation), gl / gc / rhs = g.
+__device__ __forceinline__ void cam_expand_tiles(const KbDev& d, double* S, const double* bv, double* gl,
+                                                 const double* Hs, const double* T, const double* K, const int* ci,
+                                                 const int (*ctab)[KB_MAX_CAMS], double lam2, const double* cd2) {
+  const int C = d.C, N = d.N, tid = threadIdx.x, nth = blockDim.x, wave = tid >> 6, lane = tid & 63, nw = nth >> 6;
+  const int NB6 = 6 * (N - 1), CI = C - NB6, NK = 6 * N;
+  // intrinsic x intrinsic blocks (lower) and the intrinsic gradients
+  for (int q = tid; q < N * KB_MAX_INTR * KB_MAX_INTR; q += nth) {
+    const int i = q / (KB_MAX_INTR * KB_MAX_INTR), x = (q / KB_MAX_INTR) % KB_MAX_INTR, y = q % KB_MAX_INTR;
+    const int nin = ctab[0][i], c0 = ctab[1][i];
+    if (x < nin && y <= x) {
+      const int p = c0 + x;
+      S[tidx(p, c0 + y)] += Hs[i * 256 + (6 + x) * 16 + 6 + y] + ((x == y) ? (cd2 ? cd2[p] : lam2) : 0.0);
+      if (y == 0) {
+        const double g = Hs[i * 256 + (6 + x) * 16 + 15];
+        S[tidx(C, p)] = bv[p] + g;
+        gl[p] = g;
+        d.gc[p] = g;
+        d.rhs[p] = g;
+      }
+    }
+  }
+  if (N < 2) return;
+  const int nrt = (NB6 + 15) >> 4, nct = (NB6 + CI + 16) >> 4, nks = (NK + 3) >> 2;
+  const int i16 = lane & 15, kq = lane >> 4;
+  for (int tq = wave; tq < nrt * nct; tq += nw) {
+    const int rt = tq / nct, ct = tq - rt * nct;
+    const int r = 16 * rt + i16, c = 16 * ct + i16;  // the lane's A row and B column
+    const int rj = r / 6, ra = r - 6 * rj;
+    const int cb = c < NB6 ? c / 6 : 0, cbb = c - 6 * cb;
+    const int p = c - NB6;  // intrinsic column (NB6 <= c < NB6 + CI)
+    const int pinfo = ci[min(max(p, 0), C - 1)], pcam = (pinfo >> 8) & 0xff, px = pinfo & 0xff;
+    v4d acc = {0.0, 0.0, 0.0, 0.0};
+    for (int st = 0; st < nks; ++st) {
+      const int k = 4 * st + kq, ki = k / 6, km = k - 6 * ki;
+      const int kic = min(ki, N - 1);
+      double a = K[(kic * N + min(rj, N - 1)) * 36 + km * 6 + ra];
+      a = (r < NB6 && k < NK) ? a : 0.0;
+      double b;
+      if (c < NB6) {
+        b = T[(kic * N + cb) * 36 + km * 6 + cbb];
+      } else if (c < NB6 + CI) {
+        b = Hs[kic * 256 + km * 16 + 6 + px];
+        b = (pcam == ki) ? b : 0.0;
+      } else {
+        b = Hs[kic * 256 + km * 16 + 15];
+      }
+      b = (k < NK && c <= NB6 + CI) ? b : 0.0;
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int zr = 16 * rt + kq + 4 * q;  // Z row (baseline index), column c
+      if (zr >= NB6) continue;
+      const int gr = ctab[2][zr / 6] + zr % 6;  // global row of the camera block
+      const double v = acc[q];
+      if (c < NB6) {
+        const int gc = ctab[2][c / 6] + c % 6;
+        if (gr >= gc) S[tidx(gr, gc)] += v + ((gr == gc) ? (cd2 ? cd2[gr] : lam2) : 0.0);
+      } else if (c < NB6 + CI) {
+        S[tidx(gr, p)] += v;  // baseline row, intrinsic column: lower
+      } else if (c == NB6 + CI) {
+        S[tidx(C, gr)] = bv[gr] + v;
+        gl[gr] = v;
+        d.gc[gr] = v;
+        d.rhs[gr] = v;
+      }
+    }
+  }
+}
+
 // lane k's value to every lane of its 16-lane row (DPP row_newbcast, gfx90a+): a plain VALU move, without the
-// v_readlane -> SGPR -> VALU round trip and its wait states.  k must fold to a constant (unrolled loops).
+// v_readlane -> SGPR -> VALU round trip.  k must fold to a constant (unrolled loops).
 __device__ __forceinline__ double bcast16(double v, int k) {
   switch (k) {
     case 0: return dpp_d<0x150>(v);
@@ -2001,183 +2204,59 @@ __device__ __forceinline__ double bcast16(double v, int k) {
   }
 }
 
-// diagonal tile p factored in place by one wave (lanes 0..15 hold its rows, row k broadcast by DPP row_newbcast):
-// strictly lower Ltilde, D on the diagonal, rD[16 p + r] = 1 / D_r.  Returns false on a non-positive pivot (padding
-// rows have D = 1: only real pivots can fail).
-__device__ __forceinline__ bool diag_ldl16(double* S, double* rD, int p, int lane) {
-  const int b0 = tile_base(p, p);
-  const int r = lane < 16 ? lane : 15;
-  double row[16];
+// x = Ltilde^-T z, z = (row C of the factor) D^-1, by one wave.  Lane l = 16 g + r holds the rows 16 (g + 4 s) + r,
+// s = 0, 1: tile t lives in the 16-lane group t & 3, slot t >> 2.  Tiles from the last: the tile's own triangle by 16
+// DPP row broadcasts (x_u of the group's lane u, no v_readlane in the dependency chain), then its 16 final values
+// through LDS (pub) to every lane, which subtracts them from the rows of the earlier tiles.
+__device__ __forceinline__ void panel_backsolve(const double* S, const double* rD, int C, double* pub, double (&x)[2]) {
+  const int lane = threadIdx.x & 63, g = lane >> 4, r = lane & 15;
+  int row[2];
+  double rdv[2];
 #pragma unroll
-  for (int c = 0; c < 16; ++c) row[c] = S[b0 + (r > c ? r : c) * kTS + (r > c ? c : r)];
-  bool ok = true;
-  double rd = 1.0;
-#pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    const double Dk = bcast16(row[k], k);
-    ok = ok && (Dk > 0.0);
-    const double rdk = recip_d(Dk);
-    rd = (lane == k) ? rdk : rd;
-    const double f = (lane > k) ? row[k] * rdk : 0.0;
-#pragma unroll
-    for (int j = k + 1; j < 16; ++j) row[j] -= f * bcast16(row[j], k);
+  for (int sl = 0; sl < 2; ++sl) {
+    row[sl] = 16 * (g + 4 * sl) + r;
+    const int rc = min(row[sl], C - 1);
+    const double z = S[tidx(C, rc)], rd = rD[rc];
+    rdv[sl] = rd;
+    x[sl] = row[sl] < C ? z * rd : 0.0;
   }
-  double lrow[16];
-#pragma unroll
-  for (int c = 0; c < 16; ++c) lrow[c] = row[c] * bcast16(rd, c);  // Ltilde[r][c] = (L D)[r][c] / D_c
-  if (lane < 16) {
-#pragma unroll
-    for (int c = 0; c < 16; ++c)
-      if (c <= lane) S[b0 + lane * kTS + c] = (c < lane) ? lrow[c] : row[c];  // strictly lower Ltilde, diag D
-    rD[16 * p + lane] = rd;
-  }
-  return ok;
-}
-
-// rows of panel tile (i, p) by one wave (lanes 0..15, one row each): W = S_ip Ltilde_pp^-T into Wsc (row
-// 16 (i - p - 1) + r), Ltilde_ip = W D_p^-1 in place.  Column-oriented substitution: every step updates all later
-// columns at once (a 15-deep dependency chain), each w[c] accumulated in the order c2 = 0, 1, ..., c - 1.
-__device__ __forceinline__ void panel_trsm16(double* S, const double* rD, double* Wsc, int p, int i, int lane) {
-  const int b0 = tile_base(p, p);
-  const int r = lane & 15;
-  double* srow = S + tile_base(i, p) + r * kTS;
-  double w[16];
-#pragma unroll
-  for (int c = 0; c < 16; ++c) w[c] = srow[c];
-#pragma unroll
-  for (int c2 = 0; c2 < 15; ++c2)
-#pragma unroll
-    for (int c = c2 + 1; c < 16; ++c) w[c] -= w[c2] * S[b0 + c * kTS + c2];
-  if (lane < 16) {
-    double* wrow = Wsc + (16 * (i - p - 1) + r) * kTS;
-#pragma unroll
-    for (int c = 0; c < 16; ++c) {
-      wrow[c] = w[c];
-      srow[c] = w[c] * rD[16 * p + c];
-    }
-  }
-}
-
-// trailing tile (i, j), p < j <= i: S_ij -= W_ip Ltilde_jp^T on MFMA (lane l: A[l&15][k], B[k][l&15])
-__device__ __forceinline__ void trail_update16(double* S, const double* Wsc, int p, int i, int j, int lane) {
-  const double* A = Wsc + 16 * (i - p - 1) * kTS;
-  const double* B = S + tile_base(j, p);
-  v4d acc = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    const int k = 4 * s + (lane >> 4);
-    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(A[(lane & 15) * kTS + k], B[(lane & 15) * kTS + k], acc, 0, 0, 0);
-  }
-  double* Ct = S + tile_base(i, j);
-#pragma unroll
-  for (int r = 0; r < 4; ++r) Ct[((lane >> 4) + 4 * r) * kTS + (lane & 15)] -= acc[r];
-}
-
-// Right-looking blocked LDL^T with a one-panel lookahead, two barriers per panel (8 waves):
-//   phase 1 of panel p: wave w solves the rows of panel tile i = p + 1 + w against Ltilde_pp (panel_trsm16); wave 0
-//            (i = p + 1) then applies panel p to the next diagonal tile (p + 1, p + 1) at once (it owns both operands);
-//   phase 2 of panel p: wave 0 factors diagonal tile p + 1 while the other waves apply panel p to the remaining
-//            trailing tiles.
-// The chain factor(p) -> trsm(p + 1, p) -> update(p + 1, p + 1) -> factor(p + 1) is the critical path; the bulk
-// trailing updates run beside the factorization.  Same arithmetic (and accumulation orders) as a panel-at-a-time
-// blocked factorization with the scalar right-looking LDL^T per diagonal tile.  One call site per helper: the
-// kernel runs on one CU whose instruction cache is cold at every launch, so code size is time.
-__device__ __forceinline__ void ldl_tiles(const KbDev& d, double* S, double* rD, double* Wsc, int C, int nb, int* okl) {
-  const int tid = threadIdx.x, nth = blockDim.x, wave = tid >> 6, lane = tid & 63, nw = nth >> 6;
 #pragma unroll 1
-  for (int p = 0; p < nb; ++p) {
-    // phase 2 of panel p - 1: diagonal tile p (wave 0) | trailing tiles of panel p - 1 except (p, p)
-    if (wave == 0) {
-      KB_WAVE_SYNC();
-      KB_TS(d, 20 + 4 * p);
-      const bool ok = diag_ldl16(S, rD, p, lane);
-      if (!ok && lane == 0) *okl = 0;
-      KB_TS(d, 21 + 4 * p);
-    } else if (p > 0 && wave != 4) {
-      // wave 4 shares wave 0's SIMD (waves map to SIMDs round robin): it stays idle, so the MFMA tiles do not
-      // slow the factorization on the critical path
-      const int m = nb - p;  // trailing tiles (p + ii, p + jj), 0 <= jj <= ii < m; q = 0 is (p, p)
-      const int ntiles = m * (m + 1) / 2;
-      const int wv = wave - (wave > 4);  // 1 .. nw - 2
-#pragma unroll 1
-      for (int q = wv; q < ntiles; q += nw - 2) {
-        const int ii = tri_row(q), jj = q - ii * (ii + 1) / 2;
-        trail_update16(S, Wsc, p - 1, p + ii, p + jj, lane);
-      }
-    }
-    __syncthreads();
-    if (p == 0) KB_STAMP(d, 40);
-    if (p == nb - 1) break;
-    // phase 1 of panel p
-#pragma unroll 1
-    for (int ii = wave - (wave > 4); ii < nb - p - 1 && wave != 4; ii += nw - 1)
-      panel_trsm16(S, rD, Wsc, p, p + 1 + ii, lane);
-    if (wave == 0) {
-      KB_WAVE_SYNC();  // this wave's W and Ltilde rows of tile (p + 1, p) are in LDS
-      KB_TS(d, 22 + 4 * p);
-      trail_update16(S, Wsc, p, p + 1, p + 1, lane);
-      KB_WAVE_SYNC();
-      KB_TS(d, 23 + 4 * p);
-    }
-    __syncthreads();
-    KB_TS(d, 10 + p);
-    if (p == 0) KB_STAMP(d, 41);
-  }
-}
-
-// xv (n = 16 nb entries, b on entry, zero-padded) <- (Ltilde D Ltilde^T)^-1 b, by one wave (no block barriers:
-// the wave's own LDS writes are waited for before the lanes read each other's entries)
-__device__ __forceinline__ void ldl_tiles_solve(const double* S, const double* rD, double* xv, int nb) {
-  const int lane = threadIdx.x & 63;
-  const int n = 16 * nb;
-  for (int p = 0; p < nb; ++p) {  // forward: Ltilde y = b
-    const int b0 = tile_base(p, p);
-    const int r = lane < 16 ? lane : 15;
-    double Lr[16];
+  for (int ti = (C - 1) >> 4; ti >= 0; --ti) {
+    const int tg = ti & 3, ts = ti >> 2, i0 = 16 * ti;
+    // the tile's own triangle: Ltilde[i0 + u][i0 + r], u > r (group tg's lanes; the others compute and discard)
+    double Lw[16], Le[2][16];
 #pragma unroll
-    for (int c = 0; c < 16; ++c) {
-      const double v = S[b0 + r * kTS + c];
-      Lr[c] = (c < r) ? v : 0.0;
+    for (int u = 0; u < 16; ++u) Lw[u] = S[tidx(i0 + u, i0 + min(r, u))];
+    // rows of the earlier tiles: Ltilde[i0 + u][row] (row < i0)
+#pragma unroll
+    for (int sl = 0; sl < 2; ++sl)
+#pragma unroll
+      for (int u = 0; u < 16; ++u) Le[sl][u] = S[tidx(i0 + u, min(row[sl], i0 + u))];
+    const double rdt = ts ? rdv[1] : rdv[0];  // this lane's 1/D in the tile's slot
+    double xt = ts ? x[1] : x[0];
+#pragma unroll
+    for (int u = 15; u >= 0; --u) {
+      const double xu = bcast16(xt, u);
+      const bool in = (r < u) && (i0 + u < C);
+      xt -= in ? Lw[u] * rdt * xu : 0.0;
     }
-    double xr = xv[16 * p + r];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) xr -= Lr[k] * bcast16(xr, k);
-    if (lane < 16) xv[16 * p + lane] = xr;
-    KB_WAVE_SYNC();
-    for (int g = 16 * (p + 1) + lane; g < n; g += 64) {
-      const double* lr = S + tile_base(g >> 4, p) + (g & 15) * kTS;
-      double s = 0.0;
-#pragma unroll
-      for (int c = 0; c < 16; ++c) s += lr[c] * xv[16 * p + c];
-      xv[g] -= s;
+    if (g == tg) {
+      if (ts) x[1] = xt;
+      else x[0] = xt;
+      pub[r] = xt;
     }
     KB_WAVE_SYNC();
-  }
-  for (int g = lane; g < n; g += 64) xv[g] *= rD[g];  // z = D^-1 y
-  KB_WAVE_SYNC();
-  for (int p = nb - 1; p >= 0; --p) {  // backward: Ltilde^T x = z
-    const int b0 = tile_base(p, p);
-    const int r = lane < 16 ? lane : 15;
-    double Lc[16];
+    double xp[16];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const double v = S[b0 + k * kTS + r];
-      Lc[k] = (k > r) ? v : 0.0;
+    for (int u = 0; u < 16; ++u) xp[u] = (i0 + u < C) ? pub[u] : 0.0;
+#pragma unroll
+    for (int sl = 0; sl < 2; ++sl) {
+      double acc = 0.0;
+#pragma unroll
+      for (int u = 0; u < 16; ++u) acc += Le[sl][u] * xp[u];
+      if (row[sl] < i0) x[sl] -= acc * rdv[sl];
     }
-    double xr = xv[16 * p + r];
-#pragma unroll
-    for (int k = 15; k >= 0; --k) xr -= Lc[k] * bcast16(xr, k);
-    if (lane < 16) xv[16 * p + lane] = xr;
-    KB_WAVE_SYNC();
-    if (p == 0) break;
-    for (int g = lane; g < 16 * p; g += 64) {  // rows of earlier panels: z_g -= sum_r Ltilde_{p,q}[r][g] x_p[r]
-      const double* lc = S + tile_base(p, g >> 4) + (g & 15);
-      double s = 0.0;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) s += lc[r * kTS] * xv[16 * p + r];
-      xv[g] -= s;
-    }
-    KB_WAVE_SYNC();
+    KB_WAVE_SYNC();  // pub is rewritten by the next tile
   }
 }
 
@@ -2204,7 +2283,7 @@ __global__ void __launch_bounds__(256) k_colimg(KbDev d, const double* rows, dou
     const int e = q - d.Wtot;
     if (e >= d.img_n) return;
     dst = d.simg + e;
-    const int nb = (C + 15) >> 4, n16 = 16 * nb, ntz = kTileSz * nb * (nb + 1) / 2;
+    const int nb = (C + 16) >> 4, n16 = 16 * nb, ntz = kTileSz * nb * (nb + 1) / 2;  // + the b row (row C)
     if (e < ntz) {
       const int t = e / kTileSz, w = e - t * kTileSz, r = w / kTS, cc = w - r * kTS;
       const int it = tri_row(t), jt = t - it * (it + 1) / 2;
@@ -2449,7 +2528,7 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update, int nth) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const int N = d.N, C = d.C, W = d.W, tid = threadIdx.x;
   const int Cp = C * (C + 1) / 2;
-  const int nb = (C + 15) >> 4, n16 = 16 * nb;  // CM == 0: 16 x 16 tiles
+  const int nb = (C + 16) >> 4, n16 = 16 * nb;  // CM == 0: 16 x 16 tiles, rows 0 .. C (b appended as row C)
   // CM > 0: S column-major packed lower [Cp] | bv [C + 1] (slot C: non-PD frame-block count) | gl [C] | Hs [N][256]
   // CM == 0: the k_colimg image [S lower tiles | bv (n16 + 2) | Hs [N][256]] | gl (C, even-padded)
   double* S = sm;
@@ -2458,14 +2537,13 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update, int nth) {
   double* gl = CM > 0 ? bv + C + 1 : Hs + N * 256;
   double* T = CM > 0 ? Hs + N * 256 : gl + ((C + 1) & ~1);  // [N][N][36]
   double* K = T + N * N * 36;        // [N][N][36]
-  double* Wsc = K + N * N * 36;      // CM == 0: [n16 - 16][kTS] panel scratch
-  double* rDv = Wsc + (CM > 0 ? 0 : kTS * (n16 - 16));  // CM == 0: [n16] 1/D
-  double* xv = rDv + (CM > 0 ? 0 : n16);               // CM == 0: [n16] right-hand side / solution
-  int* ci = (int*)(xv + (CM > 0 ? 0 : n16));           // [C]
+  double* Dsc = K + N * N * 36;      // CM == 0: [2][kTileSz] the factor waves' diagonal-tile scratch
+  double* rDv = Dsc + (CM > 0 ? 0 : 2 * kTileSz);  // CM == 0: [n16] 1/D
+  int* ci = (int*)(rDv + (CM > 0 ? 0 : n16));      // [C]
   __shared__ int okl;
   __shared__ double nbase[KB_MAX_CAMS * 7];  // candidate baselines
   __shared__ int ctab[3][KB_MAX_CAMS];       // per camera: #intrinsics | first intrinsic column | baseline column
-  __shared__ __attribute__((aligned(16))) double pubcol[CM > 0 ? CM : 1];  // LDL^T column broadcast
+  __shared__ __attribute__((aligned(16))) double pubcol[CM > 0 ? CM : 16];  // LDL^T column / solve broadcast
   __shared__ int fin[2];  // GN fused: done, cur after the previous pass's end
   __shared__ KbCtrl cls;
   __shared__ double cl_red[4];
@@ -2476,9 +2554,9 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update, int nth) {
   // GN fused: a pending step means the system was built at the candidate state (slot 1 - cur)
   const int bslot = (gfu && c->have_dx) ? 1 - cur : cur;
   double x[2] = {0.0, 0.0};
-  // GN fused: the previous pass's end runs in wave kFinWave: while wave 0 factors (CM > 0), else before the
-  // camera expansion
-  constexpr int kFinWave = CM > 0 ? 1 : 0;
+  // GN fused: the previous pass's end runs in wave kFinWave while the factorisation runs (CM == 0: wave 2, an
+  // update wave, idle during the first panel)
+  constexpr int kFinWave = CM > 0 ? 1 : 2;
   const bool fwave = (tid >> 6) == kFinWave;
   double dxr = 0.0;  // GN fused: max|dx_f| of the previous step, one column per rank
   if (gfu && fwave) {
@@ -2498,6 +2576,7 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update, int nth) {
     const double2* gk = reinterpret_cast<const double2*>(cam_K(d, bslot)) - n2i;
     double2* li = reinterpret_cast<double2*>(S);
     double2* lk = reinterpret_cast<double2*>(K) - n2i;
+    const int civ = d.colinfo[tid < C ? tid : 0];  // column info in the same round trip (C <= 111 < threads)
     constexpr int U = 12;
 #pragma unroll 1
     for (int q0 = tid; q0 < n2; q0 += U * nth) {
@@ -2513,7 +2592,7 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update, int nth) {
         if (q < n2) *(q < n2i ? li + q : lk + q) = v[u];
       }
     }
-    for (int p = tid; p < C; p += nth) ci[p] = d.colinfo[p];
+    if (tid < C) ci[tid] = civ;
   } else {
     solve_stage<4, CM, false>(d, bslot, K, Hs, S, bv, ci, tid, nth);
   }
@@ -2564,19 +2643,19 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update, int nth) {
     }
   };
   __syncthreads();
-  if (CM == 0 && gfu) {
-    if (fwave) finish_prev();
-    __syncthreads();
-    if (fin[0]) return;
-  }
   KB_TS(d, 2);
-  cam_expand_blocks<CM>(S, C, N, ctab, Hs, T, K, lam2, nth >> 6, gate ? nullptr : d.cond2);
-  for (int p = tid; p < C; p += nth) {
-    const double g = cam_grad_l(N, ci, Hs, K, p);
-    bv[p] += g;
-    gl[p] = g;
-    d.gc[p] = g;
-    d.rhs[p] = g;
+  if constexpr (CM > 0) {
+    cam_expand_blocks<CM>(S, C, N, ctab, Hs, T, K, lam2, nth >> 6, gate ? nullptr : d.cond2);
+    for (int p = tid; p < C; p += nth) {
+      const double g = cam_grad_l(N, ci, Hs, K, p);
+      bv[p] += g;
+      gl[p] = g;
+      d.gc[p] = g;
+      d.rhs[p] = g;
+    }
+  } else {
+    // H_cc on MFMA into the staged tiles; b + g as row C (the factorisation's right-hand side)
+    cam_expand_tiles(d, S, bv, gl, Hs, T, K, ci, ctab, lam2, gate ? nullptr : d.cond2);
   }
   __syncthreads();
   KB_TS(d, 3);
@@ -2597,23 +2676,12 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update, int nth) {
     KB_STAMP(d, 3);
     KB_STAMP(d, 4);
   } else {
-    // phase C: blocked LDL^T on 16 x 16 tiles (MFMA trailing updates); phase D: blocked solves
-#ifdef KB_STAMPS
-    if (d.dbg_flags & 1) {  // diagnostic: a first (throw-away) factorisation, then the timed one below
-      ldl_tiles(d, S, rDv, Wsc, C, nb, &okl);
-      KB_STAMP(d, 47);
-    }
-#endif
-    ldl_tiles(d, S, rDv, Wsc, C, nb, &okl);
+    // phase C: blocked LDL^T with the forward solve (row C); the previous pass's end beside the first panel
+    if (gfu && fwave) finish_prev();
+    ldl_panels(d, S, rDv, Dsc, C, nb, &okl);
     KB_TS(d, 4);
     KB_STAMP(d, 3);
-    if (tid < 64) {  // the solves run in one wave
-      for (int g = tid; g < n16; g += 64) xv[g] = g < C ? bv[g] : 0.0;
-      KB_WAVE_SYNC();
-      ldl_tiles_solve(S, rDv, xv, nb);
-#pragma unroll
-      for (int sl = 0; sl < 2; ++sl) x[sl] = (tid + 64 * sl < C) ? xv[tid + 64 * sl] : 0.0;
-    }
+    if (tid < 64) panel_backsolve(S, rDv, C, pubcol, x);  // phase D: Ltilde^T x = z, one wave
     KB_STAMP(d, 4);
   }
   __syncthreads();  // okl final

@@ -27,8 +27,7 @@ def test_library_exports_every_symbol():
 
 
 def test_no_cpu_fallback_without_device():
-    import torch
-    if torch.cuda.is_available():
+    if os.path.exists("/dev/kfd"):  # (no torch import: the product processes load only the library's HIP runtime)
         pytest.skip("GPU present")
     from kalibr_amd import capi, synth
     with pytest.raises(capi.KbError, match="no HIP device"):

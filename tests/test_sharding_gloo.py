@@ -6,8 +6,6 @@ import os
 import socket
 
 import numpy as np
-import torch.distributed as dist
-import torch.multiprocessing as mp
 
 from kalibr_amd import synth
 
@@ -22,6 +20,7 @@ def _free_port():
 
 def _worker(rank, world, port, lam, out):
     import torch
+    import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from oracle import oracle as O
@@ -52,6 +51,8 @@ def _worker(rank, world, port, lam, out):
 
 
 def test_two_rank_gloo_sharded_solve():
+    # torch is imported inside the tests only: a `pytest -m gpu` process never loads torch's bundled HIP runtime
+    import torch.multiprocessing as mp
     from oracle import oracle as O
     mgr = mp.Manager()
     out = mgr.dict()

@@ -22,10 +22,8 @@ names = {0: "entry", 1: "staged", 2: "T (+pass end)", 3: "H_cc blocks + grad", 4
 for i in range(10, 20):
     names[i] = f"  panel {i - 10}"
 for q in range(7):
-    names[20 + 4 * q] = f"    p{q} diag start"
-    names[21 + 4 * q] = f"    p{q} diag end"
-    names[22 + 4 * q] = f"    p{q} trsm end"
-    names[23 + 4 * q] = f"    p{q} tile upd end"
+    names[20 + 2 * q] = f"    p{q} factor start (after its MFMA lookahead)"
+    names[21 + 2 * q] = f"    p{q} factor end"
 for rep in range(3):
     g.set_state(p.state_init)
     g.run_gn(16)
