@@ -128,6 +128,10 @@ int kb_get_pcg_info(kb_handle* h, kb_pcg_info* info);
 
 /* LinearSystemSolver::rhs (LinearSystemSolver.hpp:47). */
 int kb_get_rhs(kb_handle* h, double* rhs_out);
+/* LinearSystemSolver::rhsJtJrhs (LinearSystemSolver.hpp:66-69): rhs^T (J^T J) rhs of the last kb_build (the reference
+ * forms ||J rhs||^2, SparseCholeskyLinearSystemSolver.cpp:106-111; DogLeg / steepest descent), on the device from
+ * the arrow blocks.  Unsharded handles. */
+int kb_rhs_jtj_rhs(kb_handle* h, double* out);
 /* Optimizer2::applyStateUpdate / revertLastStateUpdate (Optimizer2.cpp:290-318).
  * dx == NULL applies the device-resident dx of the last kb_solve. */
 int kb_apply_update(kb_handle* h, const double* dx, double* deltaX_out);

@@ -11,7 +11,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libkalibr_hip.so")
+# KB_DIAG_LIB=1 selects the diagnostic build (libkalibr_hip_stamps.so: stop points, timelines) for the tools
+LIB_PATH = os.path.join(_HERE, "libkalibr_hip_stamps.so" if os.environ.get("KB_DIAG_LIB") == "1" else "libkalibr_hip.so")
 _lib = None
 
 dp = C.POINTER(C.c_double)
@@ -20,7 +21,7 @@ dp = C.POINTER(C.c_double)
 EXPORTS = [
     "kb_create", "kb_destroy", "kb_last_error", "kb_upload_observations", "kb_set_state", "kb_set_state_flat",
     "kb_get_state_flat", "kb_state_size", "kb_num_cols", "kb_camera_cols", "kb_eval_cost", "kb_build",
-    "kb_set_constant_conditioner", "kb_set_conditioner", "kb_solve", "kb_get_rhs", "kb_apply_update", "kb_revert", "kb_get_normal_blocks",
+    "kb_set_constant_conditioner", "kb_set_conditioner", "kb_solve", "kb_get_rhs", "kb_rhs_jtj_rhs", "kb_apply_update", "kb_revert", "kb_get_normal_blocks",
     "kb_optimize", "kb_get_trace", "kb_run_gn_iterations", "kb_gn_prepare", "kb_gn_launch", "kb_build_kernel_stats",
     "kb_build_kernel_name", "kb_comm_get_unique_id",
     "kb_comm_init", "kb_comm_init_local", "kb_selftest_mfma", "kb_solve_marginal", "kb_analyze_marginal",
@@ -116,6 +117,7 @@ def lib():
         L.kb_set_conditioner.argtypes = [C.c_void_p, dp]
         L.kb_solve.argtypes = [C.c_void_p, dp, C.POINTER(C.c_int)]
         L.kb_get_rhs.argtypes = [C.c_void_p, dp]
+        L.kb_rhs_jtj_rhs.argtypes = [C.c_void_p, dp]
         L.kb_apply_update.argtypes = [C.c_void_p, dp, dp]
         L.kb_get_normal_blocks.argtypes = [C.c_void_p, dp, dp, dp, dp, dp, dp]
         L.kb_optimize.argtypes = [C.c_void_p, C.POINTER(OptimizerOptions), C.POINTER(Solution)]
@@ -290,6 +292,12 @@ class Solver:
         r = np.zeros(self.ncols)
         _check(lib().kb_get_rhs(self.h, _d(r)))
         return r
+
+    def rhs_jtj_rhs(self):
+        """kb_rhs_jtj_rhs: rhs^T (J^T J) rhs of the last build"""
+        v = C.c_double()
+        _check(lib().kb_rhs_jtj_rhs(self.h, C.byref(v)))
+        return v.value
 
     def apply_update(self, dx):
         dX = C.c_double()

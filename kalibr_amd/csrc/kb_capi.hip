@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -114,7 +115,9 @@ struct kb_handle {
   int WPB = 1;
   bool build_pipe = false;  // k_buildp (one wave per camera, N + 2 waves) instead of k_build
   bool buildp_wide = false;  // k_buildp<.., MW = 8> (multi-model rigs with <= 8 waves per block)
+  double* rjr = nullptr;     // [F + 1] kb_rhs_jtj_rhs: per-frame terms | result
   int gn_prepared = -1;      // kb_gn_prepare'd pass count, consumed by kb_gn_launch
+  size_t lds_colimg = 0;     // k_colimg's staging (per-camera sums, chains, T, column info)
   bool gn_graph = false;
   int build_threads = 64;
   size_t lds_build = 0, lds_camexp = 0, lds_schur = 0, lds_solve = 0;
@@ -403,7 +406,7 @@ kb_handle* kb_create(const kb_layout* L) {
   rc |= h->alloc(&d.ctrl, 1);
   if (h->C > 64) {  // k_solve's staged camera block (k_colimg), sized as in the LDS budget below
     const int nb = (h->C + 16) / 16;  // rows 0 .. C: the right-hand side is appended as row C
-    rc |= h->alloc(&d.simg, (size_t)kTileSz * nb * (nb + 1) / 2 + 16 * nb + 2 + 256 * (size_t)h->N);
+    rc |= h->alloc(&d.simg, (size_t)kTileSz * nb * (nb + 1) / 2 + 16 * nb + 2);
   }
   std::vector<int32_t> colinfo(h->C), tri(h->C * (h->C + 1) / 2);
   for (int i = 0; i < h->N; ++i)
@@ -442,12 +445,12 @@ kb_handle* kb_create(const kb_layout* L) {
     h->lds_schur = sizeof(double) * 16 * CZ;
     if (C <= 64) {
       h->lds_solve = sizeof(double) * (C * (C + 1) / 2 + 2 * C + 1 + N * 256 + 2 * N * N * 36) + sizeof(int) * C;
-    } else {  // 16 x 16 lower tiles (rows 0 .. C, b as row C) + the factor waves' scratch tiles + 1/D
-      // k_colimg image [lower tiles | rhs (n16 + 2) | per-camera sums] + gl + T + K + 2 scratch tiles + 1/D
+    } else {  // the k_colimg image (complete system: 16 x 16 lower tiles, b as row C | g_c) + the factored diagonal
+      // tiles and their inverses + 1/D
       const int nb = (C + 16) / 16, n16 = 16 * nb;
-      d.img_n = kTileSz * nb * (nb + 1) / 2 + n16 + 2 + N * 256;
-      h->lds_solve = sizeof(double) * (d.img_n + ((C + 1) & ~1) + 2 * N * N * 36 + 2 * kTileSz + n16) +
-                     sizeof(int) * C;
+      d.img_n = kTileSz * nb * (nb + 1) / 2 + n16 + 2;
+      h->lds_solve = sizeof(double) * (d.img_n + 2 + 2 * nb * kTileSz + n16) + sizeof(int) * C;
+      h->lds_colimg = sizeof(double) * (N * 256 + 2 * N * N * 36) + sizeof(int) * C;
     }
     h->solve_threads = C <= 64 ? 256 : 512;
     h->fn_solve = C <= 16   ? (const void*)k_solve<16>
@@ -481,6 +484,7 @@ kb_handle* kb_create(const kb_layout* L) {
   hipFuncSetAttribute((const void*)k_camexpand, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_camexp);
   hipFuncSetAttribute(h->fn_schur, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_schur);
   hipFuncSetAttribute(h->fn_solve, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_solve);
+  hipFuncSetAttribute((const void*)k_colimg, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_colimg);
   if (hipStreamSynchronize(h->stream) != hipSuccess) {
     fail("kb_create: stream sync failed");
     kb_destroy(h);
@@ -653,8 +657,8 @@ static int launch_colsum(kb_handle* h, int gate, bool finish = true) {
       nrows = 1;
     }
     double* out = sharded(h) ? h->psum_red : d.psum_local;
-    hipLaunchKernelGGL(k_colimg, dim3((d.Wtot + d.img_n + 255) / 256), dim3(256), 0, h->stream, d, rows, out, gate,
-                       nrows);
+    hipLaunchKernelGGL(k_colimg, dim3((d.Wtot + d.img_n + 255) / 256), dim3(256), h->lds_colimg, h->stream, d, rows,
+                       out, gate, nrows);
     KB_HIP(hipGetLastError());
     return 0;
   }
@@ -1015,6 +1019,20 @@ int kb_get_normal_blocks(kb_handle* h, double* Hff, double* Hfc, double* gf, dou
   return 0;
 }
 
+int kb_rhs_jtj_rhs(kb_handle* h, double* out) {
+  if (!h || !out) return fail("kb_rhs_jtj_rhs: null");
+  if (!h->uploaded) return fail("kb_rhs_jtj_rhs: no observations");
+  if (sharded(h)) return fail("kb_rhs_jtj_rhs: per-call quantity of an unsharded handle");
+  KB_HIP(hipSetDevice(h->device));
+  if (!h->rjr && h->alloc(&h->rjr, (size_t)h->F + 1)) return -1;
+  hipLaunchKernelGGL(k_rjr_frames, dim3((h->F + 3) / 4), dim3(256), 0, h->stream, h->d, h->rjr);
+  hipLaunchKernelGGL(k_rjr_final, dim3(1), dim3(256), 0, h->stream, h->d, h->rjr, h->rjr + h->F);
+  KB_HIP(hipGetLastError());
+  KB_HIP(hipMemcpyAsync(out, h->rjr + h->F, sizeof(double), hipMemcpyDeviceToHost, h->stream));
+  KB_HIP(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
 // ---------------------------------------------------------------- device-resident loop
 // One optimizer pass: build (+ fused Schur) | [schur, LM passes that keep the system] | colsum [all-reduce] |
 // solve (+ candidate camera chains) | backsub + cost, its last block: reduce, accept/revert, next prelude
@@ -1271,10 +1289,30 @@ int kb_build_kernel_stats(kb_handle* h, double* avg_ms, double* bytes_per_launch
     return 0;
   };
   const int cur0 = h->cur;
+  std::vector<hipEvent_t> ev(2 * (reps + warm), nullptr);
+  // every exit restores the snapshot (once taken) and frees the query's buffers: the handle is left as it was
+  struct Guard {
+    kb_handle* h;
+    double* save;
+    std::vector<hipEvent_t>* ev;
+    std::function<int(bool)> snap;
+    int cur0;
+    bool taken = false;
+    ~Guard() {
+      if (taken) {
+        snap(true);
+        hipStreamSynchronize(h->stream);
+        h->cur = cur0;
+      }
+      hipFree(save);
+      for (auto& e : *ev)
+        if (e) hipEventDestroy(e);
+    }
+  } guard{h, save, &ev, snap, cur0};
   if (snap(false)) return -1;
+  guard.taken = true;
   KbOpts o{1, 0x3fffffff, 0.0, -1.0, -1.0};
   if (loop_start(h, o)) return -1;
-  std::vector<hipEvent_t> ev(2 * (reps + warm));
   for (auto& e : ev) KB_HIP(hipEventCreate(&e));
   // the passes are captured in one graph, event records included, so the timed builds run exactly as in the
   // benchmarked graphs (no eager launch gaps around them); eager launches if this stack cannot capture events
@@ -1316,19 +1354,17 @@ int kb_build_kernel_stats(kb_handle* h, double* avg_ms, double* bytes_per_launch
     }
   }
   if (finish_pass(h, 1)) return -1;
-  if (snap(true)) return -1;
-  KB_HIP(hipStreamSynchronize(h->stream));
-  hipFree(save);
-  for (auto& e : ev) hipEventDestroy(e);
-  h->cur = cur0;
+  KB_HIP(hipStreamSynchronize(h->stream));  // (the guard restores the snapshot and frees the buffers)
   h->build_ms = tot / reps;
   if (avg_ms) *avg_ms = h->build_ms;
   // algorithmic bytes of one launch: observations (y 16 B + corner id 2 B per corner), view ranges (8 B per
-  // frame x camera), state and camera chains read; the previous step (dx_c, A_f, b_f) read; frame blocks
-  // (H_ff, g_f, H_fc), back-substitution rows (A_f, b_f), candidate poses and the per-block partial rows written.
+  // frame x camera), state and camera chains read; the previous step (dx_c, A_f, b_f) read; g_f (and outside GN
+  // fused passes H_ff, H_fc), back-substitution rows (A_f, b_f), candidate poses and the per-block partial rows
+  // written.
   const double C = h->C, F = h->F;
+  const double fblk = gn_fused(h, 1) ? 6.0 : 36.0 + 6.0 + 6.0 * C;
   const double bytes = 18.0 * h->NC + 8.0 * F * h->N + 8.0 * h->S + 8.0 * (12.0 * h->N + 36.0 * h->N * h->N) +
-                       8.0 * (C + F * (6 * C + 6)) + 8.0 * F * (36 + 6 + 6 * C) + 8.0 * F * (6 * C + 6 + 7) +
+                       8.0 * (C + F * (6 * C + 6)) + 8.0 * F * fblk + 8.0 * F * (6 * C + 6 + 7) +
                        8.0 * h->d.nblk * h->d.Wr;
   if (bytes_per_launch) *bytes_per_launch = bytes;
   // executed MFMA flops (2 x 16 x 16 x rows, rows padded to 64 per 32-corner phase) + ~300 VALU flops/corner
@@ -1417,21 +1453,73 @@ int kb_comm_init_local(kb_handle* const* hs, int32_t n) {
     if (hs[r]->N != hs[0]->N || hs[r]->C != hs[0]->C) return fail("kb_comm_init_local: handles of different rigs");
     F_max = std::max(F_max, hs[r]->F);
   }
+  // the group's kernels read every member's send buffer from their own device: members on different devices need
+  // peer access both ways (enabled here; groups whose devices cannot reach each other are refused)
+  for (int r = 0; r < n; ++r)
+    for (int q = 0; q < n; ++q) {
+      const int a = hs[r]->device, b = hs[q]->device;
+      if (a == b) continue;
+      int can = 0;
+      KB_HIP(hipDeviceCanAccessPeer(&can, a, b));
+      if (!can) return fail("kb_comm_init_local: devices of the group cannot access each other's memory");
+      KB_HIP(hipSetDevice(a));
+      const hipError_t e = hipDeviceEnablePeerAccess(b, 0);
+      if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
+        return fail(std::string("kb_comm_init_local: hipDeviceEnablePeerAccess: ") + hipGetErrorString(e));
+      hipGetLastError();
+    }
+  // everything that can fail runs before any handle joins: on failure the handles stay unsharded and usable
   kb_local_group* G = new kb_local_group();
   G->n = n;
   G->ready.assign(n, nullptr);
   G->done.assign(n, nullptr);
   G->src.assign(n, nullptr);
+  auto drop_group = [&]() {
+    for (auto e : G->ready)
+      if (e) hipEventDestroy(e);
+    for (auto e : G->done)
+      if (e) hipEventDestroy(e);
+    delete G;
+  };
   for (int r = 0; r < n; ++r) {
-    KB_HIP(hipSetDevice(hs[r]->device));
-    KB_HIP(hipEventCreateWithFlags(&G->ready[r], hipEventDisableTiming));
-    KB_HIP(hipEventCreateWithFlags(&G->done[r], hipEventDisableTiming));
+    if (hipSetDevice(hs[r]->device) != hipSuccess ||
+        hipEventCreateWithFlags(&G->ready[r], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&G->done[r], hipEventDisableTiming) != hipSuccess) {
+      drop_group();
+      return fail("kb_comm_init_local: event creation failed");
+    }
+  }
+  struct Saved {
+    KbDev d;
+    int nranks, rank, F_max;
+    double *psum_red, *psum_red8, *bpart_all;
+  };
+  std::vector<Saved> saved(n);
+  for (int r = 0; r < n; ++r) {
+    kb_handle* h = hs[r];
+    saved[r] = Saved{h->d, h->nranks, h->rank, h->F_max, h->psum_red, h->psum_red8, h->bpart_all};
   }
   for (int r = 0; r < n; ++r) {
-    KB_HIP(hipSetDevice(hs[r]->device));
+    if (hipSetDevice(hs[r]->device) != hipSuccess || shard_setup(hs[r], n, r, F_max)) {
+      for (int q = 0; q <= r; ++q) {  // roll back (buffers already allocated stay with the handle until kb_destroy)
+        kb_handle* h = hs[q];
+        const Saved& sv = saved[q];
+        h->d = sv.d;
+        h->nranks = sv.nranks;
+        h->rank = sv.rank;
+        h->F_max = sv.F_max;
+        h->psum_red = sv.psum_red;
+        h->psum_red8 = sv.psum_red8;
+        h->bpart_all = sv.bpart_all;
+        drop_graphs(h);
+      }
+      drop_group();
+      return fail(std::string("kb_comm_init_local: shard setup failed: ") + kb_last_error());
+    }
+  }
+  for (int r = 0; r < n; ++r) {  // publish: from here on the handles are ranks of the group
     hs[r]->lg = G;
     ++G->refs;
-    if (shard_setup(hs[r], n, r, F_max)) return -1;
   }
   return 0;
 }

@@ -118,7 +118,10 @@ struct KbDev {
 // timeline stamp (100 MHz s_memrealtime) of thread 0 at point i of the last launch, without leaving the kernel
 #define KB_TS(d, i)                                                                      \
   do {                                                                                   \
-    if (threadIdx.x == 0 && (d).dbg_ts) (d).dbg_ts[i] = __builtin_amdgcn_s_memrealtime(); \
+    if (threadIdx.x == 0 && (d).dbg_ts) {                                                \
+      (d).dbg_ts[i] = __builtin_amdgcn_s_memrealtime();                                  \
+      if ((i) == 0 || (i) == 7) (d).dbg_ts[60 + ((i) == 7)] = __builtin_amdgcn_s_memtime(); \
+    }                                                                                    \
   } while (0)
 // build-kernel timeline (k_buildp): lane 0 of the calling wave of block 0 stamps slot 64 + i
 #define KB_TSB(d, i)                                                                                        \

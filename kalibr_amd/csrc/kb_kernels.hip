@@ -69,6 +69,29 @@ __device__ __forceinline__ double dpp_d(double v) {
   return __longlong_as_double(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
 }
 
+// lane k's value to every lane of its 16-lane row (DPP row_newbcast, gfx90a+): a plain VALU move, without the
+// v_readlane -> SGPR -> VALU round trip.  k must fold to a constant (unrolled loops).
+__device__ __forceinline__ double bcast16(double v, int k) {
+  switch (k) {
+    case 0: return dpp_d<0x150>(v);
+    case 1: return dpp_d<0x151>(v);
+    case 2: return dpp_d<0x152>(v);
+    case 3: return dpp_d<0x153>(v);
+    case 4: return dpp_d<0x154>(v);
+    case 5: return dpp_d<0x155>(v);
+    case 6: return dpp_d<0x156>(v);
+    case 7: return dpp_d<0x157>(v);
+    case 8: return dpp_d<0x158>(v);
+    case 9: return dpp_d<0x159>(v);
+    case 10: return dpp_d<0x15A>(v);
+    case 11: return dpp_d<0x15B>(v);
+    case 12: return dpp_d<0x15C>(v);
+    case 13: return dpp_d<0x15D>(v);
+    case 14: return dpp_d<0x15E>(v);
+    default: return dpp_d<0x15F>(v);
+  }
+}
+
 // wave-wide sum / max, fixed order, result uniform: row butterflies by rotation, then the 4 row values
 __device__ __forceinline__ double wave_sum_d(double v) {
   v += dpp_d<0x128>(v);
@@ -960,7 +983,7 @@ __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
         for (int k = 0; k < 6; ++k) sacc += G[k * 6 + a] * H[k * 16 + 6 + q];
         sacc = has ? sacc : 0.0;  // G^T H_dI
         P[a * CZ + ctab[0][vc] + q] = sacc;
-        d.Hfc[((size_t)f * 6 + a) * C + ctab[0][vc] + q] = sacc;
+        if (!gfu) d.Hfc[((size_t)f * 6 + a) * C + ctab[0][vc] + q] = sacc;
       }
     }
     __syncthreads();
@@ -970,7 +993,7 @@ __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
         double sacc = 0.0;
         for (int i = 0; i < N; ++i) sacc += dH[i * 36 + q];
         Fh[q] = sacc;
-        d.Hff[(size_t)f * 36 + q] = sacc;
+        if (!gfu) d.Hff[(size_t)f * 36 + q] = sacc;
       } else if (q < 42) {
         double sacc = 0.0;
         for (int i = 0; i < N; ++i) sacc += dg[i * 8 + q - 36];
@@ -985,7 +1008,7 @@ __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
           for (int k = 0; k < 6; ++k) sacc += Pv[i * 36 + a * 6 + k] * K[k * 6 + b];
         }
         P[a * CZ + ctab[1][j] + b] = sacc;
-        d.Hfc[((size_t)f * 6 + a) * C + ctab[1][j] + b] = sacc;
+        if (!gfu) d.Hfc[((size_t)f * 6 + a) * C + ctab[1][j] + b] = sacc;
       }
     }
     KB_STAMP(d, 20);
@@ -1130,7 +1153,9 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
   for (int u = 0; u < kTgU; ++u) KB_KEEP(tv[u]);
   KB_KEEPS(fv.x);
   KB_KEEPS(fv.y);
-  const bool gfu = GNF && gate;  // GN fused: the previous solve's frame steps are applied here
+  // GN fused: the previous solve's frame steps are applied here, and H_ff / H_fc are not stored (only the per-call
+  // path reads them back: kb_build, k_schur, k_pcg; the fused pass consumes A_f, b_f and the Schur sums)
+  const bool gfu = GNF && gate;
   double yr[6][2], dxv[2] = {0.0, 0.0}, bq = 0.0;
   if (gfu) {
 #pragma unroll
@@ -1263,14 +1288,14 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
             if (i > j && i < N) sacc += v[i];
           if (q < 36) {
             Fh[q] = sacc;
-            d.Hff[(size_t)f * 36 + q] = sacc;
+            if (!gfu) d.Hff[(size_t)f * 36 + q] = sacc;
           } else if (q < 42) {
             P[(q - 36) * CZ + C] = sacc;
             d.gf[(size_t)f * 6 + q - 36] = sacc;
           } else {
             const int a = ab2 / 6, b = ab2 % 6;
             P[a * CZ + ctab[1][j] + b] = sacc;
-            d.Hfc[((size_t)f * 6 + a) * C + ctab[1][j] + b] = sacc;
+            if (!gfu) d.Hfc[((size_t)f * 6 + a) * C + ctab[1][j] + b] = sacc;
           }
         }
       }
@@ -1400,7 +1425,7 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
             T1[arow * 17 + i16] = t1[r];
             if (i16 >= 6 && i16 < 6 + nin) {  // G^T H_dI: the camera's intrinsic columns
               Pi[arow * CZ + ctab[0][cam] + i16 - 6] = t1[r];
-              d.Hfc[((size_t)f * 6 + arow) * C + ctab[0][cam] + i16 - 6] = t1[r];
+              if (!gfu) d.Hfc[((size_t)f * 6 + arow) * C + ctab[0][cam] + i16 - 6] = t1[r];
             } else if (i16 == 15) {
               dgv[arow] = t1[r];  // G^T g_d
             }
@@ -2009,76 +2034,304 @@ __device__ __forceinline__ void tile_sub(const double* src, double* dst, const v
   }
 }
 
-// panel q by factor wave fw (see above); Dsc: this wave's 16 x kTS scratch tile.  Returns false on a non-positive
-// pivot of a real row (< C); the b row's pivot and the identity padding are not tested.
-__device__ __forceinline__ bool panel_factor(double* S, double* rD, double* Dsc, int q, int nb, int C, int fw) {
-  const int lane = threadIdx.x & 63, r = lane & 15, t = lane >> 4;
-  if (q > 0) {
-    // lookahead: panel q-1 applied to the wave's tiles (all products first, then the stores)
-    const double* rdq = rD + 16 * (q - 1);
-    const double* Wq = S + tile_base(q, q - 1);
-    v4d acc[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int iu = u == 0 ? q : q + 3 * fw + u;
-      acc[u] = tile_prod(S + tile_base(iu < nb ? iu : q, q - 1), Wq, rdq, lane);
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int iu = u == 0 ? q : q + 3 * fw + u;
-      if (iu < nb) tile_sub(S + tile_base(iu, q), u == 0 ? Dsc : S + tile_base(iu, q), acc[u], lane);
-    }
-    KB_WAVE_SYNC();  // the wave's own tile stores, read back below by other lanes
+// v_readlane of M doubles of one lane in one asm statement: each value gets its own SGPR pair, so the reads
+// issue back to back and the FMAs that consume them do not wait on one readlane each (separate readlanes are
+// scheduled into one reused SGPR pair under k_solve's SGPR pressure, which serialises them).  L: the lane.
+template <int L>
+__device__ __forceinline__ void rl1(double v0, double& o0) {
+  const unsigned long long b0 = __double_as_longlong(v0);
+  const unsigned l0 = (unsigned)b0, h0 = (unsigned)(b0 >> 32);
+  unsigned sl0, sh0;
+  asm("s_nop 1\nv_readlane_b32 %0, %2, %4\nv_readlane_b32 %1, %3, %4\ns_nop 1"
+      : "=s"(sl0), "=s"(sh0)
+      : "v"(l0), "v"(h0), "i"(L));
+  o0 = __longlong_as_double(((unsigned long long)sh0 << 32) | sl0);
+}
+template <int L>
+__device__ __forceinline__ void rl2(double v0, double v1, double& o0, double& o1) {
+  const unsigned long long b0 = __double_as_longlong(v0);
+  const unsigned l0 = (unsigned)b0, h0 = (unsigned)(b0 >> 32);
+  unsigned sl0, sh0;
+  const unsigned long long b1 = __double_as_longlong(v1);
+  const unsigned l1 = (unsigned)b1, h1 = (unsigned)(b1 >> 32);
+  unsigned sl1, sh1;
+  asm("s_nop 1\nv_readlane_b32 %0, %4, %8\nv_readlane_b32 %1, %5, %8\nv_readlane_b32 %2, %6, %8\nv_readlane_b32 %3, %7, %8\ns_nop 1"
+      : "=s"(sl0), "=s"(sh0), "=s"(sl1), "=s"(sh1)
+      : "v"(l0), "v"(h0), "v"(l1), "v"(h1), "i"(L));
+  o0 = __longlong_as_double(((unsigned long long)sh0 << 32) | sl0);
+  o1 = __longlong_as_double(((unsigned long long)sh1 << 32) | sl1);
+}
+template <int L>
+__device__ __forceinline__ void rl3(double v0, double v1, double v2, double& o0, double& o1, double& o2) {
+  const unsigned long long b0 = __double_as_longlong(v0);
+  const unsigned l0 = (unsigned)b0, h0 = (unsigned)(b0 >> 32);
+  unsigned sl0, sh0;
+  const unsigned long long b1 = __double_as_longlong(v1);
+  const unsigned l1 = (unsigned)b1, h1 = (unsigned)(b1 >> 32);
+  unsigned sl1, sh1;
+  const unsigned long long b2 = __double_as_longlong(v2);
+  const unsigned l2 = (unsigned)b2, h2 = (unsigned)(b2 >> 32);
+  unsigned sl2, sh2;
+  asm("s_nop 1\nv_readlane_b32 %0, %6, %12\nv_readlane_b32 %1, %7, %12\nv_readlane_b32 %2, %8, %12\nv_readlane_b32 %3, %9, %12\nv_readlane_b32 %4, %10, %12\nv_readlane_b32 %5, %11, %12\ns_nop 1"
+      : "=s"(sl0), "=s"(sh0), "=s"(sl1), "=s"(sh1), "=s"(sl2), "=s"(sh2)
+      : "v"(l0), "v"(h0), "v"(l1), "v"(h1), "v"(l2), "v"(h2), "i"(L));
+  o0 = __longlong_as_double(((unsigned long long)sh0 << 32) | sl0);
+  o1 = __longlong_as_double(((unsigned long long)sh1 << 32) | sl1);
+  o2 = __longlong_as_double(((unsigned long long)sh2 << 32) | sl2);
+}
+template <int L>
+__device__ __forceinline__ void rl4(double v0, double v1, double v2, double v3, double& o0, double& o1, double& o2, double& o3) {
+  const unsigned long long b0 = __double_as_longlong(v0);
+  const unsigned l0 = (unsigned)b0, h0 = (unsigned)(b0 >> 32);
+  unsigned sl0, sh0;
+  const unsigned long long b1 = __double_as_longlong(v1);
+  const unsigned l1 = (unsigned)b1, h1 = (unsigned)(b1 >> 32);
+  unsigned sl1, sh1;
+  const unsigned long long b2 = __double_as_longlong(v2);
+  const unsigned l2 = (unsigned)b2, h2 = (unsigned)(b2 >> 32);
+  unsigned sl2, sh2;
+  const unsigned long long b3 = __double_as_longlong(v3);
+  const unsigned l3 = (unsigned)b3, h3 = (unsigned)(b3 >> 32);
+  unsigned sl3, sh3;
+  asm("s_nop 1\nv_readlane_b32 %0, %8, %16\nv_readlane_b32 %1, %9, %16\nv_readlane_b32 %2, %10, %16\nv_readlane_b32 %3, %11, %16\nv_readlane_b32 %4, %12, %16\nv_readlane_b32 %5, %13, %16\nv_readlane_b32 %6, %14, %16\nv_readlane_b32 %7, %15, %16\ns_nop 1"
+      : "=s"(sl0), "=s"(sh0), "=s"(sl1), "=s"(sh1), "=s"(sl2), "=s"(sh2), "=s"(sl3), "=s"(sh3)
+      : "v"(l0), "v"(h0), "v"(l1), "v"(h1), "v"(l2), "v"(h2), "v"(l3), "v"(h3), "i"(L));
+  o0 = __longlong_as_double(((unsigned long long)sh0 << 32) | sl0);
+  o1 = __longlong_as_double(((unsigned long long)sh1 << 32) | sl1);
+  o2 = __longlong_as_double(((unsigned long long)sh2 << 32) | sl2);
+  o3 = __longlong_as_double(((unsigned long long)sh3 << 32) | sl3);
+}
+template <int L>
+__device__ __forceinline__ void rl5(double v0, double v1, double v2, double v3, double v4, double& o0, double& o1, double& o2, double& o3, double& o4) {
+  const unsigned long long b0 = __double_as_longlong(v0);
+  const unsigned l0 = (unsigned)b0, h0 = (unsigned)(b0 >> 32);
+  unsigned sl0, sh0;
+  const unsigned long long b1 = __double_as_longlong(v1);
+  const unsigned l1 = (unsigned)b1, h1 = (unsigned)(b1 >> 32);
+  unsigned sl1, sh1;
+  const unsigned long long b2 = __double_as_longlong(v2);
+  const unsigned l2 = (unsigned)b2, h2 = (unsigned)(b2 >> 32);
+  unsigned sl2, sh2;
+  const unsigned long long b3 = __double_as_longlong(v3);
+  const unsigned l3 = (unsigned)b3, h3 = (unsigned)(b3 >> 32);
+  unsigned sl3, sh3;
+  const unsigned long long b4 = __double_as_longlong(v4);
+  const unsigned l4 = (unsigned)b4, h4 = (unsigned)(b4 >> 32);
+  unsigned sl4, sh4;
+  asm("s_nop 1\nv_readlane_b32 %0, %10, %20\nv_readlane_b32 %1, %11, %20\nv_readlane_b32 %2, %12, %20\nv_readlane_b32 %3, %13, %20\nv_readlane_b32 %4, %14, %20\nv_readlane_b32 %5, %15, %20\nv_readlane_b32 %6, %16, %20\nv_readlane_b32 %7, %17, %20\nv_readlane_b32 %8, %18, %20\nv_readlane_b32 %9, %19, %20\ns_nop 1"
+      : "=s"(sl0), "=s"(sh0), "=s"(sl1), "=s"(sh1), "=s"(sl2), "=s"(sh2), "=s"(sl3), "=s"(sh3), "=s"(sl4), "=s"(sh4)
+      : "v"(l0), "v"(h0), "v"(l1), "v"(h1), "v"(l2), "v"(h2), "v"(l3), "v"(h3), "v"(l4), "v"(h4), "i"(L));
+  o0 = __longlong_as_double(((unsigned long long)sh0 << 32) | sl0);
+  o1 = __longlong_as_double(((unsigned long long)sh1 << 32) | sl1);
+  o2 = __longlong_as_double(((unsigned long long)sh2 << 32) | sl2);
+  o3 = __longlong_as_double(((unsigned long long)sh3 << 32) | sl3);
+  o4 = __longlong_as_double(((unsigned long long)sh4 << 32) | sl4);
+}
+template <int L>
+__device__ __forceinline__ void rl6(double v0, double v1, double v2, double v3, double v4, double v5, double& o0, double& o1, double& o2, double& o3, double& o4, double& o5) {
+  const unsigned long long b0 = __double_as_longlong(v0);
+  const unsigned l0 = (unsigned)b0, h0 = (unsigned)(b0 >> 32);
+  unsigned sl0, sh0;
+  const unsigned long long b1 = __double_as_longlong(v1);
+  const unsigned l1 = (unsigned)b1, h1 = (unsigned)(b1 >> 32);
+  unsigned sl1, sh1;
+  const unsigned long long b2 = __double_as_longlong(v2);
+  const unsigned l2 = (unsigned)b2, h2 = (unsigned)(b2 >> 32);
+  unsigned sl2, sh2;
+  const unsigned long long b3 = __double_as_longlong(v3);
+  const unsigned l3 = (unsigned)b3, h3 = (unsigned)(b3 >> 32);
+  unsigned sl3, sh3;
+  const unsigned long long b4 = __double_as_longlong(v4);
+  const unsigned l4 = (unsigned)b4, h4 = (unsigned)(b4 >> 32);
+  unsigned sl4, sh4;
+  const unsigned long long b5 = __double_as_longlong(v5);
+  const unsigned l5 = (unsigned)b5, h5 = (unsigned)(b5 >> 32);
+  unsigned sl5, sh5;
+  asm("s_nop 1\nv_readlane_b32 %0, %12, %24\nv_readlane_b32 %1, %13, %24\nv_readlane_b32 %2, %14, %24\nv_readlane_b32 %3, %15, %24\nv_readlane_b32 %4, %16, %24\nv_readlane_b32 %5, %17, %24\nv_readlane_b32 %6, %18, %24\nv_readlane_b32 %7, %19, %24\nv_readlane_b32 %8, %20, %24\nv_readlane_b32 %9, %21, %24\nv_readlane_b32 %10, %22, %24\nv_readlane_b32 %11, %23, %24\ns_nop 1"
+      : "=s"(sl0), "=s"(sh0), "=s"(sl1), "=s"(sh1), "=s"(sl2), "=s"(sh2), "=s"(sl3), "=s"(sh3), "=s"(sl4), "=s"(sh4), "=s"(sl5), "=s"(sh5)
+      : "v"(l0), "v"(h0), "v"(l1), "v"(h1), "v"(l2), "v"(h2), "v"(l3), "v"(h3), "v"(l4), "v"(h4), "v"(l5), "v"(h5), "i"(L));
+  o0 = __longlong_as_double(((unsigned long long)sh0 << 32) | sl0);
+  o1 = __longlong_as_double(((unsigned long long)sh1 << 32) | sl1);
+  o2 = __longlong_as_double(((unsigned long long)sh2 << 32) | sl2);
+  o3 = __longlong_as_double(((unsigned long long)sh3 << 32) | sl3);
+  o4 = __longlong_as_double(((unsigned long long)sh4 << 32) | sl4);
+  o5 = __longlong_as_double(((unsigned long long)sh5 << 32) | sl5);
+}
+template <int L>
+__device__ __forceinline__ void rl7(double v0, double v1, double v2, double v3, double v4, double v5, double v6, double& o0, double& o1, double& o2, double& o3, double& o4, double& o5, double& o6) {
+  const unsigned long long b0 = __double_as_longlong(v0);
+  const unsigned l0 = (unsigned)b0, h0 = (unsigned)(b0 >> 32);
+  unsigned sl0, sh0;
+  const unsigned long long b1 = __double_as_longlong(v1);
+  const unsigned l1 = (unsigned)b1, h1 = (unsigned)(b1 >> 32);
+  unsigned sl1, sh1;
+  const unsigned long long b2 = __double_as_longlong(v2);
+  const unsigned l2 = (unsigned)b2, h2 = (unsigned)(b2 >> 32);
+  unsigned sl2, sh2;
+  const unsigned long long b3 = __double_as_longlong(v3);
+  const unsigned l3 = (unsigned)b3, h3 = (unsigned)(b3 >> 32);
+  unsigned sl3, sh3;
+  const unsigned long long b4 = __double_as_longlong(v4);
+  const unsigned l4 = (unsigned)b4, h4 = (unsigned)(b4 >> 32);
+  unsigned sl4, sh4;
+  const unsigned long long b5 = __double_as_longlong(v5);
+  const unsigned l5 = (unsigned)b5, h5 = (unsigned)(b5 >> 32);
+  unsigned sl5, sh5;
+  const unsigned long long b6 = __double_as_longlong(v6);
+  const unsigned l6 = (unsigned)b6, h6 = (unsigned)(b6 >> 32);
+  unsigned sl6, sh6;
+  asm("s_nop 1\nv_readlane_b32 %0, %14, %28\nv_readlane_b32 %1, %15, %28\nv_readlane_b32 %2, %16, %28\nv_readlane_b32 %3, %17, %28\nv_readlane_b32 %4, %18, %28\nv_readlane_b32 %5, %19, %28\nv_readlane_b32 %6, %20, %28\nv_readlane_b32 %7, %21, %28\nv_readlane_b32 %8, %22, %28\nv_readlane_b32 %9, %23, %28\nv_readlane_b32 %10, %24, %28\nv_readlane_b32 %11, %25, %28\nv_readlane_b32 %12, %26, %28\nv_readlane_b32 %13, %27, %28\ns_nop 1"
+      : "=s"(sl0), "=s"(sh0), "=s"(sl1), "=s"(sh1), "=s"(sl2), "=s"(sh2), "=s"(sl3), "=s"(sh3), "=s"(sl4), "=s"(sh4), "=s"(sl5), "=s"(sh5), "=s"(sl6), "=s"(sh6)
+      : "v"(l0), "v"(h0), "v"(l1), "v"(h1), "v"(l2), "v"(h2), "v"(l3), "v"(h3), "v"(l4), "v"(h4), "v"(l5), "v"(h5), "v"(l6), "v"(h6), "i"(L));
+  o0 = __longlong_as_double(((unsigned long long)sh0 << 32) | sl0);
+  o1 = __longlong_as_double(((unsigned long long)sh1 << 32) | sl1);
+  o2 = __longlong_as_double(((unsigned long long)sh2 << 32) | sl2);
+  o3 = __longlong_as_double(((unsigned long long)sh3 << 32) | sl3);
+  o4 = __longlong_as_double(((unsigned long long)sh4 << 32) | sl4);
+  o5 = __longlong_as_double(((unsigned long long)sh5 << 32) | sl5);
+  o6 = __longlong_as_double(((unsigned long long)sh6 << 32) | sl6);
+}
+
+// row[J0 .. J0 + M - 1] of lane L into bc[] (M <= 7: one asm statement)
+template <int L, int J0, int M>
+__device__ __forceinline__ void rl_chunk(const double (&row)[16], double (&bc)[16]) {
+  if constexpr (M == 1) rl1<L>(row[J0], bc[J0]);
+  else if constexpr (M == 2) rl2<L>(row[J0], row[J0 + 1], bc[J0], bc[J0 + 1]);
+  else if constexpr (M == 3) rl3<L>(row[J0], row[J0 + 1], row[J0 + 2], bc[J0], bc[J0 + 1], bc[J0 + 2]);
+  else if constexpr (M == 4)
+    rl4<L>(row[J0], row[J0 + 1], row[J0 + 2], row[J0 + 3], bc[J0], bc[J0 + 1], bc[J0 + 2], bc[J0 + 3]);
+  else if constexpr (M == 5)
+    rl5<L>(row[J0], row[J0 + 1], row[J0 + 2], row[J0 + 3], row[J0 + 4], bc[J0], bc[J0 + 1], bc[J0 + 2], bc[J0 + 3],
+           bc[J0 + 4]);
+  else if constexpr (M == 6)
+    rl6<L>(row[J0], row[J0 + 1], row[J0 + 2], row[J0 + 3], row[J0 + 4], row[J0 + 5], bc[J0], bc[J0 + 1], bc[J0 + 2],
+           bc[J0 + 3], bc[J0 + 4], bc[J0 + 5]);
+  else
+    rl7<L>(row[J0], row[J0 + 1], row[J0 + 2], row[J0 + 3], row[J0 + 4], row[J0 + 5], row[J0 + 6], bc[J0], bc[J0 + 1],
+           bc[J0 + 2], bc[J0 + 3], bc[J0 + 4], bc[J0 + 5], bc[J0 + 6]);
+}
+// row[J0 .. 15] of lane L into bc[], chunks of 7
+template <int L, int J0>
+__device__ __forceinline__ void rl_tail(const double (&row)[16], double (&bc)[16]) {
+  if constexpr (J0 < 16) {
+    constexpr int M = (16 - J0) < 7 ? (16 - J0) : 7;
+    rl_chunk<L, J0, M>(row, bc);
+    rl_tail<L, J0 + M>(row, bc);
   }
+}
+
+// 1/x by v_rcp_f64 + one Newton step (the pivot chain of the panel factorisation: one FMA pair shorter)
+__device__ __forceinline__ double recip_d1(double x) {
+  const double r = __builtin_amdgcn_rcp(x);
+  return fma(r, fma(-x, r, 1.0), r);
+}
+
+// pivot steps K .. 15 of the lane-row panel factorisation (row k of the trailing matrix broadcast from lane k).
+// Every lane applies f = row[k] / D_k: lanes above the pivot hold zeros right of their own pivot (their own step
+// cancelled them: f = 1 against their own row), so no lane mask sits in the pivot chain.
+template <int K>
+__device__ __forceinline__ void panel_steps(double (&row)[16], int lane, int q, int C, bool& ok, double& rd) {
+  if constexpr (K < 16) {
+    double bc[16];
+    rl_tail<K, K>(row, bc);  // bc[K] = D_K, bc[j] = S[K][j]
+    const double Dk = bc[K];
+    const double rdk = Dk > 0.0 ? recip_d1(Dk) : 0.0;
+    const double f = row[K] * rdk;
+#pragma unroll
+    for (int j = K + 1; j < 16; ++j) row[j] -= f * bc[j];
+    ok = ok & ((Dk > 0.0) | (16 * q + K >= C));  // bitwise: no branch per pivot
+    rd = (lane == K) ? rdk : rd;
+    panel_steps<K + 1>(row, lane, q, C, ok, rd);
+  }
+}
+
+// panel q by factor wave fw (rows in registers, one per lane: lanes 0..15 the diagonal tile, lanes 16..63 the rows of
+// tiles q+1+3fw .. q+3+3fw).  The tiles of column q are complete (every earlier panel applied).  W rows go back in
+// place, the factored diagonal tile (W strictly below, D on the diagonal) to Dfac (wave 0), 1/D to rD.  Returns false
+// on a non-positive pivot of a real row (< C); the b row's pivot and the identity padding are not tested.
+__device__ __forceinline__ bool panel_factor(const KbDev& d, double* S, double* rD, double* Dfac, int q, int nb, int C,
+                                             int fw) {
+  const int lane = threadIdx.x & 63, r = lane & 15, t = lane >> 4;
   const int ti_raw = q + 3 * fw + t;
   const bool live = t == 0 || ti_raw < nb;
-  const double* base = t == 0 ? (q > 0 ? Dsc : S + tile_base(q, q)) : S + tile_base(live ? ti_raw : q, q);
+  // the lane's row (diagonal tiles are whole, so every lane reads 16 consecutive entries)
+  double* base = S + tile_base(t == 0 ? q : (live ? ti_raw : q), q) + r * kTS;
   double row[16];
 #pragma unroll
-  for (int c = 0; c < 16; ++c) {
-    const int e = t == 0 ? (r > c ? r * kTS + c : c * kTS + r) : r * kTS + c;
-    row[c] = base[e];
-  }
+  for (int c = 0; c < 16; ++c) row[c] = base[c];
   bool ok = true;
   double rd = 1.0;
+#ifdef KB_STAMPS
 #pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    const double Dk = readlane_d(row[k], k);
-    ok = ok & ((Dk > 0.0) | (16 * q + k >= C));  // bitwise: no branch per pivot
-    const double rdk = Dk > 0.0 ? recip_d(Dk) : 0.0;
-    rd = (lane == k) ? rdk : rd;
-    const double f = (lane > k) ? row[k] * rdk : 0.0;
+  for (int c = 0; c < 16; ++c) KB_KEEP(row[c]);
+#endif
+  if (q == 2 && fw == 0) KB_TS(d, 41);
+  panel_steps<0>(row, lane, q, C, ok, rd);
+#ifdef KB_STAMPS
 #pragma unroll
-    for (int j = k + 1; j < 16; ++j) row[j] -= f * readlane_d(row[j], k);
-  }
-  if (t == 0) {
-    if (fw == 0) {
-      double* dd = S + tile_base(q, q) + r * kTS;
+  for (int c = 0; c < 16; ++c) KB_KEEP(row[c]);
+  KB_KEEP(rd);
+#endif
+  if (q == 2 && fw == 0) KB_TS(d, 42);
+  if (t > 0 && live) {
 #pragma unroll
-      for (int c = 0; c < 16; ++c)
-        if (c <= r) dd[c] = row[c];
-      rD[16 * q + r] = rd;
-    }
-  } else if (live) {
-    double* dd = S + tile_base(ti_raw, q) + r * kTS;
+    for (int c = 0; c < 16; ++c) base[c] = row[c];
+  } else if (t == 0 && fw == 0) {
+    double* dd = Dfac + q * kTileSz + r * kTS;
 #pragma unroll
     for (int c = 0; c < 16; ++c) dd[c] = row[c];
+    rD[16 * q + r] = rd;
   }
   return ok;
 }
 
-// the factorisation (every thread of the 8-wave block calls it).  Factor waves: 0 and 1 (while panel q has more
-// than three tiles below it); update waves: 2, 3, 6, 7 (waves 4 and 5 share the factor waves' SIMDs and stay idle,
-// so that the MFMA tiles do not slow the pivot chain).  okl is cleared on a non-positive real pivot.
-__device__ __forceinline__ void ldl_panels(const KbDev& d, double* S, double* rD, double* Dsc, int C, int nb, int* okl) {
+// X = Ltilde_tt^-1 of factored diagonal tile t (unit lower, Ltilde = W D^-1) into Xinv[t] (row-major, stride kTS), by
+// one wave: lane (g, r) holds X[r][4g .. 4g+3]; step m subtracts L[r][m] X[m][:] from the rows r > m, X[m] broadcast
+// within each 16-lane group by DPP (off the factorisation's critical path: the backsolve's tile mat-vecs use it)
+__device__ __forceinline__ void tile_unit_inverse(const double* Dfac, const double* rD, double* Xinv, int t) {
+  const int lane = threadIdx.x & 63, g = lane >> 4, r = lane & 15;
+  const double* Lr = Dfac + t * kTileSz + r * kTS;
+  double L[16];
+#pragma unroll
+  for (int m = 0; m < 16; ++m) L[m] = (m < r) ? Lr[m] * rD[16 * t + m] : 0.0;
+  double X[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) X[j] = (4 * g + j == r) ? 1.0 : 0.0;
+#pragma unroll
+  for (int m = 0; m < 15; ++m) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) X[j] = fma(-L[m], bcast16(X[j], m), X[j]);
+  }
+  double* xo = Xinv + t * kTileSz + r * kTS + 4 * g;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) xo[j] = X[j];
+}
+
+// the factorisation (every thread of the 8-wave block calls it); two phases per panel q:
+//   A (q > 0): column q of the trailing matrix gets panel q-1 (tiles (q + w, q), one per wave w, on MFMA);
+//   B: factor waves 0 (and 1 while panel q has more than three tiles below it) factor panel q; update waves 2, 3, 6, 7
+//      apply panel q-1 to the remaining trailing tiles (i, j), j > q (waves 4 and 5 share the factor waves' SIMDs and
+//      stay idle so that the MFMA tiles do not slow the pivot chain); wave 7 then inverts the previous panel's factored
+//      diagonal tile (Xinv, for the backsolve's mat-vecs).
+// okl is cleared on a non-positive real pivot.
+__device__ __forceinline__ void ldl_panels(const KbDev& d, double* S, double* rD, double* Dfac, double* Xinv, int C, int nb,
+                                           int* okl) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int ow = wave == 2 ? 0 : wave == 3 ? 1 : wave == 6 ? 2 : wave == 7 ? 3 : -1;
 #pragma unroll 1
   for (int q = 0; q < nb; ++q) {
+    if (q > 0) {
+      const int i = q + wave;
+      if (i < nb) {
+        const v4d acc = tile_prod(S + tile_base(i, q - 1), S + tile_base(q, q - 1), rD + 16 * (q - 1), lane);
+        tile_sub(S + tile_base(i, q), S + tile_base(i, q), acc, lane);
+      }
+      __syncthreads();
+    }
     const int nf = (nb - 1 - q) > 3 ? 2 : 1;
     if (wave < nf) {
       if (wave == 0) KB_TS(d, 20 + 2 * q);
-      const bool ok = panel_factor(S, rD, Dsc + wave * kTileSz, q, nb, C, wave);
+      const bool ok = panel_factor(d, S, rD, Dfac, q, nb, C, wave);
       if (wave == 0) {
         if (!ok && lane == 0) *okl = 0;
         KB_WAVE_SYNC();
@@ -2088,127 +2341,110 @@ __device__ __forceinline__ void ldl_panels(const KbDev& d, double* S, double* rD
       // panel q-1 on tiles (q+1+ii, q+1+jj), 0 <= jj <= ii < m
       const int m = nb - 1 - q, ntiles = m * (m + 1) / 2;
       const double* rdq = rD + 16 * (q - 1);
+      // two tiles at a time: all their operands in one round of LDS loads, then 8 MFMAs in two chains
 #pragma unroll 1
-      for (int qq = ow; qq < ntiles; qq += 4) {
-        const int ii = tri_row(qq), jj = qq - ii * (ii + 1) / 2;
-        const int i = q + 1 + ii, j = q + 1 + jj;
-        const v4d acc = tile_prod(S + tile_base(i, q - 1), S + tile_base(j, q - 1), rdq, lane);
-        tile_sub(S + tile_base(i, j), S + tile_base(i, j), acc, lane);
+      for (int qq = ow; qq < ntiles; qq += 8) {
+        const int qb = min(qq + 4, ntiles - 1);
+        const int ia = tri_row(qq), ja = qq - ia * (ia + 1) / 2, ib = tri_row(qb), jb = qb - ib * (ib + 1) / 2;
+        const double* Wia = S + tile_base(q + 1 + ia, q - 1);
+        const double* Wja = S + tile_base(q + 1 + ja, q - 1);
+        const double* Wib = S + tile_base(q + 1 + ib, q - 1);
+        const double* Wjb = S + tile_base(q + 1 + jb, q - 1);
+        const int r16 = lane & 15, kq = lane >> 4;
+        double aa[4], ba[4], ab[4], bb[4];
+#pragma unroll
+        for (int st = 0; st < 4; ++st) {
+          const int k = 4 * st + kq;
+          const double rk = rdq[k];
+          aa[st] = Wia[r16 * kTS + k];
+          ba[st] = Wja[r16 * kTS + k] * rk;
+          ab[st] = Wib[r16 * kTS + k];
+          bb[st] = Wjb[r16 * kTS + k] * rk;
+        }
+        v4d acca = {0.0, 0.0, 0.0, 0.0}, accb = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int st = 0; st < 4; ++st) {
+          acca = __builtin_amdgcn_mfma_f64_16x16x4f64(aa[st], ba[st], acca, 0, 0, 0);
+          accb = __builtin_amdgcn_mfma_f64_16x16x4f64(ab[st], bb[st], accb, 0, 0, 0);
+        }
+        double* Ta = S + tile_base(q + 1 + ia, q + 1 + ja);
+        tile_sub(Ta, Ta, acca, lane);
+        if (qq + 4 < ntiles) {  // wave-uniform
+          double* Tb = S + tile_base(q + 1 + ib, q + 1 + jb);
+          tile_sub(Tb, Tb, accb, lane);
+        }
       }
+      // the factored diagonal tiles' inverses for the backsolve, where the trailing work has thinned out: tile t at
+      // panel max(t + 1, min(4, nb - 1)) by update wave t mod 4 (the last tile, holding row C, is solved by its chain)
+      for (int t = ow; t < nb - 1; t += 4)
+        if (q == max(t + 1, min(4, nb - 1))) tile_unit_inverse(Dfac, rD, Xinv, t);
     }
     __syncthreads();
     KB_TS(d, 10 + q);
   }
 }
 
-// Camera block expansion of the tiled solve (CM == 0) on MFMA.  The baseline rows of H_cc and g_c are one product
-//   Z = Kcat^T [U | D | g]      (6(N-1) x (6(N-1) + CI + 1), inner dimension 6N):
-//   Kcat[6i + m][6j + a] = K_{i,j}[m][a] (zero for j >= i), U[6i + m][6k + b] = T_{i,k}[m][b] = (H_i,dd K_{i,k})[m][b],
-//   D[6i + m][p] = H_i[m][6 + x] for intrinsic column p = (camera i, index x) and zero for the other cameras'
-//   columns, g[6i + m] = H_i[m][15].  Z's first 6(N-1) columns are the baseline x baseline block (sum over i > max(j, k)
-//   of K_{i,j}^T H_i,dd K_{i,k}), the next CI the baseline x intrinsic block, the last the baselines' gradient
-//   (CalibrationTools.hpp:404-408 chains; the same sums as cam_entry_l / cam_grad_l).  The intrinsic x intrinsic
-//   blocks and gradients are H_i[II] and H_i[I][15] (one thread per entry).  Every entry is written by one thread:
-//   S lower tiles += H_cc (+ lambda^2 or the conditioner on the diagonal), row C of S = b + g (the right-hand side of
-//   the factorisation), gl / gc / rhs = g.
-__device__ __forceinline__ void cam_expand_tiles(const KbDev& d, double* S, const double* bv, double* gl,
-                                                 const double* Hs, const double* T, const double* K, const int* ci,
-                                                 const int (*ctab)[KB_MAX_CAMS], double lam2, const double* cd2) {
-  const int C = d.C, N = d.N, tid = threadIdx.x, nth = blockDim.x, wave = tid >> 6, lane = tid & 63, nw = nth >> 6;
-  const int NB6 = 6 * (N - 1), CI = C - NB6, NK = 6 * N;
-  // intrinsic x intrinsic blocks (lower) and the intrinsic gradients
-  for (int q = tid; q < N * KB_MAX_INTR * KB_MAX_INTR; q += nth) {
-    const int i = q / (KB_MAX_INTR * KB_MAX_INTR), x = (q / KB_MAX_INTR) % KB_MAX_INTR, y = q % KB_MAX_INTR;
-    const int nin = ctab[0][i], c0 = ctab[1][i];
-    if (x < nin && y <= x) {
-      const int p = c0 + x;
-      S[tidx(p, c0 + y)] += Hs[i * 256 + (6 + x) * 16 + 6 + y] + ((x == y) ? (cd2 ? cd2[p] : lam2) : 0.0);
-      if (y == 0) {
-        const double g = Hs[i * 256 + (6 + x) * 16 + 15];
-        S[tidx(C, p)] = bv[p] + g;
-        gl[p] = g;
-        d.gc[p] = g;
-        d.rhs[p] = g;
-      }
-    }
-  }
-  if (N < 2) return;
-  const int nrt = (NB6 + 15) >> 4, nct = (NB6 + CI + 16) >> 4, nks = (NK + 3) >> 2;
-  const int i16 = lane & 15, kq = lane >> 4;
-  for (int tq = wave; tq < nrt * nct; tq += nw) {
-    const int rt = tq / nct, ct = tq - rt * nct;
-    const int r = 16 * rt + i16, c = 16 * ct + i16;  // the lane's A row and B column
-    const int rj = r / 6, ra = r - 6 * rj;
-    const int cb = c < NB6 ? c / 6 : 0, cbb = c - 6 * cb;
-    const int p = c - NB6;  // intrinsic column (NB6 <= c < NB6 + CI)
-    const int pinfo = ci[min(max(p, 0), C - 1)], pcam = (pinfo >> 8) & 0xff, px = pinfo & 0xff;
-    v4d acc = {0.0, 0.0, 0.0, 0.0};
-    for (int st = 0; st < nks; ++st) {
-      const int k = 4 * st + kq, ki = k / 6, km = k - 6 * ki;
-      const int kic = min(ki, N - 1);
-      double a = K[(kic * N + min(rj, N - 1)) * 36 + km * 6 + ra];
-      a = (r < NB6 && k < NK) ? a : 0.0;
-      double b;
-      if (c < NB6) {
-        b = T[(kic * N + cb) * 36 + km * 6 + cbb];
-      } else if (c < NB6 + CI) {
-        b = Hs[kic * 256 + km * 16 + 6 + px];
-        b = (pcam == ki) ? b : 0.0;
-      } else {
-        b = Hs[kic * 256 + km * 16 + 15];
-      }
-      b = (k < NK && c <= NB6 + CI) ? b : 0.0;
-      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
-    }
+// one tile ti of the backsolve (panel_backsolve).  CHAIN: the tile's own triangle by 16 dependent DPP steps (the
+// last tile: its rows from C on are masked, and no inverse of it exists); otherwise by the precomputed inverse
+// X = Ltilde_tt^-1: x_t[r] = sum_{c >= r} X[c][r] y[c], 16 independent products (two accumulators).  Then the tile's
+// final values go to every lane through pub, which subtracts them from the rows of the earlier tiles.
+template <bool CHAIN>
+__device__ __forceinline__ void bs_tile(const double* S, const double* Dfac, const double* Xinv, int C, int ti,
+                                        const int (&row)[2], const double (&rdv)[2], double* pub, double (&x)[2]) {
+  const int lane = threadIdx.x & 63, g = lane >> 4, r = lane & 15;
+  const int tg = ti & 3, ts = ti >> 2, i0 = 16 * ti;
+  double M[16], Le[2][16];
+  const double* pm = (CHAIN ? Dfac : Xinv) + ti * kTileSz + r;  // column r of the factored tile / of its inverse
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int zr = 16 * rt + kq + 4 * q;  // Z row (baseline index), column c
-      if (zr >= NB6) continue;
-      const int gr = ctab[2][zr / 6] + zr % 6;  // global row of the camera block
-      const double v = acc[q];
-      if (c < NB6) {
-        const int gc = ctab[2][c / 6] + c % 6;
-        if (gr >= gc) S[tidx(gr, gc)] += v + ((gr == gc) ? (cd2 ? cd2[gr] : lam2) : 0.0);
-      } else if (c < NB6 + CI) {
-        S[tidx(gr, p)] += v;  // baseline row, intrinsic column: lower
-      } else if (c == NB6 + CI) {
-        S[tidx(C, gr)] = bv[gr] + v;
-        gl[gr] = v;
-        d.gc[gr] = v;
-        d.rhs[gr] = v;
-      }
+  for (int u = 0; u < 16; ++u) M[u] = pm[u * kTS];
+  // rows of the earlier tiles: Ltilde[i0 + u][row] (row < i0; other lanes read a valid tile and discard it)
+#pragma unroll
+  for (int sl = 0; sl < 2; ++sl) {
+    const double* pe = S + tile_base(ti, min(row[sl] >> 4, ti)) + (row[sl] & 15);
+#pragma unroll
+    for (int u = 0; u < 16; ++u) Le[sl][u] = pe[u * kTS];
+  }
+  double xt = ts ? x[1] : x[0];
+  const int lim = C - i0;  // rows of this tile below C (CHAIN only; the other tiles are whole)
+  if constexpr (CHAIN) {
+    const double rdt = ts ? rdv[1] : rdv[0];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) M[u] = (r < u && u < lim) ? M[u] * rdt : 0.0;
+#pragma unroll
+    for (int u = 15; u >= 0; --u) xt = fma(-M[u], bcast16(xt, u), xt);
+  } else {
+    double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+    for (int c = 0; c < 16; c += 2) {
+      a0 = fma(c >= r ? M[c] : 0.0, bcast16(xt, c), a0);
+      a1 = fma(c + 1 >= r ? M[c + 1] : 0.0, bcast16(xt, c + 1), a1);
     }
+    xt = a0 + a1;
   }
-}
-
-// lane k's value to every lane of its 16-lane row (DPP row_newbcast, gfx90a+): a plain VALU move, without the
-// v_readlane -> SGPR -> VALU round trip.  k must fold to a constant (unrolled loops).
-__device__ __forceinline__ double bcast16(double v, int k) {
-  switch (k) {
-    case 0: return dpp_d<0x150>(v);
-    case 1: return dpp_d<0x151>(v);
-    case 2: return dpp_d<0x152>(v);
-    case 3: return dpp_d<0x153>(v);
-    case 4: return dpp_d<0x154>(v);
-    case 5: return dpp_d<0x155>(v);
-    case 6: return dpp_d<0x156>(v);
-    case 7: return dpp_d<0x157>(v);
-    case 8: return dpp_d<0x158>(v);
-    case 9: return dpp_d<0x159>(v);
-    case 10: return dpp_d<0x15A>(v);
-    case 11: return dpp_d<0x15B>(v);
-    case 12: return dpp_d<0x15C>(v);
-    case 13: return dpp_d<0x15D>(v);
-    case 14: return dpp_d<0x15E>(v);
-    default: return dpp_d<0x15F>(v);
+  if (g == tg) {
+    if (ts) x[1] = xt;
+    else x[0] = xt;
+    pub[r] = xt;
   }
+  KB_WAVE_SYNC();
+  double xp[16];
+#pragma unroll
+  for (int u = 0; u < 16; ++u) xp[u] = (!CHAIN || u < lim) ? pub[u] : 0.0;
+#pragma unroll
+  for (int sl = 0; sl < 2; ++sl) {
+    double acc = 0.0;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) acc = fma(Le[sl][u], xp[u], acc);
+    if (row[sl] < i0) x[sl] -= acc * rdv[sl];
+  }
+  KB_WAVE_SYNC();  // pub is rewritten by the next tile
 }
 
 // x = Ltilde^-T z, z = (row C of the factor) D^-1, by one wave.  Lane l = 16 g + r holds the rows 16 (g + 4 s) + r,
-// s = 0, 1: tile t lives in the 16-lane group t & 3, slot t >> 2.  Tiles from the last: the tile's own triangle by 16
-// DPP row broadcasts (x_u of the group's lane u, no v_readlane in the dependency chain), then its 16 final values
-// through LDS (pub) to every lane, which subtracts them from the rows of the earlier tiles.
-__device__ __forceinline__ void panel_backsolve(const double* S, const double* rD, int C, double* pub, double (&x)[2]) {
+// s = 0, 1: tile t lives in the 16-lane group t & 3, slot t >> 2.  Tiles from the last (bs_tile); the result comes
+// back in x[s] = x_{l + 64 s}.
+__device__ __forceinline__ void panel_backsolve(const KbDev& d, const double* S, const double* Dfac, const double* Xinv,
+                                                const double* rD, int C, int nb, double* pub, double (&x)[2]) {
   const int lane = threadIdx.x & 63, g = lane >> 4, r = lane & 15;
   int row[2];
   double rdv[2];
@@ -2216,110 +2452,171 @@ __device__ __forceinline__ void panel_backsolve(const double* S, const double* r
   for (int sl = 0; sl < 2; ++sl) {
     row[sl] = 16 * (g + 4 * sl) + r;
     const int rc = min(row[sl], C - 1);
-    const double z = S[tidx(C, rc)], rd = rD[rc];
+    // row C's W: in place off the diagonal tile, in Dfac inside it
+    const double* zp = (rc >> 4) == (C >> 4) ? Dfac + (C >> 4) * kTileSz + (C & 15) * kTS + (rc & 15) : S + tidx(C, rc);
+    const double z = *zp, rd = rD[rc];
     rdv[sl] = rd;
     x[sl] = row[sl] < C ? z * rd : 0.0;
   }
+  int ti = (C - 1) >> 4;
+  if (ti == nb - 1) bs_tile<true>(S, Dfac, Xinv, C, ti--, row, rdv, pub, x);  // the tile holding row C
 #pragma unroll 1
-  for (int ti = (C - 1) >> 4; ti >= 0; --ti) {
-    const int tg = ti & 3, ts = ti >> 2, i0 = 16 * ti;
-    // the tile's own triangle: Ltilde[i0 + u][i0 + r], u > r (group tg's lanes; the others compute and discard)
-    double Lw[16], Le[2][16];
-#pragma unroll
-    for (int u = 0; u < 16; ++u) Lw[u] = S[tidx(i0 + u, i0 + min(r, u))];
-    // rows of the earlier tiles: Ltilde[i0 + u][row] (row < i0)
-#pragma unroll
-    for (int sl = 0; sl < 2; ++sl)
-#pragma unroll
-      for (int u = 0; u < 16; ++u) Le[sl][u] = S[tidx(i0 + u, min(row[sl], i0 + u))];
-    const double rdt = ts ? rdv[1] : rdv[0];  // this lane's 1/D in the tile's slot
-    double xt = ts ? x[1] : x[0];
-#pragma unroll
-    for (int u = 15; u >= 0; --u) {
-      const double xu = bcast16(xt, u);
-      const bool in = (r < u) && (i0 + u < C);
-      xt -= in ? Lw[u] * rdt * xu : 0.0;
-    }
-    if (g == tg) {
-      if (ts) x[1] = xt;
-      else x[0] = xt;
-      pub[r] = xt;
-    }
-    KB_WAVE_SYNC();
-    double xp[16];
-#pragma unroll
-    for (int u = 0; u < 16; ++u) xp[u] = (i0 + u < C) ? pub[u] : 0.0;
-#pragma unroll
-    for (int sl = 0; sl < 2; ++sl) {
-      double acc = 0.0;
-#pragma unroll
-      for (int u = 0; u < 16; ++u) acc += Le[sl][u] * xp[u];
-      if (row[sl] < i0) x[sl] -= acc * rdv[sl];
-    }
-    KB_WAVE_SYNC();  // pub is rewritten by the next tile
-  }
+  for (; ti >= 0; --ti) bs_tile<false>(S, Dfac, Xinv, C, ti, row, rdv, pub, x);
 }
 
 // ---------------------------------------------------------------------------------------------
 // k_colimg (C > 64): finishes the column sums as k_colfin does (out[e] = sum_r rows[r][e] over the nrows rows: the 8
 // stage-1 rows, or 1 all-reduced row when sharded; fixed order; max for the max|dx_f| columns) and writes k_solve's
-// LDS image of the camera block from the same rows:
-//   [S lower 16 x 16 tiles, stride kTS: -sum Y^T Y (diagonal tiles: lower half), identity padding beyond C |
-//    rhs (n16 + 2 slots): -sum Y^T z, slot C: the non-PD frame-block count | per-camera 16 x 16 sums, mirrored].
-// One thread per entry (the index arithmetic runs wide here, not in the one-block solve, which stages the image
-// with one contiguous copy).
+// LDS image of the complete camera system from the same rows:
+//   [S lower 16 x 16 tiles, stride kTS (diagonal tiles whole):
+//      H_cc + lambda^2 I (or the per-call conditioner) - sum Y^T Y, row C = b = g_c - sum Y^T z, rows C+1.. the identity |
+//    n16 + 2 slots: g_c (the gradient, for the step statistics), slot C: the non-PD frame-block count].
+// H_cc and g_c are the expansion of the per-camera sums through the chains K of the build state (cam_entry_l /
+// cam_grad_l: H_{I_i,I_i} = Hs_i[II], H_{B_j,I_i} = K_{i,j}^T Hs_i[dI], H_{B_j,B_k} = sum_{i > max(j,k)} K_{i,j}^T
+// Hs_i[dd] K_{i,k}).  Every block that writes image entries first stages the finished per-camera sums Hs, the chains K
+// and T = Hs[dd] K in LDS (the same fixed-order sums for every block), so the expansion runs wide here instead of in
+// the one-block camera solve.  One thread per output entry; the block holding the first image entry also writes
+// cost_build, the threads of the gradient slots gc and rhs.
 // ---------------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_colimg(KbDev d, const double* rows, double* out, int gate, int nrows) {
-  if (gate && d.ctrl->done) return;
-  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  const KbCtrl* c = d.ctrl;
+  const int done = c->done, cur = c->cur, have = c->have_dx;
+  const double lamc = c->lambda;
+  if (gate && done) return;
+  const int tid = threadIdx.x, q = blockIdx.x * blockDim.x + tid, nth = blockDim.x;
   const int N = d.N, C = d.C, Wt = d.W - d.C;
-  int src = -1;  // -1: zero, -2: one (identity padding)
-  double sg = 1.0;
-  double* dst;
+  const int nb = (C + 16) >> 4, ntz = kTileSz * nb * (nb + 1) / 2;  // + the b row (row C)
+  const int q0 = blockIdx.x * blockDim.x;
+  const bool img_block = q0 + nth > d.Wtot && q0 < d.Wtot + ntz + 16 * nb + 2;  // block-uniform
+  // ---- this thread's output: which column sum it needs (src) and what it is
+  // kind: 0 none / zero, 1 finished column sum (out), 2 camera entry (i, j), 3 b entry j, 4 identity, 5 g_c k,
+  //       6 non-PD count
+  int kind = 0, src = -1, ei = 0, ej = 0;
+  const int e = q - d.Wtot;
   if (q < d.Wtot) {
+    kind = 1;
     src = q;
-    dst = out + q;
-  } else {
-    const int e = q - d.Wtot;
-    if (e >= d.img_n) return;
-    dst = d.simg + e;
-    const int nb = (C + 16) >> 4, n16 = 16 * nb, ntz = kTileSz * nb * (nb + 1) / 2;  // + the b row (row C)
-    if (e < ntz) {
-      const int t = e / kTileSz, w = e - t * kTileSz, r = w / kTS, cc = w - r * kTS;
-      const int it = tri_row(t), jt = t - it * (it + 1) / 2;
-      const int i = 16 * it + r, j = 16 * jt + cc;
-      if (cc < 16 && (it > jt || cc <= r)) {
-        if (i < C) {
-          src = N * 136 + upper_index(j, i, C);
-          sg = -1.0;
-        } else if (i == j) {
-          src = -2;
-        }
+  } else if (e < ntz) {
+    const int t = e / kTileSz, w = e - t * kTileSz, r = w / kTS, cc = w - r * kTS;
+    const int it = tri_row(t), jt = t - it * (it + 1) / 2;
+    const int i0 = 16 * it + r, j0 = 16 * jt + cc;
+    // diagonal tiles are stored whole (both triangles), so that a lane loads its row with constant offsets
+    ei = max(i0, j0);
+    ej = min(i0, j0);
+    if (cc < 16) {
+      if (ei < C) {
+        kind = 2;
+        src = N * 136 + upper_index(ej, ei, C);
+      } else if (ei == C && ej < C) {
+        kind = 3;
+        src = N * 136 + Wt + ej;
+      } else if (ei == ej) {
+        kind = 4;
       }
-    } else if (e < ntz + n16 + 2) {
-      const int k = e - ntz;
-      if (k < C) {
-        src = N * 136 + Wt + k;
-        sg = -1.0;
-      } else if (k == C) {
-        src = N * 136 + Wt + C;
-      }
-    } else {
-      const int hq = e - ntz - n16 - 2, cam = hq >> 8, a = (hq >> 4) & 15, b = hq & 15;
-      src = cam * 136 + d16_index(min(a, b), max(a, b));
+    }
+  } else if (e < d.img_n) {
+    const int k = e - ntz;
+    ej = k;
+    if (k < C) kind = 5;
+    else if (k == C) {
+      kind = 6;
+      src = N * 136 + Wt + C;
     }
   }
-  double acc = src == -2 ? 1.0 : 0.0;
-  if (src >= 0) {
-    double v[kColsumRows];
+  // ---- round 1: the thread's column-sum rows and (image blocks) every staging load, all in flight together
+  double v8[kColsumRows];
+  {
+    const int sc = src < 0 ? 0 : src;
 #pragma unroll
-    for (int r = 0; r < kColsumRows; ++r) v[r] = rows[(size_t)(r < nrows ? r : 0) * d.Wtot + src];
+    for (int r = 0; r < kColsumRows; ++r) v8[r] = rows[(size_t)(r < nrows ? r : 0) * d.Wtot + sc];
+  }
+  double* Hs = sm;              // [N][256] symmetric per-camera sums
+  double* K = Hs + N * 256;     // [N][N][36] chains of the build state
+  double* T = K + N * N * 36;   // [N][N][36] T_{i,k} = Hs_i[dd] K_{i,k}
+  int* ci = (int*)(T + N * N * 36);  // [C] column info
+  if (img_block) {
+    const bool gfu = gate && d.gn_fused;
+    const int bslot = (gfu && have) ? 1 - cur : cur;  // as k_solve: the state the system was built at
+    const double* Kc = cam_K(d, bslot);
+    // C <= 111 bounds the rig to N <= 10 cameras: at most 6 sums of 8 rows and 15 chain entries per thread
+    constexpr int kHsU = 6, kKU = 18;
+    const int nHs = N * 136, nK = N * N * 36;
+    double kv[kKU], hv[kHsU][kColsumRows];
+#pragma unroll
+    for (int u = 0; u < kKU; ++u) kv[u] = Kc[min(tid + u * nth, nK - 1)];
+#pragma unroll
+    for (int u = 0; u < kHsU; ++u)
+#pragma unroll
+      for (int r = 0; r < kColsumRows; ++r)
+        hv[u][r] = rows[(size_t)(r < nrows ? r : 0) * d.Wtot + min(tid + u * nth, nHs - 1)];
+    const int civ = d.colinfo[min(tid, C - 1)];
+#pragma unroll
+    for (int u = 0; u < kKU; ++u)
+      if (tid + u * nth < nK) K[tid + u * nth] = kv[u];
+#pragma unroll
+    for (int u = 0; u < kHsU; ++u) {
+      const int eh = tid + u * nth;
+      if (eh < nHs) {
+        double v = 0.0;
+#pragma unroll
+        for (int r = 0; r < kColsumRows; ++r)
+          if (r < nrows) v += hv[u][r];
+        const int cam = eh / 136;
+        int a, b;
+        d16_rowcol_fast(eh - 136 * cam, a, b);
+        Hs[cam * 256 + a * 16 + b] = v;
+        Hs[cam * 256 + b * 16 + a] = v;
+      }
+    }
+    if (tid < C) ci[tid] = civ;
+    __syncthreads();
+    for (int et = tid; et < nK; et += nth) {
+      const int x = et % 36, ik = et / 36, i = ik / N, k = ik - i * N;
+      double sacc = 0.0;
+      if (k < i) {
+        const int a = x / 6, b = x % 6;
+#pragma unroll
+        for (int m = 0; m < 6; ++m) sacc += Hs[i * 256 + a * 16 + m] * K[(i * N + k) * 36 + m * 6 + b];
+      }
+      T[et] = sacc;
+    }
+    __syncthreads();
+    if (tid == 0 && blockIdx.x == d.Wtot / nth) {
+      double sc = 0.0;
+      for (int i = 0; i < N; ++i) sc += Hs[i * 256 + 255];
+      d.cost_build[0] = sc;
+    }
+  }
+  if (kind == 0 && e >= d.img_n) return;
+  // the finished column sum (fixed order; max for the max|dx_f| columns)
+  double cs = 0.0;
+  if (src >= 0) {
     const bool mx = src >= d.Wp;
 #pragma unroll
     for (int r = 0; r < kColsumRows; ++r)
-      if (r < nrows) acc = mx ? fmax(acc, v[r]) : acc + v[r];
+      if (r < nrows) cs = mx ? fmax(cs, v8[r]) : cs + v8[r];
   }
-  *dst = sg * acc;
+  if (kind == 1) {
+    out[q] = cs;
+    return;
+  }
+  double v = 0.0;
+  if (kind == 2) {
+    v = cam_entry_l(N, ci, Hs, T, K, ei, ej) - cs;
+    if (ei == ej) v += gate ? lamc * lamc : (d.cond2 ? d.cond2[ei] : d.host_lambda * d.host_lambda);
+  } else if (kind == 3) {
+    v = cam_grad_l(N, ci, Hs, K, ej) - cs;  // b
+  } else if (kind == 4) {
+    v = 1.0;  // identity padding (and the b row's diagonal)
+  } else if (kind == 5) {
+    v = cam_grad_l(N, ci, Hs, K, ej);  // g_c
+    d.gc[ej] = v;
+    d.rhs[ej] = v;
+  } else if (kind == 6) {
+    v = cs;  // non-PD frame blocks
+  }
+  d.simg[e] = v;
 }
 
 // batched global -> LDS staging of the k_solve inputs: every thread keeps U independent loads in flight
@@ -2529,16 +2826,19 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update, int nth) {
   const int N = d.N, C = d.C, W = d.W, tid = threadIdx.x;
   const int Cp = C * (C + 1) / 2;
   const int nb = (C + 16) >> 4, n16 = 16 * nb;  // CM == 0: 16 x 16 tiles, rows 0 .. C (b appended as row C)
-  // CM > 0: S column-major packed lower [Cp] | bv [C + 1] (slot C: non-PD frame-block count) | gl [C] | Hs [N][256]
-  // CM == 0: the k_colimg image [S lower tiles | bv (n16 + 2) | Hs [N][256]] | gl (C, even-padded)
+  // CM > 0: S column-major packed lower [Cp] | bv [C + 1] (slot C: non-PD frame-block count) | gl [C] | Hs [N][256] |
+  //   T, K [N][N][36] | ci [C]
+  // CM == 0: the k_colimg image [S lower tiles, complete (b as row C) | gl = g_c (n16 + 2 slots, slot C: non-PD
+  //   frame-block count)] | Dfac | Xinv | 1/D
   double* S = sm;
   double* bv = S + (CM > 0 ? Cp : kTileSz * nb * (nb + 1) / 2);
-  double* Hs = CM > 0 ? bv + 2 * C + 1 : bv + n16 + 2;
-  double* gl = CM > 0 ? bv + C + 1 : Hs + N * 256;
-  double* T = CM > 0 ? Hs + N * 256 : gl + ((C + 1) & ~1);  // [N][N][36]
-  double* K = T + N * N * 36;        // [N][N][36]
-  double* Dsc = K + N * N * 36;      // CM == 0: [2][kTileSz] the factor waves' diagonal-tile scratch
-  double* rDv = Dsc + (CM > 0 ? 0 : 2 * kTileSz);  // CM == 0: [n16] 1/D
+  double* Hs = CM > 0 ? bv + 2 * C + 1 : bv;
+  double* gl = CM > 0 ? bv + C + 1 : bv;
+  double* T = CM > 0 ? Hs + N * 256 : bv;
+  double* K = T + N * N * 36;        // CM > 0: [N][N][36]
+  double* Dfac = CM > 0 ? K + N * N * 36 : bv + ((n16 + 2 + 1) & ~1);  // CM == 0: [nb][kTileSz] factored diagonal tiles
+  double* Xinv = Dfac + (CM > 0 ? 0 : nb * kTileSz);  // CM == 0: [nb][kTileSz] their unit-lower inverses
+  double* rDv = Xinv + (CM > 0 ? 0 : nb * kTileSz);   // CM == 0: [n16] 1/D
   int* ci = (int*)(rDv + (CM > 0 ? 0 : n16));      // [C]
   __shared__ int okl;
   __shared__ double nbase[KB_MAX_CAMS * 7];  // candidate baselines
@@ -2569,30 +2869,25 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update, int nth) {
   KB_STAMP(d, 0);
   // phase A: stage K, column info, per-camera sums and the Schur sums in LDS (one row: psum)
   if constexpr (CM == 0) {
-    // the k_colimg image and the chains K of the build state: one contiguous 16-byte copy, 12 loads in flight per
-    // thread (one round trip for an 8-camera rig)
-    const int n2i = d.img_n >> 1, n2 = n2i + N * N * 18;
+    // the k_colimg image (the complete system): one contiguous 16-byte copy, 12 loads in flight per thread (one round
+    // trip for an 8-camera rig); the build's cost (k_colimg) in the same round
+    const int n2 = d.img_n >> 1;
     const double2* gi = reinterpret_cast<const double2*>(d.simg);
-    const double2* gk = reinterpret_cast<const double2*>(cam_K(d, bslot)) - n2i;
     double2* li = reinterpret_cast<double2*>(S);
-    double2* lk = reinterpret_cast<double2*>(K) - n2i;
-    const int civ = d.colinfo[tid < C ? tid : 0];  // column info in the same round trip (C <= 111 < threads)
+    const double cb0 = d.cost_build[0];
     constexpr int U = 12;
 #pragma unroll 1
     for (int q0 = tid; q0 < n2; q0 += U * nth) {
       double2 v[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int q = min(q0 + u * nth, n2 - 1);
-        v[u] = *(q < n2i ? gi + q : gk + q);
-      }
+      for (int u = 0; u < U; ++u) v[u] = gi[min(q0 + u * nth, n2 - 1)];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int q = q0 + u * nth;
-        if (q < n2) *(q < n2i ? li + q : lk + q) = v[u];
+        if (q < n2) li[q] = v[u];
       }
     }
-    if (tid < C) ci[tid] = civ;
+    if (tid == 0) cl_red[0] = cb0;
   } else {
     solve_stage<4, CM, false>(d, bslot, K, Hs, S, bv, ci, tid, nth);
   }
@@ -2605,22 +2900,24 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update, int nth) {
   if (gate && !d.gn_fused && tid == 0) c->pending = 1;
   KB_TS(d, 1);
   KB_STAMP(d, 1);
-  // phase B: camera block expansion
-  for (int q = tid; q < N * N * 36; q += nth) {
-    const int e = q % 36, ik = q / 36, i = ik / N, k = ik % N;
-    double s = 0.0;
-    if (k < i) {
-      const int a = e / 6, b = e % 6;
+  // phase B: camera block expansion (CM == 0: done by k_colimg)
+  if constexpr (CM > 0) {
+    for (int q = tid; q < N * N * 36; q += nth) {
+      const int e = q % 36, ik = q / 36, i = ik / N, k = ik % N;
+      double s = 0.0;
+      if (k < i) {
+        const int a = e / 6, b = e % 6;
 #pragma unroll
-      for (int m = 0; m < 6; ++m) s += Hs[i * 256 + a * 16 + m] * K[(i * N + k) * 36 + m * 6 + b];
+        for (int m = 0; m < 6; ++m) s += Hs[i * 256 + a * 16 + m] * K[(i * N + k) * 36 + m * 6 + b];
+      }
+      T[q] = s;
     }
-    T[q] = s;
-  }
-  if (tid == 0) {
-    double s = 0.0;
-    for (int i = 0; i < N; ++i) s += Hs[i * 256 + 255];
-    d.cost_build[0] = s;
-    cl_red[0] = s;
+    if (tid == 0) {
+      double s = 0.0;
+      for (int i = 0; i < N; ++i) s += Hs[i * 256 + 255];
+      d.cost_build[0] = s;
+      cl_red[0] = s;
+    }
   }
   // GN fused: the previous pass's end.  Its cost is this build's (the system was built at its candidate):
   // accept (GN always does) and the next prelude (Optimizer2.cpp:221-259, TrustRegionPolicy.cpp:39-52)
@@ -2653,9 +2950,6 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update, int nth) {
       d.gc[p] = g;
       d.rhs[p] = g;
     }
-  } else {
-    // H_cc on MFMA into the staged tiles; b + g as row C (the factorisation's right-hand side)
-    cam_expand_tiles(d, S, bv, gl, Hs, T, K, ci, ctab, lam2, gate ? nullptr : d.cond2);
   }
   __syncthreads();
   KB_TS(d, 3);
@@ -2678,10 +2972,10 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update, int nth) {
   } else {
     // phase C: blocked LDL^T with the forward solve (row C); the previous pass's end beside the first panel
     if (gfu && fwave) finish_prev();
-    ldl_panels(d, S, rDv, Dsc, C, nb, &okl);
+    ldl_panels(d, S, rDv, Dfac, Xinv, C, nb, &okl);
     KB_TS(d, 4);
     KB_STAMP(d, 3);
-    if (tid < 64) panel_backsolve(S, rDv, C, pubcol, x);  // phase D: Ltilde^T x = z, one wave
+    if (tid < 64) panel_backsolve(d, S, Dfac, Xinv, rDv, C, nb, pubcol, x);  // phase D: Ltilde^T x = z, one wave
     KB_STAMP(d, 4);
   }
   __syncthreads();  // okl final
@@ -2984,6 +3278,46 @@ __global__ void __launch_bounds__(512) k_backsub(KbDev d, int gate, int do_updat
 // ---------------------------------------------------------------------------------------------
 // k_cost: one wave per view on state buffer (cur ^ which); per-block partial sums (kb_eval_cost, loop start)
 // ---------------------------------------------------------------------------------------------
+// ---------------------------------------------------------------------------------------------
+// rhs^T (J^T J) rhs of the last build (LinearSystemSolver::rhsJtJrhs, LinearSystemSolver.hpp:66-69; the reference
+// forms ||J rhs||^2, SparseCholeskyLinearSystemSolver.cpp:106-111), from the arrow blocks: one wave per frame forms
+// t_f = r_f^T H_ff r_f + 2 r_f^T H_fc r_c into part[f]; k_rjr_final sums the frames in a fixed order and adds
+// r_c^T H_cc r_c.  r = [g_c | g_f] (the rhs kb_build left).
+// ---------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_rjr_frames(KbDev d, double* part) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int f = blockIdx.x * 4 + wave;
+  if (f >= d.F) return;
+  const int C = d.C;
+  const double* gf = d.gf + (size_t)f * 6;
+  double rf[6];
+#pragma unroll
+  for (int a = 0; a < 6; ++a) rf[a] = gf[a];
+  double s = 0.0;
+  for (int c = lane; c < C; c += 64) {
+    const double rc = d.gc[c];
+    double w = 0.0;
+#pragma unroll
+    for (int a = 0; a < 6; ++a) w = fma(rf[a], d.Hfc[((size_t)f * 6 + a) * C + c], w);
+    s = fma(2.0 * w, rc, s);
+  }
+  if (lane < 36) s = fma(rf[lane / 6] * d.Hff[(size_t)f * 36 + lane], rf[lane % 6], s);
+  s = wave_sum_d(s);
+  if (lane == 0) part[f] = s;
+}
+
+__global__ void __launch_bounds__(256) k_rjr_final(KbDev d, const double* part, double* out) {
+  __shared__ double sh[4];
+  const int tid = threadIdx.x, C = d.C;
+  double s = 0.0;
+  for (int f = tid; f < d.F; f += blockDim.x) s += part[f];
+  for (int q = tid; q < C * C; q += blockDim.x) s = fma(d.gc[q / C] * d.Hcc[q], d.gc[q % C], s);
+  s = wave_sum_d(s);
+  if ((tid & 63) == 0) sh[tid >> 6] = s;
+  __syncthreads();
+  if (tid == 0) out[0] = (sh[0] + sh[1]) + (sh[2] + sh[3]);
+}
+
 __global__ void __launch_bounds__(256) k_cost(KbDev d, int which) {
   KbCtrl* c = d.ctrl;
   __shared__ double part[4];

@@ -24,6 +24,19 @@
 #include "../../include/kalibr_hip.h"
 #include "kb_math.h"
 
+// diagnostic build only (KB_STAMPS, tools/gpu_sp_stops.sh): the timed kernels return after phase i when
+// KSP_DBG_STOP = i; the product library never reads the variable and has no early returns
+#ifdef KB_STAMPS
+#define KSP_STOP(i)                 \
+  do {                              \
+    if (d.dbg_stop == (i)) return;  \
+  } while (0)
+#else
+#define KSP_STOP(i) \
+  do {              \
+  } while (0)
+#endif
+
 namespace kb_internal {
 int fail(const std::string& m);
 }
@@ -669,7 +682,7 @@ __global__ void __launch_bounds__(256) k_sp_assemble(SpDev d) {
       out[q] += s;
     }
   }
-  if (d.dbg_stop == 1) return;
+  KSP_STOP(1);
   // ---- IMU samples
   const int ma = d.node_im[2 * i], mz = d.node_im[2 * i + 1];
   const int wave = tid >> 6, lane = tid & 63;
@@ -683,7 +696,7 @@ __global__ void __launch_bounds__(256) k_sp_assemble(SpDev d) {
       tb[tid] = d.ib[c0 + tid];
     }
     __syncthreads();
-    if (d.dbg_stop == 2) return;
+    KSP_STOP(2);
     // Jn^T [Jw | J_theta | -e] over the chunk's 6 nt residual rows: Jn = the samples' Jacobian columns of this
     // node's 18 rows, Jw those of nodes i and i + 1 (D_i | U_i), J_theta the 9 IMU columns, e the whitened
     // residual.  A 2 x 3 grid of 16 x 16 tiles (rows 0..17, columns 0..35 D | U, 36..44 IMU, 45 g), tiles wave and
@@ -1102,7 +1115,7 @@ __global__ void __launch_bounds__(256) k_sp_level(SpDev d, int s) {
         });
   }
   __syncthreads();
-  if (d.dbg_stop == 1) return;
+  KSP_STOP(1);
   for (int q = tid; q < 3 * NB * NB; q += blockDim.x) {
     const int part = q / (NB * NB), e = q % (NB * NB), a = e / NB, b = e % NB;
     double acc = 0.0;
@@ -1128,7 +1141,7 @@ __global__ void __launch_bounds__(256) k_sp_level(SpDev d, int s) {
     W[a * wc + 2 * NB + c] -= acc;
   }
   __syncthreads();
-  if (d.dbg_stop == 2) return;
+  KSP_STOP(2);
   if (!elim && !top) {  // stays active: D', U (to i + 2s), R' for the next level
     for (int q = tid; q < NB * NB; q += blockDim.x) {
       d.D[(size_t)i * NB * NB + q] = L[q];
@@ -1147,14 +1160,14 @@ __global__ void __launch_bounds__(256) k_sp_level(SpDev d, int s) {
     if (!ok && tid == 0) d.sc[SC_OK] = 0.0;
   }
   __syncthreads();
-  if (d.dbg_stop == 3) return;
+  KSP_STOP(3);
   if (top) {  // X_0 = L^-T L^-1 R' (forward in place in W, then backward into X_0)
     node_forward(L, id, W + 2 * NB, wc, m, W + 2 * NB, wc, tid);
     node_backsolve(L, id, W + 2 * NB, wc, m, d.X, tid);
     return;
   }
   node_forward(L, id, W, wc, wc, d.Z + (size_t)i * NB * wc, wc, tid);
-  if (d.dbg_stop == 4) return;
+  KSP_STOP(4);
   for (int q = tid; q < NB * NB; q += blockDim.x) d.Lf[(size_t)i * NB * NB + q] = L[q];
   if (tid < NB) d.Lid[(size_t)i * NB + tid] = id[tid];
 }
@@ -1214,7 +1227,7 @@ __global__ void __launch_bounds__(256) k_sp_back(SpDev d, int s) {
         });
   }
   __syncthreads();
-  if (d.dbg_stop == 1) return;
+  KSP_STOP(1);
   // T = Z_R - Z_Uin x_l - Z_U x_r on MFMA tiles: T[row][c] = Z_R[row][c] - sum_k (Z[row][k] xl[k][c] + Z[row][NB + k]
   // xr[k][c]); A = Z^T is read from the Z rows (stride 1 in k), B from xl / xr
   {
@@ -1243,7 +1256,7 @@ __global__ void __launch_bounds__(256) k_sp_back(SpDev d, int s) {
     }
   }
   __syncthreads();
-  if (d.dbg_stop == 2) return;
+  KSP_STOP(2);
   node_backsolve(L, id, T, m, m, d.X + (size_t)j * NB * m, tid);
 }
 
@@ -2088,7 +2101,9 @@ int kb_sp_upload(kb_sp_handle* h, int32_t n_frames, const double* frame_time, in
   rc |= h->alloc(&d.FH, (size_t)F * d.FHS);
   rc |= h->alloc(&d.part, (size_t)d.nblk_f * d.Wc);
   d.nblk_q = (h->n + 63) / 64;
-  if (const char* e = std::getenv("KSP_DBG_STOP")) d.dbg_stop = std::atoi(e);
+#ifdef KB_STAMPS
+  if (const char* e = std::getenv("KSP_DBG_STOP")) d.dbg_stop = std::atoi(e);  // diagnostic build only
+#endif
   rc |= h->alloc(&d.cpart, (size_t)(d.nblk_f + d.nblk_ci + d.nblk_q));
   rc |= h->alloc(&d.mcost, (size_t)h->n);
   rc |= h->alloc(&d.ipart, (size_t)d.nblk_ic * WI);

@@ -388,25 +388,10 @@ const std::vector<double>& GpuLinearSystemSolver::rhs() const {
 }
 
 double GpuLinearSystemSolver::rhsJtJrhs() {
-  // rhs^T (J^T J) rhs from the arrow blocks of the last build
+  // rhs^T (J^T J) rhs of the last build, on the device from the arrow blocks (kb_rhs_jtj_rhs)
   if (!_built) throw Exception("rhsJtJrhs: buildSystem first");
-  const size_t C = _C, F = (_JCols - _C) / 6;
-  std::vector<double> Hff(36 * F), Hfc(6 * C * F), gf(6 * F), Hcc(C * C), gc(C);
-  double cost = 0.0;
-  check(kb_get_normal_blocks(static_cast<kb_handle*>(_h), Hff.data(), Hfc.data(), gf.data(), Hcc.data(), gc.data(),
-                             &cost),
-        "kb_get_normal_blocks");
-  const std::vector<double>& r = rhs();
   double s = 0.0;
-  for (size_t a = 0; a < C; ++a)
-    for (size_t b = 0; b < C; ++b) s += r[a] * Hcc[a * C + b] * r[b];
-  for (size_t f = 0; f < F; ++f) {
-    const double* rf = &r[C + 6 * f];
-    for (int a = 0; a < 6; ++a) {
-      for (int b = 0; b < 6; ++b) s += rf[a] * Hff[36 * f + 6 * a + b] * rf[b];
-      for (size_t b = 0; b < C; ++b) s += 2.0 * rf[a] * Hfc[(6 * f + a) * C + b] * r[b];
-    }
-  }
+  check(kb_rhs_jtj_rhs(static_cast<kb_handle*>(_h), &s), "kb_rhs_jtj_rhs");
   return s;
 }
 

@@ -193,3 +193,18 @@ def test_comm_path_single_rank_is_bitwise_identical(capi, name):
     a.build()
     for k in ("Hcc", "gc", "Hff", "Hfc"):
         assert np.array_equal(a.normal_blocks()[k], b.normal_blocks()[k])
+
+
+@pytest.mark.parametrize("name", ["c2_ragged", "c4_small"])
+def test_rhs_jtj_rhs_on_device(capi, oracle_mod, name):
+    """kb_rhs_jtj_rhs (LinearSystemSolver::rhsJtJrhs) = rhs^T (J^T J) rhs of the oracle's dense normal equations"""
+    p = PROBLEMS[name]()
+    o = oracle_mod.Oracle(p)
+    g = capi.Solver(p)
+    g.set_state(p.state_init)
+    g.build()
+    A = o.arrow(p.state_init)
+    H = _dense_H(A, 0.0)
+    r = A["rhs"]
+    want = float(r @ H @ r)
+    assert abs(g.rhs_jtj_rhs() - want) <= 1e-10 * abs(want)

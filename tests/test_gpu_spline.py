@@ -165,3 +165,55 @@ def test_motion_error_removed_restores_the_plain_system(motion_case):
     o0 = O.SplineOracle(p)
     assert abs(g.eval_cost() - o0.cost(p.state_init)) <= 1e-12 * o0.cost(p.state_init)
     g.set_motion_error(W_MOTION, 2)
+
+
+# ---- full-size configs[4] (1200 frames, 279 k corners, 12 k IMU samples) against the oracle ----
+@pytest.fixture(scope="module")
+def full_case():
+    p = synth.make_spline_config()
+    return p, O.SplineOracle(p), capi.SplineSolver(p)
+
+
+def _full_threads():
+    import os
+    return max(1, min(16, len(os.sched_getaffinity(0))))
+
+
+def _compare_runs(res, st, res_o, st_o):
+    """identical iteration counts and accept/revert sequence, per-pass J within 1e-9, state within 1e-6"""
+    assert res["iterations"] == res_o["iterations"] and res["failed_iterations"] == res_o["failed_iterations"]
+    tr, tro = res["trace"], res_o["trace"]
+    assert tr.shape == tro.shape, (tr.shape, tro.shape)
+    assert np.array_equal(tr[:, 3], tro[:, 3])  # accepted flags
+    ok = np.isfinite(tro[:, 0])
+    assert np.all(np.abs(tr[ok, 0] - tro[ok, 0]) <= 1e-9 * np.abs(tro[ok, 0]))
+    assert np.allclose(tr[:, 1], tro[:, 1], rtol=1e-12, atol=0.0)  # lambda schedule
+    assert abs(res["J_final"] - res_o["J_final"]) <= 1e-9 * res_o["J_final"]
+    assert np.abs(st - st_o).max() < 1e-6
+
+
+@pytest.mark.parametrize("policy", ["gn", "lm"])
+def test_full_size_optimize_parity(full_case, policy):
+    """configs[4] at full size: GN (maxIt 20) and Kalibr2-default LM (lambda0 10) against SplineOracle"""
+    p, o, g = full_case
+    g.set_motion_error(None)
+    g.set_state(p.state_init)
+    kw = dict(policy=policy, lambda0=10.0, max_iterations=20, eps_x=1e-3, eps_j=1e-3)
+    res = g.optimize(**kw)
+    st_o, res_o = o.optimize(p.state_init, nthreads=_full_threads(), **kw)
+    _compare_runs(res, g.get_state(), res_o, st_o)
+
+
+def test_full_size_motion_error_parity(full_case):
+    """the BSplineMotionError variant at full size (GN, maxIt 20)"""
+    p, _, g = full_case
+    om = O.SplineOracle(p, motion_W=W_MOTION, motion_order=2)
+    g.set_motion_error(W_MOTION, 2)
+    try:
+        g.set_state(p.state_init)
+        kw = dict(policy="gn", lambda0=10.0, max_iterations=20, eps_x=1e-3, eps_j=1e-3)
+        res = g.optimize(**kw)
+        st_o, res_o = om.optimize(p.state_init, nthreads=_full_threads(), **kw)
+        _compare_runs(res, g.get_state(), res_o, st_o)
+    finally:
+        g.set_motion_error(None)

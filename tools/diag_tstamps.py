@@ -19,6 +19,11 @@ buf = (C.c_longlong * 64)()
 assert L.kb_diag_read_ts(g.h, buf, 64) == 0  # allocates the stamp buffer
 names = {0: "entry", 1: "staged", 2: "T (+pass end)", 3: "H_cc blocks + grad", 4: "LDL^T", 5: "solves",
          6: "stats + DV update", 7: "chains"}
+names[47] = "  expansion: intrinsic blocks done (wave 0)"
+names[48] = "  expansion: MFMA tiles done (wave 0)"
+names[40] = "    p2: lookahead done"
+names[41] = "    p2: rows loaded"
+names[42] = "    p2: 16 steps done"
 for i in range(10, 20):
     names[i] = f"  panel {i - 10}"
 for q in range(7):
@@ -32,3 +37,5 @@ for rep in range(3):
     order = sorted((buf[i] - t0, i) for i in names if buf[i] >= t0 and buf[i] - t0 < 10_000_000)
     print(f"k_solve timeline (rep {rep}, us from entry):\n" +
           "\n".join(f"{names[i]:24s} {dt / 100:8.2f}" for dt, i in order))
+    if buf[7] > buf[0]:  # shader clock over the kernel: s_memtime ticks / s_memrealtime (100 MHz) ticks
+        print(f"shader clock during k_solve: {100.0 * (buf[61] - buf[60]) / (buf[7] - buf[0]):.0f} MHz")
