@@ -657,8 +657,8 @@ static int launch_colsum(kb_handle* h, int gate, bool finish = true) {
       nrows = 1;
     }
     double* out = sharded(h) ? h->psum_red : d.psum_local;
-    hipLaunchKernelGGL(k_colimg, dim3((d.Wtot + d.img_n + 255) / 256), dim3(256), h->lds_colimg, h->stream, d, rows,
-                       out, gate, nrows);
+    hipLaunchKernelGGL(k_colimg, dim3((d.Wtot + d.img_n + kColimgThreads - 1) / kColimgThreads), dim3(kColimgThreads),
+                       h->lds_colimg, h->stream, d, rows, out, gate, nrows);
     KB_HIP(hipGetLastError());
     return 0;
   }

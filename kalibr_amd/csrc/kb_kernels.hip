@@ -1186,10 +1186,10 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
   }
   if (tid < 2 * N) ctab[tid / N][tid % N] = (tid < N) ? cam_arg(d.col_intr, tid) : cam_arg(d.col_base, tid - N);
   double* fpl = tg + (tg_lds ? nt3 : 0);
-  int cidn;  // view waves: lane = corner (lane & 31) of a 32-corner tile, Jacobian row lane >> 5 (0: u, 1: v)
+  int cidn;  // view waves: lane = corner of a 64-corner pass
   double2 yn;
   {
-    const int k = min(fv.x + (lane & 31), max(fv.y - 1, 0));
+    const int k = min(fv.x + lane, max(fv.y - 1, 0));
     cidn = d.cid[k];
     yn = d.y[k];
   }
@@ -1305,9 +1305,7 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
         const int f = f0 + it;
         int lane = threadIdx.x & 63;  // opaque per frame (see the frame waves)
         asm volatile("" : "+v"(lane));
-        // lane = corner (lane & 31) of the pass, Jacobian row r = lane >> 5; u rows 0..31, v rows 32..63 of the tile
-      // (row = lane: the 32 lanes of a write hit 16 distinct LDS bank pairs at the 17-double row stride)
-      const int r = lane >> 5, row = lane, mrow = lane >> 4, mcol = lane & 15;
+        const int mrow = lane >> 4, mcol = lane & 15;
         if (wave == 0 && it < 8) KB_TSB(d, 2 + 2 * it);
         double* vb = VB;
         const int2 fvn = d.fview[(size_t)min(f + 1, f1 - 1) * N + cam];  // the next frame's view (first loads below)
@@ -1319,61 +1317,71 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
         rt_mul(Lc, Lc + 9, Ri, ti, R, t);  // T_cam_w = L_cam T_f^-1
         v4d acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
         const int o0 = fv.x, o1 = fv.y;
-        for (int base = o0; base < o1; base += 32) {  // 32 corners = 64 rows per tile
-          const int k = base + (lane & 31);
+        for (int base = o0; base < o1; base += 64) {  // 64 corners per pass: the u rows, then the v rows in the tile
+          const int k = base + lane;
           const int cid = cidn;
           const double2 yv = yn;
-          if (base + 32 < o1) {  // software-pipelined: next tile's corner ids and keypoints
-            const int kn = min(k + 32, o1 - 1);
+          if (base + 64 < o1) {  // software-pipelined: next pass's corner ids and keypoints
+            const int kn = min(k + 64, o1 - 1);
             cidn = d.cid[kn];
             yn = d.y[kn];
           }
-          double xr[16];
+          double xu[16], xv[16];
 #pragma unroll
-          for (int q = 0; q < 16; ++q) xr[q] = 0.0;
-          if (k < o1) {
+          for (int q = 0; q < 16; ++q) {
+            xu[q] = 0.0;
+            xv[q] = 0.0;
+          }
+          if (k < o1) {  // one projection per corner: both Jacobian rows from the lane
             const double X0 = tgt[3 * cid], X1 = tgt[3 * cid + 1], X2 = tgt[3 * cid + 2];
             const double p0 = R[0] * X0 + R[1] * X1 + R[2] * X2 + t[0];
             const double p1 = R[3] * X0 + R[4] * X1 + R[5] * X2 + t[1];
             const double p2 = R[6] * X0 + R[7] * X1 + R[8] * X2 + t[2];
             double u, w, Jp[6], Ji[2 * KB_MAX_INTR];
             project_jac<MM>(model, intr, p0, p1, p2, u, w, Jp, Ji);
-            const double e = r ? yv.y - w : yv.x - u;
-            const double j0 = r ? Jp[3] : Jp[0], j1 = r ? Jp[4] : Jp[1], j2 = r ? Jp[5] : Jp[2];
-            // J_delta = -Jp [I | [p]x]   (HomogeneousExpressionNode.cpp:71-81, boxMinus)
-            xr[0] = -j0;
-            xr[1] = -j1;
-            xr[2] = -j2;
-            xr[3] = -(j1 * p2 - j2 * p1);
-            xr[4] = -(-j0 * p2 + j2 * p0);
-            xr[5] = -(j0 * p1 - j1 * p0);
-            // intrinsics: -Jp, -Jd (CameraDesignVariable.hpp(impl):38-54)
 #pragma unroll
-            for (int q = 0; q < 9; ++q) xr[6 + q] = (q < nin) ? -(r ? Ji[KB_MAX_INTR + q] : Ji[q]) : 0.0;
-            xr[15] = -e;  // column 15 carries -e: H[:,15] = rhs part, H[15][15] = chi^2
-          }
-          // the 64 rows of the pass in one tile write; rows n .. 31 and 32 + n .. 63 of a partial pass are zero: only
-          // the k-steps holding valid rows are issued (k-step ks = rows 4ks .. 4ks + 3, even ks into acc0, odd into acc1)
+            for (int r = 0; r < 2; ++r) {
+              double* xr = r ? xv : xu;
+              const double j0 = Jp[3 * r], j1 = Jp[3 * r + 1], j2 = Jp[3 * r + 2];
+              // J_delta = -Jp [I | [p]x]   (HomogeneousExpressionNode.cpp:71-81, boxMinus)
+              xr[0] = -j0;
+              xr[1] = -j1;
+              xr[2] = -j2;
+              xr[3] = -(j1 * p2 - j2 * p1);
+              xr[4] = -(-j0 * p2 + j2 * p0);
+              xr[5] = -(j0 * p1 - j1 * p0);
+              // intrinsics: -Jp, -Jd (CameraDesignVariable.hpp(impl):38-54)
 #pragma unroll
-          for (int q = 0; q < 16; ++q) Xw[row * XS + q] = xr[q];
-          KB_WAVE_SYNC();
-          const int nkh = (min(32, o1 - base) + 3) >> 2;  // valid k-steps per half
-#pragma unroll
-          for (int ks = 0; ks < 16; ks += 2) {
-            if ((ks & 7) < nkh) {
-              const double xa = Xw[(4 * ks + mrow) * XS + mcol];
-              acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(xa, xa, acc0, 0, 0, 0);
-            }
-            if (((ks + 1) & 7) < nkh) {
-              const double xb = Xw[(4 * ks + 4 + mrow) * XS + mcol];
-              acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(xb, xb, acc1, 0, 0, 0);
+              for (int q = 0; q < 9; ++q) xr[6 + q] = (q < nin) ? -Ji[KB_MAX_INTR * r + q] : 0.0;
+              xr[15] = -(r ? yv.y - w : yv.x - u);  // column 15 carries -e: H[:,15] = rhs part, H[15][15] = chi^2
             }
           }
-          KB_WAVE_SYNC();
+          // rows n .. 63 of a partial pass are zero: only the k-steps holding valid rows are issued (k-step ks = rows
+          // 4ks .. 4ks + 3, even ks into acc0, odd into acc1).  Row = lane: the lanes of a write hit distinct LDS bank
+          // pairs at the 17-double row stride.
+          const int nk = (min(64, o1 - base) + 3) >> 2;
+#pragma unroll
+          for (int r = 0; r < 2; ++r) {
+#pragma unroll
+            for (int q = 0; q < 16; ++q) Xw[lane * XS + q] = r ? xv[q] : xu[q];
+            KB_WAVE_SYNC();
+#pragma unroll
+            for (int ks = 0; ks < 16; ks += 2) {
+              if (ks < nk) {
+                const double xa = Xw[(4 * ks + mrow) * XS + mcol];
+                acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(xa, xa, acc0, 0, 0, 0);
+              }
+              if (ks + 1 < nk) {
+                const double xb = Xw[(4 * ks + 4 + mrow) * XS + mcol];
+                acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(xb, xb, acc1, 0, 0, 0);
+              }
+            }
+            KB_WAVE_SYNC();
+          }
         }
         {  // the next frame's first corner ids and keypoints, in flight during the expansion and the barrier
           fv = fvn;
-          const int k = min(fvn.x + (lane & 31), max(fvn.y - 1, 0));
+          const int k = min(fvn.x + lane, max(fvn.y - 1, 0));
           cidn = d.cid[k];
           yn = d.y[k];
         }
@@ -2478,13 +2486,16 @@ __device__ __forceinline__ void panel_backsolve(const KbDev& d, const double* S,
 // the one-block camera solve.  One thread per output entry; the block holding the first image entry also writes
 // cost_build, the threads of the gradient slots gc and rhs.
 // ---------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_colimg(KbDev d, const double* rows, double* out, int gate, int nrows) {
+constexpr int kColimgThreads = 1024;  // few, wide blocks: each image block stages the camera sums once
+__global__ void __launch_bounds__(kColimgThreads) k_colimg(KbDev d, const double* rows, double* out, int gate, int nrows) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const KbCtrl* c = d.ctrl;
   const int done = c->done, cur = c->cur, have = c->have_dx;
   const double lamc = c->lambda;
   if (gate && done) return;
   const int tid = threadIdx.x, q = blockIdx.x * blockDim.x + tid, nth = blockDim.x;
+  const bool stamp_block = blockIdx.x == d.Wtot / (int)blockDim.x;  // diagnostic timeline: the first image block
+  if (stamp_block) KB_TS(d, 50);
   const int N = d.N, C = d.C, Wt = d.W - d.C;
   const int nb = (C + 16) >> 4, ntz = kTileSz * nb * (nb + 1) / 2;  // + the b row (row C)
   const int q0 = blockIdx.x * blockDim.x;
@@ -2539,8 +2550,8 @@ __global__ void __launch_bounds__(256) k_colimg(KbDev d, const double* rows, dou
     const bool gfu = gate && d.gn_fused;
     const int bslot = (gfu && have) ? 1 - cur : cur;  // as k_solve: the state the system was built at
     const double* Kc = cam_K(d, bslot);
-    // C <= 111 bounds the rig to N <= 10 cameras: at most 6 sums of 8 rows and 15 chain entries per thread
-    constexpr int kHsU = 6, kKU = 18;
+    // C <= 111 bounds the rig to N <= 10 cameras: at most 2 sums of 8 rows and 4 chain entries per thread
+    constexpr int kHsU = 2, kKU = 4;
     const int nHs = N * 136, nK = N * N * 36;
     double kv[kKU], hv[kHsU][kColsumRows];
 #pragma unroll
@@ -2570,7 +2581,9 @@ __global__ void __launch_bounds__(256) k_colimg(KbDev d, const double* rows, dou
       }
     }
     if (tid < C) ci[tid] = civ;
+    if (stamp_block) KB_TS(d, 51);
     __syncthreads();
+    if (stamp_block) KB_TS(d, 52);
     for (int et = tid; et < nK; et += nth) {
       const int x = et % 36, ik = et / 36, i = ik / N, k = ik - i * N;
       double sacc = 0.0;
@@ -2582,6 +2595,7 @@ __global__ void __launch_bounds__(256) k_colimg(KbDev d, const double* rows, dou
       T[et] = sacc;
     }
     __syncthreads();
+    if (stamp_block) KB_TS(d, 53);
     if (tid == 0 && blockIdx.x == d.Wtot / nth) {
       double sc = 0.0;
       for (int i = 0; i < N; ++i) sc += Hs[i * 256 + 255];
@@ -2617,6 +2631,7 @@ __global__ void __launch_bounds__(256) k_colimg(KbDev d, const double* rows, dou
     v = cs;  // non-PD frame blocks
   }
   d.simg[e] = v;
+  if (stamp_block) KB_TS(d, 54);
 }
 
 // batched global -> LDS staging of the k_solve inputs: every thread keeps U independent loads in flight

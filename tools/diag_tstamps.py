@@ -37,5 +37,10 @@ for rep in range(3):
     order = sorted((buf[i] - t0, i) for i in names if buf[i] >= t0 and buf[i] - t0 < 10_000_000)
     print(f"k_solve timeline (rep {rep}, us from entry):\n" +
           "\n".join(f"{names[i]:24s} {dt / 100:8.2f}" for dt, i in order))
+    print('k_colimg stamps', [buf[i] - t0 for i in range(50, 55)])
+    if buf[54] > buf[50]:
+        print(f"k_colimg (first image block, thread 0): loads + staging {(buf[51] - buf[50]) / 100:.2f}, barrier "
+              f"{(buf[52] - buf[51]) / 100:.2f}, T + barrier {(buf[53] - buf[52]) / 100:.2f}, entry {(buf[54] - buf[53]) / 100:.2f} us;"
+              f" k_colimg end -> k_solve entry {(buf[0] - buf[54]) / 100:.2f} us")
     if buf[7] > buf[0]:  # shader clock over the kernel: s_memtime ticks / s_memrealtime (100 MHz) ticks
         print(f"shader clock during k_solve: {100.0 * (buf[61] - buf[60]) / (buf[7] - buf[0]):.0f} MHz")
