@@ -5,6 +5,7 @@
 #include <charconv>
 #include <cmath>
 #include <fstream>
+#include <limits>
 #include <sstream>
 #include <stdexcept>
 
@@ -443,44 +444,45 @@ void distort(int32_t m, const double* d, double& x, double& y, double* J) {
   y *= s;
 }
 
-// 9 x 9 symmetric eigenvector of the smallest eigenvalue (cyclic Jacobi)
-std::array<double, 9> smallest_eigvec9(std::array<double, 81> A) {
-  std::array<double, 81> V{};
-  for (int i = 0; i < 9; ++i) V[i * 9 + i] = 1.0;
+// n x n symmetric: the eigenvector of the smallest eigenvalue (cyclic Jacobi)
+template <int n>
+std::array<double, n> smallest_eigvec(std::array<double, n * n> A) {
+  std::array<double, n * n> V{};
+  for (int i = 0; i < n; ++i) V[i * n + i] = 1.0;
   for (int sweep = 0; sweep < 60; ++sweep) {
-    double off = 0.0;
-    for (int p = 0; p < 9; ++p)
-      for (int q = p + 1; q < 9; ++q) off += A[p * 9 + q] * A[p * 9 + q];
-    if (off < 1e-30) break;
-    for (int p = 0; p < 9; ++p)
-      for (int q = p + 1; q < 9; ++q) {
-        const double apq = A[p * 9 + q];
+    double off = 0.0, tot = 0.0;
+    for (int p = 0; p < n; ++p)
+      for (int q = 0; q < n; ++q) (p == q ? tot : off) += A[p * n + q] * A[p * n + q];
+    if (off <= 1e-30 * tot || off < 1e-300) break;
+    for (int p = 0; p < n; ++p)
+      for (int q = p + 1; q < n; ++q) {
+        const double apq = A[p * n + q];
         if (std::fabs(apq) < 1e-300) continue;
-        const double th = 0.5 * (A[q * 9 + q] - A[p * 9 + p]) / apq;
+        const double th = 0.5 * (A[q * n + q] - A[p * n + p]) / apq;
         const double t = (th >= 0 ? 1.0 : -1.0) / (std::fabs(th) + std::sqrt(th * th + 1.0));
         const double c = 1.0 / std::sqrt(t * t + 1.0), sn = t * c;
-        for (int k = 0; k < 9; ++k) {  // A <- J^T A J
-          const double akp = A[k * 9 + p], akq = A[k * 9 + q];
-          A[k * 9 + p] = c * akp - sn * akq;
-          A[k * 9 + q] = sn * akp + c * akq;
+        for (int k = 0; k < n; ++k) {  // A <- J^T A J
+          const double akp = A[k * n + p], akq = A[k * n + q];
+          A[k * n + p] = c * akp - sn * akq;
+          A[k * n + q] = sn * akp + c * akq;
         }
-        for (int k = 0; k < 9; ++k) {
-          const double apk = A[p * 9 + k], aqk = A[q * 9 + k];
-          A[p * 9 + k] = c * apk - sn * aqk;
-          A[q * 9 + k] = sn * apk + c * aqk;
+        for (int k = 0; k < n; ++k) {
+          const double apk = A[p * n + k], aqk = A[q * n + k];
+          A[p * n + k] = c * apk - sn * aqk;
+          A[q * n + k] = sn * apk + c * aqk;
         }
-        for (int k = 0; k < 9; ++k) {
-          const double vkp = V[k * 9 + p], vkq = V[k * 9 + q];
-          V[k * 9 + p] = c * vkp - sn * vkq;
-          V[k * 9 + q] = sn * vkp + c * vkq;
+        for (int k = 0; k < n; ++k) {
+          const double vkp = V[k * n + p], vkq = V[k * n + q];
+          V[k * n + p] = c * vkp - sn * vkq;
+          V[k * n + q] = sn * vkp + c * vkq;
         }
       }
   }
   int m = 0;
-  for (int i = 1; i < 9; ++i)
-    if (A[i * 9 + i] < A[m * 9 + m]) m = i;
-  std::array<double, 9> v{};
-  for (int k = 0; k < 9; ++k) v[k] = V[k * 9 + m];
+  for (int i = 1; i < n; ++i)
+    if (A[i * n + i] < A[m * n + m]) m = i;
+  std::array<double, n> v{};
+  for (int k = 0; k < n; ++k) v[k] = V[k * n + m];
   return v;
 }
 
@@ -505,11 +507,146 @@ std::array<double, 9> matmul3(const std::array<double, 9>& A, const std::array<d
 }
 }  // namespace
 
+namespace {
+// normalised coordinates -> undistorted by Gauss-Newton on distort(ybar) = y: 5 steps for radtan (the reference's
+// RadialTangentialDistortion::undistort loop, RadialTangentialDistortion.hpp(impl):68-98), up to 20 otherwise
+void undistort(int32_t distModel, const double* d, double& x, double& y) {
+  const double yu = x, yv = y;
+  double bx = yu, by = yv;
+  const int n = distModel == KB_PINHOLE_RADTAN ? 5 : 20;
+  for (int i = 0; i < n; ++i) {
+    double tx = bx, ty = by, F[4];
+    if (distModel == KB_PINHOLE_RADTAN) {
+      distort(distModel, d, tx, ty, F);
+    } else {  // central differences of the forward map
+      const double h = 1e-7;
+      double a0 = bx + h, a1 = by, b0 = bx - h, b1 = by, c0 = bx, c1 = by + h, e0 = bx, e1 = by - h;
+      distort(distModel, d, a0, a1, nullptr);
+      distort(distModel, d, b0, b1, nullptr);
+      distort(distModel, d, c0, c1, nullptr);
+      distort(distModel, d, e0, e1, nullptr);
+      F[0] = (a0 - b0) / (2 * h);
+      F[2] = (a1 - b1) / (2 * h);
+      F[1] = (c0 - e0) / (2 * h);
+      F[3] = (c1 - e1) / (2 * h);
+      distort(distModel, d, tx, ty, nullptr);
+    }
+    const double ex = yu - tx, ey = yv - ty;
+    // du = (F^T F)^-1 F^T e = F^-1 e for a square F
+    const double det = F[0] * F[3] - F[1] * F[2];
+    bx += (F[3] * ex - F[1] * ey) / det;
+    by += (-F[2] * ex + F[0] * ey) / det;
+    if (ex * ex + ey * ey < 1e-15) break;
+  }
+  x = bx;
+  y = by;
+}
+
+// OmniProjection::euclideanToKeypoint (OmniProjection.hpp(impl):76-114) without distortion (the initialiser's
+// cleared distortion): false behind the fov limit or off the sensor (isValid: 0 <= u < ru, 0 <= v < rv)
+bool omni_project(double xi, double fu, double fv, double cu, double cv, double ru, double rv, const double p[3],
+                  double kp[2]) {
+  const double d = std::sqrt(p[0] * p[0] + p[1] * p[1] + p[2] * p[2]);
+  const double fov = xi <= 1.0 ? xi : 1.0 / xi;  // updateTemporaries (:627-633)
+  if (p[2] <= -(fov * d)) return false;
+  const double rz = 1.0 / (p[2] + xi * d);
+  kp[0] = fu * p[0] * rz + cu;
+  kp[1] = fv * p[1] * rz + cv;
+  return kp[0] >= 0 && kp[0] < ru && kp[1] >= 0 && kp[1] < rv;
+}
+}  // namespace
+
+namespace {
+// OmniProjection::initializeIntrinsics (OmniProjection.hpp(impl):724-846): xi = 1, the image centre, then per corner
+// row of every view the conic through the centred points (u, v, 1/2, -(u^2 + v^2)/2) (cv::SVD::solveZ: the right
+// singular vector of the smallest singular value), skipped when t < 0 or the line is radial (|n_xy| > 0.95); each
+// candidate gamma = |c2 d / n_z| is scored by the mean reprojection error of the view under the pose
+// estimateTransformation finds with it, and the lowest wins.  out = (gamma0, success); gamma0 = the fallback when
+// no row scored (success false, as the reference returns).
+bool omni_focal(const std::vector<GridObservation>& observations, const AprilgridTarget& target,
+                std::optional<double> fallbackFocalLength, double& gamma0) {
+  const double cu = (observations[0].imCols - 1.0) / 2.0, cv = (observations[0].imRows - 1.0) / 2.0;
+  const double ru = (double)observations[0].imCols, rv = (double)observations[0].imRows;
+  const size_t R = target.rows(), Cn = target.cols();
+  const std::vector<double> P = target.points();
+  constexpr size_t kMinCorners = 4;
+  double minErr = std::numeric_limits<double>::max();
+  bool success = false;
+  gamma0 = 0.0;
+  for (const GridObservation& obs : observations) {
+    for (size_t r = 0; r < R; ++r) {
+      std::array<double, 16> PtP{};
+      size_t count = 0;
+      for (size_t c = 0; c < Cn; ++c) {
+        double kp[2];
+        if (!obs.imagePoint(r * Cn + c, kp)) continue;
+        const double u = kp[0] - cu, v = kp[1] - cv, row[4] = {u, v, 0.5, -0.5 * (u * u + v * v)};
+        for (int a = 0; a < 4; ++a)
+          for (int b = 0; b < 4; ++b) PtP[a * 4 + b] += row[a] * row[b];
+        ++count;
+      }
+      if (count <= kMinCorners) continue;
+      const std::array<double, 4> Cz = smallest_eigvec<4>(PtP);
+      const double t = Cz[0] * Cz[0] + Cz[1] * Cz[1] + Cz[2] * Cz[3];
+      if (t < 0) continue;
+      const double d = std::sqrt(1.0 / t), nx = Cz[0] * d, ny = Cz[1] * d;
+      if (std::hypot(nx, ny) > 0.95) continue;  // a radial line
+      const double nz = std::sqrt(1.0 - nx * nx - ny * ny);
+      const double gamma = std::fabs(Cz[2] * d / nz);
+      const double trial[5] = {1.0, gamma, gamma, cu, cv};
+      Transformation T_t_c;
+      if (!estimateTransformation(obs, target, KB_OMNI, trial, T_t_c)) continue;
+      // computeReprojectionError (:848-869): sum of |y - yhat| over the corners that project
+      const std::array<double, 9> Rm = T_t_c.C();
+      double err = 0.0;
+      size_t n = 0;
+      for (size_t i = 0; i < target.size(); ++i) {
+        double y[2], yh[2], pc[3];
+        if (!obs.imagePoint(i, y)) continue;
+        const double dx = P[3 * i] - T_t_c.t[0], dy = P[3 * i + 1] - T_t_c.t[1], dz = P[3 * i + 2] - T_t_c.t[2];
+        for (int a = 0; a < 3; ++a) pc[a] = Rm[a] * dx + Rm[3 + a] * dy + Rm[6 + a] * dz;  // C^T (P - t)
+        if (!omni_project(1.0, gamma, gamma, cu, cv, ru, rv, pc, yh)) continue;
+        err += std::hypot(y[0] - yh[0], y[1] - yh[1]);
+        ++n;
+      }
+      if (n > kMinCorners && err / n < minErr) {
+        minErr = err / n;
+        gamma0 = gamma;
+        success = true;
+      }
+    }
+  }
+  if (!success && fallbackFocalLength) gamma0 = *fallbackFocalLength;
+  return success;
+}
+}  // namespace
+
 bool initializeIntrinsics(const std::vector<GridObservation>& observations, const AprilgridTarget& target,
                           std::optional<double> fallbackFocalLength, int32_t camModel, std::vector<double>& intr) {
   if (observations.empty()) throw std::runtime_error("initializeIntrinsics: Need min. one observation");
+  if (camModel == KB_OMNI_RADTAN || camModel == KB_OMNI || camModel == KB_EUCM || camModel == KB_DS) {
+    double g = 0.0;
+    const bool ok = omni_focal(observations, target, fallbackFocalLength, g);
+    const double cu = (observations[0].imCols - 1.0) / 2.0, cv = (observations[0].imRows - 1.0) / 2.0;
+    if (camModel == KB_OMNI_RADTAN || camModel == KB_OMNI) {
+      // the omni model keeps the fallback focal length (set, but false returned) when no row scored
+      if (!ok && !fallbackFocalLength) return false;
+      intr.assign(camModel == KB_OMNI ? 5 : 9, 0.0);  // xi fu fv cu cv | distortion cleared
+      intr[0] = 1.0;
+      intr[1] = intr[2] = g;
+      intr[3] = cu;
+      intr[4] = cv;
+      return ok;
+    }
+    if (!ok) return false;  // EUCM / DS take the omni result only on success (intr untouched)
+    // ExtendedUnifiedProjection.hpp(impl):731-760: alpha = xi / 2, beta = 1, f = gamma / 2 (the same rays);
+    // DoubleSphereProjection.hpp(impl):783-812: xi = 0 (the spheres coincide), alpha = 1/2, f = gamma / 2
+    intr = camModel == KB_EUCM ? std::vector<double>{0.5, 1.0, 0.5 * g, 0.5 * g, cu, cv}
+                               : std::vector<double>{0.0, 0.5, 0.5 * g, 0.5 * g, cu, cv};
+    return true;
+  }
   const int nd = n_distortion(camModel);
-  if (nd < 0) throw std::runtime_error("initializeIntrinsics: not a pinhole camera model");
+  if (nd < 0) throw std::runtime_error("initializeIntrinsics: unknown camera model");
   const double cu = (observations[0].imCols - 1.0) / 2.0, cv = (observations[0].imRows - 1.0) / 2.0;
   const size_t R = target.rows(), Cn = target.cols();
   std::vector<double> guesses;
@@ -549,39 +686,55 @@ bool initializeIntrinsics(const std::vector<GridObservation>& observations, cons
 
 bool keypointToEuclidean(int32_t camModel, const double* intr, size_t imCols, size_t imRows, const double kp[2],
                          double out[3]) {
-  const int nd = n_distortion(camModel);
-  if (nd < 0) throw std::runtime_error("keypointToEuclidean: not a pinhole camera model");
-  const double yu = (kp[0] - intr[2]) / intr[0], yv = (kp[1] - intr[3]) / intr[1];
-  double bx = yu, by = yv;  // undistort: Gauss-Newton on distort(ybar) = y
-  const int n = camModel == KB_PINHOLE_RADTAN ? 5 : 20;
-  for (int i = 0; i < n; ++i) {
-    double tx = bx, ty = by, F[4];
-    if (camModel == KB_PINHOLE_RADTAN) {
-      distort(camModel, intr + 4, tx, ty, F);
-    } else {  // central differences of the forward map
-      const double h = 1e-7;
-      double a0 = bx + h, a1 = by, b0 = bx - h, b1 = by, c0 = bx, c1 = by + h, e0 = bx, e1 = by - h;
-      distort(camModel, intr + 4, a0, a1, nullptr);
-      distort(camModel, intr + 4, b0, b1, nullptr);
-      distort(camModel, intr + 4, c0, c1, nullptr);
-      distort(camModel, intr + 4, e0, e1, nullptr);
-      F[0] = (a0 - b0) / (2 * h);
-      F[2] = (a1 - b1) / (2 * h);
-      F[1] = (c0 - e0) / (2 * h);
-      F[3] = (c1 - e1) / (2 * h);
-      distort(camModel, intr + 4, tx, ty, nullptr);
+  switch (camModel) {
+    case KB_PINHOLE_RADTAN:
+    case KB_PINHOLE_EQUI:
+    case KB_PINHOLE_FOV: {  // PinholeProjection.hpp(impl):202-227
+      double bx = (kp[0] - intr[2]) / intr[0], by = (kp[1] - intr[3]) / intr[1];
+      undistort(camModel, intr + 4, bx, by);
+      out[0] = bx;
+      out[1] = by;
+      out[2] = 1.0;
+      return kp[0] >= 0.0 && kp[1] >= 0.0 && kp[0] < (double)imCols && kp[1] < (double)imRows;  // isValid
     }
-    const double ex = yu - tx, ey = yv - ty;
-    // du = (F^T F)^-1 F^T e = F^-1 e for a square F
-    const double det = F[0] * F[3] - F[1] * F[2];
-    bx += (F[3] * ex - F[1] * ey) / det;
-    by += (-F[2] * ex + F[0] * ey) / det;
-    if (ex * ex + ey * ey < 1e-15) break;
+    case KB_OMNI_RADTAN:
+    case KB_OMNI: {  // OmniProjection.hpp(impl):230-262 (no isValid test of the keypoint)
+      const double xi = intr[0];
+      double mx = (kp[0] - intr[3]) / intr[1], my = (kp[1] - intr[4]) / intr[2];
+      if (camModel == KB_OMNI_RADTAN) undistort(KB_PINHOLE_RADTAN, intr + 5, mx, my);
+      const double r2 = mx * mx + my * my;
+      if (!(xi <= 1.0 || r2 <= 1.0 / (xi * xi - 1))) return false;  // isUndistortedKeypointValid (:584-588)
+      out[0] = mx;
+      out[1] = my;
+      out[2] = 1 - xi * (r2 + 1) / (xi + std::sqrt(1 + (1 - xi * xi) * r2));
+      return true;
+    }
+    case KB_EUCM: {  // ExtendedUnifiedProjection.hpp(impl):248-283
+      const double alpha = intr[0], beta = intr[1];
+      const double mx = (kp[0] - intr[4]) / intr[2], my = (kp[1] - intr[5]) / intr[3], r2 = mx * mx + my * my;
+      if (!(alpha <= 0.5 || r2 <= 1.0 / (beta * (2 * alpha - 1)))) return false;  // (:612-616, :655)
+      const double gamma = 1 - alpha;
+      const double k = (1 - alpha * alpha * beta * r2) / (alpha * std::sqrt(1 - (alpha - gamma) * beta * r2) + gamma);
+      const double ninv = 1.0 / std::sqrt(r2 + k * k);
+      out[0] = mx * ninv;
+      out[1] = my * ninv;
+      out[2] = k * ninv;
+      return true;
+    }
+    case KB_DS: {  // DoubleSphereProjection.hpp(impl):271-307
+      const double xi = intr[0], alpha = intr[1];
+      const double mx = (kp[0] - intr[4]) / intr[2], my = (kp[1] - intr[5]) / intr[3], r2 = mx * mx + my * my;
+      if (!(alpha <= 0.5 || r2 <= 1.0 / (2 * alpha - 1))) return false;  // (:660-664, :703)
+      const double mz = (1 - alpha * alpha * r2) / (alpha * std::sqrt(1 - (2 * alpha - 1) * r2) + 1 - alpha);
+      const double mz2 = mz * mz;
+      const double k = (mz * xi + std::sqrt(mz2 + (1 - xi * xi) * r2)) / (mz2 + r2);
+      out[0] = k * mx;
+      out[1] = k * my;
+      out[2] = k * mz - xi;
+      return true;
+    }
+    default: throw std::runtime_error("keypointToEuclidean: unknown camera model");
   }
-  out[0] = bx;
-  out[1] = by;
-  out[2] = 1.0;
-  return kp[0] >= 0.0 && kp[1] >= 0.0 && kp[0] < (double)imCols && kp[1] < (double)imRows;  // isValid
 }
 
 bool estimateTransformation(const GridObservation& obs, const AprilgridTarget& target, int32_t camModel,
@@ -630,7 +783,7 @@ bool estimateTransformation(const GridObservation& obs, const AprilgridTarget& t
     for (int a = 0; a < 9; ++a)
       for (int b = 0; b < 9; ++b) AtA[a * 9 + b] += r1[a] * r1[b] + r2[a] * r2[b];
   }
-  const std::array<double, 9> hn = smallest_eigvec9(AtA);
+  const std::array<double, 9> hn = smallest_eigvec<9>(AtA);
   // denormalise: H = Tm^-1 Hn TM
   const std::array<double, 9> Tmi{1 / sm, 0, mx, 0, 1 / sm, my, 0, 0, 1}, TM{sM, 0, -sM * Mx, 0, sM, -sM * My, 0, 0, 1};
   std::array<double, 9> H = matmul3(Tmi, matmul3(hn, TM));

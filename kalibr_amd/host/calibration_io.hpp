@@ -4,7 +4,7 @@
 //   out: the calibration as ROS CameraInfo / TransformStamped / TFMessage YAML, as kalibr_calibrate_cameras
 //        exports it.
 // Paths are relative to the reference repository.  Target detection (AprilTags, OpenCV) is not rebuilt; the
-// pinhole initialisers (initializeIntrinsics, estimateTransformation) are, without OpenCV.
+// initialisers of every model (initializeIntrinsics, estimateTransformation) are, without OpenCV.
 #pragma once
 
 #include <array>
@@ -82,7 +82,7 @@ backend::CalibrationProblem buildRigProblem(const std::vector<int32_t>& camModel
                                             const std::vector<SyncedSet>& sets,
                                             const std::vector<Transformation>& baselineGuesses);
 
-// ---------------------------------------------------------------- initialisers (PinholeProjection)
+// ---------------------------------------------------------------- initialisers (Pinhole / Omni / EUCM / DS)
 /// PinholeProjection::initializeIntrinsics (aslam_cv/aslam_cameras/include/aslam/cameras/implementation/
 /// PinholeProjection.hpp:713-803): image centre (cols - 1) / 2, (rows - 1) / 2; focal length = the median over the
 /// complete views of |v1 - v2| / pi for the intersections v1, v2 of the circles fitted to pairs of corner rows
@@ -91,19 +91,28 @@ backend::CalibrationProblem buildRigProblem(const std::vector<int32_t>& camModel
 /// Deviation: the reference pairs row j with rows j + 1 .. target.cols() - 1 and so reads past its row array when
 /// cols > rows; here the pairs stop at the last row.  Returns false (the reference's SM_ERROR path) when neither a
 /// guess nor a fallback exists.
+/// Omni / omni-radtan (OmniProjection.hpp(impl):724-846): xi = 1, the image centre, the focal length gamma from the
+/// conic fitted to each corner row (the row's image under xi = 1), scored by the view's mean reprojection error
+/// under the pose estimateTransformation finds with it; intr = [1 gamma gamma cu cv | distortion 0].  With no
+/// scored row: the fallback focal length is set and false returned (the reference's warning path), or false.
+/// EUCM (ExtendedUnifiedProjection.hpp(impl):731-760) and DS (DoubleSphereProjection.hpp(impl):783-812) run the
+/// omni initialiser and, on success only, map it onto the same rays: EUCM [alpha 1/2, beta 1, gamma/2, gamma/2,
+/// cu, cv], DS [xi 0, alpha 1/2, gamma/2, gamma/2, cu, cv].
 bool initializeIntrinsics(const std::vector<GridObservation>& observations, const AprilgridTarget& target,
                           std::optional<double> fallbackFocalLength, int32_t camModel, std::vector<double>& intr);
 
-/// PinholeProjection::keypointToEuclidean (:202-227): normalised coordinates, the distortion inverted by 5
-/// Gauss-Newton steps for radtan (RadialTangentialDistortion.hpp(impl):68-98, the reference's loop) and up to 20
-/// for equidistant / FOV; false when the keypoint is outside the image (isValid).
+/// keypointToEuclidean of every model: pinhole (PinholeProjection.hpp(impl):202-227: normalised coordinates, the
+/// distortion inverted by 5 Gauss-Newton steps for radtan (RadialTangentialDistortion.hpp(impl):68-98) and up to 20
+/// for equidistant / FOV; false off the image, isValid); omni (OmniProjection.hpp(impl):230-262, radtan undistorted
+/// first), EUCM (ExtendedUnifiedProjection.hpp(impl):248-283), DS (DoubleSphereProjection.hpp(impl):271-307): the
+/// lifted ray, false where isUndistortedKeypointValid fails (the keypoint itself is not range-checked there).
 bool keypointToEuclidean(int32_t camModel, const double* intr, size_t imCols, size_t imRows, const double kp[2],
                          double out[3]);
 
-/// PinholeProjection::estimateTransformation (:811-880): the seen corners back-projected (kept when the ray is
-/// within 80 degrees of the axis), then the pose of the planar target from those normalised points -- solvePnP
-/// with K = I there; here a normalised-DLT homography, its decomposition into (R, t) and a Levenberg-Marquardt
-/// refinement of the normalised reprojection error.  out_T_t_c takes camera points to the target frame.  False
+/// estimateTransformation (PinholeProjection.hpp(impl):811-880; OmniProjection.hpp(impl):871-958, EUCM and DS
+/// alike): the seen corners back-projected (kept when the ray is within 80 degrees of the axis), then the pose of
+/// the planar target from those points' x/z, y/z -- solvePnP with K = I there; here a normalised-DLT homography,
+/// its decomposition into (R, t) and a Levenberg-Marquardt refinement of the normalised reprojection error.  out_T_t_c takes camera points to the target frame.  False
 /// with fewer than 4 usable corners.
 bool estimateTransformation(const GridObservation& obs, const AprilgridTarget& target, int32_t camModel,
                             const double* intr, Transformation& out_T_t_c);

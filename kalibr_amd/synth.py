@@ -242,8 +242,9 @@ def state_size(n_cams, n_frames):
 
 
 def make_problem(models, n_frames, seed, p_view=1.0, noise_px=0.3, min_corners=12,
-                 resolution=(1280, 1024), name="", init_noise=True):
-    """Synthesise an N-camera x F-frame AprilGrid problem."""
+                 resolution=(1280, 1024), name="", init_noise=True, intrinsics=None):
+    """Synthesise an N-camera x F-frame AprilGrid problem.  intrinsics: optional per-camera
+    override of the default true intrinsics (a list with None for the defaults)."""
     rng = np.random.Generator(np.random.PCG64(seed))
     W, H = resolution
     N = len(models)
@@ -267,6 +268,8 @@ def make_problem(models, n_frames, seed, p_view=1.0, noise_px=0.3, min_corners=1
             intr_truth[i, :5] = [700.0, 700.0, 640.0, 512.0, 0.9]
         else:
             raise ValueError(m)
+        if intrinsics is not None and intrinsics[i] is not None:
+            intr_truth[i, :NINTR[m]] = intrinsics[i]
     # rig: camera i+1 sits 0.12 m along -x from camera i, +-3 deg, +-5 mm
     base_T = []
     cam_T_c0 = [np.eye(4)]  # T_{ci, c0}

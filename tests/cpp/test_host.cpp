@@ -710,17 +710,24 @@ static int run_init(const CalibrationProblem& p, size_t imCols, size_t imRows) {
   for (size_t i = 0; i < N; ++i) {
     std::vector<double> intr;
     const bool ok = io::initializeIntrinsics(per_cam[i], tgt, std::nullopt, p.cam_model[i], intr);
-    char buf[128];
-    std::snprintf(buf, sizeof buf, "%s[%d, %.17g, %.17g, %.17g]", i ? ", " : "", ok ? 1 : 0, ok ? intr[0] : 0.0,
-                  ok ? intr[2] : 0.0, ok ? intr[3] : 0.0);
-    f0 += buf;
+    char buf[64];
+    f0 += i ? ", [" : "[";
+    f0 += ok ? "1" : "0";
+    for (double v : intr) {
+      std::snprintf(buf, sizeof buf, ", %.17g", v);
+      f0 += buf;
+    }
+    f0 += "]";
   }
   f0 += "]";
   std::vector<double> fb;
-  const bool fb_ok = io::initializeIntrinsics({io::GridObservation(K)}, tgt, 777.0, p.cam_model[0], fb);
+  io::GridObservation empty(K);
+  empty.imCols = imCols;
+  empty.imRows = imRows;
+  const bool fb_ok = io::initializeIntrinsics({empty}, tgt, 777.0, p.cam_model[0], fb);
   std::printf("{\"views\": %d, \"estimated\": %d, \"max_rot\": %.3e, \"max_trans\": %.3e, \"init\": %s, "
               "\"fallback_ok\": %d, \"fallback_f\": %.17g}\n",
-              n_views, n_ok, max_rot, max_trans, f0.c_str(), fb_ok ? 1 : 0, fb_ok ? fb[0] : 0.0);
+              n_views, n_ok, max_rot, max_trans, f0.c_str(), fb_ok ? 1 : 0, fb.empty() ? 0.0 : fb[fb.size() == 5 || fb.size() == 9 ? 1 : 0]);
   return 0;
 }
 

@@ -153,8 +153,57 @@ def test_initialize_intrinsics_vanishing_points(driver, tmp_path):  # noqa: F811
     when no view yields a guess."""
     p = synth.make_problem([synth.PINHOLE_EQUI], 40, seed=99, noise_px=0.0, resolution=(1280, 1024))
     r = _run_init(driver, tmp_path, p)
-    ok, f0, cu, cv = r["init"][0]
+    ok, f0, _, cu, cv = r["init"][0][:5]
     fu = p.state_truth[0]
     assert ok == 1 and abs(f0 - fu) / fu < 0.2, (f0, fu)
     assert cu == (1280 - 1) / 2 and cv == (1024 - 1) / 2
     assert r["fallback_ok"] == 1 and r["fallback_f"] == 777.0
+
+
+OMNI_EXACT = {synth.OMNI: [1.0, 450.0, 450.0, 639.5, 511.5], synth.EUCM: [0.5, 1.0, 225.0, 225.0, 639.5, 511.5],
+              synth.DS: [0.0, 0.5, 225.0, 225.0, 639.5, 511.5]}
+
+
+def test_omni_family_initializers_exact(driver, tmp_path):  # noqa: F811
+    """OmniProjection::initializeIntrinsics (OmniProjection.hpp(impl):724-846) and the EUCM / DS initialisers built
+    on it (ExtendedUnifiedProjection.hpp(impl):731-760, DoubleSphereProjection.hpp(impl):783-812).  Each row's image
+    is exactly the conic the initialiser fits when the true camera is the xi = 1 unified model (EUCM alpha = 1/2,
+    beta = 1; DS xi = 0, alpha = 1/2, all with the principal point at the image centre): noise-free keypoints give
+    back the true intrinsics (EUCM / DS focal = gamma / 2).  estimateTransformation through each model's
+    keypointToEuclidean recovers every view's pose."""
+    models = [synth.OMNI, synth.EUCM, synth.DS]
+    p = synth.make_problem(models, 24, seed=77, noise_px=0.0, resolution=(1280, 1024),
+                           intrinsics=[OMNI_EXACT[m] for m in models])
+    r = _run_init(driver, tmp_path, p)
+    assert r["estimated"] == r["views"] > 0 and r["max_rot"] < 1e-6 and r["max_trans"] < 1e-6, r
+    for i, m in enumerate(models):
+        ok, *intr = r["init"][i]
+        assert ok == 1, r
+        np.testing.assert_allclose(intr, OMNI_EXACT[m], rtol=1e-6, atol=1e-9)
+    # the omni fallback: the focal length is set, false returned (the reference's warning path)
+    assert r["fallback_ok"] == 0 and r["fallback_f"] == 777.0
+
+
+@pytest.mark.parametrize("model", [synth.OMNI_RADTAN, synth.EUCM, synth.DS])
+def test_omni_family_initializers_approximate(driver, tmp_path, model):  # noqa: F811
+    """The same initialisers on the default synthetic lenses (omni xi = 0.9 with radtan, EUCM alpha = 0.6 beta = 1.1,
+    DS xi = -0.2 alpha = 0.6) and 0.3 px noise: the initial guess is an xi = 1 / alpha = 1/2 camera whose focal
+    length matches the lens's near-axis focal length (omni 2 f / (1 + xi), EUCM f: within 15 %; DS f / (1 + xi): within
+    20 %, its rows' curvature away from the axis pulls the fitted xi = 1 focal length down by ~16 %); the
+    poses from estimateTransformation with the true intrinsics stay at the noise level."""
+    p = synth.make_problem([model] * 2, 30, seed=5, noise_px=0.3, resolution=(1280, 1024))
+    r = _run_init(driver, tmp_path, p)
+    # 0.3 px at these wide lenses' ~240-450 px near-axis focal lengths: the single-view pose is good to ~1e-2
+    assert r["estimated"] == r["views"] > 0 and r["max_rot"] < 2e-2 and r["max_trans"] < 2e-2, r
+    t = p.state_truth[: synth.NINTR[model]]
+    if model == synth.OMNI_RADTAN:
+        f_eff, k = 2 * t[1] / (1 + t[0]), 1
+    elif model == synth.EUCM:
+        f_eff, k = t[2], 2
+    else:
+        f_eff, k = t[2] / (1 + t[0]), 2
+    for i in range(2):
+        ok, *intr = r["init"][i]
+        assert ok == 1, r
+        assert abs(intr[k] - f_eff) / f_eff < (0.2 if model == synth.DS else 0.15), (intr, f_eff)
+        assert intr[k] == intr[k + 1] and intr[k + 2] == 639.5 and intr[k + 3] == 511.5
