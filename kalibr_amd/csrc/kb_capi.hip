@@ -642,19 +642,17 @@ static int allreduce_red(kb_handle* h, bool reduce = true) {
 // all-reduced as they are (one collective, no finishing kernel)
 static int launch_colsum(kb_handle* h, int gate, bool finish = true) {
   KbDev& d = h->d;
-  hipLaunchKernelGGL(k_colsum, dim3((d.Wtot + 63) / 64, kColsumRows), dim3(256), 0, h->stream, d, gate);
   if (finish && h->C > 64) {
-    // camera blocks for the tiled solve: k_colimg finishes the sums (into the consumer's row) and writes k_solve's
-    // LDS image from the same rows.  Sharded, each rank first finishes its 8 stage-1 rows into one (k_colfin) and
-    // the ranks all-reduce that single row: 8x less data on the links than the stage-1 rows (55 KB at configs[3])
+    // camera blocks for the tiled solve: the block partials summed in one pass into one row (k_colsum1), then
+    // k_colimg copies the sums (into the consumer's row) and writes k_solve's LDS image from that row.  Sharded,
+    // the ranks all-reduce the single row (55 KB at configs[3])
+    hipLaunchKernelGGL(k_colsum1, dim3((d.Wtot + 63) / 64), dim3(64 * kColsum1Waves), 0, h->stream, d, gate);
+    KB_HIP(hipGetLastError());
     const double* rows = d.part8;
-    int nrows = kColsumRows;
+    const int nrows = 1;
     if (sharded(h)) {
-      hipLaunchKernelGGL(k_colfin, dim3((d.Wtot + 255) / 256), dim3(256), 0, h->stream, d, gate);
-      KB_HIP(hipGetLastError());
-      if (coll_allreduce(h, d.psum_local, h->psum_red8, d.Wtot)) return -1;
+      if (coll_allreduce(h, d.part8, h->psum_red8, d.Wtot)) return -1;
       rows = h->psum_red8;
-      nrows = 1;
     }
     double* out = sharded(h) ? h->psum_red : d.psum_local;
     hipLaunchKernelGGL(k_colimg, dim3((d.Wtot + d.img_n + kColimgThreads - 1) / kColimgThreads), dim3(kColimgThreads),
@@ -662,6 +660,7 @@ static int launch_colsum(kb_handle* h, int gate, bool finish = true) {
     KB_HIP(hipGetLastError());
     return 0;
   }
+  hipLaunchKernelGGL(k_colsum, dim3((d.Wtot + 63) / 64, kColsumRows), dim3(256), 0, h->stream, d, gate);
   if (finish) hipLaunchKernelGGL(k_colfin, dim3((d.Wtot + 255) / 256), dim3(256), 0, h->stream, d, gate);
   KB_HIP(hipGetLastError());
   if (sharded(h)) {
@@ -1528,12 +1527,12 @@ int kb_comm_init_local(kb_handle* const* hs, int32_t n) {
 // diagnostic build only: the KB_TS timeline of the last k_solve launch (100 MHz ticks)
 int kb_diag_read_ts(kb_handle* h, long long* out, int n) {
   if (!h->d.dbg_ts) {
-    KB_HIP(hipMalloc(&h->d.dbg_ts, 128 * sizeof(long long)));
-    KB_HIP(hipMemset(h->d.dbg_ts, 0, 128 * sizeof(long long)));
+    KB_HIP(hipMalloc(&h->d.dbg_ts, 256 * sizeof(long long)));
+    KB_HIP(hipMemset(h->d.dbg_ts, 0, 256 * sizeof(long long)));
     drop_graphs(h);
     return 0;
   }
-  KB_HIP(hipMemcpy(out, h->d.dbg_ts, sizeof(long long) * std::min(n, 128), hipMemcpyDeviceToHost));
+  KB_HIP(hipMemcpy(out, h->d.dbg_ts, sizeof(long long) * std::min(n, 256), hipMemcpyDeviceToHost));
   return 0;
 }
 

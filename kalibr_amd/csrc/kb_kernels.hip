@@ -27,6 +27,10 @@ namespace kb {
 typedef double v4d __attribute__((ext_vector_type(4)));
 
 #define KB_WAVE_SYNC() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
+// an (empty) use of an accumulation register: the compiler then selects the AGPR-accumulator form of every MFMA in
+// the kernel.  With VGPR accumulators, a wave issuing back-to-back f64 MFMAs slows the VALU instructions of the other
+// waves on its SIMD ~5x (38 vs 7 cycles each); with AGPR accumulators ~2x (tools/micro/simd_share.hip)
+#define KB_MFMA_AGPR() asm volatile("" ::"a"(0))
 // materialise a loaded value at this point (an empty asm use): loads issued above cannot sink below it
 #define KB_KEEP(x) asm volatile("" ::"v"(x))
 #define KB_KEEPS(x) asm volatile("" ::"s"(x))
@@ -544,9 +548,10 @@ __device__ __forceinline__ bool frame_gj(const KbDev& d, int f, const double* Hf
 // MFMA-heavy waves), then each lane solves its columns lane and lane + 64 of [H_fc | g_f] (P, rows of 6).
 // Writes Q (rows of 6, columns 0..C) and, if `store`, A_f / b_f to HBM.  Returns false if not positive definite.
 __device__ __forceinline__ bool frame_ldl(const KbDev& d, int f, const double* Hff, double lam2, const double* P,
-                                          double* Q, int CZ, int lane, bool store) {
+                                          double* Q, int CZ, int lane, bool store, bool stamp = false) {
   const int C = d.C;
   double L[6][6], Di[6];
+  if (stamp) KB_TSB(d, 140);
   bool ok = true;
 #pragma unroll
   for (int i = 0; i < 6; ++i)
@@ -571,6 +576,7 @@ __device__ __forceinline__ bool frame_ldl(const KbDev& d, int f, const double* H
       L[i][k] = s * Di[k];
     }
   }
+  if (stamp) KB_TSB(d, 141);
 #pragma unroll
   for (int sl = 0; sl < 2; ++sl) {
     const int c = lane + 64 * sl, cc = min(c, C);
@@ -602,6 +608,7 @@ __device__ __forceinline__ bool frame_ldl(const KbDev& d, int f, const double* H
           d.bf[(size_t)f * 6 + i] = x[i];
       }
     }
+    if (stamp) KB_TSB(d, 142 + sl);
   }
   return ok;
 }
@@ -1112,6 +1119,7 @@ __device__ __forceinline__ void schur_tiles_accumulate6(const double* P, const d
 // (configs[2]) take MW = 8 (256 VGPRs, no spills, one block per CU) -- kb_capi.hip `buildp_wide`.
 template <int TT, bool GNF, unsigned MM, int MW>
 __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse) {
+  KB_MFMA_AGPR();
   KbCtrl* c = d.ctrl;
   extern __shared__ __attribute__((aligned(16))) double sm[];
   constexpr int NF = buildp_nf<TT>();
@@ -1315,10 +1323,32 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
         double Ri[9], ti[3], R[9], t[3];
         pose_inverse(fp, Ri, ti);
         rt_mul(Lc, Lc + 9, Ri, ti, R, t);  // T_cam_w = L_cam T_f^-1
+        // the view's chain G (6 x 6) for the expansion, formed while the first pass's MFMAs run (its LDS round trips
+        // off the critical path)
+        double* wv = Wv + cam * 64;
+        double* Gm = wv + 16;
+        auto make_g = [&]() {
+          if (lane == 0) {
+#pragma unroll
+            for (int q = 0; q < 9; ++q) wv[q] = R[q];
+            wv[9] = t[0];
+            wv[10] = t[1];
+            wv[11] = t[2];
+            wv[12] = fp[4];
+            wv[13] = fp[5];
+            wv[14] = fp[6];
+          }
+          KB_WAVE_SYNC();
+          if (lane < 36) Gm[lane] = chain_entry(wv, wv + 9, wv + 12, lane / 6, lane % 6);
+        };
         v4d acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
         const int o0 = fv.x, o1 = fv.y;
-        for (int base = o0; base < o1; base += 64) {  // 64 corners per pass: the u rows, then the v rows in the tile
+        const bool stv = (wave == 0 || wave == N - 1) && it == 2;  // diagnostic stamps: one steady-state frame
+        const int sto = wave == 0 ? 130 : 160;
+        int pass = 0;
+        for (int base = o0; base < o1; base += 64, ++pass) {  // 64 corners per pass: the u rows, then the v rows
           const int k = base + lane;
+          if (stv && pass < 2) KB_TSB(d, sto + 4 * pass);
           const int cid = cidn;
           const double2 yv = yn;
           if (base + 64 < o1) {  // software-pipelined: next pass's corner ids and keypoints
@@ -1356,29 +1386,49 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
               xr[15] = -(r ? yv.y - w : yv.x - u);  // column 15 carries -e: H[:,15] = rhs part, H[15][15] = chi^2
             }
           }
-          // rows n .. 63 of a partial pass are zero: only the k-steps holding valid rows are issued (k-step ks = rows
-          // 4ks .. 4ks + 3, even ks into acc0, odd into acc1).  Row = lane: the lanes of a write hit distinct LDS bank
-          // pairs at the 17-double row stride.
-          const int nk = (min(64, o1 - base) + 3) >> 2;
+          if (stv && pass < 2) KB_TSB(d, sto + 4 * pass + 1);
+          // rows n .. 63 of a partial pass are zero: only the groups of 4 k-steps (16 rows) holding valid rows are
+          // issued (k-step ks = rows 4ks .. 4ks + 3, even ks into acc0, odd into acc1), the next group's operands in
+          // flight during the current group's MFMAs (one LDS round trip per group, not per MFMA).  Row = lane: the
+          // lanes of a write hit distinct LDS bank pairs at the 17-double row stride.
+          const int ng = (min(64, o1 - base) + 15) >> 4;
 #pragma unroll
           for (int r = 0; r < 2; ++r) {
 #pragma unroll
             for (int q = 0; q < 16; ++q) Xw[lane * XS + q] = r ? xv[q] : xu[q];
             KB_WAVE_SYNC();
+            // groups g = 0..3 ping-pong between xa and xb: group g + 1's loads are issued before group g's MFMAs
+            double xa[4], xb[4];
+            auto ld = [&](double* x, int g) {
 #pragma unroll
-            for (int ks = 0; ks < 16; ks += 2) {
-              if (ks < nk) {
-                const double xa = Xw[(4 * ks + mrow) * XS + mcol];
-                acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(xa, xa, acc0, 0, 0, 0);
-              }
-              if (ks + 1 < nk) {
-                const double xb = Xw[(4 * ks + 4 + mrow) * XS + mcol];
-                acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(xb, xb, acc1, 0, 0, 0);
+              for (int u = 0; u < 4; ++u) x[u] = Xw[(16 * g + 4 * u + mrow) * XS + mcol];
+              __builtin_amdgcn_sched_barrier(0);
+            };
+            auto mf = [&](const double* x) {
+              acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(x[0], x[0], acc0, 0, 0, 0);
+              acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(x[1], x[1], acc1, 0, 0, 0);
+              acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(x[2], x[2], acc0, 0, 0, 0);
+              acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(x[3], x[3], acc1, 0, 0, 0);
+              __builtin_amdgcn_sched_barrier(0);
+            };
+            ld(xa, 0);
+            if (ng > 1) ld(xb, 1);
+            mf(xa);
+            if (ng > 1) {
+              if (ng > 2) ld(xa, 2);
+              mf(xb);
+              if (ng > 2) {
+                if (ng > 3) ld(xb, 3);
+                mf(xa);
+                if (ng > 3) mf(xb);
               }
             }
+            if (stv && pass < 2) KB_TSB(d, sto + 4 * pass + 2 + r);
+            if (r == 0 && pass == 0) make_g();
             KB_WAVE_SYNC();
           }
         }
+        if (o1 <= o0) make_g();  // a view without corners (no pass ran)
         {  // the next frame's first corner ids and keypoints, in flight during the expansion and the barrier
           fv = fvn;
           const int k = min(fvn.x + lane, max(fvn.y - 1, 0));
@@ -1393,92 +1443,80 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
           hv[q] = acc0[q] + acc1[q];
           creg[q] = creg[q] + hv[q];
         }
-        double* wv = Wv + cam * 64;
-        if (lane == 0) {
-#pragma unroll
-          for (int q = 0; q < 9; ++q) wv[q] = R[q];
-          wv[9] = t[0];
-          wv[10] = t[1];
-          wv[11] = t[2];
-          wv[12] = fp[4];
-          wv[13] = fp[5];
-          wv[14] = fp[6];
-        }
-        KB_WAVE_SYNC();
-        // expansion of view (f, cam) through the 6-D chains on three MFMA steps (no LDS copy of H):
-        //   T1 = G^T [H_dd | H_dI | . | g_d]  (A = G from LDS, B = the lane's own H registers: MFMA C layout row r of a
-        //        lane is B row r of the next k-step), rows 0..5: P_v = G^T H_dd, G^T H_dI, G^T g_d;
-        //   dH = P_v G and this camera's share of the baseline columns P_v K_{v,j} (A = P_v^T through LDS)
-        double* Gm = wv + 16;
-        if (lane < 36) Gm[lane] = chain_entry(wv, wv + 9, wv + 12, lane / 6, lane % 6);
-        KB_WAVE_SYNC();
-        double* T1 = Xw;  // [16][17] wave-local: rows 0..5 of T1
+        // expansion of view (f, cam) through the 6-D chain G on MFMA steps whose operands stay in registers:
+        //   D = H[:, d] G  (A = the lane's own H registers: H is symmetric, so C-layout row r of a lane is A's k-step r;
+        //   B = G from LDS), i.e. D[i][a] = P_v[a][i] with P_v = G^T H[d, :]: G^T H_dd, G^T H_dI, G^T g_d;
+        //   then D's C layout is the A operand P_v[:, d] of dH = P_v G and of this camera's share P_v K_{v,j} of the
+        //   baseline columns.  No LDS transposition; the chain's loads were issued before the SYRK.
         double* Cb = vb;  // P_v K_{v,j} at pair (v(v-1)/2 + j)
         double* dHv = vb + 36 * NP + cam * 36;
         double* dgv = vb + 36 * NP + N * 36 + cam * 8;
         double* Pi = vb + 36 * NP + N * 44;
         const int i16 = lane & 15, k0 = lane >> 4;
-        v4d t1 = {0.0, 0.0, 0.0, 0.0};
+        const double* Kv = Kl + (cam * (cam - 1) / 2) * 36;
+        const int nct = (6 * cam + 15) >> 4;  // 16-column tiles of [K_{v,0} | K_{v,1} | ...]
+        double gb[2], kb[3][2];
 #pragma unroll
         for (int st = 0; st < 2; ++st) {
           const int k = k0 + 4 * st;
-          const double ga = Gm[min(k, 5) * 6 + min(i16, 5)];
-          t1 = __builtin_amdgcn_mfma_f64_16x16x4f64((k < 6 && i16 < 6) ? ga : 0.0, k < 6 ? hv[st] : 0.0, t1, 0, 0, 0);
-        }
-        // T1 entry (a, j): a = k0 + 4 r, j = i16
+          const double g = Gm[min(k, 5) * 6 + min(i16, 5)];
+          gb[st] = (k < 6 && i16 < 6) ? g : 0.0;
 #pragma unroll
-        for (int r = 0; r < 2; ++r) {
-          const int arow = k0 + 4 * r;
-          if (arow < 6) {
-            T1[arow * 17 + i16] = t1[r];
-            if (i16 >= 6 && i16 < 6 + nin) {  // G^T H_dI: the camera's intrinsic columns
-              Pi[arow * CZ + ctab[0][cam] + i16 - 6] = t1[r];
-              if (!gfu) d.Hfc[((size_t)f * 6 + arow) * C + ctab[0][cam] + i16 - 6] = t1[r];
-            } else if (i16 == 15) {
-              dgv[arow] = t1[r];  // G^T g_d
+          for (int ct = 0; ct < 3; ++ct) {
+            const int c = 16 * ct + i16, cc = min(c, max(6 * cam - 1, 0)), jj = cc / 6, bb = cc - 6 * jj;
+            const double v = Kv[min(jj * 36 + min(k, 5) * 6 + bb, max(36 * cam - 1, 0))];
+            kb[ct][st] = (k < 6 && c < 6 * cam) ? v : 0.0;
+          }
+        }
+        v4d dv = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int st = 0; st < 2; ++st) dv = __builtin_amdgcn_mfma_f64_16x16x4f64(hv[st], gb[st], dv, 0, 0, 0);
+        double pa[2];  // A = P_v[:, d]: lane supplies P_v[i16][k0 + 4 st] = D[k0 + 4 st][i16]
+#pragma unroll
+        for (int st = 0; st < 2; ++st) pa[st] = (k0 + 4 * st < 6) ? dv[st] : 0.0;
+        v4d t2 = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int st = 0; st < 2; ++st) t2 = __builtin_amdgcn_mfma_f64_16x16x4f64(pa[st], gb[st], t2, 0, 0, 0);
+        v4d t3[3];
+#pragma unroll
+        for (int ct = 0; ct < 3; ++ct) {
+          t3[ct] = v4d{0.0, 0.0, 0.0, 0.0};
+          if (ct < nct) {
+#pragma unroll
+            for (int st = 0; st < 2; ++st)
+              t3[ct] = __builtin_amdgcn_mfma_f64_16x16x4f64(pa[st], kb[ct][st], t3[ct], 0, 0, 0);
+          }
+        }
+        // D entry (i, a) at lane (i & 3) * 16 + a, reg i >> 2: G^T H_dI (the camera's intrinsic columns), G^T g_d
+#pragma unroll
+        for (int r = 1; r < 4; ++r) {
+          const int i = k0 + 4 * r;
+          if (i16 < 6) {
+            if (i >= 6 && i < 6 + nin) {
+              Pi[i16 * CZ + ctab[0][cam] + i - 6] = dv[r];
+              if (!gfu) d.Hfc[((size_t)f * 6 + i16) * C + ctab[0][cam] + i - 6] = dv[r];
+            } else if (i == 15) {
+              dgv[i16] = dv[r];
             }
           }
         }
-        KB_WAVE_SYNC();
-        // A = P_v^T: lane supplies P_v[i16][k] = T1[i16][k]
-        double pa[2];
 #pragma unroll
-        for (int st = 0; st < 2; ++st) {
-          const int k = k0 + 4 * st;
-          const double v = T1[min(i16, 5) * 17 + min(k, 5)];
-          pa[st] = (k < 6 && i16 < 6) ? v : 0.0;
+        for (int r = 0; r < 2; ++r) {  // dH = P_v G: entry (a, b) at lane, reg: a = k0 + 4 r, b = i16
+          const int arow = k0 + 4 * r;
+          if (arow < 6 && i16 < 6) dHv[arow * 6 + i16] = t2[r];
         }
-        {  // dH = P_v G
-          v4d t2 = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-          for (int st = 0; st < 2; ++st) {
-            const int k = k0 + 4 * st;
-            const double gb = Gm[min(k, 5) * 6 + min(i16, 5)];
-            t2 = __builtin_amdgcn_mfma_f64_16x16x4f64(pa[st], (k < 6 && i16 < 6) ? gb : 0.0, t2, 0, 0, 0);
-          }
+        for (int ct = 0; ct < 3; ++ct) {  // P_v K_{v,j}: columns c = 6 j + b
+          const int c = 16 * ct + i16, jj = c / 6, bb = c - 6 * jj;
+          if (ct < nct && c < 6 * cam) {
 #pragma unroll
-          for (int r = 0; r < 2; ++r) {
-            const int arow = k0 + 4 * r;
-            if (arow < 6 && i16 < 6) dHv[arow * 6 + i16] = t2[r];
+            for (int r = 0; r < 2; ++r) {
+              const int arow = k0 + 4 * r;
+              if (arow < 6) Cb[(cam * (cam - 1) / 2) * 36 + jj * 36 + arow * 6 + bb] = t3[ct][r];
+            }
           }
         }
-        // P_v K_{v,j}, j < cam: columns c = 6 j + b of [K_{v,0} | K_{v,1} | ...]
-        const double* Kv = Kl + (cam * (cam - 1) / 2) * 36;
-        for (int ct = 0; 16 * ct < 6 * cam; ++ct) {
-          const int c = 16 * ct + i16, cc = min(c, 6 * cam - 1), jj = cc / 6, bb = cc - 6 * jj;
-          v4d t3 = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-          for (int st = 0; st < 2; ++st) {
-            const int k = k0 + 4 * st;
-            const double kb = Kv[jj * 36 + min(k, 5) * 6 + bb];
-            t3 = __builtin_amdgcn_mfma_f64_16x16x4f64(pa[st], (k < 6 && c < 6 * cam) ? kb : 0.0, t3, 0, 0, 0);
-          }
-#pragma unroll
-          for (int r = 0; r < 2; ++r) {
-            const int arow = k0 + 4 * r;
-            if (arow < 6 && c < 6 * cam) Cb[(cam * (cam - 1) / 2) * 36 + jj * 36 + arow * 6 + bb] = t3[r];
-          }
-        }
+        if (stv) KB_TSB(d, sto + 8);
       }
       __syncthreads();
     }
@@ -1504,7 +1542,7 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
         int lane = threadIdx.x & 63;
         asm volatile("" : "+v"(lane));
         if (fw == 0 && it <= 8) KB_TSB(d, 20 + 4 * (it - 1));
-        const bool ok = frame_ldl(d, f, Fh, lam2, P, Q, CZ, lane, fw == 0);
+        const bool ok = frame_ldl(d, f, Fh, lam2, P, Q, CZ, lane, fw == 0, fw == 0 && it == 3);
         if (!ok && lane == 0) okl = 0;
         KB_WAVE_SYNC();
         if (fw == 0 && it <= 8) KB_TSB(d, 22 + 4 * (it - 1));
@@ -1612,6 +1650,53 @@ __global__ void __launch_bounds__(256) k_colsum(KbDev d, int gate) {
       v = (d.gn_fused && e - d.Wp == d.rank) ? fmax(fmax(part[0][l], part[1][l]), fmax(part[2][l], part[3][l]))
                                              : 0.0;
     d.part8[(size_t)ry * d.Wtot + e] = v;
+  }
+}
+
+// k_colsum1: the column sums of the block partials in one pass, into part8 row 0 (the C > 64 path, whose consumer
+// k_colimg then reads one row instead of kColsumRows): block bx sums 64 columns with 16 waves, wave w the rows
+// b = w (mod 16) (all of a wave's row loads in flight at once for nblk <= 16 x 24), then the 16 wave sums in fixed
+// order.  max for the max|dx_f| columns, as k_colsum.
+constexpr int kColsum1Waves = 16;
+__global__ void __launch_bounds__(64 * kColsum1Waves) k_colsum1(KbDev d, int gate) {
+  KbCtrl* c = d.ctrl;
+  __shared__ double part[kColsum1Waves][64];
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int e = blockIdx.x * 64 + l;
+  const bool mx = e >= d.Wp;
+  const int ec = min(e, d.Wp);
+  constexpr int U = 24;
+  const int done = c->done;
+  double v[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) v[u] = d.part[(size_t)min(w + u * kColsum1Waves, d.nblk - 1) * d.Wr + ec];
+#pragma unroll
+  for (int u = 0; u < U; ++u) KB_KEEP(v[u]);
+  if (gate && done) return;
+  double s = 0.0;
+  for (int b0 = w; b0 < d.nblk; b0 += U * kColsum1Waves) {
+    if (b0 != w) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = d.part[(size_t)min(b0 + u * kColsum1Waves, d.nblk - 1) * d.Wr + ec];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const double x = (b0 + u * kColsum1Waves < d.nblk) ? v[u] : 0.0;
+      s = mx ? fmax(s, x) : s + x;
+    }
+  }
+  part[w][l] = s;
+  __syncthreads();
+  if (w == 0 && e < d.Wtot) {
+    double t = 0.0, m = 0.0;
+#pragma unroll
+    for (int q = 0; q < kColsum1Waves; ++q) {
+      t += part[q][l];
+      m = fmax(m, part[q][l]);
+    }
+    // one max column per rank: this rank's max in its own column (GN fused passes), zero elsewhere
+    if (mx) t = (d.gn_fused && e - d.Wp == d.rank) ? m : 0.0;
+    d.part8[e] = t;
   }
 }
 
@@ -3098,6 +3183,7 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update, int nth) {
 // CM > 0: 4 waves (one factors); CM == 0: 8 waves
 template <int CM>
 __global__ void __launch_bounds__(CM == 0 ? 512 : 256) k_solve(KbDev d, int gate, int do_update) {
+  if constexpr (CM == 0) KB_MFMA_AGPR();
   solve_body<CM>(d, gate, do_update, blockDim.x);  // returns early once ctrl->done (after its staging loads)
 }
 

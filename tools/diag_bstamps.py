@@ -15,8 +15,8 @@ cfg = int(sys.argv[1]) if len(sys.argv) > 1 else 4
 p = synth.make_config(cfg)
 g = capi.Solver(p)
 g.set_state(p.state_init)
-buf = (C.c_longlong * 128)()
-assert L.kb_diag_read_ts(g.h, buf, 128) == 0  # allocates the stamp buffer
+buf = (C.c_longlong * 256)()
+assert L.kb_diag_read_ts(g.h, buf, 256) == 0  # allocates the stamp buffer
 names = {0: "entry", 1: "prologue barrier", 63: "end"}
 for it in range(8):
     names[2 + 2 * it] = f"view it{it} start"
@@ -26,10 +26,21 @@ for it in range(8):
     names[22 + 4 * it] = f"  frame f{it} GJ done"
     names[23 + 4 * it] = f"  frame f{it} Schur done"
     names[52 + it] = f"view phase A of f{it} start"
+for w, o in (("wave 0", 130), ("last view wave", 160)):
+    for ps in range(2):
+        names[o + 4 * ps] = f"  [{w}] f2 pass {ps} start"
+        names[o + 4 * ps + 1] = f"  [{w}] f2 pass {ps} projected"
+        names[o + 4 * ps + 2] = f"  [{w}] f2 pass {ps} u MFMAs done"
+        names[o + 4 * ps + 3] = f"  [{w}] f2 pass {ps} v MFMAs done"
+    names[o + 8] = f"  [{w}] f2 expansion done"
+names[140] = "    [fw0] f2 elimination entry"
+names[141] = "    [fw0] f2 6x6 LDL^T done"
+names[142] = "    [fw0] f2 column slot 0 solved+stored"
+names[143] = "    [fw0] f2 column slot 1 solved+stored"
 for rep in range(2):
     g.set_state(p.state_init)
     g.run_gn(16)
-    assert L.kb_diag_read_ts(g.h, buf, 128) == 0
+    assert L.kb_diag_read_ts(g.h, buf, 256) == 0
     t0 = buf[64]
     order = sorted((buf[64 + i] - t0, i) for i in names if buf[64 + i] >= t0 and buf[64 + i] - t0 < 10_000_000)
     print(f"k_buildp block 0 timeline (rep {rep}, us from entry):\n" +
