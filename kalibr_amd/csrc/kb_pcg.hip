@@ -109,19 +109,56 @@ __device__ __forceinline__ double pcg_block_sum(double v, double* red) {
   return s;
 }
 
-// sum over blocks of part[b * stride + col] in fixed order (4 interleaved accumulators, 16 loads in flight)
-__device__ __forceinline__ double pcg_sum_blocks(const double* part, int stride, int col, int nblk) {
-  double a[4] = {0.0, 0.0, 0.0, 0.0};
-  int b = 0;
-  for (; b + 16 <= nblk; b += 16) {
-    double v[16];
+// sum of part[0 .. nblk) by one wave in a fixed order: kPcgRU loads per lane in flight per round, then the DPP tree
+__device__ __forceinline__ double pcg_sum_vec(const double* part, int nblk, int lane) {
+  double a = 0.0;
+  for (int b0 = 0; b0 < nblk; b0 += 256) {
+    double v[4];
 #pragma unroll
-    for (int u = 0; u < 16; ++u) v[u] = ld_part(part + (size_t)(b + u) * stride + col);
+    for (int u = 0; u < 4; ++u) v[u] = ld_part(part + min(b0 + lane + 64 * u, nblk - 1));
 #pragma unroll
-    for (int u = 0; u < 16; ++u) a[u & 3] += v[u];
+    for (int u = 0; u < 4; ++u) a += (b0 + lane + 64 * u < nblk) ? v[u] : 0.0;
   }
-  for (; b < nblk; ++b) a[b & 3] += ld_part(part + (size_t)b * stride + col);
-  return (a[0] + a[1]) + (a[2] + a[3]);
+  return wave_sum_d(a);
+}
+
+// out[p] = sum_b part[b * stride + p] for p < ncol - 1 and *last = the sum of column ncol - 1, every column in the
+// same fixed order (lane-strided partial sums over the blocks, then the wave's DPP tree).  A wave takes kPcgCB
+// columns at a time with all their loads in flight (kPcgRU per lane and column), so the ~27 k cross-block partials
+// of an 8-camera rig arrive in a couple of memory round trips instead of nblk / 16 dependent rounds of one thread
+// per column.
+constexpr int kPcgCB = 14, kPcgRU = 4;
+__device__ __forceinline__ void pcg_sum_columns(const double* part, int stride, int ncol, int nblk, double* out,
+                                                double* last) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+  for (int p0 = wave * kPcgCB; p0 < ncol; p0 += nw * kPcgCB) {
+    double acc[kPcgCB];
+#pragma unroll
+    for (int c = 0; c < kPcgCB; ++c) acc[c] = 0.0;
+    for (int b0 = 0; b0 < nblk; b0 += 64 * kPcgRU) {
+      double v[kPcgCB][kPcgRU];
+#pragma unroll
+      for (int c = 0; c < kPcgCB; ++c)
+#pragma unroll
+        for (int u = 0; u < kPcgRU; ++u) {
+          const int b = min(b0 + lane + 64 * u, nblk - 1), p = min(p0 + c, ncol - 1);
+          v[c][u] = ld_part(part + (size_t)b * stride + p);
+        }
+#pragma unroll
+      for (int c = 0; c < kPcgCB; ++c)
+#pragma unroll
+        for (int u = 0; u < kPcgRU; ++u) acc[c] += (b0 + lane + 64 * u < nblk) ? v[c][u] : 0.0;
+    }
+#pragma unroll
+    for (int c = 0; c < kPcgCB; ++c) {
+      const double s = wave_sum_d(acc[c]);
+      const int p = p0 + c;
+      if (lane == 0 && p < ncol) {
+        if (p < ncol - 1) out[p] = s;
+        else *last = s;
+      }
+    }
+  }
 }
 
 __global__ void __launch_bounds__(kPcgThreads) k_pcg(KbDev d, KbPcg P) {
@@ -229,8 +266,7 @@ __global__ void __launch_bounds__(kPcgThreads) k_pcg(KbDev d, KbPcg P) {
     // dn = sum_b (r_f.s_f)_b + r_c.s_c, fixed order in every block
     double v = 0.0;
     if (tid < 64) {
-      for (int q = tid; q < nblk; q += 64) v += ld_part(P.part2 + q);
-      v = wave_sum_d(v);
+      v = pcg_sum_vec(P.part2, nblk, tid);
       double c = 0.0;
       for (int p = tid; p < C; p += 64) c += rc[p] * sc[p];
       c = wave_sum_d(c);
@@ -288,11 +324,7 @@ __global__ void __launch_bounds__(kPcgThreads) k_pcg(KbDev d, KbPcg P) {
       if (tid == 0) P.part[(size_t)b * CP + C] = ok ? dq_part : NAN;  // a failed block poisons d.q
       if (!pcg_barrier(P.bar, nblk, ++nbar, &flag)) goto timeout;
       // ---- phase B: q_c, alpha, updates, s = M^-1 r, partial r_f.s_f
-      for (int p = tid; p < C + 1; p += blockDim.x) {
-        const double v = pcg_sum_blocks(P.part, CP, p, nblk);
-        if (p < C) qc[p] = v;
-        else sh_scalar[2] = v;
-      }
+      pcg_sum_columns(P.part, CP, C + 1, nblk, qc, &sh_scalar[2]);
       __syncthreads();
       if (tid < 64) {
         double c = 0.0;
@@ -328,8 +360,7 @@ __global__ void __launch_bounds__(kPcgThreads) k_pcg(KbDev d, KbPcg P) {
       // ---- phase C: dn', beta, d = s + beta d
       if (tid < 64) {
         double v = 0.0;
-        for (int q = tid; q < nblk; q += 64) v += ld_part(P.part2 + q);
-        v = wave_sum_d(v);
+        v = pcg_sum_vec(P.part2, nblk, tid);
         double c = 0.0;
         for (int p = tid; p < C; p += 64) c += rc[p] * sc[p];
         c = wave_sum_d(c);

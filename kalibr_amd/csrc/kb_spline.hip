@@ -31,9 +31,17 @@
   do {                              \
     if (d.dbg_stop == (i)) return;  \
   } while (0)
+// timeline stamp (100 MHz s_memrealtime) of thread 0 of block 0 at slot i (tools/diag_sp_ts.py)
+#define KSP_TS(i)                                                                                          \
+  do {                                                                                                     \
+    if (blockIdx.x == 0 && threadIdx.x == 0 && d.dbg_ts && (i) < 256) d.dbg_ts[i] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
 #else
 #define KSP_STOP(i) \
   do {              \
+  } while (0)
+#define KSP_TS(i) \
+  do {            \
   } while (0)
 #endif
 
@@ -101,6 +109,7 @@ struct SpDev {
   const double* QD;       // [n][324] Q blocks within node i
   const double* QU;       // [n][324] Q block node i (rows) -> node i + 1 (columns)
   double* mcost;          // [n] per-node motion cost at the build state
+  long long* dbg_ts;      // diagnostics only: [256] KSP_TS stamps
   int dbg_stop;           // diagnostics only (KSP_DBG_STOP): 0, or the phase after which the timed kernels return
   int zero_lam;           // GN pass: k_sp_imu_cc sets lambda^2 = 0 (no separate launch)
 };
@@ -1009,6 +1018,25 @@ __device__ __forceinline__ void node_forward(const double* L, const double* id, 
   }
 }
 
+// node_forward with the L loads kept per row (a compiler barrier between rows): the kernels that keep the next
+// node's operands in registers across the solve cannot hold all 171 hoisted L entries as well
+__device__ __forceinline__ void node_forward_lean(const double* L, const double* id, const double* W, int ws,
+                                                  int ncol, double* dst, int ds, int tid) {
+  for (int c = tid; c < ncol; c += blockDim.x) {
+    double z[NB];
+#pragma unroll
+    for (int row = 0; row < NB; ++row) {
+      asm volatile("" ::: "memory");
+      double v = W[row * ws + c];
+#pragma unroll
+      for (int k = 0; k < row; ++k) v -= L[row * NB + k] * z[k];
+      z[row] = v * id[row];
+    }
+#pragma unroll
+    for (int row = 0; row < NB; ++row) dst[row * ds + c] = z[row];
+  }
+}
+
 // back substitution of one 18-row node with LDS-staged operands: x = L^-T T (T row stride ts), one thread per
 // RHS column, written to out (row stride m)
 __device__ __forceinline__ void node_backsolve(const double* L, const double* id, const double* T, int ts, int m,
@@ -1258,6 +1286,300 @@ __global__ void __launch_bounds__(256) k_sp_back(SpDev d, int s) {
   __syncthreads();
   KSP_STOP(2);
   node_backsolve(L, id, T, m, m, d.X + (size_t)j * NB * m, tid);
+}
+
+// ---------------------------------------------------------------- partitioned band solve (default)
+// The block-tridiagonal coefficient system solved by nested partitioning instead of cyclic reduction: the nodes of
+// a level are cut into chunks of q consecutive nodes whose last node is the chunk's separator.  One block per chunk
+// eliminates the chunk's interior nodes in order (block Thomas: Cholesky of the node, Z = L^-1 [U_j | F_j | R_j],
+// the next node's D, its fill coupling F to the left separator and its right-hand side updated by Z_U^T Z), which
+// leaves a block-tridiagonal system over the separators (level l + 1: P = ceil(n / q) nodes).  The levels repeat
+// until at most kSpTop nodes remain; one block solves that system by the same elimination and a back-substitution
+// sweep, and the back kernels walk the levels down again (x_j = L_j^-T (Z_R - Z_U x_{j+1} - Z_F x_sepL)).
+//   configs[4]: n = 1001 -> 63 (q = 16) -> 8 (q = 8) -> top: 5 launches whose dependent chain is 15 + 7 + 8
+//   eliminations and 8 + 7 + 15 substitution steps, instead of 21 launches of one cyclic-reduction level each.
+// Level l's system: D_i = Dt_i + Dh_i (the separator's own chunk / the next chunk's elimination; Dh of the last
+// node is absent), U_i (block (i, i + 1)), R_i = Rt_i + Rh_i.  Level 0 reads the built blocks D0 + lambda^2 I, U0, R0.
+constexpr int kSpTop = 16;  // largest system the one-block top kernel solves
+constexpr int kSpWc = 36 + MAXC + 1;  // LDS row stride of [U | F | R] (m <= MAXC + 1)
+
+struct SpLvl {
+  int n, q, lvl;                          // nodes, chunk length (interior nodes + the separator), level
+  const double *Dt, *Dh, *U, *Rt, *Rh;    // this level's system (lvl 0: D0, -, U0, R0, -)
+  double *Lf, *Lid, *Z, *X;               // factors [n][324], [n][18], [n][18][36 + m]; solution [n][18][m]
+  double *nDt, *nDh, *nU, *nRt, *nRh;     // chunk kernel: the next level's system
+  const double* Xup;                      // back kernel: the next level's solution
+};
+
+// raw entry e of node i's [D (324) | U (324) | R (18 m)] at level L
+__device__ __forceinline__ double lvl_raw(const SpDev& d, const SpLvl& L, int i, int e, double lam2) {
+  const int m = d.m;
+  const bool nx = i + 1 < L.n;
+  if (e < NB * NB) {
+    const size_t o = (size_t)i * NB * NB + e;
+    return L.lvl == 0 ? L.Dt[o] + lam_diag(d, i, e, lam2) : L.Dt[o] + (nx ? L.Dh[o] : 0.0);
+  }
+  if (e < 2 * NB * NB) return L.U[(size_t)i * NB * NB + e - NB * NB];
+  const size_t o = (size_t)i * NB * m + e - 2 * NB * NB;
+  return L.lvl == 0 ? L.Rt[o] : L.Rt[o] + (nx ? L.Rh[o] : 0.0);
+}
+
+constexpr int kSpRawU = (2 * NB * NB + NB * (MAXC + 1) + 255) / 256;  // raw items per thread (256 threads)
+
+// the node update of chunk_forward on f64 MFMA tiles (see there); U tiles: rows = the 18 Z_U columns, columns =
+// [U | F | R] (D~, F, R~ of the next node); F tiles (hasL): rows = the Z_F columns, columns = [F | R] (Dh, Rh)
+__device__ __forceinline__ void chunk_update_mfma(const double* Zs, int wc, int m, const double* Raw, double* Lc,
+                                                  double* W, double* Dh, double* Rh, bool hasL, int tid) {
+  const int wave = tid >> 6, lane = tid & 63, li = lane & 15, kq = lane >> 4;
+  const int nct_u = (36 + m + 15) >> 4, nct_f = (NB + m + 15) >> 4;
+  const int nt_u = 2 * nct_u, nt = nt_u + (hasL ? 2 * nct_f : 0);
+  for (int t = wave; t < nt; t += 4) {
+    const bool fu = t >= nt_u;
+    const int tt = fu ? t - nt_u : t, nct = fu ? nct_f : nct_u;
+    const int ti = tt / nct, tj = tt - ti * nct;
+    const int ca = fu ? NB : 0, ncb = fu ? NB + m : 36 + m;
+    const int arc = min(16 * ti + li, NB - 1), bcc = min(16 * tj + li, ncb - 1);
+    v4d_t acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int st = 0; st < 5; ++st) {
+      const int k = 4 * st + kq, kc = min(k, NB - 1);
+      const double av = Zs[kc * wc + ca + arc], bv = Zs[kc * wc + ca + bcc];
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(k < NB ? av : 0.0, bv, acc, 0, 0, 0);
+    }
+    const int c = 16 * tj + li;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int a = 16 * ti + kq + 4 * r;
+      if (a < NB && c < ncb) {
+        const double val = acc[r];
+        if (!fu) {
+          if (c < NB) Lc[a * NB + c] = Raw[a * NB + c] - val;
+          else if (c < 2 * NB) W[a * wc + c] = -val;
+          else W[a * wc + c] = Raw[2 * NB * NB + a * m + c - 2 * NB] - val;
+        } else {
+          if (c < NB) Dh[a * NB + c] -= val;
+          else Rh[a * m + c - NB] -= val;
+        }
+      }
+    }
+  }
+  for (int q = tid; q < NB * NB; q += 256) W[(q / NB) * wc + q % NB] = Raw[NB * NB + q];  // U of node j + 1: raw
+}
+
+// forward elimination of nodes a .. e - 1 of one chunk (e = its separator; sepL = a - 1 when hasL) by one 256-thread
+// block.  On return Lc holds D~_e (whole), W = [U_e raw | F_e | R~_e], Dh / Rh the left separator's accumulated
+// updates (hasL).  Writes L_j, 1/diag, Z_j of every interior node.  Returns false if a node block is not PD.
+__device__ bool chunk_forward(const SpDev& d, const SpLvl& L, int a, int e, bool hasL, double lam2, double* Lc,
+                              double* idc, double* W, double* Zs, double* Dh, double* Rh, double* Raw) {
+  const int tid = threadIdx.x, m = d.m, wc = 36 + m, nraw = 2 * NB * NB + NB * m;
+  bool ok = true;
+  // node a: D -> Lc, U -> W[:, 0:18], U_{a-1}^T -> W[:, 18:36] (block (a, a-1)), R -> W[:, 36:]
+  double v[kSpRawU];
+#pragma unroll
+  for (int u = 0; u < kSpRawU; ++u) v[u] = lvl_raw(d, L, a, min(tid + 256 * u, nraw - 1), lam2);
+  double fl[2];
+  const int ua = hasL ? a - 1 : a;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int q = min(tid + 256 * u, NB * NB - 1), r = q / NB, c = q % NB;
+    fl[u] = L.U[(size_t)ua * NB * NB + c * NB + r];
+  }
+#pragma unroll
+  for (int u = 0; u < kSpRawU; ++u) {
+    const int q = tid + 256 * u;
+    if (q < NB * NB) Lc[q] = v[u];
+    else if (q < 2 * NB * NB) W[((q - NB * NB) / NB) * wc + (q - NB * NB) % NB] = v[u];
+    else if (q < nraw) W[((q - 2 * NB * NB) / m) * wc + 36 + (q - 2 * NB * NB) % m] = v[u];
+  }
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int q = tid + 256 * u;
+    if (q < NB * NB) W[(q / NB) * wc + NB + q % NB] = hasL ? fl[u] : 0.0;
+  }
+  for (int q = tid; q < NB * NB + NB * m; q += 256) {
+    if (q < NB * NB) Dh[q] = 0.0;
+    else Rh[q - NB * NB] = 0.0;
+  }
+  // node a + 1's raw blocks in flight
+#pragma unroll
+  for (int u = 0; u < kSpRawU; ++u) v[u] = lvl_raw(d, L, min(a + 1, e), min(tid + 256 * u, nraw - 1), lam2);
+  KSP_TS(100 + L.lvl);
+  for (int j = a; j < e; ++j) {
+    __syncthreads();  // Lc, W of node j complete; the previous update's Raw reads done
+    const int ts = 4 * (j - a) + 64 * L.lvl;
+    if (j - a < 12) KSP_TS(ts);
+    // node j + 1's raw blocks to LDS (their loads went out during the previous step): no registers held across the
+    // factorisation and the forward solve
+#pragma unroll
+    for (int u = 0; u < kSpRawU; ++u)
+      if (tid + 256 * u < nraw) Raw[tid + 256 * u] = v[u];
+    if (tid < 64) {
+      const bool okj = chol18_wave(Lc, idc, tid);
+      ok = ok && okj;
+    }
+    __syncthreads();
+    if (j - a < 12) KSP_TS(ts + 1);
+    node_forward_lean(Lc, idc, W, wc, wc, Zs, wc, tid);  // Z = L^-1 [U | F | R]
+    double* Lg = L.Lf + (size_t)j * NB * NB;
+    for (int q = tid; q < NB * NB; q += 256) Lg[q] = Lc[q];
+    if (tid < NB) L.Lid[(size_t)j * NB + tid] = idc[tid];
+    __syncthreads();  // Zs complete; Lc, W free
+    if (j - a < 12) KSP_TS(ts + 2);
+    // node j + 2's raw blocks in flight while node j + 1's are consumed
+    const int jn = min(j + 2, e);
+#pragma unroll
+    for (int u = 0; u < kSpRawU; ++u) v[u] = lvl_raw(d, L, jn, min(tid + 256 * u, nraw - 1), lam2);
+    double* Zg = L.Z + (size_t)j * NB * wc;
+    for (int q = tid; q < NB * wc; q += 256) Zg[q] = Zs[q];
+    // node j + 1: D~ = D - Z_U^T Z_U -> Lc, W = [U raw | -Z_U^T Z_F | R - Z_U^T Z_R]; the left separator (hasL):
+    // Dh -= Z_F^T Z_F, Rh -= Z_F^T Z_R.  The Z^T products on f64 MFMA tiles (out[a][c] = sum_k Zs[k][ca + a]
+    // Zs[k][cb + c], k < 18 in 5 steps of 4), tiles dealt round-robin to the 4 waves
+    chunk_update_mfma(Zs, wc, m, Raw, Lc, W, Dh, Rh, hasL, tid);
+    if (j - a < 12) KSP_TS(ts + 3);
+  }
+  if (a == e) {  // no interior node: the separator's raw blocks
+#pragma unroll
+    for (int u = 0; u < kSpRawU; ++u) {
+      const int q = tid + 256 * u;
+      if (q < NB * NB) Lc[q] = v[u];
+      else if (q < 2 * NB * NB) W[((q - NB * NB) / NB) * wc + (q - NB * NB) % NB] = v[u];
+      else if (q < nraw) W[((q - 2 * NB * NB) / m) * wc + 36 + (q - 2 * NB * NB) % m] = v[u];
+    }
+  }
+  __syncthreads();
+  return ok;
+}
+
+// one block per chunk of level L: eliminate the interior, write the separators' system for level L + 1
+__global__ void __launch_bounds__(256) k_sp_chunk(SpDev d, SpLvl L) {
+  __shared__ double Lc[NB * NB], idc[NB], Dh[NB * NB];
+  __shared__ __attribute__((aligned(16))) double W[NB * kSpWc], Zs[NB * kSpWc], Rh[NB * (MAXC + 1)],
+      Raw[2 * NB * NB + NB * (MAXC + 1)];
+  const int p = blockIdx.x, tid = threadIdx.x, m = d.m, wc = 36 + m;
+  const int a = p * L.q, e = min(L.n, a + L.q) - 1;
+  const bool hasL = p > 0;
+  const double lam2 = L.lvl == 0 ? d.sc[SC_LAM2] : 0.0;
+  const bool ok = chunk_forward(d, L, a, e, hasL, lam2, Lc, idc, W, Zs, Dh, Rh, Raw);
+  if (tid == 0 && !ok) d.sc[SC_OK] = 0.0;
+  // separator p of level L + 1: Dt = D~_e, Rt = R~_e; the left separator: U_{p-1} = F_e^T, Dh_{p-1}, Rh_{p-1}
+  for (int q = tid; q < NB * NB; q += 256) {
+    L.nDt[(size_t)p * NB * NB + q] = Lc[q];
+    if (hasL) {
+      const int r = q / NB, c = q % NB;
+      L.nU[(size_t)(p - 1) * NB * NB + q] = W[c * wc + NB + r];
+      L.nDh[(size_t)(p - 1) * NB * NB + q] = Dh[q];
+    }
+  }
+  for (int q = tid; q < NB * m; q += 256) {
+    L.nRt[(size_t)p * NB * m + q] = W[(q / m) * wc + 36 + q % m];
+    if (hasL) L.nRh[(size_t)(p - 1) * NB * m + q] = Rh[q];
+  }
+}
+
+// x_j = L_j^-T (Z_R - Z_U x_{j+1} - Z_F xl) for j = e - 1 down to a, x_e given (LDS xs); the node operands of the
+// next step in flight during each step.  X rows [18][m] of each node written to L.X.
+__device__ void chunk_back(const SpDev& d, const SpLvl& L, int a, int e, bool hasL, double* Ls, double* ids,
+                           double* Zs, double* xs, double* xl, double* T) {
+  const int tid = threadIdx.x, m = d.m, wc = 36 + m, nop = NB * NB + NB + NB * wc;
+  constexpr int U = (NB * NB + NB + NB * kSpWc + 255) / 256;
+  double v[U];
+  auto load = [&](int j) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int q = min(tid + 256 * u, nop - 1);
+      v[u] = q < NB * NB ? L.Lf[(size_t)j * NB * NB + q]
+             : q < NB * NB + NB ? L.Lid[(size_t)j * NB + q - NB * NB]
+                                : L.Z[(size_t)j * NB * wc + q - NB * NB - NB];
+    }
+  };
+  if (e > a) load(e - 1);
+  KSP_TS(104 + L.lvl);
+  for (int j = e - 1; j >= a; --j) {
+    __syncthreads();  // xs = x_{j+1} complete; the previous step's Ls / Zs reads done
+    const int tb = 200 + 3 * (e - 1 - j);
+    if (L.lvl == 0 && e - 1 - j < 12) KSP_TS(tb);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int q = tid + 256 * u;
+      if (q < NB * NB) Ls[q] = v[u];
+      else if (q < NB * NB + NB) ids[q - NB * NB] = v[u];
+      else if (q < nop) Zs[q - NB * NB - NB] = v[u];
+    }
+    if (j > a) load(j - 1);
+    __syncthreads();
+    {
+      // T = Z_R - [Z_U | Z_F] [x_{j+1}; xl] on f64 MFMA tiles (K = 18, or 36 with the left separator)
+      const int wave = tid >> 6, lane = tid & 63, li = lane & 15, kq = lane >> 4, nct = (m + 15) >> 4;
+      const int nst = hasL ? 9 : 5;
+      for (int t = wave; t < 2 * nct; t += 4) {
+        const int ti = t / nct, tj = t - ti * nct;
+        const int arc = min(16 * ti + li, NB - 1), bcc = min(16 * tj + li, m - 1);
+        v4d_t acc = {0.0, 0.0, 0.0, 0.0};
+        for (int st = 0; st < nst; ++st) {
+          const int k = 4 * st + kq;
+          const bool kv = hasL ? k < 2 * NB : k < NB;
+          const int kc = min(k, 2 * NB - 1);
+          const double av = Zs[arc * wc + kc];
+          const double bv = kc < NB ? xs[kc * m + bcc] : xl[(kc - NB) * m + bcc];
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(kv ? av : 0.0, bv, acc, 0, 0, 0);
+        }
+        const int c = 16 * tj + li;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int a = 16 * ti + kq + 4 * r;
+          if (a < NB && c < m) T[a * m + c] = Zs[a * wc + 36 + c] - acc[r];
+        }
+      }
+    }
+    __syncthreads();
+    if (L.lvl == 0 && e - 1 - j < 12) KSP_TS(tb + 1);
+    node_backsolve(Ls, ids, T, m, m, xs, tid);  // x_j replaces x_{j+1}
+    __syncthreads();
+    if (L.lvl == 0 && e - 1 - j < 12) KSP_TS(tb + 2);
+    double* Xg = L.X + (size_t)j * NB * m;
+    for (int q = tid; q < NB * m; q += 256) Xg[q] = xs[q];
+  }
+}
+
+// one block: the whole top-level system (n <= kSpTop) by elimination, the last node's solve and back-substitution
+__global__ void __launch_bounds__(256) k_sp_ctop(SpDev d, SpLvl L) {
+  __shared__ double Lc[NB * NB], idc[NB], Dh[NB * NB];
+  __shared__ __attribute__((aligned(16))) double W[NB * kSpWc], Zs[NB * kSpWc], Rh[NB * (MAXC + 1)],
+      Raw[2 * NB * NB + NB * (MAXC + 1)];
+  double* T = Raw;  // the back-substitution's T (Raw is free once the elimination is done)
+  const int tid = threadIdx.x, m = d.m, wc = 36 + m, e = L.n - 1;
+  const double lam2 = L.lvl == 0 ? d.sc[SC_LAM2] : 0.0;
+  bool ok = chunk_forward(d, L, 0, e, false, lam2, Lc, idc, W, Zs, Dh, Rh, Raw);
+  if (tid < 64) {
+    const bool okj = chol18_wave(Lc, idc, tid);
+    ok = ok && okj;
+  }
+  if (tid == 0 && !ok) d.sc[SC_OK] = 0.0;
+  __syncthreads();
+  // x_e = L^-T L^-1 R~_e (forward in place in W's R columns, backward into Rh as the x_{j+1} buffer)
+  node_forward_lean(Lc, idc, W + 36, wc, m, W + 36, wc, tid);
+  __syncthreads();
+  node_backsolve(Lc, idc, W + 36, wc, m, Rh, tid);
+  __syncthreads();
+  for (int q = tid; q < NB * m; q += 256) L.X[(size_t)e * NB * m + q] = Rh[q];
+  chunk_back(d, L, 0, e, false, Lc, idc, Zs, Rh, W, T);
+}
+
+// one block per chunk of level L: x of the separator and the left separator from level L + 1, then the interior
+__global__ void __launch_bounds__(256) k_sp_cback(SpDev d, SpLvl L) {
+  __shared__ double Ls[NB * NB], ids[NB];
+  __shared__ __attribute__((aligned(16))) double Zs[NB * kSpWc], xs[NB * (MAXC + 1)], xl[NB * (MAXC + 1)],
+      T[NB * (MAXC + 1)];
+  const int p = blockIdx.x, tid = threadIdx.x, m = d.m;
+  const int a = p * L.q, e = min(L.n, a + L.q) - 1;
+  const bool hasL = p > 0;
+  for (int q = tid; q < NB * m; q += 256) {
+    const double x = L.Xup[(size_t)p * NB * m + q];
+    xs[q] = x;
+    L.X[(size_t)e * NB * m + q] = x;
+    xl[q] = hasL ? L.Xup[(size_t)(p - 1) * NB * m + q] : 0.0;
+  }
+  chunk_back(d, L, a, e, hasL, Ls, ids, Zs, xs, xl, T);
 }
 
 // ---------------------------------------------------------------- Schur complement onto theta
@@ -1741,6 +2063,8 @@ struct kb_sp_handle {
   const void* fn_camsolve = nullptr;
   hipGraphExec_t gn_graph = nullptr;
   int gn_graph_n = 0;
+  std::vector<SpLvl> lv;  // partitioned band solve: lv[0 .. nl) chunk levels, lv[nl] the top system
+  bool use_cr = true;     // block cyclic reduction; KSP_PARTITION=1: the partitioned band solve
   std::vector<double> trace;
   double* host_sc = nullptr;  // pinned scalars
 
@@ -1777,6 +2101,19 @@ int launch_build(kb_sp_handle* h) {
 
 int launch_reduction(kb_sp_handle* h) {
   SpDev& d = h->d;
+  if (!h->use_cr) {  // partitioned: chunk levels down, the top system, back-substitution levels up
+    const int nl = (int)h->lv.size() - 1;
+    for (int l = 0; l < nl; ++l) {
+      const SpLvl& L = h->lv[l];
+      hipLaunchKernelGGL(k_sp_chunk, dim3((L.n + L.q - 1) / L.q), dim3(256), 0, h->stream, d, L);
+    }
+    hipLaunchKernelGGL(k_sp_ctop, dim3(1), dim3(256), 0, h->stream, d, h->lv[nl]);
+    for (int l = nl - 1; l >= 0; --l) {
+      const SpLvl& L = h->lv[l];
+      hipLaunchKernelGGL(k_sp_cback, dim3((L.n + L.q - 1) / L.q), dim3(256), 0, h->stream, d, L);
+    }
+    return 0;
+  }
   if (d.n == 1) {
     hipLaunchKernelGGL(k_sp_top, dim3(1), dim3(256), sizeof(double) * NB * d.m, h->stream, d);
     return 0;
@@ -1954,6 +2291,48 @@ kb_sp_handle* kb_sp_create(const kb_sp_layout* L) {
   rc |= h->alloc(&d.Lid, (size_t)h->n * NB);
   rc |= h->alloc(&d.Z, (size_t)h->n * NB * (36 + d.m));
   rc |= h->alloc(&d.X, (size_t)h->n * NB * d.m);
+  {
+    // partitioned band solve: level 0 is the built system; chunks of 16 nodes, then 8, until <= kSpTop remain
+    const char* ev = std::getenv("KSP_PARTITION");
+    h->use_cr = !(ev && std::atoi(ev) != 0);
+    SpLvl L0{};
+    L0.n = h->n;
+    L0.Dt = d.D0;
+    L0.U = d.U0;
+    L0.Rt = d.R0;
+    L0.Lf = d.Lf;
+    L0.Lid = d.Lid;
+    L0.Z = d.Z;
+    L0.X = d.X;
+    h->lv.push_back(L0);
+    while (h->lv.back().n > kSpTop) {
+      SpLvl& Lc = h->lv.back();
+      Lc.q = Lc.lvl == 0 ? 16 : 8;
+      SpLvl Ln{};
+      Ln.lvl = Lc.lvl + 1;
+      Ln.n = (Lc.n + Lc.q - 1) / Lc.q;
+      const size_t nn = (size_t)Ln.n;
+      double *Dt = nullptr, *Dh = nullptr, *U = nullptr, *Rt = nullptr, *Rh = nullptr;
+      rc |= h->alloc(&Dt, nn * NB * NB);
+      rc |= h->alloc(&Dh, nn * NB * NB);
+      rc |= h->alloc(&U, nn * NB * NB);
+      rc |= h->alloc(&Rt, nn * NB * d.m);
+      rc |= h->alloc(&Rh, nn * NB * d.m);
+      rc |= h->alloc(&Ln.Lf, nn * NB * NB);
+      rc |= h->alloc(&Ln.Lid, nn * NB);
+      rc |= h->alloc(&Ln.Z, nn * NB * (36 + d.m));
+      rc |= h->alloc(&Ln.X, nn * NB * d.m);
+      Ln.Dt = Lc.nDt = Dt;
+      Ln.Dh = Lc.nDh = Dh;
+      Ln.U = Lc.nU = U;
+      Ln.Rt = Lc.nRt = Rt;
+      Ln.Rh = Lc.nRh = Rh;
+      Lc.Xup = Ln.X;
+      if (rc) break;
+      h->lv.push_back(Ln);
+    }
+    h->lv.back().q = h->lv.back().n;
+  }
   d.nblk_s = (h->n + NPB - 1) / NPB;
   rc |= h->alloc(&d.spart, (size_t)d.nblk_s * d.Ws);
   rc |= h->alloc(&d.dx, (size_t)h->ncols);
@@ -2103,6 +2482,7 @@ int kb_sp_upload(kb_sp_handle* h, int32_t n_frames, const double* frame_time, in
   d.nblk_q = (h->n + 63) / 64;
 #ifdef KB_STAMPS
   if (const char* e = std::getenv("KSP_DBG_STOP")) d.dbg_stop = std::atoi(e);  // diagnostic build only
+  if (!d.dbg_ts) rc |= h->alloc(&d.dbg_ts, 256);
 #endif
   rc |= h->alloc(&d.cpart, (size_t)(d.nblk_f + d.nblk_ci + d.nblk_q));
   rc |= h->alloc(&d.mcost, (size_t)h->n);
@@ -2556,3 +2936,13 @@ int kb_sp_kernel_stats(kb_sp_handle* h, int32_t n, double* ms_out6, double* fram
 }
 
 }  // extern "C"
+
+#ifdef KB_STAMPS
+// diagnostic build only: the KSP_TS timeline (100 MHz ticks) of the last pass
+extern "C" int kb_sp_diag_read_ts(kb_sp_handle* h, long long* out, int n) {
+  if (!h->d.dbg_ts) return fail("kb_sp_diag_read_ts: no stamp buffer");
+  KSP_HIP(hipStreamSynchronize(h->stream));
+  KSP_HIP(hipMemcpy(out, h->d.dbg_ts, sizeof(long long) * std::min(n, 256), hipMemcpyDeviceToHost));
+  return 0;
+}
+#endif
