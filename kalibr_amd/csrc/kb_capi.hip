@@ -774,7 +774,7 @@ static int run_pcg(kb_handle* h, int* ok) {
   const int C = h->C, F = h->F;
   if (!h->pcg_buf) {
     if (h->alloc(&h->pcg_buf, (size_t)F * (C + 1) + F + 8) || h->alloc(&h->pcg_cb, 2 * (size_t)C) ||
-        h->alloc(&h->pcg_bar, 4))
+        h->alloc(&h->pcg_bar, kPcgBarWords))
       return -1;
     std::vector<int> cb(2 * C);
     int c = 0;
@@ -823,7 +823,7 @@ static int run_pcg(kb_handle* h, int* ok) {
   P.part2 = P.part + (size_t)F * (C + 1);
   P.info = P.part2 + F;
   P.bar = h->pcg_bar;
-  KB_HIP(hipMemsetAsync(h->pcg_bar, 0, sizeof(unsigned) * 4, h->stream));
+  KB_HIP(hipMemsetAsync(h->pcg_bar, 0, sizeof(unsigned) * kPcgBarWords, h->stream));
   KB_HIP(hipMemsetAsync(P.info, 0, sizeof(double) * 8, h->stream));
   void* args[] = {(void*)&h->d, (void*)&P};
   KB_HIP(hipLaunchCooperativeKernel((const void*)k_pcg, dim3(nblk), dim3(kPcgThreads), args, (unsigned)lds,

@@ -47,12 +47,22 @@ struct KbPcg {
 // fence there (vL1D invalidate), so no stale line of a previous round survives
 __device__ __forceinline__ double ld_part(const double* p) { return *p; }
 
-// grid barrier number `k` (1, 2, ...): every block arrives once per barrier; returns false on a spin timeout
+// grid barrier number `k` (1, 2, ...), two levels: block b arrives on the counter of its group b % kPcgGroups (one
+// 128-byte line each, bar[32 (1 + g)]); the block that completes its group (fetch_add returns k * size_g - 1)
+// arrives on the top counter bar[0], and every block waits for bar[0] >= k * ngroups.  The top counter takes
+// ngroups atomics instead of nblk (one counter serialised ~250 same-address agent-scope atomics per barrier).
+// Release / acquire at agent scope on every step; bounded spin: returns false on a timeout.
+constexpr int kPcgGroups = 16;
+constexpr int kPcgBarWords = 32 * (1 + kPcgGroups);
 __device__ __forceinline__ bool pcg_barrier(unsigned* bar, unsigned nblk, unsigned k, int* lds_flag) {
   __syncthreads();
   if (threadIdx.x == 0) {
-    __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned target = k * nblk;
+    const unsigned ng = nblk < (unsigned)kPcgGroups ? nblk : (unsigned)kPcgGroups;
+    const unsigned g = blockIdx.x % ng;
+    const unsigned gsize = nblk / ng + (g < nblk % ng ? 1u : 0u);
+    const unsigned old = __hip_atomic_fetch_add(bar + 32 * (1 + g), 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (old + 1 == k * gsize) __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned target = k * ng;
     unsigned spins = 0;
     while (__hip_atomic_load(bar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) {
       __builtin_amdgcn_s_sleep(1);

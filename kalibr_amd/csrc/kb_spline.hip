@@ -980,14 +980,15 @@ __device__ bool chol18_wave(double* A, double* id, int lane) {
     rdk = rdk * fma(-0.5 * dpos * rdk, rdk, 1.5);
     rdk = rdk * fma(-0.5 * dpos * rdk, rdk, 1.5);
     const double dk = dpos * rdk;
-    // selects instead of lane-conditional blocks: no exec-mask save / restore around each update
+    // no masks on the updates: for lanes r <= k (and r < c) the update only touches the upper triangle
+    // a[c > r], which is never read (column k's entries L[c][k] come from lanes c > k) and is written back as zero
     rid = (lane == k) ? rdk : rid;
-    a[k] = (lane == k) ? dk : (lane > k) ? a[k] * rdk : a[k];
-    const double lk = (lane > k) ? a[k] : 0.0;  // rows above the pivot take no update
+    a[k] = (lane == k) ? dk : a[k] * rdk;
+    const double lk = a[k];
 #pragma unroll
     for (int c = k + 1; c < NB; ++c) {
       const double lck = rdlane(a[k], c);
-      a[c] -= ((lane >= c) ? lk : 0.0) * lck;
+      a[c] = fma(-lk, lck, a[c]);
     }
   }
   KSP_WAVE_SYNC();
