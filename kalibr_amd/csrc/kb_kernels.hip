@@ -381,49 +381,62 @@ __device__ void pass_end_block(const KbDev& d, const KbCtrl& cin, KbCtrl* out, b
 // camera chains of a state: L_i (R|t) = B_{i-1}..B_0 and K_{i,j} (one block) -> slot `slot` of camL / camK.
 // `base` points at the N-1 baseline poses (7-stride, HBM or LDS).
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ void chain_block(const KbDev& d, const double* base, int slot, int nth) {
-  // P(i, j) = B_{i-1} ... B_{j+1} for -1 <= j < i (P(i, i-1) = I): L_i = P(i, -1), K_{i,j} from P(i, j) and B_j.
-  // One thread per pair builds its product in the reference association order (Q <- B_k Q, k = j+1 .. i-1), so
-  // every chain equals the former per-entry recomputation bit for bit; the 36 entries of K_{i,j} then read it.
-  __shared__ double sR[KB_MAX_CAMS][9], st[KB_MAX_CAMS][3];  // baseline B_j
-  // pair (i, j) at i(i+1)/2 + j + 1: R (9) | t (3); C <= 111 bounds the rig to N <= 10 cameras (55 pairs)
-  __shared__ double PR[64][12];
+// P(i, j) = B_{i-1} ... B_{j+1} for -1 <= j < i (P(i, i-1) = I): L_i = P(i, -1), K_{i,j} from P(i, j) and B_j.
+// One thread per pair builds its product in the reference association order (Q <- B_k Q, k = j+1 .. i-1), so
+// every chain equals the former per-entry recomputation bit for bit; the 36 entries of K_{i,j} then read it.
+struct ChainLds {
+  double sR[KB_MAX_CAMS][9], st[KB_MAX_CAMS][3];  // baseline B_j
+  double PR[64][12];  // pair (i, j) at i(i+1)/2 + j + 1: R (9) | t (3); C <= 111 bounds the rig to N <= 10 (55 pairs)
+};
+// part 1: the baselines and the pair products (threads tx < np; WAVE: one wave alone, wave-level LDS syncs)
+template <bool WAVE>
+__device__ __forceinline__ void chain_pairs(const KbDev& d, const double* base, ChainLds& L, int tx) {
   const int N = d.N, np = N * (N + 1) / 2;
-  double* Lo = cam_L(d, slot);
-  double* Ko = cam_K(d, slot);
-  if (threadIdx.x < N - 1) pose_rt(base + 7 * threadIdx.x, sR[threadIdx.x], st[threadIdx.x]);
-  __syncthreads();
-  if (threadIdx.x < np) {
-    const int q = threadIdx.x, i = tri_row(q), j = q - i * (i + 1) / 2 - 1;
+  if (tx < N - 1) pose_rt(base + 7 * tx, L.sR[tx], L.st[tx]);
+  if (WAVE) KB_WAVE_SYNC();
+  else __syncthreads();
+  if (tx < np) {
+    const int q = tx, i = tri_row(q), j = q - i * (i + 1) / 2 - 1;
     double QR[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, Qt[3] = {0, 0, 0};
 #pragma unroll 1
     for (int k = j + 1; k < i; ++k) {
       double R2[9], t2[3];
-      rt_mul(sR[k], st[k], QR, Qt, R2, t2);
+      rt_mul(L.sR[k], L.st[k], QR, Qt, R2, t2);
 #pragma unroll
       for (int e = 0; e < 9; ++e) QR[e] = R2[e];
 #pragma unroll
       for (int e = 0; e < 3; ++e) Qt[e] = t2[e];
     }
 #pragma unroll
-    for (int e = 0; e < 9; ++e) PR[q][e] = QR[e];
+    for (int e = 0; e < 9; ++e) L.PR[q][e] = QR[e];
 #pragma unroll
-    for (int e = 0; e < 3; ++e) PR[q][9 + e] = Qt[e];
+    for (int e = 0; e < 3; ++e) L.PR[q][9 + e] = Qt[e];
   }
-  __syncthreads();
-  for (int q = threadIdx.x; q < N * 12; q += nth) {  // L_i = P(i, -1)
+}
+// part 2 (after a barrier that follows part 1): L_i and K_{i,j} into slot `slot`
+__device__ __forceinline__ void chain_write(const KbDev& d, const ChainLds& L, int slot, int tx, int nth) {
+  const int N = d.N;
+  double* Lo = cam_L(d, slot);
+  double* Ko = cam_K(d, slot);
+  for (int q = tx; q < N * 12; q += nth) {  // L_i = P(i, -1)
     const int i = q / 12, e = q % 12;
-    Lo[q] = PR[i * (i + 1) / 2][e];
+    Lo[q] = L.PR[i * (i + 1) / 2][e];
   }
-  for (int idx = threadIdx.x; idx < N * N * 36; idx += nth) {
+  for (int idx = tx; idx < N * N * 36; idx += nth) {
     const int e = idx % 36, ij = idx / 36, i = ij / N, j = ij % N;
     double val = 0.0;
     if (j < i) {
-      const double* P = PR[i * (i + 1) / 2 + j + 1];
-      val = -chain_entry(P, P + 9, st[j], e / 6, e % 6);
+      const double* P = L.PR[i * (i + 1) / 2 + j + 1];
+      val = -chain_entry(P, P + 9, L.st[j], e / 6, e % 6);
     }
     Ko[idx] = val;
   }
+}
+__device__ __forceinline__ void chain_block(const KbDev& d, const double* base, int slot, int nth) {
+  __shared__ ChainLds L;
+  chain_pairs<false>(d, base, L, threadIdx.x);
+  __syncthreads();
+  chain_write(d, L, slot, threadIdx.x, nth);
 }
 
 // k_pre: camera chains of the current state (slot cur); gate 1 also runs the policy prelude of the first pass.
@@ -2536,8 +2549,22 @@ __device__ __forceinline__ void bs_tile(const double* S, const double* Dfac, con
 // x = Ltilde^-T z, z = (row C of the factor) D^-1, by one wave.  Lane l = 16 g + r holds the rows 16 (g + 4 s) + r,
 // s = 0, 1: tile t lives in the 16-lane group t & 3, slot t >> 2.  Tiles from the last (bs_tile); the result comes
 // back in x[s] = x_{l + 64 s}.
+// Once tile pub_tile is done (xb != nullptr), the final x of rows >= 16 pub_tile go to xb[] and *bflag is set: the
+// baseline columns, for the wave that updates the baselines and builds the camera chains meanwhile.
+__device__ __forceinline__ void bs_publish(int C, int pub_tile, double* xb, volatile int* bflag, const double (&x)[2]) {
+  const int lane = threadIdx.x & 63, g = lane >> 4, r = lane & 15;
+#pragma unroll
+  for (int sl = 0; sl < 2; ++sl) {
+    const int row = 16 * (g + 4 * sl) + r;
+    if (row >= 16 * pub_tile && row < C) xb[row] = x[sl];
+  }
+  KB_WAVE_SYNC();
+  if (lane == 0) *bflag = 1;
+}
+
 __device__ __forceinline__ void panel_backsolve(const KbDev& d, const double* S, const double* Dfac, const double* Xinv,
-                                                const double* rD, int C, int nb, double* pub, double (&x)[2]) {
+                                                const double* rD, int C, int nb, double* pub, double (&x)[2],
+                                                int pub_tile = -1, double* xb = nullptr, volatile int* bflag = nullptr) {
   const int lane = threadIdx.x & 63, g = lane >> 4, r = lane & 15;
   int row[2];
   double rdv[2];
@@ -2552,9 +2579,16 @@ __device__ __forceinline__ void panel_backsolve(const KbDev& d, const double* S,
     x[sl] = row[sl] < C ? z * rd : 0.0;
   }
   int ti = (C - 1) >> 4;
-  if (ti == nb - 1) bs_tile<true>(S, Dfac, Xinv, C, ti--, row, rdv, pub, x);  // the tile holding row C
+  if (ti == nb - 1) {
+    bs_tile<true>(S, Dfac, Xinv, C, ti, row, rdv, pub, x);  // the tile holding row C
+    if (xb && ti == pub_tile) bs_publish(C, pub_tile, xb, bflag, x);
+    --ti;
+  }
 #pragma unroll 1
-  for (; ti >= 0; --ti) bs_tile<false>(S, Dfac, Xinv, C, ti, row, rdv, pub, x);
+  for (; ti >= 0; --ti) {
+    bs_tile<false>(S, Dfac, Xinv, C, ti, row, rdv, pub, x);
+    if (xb && ti == pub_tile) bs_publish(C, pub_tile, xb, bflag, x);
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2947,6 +2981,10 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update, int nth) {
   __shared__ int fin[2];  // GN fused: done, cur after the previous pass's end
   __shared__ KbCtrl cls;
   __shared__ double cl_red[4];
+  __shared__ ChainLds chl;                     // CM == 0: the candidate chains' pair products (wave 1)
+  __shared__ int bflag;                        // CM == 0: baseline x published by the backsolve wave
+  __shared__ double xb[CM == 0 ? 128 : 1];     // CM == 0: those x (rows >= 16 pub_tile)
+  if (CM == 0 && tid == 0) bflag = 0;
   const double lam = gate ? c->lambda : d.host_lambda;
   const double lam2 = lam * lam;
   int cur = c->cur;
@@ -2964,6 +3002,16 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update, int nth) {
     const int nr = d.Wtot - d.Wp;
     dxr = psum_max_at(d, d.Wp + min(tid, nr - 1));
     for (int r = tid + 64; r < nr; r += 64) dxr = fmax(dxr, psum_max_at(d, d.Wp + r));
+  }
+  // the camera DVs of both state slots (the DV update reads slot cur, which the previous pass's end may still flip),
+  // loaded with the staging round instead of one dependent round trip after the solves
+  __shared__ double camst[2][KB_MAX_CAMS * KB_MAX_INTR + 7 * (KB_MAX_CAMS - 1)];
+  const int nst = N * KB_MAX_INTR + 7 * (N - 1);
+  double cpv[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int q = min(tid + u * nth, 2 * nst - 1), sl = q >= nst ? 1 : 0, e = q - sl * nst;
+    cpv[u] = d.state[(size_t)sl * d.S + (e < N * KB_MAX_INTR ? e : d.off_base + e - N * KB_MAX_INTR)];
   }
   KB_TS(d, 0);
   KB_STAMP(d, 0);
@@ -2992,6 +3040,11 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update, int nth) {
     solve_stage<4, CM, false>(d, bslot, K, Hs, S, bv, ci, tid, nth);
   }
   if (tid < 3 * N) ctab[tid / N][tid % N] = tid < N ? cam_arg(d.nintr, tid) : (tid < 2 * N ? cam_arg(d.col_intr, tid - N) : cam_arg(d.col_base, tid - 2 * N));
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int q = tid + u * nth;
+    if (q < 2 * nst) (&camst[0][0])[q >= nst ? (q - nst) + (KB_MAX_CAMS * KB_MAX_INTR + 7 * (KB_MAX_CAMS - 1)) : q] = cpv[u];
+  }
   __syncthreads();
   if (tid == 0) okl = (c->solve_ok != 0) && !(bv[C] > 0.0);
   // the loop's done flag is tested only here: the ctrl and staging loads above went out in one round trip, and
@@ -3039,6 +3092,79 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update, int nth) {
       fin[1] = cl.cur;
     }
   };
+  // wave 0 after the solves: camera dx, its statistics, the intrinsic (and, CM > 0, baseline) DV update into the
+  // candidate slot 1 - cu
+  auto wave0_tail = [&](int cur) {
+    const int lane = tid;
+    double mx = 0.0, dd = 0.0, dr = 0.0;
+#pragma unroll
+    for (int sl = 0; sl < 2; ++sl) {
+      const int i = lane + 64 * sl;
+      if (i < C) {
+        const double g = gl[i];
+        d.dx[i] = x[sl];
+        mx = fmax(mx, fabs(x[sl]));
+        dd += x[sl] * x[sl];
+        dr += x[sl] * g;
+      }
+    }
+    mx = wave_max_d(mx);
+    dd = wave_sum_d(dd);
+    dr = wave_sum_d(dr);
+    if (lane == 0) {
+      d.camstat[0] = mx;
+      d.camstat[1] = dd;
+      d.camstat[2] = dr;
+      if (gfu) {  // the step is applied by the next pass's build (or the finishing back-substitution)
+        c->have_dx = 1;
+        c->pending = 1;
+      }
+    }
+    if (do_update) {
+      // camera design variables: intrinsics (additive, one lane per slot) and baselines (one lane per pose)
+      const double* in = camst[cur];  // [intrinsics N * KB_MAX_INTR | baselines 7 (N - 1)] of slot cur
+      double* out = d.state + (size_t)(1 - cur) * d.S;
+      constexpr int kIntrSlots = (KB_MAX_CAMS * KB_MAX_INTR + 63) / 64;
+      double vin[kIntrSlots];
+#pragma unroll
+      for (int r = 0; r < kIntrSlots; ++r) {
+        const int q = lane + 64 * r;
+        vin[r] = (q < N * KB_MAX_INTR) ? in[q] : 0.0;
+      }
+      double bq[7];
+      const int jb = lane < N - 1 ? lane : 0;
+#pragma unroll
+      for (int q = 0; q < 7; ++q) bq[q] = in[N * KB_MAX_INTR + 7 * jb + q];
+#pragma unroll
+      for (int r = 0; r < kIntrSlots; ++r) {
+        if (64 * r >= N * KB_MAX_INTR) break;  // wave-uniform
+        const int q = lane + 64 * r;
+        const int cm = min(q / KB_MAX_INTR, N - 1), xi = q % KB_MAX_INTR;
+        const bool act = q < N * KB_MAX_INTR && xi < ctab[0][cm];
+        const int col = act ? ctab[1][cm] + xi : 0;
+        const double v0 = __shfl(x[0], col & 63), v1 = __shfl(x[1], col & 63);
+        const double dv = (col >> 6) ? v1 : v0;
+        if (q < N * KB_MAX_INTR) out[q] = vin[r] + (act ? dv : 0.0);
+      }
+      if (CM > 0 && N > 1) {  // CM == 0: wave 1 did the baselines (and the chains) beside the backsolve
+        double d6[6], nb[7];
+        const int cb = ctab[2][jb];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) {
+          const int col = cb + q;
+          const double v0 = __shfl(x[0], col & 63), v1 = __shfl(x[1], col & 63);
+          d6[q] = (col >> 6) ? v1 : v0;
+        }
+        update_pose(bq, d6, nb);
+        if (lane < N - 1)
+#pragma unroll
+          for (int q = 0; q < 7; ++q) {
+            out[d.off_base + 7 * lane + q] = nb[q];
+            nbase[7 * lane + q] = nb[q];
+          }
+      }
+    }
+  };
   __syncthreads();
   KB_TS(d, 2);
   if constexpr (CM > 0) {
@@ -3072,10 +3198,42 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update, int nth) {
   } else {
     // phase C: blocked LDL^T with the forward solve (row C); the previous pass's end beside the first panel
     if (gfu && fwave) finish_prev();
-    ldl_panels(d, S, rDv, Dfac, Xinv, C, nb, &okl);
+    ldl_panels(d, S, rDv, Dfac, Xinv, C, nb, &okl);  // ends with a block barrier: okl and fin are final
     KB_TS(d, 4);
     KB_STAMP(d, 3);
-    if (tid < 64) panel_backsolve(d, S, Dfac, Xinv, rDv, C, nb, pubcol, x);  // phase D: Ltilde^T x = z, one wave
+    // phase D: Ltilde^T x = z on wave 0; wave 1 updates the baselines from the published baseline rows and builds the
+    // candidate state's camera chains while wave 0 finishes the intrinsic rows (the baselines follow every intrinsic
+    // column, so their rows are final first)
+    const int cb0 = ctab[2][0], pub_tile = N > 1 ? cb0 >> 4 : -1;
+    const bool upd = do_update && okl && !(gfu && fin[0]);
+    if (tid < 64) {
+      panel_backsolve(d, S, Dfac, Xinv, rDv, C, nb, pubcol, x, pub_tile, xb, &bflag);
+      if (okl && !(gfu && fin[0])) wave0_tail(gfu ? fin[1] : cur);
+    } else if ((tid >> 6) == 1 && upd) {
+      const int lane = tid & 63, cu = gfu ? fin[1] : cur;
+      if (N > 1) {
+        while (*(volatile int*)&bflag == 0) __builtin_amdgcn_s_sleep(1);
+        KB_WAVE_SYNC();
+        const int jb = lane < N - 1 ? lane : 0;
+        double bq[7], d6[6], nbv[7];
+#pragma unroll
+        for (int q = 0; q < 7; ++q) bq[q] = camst[cu][N * KB_MAX_INTR + 7 * jb + q];
+        const int cb = ctab[2][jb];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) d6[q] = *(volatile double*)&xb[cb + q];
+        update_pose(bq, d6, nbv);
+        if (lane < N - 1) {
+          double* out = d.state + (size_t)(1 - cu) * d.S;
+#pragma unroll
+          for (int q = 0; q < 7; ++q) {
+            out[d.off_base + 7 * lane + q] = nbv[q];
+            nbase[7 * lane + q] = nbv[q];
+          }
+        }
+        KB_WAVE_SYNC();
+      }
+      chain_pairs<true>(d, nbase, chl, lane);  // the K entries: all waves after the barrier (chain_write)
+    }
     KB_STAMP(d, 4);
   }
   __syncthreads();  // okl final
@@ -3100,83 +3258,14 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update, int nth) {
     }
     return;
   }
-  if (tid < 64) {
-    const int lane = tid;
-    double mx = 0.0, dd = 0.0, dr = 0.0;
-#pragma unroll
-    for (int sl = 0; sl < 2; ++sl) {
-      const int i = lane + 64 * sl;
-      if (i < C) {
-        const double g = gl[i];
-        d.dx[i] = x[sl];
-        mx = fmax(mx, fabs(x[sl]));
-        dd += x[sl] * x[sl];
-        dr += x[sl] * g;
-      }
-    }
-    mx = wave_max_d(mx);
-    dd = wave_sum_d(dd);
-    dr = wave_sum_d(dr);
-    if (lane == 0) {
-      d.camstat[0] = mx;
-      d.camstat[1] = dd;
-      d.camstat[2] = dr;
-      if (gfu) {  // the step is applied by the next pass's build (or the finishing back-substitution)
-        c->have_dx = 1;
-        c->pending = 1;
-      }
-    }
-    if (do_update) {
-      // camera design variables: intrinsics (additive, one lane per slot) and baselines (one lane per pose)
-      const double* in = d.state + (size_t)cur * d.S;
-      double* out = d.state + (size_t)(1 - cur) * d.S;
-      constexpr int kIntrSlots = (KB_MAX_CAMS * KB_MAX_INTR + 63) / 64;
-      double vin[kIntrSlots];
-#pragma unroll
-      for (int r = 0; r < kIntrSlots; ++r) {
-        const int q = lane + 64 * r;
-        vin[r] = (q < N * KB_MAX_INTR) ? in[q] : 0.0;
-      }
-      double bq[7];
-      const int jb = lane < N - 1 ? lane : 0;
-#pragma unroll
-      for (int q = 0; q < 7; ++q) bq[q] = in[d.off_base + 7 * jb + q];
-#pragma unroll
-      for (int r = 0; r < kIntrSlots; ++r) {
-        if (64 * r >= N * KB_MAX_INTR) break;  // wave-uniform
-        const int q = lane + 64 * r;
-        const int cm = min(q / KB_MAX_INTR, N - 1), xi = q % KB_MAX_INTR;
-        const bool act = q < N * KB_MAX_INTR && xi < ctab[0][cm];
-        const int col = act ? ctab[1][cm] + xi : 0;
-        const double v0 = __shfl(x[0], col & 63), v1 = __shfl(x[1], col & 63);
-        const double dv = (col >> 6) ? v1 : v0;
-        if (q < N * KB_MAX_INTR) out[q] = vin[r] + (act ? dv : 0.0);
-      }
-      if (N > 1) {
-        double d6[6], nb[7];
-        const int cb = ctab[2][jb];
-#pragma unroll
-        for (int q = 0; q < 6; ++q) {
-          const int col = cb + q;
-          const double v0 = __shfl(x[0], col & 63), v1 = __shfl(x[1], col & 63);
-          d6[q] = (col >> 6) ? v1 : v0;
-        }
-        update_pose(bq, d6, nb);
-        if (lane < N - 1)
-#pragma unroll
-          for (int q = 0; q < 7; ++q) {
-            out[d.off_base + 7 * lane + q] = nb[q];
-            nbase[7 * lane + q] = nb[q];
-          }
-      }
-    }
-  }
+  if (CM > 0 && tid < 64) wave0_tail(cur);  // CM == 0: ran right after the backsolve
   KB_TS(d, 6);
   KB_STAMP(d, 5);
-  if (do_update) {
+  if (CM > 0 && do_update) {
     __syncthreads();
     chain_block(d, nbase, 1 - cur, nth);  // chains of the candidate state (k_backsub's cost, next build if accepted)
   }
+  if (CM == 0 && do_update) chain_write(d, chl, 1 - cur, tid, nth);  // pair products by wave 1 before the barrier
   KB_TS(d, 7);
 }
 

@@ -27,6 +27,18 @@
 
 namespace kb {
 
+// diagnostic build only: s_memrealtime stamps of block 0, thread 0 (slot 200 + 6 it + phase, first 8 iterations)
+#ifdef KB_STAMPS
+#define KB_PCG_TS(slot)                                                                                         \
+  do {                                                                                                          \
+    if (blockIdx.x == 0 && threadIdx.x == 0 && d.dbg_ts && (slot) < 256) d.dbg_ts[slot] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define KB_PCG_TS(slot) \
+  do {                  \
+  } while (0)
+#endif
+
 constexpr int kPcgThreads = 256;
 constexpr int kPcgMaxFpb = 16;      // frames per block
 constexpr unsigned kPcgSpinLimit = 1u << 26;
@@ -295,6 +307,8 @@ __global__ void __launch_bounds__(kPcgThreads) k_pcg(KbDev d, KbPcg P) {
     int it = 0;
     for (it = 0; it < max_it; ++it) {
       if (dn <= d0) break;
+      const int tsb = 200 + 6 * it;
+      if (it < 8) KB_PCG_TS(tsb);
       // ---- phase A: q_f, camera partials, d_f.q_f
       double dq_part = 0.0;
       for (int t = tid; t < nr; t += blockDim.x) {
@@ -332,10 +346,13 @@ __global__ void __launch_bounds__(kPcgThreads) k_pcg(KbDev d, KbPcg P) {
       }
       dq_part = pcg_block_sum(dq_part, red);
       if (tid == 0) P.part[(size_t)b * CP + C] = ok ? dq_part : NAN;  // a failed block poisons d.q
+      if (it < 8) KB_PCG_TS(tsb + 1);
       if (!pcg_barrier(P.bar, nblk, ++nbar, &flag)) goto timeout;
+      if (it < 8) KB_PCG_TS(tsb + 2);
       // ---- phase B: q_c, alpha, updates, s = M^-1 r, partial r_f.s_f
       pcg_sum_columns(P.part, CP, C + 1, nblk, qc, &sh_scalar[2]);
       __syncthreads();
+      if (it < 8) KB_PCG_TS(tsb + 3);
       if (tid < 64) {
         double c = 0.0;
         for (int p = tid; p < C; p += 64) c += dc[p] * qc[p];
@@ -366,7 +383,9 @@ __global__ void __launch_bounds__(kPcgThreads) k_pcg(KbDev d, KbPcg P) {
         v = pcg_block_sum(v, red);
         if (tid == 0) P.part2[b] = v;
       }
+      if (it < 8) KB_PCG_TS(tsb + 4);
       if (!pcg_barrier(P.bar, nblk, ++nbar, &flag)) goto timeout;
+      if (it < 8) KB_PCG_TS(tsb + 5);
       // ---- phase C: dn', beta, d = s + beta d
       if (tid < 64) {
         double v = 0.0;
