@@ -107,9 +107,13 @@ int kb_solve(kb_handle* h, double* dx_out, int* ok);
  *                    r^T M^-1 r <= tolerance * r0^T M^-1 r0 (absolute mode: or <= the previous solve's _residual).
  *                    The reference always returns true; here *ok = 0 on a singular DV block or non-positive
  *                    curvature d^T A d.  One-GPU handles only (a sharded handle returns an error).
+ *   KB_SOLVER_PCG_SCHUR  the frame blocks eliminated exactly (as KB_SOLVER_SCHUR), then the same block-Jacobi
+ *                    PCG (same options, stopping rule and _residual semantics) on the C x C camera-block Schur
+ *                    complement instead of its LDL^T, the frames back-substituted from that camera step.  One
+ *                    block, ~1 us per iteration; a different iterate sequence than KB_SOLVER_PCG's full-system CG.
  * kb_optimize always uses the direct solve (its passes are captured graphs); the per-call path
  * (kb_build / kb_solve / kb_apply_update, driven by the host Optimizer2) uses the selected solver. */
-enum kb_linear_solver { KB_SOLVER_SCHUR = 0, KB_SOLVER_PCG = 1 };
+enum kb_linear_solver { KB_SOLVER_SCHUR = 0, KB_SOLVER_PCG = 1, KB_SOLVER_PCG_SCHUR = 2 };
 typedef struct kb_pcg_options {
   double tolerance;           /* _tolerance (LinearSolverPCG default 1e-6) */
   int32_t max_iterations;     /* _maxIter (-1: number of rows, the default) */

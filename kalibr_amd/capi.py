@@ -80,7 +80,7 @@ class PcgInfo(C.Structure):
     _fields_ = [("iterations", C.c_int32), ("residual", C.c_double), ("d0", C.c_double)]
 
 
-SOLVER_SCHUR, SOLVER_PCG = 0, 1
+SOLVER_SCHUR, SOLVER_PCG, SOLVER_PCG_SCHUR = 0, 1, 2
 
 DBL_EPS = float(np.finfo(float).eps)
 
@@ -253,8 +253,9 @@ class Solver:
         return bool(ok.value), dx
 
     def set_linear_solver(self, kind="schur", tolerance=1e-6, max_iterations=-1, absolute_tolerance=True):
-        """kind "schur" (direct, default) or "pcg" (LinearSolverPCG: block-Jacobi PCG) for solve()."""
-        k = {"schur": SOLVER_SCHUR, "pcg": SOLVER_PCG}[kind]
+        """kind "schur" (direct, default), "pcg" (LinearSolverPCG: block-Jacobi PCG on the full system) or "pcg_schur"
+        (the same PCG on the camera-block Schur complement, frames eliminated exactly) for solve()."""
+        k = {"schur": SOLVER_SCHUR, "pcg": SOLVER_PCG, "pcg_schur": SOLVER_PCG_SCHUR}[kind]
         o = PcgOptions(float(tolerance), int(max_iterations), int(absolute_tolerance))
         _check(lib().kb_set_linear_solver(self.h, k, C.byref(o)))
 

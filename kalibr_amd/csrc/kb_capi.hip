@@ -158,7 +158,7 @@ struct kb_handle {
   kb_pcg_info pcg_info{0, 0.0, 0.0};
   double* cond2 = nullptr;     // setConditioner: squared diagonal [ncols] (canonical order)
   bool use_cond = false;       // kb_set_conditioner active (kb_set_constant_conditioner clears it)
-  double* pcg_buf = nullptr;   // part [F][C+1] | part2 [F] | info [8]
+  double* pcg_buf = nullptr;   // part [F][C+1] | part2 [F] | info [8] | PCG_SCHUR info [4]
   int* pcg_cb = nullptr;       // [2][C] camera DV block start / size per column
   unsigned* pcg_bar = nullptr;
 
@@ -769,11 +769,11 @@ static size_t pcg_lds(int fpb, int C, int F) {
   return sizeof(double) * (R * C + 54 * (size_t)fpb + 5 * R + 11 * (size_t)C + nrow * C) + sizeof(int) * 2 * (size_t)C;
 }
 
-static int run_pcg(kb_handle* h, int* ok) {
-  if (sharded(h)) return fail("kb_solve (PCG): not available on a sharded handle");
+// the PCG buffers and the camera DV block table (first use)
+static int ensure_pcg(kb_handle* h) {
   const int C = h->C, F = h->F;
   if (!h->pcg_buf) {
-    if (h->alloc(&h->pcg_buf, (size_t)F * (C + 1) + F + 8) || h->alloc(&h->pcg_cb, 2 * (size_t)C) ||
+    if (h->alloc(&h->pcg_buf, (size_t)F * (C + 1) + F + 12) || h->alloc(&h->pcg_cb, 2 * (size_t)C) ||
         h->alloc(&h->pcg_bar, kPcgBarWords))
       return -1;
     std::vector<int> cb(2 * C);
@@ -798,6 +798,13 @@ static int run_pcg(kb_handle* h, int* ok) {
     if (c != C) return fail("kb_solve (PCG): camera DV blocks do not cover the camera columns");
     KB_HIP(hipMemcpyAsync(h->pcg_cb, cb.data(), sizeof(int) * 2 * C, hipMemcpyHostToDevice, h->stream));
   }
+  return 0;
+}
+
+static int run_pcg(kb_handle* h, int* ok) {
+  if (sharded(h)) return fail("kb_solve (PCG): not available on a sharded handle");
+  const int C = h->C, F = h->F;
+  if (ensure_pcg(h)) return -1;
   // frames per block: >= 64 blocks when there are enough frames, H_fc rows of the block within ~120 KB of LDS
   int fpb = std::max(1, std::min(kPcgMaxFpb, (F + 63) / 64));
   while (fpb > 1 && pcg_lds(fpb, C, F) > 120 * 1024) --fpb;
@@ -842,7 +849,8 @@ static int run_pcg(kb_handle* h, int* ok) {
 
 int kb_set_linear_solver(kb_handle* h, int32_t kind, const kb_pcg_options* pcg) {
   if (!h) return fail("kb_set_linear_solver: null");
-  if (kind != KB_SOLVER_SCHUR && kind != KB_SOLVER_PCG) return fail("kb_set_linear_solver: unknown solver");
+  if (kind != KB_SOLVER_SCHUR && kind != KB_SOLVER_PCG && kind != KB_SOLVER_PCG_SCHUR)
+    return fail("kb_set_linear_solver: unknown solver");
   if (kind == KB_SOLVER_PCG && sharded(h)) return fail("kb_set_linear_solver: PCG is not available on a sharded handle");
   h->solver_kind = kind;
   h->pcg = pcg ? *pcg : kb_pcg_options{1e-6, -1, 1};
@@ -882,11 +890,31 @@ int kb_solve(kb_handle* h, double* dx_out, int* ok) {
   } cs(h);
   if (launch_schur(h, 0)) return -1;
   if (launch_colsum(h, 0)) return -1;
-  // k_solve folds the frame-block failure count and the LDL^T of S into ctrl->solve_ok
-  if (launch_solve(h, 0, 0)) return -1;
+  // k_solve folds the frame-block failure count and the LDL^T of S (or PCG on S) into ctrl->solve_ok
+  const bool pcs = h->solver_kind == KB_SOLVER_PCG_SCHUR;
+  if (pcs) {
+    if (ensure_pcg(h)) return -1;
+    h->d.pcs_cb = h->pcg_cb;
+    h->d.pcs_tol = h->pcg.tolerance;
+    h->d.pcs_prev = h->pcg_residual;
+    h->d.pcs_maxit = h->pcg.max_iterations < 0 ? h->C : h->pcg.max_iterations;
+    h->d.pcs_abs = h->pcg.absolute_tolerance ? 1 : 0;
+    h->d.pcs_info = h->pcg_buf + (size_t)h->F * (h->C + 1) + h->F + 8;  // after the full-system PCG's info [8]
+  }
+  const int rs = launch_solve(h, 0, 0);
+  h->d.pcs_cb = nullptr;
+  if (rs) return -1;
   int okd = 0;
   KB_HIP(hipMemcpyAsync(&okd, &h->d.ctrl->solve_ok, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+  double pinfo[4] = {0, 0, 0, 0};
+  if (pcs) KB_HIP(hipMemcpyAsync(pinfo, h->d.pcs_info, sizeof(pinfo), hipMemcpyDeviceToHost, h->stream));
   KB_HIP(hipStreamSynchronize(h->stream));
+  if (pcs) {
+    h->pcg_info.iterations = (int32_t)pinfo[0];
+    h->pcg_info.residual = pinfo[1];
+    h->pcg_info.d0 = pinfo[2];
+    h->pcg_residual = pinfo[1];  // _residual = 0.5 dn (linear_solver_pcg.hpp:127)
+  }
   *ok = okd;
   if (!okd) return 0;
   if (launch_backsub(h, 0, 0, 0)) return -1;

@@ -102,6 +102,13 @@ struct KbDev {
   double* simg;  // C > 64: k_solve's LDS image of the camera block (k_colimg) [img_n]
   int img_n;
   KbCtrl* ctrl;
+  // KB_SOLVER_PCG_SCHUR (per-call kb_solve only): k_solve runs block-Jacobi PCG on the Schur complement instead of
+  // the LDL^T.  pcs_cb: [2][C] camera DV block start / size per column (null: the LDL^T); pcs_info [4]: iterations,
+  // residual (dn / 2), d0, ok
+  const int* pcs_cb;
+  double pcs_tol, pcs_prev;
+  int pcs_maxit, pcs_abs;
+  double* pcs_info;
   int dbg_stop;   // diagnostic build only (KB_STAMPS): stop point of the timed kernel (-1: run to the end)
   int dbg_flags;  // diagnostic build only: bit 0 run the camera LDL^T twice (rolled)
   long long* dbg_ts;  // diagnostic build only: [128] s_memrealtime stamps: k_solve (KB_TS) | k_buildp (KB_TSB, +64)

@@ -2339,7 +2339,7 @@ template <int K>
 __device__ __forceinline__ void panel_steps(double (&row)[16], int lane, int q, int C, bool& ok, double& rd) {
   if constexpr (K < 16) {
     double bc[16];
-    rl_tail<K, K>(row, bc);  // bc[K] = D_K, bc[j] = S[K][j]
+    rl_tail<K, K>(row, bc);  // bc[K] = D_K, bc[j] = S[K][j] (reading D_K on its own first measured no faster)
     const double Dk = bc[K];
     const double rdk = Dk > 0.0 ? recip_d1(Dk) : 0.0;
     const double f = row[K] * rdk;
@@ -2949,6 +2949,128 @@ __device__ __forceinline__ void cam_expand_blocks(double* S, int C, int N, const
   }
 }
 
+// KB_SOLVER_PCG_SCHUR: LinearSolverPCG::solve (sparse_block_matrix linear_solver_pcg.hpp:58-130) on the camera
+// block's Schur complement S x = b (S = H_cc + lambda^2 I - sum H_fc^T H_ff^-1 H_fc, the frame blocks eliminated
+// exactly), M = the inverses of S's diagonal camera DV blocks (d.pcs_cb), by the whole block with S in LDS (sget).
+// Four threads per row in the mat-vec (fixed order: j = t (mod 4) partial sums, then a 2-step butterfly); dots by a
+// fixed-order block sum.  Wave 0 gets x[s] = x_{lane + 64 s}; returns false on a singular DV block or non-positive
+// curvature (the reference has no check).  Every thread of the block must call it.
+template <class SGet>
+__device__ bool schur_pcg(const KbDev& d, SGet sget, const double* b, int C, int nth, double (&xo)[2]) {
+  __shared__ double v_x[128], v_r[128], v_z[128], v_p[128], v_q[128], Minv[128][6], red[16], scal[4];
+  __shared__ int blk_ok;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = nth >> 6;
+  auto bsum = [&](double v) {  // fixed-order block sum, result uniform
+    v = wave_sum_d(v);
+    __syncthreads();
+    if (lane == 0) red[wave] = v;
+    __syncthreads();
+    double s = 0.0;
+    for (int w = 0; w < nw; ++w) s += red[w];
+    return s;
+  };
+  if (tid == 0) blk_ok = 1;
+  __syncthreads();
+  // preconditioner: one thread per DV block inverts its m x m diagonal block of S (Gauss-Jordan, partial pivoting)
+  for (int p = tid; p < C; p += nth) {
+    const int s0 = d.pcs_cb[p], m = d.pcs_cb[C + p];
+    if (s0 != p) continue;
+    double A[6][12];
+    for (int r = 0; r < m; ++r)
+      for (int c = 0; c < 2 * m; ++c) A[r][c] = c < m ? sget(p + r, p + c) : (c - m == r ? 1.0 : 0.0);
+    bool good = true;
+    for (int k = 0; k < m && good; ++k) {
+      int piv = k;
+      for (int r = k + 1; r < m; ++r)
+        if (fabs(A[r][k]) > fabs(A[piv][k])) piv = r;
+      if (!(fabs(A[piv][k]) > 0.0)) {
+        good = false;
+        break;
+      }
+      if (piv != k)
+        for (int c = 0; c < 2 * m; ++c) {
+          const double t = A[k][c];
+          A[k][c] = A[piv][c];
+          A[piv][c] = t;
+        }
+      const double inv = 1.0 / A[k][k];
+      for (int c = 0; c < 2 * m; ++c) A[k][c] *= inv;
+      for (int r = 0; r < m; ++r) {
+        if (r == k) continue;
+        const double f = A[r][k];
+        for (int c = 0; c < 2 * m; ++c) A[r][c] -= f * A[k][c];
+      }
+    }
+    if (!good) blk_ok = 0;
+    for (int r = 0; r < m; ++r)
+      for (int c = 0; c < 6; ++c) Minv[p + r][c] = (good && c < m) ? A[r][m + c] : 0.0;
+  }
+  for (int i = tid; i < 128; i += nth) {
+    v_x[i] = 0.0;
+    v_r[i] = i < C ? b[i] : 0.0;
+  }
+  __syncthreads();
+  auto precond = [&]() {  // z = M^-1 r
+    for (int i = tid; i < C; i += nth) {
+      const int s0 = d.pcs_cb[i], m = d.pcs_cb[C + i];
+      double v = 0.0;
+      for (int k = 0; k < m; ++k) v += Minv[i][k] * v_r[s0 + k];
+      v_z[i] = v;
+    }
+  };
+  precond();
+  __syncthreads();
+  for (int i = tid; i < 128; i += nth) v_p[i] = i < C ? v_z[i] : 0.0;
+  double dn = bsum(tid < C ? v_r[tid] * v_z[tid] : 0.0);
+  double d0 = d.pcs_tol * dn;
+  if (d.pcs_abs && d.pcs_prev > 0.0 && d.pcs_prev > d0) d0 = d.pcs_prev;
+  bool ok = blk_ok != 0;
+  int it = 0;
+  for (; ok && it < d.pcs_maxit; ++it) {
+    if (dn <= d0) break;
+    // q = S p: row i by threads 4i .. 4i + 3
+    const int row = tid >> 2, part = tid & 3;
+    double acc = 0.0;
+    if (row < C)
+      for (int j = part; j < C; j += 4) acc += sget(row, j) * v_p[j];
+    acc += __shfl_xor(acc, 1);
+    acc += __shfl_xor(acc, 2);
+    if (row < C && part == 0) v_q[row] = acc;
+    __syncthreads();
+    const double pq = bsum(tid < C ? v_p[tid] * v_q[tid] : 0.0);
+    if (!(pq > 0.0) || !isfinite(pq)) {
+      ok = false;
+      break;
+    }
+    const double alpha = dn / pq;
+    if (tid < C) {
+      v_x[tid] += alpha * v_p[tid];
+      v_r[tid] -= alpha * v_q[tid];
+    }
+    __syncthreads();
+    precond();
+    __syncthreads();
+    const double dnew = bsum(tid < C ? v_r[tid] * v_z[tid] : 0.0);
+    const double beta = dnew / dn;
+    dn = dnew;
+    if (tid < C) v_p[tid] = v_z[tid] + beta * v_p[tid];
+    __syncthreads();
+  }
+  if (tid == 0) {
+    scal[0] = ok ? 1.0 : 0.0;
+    d.pcs_info[0] = it;
+    d.pcs_info[1] = 0.5 * dn;
+    d.pcs_info[2] = d0;
+    d.pcs_info[3] = ok ? 1.0 : 0.0;
+  }
+  __syncthreads();
+  if (wave == 0) {
+    xo[0] = lane < C ? v_x[lane] : 0.0;
+    xo[1] = lane + 64 < C ? v_x[lane + 64] : 0.0;
+  }
+  return scal[0] != 0.0;
+}
+
 // Camera solve of one pass (one block): S = H_cc + lambda^2 I - sum Y^T Y, b = g_c - sum Y^T z staged in LDS,
 // LDL^T + solves (CM > 0: one-wave register LDL^T for C <= CM <= 64; CM == 0: block LDL^T in LDS), camera DV
 // update into state[1 - cur] and the camera chains of that candidate state into slot 1 - cur.
@@ -3186,7 +3308,10 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update, int nth) {
 #pragma unroll 1
     for (int rep = 0; rep < reps; ++rep)
 #endif
-    if (tid < 64) {
+    if (d.pcs_cb) {  // KB_SOLVER_PCG_SCHUR (per-call path: no pass end to fold in)
+      auto sget = [&](int i, int j) { return S[i >= j ? cidx(i, j, C) : cidx(j, i, C)]; };
+      if (!schur_pcg(d, sget, bv, C, nth, x)) okl = 0;
+    } else if (tid < 64) {
       const LdlOut r = ldl_solve_reg<CM>(d, S, bv, C, tid, pubcol);
       x[0] = r.x;
       if (!r.ok) okl = 0;
@@ -3198,6 +3323,15 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update, int nth) {
   } else {
     // phase C: blocked LDL^T with the forward solve (row C); the previous pass's end beside the first panel
     if (gfu && fwave) finish_prev();
+    if (d.pcs_cb) {  // KB_SOLVER_PCG_SCHUR (per-call path): S and b = row C of the k_colimg image
+      auto sget = [&](int i, int j) { return S[i >= j ? tidx(i, j) : tidx(j, i)]; };
+      double* bcol = rDv;  // b (row C of the image) as a vector; rDv is unused without the LDL^T
+      for (int j = tid; j < C; j += nth) bcol[j] = S[tidx(C, j)];
+      __syncthreads();
+      if (!schur_pcg(d, sget, bcol, C, nth, x)) okl = 0;
+      __syncthreads();
+      if (tid < 64 && okl && !(gfu && fin[0])) wave0_tail(gfu ? fin[1] : cur);
+    } else {
     ldl_panels(d, S, rDv, Dfac, Xinv, C, nb, &okl);  // ends with a block barrier: okl and fin are final
     KB_TS(d, 4);
     KB_STAMP(d, 3);
@@ -3233,6 +3367,7 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update, int nth) {
         KB_WAVE_SYNC();
       }
       chain_pairs<true>(d, nbase, chl, lane);  // the K entries: all waves after the barrier (chain_write)
+    }
     }
     KB_STAMP(d, 4);
   }

@@ -4,6 +4,9 @@ LinearSolverPCG::solve, linear_solver_pcg.hpp:58-130) against the oracle's resta
 Tolerances (FP64; the two sides sum dot products in different orders, so the CG iterates drift apart by a
 few ulps per iteration):
   first 1 and 3 iterations                      dx rel 1e-9 of max|dx| against the oracle's PCG dx
+  Schur-complement PCG (KB_SOLVER_PCG_SCHUR)   1 / 3 iterations: camera dx rel 1e-9 / 1e-8 against a numpy
+                                                restatement on the oracle's Schur complement; tight: rel 1e-8 of
+                                                the direct solve; defaults: same d0, iterations within 2 + 25 %
   reference tolerance (1e-6)                    same d0 (1e-9), iterations within 2 + 25%, error vs the direct
                                                 solve <= 3x the oracle's (CG rounding sensitivity, see test)
   dx with a tight tolerance                     rel 1e-8 of max|dx| against the direct Schur solve
@@ -147,3 +150,108 @@ def test_pcg_host_loop_reaches_direct_optimum(capi, oracle_mod):
             lam *= 10
     st_o, _ = o.optimize(p.state_init, policy="lm", lambda0=10.0, max_iterations=200, eps_x=1e-12, eps_j=1e-12)
     assert np.abs(g.get_state() - st_o).max() < 1e-6
+
+
+# ---- KB_SOLVER_PCG_SCHUR: the same PCG on the camera-block Schur complement (frames eliminated exactly) ----
+def _np_schur_pcg(S, b, sizes, tolerance, max_iterations, absolute_tolerance=True, prev_residual=-1.0):
+    """numpy restatement of LinearSolverPCG::solve (linear_solver_pcg.hpp:58-130) on S x = b with the inverses of the
+    diagonal DV blocks of S as M (test checker)."""
+    C = S.shape[0]
+    M = np.zeros((C, C))
+    c = 0
+    for m in sizes:
+        M[c:c + m, c:c + m] = np.linalg.inv(S[c:c + m, c:c + m])
+        c += m
+    x = np.zeros(C)
+    r = b.copy()
+    z = M @ r
+    p = z.copy()
+    dn = r @ z
+    d0 = tolerance * dn
+    if absolute_tolerance and prev_residual > 0 and prev_residual > d0:
+        d0 = prev_residual
+    it = 0
+    while it < max_iterations and dn > d0:
+        q = S @ p
+        a = dn / (p @ q)
+        x += a * p
+        r -= a * q
+        z = M @ r
+        dnew = r @ z
+        p = z + (dnew / dn) * p
+        dn = dnew
+        it += 1
+    return x, dict(iterations=it, residual=0.5 * dn, d0=d0)
+
+
+def _schur_system(o, p, A, lam):
+    ok, Sp, bp = o.schur_partial(A, lam, 0, p.n_frames)
+    assert ok
+    S = A["Hcc"] - Sp + lam * lam * np.eye(o.C)
+    return S, A["gc"] - bp
+
+
+@pytest.mark.parametrize("name", list(PROBLEMS))
+@pytest.mark.parametrize("lam", [0.0, 10.0])
+def test_pcg_schur_first_iterations_match_numpy(capi, oracle_mod, name, lam):
+    """1 and 3 CG iterations on the Schur complement: camera dx and _residual against the numpy restatement on the
+    oracle's Schur complement; the frames back-substituted from that camera step as the direct solve does."""
+    p = PROBLEMS[name]()
+    o = oracle_mod.Oracle(p)
+    A = o.arrow(p.state_init)
+    S, b = _schur_system(o, p, A, lam)
+    sizes = oracle_mod.pcg_camera_blocks(p.cam_model)
+    g = capi.Solver(p)
+    g.set_state(p.state_init)
+    g.build()
+    g.set_constant_conditioner(lam)
+    for k in (1, 3):
+        g.set_linear_solver("pcg_schur", tolerance=1e-30, max_iterations=k)
+        ok, dx = g.solve()
+        x, info = _np_schur_pcg(S, b, sizes, 1e-30, k)
+        assert ok and g.pcg_info()["iterations"] == info["iterations"] == k
+        # S is summed in different orders on the two sides (~1e-12 apart); at lambda = 0 three CG steps amplify that
+        # to ~2e-9 on the worst conditioned rig (c6_small)
+        assert _rel(dx[:o.C], x) < (1e-9 if k == 1 else 1e-8), k
+        assert abs(g.pcg_info()["residual"] - info["residual"]) <= 1e-8 * abs(info["residual"])
+
+
+@pytest.mark.parametrize("name", ["c1", "c2_small", "c3_small", "c4_mid", "c6_small"])
+def test_pcg_schur_tight_equals_direct(capi, name):
+    """Converged tightly, the Schur-complement PCG gives the direct solve's dx (camera and frame columns)."""
+    p = PROBLEMS[name]()
+    g = capi.Solver(p)
+    g.set_state(p.state_init)
+    g.build()
+    g.set_constant_conditioner(10.0)
+    ok_d, dx_d = g.solve()
+    g.set_linear_solver("pcg_schur", tolerance=1e-28, max_iterations=4000, absolute_tolerance=False)
+    ok_p, dx_p = g.solve()
+    assert ok_d and ok_p
+    assert _rel(dx_p, dx_d) < 1e-8, g.pcg_info()
+
+
+@pytest.mark.parametrize("name", ["c1", "c2_small", "c4_mid"])
+def test_pcg_schur_defaults_contract(capi, oracle_mod, name):
+    """LinearSolverPCG defaults (tol 1e-6, absolute mode, maxIter = the camera rows): the same threshold d0 as the
+    numpy restatement, the stopping test met, iterations within 2 + 25 %; _residual carried into the next solve."""
+    p = PROBLEMS[name]()
+    o = oracle_mod.Oracle(p)
+    A = o.arrow(p.state_init)
+    S, b = _schur_system(o, p, A, 10.0)
+    sizes = oracle_mod.pcg_camera_blocks(p.cam_model)
+    g = capi.Solver(p)
+    g.set_state(p.state_init)
+    g.build()
+    g.set_constant_conditioner(10.0)
+    g.set_linear_solver("pcg_schur")
+    ok, dx = g.solve()
+    info = g.pcg_info()
+    _, ref = _np_schur_pcg(S, b, sizes, 1e-6, o.C)
+    assert ok
+    assert abs(info["d0"] - ref["d0"]) <= 1e-9 * abs(ref["d0"])
+    assert 2.0 * info["residual"] <= info["d0"] or info["iterations"] == o.C
+    assert abs(info["iterations"] - ref["iterations"]) <= 2 + 0.25 * ref["iterations"], (info, ref)
+    r1 = info["residual"]
+    ok2, _ = g.solve()  # absolute mode: d0 = max(tol dn0, the previous _residual)
+    assert ok2 and g.pcg_info()["d0"] >= r1 * (1 - 1e-12)

@@ -1,5 +1,5 @@
-"""Wall time of one kb_solve with the direct Schur solver vs the block-Jacobi PCG solver (LinearSolverPCG
-defaults, and converged tightly) at full configs[1] / configs[3] sizes on one GPU.  Host-timed around the
+"""Wall time of one kb_solve with the direct Schur solver vs the block-Jacobi PCG solvers (on the full system and on
+the camera-block Schur complement; LinearSolverPCG defaults, and converged tightly) at full configs[1] / configs[3] sizes on one GPU.  Host-timed around the
 C-ABI call (includes the launch and one stream sync); median of `reps` solves of the same built system.
 
 usage: python tools/pcg_bench.py [reps]   -> one JSON line per (config, solver)
@@ -36,9 +36,12 @@ def main():
         t_direct = med_time(g.solve, reps)
         print(json.dumps({"config": idx, "frames": p.n_frames, "C": p.cam_cols, "solver": "schur", "ok": ok,
                           "solve_us": round(t_direct * 1e6, 1)}), flush=True)
-        for label, kw in (("pcg_default", {}), ("pcg_tight", dict(tolerance=1e-24, max_iterations=50000,
-                                                                   absolute_tolerance=False))):
-            g.set_linear_solver("pcg", **kw)
+        for kind, label, kw in (("pcg", "pcg_default", {}),
+                                ("pcg", "pcg_tight", dict(tolerance=1e-24, max_iterations=50000, absolute_tolerance=False)),
+                                ("pcg_schur", "pcg_schur_default", {}),
+                                ("pcg_schur", "pcg_schur_tight", dict(tolerance=1e-24, max_iterations=50000,
+                                                                      absolute_tolerance=False))):
+            g.set_linear_solver(kind, **kw)
             ok, dx = g.solve()
             it = g.pcg_info()["iterations"]
             t = med_time(lambda: (g.pcg_init(), g.solve()), reps)
