@@ -323,9 +323,10 @@ void GpuLinearSystemSolver::initMatrixStructure(const CalibrationProblem& p, boo
         "kb_upload_observations");
   if ((int)p.state.size() != kb_state_size(h)) throw Exception("initMatrixStructure: state size mismatch");
   check(kb_set_state_flat(h, p.state.data()), "kb_set_state_flat");
-  if (_opt.linearSolver == "pcg") {
+  if (_opt.linearSolver == "pcg" || _opt.linearSolver == "pcg_schur") {
     kb_pcg_options po{_opt.pcgTolerance, _opt.pcgMaxIterations, _opt.pcgAbsoluteTolerance ? 1 : 0};
-    check(kb_set_linear_solver(h, KB_SOLVER_PCG, &po), "kb_set_linear_solver");
+    check(kb_set_linear_solver(h, _opt.linearSolver == "pcg" ? KB_SOLVER_PCG : KB_SOLVER_PCG_SCHUR, &po),
+          "kb_set_linear_solver");
   } else if (_opt.linearSolver != "schur") {
     throw Exception("GpuLinearSystemSolver: unknown linearSolver " + _opt.linearSolver);
   }

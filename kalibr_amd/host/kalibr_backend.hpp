@@ -191,7 +191,8 @@ class TermLinearSystemSolver : public LinearSystemSolver {
 // ---------------------------------------------------------------- GPU solver over the C-ABI
 /// linearSolver: "schur" (frame-block Schur + camera-block LDL^T, the exact CHOLMOD replacement, default) or
 /// "pcg" (sparse_block_matrix LinearSolverPCG: block-Jacobi PCG, linear_solver_pcg.hpp:58-130, with its
-/// defaults tolerance 1e-6 / maxIter = rows / absoluteTolerance, linear_solver_pcg.h:39-47).
+/// defaults tolerance 1e-6 / maxIter = rows / absoluteTolerance, linear_solver_pcg.h:39-47) or "pcg_schur" (the
+/// same PCG on the camera-block Schur complement, the frame blocks eliminated exactly).
 struct GpuOptions {
   int device = 0;
   std::string linearSolver = "schur";
@@ -219,7 +220,9 @@ class GpuLinearSystemSolver : public ProblemLinearSystemSolver {
   void setConditioner(const std::vector<double>& diag) override;
   bool solveSystem(std::vector<double>& outDx) override;
   std::string name() const override {
-    return _opt.linearSolver == "pcg" ? "kalibr_hip_block_jacobi_pcg" : "kalibr_hip_schur_cholesky";
+    return _opt.linearSolver == "pcg"         ? "kalibr_hip_block_jacobi_pcg"
+           : _opt.linearSolver == "pcg_schur" ? "kalibr_hip_schur_block_jacobi_pcg"
+                                              : "kalibr_hip_schur_cholesky";
   }
   const std::vector<double>& rhs() const override;
   double rhsJtJrhs() override;
