@@ -2372,7 +2372,7 @@ __device__ __forceinline__ bool panel_factor(const KbDev& d, double* S, double* 
   for (int c = 0; c < 16; ++c) KB_KEEP(row[c]);
 #endif
   if (q == 2 && fw == 0) KB_TS(d, 41);
-  panel_steps<0>(row, lane, q, C, ok, rd);
+  panel_steps<0>(row, lane, q, C, ok, rd);  // (row K through LDS instead of readlanes: 16 steps 1.36 -> 2.72 us)
 #ifdef KB_STAMPS
 #pragma unroll
   for (int c = 0; c < 16; ++c) KB_KEEP(row[c]);
