@@ -136,8 +136,11 @@ def main_spline(args):
     g.run_gn(args.steps)
     wall = time.perf_counter() - t0
     ks = g.kernel_stats(10)
-    achieved = ks["frames_bytes"] / (ks["frames_ms"] * 1e-3) / 1e9
-    pmc = pmc_traffic_bytes(lambda n: n.startswith("void ksp::k_sp_frames<"), 5)
+    # roofline: the pass's largest single launch, the node assembly (k_sp_assemble); the pass as a whole is bound by
+    # the cyclic reduction's dependent chain of small launches
+    asm_ms, asm_bytes = g.assemble_stats(10)
+    achieved = asm_bytes / (asm_ms * 1e-3) / 1e9
+    pmc = pmc_traffic_bytes(lambda n: n.startswith("ksp::k_sp_assemble("), 5)
     value = args.steps / wall
     out = {
         "metric": METRIC, "value": value, "unit": "iterations/s", "n_gpus": 1, "steps": args.steps,
@@ -147,11 +150,12 @@ def main_spline(args):
                    "frames": p.n_frames, "cameras": p.n_cams, "corners": p.n_corners, "imu_samples": p.n_imu,
                    "spline_coefficients": p.n_coeffs, "jacobian_cols": p.total_cols, "camera_block": p.cam_cols,
                    "policy": "gauss_newton", "parallelism": "single GPU"},
-        "roofline": {"bound": "hbm", "kernel": "k_sp_frames", "achieved": achieved, "peak": HBM_PEAK_GBS,
+        "roofline": {"bound": "hbm", "kernel": "k_sp_assemble", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": (pmc[0] / (ks["frames_ms"] * 1e-3) / 1e9) if pmc else None,
+                     "traffic": (pmc[0] / (asm_ms * 1e-3) / 1e9) if pmc else None,
                      "traffic_bytes_per_launch": pmc[0] if pmc else None, "traffic_source": pmc[1] if pmc else None,
-                     "avg_ms": ks["frames_ms"], "algorithmic_bytes": ks["frames_bytes"]},
+                     "avg_ms": asm_ms, "algorithmic_bytes": asm_bytes,
+                     "frames_kernel": {"avg_ms": ks["frames_ms"], "algorithmic_bytes": ks["frames_bytes"]}},
         "pass_breakdown_ms": {k: v for k, v in ks.items() if k.endswith("_ms")},
     }
     if not args.no_cpu_baseline:

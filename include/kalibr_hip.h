@@ -304,6 +304,9 @@ int kb_sp_run_gn_iterations(kb_sp_handle* h, int32_t n_iter, double* seconds);
  * out[0] frames kernel, [1] assemble, [2] cyclic reduction (all levels), [3] Schur + camera solve,
  * [4] update + cost, [5] whole pass; bytes[0] algorithmic bytes of the frames kernel per launch. */
 int kb_sp_kernel_stats(kb_sp_handle* h, int32_t n, double* ms_out6, double* frames_bytes);
+/* Device time (ms, HIP events around each launch on the handle's stream, averaged over n launches inside built
+ * passes) and algorithmic bytes per launch of the node-assembly kernel (the pass's largest single launch). */
+int kb_sp_assemble_stats(kb_sp_handle* h, int32_t n, double* ms, double* bytes);
 
 #ifdef __cplusplus
 }

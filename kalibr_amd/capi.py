@@ -31,7 +31,7 @@ EXPORTS = [
     "kb_sp_create", "kb_sp_destroy", "kb_sp_upload", "kb_sp_state_size", "kb_sp_num_cols", "kb_sp_camera_cols",
     "kb_sp_set_state", "kb_sp_get_state", "kb_sp_eval_cost", "kb_sp_build", "kb_sp_set_constant_conditioner",
     "kb_sp_solve", "kb_sp_get_rhs", "kb_sp_apply_update", "kb_sp_revert", "kb_sp_get_system", "kb_sp_optimize",
-    "kb_sp_get_trace", "kb_sp_run_gn_iterations", "kb_sp_kernel_stats", "kb_sp_set_motion_error",
+    "kb_sp_get_trace", "kb_sp_run_gn_iterations", "kb_sp_kernel_stats", "kb_sp_assemble_stats", "kb_sp_set_motion_error",
 ]
 
 
@@ -156,6 +156,7 @@ def lib():
         L.kb_sp_get_trace.argtypes = [C.c_void_p, dp, C.c_int32]
         L.kb_sp_run_gn_iterations.argtypes = [C.c_void_p, C.c_int32, dp]
         L.kb_sp_kernel_stats.argtypes = [C.c_void_p, C.c_int32, dp, dp]
+        L.kb_sp_assemble_stats.argtypes = [C.c_void_p, C.c_int32, dp, dp]
         L.kb_sp_set_motion_error.argtypes = [C.c_void_p, dp, C.c_int32]
         _lib = L
     return _lib
@@ -490,3 +491,9 @@ class SplineSolver:
         _check(lib().kb_sp_kernel_stats(self.h, int(n), _d(ms), C.byref(fb)))
         return dict(frames_ms=ms[0], assemble_ms=ms[1], reduction_ms=ms[2], camsolve_ms=ms[3], update_cost_ms=ms[4],
                     pass_ms=ms[5], frames_bytes=fb.value)
+
+    def assemble_stats(self, n=10):
+        """(ms per launch, algorithmic bytes per launch) of the node-assembly kernel k_sp_assemble"""
+        ms, b = C.c_double(), C.c_double()
+        _check(lib().kb_sp_assemble_stats(self.h, int(n), C.byref(ms), C.byref(b)))
+        return ms.value, b.value

@@ -2887,6 +2887,40 @@ int kb_sp_run_gn_iterations(kb_sp_handle* h, int32_t n_iter, double* seconds) {
   return 0;
 }
 
+int kb_sp_assemble_stats(kb_sp_handle* h, int32_t n, double* ms, double* bytes) {
+  if (!h || !ms || !bytes || n < 1) return fail("kb_sp_assemble_stats: bad arguments");
+  if (!h->uploaded) return fail("kb_sp_assemble_stats: upload observations first");
+  KSP_HIP(hipSetDevice(h->device));
+  SpDev& d = h->d;
+  void* args[] = {&d};
+  hipEvent_t e0, e1;
+  KSP_HIP(hipEventCreate(&e0));
+  KSP_HIP(hipEventCreate(&e1));
+  double acc = 0.0;
+  for (int it = -1; it < n; ++it) {  // it = -1: warm-up
+    hipLaunchKernelGGL(k_sp_set_lam, dim3(1), dim3(64), 0, h->stream, d, 0.0);
+    KSP_HIP(hipLaunchKernel(h->fn_frames, dim3(d.nblk_f), dim3(64 * h->N), args, h->lds_frames, h->stream));
+    hipLaunchKernelGGL(k_sp_imu_cc, dim3(d.nblk_ic), dim3(64), 0, h->stream, d);
+    KSP_HIP(hipEventRecord(e0, h->stream));
+    KSP_HIP(hipLaunchKernel((const void*)k_sp_assemble, dim3(d.n), dim3(256), args, h->lds_asm, h->stream));
+    KSP_HIP(hipEventRecord(e1, h->stream));
+    KSP_HIP(hipStreamSynchronize(h->stream));
+    float t = 0.0f;
+    KSP_HIP(hipEventElapsedTime(&t, e0, e1));
+    if (it >= 0) acc += t;
+  }
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  *ms = acc / n;
+  // algorithmic bytes, each once: the frames' spline blocks (FHS doubles) with their basis (4 weights + index), the
+  // IMU samples (12 weights, 6 measurements, index), the coefficients and camera / IMU state, the node tables, the
+  // node blocks D0, U0, R0 written (+ the motion-error blocks when active)
+  *bytes = 8.0 * h->F * (d.FHS + 4) + 4.0 * h->F + h->M * (8.0 * 18 + 4.0) + 8.0 * d.S + 16.0 * h->n +
+           8.0 * h->n * (2 * NB * NB + NB * d.m) + (d.mot ? 8.0 * h->n * 2 * NB * NB : 0.0);
+  h->built = h->solved = false;
+  return 0;
+}
+
 int kb_sp_kernel_stats(kb_sp_handle* h, int32_t n, double* ms_out6, double* frames_bytes) {
   if (!h || !ms_out6 || n < 1) return fail("kb_sp_kernel_stats: bad arguments");
   if (!h->uploaded) return fail("kb_sp_kernel_stats: upload observations first");
