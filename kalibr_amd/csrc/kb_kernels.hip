@@ -2971,39 +2971,36 @@ __device__ bool schur_pcg(const KbDev& d, SGet sget, const double* b, int C, int
   };
   if (tid == 0) blk_ok = 1;
   __syncthreads();
-  // preconditioner: one thread per DV block inverts its m x m diagonal block of S (Gauss-Jordan, partial pivoting)
+  // preconditioner: one thread per DV block inverts its m x m diagonal block of S in place in its Minv rows (LDS):
+  // Gauss-Jordan without pivoting (the block is SPD); no private array, so k_solve needs no scratch
   for (int p = tid; p < C; p += nth) {
     const int s0 = d.pcs_cb[p], m = d.pcs_cb[C + p];
     if (s0 != p) continue;
-    double A[6][12];
+    double(*A)[6] = Minv + p;  // rows p .. p + m - 1
     for (int r = 0; r < m; ++r)
-      for (int c = 0; c < 2 * m; ++c) A[r][c] = c < m ? sget(p + r, p + c) : (c - m == r ? 1.0 : 0.0);
+      for (int c = 0; c < 6; ++c) A[r][c] = c < m ? sget(p + r, p + c) : 0.0;
     bool good = true;
-    for (int k = 0; k < m && good; ++k) {
-      int piv = k;
-      for (int r = k + 1; r < m; ++r)
-        if (fabs(A[r][k]) > fabs(A[piv][k])) piv = r;
-      if (!(fabs(A[piv][k]) > 0.0)) {
+    for (int k = 0; k < m; ++k) {
+      const double piv = A[k][k];
+      if (!(piv > 0.0)) {
         good = false;
         break;
       }
-      if (piv != k)
-        for (int c = 0; c < 2 * m; ++c) {
-          const double t = A[k][c];
-          A[k][c] = A[piv][c];
-          A[piv][c] = t;
-        }
-      const double inv = 1.0 / A[k][k];
-      for (int c = 0; c < 2 * m; ++c) A[k][c] *= inv;
+      const double inv = 1.0 / piv;
+      A[k][k] = 1.0;
+      for (int c = 0; c < m; ++c) A[k][c] *= inv;
       for (int r = 0; r < m; ++r) {
         if (r == k) continue;
         const double f = A[r][k];
-        for (int c = 0; c < 2 * m; ++c) A[r][c] -= f * A[k][c];
+        A[r][k] = 0.0;
+        for (int c = 0; c < m; ++c) A[r][c] -= f * A[k][c];
       }
     }
-    if (!good) blk_ok = 0;
-    for (int r = 0; r < m; ++r)
-      for (int c = 0; c < 6; ++c) Minv[p + r][c] = (good && c < m) ? A[r][m + c] : 0.0;
+    if (!good) {
+      blk_ok = 0;
+      for (int r = 0; r < m; ++r)
+        for (int c = 0; c < 6; ++c) A[r][c] = 0.0;
+    }
   }
   for (int i = tid; i < 128; i += nth) {
     v_x[i] = 0.0;

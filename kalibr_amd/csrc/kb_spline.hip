@@ -115,6 +115,16 @@ struct SpDev {
 };
 
 typedef double v4d_t __attribute__((ext_vector_type(4)));
+
+// a per-camera kernel-argument array read at a run-time index, by selects: a dynamic index into a kernel argument
+// makes the compiler copy the array into per-lane scratch (k_sp_frames: 160 B per lane, ~11 MB of scratch writes per
+// launch at configs[4])
+__device__ __forceinline__ int sp_cam_arg(const int (&a)[KB_MAX_CAMS], int i) {
+  int v = a[0];
+#pragma unroll
+  for (int k = 1; k < KB_MAX_CAMS; ++k) v = (i == k) ? a[k] : v;
+  return v;
+}
 #define KSP_WAVE_SYNC() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
 
 // ---------------------------------------------------------------- batched staging
@@ -314,7 +324,7 @@ __global__ void __launch_bounds__(512) k_sp_frames(SpDev d) {
     tA[2] = t2[2];
   }
   __syncthreads();  // target, accumulators and Gp staged
-  const int model = d.model[cam], nin = d.nin[cam];
+  const int model = sp_cam_arg(d.model, cam), nin = sp_cam_arg(d.nin, cam);
   const double* intr = st + cam * KB_MAX_INTR;
   const int mrow = lane >> 4, mcol = lane & 15;
   const int f0 = blockIdx.x * FPB, f1 = min(d.F, f0 + FPB);
@@ -337,42 +347,47 @@ __global__ void __launch_bounds__(512) k_sp_frames(SpDev d) {
         R[r * 3 + c] = RA[r * 3 + 0] * Rwb[c * 3 + 0] + RA[r * 3 + 1] * Rwb[c * 3 + 1] + RA[r * 3 + 2] * Rwb[c * 3 + 2];
 #pragma unroll
     for (int r = 0; r < 3; ++r) t[r] = tA[r] - (R[r * 3 + 0] * v[0] + R[r * 3 + 1] * v[1] + R[r * 3 + 2] * v[2]);
-    // G_v = -boxTimes(T_cam_w) JT, JT = [I, -[p]x S; 0, S]
-    if (lane < 36) {
+    // G_v = -boxTimes(T_cam_w) JT, JT = [I, -[p]x S; 0, S], all 36 entries by lane 0 with compile-time indices (a
+    // lane-per-entry form indexes R, S and [t]x at run time, which puts those arrays in per-lane scratch)
+    if (lane == 0) {
       double S[9];
       rv_S(v + 3, S);
-      const int r = lane / 6, c = lane % 6;
       const double tx[9] = {0, -t[2], t[1], t[2], 0, -t[0], -t[1], t[0], 0};
       const double px[9] = {0, -v[2], v[1], v[2], 0, -v[0], -v[1], v[0], 0};
-      double JTc[6];  // column c of JT
+      double JT[6][6], BT[6][6];
 #pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        if (c < 3) {
-          JTc[k] = (k == c) ? 1.0 : 0.0;
-          JTc[3 + k] = 0.0;
-        } else {
-          const int cc = c - 3;
-          JTc[k] = -(px[k * 3 + 0] * S[0 * 3 + cc] + px[k * 3 + 1] * S[1 * 3 + cc] + px[k * 3 + 2] * S[2 * 3 + cc]);
-          JTc[3 + k] = S[k * 3 + cc];
-        }
-      }
-      double s = 0.0;
+      for (int k = 0; k < 3; ++k)
 #pragma unroll
-      for (int k = 0; k < 6; ++k) {
-        double bt;  // boxTimes(R, t)[r][k]
-        if (r < 3) {
-          if (k < 3) {
-            bt = R[r * 3 + k];
+        for (int c = 0; c < 6; ++c) {
+          if (c < 3) {
+            JT[k][c] = (k == c) ? 1.0 : 0.0;
+            JT[3 + k][c] = 0.0;
           } else {
-            const int kk = k - 3;
-            bt = -(tx[r * 3 + 0] * R[0 * 3 + kk] + tx[r * 3 + 1] * R[1 * 3 + kk] + tx[r * 3 + 2] * R[2 * 3 + kk]);
+            const int cc = c - 3;
+            JT[k][c] = -(px[k * 3 + 0] * S[0 * 3 + cc] + px[k * 3 + 1] * S[1 * 3 + cc] + px[k * 3 + 2] * S[2 * 3 + cc]);
+            JT[3 + k][c] = S[k * 3 + cc];
           }
-        } else {
-          bt = (k < 3) ? 0.0 : R[(r - 3) * 3 + (k - 3)];
         }
-        s += bt * JTc[k];
-      }
-      Gv[cam * 36 + lane] = -s;
+#pragma unroll
+      for (int r = 0; r < 6; ++r)
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {  // boxTimes(R, t)[r][k]
+          if (r < 3)
+            BT[r][k] = k < 3 ? R[r * 3 + k]
+                             : -(tx[r * 3 + 0] * R[0 * 3 + k - 3] + tx[r * 3 + 1] * R[1 * 3 + k - 3] +
+                                 tx[r * 3 + 2] * R[2 * 3 + k - 3]);
+          else
+            BT[r][k] = k < 3 ? 0.0 : R[(r - 3) * 3 + (k - 3)];
+        }
+#pragma unroll
+      for (int r = 0; r < 6; ++r)
+#pragma unroll
+        for (int c = 0; c < 6; ++c) {
+          double s = 0.0;
+#pragma unroll
+          for (int k = 0; k < 6; ++k) s += BT[r][k] * JT[k][c];
+          Gv[cam * 36 + r * 6 + c] = -s;
+        }
     }
     // corners of view (f, cam): [J_delta | J_intr | -e] rows, SYRK on MFMA
     const int2 fv = d.fview[(size_t)f * N + cam];
@@ -1777,7 +1792,7 @@ __global__ void __launch_bounds__(512) k_sp_cost_frames(SpDev d) {
     tA[1] = t2[1];
     tA[2] = t2[2];
   }
-  const int model = d.model[cam];
+  const int model = sp_cam_arg(d.model, cam);
   const double* intr = st + cam * KB_MAX_INTR;
   double s = 0.0;
   const int f0 = blockIdx.x * FPB, f1 = min(d.F, f0 + FPB);
