@@ -89,33 +89,23 @@ __device__ __forceinline__ bool pcg_barrier(unsigned* bar, unsigned nblk, unsign
   return *lds_flag == 0;
 }
 
-// in-place inverse of an m x m block (row stride ld) by Gauss-Jordan with partial pivoting; false if singular
+// in-place inverse of an m x m diagonal DV block (row stride ld, in LDS) by Gauss-Jordan without pivoting: the blocks
+// are diagonal blocks of the PSD system, so a zero pivot means a singular block (false).  No private array: a
+// run-time sized one would put the kernel in per-lane scratch.
 __device__ bool pcg_block_inverse(double* M, int m, int ld) {
-  double A[6][12];
-  for (int r = 0; r < m; ++r)
-    for (int c = 0; c < 2 * m; ++c) A[r][c] = c < m ? M[r * ld + c] : (c - m == r ? 1.0 : 0.0);
   for (int k = 0; k < m; ++k) {
-    int piv = k;
-    for (int r = k + 1; r < m; ++r)
-      if (fabs(A[r][k]) > fabs(A[piv][k])) piv = r;
-    if (!(fabs(A[piv][k]) > 0.0)) return false;
-    if (piv != k)
-      for (int c = 0; c < 2 * m; ++c) {
-        const double t = A[k][c];
-        A[k][c] = A[piv][c];
-        A[piv][c] = t;
-      }
-    const double inv = 1.0 / A[k][k];
-    for (int c = 0; c < 2 * m; ++c) A[k][c] *= inv;
+    const double piv = M[k * ld + k];
+    if (!(fabs(piv) > 0.0)) return false;
+    const double inv = 1.0 / piv;
+    M[k * ld + k] = 1.0;
+    for (int c = 0; c < m; ++c) M[k * ld + c] *= inv;
     for (int r = 0; r < m; ++r) {
       if (r == k) continue;
-      const double f = A[r][k];
-      if (f != 0.0)
-        for (int c = 0; c < 2 * m; ++c) A[r][c] -= f * A[k][c];
+      const double f = M[r * ld + k];
+      M[r * ld + k] = 0.0;
+      for (int c = 0; c < m; ++c) M[r * ld + c] -= f * M[k * ld + c];
     }
   }
-  for (int r = 0; r < m; ++r)
-    for (int c = 0; c < m; ++c) M[r * ld + c] = A[r][m + c];
   return true;
 }
 
@@ -248,12 +238,10 @@ __global__ void __launch_bounds__(kPcgThreads) k_pcg(KbDev d, KbPcg P) {
   for (int p = tid; p < C; p += blockDim.x) {
     if (cbs[p] != p) continue;  // one thread per camera DV block (its first column)
     const int m = cbm[p];
-    double M[36];
+    double* M = Mc + p * 6;  // rows p .. p + m - 1 of Mc, inverted in place (stride 6)
     for (int r = 0; r < m; ++r)
-      for (int c = 0; c < m; ++c) M[r * m + c] = d.Hcc[(size_t)(p + r) * C + p + c] + (r == c ? lam2 : 0.0);
-    if (!pcg_block_inverse(M, m, m)) sh_scalar[0] = 0.0;
-    for (int r = 0; r < m; ++r)
-      for (int c = 0; c < 6; ++c) Mc[(p + r) * 6 + c] = c < m ? M[r * m + c] : 0.0;
+      for (int c = 0; c < 6; ++c) M[r * 6 + c] = c < m ? d.Hcc[(size_t)(p + r) * C + p + c] + (r == c ? lam2 : 0.0) : 0.0;
+    if (!pcg_block_inverse(M, m, 6)) sh_scalar[0] = 0.0;
   }
   __syncthreads();
   // s = M^-1 r (frame rows and camera entries of this block)
