@@ -978,7 +978,7 @@ __device__ __forceinline__ double ksp_recip(double x) {
 // one-wave register Cholesky of an 18 x 18 SPD matrix held in LDS (lower, row-major): lane r keeps row r in
 // registers, column k broadcast by v_readlane; the factor is written back.  Returns false if not positive
 // definite.  Call from one whole wave.
-__device__ bool chol18_wave(double* A, double* id, int lane) {
+__device__ __forceinline__ bool chol18_wave(double* A, double* id, int lane) {
   double a[NB];
 #pragma unroll
   for (int c = 0; c < NB; ++c) a[c] = lane < NB ? A[lane * NB + c] : 0.0;
