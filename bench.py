@@ -43,6 +43,8 @@ def is_build_kernel(name):
     return False
 FRAMES_PER_RANK = 500
 HBM_PEAK_GBS = 8000.0
+# FP64 dense peak of one MI355X (vector FMA and f64 MFMA run at the same rate: 256 CU x 4 SIMD x 32 flop/clk x 2.4 GHz)
+FP64_PEAK_TFS = 78.6
 
 
 def pmc_traffic_bytes(match, config):
@@ -174,6 +176,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--comm", action="store_true",
                     help="N=1 through the multi-GPU path: rendezvous, a one-rank RCCL communicator, captured RCCL")
+    ap.add_argument("--shard-of", type=int, default=0, metavar="K",
+                    help="one GPU runs rank 0's shard of a K-way split (configs[3] / configs[2]: ceil(F / K) frames) "
+                         "through a one-rank RCCL communicator: the per-rank pass of the K-GPU run (not a headline)")
     args = ap.parse_args()
     if args.config == 5:
         if args.gpus != 1:
@@ -185,6 +190,8 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.gpus > 1 and world != args.gpus:
         raise SystemExit("for --gpus N>1 launch with torch.distributed.run --nproc-per-node N")
+    if args.shard_of and (world != 1 or args.config not in (3, 4)):
+        raise SystemExit("--shard-of K: one process, configs[2] / configs[3] (--config 3 | 4)")
 
     from kalibr_amd import build as B
     from kalibr_amd import capi, rdzv, synth
@@ -193,7 +200,7 @@ def main():
 
     # host rendezvous over stdlib TCP (RCCL id broadcast, barriers, max of the wall time): no torch in this process,
     # so the library's /opt/rocm HIP runtime and RCCL are the only ones loaded
-    use_comm = world > 1 or args.comm
+    use_comm = world > 1 or args.comm or args.shard_of > 0
     grp = rdzv.TcpGroup(rank, world) if use_comm else None
     # the JSON line must be the only stdout output: native banners (RCCL prints its version at init) go to stderr
     sys.stdout.flush()
@@ -208,7 +215,9 @@ def main():
         full = synth.make_problem(synth.CONFIGS[2]["models"], FRAMES_PER_RANK * world, seed=20261015 + 2,
                                   name=synth.CONFIGS[2]["name"])
         fpr = FRAMES_PER_RANK
-    shard = full.frame_slice(rank * fpr, min(full.n_frames, (rank + 1) * fpr)) if world > 1 else full
+    if args.shard_of:  # rank 0's slice of a shard_of-way split, on this one GPU
+        fpr = (full.n_frames + args.shard_of - 1) // args.shard_of
+    shard = full.frame_slice(rank * fpr, min(full.n_frames, (rank + 1) * fpr)) if (world > 1 or args.shard_of) else full
     g = capi.Solver(shard, device=local)
     g.set_state(shard.state_init)
     if use_comm:  # --comm at N=1: the same launcher + RCCL path with a one-rank communicator
@@ -231,11 +240,16 @@ def main():
     if grp:
         wall = grp.max(wall)
 
-    # dominant kernel (the build) timing with HIP events on the handle's stream, inside GN passes
+    # dominant kernel (the build) timing with HIP events on the handle's stream, inside GN passes; the per-pass device
+    # time of iterations 1..20 from HIP events at every pass start inside one captured graph (the
+    # median of iterations 2..20, iteration 1 reported on its own)
     build_ms, bytes_per, flops_per = g.build_kernel_stats()
     kname = g.build_kernel_name()
+    pass_ms, _ = g.gn_pass_times(20)
+    pass_med = float(np.median(pass_ms[1:]))
     achieved = bytes_per / (build_ms * 1e-3) / 1e9
-    pmc = pmc_traffic_bytes(is_build_kernel, args.config) if world == 1 else None  # summaries are of N=1 runs
+    useful_tfs = flops_per / (build_ms * 1e-3) / 1e12
+    pmc = pmc_traffic_bytes(is_build_kernel, args.config) if (world == 1 and not args.shard_of) else None
 
     sys.stdout.flush()
     os.dup2(stdout_fd, 1)
@@ -248,6 +262,10 @@ def main():
                     3: "configs[2]: 4-cam 2x omni-radtan + 2x EUCM rig, 1000 frames (sharded over the GPUs when N>1), "
                        "6x5 AprilGrid, p_view=1",
                     2: "configs[1]: 2-cam stereo pinhole-radtan, 500 frames/GPU, 6x5 AprilGrid, p_view=1"}[args.config]
+        if args.shard_of:
+            workload = (f"rank 0's shard of a {args.shard_of}-way split of " + workload.split(":")[0] +
+                        f" ({shard.n_frames} of {full.n_frames} frames, all-reduce over a one-rank RCCL communicator): "
+                        "the per-rank pass of the multi-GPU run, not a headline line")
         out = {
             "metric": METRIC, "value": value, "unit": "iterations/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": 1e3 * wall / args.steps, "higher_is_better": True,
@@ -256,13 +274,21 @@ def main():
                        "frames_per_gpu": shard.n_frames, "cameras": full.n_cams, "corners_per_gpu": shard.n_corners,
                        "jacobian_cols": full.total_cols, "camera_block": full.cam_cols, "policy": "gauss_newton",
                        "parallelism": f"frame-sharded x{world}"},
-            "roofline": {"bound": "hbm", "kernel": kname, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": (pmc[0] / (build_ms * 1e-3) / 1e9) if pmc else None,
-                         "traffic_bytes_per_launch": pmc[0] if pmc else None,
-                         "traffic_source": pmc[1] if pmc else None,
-                         "avg_ms": build_ms, "algorithmic_bytes": bytes_per,
-                         "fp64_tflops": flops_per / (build_ms * 1e-3) / 1e12},
+            # the build kernel's arithmetic intensity (SURVEY 8(d) flops / algorithmic bytes, ~28 flop/B at configs[3])
+            # is above the FP64 ridge (78.6 TF/s / 8 TB/s ~ 9.8 flop/B): its roofline is the FP64 pipe, and its SQ
+            # counters put it below that, issue/latency-bound on VALU work.  The HBM view is kept beside.
+            "roofline": {"bound": "mfma", "kernel": kname, "achieved": useful_tfs, "peak": FP64_PEAK_TFS,
+                         "unit": "TFLOP/s", "frac": useful_tfs / FP64_PEAK_TFS,
+                         "traffic": pmc[0] if pmc else None, "traffic_source": pmc[1] if pmc else None,
+                         "avg_ms": build_ms, "algorithmic_flops": flops_per, "algorithmic_bytes": bytes_per,
+                         "arithmetic_intensity": flops_per / bytes_per,
+                         "limiter": "FP64 VALU issue and the per-frame dependency chain (SQ counters, DESIGN.md 6)",
+                         "hbm": {"achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                 "frac": achieved / HBM_PEAK_GBS,
+                                 "traffic_gbs": (pmc[0] / (build_ms * 1e-3) / 1e9) if pmc else None}},
+            "per_pass_median_ms": pass_med, "first_pass_ms": float(pass_ms[0]),
+            "per_pass_ms": [round(float(x), 5) for x in pass_ms],
+            "useful_fp64_tflops": flops_per / (pass_med * 1e-3) / 1e12,
             "library_seconds": sec,
             "comm": {"rccl": bool(use_comm), "ranks": world, "rendezvous": "stdlib TCP" if use_comm else None,
                      "graphed": int(graphed)},

@@ -111,6 +111,10 @@ int kb_solve(kb_handle* h, double* dx_out, int* ok);
  *                    PCG (same options, stopping rule and _residual semantics) on the C x C camera-block Schur
  *                    complement instead of its LDL^T, the frames back-substituted from that camera step.  One
  *                    block, ~1 us per iteration; a different iterate sequence than KB_SOLVER_PCG's full-system CG.
+ *                    Sharded handles are supported: every rank runs the same PCG on the all-reduced S, b, so all
+ *                    ranks hold bitwise-identical camera steps, iteration counts and _residual; each rank then
+ *                    back-substitutes its own frames.  _residual (and kb_get_pcg_info) are updated only by a
+ *                    completed solve: a failed one (*ok = 0) leaves the previous values for the next d0.
  * kb_optimize always uses the direct solve (its passes are captured graphs); the per-call path
  * (kb_build / kb_solve / kb_apply_update, driven by the host Optimizer2) uses the selected solver. */
 enum kb_linear_solver { KB_SOLVER_SCHUR = 0, KB_SOLVER_PCG = 1, KB_SOLVER_PCG_SCHUR = 2 };
@@ -134,7 +138,8 @@ int kb_get_pcg_info(kb_handle* h, kb_pcg_info* info);
 int kb_get_rhs(kb_handle* h, double* rhs_out);
 /* LinearSystemSolver::rhsJtJrhs (LinearSystemSolver.hpp:66-69): rhs^T (J^T J) rhs of the last kb_build (the reference
  * forms ||J rhs||^2, SparseCholeskyLinearSystemSolver.cpp:106-111; DogLeg / steepest descent), on the device from
- * the arrow blocks.  Unsharded handles. */
+ * the arrow blocks.  Unsharded handles.  Fails unless the last system came from kb_build: the device-resident
+ * loops (kb_optimize, kb_gn_*, kb_build_kernel_stats) overwrite or skip the per-call blocks it reads. */
 int kb_rhs_jtj_rhs(kb_handle* h, double* out);
 /* Optimizer2::applyStateUpdate / revertLastStateUpdate (Optimizer2.cpp:290-318).
  * dx == NULL applies the device-resident dx of the last kb_solve. */
@@ -171,7 +176,8 @@ int kb_analyze_marginal(kb_handle* h, const kb_marginal_options* opts, kb_margin
                         double* V_out);
 
 /* Normal-equation blocks of the last kb_build, for parity tests:
- * Hff [F][6][6], Hfc [F][6][C], gf [F][6], Hcc [C][C], gc [C], cost (chi^2 at build state). */
+ * Hff [F][6][6], Hfc [F][6][C], gf [F][6], Hcc [C][C], gc [C], cost (chi^2 at build state).  Fails after a
+ * device-resident loop until the next kb_build (as kb_rhs_jtj_rhs). */
 int kb_get_normal_blocks(kb_handle* h, double* Hff, double* Hfc, double* gf, double* Hcc, double* gc,
                          double* cost);
 
@@ -209,13 +215,23 @@ int kb_run_gn_iterations(kb_handle* h, int32_t n_iter, double* seconds);
  * every graph n_iter passes will launch, then a stream sync; kb_gn_launch = the n_iter passes and the last
  * pass's end between two stream syncs (*seconds = that wall time).  Same passes, same results.
  * kb_gn_prepare returns 1 when the passes will run as captured hipGraphs (RCCL calls included when sharded),
- * 0 when they run eagerly, < 0 on error. */
+ * 0 when they run eagerly, < 0 on error.  Any call that changes the state, the control block or the graphs in
+ * between (state setters, per-call entry points, kb_optimize, kb_comm_init, ...) voids the preparation:
+ * kb_gn_launch then fails instead of running from a stale loop start. */
 int kb_gn_prepare(kb_handle* h, int32_t n_iter);
 int kb_gn_launch(kb_handle* h, int32_t n_iter, double* seconds);
 /* Average device duration (ms) of the build kernel inside Gauss-Newton passes (runs 22 passes from the
- * current state, HIP events around each build launch on the handle's stream); algorithmic bytes and
- * flops per build launch.  The state, camera chains and control block are restored afterwards. */
+ * current state, HIP events around each build launch on the handle's stream); algorithmic bytes per build launch and
+ * the pass's algorithmic FP64 flops (projection + Jacobian, cost and local Hessian per corner, the
+ * 6-D chain expansion per view, the Schur sums per frame; not the padded MFMA work the kernel executes).  The state,
+ * camera chains and control block are restored afterwards. */
 int kb_build_kernel_stats(kb_handle* h, double* avg_ms, double* bytes_per_launch, double* flops_per_launch);
+/* Per-pass device timing of n Gauss-Newton passes from the current state (iteration 1 = the first pass after the
+ * loop start): HIP events at every pass start and around every build kernel, captured in one graph with the passes,
+ * on the handle's stream.  pass_ms [n] (pass r: from its start to the next pass's start), build_ms [n] (either may be
+ * NULL).  A query: the state, camera chains and control block are restored afterwards.  Unsharded handles time the
+ * graph; sharded ones run the passes eagerly. */
+int kb_gn_pass_times(kb_handle* h, int32_t n, double* pass_ms, double* build_ms);
 /* Name of the build kernel this handle launches ("k_buildp" or "k_build") into buf (NUL-terminated). */
 int kb_build_kernel_name(kb_handle* h, char* buf, int32_t cap);
 

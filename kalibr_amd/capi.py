@@ -23,7 +23,7 @@ EXPORTS = [
     "kb_get_state_flat", "kb_state_size", "kb_num_cols", "kb_camera_cols", "kb_eval_cost", "kb_build",
     "kb_set_constant_conditioner", "kb_set_conditioner", "kb_solve", "kb_get_rhs", "kb_rhs_jtj_rhs", "kb_apply_update", "kb_revert", "kb_get_normal_blocks",
     "kb_optimize", "kb_get_trace", "kb_run_gn_iterations", "kb_gn_prepare", "kb_gn_launch", "kb_build_kernel_stats",
-    "kb_build_kernel_name", "kb_comm_get_unique_id",
+    "kb_build_kernel_name", "kb_comm_get_unique_id", "kb_gn_pass_times",
     "kb_comm_init", "kb_comm_init_local", "kb_selftest_mfma", "kb_solve_marginal", "kb_analyze_marginal",
     # block-Jacobi PCG (LinearSolverPCG)
     "kb_set_linear_solver", "kb_pcg_init", "kb_get_pcg_info",
@@ -127,6 +127,7 @@ def lib():
         L.kb_gn_launch.argtypes = [C.c_void_p, C.c_int32, dp]
         L.kb_build_kernel_name.argtypes = [C.c_void_p, C.c_char_p, C.c_int32]
         L.kb_build_kernel_stats.argtypes = [C.c_void_p, dp, dp, dp]
+        L.kb_gn_pass_times.argtypes = [C.c_void_p, C.c_int32, dp, dp]
         L.kb_comm_get_unique_id.argtypes = [C.c_void_p]
         L.kb_comm_init.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32]
         L.kb_comm_init_local.argtypes = [C.POINTER(C.c_void_p), C.c_int32]
@@ -356,6 +357,12 @@ class Solver:
         ms, by, fl = C.c_double(), C.c_double(), C.c_double()
         _check(lib().kb_build_kernel_stats(self.h, C.byref(ms), C.byref(by), C.byref(fl)))
         return ms.value, by.value, fl.value
+
+    def gn_pass_times(self, n):
+        """(pass_ms [n], build_ms [n]) of n GN passes from the current state, device-timed (kb_gn_pass_times)"""
+        pm, bm = np.zeros(n), np.zeros(n)
+        _check(lib().kb_gn_pass_times(self.h, int(n), _d(pm), _d(bm)))
+        return pm, bm
 
     def comm_init(self, uid: bytes, nranks, rank):
         buf = C.create_string_buffer(uid, 128)

@@ -56,6 +56,7 @@ int nintr_host(int m) {
 }  // namespace
 
 constexpr int kGraphPasses = 8;  // optimizer passes per captured multi-pass graph
+constexpr int kXMaxRanks = 64;   // expanded partials: per-rank max|dx_f| slots in the image's aux area
 constexpr int kLocalMaxRanks = 16;  // kb_comm_init_local group size
 
 // In-process group of sharded handles (kb_comm_init_local): the collectives become device copies between the
@@ -114,9 +115,15 @@ struct kb_handle {
   int N = 0, F = 0, K = 0, V = 0, NC = 0, C = 0, ncols = 0, S = 0, W = 0;
   int WPB = 1;
   bool build_pipe = false;  // k_buildp (one wave per camera, N + 2 waves) instead of k_build
+  bool xexp = false;        // GN fused passes with expanded partials (C > 64, k_buildp): k_colsumx, no k_colimg
+  std::vector<int32_t> vcam;  // camera of each view (host copy: the algorithmic flop count)
+  double* ximg_part = nullptr;  // sharded + xexp: this rank's partial image (all-reduced into d.simg)
   bool buildp_wide = false;  // k_buildp<.., MW = 8> (multi-model rigs with <= 8 waves per block)
   double* rjr = nullptr;     // [F + 1] kb_rhs_jtj_rhs: per-frame terms | result
-  int gn_prepared = -1;      // kb_gn_prepare'd pass count, consumed by kb_gn_launch
+  int gn_prepared = -1;      // kb_gn_prepare'd pass count, consumed by kb_gn_launch (-1: nothing prepared; every
+                             // entry point that changes the state, the graphs or the control block resets it)
+  bool sys_valid = false;    // the per-call system of the last kb_build is intact (H_ff, H_fc, g_f, H_cc, g_c): the
+                             // device-resident loops overwrite g_c and skip the frame-block stores in GN fused passes
   size_t lds_colimg = 0;     // k_colimg's staging (per-camera sums, chains, T, column info)
   bool gn_graph = false;
   int build_threads = 64;
@@ -210,7 +217,12 @@ static void drop_graphs(kb_handle* h) {
     g = nullptr;
   }
   h->graph_policy = -1;
+  h->gn_prepared = -1;  // a prepared GN launch used these graphs
 }
+
+// anything that changes the state, the control block or the system behind a kb_gn_prepare'd loop start voids it:
+// kb_gn_launch then fails instead of timing passes from a stale prelude
+static void unprepare(kb_handle* h) { h->gn_prepared = -1; }
 
 static bool sharded(const kb_handle* h) { return h->comm || h->lg; }
 
@@ -355,7 +367,7 @@ kb_handle* kb_create(const kb_layout* L) {
     d.gframes = (h->F + 511) / 512;
   }
   d.nblk = (h->F + d.gframes - 1) / d.gframes;
-  d.nblk_bs = h->F;  // k_backsub: one block per frame
+  d.nblk_bs = h->F;  // k_backsub: one step row per frame (one wave per frame)
   d.W = h->W;
   d.Wp = h->N * 136 + h->W + 1;
   d.Wr = d.Wp + 1;
@@ -404,9 +416,9 @@ kb_handle* kb_create(const kb_layout* L) {
   rc |= h->alloc(&d.red_local, 8);
   d.red = d.red_local;
   rc |= h->alloc(&d.ctrl, 1);
-  if (h->C > 64) {  // k_solve's staged camera block (k_colimg), sized as in the LDS budget below
+  if (h->C > 64) {  // k_solve's staged camera block (k_colimg / k_colsumx), sized as in the LDS budget below
     const int nb = (h->C + 16) / 16;  // rows 0 .. C: the right-hand side is appended as row C
-    rc |= h->alloc(&d.simg, (size_t)kTileSz * nb * (nb + 1) / 2 + 16 * nb + 2);
+    rc |= h->alloc(&d.simg, (size_t)kTileSz * nb * (nb + 1) / 2 + 16 * nb + 2 + kXMaxRanks);
   }
   std::vector<int32_t> colinfo(h->C), tri(h->C * (h->C + 1) / 2);
   for (int i = 0; i < h->N; ++i)
@@ -448,11 +460,16 @@ kb_handle* kb_create(const kb_layout* L) {
     } else {  // the k_colimg image (complete system: 16 x 16 lower tiles, b as row C | g_c) + the factored diagonal
       // tiles and their inverses + 1/D
       const int nb = (C + 16) / 16, n16 = 16 * nb;
-      d.img_n = kTileSz * nb * (nb + 1) / 2 + n16 + 2;
+      // tiles | aux: g_c (n16, non-PD count at C) | cost | max|dx_f| per rank (expanded partials) | pad
+      d.img_n = kTileSz * nb * (nb + 1) / 2 + n16 + 2 + kXMaxRanks;
       h->lds_solve = sizeof(double) * (d.img_n + 2 + 2 * nb * kTileSz + n16) + sizeof(int) * C;
       h->lds_colimg = sizeof(double) * (N * 256 + 2 * N * N * 36) + sizeof(int) * C;
     }
     h->solve_threads = C <= 64 ? 256 : 512;
+    // expanded partials for the GN fused loop: k_buildp expands its own camera sums in the LDS its view tiles free
+    // (Hs [N][256] | T [N(N-1)/2][36] | H_cc, g_c [W] within the Xw + Hw regions); KB_XEXP=0 keeps k_colimg
+    h->xexp = C > 64 && h->build_pipe && N * 256 + 18 * N * (N - 1) + h->W <= N * 64 * XS + N * 256;
+    if (const char* e = std::getenv("KB_XEXP")) h->xexp = h->xexp && std::atoi(e) != 0;
     h->fn_solve = C <= 16   ? (const void*)k_solve<16>
                   : C <= 24 ? (const void*)k_solve<24>
                   : C <= 32 ? (const void*)k_solve<32>
@@ -539,6 +556,7 @@ int kb_upload_observations(kb_handle* h, int32_t n_views, int32_t n_corners, con
     if ((int)corner_id[k] >= h->K) return fail("kb_upload_observations: corner_id out of range");
   h->V = n_views;
   h->NC = n_corners;
+  h->vcam.assign(vc.begin(), vc.end());
   KbDev& d = h->d;
   d.V = n_views;
   d.NC = n_corners;
@@ -590,6 +608,7 @@ static int set_cur(kb_handle* h, int cur) {
 int kb_set_state_flat(kb_handle* h, const double* state) {
   if (!h || !state) return fail("kb_set_state_flat: null");
   KB_HIP(hipSetDevice(h->device));
+  unprepare(h);
   KB_HIP(hipMemcpyAsync(h->d.state + (size_t)h->cur * h->S, state, sizeof(double) * h->S, hipMemcpyHostToDevice, h->stream));
   KB_HIP(hipStreamSynchronize(h->stream));
   return 0;
@@ -642,6 +661,15 @@ static int allreduce_red(kb_handle* h, bool reduce = true) {
 // all-reduced as they are (one collective, no finishing kernel)
 static int launch_colsum(kb_handle* h, int gate, bool finish = true) {
   KbDev& d = h->d;
+  if (d.xexp) {
+    // expanded partials (GN fused, C > 64): the column sums go straight into the k_solve image (this rank's partial
+    // image when sharded, all-reduced into simg: 62 KB at configs[3])
+    const int nx = (h->C + 1) + (d.Wtot - h->N * 136);
+    hipLaunchKernelGGL(k_colsumx, dim3((nx + 63) / 64), dim3(64 * kColsum1Waves), 0, h->stream, d, gate);
+    KB_HIP(hipGetLastError());
+    if (sharded(h) && coll_allreduce(h, h->ximg_part, d.simg, d.img_n)) return -1;
+    return 0;
+  }
   if (finish && h->C > 64) {
     // camera blocks for the tiled solve: the block partials summed in one pass into one row (k_colsum1), then
     // k_colimg copies the sums (into the consumer's row) and writes k_solve's LDS image from that row.  Sharded,
@@ -701,8 +729,8 @@ static int launch_solve(kb_handle* h, int gate, int do_update, bool from_rows = 
 }
 
 static int launch_backsub(kb_handle* h, int gate, int do_update, int with_cost) {
-  hipLaunchKernelGGL(k_backsub, dim3(h->d.nblk_bs), dim3(64 * std::min(h->N, 8)), 0, h->stream, h->d, gate, do_update,
-                     with_cost);
+  hipLaunchKernelGGL(k_backsub, dim3((h->F + kBsFrames - 1) / kBsFrames), dim3(64 * kBsFrames), 0, h->stream, h->d, gate,
+                     do_update, with_cost);
   KB_HIP(hipGetLastError());
   return 0;
 }
@@ -712,6 +740,7 @@ int kb_eval_cost(kb_handle* h, double* J_out) {
   if (!h || !J_out) return fail("kb_eval_cost: null");
   if (!h->uploaded) return fail("kb_eval_cost: no observations");
   KB_HIP(hipSetDevice(h->device));
+  unprepare(h);  // writes red / the cost partials the prepared loop start left
   if (launch_cost(h, 0)) return -1;
   if (allreduce_red(h)) return -1;
   KB_HIP(hipMemcpyAsync(J_out, h->d.red, sizeof(double), hipMemcpyDeviceToHost, h->stream));
@@ -724,11 +753,14 @@ int kb_build(kb_handle* h, int use_mestimator) {
   if (!h->uploaded) return fail("kb_build: no observations");
   (void)use_mestimator;  // NoMEstimator: weight 1 either way (ErrorTerm.cpp:11)
   KB_HIP(hipSetDevice(h->device));
+  unprepare(h);
+  h->sys_valid = false;
   if (launch_build(h, 0, 0)) return -1;
   if (launch_colsum(h, 0)) return -1;
   hipLaunchKernelGGL(k_camexpand, dim3(1), dim3(256), h->lds_camexp, h->stream, h->d);
   KB_HIP(hipGetLastError());
   KB_HIP(hipStreamSynchronize(h->stream));
+  h->sys_valid = true;
   return 0;
 }
 
@@ -873,6 +905,7 @@ int kb_get_pcg_info(kb_handle* h, kb_pcg_info* info) {
 int kb_solve(kb_handle* h, double* dx_out, int* ok) {
   if (!h || !ok) return fail("kb_solve: null");
   KB_HIP(hipSetDevice(h->device));
+  unprepare(h);
   if (h->solver_kind == KB_SOLVER_PCG) {
     if (h->use_cond) return fail("kb_solve (PCG): a diagonal conditioner is not supported, use a constant one");
     if (run_pcg(h, ok)) return -1;
@@ -909,7 +942,9 @@ int kb_solve(kb_handle* h, double* dx_out, int* ok) {
   double pinfo[4] = {0, 0, 0, 0};
   if (pcs) KB_HIP(hipMemcpyAsync(pinfo, h->d.pcs_info, sizeof(pinfo), hipMemcpyDeviceToHost, h->stream));
   KB_HIP(hipStreamSynchronize(h->stream));
-  if (pcs) {
+  if (pcs && okd && pinfo[3] != 0.0) {
+    // only a completed solve sets _residual (linear_solver_pcg.hpp:127): a failed one (singular DV block,
+    // non-positive curvature) leaves the previous solve's values for the next absolute-tolerance d0
     h->pcg_info.iterations = (int32_t)pinfo[0];
     h->pcg_info.residual = pinfo[1];
     h->pcg_info.d0 = pinfo[2];
@@ -935,6 +970,7 @@ int kb_get_rhs(kb_handle* h, double* rhs_out) {
 int kb_apply_update(kb_handle* h, const double* dx, double* deltaX_out) {
   if (!h) return fail("kb_apply_update: null");
   KB_HIP(hipSetDevice(h->device));
+  unprepare(h);
   std::vector<double> hx;
   if (dx) {
     KB_HIP(hipMemcpyAsync(h->d.dx, dx, sizeof(double) * h->ncols, hipMemcpyHostToDevice, h->stream));
@@ -959,6 +995,7 @@ int kb_apply_update(kb_handle* h, const double* dx, double* deltaX_out) {
 int kb_revert(kb_handle* h) {
   if (!h) return fail("kb_revert: null");
   KB_HIP(hipSetDevice(h->device));
+  unprepare(h);
   if (set_cur(h, 1 - h->cur)) return -1;
   KB_HIP(hipStreamSynchronize(h->stream));
   return 0;
@@ -1010,6 +1047,7 @@ int kb_solve_marginal(kb_handle* h, const kb_marginal_options* opts, double* dx_
                       double* sv_out, double* V_out) {
   if (!h || !opts || !ok) return fail("kb_solve_marginal: null");
   KB_HIP(hipSetDevice(h->device));
+  unprepare(h);
   const int one = 1;
   KB_HIP(hipMemcpyAsync(&h->d.ctrl->solve_ok, &one, sizeof(int), hipMemcpyHostToDevice, h->stream));
   if (run_marginal(h, opts, 1, info, sv_out, V_out)) return -1;
@@ -1035,6 +1073,8 @@ int kb_analyze_marginal(kb_handle* h, const kb_marginal_options* opts, kb_margin
 
 int kb_get_normal_blocks(kb_handle* h, double* Hff, double* Hfc, double* gf, double* Hcc, double* gc, double* cost) {
   if (!h) return fail("null handle");
+  if (!h->sys_valid) return fail("kb_get_normal_blocks: no intact system (call kb_build first; the optimizer loops "
+                                 "do not leave the per-call blocks)");
   KB_HIP(hipSetDevice(h->device));
   if (Hff) KB_HIP(hipMemcpyAsync(Hff, h->d.Hff, sizeof(double) * 36 * h->F, hipMemcpyDeviceToHost, h->stream));
   if (Hfc) KB_HIP(hipMemcpyAsync(Hfc, h->d.Hfc, sizeof(double) * 6 * h->C * h->F, hipMemcpyDeviceToHost, h->stream));
@@ -1049,6 +1089,8 @@ int kb_get_normal_blocks(kb_handle* h, double* Hff, double* Hfc, double* gf, dou
 int kb_rhs_jtj_rhs(kb_handle* h, double* out) {
   if (!h || !out) return fail("kb_rhs_jtj_rhs: null");
   if (!h->uploaded) return fail("kb_rhs_jtj_rhs: no observations");
+  if (!h->sys_valid) return fail("kb_rhs_jtj_rhs: no intact system (call kb_build first; the optimizer loops do "
+                                 "not leave the per-call blocks)");
   if (sharded(h)) return fail("kb_rhs_jtj_rhs: per-call quantity of an unsharded handle");
   KB_HIP(hipSetDevice(h->device));
   if (!h->rjr && h->alloc(&h->rjr, (size_t)h->F + 1)) return -1;
@@ -1074,6 +1116,8 @@ struct GnFusedScope {
     if (on) {
       h->d.gn_fused = 1;
       h->d.fold = 0;
+      h->d.xexp = h->xexp && h->nranks <= kXMaxRanks && (!sharded(h) || h->ximg_part) ? 1 : 0;
+      h->d.ximg = sharded(h) ? h->ximg_part : h->d.simg;
     }
   }
   ~GnFusedScope() { h->d = saved; }
@@ -1113,6 +1157,54 @@ static int enqueue_pass(kb_handle* h, int policy, hipEvent_t ev0 = nullptr, hipE
   }
   return 0;
 }
+
+// device copy of the loop-visible handle state (both state buffers, the camera chains of both slots, the control block)
+// and its restore: queries and warm-up launches leave the handle as they found it
+struct Snapshot {
+  kb_handle* h;
+  double* buf = nullptr;
+  int cur0 = 0;
+  bool taken = false;
+  explicit Snapshot(kb_handle* hh) : h(hh) {}
+  Snapshot(const Snapshot&) = delete;
+  Snapshot& operator=(const Snapshot&) = delete;
+  int copy(bool restore) {
+    KbDev& dv = h->d;
+    const size_t sz[4] = {2 * (size_t)h->S * 8, 2 * 12 * (size_t)h->N * 8, 2 * 36 * (size_t)h->N * h->N * 8,
+                          sizeof(KbCtrl)};
+    void* bufs[4] = {dv.state, dv.camL, dv.camK, dv.ctrl};
+    if (!buf) {
+      size_t tot = 0;
+      for (size_t z : sz) tot += (z + 7) & ~size_t(7);
+      KB_HIP(hipMalloc(&buf, tot));
+    }
+    char* c = (char*)buf;
+    for (int q = 0; q < 4; ++q) {
+      KB_HIP(hipMemcpyAsync(restore ? bufs[q] : c, restore ? c : bufs[q], sz[q], hipMemcpyDeviceToDevice, h->stream));
+      c += (sz[q] + 7) & ~size_t(7);
+    }
+    return 0;
+  }
+  int take() {
+    cur0 = h->cur;
+    if (copy(false)) return -1;
+    taken = true;
+    return 0;
+  }
+  int restore() {
+    if (copy(true)) return -1;
+    h->cur = cur0;
+    return 0;
+  }
+  ~Snapshot() {
+    if (taken) {
+      copy(true);
+      hipStreamSynchronize(h->stream);
+      h->cur = cur0;
+    }
+    if (buf) hipFree(buf);
+  }
+};
 
 static int ensure_trace(kb_handle* h, int cap) {
   if (h->trace_cap >= cap) return 0;
@@ -1197,6 +1289,8 @@ static int finish_pass(kb_handle* h, int policy) {
 
 static int loop_start(kb_handle* h, const KbOpts& o) {
   // evaluateError on the start state (Optimizer2.cpp:192-196), optimizationStarting, first prelude
+  unprepare(h);
+  h->sys_valid = false;  // the loop's passes overwrite g_c (and skip the frame-block stores when GN fused)
   if (launch_cost(h, 0)) return -1;
   if (allreduce_red(h)) return -1;
   hipLaunchKernelGGL(k_pol_init, dim3(1), dim3(1), 0, h->stream, h->d, o);
@@ -1258,10 +1352,23 @@ int kb_gn_prepare(kb_handle* h, int32_t n_iter) {
   if (ensure_trace(h, 64)) return -1;
   // GN, convergence tests disabled (thresholds -1 keep (dX > eps && |dJ| > eps) true)
   KbOpts o{1, 0x3fffffff, 0.0, -1.0, -1.0};
-  if (loop_start(h, o)) return -1;
   h->gn_graph = graph_ok(h, 1);
   hipGraphExec_t gr = nullptr;
   if (h->gn_graph && n_iter % kGraphPasses && graph_of(h, n_iter % kGraphPasses, &gr)) return -1;
+  if (h->gn_graph) {
+    // every graph the timed launch will use runs once here, from a snapshot that is restored afterwards: a graph's
+    // first launch costs more than the later ones (measured ~0.2 ms per kb_gn_launch at configs[3] when the 8-pass graph
+    // was first launched inside it), and that is set-up, not pass time.  Sharded: every rank prepares the same n_iter,
+    // so the captured collectives of these launches are matched across the ranks.
+    Snapshot snap(h);
+    if (snap.take() || loop_start(h, o)) return -1;
+    if (n_iter >= kGraphPasses) KB_HIP(hipGraphLaunch(h->graphs[kGraphPasses], h->stream));
+    if (gr) KB_HIP(hipGraphLaunch(gr, h->stream));
+    if (snap.restore()) return -1;
+    KB_HIP(hipStreamSynchronize(h->stream));
+    snap.taken = false;
+  }
+  if (loop_start(h, o)) return -1;
   KB_HIP(hipStreamSynchronize(h->stream));
   h->gn_prepared = n_iter;
   return h->gn_graph ? 1 : 0;
@@ -1291,97 +1398,128 @@ int kb_run_gn_iterations(kb_handle* h, int32_t n_iter, double* seconds) {
   return kb_gn_launch(h, n_iter, seconds);
 }
 
+// n Gauss-Newton passes from the current state, captured in one graph so that the passes run exactly as in the
+// benchmarked graphs (eager launches if this stack cannot capture, or when sharded).  A query: the state buffers, camera
+// chains and control block are saved first and restored at the end, so the handle is left as it was.
+//   build_ms[r]: HIP events around pass r's build kernel (event nodes in the graph)
+//   pass_ms[r]:  pass r from its build's start to the next pass's build start, from an s_memrealtime stamp the build
+//                kernel's block 0 takes at entry (KbDev::pass_ts; 100 MHz), in a separate run of n + 1 passes without
+//                event nodes, which would otherwise add their own gaps to every pass
+static int timed_gn_passes(kb_handle* h, int n, std::vector<double>& pass_ms, std::vector<double>& build_ms) {
+  if (ensure_trace(h, 64)) return -1;
+  Snapshot snap(h);
+  if (snap.take()) return -1;
+  KbOpts o{1, 0x3fffffff, 0.0, -1.0, -1.0};
+  std::vector<hipEvent_t> ev(2 * n, nullptr);
+  struct EvGuard {
+    std::vector<hipEvent_t>* ev;
+    ~EvGuard() {
+      for (auto& e : *ev)
+        if (e) hipEventDestroy(e);
+    }
+  } evg{&ev};
+  for (auto& e : ev) KB_HIP(hipEventCreate(&e));
+  unsigned long long* ts = nullptr;
+  KB_HIP(hipMalloc(&ts, sizeof(unsigned long long) * (kPassTsCap + 1)));
+  struct TsGuard {
+    unsigned long long* p;
+    ~TsGuard() { hipFree(p); }
+  } tsg{ts};
+  // run = 0: build events, n passes; run = 1: pass stamps, n + 1 passes
+  auto enqueue_run = [&](int run) -> int {
+    if (run == 0) {
+      for (int r = 0; r < n; ++r)
+        if (enqueue_pass(h, 1, ev[2 * r], ev[2 * r + 1])) return -1;
+      return 0;
+    }
+    KbDev keep = h->d;
+    h->d.pass_ts = ts;
+    int rc = 0;
+    for (int r = 0; r <= n && !rc; ++r) rc = enqueue_pass(h, 1);
+    h->d = keep;
+    return rc;
+  };
+  std::vector<unsigned long long> hts(kPassTsCap + 1);
+  auto read_run = [&](int run) -> bool {
+    if (run == 0) {
+      build_ms.assign(n, 0.0);
+      for (int r = 0; r < n; ++r) {
+        float b = 0.f;
+        if (hipEventElapsedTime(&b, ev[2 * r], ev[2 * r + 1]) != hipSuccess || !(b > 0.f)) return false;
+        build_ms[r] = b;
+      }
+      return true;
+    }
+    if (hipMemcpy(hts.data(), ts, sizeof(unsigned long long) * (n + 2), hipMemcpyDeviceToHost) != hipSuccess) return false;
+    if (hts[0] < (unsigned long long)(n + 1)) return false;
+    pass_ms.assign(n, 0.0);
+    for (int r = 0; r < n; ++r) pass_ms[r] = 1e-5 * (double)(hts[r + 2] - hts[r + 1]);  // 100 MHz ticks -> ms
+    return true;
+  };
+  for (int run = 0; run < 2; ++run) {
+    if (run == 1) {
+      if (snap.restore()) return -1;
+      KB_HIP(hipMemsetAsync(ts, 0, sizeof(unsigned long long) * (kPassTsCap + 1), h->stream));
+    }
+    if (loop_start(h, o)) return -1;
+    bool ok = false;
+    if (!sharded(h) && hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal) == hipSuccess) {
+      const int rc = enqueue_run(run);
+      hipGraph_t g = nullptr;
+      const hipError_t e = hipStreamEndCapture(h->stream, &g);
+      hipGraphExec_t ge = nullptr;
+      if (!rc && e == hipSuccess && g && hipGraphInstantiate(&ge, g, nullptr, nullptr, 0) == hipSuccess) {
+        // launched twice: the first launch of a graph costs more than the later ones (kb_gn_prepare)
+        bool l = hipGraphLaunch(ge, h->stream) == hipSuccess;
+        if (l && run == 1) {
+          l = snap.restore() == 0 && hipMemsetAsync(ts, 0, sizeof(unsigned long long) * (kPassTsCap + 1), h->stream) ==
+                                         hipSuccess && loop_start(h, o) == 0;
+          l = l && hipGraphLaunch(ge, h->stream) == hipSuccess;
+        }
+        ok = l && hipStreamSynchronize(h->stream) == hipSuccess;
+        hipGraphExecDestroy(ge);
+      }
+      if (g) hipGraphDestroy(g);
+      if (ok) ok = read_run(run);  // graph-recorded events without timing data on this stack: eager instead
+      if (!ok) hipGetLastError();
+    }
+    if (!ok) {
+      if (snap.restore()) return -1;
+      if (run == 1) KB_HIP(hipMemsetAsync(ts, 0, sizeof(unsigned long long) * (kPassTsCap + 1), h->stream));
+      if (loop_start(h, o) || enqueue_run(run)) return -1;
+      KB_HIP(hipStreamSynchronize(h->stream));
+      if (!read_run(run)) return fail("timed_gn_passes: no device timing on this stack");
+    }
+    if (finish_pass(h, 1)) return -1;
+    KB_HIP(hipStreamSynchronize(h->stream));
+  }
+  return 0;  // (the snapshot restores the handle)
+}
+
+int kb_gn_pass_times(kb_handle* h, int32_t n, double* pass_ms, double* build_ms) {
+  if (!h || n < 1 || n + 1 > kPassTsCap) return fail("kb_gn_pass_times: bad args (1 <= n < 255)");
+  if (!h->uploaded) return fail("kb_gn_pass_times: no observations");
+  KB_HIP(hipSetDevice(h->device));
+  std::vector<double> pm, bm;
+  if (timed_gn_passes(h, n, pm, bm)) return -1;
+  for (int r = 0; r < n; ++r) {
+    if (pass_ms) pass_ms[r] = pm[r];
+    if (build_ms) build_ms[r] = bm[r];
+  }
+  return 0;
+}
+
 int kb_build_kernel_stats(kb_handle* h, double* avg_ms, double* bytes_per_launch, double* flops_per_launch) {
   if (!h) return fail("null handle");
   if (!h->uploaded) return fail("kb_build_kernel_stats: no observations");
   KB_HIP(hipSetDevice(h->device));
-  // Gauss-Newton passes from the current state, launched eagerly with HIP events around each build kernel: the
-  // timed launches are the build exactly as it runs inside the pass (frame steps of the previous solve applied)
+  // Gauss-Newton passes from the current state with HIP events around each build kernel: the timed launches are the
+  // build exactly as it runs inside the pass (frame steps of the previous solve applied)
   const int reps = 20, warm = 2;
-  if (ensure_trace(h, 64)) return -1;
-  // a query: the state buffers, camera chains and control block are saved here and restored at the end
-  KbDev& dv = h->d;
-  const size_t n_state = 2 * (size_t)h->S, n_L = 2 * 12 * (size_t)h->N, n_K = 2 * 36 * (size_t)h->N * h->N;
-  const size_t n_ctrl = (sizeof(KbCtrl) + sizeof(double) - 1) / sizeof(double);
-  double* save = nullptr;
-  KB_HIP(hipMalloc(&save, sizeof(double) * (n_state + n_L + n_K + n_ctrl)));
-  auto snap = [&](bool restore) -> int {
-    char* c = (char*)save;
-    void* bufs[4] = {dv.state, dv.camL, dv.camK, dv.ctrl};
-    const size_t sz[4] = {n_state * 8, n_L * 8, n_K * 8, sizeof(KbCtrl)};
-    for (int q = 0; q < 4; ++q) {
-      KB_HIP(hipMemcpyAsync(restore ? bufs[q] : c, restore ? c : bufs[q], sz[q], hipMemcpyDeviceToDevice, h->stream));
-      c += (sz[q] + 7) & ~size_t(7);
-    }
-    return 0;
-  };
-  const int cur0 = h->cur;
-  std::vector<hipEvent_t> ev(2 * (reps + warm), nullptr);
-  // every exit restores the snapshot (once taken) and frees the query's buffers: the handle is left as it was
-  struct Guard {
-    kb_handle* h;
-    double* save;
-    std::vector<hipEvent_t>* ev;
-    std::function<int(bool)> snap;
-    int cur0;
-    bool taken = false;
-    ~Guard() {
-      if (taken) {
-        snap(true);
-        hipStreamSynchronize(h->stream);
-        h->cur = cur0;
-      }
-      hipFree(save);
-      for (auto& e : *ev)
-        if (e) hipEventDestroy(e);
-    }
-  } guard{h, save, &ev, snap, cur0};
-  if (snap(false)) return -1;
-  guard.taken = true;
-  KbOpts o{1, 0x3fffffff, 0.0, -1.0, -1.0};
-  if (loop_start(h, o)) return -1;
-  for (auto& e : ev) KB_HIP(hipEventCreate(&e));
-  // the passes are captured in one graph, event records included, so the timed builds run exactly as in the
-  // benchmarked graphs (no eager launch gaps around them); eager launches if this stack cannot capture events
-  bool graphed = false;
-  if (!sharded(h) && hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal) == hipSuccess) {
-    int rc = 0;
-    for (int r = 0; r < reps + warm && !rc; ++r) rc = enqueue_pass(h, 1, ev[2 * r], ev[2 * r + 1]);
-    hipGraph_t g = nullptr;
-    const hipError_t e = hipStreamEndCapture(h->stream, &g);
-    hipGraphExec_t ge = nullptr;
-    if (!rc && e == hipSuccess && g && hipGraphInstantiate(&ge, g, nullptr, nullptr, 0) == hipSuccess) {
-      graphed = hipGraphLaunch(ge, h->stream) == hipSuccess;
-      KB_HIP(hipStreamSynchronize(h->stream));
-      hipGraphExecDestroy(ge);
-    }
-    if (g) hipGraphDestroy(g);
-    if (!graphed) hipGetLastError();
-  }
+  std::vector<double> pm, bm;
+  if (timed_gn_passes(h, reps + warm, pm, bm)) return -1;
   double tot = 0.0;
-  if (graphed) {  // graph-recorded events without timing data on this stack: measure eagerly instead
-    for (int r = warm; r < reps + warm && graphed; ++r) {
-      float ms = 0.f;
-      if (hipEventElapsedTime(&ms, ev[2 * r], ev[2 * r + 1]) != hipSuccess || !(ms > 0.f)) graphed = false;
-      tot += ms;
-    }
-    if (!graphed) {
-      hipGetLastError();
-      tot = 0.0;
-    }
-  }
-  if (!graphed) {
-    for (int r = 0; r < reps + warm; ++r)
-      if (enqueue_pass(h, 1, ev[2 * r], ev[2 * r + 1])) return -1;
-    KB_HIP(hipStreamSynchronize(h->stream));
-    for (int r = warm; r < reps + warm; ++r) {
-      float ms = 0.f;
-      KB_HIP(hipEventElapsedTime(&ms, ev[2 * r], ev[2 * r + 1]));
-      tot += ms;
-    }
-  }
-  if (finish_pass(h, 1)) return -1;
-  KB_HIP(hipStreamSynchronize(h->stream));  // (the guard restores the snapshot and frees the buffers)
+  for (int r = warm; r < reps + warm; ++r) tot += bm[r];
   h->build_ms = tot / reps;
   if (avg_ms) *avg_ms = h->build_ms;
   // algorithmic bytes of one launch: observations (y 16 B + corner id 2 B per corner), view ranges (8 B per
@@ -1394,12 +1532,17 @@ int kb_build_kernel_stats(kb_handle* h, double* avg_ms, double* bytes_per_launch
                        8.0 * (C + F * (6 * C + 6)) + 8.0 * F * fblk + 8.0 * F * (6 * C + 6 + 7) +
                        8.0 * h->d.nblk * h->d.Wr;
   if (bytes_per_launch) *bytes_per_launch = bytes;
-  // executed MFMA flops (2 x 16 x 16 x rows, rows padded to 64 per 32-corner phase) + ~300 VALU flops/corner
-  double rows = 0.0;
-  std::vector<uint32_t> vo(h->V + 1);
-  KB_HIP(hipMemcpy(vo.data(), h->d.view_off, sizeof(uint32_t) * (h->V + 1), hipMemcpyDeviceToHost));
-  for (int v = 0; v < h->V; ++v) rows += 64.0 * ((vo[v + 1] - vo[v] + 31) / 32);
-  if (flops_per_launch) *flops_per_launch = rows * 16 * 16 * 2 + 300.0 * h->NC;
+  // algorithmic FP64 flops of one pass's build (SURVEY.md 8(d) "Algorithmic FLOPs"), not the executed (padded) MFMA
+  // work: per corner ~150 (projection + Jacobian) + ~100 (the cost pass the reference runs) + ~480 (local Hessian and
+  // gradient); per view of camera i (i baselines in its chain) the 6-D adjoint expansion 2 (6 i + 6 + n_intr)^2 6; per
+  // frame the Schur sums H_fc^T [A_f | b_f] 2 * 6 * C^2 + the 6 x 6 factorisation 6^3
+  double fl = 730.0 * h->NC + F * (2.0 * 6.0 * C * C + 216.0);
+  for (int v = 0; v < h->V; ++v) {
+    const int i = h->vcam[v];
+    const double m = 6.0 * i + 6.0 + h->d.nintr[i];
+    fl += 2.0 * m * m * 6.0;
+  }
+  if (flops_per_launch) *flops_per_launch = fl;
   return 0;
 }
 
@@ -1446,6 +1589,7 @@ static int shard_setup(kb_handle* h, int nranks, int rank, int F_max) {
   h->d.bsrc = h->bpart_all;
   h->d.bsrc_rows = h->F_max * nranks;
   if (h->alloc(&h->psum_red8, (size_t)kColsumRows * h->d.Wtot)) return -1;
+  if (h->xexp && !h->ximg_part && h->alloc(&h->ximg_part, (size_t)h->d.img_n)) return -1;
   drop_graphs(h);
   KB_HIP(hipStreamSynchronize(h->stream));
   return 0;
@@ -1597,7 +1741,8 @@ int kb_diag_phase_time(kb_handle* h, int which, int stop, int reps, int flags, d
       void* args[] = {&d, &g, &zero};
       KB_HIP(hipLaunchKernel(h->fn_solve, dim3(1), dim3(h->solve_threads), args, h->lds_solve, h->stream));
     } else {
-      hipLaunchKernelGGL(k_backsub, dim3(d.nblk_bs), dim3(64 * std::min(h->N, 8)), 0, h->stream, d, 0, 1, 1);
+      hipLaunchKernelGGL(k_backsub, dim3((h->F + kBsFrames - 1) / kBsFrames), dim3(64 * kBsFrames), 0, h->stream, d, 0, 1,
+                         1);
     }
   }
   KB_HIP(hipEventRecord(e1, h->stream));

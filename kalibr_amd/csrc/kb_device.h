@@ -99,8 +99,17 @@ struct KbDev {
   const double* red_all;  // [nranks][4] all-gathered red_local (sharded runs)
   int nranks;
   double* trace;
-  double* simg;  // C > 64: k_solve's LDS image of the camera block (k_colimg) [img_n]
+  double* simg;  // C > 64: k_solve's LDS image of the camera block (k_colimg / k_colsumx) [img_n]
   int img_n;
+  // GN fused passes of the pipelined build with C > 64 ("expanded" partials): k_buildp expands its block's per-camera
+  // sums through the chains itself, so a block partial row holds [g_c (C) | cost (1) | unused .. | S - lambda^2 I
+  // (upper packed) | b | non-PD | max|dx_f|], and k_colsumx writes the column sums straight into the k_solve image
+  // (no k_colimg).  Image aux slots after the tiles: [g_c | non-PD at C] (n16) | cost | max|dx_f| per rank.
+  int xexp;
+  double* ximg;  // image the column sums are written to: simg (one GPU) or this rank's partial image (sharded)
+  // per-pass timing query only (kb_gn_pass_times): [0] arrival counter | [1 ..] s_memrealtime (100 MHz) at the start of
+  // each pass's build kernel (block 0), null otherwise
+  unsigned long long* pass_ts;
   KbCtrl* ctrl;
   // KB_SOLVER_PCG_SCHUR (per-call kb_solve only): k_solve runs block-Jacobi PCG on the Schur complement instead of
   // the LDL^T.  pcs_cb: [2][C] camera DV block start / size per column (null: the LDL^T); pcs_info [4]: iterations,
@@ -146,6 +155,17 @@ struct KbDev {
   do {              \
   } while (0)
 #endif
+
+// kb_gn_pass_times: one timestamp per pass at the build kernel's start (block 0, one lane; a vector atomic picks the
+// slot), so that the per-pass durations come from inside the captured graph without extra graph nodes
+constexpr int kPassTsCap = 255;
+__device__ __forceinline__ void pass_stamp(const KbDev& d) {
+  if (d.pass_ts && blockIdx.x == 0 && threadIdx.x == 0) {
+    const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+    const unsigned i = atomicAdd(reinterpret_cast<unsigned*>(d.pass_ts), 1u);
+    if (i < (unsigned)kPassTsCap) d.pass_ts[1 + i] = t;
+  }
+}
 
 __device__ __forceinline__ double* cam_L(const KbDev& d, int slot) { return d.camL + (size_t)slot * d.N * 12; }
 __device__ __forceinline__ double* cam_K(const KbDev& d, int slot) { return d.camK + (size_t)slot * d.N * d.N * 36; }

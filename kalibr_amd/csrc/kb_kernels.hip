@@ -54,6 +54,12 @@ __device__ __forceinline__ double readlane_d(double v, int lane) {
 
 constexpr int XS = 17;       // LDS row stride (doubles) of the 64 x 16 Jacobian-row tile
 constexpr int kTargetLds = 1536;  // target corners staged in k_build's LDS when 3 * n_target <= this
+// the camera block of the C > 64 solve in LDS (and in its global image): lower 16 x 16 tiles, tile (it, jt) at
+// (it(it+1)/2 + jt) * kTileSz, row stride kTS (see ldl_panels)
+constexpr int kTS = 17;             // tile row stride (doubles): 16 + 1 keeps row-parallel LDS accesses conflict-free
+constexpr int kTileSz = 16 * kTS;
+__device__ __forceinline__ int tile_base(int it, int jt) { return (it * (it + 1) / 2 + jt) * kTileSz; }
+__device__ __forceinline__ int tidx(int i, int j) { return tile_base(i >> 4, j >> 4) + (i & 15) * kTS + (j & 15); }
 
 // 1/x by v_rcp_f64 + two Newton steps (a short dependent chain; within an ulp of the IEEE quotient)
 __device__ __forceinline__ double recip_d(double x) {
@@ -502,6 +508,85 @@ __device__ __forceinline__ void schur_tiles_store(double* prow_schur, int C, con
   }
 }
 
+// expanded partials (GN fused, C > 64): the tiles' entries stored as EX - sum, EX = the block's camera-block expansion
+// (same packing: S upper | b), so that the column sums are S - lambda^2 I and b themselves
+template <int TW>
+__device__ __forceinline__ void schur_tiles_store_x(double* prow_schur, int C, const int* tii, const int* tjj,
+                                                    const v4d* acc, const double* EX) {
+  const int lane = threadIdx.x & 63, Wt = C * (C + 1) / 2;
+#pragma unroll
+  for (int t = 0; t < TW; ++t) {
+    if (tii[t] < 0) break;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int rg = 16 * tii[t] + (lane >> 4) + 4 * r, cg = 16 * tjj[t] + (lane & 15);
+      if (rg < C && cg <= rg) {
+        const int u = upper_index(cg, rg, C);
+        prow_schur[u] = EX[u] - acc[t][r];
+      } else if (rg == C && cg < C) {
+        prow_schur[Wt + cg] = EX[Wt + cg] - acc[t][r];
+      }
+    }
+  }
+}
+
+// column of col-major packed lower index e (C columns) == row of row-major packed upper index e
+__device__ __forceinline__ int cidx_col(int e, int C) {
+  int j = (int)((2.0f * C + 1.0f - sqrtf((2.0f * C + 1.0f) * (2.0f * C + 1.0f) - 8.0f * (float)e)) * 0.5f);
+  j = max(0, min(j, C - 1));
+  while (j > 0 && j * (2 * C - j + 1) / 2 > e) --j;
+  while ((j + 1) * (2 * C - j) / 2 <= e) ++j;
+  return j;
+}
+
+// pair index of the chain K_{i,j} (j < i) in the pair-packed LDS arrays of k_buildp
+__device__ __forceinline__ int pidx(int i, int j) { return i * (i - 1) / 2 + j; }
+
+// entry (p, q) of H_cc (any order) or, q < 0, entry p of g_c, expanded from one block's per-camera sums:
+//   H_{I_i,I_i} = Hs_i[II]; H_{I_i,B_j} = Hs_i[Id] K_{i,j} (j < i); H_{B_j,B_k} = sum_{i > max(j,k)} K_{i,j}^T T_{i,k};
+//   g_{I_i} = Hs_i[I,15]; g_{B_j} = sum_{i > j} K_{i,j}^T Hs_i[d,15]
+// Hs [N][16][16] (rows 0..5 pose, 6..14 intrinsics, 15 the -e column), Kp / Tp [pair][6][6] with T_{i,k} = Hs_i[dd] K_{i,k}
+// (the same algebra as cam_entry_l / cam_grad_l over the finished sums; CalibrationTools.hpp:32-45 chain order)
+__device__ __forceinline__ double cam_expand_entry(int N, const int* ci, const double* Hs, const double* Tp,
+                                                   const double* Kp, int p, int q) {
+  const int kp = ci[p] >> 16, ip = (ci[p] >> 8) & 0xff, xp = ci[p] & 0xff;
+  double s = 0.0;
+  if (q < 0) {
+    if (kp == 0) return Hs[ip * 256 + (6 + xp) * 16 + 15];
+    for (int i = ip + 1; i < N; ++i) {
+      const double* K = Kp + pidx(i, ip) * 36;
+#pragma unroll
+      for (int a = 0; a < 6; ++a) s += K[a * 6 + xp] * Hs[i * 256 + a * 16 + 15];
+    }
+    return s;
+  }
+  const int kq = ci[q] >> 16, iq = (ci[q] >> 8) & 0xff, xq = ci[q] & 0xff;
+  if (kp == 0 && kq == 0) {
+    if (ip == iq) s = Hs[ip * 256 + (6 + xp) * 16 + 6 + xq];
+  } else if (kp == 0 && kq == 1) {
+    if (iq < ip) {
+      const double* K = Kp + pidx(ip, iq) * 36;
+#pragma unroll
+      for (int b = 0; b < 6; ++b) s += Hs[ip * 256 + (6 + xp) * 16 + b] * K[b * 6 + xq];
+    }
+  } else if (kp == 1 && kq == 0) {
+    if (ip < iq) {
+      const double* K = Kp + pidx(iq, ip) * 36;
+#pragma unroll
+      for (int a = 0; a < 6; ++a) s += K[a * 6 + xp] * Hs[iq * 256 + a * 16 + 6 + xq];
+    }
+  } else {
+    const int m = ip > iq ? ip : iq;
+    for (int i = m + 1; i < N; ++i) {
+      const double* K = Kp + pidx(i, ip) * 36;
+      const double* T = Tp + pidx(i, iq) * 36;
+#pragma unroll
+      for (int a = 0; a < 6; ++a) s += K[a * 6 + xp] * T[a * 6 + xq];
+    }
+  }
+  return s;
+}
+
 // Gauss-Jordan elimination of [H_ff + lam2 I | H_fc | g_f] by one wave, lanes = columns (slot s: column
 // lane + 64 s), rows 0..5 in registers; pivot column k broadcast with v_readlane.  No pivoting: H_ff is SPD,
 // the pivots are the squared Cholesky diagonal (all > 0 iff positive definite).  Ends with [I | A | b]:
@@ -691,6 +776,7 @@ __device__ __forceinline__ void frame_step(const KbDev& d, int f, bool store, in
 // MM: camera-model set of the rig (kMmAll = any model; a single-model set compiles one projection)
 template <int TW, bool GNF, unsigned MM>
 __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
+  pass_stamp(d);
   KbCtrl* c = d.ctrl;
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const int N = d.N, C = d.C, WPB = d.wpb, NS = d.nsplit;
@@ -1133,6 +1219,7 @@ __device__ __forceinline__ void schur_tiles_accumulate6(const double* P, const d
 template <int TT, bool GNF, unsigned MM, int MW>
 __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse) {
   KB_MFMA_AGPR();
+  pass_stamp(d);
   KbCtrl* c = d.ctrl;
   extern __shared__ __attribute__((aligned(16))) double sm[];
   constexpr int NF = buildp_nf<TT>();
@@ -1154,6 +1241,7 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
   __shared__ int okl;
   __shared__ double cst[KB_MAX_CAMS][24];  // per camera: chain L (12) | intrinsics (10)
   __shared__ int ctab[2][KB_MAX_CAMS];      // per camera: first intrinsic column | baseline column
+  __shared__ int cil[112];                  // expanded partials: column info (kind << 16 | camera << 8 | index)
   const int W = d.W;
   const int f0 = blockIdx.x * d.gframes, f1 = min(d.F, f0 + d.gframes), G = f1 - f0;
   const bool vw = wave < N;  // view wave (camera = wave) | frame wave fw = wave - N
@@ -1206,6 +1294,9 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
     cst[cm][e] = e < 12 ? cam_L(d, bs)[cm * 12 + e] : s[cm * KB_MAX_INTR + e - 12];
   }
   if (tid < 2 * N) ctab[tid / N][tid % N] = (tid < N) ? cam_arg(d.col_intr, tid) : cam_arg(d.col_base, tid - N);
+  // expanded partials (GN fused, C > 64, KbDev::xexp): the block expands its own per-camera sums in the epilogue
+  const bool xp = GNF && gfu && fuse && d.xexp;
+  if (xp && tid < C) cil[tid] = d.colinfo[tid];
   double* fpl = tg + (tg_lds ? nt3 : 0);
   int cidn;  // view waves: lane = corner of a 64-corner pass
   double2 yn;
@@ -1530,13 +1621,70 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
           }
         }
         if (stv) KB_TSB(d, sto + 8);
+      } else if (xp) {
+        // expanded partials: the view waves are idle while the frame waves eliminate the last frame; clear the camera
+        // block's LDS image (the structural zeros, e.g. H_{I_i, B_j} for j >= i, are never written; the Xw tiles
+        // it overlaps are no longer read)
+        for (int e = tid; e < W; e += 64 * N) sm[e] = 0.0;
       }
       __syncthreads();
     }
+    if (xp) {
+      // ---- expanded partials, step 1: this camera's share of the block's camera block, straight
+      // from its local sums creg = Hs (C layout: lane l, reg q -> row (l >> 4) + 4 q, column l & 15):
+      //   H_{I,I} and g_I entries directly; D = Hs[:, d] [K_{i,0} | .. | K_{i,i-1}] on MFMA (the symmetric Hs is its own
+      //   A operand, as in the view expansion): rows 6 .. 5 + nin -> H_{I_i, B_j}, row 15 -> camera i's share of g_B,
+      //   rows 0 .. 5 -> T_i = Hs_dd K_i (the B operand of the baseline block in step 2)
+      double* EX = sm;                   // [W] H_cc upper packed | g_c
+      double* Tl = EX + W;               // [N][6][48] T_i
+      double* gB = Tl + N * 288;         // [N][48] camera i's share of g_B
+      double* cc = gB + N * 48;          // [N] chi^2 of camera i
+      const int Wt = W - C, CI = C - 6 * (N - 1), ci0 = ctab[0][cam];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {  // the camera's local sums, upper packed
-      const int a = mrow + 4 * q, b = mcol;
-      if (a <= b) prow[cam * 136 + d16_index(a, b)] = creg[q];
+      for (int q = 0; q < 4; ++q) {
+        const int a = mrow + 4 * q, b = mcol, x = a - 6, y = b - 6;
+        if (x >= 0 && x < nin && y >= x && y < nin) EX[upper_index(ci0 + x, ci0 + y, C)] = creg[q];
+        if (b == 15 && x >= 0 && x < nin) EX[Wt + ci0 + x] = creg[q];
+        if (a == 15 && b == 15) cc[cam] = creg[q];
+      }
+      if (cam > 0) {
+        const int i16 = lane & 15, k0 = lane >> 4, nct = (6 * cam + 15) >> 4;
+        const double* Kv = Kl + (cam * (cam - 1) / 2) * 36;
+        double kb[3][2];
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+          const int k = k0 + 4 * st;
+#pragma unroll
+          for (int ct = 0; ct < 3; ++ct) {
+            const int c = 16 * ct + i16, cc2 = min(c, 6 * cam - 1), jj = cc2 / 6, bb = cc2 - 6 * jj;
+            const double v = Kv[jj * 36 + min(k, 5) * 6 + bb];
+            kb[ct][st] = (k < 6 && c < 6 * cam) ? v : 0.0;
+          }
+        }
+#pragma unroll
+        for (int ct = 0; ct < 3; ++ct) {
+          if (ct >= nct) break;  // wave-uniform
+          v4d t = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+          for (int st = 0; st < 2; ++st) t = __builtin_amdgcn_mfma_f64_16x16x4f64(creg[st], kb[ct][st], t, 0, 0, 0);
+          const int n = 16 * ct + i16;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int m = k0 + 4 * r;
+            if (n < 6 * cam) {
+              if (m < 6) Tl[cam * 288 + m * 48 + n] = t[r];
+              else if (m - 6 < nin) EX[upper_index(ci0 + m - 6, CI + n, C)] = t[r];
+              else if (m == 15) gB[cam * 48 + n] = t[r];
+            }
+          }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {  // the camera's local sums, upper packed
+        const int a = mrow + 4 * q, b = mcol;
+        if (a <= b) prow[cam * 136 + d16_index(a, b)] = creg[q];
+      }
     }
   } else {
     v4d acc[TT];
@@ -1564,7 +1712,68 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
       }
       __syncthreads();
     }
-    if (fuse) schur_tiles_store<TT>(prow + N * 136, C, tii, tjj, acc);
+    if (fuse && !xp) schur_tiles_store<TT>(prow + N * 136, C, tii, tjj, acc);
+    if (xp) {
+      // the frame waves keep their tiles in registers through the view waves' expansion below, then store EX - tile
+      __syncthreads();
+      __syncthreads();
+      schur_tiles_store_x<TT>(prow + N * 136, C, tii, tjj, acc, sm);
+    }
+  }
+  if (xp && vw) {
+    // ---- expanded partials, step 2: the baseline block H_{B_j,B_k} = sum_{i > max(j,k)} K_{i,j}^T T_{i,k}, one 16 x 16
+    // tile per view wave, accumulated over the cameras in order on MFMA (A = K_i^T from the chains in LDS, B = T_i);
+    // g_B = sum_{i > j} (camera i's share) and the cost in fixed order.  The column sums k_colsumx forms are then
+    // S - lambda^2 I = H_cc - sum H_fc^T A_f and b = g_c - sum H_fc^T b_f directly: no kernel expands the finished
+    // sums (k_colimg).  The frame waves hold their Schur tiles meanwhile and pass the same two barriers.
+    double* EX = sm;
+    const double* Tl = EX + W;
+    const double* gB = Tl + N * 288;
+    const double* cc = gB + N * 48;
+    const int Wt = W - C, NB = 6 * (N - 1), CI = C - NB, ntb = (NB + 15) >> 4;
+    __syncthreads();  // step 1 complete (T_i, the camera shares of g_B, the direct entries)
+    for (int tq = wave; tq < ntb * (ntb + 1) / 2; tq += N) {
+      // tile (ta, tb), ta <= tb, of the baseline block (upper tiles in row order)
+      int ta = 0, q = tq;
+      while (q >= ntb - ta) {
+        q -= ntb - ta;
+        ++ta;
+      }
+      const int tb = ta + q;
+      {  // wave-uniform
+        const int i16 = lane & 15, k0 = lane >> 4;
+        v4d acc = {0.0, 0.0, 0.0, 0.0};
+        for (int i = 1; i < N; ++i) {
+          const double* Kv = Kl + (i * (i - 1) / 2) * 36;
+#pragma unroll
+          for (int st = 0; st < 2; ++st) {
+            const int k = k0 + 4 * st, ca = 16 * ta + i16, cb = 16 * tb + i16;
+            const int cac = min(ca, 6 * i - 1), ja = cac / 6, ya = cac - 6 * ja;
+            const double av = Kv[ja * 36 + min(k, 5) * 6 + ya];
+            const double bv = Tl[i * 288 + min(k, 5) * 48 + min(cb, 47)];
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64((k < 6 && ca < 6 * i) ? av : 0.0,
+                                                       (k < 6 && cb < 6 * i) ? bv : 0.0, acc, 0, 0, 0);
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = 16 * ta + k0 + 4 * r, col = 16 * tb + i16;
+          if (row <= col && col < NB) EX[upper_index(CI + row, CI + col, C)] = acc[r];
+        }
+      }
+    }
+    for (int n = tid; n < NB; n += 64 * N) {
+      double g = 0.0;
+      for (int i = n / 6 + 1; i < N; ++i) g += gB[i * 48 + n];
+      EX[Wt + CI + n] = g;
+    }
+    if (tid == 0) {
+      double sc = 0.0;
+      for (int i = 0; i < N; ++i) sc += cc[i];
+      prow[C] = sc;  // the block's chi^2 (the cost column)
+    }
+    __syncthreads();  // EX complete: the frame waves store EX - tile
+    for (int e = tid; e < C; e += 64 * N) prow[e] = EX[Wt + e];  // the g_c columns
   }
   __syncthreads();  // okl final
   if (wave == 0) KB_TSB(d, 63);
@@ -1710,6 +1919,77 @@ __global__ void __launch_bounds__(64 * kColsum1Waves) k_colsum1(KbDev d, int gat
     // one max column per rank: this rank's max in its own column (GN fused passes), zero elsewhere
     if (mx) t = (d.gn_fused && e - d.Wp == d.rank) ? m : 0.0;
     d.part8[e] = t;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_colsumx (GN fused passes with expanded partials, KbDev::xexp): the column sums of the block partials in one pass
+// (as k_colsum1: 16 waves x 64 columns, all of a wave's row loads in flight, the wave sums in fixed order), written
+// straight into the k_solve image d.ximg instead of a row that k_colimg would expand:
+//   S - lambda^2 I entry (a, b) -> its lower tile position (both triangles inside a diagonal tile), b_j -> row C,
+//   g_c -> the aux slots [0, C), non-PD count -> aux slot C, cost -> aux slot n16, max|dx_f| of rank r -> n16 + 1 + r.
+// Work column x: [0, C] = the g_c | cost columns, then every column from N * 136 on (S, b, non-PD, max|dx_f|).
+// The identity padding and lambda^2 are k_solve's (they must not be summed over ranks).
+// ---------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(64 * kColsum1Waves) k_colsumx(KbDev d, int gate) {
+  KbCtrl* c = d.ctrl;
+  __shared__ double part[kColsum1Waves][64];
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int N = d.N, C = d.C, nb = (C + 16) >> 4, n16 = 16 * nb;
+  const int x = blockIdx.x * 64 + l;
+  const int nx = (C + 1) + (d.Wtot - N * 136);
+  const int e = x <= C ? x : x - (C + 1) + N * 136;
+  const bool mx = e >= d.Wp;
+  const int ec = min(e, d.Wtot - 1);
+  constexpr int U = 24;
+  const int done = c->done;
+  double v[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) v[u] = d.part[(size_t)min(w + u * kColsum1Waves, d.nblk - 1) * d.Wr + ec];
+#pragma unroll
+  for (int u = 0; u < U; ++u) KB_KEEP(v[u]);
+  if (gate && done) return;
+  double s = 0.0;
+  for (int b0 = w; b0 < d.nblk; b0 += U * kColsum1Waves) {
+    if (b0 != w) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = d.part[(size_t)min(b0 + u * kColsum1Waves, d.nblk - 1) * d.Wr + ec];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const double y = (b0 + u * kColsum1Waves < d.nblk) ? v[u] : 0.0;
+      s = mx ? fmax(s, y) : s + y;
+    }
+  }
+  part[w][l] = s;
+  __syncthreads();
+  if (w != 0 || x >= nx) return;
+  double t = 0.0, m = 0.0;
+#pragma unroll
+  for (int q = 0; q < kColsum1Waves; ++q) {
+    t += part[q][l];
+    m = fmax(m, part[q][l]);
+  }
+  const int ntz = kTileSz * nb * (nb + 1) / 2, aux = ntz;
+  const int Wt = C * (C + 1) / 2, o = N * 136;
+  double* img = d.ximg;
+  if (e < C) {
+    img[aux + e] = t;  // g_c
+  } else if (e == C) {
+    img[aux + n16] = t;  // cost
+  } else if (e < o + Wt) {
+    const int u = e - o, a = cidx_col(u, C), b = u - (a * C - a * (a - 1) / 2) + a;  // a <= b
+    img[tidx(b, a)] = t;
+    if (a != b && (a >> 4) == (b >> 4)) img[tidx(a, b)] = t;  // diagonal tiles are whole
+  } else if (e < o + Wt + C) {
+    const int j = e - o - Wt;
+    img[tidx(C, j)] = t;  // b as row C
+    if ((j >> 4) == (C >> 4)) img[tidx(j, C)] = t;
+  } else if (e < d.Wp) {
+    img[aux + C] = t;  // non-PD frame blocks
+  } else {
+    const int r = e - d.Wp;  // one max column per rank: this rank's max in its own slot, zero elsewhere
+    img[aux + n16 + 1 + r] = (d.gn_fused && r == d.rank) ? m : 0.0;
   }
 }
 
@@ -2079,15 +2359,6 @@ __device__ __forceinline__ double cam_grad_l(const int N, const int* ci, const d
 // column-major packed lower index of (i, j), i >= j (== row-major packed upper index of (j, i))
 __device__ __forceinline__ int cidx(int i, int j, int C) { return j * (2 * C - j - 1) / 2 + i; }
 
-// column of col-major packed lower index e (C columns)
-__device__ __forceinline__ int cidx_col(int e, int C) {
-  int j = (int)((2.0f * C + 1.0f - sqrtf((2.0f * C + 1.0f) * (2.0f * C + 1.0f) - 8.0f * (float)e)) * 0.5f);
-  j = max(0, min(j, C - 1));
-  while (j > 0 && j * (2 * C - j + 1) / 2 > e) --j;
-  while ((j + 1) * (2 * C - j) / 2 <= e) ++j;
-  return j;
-}
-
 // ---------------------------------------------------------------------------------------------
 // Blocked LDL^T of the camera block for C > 64 (configs[3]: C = 106), the right-hand side appended as row C.
 // LDS layout: lower 16 x 16 tiles, tile (it, jt) at (it(it+1)/2 + jt) * kTileSz, row stride kTS, nb = ceil((C+1)/16)
@@ -2105,10 +2376,6 @@ __device__ __forceinline__ int cidx_col(int e, int C) {
 // Same algebra as the scalar right-looking LDL^T (SparseCholeskyLinearSystemSolver.cpp:48-89 / Cholmod(impl).hpp:
 // 387-399 factor the same matrix); only the accumulation order of the trailing updates differs.
 // ---------------------------------------------------------------------------------------------
-constexpr int kTS = 17;             // tile row stride (doubles): 16 + 1 keeps row-parallel LDS accesses conflict-free
-constexpr int kTileSz = 16 * kTS;
-__device__ __forceinline__ int tile_base(int it, int jt) { return (it * (it + 1) / 2 + jt) * kTileSz; }
-__device__ __forceinline__ int tidx(int i, int j) { return tile_base(i >> 4, j >> 4) + (i & 15) * kTS + (j & 15); }
 
 // LDS index of lower entry (i, j), i >= j, of the staged camera block: packed column-major (CM > 0) or tiles
 template <int CM>
@@ -2351,6 +2618,96 @@ __device__ __forceinline__ void panel_steps(double (&row)[16], int lane, int q, 
   }
 }
 
+// x += (lane L's y within the lane's 16-lane row) * f: one v_fmac_f64 whose src0 is read through DPP row_newbcast:L
+// (64-bit DPP, gfx90a+), so the broadcast of the pivot row costs no instruction of its own.  y and x may be the same
+// register (operands are read before the write).
+template <int L>
+__device__ __forceinline__ void fmac_bc(double& x, double y, double f) {
+  asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf" : "+v"(x) : "v"(y), "v"(f), "i"(L));
+}
+// the same after 2 wait states, for a source a VALU instruction has just written (a dependent chain of DPP reads)
+template <int L>
+__device__ __forceinline__ void fmac_bc_dep(double& x, double y, double f) {
+  asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+               : "+v"(x) : "v"(y), "v"(f), "i"(L));
+}
+template <int L>
+__device__ __forceinline__ void fmac_bc_self(double& x, double f) {
+  asm volatile("v_fmac_f64_dpp %0, %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf" : "+v"(x) : "v"(f), "i"(L));
+}
+
+// updates of step K for columns J .. 15: the below row first (it reads the pivot row's column J before the diagonal
+// row's own update of it), then the diagonal row
+template <int K, int J>
+__device__ __forceinline__ void panel2_cols(double (&dr)[16], double (&br)[16], double nfd, double nfb) {
+  if constexpr (J < 16) {
+    fmac_bc<K>(br[J], dr[J], nfb);
+    fmac_bc_self<K>(dr[J], nfd);
+    panel2_cols<K, J + 1>(dr, br, nfd, nfb);
+  }
+}
+
+// pivot steps K .. 15 of the replicated-diagonal panel factorisation (panel_factor2): every 16-lane row holds the
+// diagonal tile (lane r: its row r) and one tile below (lane r: that tile's row r).  Step K reads D_K and the pivot row's
+// entries from lane K of the lane's own 16-lane row, by DPP row_newbcast fused into the FMAs (no v_readlane / SGPR hop,
+// no LDS round trip).  Lanes above the pivot hold zeros right of their own pivot (their own step cancelled them), so no
+// lane mask sits in the pivot chain.
+template <int K>
+__device__ __forceinline__ void panel2_steps(double (&dr)[16], double (&br)[16], int r, int q, int C, bool& ok,
+                                             double& rd) {
+  if constexpr (K < 16) {
+    asm volatile("s_nop 1" ::: "memory");  // DPP read of a VGPR a VALU wrote: 2 wait states
+    const double Dk = bcast16(dr[K], K);
+    const double rdk = Dk > 0.0 ? recip_d1(Dk) : 0.0;
+    const double nfd = -(dr[K] * rdk), nfb = -(br[K] * rdk);
+    panel2_cols<K, K + 1>(dr, br, nfd, nfb);
+    ok = ok & ((Dk > 0.0) | (16 * q + K >= C));  // bitwise: no branch per pivot
+    rd = (r == K) ? rdk : rd;
+    panel2_steps<K + 1>(dr, br, r, q, C, ok, rd);
+  }
+}
+
+// panel q by factor wave fw: lane (t = lane >> 4, r = lane & 15) holds row r of the diagonal tile (every 16-lane row
+// the same copy) and row r of tile q + 1 + 4 fw + t.  The tiles of column q are complete (every earlier panel applied).
+// The below rows' W go back in place; the factored diagonal tile (W strictly below, D on the diagonal) to Dfac and 1/D
+// to rD (wave 0, lanes 0..15).  Returns false on a non-positive pivot of a real row (< C); the b row's pivot and the
+// identity padding are not tested.
+__device__ __forceinline__ bool panel_factor2(const KbDev& d, double* S, double* rD, double* Dfac, int q, int nb, int C,
+                                              int fw) {
+  const int lane = threadIdx.x & 63, r = lane & 15, t = lane >> 4;
+  const int ti = q + 1 + 4 * fw + t;
+  const bool live = ti < nb;
+  const double* dbase = S + tile_base(q, q) + r * kTS;
+  double* bbase = S + tile_base(live ? ti : q, q) + r * kTS;
+  double dr[16], br[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    dr[c] = dbase[c];
+    br[c] = bbase[c];
+  }
+  bool ok = true;
+  double rd = 1.0;
+  if (q == 2 && fw == 0) KB_TS(d, 41);
+  panel2_steps<0>(dr, br, r, q, C, ok, rd);
+#ifdef KB_STAMPS
+#pragma unroll
+  for (int c = 0; c < 16; ++c) KB_KEEP(br[c]);
+  KB_KEEP(rd);
+#endif
+  if (q == 2 && fw == 0) KB_TS(d, 42);
+  if (live) {
+#pragma unroll
+    for (int c = 0; c < 16; ++c) bbase[c] = br[c];
+  }
+  if (t == 0 && fw == 0) {
+    double* dd = Dfac + q * kTileSz + r * kTS;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) dd[c] = dr[c];
+    rD[16 * q + r] = rd;
+  }
+  return ok;
+}
+
 // panel q by factor wave fw (rows in registers, one per lane: lanes 0..15 the diagonal tile, lanes 16..63 the rows of
 // tiles q+1+3fw .. q+3+3fw).  The tiles of column q are complete (every earlier panel applied).  W rows go back in
 // place, the factored diagonal tile (W strictly below, D on the diagonal) to Dfac (wave 0), 1/D to rD.  Returns false
@@ -2434,10 +2791,18 @@ __device__ __forceinline__ void ldl_panels(const KbDev& d, double* S, double* rD
       }
       __syncthreads();
     }
-    const int nf = (nb - 1 - q) > 3 ? 2 : 1;
+#ifdef KB_PANEL_READLANE
+    const int nf = (nb - 1 - q) > 3 ? 2 : 1;  // the readlane panel: 3 tiles below per factor wave
+#else
+    const int nf = (nb - 1 - q) > 4 ? 2 : 1;  // the DPP panel: 4 tiles below per factor wave
+#endif
     if (wave < nf) {
       if (wave == 0) KB_TS(d, 20 + 2 * q);
+#ifdef KB_PANEL_READLANE
       const bool ok = panel_factor(d, S, rD, Dfac, q, nb, C, wave);
+#else
+      const bool ok = panel_factor2(d, S, rD, Dfac, q, nb, C, wave);
+#endif
       if (wave == 0) {
         if (!ok && lane == 0) *okl = 0;
         KB_WAVE_SYNC();
@@ -2588,6 +2953,126 @@ __device__ __forceinline__ void panel_backsolve(const KbDev& d, const double* S,
   for (; ti >= 0; --ti) {
     bs_tile<false>(S, Dfac, Xinv, C, ti, row, rdv, pub, x);
     if (xb && ti == pub_tile) bs_publish(C, pub_tile, xb, bflag, x);
+  }
+}
+
+// ---- the backsolve with prefetched operands (panel_backsolve2): the operands of tile ti - 1 (a column of its inverse
+// and the lane's two rows of L~ left of it) are loaded from LDS while tile ti is solved, the tile's mat-vec and the
+// updates of the earlier rows take their broadcasts through DPP fused into the FMAs, and the tile's values reach the
+// other 16-lane groups through one LDS slot without a wave-wide wait (one wave's LDS accesses complete in order).
+struct BsOps {
+  double M[16];       // column r of X_ti = Ltilde_tt^-1 (CHAIN: of the factored tile), masked to the entries it uses
+  double Le[2][16];   // Ltilde[16 ti + u][row[sl]] for the lane's rows (slots 0, 1)
+};
+
+template <bool CHAIN>
+__device__ __forceinline__ void bs2_load(const double* S, const double* Dfac, const double* Xinv, int C, int ti,
+                                         const int (&row)[2], const double (&rdv)[2], BsOps& o) {
+  const int lane = threadIdx.x & 63, r = lane & 15, ts = ti >> 2;
+  const double* pm = (CHAIN ? Dfac : Xinv) + ti * kTileSz + r;
+#pragma unroll
+  for (int u = 0; u < 16; ++u) o.M[u] = pm[u * kTS];
+#pragma unroll
+  for (int sl = 0; sl < 2; ++sl) {
+    const double* pe = S + tile_base(ti, min(row[sl] >> 4, ti)) + (row[sl] & 15);
+#pragma unroll
+    for (int u = 0; u < 16; ++u) o.Le[sl][u] = pe[u * kTS];
+  }
+  (void)C;
+  (void)rdv;
+  (void)ts;
+}
+
+template <bool CHAIN>
+__device__ __forceinline__ void bs2_solve(const BsOps& o, int C, int ti, const int (&row)[2], const double (&rdv)[2],
+                                          double* pub, double (&x)[2]) {
+  const int lane = threadIdx.x & 63, g = lane >> 4, r = lane & 15;
+  const int tg = ti & 3, ts = ti >> 2, i0 = 16 * ti;
+  double xt = ts ? x[1] : x[0];
+  const int lim = C - i0;  // rows of this tile below C (CHAIN only; the other tiles are whole)
+  if constexpr (CHAIN) {
+    const double rdt = ts ? rdv[1] : rdv[0];
+    double M[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) M[u] = (r < u && u < lim) ? -(o.M[u] * rdt) : 0.0;
+    // x[r] -= sum_{u > r} L[u][r] x[u], u from the last: 16 dependent steps, x[u] read from lane u by DPP
+#define KB_BS2_STEP(U) fmac_bc_dep<U>(xt, xt, M[U]);
+    KB_BS2_STEP(15) KB_BS2_STEP(14) KB_BS2_STEP(13) KB_BS2_STEP(12) KB_BS2_STEP(11) KB_BS2_STEP(10) KB_BS2_STEP(9)
+    KB_BS2_STEP(8) KB_BS2_STEP(7) KB_BS2_STEP(6) KB_BS2_STEP(5) KB_BS2_STEP(4) KB_BS2_STEP(3) KB_BS2_STEP(2)
+    KB_BS2_STEP(1) KB_BS2_STEP(0)
+#undef KB_BS2_STEP
+  } else {
+    // x_t[r] = sum_{c >= r} X[c][r] y[c]: 16 independent products (two accumulators), y[c] from lane c by DPP
+    double a0 = 0.0, a1 = 0.0;
+    double M[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) M[u] = (u >= r) ? o.M[u] : 0.0;
+    asm volatile("s_nop 1" ::: "memory");
+#define KB_BS2_MV(U) fmac_bc<U>(a0, xt, M[U]); fmac_bc<U + 1>(a1, xt, M[U + 1]);
+    KB_BS2_MV(0) KB_BS2_MV(2) KB_BS2_MV(4) KB_BS2_MV(6) KB_BS2_MV(8) KB_BS2_MV(10) KB_BS2_MV(12) KB_BS2_MV(14)
+#undef KB_BS2_MV
+    xt = a0 + a1;
+  }
+  if (g == tg) {
+    if (ts) x[1] = xt;
+    else x[0] = xt;
+    pub[r] = xt;
+  }
+  asm volatile("" ::: "memory");  // compiler order only: the wave's LDS write completes before its reads below
+  double xp[16];
+#pragma unroll
+  for (int u = 0; u < 16; ++u) xp[u] = (!CHAIN || u < lim) ? pub[u] : 0.0;
+#pragma unroll
+  for (int sl = 0; sl < 2; ++sl) {
+    double acc0 = 0.0, acc1 = 0.0;
+#pragma unroll
+    for (int u = 0; u < 16; u += 2) {
+      acc0 = fma(o.Le[sl][u], xp[u], acc0);
+      acc1 = fma(o.Le[sl][u + 1], xp[u + 1], acc1);
+    }
+    if (row[sl] < i0) x[sl] -= (acc0 + acc1) * rdv[sl];
+  }
+  asm volatile("" ::: "memory");  // pub is rewritten by the next tile after these reads
+}
+
+__device__ __forceinline__ void panel_backsolve2(const KbDev& d, const double* S, const double* Dfac, const double* Xinv,
+                                                 const double* rD, int C, int nb, double* pub, double (&x)[2],
+                                                 int pub_tile = -1, double* xb = nullptr, volatile int* bflag = nullptr) {
+  const int lane = threadIdx.x & 63, g = lane >> 4, r = lane & 15;
+  int row[2];
+  double rdv[2];
+#pragma unroll
+  for (int sl = 0; sl < 2; ++sl) {
+    row[sl] = 16 * (g + 4 * sl) + r;
+    const int rc = min(row[sl], C - 1);
+    const double* zp = (rc >> 4) == (C >> 4) ? Dfac + (C >> 4) * kTileSz + (C & 15) * kTS + (rc & 15) : S + tidx(C, rc);
+    const double z = *zp, rd = rD[rc];
+    rdv[sl] = rd;
+    x[sl] = row[sl] < C ? z * rd : 0.0;
+  }
+  int ti = (C - 1) >> 4;
+  BsOps A, B;
+  const bool chain = ti == nb - 1;  // the tile holding row C: no inverse, solved by its dependent chain
+  if (chain) bs2_load<true>(S, Dfac, Xinv, C, ti, row, rdv, A);
+  else bs2_load<false>(S, Dfac, Xinv, C, ti, row, rdv, A);
+  if (ti > 0) bs2_load<false>(S, Dfac, Xinv, C, ti - 1, row, rdv, B);
+  __builtin_amdgcn_sched_barrier(0);
+  if (chain) bs2_solve<true>(A, C, ti, row, rdv, pub, x);
+  else bs2_solve<false>(A, C, ti, row, rdv, pub, x);
+  if (xb && ti == pub_tile) bs_publish(C, pub_tile, xb, bflag, x);
+  --ti;
+#pragma unroll 1
+  while (ti >= 0) {  // B holds tile ti: prefetch ti - 1 into A, solve ti; then the roles swap
+    if (ti > 0) bs2_load<false>(S, Dfac, Xinv, C, ti - 1, row, rdv, A);
+    __builtin_amdgcn_sched_barrier(0);
+    bs2_solve<false>(B, C, ti, row, rdv, pub, x);
+    if (xb && ti == pub_tile) bs_publish(C, pub_tile, xb, bflag, x);
+    if (--ti < 0) break;
+    if (ti > 0) bs2_load<false>(S, Dfac, Xinv, C, ti - 1, row, rdv, B);
+    __builtin_amdgcn_sched_barrier(0);
+    bs2_solve<false>(A, C, ti, row, rdv, pub, x);
+    if (xb && ti == pub_tile) bs_publish(C, pub_tile, xb, bflag, x);
+    --ti;
   }
 }
 
@@ -3116,7 +3601,8 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update, int nth) {
   constexpr int kFinWave = CM > 0 ? 1 : 2;
   const bool fwave = (tid >> 6) == kFinWave;
   double dxr = 0.0;  // GN fused: max|dx_f| of the previous step, one column per rank
-  if (gfu && fwave) {
+  const bool xexp = CM == 0 && gfu && d.xexp;  // expanded partials: the image holds the finished sums (k_colsumx)
+  if (gfu && fwave && !xexp) {
     const int tid = threadIdx.x & 63;
     const int nr = d.Wtot - d.Wp;
     dxr = psum_max_at(d, d.Wp + min(tid, nr - 1));
@@ -3165,6 +3651,19 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update, int nth) {
     if (q < 2 * nst) (&camst[0][0])[q >= nst ? (q - nst) + (KB_MAX_CAMS * KB_MAX_INTR + 7 * (KB_MAX_CAMS - 1)) : q] = cpv[u];
   }
   __syncthreads();
+  if (xexp) {
+    // k_colsumx wrote the summed S - lambda^2 I, b and aux slots; lambda^2 and the identity padding (rows C ..) are
+    // added here, since the image may be an all-reduce over ranks; the cost and the per-rank max|dx_f| are aux slots
+    for (int i = tid; i < n16; i += nth) {
+      const int q = tidx(i, i);
+      S[q] = i < C ? S[q] + lam2 : 1.0;
+    }
+    if (tid == 0) cl_red[0] = bv[n16];
+    if (fwave) {
+      const int l = tid & 63, nr = d.nranks;
+      dxr = bv[n16 + 1 + min(l, nr - 1)];
+    }
+  }
   if (tid == 0) okl = (c->solve_ok != 0) && !(bv[C] > 0.0);
   // the loop's done flag is tested only here: the ctrl and staging loads above went out in one round trip, and
   // nothing global has been written yet
@@ -3338,7 +3837,11 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update, int nth) {
     const int cb0 = ctab[2][0], pub_tile = N > 1 ? cb0 >> 4 : -1;
     const bool upd = do_update && okl && !(gfu && fin[0]);
     if (tid < 64) {
+#ifdef KB_BACKSOLVE1
       panel_backsolve(d, S, Dfac, Xinv, rDv, C, nb, pubcol, x, pub_tile, xb, &bflag);
+#else
+      panel_backsolve2(d, S, Dfac, Xinv, rDv, C, nb, pubcol, x, pub_tile, xb, &bflag);
+#endif
       if (okl && !(gfu && fin[0])) wave0_tail(gfu ? fin[1] : cur);
     } else if ((tid >> 6) == 1 && upd) {
       const int lane = tid & 63, cu = gfu ? fin[1] : cur;
@@ -3409,10 +3912,11 @@ __global__ void __launch_bounds__(CM == 0 ? 512 : 256) k_solve(KbDev d, int gate
 }
 
 // ---------------------------------------------------------------------------------------------
-// k_backsub: one block per frame, one wave per camera view (waves = min(N, 8)).  Every wave forms
-// dx_f = L^-T (z - Y dx_c) (6 wave dot products), wave 0 stores dx / the new pose, each wave then evaluates
-// the cost of its views at the candidate state (evaluateError fused): per-frame [cost, max|dx|, dx.dx, dx.rhs].
-// All loads are issued in two dependent rounds (launch-independent ones, then those indexed by them).
+// k_backsub: one wave per frame, kBsFrames frames per block (a 2000-frame problem is 2000 waves, resident in one
+// round).  The wave forms dx_f = b_f - A_f dx_c (6 wave dot products), stores dx and the new pose, then evaluates the
+// cost of the frame's views at the candidate state (evaluateError fused), view after view in 64-corner passes with
+// the next pass's loads in flight: per-frame [cost, max|dx|, dx.dx, dx.rhs].  The launch-independent loads go out in
+// one round before the gate; the candidate chains and intrinsics are staged in LDS once per block.
 // k_post (one block) reduces the per-frame rows (+ camera stats) into red_local and, on one GPU, runs the
 // policy (accept / revert, next pass prelude); sharded runs all-reduce red first and run k_policy.
 // ---------------------------------------------------------------------------------------------
@@ -3424,20 +3928,21 @@ __global__ void __launch_bounds__(256) k_post(KbDev d, int policy) {
   pass_end_block(d, cin, &cnew, true, blockDim.x, policy != 0);
 }
 
-__global__ void __launch_bounds__(512) k_backsub(KbDev d, int gate, int do_update, int with_cost) {
+constexpr int kBsFrames = 4;  // k_backsub: frames (waves) per block
+__global__ void __launch_bounds__(64 * kBsFrames) k_backsub(KbDev d, int gate, int do_update, int with_cost) {
   KbCtrl* c = d.ctrl;
   __shared__ double tg[kTargetLds];
-  __shared__ double sc[8];
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, nw = blockDim.x >> 6, nth = blockDim.x;
-  const int f = blockIdx.x;
-  const int C = d.C, N = d.N;
+  __shared__ double cch[KB_MAX_CAMS][24];  // candidate chains L (12) | intrinsics (KB_MAX_INTR) of every camera
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, nth = blockDim.x;
+  const int C = d.C, N = d.N, F = d.F;
+  const int f = blockIdx.x * kBsFrames + wave, fc = min(f, F - 1);  // waves beyond F: loads clamped, no stores
   const bool cost_pass = do_update && with_cost;
   // ---- round 1: launch-independent loads, straight-line and unconditional (clamped) so that they are all in
   // flight together; the gate and the LDS stores come after
   const int done = c->done || (gate && d.gn_fused && !c->have_dx), sok = c->solve_ok, cur = c->cur;
   const bool tg_lds = 3 * d.K <= kTargetLds;
   const int nt3 = 3 * d.K;
-  constexpr int kTgU = 6;  // 6 x 64 >= 3 x 120 AprilGrid corners even for a one-wave block
+  constexpr int kTgU = 6;  // 6 x 256 >= 3 x 512 target corners staged in one round
   double tv[kTgU];
 #pragma unroll
   for (int u = 0; u < kTgU; ++u) tv[u] = d.target[min(tid + u * nth, nt3 - 1)];
@@ -3449,15 +3954,16 @@ __global__ void __launch_bounds__(512) k_backsub(KbDev d, int gate, int do_updat
     dxv[sl] = q < C ? v : 0.0;
 #pragma unroll
     for (int r = 0; r < 6; ++r) {
-      const double yv = d.Af[((size_t)f * 6 + r) * C + qc];
+      const double yv = d.Af[((size_t)fc * 6 + r) * C + qc];
       yr[r][sl] = q < C ? yv : 0.0;
     }
   }
-  const int cm0 = __builtin_amdgcn_readfirstlane(min(wave, N - 1));  // wave-uniform: scalar loads below
-  const int2 fv0 = d.fview[(size_t)f * N + cm0];
+  const double bq = d.bf[(size_t)fc * 6 + min(lane, 5)];
+  const int2 fvl = d.fview[(size_t)fc * N + min(lane, N - 1)];  // lane cm: the corner range of view (f, cm)
   // pin the round-1 values here: keeps the compiler from sinking the loads below the gate (one round trip)
-  KB_KEEPS(fv0.x);
-  KB_KEEPS(fv0.y);
+  KB_KEEP(fvl.x);
+  KB_KEEP(fvl.y);
+  KB_KEEP(bq);
 #pragma unroll
   for (int u = 0; u < kTgU; ++u) KB_KEEP(tv[u]);
 #pragma unroll
@@ -3466,134 +3972,118 @@ __global__ void __launch_bounds__(512) k_backsub(KbDev d, int gate, int do_updat
 #pragma unroll
     for (int r = 0; r < 6; ++r) KB_KEEP(yr[r][sl]);
   }
-  if (gate && done) return;
+  if (gate && done) return;  // block-uniform
   KB_STAMP(d, 30);
-  if (tg_lds && cost_pass) {
+  const bool work = (!gate || sok) && f < F;
+  const double* s0 = d.state + (size_t)cur * d.S;
+  double* s1 = d.state + (size_t)(1 - cur) * d.S;
+  // ---- round 2: loads indexed by round 1 (state buffers); the per-camera chains and intrinsics of the candidate state
+  // go to LDS once per block
+  if (cost_pass) {
+    if (tg_lds) {
 #pragma unroll
-    for (int u = 0; u < kTgU; ++u)
-      if (tid + u * nth < nt3) tg[tid + u * nth] = tv[u];
-    for (int q = tid + kTgU * nth; q < nt3; q += nth) tg[q] = d.target[q];
+      for (int u = 0; u < kTgU; ++u)
+        if (tid + u * nth < nt3) tg[tid + u * nth] = tv[u];
+      for (int q = tid + kTgU * nth; q < nt3; q += nth) tg[q] = d.target[q];
+    }
+    const double* Lp = cam_L(d, 1 - cur);
+    for (int q = tid; q < N * 22; q += nth) {
+      const int cm = q / 22, e = q - 22 * cm;
+      cch[cm][e] = e < 12 ? Lp[cm * 12 + e] : s1[cm * KB_MAX_INTR + e - 12];
+    }
   }
-  const bool work = !gate || sok;
-  double w[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  double pose[7];
+#pragma unroll
+  for (int q = 0; q < 7; ++q) pose[q] = do_update ? s0[d.off_frame + 7 * fc + q] : 0.0;
+  const double gq = d.gf[(size_t)fc * 6 + min(lane, 5)];
+  // dx_f = b_f - A_f dx_c (every lane ends with all six entries)
+  double w[6];
+  fdx_solve(yr, dxv, bq, w);
+  KB_STAMP(d, 31);
+  if (work && lane < 6) {
+    double xv = w[0];
+#pragma unroll
+    for (int r = 1; r < 6; ++r) xv = (lane == r) ? w[r] : xv;
+    d.dx[C + 6 * f + lane] = xv;
+    d.rhs[C + 6 * f + lane] = gq;
+  }
   double cost = 0.0;
-  if (work) {
-    // ---- round 2: loads indexed by round 1 (state buffer, corner ids of the view)
-    double pose[7], Lc[12], intr[KB_MAX_INTR];
-    const double* s0 = d.state + (size_t)cur * d.S;
-    double* s1 = d.state + (size_t)(1 - cur) * d.S;
-    if (do_update) {
+  if (do_update) {
+    double np[7];
+    update_pose(pose, w, np);  // every lane: the new pose stays in registers
+    if (work && lane < 7) {
+      double pv = np[0];
 #pragma unroll
-      for (int q = 0; q < 7; ++q) pose[q] = s0[d.off_frame + 7 * f + q];
+      for (int q = 1; q < 7; ++q) pv = (lane == q) ? np[q] : pv;
+      s1[d.off_frame + 7 * f + lane] = pv;
     }
-    int cid0[2] = {0, 0};
-    double2 y0[2];
-    if (cost_pass) {
-      const double* Lp = cam_L(d, 1 - cur) + cm0 * 12;
-#pragma unroll
-      for (int q = 0; q < 12; ++q) Lc[q] = Lp[q];
-#pragma unroll
-      for (int q = 0; q < KB_MAX_INTR; ++q) intr[q] = s1[cm0 * KB_MAX_INTR + q];
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int k = min(fv0.x + lane + 64 * u, max(fv0.y - 1, 0));
-        cid0[u] = d.cid[k];
-        y0[u] = d.y[k];
+    KB_STAMP(d, 32);
+    if (with_cost) {
+      const double* tgt = tg_lds ? tg : d.target;
+      __syncthreads();  // target and camera tables staged (every wave of the block reaches this)
+      double Ri[9], ti[3];
+      pose_inverse(np, Ri, ti);
+      // the frame's views one after the other in 64-corner passes; the next pass's corner ids and keypoints are in
+      // flight while the current pass projects (the views of a frame are contiguous, empty views are (0, 0))
+      auto lo = [&](int cm) { return __builtin_amdgcn_readlane(fvl.x, cm); };
+      auto hi = [&](int cm) { return __builtin_amdgcn_readlane(fvl.y, cm); };
+      int cm = 0, k0 = lo(0);
+      while (cm < N && k0 >= hi(cm)) {
+        ++cm;
+        if (cm < N) k0 = lo(cm);
       }
-    }
-#pragma unroll
-    for (int r = 0; r < 6; ++r) {
-      double s = yr[r][0] * dxv[0] + yr[r][1] * dxv[1];
-      s = wave_sum_d(s);
-      w[r] = d.bf[(size_t)f * 6 + r] - s;
-    }
-    KB_STAMP(d, 31);
-    if (wave == 0 && lane < 6) {
-      double xv = w[0];
-#pragma unroll
-      for (int r = 1; r < 6; ++r) xv = (lane == r) ? w[r] : xv;
-      d.dx[C + 6 * f + lane] = xv;
-      d.rhs[C + 6 * f + lane] = d.gf[(size_t)f * 6 + lane];
-    }
-    if (do_update) {
-      double np[7];
-      update_pose(pose, w, np);  // every lane: the new pose stays in registers
-      if (wave == 0 && lane < 7) {
-        double pv = np[0];
-#pragma unroll
-        for (int q = 1; q < 7; ++q) pv = (lane == q) ? np[q] : pv;
-        s1[d.off_frame + 7 * f + lane] = pv;
+      int cidn = 0;
+      double2 yn = make_double2(0.0, 0.0);
+      if (cm < N) {
+        const int k = min(k0 + lane, hi(cm) - 1);
+        cidn = d.cid[k];
+        yn = d.y[k];
       }
-      KB_STAMP(d, 32);
-      if (with_cost) {
-        const double* tgt = tg_lds ? tg : d.target;
-        if (tg_lds) __syncthreads();  // target staged
-        double Ri[9], ti[3];
-        pose_inverse(np, Ri, ti);
-        for (int cm = wave; cm < N; cm += nw) {
-          int2 fv = fv0;
-          if (cm != wave) {  // rigs with more than 8 cameras: second view of this wave (unbatched loads)
-            fv = d.fview[(size_t)f * N + cm];
-            const double* Lp = cam_L(d, 1 - cur) + cm * 12;
-#pragma unroll
-            for (int q = 0; q < 12; ++q) Lc[q] = Lp[q];
-#pragma unroll
-            for (int q = 0; q < KB_MAX_INTR; ++q) intr[q] = s1[cm * KB_MAX_INTR + q];
-          }
-          if (fv.y <= fv.x) continue;
-          double R[9], t[3];
-          rt_mul(Lc, Lc + 9, Ri, ti, R, t);  // T_cam_w = L_cam(candidate) T_f^-1
-          const int model = cam_arg(d.model, cm);
-          for (int k0 = fv.x; k0 < fv.y; k0 += 128) {
-            int cid[2];
-            double2 yv[2];
-            if (k0 == fv0.x && cm == wave) {
-#pragma unroll
-              for (int u = 0; u < 2; ++u) {
-                cid[u] = cid0[u];
-                yv[u] = y0[u];
-              }
-            } else {
-#pragma unroll
-              for (int u = 0; u < 2; ++u) {
-                const int k = min(k0 + lane + 64 * u, fv.y - 1);
-                cid[u] = d.cid[k];
-                yv[u] = d.y[k];
-              }
-            }
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-              if (k0 + lane + 64 * u < fv.y) {
-                const double X0 = tgt[3 * cid[u]], X1 = tgt[3 * cid[u] + 1], X2 = tgt[3 * cid[u] + 2];
-                const double p0 = R[0] * X0 + R[1] * X1 + R[2] * X2 + t[0];
-                const double p1 = R[3] * X0 + R[4] * X1 + R[5] * X2 + t[1];
-                const double p2 = R[6] * X0 + R[7] * X1 + R[8] * X2 + t[2];
-                double u0, u1;
-                project(model, intr, p0, p1, p2, u0, u1);
-                const double e0 = yv[u].x - u0, e1 = yv[u].y - u1;
-                cost += e0 * e0 + e1 * e1;
-              }
-            }
-          }
+      int lastc = -1;
+      double R[9], t[3];
+      while (cm < N && work) {  // wave-uniform
+        const int cc = cm, kk = k0, hc = hi(cm);
+        const int cid = cidn;
+        const double2 yv = yn;
+        k0 += 64;
+        while (cm < N && k0 >= hi(cm)) {
+          ++cm;
+          if (cm < N) k0 = lo(cm);
         }
-        cost = wave_sum_d(cost);
+        if (cm < N) {
+          const int k = min(k0 + lane, hi(cm) - 1);
+          cidn = d.cid[k];
+          yn = d.y[k];
+        }
+        if (cc != lastc) {
+          rt_mul(cch[cc], cch[cc] + 9, Ri, ti, R, t);  // T_cam_w = L_cam(candidate) T_f^-1
+          lastc = cc;
+        }
+        if (kk + lane < hc) {
+          const double X0 = tgt[3 * cid], X1 = tgt[3 * cid + 1], X2 = tgt[3 * cid + 2];
+          const double p0 = R[0] * X0 + R[1] * X1 + R[2] * X2 + t[0];
+          const double p1 = R[3] * X0 + R[4] * X1 + R[5] * X2 + t[1];
+          const double p2 = R[6] * X0 + R[7] * X1 + R[8] * X2 + t[2];
+          double u0, u1;
+          project(cam_arg(d.model, cc), cch[cc] + 12, p0, p1, p2, u0, u1);
+          const double e0 = yv.x - u0, e1 = yv.y - u1;
+          cost += e0 * e0 + e1 * e1;
+        }
       }
+      cost = wave_sum_d(cost);
     }
   }
   KB_STAMP(d, 33);
-  if (lane == 0) sc[wave] = cost;
-  __syncthreads();
-  if (tid == 0 && work) {
-    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-    for (int q = 0; q < nw; ++q) a0 += sc[q];
+  if (work && lane == 0) {
+    double a1 = 0.0, a2 = 0.0, a3 = 0.0;
 #pragma unroll
     for (int r = 0; r < 6; ++r) {
-      const double g = d.gf[(size_t)f * 6 + r];
+      const double g = readlane_d(gq, r);
       a1 = fmax(a1, fabs(w[r]));
       a2 += w[r] * w[r];
       a3 += w[r] * g;
     }
-    reinterpret_cast<double4*>(d.bpart)[f] = make_double4(a0, a1, a2, a3);
+    reinterpret_cast<double4*>(d.bpart)[f] = make_double4(cost, a1, a2, a3);
   }
 }
 

@@ -56,18 +56,34 @@ class TcpGroup:
             srv.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
             srv.bind((addr, port))
             srv.listen(self.world)
-            srv.settimeout(max(1.0, deadline - time.monotonic()))
             by_rank = {}
-            while len(by_rank) < self.world - 1:
-                c, _ = srv.accept()
-                c.settimeout(timeout)
-                hello = _recv(c)
-                if not hello.startswith(_MAGIC):
+            try:
+                while len(by_rank) < self.world - 1:
+                    left = deadline - time.monotonic()
+                    if left <= 0:
+                        raise TimeoutError(f"rank 0: {len(by_rank)} of {self.world - 1} ranks reached {addr}:{port}")
+                    srv.settimeout(left)  # recomputed per connection: foreign connects cannot extend the deadline
+                    try:
+                        c, _ = srv.accept()
+                    except socket.timeout:
+                        continue
+                    # a peer gets at most the remaining time (and 10 s) to say hello
+                    c.settimeout(max(0.1, min(10.0, deadline - time.monotonic())))
+                    peer = self._hello_rank(c)
+                    if peer is None or peer in by_rank:
+                        # not a rendezvous client, a rank id outside 1..world-1, or a duplicate rank: refused before
+                        # the handshake reply, so the refused client never takes this server for rank 0
+                        c.close()
+                        continue
+                    c.settimeout(timeout)
+                    by_rank[peer] = c
+                    _send(c, _MAGIC)
+            except BaseException:
+                for c in by_rank.values():
                     c.close()
-                    continue
-                by_rank[int(hello[len(_MAGIC):])] = c
-                _send(c, _MAGIC)
-            srv.close()
+                raise
+            finally:
+                srv.close()
             self.peers = [by_rank[r] for r in range(1, self.world)]
         else:
             while True:
@@ -84,6 +100,21 @@ class TcpGroup:
                 if time.monotonic() > deadline:
                     raise TimeoutError(f"rank {self.rank}: no rendezvous with rank 0 at {addr}:{port}")
                 time.sleep(0.2)
+
+    def _hello_rank(self, c):
+        """the rank id of a client's hello, or None for anything else (a foreign service, a malformed or truncated
+        hello, a rank outside 1..world-1)"""
+        try:
+            hello = _recv(c)
+        except (OSError, ConnectionError, struct.error):
+            return None
+        if not hello.startswith(_MAGIC):
+            return None
+        try:
+            peer = int(hello[len(_MAGIC):].decode("ascii"))
+        except (UnicodeDecodeError, ValueError):
+            return None
+        return peer if 1 <= peer < self.world else None
 
     def _gather_reply(self, payload: bytes, reply_fn):
         """every rank sends payload to rank 0; rank 0 computes reply_fn([payload of rank 0..world-1]) and sends it

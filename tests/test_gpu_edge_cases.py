@@ -128,3 +128,31 @@ def test_full_size_rig8_parity(capi, oracle_mod):
     ok, dx = g.solve()
     ok_o, dx_o = o.solve(A, 10.0, nthreads=16)
     assert ok and ok_o and _rel(dx, dx_o) < 1e-8
+
+
+def test_stale_preparation_and_system_are_refused(capi):
+    """kb_gn_launch refuses a preparation that a later call voided (state set, per-call solve, another loop), and the
+    per-call system accessors (kb_rhs_jtj_rhs, kb_get_normal_blocks) refuse to read blocks a device-resident loop
+    overwrote or skipped; a fresh kb_build makes them valid again."""
+    p = synth.make_config(2, n_frames=16)
+    g = capi.Solver(p)
+    g.set_state(p.state_init)
+    g.gn_prepare(3)
+    g.set_state(p.state_init)  # voids the prepared loop start
+    with pytest.raises(capi.KbError, match="not prepared"):
+        g.gn_launch(3)
+    g.gn_prepare(3)
+    g.build()  # a per-call entry point voids it too
+    with pytest.raises(capi.KbError, match="not prepared"):
+        g.gn_launch(3)
+    g.gn_prepare(3)
+    g.gn_launch(3)  # prepared and untouched: runs
+    with pytest.raises(capi.KbError, match="no intact system"):
+        g.rhs_jtj_rhs()
+    with pytest.raises(capi.KbError, match="no intact system"):
+        g.normal_blocks()
+    g.build()
+    assert np.isfinite(g.rhs_jtj_rhs())
+    g.optimize(policy="lm", max_iterations=3)
+    with pytest.raises(capi.KbError, match="no intact system"):
+        g.rhs_jtj_rhs()

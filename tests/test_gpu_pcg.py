@@ -255,3 +255,44 @@ def test_pcg_schur_defaults_contract(capi, oracle_mod, name):
     r1 = info["residual"]
     ok2, _ = g.solve()  # absolute mode: d0 = max(tol dn0, the previous _residual)
     assert ok2 and g.pcg_info()["d0"] >= r1 * (1 - 1e-12)
+
+
+def _without_camera(p, cam):
+    """the problem with every view of camera `cam` removed (its intrinsic block of S is then zero at lambda = 0)"""
+    keep = np.nonzero(p.view_cam != cam)[0]
+    offs = p.view_offset
+    corners = np.concatenate([np.arange(offs[v], offs[v + 1]) for v in keep])
+    counts = offs[keep + 1] - offs[keep]
+    return synth.Problem(cam_model=p.cam_model.copy(), target=p.target.copy(), view_frame=p.view_frame[keep].copy(),
+                         view_cam=p.view_cam[keep].copy(),
+                         view_offset=np.concatenate([[0], np.cumsum(counts)]).astype(np.int32),
+                         corner_id=p.corner_id[corners].copy(), y=p.y[corners].copy(), state_truth=p.state_truth,
+                         state_init=p.state_init, name=p.name + "-cam%d" % cam)
+
+
+def test_pcg_schur_failed_solve_keeps_previous_residual(capi):
+    """A failed Schur-PCG solve (a singular camera DV block: camera 1 unobserved, lambda = 0) returns ok = 0 and leaves
+    LinearSolverPCG's _residual as the last completed solve set it: the next absolute-tolerance solve's d0 is the
+    one a solver that never saw the failed attempt computes."""
+    p = _without_camera(synth.make_config(2, n_frames=30), 1)
+    runs = []
+    for with_failure in (False, True):
+        g = capi.Solver(p)
+        g.set_state(p.state_init)
+        g.build()
+        g.set_linear_solver("pcg_schur")
+        g.set_constant_conditioner(10.0)
+        ok1, _ = g.solve()
+        i1 = g.pcg_info()
+        if with_failure:
+            g.set_constant_conditioner(0.0)
+            okf, _ = g.solve()
+            assert not okf
+            assert g.pcg_info() == i1  # the failed attempt reports nothing new
+            g.set_constant_conditioner(10.0)
+        ok2, dx2 = g.solve()
+        runs.append((ok1, ok2, g.pcg_info(), dx2))
+        g.close()
+    (a1, a2, ia, dxa), (b1, b2, ib, dxb) = runs
+    assert a1 and a2 and b1 and b2
+    assert ia == ib and np.array_equal(dxa, dxb)

@@ -137,6 +137,48 @@ def test_sharded_fixed_gn_passes_and_per_call_api(capi, name):
     assert float(np.abs(dxf - dx0[C:]).max()) <= 1e-8 * float(np.abs(dx0).max())
 
 
+@pytest.mark.parametrize("name", ["c2_2ranks", "c4_3ranks"])
+def test_sharded_pcg_schur_matches_unsharded(capi, name):
+    """KB_SOLVER_PCG_SCHUR on a sharded handle: every rank runs the same block-Jacobi PCG on the all-reduced camera
+    Schur complement, so all ranks hold bitwise-identical camera steps, iteration counts and _residual; the frame
+    steps are each rank's own back-substitution.  Bars: converged tightly, the unsharded handle's PCG-on-S step (the
+    column sums group the frames differently, so the CG iterates differ in the last bits; at the reference tolerance CG
+    amplifies that, so the defaults are checked for rank agreement and the _residual carry-over only)."""
+    mk, cuts = CASES[name]
+    p = mk()
+    tight = dict(tolerance=1e-28, max_iterations=4000, absolute_tolerance=False)
+    ref = capi.Solver(p)
+    ref.set_state(p.state_init)
+    ref.set_linear_solver("pcg_schur", **tight)
+    ref.build()
+    ref.set_constant_conditioner(10.0)
+    ok0, dx0 = ref.solve()
+    solvers = _shards(capi, p, cuts)
+
+    def solve(s):
+        s.build()
+        s.set_constant_conditioner(10.0)
+        s.set_linear_solver("pcg_schur", **tight)
+        rt = s.solve()
+        s.set_linear_solver("pcg_schur")  # LinearSolverPCG defaults (absolute tolerance), _residual reset
+        r1 = s.solve()
+        a = s.pcg_info()
+        r2 = s.solve()  # absolute tolerance: d0 = max(tol dn0, the previous solve's _residual)
+        return rt, r1, a, r2, s.pcg_info()
+
+    out = _run_all(solvers, solve)
+    C = ref.C
+    assert ok0
+    for (okt, dxt), (ok1, dx1), inf, (ok2, dx2), inf2 in out:
+        assert okt and ok1 and ok2
+        assert np.array_equal(dxt[:C], out[0][0][1][:C]) and np.array_equal(dx1[:C], out[0][1][1][:C])
+        assert inf == out[0][2] and inf2 == out[0][4]  # every rank: the same PCG run
+        assert float(np.abs(dxt[:C] - dx0[:C]).max()) <= 1e-8 * float(np.abs(dx0[:C]).max())
+        assert inf2["d0"] >= inf["residual"] * (1 - 1e-12)  # LinearSolverPCG: d0 = max(tol dn, _residual)
+    dxf = np.concatenate([o[0][1][C:] for o in out])
+    assert float(np.abs(dxf - dx0[C:]).max()) <= 1e-8 * float(np.abs(dx0).max())
+
+
 def test_local_group_rejects_bad_lists(capi):
     p = synth.make_config(2, n_frames=6)
     a = capi.Solver(p)

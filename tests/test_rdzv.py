@@ -48,6 +48,73 @@ def test_world_one_is_local():
     assert g.max(2.0) == 2.0
 
 
+def _raw_client(port, payload, q, tag):
+    """a client that sends one framed hello and reports whether rank 0 answered with the handshake"""
+    import time as _t
+    deadline = _t.monotonic() + 30.0
+    while True:
+        try:
+            s = socket.create_connection(("127.0.0.1", port), timeout=2.0)
+            break
+        except OSError:
+            if _t.monotonic() > deadline:
+                q.put((tag, "no server"))
+                return
+            _t.sleep(0.1)
+    s.settimeout(10.0)
+    try:
+        s.sendall(struct.pack("<Q", len(payload)) + payload)
+        r = s.recv(64)
+        q.put((tag, "reply" if r else "closed"))
+    except OSError:
+        q.put((tag, "closed"))
+    finally:
+        s.close()
+
+
+def test_bad_hello_and_duplicate_rank_are_refused():
+    """rank 0 survives a malformed hello, an out-of-range rank and a duplicate rank id: each is closed without the
+    handshake reply, and the real ranks still form the group"""
+    import threading
+    import queue
+    port = _free_port()
+    q = queue.Queue()
+    res = {}
+
+    def server():
+        g = rdzv.TcpGroup(0, 3, addr="127.0.0.1", port=port, timeout=30.0)
+        res["server"] = g.max(1.0)
+        g.close()
+
+    t0 = threading.Thread(target=server)
+    t0.start()
+    bad = [(rdzv._MAGIC + b"x1", "malformed"), (rdzv._MAGIC + b"7", "out of range"), (b"GET / HTTP/1.0", "foreign")]
+    for payload, tag in bad:
+        _raw_client(port, payload, q, tag)
+    got = dict(q.get(timeout=30) for _ in bad)
+    assert all(v == "closed" for v in got.values()), got
+
+    out = {}
+
+    def client(r):
+        g = rdzv.TcpGroup(r, 3, addr="127.0.0.1", port=port, timeout=30.0)
+        out[r] = g.max(float(r))
+        g.close()
+
+    t1 = threading.Thread(target=client, args=(1,))
+    t1.start()
+    # wait until rank 1 is registered, then a second "rank 1" must be refused
+    import time as _t
+    _t.sleep(1.0)
+    _raw_client(port, rdzv._MAGIC + b"1", q, "duplicate")
+    assert q.get(timeout=30) == ("duplicate", "closed")
+    t2 = threading.Thread(target=client, args=(2,))
+    t2.start()
+    for t in (t0, t1, t2):
+        t.join(timeout=60)
+    assert res["server"] == 2.0 and out == {1: 2.0, 2: 2.0}
+
+
 def test_foreign_service_is_rejected():
     """a client that reaches a non-rendezvous server does not take its reply for rank 0's handshake"""
     srv = socket.socket()
