@@ -97,6 +97,20 @@ int kb_set_conditioner(kb_handle* h, const double* diag);
  * solves (J^T J + diag^2 I) dx = rhs.  *ok = 0 on a non-positive-definite system
  * (CHOLMOD failure semantics, Cholmod(impl).hpp:287-328); dx_out untouched then. */
 int kb_solve(kb_handle* h, double* dx_out, int* ok);
+/* IncrementalEstimator::addBatch on the device (aslam_incremental_calibration IncrementalEstimator.cpp:343-373,
+ * 517-527): the reference re-runs initMatrixStructure over the grown problem on every batch; here the new frames are
+ * appended to the uploaded handle in place.  kb_append_frames adds n_frames frames (their views sorted by frame,
+ * view_frame counted from 0 within the appended block, view_offsets local: [n_views + 1] from 0 to n_corners) and
+ * writes their poses ([n_frames][7], q xyzw | t) into the current state; the other design variables keep their
+ * device values.  Device buffers grow geometrically and only the new observations cross PCIe, so appending F frames
+ * one at a time moves O(F) data in total (the reference's re-initialisation: O(F^2)).  kb_drop_last_frames removes the
+ * last n_frames frames with their views and corners (a rejected batch; at least one frame stays).  Captured graphs
+ * and a kb_gn_prepare'd loop are voided.  Unsharded handles. */
+int kb_append_frames(kb_handle* h, int32_t n_frames, int32_t n_views, int32_t n_corners, const double* y,
+                     const uint16_t* corner_id, const uint32_t* view_offsets, const uint32_t* view_frame,
+                     const uint8_t* view_cam, const double* frame_poses);
+int kb_drop_last_frames(kb_handle* h, int32_t n_frames);
+
 /* Linear solver behind kb_solve ("direct or PCG by mode").
  *   KB_SOLVER_SCHUR  (default) frame-block Schur complement + dense camera-block LDL^T: the exact solve that
  *                    replaces CHOLMOD (SparseCholeskyLinearSystemSolver.cpp:48-89); parity mode.
@@ -204,6 +218,18 @@ typedef struct kb_solution {
 } kb_solution;
 
 int kb_optimize(kb_handle* h, const kb_optimizer_options* opts, kb_solution* out);
+
+/* The IncrementalEstimator's optimisation device-resident (IncrementalEstimator.cpp:46-77, 373: Optimizer2 with the
+ * GaussNewtonTrustRegionPolicy over calibration::LinearSolver): every pass builds with the frame blocks eliminated,
+ * solves the camera block by the column-scaled truncated SVD of kb_solve_marginal, updates the design variables,
+ * evaluates the cost and runs the policy (accept, convergence tests on convergence_dx / convergence_dj,
+ * max_iterations) on the device; the passes run as captured graphs and the host polls the done flag every sync_every
+ * passes.  opts->policy must be 1 (GN); opts->lambda_init is unused.  info / sv_out / V_out: the SVD of the last
+ * solve (as kb_solve_marginal reports it; any may be NULL).  kb_analyze_marginal afterwards analyses the last
+ * build, as analyzeMarginal after Optimizer2::optimize does.  Unsharded handles, C <= 112. */
+int kb_optimize_marginal(kb_handle* h, const kb_optimizer_options* opts, const kb_marginal_options* mopts,
+                         kb_solution* out, kb_marginal_info* info, double* sv_out, double* V_out);
+
 /* Per-pass trace of the last kb_optimize: [J, lambda, deltaX, accepted] x n (returns count). */
 int kb_get_trace(kb_handle* h, double* trace, int32_t cap);
 

@@ -23,7 +23,7 @@ EXPORTS = [
     "kb_get_state_flat", "kb_state_size", "kb_num_cols", "kb_camera_cols", "kb_eval_cost", "kb_build",
     "kb_set_constant_conditioner", "kb_set_conditioner", "kb_solve", "kb_get_rhs", "kb_rhs_jtj_rhs", "kb_apply_update", "kb_revert", "kb_get_normal_blocks",
     "kb_optimize", "kb_get_trace", "kb_run_gn_iterations", "kb_gn_prepare", "kb_gn_launch", "kb_build_kernel_stats",
-    "kb_build_kernel_name", "kb_comm_get_unique_id", "kb_gn_pass_times",
+    "kb_build_kernel_name", "kb_comm_get_unique_id", "kb_gn_pass_times", "kb_append_frames", "kb_drop_last_frames", "kb_optimize_marginal",
     "kb_comm_init", "kb_comm_init_local", "kb_selftest_mfma", "kb_solve_marginal", "kb_analyze_marginal",
     # block-Jacobi PCG (LinearSolverPCG)
     "kb_set_linear_solver", "kb_pcg_init", "kb_get_pcg_info",
@@ -128,6 +128,9 @@ def lib():
         L.kb_build_kernel_name.argtypes = [C.c_void_p, C.c_char_p, C.c_int32]
         L.kb_build_kernel_stats.argtypes = [C.c_void_p, dp, dp, dp]
         L.kb_gn_pass_times.argtypes = [C.c_void_p, C.c_int32, dp, dp]
+        L.kb_append_frames.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, dp, C.c_void_p, C.c_void_p,
+                                       C.c_void_p, C.c_void_p, dp]
+        L.kb_drop_last_frames.argtypes = [C.c_void_p, C.c_int32]
         L.kb_comm_get_unique_id.argtypes = [C.c_void_p]
         L.kb_comm_init.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32]
         L.kb_comm_init_local.argtypes = [C.POINTER(C.c_void_p), C.c_int32]
@@ -357,6 +360,28 @@ class Solver:
         ms, by, fl = C.c_double(), C.c_double(), C.c_double()
         _check(lib().kb_build_kernel_stats(self.h, C.byref(ms), C.byref(by), C.byref(fl)))
         return ms.value, by.value, fl.value
+
+    def append_frames(self, sub, poses=None):
+        """kb_append_frames: the frames of problem `sub` (same rig; its frames numbered from 0) appended in place;
+        poses [n_frames][7] default to the frame poses of sub.state_init"""
+        y = np.ascontiguousarray(sub.y, dtype=np.float64)
+        cid = np.ascontiguousarray(sub.corner_id, dtype=np.uint16)
+        vo = np.ascontiguousarray(sub.view_offset, dtype=np.uint32)
+        vf = np.ascontiguousarray(sub.view_frame, dtype=np.uint32)
+        vc = np.ascontiguousarray(sub.view_cam, dtype=np.uint8)
+        so = sub.n_cams * 10 + 7 * (sub.n_cams - 1)  # KB_MAX_INTR = 10
+        ps = np.ascontiguousarray(sub.state_init[so:] if poses is None else poses, dtype=np.float64)
+        _check(lib().kb_append_frames(self.h, sub.n_frames, sub.n_views, sub.n_corners, _d(y), cid.ctypes.data,
+                                      vo.ctypes.data, vf.ctypes.data, vc.ctypes.data, _d(ps)))
+        self._resize()
+
+    def drop_last_frames(self, n):
+        _check(lib().kb_drop_last_frames(self.h, int(n)))
+        self._resize()
+
+    def _resize(self):
+        self.S = lib().kb_state_size(self.h)
+        self.ncols = lib().kb_num_cols(self.h)
 
     def gn_pass_times(self, n):
         """(pass_ms [n], build_ms [n]) of n GN passes from the current state, device-timed (kb_gn_pass_times)"""

@@ -13,6 +13,7 @@
 #include <cstring>
 #include <functional>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/kalibr_hip.h"
@@ -56,7 +57,8 @@ int nintr_host(int m) {
 }  // namespace
 
 constexpr int kGraphPasses = 8;  // optimizer passes per captured multi-pass graph
-constexpr int kXMaxRanks = 64;   // expanded partials: per-rank max|dx_f| slots in the image's aux area
+constexpr int kXMaxRanks = 64;
+constexpr int kPolicyMarginal = 2;  // graph policy id of kb_optimize_marginal's passes (GN over the marginal solve)   // expanded partials: per-rank max|dx_f| slots in the image's aux area
 constexpr int kLocalMaxRanks = 16;  // kb_comm_init_local group size
 
 // In-process group of sharded handles (kb_comm_init_local): the collectives become device copies between the
@@ -117,6 +119,12 @@ struct kb_handle {
   bool build_pipe = false;  // k_buildp (one wave per camera, N + 2 waves) instead of k_build
   bool xexp = false;        // GN fused passes with expanded partials (C > 64, k_buildp): k_colsumx, no k_colimg
   std::vector<int32_t> vcam;  // camera of each view (host copy: the algorithmic flop count)
+  // growth in place (kb_append_frames / kb_drop_last_frames): device capacities and host mirrors of the view layout
+  int bpc = 1;                      // k_buildp blocks per CU (frames per block = ceil(F / (256 bpc)))
+  int F_cap = 0, V_cap = 0, NC_cap = 0;
+  std::vector<uint32_t> vo_host;    // [V + 1] view offsets
+  std::vector<int32_t> frame_v0;    // [F + 1] first view of each frame (frame_v0[F] = V)
+  size_t pcg_F = 0, rjr_F = 0, cond_n = 0;  // frame count / columns the lazily allocated buffers are sized for
   double* ximg_part = nullptr;  // sharded + xexp: this rank's partial image (all-reduced into d.simg)
   bool buildp_wide = false;  // k_buildp<.., MW = 8> (multi-model rigs with <= 8 waves per block)
   double* rjr = nullptr;     // [F + 1] kb_rhs_jtj_rhs: per-frame terms | result
@@ -158,6 +166,8 @@ struct kb_handle {
   // build-kernel timing
   double build_ms = 0.0;
   double* marg_buf = nullptr;  // marginal solver outputs: V [C][C] | sv [C] | info [8]
+  KbMarg marg{};               // kb_optimize_marginal: the k_marg arguments its captured passes use
+  size_t lds_marg = 0;
   // linear solver of kb_solve: KB_SOLVER_SCHUR (direct) or KB_SOLVER_PCG (LinearSolverPCG)
   int solver_kind = KB_SOLVER_SCHUR;
   kb_pcg_options pcg{1e-6, -1, 1};
@@ -209,6 +219,33 @@ static const void* pick_build(int mb, unsigned mm, bool pipe, bool wide) {
       return build_fn<GN, (1u << KB_OMNI_RADTAN) | (1u << KB_EUCM)>(mb, pipe, wide);
     default: return build_fn<GN, kMmAll>(mb, pipe, wide);
   }
+}
+
+// the frame-count-dependent layout: columns, state size, build blocks (frames per block), step rows
+static void set_frame_counts(kb_handle* h) {
+  KbDev& d = h->d;
+  h->ncols = h->C + 6 * h->F;
+  h->S = h->N * KB_MAX_INTR + 7 * (h->N - 1) + 7 * h->F;
+  d.F = h->F;
+  d.ncols = h->ncols;
+  if (d.S < h->S) d.S = h->S;  // d.S: the slot stride of the [2][S] state buffer (its capacity), >= the state size
+  d.gframes = h->build_pipe ? (h->F + 256 * h->bpc - 1) / (256 * h->bpc) : (h->F + 511) / 512;
+  d.nblk = (h->F + d.gframes - 1) / d.gframes;
+  d.nblk_bs = h->F;  // k_backsub: one step row per frame (one wave per frame)
+}
+
+// dynamic LDS of the build kernel (depends on the frames per block through the staged frame poses)
+static size_t build_lds(const kb_handle* h) {
+  const int N = h->N, C = h->C, WPB = h->d.wpb;
+  const int CZ = 16 * ((C + 16) / 16);  // [Y | z] row stride of the Schur tiles
+  const int tgl = (3 * h->K <= kTargetLds ? 3 * h->K : 0) + 8 * h->d.gframes;
+  if (h->build_pipe) {  // k_buildp: tiles | H | chains | 2 view buffers | frame-wave buffers | K | target, poses
+    const int np = N * (N - 1) / 2, nf = (C + 16) / 16 <= 4 ? 2 : 4;  // as build_threads
+    return sizeof(double) * (N * 64 * XS + N * 256 + N * 64 + (36 * np + 44 * N + 6 * CZ) + (40 + 6 * CZ) +
+                             nf * 6 * CZ + 36 * np + tgl);
+  }
+  return sizeof(double) * (WPB * 64 * XS + WPB * 256 + N * (256 + 256 + 64 + 36 + 36 + 8) + 36 + 16 * CZ +
+                           18 * N * (N - 1) + tgl);
 }
 
 static void drop_graphs(kb_handle* h) {
@@ -274,6 +311,41 @@ int fail(const std::string& m) {
 }
 }  // namespace kb_internal
 
+// replace a device buffer by a larger one, its first `keep` elements copied and the rest zero (kb_append_frames)
+template <class T>
+static int regrow(kb_handle* h, T** p, size_t n_new, size_t keep) {
+  using U = typename std::remove_const<T>::type;
+  void* q = nullptr;
+  const size_t bytes = std::max<size_t>(n_new, 1) * sizeof(T);
+  KB_HIP(hipMalloc(&q, bytes));
+  KB_HIP(hipMemsetAsync(q, 0, bytes, h->stream));
+  void* old = (void*)const_cast<U*>(*p);
+  if (old && keep) KB_HIP(hipMemcpyAsync(q, old, keep * sizeof(T), hipMemcpyDeviceToDevice, h->stream));
+  if (old) {
+    KB_HIP(hipStreamSynchronize(h->stream));  // the copy is done before the old buffer goes
+    auto it = std::find(h->allocs.begin(), h->allocs.end(), old);
+    if (it != h->allocs.end()) h->allocs.erase(it);
+    KB_HIP(hipFree(old));
+  }
+  h->allocs.push_back(q);
+  *p = (T*)q;
+  return 0;
+}
+
+// the frame-count-dependent launch state after kb_append_frames / kb_drop_last_frames: LDS of the build kernel,
+// captured graphs (their kernel arguments hold the old layout), prepared loops and the per-call system
+static int relayout(kb_handle* h) {
+  set_frame_counts(h);
+  h->lds_build = build_lds(h);
+  if (h->lds_build > 160 * 1024) return fail("kb_append_frames: build-kernel LDS budget exceeded for this frame count");
+  KB_HIP(hipFuncSetAttribute(h->fn_build, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_build));
+  KB_HIP(hipFuncSetAttribute(h->fn_build_gn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_build));
+  drop_graphs(h);
+  unprepare(h);
+  h->sys_valid = false;
+  return 0;
+}
+
 extern "C" {
 
 const char* kb_last_error(void) { return g_err.c_str(); }
@@ -335,12 +407,8 @@ kb_handle* kb_create(const kb_layout* L) {
     delete h;
     return nullptr;
   }
-  h->ncols = h->C + 6 * h->F;
-  h->S = h->N * KB_MAX_INTR + 7 * (h->N - 1) + 7 * h->F;
   h->W = h->C * (h->C + 1) / 2 + h->C;
   d.C = h->C;
-  d.ncols = h->ncols;
-  d.S = h->S;
   d.off_base = h->N * KB_MAX_INTR;
   d.off_frame = h->N * KB_MAX_INTR + 7 * (h->N - 1);
   d.nsplit = std::max(1, (4 + h->N - 1) / h->N);  // >= 4 waves per build block
@@ -361,13 +429,10 @@ kb_handle* kb_create(const kb_layout* L) {
     for (int i = 0; i < h->N; ++i) mm0 |= 1u << d.model[i];
     h->buildp_wide = __builtin_popcount(mm0) >= 2 && h->N + nf <= 8;
     if (const char* e = std::getenv("KB_BUILDP_WIDE")) h->buildp_wide = h->buildp_wide && std::atoi(e) != 0;
-    const int bpc = (h->N + nf <= 6 && !h->buildp_wide) ? 2 : 1;
-    d.gframes = (h->F + 256 * bpc - 1) / (256 * bpc);
-  } else {
-    d.gframes = (h->F + 511) / 512;
+    h->bpc = (h->N + nf <= 6 && !h->buildp_wide) ? 2 : 1;
   }
-  d.nblk = (h->F + d.gframes - 1) / d.gframes;
-  d.nblk_bs = h->F;  // k_backsub: one step row per frame (one wave per frame)
+  set_frame_counts(h);
+  h->F_cap = h->F;
   d.W = h->W;
   d.Wp = h->N * 136 + h->W + 1;
   d.Wr = d.Wp + 1;
@@ -383,7 +448,7 @@ kb_handle* kb_create(const kb_layout* L) {
   int rc = 0;
   double* tgt = nullptr;
   rc |= h->alloc(&tgt, 3 * (size_t)h->K);
-  rc |= h->alloc(&d.state, 2 * (size_t)h->S);
+  rc |= h->alloc(&d.state, 2 * (size_t)d.S);
   rc |= h->alloc(&d.camL, 2 * 12 * (size_t)h->N);  // [2] slots: ping-pong with the state buffers
   rc |= h->alloc(&d.camK, 2 * 36 * (size_t)h->N * h->N);
   rc |= h->alloc(&d.Hff, 36 * (size_t)h->F);
@@ -444,15 +509,8 @@ kb_handle* kb_create(const kb_layout* L) {
   {
     const int N = h->N, C = h->C, WPB = d.wpb;
     const int CZ = 16 * ((C + 16) / 16);  // [Y | z] row stride of the Schur tiles
-    const int tgl = (3 * h->K <= kTargetLds ? 3 * h->K : 0) + 8 * d.gframes;
-    if (h->build_pipe) {  // k_buildp: tiles | H | chains | 2 view buffers | frame-wave buffers | K | target, poses
-      const int np = N * (N - 1) / 2, nf = (C + 16) / 16 <= 4 ? 2 : 4;  // as build_threads
-      h->lds_build = sizeof(double) * (N * 64 * XS + N * 256 + N * 64 + (36 * np + 44 * N + 6 * CZ) +
-                                       (40 + 6 * CZ) + nf * 6 * CZ + 36 * np + tgl);
-    } else {
-      h->lds_build = sizeof(double) * (WPB * 64 * XS + WPB * 256 + N * (256 + 256 + 64 + 36 + 36 + 8) + 36 +
-                                       16 * CZ + 18 * N * (N - 1) + tgl);
-    }
+    (void)WPB;
+    h->lds_build = build_lds(h);
     h->lds_camexp = sizeof(double) * (N * 256 + N * N * 36);
     h->lds_schur = sizeof(double) * 16 * CZ;
     if (C <= 64) {
@@ -557,6 +615,12 @@ int kb_upload_observations(kb_handle* h, int32_t n_views, int32_t n_corners, con
   h->V = n_views;
   h->NC = n_corners;
   h->vcam.assign(vc.begin(), vc.end());
+  h->V_cap = n_views;
+  h->NC_cap = n_corners;
+  h->vo_host.assign(view_offsets, view_offsets + n_views + 1);
+  h->frame_v0.assign(h->F + 1, n_views);
+  for (int v = n_views - 1; v >= 0; --v) h->frame_v0[vf[v]] = v;
+  for (int f = h->F - 1; f >= 0; --f) h->frame_v0[f] = std::min(h->frame_v0[f], h->frame_v0[f + 1]);
   KbDev& d = h->d;
   d.V = n_views;
   d.NC = n_corners;
@@ -599,6 +663,139 @@ int kb_upload_observations(kb_handle* h, int32_t n_views, int32_t n_corners, con
   return 0;
 }
 
+int kb_append_frames(kb_handle* h, int32_t n_frames, int32_t n_views, int32_t n_corners, const double* y,
+                     const uint16_t* corner_id, const uint32_t* view_offsets, const uint32_t* view_frame,
+                     const uint8_t* view_cam, const double* frame_poses) {
+  if (!h) return fail("kb_append_frames: null handle");
+  if (!h->uploaded) return fail("kb_append_frames: no observations (kb_upload_observations first)");
+  if (sharded(h)) return fail("kb_append_frames: not available on a sharded handle");
+  const int nf = n_frames, nv = n_views, nc = n_corners;
+  if (nf < 1 || nv < 0 || nc < 0 || !frame_poses || (nv > 0 && (!view_offsets || !view_frame || !view_cam)) ||
+      (nc > 0 && (!y || !corner_id)))
+    return fail("kb_append_frames: bad arguments");
+  if (nv == 0 ? nc != 0 : (view_offsets[0] != 0 || (int64_t)view_offsets[nv] != nc))
+    return fail("kb_append_frames: view_offsets must start at 0 and end at n_corners");
+  KB_HIP(hipSetDevice(h->device));
+  const int N = h->N, F0 = h->F, V0 = h->V, NC0 = h->NC;
+  // host-side validation of the appended block (frames 0 .. nf - 1 of it), as kb_upload_observations
+  std::vector<int32_t> fvc((size_t)nf * N, -1), vfg(nv), vcg(nv);
+  std::vector<int2> fvr((size_t)nf * N, make_int2(0, 0));
+  std::vector<uint32_t> vog(nv);
+  for (int v = 0; v < nv; ++v) {
+    if (view_offsets[v + 1] < view_offsets[v]) return fail("kb_append_frames: view_offsets not monotone");
+    if ((int)view_frame[v] >= nf || view_cam[v] >= N) return fail("kb_append_frames: view index out of range");
+    if (v > 0 && view_frame[v] < view_frame[v - 1]) return fail("kb_append_frames: views must be sorted by frame");
+    int32_t& slot = fvc[(size_t)view_frame[v] * N + view_cam[v]];
+    if (slot >= 0) return fail("kb_append_frames: two views for one (frame, camera)");
+    slot = V0 + v;
+    fvr[(size_t)view_frame[v] * N + view_cam[v]] = make_int2(NC0 + (int)view_offsets[v], NC0 + (int)view_offsets[v + 1]);
+    vfg[v] = F0 + (int32_t)view_frame[v];
+    vcg[v] = view_cam[v];
+    vog[v] = (uint32_t)NC0 + view_offsets[v + 1];
+  }
+  for (int k = 0; k < nc; ++k)
+    if ((int)corner_id[k] >= h->K) return fail("kb_append_frames: corner_id out of range");
+  KbDev& d = h->d;
+  const int F1 = F0 + nf, V1 = V0 + nv, NC1 = NC0 + nc;
+  // capacities: geometric growth, so a sequence of single-frame appends moves O(F) data in total
+  if (F1 > h->F_cap) {
+    const size_t fc = std::max(F1, 2 * h->F_cap), C = h->C;
+    if (regrow(h, &d.Hff, 36 * fc, 0) || regrow(h, &d.Hfc, 6 * C * fc, 0) || regrow(h, &d.gf, 6 * fc, 0) ||
+        regrow(h, &d.Af, 6 * C * fc, 0) || regrow(h, &d.bf, 6 * fc, 0) || regrow(h, &d.part, fc * d.Wr, 0) ||
+        regrow(h, &d.dx, C + 6 * fc, 0) || regrow(h, &d.rhs, C + 6 * fc, 0) || regrow(h, &d.bpart, 4 * fc, 0) ||
+        regrow(h, &d.fview, fc * N, (size_t)F0 * N) || regrow(h, &d.frame_vcam, fc * N, (size_t)F0 * N))
+      return -1;
+    d.bsrc = d.bpart;
+    d.bsrc_rows = (int)fc;  // rows beyond F are never read (k_post reduces nblk_bs = F rows)
+    h->F_cap = (int)fc;
+  }
+  const int base = N * KB_MAX_INTR + 7 * (N - 1), S0 = h->S;
+  if (base + 7 * F1 > d.S) {  // the state's slot stride grows: both slots move into a larger buffer
+    const int sst = base + 7 * h->F_cap;
+    void* q = nullptr;
+    KB_HIP(hipMalloc(&q, 2 * (size_t)sst * sizeof(double)));
+    KB_HIP(hipMemsetAsync(q, 0, 2 * (size_t)sst * sizeof(double), h->stream));
+    for (int sl = 0; sl < 2; ++sl)
+      KB_HIP(hipMemcpyAsync((double*)q + (size_t)sl * sst, d.state + (size_t)sl * d.S, sizeof(double) * S0,
+                            hipMemcpyDeviceToDevice, h->stream));
+    KB_HIP(hipStreamSynchronize(h->stream));
+    auto it = std::find(h->allocs.begin(), h->allocs.end(), (void*)d.state);
+    if (it != h->allocs.end()) h->allocs.erase(it);
+    KB_HIP(hipFree(d.state));
+    h->allocs.push_back(q);
+    d.state = (double*)q;
+    d.S = sst;
+  }
+  if (V1 > h->V_cap) {
+    const size_t vc = std::max(V1, 2 * h->V_cap);
+    if (regrow(h, &d.view_off, vc + 1, (size_t)V0 + 1) || regrow(h, &d.view_frame, vc, (size_t)V0) ||
+        regrow(h, &d.view_cam, vc, (size_t)V0) || regrow(h, &d.costpart, (vc + 3) / 4, 0))
+      return -1;
+    h->V_cap = (int)vc;
+  }
+  if (NC1 > h->NC_cap) {
+    const size_t ncc = std::max(NC1, 2 * h->NC_cap);
+    if (regrow(h, &d.y, ncc, (size_t)NC0) || regrow(h, &d.cid, ncc, (size_t)NC0)) return -1;
+    h->NC_cap = (int)ncc;
+  }
+  // only the new observations cross PCIe
+  if (nc > 0) {
+    KB_HIP(hipMemcpyAsync(const_cast<double2*>(d.y) + NC0, y, sizeof(double2) * nc, hipMemcpyHostToDevice, h->stream));
+    KB_HIP(hipMemcpyAsync(const_cast<uint16_t*>(d.cid) + NC0, corner_id, sizeof(uint16_t) * nc, hipMemcpyHostToDevice,
+                          h->stream));
+  }
+  if (nv > 0) {
+    KB_HIP(hipMemcpyAsync(const_cast<uint32_t*>(d.view_off) + V0 + 1, vog.data(), sizeof(uint32_t) * nv,
+                          hipMemcpyHostToDevice, h->stream));
+    KB_HIP(hipMemcpyAsync(const_cast<int32_t*>(d.view_frame) + V0, vfg.data(), sizeof(int32_t) * nv,
+                          hipMemcpyHostToDevice, h->stream));
+    KB_HIP(hipMemcpyAsync(const_cast<int32_t*>(d.view_cam) + V0, vcg.data(), sizeof(int32_t) * nv,
+                          hipMemcpyHostToDevice, h->stream));
+  }
+  KB_HIP(hipMemcpyAsync(const_cast<int32_t*>(d.frame_vcam) + (size_t)F0 * N, fvc.data(), sizeof(int32_t) * fvc.size(),
+                        hipMemcpyHostToDevice, h->stream));
+  KB_HIP(hipMemcpyAsync(const_cast<int2*>(d.fview) + (size_t)F0 * N, fvr.data(), sizeof(int2) * fvr.size(),
+                        hipMemcpyHostToDevice, h->stream));
+  // the new frames' poses (initial guesses) into the current state buffer
+  KB_HIP(hipMemcpyAsync(d.state + (size_t)h->cur * d.S + base + 7 * F0, frame_poses, sizeof(double) * 7 * nf,
+                        hipMemcpyHostToDevice, h->stream));
+  h->F = F1;
+  h->V = V1;
+  h->NC = NC1;
+  d.V = V1;
+  d.NC = NC1;
+  d.nblk_cost = (V1 + 3) / 4;
+  for (int v = 0; v < nv; ++v) h->vcam.push_back(vcg[v]);
+  h->vo_host.insert(h->vo_host.end(), vog.begin(), vog.end());
+  h->frame_v0.resize(F1 + 1, V1);
+  for (int f = F1 - 1; f >= F0; --f) h->frame_v0[f] = h->frame_v0[f + 1];
+  for (int v = nv - 1; v >= 0; --v) h->frame_v0[vfg[v]] = V0 + v;
+  for (int f = F1 - 1; f >= F0; --f) h->frame_v0[f] = std::min(h->frame_v0[f], h->frame_v0[f + 1]);
+  if (relayout(h)) return -1;
+  KB_HIP(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+int kb_drop_last_frames(kb_handle* h, int32_t n_frames) {
+  if (!h) return fail("kb_drop_last_frames: null handle");
+  if (!h->uploaded) return fail("kb_drop_last_frames: no observations");
+  if (sharded(h)) return fail("kb_drop_last_frames: not available on a sharded handle");
+  if (n_frames < 1 || n_frames >= h->F) return fail("kb_drop_last_frames: must keep at least one frame");
+  KB_HIP(hipSetDevice(h->device));
+  const int F1 = h->F - n_frames, V1 = h->frame_v0[F1], NC1 = (int)h->vo_host[V1];
+  h->F = F1;
+  h->V = V1;
+  h->NC = NC1;
+  h->d.V = V1;
+  h->d.NC = NC1;
+  h->d.nblk_cost = (V1 + 3) / 4;
+  h->vcam.resize(V1);
+  h->vo_host.resize(V1 + 1);
+  h->frame_v0.resize(F1 + 1);
+  h->frame_v0[F1] = V1;
+  return relayout(h);
+}
+
 static int set_cur(kb_handle* h, int cur) {
   h->cur = cur;
   KB_HIP(hipMemcpyAsync(&h->d.ctrl->cur, &h->cur, sizeof(int), hipMemcpyHostToDevice, h->stream));
@@ -609,7 +806,8 @@ int kb_set_state_flat(kb_handle* h, const double* state) {
   if (!h || !state) return fail("kb_set_state_flat: null");
   KB_HIP(hipSetDevice(h->device));
   unprepare(h);
-  KB_HIP(hipMemcpyAsync(h->d.state + (size_t)h->cur * h->S, state, sizeof(double) * h->S, hipMemcpyHostToDevice, h->stream));
+  KB_HIP(hipMemcpyAsync(h->d.state + (size_t)h->cur * h->d.S, state, sizeof(double) * h->S, hipMemcpyHostToDevice,
+                        h->stream));
   KB_HIP(hipStreamSynchronize(h->stream));
   return 0;
 }
@@ -630,7 +828,8 @@ int kb_set_state(kb_handle* h, const double* poses_q, const double* poses_t, con
 int kb_get_state_flat(kb_handle* h, double* state) {
   if (!h || !state) return fail("kb_get_state_flat: null");
   KB_HIP(hipSetDevice(h->device));
-  KB_HIP(hipMemcpyAsync(state, h->d.state + (size_t)h->cur * h->S, sizeof(double) * h->S, hipMemcpyDeviceToHost, h->stream));
+  KB_HIP(hipMemcpyAsync(state, h->d.state + (size_t)h->cur * h->d.S, sizeof(double) * h->S, hipMemcpyDeviceToHost,
+                        h->stream));
   KB_HIP(hipStreamSynchronize(h->stream));
   return 0;
 }
@@ -757,7 +956,7 @@ int kb_build(kb_handle* h, int use_mestimator) {
   h->sys_valid = false;
   if (launch_build(h, 0, 0)) return -1;
   if (launch_colsum(h, 0)) return -1;
-  hipLaunchKernelGGL(k_camexpand, dim3(1), dim3(256), h->lds_camexp, h->stream, h->d);
+  hipLaunchKernelGGL(k_camexpand, dim3(1), dim3(256), h->lds_camexp, h->stream, h->d, 0);
   KB_HIP(hipGetLastError());
   KB_HIP(hipStreamSynchronize(h->stream));
   h->sys_valid = true;
@@ -774,7 +973,10 @@ int kb_set_constant_conditioner(kb_handle* h, double diag) {
 int kb_set_conditioner(kb_handle* h, const double* diag) {
   if (!h || !diag) return fail("kb_set_conditioner: null");
   KB_HIP(hipSetDevice(h->device));
-  if (!h->cond2 && h->alloc(&h->cond2, (size_t)h->ncols)) return -1;
+  if (h->cond_n < (size_t)h->ncols) {
+    if (regrow(h, &h->cond2, (size_t)h->ncols, 0)) return -1;
+    h->cond_n = (size_t)h->ncols;
+  }
   std::vector<double> sq(h->ncols);
   for (int k = 0; k < h->ncols; ++k) sq[k] = diag[k] * diag[k];  // "the square of these values" (:33-35)
   KB_HIP(hipMemcpyAsync(h->cond2, sq.data(), sizeof(double) * h->ncols, hipMemcpyHostToDevice, h->stream));
@@ -804,10 +1006,12 @@ static size_t pcg_lds(int fpb, int C, int F) {
 // the PCG buffers and the camera DV block table (first use)
 static int ensure_pcg(kb_handle* h) {
   const int C = h->C, F = h->F;
-  if (!h->pcg_buf) {
-    if (h->alloc(&h->pcg_buf, (size_t)F * (C + 1) + F + 12) || h->alloc(&h->pcg_cb, 2 * (size_t)C) ||
-        h->alloc(&h->pcg_bar, kPcgBarWords))
-      return -1;
+  if (h->pcg_F < (size_t)F) {  // (re)sized for the current frame count (kb_append_frames grows it)
+    if (regrow(h, &h->pcg_buf, (size_t)F * (C + 1) + F + 12, 0)) return -1;
+    h->pcg_F = (size_t)F;
+  }
+  if (!h->pcg_cb) {
+    if (h->alloc(&h->pcg_cb, 2 * (size_t)C) || h->alloc(&h->pcg_bar, kPcgBarWords)) return -1;
     std::vector<int> cb(2 * C);
     int c = 0;
     auto block = [&](int m) {
@@ -1026,7 +1230,7 @@ static int run_marginal(kb_handle* h, const kb_marginal_options* o, int write_dx
   if (rc) return rc;
   const size_t lds = sizeof(double) * ((size_t)C * (C + 1) / 2 + (size_t)C * C + 2 * C);
   KB_HIP(hipFuncSetAttribute((const void*)k_marg, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  hipLaunchKernelGGL(k_marg, dim3(1), dim3(kMargThreads), lds, h->stream, h->d, m);
+  hipLaunchKernelGGL(k_marg, dim3(1), dim3(kMargThreads), lds, h->stream, h->d, m, 0);
   KB_HIP(hipGetLastError());
   double inf[8];
   KB_HIP(hipMemcpyAsync(inf, m.info, sizeof(inf), hipMemcpyDeviceToHost, h->stream));
@@ -1093,7 +1297,10 @@ int kb_rhs_jtj_rhs(kb_handle* h, double* out) {
                                  "not leave the per-call blocks)");
   if (sharded(h)) return fail("kb_rhs_jtj_rhs: per-call quantity of an unsharded handle");
   KB_HIP(hipSetDevice(h->device));
-  if (!h->rjr && h->alloc(&h->rjr, (size_t)h->F + 1)) return -1;
+  if (h->rjr_F < (size_t)h->F + 1) {  // (re)sized for the current frame count (kb_append_frames grows it)
+    if (regrow(h, &h->rjr, (size_t)h->F + 1, 0)) return -1;
+    h->rjr_F = (size_t)h->F + 1;
+  }
   hipLaunchKernelGGL(k_rjr_frames, dim3((h->F + 3) / 4), dim3(256), 0, h->stream, h->d, h->rjr);
   hipLaunchKernelGGL(k_rjr_final, dim3(1), dim3(256), 0, h->stream, h->d, h->rjr, h->rjr + h->F);
   KB_HIP(hipGetLastError());
@@ -1126,7 +1333,10 @@ struct GnFusedScope {
 static bool gn_fused(const kb_handle* h, int policy) { return policy == 1 && h->gn_fuse; }
 
 // ev0 / ev1 (optional): HIP events recorded around the build kernel (kb_build_kernel_stats)
+static int enqueue_marg_pass(kb_handle* h);
+
 static int enqueue_pass(kb_handle* h, int policy, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr) {
+  if (policy == kPolicyMarginal) return enqueue_marg_pass(h);
   KbDev& d = h->d;
   auto build = [&]() -> int {
     if (ev0) KB_HIP(hipEventRecord(ev0, h->stream));
@@ -1170,7 +1380,7 @@ struct Snapshot {
   Snapshot& operator=(const Snapshot&) = delete;
   int copy(bool restore) {
     KbDev& dv = h->d;
-    const size_t sz[4] = {2 * (size_t)h->S * 8, 2 * 12 * (size_t)h->N * 8, 2 * 36 * (size_t)h->N * h->N * 8,
+    const size_t sz[4] = {2 * (size_t)dv.S * 8, 2 * 12 * (size_t)h->N * 8, 2 * 36 * (size_t)h->N * h->N * 8,
                           sizeof(KbCtrl)};
     void* bufs[4] = {dv.state, dv.camL, dv.camK, dv.ctrl};
     if (!buf) {
@@ -1332,6 +1542,92 @@ int kb_optimize(kb_handle* h, const kb_optimizer_options* opts, kb_solution* out
   out->linear_solver_failure = ctrl.lin_fail;
   out->passes = ctrl.passes;
   out->graphed = graph ? 1 : 0;
+  return 0;
+}
+
+// one pass of the device-resident IncrementalEstimator loop (Optimizer2 + GaussNewtonTrustRegionPolicy over
+// calibration::LinearSolver, IncrementalEstimator.cpp:46-77, 373): build with the frame blocks eliminated at
+// lambda = 0 (the policy's lambda), column sums, H_cc / g_c, the column-scaled truncated-SVD camera step (k_marg),
+// the candidate camera design variables and chains (k_marg_tail), the frame steps and the candidate's cost
+// (k_backsub), the pass end (k_post: accept, convergence tests, next prelude).  Every kernel is gated on ctrl.
+static int enqueue_marg_pass(kb_handle* h) {
+  if (launch_build(h, 1, 1) || launch_colsum(h, 1, true)) return -1;
+  hipLaunchKernelGGL(k_camexpand, dim3(1), dim3(256), h->lds_camexp, h->stream, h->d, 1);
+  hipLaunchKernelGGL(k_marg, dim3(1), dim3(kMargThreads), h->lds_marg, h->stream, h->d, h->marg, 1);
+  hipLaunchKernelGGL(k_marg_tail, dim3(1), dim3(256), 0, h->stream, h->d);
+  KB_HIP(hipGetLastError());
+  if (launch_backsub(h, 1, 1, 1)) return -1;
+  hipLaunchKernelGGL(k_post, dim3(1), dim3(256), 0, h->stream, h->d, 1);
+  KB_HIP(hipGetLastError());
+  return 0;
+}
+
+int kb_optimize_marginal(kb_handle* h, const kb_optimizer_options* opts, const kb_marginal_options* mopts,
+                         kb_solution* out, kb_marginal_info* info, double* sv_out, double* V_out) {
+  if (!h || !opts || !mopts || !out) return fail("kb_optimize_marginal: null");
+  if (!h->uploaded) return fail("kb_optimize_marginal: no observations");
+  if (opts->policy != 1) return fail("kb_optimize_marginal: the IncrementalEstimator's policy is Gauss-Newton (1)");
+  if (h->C > kMargMaxC) return fail("kb_optimize_marginal: camera block C > 112 is not supported");
+  if (sharded(h)) return fail("kb_optimize_marginal: not available on a sharded handle");
+  KB_HIP(hipSetDevice(h->device));
+  const int C = h->C;
+  if (!h->marg_buf && h->alloc(&h->marg_buf, (size_t)C * C + C + 8)) return -1;
+  KbMarg m{};
+  m.scaling = mopts->column_scaling ? 1 : 0;
+  m.write_dx = 1;
+  m.norm_tol = std::sqrt(2.0 * (double)h->NC * mopts->eps_norm);
+  m.eps_svd = mopts->eps_svd;
+  m.svd_tol = mopts->svd_tol;
+  m.V = h->marg_buf;
+  m.sv = m.V + (size_t)C * C;
+  m.info = m.sv + C;
+  h->lds_marg = sizeof(double) * ((size_t)C * (C + 1) / 2 + (size_t)C * C + 2 * C);
+  KB_HIP(hipFuncSetAttribute((const void*)k_marg, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_marg));
+  // the captured passes hold the k_marg arguments: other options (or a grown problem: norm_tol) recapture them
+  if (std::memcmp(&m, &h->marg, sizeof(KbMarg)) != 0) {
+    if (h->graph_policy == kPolicyMarginal) drop_graphs(h);
+    h->marg = m;
+  }
+  const int max_passes = 2 * opts->max_iterations + 1;
+  if (ensure_trace(h, max_passes + 1)) return -1;
+  KbOpts o{1, opts->max_iterations, 0.0, opts->convergence_dx, opts->convergence_dj};
+  if (loop_start(h, o)) return -1;
+  const bool graph = opts->use_graph != 0 && graph_ok(h, kPolicyMarginal);
+  const int every = opts->sync_every > 0 ? opts->sync_every : 2 * kGraphPasses;
+  KbCtrl ctrl{};
+  int passes = 0;
+  while (passes < max_passes) {
+    const int n = std::min(every, max_passes - passes);
+    if (launch_passes(h, kPolicyMarginal, n, graph)) return -1;
+    passes += n;
+    KB_HIP(hipMemcpyAsync(&ctrl, h->d.ctrl, sizeof(KbCtrl), hipMemcpyDeviceToHost, h->stream));
+    KB_HIP(hipStreamSynchronize(h->stream));
+    if (ctrl.done) break;
+  }
+  if (finish_pass(h, kPolicyMarginal)) return -1;
+  double inf[8];
+  KB_HIP(hipMemcpyAsync(&ctrl, h->d.ctrl, sizeof(KbCtrl), hipMemcpyDeviceToHost, h->stream));
+  KB_HIP(hipMemcpyAsync(inf, m.info, sizeof(inf), hipMemcpyDeviceToHost, h->stream));
+  if (sv_out) KB_HIP(hipMemcpyAsync(sv_out, m.sv, sizeof(double) * C, hipMemcpyDeviceToHost, h->stream));
+  if (V_out) KB_HIP(hipMemcpyAsync(V_out, m.V, sizeof(double) * C * C, hipMemcpyDeviceToHost, h->stream));
+  KB_HIP(hipStreamSynchronize(h->stream));
+  h->cur = ctrl.cur;
+  out->J_start = ctrl.J_start;
+  out->J_final = ctrl.p_J;
+  out->dx_final = ctrl.deltaX;
+  out->dj_final = ctrl.deltaJ;
+  out->iterations = ctrl.iterations;
+  out->failed_iterations = ctrl.failed_iterations;
+  out->linear_solver_failure = ctrl.lin_fail;
+  out->passes = ctrl.passes;
+  out->graphed = graph ? 1 : 0;
+  if (info) {
+    info->rank = (int32_t)inf[0];
+    info->sweeps = (int32_t)inf[1];
+    info->tolerance = inf[2];
+    info->sv_gap = inf[3];
+    info->sv_log2_sum = inf[4];
+  }
   return 0;
 }
 

@@ -2101,7 +2101,8 @@ __device__ double cam_grad(const KbDev& d, const double* Hs, int p) {
 }
 
 // per-call path: H_cc, g_c, cost at the build state (kb_get_normal_blocks / kb_get_rhs)
-__global__ void __launch_bounds__(256) k_camexpand(KbDev d) {
+__global__ void __launch_bounds__(256) k_camexpand(KbDev d, int gate) {
+  if (gate && d.ctrl->done) return;
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const int N = d.N, C = d.C;
   double* Hs = sm;
@@ -2145,7 +2146,8 @@ __device__ __forceinline__ void rr_pair(int m, int r, int k, int& p, int& q) {  
   q = max(a, b);
 }
 
-__global__ void __launch_bounds__(kMargThreads) k_marg(KbDev d, KbMarg mo) {
+__global__ void __launch_bounds__(kMargThreads) k_marg(KbDev d, KbMarg mo, int gate) {
+  if (gate && (d.ctrl->done || !d.ctrl->do_build)) return;
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const int C = d.C, n = C, m = C + (C & 1), h = m / 2, tid = threadIdx.x, nth = blockDim.x;
   const int np = n * (n + 1) / 2, Wt = d.W - C, o0 = d.N * 136;
@@ -2306,6 +2308,61 @@ __global__ void __launch_bounds__(kMargThreads) k_marg(KbDev d, KbMarg mo) {
     mo.info[4] = stat[2];
     if (!okl) d.ctrl->solve_ok = 0;
   }
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_marg_tail (kb_optimize_marginal, the device-resident IncrementalEstimator loop): after k_marg's truncated-SVD
+// camera step, what k_solve's tail does after its LDL^T -- the camera dx statistics (max |dx_c|, dx_c.dx_c, dx_c.g_c),
+// the camera design variables of the candidate slot (intrinsics additive, baselines by the pose update) and the
+// candidate's camera chains -- and the pass is marked pending for k_backsub / k_post
+// ---------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_marg_tail(KbDev d) {
+  KbCtrl* c = d.ctrl;
+  __shared__ double nbase[KB_MAX_CAMS * 7];
+  const int done = c->done, sok = c->solve_ok, cur = c->cur;
+  if (done) return;
+  const int tid = threadIdx.x, nth = blockDim.x, C = d.C, N = d.N;
+  if (tid == 0) c->pending = 1;
+  if (!sok) return;
+  if (tid < 64) {
+    double mx = 0.0, dd = 0.0, dr = 0.0;
+    for (int i = tid; i < C; i += 64) {
+      const double x = d.dx[i], g = d.gc[i];
+      mx = fmax(mx, fabs(x));
+      dd += x * x;
+      dr += x * g;
+    }
+    mx = wave_max_d(mx);
+    dd = wave_sum_d(dd);
+    dr = wave_sum_d(dr);
+    if (tid == 0) {
+      d.camstat[0] = mx;
+      d.camstat[1] = dd;
+      d.camstat[2] = dr;
+    }
+  }
+  const double* in = d.state + (size_t)cur * d.S;
+  double* out = d.state + (size_t)(1 - cur) * d.S;
+  for (int q = tid; q < N * KB_MAX_INTR; q += nth) {
+    const int cm = q / KB_MAX_INTR, x = q - KB_MAX_INTR * cm;
+    out[q] = in[q] + (x < cam_arg(d.nintr, cm) ? d.dx[cam_arg(d.col_intr, cm) + x] : 0.0);
+  }
+  for (int j = tid; j < N - 1; j += nth) {
+    double bq[7], d6[6], nb[7];
+#pragma unroll
+    for (int q = 0; q < 7; ++q) bq[q] = in[d.off_base + 7 * j + q];
+    const int cb = cam_arg(d.col_base, j);
+#pragma unroll
+    for (int q = 0; q < 6; ++q) d6[q] = d.dx[cb + q];
+    update_pose(bq, d6, nb);
+#pragma unroll
+    for (int q = 0; q < 7; ++q) {
+      out[d.off_base + 7 * j + q] = nb[q];
+      nbase[7 * j + q] = nb[q];
+    }
+  }
+  __syncthreads();
+  chain_block(d, nbase, 1 - cur, nth);  // chains of the candidate (k_backsub's cost, the next build if accepted)
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -333,6 +333,7 @@ void GpuLinearSystemSolver::initMatrixStructure(const CalibrationProblem& p, boo
   _JRows = 2 * (size_t)p.n_corners();
   _JCols = (size_t)kb_num_cols(h);
   _C = (size_t)kb_camera_cols(h);
+  _F = (size_t)p.n_frames;
   _rhs.assign(_JCols, 0.0);
   _diagonalConditioner.assign(_JCols, 0.0);
   _conditioner = 0.0;
@@ -410,6 +411,44 @@ int GpuLinearSystemSolver::lastPcgIterations() const {
   kb_pcg_info info{};
   check(kb_get_pcg_info(static_cast<kb_handle*>(_h), &info), "kb_get_pcg_info");
   return info.iterations;
+}
+
+bool GpuLinearSystemSolver::appendFrames(const CalibrationProblem& p, size_t f0) {
+  if (!_h || _F != f0 || (size_t)p.n_frames <= f0) return false;
+  // the views of frames >= f0 (views are sorted by frame), renumbered from 0, offsets made local
+  const size_t v0 = std::lower_bound(p.view_frame.begin(), p.view_frame.end(), (uint32_t)f0) - p.view_frame.begin();
+  const size_t nv = p.view_frame.size() - v0, c0 = p.view_offset[v0], nc = p.corner_id.size() - c0;
+  std::vector<uint32_t> vo(nv + 1), vf(nv);
+  for (size_t v = 0; v <= nv; ++v) vo[v] = p.view_offset[v0 + v] - (uint32_t)c0;
+  for (size_t v = 0; v < nv; ++v) vf[v] = p.view_frame[v0 + v] - (uint32_t)f0;
+  const size_t nf = (size_t)p.n_frames - f0, so = p.state.size() - 7 * (size_t)p.n_frames;
+  kb_handle* h = static_cast<kb_handle*>(_h);
+  check(kb_append_frames(h, (int32_t)nf, (int32_t)nv, (int32_t)nc, p.y.data() + 2 * c0, p.corner_id.data() + c0,
+                         vo.data(), vf.data(), p.view_cam.data() + v0, p.state.data() + so + 7 * f0),
+        "kb_append_frames");
+  if ((int)p.state.size() != kb_state_size(h)) throw Exception("appendFrames: state size mismatch");
+  check(kb_set_state_flat(h, p.state.data()), "kb_set_state_flat");
+  _F = (size_t)p.n_frames;
+  _JRows = 2 * (size_t)p.n_corners();
+  _JCols = (size_t)kb_num_cols(h);
+  _rhs.assign(_JCols, 0.0);
+  _diagonalConditioner.assign(_JCols, 0.0);
+  _built = false;
+  _rhs_valid = false;
+  return true;
+}
+
+void GpuLinearSystemSolver::dropLastFrames(size_t n, const std::vector<double>& st) {
+  kb_handle* h = static_cast<kb_handle*>(_h);
+  check(kb_drop_last_frames(h, (int32_t)n), "kb_drop_last_frames");
+  _F -= n;
+  if ((int)st.size() != kb_state_size(h)) throw Exception("dropLastFrames: state size mismatch");
+  check(kb_set_state_flat(h, st.data()), "kb_set_state_flat");
+  _JCols = (size_t)kb_num_cols(h);
+  _rhs.assign(_JCols, 0.0);
+  _diagonalConditioner.assign(_JCols, 0.0);
+  _built = false;
+  _rhs_valid = false;
 }
 
 std::vector<double> GpuLinearSystemSolver::state() const {
@@ -660,6 +699,59 @@ void GpuMarginalLinearSolver::initMatrixStructure(const CalibrationProblem& p, b
   _V.clear();
 }
 
+bool GpuMarginalLinearSolver::appendFrames(const CalibrationProblem& p, size_t firstFrame) {
+  if (!_g.appendFrames(p, firstFrame)) return false;
+  _JRows = _g.JRows();
+  _JCols = _g.JCols();
+  _diagonalConditioner.assign(_JCols, 0.0);
+  _svdRank = -1;  // a new problem for the marginal statistics, as after initMatrixStructure
+  _svdTolerance = _svGap = -1.0;
+  _sv.clear();
+  _V.clear();
+  return true;
+}
+
+bool GpuMarginalLinearSolver::dropLastFrames(size_t n, const std::vector<double>& st) {
+  _g.dropLastFrames(n, st);
+  _JRows = _g.JRows();
+  _JCols = _g.JCols();
+  _diagonalConditioner.assign(_JCols, 0.0);
+  return true;
+}
+
+static kb_marginal_options marg_opts(const LinearSolverOptions& o);
+
+bool GpuMarginalLinearSolver::optimizeDevice(const Optimizer2Options& oo, SolutionReturnValue& srv) {
+  if (!deviceLoop || !_g.handle() || _g.cameraCols() > 112) return false;
+  kb_optimizer_options o{};
+  o.policy = 1;  // GaussNewtonTrustRegionPolicy (IncrementalEstimator.cpp:66-71)
+  o.max_iterations = oo.maxIterations;
+  o.convergence_dx = oo.convergenceDeltaX;
+  o.convergence_dj = oo.convergenceDeltaJ;
+  o.sync_every = 0;
+  o.use_graph = 1;
+  kb_marginal_options m = marg_opts(_lopt);
+  kb_solution s{};
+  kb_marginal_info inf{};
+  const size_t C = _g.cameraCols();
+  _sv.resize(C);
+  _V.resize(C * C);
+  if (kb_optimize_marginal(static_cast<kb_handle*>(_g.handle()), &o, &m, &s, &inf, _sv.data(), _V.data()) < 0)
+    throw Exception(std::string("kb_optimize_marginal: ") + kb_last_error());
+  _svdRank = inf.rank;
+  _svdTolerance = inf.tolerance;
+  _svGap = inf.sv_gap;
+  srv = SolutionReturnValue{};
+  srv.JStart = s.J_start;
+  srv.JFinal = s.J_final;
+  srv.dXFinal = s.dx_final;
+  srv.dJFinal = s.dj_final;
+  srv.iterations = s.iterations;
+  srv.failedIterations = s.failed_iterations;
+  srv.linearSolverFailure = s.linear_solver_failure != 0;
+  return true;
+}
+
 static kb_marginal_options marg_opts(const LinearSolverOptions& o) {
   kb_marginal_options m{};
   m.column_scaling = o.columnScaling ? 1 : 0;
@@ -749,10 +841,16 @@ IncrementalEstimator::ReturnValue IncrementalEstimator::addBatch(const Calibrati
   // insert the new batch; save the design variables in case it is rejected (:343-351)
   const std::vector<double> saved = _problem.state;
   appendBatch(batch);
-  // Optimizer2::initialize -> initMatrixStructure over the grown problem, then optimize (:373)
-  _solver->initMatrixStructure(_problem, false);
-  Optimizer2 optimizer(_optOptions);
-  const SolutionReturnValue srv = optimizer.optimize();
+  // Optimizer2::initialize -> initMatrixStructure over the grown problem, then optimize (:373).  The reference
+  // re-initialises the whole structure; a solver that holds the accepted frames appends the new one in place
+  // (kb_append_frames: only the batch's observations are uploaded) instead
+  if (!_solver->appendFrames(_problem, (size_t)_problem.n_frames - 1)) _solver->initMatrixStructure(_problem, false);
+  // the optimisation itself: device-resident when the solver runs it (kb_optimize_marginal), else the host loop
+  SolutionReturnValue srv;
+  if (!_solver->optimizeDevice(_optOptions, srv)) {
+    Optimizer2 optimizer(_optOptions);
+    srv = optimizer.optimize();
+  }
   ReturnValue ret;
   ret.numIterations = (size_t)srv.iterations;
   ret.JStart = srv.JStart;
@@ -797,6 +895,9 @@ IncrementalEstimator::ReturnValue IncrementalEstimator::addBatch(const Calibrati
   if (!keep) {  // restore the design variables and drop the batch (:517-527)
     removeLastBatch(batch.view_cam.size(), batch.corner_id.size());
     _problem.state = saved;
+    // the solver keeps the accepted frames with their restored values for the next append (a solver that cannot, or
+    // a first batch rejected, leaves frames the problem does not hold: the next addBatch re-initialises)
+    if (_problem.n_frames > 0) _solver->dropLastFrames(1, saved);
   }
   ret.elapsedTime = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   return ret;

@@ -235,12 +235,19 @@ class GpuLinearSystemSolver : public ProblemLinearSystemSolver {
   void* handle() const { return _h; }
   /// PCG iterations of the last solveSystem (0 with the direct solver)
   int lastPcgIterations() const;
+  /// the problem's frames from `firstFrame` on appended to the uploaded handle in place (kb_append_frames), the
+  /// handle holding exactly frames [0, firstFrame) of `problem` before; then the whole state set from problem.state.
+  /// Returns false (nothing changed) when the handle does not hold that prefix; initMatrixStructure then applies.
+  bool appendFrames(const CalibrationProblem& problem, size_t firstFrame);
+  /// the last n frames removed (kb_drop_last_frames), then the state set to `state` (the smaller problem's)
+  void dropLastFrames(size_t n, const std::vector<double>& state);
+  size_t framesHeld() const { return _F; }
 
  private:
   void check(int rc, const char* what) const;
   void* _h = nullptr;
   GpuOptions _opt;
-  size_t _C = 0;
+  size_t _C = 0, _F = 0;
   double _conditioner = 0.0;
   bool _built = false;
   mutable bool _rhs_valid = false;
@@ -269,6 +276,15 @@ class MarginalLinearSystemSolver : public LinearSystemSolver {
   /// LinearSolver::analyzeMarginal (LinearSolver.cpp:468-528): SVD of the unscaled marginal system of the
   /// last build.  As in the reference the rank is the one of the last solve.
   virtual void analyzeMarginal() = 0;
+  /// in-place growth for the IncrementalEstimator (kb_append_frames): false if not supported or the solver does not
+  /// hold frames [0, firstFrame) of `problem`, and then initMatrixStructure is called instead
+  virtual bool appendFrames(const CalibrationProblem& /*problem*/, size_t /*firstFrame*/) { return false; }
+  /// drop the last n frames and set `state` (a rejected batch); false if not supported
+  virtual bool dropLastFrames(size_t /*n*/, const std::vector<double>& /*state*/) { return false; }
+  /// Optimizer2::optimize with the GaussNewtonTrustRegionPolicy over this solver, run device-resident
+  /// (kb_optimize_marginal); false if not supported (the host Optimizer2 runs instead).  Leaves the SVD statistics
+  /// of the last solve, as solveSystem does.
+  virtual bool optimizeDevice(const struct Optimizer2Options& /*o*/, struct SolutionReturnValue& /*out*/) { return false; }
   const LinearSolverOptions& getOptions() const { return _lopt; }
   std::ptrdiff_t getSVDRank() const { return _svdRank; }
   std::ptrdiff_t getSVDRankDeficiency() const { return _svdRank == -1 ? -1 : (std::ptrdiff_t)_sv.size() - _svdRank; }
@@ -307,6 +323,12 @@ class GpuMarginalLinearSolver : public MarginalLinearSystemSolver {
   void revertLastStateUpdate() override { _g.revertLastStateUpdate(); }
   std::vector<double> state() const override { return _g.state(); }
   void analyzeMarginal() override;
+  bool appendFrames(const CalibrationProblem& problem, size_t firstFrame) override;
+  bool dropLastFrames(size_t n, const std::vector<double>& state) override;
+  bool optimizeDevice(const Optimizer2Options& o, SolutionReturnValue& out) override;
+  GpuLinearSystemSolver& gpu() { return _g; }
+  /// false: optimizeDevice declines and the IncrementalEstimator drives the per-call host loop (parity / timing)
+  bool deviceLoop = true;
 
  private:
   GpuLinearSystemSolver _g;

@@ -24,6 +24,8 @@
 // Prints one JSON line.  The oracle is test infrastructure only (oracle/kb_oracle.h).
 #include <algorithm>
 #include <cfloat>
+#include <chrono>
+#include <numeric>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -284,12 +286,12 @@ static std::vector<CalibrationBatch> batches_of(const CalibrationProblem& p) {
 
 struct IncrRun {
   std::vector<int> accepted;
-  std::vector<double> gain, state;
+  std::vector<double> gain, state, secs;
   std::vector<long> rank, iters;
 };
 
 static IncrRun run_estimator(const CalibrationProblem& p, std::shared_ptr<MarginalLinearSystemSolver> solver,
-                             double delta, int maxIt) {
+                             double delta, int maxIt, size_t max_batches = (size_t)-1) {
   IncrementalEstimator::Options eo;
   eo.infoGainDelta = delta;
   eo.checkValidity = true;  // CalibrateCameras.cpp:258-261
@@ -298,8 +300,10 @@ static IncrRun run_estimator(const CalibrationProblem& p, std::shared_ptr<Margin
   oo.nThreads = 4;
   IncrementalEstimator est(base_of(p), solver, eo, oo);
   IncrRun r;
-  for (const auto& b : batches_of(p)) {
-    auto rv = est.addBatch(b);
+  const auto bs = batches_of(p);
+  for (size_t q = 0; q < bs.size() && q < max_batches; ++q) {
+    auto rv = est.addBatch(bs[q]);
+    r.secs.push_back(rv.elapsedTime);
     r.accepted.push_back(rv.batchAccepted ? 1 : 0);
     r.gain.push_back(rv.informationGain);
     r.rank.push_back((long)rv.rankTheta);
@@ -804,6 +808,50 @@ int main(int argc, char** argv) {
     if (mode == "io") return run_io(p, argv[3]);
     if (mode == "init") return run_init(p, (size_t)std::atol(argv[3]), (size_t)std::atol(argv[4]));
     if (mode == "terms-cpu" || mode == "terms-gpu") return run_terms(p, mode == "terms-gpu", pol, maxIt);
+    if (mode == "incr-time") {
+      // the whole addBatch sequence over GpuMarginalLinearSolver (in-place appends), then the same estimator over the
+      // oracle's marginal solver for the first argv[5] batches (the CPU side of the comparison)
+      const double delta = std::atof(argv[3]);
+      const size_t kcpu = argc > 5 ? (size_t)std::atol(argv[5]) : 50;
+      const int threads = argc > 6 ? std::atoi(argv[6]) : 16;
+      LinearSolverOptions lo;
+      lo.columnScaling = true;  // CalibrateCameras.cpp:263-267
+      lo.epsSVD = 1e-6;
+      auto t0 = std::chrono::steady_clock::now();
+      const IncrRun g = run_estimator(p, std::make_shared<GpuMarginalLinearSolver>(lo), delta, maxIt);
+      const double gsec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      // the same estimator over the same GPU solver, its optimisation driven from the host per call (no kb_optimize_marginal)
+      auto hl = std::make_shared<GpuMarginalLinearSolver>(lo);
+      hl->deviceLoop = false;
+      t0 = std::chrono::steady_clock::now();
+      const IncrRun gh = run_estimator(p, hl, delta, maxIt);
+      const double ghsec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      t0 = std::chrono::steady_clock::now();
+      const IncrRun c = run_estimator(p, std::make_shared<OracleMarginalSolver>(lo, threads), delta, maxIt, kcpu);
+      const double csec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      double g_k = 0.0, c_k = 0.0;
+      long it_g = 0, it_gk = 0, acc_g = 0;
+      for (size_t q = 0; q < g.secs.size(); ++q) {
+        it_g += g.iters[q];
+        acc_g += g.accepted[q];
+        if (q < c.secs.size()) {
+          g_k += g.secs[q];
+          c_k += c.secs[q];
+          it_gk += g.iters[q];
+        }
+      }
+      bool same = true, same_h = gh.accepted == g.accepted && gh.iters == g.iters;
+      for (size_t q = 0; q < c.accepted.size(); ++q) same = same && c.accepted[q] == g.accepted[q] && c.iters[q] == g.iters[q];
+      std::printf(
+          "{\"batches\": %zu, \"gpu_seconds\": %.6f, \"gpu_accepted\": %ld, \"gpu_gn_iterations\": %ld, "
+          "\"cpu_batches\": %zu, \"cpu_threads\": %d, \"cpu_seconds\": %.6f, \"gpu_seconds_same_batches\": %.6f, "
+          "\"gn_iterations_same_batches\": %ld, \"same_decisions\": %s, \"wall_gpu\": %.6f, \"wall_cpu\": %.6f, "
+          "\"gpu_host_loop_seconds\": %.6f, \"host_loop_same_decisions\": %s, \"state_diff_host_loop\": %.3e}\n",
+          g.secs.size(), std::accumulate(g.secs.begin(), g.secs.end(), 0.0), acc_g, it_g, c.secs.size(), threads, c_k,
+          g_k, it_gk, same ? "true" : "false", gsec, csec, ghsec, same_h ? "true" : "false",
+          maxdiff(g.state, gh.state, 0, g.state.size()));
+      return 0;
+    }
     if (mode == "incr-cpu" || mode == "incr-gpu") {
       const double delta = std::atof(argv[3]);
       LinearSolverOptions lo;

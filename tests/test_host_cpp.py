@@ -93,8 +93,11 @@ def test_incremental_estimator_matches_oracle(driver, tmp_path, cfg, frames, del
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cfg,frames,delta", [(1, 10, 0.2), (2, 8, 5.0)])
+@pytest.mark.parametrize("cfg,frames,delta", [(1, 10, 0.2), (2, 8, 5.0), (1, 120, 0.2), (2, 100, 0.2)])
 def test_incremental_estimator_gpu_matches_oracle(driver, tmp_path, cfg, frames, delta):
+    """The GPU estimator (GpuMarginalLinearSolver: every accepted batch appended to the device handle in place,
+    kb_append_frames; a rejected one dropped, kb_drop_last_frames) takes the oracle-backed estimator's decisions:
+    same accept / reject sequence, ranks and GN iteration counts, state within 1e-6 -- up to 120 batches."""
     p = synth.make_config(cfg, n_frames=frames)
     r = run_incr(driver, tmp_path, "incr-gpu", p, delta, 20)
     assert r["accepted"] == r["ref_accepted"] and r["rank"] == r["ref_rank"], r
