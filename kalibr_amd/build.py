@@ -61,6 +61,14 @@ def build_host(force=False):
     return HOST_OUT
 
 
+def build_variant(name, defines):
+    """A measurement variant of the library (kernel alternatives behind -D switches) as libkalibr_hip_<name>.so,
+    selected by KB_VARIANT_LIB=<name> (tools and A/B runs only; the product loads libkalibr_hip.so)."""
+    out = os.path.join(HERE, "libkalibr_hip_%s.so" % name)
+    _compile_link(out, ["-D" + x for x in defines])
+    return out
+
+
 def build_stamps():
     """Diagnostic variant with per-phase s_memrealtime stamps (tools/diag_stamps.py only)."""
     out = os.path.join(HERE, "libkalibr_hip_stamps.so")

@@ -13,6 +13,9 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # KB_DIAG_LIB=1 selects the diagnostic build (libkalibr_hip_stamps.so: stop points, timelines) for the tools
 LIB_PATH = os.path.join(_HERE, "libkalibr_hip_stamps.so" if os.environ.get("KB_DIAG_LIB") == "1" else "libkalibr_hip.so")
+# KB_VARIANT_LIB=<name>: a measurement variant built by kalibr_amd/build.py build_variant (tools only)
+if os.environ.get("KB_VARIANT_LIB"):
+    LIB_PATH = os.path.join(_HERE, "libkalibr_hip_%s.so" % os.environ["KB_VARIANT_LIB"])
 _lib = None
 
 dp = C.POINTER(C.c_double)
@@ -314,7 +317,8 @@ class Solver:
         _check(lib().kb_revert(self.h))
 
     def normal_blocks(self):
-        F, Cc = self.prob.n_frames, self.C
+        Cc = self.C
+        F = (self.ncols - Cc) // 6  # the handle's frames (kb_append_frames / kb_drop_last_frames change them)
         out = dict(Hff=np.zeros((F, 6, 6)), Hfc=np.zeros((F, 6, Cc)), gf=np.zeros((F, 6)), Hcc=np.zeros((Cc, Cc)),
                    gc=np.zeros(Cc), cost=np.zeros(1))
         _check(lib().kb_get_normal_blocks(self.h, _d(out["Hff"]), _d(out["Hfc"]), _d(out["gf"]), _d(out["Hcc"]),

@@ -1242,6 +1242,7 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
   __shared__ double cst[KB_MAX_CAMS][24];  // per camera: chain L (12) | intrinsics (10)
   __shared__ int ctab[2][KB_MAX_CAMS];      // per camera: first intrinsic column | baseline column
   __shared__ int cil[112];                  // expanded partials: column info (kind << 16 | camera << 8 | index)
+  __shared__ int xcnt;                      // expanded partials: view waves done with their camera's share
   const int W = d.W;
   const int f0 = blockIdx.x * d.gframes, f1 = min(d.F, f0 + d.gframes), G = f1 - f0;
   const bool vw = wave < N;  // view wave (camera = wave) | frame wave fw = wave - N
@@ -1345,7 +1346,10 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
   }
   const double* tgt = tg_lds ? tg : d.target;
   const double lam2 = lam * lam;
-  if (tid == 0) okl = 1;
+  if (tid == 0) {
+    okl = 1;
+    xcnt = 0;
+  }
   __syncthreads();
   if (wave == 0) KB_TSB(d, 1);
 
@@ -1412,7 +1416,8 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
         }
       }
       __syncthreads();
-      if (it < G) {
+      if (it == G) break;  // the last frame's elimination runs on the frame waves now (the expansion below meanwhile)
+      {
         // ---------------- phase B: view (f, cam)
         const int f = f0 + it;
         int lane = threadIdx.x & 63;  // opaque per frame (see the frame waves)
@@ -1621,25 +1626,26 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
           }
         }
         if (stv) KB_TSB(d, sto + 8);
-      } else if (xp) {
-        // expanded partials: the view waves are idle while the frame waves eliminate the last frame; clear the camera
-        // block's LDS image (the structural zeros, e.g. H_{I_i, B_j} for j >= i, are never written; the Xw tiles
-        // it overlaps are no longer read)
-        for (int e = tid; e < W; e += 64 * N) sm[e] = 0.0;
       }
       __syncthreads();
     }
     if (xp) {
-      // ---- expanded partials, step 1: this camera's share of the block's camera block, straight
-      // from its local sums creg = Hs (C layout: lane l, reg q -> row (l >> 4) + 4 q, column l & 15):
-      //   H_{I,I} and g_I entries directly; D = Hs[:, d] [K_{i,0} | .. | K_{i,i-1}] on MFMA (the symmetric Hs is its own
-      //   A operand, as in the view expansion): rows 6 .. 5 + nin -> H_{I_i, B_j}, row 15 -> camera i's share of g_B,
-      //   rows 0 .. 5 -> T_i = Hs_dd K_i (the B operand of the baseline block in step 2)
-      double* EX = sm;                   // [W] H_cc upper packed | g_c
-      double* Tl = EX + W;               // [N][6][48] T_i
-      double* gB = Tl + N * 288;         // [N][48] camera i's share of g_B
-      double* cc = gB + N * 48;          // [N] chi^2 of camera i
-      const int Wt = W - C, CI = C - 6 * (N - 1), ci0 = ctab[0][cam];
+      // ---- expanded partials, while the frame waves eliminate the block's last frame (the view waves
+      // are idle in that phase, and the Xw tiles the image overlaps are no longer read).  The block's share of the
+      // camera block, H_cc and g_c upper packed, expanded from the view waves' local sums creg = Hs (C layout: lane l,
+      // reg q -> row (l >> 4) + 4 q, column l & 15) through the chains K of the build state (Kl):
+      //   step 1 (each view wave, its camera i): H_{I_i,I_i} and g_{I_i} directly; D = Hs[:, d] [K_{i,0} | .. |
+      //     K_{i,i-1}] on MFMA (the symmetric Hs is its own A operand): rows 6 .. 5 + nin -> H_{I_i,B_j}, row 15 -> the
+      //     camera's share of g_B, rows 0 .. 5 -> T_i = Hs_dd K_i; the structural zeros of its rows;
+      //   step 2 (after the view waves meet): H_{B_j,B_k} = sum_{i > max(j,k)} K_{i,j}^T T_{i,k}, one 16 x 16 tile per
+      //     view wave accumulated over the cameras in order on MFMA; g_B; the cost.
+      // The column sums k_colsumx forms are then S - lambda^2 I = H_cc - sum H_fc^T A_f and b = g_c - sum H_fc^T b_f.
+      double* EX = sm;            // [W] H_cc upper packed | g_c
+      double* Tl = EX + W;        // [N][6][48] T_i
+      double* gB = Tl + N * 288;  // [N][48] camera i's share of g_B
+      double* cc = gB + N * 48;   // [N] chi^2 of camera i
+      const int Wt = W - C, NB = 6 * (N - 1), CI = C - NB, ci0 = ctab[0][cam];
+      const int i16 = lane & 15, k0 = lane >> 4;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int a = mrow + 4 * q, b = mcol, x = a - 6, y = b - 6;
@@ -1648,7 +1654,7 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
         if (a == 15 && b == 15) cc[cam] = creg[q];
       }
       if (cam > 0) {
-        const int i16 = lane & 15, k0 = lane >> 4, nct = (6 * cam + 15) >> 4;
+        const int nct = (6 * cam + 15) >> 4;
         const double* Kv = Kl + (cam * (cam - 1) / 2) * 36;
         double kb[3][2];
 #pragma unroll
@@ -1679,7 +1685,59 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
           }
         }
       }
-    } else {
+      {  // the structural zeros of the camera's rows: H_{I_cam, I_k} (k > cam) and H_{I_cam, B_j} (j >= cam)
+        const int nz1 = CI - (ci0 + nin), nzr = nz1 + NB - 6 * cam;
+        for (int e = lane; e < nin * nzr; e += 64) {
+          const int x = e / nzr, k = e - x * nzr;
+          const int q = k < nz1 ? ci0 + nin + k : CI + 6 * cam + (k - nz1);
+          EX[upper_index(ci0 + x, q, C)] = 0.0;
+        }
+      }
+      // the view waves meet (an LDS counter: the frame waves are not at a block barrier now) before the baseline
+      // tiles read every camera's T_i
+      KB_WAVE_SYNC();
+      if (lane == 0) atomicAdd(&xcnt, 1);
+      while (__hip_atomic_load(&xcnt, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < N) __builtin_amdgcn_s_sleep(1);
+      const int ntb = (NB + 15) >> 4;
+      for (int tq = wave; tq < ntb * (ntb + 1) / 2; tq += N) {  // tile (ta, tb), ta <= tb, upper tiles in row order
+        int ta = 0, q = tq;
+        while (q >= ntb - ta) {
+          q -= ntb - ta;
+          ++ta;
+        }
+        const int tb = ta + q;
+        v4d acc = {0.0, 0.0, 0.0, 0.0};
+        for (int i = 1; i < N; ++i) {
+          const double* Kv = Kl + (i * (i - 1) / 2) * 36;
+#pragma unroll
+          for (int st = 0; st < 2; ++st) {
+            const int k = k0 + 4 * st, ca = 16 * ta + i16, cb = 16 * tb + i16;
+            const int cac = min(ca, 6 * i - 1), ja = cac / 6, ya = cac - 6 * ja;
+            const double av = Kv[ja * 36 + min(k, 5) * 6 + ya];
+            const double bv = Tl[i * 288 + min(k, 5) * 48 + min(cb, 47)];
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64((k < 6 && ca < 6 * i) ? av : 0.0,
+                                                       (k < 6 && cb < 6 * i) ? bv : 0.0, acc, 0, 0, 0);
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = 16 * ta + k0 + 4 * r, col = 16 * tb + i16;
+          if (row <= col && col < NB) EX[upper_index(CI + row, CI + col, C)] = acc[r];
+        }
+      }
+      for (int n = tid; n < NB; n += 64 * N) {
+        double g = 0.0;
+        for (int i = n / 6 + 1; i < N; ++i) g += gB[i * 48 + n];
+        EX[Wt + CI + n] = g;
+      }
+      if (tid == 0) {
+        double sc = 0.0;
+        for (int i = 0; i < N; ++i) sc += cc[i];
+        prow[C] = sc;  // the block's chi^2 (the cost column)
+      }
+    }
+    __syncthreads();  // the frame waves' last barrier (after the last frame's elimination)
+    if (!xp) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {  // the camera's local sums, upper packed
         const int a = mrow + 4 * q, b = mcol;
@@ -1713,67 +1771,13 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
       __syncthreads();
     }
     if (fuse && !xp) schur_tiles_store<TT>(prow + N * 136, C, tii, tjj, acc);
-    if (xp) {
-      // the frame waves keep their tiles in registers through the view waves' expansion below, then store EX - tile
-      __syncthreads();
-      __syncthreads();
-      schur_tiles_store_x<TT>(prow + N * 136, C, tii, tjj, acc, sm);
-    }
+    // expanded partials: the view waves expanded the camera block during the last frame's elimination
+    if (xp) schur_tiles_store_x<TT>(prow + N * 136, C, tii, tjj, acc, sm);
   }
   if (xp && vw) {
-    // ---- expanded partials, step 2: the baseline block H_{B_j,B_k} = sum_{i > max(j,k)} K_{i,j}^T T_{i,k}, one 16 x 16
-    // tile per view wave, accumulated over the cameras in order on MFMA (A = K_i^T from the chains in LDS, B = T_i);
-    // g_B = sum_{i > j} (camera i's share) and the cost in fixed order.  The column sums k_colsumx forms are then
-    // S - lambda^2 I = H_cc - sum H_fc^T A_f and b = g_c - sum H_fc^T b_f directly: no kernel expands the finished
-    // sums (k_colimg).  The frame waves hold their Schur tiles meanwhile and pass the same two barriers.
-    double* EX = sm;
-    const double* Tl = EX + W;
-    const double* gB = Tl + N * 288;
-    const double* cc = gB + N * 48;
-    const int Wt = W - C, NB = 6 * (N - 1), CI = C - NB, ntb = (NB + 15) >> 4;
-    __syncthreads();  // step 1 complete (T_i, the camera shares of g_B, the direct entries)
-    for (int tq = wave; tq < ntb * (ntb + 1) / 2; tq += N) {
-      // tile (ta, tb), ta <= tb, of the baseline block (upper tiles in row order)
-      int ta = 0, q = tq;
-      while (q >= ntb - ta) {
-        q -= ntb - ta;
-        ++ta;
-      }
-      const int tb = ta + q;
-      {  // wave-uniform
-        const int i16 = lane & 15, k0 = lane >> 4;
-        v4d acc = {0.0, 0.0, 0.0, 0.0};
-        for (int i = 1; i < N; ++i) {
-          const double* Kv = Kl + (i * (i - 1) / 2) * 36;
-#pragma unroll
-          for (int st = 0; st < 2; ++st) {
-            const int k = k0 + 4 * st, ca = 16 * ta + i16, cb = 16 * tb + i16;
-            const int cac = min(ca, 6 * i - 1), ja = cac / 6, ya = cac - 6 * ja;
-            const double av = Kv[ja * 36 + min(k, 5) * 6 + ya];
-            const double bv = Tl[i * 288 + min(k, 5) * 48 + min(cb, 47)];
-            acc = __builtin_amdgcn_mfma_f64_16x16x4f64((k < 6 && ca < 6 * i) ? av : 0.0,
-                                                       (k < 6 && cb < 6 * i) ? bv : 0.0, acc, 0, 0, 0);
-          }
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = 16 * ta + k0 + 4 * r, col = 16 * tb + i16;
-          if (row <= col && col < NB) EX[upper_index(CI + row, CI + col, C)] = acc[r];
-        }
-      }
-    }
-    for (int n = tid; n < NB; n += 64 * N) {
-      double g = 0.0;
-      for (int i = n / 6 + 1; i < N; ++i) g += gB[i * 48 + n];
-      EX[Wt + CI + n] = g;
-    }
-    if (tid == 0) {
-      double sc = 0.0;
-      for (int i = 0; i < N; ++i) sc += cc[i];
-      prow[C] = sc;  // the block's chi^2 (the cost column)
-    }
-    __syncthreads();  // EX complete: the frame waves store EX - tile
-    for (int e = tid; e < C; e += 64 * N) prow[e] = EX[Wt + e];  // the g_c columns
+    // expanded partials: the g_c columns of the block's partial row (the cost column was written in the idle phase)
+    const double* EX = sm;
+    for (int e = tid; e < C; e += 64 * N) prow[e] = EX[W - C + e];
   }
   __syncthreads();  // okl final
   if (wave == 0) KB_TSB(d, 63);
@@ -2693,6 +2697,21 @@ __device__ __forceinline__ void fmac_bc_self(double& x, double f) {
   asm volatile("v_fmac_f64_dpp %0, %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf" : "+v"(x) : "v"(f), "i"(L));
 }
 
+// lane L's v within the lane's 16-lane row (64-bit DPP row_newbcast as two 32-bit moves), after 2 wait states: the
+// DPP read hazard of a VGPR that a VALU instruction has just written is not seen by the compiler through inline asm,
+// so the wait sits inside the statement
+template <int L>
+__device__ __forceinline__ double bcast16_dep(double v) {
+  const unsigned long long b = __double_as_longlong(v);
+  unsigned lo = (unsigned)b, hi = (unsigned)(b >> 32), olo, ohi;
+  asm volatile(
+      "s_nop 1\n\tv_mov_b32_dpp %0, %2 row_newbcast:%4 row_mask:0xf bank_mask:0xf\n\t"
+      "v_mov_b32_dpp %1, %3 row_newbcast:%4 row_mask:0xf bank_mask:0xf"
+      : "=&v"(olo), "=&v"(ohi)
+      : "v"(lo), "v"(hi), "i"(L));
+  return __longlong_as_double(((unsigned long long)ohi << 32) | olo);
+}
+
 // updates of step K for columns J .. 15: the below row first (it reads the pivot row's column J before the diagonal
 // row's own update of it), then the diagonal row
 template <int K, int J>
@@ -2713,8 +2732,9 @@ template <int K>
 __device__ __forceinline__ void panel2_steps(double (&dr)[16], double (&br)[16], int r, int q, int C, bool& ok,
                                              double& rd) {
   if constexpr (K < 16) {
-    asm volatile("s_nop 1" ::: "memory");  // DPP read of a VGPR a VALU wrote: 2 wait states
-    const double Dk = bcast16(dr[K], K);
+    // D_K from lane K (its row's pivot), with the DPP wait inside the statement: dr[K] may have been written by the
+    // previous step's last FMA just before (K = 15); every later DPP read of this step follows it
+    const double Dk = bcast16_dep<K>(dr[K]);
     const double rdk = Dk > 0.0 ? recip_d1(Dk) : 0.0;
     const double nfd = -(dr[K] * rdk), nfb = -(br[K] * rdk);
     panel2_cols<K, K + 1>(dr, br, nfd, nfb);
@@ -3013,10 +3033,9 @@ __device__ __forceinline__ void panel_backsolve(const KbDev& d, const double* S,
   }
 }
 
-// ---- the backsolve with prefetched operands (panel_backsolve2): the operands of tile ti - 1 (a column of its inverse
-// and the lane's two rows of L~ left of it) are loaded from LDS while tile ti is solved, the tile's mat-vec and the
-// updates of the earlier rows take their broadcasts through DPP fused into the FMAs, and the tile's values reach the
-// other 16-lane groups through one LDS slot without a wave-wide wait (one wave's LDS accesses complete in order).
+// ---- the backsolve with DPP-fused broadcasts (panel_backsolve2): the tile's mat-vec and its dependent chain take their
+// broadcasts through DPP fused into the FMAs, and the tile's values reach the other 16-lane groups through one LDS slot
+// without a wave-wide wait (one wave's LDS accesses complete in order).
 struct BsOps {
   double M[16];       // column r of X_ti = Ltilde_tt^-1 (CHAIN: of the factored tile), masked to the entries it uses
   double Le[2][16];   // Ltilde[16 ti + u][row[sl]] for the lane's rows (slots 0, 1)
@@ -3064,9 +3083,11 @@ __device__ __forceinline__ void bs2_solve(const BsOps& o, int C, int ti, const i
     double M[16];
 #pragma unroll
     for (int u = 0; u < 16; ++u) M[u] = (u >= r) ? o.M[u] : 0.0;
-    asm volatile("s_nop 1" ::: "memory");
+    // the first DPP read of xt waits inside its statement (xt was just selected by a VALU instruction)
+    fmac_bc_dep<0>(a0, xt, M[0]);
+    fmac_bc<1>(a1, xt, M[1]);
 #define KB_BS2_MV(U) fmac_bc<U>(a0, xt, M[U]); fmac_bc<U + 1>(a1, xt, M[U + 1]);
-    KB_BS2_MV(0) KB_BS2_MV(2) KB_BS2_MV(4) KB_BS2_MV(6) KB_BS2_MV(8) KB_BS2_MV(10) KB_BS2_MV(12) KB_BS2_MV(14)
+    KB_BS2_MV(2) KB_BS2_MV(4) KB_BS2_MV(6) KB_BS2_MV(8) KB_BS2_MV(10) KB_BS2_MV(12) KB_BS2_MV(14)
 #undef KB_BS2_MV
     xt = a0 + a1;
   }
@@ -3107,29 +3128,21 @@ __device__ __forceinline__ void panel_backsolve2(const KbDev& d, const double* S
     rdv[sl] = rd;
     x[sl] = row[sl] < C ? z * rd : 0.0;
   }
+  // one tile's operands at a time (a ping-pong prefetch of the next tile's 48 doubles spilled the kernel): they do not
+  // depend on x, so their LDS loads go out ahead of the tile's dependent chain anyway
   int ti = (C - 1) >> 4;
-  BsOps A, B;
-  const bool chain = ti == nb - 1;  // the tile holding row C: no inverse, solved by its dependent chain
-  if (chain) bs2_load<true>(S, Dfac, Xinv, C, ti, row, rdv, A);
-  else bs2_load<false>(S, Dfac, Xinv, C, ti, row, rdv, A);
-  if (ti > 0) bs2_load<false>(S, Dfac, Xinv, C, ti - 1, row, rdv, B);
-  __builtin_amdgcn_sched_barrier(0);
-  if (chain) bs2_solve<true>(A, C, ti, row, rdv, pub, x);
-  else bs2_solve<false>(A, C, ti, row, rdv, pub, x);
-  if (xb && ti == pub_tile) bs_publish(C, pub_tile, xb, bflag, x);
-  --ti;
-#pragma unroll 1
-  while (ti >= 0) {  // B holds tile ti: prefetch ti - 1 into A, solve ti; then the roles swap
-    if (ti > 0) bs2_load<false>(S, Dfac, Xinv, C, ti - 1, row, rdv, A);
-    __builtin_amdgcn_sched_barrier(0);
-    bs2_solve<false>(B, C, ti, row, rdv, pub, x);
-    if (xb && ti == pub_tile) bs_publish(C, pub_tile, xb, bflag, x);
-    if (--ti < 0) break;
-    if (ti > 0) bs2_load<false>(S, Dfac, Xinv, C, ti - 1, row, rdv, B);
-    __builtin_amdgcn_sched_barrier(0);
-    bs2_solve<false>(A, C, ti, row, rdv, pub, x);
+  BsOps A;
+  if (ti == nb - 1) {  // the tile holding row C: no inverse, solved by its dependent chain
+    bs2_load<true>(S, Dfac, Xinv, C, ti, row, rdv, A);
+    bs2_solve<true>(A, C, ti, row, rdv, pub, x);
     if (xb && ti == pub_tile) bs_publish(C, pub_tile, xb, bflag, x);
     --ti;
+  }
+#pragma unroll 1
+  for (; ti >= 0; --ti) {
+    bs2_load<false>(S, Dfac, Xinv, C, ti, row, rdv, A);
+    bs2_solve<false>(A, C, ti, row, rdv, pub, x);
+    if (xb && ti == pub_tile) bs_publish(C, pub_tile, xb, bflag, x);
   }
 }
 

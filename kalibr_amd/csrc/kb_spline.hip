@@ -12,6 +12,7 @@
 //   spline DVs (additive 6-vectors)             aslam_splines/src/BSplinePoseDesignVariable.cpp:9-19
 //   B-spline basis (host side, kb_sp_upload)    bsplines/src/BSpline.cpp:58-152, 237-387
 #include <hip/hip_runtime.h>
+#include <type_traits>
 
 #include <algorithm>
 #include <chrono>
@@ -975,10 +976,131 @@ __device__ __forceinline__ double ksp_recip(double x) {
   return fma(r, e, r);
 }
 
+// ---- the 18 x 18 Cholesky with the pivot-row broadcasts fused into the FMAs (chol18_dpp, the default)
+// x += (lane L's y within the lane's 16-lane row) * f by one v_fmac_f64 with a DPP row_newbcast source (64-bit DPP,
+// gfx90a+); y may be x itself (operands are read before the write)
+template <int L>
+__device__ __forceinline__ void ksp_fmac_bc(double& x, double y, double f) {
+  asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf" : "+v"(x) : "v"(y), "v"(f), "i"(L));
+}
+template <int L>
+__device__ __forceinline__ void ksp_fmac_bc_self(double& x, double f) {
+  asm volatile("v_fmac_f64_dpp %0, %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf" : "+v"(x) : "v"(f), "i"(L));
+}
+// lane L's v within its 16-lane row after 2 wait states (the compiler does not see the DPP hazard of a VGPR an inline
+// asm VALU instruction has just written)
+template <int L>
+__device__ __forceinline__ double ksp_bcast_dep(double v) {
+  const unsigned long long b = __double_as_longlong(v);
+  unsigned lo = (unsigned)b, hi = (unsigned)(b >> 32), olo, ohi;
+  asm volatile(
+      "s_nop 1\n\tv_mov_b32_dpp %0, %2 row_newbcast:%4 row_mask:0xf bank_mask:0xf\n\t"
+      "v_mov_b32_dpp %1, %3 row_newbcast:%4 row_mask:0xf bank_mask:0xf"
+      : "=&v"(olo), "=&v"(ohi)
+      : "v"(lo), "v"(hi), "i"(L));
+  return __longlong_as_double(((unsigned long long)ohi << 32) | olo);
+}
+template <int K, int J>
+__device__ __forceinline__ void chol18_cols(double (&dr)[NB], double (&br)[NB], double nfd, double nfb) {
+  if constexpr (J < NB) {
+    ksp_fmac_bc<K>(br[J], dr[J], nfb);  // the below row first: it reads the pivot row's column J before its update
+    ksp_fmac_bc_self<K>(dr[J], nfd);
+    chol18_cols<K, J + 1>(dr, br, nfd, nfb);
+  }
+}
+// pivot steps K .. 15 (the LDL^T form: W = L D kept in place, D_K on the diagonal), 1/sqrt(D_K) collected in rs[K]
+template <int K>
+__device__ __forceinline__ void chol18_steps(double (&dr)[NB], double (&br)[NB], double (&rs)[16], bool& ok) {
+  if constexpr (K < 16) {
+    const double Dk = ksp_bcast_dep<K>(dr[K]);
+    const bool pos = Dk > 0.0;
+    const double rdk = pos ? ksp_recip(Dk) : 0.0;
+    const double nfd = -(dr[K] * rdk), nfb = -(br[K] * rdk);
+    chol18_cols<K, K + 1>(dr, br, nfd, nfb);
+    ok = ok && pos;
+    // 1 / sqrt(D_K) by v_rsq_f64 + two Newton steps, off the pivot chain (only the final scaling reads it)
+    const double dpos = pos ? Dk : 1.0;
+    double r = __builtin_amdgcn_rsq(dpos);
+    r = r * fma(-0.5 * dpos * r, r, 1.5);
+    rs[K] = r * fma(-0.5 * dpos * r, r, 1.5);
+    chol18_steps<K + 1>(dr, br, rs, ok);
+  }
+}
+
+// one-wave Cholesky of an 18 x 18 SPD matrix in LDS (row-major, both triangles), written back as the lower factor L
+// with id = 1 / diag(L).  Columns 0..15 as one panel: every 16-lane row of the wave holds rows 0..15 (lane r: row r)
+// and lanes 16, 17 also rows 16, 17 of the matrix; step K takes D_K and the pivot row from lane K of its own 16-lane row
+// by DPP (fused into the FMAs: no v_readlane / SGPR round trip, which the readlane version pays twice per broadcast
+// double).  Then the 2 x 2 trailing block (rows 16, 17) and the scaling W D^-1/2 -> L.  Returns false if not positive
+// definite.  Call from one whole wave.
+__device__ __forceinline__ bool chol18_dpp(double* A, double* id, int lane) {
+  const int r = lane & 15, g = lane >> 4;
+  const int br_row = (g == 1 && r < 2) ? 16 + r : r;  // lanes 16, 17: rows 16, 17 (the others: a copy, unused)
+  double dr[NB], br[NB], rs[16];
+#pragma unroll
+  for (int c = 0; c < NB; ++c) {
+    dr[c] = A[r * NB + c];
+    br[c] = A[br_row * NB + c];
+  }
+  bool ok = true;
+  chol18_steps<0>(dr, br, rs, ok);
+  // trailing 2 x 2 (rows 16, 17 after the panel): D_16 = br[16] of lane 16, w = br[16] of lane 17, D_17 = br[17] of
+  // lane 17 - w^2 / D_16
+  // v_readlane of VGPRs the inline-asm FMAs just wrote: the wait states inside the statement
+  auto rl_dep = [](double v, auto lane_c) {
+    constexpr int LN = decltype(lane_c)::value;
+    const unsigned long long b = __double_as_longlong(v);
+    unsigned lo = (unsigned)b, hi = (unsigned)(b >> 32), slo, shi;
+    asm volatile("s_nop 4\n\tv_readlane_b32 %0, %2, %4\n\tv_readlane_b32 %1, %3, %4\n\ts_nop 1"
+                 : "=s"(slo), "=s"(shi)
+                 : "v"(lo), "v"(hi), "i"(LN));
+    return __longlong_as_double(((unsigned long long)shi << 32) | slo);
+  };
+  const double d16 = rl_dep(br[16], std::integral_constant<int, 16>{});
+  const double w17 = rl_dep(br[16], std::integral_constant<int, 17>{});
+  const double a17 = rl_dep(br[17], std::integral_constant<int, 17>{});
+  const bool p16 = d16 > 0.0;
+  const double r16 = p16 ? ksp_recip(d16) : 0.0;
+  const double d17 = a17 - w17 * w17 * r16;
+  const bool p17 = d17 > 0.0;
+  ok = ok && p16 && p17;
+  auto rsq2 = [](double x) {
+    const double dp = x > 0.0 ? x : 1.0;
+    double q = __builtin_amdgcn_rsq(dp);
+    q = q * fma(-0.5 * dp * q, q, 1.5);
+    return q * fma(-0.5 * dp * q, q, 1.5);
+  };
+  const double s16 = rsq2(d16), s17 = rsq2(d17);
+  KSP_WAVE_SYNC();
+  if (lane < NB) {  // rows 0..15: lanes 0..15 (dr); rows 16, 17: lanes 16, 17 (br)
+    const double* row = lane < 16 ? dr : br;
+    double out[NB];
+    double idr = 1.0;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      // W[row][c] / sqrt(D_c) below the diagonal, sqrt(D_row) = D_row / sqrt(D_row) on it, zero above
+      const double v = row[c] * rs[c];
+      out[c] = c <= lane ? v : 0.0;
+      idr = (c == lane) ? rs[c] : idr;
+    }
+    out[16] = lane == 16 ? d16 * s16 : lane == 17 ? w17 * s16 : 0.0;
+    out[17] = lane == 17 ? d17 * s17 : 0.0;
+    idr = lane == 16 ? s16 : lane == 17 ? s17 : idr;
+#pragma unroll
+    for (int c = 0; c < NB; ++c) A[lane * NB + c] = out[c];
+    id[lane] = idr;
+  }
+  KSP_WAVE_SYNC();
+  return ok;
+}
+
 // one-wave register Cholesky of an 18 x 18 SPD matrix held in LDS (lower, row-major): lane r keeps row r in
 // registers, column k broadcast by v_readlane; the factor is written back.  Returns false if not positive
 // definite.  Call from one whole wave.
 __device__ __forceinline__ bool chol18_wave(double* A, double* id, int lane) {
+#ifndef KSP_CHOL_READLANE
+  return chol18_dpp(A, id, lane);
+#endif
   double a[NB];
 #pragma unroll
   for (int c = 0; c < NB; ++c) a[c] = lane < NB ? A[lane * NB + c] : 0.0;

@@ -728,8 +728,8 @@ bool GpuMarginalLinearSolver::optimizeDevice(const Optimizer2Options& oo, Soluti
   o.max_iterations = oo.maxIterations;
   o.convergence_dx = oo.convergenceDeltaX;
   o.convergence_dj = oo.convergenceDeltaJ;
-  o.sync_every = 0;
-  o.use_graph = 1;
+  o.sync_every = syncEvery;
+  o.use_graph = useGraph ? 1 : 0;
   kb_marginal_options m = marg_opts(_lopt);
   kb_solution s{};
   kb_marginal_info inf{};

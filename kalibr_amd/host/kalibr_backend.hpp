@@ -329,6 +329,10 @@ class GpuMarginalLinearSolver : public MarginalLinearSystemSolver {
   GpuLinearSystemSolver& gpu() { return _g; }
   /// false: optimizeDevice declines and the IncrementalEstimator drives the per-call host loop (parity / timing)
   bool deviceLoop = true;
+  /// the device loop's launches: captured pass graphs (recaptured whenever the frame count changed) or eager
+  /// launches; passes between host checks of the loop state (0: the library default)
+  bool useGraph = true;
+  int syncEvery = 0;
 
  private:
   GpuLinearSystemSolver _g;

@@ -7,7 +7,7 @@ from collections import defaultdict
 
 d, out, wl = sys.argv[1], sys.argv[2], sys.argv[3]
 acc = defaultdict(lambda: defaultdict(list))
-for sub in ("pmc_sq1", "pmc_sq2"):
+for sub in ("pmc_sq1", "pmc_sq2", "pmc_sq3"):
     try:
         rows = csv.DictReader(open(f"{d}/{sub}/pmc_counter_collection.csv"))
     except OSError:
