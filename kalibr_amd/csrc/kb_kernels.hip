@@ -2847,6 +2847,34 @@ __device__ __forceinline__ void tile_unit_inverse(const double* Dfac, const doub
   for (int j = 0; j < 4; ++j) xo[j] = X[j];
 }
 
+// tile_unit_inverse with the broadcasts fused into the FMAs (DPP row_newbcast source operand): 60 dependent-free FMAs
+// per lane in 15 steps of 4 independent columns
+template <int M>
+__device__ __forceinline__ void tui_steps(double (&X)[4], const double (&nL)[16]) {
+  if constexpr (M < 15) {
+    if constexpr (M == 0) fmac_bc_dep<M>(X[0], X[0], nL[M]);  // X was just initialised by VALU moves
+    else fmac_bc<M>(X[0], X[0], nL[M]);
+    fmac_bc<M>(X[1], X[1], nL[M]);
+    fmac_bc<M>(X[2], X[2], nL[M]);
+    fmac_bc<M>(X[3], X[3], nL[M]);
+    tui_steps<M + 1>(X, nL);
+  }
+}
+__device__ __forceinline__ void tile_unit_inverse2(const double* Dfac, const double* rD, double* Xinv, int t) {
+  const int lane = threadIdx.x & 63, g = lane >> 4, r = lane & 15;
+  const double* Lr = Dfac + t * kTileSz + r * kTS;
+  double nL[16];
+#pragma unroll
+  for (int m = 0; m < 16; ++m) nL[m] = (m < r) ? -(Lr[m] * rD[16 * t + m]) : 0.0;
+  double X[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) X[j] = (4 * g + j == r) ? 1.0 : 0.0;
+  tui_steps<0>(X, nL);
+  double* xo = Xinv + t * kTileSz + r * kTS + 4 * g;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) xo[j] = X[j];
+}
+
 // the factorisation (every thread of the 8-wave block calls it); two phases per panel q:
 //   A (q > 0): column q of the trailing matrix gets panel q-1 (tiles (q + w, q), one per wave w, on MFMA);
 //   B: factor waves 0 (and 1 while panel q has more than three tiles below it) factor panel q; update waves 2, 3, 6, 7
@@ -2890,6 +2918,8 @@ __device__ __forceinline__ void ldl_panels(const KbDev& d, double* S, double* rD
       const int m = nb - 1 - q, ntiles = m * (m + 1) / 2;
       const double* rdq = rD + 16 * (q - 1);
       // two tiles at a time: all their operands in one round of LDS loads, then 8 MFMAs in two chains
+      // (four tiles per round, one round for the 15 tiles of the first trailing update at C = 106, measured slower:
+      // panel 1 2.52 -> 2.76 us, tools/micro/camera_solve)
 #pragma unroll 1
       for (int qq = ow; qq < ntiles; qq += 8) {
         const int qb = min(qq + 4, ntiles - 1);
@@ -2922,10 +2952,13 @@ __device__ __forceinline__ void ldl_panels(const KbDev& d, double* S, double* rD
           tile_sub(Tb, Tb, accb, lane);
         }
       }
-      // the factored diagonal tiles' inverses for the backsolve, where the trailing work has thinned out: tile t at
-      // panel max(t + 1, min(4, nb - 1)) by update wave t mod 4 (the last tile, holding row C, is solved by its chain)
-      for (int t = ow; t < nb - 1; t += 4)
-        if (q == max(t + 1, min(4, nb - 1))) tile_unit_inverse(Dfac, rD, Xinv, t);
+    } else if ((wave == 1 || wave == 5) && q >= 2) {
+      // the factored diagonal tiles' inverses for the backsolve on SIMD 1, idle once panel q has one factor wave
+      // (q >= 2 for C <= 111): tile t at panel t + 2 on wave 1, the last one (t = nb - 2) at the last panel on wave 5;
+      // the last tile, holding row C, is solved by its chain
+      // (while wave 1 still factors, i.e. nf == 2 in the readlane variant, wave 5 takes tile q - 2)
+      const int t = (wave == 1 || nf == 2) ? q - 2 : (q == nb - 1 ? nb - 2 : -1);
+      if (t >= 0) tile_unit_inverse2(Dfac, rD, Xinv, t);
     }
     __syncthreads();
     KB_TS(d, 10 + q);
@@ -3144,6 +3177,130 @@ __device__ __forceinline__ void panel_backsolve2(const KbDev& d, const double* S
     bs2_solve<false>(A, C, ti, row, rdv, pub, x);
     if (xb && ti == pub_tile) bs_publish(C, pub_tile, xb, bflag, x);
   }
+}
+
+// ---- the replicated backsolve (panel_backsolve3, measured and not kept: KB_BACKSOLVE3): every 16-lane row of the
+// wave runs the whole
+// backward solve, lane (g, r) holding y_t[r] (row 16 t + r) of every tile t.  Tile t's values then reach the rows of
+// the earlier tiles by DPP row_newbcast inside the lane's own 16-lane row: no LDS publication and no cross-row move.
+// The solve is a fixed sequence of ops, each 16 DPP-fused FMAs over one column of a tile: op (T, T) forms x_T (the
+// mat-vec X_T^T y_T, or the last tile's dependent chain), ops (T, s), s = T-1 .. 0, update y_s by x_T.  Each op's 16
+// operands are loaded from LDS before the previous op's FMAs issue (inline asm is a scheduling boundary, so the
+// prefetch is written out), and masks are multiplications so that no load becomes conditional.  On one CU
+// (tools/micro/camera_solve) it takes 4.7 us with a warm instruction cache and 8.4 us cold (its ~6 KB of straight-line
+// code runs once per launch), against 3.4 us for panel_backsolve2's tile loop either way.
+struct Bs3 {
+  const KbDev* d;  // diagnostic stamps only
+  const double* S;
+  const double* Dfac;
+  const double* Xinv;
+  int C, nb, r;
+};
+
+// operand column of op (T, SS): column r of X_T (the unit-lower tile inverse, exact zeros above its diagonal) or, for
+// the last tile (its chain), of the factored diagonal tile; of tile (T, SS) for an update
+template <int T, int SS>
+__device__ __forceinline__ void bs3_load(const Bs3& b, double (&w)[16]) {
+  const double* pe = (SS == T ? ((T == b.nb - 1) ? b.Dfac : b.Xinv) + T * kTileSz : b.S + tile_base(T, SS)) + b.r;
+#pragma unroll
+  for (int u = 0; u < 16; ++u) w[u] = pe[u * kTS];
+}
+
+template <int T, int SS, int P>
+__device__ __forceinline__ void bs3_op(const Bs3& b, double (&y)[8], const double (&rdv)[8], double& xt,
+                                       double (&w0)[16], double (&w1)[16], int pub_tile, double* xb,
+                                       volatile int* bflag) {
+  if constexpr (T >= 0) {
+    double(&w)[16] = P ? w1 : w0;   // this op's operands (loaded by the previous op)
+    double(&wn)[16] = P ? w0 : w1;  // the next op's
+    constexpr int NT = SS > 0 ? T : T - 1, NS = SS > 0 ? SS - 1 : T - 1;
+    if constexpr (NT >= 0) bs3_load<NT, NS>(b, wn);
+    if constexpr (SS == T) {
+      const int r = b.r, lim = b.C - 16 * T;
+      KB_TS(*b.d, 240 + T);
+      xt = y[T];
+      if (T == b.nb - 1) {  // wave-uniform: the tile holding row C, solved by its dependent chain (rows >= C: x = 0)
+        double M[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) M[u] = -(w[u] * rdv[T]) * ((r < u && u < lim) ? 1.0 : 0.0);
+        // x[r] -= sum_{u > r} L[u][r] x[u], u from the last: 16 dependent steps, x[u] read from lane u by DPP
+#define KB_BS3_STEP(U) fmac_bc_dep<U>(xt, xt, M[U]);
+        KB_BS3_STEP(15) KB_BS3_STEP(14) KB_BS3_STEP(13) KB_BS3_STEP(12) KB_BS3_STEP(11) KB_BS3_STEP(10)
+        KB_BS3_STEP(9) KB_BS3_STEP(8) KB_BS3_STEP(7) KB_BS3_STEP(6) KB_BS3_STEP(5) KB_BS3_STEP(4) KB_BS3_STEP(3)
+        KB_BS3_STEP(2) KB_BS3_STEP(1) KB_BS3_STEP(0)
+#undef KB_BS3_STEP
+      } else {
+        // x_t[r] = sum_{c >= r} X[c][r] y[c] (X lower: the c < r terms are exact zeros), y[c] from lane c by DPP
+        double a0 = 0.0, a1 = 0.0;
+        fmac_bc_dep<0>(a0, xt, w[0]);
+        fmac_bc<1>(a1, xt, w[1]);
+#define KB_BS3_MV(U) fmac_bc<U>(a0, xt, w[U]); fmac_bc<U + 1>(a1, xt, w[U + 1]);
+        KB_BS3_MV(2) KB_BS3_MV(4) KB_BS3_MV(6) KB_BS3_MV(8) KB_BS3_MV(10) KB_BS3_MV(12) KB_BS3_MV(14)
+#undef KB_BS3_MV
+        xt = a0 + a1;
+      }
+      y[T] = xt;
+      if (xb && T == pub_tile) {  // the baseline rows are final: publish them for the baseline / chain wave
+        if ((threadIdx.x & 63) < 16) {
+#pragma unroll
+          for (int t = T; t < 8; ++t)
+            if (t < b.nb && 16 * t + r < b.C) xb[16 * t + r] = y[t];
+        }
+        KB_WAVE_SYNC();
+        if ((threadIdx.x & 63) == 0) *bflag = 1;
+      }
+    } else {
+      // y_s[r] -= (1/D of row 16 s + r) sum_u W[16 T + u][16 s + r] x_T[u], x_T[u] from lane u by DPP (rows >= C of the
+      // last tile carry x = 0)
+      double a0 = 0.0, a1 = 0.0;
+      if constexpr (SS == T - 1) fmac_bc_dep<0>(a0, xt, w[0]);
+      else fmac_bc<0>(a0, xt, w[0]);
+      fmac_bc<1>(a1, xt, w[1]);
+#define KB_BS3_MV(U) fmac_bc<U>(a0, xt, w[U]); fmac_bc<U + 1>(a1, xt, w[U + 1]);
+      KB_BS3_MV(2) KB_BS3_MV(4) KB_BS3_MV(6) KB_BS3_MV(8) KB_BS3_MV(10) KB_BS3_MV(12) KB_BS3_MV(14)
+#undef KB_BS3_MV
+      y[SS] -= (a0 + a1) * rdv[SS];
+    }
+    bs3_op<NT, NS, 1 - P>(b, y, rdv, xt, w0, w1, pub_tile, xb, bflag);
+  }
+}
+
+// entry at the last tile T = nb - 1 (nb in 5..7 for 64 < C <= 111)
+template <int T>
+__device__ __forceinline__ void bs3_run(const Bs3& b, double (&y)[8], const double (&rdv)[8], int pub_tile, double* xb,
+                                        volatile int* bflag) {
+  double w0[16], w1[16], xt = 0.0;
+  bs3_load<T, T>(b, w0);
+  bs3_op<T, T, 0>(b, y, rdv, xt, w0, w1, pub_tile, xb, bflag);
+}
+
+// x = Ltilde^-T z as panel_backsolve (same operands, same result layout: x[s] = x_{l + 64 s}), nb <= 7
+__device__ __forceinline__ void panel_backsolve3(const KbDev& d, const double* S, const double* Dfac, const double* Xinv,
+                                                 const double* rD, int C, int nb, double (&x)[2], int pub_tile = -1,
+                                                 double* xb = nullptr, volatile int* bflag = nullptr) {
+  const int lane = threadIdx.x & 63, g = lane >> 4, r = lane & 15;
+  Bs3 b{&d, S, Dfac, Xinv, C, nb, r};
+  double y[8], rdv[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const int row = 16 * t + r, rc = min(row, C - 1);
+    // row C's W: in place off the diagonal tile, in Dfac inside it
+    const double* zp = (rc >> 4) == (C >> 4) ? Dfac + (C >> 4) * kTileSz + (C & 15) * kTS + (rc & 15) : S + tidx(C, rc);
+    const double z = *zp, rd = rD[rc];
+    rdv[t] = rd;
+    y[t] = (t < nb && row < C) ? z * rd : 0.0;
+  }
+  if (nb == 7) bs3_run<6>(b, y, rdv, pub_tile, xb, bflag);
+  else if (nb == 6) bs3_run<5>(b, y, rdv, pub_tile, xb, bflag);
+  else bs3_run<4>(b, y, rdv, pub_tile, xb, bflag);
+  double x0 = y[0], x1 = y[4];
+#pragma unroll
+  for (int t = 1; t < 4; ++t) {
+    x0 = g == t ? y[t] : x0;
+    x1 = g == t ? y[t + 4] : x1;
+  }
+  x[0] = x0;
+  x[1] = x1;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -3907,11 +4064,14 @@ __device__ void solve_body(const KbDev& d, int gate, int do_update, int nth) {
     const int cb0 = ctab[2][0], pub_tile = N > 1 ? cb0 >> 4 : -1;
     const bool upd = do_update && okl && !(gfu && fin[0]);
     if (tid < 64) {
-#ifdef KB_BACKSOLVE1
+#if defined(KB_BACKSOLVE1)
       panel_backsolve(d, S, Dfac, Xinv, rDv, C, nb, pubcol, x, pub_tile, xb, &bflag);
+#elif defined(KB_BACKSOLVE3)
+      panel_backsolve3(d, S, Dfac, Xinv, rDv, C, nb, x, pub_tile, xb, &bflag);
 #else
       panel_backsolve2(d, S, Dfac, Xinv, rDv, C, nb, pubcol, x, pub_tile, xb, &bflag);
 #endif
+      KB_TS(d, 8);
       if (okl && !(gfu && fin[0])) wave0_tail(gfu ? fin[1] : cur);
     } else if ((tid >> 6) == 1 && upd) {
       const int lane = tid & 63, cu = gfu ? fin[1] : cur;

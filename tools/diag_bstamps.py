@@ -1,5 +1,5 @@
 """Diagnostic: timeline of block 0 of the last pipelined build (k_buildp) inside GN passes (KB_TSB stamps,
-s_memrealtime 100 MHz), diagnostic library only: python tools/diag_bstamps.py [config]"""
+s_memrealtime 100 MHz), diagnostic library only: python tools/diag_bstamps.py [config] [n_frames]"""
 import ctypes as C
 import os
 import sys
@@ -12,7 +12,7 @@ capi.LIB_PATH = os.path.join(ROOT, "kalibr_amd", "libkalibr_hip_stamps.so")
 L = capi.lib()
 L.kb_diag_read_ts.argtypes = [C.c_void_p, C.POINTER(C.c_longlong), C.c_int]
 cfg = int(sys.argv[1]) if len(sys.argv) > 1 else 4
-p = synth.make_config(cfg)
+p = synth.make_config(cfg, n_frames=int(sys.argv[2])) if len(sys.argv) > 2 else synth.make_config(cfg)
 g = capi.Solver(p)
 g.set_state(p.state_init)
 buf = (C.c_longlong * 256)()

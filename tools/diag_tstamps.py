@@ -15,10 +15,10 @@ cfg = int(sys.argv[1]) if len(sys.argv) > 1 else 4
 p = synth.make_config(cfg)
 g = capi.Solver(p)
 g.set_state(p.state_init)
-buf = (C.c_longlong * 64)()
-assert L.kb_diag_read_ts(g.h, buf, 64) == 0  # allocates the stamp buffer
+buf = (C.c_longlong * 256)()
+assert L.kb_diag_read_ts(g.h, buf, 256) == 0  # allocates the stamp buffer
 names = {0: "entry", 1: "staged", 2: "T (+pass end)", 3: "H_cc blocks + grad", 4: "LDL^T", 5: "solves",
-         6: "stats + DV update", 7: "chains"}
+         6: "stats + DV update", 7: "chains", 8: "  backsolve done (wave 0)"}
 names[47] = "  expansion: intrinsic blocks done (wave 0)"
 names[48] = "  expansion: MFMA tiles done (wave 0)"
 names[40] = "    p2: lookahead done"
@@ -26,13 +26,15 @@ names[41] = "    p2: rows loaded"
 names[42] = "    p2: 16 steps done"
 for i in range(10, 20):
     names[i] = f"  panel {i - 10}"
+for t in range(7):
+    names[240 + t] = f"    backsolve tile {t} start"
 for q in range(7):
     names[20 + 2 * q] = f"    p{q} factor start (after its MFMA lookahead)"
     names[21 + 2 * q] = f"    p{q} factor end"
 for rep in range(3):
     g.set_state(p.state_init)
     g.run_gn(16)
-    assert L.kb_diag_read_ts(g.h, buf, 64) == 0
+    assert L.kb_diag_read_ts(g.h, buf, 256) == 0
     t0 = buf[0]
     order = sorted((buf[i] - t0, i) for i in names if buf[i] >= t0 and buf[i] - t0 < 10_000_000)
     print(f"k_solve timeline (rep {rep}, us from entry):\n" +

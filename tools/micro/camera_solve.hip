@@ -10,8 +10,8 @@
 
 using namespace kb;
 
-// mode 0: the k_solve block (8 waves); mode 1: the same with the update waves' trailing tiles skipped (timing only)
-__global__ void __launch_bounds__(512) k_cam(KbDev d, const double* img, int n_img, int C, double* x_out, int reps) {
+// bsv: the backsolve variant (1: panel_backsolve, 2: panel_backsolve2, 3: panel_backsolve3, the default)
+__global__ void __launch_bounds__(512) k_cam(KbDev d, const double* img, int n_img, int C, double* x_out, int reps, int bsv) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const int nb = (C + 16) >> 4;
   double* S = sm;
@@ -28,7 +28,11 @@ __global__ void __launch_bounds__(512) k_cam(KbDev d, const double* img, int n_i
     KB_TS(d, 0);
     ldl_panels(d, S, rD, Dfac, Xinv, C, nb, &okl);
     KB_TS(d, 4);
-    if (threadIdx.x < 64) panel_backsolve(d, S, Dfac, Xinv, rD, C, nb, pub, x);
+    if (threadIdx.x < 64) {
+      if (bsv == 1) panel_backsolve(d, S, Dfac, Xinv, rD, C, nb, pub, x);
+      else if (bsv == 2) panel_backsolve2(d, S, Dfac, Xinv, rD, C, nb, pub, x);
+      else panel_backsolve3(d, S, Dfac, Xinv, rD, C, nb, x);
+    }
     __syncthreads();
     KB_TS(d, 5);
   }
@@ -83,29 +87,35 @@ int main() {
   long long* ts;
   (void)hipMalloc(&dimg, n_img * 8);
   (void)hipMalloc(&dx, 128 * 8);
-  (void)hipMalloc(&ts, 128 * 8);
+  (void)hipMalloc(&ts, 256 * 8);
   (void)hipMemcpy(dimg, img.data(), n_img * 8, hipMemcpyHostToDevice);
-  (void)hipMemset(ts, 0, 128 * 8);
+  (void)hipMemset(ts, 0, 256 * 8);
   KbDev d{};
   d.dbg_ts = ts;
   const size_t lds = 8 * (n_img + 2 * nb * kTileSz + 16 * nb);
   (void)hipFuncSetAttribute((const void*)k_cam, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  for (int bsv : {1, 2, 3})
   for (int reps : {1, 3}) {
-    hipLaunchKernelGGL(k_cam, dim3(1), dim3(512), lds, 0, d, dimg, n_img, C, dx, reps);
+    hipLaunchKernelGGL(k_cam, dim3(1), dim3(512), lds, 0, d, dimg, n_img, C, dx, reps, bsv);
     (void)hipDeviceSynchronize();
-    long long t[128];
+    long long t[256];
     std::vector<double> x(128);
-    (void)hipMemcpy(t, ts, 128 * 8, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(t, ts, 256 * 8, hipMemcpyDeviceToHost);
     (void)hipMemcpy(x.data(), dx, 128 * 8, hipMemcpyDeviceToHost);
     double err = 0.0, nx = 0.0;
     for (int i = 0; i < C; ++i) {
       err = std::fmax(err, std::fabs(x[i] - xs[i]));
       nx = std::fmax(nx, std::fabs(xs[i]));
     }
-    std::printf("reps %d (last rep timed): ok %g, max|x - x_host| / max|x| = %.3g\n", reps, x[127], err / nx);
+    std::printf("backsolve v%d, reps %d (last rep timed): ok %g, max|x - x_host| / max|x| = %.3g\n", bsv, reps, x[127], err / nx);
     std::printf("  factor start->end %.2f us, backsolve %.2f us\n", (t[4] - t[0]) / 100.0, (t[5] - t[4]) / 100.0);
     std::printf("  panel 2 detail: lookahead phase (panel 1 end -> factor start) %.2f, row loads %.2f, 16 steps %.2f, stores %.2f us\n",
                 (t[24] - t[11]) / 100.0, (t[41] - t[24]) / 100.0, (t[42] - t[41]) / 100.0, (t[25] - t[42]) / 100.0);
+    if (bsv == 3) {
+      std::printf("  backsolve3 tile starts (us after factor end):");
+      for (int q = nb - 1; q >= 0; --q) std::printf(" %d:%.2f", q, (t[240 + q] - t[4]) / 100.0);
+      std::printf("\n");
+    }
     for (int q = 0; q < nb; ++q)
       std::printf("  panel %d: factor %.2f us (start at %.2f), panel end at %.2f\n", q, (t[21 + 2 * q] - t[20 + 2 * q]) / 100.0,
                   (t[20 + 2 * q] - t[0]) / 100.0, (t[10 + q] - t[0]) / 100.0);
