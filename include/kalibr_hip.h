@@ -328,6 +328,12 @@ int kb_sp_set_constant_conditioner(kb_sp_handle* h, double diag);
  * reference's buildHessianImplementation).  W [6][6] symmetric (row-major); derivative_order >= order is reduced to
  * order - 1 as the reference does; W == NULL removes the term. */
 int kb_sp_set_motion_error(kb_sp_handle* h, const double* W, int32_t derivative_order);
+/* ErrorTermEuclidean priors on the spline position: n terms ErrorTermEuclidean(bsp.position(times[k]), priors[k],
+ * N[k]) (aslam_backend_expressions ErrorTermEuclidean.cpp:10-23,50-66 over BSplinePoseDesignVariable::position,
+ * BSplinePoseDesignVariable.cpp:91-103): e = p(t_k) - prior_k, chi^2 = e^T N_k^-1 e, Jacobian w_j(t_k) [I_3 | 0] on the
+ * active coefficients.  times [n] inside the spline interval, priors [n][3], N [n][3][3] symmetric positive definite
+ * covariances (the reference's first constructor); n == 0 removes the terms. */
+int kb_sp_set_position_priors(kb_sp_handle* h, int32_t n, const double* times, const double* priors, const double* N);
 int kb_sp_solve(kb_sp_handle* h, double* dx_out, int* ok);
 int kb_sp_get_rhs(kb_sp_handle* h, double* rhs_out);
 int kb_sp_apply_update(kb_sp_handle* h, const double* dx, double* deltaX_out);

@@ -35,6 +35,7 @@ EXPORTS = [
     "kb_sp_set_state", "kb_sp_get_state", "kb_sp_eval_cost", "kb_sp_build", "kb_sp_set_constant_conditioner",
     "kb_sp_solve", "kb_sp_get_rhs", "kb_sp_apply_update", "kb_sp_revert", "kb_sp_get_system", "kb_sp_optimize",
     "kb_sp_get_trace", "kb_sp_run_gn_iterations", "kb_sp_kernel_stats", "kb_sp_assemble_stats", "kb_sp_set_motion_error",
+    "kb_sp_set_position_priors",
 ]
 
 
@@ -165,6 +166,7 @@ def lib():
         L.kb_sp_kernel_stats.argtypes = [C.c_void_p, C.c_int32, dp, dp]
         L.kb_sp_assemble_stats.argtypes = [C.c_void_p, C.c_int32, dp, dp]
         L.kb_sp_set_motion_error.argtypes = [C.c_void_p, dp, C.c_int32]
+        L.kb_sp_set_position_priors.argtypes = [C.c_void_p, C.c_int32, dp, dp, dp]
         _lib = L
     return _lib
 
@@ -453,6 +455,18 @@ class SplineSolver:
             return
         self._motion_W = np.ascontiguousarray(W, dtype=np.float64).reshape(6, 6)
         _check(lib().kb_sp_set_motion_error(self.h, _d(self._motion_W), int(derivative_order)))
+
+    def set_position_priors(self, times=None, priors=None, N=None):
+        """ErrorTermEuclidean priors on the spline position p(t_k) (times [n], priors [n][3], covariances N [n][3][3]);
+        no arguments removes them."""
+        if times is None:
+            _check(lib().kb_sp_set_position_priors(self.h, 0, None, None, None))
+            return
+        self._pos = (np.ascontiguousarray(times, dtype=np.float64).reshape(-1),
+                     np.ascontiguousarray(priors, dtype=np.float64).reshape(-1, 3),
+                     np.ascontiguousarray(N, dtype=np.float64).reshape(-1, 3, 3))
+        t, pr, n3 = self._pos
+        _check(lib().kb_sp_set_position_priors(self.h, t.size, _d(t), _d(pr), _d(n3)))
 
     def set_state(self, state):
         st = np.ascontiguousarray(state, dtype=np.float64)

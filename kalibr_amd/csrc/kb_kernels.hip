@@ -198,6 +198,25 @@ __device__ __forceinline__ double chain_entry(const double* R, const double* tq,
   return 0.0;
 }
 
+// chain_entry from wave-uniform registers (R, t_q, t_m) for a lane-dependent entry (a, b): the same products, picked by
+// selects instead of lane-dependent LDS reads in divergent branches.  s = (R_a x t_m)_b and u = (t_q x R_{:,b})_a are
+// chain_entry's two terms of the rotation block.
+__device__ __forceinline__ double chain_entry_reg(const double (&R)[9], const double (&tq)[3], const double* tm, int a,
+                                                  int b) {
+  const int ra = a < 3 ? a : a - 3, rb = b < 3 ? b : b - 3;
+  const double r0 = ra == 0 ? R[0] : ra == 1 ? R[3] : R[6];
+  const double r1 = ra == 0 ? R[1] : ra == 1 ? R[4] : R[7];
+  const double r2 = ra == 0 ? R[2] : ra == 1 ? R[5] : R[8];
+  const double c0 = rb == 0 ? R[0] : rb == 1 ? R[1] : R[2];
+  const double c1 = rb == 0 ? R[3] : rb == 1 ? R[4] : R[5];
+  const double c2 = rb == 0 ? R[6] : rb == 1 ? R[7] : R[8];
+  const double rab = rb == 0 ? r0 : rb == 1 ? r1 : r2;
+  const double s0 = r1 * tm[2] - r2 * tm[1], s1 = -r0 * tm[2] + r2 * tm[0], s2 = r0 * tm[1] - r1 * tm[0];
+  const double u0 = -tq[2] * c1 + tq[1] * c2, u1 = tq[2] * c0 - tq[0] * c2, u2 = -tq[1] * c0 + tq[0] * c1;
+  const double sv = rb == 0 ? s0 : rb == 1 ? s1 : s2, uv = ra == 0 ? u0 : ra == 1 ? u1 : u2;
+  return (a < 3 && b < 3) ? sv + uv : (a < 3 || b < 3) ? -rab : 0.0;
+}
+
 // ---------------------------------------------------------------------------------------------
 // policy: while-condition (Optimizer2.cpp:215-219) + TrustRegionPolicy::solveSystem prelude
 // (TrustRegionPolicy.cpp:39-52) + LM lambda schedule (LevenbergMarquardtTrustRegionPolicy.cpp:50-84)
@@ -1432,23 +1451,13 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
         double Ri[9], ti[3], R[9], t[3];
         pose_inverse(fp, Ri, ti);
         rt_mul(Lc, Lc + 9, Ri, ti, R, t);  // T_cam_w = L_cam T_f^-1
-        // the view's chain G (6 x 6) for the expansion, formed while the first pass's MFMAs run (its LDS round trips
-        // off the critical path)
-        double* wv = Wv + cam * 64;
-        double* Gm = wv + 16;
+        // the view's chain G (6 x 6) for the expansion, formed while the first pass's MFMAs run: every lane holds
+        // T_cam_w and the frame translation in registers, so lane e < 36 picks entry e by selects (no LDS staging;
+        // wave 0's first v-row segment 2.2 -> 1.2 us, the frame period unchanged: the second view wave of each SIMD
+        // sets it)
+        double* Gm = Wv + cam * 64 + 16;
         auto make_g = [&]() {
-          if (lane == 0) {
-#pragma unroll
-            for (int q = 0; q < 9; ++q) wv[q] = R[q];
-            wv[9] = t[0];
-            wv[10] = t[1];
-            wv[11] = t[2];
-            wv[12] = fp[4];
-            wv[13] = fp[5];
-            wv[14] = fp[6];
-          }
-          KB_WAVE_SYNC();
-          if (lane < 36) Gm[lane] = chain_entry(wv, wv + 9, wv + 12, lane / 6, lane % 6);
+          if (lane < 36) Gm[lane] = chain_entry_reg(R, t, fp + 4, lane / 6, lane % 6);
         };
         v4d acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
         const int o0 = fv.x, o1 = fv.y;

@@ -109,7 +109,16 @@ struct SpDev {
   int nblk_q;             // k_sp_cost_motion blocks (64 nodes each)
   const double* QD;       // [n][324] Q blocks within node i
   const double* QU;       // [n][324] Q block node i (rows) -> node i + 1 (columns)
-  double* mcost;          // [n] per-node motion cost at the build state
+  double* mcost;          // [n] per-node motion (+ prior) cost at the build state
+  // ErrorTermEuclidean priors on p(t) (kb_sp_set_position_priors), sorted by first coefficient: e = p(t_k) - prior_k,
+  // chi^2 = e^T invR e, J = w_j [I_3 | 0] on coefficient pb + j
+  int npos;               // 0: none
+  int cq;                 // coefficient-only terms present (motion or priors): node cost kernels + reductions run
+  const int* pb;          // [npos] first coefficient
+  const double* pw;       // [npos][4] value weights
+  const double* pp;       // [npos][3] prior
+  const double* pW;       // [npos][9] invR
+  const int* node_pp;     // [n][4] priors touching node i (b in [3i-3, 3i+2]) | owned by it (b in [3i, 3i+2])
   long long* dbg_ts;      // diagnostics only: [256] KSP_TS stamps
   int dbg_stop;           // diagnostics only (KSP_DBG_STOP): 0, or the phase after which the timed kernels return
   int zero_lam;           // GN pass: k_sp_imu_cc sets lambda^2 = 0 (no separate launch)
@@ -782,6 +791,7 @@ __global__ void __launch_bounds__(256) k_sp_assemble(SpDev d) {
     }
   }
   __syncthreads();
+  double node_cost = 0.0;  // thread 0: the node's coefficient-only terms at the build state (motion, own priors)
   if (d.mot) {  // BSplineMotionError::buildHessianImplementation (BSplineMotionError.hpp:96-160): H += Q, g -= Q c
     __shared__ double cn[3 * NB];  // coefficients of nodes i - 1, i, i + 1 (0 outside [0, K))
     for (int q = tid; q < 3 * NB; q += nth) {
@@ -808,10 +818,82 @@ __global__ void __launch_bounds__(256) k_sp_assemble(SpDev d) {
       }
 #pragma unroll
       for (int o = 32; o > 0; o >>= 1) nc += __shfl_xor(nc, o);
-      if (tid == 0) d.mcost[i] = nc;
+      if (tid == 0) node_cost = nc;
     }
     __syncthreads();
   }
+  if (d.npos) {
+    // ErrorTermEuclidean priors touching the node (ErrorTermEuclidean.cpp:50-66 over BSplinePositionExpressionNode,
+    // BSplineExpressions.cpp:132-149): per prior e, invR e and chi^2 staged in LDS (one thread per prior), then every
+    // output entry sums its priors in order: D / U += w_r w_c invR (position rows / columns), rhs -= w_r (invR e)
+    __shared__ double pe[TCH][4];    // invR e | chi^2
+    __shared__ double pwl[TCH][13];  // w [4] | invR [9]
+    __shared__ int pbl[TCH];
+    const int pa = d.node_pp[4 * i], pz = d.node_pp[4 * i + 1], oa = d.node_pp[4 * i + 2], oz = d.node_pp[4 * i + 3];
+    double pc = 0.0;
+    for (int c0 = pa; c0 < pz; c0 += TCH) {
+      const int nt = min(TCH, pz - c0);
+      __syncthreads();
+      if (tid < nt) {
+        const int k = c0 + tid, b = d.pb[k];
+        const double* w = d.pw + 4 * k;
+        const double* cf = d.state + d.off_coef + 6 * b;
+        double e[3];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+          double v = 0.0;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v += w[j] * cf[6 * j + a];
+          e[a] = v - d.pp[3 * k + a];
+        }
+        const double* W = d.pW + 9 * k;
+        double c2 = 0.0;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+          const double we = W[3 * a] * e[0] + W[3 * a + 1] * e[1] + W[3 * a + 2] * e[2];
+          pe[tid][a] = we;
+          c2 += e[a] * we;
+        }
+        pe[tid][3] = c2;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) pwl[tid][j] = w[j];
+#pragma unroll
+        for (int q = 0; q < 9; ++q) pwl[tid][4 + q] = W[q];
+        pbl[tid] = b;
+      }
+      __syncthreads();
+      for (int q = tid; q < nout; q += nth) {
+        double sacc = 0.0;
+        if (q < 2 * NB * NB) {
+          const int blk = q / (NB * NB), e = q % (NB * NB), r = e / NB, c = e % NB, a = r % 6, bb = c % 6;
+          if (a < 3 && bb < 3) {
+            const int kr = k0 + r / 6, kc = k0 + SB * blk + c / 6;
+            for (int t = 0; t < nt; ++t) {
+              const int jr = kr - pbl[t], jc = kc - pbl[t];
+              if (jr < 0 || jr > 3 || jc < 0 || jc > 3) continue;
+              sacc += pwl[t][jr] * pwl[t][jc] * pwl[t][4 + 3 * a + bb];
+            }
+          }
+        } else {
+          const int e = q - 2 * NB * NB, r = e / m, col = e % m, a = r % 6;
+          if (col == C && a < 3) {
+            const int kr = k0 + r / 6;
+            for (int t = 0; t < nt; ++t) {
+              const int jr = kr - pbl[t];
+              if (jr < 0 || jr > 3) continue;
+              sacc -= pwl[t][jr] * pe[t][a];
+            }
+          }
+        }
+        out[q] += sacc;
+      }
+      if (tid == 0)  // the node's own priors' chi^2, in order
+        for (int t = max(oa, c0) - c0; t < min(oz, c0 + nt) - c0; ++t) pc += pe[t][3];
+    }
+    node_cost += pc;
+    __syncthreads();
+  }
+  if (d.cq && tid == 0) d.mcost[i] = node_cost;
   // padded rows (coefficients >= K): identity diagonal, no coupling
   for (int q = tid; q < nout; q += nth) {
     double v = out[q];
@@ -1977,7 +2059,8 @@ __global__ void __launch_bounds__(256) k_sp_cost_imu(SpDev d) {
 }
 
 // BSplineMotionError::evaluateErrorImplementation (BSplineMotionError.hpp:62-78): c^T Q c of the current state,
-// one node per lane (c_i^T QD_i c_i + 2 c_i^T QU_i c_(i+1)) -> cpart[nblk_f + nblk_ci + block]
+// one node per lane (c_i^T QD_i c_i + 2 c_i^T QU_i c_(i+1), + the node's own priors' chi^2) -> cpart[nblk_f + nblk_ci +
+// block]
 __global__ void __launch_bounds__(64) k_sp_cost_motion(SpDev d) {
   const int i = blockIdx.x * 64 + threadIdx.x;
   double s = 0.0;
@@ -1989,17 +2072,41 @@ __global__ void __launch_bounds__(64) k_sp_cost_motion(SpDev d) {
       ci[q] = k < d.K ? d.state[d.off_coef + 6 * k + q % 6] : 0.0;
       cj[q] = k1 < d.K ? d.state[d.off_coef + 6 * k1 + q % 6] : 0.0;
     }
-    const double* QDi = d.QD + (size_t)i * NB * NB;
-    const double* QUi = d.QU + (size_t)i * NB * NB;
+    if (d.mot) {
+      const double* QDi = d.QD + (size_t)i * NB * NB;
+      const double* QUi = d.QU + (size_t)i * NB * NB;
 #pragma unroll
-    for (int r = 0; r < NB; ++r) {
-      double a = 0.0, w = 0.0;
+      for (int r = 0; r < NB; ++r) {
+        double a = 0.0, w = 0.0;
 #pragma unroll
-      for (int c = 0; c < NB; ++c) {
-        a += QDi[r * NB + c] * ci[c];
-        w += QUi[r * NB + c] * cj[c];
+        for (int c = 0; c < NB; ++c) {
+          a += QDi[r * NB + c] * ci[c];
+          w += QUi[r * NB + c] * cj[c];
+        }
+        s += ci[r] * (a + 2.0 * w);
       }
-      s += ci[r] * (a + 2.0 * w);
+    }
+    if (d.npos) {  // the node's own ErrorTermEuclidean priors (first coefficient in 3i .. 3i+2), as k_sp_assemble
+      double pc = 0.0;
+      for (int k = d.node_pp[4 * i + 2]; k < d.node_pp[4 * i + 3]; ++k) {
+        const int b = d.pb[k];
+        const double* w = d.pw + 4 * k;
+        const double* cf = d.state + d.off_coef + 6 * b;
+        double e[3];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+          double v = 0.0;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v += w[j] * cf[6 * j + a];
+          e[a] = v - d.pp[3 * k + a];
+        }
+        const double* W = d.pW + 9 * k;
+        double c2 = 0.0;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) c2 += e[a] * (W[3 * a] * e[0] + W[3 * a + 1] * e[1] + W[3 * a + 2] * e[2]);
+        pc += c2;
+      }
+      s += pc;
     }
   }
 #pragma unroll
@@ -2028,7 +2135,7 @@ __global__ void __launch_bounds__(64) k_sp_cost_reduce(SpDev d, int with_dx) {
   const int tid = threadIdx.x;
   double s = 0.0, mx = 0.0;
 #pragma unroll 8
-  for (int q = tid; q < d.nblk_f + d.nblk_ci + (d.mot ? d.nblk_q : 0); q += 64) s += d.cpart[q];
+  for (int q = tid; q < d.nblk_f + d.nblk_ci + (d.cq ? d.nblk_q : 0); q += 64) s += d.cpart[q];
   if (with_dx) {
 #pragma unroll 8
     for (int q = tid; q < d.n; q += 64) mx = fmax(mx, d.dmax[q]);
@@ -2233,7 +2340,7 @@ int launch_build(kb_sp_handle* h) {
   hipLaunchKernelGGL(k_sp_imu_cc, dim3(d.nblk_ic), dim3(64), 0, h->stream, d);  // sets lambda^2 = 0 in a GN pass
   KSP_HIP(hipLaunchKernel((const void*)k_sp_assemble, dim3(d.n), dim3(256), args, h->lds_asm, h->stream));
   hipLaunchKernelGGL(k_sp_reduce_cc, dim3((d.Wc + 63) / 64), dim3(64 * RW), 0, h->stream, d);
-  if (d.mot) hipLaunchKernelGGL(k_sp_mcost_build, dim3(1), dim3(256), 0, h->stream, d);
+  if (d.cq) hipLaunchKernelGGL(k_sp_mcost_build, dim3(1), dim3(256), 0, h->stream, d);
   return 0;
 }
 
@@ -2282,7 +2389,7 @@ int launch_cost(kb_sp_handle* h, int with_dx) {
   void* args[] = {&d};
   KSP_HIP(hipLaunchKernel(h->fn_cost, dim3(d.nblk_f), dim3(64 * h->N), args, 0, h->stream));
   hipLaunchKernelGGL(k_sp_cost_imu, dim3(d.nblk_ci), dim3(256), 0, h->stream, d);
-  if (d.mot) hipLaunchKernelGGL(k_sp_cost_motion, dim3(d.nblk_q), dim3(64), 0, h->stream, d);
+  if (d.cq) hipLaunchKernelGGL(k_sp_cost_motion, dim3(d.nblk_q), dim3(64), 0, h->stream, d);
   hipLaunchKernelGGL(k_sp_cost_reduce, dim3(1), dim3(64), 0, h->stream, d, with_dx);
   return 0;
 }
@@ -2710,6 +2817,7 @@ int kb_sp_set_motion_error(kb_sp_handle* h, const double* W, int32_t derivative_
   }
   if (!W) {
     h->d.mot = 0;
+    h->d.cq = h->d.npos > 0;
     return 0;
   }
   int m = derivative_order;
@@ -2753,6 +2861,87 @@ int kb_sp_set_motion_error(kb_sp_handle* h, const double* W, int32_t derivative_
                          h->stream));
   KSP_HIP(hipStreamSynchronize(h->stream));
   d.mot = 1;
+  d.cq = 1;
+  return 0;
+}
+
+int kb_sp_set_position_priors(kb_sp_handle* h, int32_t n, const double* times, const double* priors,
+                              const double* N) {
+  if (!h) return fail("kb_sp_set_position_priors: null handle");
+  if (n < 0 || (n > 0 && (!times || !priors || !N))) return fail("kb_sp_set_position_priors: bad arguments");
+  KSP_HIP(hipSetDevice(h->device));
+  if (h->gn_graph) {  // captured passes hold the old SpDev
+    hipGraphExecDestroy(h->gn_graph);
+    h->gn_graph = nullptr;
+  }
+  SpDev& d = h->d;
+  if (n == 0) {
+    d.npos = 0;
+    d.cq = d.mot;
+    return 0;
+  }
+  // per prior: first coefficient and value weights (BSpline::evalDAndJacobian(t, 0)), invR = N^-1 (ErrorTermEuclidean's
+  // first constructor, ErrorTermEuclidean.cpp:10-23: setInvR(N.inverse())); sorted by first coefficient, then time
+  std::vector<int> ord(n), b(n);
+  std::vector<double> w(4 * (size_t)n), W(9 * (size_t)n);
+  for (int k = 0; k < n; ++k) {
+    b[k] = basis_weights(h->knots, ORD, times[k], 0, &w[4 * (size_t)k]);
+    if (b[k] < 0) return fail("kb_sp_set_position_priors: prior time outside the spline interval");
+    const double* M = N + 9 * (size_t)k;
+    for (int r = 0; r < 3; ++r)
+      for (int c = 0; c < r; ++c)
+        if (std::fabs(M[3 * r + c] - M[3 * c + r]) > 1e-12 * (std::fabs(M[3 * r + c]) + std::fabs(M[3 * c + r])))
+          return fail("kb_sp_set_position_priors: N must be symmetric");
+    const double c00 = M[4] * M[8] - M[5] * M[7], c01 = M[5] * M[6] - M[3] * M[8], c02 = M[3] * M[7] - M[4] * M[6];
+    const double det = M[0] * c00 + M[1] * c01 + M[2] * c02;
+    if (!(det > 0.0) || !(M[0] > 0.0)) return fail("kb_sp_set_position_priors: N must be positive definite");
+    double* I = &W[9 * (size_t)k];  // adjugate / det
+    I[0] = c00 / det;
+    I[1] = (M[2] * M[7] - M[1] * M[8]) / det;
+    I[2] = (M[1] * M[5] - M[2] * M[4]) / det;
+    I[3] = c01 / det;
+    I[4] = (M[0] * M[8] - M[2] * M[6]) / det;
+    I[5] = (M[2] * M[3] - M[0] * M[5]) / det;
+    I[6] = c02 / det;
+    I[7] = (M[1] * M[6] - M[0] * M[7]) / det;
+    I[8] = (M[0] * M[4] - M[1] * M[3]) / det;
+    ord[k] = k;
+  }
+  std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) { return b[x] < b[y]; });
+  std::vector<int> pb(n);
+  std::vector<double> pw(4 * (size_t)n), pp(3 * (size_t)n), pW(9 * (size_t)n);
+  for (int q = 0; q < n; ++q) {
+    const int k = ord[q];
+    pb[q] = b[k];
+    for (int j = 0; j < 4; ++j) pw[4 * (size_t)q + j] = w[4 * (size_t)k + j];
+    for (int a = 0; a < 3; ++a) pp[3 * (size_t)q + a] = priors[3 * (size_t)k + a];
+    for (int e = 0; e < 9; ++e) pW[9 * (size_t)q + e] = W[9 * (size_t)k + e];
+  }
+  std::vector<int> npp(4 * (size_t)h->n);
+  for (int i = 0; i < h->n; ++i) {
+    npp[4 * i] = (int)(std::lower_bound(pb.begin(), pb.end(), SB * i - 3) - pb.begin());
+    npp[4 * i + 1] = (int)(std::upper_bound(pb.begin(), pb.end(), SB * i + 2) - pb.begin());
+    npp[4 * i + 2] = (int)(std::lower_bound(pb.begin(), pb.end(), SB * i) - pb.begin());
+    npp[4 * i + 3] = npp[4 * i + 1];
+  }
+  int *dpb = nullptr, *dnp = nullptr;
+  double *dpw = nullptr, *dpp = nullptr, *dpW = nullptr;
+  if (h->alloc(&dpb, n) || h->alloc(&dpw, 4 * (size_t)n) || h->alloc(&dpp, 3 * (size_t)n) ||
+      h->alloc(&dpW, 9 * (size_t)n) || h->alloc(&dnp, npp.size()))
+    return -1;
+  KSP_HIP(hipMemcpyAsync(dpb, pb.data(), sizeof(int) * n, hipMemcpyHostToDevice, h->stream));
+  KSP_HIP(hipMemcpyAsync(dpw, pw.data(), sizeof(double) * pw.size(), hipMemcpyHostToDevice, h->stream));
+  KSP_HIP(hipMemcpyAsync(dpp, pp.data(), sizeof(double) * pp.size(), hipMemcpyHostToDevice, h->stream));
+  KSP_HIP(hipMemcpyAsync(dpW, pW.data(), sizeof(double) * pW.size(), hipMemcpyHostToDevice, h->stream));
+  KSP_HIP(hipMemcpyAsync(dnp, npp.data(), sizeof(int) * npp.size(), hipMemcpyHostToDevice, h->stream));
+  KSP_HIP(hipStreamSynchronize(h->stream));
+  d.pb = dpb;
+  d.pw = dpw;
+  d.pp = dpp;
+  d.pW = dpW;
+  d.node_pp = dnp;
+  d.npos = n;
+  d.cq = 1;
   return 0;
 }
 
@@ -3075,7 +3264,7 @@ int kb_sp_kernel_stats(kb_sp_handle* h, int32_t n, double* ms_out6, double* fram
     hipLaunchKernelGGL(k_sp_imu_cc, dim3(d.nblk_ic), dim3(64), 0, h->stream, d);
     KSP_HIP(hipLaunchKernel((const void*)k_sp_assemble, dim3(d.n), dim3(256), args, h->lds_asm, h->stream));
     hipLaunchKernelGGL(k_sp_reduce_cc, dim3((d.Wc + 63) / 64), dim3(64 * RW), 0, h->stream, d);
-    if (d.mot) hipLaunchKernelGGL(k_sp_mcost_build, dim3(1), dim3(256), 0, h->stream, d);
+    if (d.cq) hipLaunchKernelGGL(k_sp_mcost_build, dim3(1), dim3(256), 0, h->stream, d);
     KSP_HIP(hipEventRecord(ev[2], h->stream));
     launch_reduction(h);
     KSP_HIP(hipEventRecord(ev[3], h->stream));

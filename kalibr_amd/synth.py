@@ -692,3 +692,28 @@ def make_spline_config(n_frames=None, seed_offset=0, **kw):
     """configs[4]: '2-cam + IMU continuous-time B-spline (aslam_splines) calibration, 1200 frames'."""
     return make_spline_problem([PINHOLE_RADTAN] * 2, n_frames or 1200, seed=20261015 + 5 + seed_offset,
                                name="2-cam + IMU continuous-time B-spline calibration, 1200 frames", **kw)
+
+
+def make_position_priors(p, n, sigma=0.002, seed=7, rate=None, anisotropic=True):
+    """ErrorTermEuclidean priors on the spline position (e.g. a motion-capture or GNSS track): n times spread over
+    the spline's valid range (or every 1/rate s), priors = the true p(t) plus noise, covariances N (sigma^2 I, or a
+    random SPD of that scale).  Returns (times [n], priors [n][3], N [n][3][3])."""
+    rng = np.random.default_rng(seed)
+    o, kn = p.order, p.knots
+    t0, t1 = kn[o - 1], kn[kn.size - o]
+    if rate:
+        t = t0 + np.arange(int(np.floor((t1 - t0) * rate + 1e-9)) + 1) / rate
+    else:
+        t = np.sort(rng.uniform(t0, t1, n))
+    c = p.state_truth[p.off_coeff:].reshape(-1, 6)
+    pr = np.array([spline_eval(o, kn, c, tk, 0)[:3] for tk in t])
+    N = np.zeros((t.size, 3, 3))
+    for k in range(t.size):
+        if anisotropic:
+            A = rng.normal(size=(3, 3))
+            Q, _ = np.linalg.qr(A)
+            N[k] = sigma ** 2 * (Q @ np.diag(rng.uniform(0.5, 2.0, 3)) @ Q.T)
+        else:
+            N[k] = sigma ** 2 * np.eye(3)
+        pr[k] += np.linalg.cholesky(N[k]) @ rng.normal(size=3)
+    return t, pr, N

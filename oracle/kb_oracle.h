@@ -210,6 +210,13 @@ typedef struct {
    * Q = curveQuadraticIntegralSparse(W, order) (BSpline.cpp:1585-1622); NULL = no motion term */
   const double* motion_W; /* [6][6] symmetric */
   int motion_order;       /* errorTermOrder (BSplineMotionError default 2: acceleration) */
+  /* optional ErrorTermEuclidean priors on the spline position (ErrorTermEuclidean.cpp:9-66 over
+   * BSplinePoseDesignVariable::position(t_k), BSplinePoseDesignVariable.cpp:91-103 / BSplineExpressions.cpp:132-149):
+   * e_k = p(t_k) - prior_k, chi^2_k = e_k^T invR_k e_k, J = w_j(t_k) [I_3 | 0] on coefficient bidx + j */
+  int n_pos;
+  const double* pos_time;  /* [n_pos] */
+  const double* pos_prior; /* [n_pos][3] */
+  const double* pos_invR;  /* [n_pos][3][3] symmetric (the reference's setInvR(N^-1)) */
 } kbo_sp_problem;
 
 typedef struct {
@@ -236,6 +243,10 @@ int kbo_sp_cam_cols(const kbo_sp_problem* P);
 int kbo_sp_total_cols(const kbo_sp_problem* P);
 double kbo_sp_reproj_dense(const kbo_sp_problem* P, const double* st, int v, int k, double e[2], double* J, int ncols);
 double kbo_sp_imu_dense(const kbo_sp_problem* P, const double* st, int m, double e[6], double* J, int ncols);
+/* ErrorTermEuclidean prior k: whitening-free residual e = p(t_k) - prior_k and its dense Jacobian rows [3][ncols];
+ * returns e^T invR e (0 and e = 0 outside the spline's time range) */
+double kbo_sp_pos_dense(const kbo_sp_problem* P, const double* st, int k, double e[3], double* J, int ncols);
+double kbo_sp_pos_cost(const kbo_sp_problem* P, const double* st);
 double kbo_sp_eval_cost(const kbo_sp_problem* P, const double* st, int nthreads);
 int kbo_sp_system_alloc(const kbo_sp_problem* P, kbo_sp_system* A);
 void kbo_sp_system_free(kbo_sp_system* A);

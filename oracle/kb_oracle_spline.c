@@ -619,6 +619,67 @@ static double sp_motion_terms(const kbo_sp_problem* P, const double* st, double*
 
 double kbo_sp_motion_cost(const kbo_sp_problem* P, const double* st) { return sp_motion_terms(P, st, NULL, NULL); }
 
+/* ------------------------------------------------------------------ ErrorTermEuclidean priors on p(t) */
+/* evaluateErrorImplementation (ErrorTermEuclidean.cpp:50-57): e = t.toEuclidean() - prior, chi^2 = e^T invR e;
+ * t = BSplinePositionExpressionNode: p(t) = eval(t).head<3>() (BSplineExpressions.cpp:132-136), its Jacobian the
+ * first three rows of evalDAndJacobian(t, 0) per coefficient DV (:138-149): w_j(t) on the coefficient's p columns.
+ * Returns chi^2; *bidx = the first coefficient (-1 outside the time range: the term is skipped). */
+static double sp_pos(const kbo_sp_problem* P, const double* st, int k, double e[3], double* w, int* bidx) {
+  double v[6];
+  const int b = sp_eval(P, st, P->pos_time[k], 0, v, w);
+  *bidx = b;
+  if (b < 0) {
+    e[0] = e[1] = e[2] = 0.0;
+    return 0.0;
+  }
+  for (int a = 0; a < 3; ++a) e[a] = v[a] - P->pos_prior[3 * k + a];
+  const double* W = P->pos_invR + 9 * k;
+  double c = 0.0;
+  for (int a = 0; a < 3; ++a)
+    for (int bb = 0; bb < 3; ++bb) c += e[a] * W[3 * a + bb] * e[bb];
+  return c;
+}
+
+double kbo_sp_pos_dense(const kbo_sp_problem* P, const double* st, int k, double e[3], double* J, int ncols) {
+  double w[8];
+  int b;
+  const double c = sp_pos(P, st, k, e, w, &b);
+  memset(J, 0, sizeof(double) * 3 * (size_t)ncols);
+  if (b < 0) return 0.0;
+  const int c0 = kbo_sp_cam_cols(P);
+  for (int j = 0; j < P->order; ++j)
+    for (int a = 0; a < 3; ++a) J[(size_t)a * ncols + c0 + 6 * (b + j) + a] = w[j];
+  return c;
+}
+
+/* the priors' share of the normal equations (ErrorTermFs: H += J^T invR J, rhs -= J^T invR e) and of the cost */
+static double sp_pos_terms(const kbo_sp_problem* P, const double* st, double* Hband, double* gs) {
+  const int o = P->order;
+  double cost = 0.0;
+  for (int k = 0; k < P->n_pos; ++k) {
+    double e[3], w[8];
+    int b;
+    cost += sp_pos(P, st, k, e, w, &b);
+    if (b < 0) continue;
+    const double* W = P->pos_invR + 9 * k;
+    double We[3];
+    for (int a = 0; a < 3; ++a) We[a] = W[3 * a] * e[0] + W[3 * a + 1] * e[1] + W[3 * a + 2] * e[2];
+    for (int i = 0; i < o; ++i) {
+      if (gs)
+        for (int a = 0; a < 3; ++a) gs[6 * (b + i) + a] -= w[i] * We[a];
+      if (Hband)
+        for (int j = i; j < o; ++j) {
+          double* Hb = Hband + ((size_t)(b + i) * o + (j - i)) * 36;
+          for (int a = 0; a < 3; ++a)
+            for (int c = 0; c < 3; ++c) Hb[6 * a + c] += w[i] * w[j] * W[3 * a + c];
+        }
+    }
+  }
+  return cost;
+}
+
+double kbo_sp_pos_cost(const kbo_sp_problem* P, const double* st) { return sp_pos_terms(P, st, NULL, NULL); }
+
 double kbo_sp_eval_cost(const kbo_sp_problem* P, const double* st, int nthreads) {
   if (nthreads < 1) nthreads = 1;
   if (nthreads > 256) nthreads = 256;
@@ -628,7 +689,8 @@ double kbo_sp_eval_cost(const kbo_sp_problem* P, const double* st, int nthreads)
   sp_parallel(nthreads, sp_cost_job, &c);
   double s = 0.0;
   for (int t = 0; t < nthreads; ++t) s += c.part[t];
-  return s + sp_motion_terms(P, st, NULL, NULL);  /* evaluateErrorImplementation: c^T Q c */
+  return s + sp_motion_terms(P, st, NULL, NULL)  /* evaluateErrorImplementation: c^T Q c */
+           + sp_pos_terms(P, st, NULL, NULL);    /* ErrorTermEuclidean priors */
 }
 
 /* ------------------------------------------------------------------ normal equations */
@@ -768,6 +830,7 @@ void kbo_sp_build(const kbo_sp_problem* P, const double* st, int nthreads, kbo_s
   for (int a = 0; a < C; ++a)
     for (int b = 0; b < a; ++b) A->Hcc[a * C + b] = A->Hcc[b * C + a];
   A->cost += sp_motion_terms(P, st, A->Hband, A->gs);  /* BSplineMotionError::buildHessianImplementation */
+  A->cost += sp_pos_terms(P, st, A->Hband, A->gs);     /* ErrorTermEuclidean priors */
 }
 
 /* ------------------------------------------------------------------ solve */

@@ -331,7 +331,8 @@ class _SpProblem(C.Structure):
                 ("n_corners", C.c_int), ("view_frame", ip), ("view_cam", ip), ("view_offset", ip),
                 ("corner_id", ip), ("y", dp), ("n_imu", C.c_int), ("imu_time", dp), ("imu_gyro", dp),
                 ("imu_acc", dp), ("sigma_gyro", C.c_double), ("sigma_acc", C.c_double), ("motion_W", dp),
-                ("motion_order", C.c_int)]
+                ("motion_order", C.c_int), ("n_pos", C.c_int), ("pos_time", dp), ("pos_prior", dp),
+                ("pos_invR", dp)]
 
 
 class _SpSystem(C.Structure):
@@ -343,7 +344,7 @@ def _sp_lib():
     L = lib()
     if not getattr(L, "_sp_ready", False):
         for f in ("kbo_sp_eval_cost", "kbo_sp_reproj_dense", "kbo_sp_imu_dense", "kbo_sp_apply_update",
-                  "kbo_sp_time_gn", "kbo_sp_motion_cost"):
+                  "kbo_sp_time_gn", "kbo_sp_motion_cost", "kbo_sp_pos_dense", "kbo_sp_pos_cost"):
             getattr(L, f).restype = C.c_double
         L.kbo_bspline_weights.argtypes = [C.c_int, dp, C.c_int, C.c_double, C.c_int, dp]
         L.kbo_bspline_basis.argtypes = [C.c_int, dp, C.c_int, dp]
@@ -380,8 +381,10 @@ def rv_dSv(a, v):
 class SplineOracle:
     """configs[4] restatement over one SplineProblem (kalibr_amd/synth.py)."""
 
-    def __init__(self, prob, motion_W=None, motion_order=2):
-        """motion_W (6 x 6, optional): add a BSplineMotionError of that weight and derivative order."""
+    def __init__(self, prob, motion_W=None, motion_order=2, position_priors=None):
+        """motion_W (6 x 6, optional): add a BSplineMotionError of that weight and derivative order.
+        position_priors (optional): (times [n], priors [n][3], N [n][3][3] covariances) -- ErrorTermEuclidean terms
+        on the spline position p(t_k) with invR = N^-1, as the reference's first constructor sets it."""
         self.prob = prob
         k = self._keep = dict(
             knots=np.ascontiguousarray(prob.knots, dtype=np.float64),
@@ -404,6 +407,14 @@ class SplineOracle:
         if motion_W is not None:
             k["motion_W"] = np.ascontiguousarray(motion_W, dtype=np.float64).reshape(6, 6)
             self.P.motion_W = _d(k["motion_W"])
+        self.P.n_pos = 0
+        if position_priors is not None:
+            t, pr, N = position_priors
+            k["pos_time"] = np.ascontiguousarray(t, dtype=np.float64).reshape(-1)
+            k["pos_prior"] = np.ascontiguousarray(pr, dtype=np.float64).reshape(-1, 3)
+            k["pos_invR"] = np.ascontiguousarray(np.linalg.inv(np.asarray(N, dtype=np.float64).reshape(-1, 3, 3)))
+            self.P.n_pos = k["pos_time"].size
+            self.P.pos_time, self.P.pos_prior, self.P.pos_invR = _d(k["pos_time"]), _d(k["pos_prior"]), _d(k["pos_invR"])
         L = _sp_lib()
         self.C = L.kbo_sp_cam_cols(C.byref(self.P))
         self.K = L.kbo_sp_num_coeffs(C.byref(self.P))
@@ -468,6 +479,17 @@ class SplineOracle:
         """q[k][d] = int b_k^(m) b_(k+d)^(m) dt (None without a motion term)"""
         q = np.zeros((self.K, self.prob.order))
         return q if _sp_lib().kbo_sp_motion_band(C.byref(self.P), _d(q)) else None
+
+    def pos_dense(self, state, k):
+        """ErrorTermEuclidean prior k: e = p(t_k) - prior_k (unwhitened) and its Jacobian rows; returns (chi2, e, J)"""
+        st = np.ascontiguousarray(state, dtype=np.float64)
+        e, J = np.zeros(3), np.zeros((3, self.ncols))
+        c = _sp_lib().kbo_sp_pos_dense(C.byref(self.P), _d(st), k, _d(e), _d(J), self.ncols)
+        return c, e, J
+
+    def pos_cost(self, state):
+        st = np.ascontiguousarray(state, dtype=np.float64)
+        return _sp_lib().kbo_sp_pos_cost(C.byref(self.P), _d(st))
 
     def motion_cost(self, state):
         st = np.ascontiguousarray(state, dtype=np.float64)

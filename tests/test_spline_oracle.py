@@ -265,3 +265,57 @@ def test_motion_error_hessian_and_rhs(small):
         ok, dx = o.solve(s1, lam)
         ok2, dx2 = o.solve(s1, lam, dense=True)
         assert ok and ok2 and np.abs(dx - dx2).max() <= 1e-8 * np.abs(dx2).max()
+
+
+def test_position_prior_jacobian_and_cost(small):
+    """ErrorTermEuclidean (ErrorTermEuclidean.cpp:50-66) on BSplinePoseDesignVariable::position(t_k): e = p(t) -
+    prior, chi^2 = e^T N^-1 e, J = the first three rows of evalDAndJacobian(t, 0) -- checked against central
+    differences under the DV update rules (the ErrorTermTestHarness pattern), and chi^2 against a numpy restatement."""
+    p, _ = small
+    pri = synth.make_position_priors(p, 12, seed=11)
+    o = O.SplineOracle(p, position_priors=pri)
+    st = p.state_init
+    c = st[p.off_coeff:].reshape(-1, 6)
+    total = 0.0
+    for k in range(pri[0].size):
+        chi2, e, J = o.pos_dense(st, k)
+        e_np = synth.spline_eval(p.order, p.knots, c, pri[0][k], 0)[:3] - pri[1][k]
+        assert np.allclose(e, e_np, rtol=0, atol=1e-13)
+        assert abs(chi2 - e_np @ np.linalg.solve(pri[2][k], e_np)) <= 1e-10 * chi2
+        total += chi2
+        Jn = _fd_jac(o, lambda s: o.pos_dense(s, k)[1:], st)
+        assert np.abs(J - Jn).max() < 1e-7, k
+        assert not J[:, :o.C].any()  # only the spline coefficients' p columns
+    assert abs(o.pos_cost(st) - total) <= 1e-12 * total
+
+
+def test_position_prior_normal_equations(small):
+    """The priors' share of the system: H += J^T N^-1 J, rhs -= J^T N^-1 e, cost += chi^2 (ErrorTermFs), from the
+    dense term rows; the banded solve agrees with the dense one."""
+    p, _ = small
+    pri = synth.make_position_priors(p, 20, seed=5)
+    o0, o = O.SplineOracle(p), O.SplineOracle(p, position_priors=pri)
+    st = p.state_init
+    s0, s1 = o0.system(st), o.system(st)
+    Cc, K = o.C, o.K
+    Hp = np.zeros((o.ncols, o.ncols))
+    gp = np.zeros(o.ncols)
+    cp = 0.0
+    for k in range(pri[0].size):
+        chi2, e, J = o.pos_dense(st, k)
+        Wk = np.linalg.inv(pri[2][k])
+        Hp += J.T @ Wk @ J
+        gp -= J.T @ Wk @ e
+        cp += chi2
+    assert abs((s1["cost"] - s0["cost"]) - cp) <= 1e-12 * s1["cost"]
+    assert np.abs(s1["Hcc"] - s0["Hcc"]).max() == 0.0 and np.abs(s1["Hsc"] - s0["Hsc"]).max() == 0.0
+    for k in range(K):
+        for d in range(p.order):
+            if k + d < K:
+                blk = Hp[Cc + 6 * k: Cc + 6 * k + 6, Cc + 6 * (k + d): Cc + 6 * (k + d) + 6]
+                assert np.abs(s1["Hband"][k, d] - s0["Hband"][k, d] - blk).max() <= 1e-9 * np.abs(Hp).max()
+    assert np.abs(s1["gs"] - s0["gs"] - gp[Cc:]).max() <= 1e-9 * max(1.0, np.abs(gp).max())
+    for lam in (0.0, 10.0):
+        ok, dx = o.solve(s1, lam)
+        ok2, dx2 = o.solve(s1, lam, dense=True)
+        assert ok and ok2 and np.abs(dx - dx2).max() <= 1e-8 * np.abs(dx2).max()
