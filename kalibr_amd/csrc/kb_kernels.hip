@@ -198,22 +198,25 @@ __device__ __forceinline__ double chain_entry(const double* R, const double* tq,
   return 0.0;
 }
 
-// chain_entry from wave-uniform registers (R, t_q, t_m) for a lane-dependent entry (a, b): the same products, picked by
-// selects instead of lane-dependent LDS reads in divergent branches.  s = (R_a x t_m)_b and u = (t_q x R_{:,b})_a are
-// chain_entry's two terms of the rotation block.
+// chain_entry from wave-uniform registers (R, t_q, t_m) for a lane-dependent entry (a, b): the same products, the
+// lane's row / column of R picked by 0/1 weights (exact: one weight is 1, the others 0).  s = (R_a x t_m)_b and
+// u = (t_q x R_{:,b})_a are chain_entry's two terms of the rotation block.  (Selects among R's entries here were
+// folded by the compiler into a run-time index into R, which put R in per-lane scratch.)
 __device__ __forceinline__ double chain_entry_reg(const double (&R)[9], const double (&tq)[3], const double* tm, int a,
                                                   int b) {
   const int ra = a < 3 ? a : a - 3, rb = b < 3 ? b : b - 3;
-  const double r0 = ra == 0 ? R[0] : ra == 1 ? R[3] : R[6];
-  const double r1 = ra == 0 ? R[1] : ra == 1 ? R[4] : R[7];
-  const double r2 = ra == 0 ? R[2] : ra == 1 ? R[5] : R[8];
-  const double c0 = rb == 0 ? R[0] : rb == 1 ? R[1] : R[2];
-  const double c1 = rb == 0 ? R[3] : rb == 1 ? R[4] : R[5];
-  const double c2 = rb == 0 ? R[6] : rb == 1 ? R[7] : R[8];
-  const double rab = rb == 0 ? r0 : rb == 1 ? r1 : r2;
+  const double ma0 = ra == 0 ? 1.0 : 0.0, ma1 = ra == 1 ? 1.0 : 0.0, ma2 = ra == 2 ? 1.0 : 0.0;
+  const double mb0 = rb == 0 ? 1.0 : 0.0, mb1 = rb == 1 ? 1.0 : 0.0, mb2 = rb == 2 ? 1.0 : 0.0;
+  const double r0 = ma0 * R[0] + ma1 * R[3] + ma2 * R[6];
+  const double r1 = ma0 * R[1] + ma1 * R[4] + ma2 * R[7];
+  const double r2 = ma0 * R[2] + ma1 * R[5] + ma2 * R[8];
+  const double c0 = mb0 * R[0] + mb1 * R[1] + mb2 * R[2];
+  const double c1 = mb0 * R[3] + mb1 * R[4] + mb2 * R[5];
+  const double c2 = mb0 * R[6] + mb1 * R[7] + mb2 * R[8];
+  const double rab = mb0 * r0 + mb1 * r1 + mb2 * r2;
   const double s0 = r1 * tm[2] - r2 * tm[1], s1 = -r0 * tm[2] + r2 * tm[0], s2 = r0 * tm[1] - r1 * tm[0];
   const double u0 = -tq[2] * c1 + tq[1] * c2, u1 = tq[2] * c0 - tq[0] * c2, u2 = -tq[1] * c0 + tq[0] * c1;
-  const double sv = rb == 0 ? s0 : rb == 1 ? s1 : s2, uv = ra == 0 ? u0 : ra == 1 ? u1 : u2;
+  const double sv = mb0 * s0 + mb1 * s1 + mb2 * s2, uv = ma0 * u0 + ma1 * u1 + ma2 * u2;
   return (a < 3 && b < 3) ? sv + uv : (a < 3 || b < 3) ? -rab : 0.0;
 }
 
@@ -1302,17 +1305,46 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
     }
     KB_KEEP(bq);
   }
+  // the state-slot-indexed loads (camera chains and intrinsics of the build state, K_{i,j}, the block's first frame
+  // poses) from both ping-pong slots in this round too, picked once the control block is in: one dependent round trip
+  // less before the first corner pass
+  const int nK = 18 * N * (N - 1);
+  double csv[2] = {0.0, 0.0}, kv[2][2] = {{0.0, 0.0}, {0.0, 0.0}}, fps[2][7];
+  {
+    const int cm = min(tid / 22, N - 1), e = tid % 22;
+#pragma unroll
+    for (int sl = 0; sl < 2; ++sl)
+      csv[sl] = e < 12 ? cam_L(d, sl)[cm * 12 + e] : d.state[(size_t)sl * d.S + cm * KB_MAX_INTR + e - 12];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int q = min(tid + u * nth, nK - 1), ee = q % 36, ij = q / 36;
+      int i = 1;
+      while (i * (i + 1) / 2 <= ij) ++i;
+      const int j = ij - i * (i - 1) / 2;
+#pragma unroll
+      for (int sl = 0; sl < 2; ++sl) kv[sl][u] = nK > 0 ? cam_K(d, sl)[(size_t)(i * N + j) * 36 + ee] : 0.0;
+    }
+    const int fj = f0 + min(wave, G - 1);
+#pragma unroll
+    for (int sl = 0; sl < 2; ++sl)
+#pragma unroll
+      for (int q = 0; q < 7; ++q) fps[sl][q] = d.state[(size_t)sl * d.S + d.off_frame + 7 * fj + q];
+#pragma unroll
+    for (int sl = 0; sl < 2; ++sl) {
+      KB_KEEP(csv[sl]);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) KB_KEEP(kv[sl][u]);
+#pragma unroll
+      for (int q = 0; q < 7; ++q) KB_KEEP(fps[sl][q]);
+    }
+  }
   if (gate && (done || !dob)) return;
   const bool upd = gfu && cin.have_dx;
   const int bs = upd ? 1 - cur : cur;
   // ---- round 2: loads indexed by round 1
-  const double* s = d.state + (size_t)bs * d.S;
   const double* sf = d.state + (size_t)cur * d.S;
   double* snew = d.state + (size_t)(1 - cur) * d.S;
-  if (tid < N * 22) {
-    const int cm = tid / 22, e = tid % 22;
-    cst[cm][e] = e < 12 ? cam_L(d, bs)[cm * 12 + e] : s[cm * KB_MAX_INTR + e - 12];
-  }
+  if (tid < N * 22) cst[tid / 22][tid % 22] = bs ? csv[1] : csv[0];
   if (tid < 2 * N) ctab[tid / N][tid % N] = (tid < N) ? cam_arg(d.col_intr, tid) : cam_arg(d.col_base, tid - N);
   // expanded partials (GN fused, C > 64, KbDev::xexp): the block expands its own per-camera sums in the epilogue
   const bool xp = GNF && gfu && fuse && d.xexp;
@@ -1325,21 +1357,31 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
     cidn = d.cid[k];
     yn = d.y[k];
   }
-  const double* Kc = cam_K(d, bs);
-  for (int q = tid; q < 18 * N * (N - 1); q += nth) {
-    const int e = q % 36, ij = q / 36;
-    int i = 1;
-    while (i * (i + 1) / 2 <= ij) ++i;
-    const int j = ij - i * (i - 1) / 2;
-    Kl[q] = Kc[(size_t)(i * N + j) * 36 + e];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+    if (tid + u * nth < nK) Kl[tid + u * nth] = bs ? kv[1][u] : kv[0][u];
+  if (nK > 2 * nth) {  // rigs whose chain table outgrows two entries per thread
+    const double* Kc = cam_K(d, bs);
+    for (int q = tid + 2 * nth; q < nK; q += nth) {
+      const int e = q % 36, ij = q / 36;
+      int i = 1;
+      while (i * (i + 1) / 2 <= ij) ++i;
+      const int j = ij - i * (i - 1) / 2;
+      Kl[q] = Kc[(size_t)(i * N + j) * 36 + e];
+    }
   }
   KB_KEEPS(cidn);
   // the previous solve's frame steps: wave j moves frame f0 + j (then f0 + j + NW, ...) and stages its pose
   double wmax = 0.0;
   for (int j = wave; j < G; j += NW) {
     double fp[7];
+    if (j == wave) {
 #pragma unroll
-    for (int q = 0; q < 7; ++q) fp[q] = sf[d.off_frame + 7 * (f0 + j) + q];
+      for (int q = 0; q < 7; ++q) fp[q] = cur ? fps[1][q] : fps[0][q];
+    } else {
+#pragma unroll
+      for (int q = 0; q < 7; ++q) fp[q] = sf[d.off_frame + 7 * (f0 + j) + q];
+    }
     if (upd) {
       if (j == wave) {
         frame_step(d, f0 + j, true, lane, yr, dxv, bq, fp, snew, wmax);

@@ -1223,8 +1223,9 @@ __device__ __forceinline__ bool chol18_wave(double* A, double* id, int lane) {
 // L Z = W (lower L in LDS, inverse diagonal id), one thread per column of the [18][ws] LDS tile W, written to
 // dst (row stride ds)
 __device__ __forceinline__ void node_forward(const double* L, const double* id, const double* W, int ws, int ncol,
-                                             double* dst, int ds, int tid) {
-  for (int c = tid; c < ncol; c += blockDim.x) {
+                                             double* dst, int ds, int tid, int nth = -1) {
+  if (nth < 0) nth = blockDim.x;
+  for (int c = tid; c < ncol; c += nth) {
     double z[NB];
 #pragma unroll
     for (int row = 0; row < NB; ++row) {
@@ -1241,8 +1242,9 @@ __device__ __forceinline__ void node_forward(const double* L, const double* id, 
 // node_forward with the L loads kept per row (a compiler barrier between rows): the kernels that keep the next
 // node's operands in registers across the solve cannot hold all 171 hoisted L entries as well
 __device__ __forceinline__ void node_forward_lean(const double* L, const double* id, const double* W, int ws,
-                                                  int ncol, double* dst, int ds, int tid) {
-  for (int c = tid; c < ncol; c += blockDim.x) {
+                                                  int ncol, double* dst, int ds, int tid, int nth = -1) {
+  if (nth < 0) nth = blockDim.x;
+  for (int c = tid; c < ncol; c += nth) {
     double z[NB];
 #pragma unroll
     for (int row = 0; row < NB; ++row) {
@@ -1260,13 +1262,34 @@ __device__ __forceinline__ void node_forward_lean(const double* L, const double*
 // back substitution of one 18-row node with LDS-staged operands: x = L^-T T (T row stride ts), one thread per
 // RHS column, written to out (row stride m)
 __device__ __forceinline__ void node_backsolve(const double* L, const double* id, const double* T, int ts, int m,
-                                               double* out, int tid) {
-  for (int c = tid; c < m; c += blockDim.x) {
+                                               double* out, int tid, int nth = -1) {
+  if (nth < 0) nth = blockDim.x;
+  for (int c = tid; c < m; c += nth) {
     double z[NB];
 #pragma unroll
     for (int row = 0; row < NB; ++row) z[row] = T[row * ts + c];
 #pragma unroll
     for (int row = NB - 1; row >= 0; --row) {
+      double v = z[row];
+#pragma unroll
+      for (int k = row + 1; k < NB; ++k) v -= L[k * NB + row] * z[k];
+      z[row] = v * id[row];
+    }
+#pragma unroll
+    for (int row = 0; row < NB; ++row) out[row * m + c] = z[row];
+  }
+}
+
+// node_backsolve with the L loads kept per row (see node_forward_lean)
+__device__ __forceinline__ void node_backsolve_lean(const double* L, const double* id, const double* T, int ts, int m,
+                                                    double* out, int tid, int nth) {
+  for (int c = tid; c < m; c += nth) {
+    double z[NB];
+#pragma unroll
+    for (int row = 0; row < NB; ++row) z[row] = T[row * ts + c];
+#pragma unroll
+    for (int row = NB - 1; row >= 0; --row) {
+      asm volatile("" ::: "memory");
       double v = z[row];
 #pragma unroll
       for (int k = row + 1; k < NB; ++k) v -= L[k * NB + row] * z[k];
@@ -1320,14 +1343,14 @@ __global__ void __launch_bounds__(256) k_sp_elim1(SpDev d) {
 // fused level: node i (i % 2s == 0) absorbs its level-s eliminated neighbours i -+ s, then either is
 // eliminated at level 2s (Cholesky + Z_i with the couplings to i -+ 2s it computes itself), stays for the next
 // level, or -- node 0 once no partner is left -- solves X_0 = D_0^-1 R_0.
-__global__ void __launch_bounds__(256) k_sp_level(SpDev d, int s) {
-  __shared__ double L[NB * NB];
-  __shared__ double id[NB];
-  __shared__ double Ui[NB * NB];  // coupling (i - 2s) -> i
-  __shared__ double Uo[NB * NB];  // coupling i -> (i + 2s)
-  extern __shared__ __attribute__((aligned(16))) double sm[];  // Zl [18][wc] | Zr [18][wc] | W [18][wc]
-  const int i = 2 * s * blockIdx.x, tid = threadIdx.x, m = d.m, wc = 36 + m;
-  if (i >= d.n) return;
+// level_step: one node's share, by the `nth` threads of a node group (tid = the thread's index in the group); every
+// thread of the block calls it (act: the group has a node at this level), with the same three block barriers on every
+// path, so that k_sp_deep can run several groups (and several levels) in one block.  L, id, Ui, Uo and sm (Zl | Zr | W,
+// [18][wc] each) are the group's LDS.
+template <bool LEAN>  // LEAN: k_sp_deep's 1024-thread block (128 VGPRs): fewer loads in flight, per-row forward solve
+__device__ __forceinline__ void level_step(const SpDev& d, int s, int i, bool act, int tid, int nth, double* L,
+                                           double* id, double* Ui, double* Uo, double* sm) {
+  const int m = d.m, wc = 36 + m;
   const int jl = i - s, jr = i + s;
   const bool hl = jl >= 0, hr = jr < d.n;
   const bool elim = (i % (4 * s)) == 2 * s;  // eliminated at level 2s
@@ -1335,7 +1358,7 @@ __global__ void __launch_bounds__(256) k_sp_level(SpDev d, int s) {
   double* Zl = sm;
   double* Zr = Zl + NB * wc;
   double* W = Zr + NB * wc;  // [Ui^T | Uo | R']
-  {
+  if (act) {
     // Zl | Zr | D_i (into L) | R_i (into W's R columns) in one batch of loads; absent neighbours read node i's Z
     // slot (any valid address) and store zeros
     const double* Zsl = d.Z + (size_t)(hl ? jl : i) * NB * wc;
@@ -1344,8 +1367,8 @@ __global__ void __launch_bounds__(256) k_sp_level(SpDev d, int s) {
     const double* Ri = (s == 1 ? d.R0 : d.R) + (size_t)i * NB * m;
     const double lam2 = s == 1 ? d.sc[SC_LAM2] : 0.0;
     const int nz = NB * wc;
-    ksp_batched<15>(
-        2 * nz + NB * NB + NB * m, tid, blockDim.x,
+    ksp_batched<LEAN ? 6 : 15>(
+        2 * nz + NB * NB + NB * m, tid, nth,
         [&](int q) {
           return q < nz ? Zsl[q] : q < 2 * nz ? Zsr[q - nz] : q < 2 * nz + NB * NB ? Di[q - 2 * nz] : Ri[q - 2 * nz - NB * NB];
         },
@@ -1364,60 +1387,81 @@ __global__ void __launch_bounds__(256) k_sp_level(SpDev d, int s) {
   }
   __syncthreads();
   KSP_STOP(1);
-  for (int q = tid; q < 3 * NB * NB; q += blockDim.x) {
-    const int part = q / (NB * NB), e = q % (NB * NB), a = e / NB, b = e % NB;
-    double acc = 0.0;
-    if (part == 0) {  // D' = D - Zl_U^T Zl_U - Zr_Uin^T Zr_Uin
+  if (act) {
+    for (int q = tid; q < 3 * NB * NB; q += nth) {
+      const int part = q / (NB * NB), e = q % (NB * NB), a = e / NB, b = e % NB;
+      double acc = 0.0;
+      if (part == 0) {  // D' = D - Zl_U^T Zl_U - Zr_Uin^T Zr_Uin
 #pragma unroll
-      for (int k = 0; k < NB; ++k) acc += Zl[k * wc + NB + a] * Zl[k * wc + NB + b] + Zr[k * wc + a] * Zr[k * wc + b];
-      L[e] -= acc;
-    } else if (part == 1) {  // Uo = -Zr_Uin^T Zr_U
+        for (int k = 0; k < NB; ++k) acc += Zl[k * wc + NB + a] * Zl[k * wc + NB + b] + Zr[k * wc + a] * Zr[k * wc + b];
+        L[e] -= acc;
+      } else if (part == 1) {  // Uo = -Zr_Uin^T Zr_U
 #pragma unroll
-      for (int k = 0; k < NB; ++k) acc += Zr[k * wc + a] * Zr[k * wc + NB + b];
-      Uo[e] = -acc;
-    } else {  // Ui = -Zl_Uin^T Zl_U  (rows i - 2s, cols i)
+        for (int k = 0; k < NB; ++k) acc += Zr[k * wc + a] * Zr[k * wc + NB + b];
+        Uo[e] = -acc;
+      } else {  // Ui = -Zl_Uin^T Zl_U  (rows i - 2s, cols i)
 #pragma unroll
-      for (int k = 0; k < NB; ++k) acc += Zl[k * wc + a] * Zl[k * wc + NB + b];
-      Ui[e] = -acc;
+        for (int k = 0; k < NB; ++k) acc += Zl[k * wc + a] * Zl[k * wc + NB + b];
+        Ui[e] = -acc;
+      }
     }
-  }
-  for (int q = tid; q < NB * m; q += blockDim.x) {  // R' = R - Zl_U^T Zl_R - Zr_Uin^T Zr_R
-    const int a = q / m, c = q % m;
-    double acc = 0.0;
+    for (int q = tid; q < NB * m; q += nth) {  // R' = R - Zl_U^T Zl_R - Zr_Uin^T Zr_R
+      const int a = q / m, c = q % m;
+      double acc = 0.0;
 #pragma unroll
-    for (int k = 0; k < NB; ++k) acc += Zl[k * wc + NB + a] * Zl[k * wc + 2 * NB + c] + Zr[k * wc + a] * Zr[k * wc + 2 * NB + c];
-    W[a * wc + 2 * NB + c] -= acc;
+      for (int k = 0; k < NB; ++k) acc += Zl[k * wc + NB + a] * Zl[k * wc + 2 * NB + c] + Zr[k * wc + a] * Zr[k * wc + 2 * NB + c];
+      W[a * wc + 2 * NB + c] -= acc;
+    }
   }
   __syncthreads();
   KSP_STOP(2);
-  if (!elim && !top) {  // stays active: D', U (to i + 2s), R' for the next level
-    for (int q = tid; q < NB * NB; q += blockDim.x) {
+  const bool fin = act && (elim || top);
+  if (act && !fin) {  // stays active: D', U (to i + 2s), R' for the next level
+    for (int q = tid; q < NB * NB; q += nth) {
       d.D[(size_t)i * NB * NB + q] = L[q];
       d.U[(size_t)i * NB * NB + q] = Uo[q];
     }
-    for (int q = tid; q < NB * m; q += blockDim.x) d.R[(size_t)i * NB * m + q] = W[(q / m) * wc + 2 * NB + q % m];
-    return;
+    for (int q = tid; q < NB * m; q += nth) d.R[(size_t)i * NB * m + q] = W[(q / m) * wc + 2 * NB + q % m];
   }
-  for (int q = tid; q < NB * NB; q += blockDim.x) {
-    const int a = q / NB, b = q % NB;
-    W[a * wc + b] = Ui[b * NB + a];  // Ui^T
-    W[a * wc + NB + b] = Uo[q];
-  }
-  if (tid < 64) {
-    const bool ok = chol18_wave(L, id, tid);
-    if (!ok && tid == 0) d.sc[SC_OK] = 0.0;
+  if (fin) {
+    for (int q = tid; q < NB * NB; q += nth) {
+      const int a = q / NB, b = q % NB;
+      W[a * wc + b] = Ui[b * NB + a];  // Ui^T
+      W[a * wc + NB + b] = Uo[q];
+    }
+    if (tid < 64) {
+      const bool ok = chol18_wave(L, id, tid);
+      if (!ok && tid == 0) d.sc[SC_OK] = 0.0;
+    }
   }
   __syncthreads();
   KSP_STOP(3);
-  if (top) {  // X_0 = L^-T L^-1 R' (forward in place in W, then backward into X_0)
-    node_forward(L, id, W + 2 * NB, wc, m, W + 2 * NB, wc, tid);
-    node_backsolve(L, id, W + 2 * NB, wc, m, d.X, tid);
-    return;
+  if (fin && top) {  // X_0 = L^-T L^-1 R' (forward in place in W, then backward into X_0)
+    if (LEAN) {
+      node_forward_lean(L, id, W + 2 * NB, wc, m, W + 2 * NB, wc, tid, nth);
+      node_backsolve_lean(L, id, W + 2 * NB, wc, m, d.X, tid, nth);
+    } else {
+      node_forward(L, id, W + 2 * NB, wc, m, W + 2 * NB, wc, tid, nth);
+      node_backsolve(L, id, W + 2 * NB, wc, m, d.X, tid, nth);
+    }
+  } else if (fin) {
+    if (LEAN) node_forward_lean(L, id, W, wc, wc, d.Z + (size_t)i * NB * wc, wc, tid, nth);
+    else node_forward(L, id, W, wc, wc, d.Z + (size_t)i * NB * wc, wc, tid, nth);
+    KSP_STOP(4);
+    for (int q = tid; q < NB * NB; q += nth) d.Lf[(size_t)i * NB * NB + q] = L[q];
+    if (tid < NB) d.Lid[(size_t)i * NB + tid] = id[tid];
   }
-  node_forward(L, id, W, wc, wc, d.Z + (size_t)i * NB * wc, wc, tid);
-  KSP_STOP(4);
-  for (int q = tid; q < NB * NB; q += blockDim.x) d.Lf[(size_t)i * NB * NB + q] = L[q];
-  if (tid < NB) d.Lid[(size_t)i * NB + tid] = id[tid];
+}
+
+__global__ void __launch_bounds__(256) k_sp_level(SpDev d, int s) {
+  __shared__ double L[NB * NB];
+  __shared__ double id[NB];
+  __shared__ double Ui[NB * NB];  // coupling (i - 2s) -> i
+  __shared__ double Uo[NB * NB];  // coupling i -> (i + 2s)
+  extern __shared__ __attribute__((aligned(16))) double sm[];  // Zl [18][wc] | Zr [18][wc] | W [18][wc]
+  const int i = 2 * s * blockIdx.x;
+  if (i >= d.n) return;  // block-uniform
+  level_step<false>(d, s, i, true, threadIdx.x, blockDim.x, L, id, Ui, Uo, sm);
 }
 
 __global__ void __launch_bounds__(256) k_sp_top(SpDev d) {
@@ -1438,19 +1482,19 @@ __global__ void __launch_bounds__(256) k_sp_top(SpDev d) {
   node_backsolve(L, id, T, m, m, d.X, tid);
 }
 
-__global__ void __launch_bounds__(256) k_sp_back(SpDev d, int s) {
-  __shared__ double L[NB * NB];
-  __shared__ double id[NB];
-  extern __shared__ __attribute__((aligned(16))) double sm[];  // Z [18][wc] | xl [18][m] | xr [18][m] | T [18][m]
-  const int j = s + 2 * s * blockIdx.x, tid = threadIdx.x, m = d.m, wc = 36 + m;
-  if (j >= d.n) return;
+// back_step: node j's back substitution by a node group (the contract of level_step: every thread of the block
+// calls it, two block barriers on every path); L, id and sm (Z [18][wc] | xl | xr | T [18][m]) are the group's LDS
+template <bool LEAN>
+__device__ __forceinline__ void back_step(const SpDev& d, int s, int j, bool act, int tid, int nth, double* L,
+                                          double* id, double* sm) {
+  const int m = d.m, wc = 36 + m;
   const int l = j - s, r = j + s;
   const bool hr = r < d.n;
   double* Z = sm;
   double* xl = Z + NB * wc;
   double* xr = xl + NB * m;
   double* T = xr + NB * m;
-  {
+  if (act) {
     // L_j | 1/diag | Z_j | x_l | x_r in one batch of loads (x_r of an absent neighbour: zeros)
     const double* Ls = d.Lf + (size_t)j * NB * NB;
     const double* Is = d.Lid + (size_t)j * NB;
@@ -1458,8 +1502,8 @@ __global__ void __launch_bounds__(256) k_sp_back(SpDev d, int s) {
     const double* Xl = d.X + (size_t)l * NB * m;
     const double* Xr = d.X + (size_t)(hr ? r : l) * NB * m;
     const int n0 = NB * NB, n1 = n0 + NB, n2 = n1 + NB * wc, n3 = n2 + NB * m;
-    ksp_batched<13>(
-        n3 + NB * m, tid, blockDim.x,
+    ksp_batched<LEAN ? 6 : 13>(
+        n3 + NB * m, tid, nth,
         [&](int q) { return q < n0 ? Ls[q] : q < n1 ? Is[q - n0] : q < n2 ? Zs[q - n1] : q < n3 ? Xl[q - n2] : Xr[q - n3]; },
         [&](int q, double v) {
           if (q < n0)
@@ -1478,8 +1522,8 @@ __global__ void __launch_bounds__(256) k_sp_back(SpDev d, int s) {
   KSP_STOP(1);
   // T = Z_R - Z_Uin x_l - Z_U x_r on MFMA tiles: T[row][c] = Z_R[row][c] - sum_k (Z[row][k] xl[k][c] + Z[row][NB + k]
   // xr[k][c]); A = Z^T is read from the Z rows (stride 1 in k), B from xl / xr
-  {
-    const int wave = tid >> 6, lane = tid & 63, nw = blockDim.x >> 6, nct = (m + 15) >> 4;
+  if (act) {
+    const int wave = tid >> 6, lane = tid & 63, nw = nth >> 6, nct = (m + 15) >> 4;
     for (int t = wave; t < 2 * nct; t += nw) {
       const int ti = t / nct, tj = t % nct, i = lane & 15;
       const int rc = min(16 * ti + i, NB - 1), cc = min(16 * tj + i, m - 1);
@@ -1497,15 +1541,61 @@ __global__ void __launch_bounds__(256) k_sp_back(SpDev d, int s) {
       }
       const int c = 16 * tj + (lane & 15);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = 16 * ti + (lane >> 4) + 4 * r;
-        if (row < NB && c < m) T[row * m + c] = Z[row * wc + 2 * NB + c] - acc[r];
+      for (int rr = 0; rr < 4; ++rr) {
+        const int row = 16 * ti + (lane >> 4) + 4 * rr;
+        if (row < NB && c < m) T[row * m + c] = Z[row * wc + 2 * NB + c] - acc[rr];
       }
     }
   }
   __syncthreads();
   KSP_STOP(2);
-  node_backsolve(L, id, T, m, m, d.X + (size_t)j * NB * m, tid);
+  if (act) {
+    if (LEAN) node_backsolve_lean(L, id, T, m, m, d.X + (size_t)j * NB * m, tid, nth);
+    else node_backsolve(L, id, T, m, m, d.X + (size_t)j * NB * m, tid, nth);
+  }
+}
+
+__global__ void __launch_bounds__(256) k_sp_back(SpDev d, int s) {
+  __shared__ double L[NB * NB];
+  __shared__ double id[NB];
+  extern __shared__ __attribute__((aligned(16))) double sm[];  // Z [18][wc] | xl [18][m] | xr [18][m] | T [18][m]
+  const int j = s + 2 * s * blockIdx.x;
+  if (j >= d.n) return;  // block-uniform
+  back_step<false>(d, s, j, true, threadIdx.x, blockDim.x, L, id, sm);
+}
+
+// the deep levels in one block (round 4): once a level has at most kSpDeepGroups nodes, the remaining levels down to
+// the top and back up to the same stride run in one block of kSpDeepGroups node groups of kSpDeepGT threads, a block
+// barrier between levels instead of a kernel boundary (the L2 writeback and the launch of every level, and the
+// operands come back from the CU's own cache).  Levels s_deep .. top, then the back substitution top .. s_deep.
+constexpr int kSpDeepGroups = 4;
+constexpr int kSpDeepGT = 128;  // threads per node group: the block keeps the per-level kernels' 256-VGPR budget
+__global__ void __launch_bounds__(kSpDeepGT * kSpDeepGroups) k_sp_deep(SpDev d, int s_deep) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  // wave-uniform group index: the per-node branches (active, eliminated, top) are scalar branches
+  const int g = __builtin_amdgcn_readfirstlane(threadIdx.x / kSpDeepGT), tid = threadIdx.x % kSpDeepGT;
+  // the group size as an opaque value, as blockDim.x is in k_sp_level / k_sp_back: a compile-time stride lets the
+  // compiler unroll the strided output loops and hoist their operands (hundreds of spilled VGPRs)
+  int nth = kSpDeepGT;
+  asm volatile("" : "+s"(nth));
+  const int wc = 36 + d.m, per = 3 * NB * NB + NB + 3 * NB * wc;  // the group's LDS: L | Ui | Uo | id | Zl | Zr | W
+  double* L = sm + (size_t)g * per;
+  double* Ui = L + NB * NB;
+  double* Uo = Ui + NB * NB;
+  double* id = Uo + NB * NB;
+  double* gsm = id + NB;
+  int s = s_deep;
+  for (;; s *= 2) {
+    const int i = 2 * s * g;
+    level_step<true>(d, s, i, i < d.n, tid, nth, L, id, Ui, Uo, gsm);
+    __syncthreads();  // this level's D / U / R / Z / X stores before the next level's loads
+    if (2 * s >= d.n) break;
+  }
+  for (; s >= s_deep; s /= 2) {
+    const int j = s + 2 * s * g;
+    back_step<true>(d, s, j, j < d.n, tid, nth, L, id, gsm);
+    __syncthreads();
+  }
 }
 
 // ---------------------------------------------------------------- partitioned band solve (default)
@@ -2310,6 +2400,9 @@ struct kb_sp_handle {
   int gn_graph_n = 0;
   std::vector<SpLvl> lv;  // partitioned band solve: lv[0 .. nl) chunk levels, lv[nl] the top system
   bool use_cr = true;     // block cyclic reduction; KSP_PARTITION=1: the partitioned band solve
+  int s_deep = 0;         // first stride run by k_sp_deep (0: one launch per level)
+  int deep_groups = 0;    // k_sp_deep's node groups (kSpDeepGT threads each)
+  size_t lds_deep = 0;
   std::vector<double> trace;
   double* host_sc = nullptr;  // pinned scalars
 
@@ -2365,8 +2458,13 @@ int launch_reduction(kb_sp_handle* h) {
   }
   hipLaunchKernelGGL(k_sp_elim1, dim3(d.n / 2), dim3(256), h->lds_elim, h->stream, d);
   int s = 1;
-  for (; s < d.n; s *= 2)
+  const int sd = h->s_deep;
+  for (; s < d.n && !(sd && s >= sd); s *= 2)
     hipLaunchKernelGGL(k_sp_level, dim3((d.n + 2 * s - 1) / (2 * s)), dim3(256), h->lds_level, h->stream, d, s);
+  if (sd && s < d.n) {  // the remaining levels down and back up to stride sd in one block
+    hipLaunchKernelGGL(k_sp_deep, dim3(1), dim3(kSpDeepGT * h->deep_groups), h->lds_deep, h->stream, d, sd);
+    s = sd;
+  }
   for (s /= 2; s >= 1; s /= 2) {
     const int ne = (d.n - s + 2 * s - 1) / (2 * s);
     hipLaunchKernelGGL(k_sp_back, dim3(ne), dim3(256), h->lds_back, h->stream, d, s);
@@ -2626,6 +2724,24 @@ kb_sp_handle* kb_sp_create(const kb_sp_layout* L) {
   hipFuncSetAttribute((const void*)k_sp_level, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_level);
   hipFuncSetAttribute((const void*)k_sp_elim1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_elim);
   hipFuncSetAttribute((const void*)k_sp_back, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_back);
+  {
+    // the deep levels in one block (k_sp_deep, KSP_DEEP=1; measured and not kept: configs[4] 2,227 -> 1,998 GN it/s,
+    // the one-block kernel 118 us against 74 us for the six launches it replaces -- four nodes share one CU's SIMDs
+    // and LDS port where each level kernel gives a node a CU of its own, which outweighs the saved launches): as
+    // many node groups as the LDS holds (<= kSpDeepGroups), from the first stride whose level has at most that many
+    // nodes
+    const size_t per = sizeof(double) * (3 * NB * NB + NB + 3 * NB * (36 + d.m));
+    h->deep_groups = (int)std::min<size_t>(kSpDeepGroups, (160 * 1024) / per);
+    h->s_deep = 0;
+    const char* ev = std::getenv("KSP_DEEP");
+    if (h->deep_groups >= 2 && h->n >= 2 && ev && std::atoi(ev) != 0) {
+      int sd = 1;
+      while ((h->n + 2 * sd - 1) / (2 * sd) > h->deep_groups) sd *= 2;
+      h->s_deep = sd;
+      h->lds_deep = per * h->deep_groups;
+      hipFuncSetAttribute((const void*)k_sp_deep, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_deep);
+    }
+  }
   hipFuncSetAttribute((const void*)k_sp_schur, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_schur);
   if (hipStreamSynchronize(h->stream) != hipSuccess) {
     fail("kb_sp_create: stream sync failed");

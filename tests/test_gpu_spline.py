@@ -292,3 +292,17 @@ def test_position_prior_removed_and_bad_input(prior_case):
     with pytest.raises(capi.KbError):  # not positive definite
         g.set_position_priors(pri[0], pri[1], -pri[2])
     g.set_position_priors(*pri)
+
+
+def test_deep_level_kernel_parity(monkeypatch):
+    """KSP_DEEP=1 (the cyclic reduction's deep levels in one block, measured slower and kept opt-in) gives the same
+    GN run as the oracle"""
+    monkeypatch.setenv("KSP_DEEP", "1")
+    p = synth.make_spline_config(n_frames=40)
+    g = capi.SplineSolver(p)
+    o = O.SplineOracle(p)
+    g.set_state(p.state_init)
+    kw = dict(policy="gn", lambda0=10.0, max_iterations=10, eps_x=1e-3, eps_j=1e-3)
+    res = g.optimize(**kw)
+    st_o, res_o = o.optimize(p.state_init, nthreads=4, **kw)
+    _compare_runs(res, g.get_state(), res_o, st_o)
