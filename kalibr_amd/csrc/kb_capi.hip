@@ -235,14 +235,22 @@ static void set_frame_counts(kb_handle* h) {
 }
 
 // dynamic LDS of the build kernel (depends on the frames per block through the staged frame poses)
-static size_t build_lds(const kb_handle* h) {
+// k_buildp's static LDS (control copies, chain / intrinsic table, column info, counters) is below this
+constexpr size_t kBuildpStaticLds = 4096;
+static size_t build_lds(kb_handle* h) {
   const int N = h->N, C = h->C, WPB = h->d.wpb;
   const int CZ = 16 * ((C + 16) / 16);  // [Y | z] row stride of the Schur tiles
   const int tgl = (3 * h->K <= kTargetLds ? 3 * h->K : 0) + 8 * h->d.gframes;
-  if (h->build_pipe) {  // k_buildp: tiles | H | chains | 2 view buffers | frame-wave buffers | K | target, poses
+  if (h->build_pipe) {  // k_buildp: tiles | H | chains G | view outputs | frame sums | frame-wave buffers | K | target,
+                        // poses | the second view-output buffer
     const int np = N * (N - 1) / 2, nf = (C + 16) / 16 <= 4 ? 2 : 4;  // as build_threads
-    return sizeof(double) * (N * 64 * XS + N * 256 + N * 64 + (36 * np + 44 * N + 6 * CZ) + (40 + 6 * CZ) +
-                             nf * 6 * CZ + 36 * np + tgl);
+    const size_t vbs = 36 * np + 44 * N + 6 * CZ;
+    const size_t base = N * 64 * XS + N * 256 + N * 36 + 2 * vbs + (40 + 6 * CZ) + nf * 6 * CZ + 36 * np +
+                        8 * h->d.gframes;
+    // the target corners are staged when they fit beside the rest
+    const bool tg = 3 * h->K <= kTargetLds && sizeof(double) * (base + 3 * h->K) + kBuildpStaticLds <= 160 * 1024;
+    h->d.bp_tg = tg ? 1 : 0;
+    return sizeof(double) * (base + (tg ? 3 * h->K : 0));
   }
   return sizeof(double) * (WPB * 64 * XS + WPB * 256 + N * (256 + 256 + 64 + 36 + 36 + 8) + 36 + 16 * CZ +
                            18 * N * (N - 1) + tgl);
@@ -337,7 +345,8 @@ static int regrow(kb_handle* h, T** p, size_t n_new, size_t keep) {
 static int relayout(kb_handle* h) {
   set_frame_counts(h);
   h->lds_build = build_lds(h);
-  if (h->lds_build > 160 * 1024) return fail("kb_append_frames: build-kernel LDS budget exceeded for this frame count");
+  if (h->lds_build + (h->build_pipe ? kBuildpStaticLds : 0) > 160 * 1024)
+    return fail("kb_append_frames: build-kernel LDS budget exceeded for this frame count");
   KB_HIP(hipFuncSetAttribute(h->fn_build, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_build));
   KB_HIP(hipFuncSetAttribute(h->fn_build_gn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_build));
   drop_graphs(h);
@@ -534,7 +543,8 @@ kb_handle* kb_create(const kb_layout* L) {
                   : C <= 48 ? (const void*)k_solve<48>
                   : C <= 64 ? (const void*)k_solve<64>
                             : (const void*)k_solve<0>;
-    if (h->lds_build > 160 * 1024 || h->lds_solve > 160 * 1024 || h->lds_camexp > 160 * 1024) {
+    if (h->lds_build + (h->build_pipe ? kBuildpStaticLds : 0) > 160 * 1024 || h->lds_solve > 160 * 1024 ||
+        h->lds_camexp > 160 * 1024) {
       fail("kb_create: LDS budget exceeded for this rig");
       kb_destroy(h);
       return nullptr;

@@ -106,6 +106,7 @@ struct KbDev {
   // (upper packed) | b | non-PD | max|dx_f|], and k_colsumx writes the column sums straight into the k_solve image
   // (no k_colimg).  Image aux slots after the tiles: [g_c | non-PD at C] (n16) | cost | max|dx_f| per rank.
   int xexp;
+  int bp_tg;   // k_buildp: the target corners staged in LDS (the host's LDS budget decides)
   double* ximg;  // image the column sums are written to: simg (one GPU) or this rank's partial image (sharded)
   // per-pass timing query only (kb_gn_pass_times): [0] arrival counter | [1 ..] s_memrealtime (100 MHz) at the start of
   // each pass's build kernel (block 0), null otherwise

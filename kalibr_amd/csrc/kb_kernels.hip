@@ -1252,8 +1252,8 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
   const int VBS = 36 * NP + 44 * N + 6 * CZ, FBS = 6 * CZ;
   double* Xw = sm + wave * 64 * XS;     // [N][64][XS] view waves' Jacobian-row tiles (P_v after the SYRK)
   double* Hw = sm + N * 64 * XS;        // [N][256] view local Hessians
-  double* Wv = Hw + N * 256;            // [N][64]: R(9) t(3) tf(3) | G(36) at +16
-  double* VB = Wv + N * 64;             // [VBS] view outputs: P_i K_{i,j} [NP][36] | dH [N][36] | dg [N][8] |
+  double* Wv = Hw + N * 256;            // [N][36]: each view's chain G
+  double* VB = Wv + N * 36;             // [VBS] view outputs: P_i K_{i,j} [NP][36] | dH [N][36] | dg [N][8] |
                                         //   intrinsic columns [6][CZ]
   double* FI = VB + VBS;                // [40 + 6 CZ] frame sums: H_ff | [H_fc | g_f] (rows of 6)
   double* FB = FI + 40 + 6 * CZ;        // [NF][FBS] frame wave's [A_f | b_f]
@@ -1265,6 +1265,7 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
   __shared__ int ctab[2][KB_MAX_CAMS];      // per camera: first intrinsic column | baseline column
   __shared__ int cil[112];                  // expanded partials: column info (kind << 16 | camera << 8 | index)
   __shared__ int xcnt;                      // expanded partials: view waves done with their camera's share
+  __shared__ int fcnt;                      // frame waves done with their share of a frame's sums (monotonic)
   const int W = d.W;
   const int f0 = blockIdx.x * d.gframes, f1 = min(d.F, f0 + d.gframes), G = f1 - f0;
   const bool vw = wave < N;  // view wave (camera = wave) | frame wave fw = wave - N
@@ -1274,7 +1275,7 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
   const KbCtrl cin = *c;
   const int done = cin.done, dob = cin.do_build, cur = cin.cur;
   const double lam = gate ? cin.lambda : d.host_lambda;
-  const bool tg_lds = d.K * 3 <= kTargetLds;
+  const bool tg_lds = d.bp_tg;  // the host decides (its LDS budget holds a second view-output buffer)
   const int nt3 = 3 * d.K;
   constexpr int kTgU = 2;
   double tv[kTgU];
@@ -1350,6 +1351,9 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
   const bool xp = GNF && gfu && fuse && d.xexp;
   if (xp && tid < C) cil[tid] = d.colinfo[tid];
   double* fpl = tg + (tg_lds ? nt3 : 0);
+  // the view outputs are double-buffered: frame f's in VB (f - f0 even) or VB1 (odd), so that the frame waves sum
+  // frame f - 1 while the view waves run frame f
+  double* VB1 = fpl + 8 * d.gframes;
   int cidn;  // view waves: lane = corner of a 64-corner pass
   double2 yn;
   {
@@ -1410,6 +1414,7 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
   if (tid == 0) {
     okl = 1;
     xcnt = 0;
+    fcnt = 0;
   }
   __syncthreads();
   if (wave == 0) KB_TSB(d, 1);
@@ -1418,66 +1423,16 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
   double* prow = d.part + (size_t)blockIdx.x * d.Wr;
   double* Fh = FI;      // frame inputs of the frame being eliminated: H_ff (40) | [H_fc | g_f] [6][CZ]
   double* P = FI + 40;
-  // iteration it: phase A (view waves) the frame sums of frame it - 1 -> FI; barrier; phase B: view waves run the
-  // views of frame it -> VB, frame waves eliminate frame it - 1 from FI; barrier.  The roles run separate loops
-  // with the same barrier count (2 (G + 1)), so neither holds the other's registers.
+  // iteration it: the view waves run the views of frame it -> VB[it & 1]; the frame waves sum frame it - 1 over its
+  // views (VB[(it - 1) & 1] -> FI, split over the frame waves, an LDS counter between them) and eliminate it; one
+  // block barrier per frame.  The roles run separate loops with the same barrier count (G, then one after the last
+  // frame), so neither holds the other's registers; the frame sums are off the view waves' chain.
   if (vw) {
     const int model = cam_arg(d.model, cam), nin = mm_nintr<MM>() ? mm_nintr<MM>() : cam_arg(d.nintr, cam);
     const double* Lc = cst[cam];
     const double* intr = cst[cam] + 12;
     v4d creg = {0.0, 0.0, 0.0, 0.0};  // the camera's local sums over the block's frames
-    for (int it = 0; it <= G; ++it) {
-      if (it > 0) {
-        if (wave == 0 && it <= 8) KB_TSB(d, 51 + it);
-        // ---------------- phase A: sums of frame f - 1 over its views (camera order), all view waves
-        const int f = f0 + it - 1;
-        const double* Cb = VB;
-        const double* dHv = VB + 36 * NP;
-        const double* dgv = VB + 36 * NP + N * 36;
-        const double* Pi = VB + 36 * NP + N * 44;
-        const int CI = C - 6 * (N - 1);  // intrinsic columns [0, CI)
-        const int nsum = 42 + 36 * (N - 1);
-        for (int q = tid; q < nsum + 6 * CI; q += 64 * N) {
-          if (q >= nsum) {  // the views' intrinsic columns
-            const int e = q - nsum, a = e / CI, cc = e - a * CI;
-            P[a * CZ + cc] = Pi[a * CZ + cc];
-            continue;
-          }
-          // every term of an output is loaded at once (clamped addresses), then summed in camera order
-          double v[kBuildpMaxCams];
-          if (q < 42) {
-            const double* src = q < 36 ? dHv + q : dgv + q - 36;
-            const int stride = q < 36 ? 36 : 8;
-#pragma unroll
-            for (int i = 0; i < kBuildpMaxCams; ++i) v[i] = src[min(i, N - 1) * stride];
-          } else {  // H_f,B_j = sum_{i > j} P_i K_{i,j} (the views' products)
-            const int e = q - 42, j = e / 36, ab2 = e % 36;
-#pragma unroll
-            for (int i = 0; i < kBuildpMaxCams; ++i) {
-              const int ii = min(max(i, j + 1), N - 1);
-              v[i] = Cb[(ii * (ii - 1) / 2 + j) * 36 + ab2];
-            }
-          }
-          const int e = q - 42, j = q < 42 ? -1 : e / 36, ab2 = e - 36 * j;
-          double sacc = 0.0;
-#pragma unroll
-          for (int i = 0; i < kBuildpMaxCams; ++i)
-            if (i > j && i < N) sacc += v[i];
-          if (q < 36) {
-            Fh[q] = sacc;
-            if (!gfu) d.Hff[(size_t)f * 36 + q] = sacc;
-          } else if (q < 42) {
-            P[(q - 36) * CZ + C] = sacc;
-            d.gf[(size_t)f * 6 + q - 36] = sacc;
-          } else {
-            const int a = ab2 / 6, b = ab2 % 6;
-            P[a * CZ + ctab[1][j] + b] = sacc;
-            if (!gfu) d.Hfc[((size_t)f * 6 + a) * C + ctab[1][j] + b] = sacc;
-          }
-        }
-      }
-      __syncthreads();
-      if (it == G) break;  // the last frame's elimination runs on the frame waves now (the expansion below meanwhile)
+    for (int it = 0; it < G; ++it) {
       {
         // ---------------- phase B: view (f, cam)
         const int f = f0 + it;
@@ -1485,7 +1440,7 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
         asm volatile("" : "+v"(lane));
         const int mrow = lane >> 4, mcol = lane & 15;
         if (wave == 0 && it < 8) KB_TSB(d, 2 + 2 * it);
-        double* vb = VB;
+        double* vb = (it & 1) ? VB1 : VB;
         const int2 fvn = d.fview[(size_t)min(f + 1, f1 - 1) * N + cam];  // the next frame's view (first loads below)
         double fp[7];
 #pragma unroll
@@ -1497,7 +1452,7 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
         // T_cam_w and the frame translation in registers, so lane e < 36 picks entry e by selects (no LDS staging;
         // wave 0's first v-row segment 2.2 -> 1.2 us, the frame period unchanged: the second view wave of each SIMD
         // sets it)
-        double* Gm = Wv + cam * 64 + 16;
+        double* Gm = Wv + cam * 36;
         auto make_g = [&]() {
           if (lane < 36) Gm[lane] = chain_entry_reg(R, t, fp + 4, lane / 6, lane % 6);
         };
@@ -1787,7 +1742,7 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
         prow[C] = sc;  // the block's chi^2 (the cost column)
       }
     }
-    __syncthreads();  // the frame waves' last barrier (after the last frame's elimination)
+    __syncthreads();  // the frame waves' last barrier (after the last frame's sums and elimination)
     if (!xp) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {  // the camera's local sums, upper packed
@@ -1802,10 +1757,65 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
     for (int t = 0; t < TT; ++t) acc[t] = v4d{0.0, 0.0, 0.0, 0.0};
     schur_tiles_assign_fw<TT>(fuse ? nbz : 0, fw, tii, tjj);
     double* Q = FB + fw * FBS;  // this frame wave's [A_f | b_f] [6][CZ]
+    const int CI = C - 6 * (N - 1);  // intrinsic columns [0, CI)
+    const int nsum = 42 + 36 * (N - 1);
     for (int it = 0; it <= G; ++it) {
-      __syncthreads();  // phase A: the view waves sum frame it - 1 into FI
+      if (it > 0) {
+        // ---------------- phase A: sums of frame f = f0 + it - 1 over its views (camera order), the frame waves' share
+        const int f = f0 + it - 1;
+        if (fw == 0 && it <= 8) KB_TSB(d, 51 + it);
+        const double* VBp = ((it - 1) & 1) ? VB1 : VB;
+        const double* Cb = VBp;
+        const double* dHv = VBp + 36 * NP;
+        const double* dgv = VBp + 36 * NP + N * 36;
+        const double* Pi = VBp + 36 * NP + N * 44;
+        for (int q = fw * 64 + lane; q < nsum + 6 * CI; q += 64 * NF) {
+          if (q >= nsum) {  // the views' intrinsic columns
+            const int e = q - nsum, a = e / CI, cc = e - a * CI;
+            P[a * CZ + cc] = Pi[a * CZ + cc];
+            continue;
+          }
+          // every term of an output is loaded at once (clamped addresses), then summed in camera order
+          double v[kBuildpMaxCams];
+          if (q < 42) {
+            const double* src = q < 36 ? dHv + q : dgv + q - 36;
+            const int stride = q < 36 ? 36 : 8;
+#pragma unroll
+            for (int i = 0; i < kBuildpMaxCams; ++i) v[i] = src[min(i, N - 1) * stride];
+          } else {  // H_f,B_j = sum_{i > j} P_i K_{i,j} (the views' products)
+            const int e = q - 42, j = e / 36, ab2 = e % 36;
+#pragma unroll
+            for (int i = 0; i < kBuildpMaxCams; ++i) {
+              const int ii = min(max(i, j + 1), N - 1);
+              v[i] = Cb[(ii * (ii - 1) / 2 + j) * 36 + ab2];
+            }
+          }
+          const int e = q - 42, j = q < 42 ? -1 : e / 36, ab2 = e - 36 * j;
+          double sacc = 0.0;
+#pragma unroll
+          for (int i = 0; i < kBuildpMaxCams; ++i)
+            if (i > j && i < N) sacc += v[i];
+          if (q < 36) {
+            Fh[q] = sacc;
+            if (!gfu) d.Hff[(size_t)f * 36 + q] = sacc;
+          } else if (q < 42) {
+            P[(q - 36) * CZ + C] = sacc;
+            d.gf[(size_t)f * 6 + q - 36] = sacc;
+          } else {
+            const int a = ab2 / 6, b = ab2 % 6;
+            P[a * CZ + ctab[1][j] + b] = sacc;
+            if (!gfu) d.Hfc[((size_t)f * 6 + a) * C + ctab[1][j] + b] = sacc;
+          }
+        }
+        // the frame waves meet (an LDS counter: the view waves are in their next frame) before the elimination reads
+        // every sum
+        KB_WAVE_SYNC();
+        if (lane == 0) atomicAdd(&fcnt, 1);
+        while (__hip_atomic_load(&fcnt, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < NF * it)
+          __builtin_amdgcn_s_sleep(1);
+      }
       if (it > 0 && fuse) {
-        // ---------------- phase B: frame f = it - 1 (one behind the views): elimination + Schur tiles
+        // ---------------- frame f = it - 1 (one behind the views): elimination + Schur tiles
         const int f = f0 + it - 1;
         // an opaque lane id per frame: the lane-dependent addresses and selects of the elimination are recomputed
         // here instead of being hoisted out of the loop (which spills at this kernel's register budget)
@@ -1819,8 +1829,9 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
         schur_tiles_accumulate6<TT>(P, Q, CZ, tii, tjj, acc, lane);
         if (fw == 0 && it <= 8) KB_TSB(d, 23 + 4 * (it - 1));
       }
-      __syncthreads();
+      if (it < G) __syncthreads();  // the view waves' frame it is in VB[it & 1]
     }
+    __syncthreads();  // the view waves' last barrier (their expansion of the block's camera sums is done)
     if (fuse && !xp) schur_tiles_store<TT>(prow + N * 136, C, tii, tjj, acc);
     // expanded partials: the view waves expanded the camera block during the last frame's elimination
     if (xp) schur_tiles_store_x<TT>(prow + N * 136, C, tii, tjj, acc, sm);
