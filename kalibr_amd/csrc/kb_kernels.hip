@@ -1255,8 +1255,9 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
   double* Wv = Hw + N * 256;            // [N][36]: each view's chain G
   double* VB = Wv + N * 36;             // [VBS] view outputs: P_i K_{i,j} [NP][36] | dH [N][36] | dg [N][8] |
                                         //   intrinsic columns [6][CZ]
-  double* FI = VB + VBS;                // [40 + 6 CZ] frame sums: H_ff | [H_fc | g_f] (rows of 6)
-  double* FB = FI + 40 + 6 * CZ;        // [NF][FBS] frame wave's [A_f | b_f]
+  double* FI = VB + VBS;                // [40] frame sums: H_ff ([H_fc | g_f] is summed into the view buffer's
+                                        //   intrinsic-column rows, whose other columns the views leave free)
+  double* FB = FI + 40;                 // [NF][FBS] frame wave's [A_f | b_f]
   double* Kl = FB + NF * FBS;           // [NP][36] K_{i,j}, j < i, at (i(i-1)/2 + j)
   double* tg = Kl + 36 * NP;            // [n_target][3] target corners (when staged) | frame poses [gframes][8]
   __shared__ double wmx[kBuildpMaxCams + 4];
@@ -1421,8 +1422,7 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
 
   const int mrow = lane >> 4, mcol = lane & 15;
   double* prow = d.part + (size_t)blockIdx.x * d.Wr;
-  double* Fh = FI;      // frame inputs of the frame being eliminated: H_ff (40) | [H_fc | g_f] [6][CZ]
-  double* P = FI + 40;
+  double* Fh = FI;      // frame inputs of the frame being eliminated: H_ff (40); [H_fc | g_f] [6][CZ] in its view buffer
   // iteration it: the view waves run the views of frame it -> VB[it & 1]; the frame waves sum frame it - 1 over its
   // views (VB[(it - 1) & 1] -> FI, split over the frame waves, an LDS counter between them) and eliminate it; one
   // block barrier per frame.  The roles run separate loops with the same barrier count (G, then one after the last
@@ -1751,30 +1751,28 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
       }
     }
   } else {
+    // the frame waves are the youngest waves of their SIMDs, so age-ordered issue serves them last; their frame sums
+    // and elimination are on the per-frame critical path (priority 1: configs[3] 7,187 -> 7,232 GN it/s, the 250-frame
+    // shard 14,568 -> 14,750; priority 3 measured the same)
+    __builtin_amdgcn_s_setprio(1);
     v4d acc[TT];
     int tii[TT], tjj[TT];
 #pragma unroll
     for (int t = 0; t < TT; ++t) acc[t] = v4d{0.0, 0.0, 0.0, 0.0};
     schur_tiles_assign_fw<TT>(fuse ? nbz : 0, fw, tii, tjj);
     double* Q = FB + fw * FBS;  // this frame wave's [A_f | b_f] [6][CZ]
-    const int CI = C - 6 * (N - 1);  // intrinsic columns [0, CI)
-    const int nsum = 42 + 36 * (N - 1);
+    const int nsum = 42 + 36 * (N - 1);  // H_ff, g_f and the baseline columns (the intrinsic ones are in place)
     for (int it = 0; it <= G; ++it) {
       if (it > 0) {
         // ---------------- phase A: sums of frame f = f0 + it - 1 over its views (camera order), the frame waves' share
         const int f = f0 + it - 1;
         if (fw == 0 && it <= 8) KB_TSB(d, 51 + it);
-        const double* VBp = ((it - 1) & 1) ? VB1 : VB;
+        double* VBp = ((it - 1) & 1) ? VB1 : VB;
         const double* Cb = VBp;
         const double* dHv = VBp + 36 * NP;
         const double* dgv = VBp + 36 * NP + N * 36;
-        const double* Pi = VBp + 36 * NP + N * 44;
-        for (int q = fw * 64 + lane; q < nsum + 6 * CI; q += 64 * NF) {
-          if (q >= nsum) {  // the views' intrinsic columns
-            const int e = q - nsum, a = e / CI, cc = e - a * CI;
-            P[a * CZ + cc] = Pi[a * CZ + cc];
-            continue;
-          }
+        double* P = VBp + 36 * NP + N * 44;  // [H_fc | g_f]: the views wrote the intrinsic columns in place
+        for (int q = fw * 64 + lane; q < nsum; q += 64 * NF) {
           // every term of an output is loaded at once (clamped addresses), then summed in camera order
           double v[kBuildpMaxCams];
           if (q < 42) {
@@ -1822,6 +1820,7 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
         int lane = threadIdx.x & 63;
         asm volatile("" : "+v"(lane));
         if (fw == 0 && it <= 8) KB_TSB(d, 20 + 4 * (it - 1));
+        double* P = (((it - 1) & 1) ? VB1 : VB) + 36 * NP + N * 44;
         const bool ok = frame_ldl(d, f, Fh, lam2, P, Q, CZ, lane, fw == 0, fw == 0 && it == 3);
         if (!ok && lane == 0) okl = 0;
         KB_WAVE_SYNC();
