@@ -1251,8 +1251,8 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
   const int nbz = (C + 16) >> 4, CZ = 16 * nbz;
   const int VBS = 36 * NP + 44 * N + 6 * CZ, FBS = 6 * CZ;
   double* Xw = sm + wave * 64 * XS;     // [N][64][XS] view waves' Jacobian-row tiles (P_v after the SYRK)
-  double* Hw = sm + N * 64 * XS;        // [N][256] view local Hessians
-  double* Wv = Hw + N * 256;            // [N][36]: each view's chain G
+  double* PvL = sm + N * 64 * XS;       // [2][N][128] each view's P_v[:, d] (MFMA A-operand layout), by frame parity
+  double* Wv = PvL + N * 256;           // [N][36]: each view's chain G
   double* VB = Wv + N * 36;             // [VBS] view outputs: P_i K_{i,j} [NP][36] | dH [N][36] | dg [N][8] |
                                         //   intrinsic columns [6][CZ]
   double* FI = VB + VBS;                // [40] frame sums: H_ff ([H_fc | g_f] is summed into the view buffer's
@@ -1563,25 +1563,16 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
         //   B = G from LDS), i.e. D[i][a] = P_v[a][i] with P_v = G^T H[d, :]: G^T H_dd, G^T H_dI, G^T g_d;
         //   then D's C layout is the A operand P_v[:, d] of dH = P_v G and of this camera's share P_v K_{v,j} of the
         //   baseline columns.  No LDS transposition; the chain's loads were issued before the SYRK.
-        double* Cb = vb;  // P_v K_{v,j} at pair (v(v-1)/2 + j)
         double* dHv = vb + 36 * NP + cam * 36;
         double* dgv = vb + 36 * NP + N * 36 + cam * 8;
         double* Pi = vb + 36 * NP + N * 44;
         const int i16 = lane & 15, k0 = lane >> 4;
-        const double* Kv = Kl + (cam * (cam - 1) / 2) * 36;
-        const int nct = (6 * cam + 15) >> 4;  // 16-column tiles of [K_{v,0} | K_{v,1} | ...]
-        double gb[2], kb[3][2];
+        double gb[2];
 #pragma unroll
         for (int st = 0; st < 2; ++st) {
           const int k = k0 + 4 * st;
           const double g = Gm[min(k, 5) * 6 + min(i16, 5)];
           gb[st] = (k < 6 && i16 < 6) ? g : 0.0;
-#pragma unroll
-          for (int ct = 0; ct < 3; ++ct) {
-            const int c = 16 * ct + i16, cc = min(c, max(6 * cam - 1, 0)), jj = cc / 6, bb = cc - 6 * jj;
-            const double v = Kv[min(jj * 36 + min(k, 5) * 6 + bb, max(36 * cam - 1, 0))];
-            kb[ct][st] = (k < 6 && c < 6 * cam) ? v : 0.0;
-          }
         }
         v4d dv = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -1592,15 +1583,11 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
         v4d t2 = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int st = 0; st < 2; ++st) t2 = __builtin_amdgcn_mfma_f64_16x16x4f64(pa[st], gb[st], t2, 0, 0, 0);
-        v4d t3[3];
+        // this camera's share P_v K_{v,j} of the baseline columns is formed by the frame waves (their per-frame chain
+        // has the slack): the A operand goes to LDS in its register layout, buffer it & 1
+        if (cam > 0) {
 #pragma unroll
-        for (int ct = 0; ct < 3; ++ct) {
-          t3[ct] = v4d{0.0, 0.0, 0.0, 0.0};
-          if (ct < nct) {
-#pragma unroll
-            for (int st = 0; st < 2; ++st)
-              t3[ct] = __builtin_amdgcn_mfma_f64_16x16x4f64(pa[st], kb[ct][st], t3[ct], 0, 0, 0);
-          }
+          for (int st = 0; st < 2; ++st) PvL[(it & 1) * N * 128 + cam * 128 + st * 64 + lane] = pa[st];
         }
         // D entry (i, a) at lane (i & 3) * 16 + a, reg i >> 2: G^T H_dI (the camera's intrinsic columns), G^T g_d
 #pragma unroll
@@ -1619,17 +1606,6 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
         for (int r = 0; r < 2; ++r) {  // dH = P_v G: entry (a, b) at lane, reg: a = k0 + 4 r, b = i16
           const int arow = k0 + 4 * r;
           if (arow < 6 && i16 < 6) dHv[arow * 6 + i16] = t2[r];
-        }
-#pragma unroll
-        for (int ct = 0; ct < 3; ++ct) {  // P_v K_{v,j}: columns c = 6 j + b
-          const int c = 16 * ct + i16, jj = c / 6, bb = c - 6 * jj;
-          if (ct < nct && c < 6 * cam) {
-#pragma unroll
-            for (int r = 0; r < 2; ++r) {
-              const int arow = k0 + 4 * r;
-              if (arow < 6) Cb[(cam * (cam - 1) / 2) * 36 + jj * 36 + arow * 6 + bb] = t3[ct][r];
-            }
-          }
         }
         if (stv) KB_TSB(d, sto + 8);
       }
@@ -1768,10 +1744,44 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
         const int f = f0 + it - 1;
         if (fw == 0 && it <= 8) KB_TSB(d, 51 + it);
         double* VBp = ((it - 1) & 1) ? VB1 : VB;
-        const double* Cb = VBp;
+        double* Cb = VBp;
         const double* dHv = VBp + 36 * NP;
         const double* dgv = VBp + 36 * NP + N * 36;
         double* P = VBp + 36 * NP + N * 44;  // [H_fc | g_f]: the views wrote the intrinsic columns in place
+        {
+          // each view's share of the baseline columns, P_v K_{v,j} (j < v), one 16-column tile job at a time over the
+          // frame waves: the views' A operands from LDS (their register layout), K_{v,j} from Kl
+          const double* pab = PvL + ((it - 1) & 1) * N * 128;
+          const int i16 = lane & 15, k0 = lane >> 4;
+          int job = 0;
+          for (int v = 1; v < N; ++v) {
+            const int nct = (6 * v + 15) >> 4;  // 16-column tiles of [K_{v,0} | K_{v,1} | ...]
+            const double* Kv = Kl + (v * (v - 1) / 2) * 36;
+            for (int ct = 0; ct < nct; ++ct, ++job) {
+              if (job % NF != fw) continue;  // wave-uniform
+              v4d t3 = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+              for (int st = 0; st < 2; ++st) {
+                const int k = k0 + 4 * st, c = 16 * ct + i16, cc = min(c, 6 * v - 1), jj = cc / 6, bb = cc - 6 * jj;
+                const double kv = Kv[jj * 36 + min(k, 5) * 6 + bb];
+                t3 = __builtin_amdgcn_mfma_f64_16x16x4f64(pab[v * 128 + st * 64 + lane],
+                                                          (k < 6 && c < 6 * v) ? kv : 0.0, t3, 0, 0, 0);
+              }
+              const int c = 16 * ct + i16, jj = c / 6, bb = c - 6 * jj;
+              if (c < 6 * v) {
+#pragma unroll
+                for (int r = 0; r < 2; ++r) {
+                  const int arow = k0 + 4 * r;
+                  if (arow < 6) Cb[(v * (v - 1) / 2) * 36 + jj * 36 + arow * 6 + bb] = t3[r];
+                }
+              }
+            }
+          }
+          KB_WAVE_SYNC();
+          if (lane == 0) atomicAdd(&fcnt, 1);
+          while (__hip_atomic_load(&fcnt, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < NF * (2 * it - 1))
+            __builtin_amdgcn_s_sleep(1);
+        }
         for (int q = fw * 64 + lane; q < nsum; q += 64 * NF) {
           // every term of an output is loaded at once (clamped addresses), then summed in camera order
           double v[kBuildpMaxCams];
@@ -1809,7 +1819,7 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
         // every sum
         KB_WAVE_SYNC();
         if (lane == 0) atomicAdd(&fcnt, 1);
-        while (__hip_atomic_load(&fcnt, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < NF * it)
+        while (__hip_atomic_load(&fcnt, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < NF * 2 * it)
           __builtin_amdgcn_s_sleep(1);
       }
       if (it > 0 && fuse) {
