@@ -244,7 +244,7 @@ static size_t build_lds(kb_handle* h) {
   if (h->build_pipe) {  // k_buildp: tiles | H | chains G | view outputs | frame sums | frame-wave buffers | K | target,
                         // poses | the second view-output buffer
     const int np = N * (N - 1) / 2, nf = (C + 16) / 16 <= 4 ? 2 : 4;  // as build_threads
-    const size_t vbs = 36 * np + 44 * N + 6 * CZ;
+    const size_t vbs = 44 * N + 6 * CZ;  // view outputs dH | dg | intrinsic columns (+ the frame sums in place)
     const size_t base = N * 64 * XS + N * 256 + N * 36 + 2 * vbs + 40 + nf * 6 * CZ + 36 * np + 8 * h->d.gframes;
     // the target corners are staged when they fit beside the rest
     const bool tg = 3 * h->K <= kTargetLds && sizeof(double) * (base + 3 * h->K) + kBuildpStaticLds <= 160 * 1024;

@@ -1249,11 +1249,11 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, nth = blockDim.x;
   const int tid = threadIdx.x;
   const int nbz = (C + 16) >> 4, CZ = 16 * nbz;
-  const int VBS = 36 * NP + 44 * N + 6 * CZ, FBS = 6 * CZ;
+  const int VBS = 44 * N + 6 * CZ, FBS = 6 * CZ;
   double* Xw = sm + wave * 64 * XS;     // [N][64][XS] view waves' Jacobian-row tiles (P_v after the SYRK)
   double* PvL = sm + N * 64 * XS;       // [2][N][128] each view's P_v[:, d] (MFMA A-operand layout), by frame parity
   double* Wv = PvL + N * 256;           // [N][36]: each view's chain G
-  double* VB = Wv + N * 36;             // [VBS] view outputs: P_i K_{i,j} [NP][36] | dH [N][36] | dg [N][8] |
+  double* VB = Wv + N * 36;             // [VBS] view outputs: dH [N][36] | dg [N][8] |
                                         //   intrinsic columns [6][CZ]
   double* FI = VB + VBS;                // [40] frame sums: H_ff ([H_fc | g_f] is summed into the view buffer's
                                         //   intrinsic-column rows, whose other columns the views leave free)
@@ -1563,9 +1563,9 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
         //   B = G from LDS), i.e. D[i][a] = P_v[a][i] with P_v = G^T H[d, :]: G^T H_dd, G^T H_dI, G^T g_d;
         //   then D's C layout is the A operand P_v[:, d] of dH = P_v G and of this camera's share P_v K_{v,j} of the
         //   baseline columns.  No LDS transposition; the chain's loads were issued before the SYRK.
-        double* dHv = vb + 36 * NP + cam * 36;
-        double* dgv = vb + 36 * NP + N * 36 + cam * 8;
-        double* Pi = vb + 36 * NP + N * 44;
+        double* dHv = vb + cam * 36;
+        double* dgv = vb + N * 36 + cam * 8;
+        double* Pi = vb + N * 44;
         const int i16 = lane & 15, k0 = lane >> 4;
         double gb[2];
 #pragma unroll
@@ -1744,44 +1744,11 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
         const int f = f0 + it - 1;
         if (fw == 0 && it <= 8) KB_TSB(d, 51 + it);
         double* VBp = ((it - 1) & 1) ? VB1 : VB;
-        double* Cb = VBp;
-        const double* dHv = VBp + 36 * NP;
-        const double* dgv = VBp + 36 * NP + N * 36;
-        double* P = VBp + 36 * NP + N * 44;  // [H_fc | g_f]: the views wrote the intrinsic columns in place
-        {
-          // each view's share of the baseline columns, P_v K_{v,j} (j < v), one 16-column tile job at a time over the
-          // frame waves: the views' A operands from LDS (their register layout), K_{v,j} from Kl
-          const double* pab = PvL + ((it - 1) & 1) * N * 128;
-          const int i16 = lane & 15, k0 = lane >> 4;
-          int job = 0;
-          for (int v = 1; v < N; ++v) {
-            const int nct = (6 * v + 15) >> 4;  // 16-column tiles of [K_{v,0} | K_{v,1} | ...]
-            const double* Kv = Kl + (v * (v - 1) / 2) * 36;
-            for (int ct = 0; ct < nct; ++ct, ++job) {
-              if (job % NF != fw) continue;  // wave-uniform
-              v4d t3 = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-              for (int st = 0; st < 2; ++st) {
-                const int k = k0 + 4 * st, c = 16 * ct + i16, cc = min(c, 6 * v - 1), jj = cc / 6, bb = cc - 6 * jj;
-                const double kv = Kv[jj * 36 + min(k, 5) * 6 + bb];
-                t3 = __builtin_amdgcn_mfma_f64_16x16x4f64(pab[v * 128 + st * 64 + lane],
-                                                          (k < 6 && c < 6 * v) ? kv : 0.0, t3, 0, 0, 0);
-              }
-              const int c = 16 * ct + i16, jj = c / 6, bb = c - 6 * jj;
-              if (c < 6 * v) {
-#pragma unroll
-                for (int r = 0; r < 2; ++r) {
-                  const int arow = k0 + 4 * r;
-                  if (arow < 6) Cb[(v * (v - 1) / 2) * 36 + jj * 36 + arow * 6 + bb] = t3[r];
-                }
-              }
-            }
-          }
-          KB_WAVE_SYNC();
-          if (lane == 0) atomicAdd(&fcnt, 1);
-          while (__hip_atomic_load(&fcnt, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < NF * (2 * it - 1))
-            __builtin_amdgcn_s_sleep(1);
-        }
+        const double* dHv = VBp;
+        const double* dgv = VBp + N * 36;
+        double* P = VBp + N * 44;  // [H_fc | g_f]: the views wrote the intrinsic columns in place
+        // the views' P_v (their MFMA A operands, entry (a, k) at register k >> 2, lane 16 (k & 3) + a)
+        const double* pab = PvL + ((it - 1) & 1) * N * 128;
         for (int q = fw * 64 + lane; q < nsum; q += 64 * NF) {
           // every term of an output is loaded at once (clamped addresses), then summed in camera order
           double v[kBuildpMaxCams];
@@ -1790,19 +1757,26 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
             const int stride = q < 36 ? 36 : 8;
 #pragma unroll
             for (int i = 0; i < kBuildpMaxCams; ++i) v[i] = src[min(i, N - 1) * stride];
-          } else {  // H_f,B_j = sum_{i > j} P_i K_{i,j} (the views' products)
-            const int e = q - 42, j = e / 36, ab2 = e % 36;
-#pragma unroll
-            for (int i = 0; i < kBuildpMaxCams; ++i) {
-              const int ii = min(max(i, j + 1), N - 1);
-              v[i] = Cb[(ii * (ii - 1) / 2 + j) * 36 + ab2];
-            }
           }
           const int e = q - 42, j = q < 42 ? -1 : e / 36, ab2 = e - 36 * j;
           double sacc = 0.0;
+          if (q < 42) {
 #pragma unroll
-          for (int i = 0; i < kBuildpMaxCams; ++i)
-            if (i > j && i < N) sacc += v[i];
+            for (int i = 0; i < kBuildpMaxCams; ++i)
+              if (i < N) sacc += v[i];
+          } else {
+            // H_f,B_j = sum_{i > j} P_i K_{i,j}: each camera's product (6 FMAs on the VALU: the MFMA pipes are busy with
+            // the views' SYRK) added in camera order
+            const int a = ab2 / 6, b = ab2 - 6 * a;
+            for (int i = j + 1; i < N; ++i) {
+              const double* pv = pab + i * 128 + a;
+              const double* kp = Kl + (i * (i - 1) / 2 + j) * 36 + b;
+              double pr = 0.0;
+#pragma unroll
+              for (int k = 0; k < 6; ++k) pr = fma(pv[(k >> 2) * 64 + 16 * (k & 3)], kp[k * 6], pr);
+              sacc += pr;
+            }
+          }
           if (q < 36) {
             Fh[q] = sacc;
             if (!gfu) d.Hff[(size_t)f * 36 + q] = sacc;
@@ -1818,8 +1792,9 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
         // the frame waves meet (an LDS counter: the view waves are in their next frame) before the elimination reads
         // every sum
         KB_WAVE_SYNC();
+        if (it == 3) KB_TSB(d, 184 + fw);
         if (lane == 0) atomicAdd(&fcnt, 1);
-        while (__hip_atomic_load(&fcnt, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < NF * 2 * it)
+        while (__hip_atomic_load(&fcnt, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < NF * it)
           __builtin_amdgcn_s_sleep(1);
       }
       if (it > 0 && fuse) {
@@ -1830,7 +1805,7 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
         int lane = threadIdx.x & 63;
         asm volatile("" : "+v"(lane));
         if (fw == 0 && it <= 8) KB_TSB(d, 20 + 4 * (it - 1));
-        double* P = (((it - 1) & 1) ? VB1 : VB) + 36 * NP + N * 44;
+        double* P = (((it - 1) & 1) ? VB1 : VB) + N * 44;
         const bool ok = frame_ldl(d, f, Fh, lam2, P, Q, CZ, lane, fw == 0, fw == 0 && it == 3);
         if (!ok && lane == 0) okl = 0;
         KB_WAVE_SYNC();

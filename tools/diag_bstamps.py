@@ -33,6 +33,10 @@ for w, o in (("wave 0", 130), ("last view wave", 160)):
         names[o + 4 * ps + 2] = f"  [{w}] f2 pass {ps} u MFMAs done"
         names[o + 4 * ps + 3] = f"  [{w}] f2 pass {ps} v MFMAs done"
     names[o + 8] = f"  [{w}] f2 expansion done"
+for w in range(4):
+    names[176 + w] = f"    [fw{w}] f2 products done"
+    names[184 + w] = f"    [fw{w}] f2 sums done"
+names[180] = "    [fw0] f2 products met"
 names[140] = "    [fw0] f2 elimination entry"
 names[141] = "    [fw0] f2 6x6 LDL^T done"
 names[142] = "    [fw0] f2 column slot 0 solved+stored"
