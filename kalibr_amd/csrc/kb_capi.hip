@@ -243,9 +243,9 @@ static size_t build_lds(kb_handle* h) {
   const int tgl = (3 * h->K <= kTargetLds ? 3 * h->K : 0) + 8 * h->d.gframes;
   if (h->build_pipe) {  // k_buildp: tiles | H | chains G | view outputs | frame sums | frame-wave buffers | K | target,
                         // poses | the second view-output buffer
-    const int np = N * (N - 1) / 2, nf = (C + 16) / 16 <= 4 ? 2 : 4;  // as build_threads
+    const int np = N * (N - 1) / 2;
     const size_t vbs = 44 * N + 6 * CZ;  // view outputs dH | dg | intrinsic columns (+ the frame sums in place)
-    const size_t base = N * 64 * XS + N * 256 + N * 36 + 2 * vbs + 40 + nf * 6 * CZ + 36 * np + 8 * h->d.gframes;
+    const size_t base = N * 64 * XS + N * 256 + N * 36 + 2 * vbs + 40 + 6 * CZ + 36 * np + 8 * h->d.gframes;
     // the target corners are staged when they fit beside the rest
     const bool tg = 3 * h->K <= kTargetLds && sizeof(double) * (base + 3 * h->K) + kBuildpStaticLds <= 160 * 1024;
     h->d.bp_tg = tg ? 1 : 0;

@@ -733,6 +733,69 @@ __device__ __forceinline__ bool frame_ldl(const KbDev& d, int f, const double* H
   return ok;
 }
 
+// frame_ldl for a column range: each of the k_buildp frame waves factors the 6 x 6 block redundantly and solves its
+// own columns c0 <= c < c1 of [H_fc | g_f] into the shared Q (the frame waves meet before the Schur tiles read it)
+__device__ __forceinline__ bool frame_ldl_cols(const KbDev& d, int f, const double* Hff, double lam2, const double* P,
+                                               double* Q, int CZ, int lane, int c0, int c1, bool stamp = false) {
+  const int C = d.C;
+  double L[6][6], Di[6];
+  if (stamp) KB_TSB(d, 140);
+  bool ok = true;
+#pragma unroll
+  for (int i = 0; i < 6; ++i)
+#pragma unroll
+    for (int j = 0; j <= i; ++j) L[i][j] = Hff[i * 6 + j] + (i == j ? lam2 : 0.0);
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    double v[6];
+#pragma unroll
+    for (int j = 0; j < k; ++j) v[j] = L[k][j] * L[j][j];
+    double dk = L[k][k];
+#pragma unroll
+    for (int j = 0; j < k; ++j) dk -= L[k][j] * v[j];
+    ok = ok && (dk > 0.0);
+    L[k][k] = dk;
+    Di[k] = recip_d(dk);
+#pragma unroll
+    for (int i = k + 1; i < 6; ++i) {
+      double s = L[i][k];
+#pragma unroll
+      for (int j = 0; j < k; ++j) s -= L[i][j] * v[j];
+      L[i][k] = s * Di[k];
+    }
+  }
+  if (stamp) KB_TSB(d, 141);
+  for (int c = c0 + lane; c < c1; c += 64) {
+    double x[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {  // L y = b
+      double s = P[i * CZ + c];
+#pragma unroll
+      for (int j = 0; j < i; ++j) s -= L[i][j] * x[j];
+      x[i] = s;
+    }
+#pragma unroll
+    for (int i = 0; i < 6; ++i) x[i] *= Di[i];
+#pragma unroll
+    for (int i = 5; i >= 0; --i) {  // L^T x = D^-1 y
+      double s = x[i];
+#pragma unroll
+      for (int j = i + 1; j < 6; ++j) s -= L[j][i] * x[j];
+      x[i] = s;
+    }
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      Q[i * CZ + c] = x[i];
+      if (c < C)
+        d.Af[((size_t)f * 6 + i) * C + c] = x[i];
+      else
+        d.bf[(size_t)f * 6 + i] = x[i];
+    }
+  }
+  if (stamp) KB_TSB(d, 142);
+  return ok;
+}
+
 // dx_f = b_f - A_f dx_c.  Lane slot sl holds column lane + 64 sl of A_f (zero beyond C); lanes 0..5 hold b_f.
 __device__ __forceinline__ void fdx_load(const KbDev& d, int f, int lane, double (&ar)[6][2], double& bq) {
   const int C = d.C;
@@ -1257,8 +1320,8 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
                                         //   intrinsic columns [6][CZ]
   double* FI = VB + VBS;                // [40] frame sums: H_ff ([H_fc | g_f] is summed into the view buffer's
                                         //   intrinsic-column rows, whose other columns the views leave free)
-  double* FB = FI + 40;                 // [NF][FBS] frame wave's [A_f | b_f]
-  double* Kl = FB + NF * FBS;           // [NP][36] K_{i,j}, j < i, at (i(i-1)/2 + j)
+  double* FB = FI + 40;                 // [FBS] the frame's [A_f | b_f] (each frame wave solves a column range)
+  double* Kl = FB + FBS;           // [NP][36] K_{i,j}, j < i, at (i(i-1)/2 + j)
   double* tg = Kl + 36 * NP;            // [n_target][3] target corners (when staged) | frame poses [gframes][8]
   __shared__ double wmx[kBuildpMaxCams + 4];
   __shared__ int okl;
@@ -1730,14 +1793,22 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
     // the frame waves are the youngest waves of their SIMDs, so age-ordered issue serves them last; their frame sums
     // and elimination are on the per-frame critical path (priority 1: configs[3] 7,187 -> 7,232 GN it/s, the 250-frame
     // shard 14,568 -> 14,750; priority 3 measured the same)
-    __builtin_amdgcn_s_setprio(1);
+#ifndef KB_FW_PRIO
+#define KB_FW_PRIO 1
+#endif
+    __builtin_amdgcn_s_setprio(KB_FW_PRIO);
     v4d acc[TT];
     int tii[TT], tjj[TT];
 #pragma unroll
     for (int t = 0; t < TT; ++t) acc[t] = v4d{0.0, 0.0, 0.0, 0.0};
     schur_tiles_assign_fw<TT>(fuse ? nbz : 0, fw, tii, tjj);
-    double* Q = FB + fw * FBS;  // this frame wave's [A_f | b_f] [6][CZ]
-    const int nsum = 42 + 36 * (N - 1);  // H_ff, g_f and the baseline columns (the intrinsic ones are in place)
+    double* Q = FB;  // [A_f | b_f] [6][CZ]
+    const int qcw = (C + NF) / NF, qc0 = fw * qcw, qc1 = min(C + 1, qc0 + qcw);  // this wave's columns
+    int mt = 0;  // frame-wave meetings so far (x NF arrivals)
+    // the baseline columns (36 (N - 1): the N - 1 - j products of column block j first, so the costliest lanes are
+    // spread over waves 0..1), then H_ff (its upper triangle, mirrored: 21 sums) and g_f on the cheapest wave: one
+    // lane per output (243 at N = 7) over the 4 frame waves; the intrinsic columns are in place
+    const int nbl = 36 * (N - 1), nsum = nbl + 27;
     for (int it = 0; it <= G; ++it) {
       if (it > 0) {
         // ---------------- phase A: sums of frame f = f0 + it - 1 over its views (camera order), the frame waves' share
@@ -1750,52 +1821,71 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
         // the views' P_v (their MFMA A operands, entry (a, k) at register k >> 2, lane 16 (k & 3) + a)
         const double* pab = PvL + ((it - 1) & 1) * N * 128;
         for (int q = fw * 64 + lane; q < nsum; q += 64 * NF) {
-          // every term of an output is loaded at once (clamped addresses), then summed in camera order
-          double v[kBuildpMaxCams];
-          if (q < 42) {
-            const double* src = q < 36 ? dHv + q : dgv + q - 36;
-            const int stride = q < 36 ? 36 : 8;
+          double sacc = 0.0;
+          if (q < nbl) {
+            // H_f,B_j = sum_{i > j} P_i K_{i,j}: each camera's product (6 FMAs on the VALU: the MFMA pipes are busy with
+            // the views' SYRK) added in camera order, two cameras' operands loaded at once (the second clamped to a
+            // valid chain and dropped past the last camera)
+            const int j = q / 36, ab2 = q - 36 * j, a = ab2 / 6, b = ab2 - 6 * a;
+            for (int i = j + 1; i < N; i += 2) {
+              const int i1 = min(i + 1, N - 1);
+              const double* pv0 = pab + i * 128 + a;
+              const double* pv1 = pab + i1 * 128 + a;
+              const double* kp0 = Kl + (i * (i - 1) / 2 + j) * 36 + b;
+              const double* kp1 = Kl + (i1 * (i1 - 1) / 2 + j) * 36 + b;
+              double x0[6], x1[6], k0[6], k1[6];
+#pragma unroll
+              for (int k = 0; k < 6; ++k) {
+                x0[k] = pv0[(k >> 2) * 64 + 16 * (k & 3)];
+                k0[k] = kp0[k * 6];
+                x1[k] = pv1[(k >> 2) * 64 + 16 * (k & 3)];
+                k1[k] = kp1[k * 6];
+              }
+              double pr0 = 0.0, pr1 = 0.0;
+#pragma unroll
+              for (int k = 0; k < 6; ++k) {
+                pr0 = fma(x0[k], k0[k], pr0);
+                pr1 = fma(x1[k], k1[k], pr1);
+              }
+              sacc += pr0;
+              if (i + 1 < N) sacc += pr1;
+            }
+            P[a * CZ + ctab[1][j] + b] = sacc;
+            if (!gfu) d.Hfc[((size_t)f * 6 + a) * C + ctab[1][j] + b] = sacc;
+          } else {
+            const int e = q - nbl;
+            int hr = 0, hc = e;  // H_ff entry (hr, hc), hr <= hc (e < 21), else g_f entry e - 21
+            if (e < 21)
+              while (hc >= 6 - hr) hc -= 6 - hr++;
+            hc += hr;
+            const double* src = e < 21 ? dHv + hr * 6 + hc : dgv + e - 21;
+            const int stride = e < 21 ? 36 : 8;
+            double v[kBuildpMaxCams];
 #pragma unroll
             for (int i = 0; i < kBuildpMaxCams; ++i) v[i] = src[min(i, N - 1) * stride];
-          }
-          const int e = q - 42, j = q < 42 ? -1 : e / 36, ab2 = e - 36 * j;
-          double sacc = 0.0;
-          if (q < 42) {
 #pragma unroll
             for (int i = 0; i < kBuildpMaxCams; ++i)
               if (i < N) sacc += v[i];
-          } else {
-            // H_f,B_j = sum_{i > j} P_i K_{i,j}: each camera's product (6 FMAs on the VALU: the MFMA pipes are busy with
-            // the views' SYRK) added in camera order
-            const int a = ab2 / 6, b = ab2 - 6 * a;
-            for (int i = j + 1; i < N; ++i) {
-              const double* pv = pab + i * 128 + a;
-              const double* kp = Kl + (i * (i - 1) / 2 + j) * 36 + b;
-              double pr = 0.0;
-#pragma unroll
-              for (int k = 0; k < 6; ++k) pr = fma(pv[(k >> 2) * 64 + 16 * (k & 3)], kp[k * 6], pr);
-              sacc += pr;
+            if (e < 21) {
+              Fh[hr * 6 + hc] = sacc;
+              Fh[hc * 6 + hr] = sacc;
+              if (!gfu) {
+                d.Hff[(size_t)f * 36 + hr * 6 + hc] = sacc;
+                d.Hff[(size_t)f * 36 + hc * 6 + hr] = sacc;
+              }
+            } else {
+              P[(e - 21) * CZ + C] = sacc;
+              d.gf[(size_t)f * 6 + e - 21] = sacc;
             }
-          }
-          if (q < 36) {
-            Fh[q] = sacc;
-            if (!gfu) d.Hff[(size_t)f * 36 + q] = sacc;
-          } else if (q < 42) {
-            P[(q - 36) * CZ + C] = sacc;
-            d.gf[(size_t)f * 6 + q - 36] = sacc;
-          } else {
-            const int a = ab2 / 6, b = ab2 % 6;
-            P[a * CZ + ctab[1][j] + b] = sacc;
-            if (!gfu) d.Hfc[((size_t)f * 6 + a) * C + ctab[1][j] + b] = sacc;
           }
         }
         // the frame waves meet (an LDS counter: the view waves are in their next frame) before the elimination reads
         // every sum
         KB_WAVE_SYNC();
         if (it == 3) KB_TSB(d, 184 + fw);
+        mt += NF;
         if (lane == 0) atomicAdd(&fcnt, 1);
-        while (__hip_atomic_load(&fcnt, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < NF * it)
-          __builtin_amdgcn_s_sleep(1);
+        while (__hip_atomic_load(&fcnt, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < mt) __builtin_amdgcn_s_sleep(1);
       }
       if (it > 0 && fuse) {
         // ---------------- frame f = it - 1 (one behind the views): elimination + Schur tiles
@@ -1806,9 +1896,14 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
         asm volatile("" : "+v"(lane));
         if (fw == 0 && it <= 8) KB_TSB(d, 20 + 4 * (it - 1));
         double* P = (((it - 1) & 1) ? VB1 : VB) + N * 44;
-        const bool ok = frame_ldl(d, f, Fh, lam2, P, Q, CZ, lane, fw == 0, fw == 0 && it == 3);
-        if (!ok && lane == 0) okl = 0;
+        const bool ok = frame_ldl_cols(d, f, Fh, lam2, P, Q, CZ, lane, qc0, qc1, fw == 0 && it == 3);
+        if (!ok && lane == 0 && fw == 0) okl = 0;
+        // the frame waves meet again before the Schur tiles read every column of Q (the next frame's elimination
+        // writes Q only after the next frame's sums meeting, which every wave reaches after its Schur tiles)
         KB_WAVE_SYNC();
+        mt += NF;
+        if (lane == 0) atomicAdd(&fcnt, 1);
+        while (__hip_atomic_load(&fcnt, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < mt) __builtin_amdgcn_s_sleep(1);
         if (fw == 0 && it <= 8) KB_TSB(d, 22 + 4 * (it - 1));
         schur_tiles_accumulate6<TT>(P, Q, CZ, tii, tjj, acc, lane);
         if (fw == 0 && it <= 8) KB_TSB(d, 23 + 4 * (it - 1));
