@@ -1614,6 +1614,7 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
           yn = d.y[k];
         }
         if (wave == 0 && it < 8) KB_TSB(d, 3 + 2 * it);
+        if (it == 3 && wave < 8) KB_TSB(d, 144 + wave);
         // f64 MFMA C/D layout: lane l, reg r -> row (l>>4) + 4r, col l&15
         v4d hv;
 #pragma unroll
@@ -1671,6 +1672,7 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
           if (arow < 6 && i16 < 6) dHv[arow * 6 + i16] = t2[r];
         }
         if (stv) KB_TSB(d, sto + 8);
+        if (it == 3 && wave < 8) KB_TSB(d, 152 + wave);
       }
       __syncthreads();
     }

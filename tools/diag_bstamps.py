@@ -37,6 +37,9 @@ for w in range(4):
     names[176 + w] = f"    [fw{w}] f2 products done"
     names[184 + w] = f"    [fw{w}] f2 sums done"
 names[180] = "    [fw0] f2 products met"
+for w in range(8):
+    names[144 + w] = f"      [view wave {w}] f3 SYRK done"
+    names[152 + w] = f"      [view wave {w}] f3 expansion done"
 names[140] = "    [fw0] f2 elimination entry"
 names[141] = "    [fw0] f2 6x6 LDL^T done"
 names[142] = "    [fw0] f2 column slot 0 solved+stored"
