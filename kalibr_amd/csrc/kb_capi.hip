@@ -57,6 +57,7 @@ int nintr_host(int m) {
 }  // namespace
 
 constexpr int kGraphPasses = 8;  // optimizer passes per captured multi-pass graph
+constexpr int kGnOneGraph = 64;  // kb_gn_launch: runs of up to this many GN passes are one graph (with the loop's end)
 constexpr int kXMaxRanks = 64;
 constexpr int kPolicyMarginal = 2;  // graph policy id of kb_optimize_marginal's passes (GN over the marginal solve)   // expanded partials: per-rank max|dx_f| slots in the image's aux area
 constexpr int kLocalMaxRanks = 16;  // kb_comm_init_local group size
@@ -122,6 +123,7 @@ struct kb_handle {
   // growth in place (kb_append_frames / kb_drop_last_frames): device capacities and host mirrors of the view layout
   int bpc = 1;                      // k_buildp blocks per CU (frames per block = ceil(F / (256 bpc)))
   int F_cap = 0, V_cap = 0, NC_cap = 0;
+  int part_rows = 0;                // rows of d.part (build blocks it holds): nblk(F) is not monotone in F
   std::vector<uint32_t> vo_host;    // [V + 1] view offsets
   std::vector<int32_t> frame_v0;    // [F + 1] first view of each frame (frame_v0[F] = V)
   size_t pcg_F = 0, rjr_F = 0, cond_n = 0;  // frame count / columns the lazily allocated buffers are sized for
@@ -150,6 +152,10 @@ struct kb_handle {
   // a run of n passes launches n / kGraphPasses full graphs and one graph of the remainder (captured on first use)
   hipGraphExec_t graphs[kGraphPasses + 1] = {};
   int graph_policy = -1;
+  // kb_gn_prepare / kb_gn_launch: the last gn_tail_n GN passes and the loop's end (the last step's back-substitution
+  // and k_post) in one graph, after gn_head passes of whole kGraphPasses graphs
+  hipGraphExec_t gn_tail = nullptr, gn_big = nullptr;  // gn_big: kGnOneGraph passes (the head of longer runs)
+  int gn_tail_n = -1, gn_head = 0;
   bool graph_failed = false;  // capture of the RCCL calls failed once: eager passes from then on
   int graph_trace_cap = 0;
   double* trace = nullptr;
@@ -221,6 +227,11 @@ static const void* pick_build(int mb, unsigned mm, bool pipe, bool wide) {
   }
 }
 
+// frames per build block for F frames
+static int gframes_for(const kb_handle* h, int F) {
+  return h->build_pipe ? (F + 256 * h->bpc - 1) / (256 * h->bpc) : (F + 511) / 512;
+}
+
 // the frame-count-dependent layout: columns, state size, build blocks (frames per block), step rows
 static void set_frame_counts(kb_handle* h) {
   KbDev& d = h->d;
@@ -229,30 +240,39 @@ static void set_frame_counts(kb_handle* h) {
   d.F = h->F;
   d.ncols = h->ncols;
   if (d.S < h->S) d.S = h->S;  // d.S: the slot stride of the [2][S] state buffer (its capacity), >= the state size
-  d.gframes = h->build_pipe ? (h->F + 256 * h->bpc - 1) / (256 * h->bpc) : (h->F + 511) / 512;
+  d.gframes = gframes_for(h, h->F);
   d.nblk = (h->F + d.gframes - 1) / d.gframes;
   d.nblk_bs = h->F;  // k_backsub: one step row per frame (one wave per frame)
 }
 
-// dynamic LDS of the build kernel (depends on the frames per block through the staged frame poses)
-// k_buildp's static LDS (control copies, chain / intrinsic table, column info, counters) is below this
+// dynamic LDS of the build kernel at `gframes` frames per block (the staged frame poses); *tg: the target corners
+// are staged in LDS too.  k_buildp's static LDS (control copies, chain / intrinsic table, column info, counters) is
+// below this
 constexpr size_t kBuildpStaticLds = 4096;
-static size_t build_lds(kb_handle* h) {
+static size_t build_lds_for(const kb_handle* h, int gframes, int* tg_out) {
   const int N = h->N, C = h->C, WPB = h->d.wpb;
   const int CZ = 16 * ((C + 16) / 16);  // [Y | z] row stride of the Schur tiles
-  const int tgl = (3 * h->K <= kTargetLds ? 3 * h->K : 0) + 8 * h->d.gframes;
+  const int tgl = (3 * h->K <= kTargetLds ? 3 * h->K : 0) + 8 * gframes;
   if (h->build_pipe) {  // k_buildp: tiles | H | chains G | view outputs | frame sums | frame-wave buffers | K | target,
                         // poses | the second view-output buffer
     const int np = N * (N - 1) / 2;
     const size_t vbs = 44 * N + 6 * CZ;  // view outputs dH | dg | intrinsic columns (+ the frame sums in place)
-    const size_t base = N * 64 * XS + N * 256 + N * 36 + 2 * vbs + 40 + 6 * CZ + 36 * np + 8 * h->d.gframes;
+    const size_t base = N * 64 * XS + N * 256 + N * 36 + 2 * vbs + 40 + 6 * CZ + 36 * np + 8 * gframes;
     // the target corners are staged when they fit beside the rest
     const bool tg = 3 * h->K <= kTargetLds && sizeof(double) * (base + 3 * h->K) + kBuildpStaticLds <= 160 * 1024;
-    h->d.bp_tg = tg ? 1 : 0;
+    if (tg_out) *tg_out = tg ? 1 : 0;
     return sizeof(double) * (base + (tg ? 3 * h->K : 0));
   }
+  if (tg_out) *tg_out = 0;
   return sizeof(double) * (WPB * 64 * XS + WPB * 256 + N * (256 + 256 + 64 + 36 + 36 + 8) + 36 + 16 * CZ +
                            18 * N * (N - 1) + tgl);
+}
+
+static size_t build_lds(kb_handle* h) { return build_lds_for(h, h->d.gframes, &h->d.bp_tg); }
+
+// the build kernel's LDS fits at F frames (checked before kb_append_frames / kb_drop_last_frames change anything)
+static bool build_lds_fits(const kb_handle* h, int F) {
+  return build_lds_for(h, gframes_for(h, F), nullptr) + (h->build_pipe ? kBuildpStaticLds : 0) <= 160 * 1024;
 }
 
 static void drop_graphs(kb_handle* h) {
@@ -260,6 +280,10 @@ static void drop_graphs(kb_handle* h) {
     if (g) hipGraphExecDestroy(g);
     g = nullptr;
   }
+  if (h->gn_tail) hipGraphExecDestroy(h->gn_tail);
+  if (h->gn_big) hipGraphExecDestroy(h->gn_big);
+  h->gn_tail = h->gn_big = nullptr;
+  h->gn_tail_n = -1;
   h->graph_policy = -1;
   h->gn_prepared = -1;  // a prepared GN launch used these graphs
 }
@@ -341,16 +365,21 @@ static int regrow(kb_handle* h, T** p, size_t n_new, size_t keep) {
 
 // the frame-count-dependent launch state after kb_append_frames / kb_drop_last_frames: LDS of the build kernel,
 // captured graphs (their kernel arguments hold the old layout), prepared loops and the per-call system
+// (the callers check build_lds_fits for the new frame count before they change the handle)
 static int relayout(kb_handle* h) {
-  set_frame_counts(h);
-  h->lds_build = build_lds(h);
-  if (h->lds_build + (h->build_pipe ? kBuildpStaticLds : 0) > 160 * 1024)
-    return fail("kb_append_frames: build-kernel LDS budget exceeded for this frame count");
-  KB_HIP(hipFuncSetAttribute(h->fn_build, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_build));
-  KB_HIP(hipFuncSetAttribute(h->fn_build_gn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_build));
   drop_graphs(h);
   unprepare(h);
   h->sys_valid = false;
+  set_frame_counts(h);
+  h->lds_build = build_lds(h);
+  // one partial row per build block: fewer frames can mean more blocks (one frame per block below 256 bpc frames,
+  // several above), so a dropped batch may need more rows than the handle was created with
+  if (h->d.nblk > h->part_rows) {
+    if (regrow(h, &h->d.part, (size_t)h->d.nblk * h->d.Wr, 0)) return -1;
+    h->part_rows = h->d.nblk;
+  }
+  KB_HIP(hipFuncSetAttribute(h->fn_build, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_build));
+  KB_HIP(hipFuncSetAttribute(h->fn_build_gn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_build));
   return 0;
 }
 
@@ -380,6 +409,13 @@ kb_handle* kb_create(const kb_layout* L) {
   }
   kb_handle* h = new kb_handle();
   h->device = L->device;
+  if (const char* e = std::getenv("KB_SCHED")) {  // measurement option: how the host waits in stream syncs
+    const unsigned fl = !std::strcmp(e, "spin") ? hipDeviceScheduleSpin
+                        : !std::strcmp(e, "yield") ? hipDeviceScheduleYield
+                        : !std::strcmp(e, "block") ? hipDeviceScheduleBlockingSync : hipDeviceScheduleAuto;
+    hipSetDevice(h->device);
+    hipSetDeviceFlags(fl);
+  }
   if (hipSetDevice(h->device) != hipSuccess || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
     fail("kb_create: cannot select device / create stream");
     delete h;
@@ -465,6 +501,7 @@ kb_handle* kb_create(const kb_layout* L) {
   rc |= h->alloc(&d.Af, 6 * (size_t)h->C * h->F);
   rc |= h->alloc(&d.bf, 6 * (size_t)h->F);
   rc |= h->alloc(&d.part, (size_t)d.nblk * d.Wr);
+  h->part_rows = d.nblk;
   rc |= h->alloc(&d.part8, (size_t)kColsumRows * d.Wtot);
   rc |= h->alloc(&d.psum_local, (size_t)d.Wtot);
   d.psum = d.psum_local;
@@ -706,15 +743,26 @@ int kb_append_frames(kb_handle* h, int32_t n_frames, int32_t n_views, int32_t n_
     if ((int)corner_id[k] >= h->K) return fail("kb_append_frames: corner_id out of range");
   KbDev& d = h->d;
   const int F1 = F0 + nf, V1 = V0 + nv, NC1 = NC0 + nc;
+  // a rejected append leaves the handle as it was: the layout is checked before anything changes, and a failed
+  // regrow below only leaves some buffers larger (their contents kept where they matter), never a new frame count
+  if (!build_lds_fits(h, F1)) return fail("kb_append_frames: build-kernel LDS budget exceeded for this frame count");
+  // buffers may move from here on: the captured graphs' arguments would hold freed ones (recaptured on next use)
+  drop_graphs(h);
+  h->sys_valid = false;
   // capacities: geometric growth, so a sequence of single-frame appends moves O(F) data in total
   if (F1 > h->F_cap) {
     const size_t fc = std::max(F1, 2 * h->F_cap), C = h->C;
-    if (regrow(h, &d.Hff, 36 * fc, 0) || regrow(h, &d.Hfc, 6 * C * fc, 0) || regrow(h, &d.gf, 6 * fc, 0) ||
-        regrow(h, &d.Af, 6 * C * fc, 0) || regrow(h, &d.bf, 6 * fc, 0) || regrow(h, &d.part, fc * d.Wr, 0) ||
-        regrow(h, &d.dx, C + 6 * fc, 0) || regrow(h, &d.rhs, C + 6 * fc, 0) || regrow(h, &d.bpart, 4 * fc, 0) ||
-        regrow(h, &d.fview, fc * N, (size_t)F0 * N) || regrow(h, &d.frame_vcam, fc * N, (size_t)F0 * N))
-      return -1;
-    d.bsrc = d.bpart;
+    const bool bad = regrow(h, &d.Hff, 36 * fc, 0) || regrow(h, &d.Hfc, 6 * C * fc, 0) || regrow(h, &d.gf, 6 * fc, 0) ||
+                     regrow(h, &d.Af, 6 * C * fc, 0) || regrow(h, &d.bf, 6 * fc, 0) ||
+                     regrow(h, &d.dx, C + 6 * fc, 0) || regrow(h, &d.rhs, C + 6 * fc, 0) ||
+                     regrow(h, &d.bpart, 4 * fc, 0) || regrow(h, &d.fview, fc * N, (size_t)F0 * N) ||
+                     regrow(h, &d.frame_vcam, fc * N, (size_t)F0 * N);
+    d.bsrc = d.bpart;  // whether or not every buffer grew: bsrc never points at a freed one
+    if (bad) return -1;
+    if ((size_t)h->part_rows < fc) {
+      if (regrow(h, &d.part, fc * d.Wr, 0)) return -1;
+      h->part_rows = (int)fc;
+    }
     d.bsrc_rows = (int)fc;  // rows beyond F are never read (k_post reduces nblk_bs = F rows)
     h->F_cap = (int)fc;
   }
@@ -792,6 +840,7 @@ int kb_drop_last_frames(kb_handle* h, int32_t n_frames) {
   if (n_frames < 1 || n_frames >= h->F) return fail("kb_drop_last_frames: must keep at least one frame");
   KB_HIP(hipSetDevice(h->device));
   const int F1 = h->F - n_frames, V1 = h->frame_v0[F1], NC1 = (int)h->vo_host[V1];
+  if (!build_lds_fits(h, F1)) return fail("kb_drop_last_frames: build-kernel LDS budget exceeded for this frame count");
   h->F = F1;
   h->V = V1;
   h->NC = NC1;
@@ -1650,6 +1699,26 @@ int kb_get_trace(kb_handle* h, double* trace, int32_t cap) {
   return n;
 }
 
+// `passes` GN passes (+ the loop's end when `with_end`) captured as one graph
+static int capture_gn(kb_handle* h, int passes, bool with_end, hipGraphExec_t* out) {
+  hipGraph_t g = nullptr;
+  KB_HIP(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
+  int rc = 0;
+  for (int i = 0; i < passes && !rc; ++i) rc = enqueue_pass(h, 1);
+  if (!rc && with_end) rc = finish_pass(h, 1);
+  const hipError_t e = hipStreamEndCapture(h->stream, &g);
+  if (rc) {
+    if (g) hipGraphDestroy(g);
+    return rc;
+  }
+  if (e != hipSuccess) return fail(std::string("hipStreamEndCapture: ") + hipGetErrorString(e));
+  const hipError_t ei = hipGraphInstantiate(out, g, nullptr, nullptr, 0);
+  hipGraphDestroy(g);
+  if (ei != hipSuccess) return fail(std::string("hipGraphInstantiate: ") + hipGetErrorString(ei));
+  KB_HIP(hipGraphUpload(*out, h->stream));
+  return 0;
+}
+
 int kb_gn_prepare(kb_handle* h, int32_t n_iter) {
   if (!h || n_iter < 0) return fail("kb_gn_prepare: bad args");
   if (!h->uploaded) return fail("kb_gn_prepare: no observations");
@@ -1658,17 +1727,28 @@ int kb_gn_prepare(kb_handle* h, int32_t n_iter) {
   // GN, convergence tests disabled (thresholds -1 keep (dX > eps && |dJ| > eps) true)
   KbOpts o{1, 0x3fffffff, 0.0, -1.0, -1.0};
   h->gn_graph = graph_ok(h, 1);
-  hipGraphExec_t gr = nullptr;
-  if (h->gn_graph && n_iter % kGraphPasses && graph_of(h, n_iter % kGraphPasses, &gr)) return -1;
   if (h->gn_graph) {
+    // up to kGnOneGraph passes run as one graph with the loop's end (the last step's back-substitution and k_post)
+    // captured behind them: no graph-to-graph gap and no eager launch inside the timed region.  Longer runs launch
+    // whole kGnOneGraph-pass graphs first and the last 1..kGnOneGraph passes with the end as the tail graph.
+    const int t = n_iter <= kGnOneGraph ? n_iter : (n_iter % kGnOneGraph ? n_iter % kGnOneGraph : kGnOneGraph);
+    if (n_iter > t && !h->gn_big && capture_gn(h, kGnOneGraph, false, &h->gn_big)) return -1;
+    if (h->gn_tail_n != t) {
+      if (h->gn_tail) hipGraphExecDestroy(h->gn_tail);
+      h->gn_tail = nullptr;
+      h->gn_tail_n = -1;
+      if (capture_gn(h, t, true, &h->gn_tail)) return -1;
+      h->gn_tail_n = t;
+    }
+    h->gn_head = n_iter - t;
     // every graph the timed launch will use runs once here, from a snapshot that is restored afterwards: a graph's
     // first launch costs more than the later ones (measured ~0.2 ms per kb_gn_launch at configs[3] when the 8-pass graph
     // was first launched inside it), and that is set-up, not pass time.  Sharded: every rank prepares the same n_iter,
     // so the captured collectives of these launches are matched across the ranks.
     Snapshot snap(h);
     if (snap.take() || loop_start(h, o)) return -1;
-    if (n_iter >= kGraphPasses) KB_HIP(hipGraphLaunch(h->graphs[kGraphPasses], h->stream));
-    if (gr) KB_HIP(hipGraphLaunch(gr, h->stream));
+    if (h->gn_head > 0) KB_HIP(hipGraphLaunch(h->gn_big, h->stream));
+    KB_HIP(hipGraphLaunch(h->gn_tail, h->stream));
     if (snap.restore()) return -1;
     KB_HIP(hipStreamSynchronize(h->stream));
     snap.taken = false;
@@ -1685,11 +1765,38 @@ int kb_gn_launch(kb_handle* h, int32_t n_iter, double* seconds) {
   h->gn_prepared = -1;
   KB_HIP(hipSetDevice(h->device));
   const bool graph = h->gn_graph;
+  if (graph && (!h->gn_tail || h->gn_head + h->gn_tail_n != n_iter))
+    return fail("kb_gn_launch: the prepared graphs do not cover this pass count");
+  // KB_LAUNCH_DIAG=1 (diagnostics only): HIP events around the launches, and the host time to return from the
+  // launches and from the sync, printed to stderr
+  static const bool diag = std::getenv("KB_LAUNCH_DIAG") != nullptr;
+  hipEvent_t de[2] = {nullptr, nullptr};
+  if (diag) {
+    KB_HIP(hipEventCreate(&de[0]));
+    KB_HIP(hipEventCreate(&de[1]));
+    KB_HIP(hipEventRecord(de[0], h->stream));
+  }
   const auto t0 = std::chrono::steady_clock::now();
-  if (launch_passes(h, 1, n_iter, graph)) return -1;
-  if (finish_pass(h, 1)) return -1;
+  if (graph) {
+    for (int i = 0; i < h->gn_head; i += kGnOneGraph) KB_HIP(hipGraphLaunch(h->gn_big, h->stream));
+    KB_HIP(hipGraphLaunch(h->gn_tail, h->stream));
+  } else {
+    if (launch_passes(h, 1, n_iter, false)) return -1;
+    if (finish_pass(h, 1)) return -1;
+  }
+  const auto tl = std::chrono::steady_clock::now();
+  if (diag) KB_HIP(hipEventRecord(de[1], h->stream));
   KB_HIP(hipStreamSynchronize(h->stream));
   const auto t1 = std::chrono::steady_clock::now();
+  if (diag) {
+    float ms = 0.f;
+    hipEventElapsedTime(&ms, de[0], de[1]);
+    std::fprintf(stderr, "kb_gn_launch n=%d graph=%d host_launch_us=%.1f host_total_us=%.1f dev_span_us=%.1f\n", n_iter,
+                 graph ? 1 : 0, 1e6 * std::chrono::duration<double>(tl - t0).count(),
+                 1e6 * std::chrono::duration<double>(t1 - t0).count(), 1e3 * ms);
+    hipEventDestroy(de[0]);
+    hipEventDestroy(de[1]);
+  }
   if (seconds) *seconds = std::chrono::duration<double>(t1 - t0).count();
   KbCtrl ctrl{};
   KB_HIP(hipMemcpy(&ctrl, h->d.ctrl, sizeof(KbCtrl), hipMemcpyDeviceToHost));
@@ -1838,10 +1945,11 @@ int kb_build_kernel_stats(kb_handle* h, double* avg_ms, double* bytes_per_launch
                        8.0 * h->d.nblk * h->d.Wr;
   if (bytes_per_launch) *bytes_per_launch = bytes;
   // algorithmic FP64 flops of one pass's build (SURVEY.md 8(d) "Algorithmic FLOPs"), not the executed (padded) MFMA
-  // work: per corner ~150 (projection + Jacobian) + ~100 (the cost pass the reference runs) + ~480 (local Hessian and
-  // gradient); per view of camera i (i baselines in its chain) the 6-D adjoint expansion 2 (6 i + 6 + n_intr)^2 6; per
-  // frame the Schur sums H_fc^T [A_f | b_f] 2 * 6 * C^2 + the 6 x 6 factorisation 6^3
-  double fl = 730.0 * h->NC + F * (2.0 * 6.0 * C * C + 216.0);
+  // work, and only the terms this kernel performs: per corner ~150 (projection + Jacobian; the candidate's chi^2 reuses
+  // the residual, so SURVEY's separate ~100-flop cost pass is not counted) + ~480 (local Hessian and gradient); per view
+  // of camera i (i baselines in its chain) the 6-D adjoint expansion 2 (6 i + 6 + n_intr)^2 6; per frame the Schur sums
+  // H_fc^T [A_f | b_f] 2 * 6 * C^2 + the 6 x 6 factorisation 6^3
+  double fl = 630.0 * h->NC + F * (2.0 * 6.0 * C * C + 216.0);
   for (int v = 0; v < h->V; ++v) {
     const int i = h->vcam[v];
     const double m = 6.0 * i + 6.0 + h->d.nintr[i];

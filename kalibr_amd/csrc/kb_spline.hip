@@ -2417,6 +2417,14 @@ struct kb_sp_handle {
     *p = (T*)q;
     return 0;
   }
+  // free a buffer alloc() made (nullptr: no-op); the stream must be idle with respect to it
+  void release(const void* p) {
+    if (!p) return;
+    auto it = std::find(allocs.begin(), allocs.end(), const_cast<void*>(p));
+    if (it == allocs.end()) return;
+    allocs.erase(it);
+    hipFree(const_cast<void*>(p));
+  }
 };
 
 namespace {
@@ -2991,11 +2999,22 @@ int kb_sp_set_position_priors(kb_sp_handle* h, int32_t n, const double* times, c
     h->gn_graph = nullptr;
   }
   SpDev& d = h->d;
-  if (n == 0) {
+  // the previous call's prior tables go (repeated calls do not accumulate device buffers)
+  auto drop_priors = [&]() -> int {
+    KSP_HIP(hipStreamSynchronize(h->stream));
+    h->release(d.pb);
+    h->release(d.pw);
+    h->release(d.pp);
+    h->release(d.pW);
+    h->release(d.node_pp);
+    d.pb = nullptr;
+    d.pw = d.pp = d.pW = nullptr;
+    d.node_pp = nullptr;
     d.npos = 0;
     d.cq = d.mot;
     return 0;
-  }
+  };
+  if (n == 0) return drop_priors();
   // per prior: first coefficient and value weights (BSpline::evalDAndJacobian(t, 0)), invR = N^-1 (ErrorTermEuclidean's
   // first constructor, ErrorTermEuclidean.cpp:10-23: setInvR(N.inverse())); sorted by first coefficient, then time
   std::vector<int> ord(n), b(n);
@@ -3010,7 +3029,9 @@ int kb_sp_set_position_priors(kb_sp_handle* h, int32_t n, const double* times, c
           return fail("kb_sp_set_position_priors: N must be symmetric");
     const double c00 = M[4] * M[8] - M[5] * M[7], c01 = M[5] * M[6] - M[3] * M[8], c02 = M[3] * M[7] - M[4] * M[6];
     const double det = M[0] * c00 + M[1] * c01 + M[2] * c02;
-    if (!(det > 0.0) || !(M[0] > 0.0)) return fail("kb_sp_set_position_priors: N must be positive definite");
+    // Sylvester: all three leading principal minors positive (diag(1, -1, -1) has det > 0 and M00 > 0)
+    if (!(M[0] > 0.0) || !(M[0] * M[4] - M[1] * M[3] > 0.0) || !(det > 0.0))
+      return fail("kb_sp_set_position_priors: N must be positive definite");
     double* I = &W[9 * (size_t)k];  // adjugate / det
     I[0] = c00 / det;
     I[1] = (M[2] * M[7] - M[1] * M[8]) / det;
@@ -3042,6 +3063,7 @@ int kb_sp_set_position_priors(kb_sp_handle* h, int32_t n, const double* times, c
   }
   int *dpb = nullptr, *dnp = nullptr;
   double *dpw = nullptr, *dpp = nullptr, *dpW = nullptr;
+  if (drop_priors()) return -1;  // inputs validated: the old tables are replaced
   if (h->alloc(&dpb, n) || h->alloc(&dpw, 4 * (size_t)n) || h->alloc(&dpp, 3 * (size_t)n) ||
       h->alloc(&dpW, 9 * (size_t)n) || h->alloc(&dnp, npp.size()))
     return -1;

@@ -17,6 +17,7 @@ import struct
 import time
 
 _MAGIC = b"KBRDZV01"
+_MAX_HELLO = len(_MAGIC) + 16  # magic + a decimal rank id
 
 
 def _send(sock, data: bytes):
@@ -105,7 +106,12 @@ class TcpGroup:
         """the rank id of a client's hello, or None for anything else (a foreign service, a malformed or truncated
         hello, a rank outside 1..world-1)"""
         try:
-            hello = _recv(c)
+            (n,) = struct.unpack("<Q", _recv_exact(c, 8))
+            # a hello is the magic and a rank id: an unframed foreign client's first bytes read as a huge length,
+            # which is refused before anything is allocated for it
+            if n > _MAX_HELLO:
+                return None
+            hello = _recv_exact(c, n)
         except (OSError, ConnectionError, struct.error):
             return None
         if not hello.startswith(_MAGIC):

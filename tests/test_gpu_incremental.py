@@ -71,6 +71,21 @@ def test_append_and_drop_match_fresh_handles(capi, cfg, nf, first, chunk, pv):
     assert np.array_equal(g.get_state(), full.get_state())
 
 
+def test_drop_on_fresh_handle_across_frames_per_block(capi):
+    """a freshly created handle dropped across a change of the build's frames per block: configs[3]'s rig at 300 frames
+    runs 150 build blocks of 2 frames, at 256 frames 256 blocks of one, so the handle needs more partial rows than it
+    was created with (they are regrown) and matches a fresh 256-frame handle bitwise"""
+    p = synth.make_config(4, n_frames=300)
+    g, _ = _fresh(capi, p, 300)
+    g.drop_last_frames(44)
+    ref, sub = _fresh(capi, p, 256)
+    g.set_state(sub.state_init)
+    _same(g, ref, "dropped 300 -> 256")
+    g.run_gn(2)
+    ref.run_gn(2)
+    assert np.array_equal(g.get_state(), ref.get_state())
+
+
 def test_append_validation(capi):
     p = synth.make_config(2, n_frames=8)
     g, _ = _fresh(capi, p, 4)

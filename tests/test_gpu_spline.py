@@ -291,7 +291,16 @@ def test_position_prior_removed_and_bad_input(prior_case):
         g.set_position_priors(pri[0] + 1e3, pri[1], pri[2])
     with pytest.raises(capi.KbError):  # not positive definite
         g.set_position_priors(pri[0], pri[1], -pri[2])
+    # det > 0 and N00 > 0, but indefinite: diag(1, -1, -1) (the 2 x 2 leading minor is negative)
+    indef = np.broadcast_to(np.diag([1.0, -1.0, -1.0]), pri[2].shape).copy()
+    with pytest.raises(capi.KbError):
+        g.set_position_priors(pri[0], pri[1], indef)
+    # repeated calls replace the prior tables (no accumulation, same system)
     g.set_position_priors(*pri)
+    J1 = g.eval_cost()
+    for _ in range(3):
+        g.set_position_priors(*pri)
+    assert g.eval_cost() == J1
 
 
 def test_deep_level_kernel_parity(case, monkeypatch):

@@ -3,6 +3,7 @@ ranks, world sizes 1 and 3, rank processes started out of order (CPU)."""
 import multiprocessing as mp
 import socket
 import struct
+import time
 
 from kalibr_amd import rdzv
 
@@ -48,8 +49,9 @@ def test_world_one_is_local():
     assert g.max(2.0) == 2.0
 
 
-def _raw_client(port, payload, q, tag):
-    """a client that sends one framed hello and reports whether rank 0 answered with the handshake"""
+def _raw_client(port, payload, q, tag, framed=True):
+    """a client that sends one hello (framed with its length, or the raw bytes of a foreign protocol) and reports
+    whether rank 0 answered with the handshake"""
     import time as _t
     deadline = _t.monotonic() + 30.0
     while True:
@@ -63,7 +65,7 @@ def _raw_client(port, payload, q, tag):
             _t.sleep(0.1)
     s.settimeout(10.0)
     try:
-        s.sendall(struct.pack("<Q", len(payload)) + payload)
+        s.sendall((struct.pack("<Q", len(payload)) if framed else b"") + payload)
         r = s.recv(64)
         q.put((tag, "reply" if r else "closed"))
     except OSError:
@@ -91,7 +93,11 @@ def test_bad_hello_and_duplicate_rank_are_refused():
     bad = [(rdzv._MAGIC + b"x1", "malformed"), (rdzv._MAGIC + b"7", "out of range"), (b"GET / HTTP/1.0", "foreign")]
     for payload, tag in bad:
         _raw_client(port, payload, q, tag)
-    got = dict(q.get(timeout=30) for _ in bad)
+    # unframed: 'GET / HT' reads as a ~6e18-byte length, which must be refused at once (no allocation, no wait)
+    t_raw = time.monotonic()
+    _raw_client(port, b"GET / HTTP/1.1\r\nHost: x\r\n\r\n", q, "unframed", framed=False)
+    got = dict(q.get(timeout=30) for _ in range(len(bad) + 1))
+    assert time.monotonic() - t_raw < 5.0
     assert all(v == "closed" for v in got.values()), got
 
     out = {}
