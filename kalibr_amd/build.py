@@ -43,6 +43,7 @@ def build(force=False):
 
 HOST_SRC = os.path.join(HERE, "host", "kalibr_backend.cpp")
 HOST_IO_SRC = os.path.join(HERE, "host", "calibration_io.cpp")
+HOST_TOOLS_SRC = os.path.join(HERE, "host", "calibration_tools.cpp")
 HOST_OUT = os.path.join(HERE, "libkalibr_backend.so")
 INCLUDE = os.path.join(HERE, "..", "include")
 CXX = os.environ.get("CXX", "g++")
@@ -51,10 +52,10 @@ CXX = os.environ.get("CXX", "g++")
 def build_host(force=False):
     """C++ host layer (LinearSystemSolver / TrustRegionPolicy / Optimizer2 mirror, observation packing and YAML
     export) linked to libkalibr_hip.so."""
-    deps = [HOST_SRC, HOST_IO_SRC, os.path.join(HERE, "host", "kalibr_backend.hpp"),
-            os.path.join(HERE, "host", "calibration_io.hpp"), OUT]
+    deps = [HOST_SRC, HOST_IO_SRC, HOST_TOOLS_SRC, os.path.join(HERE, "host", "kalibr_backend.hpp"),
+            os.path.join(HERE, "host", "calibration_io.hpp"), os.path.join(HERE, "host", "calibration_tools.hpp"), OUT]
     if force or not os.path.exists(HOST_OUT) or any(os.path.getmtime(p) > os.path.getmtime(HOST_OUT) for p in deps):
-        cmd = [CXX, "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-I", INCLUDE, "-o", HOST_OUT + ".tmp", HOST_SRC, HOST_IO_SRC,
+        cmd = [CXX, "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-I", INCLUDE, "-o", HOST_OUT + ".tmp", HOST_SRC, HOST_IO_SRC, HOST_TOOLS_SRC,
                "-L", HERE, "-lkalibr_hip", "-Wl,-rpath,$ORIGIN"]
         subprocess.run(cmd, check=True)
         os.replace(HOST_OUT + ".tmp", HOST_OUT)

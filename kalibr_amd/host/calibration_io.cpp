@@ -58,6 +58,9 @@ std::array<double, 9> Transformation::C() const { return quat2r(q); }
 Transformation Transformation::operator*(const Transformation& rhs) const {
   Transformation out;
   out.q = qplus(q, rhs.q);
+  // Transformation(q, t) normalises its quaternion (Transformation.cpp:31-35)
+  const double qn = std::sqrt(out.q[0] * out.q[0] + out.q[1] * out.q[1] + out.q[2] * out.q[2] + out.q[3] * out.q[3]);
+  for (double& v : out.q) v /= qn;
   const std::array<double, 9> R = C();
   for (int r = 0; r < 3; ++r) out.t[r] = R[3 * r] * rhs.t[0] + R[3 * r + 1] * rhs.t[1] + R[3 * r + 2] * rhs.t[2] + t[r];
   return out;

@@ -24,7 +24,7 @@ namespace io {
 struct Transformation {
   std::array<double, 4> q{0.0, 0.0, 0.0, 1.0};
   std::array<double, 3> t{0.0, 0.0, 0.0};
-  /// operator* (Transformation.cpp:95-98): q = qplus(q_a, q_b), t = C(q_a) t_b + t_a
+  /// operator* (Transformation.cpp:95-98): q = qplus(q_a, q_b) normalised, t = C(q_a) t_b + t_a
   Transformation operator*(const Transformation& rhs) const;
   /// the rotation matrix (quat2r, quaternion_algebra.cpp:77-101), row-major
   std::array<double, 9> C() const;

@@ -607,7 +607,12 @@ SolutionReturnValue Optimizer2::optimize() {
 }
 
 SolutionReturnValue Optimizer2::optimizeOnDevice(int syncEvery) {
-  auto gpu = std::dynamic_pointer_cast<GpuLinearSystemSolver>(_options.linearSystemSolver);
+  // the GPU solver itself, or behind the design-variable / error-term layer (the device runs the canonical problem;
+  // the caller pulls the optimised values into its design variables)
+  GpuLinearSystemSolver* gpu = dynamic_cast<GpuLinearSystemSolver*>(_options.linearSystemSolver.get());
+  if (!gpu)
+    if (auto* ts = dynamic_cast<TermLinearSystemSolver*>(_options.linearSystemSolver.get()))
+      gpu = dynamic_cast<GpuLinearSystemSolver*>(&ts->inner());
   if (!gpu) throw Exception("optimizeOnDevice: the linear system solver is not a GpuLinearSystemSolver");
   auto policy = _options.trustRegionPolicy;
   if (!policy) throw Exception("The trust region policy is null");

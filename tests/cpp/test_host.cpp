@@ -21,6 +21,13 @@
 //                                                 intrinsics vs the state's T_t_c; initializeIntrinsics of each camera
 //   test_host io <problem.bin> <outdir> 0       : observation records -> buildRigProblem (must rebuild the packed
 //                                                 problem), targetPoseGuess per frame, exportCalibration YAML
+//   test_host tools-unit x x x                  : median, rotation vectors, getTransform, synchronized sets, camera
+//                                                 graph and Dijkstra of calibration_tools on hand-made inputs
+//   test_host pipeline <problem.bin> <outdir> cpu|gpu|gpu-host : the kalibr_calibrate_cameras stage sequence
+//                                                 (calibration_tools: single camera, sync, camera graph, stereo
+//                                                 pairs, rig, incremental estimator, YAML export) from per-camera
+//                                                 observation lists over the oracle (cpu) or the GPU solvers
+//                                                 (gpu: device-resident loops; gpu-host: host-driven Optimizer2)
 // Prints one JSON line.  The oracle is test infrastructure only (oracle/kb_oracle.h).
 #include <algorithm>
 #include <cfloat>
@@ -36,6 +43,7 @@
 #include <vector>
 
 #include "calibration_io.hpp"
+#include "calibration_tools.hpp"
 #include "kalibr_backend.hpp"
 #include "kalibr_hip.h"
 #include "kb_oracle.h"
@@ -802,16 +810,222 @@ static int run_io(const CalibrationProblem& p, const std::string& outdir) {
   return 0;
 }
 
+// ---------------------------------------------------------------- the calibration stage sequence (calibration_tools)
+static std::string jv(const double* v, size_t n) {
+  std::string s = "[";
+  char buf[40];
+  for (size_t i = 0; i < n; ++i) {
+    std::snprintf(buf, sizeof buf, "%s%.17g", i ? ", " : "", v[i]);
+    s += buf;
+  }
+  return s + "]";
+}
+static std::string jv(const std::vector<double>& v) { return jv(v.data(), v.size()); }
+static std::string jT(const kalibr_amd::io::Transformation& T) {
+  const double v[7] = {T.q[0], T.q[1], T.q[2], T.q[3], T.t[0], T.t[1], T.t[2]};
+  return jv(v, 7);
+}
+
+// per-camera observation lists of the packed problem, time-stamped f * 0.1 s + c * 1 ms.  With three cameras the views
+// are thinned so that the camera graph is the chain 0 - 1 - 2: frames f % 12 < 5 drop camera 2, 5 <= f % 12 < 10 drop
+// camera 0 (camera 1 sees every set; cameras 0 and 2 share only the remaining frames)
+static std::vector<std::vector<kalibr_amd::io::GridObservation>> observations_by_camera(const CalibrationProblem& p,
+                                                                                      size_t W, size_t H) {
+  namespace io = kalibr_amd::io;
+  const size_t N = p.n_cams(), K = p.n_target();
+  std::vector<std::vector<io::GridObservation>> out(N);
+  for (int v = 0; v < p.n_views(); ++v) {
+    const size_t f = p.view_frame[v], c = p.view_cam[v];
+    if (N == 3 && ((f % 12 < 5 && c == 2) || (f % 12 >= 5 && f % 12 < 10 && c == 0))) continue;
+    io::GridObservation o(K);
+    o.imCols = W;
+    o.imRows = H;
+    o.time = 0.1 * (double)f + 0.001 * (double)c;
+    for (uint32_t k = p.view_offset[v]; k < p.view_offset[v + 1]; ++k)
+      o.updateImagePoint(p.corner_id[k], p.y[2 * k], p.y[2 * k + 1]);
+    out[c].push_back(o);
+  }
+  return out;
+}
+
+static int run_pipeline(const CalibrationProblem& p, const std::string& outdir, const std::string& kind) {
+  namespace io = kalibr_amd::io;
+  namespace tl = kalibr_amd::tools;
+  const size_t N = p.n_cams();
+  io::AprilgridTarget tgt;
+  const auto byCam = observations_by_camera(p, 1280, 1024);
+  tl::StageOptions so;
+  LinearSolverOptions lo;
+  lo.columnScaling = true;  // CalibrateCameras.cpp:263-267
+  lo.epsSVD = 1e-6;
+  std::shared_ptr<MarginalLinearSystemSolver> est;
+  if (kind == "cpu") {
+    so.solver = []() -> std::shared_ptr<ProblemLinearSystemSolver> { return std::make_shared<OracleProblemSolver>(); };
+    est = std::make_shared<OracleMarginalSolver>(lo, 4);
+  } else {
+    so.solver = []() -> std::shared_ptr<ProblemLinearSystemSolver> { return std::make_shared<GpuLinearSystemSolver>(); };
+    so.deviceLoop = kind == "gpu";
+    auto g = std::make_shared<GpuMarginalLinearSolver>(lo);
+    g->deviceLoop = kind == "gpu";
+    est = g;
+  }
+  tl::CalibrateCamerasOptions co;
+  co.focalLengths.assign(N, std::nullopt);
+  const auto t0 = std::chrono::steady_clock::now();
+  const tl::CalibrateCamerasResult r = tl::calibrateCameras(p.cam_model, byCam, tgt, co, so, est);
+  const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  std::vector<std::string> names;
+  std::vector<std::pair<size_t, size_t>> sizes;
+  for (size_t i = 0; i < N; ++i) {
+    names.push_back("cam" + std::to_string(i));
+    sizes.emplace_back(1280, 1024);
+  }
+  const auto files = io::exportCalibration(outdir, names, p.cam_model, sizes, r.finalState);
+  auto cams = [](const std::vector<tl::CameraCalibrator>& c) {
+    std::string s = "[";
+    for (size_t i = 0; i < c.size(); ++i) s += (i ? ", " : "") + jv(c[i].intrinsics);
+    return s + "]";
+  };
+  auto trs = [](const std::vector<io::Transformation>& t) {
+    std::string s = "[";
+    for (size_t i = 0; i < t.size(); ++i) s += (i ? ", " : "") + jT(t[i]);
+    return s + "]";
+  };
+  auto stages = [](const std::vector<tl::StageResult>& v) {
+    std::string s = "[";
+    for (size_t i = 0; i < v.size(); ++i) {
+      const double a[7] = {(double)v[i].ret.iterations, (double)v[i].ret.failedIterations, v[i].ret.JStart,
+                           v[i].ret.JFinal, (double)v[i].frames, (double)v[i].views, (double)v[i].terms};
+      s += (i ? ", " : "") + jv(a, 7);
+    }
+    return s + "]";
+  };
+  std::vector<double> prev(r.graphSearch.previous.begin(), r.graphSearch.previous.end());
+  std::vector<double> pairs;
+  for (const auto& pr : r.stereoPairs) {
+    pairs.push_back((double)pr.first);
+    pairs.push_back((double)pr.second);
+  }
+  size_t with[8] = {0};
+  for (const auto& s : r.syncedSets) {
+    size_t n = 0;
+    for (const auto& o : s) n += o ? 1 : 0;
+    with[std::min<size_t>(n, 7)]++;
+  }
+  const std::vector<double> withv(with, with + 8);
+  std::vector<double> acc(r.batchAccepted.begin(), r.batchAccepted.end()), its(r.batchIterations.begin(), r.batchIterations.end()),
+      rk(r.batchRank.begin(), r.batchRank.end());
+  const std::vector<double> calib(r.finalState.begin(), r.finalState.begin() + (long)(N * KB_MAX_INTR + 7 * (N - 1)));
+  std::printf(
+      "{\"seconds\": %.4f, \"n_sets\": %zu, \"cams_per_set\": %s, \"distance\": %s, \"previous\": %s, \"pairs\": %s, "
+      "\"single\": %s, \"after_single\": %s, \"stereo\": %s, \"after_stereo\": %s, \"optimal\": %s, "
+      "\"baseline_guesses\": %s, \"rig\": %s, \"rig_baselines\": %s, \"after_rig\": %s, \"accepted\": %s, "
+      "\"batch_iterations\": %s, \"batch_rank\": %s, \"accepted_batches\": %zu, \"final_calibration\": %s, "
+      "\"final_baselines\": %s, \"final_frames\": %zu, \"files\": %zu}\n",
+      secs, r.syncedSets.size(), jv(withv).c_str(), jv(r.graphSearch.distance).c_str(), jv(prev).c_str(),
+      jv(pairs).c_str(), stages(r.single).c_str(), cams(r.afterSingle).c_str(), stages(r.stereo).c_str(),
+      cams(r.afterStereo).c_str(),
+      [&]() {
+        std::vector<io::Transformation> t;
+        for (const auto& pr : r.stereoPairs) t.push_back(r.optimalBaselines.at(pr));
+        return trs(t);
+      }().c_str(),
+      trs(r.baselineGuesses).c_str(), stages({r.rig}).c_str(), trs(r.rigBaselines).c_str(), cams(r.afterRig).c_str(),
+      jv(acc).c_str(), jv(its).c_str(), jv(rk).c_str(), r.acceptedBatches, jv(calib).c_str(),
+      trs(r.finalBaselines).c_str(), (r.finalState.size() - calib.size()) / 7, files.size());
+  return 0;
+}
+
+// the graph / sync / median / rotation-vector helpers of calibration_tools on hand-made inputs (tests/test_pipeline.py
+// recomputes every value independently)
+static int run_tools_unit() {
+  namespace io = kalibr_amd::io;
+  namespace tl = kalibr_amd::tools;
+  std::string o = "{";
+  o += "\"median_odd\": " + std::to_string(tl::median({3.0, 1.0, 2.0})) + ", \"median_even\": " +
+       std::to_string(tl::median({3.0, 1.0, 2.0, 5.0}));
+  // rotation vectors: C(p) and the round trip
+  const double ps[4][3] = {{0.1, -0.2, 0.3}, {1e-9, 0.0, 0.0}, {2.5, 0.3, -0.4}, {0.0, 0.0, 0.0}};
+  o += ", \"rv\": [";
+  for (int k = 0; k < 4; ++k) {
+    const auto C = tl::parametersToRotationMatrix({ps[k][0], ps[k][1], ps[k][2]});
+    const auto q = tl::rotationMatrixToParameters(C);
+    std::vector<double> v(C.begin(), C.end());
+    v.insert(v.end(), q.begin(), q.end());
+    o += (k ? ", " : "") + jv(v);
+  }
+  o += "]";
+  // transformations of a hand-made tree 0 <- 2 <- 1 (previous = [0, 2, 0]) and a star 0 <- 1, 0 <- 2
+  io::Transformation Ta, Tb;
+  Ta.q = {0.1, -0.05, 0.02, 0.0};
+  Ta.q[3] = std::sqrt(1 - 0.1 * 0.1 - 0.05 * 0.05 - 0.02 * 0.02);
+  Ta.t = {0.12, -0.01, 0.02};
+  Tb.q = {-0.03, 0.08, 0.01, 0.0};
+  Tb.q[3] = std::sqrt(1 - 0.03 * 0.03 - 0.08 * 0.08 - 0.01 * 0.01);
+  Tb.t = {-0.2, 0.05, 0.01};
+  std::map<std::pair<size_t, size_t>, io::Transformation> m{{{1, 2}, Ta}, {{2, 0}, Tb}};
+  tl::DijkstraResult tree;
+  tree.distance = {0.0, 2.0, 1.0};
+  tree.previous = {0, 2, 0};
+  o += ", \"Ta\": " + jT(Ta) + ", \"Tb\": " + jT(Tb) + ", \"T01\": " + jT(tl::getTransform(m, tree, 0, 1)) +
+       ", \"T10\": " + jT(tl::getTransform(m, tree, 1, 0)) + ", \"T21\": " + jT(tl::getTransform(m, tree, 2, 1)) +
+       ", \"inv_Ta\": " + jT(tl::inverse(Ta)) + ", \"Ta_Tb\": " + jT(Ta * Tb);
+  tl::DijkstraResult star;
+  star.distance = {0.0, 1.0, 1.5};
+  star.previous = {0, 0, 0};
+  int star_throws = 0;
+  try {
+    tl::getTransform({{{1, 0}, Ta}, {{2, 0}, Tb}}, star, 1, 2);
+  } catch (const std::exception&) {
+    star_throws = 1;
+  }
+  o += ", \"star_throws\": " + std::to_string(star_throws);
+  // synchronized sets: camera c's observation times, tolerance 0.02; each observation marks corner (c * 10 + i)
+  const std::vector<std::vector<double>> times{{0.0, 0.1, 0.25, 0.4}, {0.005, 0.1, 0.3}, {0.03, 0.26, 0.41, 0.9}};
+  const size_t K = 120;
+  std::vector<std::vector<io::GridObservation>> byCam(3);
+  for (size_t c = 0; c < 3; ++c)
+    for (size_t i = 0; i < times[c].size(); ++i) {
+      io::GridObservation ob(K);
+      ob.time = times[c][i];
+      for (size_t k = 0; k < 20 + 10 * c + i; ++k) ob.updateImagePoint((k * 7 + c) % K, 1.0, 2.0);  // ragged overlap
+      byCam[c].push_back(ob);
+    }
+  const auto sets = tl::synchronizeObservations(byCam, 0.02);
+  o += ", \"sets\": [";
+  for (size_t s = 0; s < sets.size(); ++s) {
+    std::vector<double> t;
+    for (const auto& ob : sets[s]) t.push_back(ob ? ob->time : -1.0);
+    o += (s ? ", " : "") + jv(t);
+  }
+  o += "]";
+  const tl::CameraGraph g = tl::buildCameraGraph(sets);
+  o += ", \"edges\": [";
+  bool first = true;
+  for (const auto& kv : g.edges) {
+    const double e[3] = {(double)kv.first.first, (double)kv.first.second, kv.second};
+    o += (first ? "" : ", ") + jv(e, 3);
+    first = false;
+  }
+  const tl::DijkstraResult d = tl::dijkstra(g, 0);
+  std::vector<double> pv(d.previous.begin(), d.previous.end());
+  o += "], \"dist\": " + jv(d.distance) + ", \"prev\": " + jv(pv) + "}";
+  std::printf("%s\n", o.c_str());
+  return 0;
+}
+
 int main(int argc, char** argv) {
   if (argc < 5) {
     std::fprintf(stderr, "usage: test_host cpu|gpu problem.bin lm|gn maxIt\n");
     return 2;
   }
   const std::string mode = argv[1], pol = argv[3];
+  if (mode == "tools-unit") return run_tools_unit();
   const int maxIt = std::atoi(argv[4]);
   try {
     CalibrationProblem p = load(argv[2]);
     if (mode == "io") return run_io(p, argv[3]);
+    if (mode == "pipeline") return run_pipeline(p, argv[3], argv[4]);
     if (mode == "init") return run_init(p, (size_t)std::atol(argv[3]), (size_t)std::atol(argv[4]));
     if (mode == "terms-cpu" || mode == "terms-gpu") return run_terms(p, mode == "terms-gpu", pol, maxIt);
     if (mode == "incr-time") {

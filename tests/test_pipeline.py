@@ -1,0 +1,209 @@
+"""The kalibr_calibrate_cameras stage sequence (kalibr_amd/host/calibration_tools.*):
+per-camera observation lists -> CalibrateSingleCamera (initializeIntrinsics + LM bundle adjustment) per camera ->
+SynchronizedObservationView -> BuildCameraGraph + Dijkstra -> CalibrateStereoPair (median-PnP baseline guess) per
+camera and its predecessor -> consecutive baseline guesses (inverse / GetTransform) -> CalibrateMultiCameraRig ->
+IncrementalEstimator::addBatch per synchronized set -> CameraInfo / TFMessage YAML
+(aslam_offline_calibration/kalibr2_ros/src/CalibrateCameras.cpp:142-356, kalibr2/include/kalibr2/CalibrationTools.hpp:93-521,
+kalibr2/src/CameraGraph.cpp, SynchronizedObservationView.cpp, BasicMathUtils.cpp).
+
+CPU: the helpers against independent numpy restatements of the reference formulas; the whole sequence over the
+oracle-backed solvers recovers the synthetic truth.  GPU: the same sequence over the GPU solvers (device-resident
+Optimizer2 loops, and the host-driven loop) takes the oracle run's decisions at every stage -- same camera graph,
+iteration counts and batch acceptances -- with every stage's intrinsics and extrinsics within 1e-6 and the same YAML.
+The three-camera rig is thinned so that its camera graph is the chain 0 - 1 - 2 (tests/cpp/test_host.cpp); its
+stereo stage of camera 2 exercises the reference's camera-H-only pose guess T_H * T_H_L^-1
+(CalibrationTools.hpp:251-252).
+"""
+import json
+import subprocess
+
+import numpy as np
+import pytest
+import yaml
+
+from kalibr_amd import synth
+from tests.host_problem import write_problem
+from tests.test_host_cpp import driver  # noqa: F401  (fixture: builds tests/cpp/test_host.cpp)
+
+KB_MAX_INTR = 10
+
+
+def _run(driver, *args, timeout=900):  # noqa: F811
+    r = subprocess.run([driver, *map(str, args)], capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def _T(v):
+    """4x4 of a [qx qy qz qw tx ty tz] JPL transformation"""
+    T = np.eye(4)
+    T[:3, :3] = synth.quat2r(np.asarray(v[:4]))
+    T[:3, 3] = v[4:7]
+    return T
+
+
+def _skew(p):
+    return np.array([[0, -p[2], p[1]], [p[2], 0, -p[0]], [-p[1], p[0], 0]])
+
+
+def test_tools_helpers_against_independent_restatements(driver):  # noqa: F811
+    r = _run(driver, "tools-unit", "x", "x", "x")
+    # math::median: nth_element at size / 2
+    assert r["median_odd"] == 2.0 and r["median_even"] == 3.0
+    # RotationVector: C(p) = exp(-[p]x) (the formula of RotationVector.cpp:40-43), and back
+    for p, row in zip([[0.1, -0.2, 0.3], [1e-9, 0, 0], [2.5, 0.3, -0.4], [0, 0, 0]], r["rv"]):
+        p = np.array(p)
+        a = np.linalg.norm(p)
+        K = _skew(p / a) if a > 0 else np.zeros((3, 3))
+        C = np.eye(3) - np.sin(a) * K + (1 - np.cos(a)) * K @ K
+        assert np.abs(np.array(row[:9]).reshape(3, 3) - C).max() < 1e-15
+        back = p if np.arccos(np.clip((np.trace(C) - 1) / 2, -1, 1)) >= 1e-14 else np.zeros(3)
+        assert np.abs(np.array(row[9:]) - back).max() < 1e-13
+    Ta, Tb = _T(r["Ta"]), _T(r["Tb"])
+    # GetTransform on the tree 0 <- 2 <- 1: the path transforms multiplied in path order (the reference's
+    # std::accumulate order), inverted when the left node is the nearer one
+    assert np.abs(_T(r["T01"]) - np.linalg.inv(Ta @ Tb)).max() < 1e-14
+    assert np.abs(_T(r["T10"]) - Ta @ Tb).max() < 1e-14
+    assert np.abs(_T(r["T21"]) - np.linalg.inv(Ta)).max() < 1e-14
+    assert np.abs(_T(r["inv_Ta"]) - np.linalg.inv(Ta)).max() < 1e-14
+    assert np.abs(_T(r["Ta_Tb"]) - Ta @ Tb).max() < 1e-14
+    assert r["star_throws"] == 1  # the nearer node is not on the further one's path: the reference never returns
+    # SynchronizedObservationView: pivot = oldest head, window [t, t + 0.02]
+    times = [[0.0, 0.1, 0.25, 0.4], [0.005, 0.1, 0.3], [0.03, 0.26, 0.41, 0.9]]
+    heads, sets = [0, 0, 0], []
+    while True:
+        live = [c for c in range(3) if heads[c] < len(times[c])]
+        if not live:
+            break
+        piv = min(live, key=lambda c: (times[c][heads[c]], c))
+        t0 = times[piv][heads[piv]]
+        s = [-1.0] * 3
+        for c in live:
+            if t0 <= times[c][heads[c]] <= t0 + 0.02:
+                s[c] = times[c][heads[c]]
+                heads[c] += 1
+        sets.append(s)
+    assert r["sets"] == sets
+    # BuildCameraGraph: weight 1 / (common corners over the sets); observation i of camera c sees corners
+    # (k * 7 + c) % 120 for k < 20 + 10 c + i
+    def corners(c, t):
+        i = times[c].index(t)
+        return {(k * 7 + c) % 120 for k in range(20 + 10 * c + i)}
+    common = {}
+    for s in sets:
+        for i in range(3):
+            for j in range(i + 1, 3):
+                n = len(corners(i, s[i]) & corners(j, s[j])) if s[i] >= 0 and s[j] >= 0 else 0
+                common[(i, j)] = common.get((i, j), 0) + n
+    edges = {(i, j): 1.0 / n for (i, j), n in common.items() if n > 0}
+    assert {(int(a), int(b)): w for a, b, w in r["edges"]} == edges
+    # Dijkstra from camera 0
+    dist, prev, done = [0.0, np.inf, np.inf], [0, -1, -1], set()
+    while len(done) < 3:
+        u = min((d, i) for i, d in enumerate(dist) if i not in done)[1]
+        done.add(u)
+        for (a, b), w in edges.items():
+            for x, y in ((a, b), (b, a)):
+                if x == u and y not in done and dist[u] + w < dist[y]:
+                    dist[y], prev[y] = dist[u] + w, u
+    assert r["dist"] == dist and r["prev"] == prev
+
+
+@pytest.fixture(scope="module")
+def rig3():
+    return synth.make_problem([synth.PINHOLE_RADTAN] * 3, 48, seed=5150)
+
+
+def _pipeline(driver, tmp_path, p, kind):  # noqa: F811
+    path = str(tmp_path / f"p_{kind}.bin")
+    write_problem(path, p)
+    out = tmp_path / f"yaml_{kind}"
+    out.mkdir()
+    return _run(driver, "pipeline", path, out, kind), out
+
+
+def test_pipeline_over_the_oracle_recovers_the_rig(driver, tmp_path, rig3):  # noqa: F811
+    r, out = _pipeline(driver, tmp_path, rig3, "cpu")
+    N = 3
+    truth = rig3.state_truth
+    # the thinned sets give the chain 0 - 1 - 2, so camera 1 pairs with 0 and camera 2 with 1
+    assert r["previous"] == [0, 0, 1] and r["pairs"] == [1, 0, 2, 1]
+    assert r["n_sets"] == 48 and r["cams_per_set"][2] == 40 and r["cams_per_set"][3] == 8
+    for stages in (r["single"], r["stereo"], r["rig"]):
+        for it, failed, j0, j1, frames, views, terms in stages:
+            assert 0 < it < 200 and j1 < j0 and terms > 0
+    # a stereo stage's baseline is T_H_L = T_{c_prev, c_i}; the consecutive guesses are their inverses
+    for (i, prev), T in zip(zip(r["pairs"][::2], r["pairs"][1::2]), r["optimal"]):
+        g = _T(r["baseline_guesses"][i - 1])
+        assert np.abs(np.linalg.inv(_T(T)) - g).max() < 1e-12
+    # every stage moves the intrinsics close to the truth (0.3 px noise); the final calibration is within 2 px / 5e-3
+    # of the truth, the baselines within 2 mm / 0.2 deg
+    intr_t = truth[: N * KB_MAX_INTR].reshape(N, KB_MAX_INTR)
+    for key in ("after_single", "after_stereo", "after_rig"):
+        a = np.array(r[key])
+        assert np.abs(a[:, :4] - intr_t[:, :4]).max() < 3.0, key
+    fin = np.array(r["final_calibration"])
+    fi = fin[: N * KB_MAX_INTR].reshape(N, KB_MAX_INTR)
+    assert np.abs(fi[:, :4] - intr_t[:, :4]).max() < 2.0
+    assert np.abs(fi[:, 4:6] - intr_t[:, 4:6]).max() < 5e-3
+    for j in range(N - 1):
+        B = _T(r["final_baselines"][j])
+        Bt = _T(truth[N * KB_MAX_INTR + 7 * j: N * KB_MAX_INTR + 7 * j + 7])
+        assert np.abs(B[:3, 3] - Bt[:3, 3]).max() < 2e-3
+        ang = np.arccos(np.clip((np.trace(B[:3, :3].T @ Bt[:3, :3]) - 1) / 2, -1, 1))
+        assert np.degrees(ang) < 0.2
+    assert r["accepted"][0] == 1 and r["accepted_batches"] == r["final_frames"] == sum(r["accepted"])
+    # the export: one CameraInfo per camera and the chain transforms (two baselines: a TFMessage)
+    assert r["files"] == 4
+    c0 = yaml.safe_load(open(out / "calibration_cam0.yaml"))
+    assert abs(c0["k"][0] - fi[0, 0]) < 1e-9 and c0["distortion_model"] == "plumb_bob"
+    tf = yaml.safe_load(open(out / "camera_chain_transforms.yaml"))
+    assert len(tf["transforms"]) == 2
+
+
+def _yaml_values(d, prefix=""):
+    """flatten a parsed YAML document into {path: value}"""
+    out = {}
+    if isinstance(d, dict):
+        for k, v in d.items():
+            out.update(_yaml_values(v, f"{prefix}/{k}"))
+    elif isinstance(d, list):
+        for i, v in enumerate(d):
+            out.update(_yaml_values(v, f"{prefix}[{i}]"))
+    else:
+        out[prefix] = d
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["gpu", "gpu-host"])
+def test_pipeline_gpu_matches_oracle(driver, tmp_path, rig3, kind):  # noqa: F811
+    """observations -> initialisers -> single -> stereo -> rig -> incremental estimator -> YAML over the GPU solvers
+    (gpu: device-resident LM / GN loops, kb_optimize and kb_optimize_marginal; gpu-host: the host Optimizer2 over the
+    per-call C-ABI) against the same sequence over the oracle"""
+    ref, out_ref = _pipeline(driver, tmp_path, rig3, "cpu")
+    r, out = _pipeline(driver, tmp_path, rig3, kind)
+    for k in ("n_sets", "cams_per_set", "previous", "pairs", "accepted", "batch_iterations", "batch_rank",
+              "accepted_batches", "final_frames", "files"):
+        assert r[k] == ref[k], k
+    assert np.allclose(r["distance"], ref["distance"], rtol=1e-12, atol=0)
+    for k in ("single", "stereo", "rig"):  # iterations, failed iterations, frames, views, terms identical; J to 1e-9
+        a, b = np.array(r[k]), np.array(ref[k])
+        assert np.array_equal(a[:, [0, 1, 4, 5, 6]], b[:, [0, 1, 4, 5, 6]]), k
+        assert np.abs(a[:, 2:4] - b[:, 2:4]).max() <= 1e-9 * np.abs(b[:, 2:4]).max(), k
+    # north_star: intrinsics / extrinsics within 1e-6 at every stage
+    for k in ("after_single", "after_stereo", "optimal", "baseline_guesses", "rig_baselines", "after_rig",
+              "final_calibration", "final_baselines"):
+        assert np.abs(np.array(r[k]) - np.array(ref[k])).max() < 1e-6, k
+    # the exported YAML: the same files and fields, numbers within 1e-6
+    names = sorted(p.name for p in out_ref.iterdir())
+    assert sorted(p.name for p in out.iterdir()) == names
+    for n in names:
+        a = _yaml_values(yaml.safe_load(open(out / n)))
+        b = _yaml_values(yaml.safe_load(open(out_ref / n)))
+        assert a.keys() == b.keys(), n
+        for key in b:
+            if isinstance(b[key], float):
+                assert abs(a[key] - b[key]) < 1e-6, (n, key)
+            else:
+                assert a[key] == b[key], (n, key)
