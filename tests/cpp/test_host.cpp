@@ -1042,14 +1042,25 @@ int main(int argc, char** argv) {
       auto t0 = std::chrono::steady_clock::now();
       const IncrRun g = run_estimator(p, std::make_shared<GpuMarginalLinearSolver>(lo), delta, maxIt);
       const double gsec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-      // the device loop without pass graphs: eager launches, the loop state read back every `sync` passes
+      // the device loop without pass graphs: eager launches, the loop state read back every `sync` passes (1, 2, 4)
       const int sync = std::getenv("KB_INCR_SYNC") ? std::atoi(std::getenv("KB_INCR_SYNC")) : 2;
-      auto ge = std::make_shared<GpuMarginalLinearSolver>(lo);
-      ge->useGraph = false;
-      ge->syncEvery = sync;
-      t0 = std::chrono::steady_clock::now();
-      const IncrRun gev = run_estimator(p, ge, delta, maxIt);
-      const double gesec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      std::string eager_json = "{";
+      IncrRun gev;
+      double gesec = 0.0;
+      for (int sv : {1, 2, 4}) {
+        auto ge = std::make_shared<GpuMarginalLinearSolver>(lo);
+        ge->useGraph = false;
+        ge->syncEvery = sv;
+        t0 = std::chrono::steady_clock::now();
+        const IncrRun rr = run_estimator(p, ge, delta, maxIt);
+        const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        eager_json += (sv > 1 ? ", \"" : "\"") + std::to_string(sv) + "\": " + std::to_string(sec);
+        if (sv == sync || sv == 1) {
+          gev = rr;
+          gesec = sec;
+        }
+      }
+      eager_json += "}";
       // the same estimator over the same GPU solver, its optimisation driven from the host per call (no kb_optimize_marginal)
       auto hl = std::make_shared<GpuMarginalLinearSolver>(lo);
       hl->deviceLoop = false;
@@ -1077,11 +1088,13 @@ int main(int argc, char** argv) {
           "\"cpu_batches\": %zu, \"cpu_threads\": %d, \"cpu_seconds\": %.6f, \"gpu_seconds_same_batches\": %.6f, "
           "\"gn_iterations_same_batches\": %ld, \"same_decisions\": %s, \"wall_gpu\": %.6f, \"wall_cpu\": %.6f, "
           "\"gpu_host_loop_seconds\": %.6f, \"host_loop_same_decisions\": %s, \"state_diff_host_loop\": %.3e, "
-          "\"gpu_eager_seconds\": %.6f, \"eager_sync_every\": %d, \"eager_same_decisions\": %s, \"state_diff_eager\": %.3e}\n",
+          "\"gpu_eager_seconds\": %.6f, \"eager_sync_every\": %d, \"eager_same_decisions\": %s, \"state_diff_eager\": %.3e, "
+          "\"gpu_eager_seconds_by_sync\": %s}\n",
           g.secs.size(), std::accumulate(g.secs.begin(), g.secs.end(), 0.0), acc_g, it_g, c.secs.size(), threads, c_k,
           g_k, it_gk, same ? "true" : "false", gsec, csec, ghsec, same_h ? "true" : "false",
           maxdiff(g.state, gh.state, 0, g.state.size()), gesec, sync,
-          gev.accepted == g.accepted && gev.iters == g.iters ? "true" : "false", maxdiff(g.state, gev.state, 0, g.state.size()));
+          gev.accepted == g.accepted && gev.iters == g.iters ? "true" : "false", maxdiff(g.state, gev.state, 0, g.state.size()),
+          eager_json.c_str());
       return 0;
     }
     if (mode == "incr-cpu" || mode == "incr-gpu") {
