@@ -1473,7 +1473,8 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
       if (tid + u * nth < nt3) tg[tid + u * nth] = tv[u];
     for (int q = tid + kTgU * nth; q < nt3; q += nth) tg[q] = d.target[q];
   }
-  const double* tgt = tg_lds ? tg : d.target;
+  const double* tgt = tg_lds ? tg : d.target;  // (KB_CORNER_OLD; the corner passes branch on tg_lds)
+  (void)tgt;
   const double lam2 = lam * lam;
   if (tid == 0) {
     okl = 1;
@@ -1534,6 +1535,7 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
             cidn = d.cid[kn];
             yn = d.y[kn];
           }
+#ifdef KB_CORNER_OLD
           double xu[16], xv[16];
 #pragma unroll
           for (int q = 0; q < 16; ++q) {
@@ -1564,6 +1566,48 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
               xr[15] = -(r ? yv.y - w : yv.x - u);  // column 15 carries -e: H[:,15] = rhs part, H[15][15] = chi^2
             }
           }
+          const bool valid = true;
+#else
+          // one projection per corner: both Jacobian rows from the lane.  The rows are written un-negated,
+          // [dy/dtheta | e] = -[de/dtheta | -e]: the SYRK of a row and of its negation are bitwise equal, so the sign
+          // flips of J_delta = -Jp [I | [p]x] and of the intrinsic rows -Jp, -Jd (CameraDesignVariable.hpp(impl):38-54)
+          // are not spent.  Lanes past the view's last corner leave xu / xv undefined and store zero rows instead (no
+          // 32-register zero initialisation per pass).
+          const bool valid = k < o1;
+          double xu[16], xv[16];
+          if (valid) {
+            double X0, X1, X2;
+            if (tg_lds) {  // the staged corners through ds_read (a select of the two pointers compiles to flat loads)
+              X0 = tg[3 * cid];
+              X1 = tg[3 * cid + 1];
+              X2 = tg[3 * cid + 2];
+            } else {
+              X0 = d.target[3 * cid];
+              X1 = d.target[3 * cid + 1];
+              X2 = d.target[3 * cid + 2];
+            }
+            const double p0 = R[0] * X0 + R[1] * X1 + R[2] * X2 + t[0];
+            const double p1 = R[3] * X0 + R[4] * X1 + R[5] * X2 + t[1];
+            const double p2 = R[6] * X0 + R[7] * X1 + R[8] * X2 + t[2];
+            double u, w, Jp[6], Ji[2 * KB_MAX_INTR];
+            project_jac<MM>(model, intr, p0, p1, p2, u, w, Jp, Ji);
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+              double* xr = r ? xv : xu;
+              const double j0 = Jp[3 * r], j1 = Jp[3 * r + 1], j2 = Jp[3 * r + 2];
+              // Jp [I | [p]x]   (HomogeneousExpressionNode.cpp:71-81, boxMinus)
+              xr[0] = j0;
+              xr[1] = j1;
+              xr[2] = j2;
+              xr[3] = j1 * p2 - j2 * p1;
+              xr[4] = -j0 * p2 + j2 * p0;
+              xr[5] = j0 * p1 - j1 * p0;
+#pragma unroll
+              for (int q = 0; q < 9; ++q) xr[6 + q] = (q < nin) ? Ji[KB_MAX_INTR * r + q] : 0.0;
+              xr[15] = r ? yv.y - w : yv.x - u;  // column 15 carries e: H[:,15] = rhs part, H[15][15] = chi^2
+            }
+          }
+#endif
           if (stv && pass < 2) KB_TSB(d, sto + 4 * pass + 1);
           // rows n .. 63 of a partial pass are zero: only the groups of 4 k-steps (16 rows) holding valid rows are
           // issued (k-step ks = rows 4ks .. 4ks + 3, even ks into acc0, odd into acc1), the next group's operands in
@@ -1572,8 +1616,13 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
           const int ng = (min(64, o1 - base) + 15) >> 4;
 #pragma unroll
           for (int r = 0; r < 2; ++r) {
+            if (valid) {
 #pragma unroll
-            for (int q = 0; q < 16; ++q) Xw[lane * XS + q] = r ? xv[q] : xu[q];
+              for (int q = 0; q < 16; ++q) Xw[lane * XS + q] = r ? xv[q] : xu[q];
+            } else {
+#pragma unroll
+              for (int q = 0; q < 16; ++q) Xw[lane * XS + q] = 0.0;
+            }
             KB_WAVE_SYNC();
             // groups g = 0..3 ping-pong between xa and xb: group g + 1's loads are issued before group g's MFMAs
             double xa[4], xb[4];

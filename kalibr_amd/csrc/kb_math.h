@@ -19,6 +19,16 @@ namespace kb {
 // eps^(1/4) for doubles == 2^-13 exactly (quaternion_algebra.cpp:10-13)
 constexpr double kEps4thRoot = 1.220703125e-4;
 
+// 1/z of a projection: v_rcp_f64 + two Newton steps, within an ulp of the IEEE quotient (the division's scale /
+// fixup sequence is ~10 dependent instructions on every corner's chain)
+__device__ __forceinline__ double proj_recip(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  double e = fma(-x, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-x, r, 1.0);
+  return fma(r, e, r);
+}
+
 __device__ __forceinline__ void quat2r(const double* q, double* R) {
   R[0] = q[0] * q[0] - q[1] * q[1] - q[2] * q[2] + q[3] * q[3];
   R[1] = q[0] * q[1] * 2.0 + q[2] * q[3] * 2.0;
@@ -151,7 +161,7 @@ __device__ __forceinline__ void project(int model, const double* in, double px, 
   else if (MM == (1u << KB_PINHOLE_EQUI)) model = KB_PINHOLE_EQUI;
   else if (MM == (1u << KB_PINHOLE_FOV)) model = KB_PINHOLE_FOV;
   if (KB_MM(KB_PINHOLE_RADTAN) && model == KB_PINHOLE_RADTAN) {
-    const double rz = 1.0 / pz;
+    const double rz = proj_recip(pz);
     double x = px * rz, y = py * rz;
     radtan_only(in + 4, x, y);
     u = in[0] * x + in[2];
@@ -177,7 +187,7 @@ __device__ __forceinline__ void project(int model, const double* in, double px, 
     u = in[2] * (px * ninv) + in[4];
     v = in[3] * (py * ninv) + in[5];
   } else if (KB_MM(KB_PINHOLE_EQUI) || KB_MM(KB_PINHOLE_FOV)) {  // pinhole + equidistant / FOV
-    const double rz = 1.0 / pz;
+    const double rz = proj_recip(pz);
     double x = px * rz, y = py * rz;
     if (KB_MM(KB_PINHOLE_EQUI) && (!KB_MM(KB_PINHOLE_FOV) || model == KB_PINHOLE_EQUI))
       equi(in + 4, x, y, nullptr, nullptr);
@@ -203,7 +213,7 @@ __device__ __forceinline__ void project_jac(int model, const double* in, double 
   else if (MM == (1u << KB_PINHOLE_FOV)) model = KB_PINHOLE_FOV;
   if (KB_MM(KB_PINHOLE_RADTAN) && model == KB_PINHOLE_RADTAN) {
     const double fu = in[0], fv = in[1];
-    const double rz = 1.0 / pz, rz2 = rz * rz;
+    const double rz = proj_recip(pz), rz2 = rz * rz;
     const double ux = px * rz, uy = py * rz;
     double x = ux, y = uy, Jd[4];
     radtan(in + 4, x, y, Jd);
@@ -303,7 +313,7 @@ __device__ __forceinline__ void project_jac(int model, const double* in, double 
   } else if (KB_MM(KB_PINHOLE_EQUI) || KB_MM(KB_PINHOLE_FOV)) {  // pinhole + equidistant (4) / FOV (1)
     const bool eq = KB_MM(KB_PINHOLE_EQUI) && (!KB_MM(KB_PINHOLE_FOV) || model == KB_PINHOLE_EQUI);
     const double fu = in[0], fv = in[1];
-    const double rz = 1.0 / pz, rz2 = rz * rz;
+    const double rz = proj_recip(pz), rz2 = rz * rz;
     double x = px * rz, y = py * rz, Jd[4], Jk[8];
     if (eq)
       equi(in + 4, x, y, Jd, Jk);

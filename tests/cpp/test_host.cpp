@@ -829,14 +829,18 @@ static std::string jT(const kalibr_amd::io::Transformation& T) {
 // per-camera observation lists of the packed problem, time-stamped f * 0.1 s + c * 1 ms.  With three cameras the views
 // are thinned so that the camera graph is the chain 0 - 1 - 2: frames f % 12 < 5 drop camera 2, 5 <= f % 12 < 10 drop
 // camera 0 (camera 1 sees every set; cameras 0 and 2 share only the remaining frames)
+// pattern 2 (three cameras): frame 6 is seen by camera 2 alone, so the stereo stage of camera 1 with camera 0 meets a
+// set seen by neither before later sets with views (the reference's out-of-range target_pose_dvs index)
 static std::vector<std::vector<kalibr_amd::io::GridObservation>> observations_by_camera(const CalibrationProblem& p,
-                                                                                      size_t W, size_t H) {
+                                                                                      size_t W, size_t H,
+                                                                                      int pattern = 1) {
   namespace io = kalibr_amd::io;
   const size_t N = p.n_cams(), K = p.n_target();
   std::vector<std::vector<io::GridObservation>> out(N);
   for (int v = 0; v < p.n_views(); ++v) {
     const size_t f = p.view_frame[v], c = p.view_cam[v];
     if (N == 3 && ((f % 12 < 5 && c == 2) || (f % 12 >= 5 && f % 12 < 10 && c == 0))) continue;
+    if (N == 3 && pattern == 2 && f == 6 && c != 2) continue;
     io::GridObservation o(K);
     o.imCols = W;
     o.imRows = H;
@@ -853,7 +857,8 @@ static int run_pipeline(const CalibrationProblem& p, const std::string& outdir, 
   namespace tl = kalibr_amd::tools;
   const size_t N = p.n_cams();
   io::AprilgridTarget tgt;
-  const auto byCam = observations_by_camera(p, 1280, 1024);
+  const int pattern = std::getenv("KB_PIPELINE_PATTERN") ? std::atoi(std::getenv("KB_PIPELINE_PATTERN")) : 1;
+  const auto byCam = observations_by_camera(p, 1280, 1024, pattern);
   tl::StageOptions so;
   LinearSolverOptions lo;
   lo.columnScaling = true;  // CalibrateCameras.cpp:263-267

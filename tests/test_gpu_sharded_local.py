@@ -204,3 +204,25 @@ def test_configs3_eight_shards_on_one_gpu(capi):
     d = float(np.abs(st - s0).max())
     print(f"configs[3] 8 in-process shards: max|sharded - unsharded| after 4 GN passes = {d:.2e}")
     assert d < 1e-9
+
+
+@pytest.mark.parametrize("policy", ["lm", "gn"])
+def test_configs3_eight_shards_full_optimize_against_oracle(capi, oracle_mod, policy):
+    """The N=8 layout (configs[3], 8 x 250 frames, in-process ranks) through a whole Optimizer2 run with Kalibr2's
+    settings, against the CPU oracle on the unsharded problem: the same iteration counts and accept / revert trace,
+    J within 1e-9, every intrinsic, baseline and frame pose within 1e-6 (north_star)"""
+    p = synth.make_config(4)
+    kw = dict(policy=policy, lambda0=10.0, max_iterations=200 if policy == "lm" else 20, eps_x=1e-3, eps_j=1.0)
+    solvers = _shards(capi, p, [250 * r for r in range(1, 8)])
+    res = _run_all(solvers, lambda s: s.optimize(**kw))
+    st = _joined_state(p, [s.get_state() for s in solvers])
+    for s in solvers:
+        s.close()
+    st_o, r_o = oracle_mod.Oracle(p).optimize(p.state_init, nthreads=16, **kw)
+    print(f"configs[3] 8 shards {policy}: iterations {[r['iterations'] for r in res][0]} / oracle {r_o['iterations']}, "
+          f"J {res[0]['J_final']!r} / {r_o['J_final']!r}, max|state - oracle| {np.abs(st - st_o).max():.3e}")
+    for r in res:
+        assert r["iterations"] == r_o["iterations"] and r["failed_iterations"] == r_o["failed_iterations"]
+        assert np.array_equal(r["trace"][:, 3], r_o["trace"][:, 3])
+        assert abs(r["J_final"] - r_o["J_final"]) <= 1e-9 * r_o["J_final"]
+    assert float(np.abs(st - st_o).max()) < 1e-6

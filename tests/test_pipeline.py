@@ -207,3 +207,18 @@ def test_pipeline_gpu_matches_oracle(driver, tmp_path, rig3, kind):  # noqa: F81
                 assert abs(a[key] - b[key]) < 1e-6, (n, key)
             else:
                 assert a[key] == b[key], (n, key)
+
+
+def test_pipeline_refuses_the_stereo_index_overrun(driver, tmp_path, rig3):  # noqa: F811
+    """a synchronized set seen by neither camera of a stereo pair, before later sets with views: the reference indexes
+    target_pose_dvs past its end (CalibrationTools.hpp:244-283, undefined behaviour); the restatement raises"""
+    import os
+    path = str(tmp_path / "p.bin")
+    write_problem(path, rig3)
+    out = tmp_path / "yaml"
+    out.mkdir()
+    env = dict(os.environ, KB_PIPELINE_PATTERN="2")
+    r = subprocess.run([driver, "pipeline", path, str(out), "cpu"], capture_output=True, text=True, timeout=900,
+                       env=env)
+    assert r.returncode == 1
+    assert "target_pose_dvs" in r.stdout, r.stdout[-2000:]
