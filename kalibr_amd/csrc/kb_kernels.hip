@@ -1575,8 +1575,16 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
           // 32-register zero initialisation per pass).
           const bool valid = k < o1;
           double xu[16], xv[16];
+#ifndef KB_CORNER_NOZERO
+#pragma unroll
+          for (int q = 0; q < 16; ++q) {
+            xu[q] = 0.0;
+            xv[q] = 0.0;
+          }
+#endif
           if (valid) {
             double X0, X1, X2;
+#ifdef KB_CORNER_TGB
             if (tg_lds) {  // the staged corners through ds_read (a select of the two pointers compiles to flat loads)
               X0 = tg[3 * cid];
               X1 = tg[3 * cid + 1];
@@ -1586,6 +1594,11 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
               X1 = d.target[3 * cid + 1];
               X2 = d.target[3 * cid + 2];
             }
+#else
+            X0 = tgt[3 * cid];
+            X1 = tgt[3 * cid + 1];
+            X2 = tgt[3 * cid + 2];
+#endif
             const double p0 = R[0] * X0 + R[1] * X1 + R[2] * X2 + t[0];
             const double p1 = R[3] * X0 + R[4] * X1 + R[5] * X2 + t[1];
             const double p2 = R[6] * X0 + R[7] * X1 + R[8] * X2 + t[2];
@@ -1616,6 +1629,7 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
           const int ng = (min(64, o1 - base) + 15) >> 4;
 #pragma unroll
           for (int r = 0; r < 2; ++r) {
+#ifdef KB_CORNER_NOZERO
             if (valid) {
 #pragma unroll
               for (int q = 0; q < 16; ++q) Xw[lane * XS + q] = r ? xv[q] : xu[q];
@@ -1623,6 +1637,11 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
 #pragma unroll
               for (int q = 0; q < 16; ++q) Xw[lane * XS + q] = 0.0;
             }
+#else
+            (void)valid;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) Xw[lane * XS + q] = r ? xv[q] : xu[q];
+#endif
             KB_WAVE_SYNC();
             // groups g = 0..3 ping-pong between xa and xb: group g + 1's loads are issued before group g's MFMAs
             double xa[4], xb[4];

@@ -846,24 +846,33 @@ IncrementalEstimator::ReturnValue IncrementalEstimator::addBatch(const Calibrati
   // insert the new batch; save the design variables in case it is rejected (:343-351)
   const std::vector<double> saved = _problem.state;
   appendBatch(batch);
+  auto lap = [&, tl = t0](int k) mutable {  // the per-phase host time (profile[])
+    const auto tn = std::chrono::steady_clock::now();
+    profile[k] += std::chrono::duration<double>(tn - tl).count();
+    tl = tn;
+  };
   // Optimizer2::initialize -> initMatrixStructure over the grown problem, then optimize (:373).  The reference
   // re-initialises the whole structure; a solver that holds the accepted frames appends the new one in place
   // (kb_append_frames: only the batch's observations are uploaded) instead
   if (!_solver->appendFrames(_problem, (size_t)_problem.n_frames - 1)) _solver->initMatrixStructure(_problem, false);
+  lap(0);
   // the optimisation itself: device-resident when the solver runs it (kb_optimize_marginal), else the host loop
   SolutionReturnValue srv;
   if (!_solver->optimizeDevice(_optOptions, srv)) {
     Optimizer2 optimizer(_optOptions);
     srv = optimizer.optimize();
   }
+  lap(1);
   ReturnValue ret;
   ret.numIterations = (size_t)srv.iterations;
   ret.JStart = srv.JStart;
   ret.JFinal = srv.JFinal;
   if (_solver->getOptions().columnScaling) ret.singularValuesScaled = _solver->getSingularValues();  // :384-397
   const std::vector<double> state = _solver->state();
+  lap(2);
   // analyze the unscaled marginal system (:400)
   _solver->analyzeMarginal();
+  lap(3);
   ret.rankTheta = _solver->getSVDRank();
   ret.rankThetaDeficiency = _solver->getSVDRankDeficiency();
   ret.svdTolerance = _solver->getSVDTolerance();
@@ -902,8 +911,11 @@ IncrementalEstimator::ReturnValue IncrementalEstimator::addBatch(const Calibrati
     _problem.state = saved;
     // the solver keeps the accepted frames with their restored values for the next append (a solver that cannot, or
     // a first batch rejected, leaves frames the problem does not hold: the next addBatch re-initialises)
+    lap(4);
     if (_problem.n_frames > 0) _solver->dropLastFrames(1, saved);
+    lap(5);
   }
+  lap(4);
   ret.elapsedTime = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   return ret;
 }

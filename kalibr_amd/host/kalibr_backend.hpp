@@ -483,6 +483,9 @@ class IncrementalEstimator {
   std::ptrdiff_t getRankTheta() const { return _rankTheta; }
   double getSvLog2Sum() const { return _svLog2Sum; }
   const Options& getOptions() const { return _options; }
+  /// host seconds spent per phase over all addBatch calls: append / initMatrixStructure, optimize, state read-back,
+  /// analyzeMarginal, the host bookkeeping, the drop of a rejected batch
+  double profile[6] = {0, 0, 0, 0, 0, 0};
 
  private:
   void appendBatch(const CalibrationBatch& b);

@@ -297,6 +297,7 @@ struct IncrRun {
   std::vector<int> accepted;
   std::vector<double> gain, state, secs;
   std::vector<long> rank, iters;
+  std::vector<double> profile;  // IncrementalEstimator::profile
 };
 
 static IncrRun run_estimator(const CalibrationProblem& p, std::shared_ptr<MarginalLinearSystemSolver> solver,
@@ -319,6 +320,7 @@ static IncrRun run_estimator(const CalibrationProblem& p, std::shared_ptr<Margin
     r.iters.push_back((long)rv.numIterations);
   }
   r.state = est.getProblem().state;
+  r.profile.assign(est.profile, est.profile + 6);
   return r;
 }
 
@@ -1060,6 +1062,7 @@ int main(int argc, char** argv) {
         const IncrRun rr = run_estimator(p, ge, delta, maxIt);
         const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         eager_json += (sv > 1 ? ", \"" : "\"") + std::to_string(sv) + "\": " + std::to_string(sec);
+        eager_json += ", \"profile_" + std::to_string(sv) + "\": " + jv(rr.profile);
         if (sv == sync || sv == 1) {
           gev = rr;
           gesec = sec;
@@ -1094,12 +1097,12 @@ int main(int argc, char** argv) {
           "\"gn_iterations_same_batches\": %ld, \"same_decisions\": %s, \"wall_gpu\": %.6f, \"wall_cpu\": %.6f, "
           "\"gpu_host_loop_seconds\": %.6f, \"host_loop_same_decisions\": %s, \"state_diff_host_loop\": %.3e, "
           "\"gpu_eager_seconds\": %.6f, \"eager_sync_every\": %d, \"eager_same_decisions\": %s, \"state_diff_eager\": %.3e, "
-          "\"gpu_eager_seconds_by_sync\": %s}\n",
+          "\"gpu_eager_seconds_by_sync\": %s, \"profile_graph\": %s, \"profile_host_loop\": %s}\n",
           g.secs.size(), std::accumulate(g.secs.begin(), g.secs.end(), 0.0), acc_g, it_g, c.secs.size(), threads, c_k,
           g_k, it_gk, same ? "true" : "false", gsec, csec, ghsec, same_h ? "true" : "false",
           maxdiff(g.state, gh.state, 0, g.state.size()), gesec, sync,
           gev.accepted == g.accepted && gev.iters == g.iters ? "true" : "false", maxdiff(g.state, gev.state, 0, g.state.size()),
-          eager_json.c_str());
+          eager_json.c_str(), jv(g.profile).c_str(), jv(gh.profile).c_str());
       return 0;
     }
     if (mode == "incr-cpu" || mode == "incr-gpu") {
