@@ -1044,6 +1044,16 @@ int main(int argc, char** argv) {
       LinearSolverOptions lo;
       lo.columnScaling = true;  // CalibrateCameras.cpp:263-267
       lo.epsSVD = 1e-6;
+      if (std::getenv("KB_INCR_EAGER_ONLY")) {  // profiling runs: the eager device loop only (no pass graphs)
+        auto ge = std::make_shared<GpuMarginalLinearSolver>(lo);
+        ge->useGraph = false;
+        ge->syncEvery = 2;
+        const auto te = std::chrono::steady_clock::now();
+        const IncrRun rr = run_estimator(p, ge, delta, maxIt);
+        const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - te).count();
+        std::printf("{\"gpu_eager_seconds\": %.6f, \"profile\": %s}\n", sec, jv(rr.profile).c_str());
+        return 0;
+      }
       // untimed warm-up: code-object load and the first launches of every kernel the runs below use
       run_estimator(p, std::make_shared<GpuMarginalLinearSolver>(lo), delta, maxIt, 4);
       auto t0 = std::chrono::steady_clock::now();
