@@ -171,7 +171,7 @@ struct kb_handle {
   int F_max = 0;
   // build-kernel timing
   double build_ms = 0.0;
-  double* marg_buf = nullptr;  // marginal solver outputs: V [C][C] | sv [C] | info [8]
+  double* marg_buf = nullptr;  // marginal solver outputs, solve then analyze: V [C][C] | sv [C] | info [8]
   KbMarg marg{};               // kb_optimize_marginal: the k_marg arguments its captured passes use
   size_t lds_marg = 0;
   // linear solver of kb_solve: KB_SOLVER_SCHUR (direct) or KB_SOLVER_PCG (LinearSolverPCG)
@@ -1264,19 +1264,32 @@ int kb_revert(kb_handle* h) {
 }
 
 // ---------------------------------------------------------------- marginal SVD solver (calibration::LinearSolver)
+// the k_marg instance for C: full-storage Omega while it fits in LDS, packed upper beyond
+using MargKernel = void (*)(KbDev, KbMarg, int);
+static MargKernel marg_kernel(int C) { return marg_full(C) ? k_marg<true> : k_marg<false>; }
+static const void* marg_fn(int C) { return (const void*)marg_kernel(C); }
+
+// warm-started Jacobi sweeps (k_marg) unless KB_MARG_COLD is set (A/B runs: every call from V = I, as Eigen::JacobiSVD)
+static int marg_warm() {
+  static const int w = std::getenv("KB_MARG_COLD") ? 0 : 1;
+  return w;
+}
+
 static int run_marginal(kb_handle* h, const kb_marginal_options* o, int write_dx, kb_marginal_info* info,
                         double* sv_out, double* V_out) {
   if (h->C > kMargMaxC) return fail("marginal solver: camera block C > 112 is not supported");
   if (sharded(h)) return fail("marginal solver: not available on a sharded handle");
   const int C = h->C;
-  if (!h->marg_buf && h->alloc(&h->marg_buf, (size_t)C * C + C + 8)) return -1;
-  KbMarg m;
+  const size_t mstride = (size_t)C * C + C + 8;
+  if (!h->marg_buf && h->alloc(&h->marg_buf, 2 * mstride)) return -1;
+  KbMarg m{};
   m.scaling = o->column_scaling ? 1 : 0;
   m.write_dx = write_dx;
+  m.warm = marg_warm();
   m.norm_tol = std::sqrt(2.0 * (double)h->NC * o->eps_norm);  // rows of J: 2 per corner
   m.eps_svd = o->eps_svd;
   m.svd_tol = o->svd_tol;
-  m.V = h->marg_buf;
+  m.V = h->marg_buf + (write_dx ? 0 : mstride);  // solve and analyzeMarginal keep their own warm-start V
   m.sv = m.V + (size_t)C * C;
   m.info = m.sv + C;
   // the frame blocks eliminated at lambda = 0 (stored H_ff, H_fc, g_f of the last build), column sums finished
@@ -1286,9 +1299,10 @@ static int run_marginal(kb_handle* h, const kb_marginal_options* o, int write_dx
   if (!rc) rc = launch_colsum(h, 0);
   h->d.host_lambda = lam_saved;
   if (rc) return rc;
-  const size_t lds = sizeof(double) * ((size_t)C * (C + 1) / 2 + (size_t)C * C + 2 * C);
-  KB_HIP(hipFuncSetAttribute((const void*)k_marg, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  hipLaunchKernelGGL(k_marg, dim3(1), dim3(kMargThreads), lds, h->stream, h->d, m, 0);
+  bool stage_v0;
+  const size_t lds = sizeof(double) * (size_t)marg_lds_doubles(C, stage_v0);
+  KB_HIP(hipFuncSetAttribute(marg_fn(C), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL(marg_kernel(C), dim3(1), dim3(marg_threads(C)), lds, h->stream, h->d, m, 0);
   KB_HIP(hipGetLastError());
   double inf[8];
   KB_HIP(hipMemcpyAsync(inf, m.info, sizeof(inf), hipMemcpyDeviceToHost, h->stream));
@@ -1611,7 +1625,7 @@ int kb_optimize(kb_handle* h, const kb_optimizer_options* opts, kb_solution* out
 static int enqueue_marg_pass(kb_handle* h) {
   if (launch_build(h, 1, 1) || launch_colsum(h, 1, true)) return -1;
   hipLaunchKernelGGL(k_camexpand, dim3(1), dim3(256), h->lds_camexp, h->stream, h->d, 1);
-  hipLaunchKernelGGL(k_marg, dim3(1), dim3(kMargThreads), h->lds_marg, h->stream, h->d, h->marg, 1);
+  hipLaunchKernelGGL(marg_kernel(h->C), dim3(1), dim3(marg_threads(h->C)), h->lds_marg, h->stream, h->d, h->marg, 1);
   hipLaunchKernelGGL(k_marg_tail, dim3(1), dim3(256), 0, h->stream, h->d);
   KB_HIP(hipGetLastError());
   if (launch_backsub(h, 1, 1, 1)) return -1;
@@ -1629,18 +1643,20 @@ int kb_optimize_marginal(kb_handle* h, const kb_optimizer_options* opts, const k
   if (sharded(h)) return fail("kb_optimize_marginal: not available on a sharded handle");
   KB_HIP(hipSetDevice(h->device));
   const int C = h->C;
-  if (!h->marg_buf && h->alloc(&h->marg_buf, (size_t)C * C + C + 8)) return -1;
+  if (!h->marg_buf && h->alloc(&h->marg_buf, 2 * ((size_t)C * C + C + 8))) return -1;
   KbMarg m{};
   m.scaling = mopts->column_scaling ? 1 : 0;
   m.write_dx = 1;
+  m.warm = marg_warm();
   m.norm_tol = std::sqrt(2.0 * (double)h->NC * mopts->eps_norm);
   m.eps_svd = mopts->eps_svd;
   m.svd_tol = mopts->svd_tol;
   m.V = h->marg_buf;
   m.sv = m.V + (size_t)C * C;
   m.info = m.sv + C;
-  h->lds_marg = sizeof(double) * ((size_t)C * (C + 1) / 2 + (size_t)C * C + 2 * C);
-  KB_HIP(hipFuncSetAttribute((const void*)k_marg, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_marg));
+  bool stage_v0;
+  h->lds_marg = sizeof(double) * (size_t)marg_lds_doubles(C, stage_v0);
+  KB_HIP(hipFuncSetAttribute(marg_fn(C), hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_marg));
   // the captured passes hold the k_marg arguments: other options (or a grown problem: norm_tol) recapture them
   if (std::memcmp(&m, &h->marg, sizeof(KbMarg)) != 0) {
     if (h->graph_policy == kPolicyMarginal) drop_graphs(h);
@@ -2118,6 +2134,14 @@ int kb_diag_read_ts(kb_handle* h, long long* out, int n) {
     return 0;
   }
   KB_HIP(hipMemcpy(out, h->d.dbg_ts, sizeof(long long) * std::min(n, 256), hipMemcpyDeviceToHost));
+  return 0;
+}
+
+// diagnostic build only: the dbg_flags every later launch of the handle's kernels sees (k_marg: bit 1 skips the
+// rounds' work, bit 2 skips the rotations)
+int kb_diag_set_flags(kb_handle* h, int flags) {
+  h->d.dbg_flags = flags;
+  drop_graphs(h);
   return 0;
 }
 

@@ -42,14 +42,24 @@ constexpr int kMargThreads = 1024;
 constexpr int kMargMaxC = 112;         // packed Omega + V in LDS: C(C+1)/2 + C^2 + 2C doubles <= 160 KB
 constexpr int kMargMaxSweeps = 40;
 constexpr double kMargJacobiTol = 1.1102230246251565e-16;  // skip |a_pq| <= 2^-53 sqrt|a_pp a_qq|
+constexpr int kMargItems = 8;    // k_marg items (2x2 blocks, rows of V) per thread at C <= kMargMaxC
+constexpr int kMargWarmMax = 32;
+constexpr int kMargLdsStage = 19000;  // dynamic LDS doubles up to which V0 is staged in LDS too (static ~5 KB beside)  // consecutive warm starts before a cold (identity) start bounds V's orthogonality drift
+// block size of k_marg: one thread per 2x2 block of pairs and per (row of V, pair), whole waves
+inline int marg_threads(int C) {
+  const int h = (C + (C & 1)) / 2, items = h * (h + 1) / 2 + C * h;
+  const int t = (items + 63) / 64 * 64;
+  return t < kMargThreads ? t : kMargThreads;
+}
 struct KbMarg {
   int scaling;      // LinearSolverOptions::columnScaling
   int write_dx;     // 1: solve (dx_c into d.dx); 0: analyzeMarginal (SVD only)
+  int warm;         // 1: start the sweeps from the previous call's V (info[5] counts the warm chain)
   double norm_tol;  // sqrt(rows * epsNorm)
   double eps_svd, svd_tol;
   double* sv;    // [C] singular values, descending
   double* V;     // [C][C] row-major, right singular vector j in column j
-  double* info;  // [8]: rank, sweeps, tolerance, sv gap, log2 sum of the first rank singular values
+  double* info;  // [8]: rank, sweeps, tolerance, sv gap, log2 sum of the first rank singular values, warm chain
 };
 
 struct KbDev {
@@ -145,7 +155,18 @@ struct KbDev {
   do {                                                                                                      \
     if (blockIdx.x == 0 && (threadIdx.x & 63) == 0 && (d).dbg_ts) (d).dbg_ts[64 + (i)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
+// k_marg timeline: thread 0 stamps slot 200 + i (s_memtime shader clock at i = 0 and 11 into 216 / 217)
+#define KB_TSM(d, i)                                                                     \
+  do {                                                                                   \
+    if (threadIdx.x == 0 && (d).dbg_ts) {                                                \
+      (d).dbg_ts[200 + (i)] = __builtin_amdgcn_s_memrealtime();                          \
+      if ((i) == 0 || (i) == 11) (d).dbg_ts[216 + ((i) == 11)] = __builtin_amdgcn_s_memtime(); \
+    }                                                                                    \
+  } while (0)
 #else
+#define KB_TSM(d, i) \
+  do {               \
+  } while (0)
 #define KB_TSB(d, i) \
   do {               \
   } while (0)

@@ -2337,181 +2337,612 @@ __global__ void __launch_bounds__(256) k_camexpand(KbDev d, int gate) {
 // analyzeMarginal :468-528) on the Schur-reduced system the build + k_schur (lambda = 0) + k_colsum produced:
 //   S = H_cc - sum H_fc^T A_f,  b = g_c - sum H_fc^T b_f   (= Omega, b_r of reduceLeft/RightHandSide)
 //   column scaling G_j = 1/sqrt(H_cc[j][j]) (0 below sqrt(rows * epsNorm), linalg.cpp:128-152)
-//   SVD of G S G (Eigen::JacobiSVD, linalg.cpp:412-424) by cyclic two-sided Jacobi: the symmetric matrix packed
-//   upper in LDS, V in LDS; the round-robin parallel ordering applies C/2 disjoint rotations per round, each
-//   2x2 block (pair k, pair l) rotated in place by one thread (rows by k, then columns by l); 2 barriers/round
+//   SVD of G S G (Eigen::JacobiSVD, linalg.cpp:412-424) by cyclic two-sided Jacobi: the off-diagonal of the symmetric
+//   matrix packed upper in LDS, V in LDS; the round-robin parallel ordering applies C/2 disjoint rotations per round.
+//   One barrier per round: every thread owns one 2x2 block (pair k, pair l) or one (row of V, pair k) and derives the
+//   rotations it needs itself from ping-pong copies of the diagonal and of the round's pair entries a_pq, which the
+//   previous round's block owners wrote (each next-round pair entry lies in exactly one of this round's blocks);
+//   a parallel threshold test before each sweep replaces the rotation-free sweep that ends the cyclic Jacobi
 //   truncation at rankTol = sv_0 epsSVD C, x_r = G V_r diag(1/w) V_r^T G b (solveSVD, linalg.cpp:426-443)
-// One block of kMargThreads.  LDS: C(C+1)/2 + C^2 + 2C doubles (C <= kMargMaxC).
+// Warm start (mo.warm): the sweeps run on V0^T (G S G) V0 from the previous call's V0 (sorted columns, any orthogonal
+// matrix is a valid start), V = V0 J...; the successive systems of a GN loop differ little, so the start is nearly
+// diagonal and the quadratic convergence takes 2-3 sweeps instead of 8-10.  Every kMargWarmMax-th call is cold.
+// One block of marg_threads(C).  LDS: marg_lds_doubles(C) doubles (C <= kMargMaxC).
 // ---------------------------------------------------------------------------------------------
 __device__ __forceinline__ int pk_up(int i, int j, int n) {  // packed upper index, any order
   const int a = min(i, j), b = max(i, j);
   return a * n - a * (a - 1) / 2 + (b - a);
 }
 
-__device__ __forceinline__ void rr_pair(int m, int r, int k, int& p, int& q) {  // round-robin pairing
-  int a, b;
-  if (k == 0) {
-    a = r;
-    b = m - 1;
-  } else {
-    a = (r + k) % (m - 1);
-    b = (r - k + (m - 1)) % (m - 1);
-  }
+// pair k of round r (M1 = m - 1 rounds per sweep): {r, M1} for k = 0, {(r + k) % M1, (r - k) % M1} otherwise
+__device__ __forceinline__ void rr_pair(int M1, int r, int k, int& p, int& q) {
+  int a = r + k, b = r - k;
+  if (a >= M1) a -= M1;
+  if (b < 0) b += M1;
+  if (k == 0) b = M1;
   p = min(a, b);
   q = max(a, b);
 }
 
+// pair k of round r in the round-robin's own orientation: a = (r + k) % M1, b = (r - k) % M1 (b = M1 for k = 0)
+__device__ __forceinline__ void rr_ab(int M1, int r, int k, int& a, int& b) {
+  a = r + k;
+  b = r - k;
+  if (a >= M1) a -= M1;
+  if (b < 0) b += M1;
+  if (k == 0) b = M1;
+}
+
+// the pair of round r holding index i: its slot k, and i's partner
+__device__ __forceinline__ int rr_slot(int M1, int h, int r, int i, int& partner) {
+  if (i == M1) {
+    partner = r;
+    return 0;
+  }
+  int k1 = i - r;
+  if (k1 < 0) k1 += M1;
+  if (k1 == 0) {
+    partner = M1;
+    return 0;
+  }
+  if (k1 < h) {
+    int b = r - k1;
+    partner = b < 0 ? b + M1 : b;
+    return k1;
+  }
+  const int k = M1 - k1;
+  int a = r + k;
+  partner = a >= M1 ? a - M1 : a;
+  return k;
+}
+
+// 1/sqrt(x), x a normal double: v_rsq_f64 + two Newton steps
+__device__ __forceinline__ double marg_rsq(double x) {
+  double y = __builtin_amdgcn_rsq(x);
+  const double hx = 0.5 * x;
+  y = fma(y, fma(-hx * y, y, 0.5), y);
+  return fma(y, fma(-hx * y, y, 0.5), y);
+}
+
+// the rotation threshold (Eigen's JacobiSVD test) |a_pq| > tol sqrt|a_pp a_qq|, squared (no sqrt on the chain);
+// a_pq^2 underflowing against a zero diagonal product still rotates, as the unsquared test does
+__device__ __forceinline__ bool marg_big(double app, double aqq, double apq) {
+  const double a2 = apq * apq, pq = fabs(app * aqq);
+  return (apq != 0.0) & ((a2 > (kMargJacobiTol * kMargJacobiTol) * pq) | ((a2 == 0.0) & (pq == 0.0)));
+}
+
+// sym.schur2's quotient form for magnitudes outside the half-angle form's range
+__device__ __attribute__((noinline)) void marg_rot_wide(double dd, double e, double& c, double& s, double& t) {
+  const double th = dd / e, ath = fabs(th);
+  t = ath > 1e150 ? 0.5 / th : (th >= 0.0 ? 1.0 : -1.0) / (ath + sqrt(th * th + 1.0));
+  c = 1.0 / sqrt(t * t + 1.0);
+  s = t * c;
+}
+
+// the symmetric Schur rotation of one pair (the 2x2 step of the two-sided Jacobi), c = 1, s = t = 0 at or below the
+// threshold.  t = tan(theta) is the root of t^2 + 2 th t - 1 = 0 of smaller magnitude, th = (a_qq - a_pp) / (2 a_pq)
+// (Golub & Van Loan's sym.schur2); here from the half-angle identities without a division or an IEEE sqrt on the
+// serial chain: d = a_qq - a_pp, e = 2 a_pq, r = |(d, e)|, cos 2theta = |d| / r, c^2 = (1 + cos 2theta) / 2,
+// s = sgn(d) e / (2 r c), t = s / c -- two Newton-refined v_rsq.  Magnitudes outside [1e-140, 1e140] (never met by
+// the scaled system) take the quotient form.
+__device__ __forceinline__ bool marg_rot(double app, double aqq, double apq, double& c, double& s, double& t) {
+  const bool big = marg_big(app, aqq, apq);
+  const double dd = aqq - app, e = 2.0 * apq, ad = fabs(dd), ae = fabs(e);
+  const double ir = marg_rsq(fma(dd, dd, e * e));
+  const double hh = fma(0.5 * ad, ir, 0.5);
+  const double ic = marg_rsq(hh);
+  double ss = (dd >= 0.0 ? 0.5 : -0.5) * e * ir * ic, cc = hh * ic, tt = ss * ic;
+  if (__builtin_expect(big & !((ad < 1e140) & (ae < 1e140) & ((ad > 1e-140) | (ae > 1e-140))), 0))
+    marg_rot_wide(dd, e, cc, ss, tt);
+  c = big ? cc : 1.0;
+  s = big ? ss : 0.0;
+  t = big ? tt : 0.0;
+  return big;
+}
+
+// LDS of k_marg in doubles.  Full storage (kFull: both triangles of Omega, C padded to even m, V [C][m]) while it fits,
+// else packed upper Omega and V [C][C]; then G, b_s, and V0 (the warm start) when it fits beside them
+__host__ __device__ __forceinline__ bool marg_full(int C) {
+  const int m = C + (C & 1);
+  return m * m + C * m + 2 * C <= kMargLdsStage;
+}
+__host__ __device__ __forceinline__ int marg_lds_doubles(int C, bool& stage_v0) {
+  const int m = C + (C & 1);
+  const int base = marg_full(C) ? m * m + C * m + 2 * C : C * (C + 1) / 2 + C * C + 2 * C;
+  stage_v0 = base + C * C <= kMargLdsStage;
+  return stage_v0 ? base + C * C : base;
+}
+
+// round r's partner test of an entry (x, y), x != y (round-robin: {r, M1} and pairs with x + y = 2r mod M1)
+__device__ __forceinline__ bool rr_is_pair(int M1, int r, int c2, int x, int y) {
+  if (y == M1) return x == r;
+  if (x == M1) return y == r;
+  const int s = x + y;
+  return (s >= M1 ? s - M1 : s) == c2;
+}
+
+template <bool kFull>
 __global__ void __launch_bounds__(kMargThreads) k_marg(KbDev d, KbMarg mo, int gate) {
   if (gate && (d.ctrl->done || !d.ctrl->do_build)) return;
   extern __shared__ __attribute__((aligned(16))) double sm[];
-  const int C = d.C, n = C, m = C + (C & 1), h = m / 2, tid = threadIdx.x, nth = blockDim.x;
-  const int np = n * (n + 1) / 2, Wt = d.W - C, o0 = d.N * 136;
-  double* A = sm;       // [np] packed upper
-  double* V = A + np;   // [n][n]
-  double* G = V + n * n;  // [n]
-  double* bs = G + n;     // [n]
-  __shared__ double cs[2 * (kMargMaxC / 2 + 1)];
-  __shared__ int pq[2 * (kMargMaxC / 2 + 1)];
-  __shared__ int nrot, okl;
+  KB_TSM(d, 0);
+  const int C = d.C, n = C, m = C + (C & 1), h = m / 2, M1 = m - 1, tid = threadIdx.x, nth = blockDim.x;
+  const int lane = tid & 63;
+  const int Wt = d.W - C, o0 = d.N * 136;
+  const int ld = kFull ? m : n;  // row stride of V (and of A when full)
+  bool stage;
+  marg_lds_doubles(C, stage);
+  double* A = sm;                                          // Omega: [m][m] full, or [C(C+1)/2] packed upper
+  double* V = A + (kFull ? m * m : n * (n + 1) / 2);       // [n][ld]
+  double* G = V + n * ld;                                  // [n]
+  double* bs = G + n;                                      // [n]
+  double* V0s = bs + n;                                    // [n][n] when staged
+  auto aix = [&](int i, int j) { return kFull ? i * m + j : pk_up(i, j, n); };
+  __shared__ double dg[2][kMargMaxC];          // diagonal, ping-pong by round
+  __shared__ double ap[2][kMargMaxC];          // a_pq of the round's pairs: by slot k (packed: ping-pong by round)
+  __shared__ double csr[kMargMaxC];            // full storage: (c, s) of the round's pairs, slot k at 2k
+  __shared__ int flag[3];
+  __shared__ int okl, swarm;
   __shared__ double wsort[kMargMaxC];
   __shared__ int perm[kMargMaxC];
   __shared__ double tco[kMargMaxC];
   __shared__ double stat[4];
   __shared__ int srank;
-  // ---- load: scaling, Omega = G S G, b_s = G b, V = I
+  // ---- load: scaling, Omega = G S G, b_s = G b
   for (int i = tid; i < n; i += nth) {
     const double nrm = sqrt(d.Hcc[(size_t)i * C + i]);
     G[i] = mo.scaling ? (nrm < mo.norm_tol ? 0.0 : 1.0 / nrm) : 1.0;
   }
-  if (tid == 0) okl = !(psum_at(d, o0 + Wt + C) > 0.0);  // non-PD frame blocks
-  __syncthreads();
-  for (int e = tid; e < n * n; e += nth) {
-    const int i = e / n, j = e % n;
-    V[e] = (i == j) ? 1.0 : 0.0;
-    if (j >= i) A[pk_up(i, j, n)] = G[i] * (d.Hcc[(size_t)i * C + j] - psum_at(d, o0 + upper_index(i, j, C))) * G[j];
+  if (tid == 0) {
+    okl = !(psum_at(d, o0 + Wt + C) > 0.0);  // non-PD frame blocks
+    const int chain = (int)mo.info[5];
+    swarm = (mo.warm && chain >= 1 && chain < kMargWarmMax) ? chain : 0;
+    flag[0] = flag[1] = flag[2] = 0;
   }
+  __syncthreads();
+  KB_TSM(d, 1);
+  const int warm = swarm;
+  for (int e = tid; e < n * n; e += nth) {
+    const int i = e / n, j = e - i * n;
+    if (j >= i) {
+      const double v = G[i] * (d.Hcc[(size_t)i * C + j] - psum_at(d, o0 + upper_index(i, j, C))) * G[j];
+      A[aix(i, j)] = v;
+      if (kFull) A[j * m + i] = v;
+    }
+    if (warm && stage) V0s[e] = mo.V[e];
+  }
+  if (kFull && m > n)  // the padding row / column of an odd C: the dummy index of the round-robin, never rotated
+    for (int i = tid; i < m; i += nth) {
+      A[n * m + i] = 0.0;
+      A[i * m + n] = 0.0;
+      if (i < n) V[i * ld + n] = 0.0;
+    }
   for (int i = tid; i < n; i += nth) bs[i] = G[i] * (d.gc[i] - psum_at(d, o0 + Wt + i));
-  // ---- Jacobi sweeps
-  int sweeps = 0;
-  const int nblk = h * (h + 1) / 2;
-  for (; sweeps < kMargMaxSweeps; ++sweeps) {
-    if (tid == 0) nrot = 0;
+  __syncthreads();
+  KB_TSM(d, 2);
+  if (warm) {  // Omega <- V0^T Omega V0 (T = Omega V0 staged in V), V <- V0
+    const double* V0 = stage ? V0s : mo.V;
+    for (int e = tid; e < n * n; e += nth) {
+      const int i = e / n, j = e - i * n;
+      double s0 = 0.0, s1 = 0.0;
+      int a = 0;
+      for (; a + 1 < n; a += 2) {
+        s0 += A[aix(i, a)] * V0[a * n + j];
+        s1 += A[aix(i, a + 1)] * V0[(a + 1) * n + j];
+      }
+      if (a < n) s0 += A[aix(i, a)] * V0[a * n + j];
+      V[i * ld + j] = s0 + s1;
+    }
     __syncthreads();
-    for (int r = 0; r < m - 1; ++r) {
-      for (int k = tid; k < h; k += nth) {
-        int p, q;
-        rr_pair(m, r, k, p, q);
-        double c = 1.0, sn = 0.0;
-        if (q < n) {
-          const double apq = A[pk_up(p, q, n)], app = A[pk_up(p, p, n)], aqq = A[pk_up(q, q, n)];
-          if (apq != 0.0 && fabs(apq) > kMargJacobiTol * sqrt(fabs(app * aqq))) {
-            const double th = (aqq - app) / (2.0 * apq);
-            const double t = (th >= 0.0 ? 1.0 : -1.0) / (fabs(th) + sqrt(th * th + 1.0));
-            c = 1.0 / sqrt(t * t + 1.0);
-            sn = t * c;
-            atomicAdd(&nrot, 1);
+    for (int e = tid; e < n * n; e += nth) {
+      const int i = e / n, j = e - i * n;
+      if (j < i) continue;
+      double s0 = 0.0, s1 = 0.0;
+      int a = 0;
+      for (; a + 1 < n; a += 2) {
+        s0 += V0[a * n + i] * V[a * ld + j];
+        s1 += V0[(a + 1) * n + i] * V[(a + 1) * ld + j];
+      }
+      if (a < n) s0 += V0[a * n + i] * V[a * ld + j];
+      A[aix(i, j)] = s0 + s1;
+      if (kFull) A[j * m + i] = s0 + s1;
+    }
+    __syncthreads();
+    for (int e = tid; e < n * n; e += nth) {
+      const int i = e / n, j = e - i * n;
+      V[i * ld + j] = V0[e];
+    }
+  } else {
+    for (int e = tid; e < n * n; e += nth) {
+      const int i = e / n, j = e - i * n;
+      V[i * ld + j] = (i == j) ? 1.0 : 0.0;
+    }
+  }
+  KB_TSM(d, 3);
+  int sweeps = 0;
+  const double* w;
+  if constexpr (kFull) {
+    // ---- full storage: two barriers per round.  Phase A (lanes k < h of wave 0): the rotation of pair k in the
+    // (a, b) orientation of the round-robin from the diagonal and the pair entry, its (c, s) into LDS, the pair's own
+    // 2x2 step (diagonal, pair entry exactly 0).  Phase B (every item): an off-diagonal block (k < l) rotated by both
+    // pairs, or a (row of V, pair).  The next round's pair entries lie each in exactly one of this round's
+    // off-diagonal blocks, at positions fixed over the rounds (the round-robin is shift-invariant), so every block
+    // carries up to two precomputed (entry, slot) selectors and writes them into ap by slot.
+    double* dgs = dg[0];
+    double* aps = ap[0];
+    for (int i = tid; i < m; i += nth) dgs[i] = A[i * m + i];
+    for (int k = tid; k < h; k += nth) {
+      int a, b;
+      rr_ab(M1, 0, k, a, b);
+      aps[k] = A[a * m + b];
+    }
+    const int nob = h * (h - 1) / 2, total = nob + n * h, nit = (total + nth - 1) / nth;
+    static_assert(kMargThreads * kMargItems >= (kMargMaxC / 2) * (kMargMaxC / 2 - 1) / 2 + kMargMaxC * (kMargMaxC / 2),
+                  "k_marg items per thread");
+    int ik[kMargItems], il[kMargItems], isel[kMargItems];
+    const int rn0 = M1 > 1 ? 1 : 0, c20 = (2 * rn0) % M1;
+#pragma unroll
+    for (int j = 0; j < kMargItems; ++j) {
+      const int bI = tid + j * nth;
+      ik[j] = -1;
+      il[j] = 0;
+      isel[j] = 0;
+      if (bI < nob) {  // strictly upper (k, l): index k (2h - k - 1) / 2 + (l - k - 1)
+        const float b2 = 2.0f * h - 1.0f;
+        int k = (int)((b2 - sqrtf(b2 * b2 - 8.0f * bI)) * 0.5f);
+        k = max(0, min(k, h - 2));
+        while (k > 0 && k * (2 * h - k - 1) / 2 > bI) --k;
+        while (k + 1 < h - 1 && (k + 1) * (2 * h - k - 2) / 2 <= bI) ++k;
+        const int l = bI - k * (2 * h - k - 1) / 2 + k + 1;
+        ik[j] = k;
+        il[j] = l;
+        int ak, bk, al, bl, sel = 0, ns = 0;
+        rr_ab(M1, 0, k, ak, bk);
+        rr_ab(M1, 0, l, al, bl);
+        for (int e = 0; e < 4; ++e) {  // entry e = (row a_k | b_k) x (column a_l | b_l), its slot next round
+          const int x = (e >> 1) ? bk : ak, y = (e & 1) ? bl : al;
+          if (ns < 2 && rr_is_pair(M1, rn0, c20, x, y)) {
+            int partner;
+            const int K = rr_slot(M1, h, rn0, x, partner);
+            sel |= (1 | (e << 1) | (K << 3)) << (12 * ns);
+            ++ns;
           }
         }
-        pq[2 * k] = p;
-        pq[2 * k + 1] = q;
-        cs[2 * k] = c;
-        cs[2 * k + 1] = sn;
+        isel[j] = sel;
+      } else if (bI < total) {
+        const int e = bI - nob, i = e / h;
+        ik[j] = e - i * h;
+        il[j] = -1 - i;
       }
-      __syncthreads();
-      for (int bI = tid; bI < nblk + n * h; bI += nth) {
-        if (bI < nblk) {  // 2x2 block (k, l), l >= k, of the upper triangle of pairs
-          int k = (int)((2.0f * h + 1.0f - sqrtf((2.0f * h + 1.0f) * (2.0f * h + 1.0f) - 8.0f * bI)) * 0.5f);
-          k = max(0, min(k, h - 1));
-          while (k > 0 && k * (2 * h - k + 1) / 2 > bI) --k;
-          while (k + 1 < h && (k + 1) * (2 * h - k) / 2 <= bI) ++k;
-          const int l = k + (bI - k * (2 * h - k + 1) / 2);
-          const int p = pq[2 * k], q = pq[2 * k + 1];
-          const double ck = cs[2 * k], sk = cs[2 * k + 1];
-          if (l == k) {
-            if (q < n && sk != 0.0) {
-              const int ipq = pk_up(p, q, n);
-              const double apq = A[ipq], t = sk / ck;
-              A[pk_up(p, p, n)] -= t * apq;
-              A[pk_up(q, q, n)] += t * apq;
-              A[ipq] = 0.0;
+    }
+    __syncthreads();
+    KB_TSM(d, 4);
+    for (;; ++sweeps) {
+      {
+        bool v = false;
+        for (int e = tid; e < n * n; e += nth) {
+          const int i = e / n, j = e - i * n;
+          if (j > i) v = v || marg_big(dgs[i], dgs[j], A[i * m + j]);
+        }
+        if (tid == 0) flag[(sweeps + 1) % 3] = 0;  // last read after sweep - 2's test
+        if (__any(v) && lane == 0) flag[sweeps % 3] = 1;
+        __syncthreads();
+        if (flag[sweeps % 3] == 0 || sweeps == kMargMaxSweeps) break;
+      }
+      if (sweeps == 0) KB_TSM(d, 5);
+      for (int r = 0; r < M1; ++r) {
+        if (tid < h) {  // phase A
+          int a, b;
+          rr_ab(M1, r, tid, a, b);
+          const double aaa = dgs[a], abb = dgs[b], aab = aps[tid];
+          double c, sn, t;
+#ifdef KB_STAMPS
+          const bool rot = (d.dbg_flags & 4) ? (c = 1.0, sn = 0.0, t = 0.0, false) : marg_rot(aaa, abb, aab, c, sn, t);
+#else
+          const bool rot = marg_rot(aaa, abb, aab, c, sn, t);
+#endif
+          csr[2 * tid] = c;
+          csr[2 * tid + 1] = sn;
+          if (rot) {
+            dgs[a] = aaa - t * aab;
+            dgs[b] = abb + t * aab;
+            A[a * m + b] = 0.0;
+            A[b * m + a] = 0.0;
+          }
+          if (M1 == 1) aps[tid] = rot ? 0.0 : aab;  // one round per sweep: the same pair next round
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < kMargItems; ++j) {  // phase B
+          if (j >= nit) break;  // block-uniform
+          const int k = ik[j], l = il[j];
+          if (k < 0) continue;
+          int ak, bk;
+          rr_ab(M1, r, k, ak, bk);
+          const double ck = csr[2 * k], sk = csr[2 * k + 1];
+          if (l >= 0) {  // off-diagonal block (k, l): rows by pair k, columns by pair l (unrotated: y = x exactly)
+            int al, bl;
+            rr_ab(M1, r, l, al, bl);
+            const double cl = csr[2 * l], sl = csr[2 * l + 1];
+            const double x00 = A[ak * m + al], x01 = A[ak * m + bl], x10 = A[bk * m + al], x11 = A[bk * m + bl];
+            const double t00 = ck * x00 - sk * x10, t01 = ck * x01 - sk * x11;
+            const double t10 = sk * x00 + ck * x10, t11 = sk * x01 + ck * x11;
+            const double y00 = cl * t00 - sl * t01, y01 = sl * t00 + cl * t01;
+            const double y10 = cl * t10 - sl * t11, y11 = sl * t10 + cl * t11;
+            if (sk != 0.0 || sl != 0.0) {
+              A[ak * m + al] = y00;
+              A[al * m + ak] = y00;
+              A[ak * m + bl] = y01;
+              A[bl * m + ak] = y01;
+              A[bk * m + al] = y10;
+              A[al * m + bk] = y10;
+              A[bk * m + bl] = y11;
+              A[bl * m + bk] = y11;
+            }
+            const int sel = isel[j];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+              const int su = sel >> (12 * u);
+              if (su & 1) {
+                const int e = (su >> 1) & 3;
+                aps[(su >> 3) & 0x1ff] = e == 0 ? y00 : e == 1 ? y01 : e == 2 ? y10 : y11;
+              }
+            }
+          } else if (sk != 0.0) {  // V <- V J: row i, pair k
+            double* Vi = V + (-1 - l) * ld;
+            const double va = Vi[ak], vb = Vi[bk];
+            Vi[ak] = ck * va - sk * vb;
+            Vi[bk] = sk * va + ck * vb;
+          }
+        }
+        __syncthreads();
+        if (sweeps == 0 && r == 0) KB_TSM(d, 6);
+      }
+      if (sweeps == 0) KB_TSM(d, 7);
+    }
+    w = dgs;
+  } else {
+    // ---- round 0's diagonal and pair entries
+    for (int i = tid; i < n; i += nth) dg[0][i] = A[aix(i, i)];
+    if (kFull && m > n && tid == 0) dg[0][n] = 0.0;
+    __syncthreads();
+    for (int k = tid; k < h; k += nth) {
+      int p, q;
+      rr_pair(M1, 0, k, p, q);
+      if (kFull) ap[0][p] = A[p * m + q];
+      else ap[0][k] = q < n ? A[pk_up(p, q, n)] : 0.0;
+    }
+    // ---- this thread's items, fixed over the rounds: [0, nblk) the 2x2 blocks (k <= l) of the pairs, then
+    // [nblk, nblk + n h) (row i of V, pair k); il = -1 - i marks a V item, ik = -1 an idle slot
+    const int nblk = h * (h + 1) / 2, total = nblk + n * h, nit = (total + nth - 1) / nth;
+    static_assert(kMargThreads * kMargItems >= (kMargMaxC / 2) * (kMargMaxC / 2 + 1) / 2 + kMargMaxC * (kMargMaxC / 2),
+                  "k_marg items per thread");
+    int ik[kMargItems], il[kMargItems];
+  #pragma unroll
+    for (int j = 0; j < kMargItems; ++j) {
+      const int bI = tid + j * nth;
+      ik[j] = -1;
+      il[j] = 0;
+      if (bI < nblk) {  // upper (k, l): index k (2h - k + 1) / 2 + (l - k)
+        int k = (int)((2.0f * h + 1.0f - sqrtf((2.0f * h + 1.0f) * (2.0f * h + 1.0f) - 8.0f * bI)) * 0.5f);
+        k = max(0, min(k, h - 1));
+        while (k > 0 && k * (2 * h - k + 1) / 2 > bI) --k;
+        while (k + 1 < h && (k + 1) * (2 * h - k) / 2 <= bI) ++k;
+        ik[j] = k;
+        il[j] = k + (bI - k * (2 * h - k + 1) / 2);
+      } else if (bI < total) {
+        const int e = bI - nblk, i = e / h;
+        ik[j] = e - i * h;
+        il[j] = -1 - i;
+      }
+    }
+    __syncthreads();
+    KB_TSM(d, 4);
+    // ---- Jacobi sweeps.  Each sweep is preceded by the convergence test of the sweep it would be: no pair above the
+    // rotation threshold means no rotation anywhere in it (nothing changes), so the loop ends without running it.
+    // One barrier per round: every item derives the rotations it needs from dg / ap of the round, which the previous
+    // round's owners wrote (each next-round pair entry lies in exactly one of this round's off-diagonal blocks).
+    int it = 0;
+    for (;; ++sweeps) {
+      {
+        const double* dgc = dg[it & 1];
+        bool v = false;
+        for (int e = tid; e < n * n; e += nth) {
+          const int i = e / n, j = e - i * n;
+          if (j > i) v = v || marg_big(dgc[i], dgc[j], A[aix(i, j)]);
+        }
+        if (tid == 0) flag[(sweeps + 1) % 3] = 0;  // last read after sweep - 2's test
+        if (__any(v) && lane == 0) flag[sweeps % 3] = 1;
+        __syncthreads();
+        if (flag[sweeps % 3] == 0 || sweeps == kMargMaxSweeps) break;
+      }
+      if (sweeps == 0) KB_TSM(d, 5);
+      for (int r = 0; r < M1; ++r, ++it) {
+        const int cur = it & 1, nx = cur ^ 1, rn = (r + 1 == M1) ? 0 : r + 1;
+        const int c2 = (2 * rn) % M1;
+        const double* dgc = dg[cur];
+        const double* apc = ap[cur];
+        double* dgn = dg[nx];
+        double* apn = ap[nx];
+  #ifdef KB_STAMPS
+        if (d.dbg_flags & 2) {
+          __syncthreads();
+          continue;
+        }
+  #endif
+  #pragma unroll
+        for (int j = 0; j < kMargItems; ++j) {
+          if (j >= nit) break;  // block-uniform
+          const int k = ik[j], l = il[j];
+          if (k < 0) continue;
+          int p, q;
+          rr_pair(M1, r, k, p, q);
+          if constexpr (kFull) {
+            // padded: every index < m is valid storage, the dummy pair's a_pq is 0 and never rotates.  Straight-line:
+            // every item reads its pairs' diagonal / a_pq and its 2x2 entries (rows p, q of Omega for a block, row i of
+            // V twice for a V item) up front, derives both rotations, and only the writes are predicated
+            const bool isV = l < 0, isD = l == k;
+            int r2, s2;
+            rr_pair(M1, r, isV ? k : l, r2, s2);
+            const int row0 = isV ? -1 - l : p, row1 = isV ? row0 : q;
+            const double* base = isV ? V : A;
+            const double app = dgc[p], aqq = dgc[q], apq = apc[p];
+            const double arr = dgc[r2], ass = dgc[s2], ars = apc[r2];
+            const double x00 = base[row0 * ld + r2], x01 = base[row0 * ld + s2];
+            const double x10 = base[row1 * ld + r2], x11 = base[row1 * ld + s2];
+            double ck, sk, tk, cl, sl, tl;
+  #ifdef KB_STAMPS
+            const bool rk = (d.dbg_flags & 4) ? (ck = 1.0, sk = 0.0, tk = 0.0, false) : marg_rot(app, aqq, apq, ck, sk, tk);
+            const bool rl = (d.dbg_flags & 4) ? (cl = 1.0, sl = 0.0, tl = 0.0, false) : marg_rot(arr, ass, ars, cl, sl, tl);
+  #else
+            const bool rk = marg_rot(app, aqq, apq, ck, sk, tk);
+            const bool rl = marg_rot(arr, ass, ars, cl, sl, tl);
+  #endif
+            const double cr = isV ? 1.0 : ck, sr = isV ? 0.0 : sk;  // a V item rotates its columns only
+            const double t00 = cr * x00 - sr * x10, t01 = cr * x01 - sr * x11;
+            const double t10 = sr * x00 + cr * x10, t11 = sr * x01 + cr * x11;
+            const double y00 = cl * t00 - sl * t01, y01 = sl * t00 + cl * t01;
+            const double y10 = cl * t10 - sl * t11, y11 = sl * t10 + cl * t11;
+            if (isD) {  // diagonal block: the pair's own 2x2 step, the pair entry exactly 0
+              dgn[p] = rk ? app - tk * apq : app;
+              dgn[q] = rk ? aqq + tk * apq : aqq;
+              if (rk) {
+                A[p * m + q] = 0.0;
+                A[q * m + p] = 0.0;
+              }
+              if (M1 == 1) apn[p] = rk ? 0.0 : apq;  // one round per sweep: the same pair next round
+            } else if (isV) {  // V <- V J: row i, pair k
+              if (rl) {
+                V[row0 * ld + r2] = y00;
+                V[row0 * ld + s2] = y01;
+              }
+            } else {  // off-diagonal block (k, l): rows by pair k, columns by pair l (unrotated: y = x exactly)
+              if (rk || rl) {
+                A[p * m + r2] = y00;
+                A[r2 * m + p] = y00;
+                A[p * m + s2] = y01;
+                A[s2 * m + p] = y01;
+                A[q * m + r2] = y10;
+                A[r2 * m + q] = y10;
+                A[q * m + s2] = y11;
+                A[s2 * m + q] = y11;
+              }
+              if (rr_is_pair(M1, rn, c2, p, r2)) apn[min(p, r2)] = y00;
+              if (rr_is_pair(M1, rn, c2, p, s2)) apn[min(p, s2)] = y01;
+              if (rr_is_pair(M1, rn, c2, q, r2)) apn[min(q, r2)] = y10;
+              if (rr_is_pair(M1, rn, c2, q, s2)) apn[min(q, s2)] = y11;
             }
           } else {
-            const int r2 = pq[2 * l], s2 = pq[2 * l + 1];
-            const double cl = cs[2 * l], sl = cs[2 * l + 1];
-            if (sk != 0.0 || sl != 0.0) {
-              const bool rv = r2 < n, sv = s2 < n, qv = q < n;
-              const double apr = rv ? A[pk_up(p, r2, n)] : 0.0, aps = sv ? A[pk_up(p, s2, n)] : 0.0;
-              const double aqr = (qv && rv) ? A[pk_up(q, r2, n)] : 0.0, aqs = (qv && sv) ? A[pk_up(q, s2, n)] : 0.0;
-              const double tpr = ck * apr - sk * aqr, tps = ck * aps - sk * aqs;
-              const double tqr = sk * apr + ck * aqr, tqs = sk * aps + ck * aqs;
-              if (rv) A[pk_up(p, r2, n)] = cl * tpr - sl * tps;
-              if (sv) A[pk_up(p, s2, n)] = sl * tpr + cl * tps;
-              if (qv && rv) A[pk_up(q, r2, n)] = cl * tqr - sl * tqs;
-              if (qv && sv) A[pk_up(q, s2, n)] = sl * tqr + cl * tqs;
+            const bool qv = q < n;
+            const double app = dgc[p], aqq = qv ? dgc[q] : 0.0, apq = qv ? apc[k] : 0.0;
+            double ck, sk, tk;
+            const bool rk = marg_rot(app, aqq, apq, ck, sk, tk);
+            if (l == k) {
+              if (rk) {
+                dgn[p] = app - tk * apq;
+                dgn[q] = aqq + tk * apq;
+                A[pk_up(p, q, n)] = 0.0;
+              } else {
+                dgn[p] = app;
+                if (qv) dgn[q] = aqq;
+              }
+              if (M1 == 1) apn[k] = rk ? 0.0 : apq;
+            } else if (l >= 0) {
+              int r2, s2;
+              rr_pair(M1, r, l, r2, s2);
+              const bool sv = s2 < n;
+              const int ipr = pk_up(p, r2, n), ips = pk_up(p, s2, n), iqr = pk_up(q, r2, n), iqs = pk_up(q, s2, n);
+              double apr = A[ipr], aps = sv ? A[ips] : 0.0, aqr = qv ? A[iqr] : 0.0, aqs = (qv && sv) ? A[iqs] : 0.0;
+              double cl, sl, tl;
+              const bool rl = marg_rot(dgc[r2], sv ? dgc[s2] : 0.0, sv ? apc[l] : 0.0, cl, sl, tl);
+              if (rk || rl) {
+                const double tpr = ck * apr - sk * aqr, tps = ck * aps - sk * aqs;
+                const double tqr = sk * apr + ck * aqr, tqs = sk * aps + ck * aqs;
+                apr = cl * tpr - sl * tps;
+                aps = sl * tpr + cl * tps;
+                aqr = cl * tqr - sl * tqs;
+                aqs = sl * tqr + cl * tqs;
+                A[ipr] = apr;
+                if (sv) A[ips] = aps;
+                if (qv) A[iqr] = aqr;
+                if (qv && sv) A[iqs] = aqs;
+              }
+              int pa;
+              int kk = rr_slot(M1, h, rn, p, pa);
+              if (pa == r2) apn[kk] = apr;
+              else if (sv && pa == s2) apn[kk] = aps;
+              if (qv) {
+                kk = rr_slot(M1, h, rn, q, pa);
+                if (pa == r2) apn[kk] = aqr;
+                else if (sv && pa == s2) apn[kk] = aqs;
+              }
+            } else if (rk) {
+              double* Vi = V + (-1 - l) * ld;
+              const double vp = Vi[p], vq = Vi[q];
+              Vi[p] = ck * vp - sk * vq;
+              Vi[q] = sk * vp + ck * vq;
             }
           }
-        } else {  // V <- V J: row i, pair k
-          const int e = bI - nblk, i = e / h, k = e % h;
-          const int p = pq[2 * k], q = pq[2 * k + 1];
-          const double c = cs[2 * k], sn = cs[2 * k + 1];
-          if (q < n && sn != 0.0) {
-            const double vp = V[i * n + p], vq = V[i * n + q];
-            V[i * n + p] = c * vp - sn * vq;
-            V[i * n + q] = sn * vp + c * vq;
-          }
         }
+        __syncthreads();
+        if (sweeps == 0 && r == 0) KB_TSM(d, 6);
       }
-      __syncthreads();
+      if (sweeps == 0) KB_TSM(d, 7);
     }
-    const int nr = nrot;
-    __syncthreads();
-    if (nr == 0) break;
+    w = dg[it & 1];
   }
+  KB_TSM(d, 8);
   // ---- sort by |w| descending (ties: lower index first); singular values |w|
   for (int i = tid; i < n; i += nth) {
-    const double wi = A[pk_up(i, i, n)], ai = fabs(wi);
+    const double wi = w[i], ai = fabs(wi);
     int pos = 0;
     for (int j = 0; j < n; ++j) {
-      const double aj = fabs(A[pk_up(j, j, n)]);
+      const double aj = fabs(w[j]);
       pos += (aj > ai || (aj == ai && j < i)) ? 1 : 0;
     }
     wsort[pos] = wi;
     perm[pos] = i;
   }
   __syncthreads();
+  KB_TSM(d, 9);
   for (int e = tid; e < n * n; e += nth) {
-    const int r = e / n, j = e % n;
-    mo.V[e] = V[r * n + perm[j]];
+    const int r = e / n, j = e - r * n;
+    mo.V[e] = V[r * ld + perm[j]];
   }
   for (int j = tid; j < n; j += nth) mo.sv[j] = fabs(wsort[j]);
-  if (tid == 0) {  // rankTol, estimateNumericalRank, svGap, log2 sum (linalg.cpp:243-282; LinearSolver.cpp:197-201)
+  if (tid < 64) {  // rankTol, estimateNumericalRank, svGap, log2 sum (linalg.cpp:243-282; LinearSolver.cpp:197-201)
     const double tol = (mo.svd_tol != -1.0) ? mo.svd_tol : fabs(wsort[0]) * mo.eps_svd * n;
-    int rank = n;
-    for (int i = n - 1; i > 0; --i) {
-      if (fabs(wsort[i]) > tol) break;
-      --rank;
-    }
+    // estimateNumericalRank counts down from the end while |w| <= tol: rank = 1 + the last index above tol (>= 1)
+    int last = 0;
+    for (int i = lane; i < n; i += 64)
+      if (fabs(wsort[i]) > tol) last = max(last, i);
+    for (int o = 32; o > 0; o >>= 1) last = max(last, __shfl_xor(last, o));
+    const int rank = last + 1;
     double l2 = 0.0;
-    for (int i = 0; i < rank; ++i) l2 += log(fabs(wsort[i]));
-    srank = rank;
-    stat[0] = tol;
-    stat[1] = rank < n ? fabs(wsort[rank - 1]) / fabs(wsort[rank]) : __builtin_inf();
-    stat[2] = l2 / log(2.0);
+    for (int i = lane; i < rank; i += 64) l2 += log(fabs(wsort[i]));
+    for (int o = 32; o > 0; o >>= 1) l2 += __shfl_xor(l2, o);
+    if (lane == 0) {
+      srank = rank;
+      stat[0] = tol;
+      stat[1] = rank < n ? fabs(wsort[rank - 1]) / fabs(wsort[rank]) : __builtin_inf();
+      stat[2] = l2 / log(2.0);
+    }
   }
   __syncthreads();
+  KB_TSM(d, 10);
   const int rank = srank;
   // ---- truncated solve: t_j = (v_j . b_s) / w_j, x = G V_r t
   for (int j = tid; j < rank; j += nth) {
     const int pj = perm[j];
     double s = 0.0;
-    for (int i = 0; i < n; ++i) s += V[i * n + pj] * bs[i];
+    for (int i = 0; i < n; ++i) s += V[i * ld + pj] * bs[i];
     tco[j] = s / wsort[j];
   }
   __syncthreads();
   if (mo.write_dx) {
     for (int i = tid; i < n; i += nth) {
       double s = 0.0;
-      for (int j = 0; j < rank; ++j) s += V[i * n + perm[j]] * tco[j];
+      for (int j = 0; j < rank; ++j) s += V[i * ld + perm[j]] * tco[j];
       d.dx[i] = G[i] * s;
     }
   }
@@ -2521,8 +2952,12 @@ __global__ void __launch_bounds__(kMargThreads) k_marg(KbDev d, KbMarg mo, int g
     mo.info[2] = stat[0];
     mo.info[3] = stat[1];
     mo.info[4] = stat[2];
+    bool fin = true;
+    for (int i = 0; i < n; ++i) fin = fin && isfinite(wsort[i]);
+    mo.info[5] = fin ? (double)(warm ? warm + 1 : 1) : 0.0;  // a non-finite result restarts cold
     if (!okl) d.ctrl->solve_ok = 0;
   }
+  KB_TSM(d, 11);
 }
 
 // ---------------------------------------------------------------------------------------------
