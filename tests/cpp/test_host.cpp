@@ -1044,10 +1044,8 @@ int main(int argc, char** argv) {
       LinearSolverOptions lo;
       lo.columnScaling = true;  // CalibrateCameras.cpp:263-267
       lo.epsSVD = 1e-6;
-      if (std::getenv("KB_INCR_EAGER_ONLY")) {  // profiling runs: the eager device loop only (no pass graphs)
+      if (std::getenv("KB_INCR_EAGER_ONLY")) {  // profiling runs: the default (eager) device loop only
         auto ge = std::make_shared<GpuMarginalLinearSolver>(lo);
-        ge->useGraph = false;
-        ge->syncEvery = 2;
         const auto te = std::chrono::steady_clock::now();
         const IncrRun rr = run_estimator(p, ge, delta, maxIt);
         const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - te).count();
@@ -1079,6 +1077,13 @@ int main(int argc, char** argv) {
         }
       }
       eager_json += "}";
+      // the device loop over captured pass graphs (recaptured whenever a batch appends frames)
+      auto gg = std::make_shared<GpuMarginalLinearSolver>(lo);
+      gg->useGraph = true;
+      gg->syncEvery = 0;
+      t0 = std::chrono::steady_clock::now();
+      const IncrRun gr = run_estimator(p, gg, delta, maxIt);
+      const double grsec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
       // the same estimator over the same GPU solver, its optimisation driven from the host per call (no kb_optimize_marginal)
       auto hl = std::make_shared<GpuMarginalLinearSolver>(lo);
       hl->deviceLoop = false;
@@ -1107,12 +1112,16 @@ int main(int argc, char** argv) {
           "\"gn_iterations_same_batches\": %ld, \"same_decisions\": %s, \"wall_gpu\": %.6f, \"wall_cpu\": %.6f, "
           "\"gpu_host_loop_seconds\": %.6f, \"host_loop_same_decisions\": %s, \"state_diff_host_loop\": %.3e, "
           "\"gpu_eager_seconds\": %.6f, \"eager_sync_every\": %d, \"eager_same_decisions\": %s, \"state_diff_eager\": %.3e, "
-          "\"gpu_eager_seconds_by_sync\": %s, \"profile_graph\": %s, \"profile_host_loop\": %s}\n",
+          "\"gpu_eager_seconds_by_sync\": %s, \"gpu_default\": \"device loop, eager launches, sync every 2 passes\", "
+          "\"speedup_same_batches\": %.3f, \"gpu_graph_seconds\": %.6f, \"graph_same_decisions\": %s, "
+          "\"state_diff_graph\": %.3e, \"profile_default\": %s, \"profile_graph\": %s, \"profile_host_loop\": %s}\n",
           g.secs.size(), std::accumulate(g.secs.begin(), g.secs.end(), 0.0), acc_g, it_g, c.secs.size(), threads, c_k,
           g_k, it_gk, same ? "true" : "false", gsec, csec, ghsec, same_h ? "true" : "false",
           maxdiff(g.state, gh.state, 0, g.state.size()), gesec, sync,
           gev.accepted == g.accepted && gev.iters == g.iters ? "true" : "false", maxdiff(g.state, gev.state, 0, g.state.size()),
-          eager_json.c_str(), jv(g.profile).c_str(), jv(gh.profile).c_str());
+          eager_json.c_str(), g_k > 0.0 ? c_k / g_k : 0.0, grsec,
+          gr.accepted == g.accepted && gr.iters == g.iters ? "true" : "false", maxdiff(g.state, gr.state, 0, g.state.size()),
+          jv(g.profile).c_str(), jv(gr.profile).c_str(), jv(gh.profile).c_str());
       return 0;
     }
     if (mode == "incr-cpu" || mode == "incr-gpu") {
