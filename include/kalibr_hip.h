@@ -271,6 +271,13 @@ int kb_comm_init(kb_handle* h, const void* unique_id128, int32_t nranks, int32_t
  * then be driven from its own host thread: the collectives of a pass meet in a host barrier (60 s timeout ->
  * error).  Passes run eagerly, not graph-captured.  Used to test the sharded path with several ranks on one GPU. */
 int kb_comm_init_local(kb_handle* const* handles, int32_t n);
+/* Direct all-reduce of the sharded camera-block image (C > 64, GN fused passes; replaces the collective of
+ * LinearSystemSolver.cpp:81-92's host sum): kb_comm_init / kb_comm_init_local map every rank's exchange region (IPC
+ * handles all-gathered over the communicator; the members' buffers in-process), self-test one exchange, and from then
+ * on k_xar sums the ranks' partial images in rank order on every rank, reading the peers over xGMI -- no RCCL
+ * collective for it, bitwise-identical images on all ranks.  KB_DIRECT_AR=0, a failed mapping or a failed self-test
+ * (agreed over all ranks) keep the collective.  Returns 1 when the handle uses the direct path. */
+int kb_comm_direct(const kb_handle* h);
 
 /* Self test of the f64 MFMA fragment layout used by the build kernel (A = I, asymmetric B). */
 int kb_selftest_mfma(double* max_err);

@@ -128,6 +128,7 @@ struct kb_handle {
   std::vector<int32_t> frame_v0;    // [F + 1] first view of each frame (frame_v0[F] = V)
   size_t pcg_F = 0, rjr_F = 0, cond_n = 0;  // frame count / columns the lazily allocated buffers are sized for
   double* ximg_part = nullptr;  // sharded + xexp: this rank's partial image (all-reduced into d.simg)
+  std::vector<void*> xar_opened;  // peers' exchange regions mapped by IPC handles (closed by kb_destroy)
   bool buildp_wide = false;  // k_buildp<.., MW = 8> (multi-model rigs with <= 8 waves per block)
   double* rjr = nullptr;     // [F + 1] kb_rhs_jtj_rhs: per-frame terms | result
   int gn_prepared = -1;      // kb_gn_prepare'd pass count, consumed by kb_gn_launch (-1: nothing prepared; every
@@ -293,6 +294,11 @@ static void drop_graphs(kb_handle* h) {
 static void unprepare(kb_handle* h) { h->gn_prepared = -1; }
 
 static bool sharded(const kb_handle* h) { return h->comm || h->lg; }
+
+// a k_xar wait that timed out (a peer rank never published its partial image): the pass results are void
+static int comm_check(const KbCtrl& c) {
+  return c.comm_err ? fail("direct all-reduce (k_xar): a peer rank did not arrive within 2 s") : 0;
+}
 
 // one collective of the in-process group: every member publishes its send buffer and an event, waits for all
 // members' events, copies / sums on its own stream, then waits until every member has read its buffer
@@ -619,6 +625,7 @@ void kb_destroy(kb_handle* h) {
   hipSetDevice(h->device);
   if (h->stream) hipStreamSynchronize(h->stream);
   drop_graphs(h);
+  for (void* p : h->xar_opened) hipIpcCloseMemHandle(p);
   if (h->comm) ncclCommDestroy(h->comm);
   if (h->lg && --h->lg->refs == 0) {
     for (auto e : h->lg->ready) hipEventDestroy(e);
@@ -924,7 +931,14 @@ static int launch_colsum(kb_handle* h, int gate, bool finish = true) {
     const int nx = (h->C + 1) + (d.Wtot - h->N * 136);
     hipLaunchKernelGGL(k_colsumx, dim3((nx + 63) / 64), dim3(64 * kColsum1Waves), 0, h->stream, d, gate);
     KB_HIP(hipGetLastError());
-    if (sharded(h) && coll_allreduce(h, h->ximg_part, d.simg, d.img_n)) return -1;
+    if (sharded(h)) {
+      if (d.xar) {  // direct: every rank sums the ranks' partial images itself (k_xar)
+        hipLaunchKernelGGL(k_xar, dim3(kXarBlocks), dim3(256), 0, h->stream, d, gate);
+        KB_HIP(hipGetLastError());
+      } else if (coll_allreduce(h, h->ximg_part, d.simg, d.img_n)) {
+        return -1;
+      }
+    }
     return 0;
   }
   if (finish && h->C > 64) {
@@ -1600,10 +1614,12 @@ int kb_optimize(kb_handle* h, const kb_optimizer_options* opts, kb_solution* out
     passes += n;
     KB_HIP(hipMemcpyAsync(&ctrl, h->d.ctrl, sizeof(KbCtrl), hipMemcpyDeviceToHost, h->stream));
     KB_HIP(hipStreamSynchronize(h->stream));
+    if (comm_check(ctrl)) return -1;
     if (ctrl.done) break;
   }
   if (finish_pass(h, opts->policy)) return -1;
   KB_HIP(hipMemcpy(&ctrl, h->d.ctrl, sizeof(KbCtrl), hipMemcpyDeviceToHost));
+  if (comm_check(ctrl)) return -1;
   h->cur = ctrl.cur;
   out->J_start = ctrl.J_start;
   out->J_final = ctrl.p_J;
@@ -1817,6 +1833,7 @@ int kb_gn_launch(kb_handle* h, int32_t n_iter, double* seconds) {
   KbCtrl ctrl{};
   KB_HIP(hipMemcpy(&ctrl, h->d.ctrl, sizeof(KbCtrl), hipMemcpyDeviceToHost));
   h->cur = ctrl.cur;
+  if (comm_check(ctrl)) return -1;
   if (ctrl.iterations != n_iter) return fail("kb_gn_launch: linear solver failures during the timed passes");
   return 0;
 }
@@ -2024,6 +2041,170 @@ static int shard_setup(kb_handle* h, int nranks, int rank, int F_max) {
   return 0;
 }
 
+// ---------------------------------------------------------------- direct all-reduce (k_xar) setup
+// KB_DIRECT_AR=0 keeps the collective (RCCL / the in-process copies) for the sharded image
+static bool xar_env_on() {
+  const char* e = std::getenv("KB_DIRECT_AR");
+  return !(e && e[0] == '0');
+}
+
+// this rank's exchange region: flags + two image halves, zeroed (the base of its own allocation: IPC-exportable)
+static int xar_region(kb_handle* h, double** out) {
+  return h->alloc(out, (size_t)kXarFlagDoubles + 2 * (size_t)h->d.img_n);
+}
+
+static int xar_install(kb_handle* h, double* own, const std::vector<double*>& peers) {
+  double** tab = nullptr;
+  if (h->alloc(&tab, peers.size())) return -1;
+  KB_HIP(hipMemcpyAsync(tab, peers.data(), sizeof(double*) * peers.size(), hipMemcpyHostToDevice, h->stream));
+  KB_HIP(hipStreamSynchronize(h->stream));
+  h->d.xar_buf = own;
+  h->d.xar_peers = tab;
+  h->d.xar = 1;
+  drop_graphs(h);
+  return 0;
+}
+
+static void xar_uninstall(kb_handle* h) {
+  h->d.xar = 0;
+  drop_graphs(h);
+}
+
+// self-test, part 1 (every rank, concurrently): known partial images, one k_xar launch
+static int xar_selftest_launch(kb_handle* h) {
+  unsigned long long f0 = 0;
+  KB_HIP(hipMemcpyAsync(&f0, h->d.xar_buf, sizeof(f0), hipMemcpyDeviceToHost, h->stream));
+  KB_HIP(hipStreamSynchronize(h->stream));
+  hipLaunchKernelGGL(k_xar_fill, dim3((h->d.img_n + 255) / 256), dim3(256), 0, h->stream, h->d, (int)((f0 + 1) & 1));
+  hipLaunchKernelGGL(k_xar, dim3(kXarBlocks), dim3(256), 0, h->stream, h->d, 0);
+  KB_HIP(hipGetLastError());
+  return 0;
+}
+
+// part 2: the exact sums arrived, no timeout; the control block's error flag cleared again
+static int xar_selftest_check(kb_handle* h, int& ok) {
+  std::vector<double> img(h->d.img_n);
+  KbCtrl ctrl{};
+  KB_HIP(hipMemcpyAsync(img.data(), h->d.simg, sizeof(double) * img.size(), hipMemcpyDeviceToHost, h->stream));
+  KB_HIP(hipMemcpyAsync(&ctrl, h->d.ctrl, sizeof(KbCtrl), hipMemcpyDeviceToHost, h->stream));
+  KB_HIP(hipStreamSynchronize(h->stream));
+  const double R = h->nranks, base = R * (R + 1) / 2 * 0.125;
+  ok = ctrl.comm_err ? 0 : 1;
+  for (size_t i = 0; i < img.size() && ok; ++i) ok = img[i] == base + R * (double)(i % 7);
+  const int zero = 0;
+  KB_HIP(hipMemcpyAsync(&h->d.ctrl->comm_err, &zero, sizeof(int), hipMemcpyHostToDevice, h->stream));
+  // both image halves back to zeros: k_colsumx writes only the image's live entries, the rest must sum to 0
+  KB_HIP(hipMemsetAsync(h->d.xar_buf + kXarFlagDoubles, 0, sizeof(double) * 2 * (size_t)h->d.img_n, h->stream));
+  KB_HIP(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+// multi-process ranks (RCCL communicator up): export this rank's region as an IPC handle, all-gather the handles,
+// map the peers', self-test; every step's outcome is agreed over the communicator (all ranks enable the direct path
+// or none does), every rank runs the same collectives whatever its own outcome
+static int xar_setup_rccl(kb_handle* h) {
+  if (!h->xexp || h->nranks < 2 || h->nranks > kXMaxRanksDev) return 0;
+  int ok = xar_env_on() ? 1 : 0;
+  double* own = nullptr;
+  hipIpcMemHandle_t mh;
+  std::memset(&mh, 0, sizeof(mh));
+  if (ok && xar_region(h, &own)) ok = 0;
+  if (ok && hipIpcGetMemHandle(&mh, own) != hipSuccess) {
+    hipGetLastError();
+    ok = 0;
+  }
+  constexpr size_t kSlot = sizeof(hipIpcMemHandle_t) + 8;
+  char* dx = nullptr;
+  KB_HIP(hipMalloc(&dx, kSlot * (h->nranks + 1)));
+  std::vector<char> slot(kSlot, 0);
+  std::memcpy(slot.data(), &mh, sizeof(mh));
+  std::memcpy(slot.data() + sizeof(mh), &ok, sizeof(int));
+  KB_HIP(hipMemcpyAsync(dx, slot.data(), kSlot, hipMemcpyHostToDevice, h->stream));
+  KB_NCCL(ncclAllGather(dx, dx + kSlot, kSlot, ncclChar, h->comm, h->stream));
+  std::vector<char> all(kSlot * h->nranks);
+  KB_HIP(hipMemcpyAsync(all.data(), dx + kSlot, all.size(), hipMemcpyDeviceToHost, h->stream));
+  KB_HIP(hipStreamSynchronize(h->stream));
+  std::vector<double*> peers(h->nranks, nullptr);
+  for (int q = 0; q < h->nranks && ok; ++q) {
+    int okq = 0;
+    std::memcpy(&okq, all.data() + kSlot * q + sizeof(mh), sizeof(int));
+    if (!okq) ok = 0;
+  }
+  for (int q = 0; q < h->nranks && ok; ++q) {
+    if (q == h->rank) {
+      peers[q] = own;
+      continue;
+    }
+    hipIpcMemHandle_t hq;
+    std::memcpy(&hq, all.data() + kSlot * q, sizeof(hq));
+    void* p = nullptr;
+    if (hipIpcOpenMemHandle(&p, hq, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+      hipGetLastError();
+      ok = 0;
+      break;
+    }
+    h->xar_opened.push_back(p);
+    peers[q] = (double*)p;
+  }
+  auto agree = [&](int v) -> int {  // min over ranks
+    int* di = (int*)dx;
+    if (hipMemcpyAsync(di, &v, sizeof(int), hipMemcpyHostToDevice, h->stream) != hipSuccess) return 0;
+    if (ncclAllReduce(di, di, 1, ncclInt32, ncclMin, h->comm, h->stream) != ncclSuccess) return 0;
+    int r = 0;
+    if (hipMemcpyAsync(&r, di, sizeof(int), hipMemcpyDeviceToHost, h->stream) != hipSuccess) return 0;
+    if (hipStreamSynchronize(h->stream) != hipSuccess) return 0;
+    return r;
+  };
+  ok = agree(ok);
+  if (ok && xar_install(h, own, peers)) ok = 0;
+  ok = agree(ok);
+  if (ok) {
+    int t = 0;
+    if (xar_selftest_launch(h) || xar_selftest_check(h, t)) t = 0;
+    ok = agree(t);
+  }
+  if (!ok && h->d.xar) xar_uninstall(h);
+  hipFree(dx);
+  return 0;
+}
+
+// in-process groups: the members' regions directly (same process, peer access enabled by kb_comm_init_local).  The
+// members' k_xar launches must run concurrently, which separate devices guarantee.  Members sharing one device depend
+// on the hardware queues co-scheduling them while the group's other collectives (host barriers, cross-stream event
+// waits) hold the members' streams in step: measured reliable for 2 members, not for 3 (a k_xar that waits in vain
+// times out), so a shared device takes the direct path at 2 members only.  The self-test, run on every member's
+// stream before any member syncs, proves the co-scheduling before the group relies on it.
+static void xar_setup_local(kb_handle* const* hs, int n) {
+  if (n < 2 || n > kXMaxRanksDev || !xar_env_on()) return;
+  bool distinct = true;
+  for (int r = 0; r < n; ++r) {
+    if (!hs[r]->xexp) return;
+    for (int q = 0; q < r; ++q) distinct = distinct && hs[q]->device != hs[r]->device;
+  }
+  if (!distinct && n > 2) return;
+  std::vector<double*> regs(n, nullptr);
+  for (int r = 0; r < n; ++r)
+    if (hipSetDevice(hs[r]->device) != hipSuccess || xar_region(hs[r], &regs[r])) return;
+  int ok = 1;
+  for (int r = 0; r < n && ok; ++r)
+    if (hipSetDevice(hs[r]->device) != hipSuccess || xar_install(hs[r], regs[r], regs)) ok = 0;
+  for (int r = 0; r < n && ok; ++r)
+    if (hipSetDevice(hs[r]->device) != hipSuccess || xar_selftest_launch(hs[r])) ok = 0;
+  for (int r = 0; r < n && ok; ++r) {
+    int t = 0;
+    if (hipSetDevice(hs[r]->device) != hipSuccess || xar_selftest_check(hs[r], t)) t = 0;
+    ok = t;
+  }
+  if (!ok)
+    for (int r = 0; r < n; ++r) {
+      hipSetDevice(hs[r]->device);
+      if (hs[r]->d.xar) xar_uninstall(hs[r]);
+    }
+  hipGetLastError();
+}
+
+int kb_comm_direct(const kb_handle* h) { return h && h->d.xar ? 1 : 0; }
+
 int kb_comm_init(kb_handle* h, const void* uid, int32_t nranks, int32_t rank) {
   if (!h || !uid) return fail("kb_comm_init: null");
   KB_HIP(hipSetDevice(h->device));
@@ -2039,7 +2220,8 @@ int kb_comm_init(kb_handle* h, const void* uid, int32_t nranks, int32_t rank) {
   int F_max = 0;
   KB_HIP(hipMemcpyAsync(&F_max, fm, sizeof(int), hipMemcpyDeviceToHost, h->stream));
   KB_HIP(hipStreamSynchronize(h->stream));
-  return shard_setup(h, nranks, rank, F_max);
+  if (shard_setup(h, nranks, rank, F_max)) return -1;
+  return xar_setup_rccl(h);
 }
 
 int kb_comm_init_local(kb_handle* const* hs, int32_t n) {
@@ -2121,6 +2303,7 @@ int kb_comm_init_local(kb_handle* const* hs, int32_t n) {
     hs[r]->lg = G;
     ++G->refs;
   }
+  xar_setup_local(hs, n);
   return 0;
 }
 

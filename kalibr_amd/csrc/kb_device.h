@@ -25,6 +25,7 @@ struct KbCtrl {
   int iterations, failed_iterations, max_iterations, policy, n_trace, passes;
   int pending;  // a pass ran its solve: its accept/revert + the next prelude are still to apply
   int have_dx;  // GN fused passes: the last solve's dx is still to apply (by the next build or the finish)
+  int comm_err;  // k_xar: a peer rank did not arrive within kXarTimeoutTicks (the host fails the call)
   double J, p_J, J_start, deltaX, deltaJ, eps_x, eps_j;
   double pol_J, pol_pJ, last_succ, lambda, mu;
   double dxdx, dxrhs;
@@ -36,6 +37,10 @@ struct KbOpts {
 };
 
 constexpr int kColsumRows = 8;  // stage-1 row splits of the block partial reduction
+constexpr int kXarBlocks = 32;        // k_xar blocks (each sums one chunk of the image over the ranks)
+constexpr int kXMaxRanksDev = 64;     // k_xar ranks (peer table in LDS)
+constexpr int kXarFlagDoubles = 64;   // flag area of an exchange region (kXarBlocks u64, padded to 512 B)
+constexpr unsigned long long kXarTimeoutTicks = 200000000ull;  // 2 s of s_memrealtime (100 MHz)
 
 // k_marg (marginal truncated-SVD camera solve, aslam_incremental_calibration LinearSolver)
 constexpr int kMargThreads = 1024;
@@ -43,8 +48,8 @@ constexpr int kMargMaxC = 112;         // packed Omega + V in LDS: C(C+1)/2 + C^
 constexpr int kMargMaxSweeps = 40;
 constexpr double kMargJacobiTol = 1.1102230246251565e-16;  // skip |a_pq| <= 2^-53 sqrt|a_pp a_qq|
 constexpr int kMargItems = 8;    // k_marg items (2x2 blocks, rows of V) per thread at C <= kMargMaxC
-constexpr int kMargWarmMax = 32;
-constexpr int kMargLdsStage = 19000;  // dynamic LDS doubles up to which V0 is staged in LDS too (static ~5 KB beside)  // consecutive warm starts before a cold (identity) start bounds V's orthogonality drift
+constexpr int kMargWarmMax = 32;     // consecutive warm starts before a cold (identity) start bounds V's orthogonality drift
+constexpr int kMargLdsStage = 19000;  // dynamic LDS doubles up to which V0 is staged in LDS too (static ~7 KB beside)
 // block size of k_marg: one thread per 2x2 block of pairs and per (row of V, pair), whole waves
 inline int marg_threads(int C) {
   const int h = (C + (C & 1)) / 2, items = h * (h + 1) / 2 + C * h;
@@ -118,6 +123,12 @@ struct KbDev {
   int xexp;
   int bp_tg;   // k_buildp: the target corners staged in LDS (the host's LDS budget decides)
   double* ximg;  // image the column sums are written to: simg (one GPU) or this rank's partial image (sharded)
+  // direct all-reduce of the sharded image (k_xar, kb_comm_init / kb_comm_init_local): this rank's exchange region
+  // [kXarFlagDoubles flags (one u64 per k_xar block) | partial image, even launches | odd launches] and the regions of
+  // every rank (rank order; peers mapped by IPC handles), k_colsumx writes its partial image into the region
+  int xar;
+  double* xar_buf;
+  double* const* xar_peers;
   // per-pass timing query only (kb_gn_pass_times): [0] arrival counter | [1 ..] s_memrealtime (100 MHz) at the start of
   // each pass's build kernel (block 0), null otherwise
   unsigned long long* pass_ts;

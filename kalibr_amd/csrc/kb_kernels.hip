@@ -2155,7 +2155,7 @@ __global__ void __launch_bounds__(64 * kColsum1Waves) k_colsumx(KbDev d, int gat
   const int nx = (C + 1) + (d.Wtot - N * 136);
   const int e = x <= C ? x : x - (C + 1) + N * 136;
   const bool mx = e >= d.Wp;
-  const int ec = min(e, d.Wtot - 1);
+  const int ec = min(e, d.Wp);  // the block rows hold one max|dx_f| column (Wp); rank r's image slot takes it
   constexpr int U = 24;
   const int done = c->done;
   double v[U];
@@ -2188,6 +2188,10 @@ __global__ void __launch_bounds__(64 * kColsum1Waves) k_colsumx(KbDev d, int gat
   const int ntz = kTileSz * nb * (nb + 1) / 2, aux = ntz;
   const int Wt = C * (C + 1) / 2, o = N * 136;
   double* img = d.ximg;
+  if (d.xar) {  // direct all-reduce: the partial image of launch v = flags + 1 goes to region half v & 1 (k_xar)
+    const unsigned long long f0 = reinterpret_cast<const unsigned long long*>(d.xar_buf)[0];
+    img = d.xar_buf + kXarFlagDoubles + (size_t)((f0 + 1) & 1) * d.img_n;
+  }
   if (e < C) {
     img[aux + e] = t;  // g_c
   } else if (e == C) {
@@ -2206,6 +2210,68 @@ __global__ void __launch_bounds__(64 * kColsum1Waves) k_colsumx(KbDev d, int gat
     const int r = e - d.Wp;  // one max column per rank: this rank's max in its own slot, zero elsewhere
     img[aux + n16 + 1 + r] = (d.gn_fused && r == d.rank) ? m : 0.0;
   }
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_xar: the direct all-reduce of the sharded k_solve image over xGMI (replaces the one collective
+// of LinearSystemSolver.cpp:81-92's host sum): every rank's k_colsumx left its partial image in its own exchange
+// region (half v & 1 of launch v); block b publishes "launch v" in its flag slot (system-scope release after an L2
+// write-back), waits until every rank's block b has published v, then sums chunk b of the image over the ranks in
+// rank order, reading the peers' regions over xGMI (system-scope loads), into d.simg.  Every rank sums the same
+// values in the same order: bitwise-identical images on all ranks, and identical to the in-process group's rank-order
+// sums.  Reuse: a rank overwrites half v & 1 at launch v + 2, which needs every peer at v + 1, i.e. done reading v.
+// A peer that never arrives ends the wait after kXarTimeoutTicks (2 s): ctrl->comm_err, the host fails the call.
+// ---------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_xar(KbDev d, int gate) {
+  KbCtrl* c = d.ctrl;
+  if (gate && c->done) return;
+  __shared__ unsigned long long sv;
+  __shared__ int err;
+  __shared__ const double* pp[kXMaxRanksDev];
+  const int b = blockIdx.x, tid = threadIdx.x, R = d.nranks;
+  unsigned long long* own = reinterpret_cast<unsigned long long*>(d.xar_buf);
+  if (tid < R) pp[tid] = d.xar_peers[tid];
+  if (tid == 0) {
+    const unsigned long long v = own[b] + 1;  // only block b of this rank writes slot b
+    sv = v;
+    err = 0;
+    __threadfence_system();  // this rank's partial image (k_colsumx, earlier on the stream) out of L2
+    __hip_atomic_store(own + b, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  __syncthreads();
+  const unsigned long long v = sv;
+  if (tid < R) {  // lane q waits for rank q's block b
+    const unsigned long long* pf = reinterpret_cast<const unsigned long long*>(pp[tid]) + b;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(pf, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < v) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > kXarTimeoutTicks) {
+        err = 1;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  const int n = d.img_n, per = (n + gridDim.x - 1) / gridDim.x, i0 = b * per, i1 = min(n, i0 + per);
+  const size_t off = kXarFlagDoubles + (size_t)(v & 1) * n;
+  for (int i = i0 + tid; i < i1; i += blockDim.x) {
+    const unsigned long long* p0 = reinterpret_cast<const unsigned long long*>(pp[0] + off + i);
+    double s = __longlong_as_double(__hip_atomic_load(p0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+    for (int q = 1; q < R; ++q) {
+      const unsigned long long* pq = reinterpret_cast<const unsigned long long*>(pp[q] + off + i);
+      s += __longlong_as_double(__hip_atomic_load(pq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+    }
+    d.simg[i] = s;
+  }
+  if (tid == 0 && err) c->comm_err = 1;
+}
+
+// k_xar self-test input: rank r's image half `half` = (r + 1) / 8 + (i % 7) (exact sums in any order)
+__global__ void __launch_bounds__(256) k_xar_fill(KbDev d, int half) {
+  double* img = d.xar_buf + kXarFlagDoubles + (size_t)half * d.img_n;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < d.img_n; i += gridDim.x * blockDim.x)
+    img[i] = (d.rank + 1) * 0.125 + (double)(i % 7);
 }
 
 // psum_local[e] = sum_r part8[r][e] (fixed order)

@@ -89,6 +89,9 @@ def test_sharded_optimize_matches_unsharded(capi, oracle_mod, name, policy):
         assert np.array_equal(r["trace"][:, 3], r0["trace"][:, 3])  # accept / revert sequence
         assert abs(r["J_final"] - r0["J_final"]) <= 1e-12 * r0["J_final"]
         assert r["J_final"] == res[0]["J_final"]  # every rank holds the same reduced numbers
+        # max|dx| (the eps_x test): every rank's frame-step maximum reaches the reduction (GN fused passes: one image
+        # slot per rank)
+        assert np.allclose(r["trace"][:, 2], r0["trace"][:, 2], rtol=1e-9, atol=0.0)
     d = float(np.abs(st - s0).max())
     assert d < 1e-9, d
     assert res[0]["iterations"] == r_o["iterations"]
@@ -226,3 +229,37 @@ def test_configs3_eight_shards_full_optimize_against_oracle(capi, oracle_mod, po
         assert np.array_equal(r["trace"][:, 3], r_o["trace"][:, 3])
         assert abs(r["J_final"] - r_o["J_final"]) <= 1e-9 * r_o["J_final"]
     assert float(np.abs(st - st_o).max()) < 1e-6
+
+
+@pytest.mark.parametrize("name", ["c4_2ranks"])
+def test_direct_allreduce_bitwise_equals_copies(capi, name, monkeypatch):
+    """k_xar, the direct all-reduce of the sharded camera-block image (C > 64): the group's members read each other's
+    partial images and sum them in rank order, as the in-process copies do -- bitwise-identical states and traces.
+    With KB_DIRECT_AR=0 the group keeps the copies.  (Members sharing one device take the direct path at 2 members:
+    at 3 the hardware queues do not always co-schedule their k_xar launches; 3 ranks run the copies.)"""
+    mk, cuts = CASES[name]
+    p = mk()
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("KB_DIRECT_AR", mode)
+        solvers = _shards(capi, p, cuts)
+        assert all(s.comm_direct() == (mode == "1") for s in solvers)
+        if mode == "1":  # and 3 members on the one device keep the copies
+            three = _shards(capi, p, [5, 16])
+            assert not any(s.comm_direct() for s in three)
+            for s in three:
+                s.close()
+        _run_all(solvers, lambda s: s.run_gn(6))
+        gn = [s.get_state() for s in solvers]
+        subs = [p.frame_slice(a, b) for a, b in zip([0] + cuts, cuts + [p.n_frames])]
+        for s, sub in zip(solvers, subs):
+            s.set_state(sub.state_init)
+        res = _run_all(solvers, lambda s: s.optimize(policy="gn", max_iterations=20, eps_x=1e-3, eps_j=1.0))
+        out[mode] = (gn, [s.get_state() for s in solvers], res)
+        for s in solvers:
+            s.close()
+    for a, b in zip(out["0"][0] + out["0"][1], out["1"][0] + out["1"][1]):
+        assert np.array_equal(a, b)
+    for r0, r1 in zip(out["0"][2], out["1"][2]):
+        assert r0["iterations"] == r1["iterations"] and r0["J_final"] == r1["J_final"]
+        assert np.array_equal(r0["trace"], r1["trace"])
