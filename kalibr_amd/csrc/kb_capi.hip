@@ -1316,7 +1316,7 @@ static int run_marginal(kb_handle* h, const kb_marginal_options* o, int write_dx
   bool stage_v0;
   const size_t lds = sizeof(double) * (size_t)marg_lds_doubles(C, stage_v0);
   KB_HIP(hipFuncSetAttribute(marg_fn(C), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  hipLaunchKernelGGL(marg_kernel(C), dim3(1), dim3(marg_threads(C)), lds, h->stream, h->d, m, 0);
+  hipLaunchKernelGGL(marg_kernel(C), dim3(1), dim3(marg_block(C)), lds, h->stream, h->d, m, 0);
   KB_HIP(hipGetLastError());
   double inf[8];
   KB_HIP(hipMemcpyAsync(inf, m.info, sizeof(inf), hipMemcpyDeviceToHost, h->stream));
@@ -1641,7 +1641,7 @@ int kb_optimize(kb_handle* h, const kb_optimizer_options* opts, kb_solution* out
 static int enqueue_marg_pass(kb_handle* h) {
   if (launch_build(h, 1, 1) || launch_colsum(h, 1, true)) return -1;
   hipLaunchKernelGGL(k_camexpand, dim3(1), dim3(256), h->lds_camexp, h->stream, h->d, 1);
-  hipLaunchKernelGGL(marg_kernel(h->C), dim3(1), dim3(marg_threads(h->C)), h->lds_marg, h->stream, h->d, h->marg, 1);
+  hipLaunchKernelGGL(marg_kernel(h->C), dim3(1), dim3(marg_block(h->C)), h->lds_marg, h->stream, h->d, h->marg, 1);
   hipLaunchKernelGGL(k_marg_tail, dim3(1), dim3(256), 0, h->stream, h->d);
   KB_HIP(hipGetLastError());
   if (launch_backsub(h, 1, 1, 1)) return -1;

@@ -49,9 +49,10 @@ constexpr int kMargMaxSweeps = 40;
 constexpr double kMargJacobiTol = 1.1102230246251565e-16;  // skip |a_pq| <= 2^-53 sqrt|a_pp a_qq|
 constexpr int kMargItems = 8;    // k_marg items (2x2 blocks, rows of V) per thread at C <= kMargMaxC
 constexpr int kMargWarmMax = 32;     // consecutive warm starts before a cold (identity) start bounds V's orthogonality drift
+constexpr int kMargFullMaxC = 96;   // largest C whose full-storage Omega (padded to even) + V fit kMargLdsStage
 constexpr int kMargLdsStage = 19000;  // dynamic LDS doubles up to which V0 is staged in LDS too (static ~7 KB beside)
 // block size of k_marg: one thread per 2x2 block of pairs and per (row of V, pair), whole waves
-inline int marg_threads(int C) {
+__host__ __device__ inline int marg_threads(int C) {
   const int h = (C + (C & 1)) / 2, items = h * (h + 1) / 2 + C * h;
   const int t = (items + 63) / 64 * 64;
   return t < kMargThreads ? t : kMargThreads;

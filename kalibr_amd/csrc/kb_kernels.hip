@@ -2519,6 +2519,12 @@ __host__ __device__ __forceinline__ int marg_lds_doubles(int C, bool& stage_v0) 
   return stage_v0 ? base + C * C : base;
 }
 
+// k_marg's block: one thread per item (marg_threads), plus wave 0 for the rotations when Omega is stored full
+__host__ __device__ __forceinline__ int marg_block(int C) {
+  const int t = marg_threads(C) + (marg_full(C) ? 64 : 0);
+  return t < kMargThreads ? t : kMargThreads;
+}
+
 // round r's partner test of an entry (x, y), x != y (round-robin: {r, M1} and pairs with x + y = 2r mod M1)
 __device__ __forceinline__ bool rr_is_pair(int M1, int r, int c2, int x, int y) {
   if (y == M1) return x == r;
@@ -2546,7 +2552,8 @@ __global__ void __launch_bounds__(kMargThreads) k_marg(KbDev d, KbMarg mo, int g
   auto aix = [&](int i, int j) { return kFull ? i * m + j : pk_up(i, j, n); };
   __shared__ double dg[2][kMargMaxC];          // diagonal, ping-pong by round
   __shared__ double ap[2][kMargMaxC];          // a_pq of the round's pairs: by slot k (packed: ping-pong by round)
-  __shared__ double csr[kMargMaxC];            // full storage: (c, s) of the round's pairs, slot k at 2k
+  __shared__ double csr[2 * kMargMaxC];        // full storage: (c, s) of round r's pairs at (r & 1) kMargMaxC + 2k
+  __shared__ int prodkl[64], prodsel[64], nprod;  // full storage: the producer blocks (k | l << 8, selectors)
   __shared__ int flag[3];
   __shared__ int okl, swarm;
   __shared__ double wsort[kMargMaxC];
@@ -2628,12 +2635,15 @@ __global__ void __launch_bounds__(kMargThreads) k_marg(KbDev d, KbMarg mo, int g
   int sweeps = 0;
   const double* w;
   if constexpr (kFull) {
-    // ---- full storage: two barriers per round.  Phase A (lanes k < h of wave 0): the rotation of pair k in the
-    // (a, b) orientation of the round-robin from the diagonal and the pair entry, its (c, s) into LDS, the pair's own
-    // 2x2 step (diagonal, pair entry exactly 0).  Phase B (every item): an off-diagonal block (k < l) rotated by both
-    // pairs, or a (row of V, pair).  The next round's pair entries lie each in exactly one of this round's
-    // off-diagonal blocks, at positions fixed over the rounds (the round-robin is shift-invariant), so every block
-    // carries up to two precomputed (entry, slot) selectors and writes them into ap by slot.
+    // ---- full storage: one barrier per round, the rotations one round ahead.  Round r's rotations (c, s) are in
+    // csr[r & 1] before round r starts.  During round r, wave 0 (a) applies round r to the off-diagonal blocks that hold
+    // the next round's pair entries ("producer" blocks: fixed over the rounds, since the round-robin is
+    // shift-invariant; each holds one or two of them), writes those entries into ap by slot, then (b) lanes k < h
+    // compute round r + 1's rotation of pair k from the diagonal and ap (division-free half-angle form), publish it in
+    // csr[(r + 1) & 1], and apply the pair's own 2x2 step (diagonal, pair entry exactly 0).  Meanwhile the other waves
+    // apply round r (csr[r & 1]) to the remaining off-diagonal blocks (rows by pair k, columns by pair l) and to V
+    // (row i, pair k).  Wave 0 owns everything round r + 1's rotations read, so the two run side by side; the round
+    // ends in one block barrier.  Round 0 of a sweep is computed after the sweep's convergence test (one extra barrier).
     double* dgs = dg[0];
     double* aps = ap[0];
     for (int i = tid; i < m; i += nth) dgs[i] = A[i * m + i];
@@ -2642,17 +2652,21 @@ __global__ void __launch_bounds__(kMargThreads) k_marg(KbDev d, KbMarg mo, int g
       rr_ab(M1, 0, k, a, b);
       aps[k] = A[a * m + b];
     }
-    const int nob = h * (h - 1) / 2, total = nob + n * h, nit = (total + nth - 1) / nth;
-    static_assert(kMargThreads * kMargItems >= (kMargMaxC / 2) * (kMargMaxC / 2 - 1) / 2 + kMargMaxC * (kMargMaxC / 2),
-                  "k_marg items per thread");
+    if (tid == 0) nprod = 0;
+    const int nob = h * (h - 1) / 2, total = nob + n * h, ith = nth - 64, nit = (total + ith - 1) / ith;
+    static_assert((kMargFullMaxC / 2) * (kMargFullMaxC / 2 - 1) / 2 + kMargFullMaxC * (kMargFullMaxC / 2) <=
+                      (kMargThreads - 64) * kMargItems,
+                  "k_marg items per thread (full storage)");
     int ik[kMargItems], il[kMargItems], isel[kMargItems];
     const int rn0 = M1 > 1 ? 1 : 0, c20 = (2 * rn0) % M1;
+    __syncthreads();
 #pragma unroll
     for (int j = 0; j < kMargItems; ++j) {
-      const int bI = tid + j * nth;
+      const int bI = tid - 64 + j * ith;
       ik[j] = -1;
       il[j] = 0;
       isel[j] = 0;
+      if (tid < 64) continue;
       if (bI < nob) {  // strictly upper (k, l): index k (2h - k - 1) / 2 + (l - k - 1)
         const float b2 = 2.0f * h - 1.0f;
         int k = (int)((b2 - sqrtf(b2 * b2 - 8.0f * bI)) * 0.5f);
@@ -2674,7 +2688,12 @@ __global__ void __launch_bounds__(kMargThreads) k_marg(KbDev d, KbMarg mo, int g
             ++ns;
           }
         }
-        isel[j] = sel;
+        if (sel) {  // a producer block: wave 0's
+          const int q = atomicAdd(&nprod, 1);
+          prodkl[q] = k | (l << 8);
+          prodsel[q] = sel;
+          ik[j] = -1;
+        }
       } else if (bI < total) {
         const int e = bI - nob, i = e / h;
         ik[j] = e - i * h;
@@ -2682,7 +2701,60 @@ __global__ void __launch_bounds__(kMargThreads) k_marg(KbDev d, KbMarg mo, int g
       }
     }
     __syncthreads();
+    // wave 0: lane L < nprod owns producer block L
+    int pk = 0, pl = 0, psel = 0;
+    if (tid < 64 && lane < nprod) {
+      pk = prodkl[lane] & 0xff;
+      pl = prodkl[lane] >> 8;
+      psel = prodsel[lane];
+    }
     KB_TSM(d, 4);
+    // the rotation of pair k of round rr (lanes k < h of wave 0) into csr[rr & 1], and the pair's own 2x2 step
+    auto pair_step = [&](int rr, int k) {
+      int a, b;
+      rr_ab(M1, rr, k, a, b);
+      const double aaa = dgs[a], abb = dgs[b], aab = aps[k];
+      double c, sn, t;
+#ifdef KB_STAMPS
+      const bool rot = (d.dbg_flags & 4) ? (c = 1.0, sn = 0.0, t = 0.0, false) : marg_rot(aaa, abb, aab, c, sn, t);
+#else
+      const bool rot = marg_rot(aaa, abb, aab, c, sn, t);
+#endif
+      double* cs = csr + (rr & 1) * kMargMaxC;
+      cs[2 * k] = c;
+      cs[2 * k + 1] = sn;
+      if (rot) {
+        dgs[a] = aaa - t * aab;
+        dgs[b] = abb + t * aab;
+        A[a * m + b] = 0.0;
+        A[b * m + a] = 0.0;
+      }
+      if (M1 == 1) aps[k] = rot ? 0.0 : aab;  // one round per sweep: the same pair next round
+    };
+    // an off-diagonal block (k, l) of round r with the rotations cs (unrotated: y = x exactly); returns y
+    auto block_step = [&](int r, int k, int l, const double* cs, double (&y)[4]) {
+      int ak, bk, al, bl;
+      rr_ab(M1, r, k, ak, bk);
+      rr_ab(M1, r, l, al, bl);
+      const double ck = cs[2 * k], sk = cs[2 * k + 1], cl = cs[2 * l], sl = cs[2 * l + 1];
+      const double x00 = A[ak * m + al], x01 = A[ak * m + bl], x10 = A[bk * m + al], x11 = A[bk * m + bl];
+      const double t00 = ck * x00 - sk * x10, t01 = ck * x01 - sk * x11;
+      const double t10 = sk * x00 + ck * x10, t11 = sk * x01 + ck * x11;
+      y[0] = cl * t00 - sl * t01;
+      y[1] = sl * t00 + cl * t01;
+      y[2] = cl * t10 - sl * t11;
+      y[3] = sl * t10 + cl * t11;
+      if (sk != 0.0 || sl != 0.0) {
+        A[ak * m + al] = y[0];
+        A[al * m + ak] = y[0];
+        A[ak * m + bl] = y[1];
+        A[bl * m + ak] = y[1];
+        A[bk * m + al] = y[2];
+        A[al * m + bk] = y[2];
+        A[bk * m + bl] = y[3];
+        A[bl * m + bk] = y[3];
+      }
+    };
     for (;; ++sweeps) {
       {
         bool v = false;
@@ -2695,70 +2767,45 @@ __global__ void __launch_bounds__(kMargThreads) k_marg(KbDev d, KbMarg mo, int g
         __syncthreads();
         if (flag[sweeps % 3] == 0 || sweeps == kMargMaxSweeps) break;
       }
+      if (tid < h) pair_step(0, tid);  // round 0's rotations
+      __syncthreads();
       if (sweeps == 0) KB_TSM(d, 5);
       for (int r = 0; r < M1; ++r) {
-        if (tid < h) {  // phase A
-          int a, b;
-          rr_ab(M1, r, tid, a, b);
-          const double aaa = dgs[a], abb = dgs[b], aab = aps[tid];
-          double c, sn, t;
-#ifdef KB_STAMPS
-          const bool rot = (d.dbg_flags & 4) ? (c = 1.0, sn = 0.0, t = 0.0, false) : marg_rot(aaa, abb, aab, c, sn, t);
-#else
-          const bool rot = marg_rot(aaa, abb, aab, c, sn, t);
-#endif
-          csr[2 * tid] = c;
-          csr[2 * tid + 1] = sn;
-          if (rot) {
-            dgs[a] = aaa - t * aab;
-            dgs[b] = abb + t * aab;
-            A[a * m + b] = 0.0;
-            A[b * m + a] = 0.0;
-          }
-          if (M1 == 1) aps[tid] = rot ? 0.0 : aab;  // one round per sweep: the same pair next round
-        }
-        __syncthreads();
-#pragma unroll
-        for (int j = 0; j < kMargItems; ++j) {  // phase B
-          if (j >= nit) break;  // block-uniform
-          const int k = ik[j], l = il[j];
-          if (k < 0) continue;
-          int ak, bk;
-          rr_ab(M1, r, k, ak, bk);
-          const double ck = csr[2 * k], sk = csr[2 * k + 1];
-          if (l >= 0) {  // off-diagonal block (k, l): rows by pair k, columns by pair l (unrotated: y = x exactly)
-            int al, bl;
-            rr_ab(M1, r, l, al, bl);
-            const double cl = csr[2 * l], sl = csr[2 * l + 1];
-            const double x00 = A[ak * m + al], x01 = A[ak * m + bl], x10 = A[bk * m + al], x11 = A[bk * m + bl];
-            const double t00 = ck * x00 - sk * x10, t01 = ck * x01 - sk * x11;
-            const double t10 = sk * x00 + ck * x10, t11 = sk * x01 + ck * x11;
-            const double y00 = cl * t00 - sl * t01, y01 = sl * t00 + cl * t01;
-            const double y10 = cl * t10 - sl * t11, y11 = sl * t10 + cl * t11;
-            if (sk != 0.0 || sl != 0.0) {
-              A[ak * m + al] = y00;
-              A[al * m + ak] = y00;
-              A[ak * m + bl] = y01;
-              A[bl * m + ak] = y01;
-              A[bk * m + al] = y10;
-              A[al * m + bk] = y10;
-              A[bk * m + bl] = y11;
-              A[bl * m + bk] = y11;
-            }
-            const int sel = isel[j];
+        const double* cs = csr + (r & 1) * kMargMaxC;
+        if (tid < 64) {
+          if (lane < nprod) {  // (a) the producer blocks: round r, then the next round's pair entries by slot
+            double y[4];
+            block_step(r, pk, pl, cs, y);
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
-              const int su = sel >> (12 * u);
+              const int su = psel >> (12 * u);
               if (su & 1) {
                 const int e = (su >> 1) & 3;
-                aps[(su >> 3) & 0x1ff] = e == 0 ? y00 : e == 1 ? y01 : e == 2 ? y10 : y11;
+                aps[(su >> 3) & 0x1ff] = e == 0 ? y[0] : e == 1 ? y[1] : e == 2 ? y[2] : y[3];
               }
             }
-          } else if (sk != 0.0) {  // V <- V J: row i, pair k
-            double* Vi = V + (-1 - l) * ld;
-            const double va = Vi[ak], vb = Vi[bk];
-            Vi[ak] = ck * va - sk * vb;
-            Vi[bk] = sk * va + ck * vb;
+          }
+          if (r + 1 < M1 && lane < h) pair_step(r + 1, lane);  // (b) round r + 1's rotations (the wave's own writes)
+        } else {
+#pragma unroll
+          for (int j = 0; j < kMargItems; ++j) {
+            if (j >= nit) break;  // block-uniform
+            const int k = ik[j], l = il[j];
+            if (k < 0) continue;
+            if (l >= 0) {
+              double y[4];
+              block_step(r, k, l, cs, y);
+            } else {
+              const double ck = cs[2 * k], sk = cs[2 * k + 1];
+              if (sk != 0.0) {  // V <- V J: row i, pair k
+                int ak, bk;
+                rr_ab(M1, r, k, ak, bk);
+                double* Vi = V + (-1 - l) * ld;
+                const double va = Vi[ak], vb = Vi[bk];
+                Vi[ak] = ck * va - sk * vb;
+                Vi[bk] = sk * va + ck * vb;
+              }
+            }
           }
         }
         __syncthreads();
