@@ -229,6 +229,12 @@ int kb_optimize(kb_handle* h, const kb_optimizer_options* opts, kb_solution* out
  * build, as analyzeMarginal after Optimizer2::optimize does.  Unsharded handles, C <= 112. */
 int kb_optimize_marginal(kb_handle* h, const kb_optimizer_options* opts, const kb_marginal_options* mopts,
                          kb_solution* out, kb_marginal_info* info, double* sv_out, double* V_out);
+/* kb_optimize_marginal followed by kb_analyze_marginal of the last build on the same stream, before the one host
+ * sync that ends the loop (the IncrementalEstimator's optimize + analyzeMarginal pair, IncrementalEstimator.cpp:373,
+ * 400): analyze_info / analyze_sv_out / analyze_V_out are what kb_analyze_marginal would return (any may be NULL). */
+int kb_optimize_marginal_analyze(kb_handle* h, const kb_optimizer_options* opts, const kb_marginal_options* mopts,
+                                 kb_solution* out, kb_marginal_info* info, double* sv_out, double* V_out,
+                                 kb_marginal_info* analyze_info, double* analyze_sv_out, double* analyze_V_out);
 
 /* Per-pass trace of the last kb_optimize: [J, lambda, deltaX, accepted] x n (returns count). */
 int kb_get_trace(kb_handle* h, double* trace, int32_t cap);

@@ -26,7 +26,7 @@ EXPORTS = [
     "kb_get_state_flat", "kb_state_size", "kb_num_cols", "kb_camera_cols", "kb_eval_cost", "kb_build",
     "kb_set_constant_conditioner", "kb_set_conditioner", "kb_solve", "kb_get_rhs", "kb_rhs_jtj_rhs", "kb_apply_update", "kb_revert", "kb_get_normal_blocks",
     "kb_optimize", "kb_get_trace", "kb_run_gn_iterations", "kb_gn_prepare", "kb_gn_launch", "kb_build_kernel_stats",
-    "kb_build_kernel_name", "kb_comm_get_unique_id", "kb_gn_pass_times", "kb_append_frames", "kb_drop_last_frames", "kb_optimize_marginal",
+    "kb_build_kernel_name", "kb_comm_get_unique_id", "kb_gn_pass_times", "kb_append_frames", "kb_drop_last_frames", "kb_optimize_marginal", "kb_optimize_marginal_analyze",
     "kb_comm_init", "kb_comm_init_local", "kb_comm_direct", "kb_selftest_mfma", "kb_solve_marginal", "kb_analyze_marginal",
     # block-Jacobi PCG (LinearSolverPCG)
     "kb_set_linear_solver", "kb_pcg_init", "kb_get_pcg_info",

@@ -1289,8 +1289,20 @@ static int marg_warm() {
   return w;
 }
 
-static int run_marginal(kb_handle* h, const kb_marginal_options* o, int write_dx, kb_marginal_info* info,
-                        double* sv_out, double* V_out) {
+static void marg_info(const double* inf, kb_marginal_info* info) {
+  if (!info) return;
+  info->rank = (int32_t)inf[0];
+  info->sweeps = (int32_t)inf[1];
+  info->tolerance = inf[2];
+  info->sv_gap = inf[3];
+  info->sv_log2_sum = inf[4];
+}
+
+// the marginal camera solve (write_dx) or analyzeMarginal (unscaled SVD only) enqueued on the stream: the frame blocks
+// of the last build eliminated at lambda = 0, the column sums, k_marg, and the copies of info [8] / sv / V out (the
+// caller syncs)
+static int enqueue_marginal(kb_handle* h, const kb_marginal_options* o, int write_dx, double* inf, double* sv_out,
+                            double* V_out) {
   if (h->C > kMargMaxC) return fail("marginal solver: camera block C > 112 is not supported");
   if (sharded(h)) return fail("marginal solver: not available on a sharded handle");
   const int C = h->C;
@@ -1306,7 +1318,6 @@ static int run_marginal(kb_handle* h, const kb_marginal_options* o, int write_dx
   m.V = h->marg_buf + (write_dx ? 0 : mstride);  // solve and analyzeMarginal keep their own warm-start V
   m.sv = m.V + (size_t)C * C;
   m.info = m.sv + C;
-  // the frame blocks eliminated at lambda = 0 (stored H_ff, H_fc, g_f of the last build), column sums finished
   const double lam_saved = h->d.host_lambda;
   h->d.host_lambda = 0.0;
   int rc = launch_schur(h, 0);
@@ -1318,18 +1329,18 @@ static int run_marginal(kb_handle* h, const kb_marginal_options* o, int write_dx
   KB_HIP(hipFuncSetAttribute(marg_fn(C), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipLaunchKernelGGL(marg_kernel(C), dim3(1), dim3(marg_block(C)), lds, h->stream, h->d, m, 0);
   KB_HIP(hipGetLastError());
-  double inf[8];
-  KB_HIP(hipMemcpyAsync(inf, m.info, sizeof(inf), hipMemcpyDeviceToHost, h->stream));
+  KB_HIP(hipMemcpyAsync(inf, m.info, sizeof(double) * 8, hipMemcpyDeviceToHost, h->stream));
   if (sv_out) KB_HIP(hipMemcpyAsync(sv_out, m.sv, sizeof(double) * C, hipMemcpyDeviceToHost, h->stream));
   if (V_out) KB_HIP(hipMemcpyAsync(V_out, m.V, sizeof(double) * C * C, hipMemcpyDeviceToHost, h->stream));
+  return 0;
+}
+
+static int run_marginal(kb_handle* h, const kb_marginal_options* o, int write_dx, kb_marginal_info* info,
+                        double* sv_out, double* V_out) {
+  double inf[8];
+  if (enqueue_marginal(h, o, write_dx, inf, sv_out, V_out)) return -1;
   KB_HIP(hipStreamSynchronize(h->stream));
-  if (info) {
-    info->rank = (int32_t)inf[0];
-    info->sweeps = (int32_t)inf[1];
-    info->tolerance = inf[2];
-    info->sv_gap = inf[3];
-    info->sv_log2_sum = inf[4];
-  }
+  marg_info(inf, info);
   return 0;
 }
 
@@ -1650,8 +1661,9 @@ static int enqueue_marg_pass(kb_handle* h) {
   return 0;
 }
 
-int kb_optimize_marginal(kb_handle* h, const kb_optimizer_options* opts, const kb_marginal_options* mopts,
-                         kb_solution* out, kb_marginal_info* info, double* sv_out, double* V_out) {
+static int optimize_marginal(kb_handle* h, const kb_optimizer_options* opts, const kb_marginal_options* mopts,
+                             kb_solution* out, kb_marginal_info* info, double* sv_out, double* V_out, bool analyze,
+                             kb_marginal_info* ainfo, double* asv_out, double* aV_out) {
   if (!h || !opts || !mopts || !out) return fail("kb_optimize_marginal: null");
   if (!h->uploaded) return fail("kb_optimize_marginal: no observations");
   if (opts->policy != 1) return fail("kb_optimize_marginal: the IncrementalEstimator's policy is Gauss-Newton (1)");
@@ -1695,12 +1707,18 @@ int kb_optimize_marginal(kb_handle* h, const kb_optimizer_options* opts, const k
     if (ctrl.done) break;
   }
   if (finish_pass(h, kPolicyMarginal)) return -1;
-  double inf[8];
+  double inf[8], ainf[8];
   KB_HIP(hipMemcpyAsync(&ctrl, h->d.ctrl, sizeof(KbCtrl), hipMemcpyDeviceToHost, h->stream));
   KB_HIP(hipMemcpyAsync(inf, m.info, sizeof(inf), hipMemcpyDeviceToHost, h->stream));
   if (sv_out) KB_HIP(hipMemcpyAsync(sv_out, m.sv, sizeof(double) * C, hipMemcpyDeviceToHost, h->stream));
   if (V_out) KB_HIP(hipMemcpyAsync(V_out, m.V, sizeof(double) * C * C, hipMemcpyDeviceToHost, h->stream));
+  if (analyze) {  // analyzeMarginal of the last built system, in the same stream sync (IncrementalEstimator.cpp:400)
+    kb_marginal_options un = *mopts;
+    un.column_scaling = 0;
+    if (enqueue_marginal(h, &un, 0, ainf, asv_out, aV_out)) return -1;
+  }
   KB_HIP(hipStreamSynchronize(h->stream));
+  if (analyze) marg_info(ainf, ainfo);
   h->cur = ctrl.cur;
   out->J_start = ctrl.J_start;
   out->J_final = ctrl.p_J;
@@ -1719,6 +1737,18 @@ int kb_optimize_marginal(kb_handle* h, const kb_optimizer_options* opts, const k
     info->sv_log2_sum = inf[4];
   }
   return 0;
+}
+
+int kb_optimize_marginal(kb_handle* h, const kb_optimizer_options* opts, const kb_marginal_options* mopts,
+                         kb_solution* out, kb_marginal_info* info, double* sv_out, double* V_out) {
+  return optimize_marginal(h, opts, mopts, out, info, sv_out, V_out, false, nullptr, nullptr, nullptr);
+}
+
+int kb_optimize_marginal_analyze(kb_handle* h, const kb_optimizer_options* opts, const kb_marginal_options* mopts,
+                                 kb_solution* out, kb_marginal_info* info, double* sv_out, double* V_out,
+                                 kb_marginal_info* analyze_info, double* analyze_sv_out, double* analyze_V_out) {
+  return optimize_marginal(h, opts, mopts, out, info, sv_out, V_out, true, analyze_info, analyze_sv_out,
+                           analyze_V_out);
 }
 
 int kb_get_trace(kb_handle* h, double* trace, int32_t cap) {

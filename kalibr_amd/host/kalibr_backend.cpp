@@ -694,6 +694,7 @@ GpuMarginalLinearSolver::GpuMarginalLinearSolver(const LinearSolverOptions& o, c
 }
 
 void GpuMarginalLinearSolver::initMatrixStructure(const CalibrationProblem& p, bool useDiagonalConditioner) {
+  _analyzed = false;  // a changed system voids the fused analyzeMarginal result
   _g.initMatrixStructure(p, useDiagonalConditioner);
   _JRows = _g.JRows();
   _JCols = _g.JCols();
@@ -705,6 +706,7 @@ void GpuMarginalLinearSolver::initMatrixStructure(const CalibrationProblem& p, b
 }
 
 bool GpuMarginalLinearSolver::appendFrames(const CalibrationProblem& p, size_t firstFrame) {
+  _analyzed = false;  // a changed system voids the fused analyzeMarginal result
   if (!_g.appendFrames(p, firstFrame)) return false;
   _JRows = _g.JRows();
   _JCols = _g.JCols();
@@ -717,6 +719,7 @@ bool GpuMarginalLinearSolver::appendFrames(const CalibrationProblem& p, size_t f
 }
 
 bool GpuMarginalLinearSolver::dropLastFrames(size_t n, const std::vector<double>& st) {
+  _analyzed = false;  // a changed system voids the fused analyzeMarginal result
   _g.dropLastFrames(n, st);
   _JRows = _g.JRows();
   _JCols = _g.JCols();
@@ -741,8 +744,21 @@ bool GpuMarginalLinearSolver::optimizeDevice(const Optimizer2Options& oo, Soluti
   const size_t C = _g.cameraCols();
   _sv.resize(C);
   _V.resize(C * C);
-  if (kb_optimize_marginal(static_cast<kb_handle*>(_g.handle()), &o, &m, &s, &inf, _sv.data(), _V.data()) < 0)
+  _analyzed = false;
+  if (fuseAnalyze) {
+    kb_marginal_info ainf{};
+    _asv.resize(C);
+    _aV.resize(C * C);
+    if (kb_optimize_marginal_analyze(static_cast<kb_handle*>(_g.handle()), &o, &m, &s, &inf, _sv.data(), _V.data(),
+                                     &ainf, _asv.data(), _aV.data()) < 0)
+      throw Exception(std::string("kb_optimize_marginal_analyze: ") + kb_last_error());
+    _aRank = ainf.rank;
+    _aTol = ainf.tolerance;
+    _aGap = ainf.sv_gap;
+    _analyzed = true;
+  } else if (kb_optimize_marginal(static_cast<kb_handle*>(_g.handle()), &o, &m, &s, &inf, _sv.data(), _V.data()) < 0) {
     throw Exception(std::string("kb_optimize_marginal: ") + kb_last_error());
+  }
   _svdRank = inf.rank;
   _svdTolerance = inf.tolerance;
   _svGap = inf.sv_gap;
@@ -767,6 +783,7 @@ static kb_marginal_options marg_opts(const LinearSolverOptions& o) {
 }
 
 bool GpuMarginalLinearSolver::solveSystem(std::vector<double>& outDx) {
+  _analyzed = false;  // a changed system voids the fused analyzeMarginal result
   const size_t C = _g.cameraCols();
   std::vector<double> dx(_JCols);
   _sv.resize(C);
@@ -786,12 +803,21 @@ bool GpuMarginalLinearSolver::solveSystem(std::vector<double>& outDx) {
 
 void GpuMarginalLinearSolver::analyzeMarginal() {
   const size_t C = _g.cameraCols();
-  _sv.resize(C);
-  _V.resize(C * C);
-  kb_marginal_options m = marg_opts(_lopt);
   kb_marginal_info inf{};
-  if (kb_analyze_marginal(static_cast<kb_handle*>(_g.handle()), &m, &inf, _sv.data(), _V.data()) < 0)
-    throw Exception(std::string("kb_analyze_marginal: ") + kb_last_error());
+  if (_analyzed) {  // the device loop analysed the last build already (kb_optimize_marginal_analyze)
+    _sv = _asv;
+    _V = _aV;
+    inf.rank = _aRank;
+    inf.tolerance = _aTol;
+    inf.sv_gap = _aGap;
+    _analyzed = false;
+  } else {
+    _sv.resize(C);
+    _V.resize(C * C);
+    kb_marginal_options m = marg_opts(_lopt);
+    if (kb_analyze_marginal(static_cast<kb_handle*>(_g.handle()), &m, &inf, _sv.data(), _V.data()) < 0)
+      throw Exception(std::string("kb_analyze_marginal: ") + kb_last_error());
+  }
   // rank, tolerance and gap stay those of the last solve when there was one (LinearSolver.cpp:518-524)
   if (_svdRank == -1) {
     _svdRank = inf.rank;

@@ -313,7 +313,10 @@ class GpuMarginalLinearSolver : public MarginalLinearSystemSolver {
                                    const GpuOptions& g = GpuOptions());
   void initMatrixStructure(const CalibrationProblem& problem, bool useDiagonalConditioner) override;
   double evaluateError(size_t nThreads, bool useMEstimator) override { return _g.evaluateError(nThreads, useMEstimator); }
-  void buildSystem(size_t nThreads, bool useMEstimator) override { _g.buildSystem(nThreads, useMEstimator); }
+  void buildSystem(size_t nThreads, bool useMEstimator) override {
+    _analyzed = false;
+    _g.buildSystem(nThreads, useMEstimator);
+  }
   void setConstantConditioner(double d) override { LinearSystemSolver::setConstantConditioner(d); }  // ignored (:247-280)
   bool solveSystem(std::vector<double>& outDx) override;
   std::string name() const override { return "kalibr_hip_marginal_svd"; }
@@ -334,9 +337,16 @@ class GpuMarginalLinearSolver : public MarginalLinearSystemSolver {
   /// configs[1]'s 500 batches eager launches with a check every 2 passes take 0.35 s, recaptured graphs 0.61 s
   bool useGraph = false;
   int syncEvery = 2;
+  /// the device loop also analyses the last build before its one host sync (kb_optimize_marginal_analyze); the next
+  /// analyzeMarginal() then takes that result instead of a second call
+  bool fuseAnalyze = true;
 
  private:
   GpuLinearSystemSolver _g;
+  bool _analyzed = false;  // _asv / _aV / _ainfo hold analyzeMarginal's result for the current system
+  std::vector<double> _asv, _aV;
+  int _aRank = -1;
+  double _aTol = 0.0, _aGap = 0.0;
 };
 
 // ---------------------------------------------------------------- trust-region policies
