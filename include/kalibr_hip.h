@@ -284,6 +284,13 @@ int kb_comm_init_local(kb_handle* const* handles, int32_t n);
  * collective for it, bitwise-identical images on all ranks.  KB_DIRECT_AR=0, a failed mapping or a failed self-test
  * (agreed over all ranks) keep the collective.  Returns 1 when the handle uses the direct path. */
 int kb_comm_direct(const kb_handle* h);
+/* The IPC half of the direct all-reduce on its own (test hook: RCCL refuses several ranks on one device, so the
+ * multi-process mapping is tested with processes sharing one GPU).  kb_xar_export writes this handle's exchange-region
+ * IPC handle (64 bytes); kb_xar_test maps the peers' regions from handles64 [nranks][64] (own slot ignored) and runs
+ * the self-test exchange with them: *ok = 1 when every rank's known values arrived in rank-order sums, 0 when not or
+ * when a peer did not take part within 2 s.  The handle stays unsharded.  C > 64 only. */
+int kb_xar_export(kb_handle* h, void* handle_out64);
+int kb_xar_test(kb_handle* h, int32_t nranks, int32_t rank, const void* handles64, int32_t* ok);
 
 /* Self test of the f64 MFMA fragment layout used by the build kernel (A = I, asymmetric B). */
 int kb_selftest_mfma(double* max_err);

@@ -27,7 +27,7 @@ EXPORTS = [
     "kb_set_constant_conditioner", "kb_set_conditioner", "kb_solve", "kb_get_rhs", "kb_rhs_jtj_rhs", "kb_apply_update", "kb_revert", "kb_get_normal_blocks",
     "kb_optimize", "kb_get_trace", "kb_run_gn_iterations", "kb_gn_prepare", "kb_gn_launch", "kb_build_kernel_stats",
     "kb_build_kernel_name", "kb_comm_get_unique_id", "kb_gn_pass_times", "kb_append_frames", "kb_drop_last_frames", "kb_optimize_marginal", "kb_optimize_marginal_analyze",
-    "kb_comm_init", "kb_comm_init_local", "kb_comm_direct", "kb_selftest_mfma", "kb_solve_marginal", "kb_analyze_marginal",
+    "kb_comm_init", "kb_comm_init_local", "kb_comm_direct", "kb_xar_export", "kb_xar_test", "kb_selftest_mfma", "kb_solve_marginal", "kb_analyze_marginal",
     # block-Jacobi PCG (LinearSolverPCG)
     "kb_set_linear_solver", "kb_pcg_init", "kb_get_pcg_info",
     # configs[4]: B-spline pose trajectory + IMU
@@ -139,6 +139,8 @@ def lib():
         L.kb_comm_init.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32]
         L.kb_comm_init_local.argtypes = [C.POINTER(C.c_void_p), C.c_int32]
         L.kb_comm_direct.argtypes = [C.c_void_p]
+        L.kb_xar_export.argtypes = [C.c_void_p, C.c_void_p]
+        L.kb_xar_test.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.POINTER(C.c_int32)]
         L.kb_selftest_mfma.argtypes = [dp]
         L.kb_set_linear_solver.argtypes = [C.c_void_p, C.c_int32, C.POINTER(PcgOptions)]
         L.kb_pcg_init.argtypes = [C.c_void_p]
@@ -399,6 +401,19 @@ class Solver:
     def comm_init(self, uid: bytes, nranks, rank):
         buf = C.create_string_buffer(uid, 128)
         _check(lib().kb_comm_init(self.h, buf, int(nranks), int(rank)))
+
+    def xar_export(self):
+        """kb_xar_export: this handle's exchange-region IPC handle (64 bytes)."""
+        buf = C.create_string_buffer(64)
+        _check(lib().kb_xar_export(self.h, buf))
+        return buf.raw
+
+    def xar_test(self, nranks, rank, handles: bytes):
+        """kb_xar_test: the direct all-reduce's self-test exchange with the peers' exported regions."""
+        ok = C.c_int32(0)
+        buf = C.create_string_buffer(handles, len(handles))
+        _check(lib().kb_xar_test(self.h, int(nranks), int(rank), buf, C.byref(ok)))
+        return bool(ok.value)
 
     def comm_direct(self):
         """kb_comm_direct: the sharded image is all-reduced by k_xar (peers read over xGMI), not a collective."""

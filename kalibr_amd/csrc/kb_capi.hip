@@ -2235,6 +2235,74 @@ static void xar_setup_local(kb_handle* const* hs, int n) {
 
 int kb_comm_direct(const kb_handle* h) { return h && h->d.xar ? 1 : 0; }
 
+// ---- the IPC half of the direct all-reduce on its own, for a test with several processes on one GPU (RCCL refuses
+// two ranks on one device, so kb_comm_init cannot be run that way): export this handle's exchange region, then map
+// the peers' regions from their exported handles and run the self-test exchange (known values, rank-order sums,
+// the 2 s wait bound).  The handle stays unsharded: its rank / rank count are set only for the exchange.
+int kb_xar_export(kb_handle* h, void* handle_out64) {
+  if (!h || !handle_out64) return fail("kb_xar_export: null");
+  if (!h->xexp) return fail("kb_xar_export: the direct all-reduce needs a camera block C > 64");
+  KB_HIP(hipSetDevice(h->device));
+  if (!h->d.xar_buf) {
+    double* own = nullptr;
+    if (xar_region(h, &own)) return -1;
+    KB_HIP(hipStreamSynchronize(h->stream));
+    h->d.xar_buf = own;
+  }
+  hipIpcMemHandle_t mh;
+  KB_HIP(hipIpcGetMemHandle(&mh, h->d.xar_buf));
+  static_assert(sizeof(hipIpcMemHandle_t) <= 64, "IPC handle size");
+  std::memset(handle_out64, 0, 64);
+  std::memcpy(handle_out64, &mh, sizeof(mh));
+  return 0;
+}
+
+int kb_xar_test(kb_handle* h, int32_t nranks, int32_t rank, const void* handles64, int32_t* ok) {
+  if (!h || !handles64 || !ok) return fail("kb_xar_test: null");
+  if (!h->d.xar_buf) return fail("kb_xar_test: kb_xar_export first");
+  if (sharded(h)) return fail("kb_xar_test: the handle is sharded");
+  if (nranks < 2 || nranks > kXMaxRanksDev || rank < 0 || rank >= nranks) return fail("kb_xar_test: bad rank");
+  KB_HIP(hipSetDevice(h->device));
+  *ok = 0;
+  std::vector<double*> peers(nranks, nullptr);
+  std::vector<void*> opened;
+  int rc = 0;
+  for (int q = 0; q < nranks && !rc; ++q) {
+    if (q == rank) {
+      peers[q] = h->d.xar_buf;
+      continue;
+    }
+    hipIpcMemHandle_t hq;
+    std::memcpy(&hq, (const char*)handles64 + 64 * q, sizeof(hq));
+    void* p = nullptr;
+    if (hipIpcOpenMemHandle(&p, hq, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+      hipGetLastError();
+      rc = fail("kb_xar_test: hipIpcOpenMemHandle failed");
+      break;
+    }
+    opened.push_back(p);
+    peers[q] = (double*)p;
+  }
+  const KbDev saved = h->d;
+  if (!rc) {
+    h->d.rank = rank;
+    h->d.nranks = nranks;
+    h->nranks = nranks;
+    h->rank = rank;
+    int t = 0;
+    if (xar_install(h, h->d.xar_buf, peers) || xar_selftest_launch(h) || xar_selftest_check(h, t)) rc = -1;
+    *ok = t;
+    h->nranks = 1;
+    h->rank = 0;
+  }
+  const double* region = h->d.xar_buf;
+  h->d = saved;
+  h->d.xar_buf = const_cast<double*>(region);
+  drop_graphs(h);
+  for (void* p : opened) hipIpcCloseMemHandle(p);
+  return rc;
+}
+
 int kb_comm_init(kb_handle* h, const void* uid, int32_t nranks, int32_t rank) {
   if (!h || !uid) return fail("kb_comm_init: null");
   KB_HIP(hipSetDevice(h->device));
