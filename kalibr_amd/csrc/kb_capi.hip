@@ -2144,8 +2144,8 @@ static int xar_setup_rccl(kb_handle* h) {
     ok = 0;
   }
   constexpr size_t kSlot = sizeof(hipIpcMemHandle_t) + 8;
-  char* dx = nullptr;
-  KB_HIP(hipMalloc(&dx, kSlot * (h->nranks + 1)));
+  char* dx = nullptr;  // the exchange scratch (handle-owned: freed by kb_destroy on every return path)
+  if (h->alloc(&dx, kSlot * (h->nranks + 1))) return -1;
   std::vector<char> slot(kSlot, 0);
   std::memcpy(slot.data(), &mh, sizeof(mh));
   std::memcpy(slot.data() + sizeof(mh), &ok, sizeof(int));
@@ -2194,7 +2194,6 @@ static int xar_setup_rccl(kb_handle* h) {
     ok = agree(t);
   }
   if (!ok && h->d.xar) xar_uninstall(h);
-  hipFree(dx);
   return 0;
 }
 
