@@ -2255,12 +2255,22 @@ __global__ void __launch_bounds__(256) k_xar(KbDev d, int gate) {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   const int n = d.img_n, per = (n + gridDim.x - 1) / gridDim.x, i0 = b * per, i1 = min(n, i0 + per);
   const size_t off = kXarFlagDoubles + (size_t)(v & 1) * n;
+  // every rank's value of an entry is requested before any is summed (8 remote loads in flight per group), the sum
+  // itself in rank order
+  constexpr int kG = 8;
   for (int i = i0 + tid; i < i1; i += blockDim.x) {
-    const unsigned long long* p0 = reinterpret_cast<const unsigned long long*>(pp[0] + off + i);
-    double s = __longlong_as_double(__hip_atomic_load(p0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
-    for (int q = 1; q < R; ++q) {
-      const unsigned long long* pq = reinterpret_cast<const unsigned long long*>(pp[q] + off + i);
-      s += __longlong_as_double(__hip_atomic_load(pq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+    double s = 0.0;
+    for (int q0 = 0; q0 < R; q0 += kG) {
+      double v[kG];
+#pragma unroll
+      for (int u = 0; u < kG; ++u) {
+        const int q = min(q0 + u, R - 1);
+        v[u] = __longlong_as_double(__hip_atomic_load(reinterpret_cast<const unsigned long long*>(pp[q] + off + i),
+                                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+      }
+#pragma unroll
+      for (int u = 0; u < kG; ++u)
+        if (q0 + u < R) s = (q0 + u == 0) ? v[u] : s + v[u];
     }
     d.simg[i] = s;
   }
