@@ -1650,9 +1650,14 @@ int kb_optimize(kb_handle* h, const kb_optimizer_options* opts, kb_solution* out
 // the candidate camera design variables and chains (k_marg_tail), the frame steps and the candidate's cost
 // (k_backsub), the pass end (k_post: accept, convergence tests, next prelude).  Every kernel is gated on ctrl.
 static int enqueue_marg_pass(kb_handle* h) {
-  if (launch_build(h, 1, 1) || launch_colsum(h, 1, true)) return -1;
-  hipLaunchKernelGGL(k_camexpand, dim3(1), dim3(256), h->lds_camexp, h->stream, h->d, 1);
-  hipLaunchKernelGGL(marg_kernel(h->C), dim3(1), dim3(marg_block(h->C)), h->lds_marg, h->stream, h->d, h->marg, 1);
+  if (launch_build(h, 1, 1) || launch_colsum(h, 1, false)) return -1;
+  // the two column-sum consumers (k_camexpand, k_marg) sum the kColsumRows stage-1 rows themselves, in k_colfin's
+  // order: one launch less per pass
+  KbDev dr = h->d;
+  dr.psum = dr.part8;
+  dr.psum_rows = kColsumRows;
+  hipLaunchKernelGGL(k_camexpand, dim3(1), dim3(256), h->lds_camexp, h->stream, dr, 1);
+  hipLaunchKernelGGL(marg_kernel(h->C), dim3(1), dim3(marg_block(h->C)), h->lds_marg, h->stream, dr, h->marg, 1);
   hipLaunchKernelGGL(k_marg_tail, dim3(1), dim3(256), 0, h->stream, h->d);
   KB_HIP(hipGetLastError());
   if (launch_backsub(h, 1, 1, 1)) return -1;
