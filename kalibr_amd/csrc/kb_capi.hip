@@ -1647,7 +1647,7 @@ int kb_optimize(kb_handle* h, const kb_optimizer_options* opts, kb_solution* out
 // one pass of the device-resident IncrementalEstimator loop (Optimizer2 + GaussNewtonTrustRegionPolicy over
 // calibration::LinearSolver, IncrementalEstimator.cpp:46-77, 373): build with the frame blocks eliminated at
 // lambda = 0 (the policy's lambda), column sums, H_cc / g_c, the column-scaled truncated-SVD camera step (k_marg),
-// the candidate camera design variables and chains (k_marg_tail), the frame steps and the candidate's cost
+// the candidate camera design variables and chains (the end of the gated k_marg), the frame steps and the candidate's cost
 // (k_backsub), the pass end (k_post: accept, convergence tests, next prelude).  Every kernel is gated on ctrl.
 static int enqueue_marg_pass(kb_handle* h) {
   if (launch_build(h, 1, 1) || launch_colsum(h, 1, false)) return -1;
@@ -1658,7 +1658,6 @@ static int enqueue_marg_pass(kb_handle* h) {
   dr.psum_rows = kColsumRows;
   hipLaunchKernelGGL(k_camexpand, dim3(1), dim3(256), h->lds_camexp, h->stream, dr, 1);
   hipLaunchKernelGGL(marg_kernel(h->C), dim3(1), dim3(marg_block(h->C)), h->lds_marg, h->stream, dr, h->marg, 1);
-  hipLaunchKernelGGL(k_marg_tail, dim3(1), dim3(256), 0, h->stream, h->d);
   KB_HIP(hipGetLastError());
   if (launch_backsub(h, 1, 1, 1)) return -1;
   hipLaunchKernelGGL(k_post, dim3(1), dim3(256), 0, h->stream, h->d, 1);

@@ -2543,9 +2543,19 @@ __device__ __forceinline__ bool rr_is_pair(int M1, int r, int c2, int x, int y) 
   return (s >= M1 ? s - M1 : s) == c2;
 }
 
+__device__ void marg_tail(const KbDev& d, double* nbase, int sok);
+
 template <bool kFull>
 __global__ void __launch_bounds__(kMargThreads) k_marg(KbDev d, KbMarg mo, int gate) {
-  if (gate && (d.ctrl->done || !d.ctrl->do_build)) return;
+  __shared__ double nbase[KB_MAX_CAMS * 7];  // gated: the candidate baselines (marg_tail)
+  __shared__ int sok0;
+  if (gate) {
+    if (d.ctrl->done) return;
+    if (!d.ctrl->do_build) {  // no new system: the camera step's tail alone, as the separate tail kernel ran it
+      marg_tail(d, nbase, d.ctrl->solve_ok);
+      return;
+    }
+  }
   extern __shared__ __attribute__((aligned(16))) double sm[];
   KB_TSM(d, 0);
   const int C = d.C, n = C, m = C + (C & 1), h = m / 2, M1 = m - 1, tid = threadIdx.x, nth = blockDim.x;
@@ -2578,6 +2588,7 @@ __global__ void __launch_bounds__(kMargThreads) k_marg(KbDev d, KbMarg mo, int g
   }
   if (tid == 0) {
     okl = !(psum_at(d, o0 + Wt + C) > 0.0);  // non-PD frame blocks
+    sok0 = gate ? d.ctrl->solve_ok : 1;
     const int chain = (int)mo.info[5];
     swarm = (mo.warm && chain >= 1 && chain < kMargWarmMax) ? chain : 0;
     flag[0] = flag[1] = flag[2] = 0;
@@ -3081,19 +3092,22 @@ __global__ void __launch_bounds__(kMargThreads) k_marg(KbDev d, KbMarg mo, int g
     if (!okl) d.ctrl->solve_ok = 0;
   }
   KB_TSM(d, 11);
+  if (gate) {  // the device loop: the camera step's statistics, design variables and chains (marg_tail)
+    __syncthreads();  // dx_c written
+    marg_tail(d, nbase, sok0 && okl);
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
-// k_marg_tail (kb_optimize_marginal, the device-resident IncrementalEstimator loop): after k_marg's truncated-SVD
+// marg_tail (kb_optimize_marginal, the device-resident IncrementalEstimator loop; the end of the gated k_marg): after its truncated-SVD
 // camera step, what k_solve's tail does after its LDL^T -- the camera dx statistics (max |dx_c|, dx_c.dx_c, dx_c.g_c),
 // the camera design variables of the candidate slot (intrinsics additive, baselines by the pose update) and the
 // candidate's camera chains -- and the pass is marked pending for k_backsub / k_post
 // ---------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_marg_tail(KbDev d) {
+// sok: the solve succeeded (ctrl->solve_ok after k_marg); every thread of the block calls it
+__device__ void marg_tail(const KbDev& d, double* nbase, int sok) {
   KbCtrl* c = d.ctrl;
-  __shared__ double nbase[KB_MAX_CAMS * 7];
-  const int done = c->done, sok = c->solve_ok, cur = c->cur;
-  if (done) return;
+  const int cur = c->cur;
   const int tid = threadIdx.x, nth = blockDim.x, C = d.C, N = d.N;
   if (tid == 0) c->pending = 1;
   if (!sok) return;
