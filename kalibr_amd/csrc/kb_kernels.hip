@@ -511,8 +511,10 @@ __device__ __forceinline__ void schur_tiles_assign(int nbz, int* tii, int* tjj) 
   }
 }
 
-// the tiles' entries into the block's partial row: sum Y^T Y upper packed (a <= b) | sum Y^T z
-template <int TW>
+// the tiles' entries into the block's partial row: sum Y^T Y upper packed (a <= b) | sum Y^T z.  kT: the tiles are
+// held transposed (schur_tiles_accumulate6: lane l, reg r -> tile row l & 15, column (l >> 4) + 4 r), so that the 16
+// lanes of a row group write 16 consecutive entries of a packed row (coalesced) instead of 16 rows
+template <int TW, bool kT = false>
 __device__ __forceinline__ void schur_tiles_store(double* prow_schur, int C, const int* tii, const int* tjj,
                                                   const v4d* acc) {
   const int lane = threadIdx.x & 63, Wt = C * (C + 1) / 2;
@@ -521,7 +523,8 @@ __device__ __forceinline__ void schur_tiles_store(double* prow_schur, int C, con
     if (tii[t] < 0) break;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int rg = 16 * tii[t] + (lane >> 4) + 4 * r, cg = 16 * tjj[t] + (lane & 15);
+      const int ra = kT ? (lane & 15) : (lane >> 4) + 4 * r, ca = kT ? (lane >> 4) + 4 * r : (lane & 15);
+      const int rg = 16 * tii[t] + ra, cg = 16 * tjj[t] + ca;
       if (rg < C && cg <= rg)
         prow_schur[upper_index(cg, rg, C)] = acc[t][r];
       else if (rg == C && cg < C)
@@ -532,7 +535,7 @@ __device__ __forceinline__ void schur_tiles_store(double* prow_schur, int C, con
 
 // expanded partials (GN fused, C > 64): the tiles' entries stored as EX - sum, EX = the block's camera-block expansion
 // (same packing: S upper | b), so that the column sums are S - lambda^2 I and b themselves
-template <int TW>
+template <int TW, bool kT = false>
 __device__ __forceinline__ void schur_tiles_store_x(double* prow_schur, int C, const int* tii, const int* tjj,
                                                     const v4d* acc, const double* EX) {
   const int lane = threadIdx.x & 63, Wt = C * (C + 1) / 2;
@@ -541,7 +544,8 @@ __device__ __forceinline__ void schur_tiles_store_x(double* prow_schur, int C, c
     if (tii[t] < 0) break;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int rg = 16 * tii[t] + (lane >> 4) + 4 * r, cg = 16 * tjj[t] + (lane & 15);
+      const int ra = kT ? (lane & 15) : (lane >> 4) + 4 * r, ca = kT ? (lane >> 4) + 4 * r : (lane & 15);
+      const int rg = 16 * tii[t] + ra, cg = 16 * tjj[t] + ca;
       if (rg < C && cg <= rg) {
         const int u = upper_index(cg, rg, C);
         prow_schur[u] = EX[u] - acc[t][r];
@@ -1292,7 +1296,8 @@ __device__ __forceinline__ void schur_tiles_accumulate6(const double* P, const d
       const int k = 4 * s + (lane >> 4);
       const int kc = min(k, 5);
       const double a = ya[kc * CZ], b = yb[kc * CZ];
-      acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(k < 6 ? a : 0.0, k < 6 ? b : 0.0, acc[t], 0, 0, 0);
+      // the tile transposed (B = the P rows, A = the Q columns): the stores write packed rows coalesced (kT)
+      acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(k < 6 ? b : 0.0, k < 6 ? a : 0.0, acc[t], 0, 0, 0);
     }
     __builtin_amdgcn_sched_barrier(0);  // one tile's operands at a time (hoisting all of them spills)
   }
@@ -1981,9 +1986,9 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
       if (it < G) __syncthreads();  // the view waves' frame it is in VB[it & 1]
     }
     __syncthreads();  // the view waves' last barrier (their expansion of the block's camera sums is done)
-    if (fuse && !xp) schur_tiles_store<TT>(prow + N * 136, C, tii, tjj, acc);
+    if (fuse && !xp) schur_tiles_store<TT, true>(prow + N * 136, C, tii, tjj, acc);
     // expanded partials: the view waves expanded the camera block during the last frame's elimination
-    if (xp) schur_tiles_store_x<TT>(prow + N * 136, C, tii, tjj, acc, sm);
+    if (xp) schur_tiles_store_x<TT, true>(prow + N * 136, C, tii, tjj, acc, sm);
   }
   if (xp && vw) {
     // expanded partials: the g_c columns of the block's partial row (the cost column was written in the idle phase)
