@@ -332,6 +332,28 @@ class Solver:
         return out
 
     # -- device-resident Optimizer2 --
+    def optimize_marginal(self, max_iterations=20, eps_x=1e-3, eps_j=1e-3, opts=None, analyze=False, sync_every=2,
+                          use_graph=False):
+        """kb_optimize_marginal (the IncrementalEstimator's device loop: GN over the truncated-SVD camera solve);
+        analyze: kb_optimize_marginal_analyze, the last build's analyzeMarginal in the same sync.  Returns
+        (solution dict, marginal info of the last solve, analyze info or None)."""
+        mo = opts or marginal_options()
+        o = OptimizerOptions(1, 0.0, max_iterations, eps_x, eps_j, sync_every, int(use_graph))
+        s = Solution()
+        sv, V = np.zeros(self.C), np.zeros((self.C, self.C))
+        inf = MarginalInfo()
+        if analyze:
+            asv, aV = np.zeros(self.C), np.zeros((self.C, self.C))
+            ainf = MarginalInfo()
+            _check(lib().kb_optimize_marginal_analyze(self.h, C.byref(o), C.byref(mo), C.byref(s), C.byref(inf),
+                                                      _d(sv), _d(V), C.byref(ainf), _d(asv), _d(aV)))
+            a = self._minfo(ainf, asv, aV)
+        else:
+            _check(lib().kb_optimize_marginal(self.h, C.byref(o), C.byref(mo), C.byref(s), C.byref(inf), _d(sv), _d(V)))
+            a = None
+        res = {f: getattr(s, f) for f, _ in Solution._fields_}
+        return res, self._minfo(inf, sv, V), a
+
     def optimize(self, policy="lm", lambda0=10.0, max_iterations=200, eps_x=1e-3, eps_j=1.0, sync_every=4,
                  use_graph=True):
         o = OptimizerOptions(0 if policy == "lm" else 1, lambda0, max_iterations, eps_x, eps_j, sync_every,

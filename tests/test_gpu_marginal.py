@@ -100,3 +100,29 @@ def test_gn_marginal_loop_matches_oracle(capi, oracle_mod, name):
     assert info["rank"] == r_o["solve_info"]["rank"]
     ai = g.analyze_marginal()
     assert np.abs(ai["sv"] - r_o["analyze_info"]["sv"]).max() <= 1e-9 * r_o["analyze_info"]["sv"][0]
+
+
+@pytest.mark.parametrize("name", ["c1", "c2_small"])
+def test_device_loop_with_fused_analyze(capi, oracle_mod, name):
+    """kb_optimize_marginal (the estimator's device loop) against the oracle's GN + marginal loop, and its fused
+    analyzeMarginal (kb_optimize_marginal_analyze) bitwise equal to the separate kb_analyze_marginal call."""
+    p = PROBLEMS[name]()
+    st_o, r_o = oracle_mod.Oracle(p).optimize(p.state_init, policy="gn", max_iterations=20, eps_x=1e-3, eps_j=1e-3,
+                                               marg=oracle_mod.marg_opts(2 * p.n_corners))
+    out = []
+    for fused in (True, False):
+        g = capi.Solver(p)
+        g.set_state(p.state_init)
+        sol, info, ai = g.optimize_marginal(analyze=fused)
+        if not fused:
+            ai = g.analyze_marginal()
+        out.append((sol, info, ai, g.get_state()))
+        g.close()
+    (s1, i1, a1, x1), (s2, i2, a2, x2) = out
+    assert s1["iterations"] == s2["iterations"] == r_o["iterations"]
+    assert np.array_equal(x1, x2)
+    assert abs(s1["J_final"] - r_o["J_final"]) <= 1e-9 * r_o["J_final"]
+    assert np.abs(x1 - st_o).max() < 1e-6
+    assert i1["rank"] == r_o["solve_info"]["rank"]
+    assert np.array_equal(a1["sv"], a2["sv"]) and np.array_equal(a1["V"], a2["V"]) and a1["rank"] == a2["rank"]
+    assert np.abs(a1["sv"] - r_o["analyze_info"]["sv"]).max() <= 1e-9 * r_o["analyze_info"]["sv"][0]
