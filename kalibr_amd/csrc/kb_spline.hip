@@ -37,7 +37,15 @@
   do {                                                                                                     \
     if (blockIdx.x == 0 && threadIdx.x == 0 && d.dbg_ts && (i) < 256) d.dbg_ts[i] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
+// the same for thread 0 of block b
+#define KSP_TSB(b, i)                                                                                      \
+  do {                                                                                                     \
+    if (blockIdx.x == (b) && threadIdx.x == 0 && d.dbg_ts && (i) < 256) d.dbg_ts[i] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
 #else
+#define KSP_TSB(b, i) \
+  do {                \
+  } while (0)
 #define KSP_STOP(i) \
   do {              \
   } while (0)
@@ -136,6 +144,30 @@ __device__ __forceinline__ int sp_cam_arg(const int (&a)[KB_MAX_CAMS], int i) {
   return v;
 }
 #define KSP_WAVE_SYNC() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
+
+// ---------------------------------------------------------------- segment-wise staging (round 5)
+// A segment is `len` consecutive doubles.  Thread tid takes items tid + u nth, u < U, with the source index clamped
+// (no branch around the load), so the loads of all of a kernel's segments are in flight before its first store; items
+// from U nth on (rigs wider than the U sizing) follow one by one.  An item's address is one add: the packed
+// ksp_batched staging of the cyclic-reduction kernels spent ~50 VALU instructions per item on segment selects and
+// run-time divisions, 3.1-3.4 us of each 11 us level (tools/diag_sp_levels.py).
+template <int U>
+__device__ __forceinline__ void seg_ld(double (&v)[U], const double* src, int len, int tid, int nth) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) v[u] = src[min(tid + u * nth, len - 1)];
+}
+template <int U, class St>
+__device__ __forceinline__ void seg_st(const double (&v)[U], const double* src, int len, int tid, int nth, St st) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int q = tid + u * nth;
+    if (q < len) st(q, v[u]);
+  }
+  for (int q = tid + U * nth; q < len; q += nth) st(q, src[q]);
+}
+// q / m for q < 2^20 and m <= 128 by a float product: (q + 1/2) / m keeps >= 1/(2m) from an integer, far above the
+// float rounding error
+__device__ __forceinline__ int div_small(int q, float rinv) { return (int)(((float)q + 0.5f) * rinv); }
 
 // ---------------------------------------------------------------- batched staging
 // Copies with U independent loads in flight per thread.  A runtime-bounded loop of load / store pairs waits for
@@ -1057,6 +1089,11 @@ __device__ __forceinline__ double ksp_recip(double x) {
   e = fma(-x, r, 1.0);
   return fma(r, e, r);
 }
+// the pivot chain's reciprocal: v_rcp_f64 + one Newton step (as k_solve's panel factor; two FMAs shorter per pivot)
+__device__ __forceinline__ double ksp_recip1(double x) {
+  const double r = __builtin_amdgcn_rcp(x);
+  return fma(r, fma(-x, r, 1.0), r);
+}
 
 // ---- the 18 x 18 Cholesky with the pivot-row broadcasts fused into the FMAs (chol18_dpp, the default)
 // x += (lane L's y within the lane's 16-lane row) * f by one v_fmac_f64 with a DPP row_newbcast source (64-bit DPP,
@@ -1096,7 +1133,7 @@ __device__ __forceinline__ void chol18_steps(double (&dr)[NB], double (&br)[NB],
   if constexpr (K < 16) {
     const double Dk = ksp_bcast_dep<K>(dr[K]);
     const bool pos = Dk > 0.0;
-    const double rdk = pos ? ksp_recip(Dk) : 0.0;
+    const double rdk = pos ? ksp_recip1(Dk) : 0.0;
     const double nfd = -(dr[K] * rdk), nfb = -(br[K] * rdk);
     chol18_cols<K, K + 1>(dr, br, nfd, nfb);
     ok = ok && pos;
@@ -1226,13 +1263,16 @@ __device__ __forceinline__ void node_forward(const double* L, const double* id, 
                                              double* dst, int ds, int tid, int nth = -1) {
   if (nth < 0) nth = blockDim.x;
   for (int c = tid; c < ncol; c += nth) {
+    // right-looking: once z[k] is final it updates every later row, so the dependent chain is one FMA and one
+    // multiply per row (the left-looking dot products chained all 153 FMAs)
     double z[NB];
 #pragma unroll
-    for (int row = 0; row < NB; ++row) {
-      double v = W[row * ws + c];
+    for (int row = 0; row < NB; ++row) z[row] = W[row * ws + c];
 #pragma unroll
-      for (int k = 0; k < row; ++k) v -= L[row * NB + k] * z[k];
-      z[row] = v * id[row];
+    for (int k = 0; k < NB; ++k) {
+      z[k] *= id[k];
+#pragma unroll
+      for (int row = k + 1; row < NB; ++row) z[row] -= L[row * NB + k] * z[k];
     }
 #pragma unroll
     for (int row = 0; row < NB; ++row) dst[row * ds + c] = z[row];
@@ -1247,12 +1287,13 @@ __device__ __forceinline__ void node_forward_lean(const double* L, const double*
   for (int c = tid; c < ncol; c += nth) {
     double z[NB];
 #pragma unroll
-    for (int row = 0; row < NB; ++row) {
-      asm volatile("" ::: "memory");
-      double v = W[row * ws + c];
+    for (int row = 0; row < NB; ++row) z[row] = W[row * ws + c];
 #pragma unroll
-      for (int k = 0; k < row; ++k) v -= L[row * NB + k] * z[k];
-      z[row] = v * id[row];
+    for (int k = 0; k < NB; ++k) {  // the arithmetic of node_forward, in the same order
+      asm volatile("" ::: "memory");
+      z[k] *= id[k];
+#pragma unroll
+      for (int row = k + 1; row < NB; ++row) z[row] -= L[row * NB + k] * z[k];
     }
 #pragma unroll
     for (int row = 0; row < NB; ++row) dst[row * ds + c] = z[row];
@@ -1268,12 +1309,12 @@ __device__ __forceinline__ void node_backsolve(const double* L, const double* id
     double z[NB];
 #pragma unroll
     for (int row = 0; row < NB; ++row) z[row] = T[row * ts + c];
+    // right-looking (see node_forward)
 #pragma unroll
-    for (int row = NB - 1; row >= 0; --row) {
-      double v = z[row];
+    for (int k = NB - 1; k >= 0; --k) {
+      z[k] *= id[k];
 #pragma unroll
-      for (int k = row + 1; k < NB; ++k) v -= L[k * NB + row] * z[k];
-      z[row] = v * id[row];
+      for (int row = 0; row < k; ++row) z[row] -= L[k * NB + row] * z[k];
     }
 #pragma unroll
     for (int row = 0; row < NB; ++row) out[row * m + c] = z[row];
@@ -1288,12 +1329,11 @@ __device__ __forceinline__ void node_backsolve_lean(const double* L, const doubl
 #pragma unroll
     for (int row = 0; row < NB; ++row) z[row] = T[row * ts + c];
 #pragma unroll
-    for (int row = NB - 1; row >= 0; --row) {
+    for (int k = NB - 1; k >= 0; --k) {  // the arithmetic of node_backsolve, in the same order
       asm volatile("" ::: "memory");
-      double v = z[row];
+      z[k] *= id[k];
 #pragma unroll
-      for (int k = row + 1; k < NB; ++k) v -= L[k * NB + row] * z[k];
-      z[row] = v * id[row];
+      for (int row = 0; row < k; ++row) z[row] -= L[k * NB + row] * z[k];
     }
 #pragma unroll
     for (int row = 0; row < NB; ++row) out[row * m + c] = z[row];
@@ -1307,6 +1347,7 @@ __global__ void __launch_bounds__(256) k_sp_elim1(SpDev d) {
   extern __shared__ __attribute__((aligned(16))) double W[];  // [18][36 + m]
   const int j = 1 + 2 * blockIdx.x, tid = threadIdx.x, m = d.m, wc = 36 + m;
   if (j >= d.n) return;
+  KSP_TSB(1, 112);
   const int l = j - 1, r = j + 1;
   const double* Ul = d.U0 + (size_t)l * NB * NB;
   const double* Uj = d.U0 + (size_t)j * NB * NB;
@@ -1314,30 +1355,109 @@ __global__ void __launch_bounds__(256) k_sp_elim1(SpDev d) {
   const double* Dj = d.D0 + (size_t)j * NB * NB;
   const double lam2 = d.sc[SC_LAM2];
   const bool hr = r < d.n;
-  ksp_batched<7>(
-      NB * NB + NB * wc, tid, blockDim.x,
-      [&](int q) {
-        if (q < NB * NB) return Dj[q];
-        const int e = q - NB * NB, row = e / wc, c = e % wc;
-        return c < NB ? Ul[c * NB + row] : c < 2 * NB ? Uj[row * NB + c - NB] : Rj[row * m + c - 2 * NB];
-      },
-      [&](int q, double v) {
-        if (q < NB * NB) {
-          L[q] = v + lam_diag(d, j, q, lam2);
-        } else {
-          const int e = q - NB * NB, c = e % wc;
-          W[e] = (c >= NB && c < 2 * NB && !hr) ? 0.0 : v;
-        }
-      });
+  const int nth = blockDim.x;
+  // D_j | U_{j-1} | U_j | R_j as four segments, written as L and W = [U_{j-1}^T | U_j | R_j]
+  double vd[2], vul[2], vuj[2], vr[3];
+  seg_ld(vd, Dj, NB * NB, tid, nth);
+  seg_ld(vul, Ul, NB * NB, tid, nth);
+  seg_ld(vuj, Uj, NB * NB, tid, nth);
+  seg_ld(vr, Rj, NB * m, tid, nth);
+  seg_st(vd, Dj, NB * NB, tid, nth, [&](int q, double v) { L[q] = v + lam_diag(d, j, q, lam2); });
+  seg_st(vul, Ul, NB * NB, tid, nth, [&](int q, double v) { W[(q % NB) * wc + q / NB] = v; });
+  seg_st(vuj, Uj, NB * NB, tid, nth, [&](int q, double v) { W[(q / NB) * wc + NB + q % NB] = hr ? v : 0.0; });
+  const float rinv = 1.0f / (float)m;
+  seg_st(vr, Rj, NB * m, tid, nth, [&](int q, double v) {
+    const int r = div_small(q, rinv);
+    W[r * wc + 2 * NB + (q - r * m)] = v;
+  });
   __syncthreads();
+  KSP_TSB(1, 113);
   if (tid < 64) {
     const bool ok = chol18_wave(L, id, tid);
     if (!ok && tid == 0) d.sc[SC_OK] = 0.0;
   }
   __syncthreads();
+  KSP_TSB(1, 114);
   node_forward(L, id, W, wc, wc, d.Z + (size_t)j * NB * wc, wc, tid);
   for (int q = tid; q < NB * NB; q += blockDim.x) d.Lf[(size_t)j * NB * NB + q] = L[q];
   if (tid < NB) d.Lid[(size_t)j * NB + tid] = id[tid];
+  KSP_TSB(1, 115);
+}
+
+// the absorption products of level_step on f64 MFMA tiles (round 5; the scalar loops before read 72 LDS operands per
+// entry and took 4.5 us of a 12 us level).  With P_l = Zl_U^T Zl and P_r = Zr_Uin^T Zr (18 x wc each):
+//   D' = D - P_l[:, U] - P_r[:, Uin],  R' = R - P_l[:, R] - P_r[:, R]   (both sides: 8 tiles over [D | R], 2 x 4)
+//   Ui = -P_l[:, Uin]^T                                                  (left only: 4 tiles, 2 x 2)
+//   Uo = -P_r[:, U]                                                      (right only: 4 tiles, 2 x 2)
+// K = 18 in five steps of 4 per side.  The tile kind is wave-uniform and no operand is masked but the k >= 18 rows of
+// the last step: rows >= 18 and columns past a part's end read valid LDS (the Z tiles run on into the next buffer) and
+// their outputs are not stored.  ~100 instructions per tile instead of ~400 with per-lane part selects and masks.
+__device__ __forceinline__ void level_products(const SpDev& d, const double* Zl, const double* Zr, double* L, double* Ui,
+                                               double* Uo, double* W, int m, int wc, int tid, int nth, int tsb) {
+  // the wave index as a scalar: tile indices and kinds are wave-uniform (scalar branches, no exec masking)
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, nw = nth >> 6, i16 = lane & 15, kq = lane >> 4;
+  const int ncb = (NB + m + 15) >> 4;  // column tiles of [D | R]
+  const int nt = 2 * ncb + 8;
+  const bool k4 = 16 + kq < NB;  // the last k step's rows 16 + kq exist
+  int ko[5];                     // the lane's Z row offsets of the five k steps
+#pragma unroll
+  for (int st = 0; st < 5; ++st) ko[st] = min(4 * st + kq, NB - 1) * wc;
+  __shared__ double junk[64];    // the stores of rows / columns outside a part land here (no branch per store)
+  KSP_TSB(tsb, 240);
+  for (int t = wave; t < nt; t += nw) {
+    int kind, ti, tj;
+    if (t < 2 * ncb) {
+      kind = 0, ti = t / ncb, tj = t % ncb;
+    } else {
+      const int u = t - 2 * ncb;
+      kind = 1 + (u >> 2), ti = (u >> 1) & 1, tj = u & 1;
+    }
+    const int r = 16 * ti + i16, c = 16 * tj + i16;  // the lane's A row and B column within the tile's part
+    // column offsets in a Z row: kind 0: [D | R] column c -> U / Uin + c, then R; kind 1 (Ui, left): Uin + c;
+    // kind 2 (Uo, right): U + c
+    const int cl = kind == 0 ? (c < NB ? NB + c : 2 * NB + c - NB) : c;
+    const int cr = kind == 0 ? (c < NB ? c : 2 * NB + c - NB) : NB + c;
+    double al[5], bl[5], ar[5], br[5];
+#pragma unroll
+    for (int st = 0; st < 5; ++st) {
+      al[st] = Zl[ko[st] + NB + r];
+      bl[st] = Zl[ko[st] + cl];
+      ar[st] = Zr[ko[st] + r];
+      br[st] = Zr[ko[st] + cr];
+    }
+    al[4] = k4 ? al[4] : 0.0;
+    ar[4] = k4 ? ar[4] : 0.0;
+    __builtin_amdgcn_sched_barrier(0);
+    v4d_t accl = {0.0, 0.0, 0.0, 0.0}, accr = {0.0, 0.0, 0.0, 0.0};
+    if (kind != 2) {
+#pragma unroll
+      for (int st = 0; st < 5; ++st) accl = __builtin_amdgcn_mfma_f64_16x16x4f64(al[st], bl[st], accl, 0, 0, 0);
+    }
+    if (kind != 1) {
+#pragma unroll
+      for (int st = 0; st < 5; ++st) accr = __builtin_amdgcn_mfma_f64_16x16x4f64(ar[st], br[st], accr, 0, 0, 0);
+    }
+    const v4d_t acc = accl + accr;
+    // output column c of this lane, rows 16 ti + kq + 4 rr: the destination by selects, the store unconditional
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int row = 16 * ti + kq + 4 * rr;
+      const bool rv = row < NB;
+      double* dst = junk + lane;
+      if (kind == 0) {
+        dst = (rv && c < NB) ? L + row * NB + c : (rv && c < NB + m) ? W + row * wc + NB + c : dst;
+        *dst = *dst - acc[rr];
+      } else {
+        if (kind == 1) dst = (rv && c < NB) ? Ui + c * NB + row : dst;
+        else dst = (rv && c < NB) ? Uo + row * NB + c : dst;
+        *dst = -acc[rr];
+      }
+    }
+#ifdef KB_STAMPS
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (t < 16) KSP_TSB(tsb, 241 + t / nw);
+#endif
+  }
 }
 
 // fused level: node i (i % 2s == 0) absorbs its level-s eliminated neighbours i -+ s, then either is
@@ -1358,6 +1478,9 @@ __device__ __forceinline__ void level_step(const SpDev& d, int s, int i, bool ac
   double* Zl = sm;
   double* Zr = Zl + NB * wc;
   double* W = Zr + NB * wc;  // [Ui^T | Uo | R']
+  // diagnostics: block 1 of the level (block 0 once it is alone), slots 120 + 6 lv + k (tools/diag_sp_levels.py)
+  const int tsb = gridDim.x > 1 ? 1 : 0, tsl = 120 + 6 * (31 - __clz(s));
+  if (!LEAN) KSP_TSB(tsb, tsl);
   if (act) {
     // Zl | Zr | D_i (into L) | R_i (into W's R columns) in one batch of loads; absent neighbours read node i's Z
     // slot (any valid address) and store zeros
@@ -1367,54 +1490,28 @@ __device__ __forceinline__ void level_step(const SpDev& d, int s, int i, bool ac
     const double* Ri = (s == 1 ? d.R0 : d.R) + (size_t)i * NB * m;
     const double lam2 = s == 1 ? d.sc[SC_LAM2] : 0.0;
     const int nz = NB * wc;
-    ksp_batched<LEAN ? 6 : 15>(
-        2 * nz + NB * NB + NB * m, tid, nth,
-        [&](int q) {
-          return q < nz ? Zsl[q] : q < 2 * nz ? Zsr[q - nz] : q < 2 * nz + NB * NB ? Di[q - 2 * nz] : Ri[q - 2 * nz - NB * NB];
-        },
-        [&](int q, double v) {
-          if (q < nz) {
-            Zl[q] = hl ? v : 0.0;
-          } else if (q < 2 * nz) {
-            Zr[q - nz] = hr ? v : 0.0;
-          } else if (q < 2 * nz + NB * NB) {
-            L[q - 2 * nz] = v + lam_diag(d, i, q - 2 * nz, lam2);
-          } else {
-            const int e = q - 2 * nz - NB * NB;
-            W[(e / m) * wc + 2 * NB + e % m] = v;
-          }
-        });
+    constexpr int UZ = LEAN ? 3 : 6, UD = LEAN ? 3 : 2, UR = LEAN ? 3 : 3;
+    double vl[UZ], vr[UZ], vd[UD], vq[UR];
+    seg_ld(vl, Zsl, nz, tid, nth);
+    seg_ld(vr, Zsr, nz, tid, nth);
+    seg_ld(vd, Di, NB * NB, tid, nth);
+    seg_ld(vq, Ri, NB * m, tid, nth);
+    seg_st(vl, Zsl, nz, tid, nth, [&](int q, double v) { Zl[q] = hl ? v : 0.0; });
+    seg_st(vr, Zsr, nz, tid, nth, [&](int q, double v) { Zr[q] = hr ? v : 0.0; });
+    seg_st(vd, Di, NB * NB, tid, nth, [&](int q, double v) { L[q] = v + lam_diag(d, i, q, lam2); });
+    const float rinv = 1.0f / (float)m;
+    seg_st(vq, Ri, NB * m, tid, nth, [&](int q, double v) {
+      const int r = div_small(q, rinv);
+      W[r * wc + 2 * NB + (q - r * m)] = v;
+    });
   }
   __syncthreads();
   KSP_STOP(1);
-  if (act) {
-    for (int q = tid; q < 3 * NB * NB; q += nth) {
-      const int part = q / (NB * NB), e = q % (NB * NB), a = e / NB, b = e % NB;
-      double acc = 0.0;
-      if (part == 0) {  // D' = D - Zl_U^T Zl_U - Zr_Uin^T Zr_Uin
-#pragma unroll
-        for (int k = 0; k < NB; ++k) acc += Zl[k * wc + NB + a] * Zl[k * wc + NB + b] + Zr[k * wc + a] * Zr[k * wc + b];
-        L[e] -= acc;
-      } else if (part == 1) {  // Uo = -Zr_Uin^T Zr_U
-#pragma unroll
-        for (int k = 0; k < NB; ++k) acc += Zr[k * wc + a] * Zr[k * wc + NB + b];
-        Uo[e] = -acc;
-      } else {  // Ui = -Zl_Uin^T Zl_U  (rows i - 2s, cols i)
-#pragma unroll
-        for (int k = 0; k < NB; ++k) acc += Zl[k * wc + a] * Zl[k * wc + NB + b];
-        Ui[e] = -acc;
-      }
-    }
-    for (int q = tid; q < NB * m; q += nth) {  // R' = R - Zl_U^T Zl_R - Zr_Uin^T Zr_R
-      const int a = q / m, c = q % m;
-      double acc = 0.0;
-#pragma unroll
-      for (int k = 0; k < NB; ++k) acc += Zl[k * wc + NB + a] * Zl[k * wc + 2 * NB + c] + Zr[k * wc + a] * Zr[k * wc + 2 * NB + c];
-      W[a * wc + 2 * NB + c] -= acc;
-    }
-  }
+  if (!LEAN) KSP_TSB(tsb, tsl + 1);
+  if (act) level_products(d, Zl, Zr, L, Ui, Uo, W, m, wc, tid, nth, LEAN ? -1 : tsb);
   __syncthreads();
   KSP_STOP(2);
+  if (!LEAN) KSP_TSB(tsb, tsl + 2);
   const bool fin = act && (elim || top);
   if (act && !fin) {  // stays active: D', U (to i + 2s), R' for the next level
     for (int q = tid; q < NB * NB; q += nth) {
@@ -1436,6 +1533,7 @@ __device__ __forceinline__ void level_step(const SpDev& d, int s, int i, bool ac
   }
   __syncthreads();
   KSP_STOP(3);
+  if (!LEAN) KSP_TSB(tsb, tsl + 3);
   if (fin && top) {  // X_0 = L^-T L^-1 R' (forward in place in W, then backward into X_0)
     if (LEAN) {
       node_forward_lean(L, id, W + 2 * NB, wc, m, W + 2 * NB, wc, tid, nth);
@@ -1451,6 +1549,7 @@ __device__ __forceinline__ void level_step(const SpDev& d, int s, int i, bool ac
     for (int q = tid; q < NB * NB; q += nth) d.Lf[(size_t)i * NB * NB + q] = L[q];
     if (tid < NB) d.Lid[(size_t)i * NB + tid] = id[tid];
   }
+  if (!LEAN) KSP_TSB(tsb, tsl + 4);
 }
 
 __global__ void __launch_bounds__(256) k_sp_level(SpDev d, int s) {
@@ -1482,6 +1581,46 @@ __global__ void __launch_bounds__(256) k_sp_top(SpDev d) {
   node_backsolve(L, id, T, m, m, d.X, tid);
 }
 
+// T = Z_R - Z_Uin x_l - Z_U x_r of one node on MFMA tiles (the node group's nth threads): T[row][c] = Z_R[row][c] -
+// sum_k (Z[row][k] xl[k][c] + Z[row][NB + k] xr[k][c]); A = Z^T is read from the Z rows (stride 1 in k), B from xl / xr
+__device__ __forceinline__ void back_T(const double* Z, const double* xl, const double* xr, double* T, int m, int wc,
+                                       int tid, int nth) {
+  const int wave = tid >> 6, lane = tid & 63, nw = nth >> 6, nct = (m + 15) >> 4;
+  for (int t = wave; t < 2 * nct; t += nw) {
+    const int ti = t / nct, tj = t % nct, i = lane & 15;
+    const int rc = min(16 * ti + i, NB - 1), cc = min(16 * tj + i, m - 1);
+    const bool rv = 16 * ti + i < NB, cv = 16 * tj + i < m;
+    // operands first (see level_products), the two sides in two accumulator chains
+    double av[2][5], bv[2][5];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const double* B = h ? xr : xl;
+#pragma unroll
+      for (int st = 0; st < 5; ++st) {
+        const int kc = min(4 * st + (lane >> 4), NB - 1);
+        av[h][st] = Z[rc * wc + h * NB + kc];
+        bv[h][st] = B[kc * m + cc];
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    v4d_t ac[2] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
+#pragma unroll
+    for (int st = 0; st < 5; ++st) {
+      const bool kv = 4 * st + (lane >> 4) < NB;
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        ac[h] = __builtin_amdgcn_mfma_f64_16x16x4f64((kv && rv) ? av[h][st] : 0.0, (kv && cv) ? bv[h][st] : 0.0, ac[h], 0, 0, 0);
+    }
+    const v4d_t acc = ac[0] + ac[1];
+    const int c = 16 * tj + (lane & 15);
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int row = 16 * ti + (lane >> 4) + 4 * rr;
+      if (row < NB && c < m) T[row * m + c] = Z[row * wc + 2 * NB + c] - acc[rr];
+    }
+  }
+}
+
 // back_step: node j's back substitution by a node group (the contract of level_step: every thread of the block
 // calls it, two block barriers on every path); L, id and sm (Z [18][wc] | xl | xr | T [18][m]) are the group's LDS
 template <bool LEAN>
@@ -1494,6 +1633,8 @@ __device__ __forceinline__ void back_step(const SpDev& d, int s, int j, bool act
   double* xl = Z + NB * wc;
   double* xr = xl + NB * m;
   double* T = xr + NB * m;
+  const int tsl = 190 + 4 * (31 - __clz(s));
+  if (!LEAN) KSP_TSB(0, tsl);
   if (act) {
     // L_j | 1/diag | Z_j | x_l | x_r in one batch of loads (x_r of an absent neighbour: zeros)
     const double* Ls = d.Lf + (size_t)j * NB * NB;
@@ -1501,58 +1642,31 @@ __device__ __forceinline__ void back_step(const SpDev& d, int s, int j, bool act
     const double* Zs = d.Z + (size_t)j * NB * wc;
     const double* Xl = d.X + (size_t)l * NB * m;
     const double* Xr = d.X + (size_t)(hr ? r : l) * NB * m;
-    const int n0 = NB * NB, n1 = n0 + NB, n2 = n1 + NB * wc, n3 = n2 + NB * m;
-    ksp_batched<LEAN ? 6 : 13>(
-        n3 + NB * m, tid, nth,
-        [&](int q) { return q < n0 ? Ls[q] : q < n1 ? Is[q - n0] : q < n2 ? Zs[q - n1] : q < n3 ? Xl[q - n2] : Xr[q - n3]; },
-        [&](int q, double v) {
-          if (q < n0)
-            L[q] = v;
-          else if (q < n1)
-            id[q - n0] = v;
-          else if (q < n2)
-            Z[q - n1] = v;
-          else if (q < n3)
-            xl[q - n2] = v;
-          else
-            xr[q - n3] = hr ? v : 0.0;
-        });
+    constexpr int UL = 2, UZ = LEAN ? 3 : 6, UX = LEAN ? 3 : 3;
+    double vL[UL], vI[1], vZ[UZ], vxl[UX], vxr[UX];
+    seg_ld(vL, Ls, NB * NB, tid, nth);
+    seg_ld(vI, Is, NB, tid, nth);
+    seg_ld(vZ, Zs, NB * wc, tid, nth);
+    seg_ld(vxl, Xl, NB * m, tid, nth);
+    seg_ld(vxr, Xr, NB * m, tid, nth);
+    seg_st(vL, Ls, NB * NB, tid, nth, [&](int q, double v) { L[q] = v; });
+    seg_st(vI, Is, NB, tid, nth, [&](int q, double v) { id[q] = v; });
+    seg_st(vZ, Zs, NB * wc, tid, nth, [&](int q, double v) { Z[q] = v; });
+    seg_st(vxl, Xl, NB * m, tid, nth, [&](int q, double v) { xl[q] = v; });
+    seg_st(vxr, Xr, NB * m, tid, nth, [&](int q, double v) { xr[q] = hr ? v : 0.0; });
   }
   __syncthreads();
   KSP_STOP(1);
-  // T = Z_R - Z_Uin x_l - Z_U x_r on MFMA tiles: T[row][c] = Z_R[row][c] - sum_k (Z[row][k] xl[k][c] + Z[row][NB + k]
-  // xr[k][c]); A = Z^T is read from the Z rows (stride 1 in k), B from xl / xr
-  if (act) {
-    const int wave = tid >> 6, lane = tid & 63, nw = nth >> 6, nct = (m + 15) >> 4;
-    for (int t = wave; t < 2 * nct; t += nw) {
-      const int ti = t / nct, tj = t % nct, i = lane & 15;
-      const int rc = min(16 * ti + i, NB - 1), cc = min(16 * tj + i, m - 1);
-      const bool rv = 16 * ti + i < NB, cv = 16 * tj + i < m;
-      v4d_t acc = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const double* B = h ? xr : xl;
-#pragma unroll
-        for (int st = 0; st < 5; ++st) {
-          const int k = 4 * st + (lane >> 4), kc = min(k, NB - 1);
-          const double a = Z[rc * wc + h * NB + kc], b = B[kc * m + cc];
-          acc = __builtin_amdgcn_mfma_f64_16x16x4f64((k < NB && rv) ? a : 0.0, (k < NB && cv) ? b : 0.0, acc, 0, 0, 0);
-        }
-      }
-      const int c = 16 * tj + (lane & 15);
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        const int row = 16 * ti + (lane >> 4) + 4 * rr;
-        if (row < NB && c < m) T[row * m + c] = Z[row * wc + 2 * NB + c] - acc[rr];
-      }
-    }
-  }
+  if (!LEAN) KSP_TSB(0, tsl + 1);
+  if (act) back_T(Z, xl, xr, T, m, wc, tid, nth);
   __syncthreads();
   KSP_STOP(2);
+  if (!LEAN) KSP_TSB(0, tsl + 2);
   if (act) {
     if (LEAN) node_backsolve_lean(L, id, T, m, m, d.X + (size_t)j * NB * m, tid, nth);
     else node_backsolve(L, id, T, m, m, d.X + (size_t)j * NB * m, tid, nth);
   }
+  if (!LEAN) KSP_TSB(0, tsl + 3);
 }
 
 __global__ void __launch_bounds__(256) k_sp_back(SpDev d, int s) {
@@ -1562,6 +1676,84 @@ __global__ void __launch_bounds__(256) k_sp_back(SpDev d, int s) {
   const int j = s + 2 * s * blockIdx.x;
   if (j >= d.n) return;  // block-uniform
   back_step<false>(d, s, j, true, threadIdx.x, blockDim.x, L, id, sm);
+}
+
+// two back-substitution levels in one launch (round 5): strides 2s and s.  Block b takes node j = s + 2sb of stride s.
+// Of its neighbours j -+ s (multiples of 2s) the odd multiple of 2s, k, belongs to stride 2s: the block solves it first
+// (x_{k -+ 2s} are known), then j from x_k (in LDS) and its other neighbour o.  x_k is solved by the blocks on both
+// sides of it from the same operands by the same instructions, so both copies are bitwise equal; the block with
+// k = j + s stores it (node k - s always exists).  One launch, one batch of operand loads and one launch gap instead
+// of two; every value is computed as by two k_sp_back launches.
+__global__ void __launch_bounds__(256) k_sp_back2(SpDev d, int s) {
+  __shared__ double L[2][NB * NB];
+  __shared__ double id[2][NB];
+  // node k: Zk [18][wc] | xa | xb [18][m]; node j: Zj [18][wc] | xjl | xjr [18][m]; T [18][m]
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  const int b = blockIdx.x, j = s + 2 * s * b, tid = threadIdx.x, nth = blockDim.x;
+  if (j >= d.n) return;  // block-uniform
+  const int tsl = 190 + 4 * (31 - __clz(s));  // diagnostics: the stride-s slots (x_k done in place of T)
+  KSP_TSB(0, tsl);
+  const int m = d.m, wc = 36 + m, n = d.n;
+  const bool kl = (b & 1) != 0;  // k = j - s (b odd) or k = j + s (b even)
+  const int k = kl ? j - s : j + s, o = kl ? j + s : j - s;
+  const bool hk = k < n, ho = o < n, hkb = k + 2 * s < n;
+  double* Zk = sm;
+  double* xa = Zk + NB * wc;
+  double* xb = xa + NB * m;
+  double* Zj = xb + NB * m;
+  double* xjl = Zj + NB * wc;
+  double* xjr = xjl + NB * m;
+  double* T = xjr + NB * m;
+  double* xk = kl ? xjl : xjr;  // x_k among node j's operands
+  double* xo = kl ? xjr : xjl;
+  {
+    // L_k | 1/diag_k | Z_k | x_{k-2s} | x_{k+2s} | L_j | 1/diag_j | Z_j | x_o in one batch (absent nodes: zeros; their
+    // loads read node j's slots)
+    const int kc = hk ? k : j;
+    const double* Lks = d.Lf + (size_t)kc * NB * NB;
+    const double* Iks = d.Lid + (size_t)kc * NB;
+    const double* Zks = d.Z + (size_t)kc * NB * wc;
+    const double* Xas = d.X + (size_t)(hk ? k - 2 * s : j - s) * NB * m;
+    const double* Xbs = d.X + (size_t)(hkb ? k + 2 * s : j - s) * NB * m;
+    const double* Ljs = d.Lf + (size_t)j * NB * NB;
+    const double* Ijs = d.Lid + (size_t)j * NB;
+    const double* Zjs = d.Z + (size_t)j * NB * wc;
+    const double* Xos = d.X + (size_t)(ho ? o : j - s) * NB * m;
+    if (!hk)
+      for (int q = tid; q < NB * m; q += nth) xk[q] = 0.0;
+    double vLk[2], vIk[1], vZk[6], vxa[3], vxb[3], vLj[2], vIj[1], vZj[6], vxo[3];
+    seg_ld(vLk, Lks, NB * NB, tid, nth);
+    seg_ld(vIk, Iks, NB, tid, nth);
+    seg_ld(vZk, Zks, NB * wc, tid, nth);
+    seg_ld(vxa, Xas, NB * m, tid, nth);
+    seg_ld(vxb, Xbs, NB * m, tid, nth);
+    seg_ld(vLj, Ljs, NB * NB, tid, nth);
+    seg_ld(vIj, Ijs, NB, tid, nth);
+    seg_ld(vZj, Zjs, NB * wc, tid, nth);
+    seg_ld(vxo, Xos, NB * m, tid, nth);
+    seg_st(vLk, Lks, NB * NB, tid, nth, [&](int q, double v) { L[0][q] = v; });
+    seg_st(vIk, Iks, NB, tid, nth, [&](int q, double v) { id[0][q] = v; });
+    seg_st(vZk, Zks, NB * wc, tid, nth, [&](int q, double v) { Zk[q] = v; });
+    seg_st(vxa, Xas, NB * m, tid, nth, [&](int q, double v) { xa[q] = v; });
+    seg_st(vxb, Xbs, NB * m, tid, nth, [&](int q, double v) { xb[q] = hkb ? v : 0.0; });
+    seg_st(vLj, Ljs, NB * NB, tid, nth, [&](int q, double v) { L[1][q] = v; });
+    seg_st(vIj, Ijs, NB, tid, nth, [&](int q, double v) { id[1][q] = v; });
+    seg_st(vZj, Zjs, NB * wc, tid, nth, [&](int q, double v) { Zj[q] = v; });
+    seg_st(vxo, Xos, NB * m, tid, nth, [&](int q, double v) { xo[q] = ho ? v : 0.0; });
+  }
+  __syncthreads();
+  KSP_TSB(0, tsl + 1);
+  if (hk) back_T(Zk, xa, xb, T, m, wc, tid, nth);  // block-uniform branches
+  __syncthreads();
+  if (hk) node_backsolve(L[0], id[0], T, m, m, xk, tid, nth);
+  __syncthreads();
+  KSP_TSB(0, tsl + 2);
+  if (hk && !kl)
+    for (int q = tid; q < NB * m; q += nth) d.X[(size_t)k * NB * m + q] = xk[q];
+  back_T(Zj, xjl, xjr, T, m, wc, tid, nth);
+  __syncthreads();
+  node_backsolve(L[1], id[1], T, m, m, d.X + (size_t)j * NB * m, tid, nth);
+  KSP_TSB(0, tsl + 3);
 }
 
 // the deep levels in one block (round 4): once a level has at most kSpDeepGroups nodes, the remaining levels down to
@@ -1989,7 +2181,7 @@ __global__ void __launch_bounds__(64) k_sp_camsolve(SpDev d) {
   for (int k = 0; k < CM; ++k) {
     const double Dk = rdlane(a[k], k);
     ok = ok && (Dk > 0.0);
-    const double rdk = ksp_recip(Dk);
+    const double rdk = ksp_recip1(Dk);
     rD = (lane == k) ? rdk : rD;
     const double f = (lane > k) ? a[k] * rdk : 0.0;
 #pragma unroll
@@ -2392,7 +2584,8 @@ struct kb_sp_handle {
   std::vector<void*> allocs;
   double lambda = 0.0;
   bool uploaded = false, built = false, solved = false;
-  size_t lds_frames = 0, lds_asm = 0, lds_elim = 0, lds_level = 0, lds_schur = 0, lds_back = 0;
+  size_t lds_frames = 0, lds_asm = 0, lds_elim = 0, lds_level = 0, lds_schur = 0, lds_back = 0, lds_back2 = 0;
+  bool back2 = true;       // k_sp_back2: two back-substitution strides per launch
   const void* fn_frames = nullptr;
   const void* fn_cost = nullptr;
   const void* fn_camsolve = nullptr;
@@ -2473,9 +2666,21 @@ int launch_reduction(kb_sp_handle* h) {
     hipLaunchKernelGGL(k_sp_deep, dim3(1), dim3(kSpDeepGT * h->deep_groups), h->lds_deep, h->stream, d, sd);
     s = sd;
   }
-  for (s /= 2; s >= 1; s /= 2) {
-    const int ne = (d.n - s + 2 * s - 1) / (2 * s);
-    hipLaunchKernelGGL(k_sp_back, dim3(ne), dim3(256), h->lds_back, h->stream, d, s);
+  // back-substitution strides s/2 .. 1: with k_sp_back2 two per launch (an odd count leaves the top one single)
+  int nb = 0;
+  for (int t = s / 2; t >= 1; t /= 2) ++nb;
+  for (s /= 2; s >= 1;) {
+    if (h->back2 && (nb & 1) == 0) {
+      const int sl = s / 2, ne = (d.n - sl + 2 * sl - 1) / (2 * sl);
+      hipLaunchKernelGGL(k_sp_back2, dim3(ne), dim3(256), h->lds_back2, h->stream, d, sl);
+      s /= 4;
+      nb -= 2;
+    } else {
+      const int ne = (d.n - s + 2 * s - 1) / (2 * s);
+      hipLaunchKernelGGL(k_sp_back, dim3(ne), dim3(256), h->lds_back, h->stream, d, s);
+      s /= 2;
+      nb -= 1;
+    }
   }
   return 0;
 }
@@ -2717,6 +2922,11 @@ kb_sp_handle* kb_sp_create(const kb_sp_layout* L) {
   h->lds_elim = sizeof(double) * NB * (36 + d.m);
   h->lds_level = 3 * h->lds_elim;
   h->lds_back = h->lds_elim + sizeof(double) * 3 * NB * d.m;
+  h->lds_back2 = 2 * h->lds_elim + sizeof(double) * 5 * NB * d.m;
+  {
+    const char* ev = std::getenv("KSP_BACK2");  // two back-substitution strides per launch (default on)
+    h->back2 = !(ev && std::atoi(ev) == 0);
+  }
   h->lds_schur = sizeof(double) * (2 * NB * d.m + d.Ws) + sizeof(short2) * d.Ws;
   h->lds_asm = sizeof(double) * (2 * NB * NB + NB * d.m + std::max(TCH * IST, TCF * d.FHS));
   h->lds_frames = sizeof(double) * (h->N * 64 * XS + h->N * 256 + 2 * h->N * 36 + 2 * h->N * h->N * 36 + d.Wc +
@@ -2732,6 +2942,7 @@ kb_sp_handle* kb_sp_create(const kb_sp_layout* L) {
   hipFuncSetAttribute((const void*)k_sp_level, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_level);
   hipFuncSetAttribute((const void*)k_sp_elim1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_elim);
   hipFuncSetAttribute((const void*)k_sp_back, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_back);
+  hipFuncSetAttribute((const void*)k_sp_back2, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_back2);
   {
     // the deep levels in one block (k_sp_deep, KSP_DEEP=1; measured and not kept: configs[4] 2,227 -> 1,998 GN it/s,
     // the one-block kernel 118 us against 74 us for the six launches it replaces -- four nodes share one CU's SIMDs
