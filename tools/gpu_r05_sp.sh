@@ -9,7 +9,7 @@ timeout -k 10 300 python -u -m pytest tests/test_gpu_spline.py -m gpu -x -q --ti
 tail -1 $O/gputests.log
 for v in 0 1; do
   KSP_BACK2=$v timeout -k 10 200 python3 tools/diag_sp_levels.py > $O/levels_b$v.log 2>&1 || { cat $O/levels_b$v.log; exit 1; }
-  echo "== KSP_BACK2=$v"; grep -A30 "^rep 2" $O/levels_b$v.log | grep "elim\|level\|back\|total"
+  echo "== KSP_BACK2=$v"; grep -A30 "^rep 2" $O/levels_b$v.log | grep "elim\|level\|back\|total\|tile"
 done
 for v in 0 1; do
   KSP_BACK2=$v timeout -k 10 200 python3 bench.py --config 5 --no-cpu-baseline > $O/bench_b$v.json 2> $O/bench_b$v.err || { cat $O/bench_b$v.err; exit 1; }
