@@ -1392,8 +1392,12 @@ __global__ void __launch_bounds__(256) k_sp_elim1(SpDev d) {
 // K = 18 in five steps of 4 per side.  The tile kind is wave-uniform and no operand is masked but the k >= 18 rows of
 // the last step: rows >= 18 and columns past a part's end read valid LDS (the Z tiles run on into the next buffer) and
 // their outputs are not stored.  ~100 instructions per tile instead of ~400 with per-lane part selects and masks.
-__device__ __forceinline__ void level_products(const SpDev& d, const double* Zl, const double* Zr, double* L, double* Ui,
-                                               double* Uo, double* W, int m, int wc, int tid, int nth, int tsb) {
+// Ui^T and Uo go straight into W's first 36 columns (the forward solve's [Ui^T | Uo | R']).  With chol (4 waves only) the
+// four tiles holding D' (tj = 0, 1 of kind 0) come first, on waves 0 and 1; wave 1 then raises *dflag and wave 0, once
+// it sees it, factors D' (chol18_wave) while waves 1..3 finish the other tiles, none of which touches L.
+__device__ __forceinline__ void level_products(const SpDev& d, const double* Zl, const double* Zr, double* L, double* id,
+                                               double* W, int m, int wc, int tid, int nth, int tsb, bool chol,
+                                               int* dflag) {
   // the wave index as a scalar: tile indices and kinds are wave-uniform (scalar branches, no exec masking)
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, nw = nth >> 6, i16 = lane & 15, kq = lane >> 4;
   const int ncb = (NB + m + 15) >> 4;  // column tiles of [D | R]
@@ -1404,7 +1408,36 @@ __device__ __forceinline__ void level_products(const SpDev& d, const double* Zl,
   for (int st = 0; st < 5; ++st) ko[st] = min(4 * st + kq, NB - 1) * wc;
   __shared__ double junk[64];    // the stores of rows / columns outside a part land here (no branch per store)
   KSP_TSB(tsb, 240);
-  for (int t = wave; t < nt; t += nw) {
+  // chol: D' tiles (ti, tj) = (0,0), (1,0) on wave 0 and (0,1), (1,1) on wave 1 (order slots 0..3), the rest (slots
+  // 4..nt-1) round-robin over waves 1..3; otherwise slot = t round-robin over all waves
+  const bool ord = chol && nw == 4;
+  const int first = ord ? (wave == 0 ? 0 : wave == 1 ? 2 : 3 + wave) : wave;
+  int step = ord ? (wave <= 1 ? 1 : 3) : nw;
+  for (int slot = first;; slot += step) {
+    if (ord) {
+      if (wave == 0 && slot == 2) {  // both D' tiles of wave 0 stored: wait for wave 1's, then factor
+        while (__hip_atomic_load(dflag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) __builtin_amdgcn_s_sleep(1);
+        const bool ok = chol18_wave(L, id, lane);
+        if (!ok && lane == 0) d.sc[SC_OK] = 0.0;
+        break;
+      }
+      if (wave == 1 && slot == 4) {  // wave 1's D' tiles stored: release them to wave 0, then slots 4, 7, 10, ..
+        __hip_atomic_store(dflag, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        step = 3;
+      }
+    }
+    if (slot >= nt) break;
+    // slot -> tile: with ord, slots 0..3 are the D' tiles and 4.. the others in the plain order without them
+    int t = slot;
+    if (ord) {
+      if (slot < 4) {
+        t = (slot & 1) * ncb + (slot >> 1);  // (ti, tj) = (slot & 1, slot >> 1)
+      } else {
+        const int o = slot - 4;  // the non-D' tiles: kind 0 with tj >= 2 (2 (ncb - 2) of them), then kinds 1 and 2
+        const int n0 = ncb - 2;
+        t = o < 2 * n0 ? (o / n0) * ncb + 2 + o % n0 : 2 * ncb + o - 2 * n0;
+      }
+    }
     int kind, ti, tj;
     if (t < 2 * ncb) {
       kind = 0, ti = t / ncb, tj = t % ncb;
@@ -1448,15 +1481,11 @@ __device__ __forceinline__ void level_products(const SpDev& d, const double* Zl,
         dst = (rv && c < NB) ? L + row * NB + c : (rv && c < NB + m) ? W + row * wc + NB + c : dst;
         *dst = *dst - acc[rr];
       } else {
-        if (kind == 1) dst = (rv && c < NB) ? Ui + c * NB + row : dst;
-        else dst = (rv && c < NB) ? Uo + row * NB + c : dst;
+        // W[row][c] = Ui^T[row][c] = Ui[c][row]; W[row][NB + c] = Uo[row][c]
+        dst = (rv && c < NB) ? W + row * wc + (kind == 1 ? 0 : NB) + c : dst;
         *dst = -acc[rr];
       }
     }
-#ifdef KB_STAMPS
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (t < 16) KSP_TSB(tsb, 241 + t / nw);
-#endif
   }
 }
 
@@ -1481,6 +1510,9 @@ __device__ __forceinline__ void level_step(const SpDev& d, int s, int i, bool ac
   // diagnostics: block 1 of the level (block 0 once it is alone), slots 120 + 6 lv + k (tools/diag_sp_levels.py)
   const int tsb = gridDim.x > 1 ? 1 : 0, tsl = 120 + 6 * (31 - __clz(s));
   if (!LEAN) KSP_TSB(tsb, tsl);
+  const bool fin = act && (elim || top);
+  __shared__ int dflag;  // level_products: wave 1's D' tiles stored (reset before the first barrier)
+  if (tid == 0) dflag = 0;
   if (act) {
     // Zl | Zr | D_i (into L) | R_i (into W's R columns) in one batch of loads; absent neighbours read node i's Z
     // slot (any valid address) and store zeros
@@ -1508,30 +1540,23 @@ __device__ __forceinline__ void level_step(const SpDev& d, int s, int i, bool ac
   __syncthreads();
   KSP_STOP(1);
   if (!LEAN) KSP_TSB(tsb, tsl + 1);
-  if (act) level_products(d, Zl, Zr, L, Ui, Uo, W, m, wc, tid, nth, LEAN ? -1 : tsb);
+  // (4-wave groups: a finishing node's Cholesky inside, on wave 0, behind its D' tiles)
+  const bool early = !LEAN && fin && nth == 256;
+  if (act) level_products(d, Zl, Zr, L, id, W, m, wc, tid, nth, LEAN ? -1 : tsb, early, &dflag);
   __syncthreads();
   KSP_STOP(2);
   if (!LEAN) KSP_TSB(tsb, tsl + 2);
-  const bool fin = act && (elim || top);
-  if (act && !fin) {  // stays active: D', U (to i + 2s), R' for the next level
-    for (int q = tid; q < NB * NB; q += nth) {
-      d.D[(size_t)i * NB * NB + q] = L[q];
-      d.U[(size_t)i * NB * NB + q] = Uo[q];
-    }
+  if (act && !fin) {  // stays active: D', R' for the next level (the coupling is recomputed from Z by both nodes)
+    for (int q = tid; q < NB * NB; q += nth) d.D[(size_t)i * NB * NB + q] = L[q];
     for (int q = tid; q < NB * m; q += nth) d.R[(size_t)i * NB * m + q] = W[(q / m) * wc + 2 * NB + q % m];
   }
-  if (fin) {
-    for (int q = tid; q < NB * NB; q += nth) {
-      const int a = q / NB, b = q % NB;
-      W[a * wc + b] = Ui[b * NB + a];  // Ui^T
-      W[a * wc + NB + b] = Uo[q];
-    }
-    if (tid < 64) {
+  if (LEAN || !early) {  // the Cholesky after the products (k_sp_deep's groups: the same barriers on every path)
+    if (fin && tid < 64) {
       const bool ok = chol18_wave(L, id, tid);
       if (!ok && tid == 0) d.sc[SC_OK] = 0.0;
     }
+    __syncthreads();
   }
-  __syncthreads();
   KSP_STOP(3);
   if (!LEAN) KSP_TSB(tsb, tsl + 3);
   if (fin && top) {  // X_0 = L^-T L^-1 R' (forward in place in W, then backward into X_0)
