@@ -155,6 +155,13 @@ int kb_get_rhs(kb_handle* h, double* rhs_out);
  * the arrow blocks.  Unsharded handles.  Fails unless the last system came from kb_build: the device-resident
  * loops (kb_optimize, kb_gn_*, kb_build_kernel_stats) overwrite or skip the per-call blocks it reads. */
 int kb_rhs_jtj_rhs(kb_handle* h, double* out);
+/* CameraCalibrator::PrintReprojectionErrorStatistics (kalibr2/include/kalibr2/CameraCalibrator.hpp:368-411, called per
+ * camera after the estimator by kalibr2_ros/src/CalibrateCameras.cpp:318) on the device, for every camera of the
+ * handle at its current state: e = y - yhat of every term (ReprojectionError::getPredictedMeasurement), then
+ * out[cam][6] = [n, mean_u, mean_v, std_u, std_v, rmse] with the sample standard deviation (N - 1; 0 when n < 2) of a
+ * second pass about the mean, and the reference's "RMSE" = |sum e| / sqrt(n) (the norm of the error SUM, kept as the
+ * reference prints it).  A camera without terms gets zeros.  Sharded handles sum over all ranks' frames. */
+int kb_reprojection_error_stats(kb_handle* h, double* out);
 /* Optimizer2::applyStateUpdate / revertLastStateUpdate (Optimizer2.cpp:290-318).
  * dx == NULL applies the device-resident dx of the last kb_solve. */
 int kb_apply_update(kb_handle* h, const double* dx, double* deltaX_out);

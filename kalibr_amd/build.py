@@ -7,7 +7,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 SRC = os.path.join(HERE, "csrc", "kb_capi.hip")
 SRC_SPLINE = os.path.join(HERE, "csrc", "kb_spline.hip")
 OUT = os.path.join(HERE, "libkalibr_hip.so")
-DEPS = ["kb_capi.hip", "kb_kernels.hip", "kb_pcg.hip", "kb_device.h", "kb_math.h", "kb_spline.hip"]
+DEPS = ["kb_capi.hip", "kb_kernels.hip", "kb_pcg.hip", "kb_device.h", "kb_math.h", "kb_spline.hip", "kb_build_tu.hip"]
+SRC_BUILD_TU = os.path.join(HERE, "csrc", "kb_build_tu.hip")
+N_BUILD_TU = 9  # camera-model sets, one translation unit each (kb_build_tu.hip -DKB_TU_ID=i)
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wno-unused-result", "-Wno-unused-value"]
 
@@ -21,14 +23,23 @@ def needs_build():
 
 
 def _compile_link(out, extra=()):
-    """The two translation units compiled in parallel (hipcc -c, relocatable device code not needed: each TU owns
-    its kernels), then linked into one shared library."""
-    objs = [out + ".capi.o", out + ".spline.o"]
+    """The translation units (kb_capi.hip, kb_spline.hip and the nine per-model-set build-kernel units of
+    kb_build_tu.hip) compiled in parallel (hipcc -c, no relocatable device code: each TU owns its kernels), then
+    linked into one shared library."""
+    jobs = [(out + ".capi.o", SRC, []), (out + ".spline.o", SRC_SPLINE, [])]
+    jobs += [(out + ".b%d.o" % i, SRC_BUILD_TU, ["-DKB_TU_ID=%d" % i]) for i in range(N_BUILD_TU)]
     cflags = [f for f in FLAGS if f != "-shared"] + list(extra)
-    procs = [subprocess.Popen([HIPCC] + cflags + ["-c", "-o", o, s]) for o, s in zip(objs, [SRC, SRC_SPLINE])]
-    rcs = [p.wait() for p in procs]
+    width = max(1, min(len(jobs), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4))))
+    pending, running, rcs = list(jobs), [], []
+    while pending or running:
+        while pending and len(running) < width:
+            o, s, d = pending.pop(0)
+            running.append(subprocess.Popen([HIPCC] + cflags + d + ["-c", "-o", o, s]))
+        running[0].wait()
+        rcs.append(running.pop(0).returncode)
     if any(rcs):
         raise subprocess.CalledProcessError(max(rcs), "hipcc -c")
+    objs = [o for o, _, _ in jobs]
     subprocess.run([HIPCC] + FLAGS + list(extra) + ["-o", out + ".tmp"] + objs + ["-lrccl"], check=True)
     os.replace(out + ".tmp", out)
     for o in objs:

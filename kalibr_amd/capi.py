@@ -24,7 +24,7 @@ dp = C.POINTER(C.c_double)
 EXPORTS = [
     "kb_create", "kb_destroy", "kb_last_error", "kb_upload_observations", "kb_set_state", "kb_set_state_flat",
     "kb_get_state_flat", "kb_state_size", "kb_num_cols", "kb_camera_cols", "kb_eval_cost", "kb_build",
-    "kb_set_constant_conditioner", "kb_set_conditioner", "kb_solve", "kb_get_rhs", "kb_rhs_jtj_rhs", "kb_apply_update", "kb_revert", "kb_get_normal_blocks",
+    "kb_set_constant_conditioner", "kb_set_conditioner", "kb_solve", "kb_get_rhs", "kb_rhs_jtj_rhs", "kb_reprojection_error_stats", "kb_apply_update", "kb_revert", "kb_get_normal_blocks",
     "kb_optimize", "kb_get_trace", "kb_run_gn_iterations", "kb_gn_prepare", "kb_gn_launch", "kb_build_kernel_stats",
     "kb_build_kernel_name", "kb_comm_get_unique_id", "kb_gn_pass_times", "kb_append_frames", "kb_drop_last_frames", "kb_optimize_marginal", "kb_optimize_marginal_analyze",
     "kb_comm_init", "kb_comm_init_local", "kb_comm_direct", "kb_xar_export", "kb_xar_test", "kb_selftest_mfma", "kb_solve_marginal", "kb_analyze_marginal",
@@ -122,6 +122,7 @@ def lib():
         L.kb_solve.argtypes = [C.c_void_p, dp, C.POINTER(C.c_int)]
         L.kb_get_rhs.argtypes = [C.c_void_p, dp]
         L.kb_rhs_jtj_rhs.argtypes = [C.c_void_p, dp]
+        L.kb_reprojection_error_stats.argtypes = [C.c_void_p, dp]
         L.kb_apply_update.argtypes = [C.c_void_p, dp, dp]
         L.kb_get_normal_blocks.argtypes = [C.c_void_p, dp, dp, dp, dp, dp, dp]
         L.kb_optimize.argtypes = [C.c_void_p, C.POINTER(OptimizerOptions), C.POINTER(Solution)]
@@ -312,6 +313,13 @@ class Solver:
         v = C.c_double()
         _check(lib().kb_rhs_jtj_rhs(self.h, C.byref(v)))
         return v.value
+
+    def reprojection_error_stats(self):
+        """kb_reprojection_error_stats: per camera [n, mean_u, mean_v, std_u, std_v, rmse] of the current state
+        (CameraCalibrator.hpp:368-411; rmse = |sum e| / sqrt(n) as the reference prints it)"""
+        out = np.zeros((self.prob.n_cams, 6))
+        _check(lib().kb_reprojection_error_stats(self.h, _d(out)))
+        return out
 
     def apply_update(self, dx):
         dX = C.c_double()

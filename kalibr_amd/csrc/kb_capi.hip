@@ -129,6 +129,8 @@ struct kb_handle {
   size_t pcg_F = 0, rjr_F = 0, cond_n = 0;  // frame count / columns the lazily allocated buffers are sized for
   double* ximg_part = nullptr;  // sharded + xexp: this rank's partial image (all-reduced into d.simg)
   std::vector<void*> xar_opened;  // peers' exchange regions mapped by IPC handles (closed by kb_destroy)
+  bool xar_failed = false;        // a k_xar wait of this rank timed out (comm_check): agreed on at the next loop start
+  double* xar_agree_buf = nullptr;  // [2]: this rank's failure flag | the sum over the ranks
   bool buildp_wide = false;  // k_buildp<.., MW = 8> (multi-model rigs with <= 8 waves per block)
   double* rjr = nullptr;     // [F + 1] kb_rhs_jtj_rhs: per-frame terms | result
   int gn_prepared = -1;      // kb_gn_prepare'd pass count, consumed by kb_gn_launch (-1: nothing prepared; every
@@ -199,32 +201,33 @@ struct kb_handle {
   }
 };
 
-// mb: Schur tiles per wave of k_build (1 | 4 | 7), or per frame wave of k_buildp (5: 2 frame waves | 7: 4) when pipe
-template <bool GN, unsigned MM>
-static const void* build_fn(int mb, bool pipe, bool wide) {
-  constexpr int MWN = kBuildpMaxCams + 4;
-  if constexpr (__builtin_popcount(MM) >= 2) {  // multi-model view roles: the spill-free 8-wave variant
-    if (pipe && wide) return mb == 5 ? (const void*)k_buildp<5, GN, MM, 8> : (const void*)k_buildp<7, GN, MM, 8>;
-  }
-  if (pipe) return mb == 5 ? (const void*)k_buildp<5, GN, MM, MWN> : (const void*)k_buildp<7, GN, MM, MWN>;
-  return mb == 1 ? (const void*)k_build<1, GN, MM> : mb == 4 ? (const void*)k_build<4, GN, MM>
-                                                             : (const void*)k_build<7, GN, MM>;
-}
+// The build kernels of each camera-model set live in their own translation unit (kb_build_tu.hip, -DKB_TU_ID=id):
+// kb_build_fn_<id>(gn, mb, pipe, wide) returns the k_build / k_buildp instantiation (mb: Schur tiles per wave of
+// k_build 1 | 4 | 7, or per frame wave of k_buildp 5 | 7).
+#define KB_BUILD_TU_DECL(id) const void* kb_build_fn_##id(bool gn, int mb, bool pipe, bool wide);
+KB_BUILD_TU_DECL(0)
+KB_BUILD_TU_DECL(1)
+KB_BUILD_TU_DECL(2)
+KB_BUILD_TU_DECL(3)
+KB_BUILD_TU_DECL(4)
+KB_BUILD_TU_DECL(5)
+KB_BUILD_TU_DECL(6)
+KB_BUILD_TU_DECL(7)
+KB_BUILD_TU_DECL(8)
 
 // Build kernel for the rig's camera-model set `mm` (bit m = model m present).
 template <bool GN>
 static const void* pick_build(int mb, unsigned mm, bool pipe, bool wide) {
   switch (mm) {
-    case 1u << KB_PINHOLE_RADTAN: return build_fn<GN, 1u << KB_PINHOLE_RADTAN>(mb, pipe, wide);
-    case 1u << KB_OMNI_RADTAN: return build_fn<GN, 1u << KB_OMNI_RADTAN>(mb, pipe, wide);
-    case 1u << KB_EUCM: return build_fn<GN, 1u << KB_EUCM>(mb, pipe, wide);
-    case 1u << KB_OMNI: return build_fn<GN, 1u << KB_OMNI>(mb, pipe, wide);
-    case 1u << KB_DS: return build_fn<GN, 1u << KB_DS>(mb, pipe, wide);
-    case 1u << KB_PINHOLE_EQUI: return build_fn<GN, 1u << KB_PINHOLE_EQUI>(mb, pipe, wide);
-    case 1u << KB_PINHOLE_FOV: return build_fn<GN, 1u << KB_PINHOLE_FOV>(mb, pipe, wide);
-    case (1u << KB_OMNI_RADTAN) | (1u << KB_EUCM):
-      return build_fn<GN, (1u << KB_OMNI_RADTAN) | (1u << KB_EUCM)>(mb, pipe, wide);
-    default: return build_fn<GN, kMmAll>(mb, pipe, wide);
+    case 1u << KB_PINHOLE_RADTAN: return kb_build_fn_0(GN, mb, pipe, wide);
+    case 1u << KB_OMNI_RADTAN: return kb_build_fn_1(GN, mb, pipe, wide);
+    case 1u << KB_EUCM: return kb_build_fn_2(GN, mb, pipe, wide);
+    case 1u << KB_OMNI: return kb_build_fn_3(GN, mb, pipe, wide);
+    case 1u << KB_DS: return kb_build_fn_4(GN, mb, pipe, wide);
+    case 1u << KB_PINHOLE_EQUI: return kb_build_fn_5(GN, mb, pipe, wide);
+    case 1u << KB_PINHOLE_FOV: return kb_build_fn_6(GN, mb, pipe, wide);
+    case (1u << KB_OMNI_RADTAN) | (1u << KB_EUCM): return kb_build_fn_7(GN, mb, pipe, wide);
+    default: return kb_build_fn_8(GN, mb, pipe, wide);
   }
 }
 
@@ -296,8 +299,11 @@ static void unprepare(kb_handle* h) { h->gn_prepared = -1; }
 static bool sharded(const kb_handle* h) { return h->comm || h->lg; }
 
 // a k_xar wait that timed out (a peer rank never published its partial image): the pass results are void
-static int comm_check(const KbCtrl& c) {
-  return c.comm_err ? fail("direct all-reduce (k_xar): a peer rank did not arrive within 2 s") : 0;
+static int comm_check(kb_handle* h, const KbCtrl& c) {
+  if (!c.comm_err) return 0;
+  h->xar_failed = true;  // the next loop start agrees with the other ranks on leaving the direct path
+  return fail("direct all-reduce (k_xar): a peer rank did not arrive within the wait bound (KB_XAR_TIMEOUT_MS); the "
+              "handle switches to the RCCL collective at its next loop start");
 }
 
 // one collective of the in-process group: every member publishes its send buffer and an event, waits for all
@@ -848,6 +854,13 @@ int kb_drop_last_frames(kb_handle* h, int32_t n_frames) {
   KB_HIP(hipSetDevice(h->device));
   const int F1 = h->F - n_frames, V1 = h->frame_v0[F1], NC1 = (int)h->vo_host[V1];
   if (!build_lds_fits(h, F1)) return fail("kb_drop_last_frames: build-kernel LDS budget exceeded for this frame count");
+  {  // fewer frames can mean more build blocks: the partial rows grow first, so a failure leaves the handle as it was
+    const int g1 = gframes_for(h, F1), nblk1 = (F1 + g1 - 1) / g1;
+    if (nblk1 > h->part_rows) {
+      if (regrow(h, &h->d.part, (size_t)nblk1 * h->d.Wr, 0)) return -1;
+      h->part_rows = nblk1;
+    }
+  }
   h->F = F1;
   h->V = V1;
   h->NC = NC1;
@@ -1387,6 +1400,47 @@ int kb_get_normal_blocks(kb_handle* h, double* Hff, double* Hfc, double* gf, dou
   return 0;
 }
 
+int kb_reprojection_error_stats(kb_handle* h, double* out) {
+  if (!h || !out) return fail("kb_reprojection_error_stats: null");
+  if (!h->uploaded) return fail("kb_reprojection_error_stats: no observations");
+  KB_HIP(hipSetDevice(h->device));
+  const int N = h->N, V = h->V;
+  double* buf = nullptr;  // vpart [V][3] | pass-one sums [N][3] (+ [N][3] over ranks) | pass-two sums (same)
+  const size_t nv = 3 * (size_t)std::max(V, 1), ns = 3 * (size_t)N;
+  KB_HIP(hipMalloc(&buf, sizeof(double) * (nv + 4 * ns)));
+  double *vpart = buf, *s1 = buf + nv, *s1r = s1 + ns, *s2 = s1r + ns, *s2r = s2 + ns;
+  auto pass = [&](const double* sums, double* o, double* orr) -> int {
+    hipLaunchKernelGGL(k_rstats, dim3((V + 3) / 4), dim3(256), 0, h->stream, h->d, sums, vpart);
+    hipLaunchKernelGGL(k_rstats_red, dim3(N), dim3(256), 0, h->stream, h->d, vpart, o);
+    KB_HIP(hipGetLastError());
+    if (!sharded(h)) return hipMemcpyAsync(orr, o, sizeof(double) * ns, hipMemcpyDeviceToDevice, h->stream) == hipSuccess ? 0 : -1;
+    return coll_allreduce(h, o, orr, ns);  // the ranks' frames: counts and sums over all of them
+  };
+  std::vector<double> a(ns), b(ns);
+  int rc = V > 0 ? pass(nullptr, s1, s1r) : 0;
+  if (!rc && V > 0) rc = pass(s1r, s2, s2r);
+  if (!rc && V > 0) {
+    if (hipMemcpyAsync(a.data(), s1r, sizeof(double) * ns, hipMemcpyDeviceToHost, h->stream) != hipSuccess ||
+        hipMemcpyAsync(b.data(), s2r, sizeof(double) * ns, hipMemcpyDeviceToHost, h->stream) != hipSuccess)
+      rc = -1;
+  }
+  if (hipStreamSynchronize(h->stream) != hipSuccess) rc = -1;
+  hipFree(buf);
+  if (rc) return fail("kb_reprojection_error_stats: device pass failed");
+  // per camera [n, mean (2), sample std (2, N - 1), "RMSE" = |sum e| / sqrt(n)] (CameraCalibrator.hpp:378-410)
+  for (int c = 0; c < N; ++c) {
+    const double n = V > 0 ? a[3 * c] : 0.0;
+    double* o = out + 6 * c;
+    o[0] = n;
+    o[1] = n > 0 ? a[3 * c + 1] / n : 0.0;
+    o[2] = n > 0 ? a[3 * c + 2] / n : 0.0;
+    o[3] = n > 1 ? std::sqrt(b[3 * c + 1] / (n - 1.0)) : 0.0;
+    o[4] = n > 1 ? std::sqrt(b[3 * c + 2] / (n - 1.0)) : 0.0;
+    o[5] = n > 0 ? std::sqrt(a[3 * c + 1] * a[3 * c + 1] + a[3 * c + 2] * a[3 * c + 2]) / std::sqrt(n) : 0.0;
+  }
+  return 0;
+}
+
 int kb_rhs_jtj_rhs(kb_handle* h, double* out) {
   if (!h || !out) return fail("kb_rhs_jtj_rhs: null");
   if (!h->uploaded) return fail("kb_rhs_jtj_rhs: no observations");
@@ -1594,8 +1648,27 @@ static int finish_pass(kb_handle* h, int policy) {
   return 0;
 }
 
+// a loop start on a rank of a direct all-reduce group: the ranks agree (a sum over the collective, so every rank
+// runs it whatever its own outcome) whether any of them saw a k_xar wait time out since the last loop start; if one
+// did, every rank leaves the direct path for the collective for good.  The flag counters of the ranks may have
+// drifted apart in the failed batch (a failing rank skips its remaining passes), so the direct path is not resumed.
+static void xar_uninstall(kb_handle* h);
+static int xar_agree(kb_handle* h) {
+  if (!sharded(h) || !h->d.xar) return 0;
+  const double mine = h->xar_failed ? 1.0 : 0.0;
+  double sum = 0.0;
+  KB_HIP(hipMemcpyAsync(h->xar_agree_buf, &mine, sizeof(double), hipMemcpyHostToDevice, h->stream));
+  if (coll_allreduce(h, h->xar_agree_buf, h->xar_agree_buf + 1, 1)) return -1;
+  KB_HIP(hipMemcpyAsync(&sum, h->xar_agree_buf + 1, sizeof(double), hipMemcpyDeviceToHost, h->stream));
+  KB_HIP(hipStreamSynchronize(h->stream));
+  if (sum > 0.0) xar_uninstall(h);
+  h->xar_failed = false;
+  return 0;
+}
+
 static int loop_start(kb_handle* h, const KbOpts& o) {
   // evaluateError on the start state (Optimizer2.cpp:192-196), optimizationStarting, first prelude
+  if (xar_agree(h)) return -1;
   unprepare(h);
   h->sys_valid = false;  // the loop's passes overwrite g_c (and skip the frame-block stores when GN fused)
   if (launch_cost(h, 0)) return -1;
@@ -1625,12 +1698,12 @@ int kb_optimize(kb_handle* h, const kb_optimizer_options* opts, kb_solution* out
     passes += n;
     KB_HIP(hipMemcpyAsync(&ctrl, h->d.ctrl, sizeof(KbCtrl), hipMemcpyDeviceToHost, h->stream));
     KB_HIP(hipStreamSynchronize(h->stream));
-    if (comm_check(ctrl)) return -1;
+    if (comm_check(h, ctrl)) return -1;
     if (ctrl.done) break;
   }
   if (finish_pass(h, opts->policy)) return -1;
   KB_HIP(hipMemcpy(&ctrl, h->d.ctrl, sizeof(KbCtrl), hipMemcpyDeviceToHost));
-  if (comm_check(ctrl)) return -1;
+  if (comm_check(h, ctrl)) return -1;
   h->cur = ctrl.cur;
   out->J_start = ctrl.J_start;
   out->J_final = ctrl.p_J;
@@ -1708,6 +1781,7 @@ static int optimize_marginal(kb_handle* h, const kb_optimizer_options* opts, con
     passes += n;
     KB_HIP(hipMemcpyAsync(&ctrl, h->d.ctrl, sizeof(KbCtrl), hipMemcpyDeviceToHost, h->stream));
     KB_HIP(hipStreamSynchronize(h->stream));
+    if (comm_check(h, ctrl)) return -1;
     if (ctrl.done) break;
   }
   if (finish_pass(h, kPolicyMarginal)) return -1;
@@ -1722,6 +1796,7 @@ static int optimize_marginal(kb_handle* h, const kb_optimizer_options* opts, con
     if (enqueue_marginal(h, &un, 0, ainf, asv_out, aV_out)) return -1;
   }
   KB_HIP(hipStreamSynchronize(h->stream));
+  if (comm_check(h, ctrl)) return -1;
   if (analyze) marg_info(ainf, ainfo);
   h->cur = ctrl.cur;
   out->J_start = ctrl.J_start;
@@ -1792,6 +1867,7 @@ int kb_gn_prepare(kb_handle* h, int32_t n_iter) {
   if (ensure_trace(h, 64)) return -1;
   // GN, convergence tests disabled (thresholds -1 keep (dX > eps && |dJ| > eps) true)
   KbOpts o{1, 0x3fffffff, 0.0, -1.0, -1.0};
+  if (xar_agree(h)) return -1;  // before the captures (leaving the direct path drops the graphs)
   h->gn_graph = graph_ok(h, 1);
   if (h->gn_graph) {
     // up to kGnOneGraph passes run as one graph with the loop's end (the last step's back-substitution and k_post)
@@ -1867,7 +1943,7 @@ int kb_gn_launch(kb_handle* h, int32_t n_iter, double* seconds) {
   KbCtrl ctrl{};
   KB_HIP(hipMemcpy(&ctrl, h->d.ctrl, sizeof(KbCtrl), hipMemcpyDeviceToHost));
   h->cur = ctrl.cur;
-  if (comm_check(ctrl)) return -1;
+  if (comm_check(h, ctrl)) return -1;
   if (ctrl.iterations != n_iter) return fail("kb_gn_launch: linear solver failures during the timed passes");
   return 0;
 }
@@ -2082,6 +2158,14 @@ static bool xar_env_on() {
   return !(e && e[0] == '0');
 }
 
+// KB_DIRECT_AR=force (tests on a one-GPU box only): an in-process group of two members on ONE device takes the direct
+// path too.  The product rule is one rank per device; two members sharing a device rely on the hardware queues
+// running both members' k_xar launches at once (measured reliable for two members, not for three).
+static bool xar_env_force() {
+  const char* e = std::getenv("KB_DIRECT_AR");
+  return e && !std::strcmp(e, "force");
+}
+
 // this rank's exchange region: flags + two image halves, zeroed (the base of its own allocation: IPC-exportable)
 static int xar_region(kb_handle* h, double** out) {
   return h->alloc(out, (size_t)kXarFlagDoubles + 2 * (size_t)h->d.img_n);
@@ -2090,6 +2174,13 @@ static int xar_region(kb_handle* h, double** out) {
 static int xar_install(kb_handle* h, double* own, const std::vector<double*>& peers) {
   double** tab = nullptr;
   if (h->alloc(&tab, peers.size())) return -1;
+  if (!h->xar_agree_buf && h->alloc(&h->xar_agree_buf, 2)) return -1;
+  h->d.xar_timeout = kXarTimeoutTicks;
+  if (const char* e = std::getenv("KB_XAR_TIMEOUT_MS")) {  // the wait bound of k_xar (ms; s_memrealtime runs at 100 MHz)
+    const long ms = std::atol(e);
+    if (ms > 0) h->d.xar_timeout = 100000ull * (unsigned long long)ms;
+  }
+  h->xar_failed = false;
   KB_HIP(hipMemcpyAsync(tab, peers.data(), sizeof(double*) * peers.size(), hipMemcpyHostToDevice, h->stream));
   KB_HIP(hipStreamSynchronize(h->stream));
   h->d.xar_buf = own;
@@ -2133,9 +2224,12 @@ static int xar_selftest_check(kb_handle* h, int& ok) {
   return 0;
 }
 
-// multi-process ranks (RCCL communicator up): export this rank's region as an IPC handle, all-gather the handles,
-// map the peers', self-test; every step's outcome is agreed over the communicator (all ranks enable the direct path
-// or none does), every rank runs the same collectives whatever its own outcome
+// multi-process ranks (RCCL communicator up): export this rank's region as an IPC handle, all-gather the handles and
+// the ranks' PCI locations, map the peers', self-test; every step's outcome is agreed over the communicator (all ranks
+// enable the direct path or none does), and every rank runs the same collectives whatever its own outcome: a local
+// failure only clears `ok` (the exchange scratch is the handle's image buffer, so nothing is allocated here before the
+// collectives).  The direct path needs one rank per device (distinct PCI locations); RCCL refuses two ranks on one
+// device anyway, and a shared device would leave k_xar's co-scheduling to the hardware queues.
 static int xar_setup_rccl(kb_handle* h) {
   if (!h->xexp || h->nranks < 2 || h->nranks > kXMaxRanksDev) return 0;
   int ok = xar_env_on() ? 1 : 0;
@@ -2143,26 +2237,37 @@ static int xar_setup_rccl(kb_handle* h) {
   hipIpcMemHandle_t mh;
   std::memset(&mh, 0, sizeof(mh));
   if (ok && xar_region(h, &own)) ok = 0;
-  if (ok && hipIpcGetMemHandle(&mh, own) != hipSuccess) {
-    hipGetLastError();
+  if (ok && hipIpcGetMemHandle(&mh, own) != hipSuccess) ok = 0;
+  int pci[3] = {-1, -1, -1};
+  if (hipDeviceGetAttribute(&pci[0], hipDeviceAttributePciDomainID, h->device) != hipSuccess ||
+      hipDeviceGetAttribute(&pci[1], hipDeviceAttributePciBusId, h->device) != hipSuccess ||
+      hipDeviceGetAttribute(&pci[2], hipDeviceAttributePciDeviceId, h->device) != hipSuccess)
     ok = 0;
-  }
+  hipGetLastError();
+  const int loc = ((pci[0] & 0xffff) << 16) | ((pci[1] & 0xff) << 8) | (pci[2] & 0xff);
   constexpr size_t kSlot = sizeof(hipIpcMemHandle_t) + 8;
-  char* dx = nullptr;  // the exchange scratch (handle-owned: freed by kb_destroy on every return path)
-  if (h->alloc(&dx, kSlot * (h->nranks + 1))) return -1;
+  static_assert(kSlot * (kXMaxRanksDev + 1) <= 8 * 16 * 16 * 15, "exchange scratch within the smallest C > 64 image");
+  char* dx = reinterpret_cast<char*>(h->d.simg);  // scratch: the image buffer (rewritten by every pass)
   std::vector<char> slot(kSlot, 0);
   std::memcpy(slot.data(), &mh, sizeof(mh));
   std::memcpy(slot.data() + sizeof(mh), &ok, sizeof(int));
-  KB_HIP(hipMemcpyAsync(dx, slot.data(), kSlot, hipMemcpyHostToDevice, h->stream));
+  std::memcpy(slot.data() + sizeof(mh) + sizeof(int), &loc, sizeof(int));
+  if (hipMemcpyAsync(dx, slot.data(), kSlot, hipMemcpyHostToDevice, h->stream) != hipSuccess) ok = 0;
   KB_NCCL(ncclAllGather(dx, dx + kSlot, kSlot, ncclChar, h->comm, h->stream));
-  std::vector<char> all(kSlot * h->nranks);
-  KB_HIP(hipMemcpyAsync(all.data(), dx + kSlot, all.size(), hipMemcpyDeviceToHost, h->stream));
-  KB_HIP(hipStreamSynchronize(h->stream));
+  std::vector<char> all(kSlot * h->nranks, 0);
+  if (hipMemcpyAsync(all.data(), dx + kSlot, all.size(), hipMemcpyDeviceToHost, h->stream) != hipSuccess ||
+      hipStreamSynchronize(h->stream) != hipSuccess)
+    ok = 0;
+  hipGetLastError();
   std::vector<double*> peers(h->nranks, nullptr);
+  std::vector<int> locs(h->nranks, 0);
   for (int q = 0; q < h->nranks && ok; ++q) {
     int okq = 0;
     std::memcpy(&okq, all.data() + kSlot * q + sizeof(mh), sizeof(int));
+    std::memcpy(&locs[q], all.data() + kSlot * q + sizeof(mh) + sizeof(int), sizeof(int));
     if (!okq) ok = 0;
+    for (int r = 0; r < q && ok; ++r)
+      if (locs[r] == locs[q]) ok = 0;  // two ranks on one device: the collective, not the direct path
   }
   for (int q = 0; q < h->nranks && ok; ++q) {
     if (q == h->rank) {
@@ -2180,14 +2285,15 @@ static int xar_setup_rccl(kb_handle* h) {
     h->xar_opened.push_back(p);
     peers[q] = (double*)p;
   }
-  auto agree = [&](int v) -> int {  // min over ranks
+  auto agree = [&](int v) -> int {  // min over ranks (the collective runs whatever the copies did)
     int* di = (int*)dx;
-    if (hipMemcpyAsync(di, &v, sizeof(int), hipMemcpyHostToDevice, h->stream) != hipSuccess) return 0;
-    if (ncclAllReduce(di, di, 1, ncclInt32, ncclMin, h->comm, h->stream) != ncclSuccess) return 0;
     int r = 0;
-    if (hipMemcpyAsync(&r, di, sizeof(int), hipMemcpyDeviceToHost, h->stream) != hipSuccess) return 0;
-    if (hipStreamSynchronize(h->stream) != hipSuccess) return 0;
-    return r;
+    if (hipMemcpyAsync(di, &v, sizeof(int), hipMemcpyHostToDevice, h->stream) != hipSuccess) v = 0;
+    if (ncclAllReduce(di, di, 1, ncclInt32, ncclMin, h->comm, h->stream) != ncclSuccess) return 0;
+    if (hipMemcpyAsync(&r, di, sizeof(int), hipMemcpyDeviceToHost, h->stream) != hipSuccess) r = 0;
+    if (hipStreamSynchronize(h->stream) != hipSuccess) r = 0;
+    hipGetLastError();
+    return std::min(r, v);
   };
   ok = agree(ok);
   if (ok && xar_install(h, own, peers)) ok = 0;
@@ -2198,15 +2304,15 @@ static int xar_setup_rccl(kb_handle* h) {
     ok = agree(t);
   }
   if (!ok && h->d.xar) xar_uninstall(h);
+  hipGetLastError();
   return 0;
 }
 
 // in-process groups: the members' regions directly (same process, peer access enabled by kb_comm_init_local).  The
-// members' k_xar launches must run concurrently, which separate devices guarantee.  Members sharing one device depend
-// on the hardware queues co-scheduling them while the group's other collectives (host barriers, cross-stream event
-// waits) hold the members' streams in step: measured reliable for 2 members, not for 3 (a k_xar that waits in vain
-// times out), so a shared device takes the direct path at 2 members only.  The self-test, run on every member's
-// stream before any member syncs, proves the co-scheduling before the group relies on it.
+// members' k_xar launches must run concurrently, which separate devices guarantee: the direct path needs one member
+// per device, and a group with two members on one device keeps the copies (KB_DIRECT_AR=force lets a two-member group
+// on one device take it, for the tests on a one-GPU box).  The self-test, run on every member's stream before any
+// member syncs, proves the exchange before the group relies on it.
 static void xar_setup_local(kb_handle* const* hs, int n) {
   if (n < 2 || n > kXMaxRanksDev || !xar_env_on()) return;
   bool distinct = true;
@@ -2214,7 +2320,7 @@ static void xar_setup_local(kb_handle* const* hs, int n) {
     if (!hs[r]->xexp) return;
     for (int q = 0; q < r; ++q) distinct = distinct && hs[q]->device != hs[r]->device;
   }
-  if (!distinct && n > 2) return;
+  if (!distinct && !(xar_env_force() && n == 2)) return;
   std::vector<double*> regs(n, nullptr);
   for (int r = 0; r < n; ++r)
     if (hipSetDevice(hs[r]->device) != hipSuccess || xar_region(hs[r], &regs[r])) return;

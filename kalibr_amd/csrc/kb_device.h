@@ -25,7 +25,7 @@ struct KbCtrl {
   int iterations, failed_iterations, max_iterations, policy, n_trace, passes;
   int pending;  // a pass ran its solve: its accept/revert + the next prelude are still to apply
   int have_dx;  // GN fused passes: the last solve's dx is still to apply (by the next build or the finish)
-  int comm_err;  // k_xar: a peer rank did not arrive within kXarTimeoutTicks (the host fails the call)
+  int comm_err;  // k_xar: a peer rank did not arrive within the wait bound (the pass batch ends, the host fails the call)
   double J, p_J, J_start, deltaX, deltaJ, eps_x, eps_j;
   double pol_J, pol_pJ, last_succ, lambda, mu;
   double dxdx, dxrhs;
@@ -40,7 +40,7 @@ constexpr int kColsumRows = 8;  // stage-1 row splits of the block partial reduc
 constexpr int kXarBlocks = 32;        // k_xar blocks (each sums one chunk of the image over the ranks)
 constexpr int kXMaxRanksDev = 64;     // k_xar ranks (peer table in LDS)
 constexpr int kXarFlagDoubles = 64;   // flag area of an exchange region (kXarBlocks u64, padded to 512 B)
-constexpr unsigned long long kXarTimeoutTicks = 200000000ull;  // 2 s of s_memrealtime (100 MHz)
+constexpr unsigned long long kXarTimeoutTicks = 1000000000ull;  // default wait bound: 10 s of s_memrealtime (100 MHz)
 
 // k_marg (marginal truncated-SVD camera solve, aslam_incremental_calibration LinearSolver)
 constexpr int kMargThreads = 1024;
@@ -130,6 +130,7 @@ struct KbDev {
   int xar;
   double* xar_buf;
   double* const* xar_peers;
+  unsigned long long xar_timeout;  // k_xar's wait bound in s_memrealtime ticks (KB_XAR_TIMEOUT_MS, default kXarTimeoutTicks)
   // per-pass timing query only (kb_gn_pass_times): [0] arrival counter | [1 ..] s_memrealtime (100 MHz) at the start of
   // each pass's build kernel (block 0), null otherwise
   unsigned long long* pass_ts;

@@ -2151,6 +2151,12 @@ __global__ void __launch_bounds__(64 * kColsum1Waves) k_colsum1(KbDev d, int gat
 // Work column x: [0, C] = the g_c | cost columns, then every column from N * 136 on (S, b, non-PD, max|dx_f|).
 // The identity padding and lambda^2 are k_solve's (they must not be summed over ranks).
 // ---------------------------------------------------------------------------------------------
+// a store of the direct all-reduce's exchange region: system scope (a write-through to memory, acknowledged there)
+__device__ __forceinline__ void xar_store(double* p, double v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __global__ void __launch_bounds__(64 * kColsum1Waves) k_colsumx(KbDev d, int gate) {
   KbCtrl* c = d.ctrl;
   __shared__ double part[kColsum1Waves][64];
@@ -2193,27 +2199,36 @@ __global__ void __launch_bounds__(64 * kColsum1Waves) k_colsumx(KbDev d, int gat
   const int ntz = kTileSz * nb * (nb + 1) / 2, aux = ntz;
   const int Wt = C * (C + 1) / 2, o = N * 136;
   double* img = d.ximg;
-  if (d.xar) {  // direct all-reduce: the partial image of launch v = flags + 1 goes to region half v & 1 (k_xar)
+  const bool sys = d.xar != 0;
+  if (sys) {  // direct all-reduce: the partial image of launch v = flags + 1 goes to region half v & 1 (k_xar)
     const unsigned long long f0 = reinterpret_cast<const unsigned long long*>(d.xar_buf)[0];
     img = d.xar_buf + kXarFlagDoubles + (size_t)((f0 + 1) & 1) * d.img_n;
   }
+  // the exchange region is written with system-scope stores: each is acknowledged only once it is in memory, past
+  // every L2, so when this kernel has completed the peers' system-scope loads (k_xar) see it, whatever any L2 holds
+  auto put = [&](int i, double v) {
+    if (sys)
+      xar_store(img + i, v);
+    else
+      img[i] = v;
+  };
   if (e < C) {
-    img[aux + e] = t;  // g_c
+    put(aux + e, t);  // g_c
   } else if (e == C) {
-    img[aux + n16] = t;  // cost
+    put(aux + n16, t);  // cost
   } else if (e < o + Wt) {
     const int u = e - o, a = cidx_col(u, C), b = u - (a * C - a * (a - 1) / 2) + a;  // a <= b
-    img[tidx(b, a)] = t;
-    if (a != b && (a >> 4) == (b >> 4)) img[tidx(a, b)] = t;  // diagonal tiles are whole
+    put(tidx(b, a), t);
+    if (a != b && (a >> 4) == (b >> 4)) put(tidx(a, b), t);  // diagonal tiles are whole
   } else if (e < o + Wt + C) {
     const int j = e - o - Wt;
-    img[tidx(C, j)] = t;  // b as row C
-    if ((j >> 4) == (C >> 4)) img[tidx(j, C)] = t;
+    put(tidx(C, j), t);  // b as row C
+    if ((j >> 4) == (C >> 4)) put(tidx(j, C), t);
   } else if (e < d.Wp) {
-    img[aux + C] = t;  // non-PD frame blocks
+    put(aux + C, t);  // non-PD frame blocks
   } else {
     const int r = e - d.Wp;  // one max column per rank: this rank's max in its own slot, zero elsewhere
-    img[aux + n16 + 1 + r] = (d.gn_fused && r == d.rank) ? m : 0.0;
+    put(aux + n16 + 1 + r, (d.gn_fused && r == d.rank) ? m : 0.0);
   }
 }
 
@@ -2225,7 +2240,11 @@ __global__ void __launch_bounds__(64 * kColsum1Waves) k_colsumx(KbDev d, int gat
 // rank order, reading the peers' regions over xGMI (system-scope loads), into d.simg.  Every rank sums the same
 // values in the same order: bitwise-identical images on all ranks, and identical to the in-process group's rank-order
 // sums.  Reuse: a rank overwrites half v & 1 at launch v + 2, which needs every peer at v + 1, i.e. done reading v.
-// A peer that never arrives ends the wait after kXarTimeoutTicks (2 s): ctrl->comm_err, the host fails the call.
+// Ordering: k_colsumx wrote the partial image with system-scope stores and has completed (same stream), so the image is
+// in memory before the flag's system-scope release; a peer reads the halves with system-scope loads only after its
+// system-scope acquire of that flag.  A peer that never arrives ends the wait after d.xar_timeout ticks
+// (KB_XAR_TIMEOUT_MS, default 10 s): ctrl->comm_err and ctrl->done, so every later kernel of the enqueued passes
+// skips, and the host fails the call and agrees with the other ranks on the RCCL collective from then on.
 // ---------------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_xar(KbDev d, int gate) {
   KbCtrl* c = d.ctrl;
@@ -2240,7 +2259,6 @@ __global__ void __launch_bounds__(256) k_xar(KbDev d, int gate) {
     const unsigned long long v = own[b] + 1;  // only block b of this rank writes slot b
     sv = v;
     err = 0;
-    __threadfence_system();  // this rank's partial image (k_colsumx, earlier on the stream) out of L2
     __hip_atomic_store(own + b, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   __syncthreads();
@@ -2249,7 +2267,7 @@ __global__ void __launch_bounds__(256) k_xar(KbDev d, int gate) {
     const unsigned long long* pf = reinterpret_cast<const unsigned long long*>(pp[tid]) + b;
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     while (__hip_atomic_load(pf, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < v) {
-      if (__builtin_amdgcn_s_memrealtime() - t0 > kXarTimeoutTicks) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > d.xar_timeout) {
         err = 1;
         break;
       }
@@ -2279,14 +2297,17 @@ __global__ void __launch_bounds__(256) k_xar(KbDev d, int gate) {
     }
     d.simg[i] = s;
   }
-  if (tid == 0 && err) c->comm_err = 1;
+  if (tid == 0 && err) {  // the pass results are void: the rest of the enqueued passes skips (every kernel checks done)
+    c->comm_err = 1;
+    c->done = 1;
+  }
 }
 
 // k_xar self-test input: rank r's image half `half` = (r + 1) / 8 + (i % 7) (exact sums in any order)
 __global__ void __launch_bounds__(256) k_xar_fill(KbDev d, int half) {
   double* img = d.xar_buf + kXarFlagDoubles + (size_t)half * d.img_n;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < d.img_n; i += gridDim.x * blockDim.x)
-    img[i] = (d.rank + 1) * 0.125 + (double)(i % 7);
+    xar_store(img + i, (d.rank + 1) * 0.125 + (double)(i % 7));  // the stores k_colsumx uses
 }
 
 // psum_local[e] = sum_r part8[r][e] (fixed order)
@@ -5207,6 +5228,75 @@ __global__ void __launch_bounds__(256) k_reduce_cost(KbDev d) {
 }
 
 // red = fixed-order reduction of the all-gathered per-rank [cost, dx.dx, dx.rhs] (sum) and max|dx| (max)
+// ---------------------------------------------------------------------------------------------
+// Reprojection-error statistics of the current state (CameraCalibrator.hpp:368-411, printed per camera by
+// CalibrateCameras.cpp:318): e = y - yhat of every term (ReprojectionError::getPredictedMeasurement,
+// ReprojectionError.hpp(impl):98-106).  Two passes as the reference's: k_rstats with sums == null gives per view
+// [count, sum e_u, sum e_v]; with the per-camera sums of pass one it gives [count, sum (e_u - mean_u)^2,
+// sum (e_v - mean_v)^2] (one wave per view, fixed-order wave sums); k_rstats_red sums a camera's views in a fixed
+// order (one block per camera).
+// ---------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_rstats(KbDev d, const double* sums, double* vpart) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int v = blockIdx.x * 4 + wave;
+  if (v >= d.V) return;  // wave-uniform
+  const double* s = d.state + (size_t)d.ctrl->cur * d.S;
+  const int f = d.view_frame[v], cam = d.view_cam[v];
+  double R[9], t[3];
+  cam_from_state(d, s, cam, s + d.off_frame + 7 * f, R, t);
+  const int model = cam_arg(d.model, cam);
+  const double* intr = s + cam * KB_MAX_INTR;
+  double mu = 0.0, mv = 0.0;
+  if (sums) {
+    const double n = sums[3 * cam];
+    mu = sums[3 * cam + 1] / n;
+    mv = sums[3 * cam + 2] / n;
+  }
+  const int o0 = d.view_off[v], o1 = d.view_off[v + 1];
+  double a0 = 0.0, a1 = 0.0;
+  for (int k = o0 + lane; k < o1; k += 64) {
+    const int cid = d.cid[k];
+    const double X0 = d.target[3 * cid], X1 = d.target[3 * cid + 1], X2 = d.target[3 * cid + 2];
+    const double p0 = R[0] * X0 + R[1] * X1 + R[2] * X2 + t[0];
+    const double p1 = R[3] * X0 + R[4] * X1 + R[5] * X2 + t[1];
+    const double p2 = R[6] * X0 + R[7] * X1 + R[8] * X2 + t[2];
+    double u, w;
+    project(model, intr, p0, p1, p2, u, w);
+    const double2 yv = d.y[k];
+    const double e0 = yv.x - u, e1 = yv.y - w;
+    if (sums) {
+      a0 += (e0 - mu) * (e0 - mu);
+      a1 += (e1 - mv) * (e1 - mv);
+    } else {
+      a0 += e0;
+      a1 += e1;
+    }
+  }
+  a0 = wave_sum_d(a0);
+  a1 = wave_sum_d(a1);
+  if (lane == 0) {
+    vpart[3 * (size_t)v] = (double)(o1 - o0);
+    vpart[3 * (size_t)v + 1] = a0;
+    vpart[3 * (size_t)v + 2] = a1;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_rstats_red(KbDev d, const double* vpart, double* out) {
+  __shared__ double sh[256];
+  const int cam = blockIdx.x;
+  double a[3] = {0.0, 0.0, 0.0};
+  for (int v = threadIdx.x; v < d.V; v += blockDim.x)
+    if (d.view_cam[v] == cam)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) a[q] += vpart[3 * (size_t)v + q];
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const double r = block_reduce(a[q], sh, false);
+    if (threadIdx.x == 0) out[3 * cam + q] = r;
+    __syncthreads();
+  }
+}
+
 __device__ __forceinline__ void red_gather(const KbDev& d, double* red) {
   red[0] = red[1] = red[2] = red[3] = 0.0;
   for (int r = 0; r < d.nranks; ++r) {
@@ -5270,6 +5360,7 @@ __global__ void k_pol_init(KbDev d, KbOpts o) {
   c->passes = 0;
   c->pending = 0;
   c->have_dx = 0;
+  c->comm_err = 0;  // (the host agreed on the transport at the loop start: a failed direct path is off by now)
 }
 
 // per-call update (kb_apply_update): all DVs from state[cur] -> state[1-cur]

@@ -1494,11 +1494,11 @@ __device__ __forceinline__ void level_products(const SpDev& d, const double* Zl,
 // level, or -- node 0 once no partner is left -- solves X_0 = D_0^-1 R_0.
 // level_step: one node's share, by the `nth` threads of a node group (tid = the thread's index in the group); every
 // thread of the block calls it (act: the group has a node at this level), with the same three block barriers on every
-// path, so that k_sp_deep can run several groups (and several levels) in one block.  L, id, Ui, Uo and sm (Zl | Zr | W,
-// [18][wc] each) are the group's LDS.
+// path, so that k_sp_deep can run several groups (and several levels) in one block.  L, id and sm (Zl | Zr | W,
+// [18][wc] each) are the group's LDS (the couplings Ui, Uo are formed in W, the forward solve's operand).
 template <bool LEAN>  // LEAN: k_sp_deep's 1024-thread block (128 VGPRs): fewer loads in flight, per-row forward solve
 __device__ __forceinline__ void level_step(const SpDev& d, int s, int i, bool act, int tid, int nth, double* L,
-                                           double* id, double* Ui, double* Uo, double* sm) {
+                                           double* id, double* sm) {
   const int m = d.m, wc = 36 + m;
   const int jl = i - s, jr = i + s;
   const bool hl = jl >= 0, hr = jr < d.n;
@@ -1580,12 +1580,10 @@ __device__ __forceinline__ void level_step(const SpDev& d, int s, int i, bool ac
 __global__ void __launch_bounds__(256) k_sp_level(SpDev d, int s) {
   __shared__ double L[NB * NB];
   __shared__ double id[NB];
-  __shared__ double Ui[NB * NB];  // coupling (i - 2s) -> i
-  __shared__ double Uo[NB * NB];  // coupling i -> (i + 2s)
   extern __shared__ __attribute__((aligned(16))) double sm[];  // Zl [18][wc] | Zr [18][wc] | W [18][wc]
   const int i = 2 * s * blockIdx.x;
   if (i >= d.n) return;  // block-uniform
-  level_step<false>(d, s, i, true, threadIdx.x, blockDim.x, L, id, Ui, Uo, sm);
+  level_step<false>(d, s, i, true, threadIdx.x, blockDim.x, L, id, sm);
 }
 
 __global__ void __launch_bounds__(256) k_sp_top(SpDev d) {
@@ -1786,6 +1784,8 @@ __global__ void __launch_bounds__(256) k_sp_back2(SpDev d, int s) {
 // barrier between levels instead of a kernel boundary (the L2 writeback and the launch of every level, and the
 // operands come back from the CU's own cache).  Levels s_deep .. top, then the back substitution top .. s_deep.
 constexpr int kSpDeepGroups = 4;
+// LDS of one k_sp_deep node group, in doubles: L | id | Zl | Zr | W ([18][36 + m] each)
+__host__ __device__ constexpr int kSpDeepPer(int m) { return NB * NB + NB + 3 * NB * (36 + m); }
 constexpr int kSpDeepGT = 128;  // threads per node group: the block keeps the per-level kernels' 256-VGPR budget
 __global__ void __launch_bounds__(kSpDeepGT * kSpDeepGroups) k_sp_deep(SpDev d, int s_deep) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
@@ -1795,16 +1795,14 @@ __global__ void __launch_bounds__(kSpDeepGT * kSpDeepGroups) k_sp_deep(SpDev d, 
   // compiler unroll the strided output loops and hoist their operands (hundreds of spilled VGPRs)
   int nth = kSpDeepGT;
   asm volatile("" : "+s"(nth));
-  const int wc = 36 + d.m, per = 3 * NB * NB + NB + 3 * NB * wc;  // the group's LDS: L | Ui | Uo | id | Zl | Zr | W
+  const int wc = 36 + d.m, per = kSpDeepPer(d.m);  // the group's LDS: L | id | Zl | Zr | W
   double* L = sm + (size_t)g * per;
-  double* Ui = L + NB * NB;
-  double* Uo = Ui + NB * NB;
-  double* id = Uo + NB * NB;
+  double* id = L + NB * NB;
   double* gsm = id + NB;
   int s = s_deep;
   for (;; s *= 2) {
     const int i = 2 * s * g;
-    level_step<true>(d, s, i, i < d.n, tid, nth, L, id, Ui, Uo, gsm);
+    level_step<true>(d, s, i, i < d.n, tid, nth, L, id, gsm);
     __syncthreads();  // this level's D / U / R / Z / X stores before the next level's loads
     if (2 * s >= d.n) break;
   }
@@ -2866,7 +2864,6 @@ kb_sp_handle* kb_sp_create(const kb_sp_layout* L) {
   rc |= h->alloc(&d.U0, (size_t)h->n * NB * NB);
   rc |= h->alloc(&d.R0, (size_t)h->n * NB * d.m);
   rc |= h->alloc(&d.D, (size_t)h->n * NB * NB);
-  rc |= h->alloc(&d.U, (size_t)h->n * NB * NB);
   rc |= h->alloc(&d.R, (size_t)h->n * NB * d.m);
   rc |= h->alloc(&d.Lf, (size_t)h->n * NB * NB);
   rc |= h->alloc(&d.Lid, (size_t)h->n * NB);
@@ -2974,7 +2971,7 @@ kb_sp_handle* kb_sp_create(const kb_sp_layout* L) {
     // and LDS port where each level kernel gives a node a CU of its own, which outweighs the saved launches): as
     // many node groups as the LDS holds (<= kSpDeepGroups), from the first stride whose level has at most that many
     // nodes
-    const size_t per = sizeof(double) * (3 * NB * NB + NB + 3 * NB * (36 + d.m));
+    const size_t per = sizeof(double) * kSpDeepPer(d.m);
     h->deep_groups = (int)std::min<size_t>(kSpDeepGroups, (160 * 1024) / per);
     h->s_deep = 0;
     const char* ev = std::getenv("KSP_DEEP");

@@ -570,6 +570,7 @@ CalibrateCamerasResult calibrateCameras(const std::vector<int32_t>& models,
   oo.nThreads = 16;
   oo.verbose = opt.verbose;
   backend::IncrementalEstimator est(base, estimatorSolver, eo, oo);
+  std::vector<backend::CalibrationBatch> processed;  // every batch handed to addBatch (the statistics' terms)
   for (const SyncedSet& s : res.syncedSets) {
     if (opt.maxBatches && res.acceptedBatches >= *opt.maxBatches) break;
     // the guess uses the calibrators' live intrinsics (the estimator's DVs) and the rig stage's baselines, which
@@ -597,6 +598,7 @@ CalibrateCamerasResult calibrateCameras(const std::vector<int32_t>& models,
       b.view_offset.push_back((uint32_t)b.corner_id.size());
     }
     const auto rv = est.addBatch(b);
+    processed.push_back(b);
     res.processedBatches++;
     if (rv.numIterations > (size_t)oo.maxIterations) throw std::runtime_error("Optimizer reached max iterations. Something went wrong.");
     res.batchAccepted.push_back(rv.batchAccepted ? 1 : 0);
@@ -615,6 +617,41 @@ CalibrateCamerasResult calibrateCameras(const std::vector<int32_t>& models,
     std::copy(p, p + 4, B.q.begin());
     std::copy(p + 4, p + 7, B.t.begin());
     res.finalBaselines.push_back(Transformation::fromMatrix(B.C(), B.t));
+  }
+  // the final reprojection-error statistics (CalibrateCameras.cpp:316-318): one frame per processed batch, its views
+  // in camera order and corners in target order (the order the reference's calibrators stored the terms)
+  if (stages.solver && !processed.empty()) {
+    backend::CalibrationProblem sp;
+    sp.cam_model = models;
+    sp.target = target.points();
+    sp.state.assign(res.finalState.begin(), res.finalState.begin() + (long)(N * KB_MAX_INTR + 7 * (N - 1)));
+    size_t kept = 0;
+    const size_t so = N * KB_MAX_INTR + 7 * (N - 1);
+    for (size_t bi = 0; bi < processed.size(); ++bi) {
+      const backend::CalibrationBatch& b = processed[bi];
+      for (size_t v = 0; v < b.view_cam.size(); ++v) {
+        sp.view_frame.push_back((uint32_t)bi);
+        sp.view_cam.push_back(b.view_cam[v]);
+        sp.view_offset.push_back((uint32_t)sp.corner_id.size());
+        for (uint32_t k = b.view_offset[v]; k < b.view_offset[v + 1]; ++k) {
+          sp.corner_id.push_back(b.corner_id[k]);
+          sp.y.push_back(b.y[2 * k]);
+          sp.y.push_back(b.y[2 * k + 1]);
+        }
+      }
+      if (res.batchAccepted[bi]) {  // the estimator's pose of the kept batch (its frames in acceptance order)
+        sp.state.insert(sp.state.end(), res.finalState.begin() + (long)(so + 7 * kept),
+                        res.finalState.begin() + (long)(so + 7 * kept + 7));
+        ++kept;
+      } else {
+        sp.state.insert(sp.state.end(), b.frame_pose.begin(), b.frame_pose.end());
+      }
+    }
+    sp.view_offset.push_back((uint32_t)sp.corner_id.size());
+    sp.n_frames = (int)processed.size();
+    auto sv = stages.solver();
+    sv->initMatrixStructure(sp, false);
+    res.reprojectionErrorStatistics = sv->reprojectionErrorStatistics();
   }
   return res;
 }

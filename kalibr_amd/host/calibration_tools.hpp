@@ -161,6 +161,13 @@ struct CalibrateCamerasResult {
   std::vector<long> batchIterations, batchRank;
   size_t acceptedBatches = 0, processedBatches = 0;
   std::vector<double> finalState;  // the estimator's state: intrinsics | baselines | accepted target poses
+  /// the numbers CalibrateCameras.cpp:316-318 prints per camera (CameraCalibrator::PrintReprojectionErrorStatistics,
+  /// CameraCalibrator.hpp:368-411) over the terms of EVERY processed batch, as the reference's calibrators store them
+  /// at CreateBatchProblem (CalibrationTools.hpp:511) whether the batch is kept or not, at the final intrinsics and
+  /// baselines and each batch's final target pose (kept: the estimator's; rejected: the guess, which
+  /// IncrementalEstimator::addBatch restores, IncrementalEstimator.cpp:348-350, 512-518): per camera
+  /// [n, mean_u, mean_v, std_u, std_v, rmse], computed by the stage solver (the device for GpuLinearSystemSolver)
+  std::vector<std::array<double, 6>> reprojectionErrorStatistics;
 };
 
 /// `estimatorSolver` is the IncrementalEstimator's marginal solver (GpuMarginalLinearSolver in production)

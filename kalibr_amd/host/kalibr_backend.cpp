@@ -334,6 +334,7 @@ void GpuLinearSystemSolver::initMatrixStructure(const CalibrationProblem& p, boo
   _JCols = (size_t)kb_num_cols(h);
   _C = (size_t)kb_camera_cols(h);
   _F = (size_t)p.n_frames;
+  _N = (size_t)p.n_cams();
   _rhs.assign(_JCols, 0.0);
   _diagonalConditioner.assign(_JCols, 0.0);
   _conditioner = 0.0;
@@ -429,6 +430,7 @@ bool GpuLinearSystemSolver::appendFrames(const CalibrationProblem& p, size_t f0)
   if ((int)p.state.size() != kb_state_size(h)) throw Exception("appendFrames: state size mismatch");
   check(kb_set_state_flat(h, p.state.data()), "kb_set_state_flat");
   _F = (size_t)p.n_frames;
+  _N = (size_t)p.n_cams();
   _JRows = 2 * (size_t)p.n_corners();
   _JCols = (size_t)kb_num_cols(h);
   _rhs.assign(_JCols, 0.0);
@@ -455,6 +457,14 @@ std::vector<double> GpuLinearSystemSolver::state() const {
   std::vector<double> s((size_t)kb_state_size(static_cast<kb_handle*>(_h)));
   check(kb_get_state_flat(static_cast<kb_handle*>(_h), s.data()), "kb_get_state_flat");
   return s;
+}
+
+std::vector<std::array<double, 6>> GpuLinearSystemSolver::reprojectionErrorStatistics() {
+  if (!_h) throw Exception("reprojectionErrorStatistics: initMatrixStructure first");
+  kb_handle* h = static_cast<kb_handle*>(_h);
+  std::vector<std::array<double, 6>> out(_N);
+  check(kb_reprojection_error_stats(h, out[0].data()), "kb_reprojection_error_stats");
+  return out;
 }
 
 void GpuLinearSystemSolver::setState(const std::vector<double>& s) {

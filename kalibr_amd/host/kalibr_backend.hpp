@@ -26,6 +26,7 @@
 #include <ostream>
 #include <stdexcept>
 #include <string>
+#include <array>
 #include <vector>
 
 namespace kalibr_amd {
@@ -97,6 +98,11 @@ class ProblemLinearSystemSolver : public LinearSystemSolver {
   virtual void initMatrixStructure(const CalibrationProblem& problem, bool useDiagonalConditioner) = 0;
   /// flat design-variable values (include/kalibr_hip.h layout)
   virtual std::vector<double> state() const = 0;
+  /// CameraCalibrator::PrintReprojectionErrorStatistics (CameraCalibrator.hpp:368-411) of every camera at the current
+  /// state: [n, mean_u, mean_v, std_u, std_v, rmse] (sample std; rmse = |sum e| / sqrt(n), as the reference prints it)
+  virtual std::vector<std::array<double, 6>> reprojectionErrorStatistics() {
+    throw Exception(name() + ": no reprojection-error statistics");
+  }
 };
 
 // ---------------------------------------------------------------- design variables and error terms
@@ -230,6 +236,7 @@ class GpuLinearSystemSolver : public ProblemLinearSystemSolver {
   void revertLastStateUpdate() override;
 
   std::vector<double> state() const override;
+  std::vector<std::array<double, 6>> reprojectionErrorStatistics() override;  // kb_reprojection_error_stats
   void setState(const std::vector<double>& s);
   size_t cameraCols() const { return _C; }
   void* handle() const { return _h; }
@@ -247,7 +254,7 @@ class GpuLinearSystemSolver : public ProblemLinearSystemSolver {
   void check(int rc, const char* what) const;
   void* _h = nullptr;
   GpuOptions _opt;
-  size_t _C = 0, _F = 0;
+  size_t _C = 0, _F = 0, _N = 0;
   double _conditioner = 0.0;
   bool _built = false;
   mutable bool _rhs_valid = false;

@@ -615,6 +615,48 @@ double kbo_term_dense(const kbo_problem* P, const double* st, int v, int k, doub
 }
 
 /* ------------------------------------------------------------------ */
+/* reprojection-error statistics: CameraCalibrator.hpp:368-411 (two passes, in term order) */
+/* ------------------------------------------------------------------ */
+void kbo_reprojection_stats(const kbo_problem* P, const double* st, double* out) {
+  for (int c = 0; c < P->n_cams; ++c) {
+    double n = 0.0, s0 = 0.0, s1 = 0.0, q0 = 0.0, q1 = 0.0;
+    for (int v = 0; v < P->n_views; ++v) { /* pass 1: std::accumulate of the error vectors */
+      if (P->view_cam[v] != c) continue;
+      const int nk = P->view_offset[v + 1] - P->view_offset[v];
+      for (int k = 0; k < nk; ++k) {
+        double e[2];
+        term_blocks(P, st, v, k, e, NULL, NULL, NULL);
+        s0 += e[0];
+        s1 += e[1];
+        n += 1.0;
+      }
+    }
+    double* o = out + 6 * c;
+    for (int q = 0; q < 6; ++q) o[q] = 0.0;
+    if (n == 0.0) continue;
+    const double m0 = s0 / n, m1 = s1 / n;
+    if (n > 1.0) { /* pass 2: squared differences from the mean, divided by N - 1 */
+      for (int v = 0; v < P->n_views; ++v) {
+        if (P->view_cam[v] != c) continue;
+        const int nk = P->view_offset[v + 1] - P->view_offset[v];
+        for (int k = 0; k < nk; ++k) {
+          double e[2];
+          term_blocks(P, st, v, k, e, NULL, NULL, NULL);
+          q0 += (e[0] - m0) * (e[0] - m0);
+          q1 += (e[1] - m1) * (e[1] - m1);
+        }
+      }
+      o[3] = sqrt(q0 / (n - 1.0));
+      o[4] = sqrt(q1 / (n - 1.0));
+    }
+    o[0] = n;
+    o[1] = m0;
+    o[2] = m1;
+    o[5] = sqrt(s0 * s0 + s1 * s1) / sqrt(n); /* sum_of_errors.norm() / sqrt(size) */
+  }
+}
+
+/* ------------------------------------------------------------------ */
 /* cost: LinearSystemSolver::evaluateError (LinearSystemSolver.cpp:12-23,81-92) */
 /* ------------------------------------------------------------------ */
 

@@ -79,6 +79,13 @@ double kbo_term_dense(const kbo_problem* P, const double* state, int view, int k
 /* --- cost (LinearSystemSolver::evaluateError) --- */
 double kbo_eval_cost(const kbo_problem* P, const double* state, int nthreads);
 
+/* --- CameraCalibrator::PrintReprojectionErrorStatistics (kalibr2/include/kalibr2/CameraCalibrator.hpp:368-411) ---
+ * per camera: the terms flattened view by view in problem order, corners in order (per_view_reprojection_errors_,
+ * CameraCalibrator.hpp:140-152), e = y - yhat; sum in order (std::accumulate), mean = sum / n, the sample standard
+ * deviation of a second pass (N - 1; 0 for n < 2), "RMSE" = |sum| / sqrt(n).  out[n_cams][6] =
+ * [n, mean_u, mean_v, std_u, std_v, rmse]; a camera without terms gets zeros (the reference prints and returns). */
+void kbo_reprojection_stats(const kbo_problem* P, const double* state, double* out);
+
 /* --- arrow normal equations --- */
 typedef struct {
   int C, F;

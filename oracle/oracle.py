@@ -158,6 +158,13 @@ class Oracle:
         st = np.ascontiguousarray(state, dtype=np.float64)
         return lib().kbo_eval_cost(C.byref(self.P), _d(st), nthreads)
 
+    def reprojection_stats(self, state):
+        """kbo_reprojection_stats: per camera [n, mean_u, mean_v, std_u, std_v, rmse] (CameraCalibrator.hpp:368-411)"""
+        st = np.ascontiguousarray(state, dtype=np.float64)
+        out = np.zeros((self.P.n_cams, 6))
+        lib().kbo_reprojection_stats(C.byref(self.P), _d(st), _d(out))
+        return out
+
     def term_dense(self, state, view, k):
         st = np.ascontiguousarray(state, dtype=np.float64)
         J = np.zeros((2, self.ncols))

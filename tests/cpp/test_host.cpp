@@ -30,6 +30,7 @@
 //                                                 (gpu: device-resident loops; gpu-host: host-driven Optimizer2)
 // Prints one JSON line.  The oracle is test infrastructure only (oracle/kb_oracle.h).
 #include <algorithm>
+#include <array>
 #include <cfloat>
 #include <chrono>
 #include <numeric>
@@ -158,6 +159,11 @@ class OracleLinearSystemSolver : public LinearSystemSolver {
   }
   void revertLastStateUpdate() override { _state = _backup; }
   const std::vector<double>& state() const { return _state; }
+  std::vector<std::array<double, 6>> reprojectionErrorStatistics() {
+    std::vector<std::array<double, 6>> out(_op.P.n_cams);
+    kbo_reprojection_stats(&_op.P, _state.data(), out[0].data());
+    return out;
+  }
 
  private:
   OracleProblem _op;
@@ -423,6 +429,7 @@ class OracleProblemSolver : public ProblemLinearSystemSolver {
   double rhsJtJrhs() override { return 0.0; }
   double applyStateUpdate(const std::vector<double>& dx) override { return _s->applyStateUpdate(dx); }
   void revertLastStateUpdate() override { _s->revertLastStateUpdate(); }
+  std::vector<std::array<double, 6>> reprojectionErrorStatistics() override { return _s->reprojectionErrorStatistics(); }
 
  private:
   std::unique_ptr<OracleLinearSystemSolver> _s;
@@ -928,7 +935,7 @@ static int run_pipeline(const CalibrationProblem& p, const std::string& outdir, 
       "\"single\": %s, \"after_single\": %s, \"stereo\": %s, \"after_stereo\": %s, \"optimal\": %s, "
       "\"baseline_guesses\": %s, \"rig\": %s, \"rig_baselines\": %s, \"after_rig\": %s, \"accepted\": %s, "
       "\"batch_iterations\": %s, \"batch_rank\": %s, \"accepted_batches\": %zu, \"final_calibration\": %s, "
-      "\"final_baselines\": %s, \"final_frames\": %zu, \"files\": %zu}\n",
+      "\"final_baselines\": %s, \"final_frames\": %zu, \"files\": %zu, \"reproj_stats\": %s}\n",
       secs, r.syncedSets.size(), jv(withv).c_str(), jv(r.graphSearch.distance).c_str(), jv(prev).c_str(),
       jv(pairs).c_str(), stages(r.single).c_str(), cams(r.afterSingle).c_str(), stages(r.stereo).c_str(),
       cams(r.afterStereo).c_str(),
@@ -939,7 +946,13 @@ static int run_pipeline(const CalibrationProblem& p, const std::string& outdir, 
       }().c_str(),
       trs(r.baselineGuesses).c_str(), stages({r.rig}).c_str(), trs(r.rigBaselines).c_str(), cams(r.afterRig).c_str(),
       jv(acc).c_str(), jv(its).c_str(), jv(rk).c_str(), r.acceptedBatches, jv(calib).c_str(),
-      trs(r.finalBaselines).c_str(), (r.finalState.size() - calib.size()) / 7, files.size());
+      trs(r.finalBaselines).c_str(), (r.finalState.size() - calib.size()) / 7, files.size(),
+      [&]() {
+        std::string s = "[";
+        for (size_t i = 0; i < r.reprojectionErrorStatistics.size(); ++i)
+          s += (i ? ", " : "") + jv(r.reprojectionErrorStatistics[i].data(), 6);
+        return s + "]";
+      }().c_str());
   return 0;
 }
 

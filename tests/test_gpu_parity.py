@@ -208,3 +208,23 @@ def test_rhs_jtj_rhs_on_device(capi, oracle_mod, name):
     r = A["rhs"]
     want = float(r @ H @ r)
     assert abs(g.rhs_jtj_rhs() - want) <= 1e-10 * abs(want)
+
+
+@pytest.mark.parametrize("name", ["c1", "c2_ragged", "c3_small", "c4_small", "c6_small"])
+def test_reprojection_error_stats(capi, oracle_mod, name):
+    """kb_reprojection_error_stats (CameraCalibrator.hpp:368-411 on the device) against kbo_reprojection_stats, at
+    the initial state and after an LM run: term counts exact, mean / sample std / the reference's RMSE (|sum e| /
+    sqrt(n)) within 1e-9 (the sums run in a different order)"""
+    p = PROBLEMS[name]()
+    o = oracle_mod.Oracle(p)
+    g = capi.Solver(p)
+    g.set_state(p.state_init)
+    for step in range(2):
+        st = g.get_state()
+        a, b = g.reprojection_error_stats(), o.reprojection_stats(st)
+        assert np.array_equal(a[:, 0], b[:, 0])
+        assert np.all(b[:, 0] > 0)
+        assert np.abs(a[:, 1:] - b[:, 1:]).max() <= 1e-9 * max(1.0, np.abs(b[:, 1:]).max()), (step, a, b)
+        if step == 0:
+            g.optimize(policy="lm", lambda0=10.0, max_iterations=30, eps_x=1e-3, eps_j=1.0)
+    g.close()

@@ -235,16 +235,22 @@ def test_configs3_eight_shards_full_optimize_against_oracle(capi, oracle_mod, po
 def test_direct_allreduce_bitwise_equals_copies(capi, name, monkeypatch):
     """k_xar, the direct all-reduce of the sharded camera-block image (C > 64): the group's members read each other's
     partial images and sum them in rank order, as the in-process copies do -- bitwise-identical states and traces.
-    With KB_DIRECT_AR=0 the group keeps the copies.  (Members sharing one device take the direct path at 2 members:
-    at 3 the hardware queues do not always co-schedule their k_xar launches; 3 ranks run the copies.)"""
+    With KB_DIRECT_AR=0 the group keeps the copies.  The direct path needs one member per device: on this one-GPU box
+    the default keeps the copies, and KB_DIRECT_AR=force (tests only) lets a two-member group share the device."""
     mk, cuts = CASES[name]
     p = mk()
     out = {}
-    for mode in ("0", "1"):
+    monkeypatch.setenv("KB_DIRECT_AR", "1")  # the product rule: members on one device keep the copies
+    for cc in ([13], [5, 16]):
+        shared = _shards(capi, p, cc)
+        assert not any(s.comm_direct() for s in shared)
+        for s in shared:
+            s.close()
+    for mode in ("0", "force"):
         monkeypatch.setenv("KB_DIRECT_AR", mode)
         solvers = _shards(capi, p, cuts)
-        assert all(s.comm_direct() == (mode == "1") for s in solvers)
-        if mode == "1":  # and 3 members on the one device keep the copies
+        assert all(s.comm_direct() == (mode == "force") for s in solvers)
+        if mode == "force":  # three members on the one device keep the copies even when forced
             three = _shards(capi, p, [5, 16])
             assert not any(s.comm_direct() for s in three)
             for s in three:
@@ -258,8 +264,69 @@ def test_direct_allreduce_bitwise_equals_copies(capi, name, monkeypatch):
         out[mode] = (gn, [s.get_state() for s in solvers], res)
         for s in solvers:
             s.close()
-    for a, b in zip(out["0"][0] + out["0"][1], out["1"][0] + out["1"][1]):
+    for a, b in zip(out["0"][0] + out["0"][1], out["force"][0] + out["force"][1]):
         assert np.array_equal(a, b)
-    for r0, r1 in zip(out["0"][2], out["1"][2]):
+    for r0, r1 in zip(out["0"][2], out["force"][2]):
         assert r0["iterations"] == r1["iterations"] and r0["J_final"] == r1["J_final"]
         assert np.array_equal(r0["trace"], r1["trace"])
+
+
+def test_direct_allreduce_peer_drop_then_retry(capi, monkeypatch):
+    """A rank whose peer stops taking part in the direct all-reduce: its k_xar gives up after the wait bound
+    (KB_XAR_TIMEOUT_MS), ends the enqueued passes (ctrl done) and the call fails; at the next loop start the ranks
+    agree to leave the direct path, and the retried optimize runs over the copies -- bitwise equal to a group that
+    used the copies from the start."""
+    mk, cuts = CASES["c4_2ranks"]
+    p = mk()
+    subs = [p.frame_slice(a, b) for a, b in zip([0] + cuts, cuts + [p.n_frames])]
+    kw = dict(policy="gn", max_iterations=20, eps_x=1e-3, eps_j=1.0)
+    monkeypatch.setenv("KB_DIRECT_AR", "0")
+    ref = _shards(capi, p, cuts)
+    r_ref = _run_all(ref, lambda s: s.optimize(**kw))
+    st_ref = [s.get_state() for s in ref]
+    for s in ref:
+        s.close()
+    monkeypatch.setenv("KB_DIRECT_AR", "force")
+    monkeypatch.setenv("KB_XAR_TIMEOUT_MS", "300")
+    solvers = _shards(capi, p, cuts)
+    assert all(s.comm_direct() for s in solvers)
+
+    def uneven(s):  # rank 1 stops after 2 passes: rank 0's third k_xar waits in vain
+        try:
+            s.run_gn(5 if s is solvers[0] else 2)
+            return None
+        except RuntimeError as e:
+            return str(e)
+
+    errs = _run_all(solvers, uneven)
+    assert errs[0] is not None and "k_xar" in errs[0], errs
+    assert errs[1] is None, errs
+    assert all(s.comm_direct() for s in solvers)  # still installed: the agreement is at the next loop start
+    for s, sub in zip(solvers, subs):
+        s.set_state(sub.state_init)
+    res = _run_all(solvers, lambda s: s.optimize(**kw))
+    assert not any(s.comm_direct() for s in solvers)
+    for a, b in zip(st_ref, [s.get_state() for s in solvers]):
+        assert np.array_equal(a, b)
+    for r0, r1 in zip(r_ref, res):
+        assert r0["iterations"] == r1["iterations"] and r0["J_final"] == r1["J_final"]
+    for s in solvers:
+        s.close()
+
+
+@pytest.mark.parametrize("name", ["c2_2ranks", "c4_3ranks"])
+def test_sharded_reprojection_error_stats(capi, name):
+    """kb_reprojection_error_stats on a sharded group: every rank returns the statistics over ALL ranks' terms (the
+    per-camera sums all-reduced between the two passes), equal to the unsharded handle's to rounding"""
+    mk, cuts = CASES[name]
+    p = mk()
+    ref = capi.Solver(p)
+    ref.set_state(p.state_init)
+    want = ref.reprojection_error_stats()
+    solvers = _shards(capi, p, cuts)
+    got = _run_all(solvers, lambda s: s.reprojection_error_stats())
+    for g in got:
+        assert np.array_equal(g[:, 0], want[:, 0])
+        assert np.abs(g[:, 1:] - want[:, 1:]).max() <= 1e-12 * np.abs(want[:, 1:]).max()
+    for s in solvers + [ref]:
+        s.close()

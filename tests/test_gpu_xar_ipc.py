@@ -4,7 +4,8 @@ multi-GPU node.  RCCL refuses several ranks on one device, so the mapping is exe
 the one GPU (kb_xar_export / kb_xar_test, the hook that runs exactly the IPC and exchange code of kb_comm_init).
 
 Bars: every rank's self-test exchange returns the exact rank-order sums (ok on all ranks); with a peer that does not
-take part, the waiting rank's k_xar gives up after its 2 s bound and reports failure (no hang)."""
+take part, the waiting rank's k_xar gives up after its wait bound (KB_XAR_TIMEOUT_MS, 2 s here; 10 s by default) and
+reports failure (no hang)."""
 import multiprocessing as mp
 import os
 import time
@@ -76,7 +77,8 @@ def test_ipc_exchange_between_processes(nranks):
     assert all(r[0] is True for r in res), res
 
 
-def test_ipc_absent_peer_times_out():
+def test_ipc_absent_peer_times_out(monkeypatch):
+    monkeypatch.setenv("KB_XAR_TIMEOUT_MS", "2000")  # inherited by the spawned ranks
     res = _run([True, False])
     ok, sec = res[0]
     assert ok is False, res

@@ -287,3 +287,45 @@ def test_pcg_preconditioner_blocks(oracle_mod):
     assert oracle_mod.pcg_camera_blocks([synth.OMNI_RADTAN, synth.EUCM, synth.PINHOLE_FOV]) == [5, 4, 6, 4, 1, 3, 3, 3, 3]
     p = synth.make_config(3, n_frames=4)
     assert sum(oracle_mod.pcg_camera_blocks(p.cam_model)) == p.cam_cols
+
+
+def _numpy_residuals(p, st):
+    """e = y - yhat of every term by synth's numpy projection and 4x4 chains (independent of the oracle's C maths):
+    T_cam_w = B_{c-1} .. B_0 T_f^-1, the state layout of include/kalibr_hip.h"""
+    N = p.n_cams
+    ob, of = N * synth.MAX_INTR, N * synth.MAX_INTR + 7 * (N - 1)
+    E, cams = [], []
+    for v in range(p.n_views):
+        f, c = int(p.view_frame[v]), int(p.view_cam[v])
+        T = synth.inv_T(synth.pose_to_T(st[of + 7 * f: of + 7 * f + 7]))
+        for j in range(c):
+            T = synth.pose_to_T(st[ob + 7 * j: ob + 7 * j + 7]) @ T
+        o0, o1 = int(p.view_offset[v]), int(p.view_offset[v + 1])
+        X = p.target[p.corner_id[o0:o1]]
+        pc = (T[:3, :3] @ X.T).T + T[:3, 3]
+        kp, _ = synth.project(int(p.cam_model[c]), st[c * synth.MAX_INTR:(c + 1) * synth.MAX_INTR], pc)
+        E.append(p.y[o0:o1] - kp)
+        cams += [c] * (o1 - o0)
+    return np.concatenate(E), np.array(cams)
+
+
+@pytest.mark.parametrize("cfg", [1, 2, 3])
+def test_reprojection_stats_restatement(oracle_mod, cfg):
+    """kbo_reprojection_stats (CameraCalibrator::PrintReprojectionErrorStatistics, CameraCalibrator.hpp:368-411)
+    against numpy over independently computed residuals: per camera the mean, the sample std (ddof = 1) and the
+    reference's "RMSE" = |sum e| / sqrt(n), on ragged views of three rigs (pinhole-radtan, omni-radtan + EUCM,
+    pinhole 4-cam) at the perturbed initial state"""
+    p = synth.make_config(cfg, n_frames=6, p_view=0.8, seed_offset=11)
+    st = p.state_init
+    out = oracle_mod.Oracle(p).reprojection_stats(st)
+    E, cams = _numpy_residuals(p, st)
+    for c in range(p.n_cams):
+        Ec = E[cams == c]
+        assert out[c, 0] == len(Ec)
+        if len(Ec) == 0:
+            assert np.all(out[c] == 0.0)
+            continue
+        scale = np.abs(Ec).max()
+        assert np.abs(out[c, 1:3] - Ec.mean(0)).max() <= 1e-9 * scale
+        assert np.abs(out[c, 3:5] - Ec.std(0, ddof=1)).max() <= 1e-9 * scale
+        assert abs(out[c, 5] - np.linalg.norm(Ec.sum(0)) / np.sqrt(len(Ec))) <= 1e-9 * scale * np.sqrt(len(Ec))

@@ -153,6 +153,12 @@ def test_pipeline_over_the_oracle_recovers_the_rig(driver, tmp_path, rig3):  # n
         ang = np.arccos(np.clip((np.trace(B[:3, :3].T @ Bt[:3, :3]) - 1) / 2, -1, 1))
         assert np.degrees(ang) < 0.2
     assert r["accepted"][0] == 1 and r["accepted_batches"] == r["final_frames"] == sum(r["accepted"])
+    # the final reprojection-error statistics (CameraCalibrator.hpp:368-411) over every processed batch's terms: the
+    # reference's "RMSE" is |sum e| / sqrt(n) = sqrt(n) |mean|; 0.3 px noise per axis
+    st = np.array(r["reproj_stats"])
+    assert st.shape == (N, 6) and np.all(st[:, 0] > 0)
+    assert np.abs(st[:, 5] - np.sqrt(st[:, 0]) * np.hypot(st[:, 1], st[:, 2])).max() < 1e-9
+    assert np.abs(st[:, 1:3]).max() < 0.05 and np.all((st[:, 3:5] > 0.2) & (st[:, 3:5] < 0.5))
     # the export: one CameraInfo per camera and the chain transforms (two baselines: a TFMessage)
     assert r["files"] == 4
     c0 = yaml.safe_load(open(out / "calibration_cam0.yaml"))
@@ -199,6 +205,11 @@ def test_pipeline_gpu_matches_oracle(driver, tmp_path, rig3, kind):  # noqa: F81
     for k in ("after_single", "after_stereo", "optimal", "baseline_guesses", "rig_baselines", "after_rig",
               "final_calibration", "final_baselines"):
         assert np.abs(np.array(r[k]) - np.array(ref[k])).max() < 1e-6, k
+    # the final reprojection-error statistics (on the device for the GPU runs): the same term counts; the numbers
+    # follow the final states, which agree to 1e-6
+    a, b = np.array(r["reproj_stats"]), np.array(ref["reproj_stats"])
+    assert np.array_equal(a[:, 0], b[:, 0])
+    assert np.abs(a[:, 1:] - b[:, 1:]).max() < 1e-6
     # the exported YAML: the same files and fields, numbers within 1e-6
     names = sorted(p.name for p in out_ref.iterdir())
     assert sorted(p.name for p in out.iterdir()) == names
