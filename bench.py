@@ -286,15 +286,17 @@ def main():
                        "frames_per_gpu": shard.n_frames, "cameras": full.n_cams, "corners_per_gpu": shard.n_corners,
                        "jacobian_cols": full.total_cols, "camera_block": full.cam_cols, "policy": "gauss_newton",
                        "parallelism": f"frame-sharded x{world}"},
-            # the build kernel's arithmetic intensity (SURVEY 8(d) flops / algorithmic bytes, ~28 flop/B at configs[3])
-            # is above the FP64 ridge (78.6 TF/s / 8 TB/s ~ 9.8 flop/B): its roofline is the FP64 pipe, and its SQ
-            # counters put it below that, issue/latency-bound on VALU work.  The HBM view is kept beside.
+            # the build kernel's arithmetic intensity (SURVEY 8(d) flops / algorithmic bytes: 1.69 GFLOP over 67.6 MB,
+            # ~25 flop/B at configs[3]) is above the FP64 ridge (78.6 TF/s / 8 TB/s ~ 9.8 flop/B): its roofline is the
+            # FP64 compute pipe, which the f64 MFMAs and the f64 VALU work of one SIMD share (their issue serialises,
+            # DESIGN.md 3c), so "mfma" names the compute bound.  The HBM view is kept beside.
             "roofline": {"bound": "mfma", "kernel": kname, "achieved": useful_tfs, "peak": FP64_PEAK_TFS,
                          "unit": "TFLOP/s", "frac": useful_tfs / FP64_PEAK_TFS,
                          "traffic": pmc[0] if pmc else None, "traffic_source": pmc[1] if pmc else None,
                          "avg_ms": build_ms, "algorithmic_flops": flops_per, "algorithmic_bytes": bytes_per,
                          "arithmetic_intensity": flops_per / bytes_per,
-                         "limiter": "FP64 VALU issue and the per-frame dependency chain (SQ counters, DESIGN.md 6)",
+                         "limiter": "the SIMD's FP64 pipe (f64 MFMA + f64 VALU issue of the view waves, serialised) "
+                                    "and the per-frame dependency chain (SQ counters, DESIGN.md 3c, 6)",
                          "hbm": {"achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                  "frac": achieved / HBM_PEAK_GBS,
                                  "traffic_gbs": (pmc[0] / (build_ms * 1e-3) / 1e9) if pmc else None}},

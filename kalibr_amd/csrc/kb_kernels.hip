@@ -1525,7 +1525,16 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
         auto make_g = [&]() {
           if (lane < 36) Gm[lane] = chain_entry_reg(R, t, fp + 4, lane / 6, lane % 6);
         };
+#ifdef KB_SYRK16
         v4d acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+#else
+        // the SYRK on v_mfma_f64_4x4x4f64 (4 blocks of 4 x 4): only the 10 upper 4 x 4 blocks of the symmetric 16 x 16
+        // [J | e]^T [J | e] are formed (2.5 instructions of ~17 cycles per 4 rows, against one 64-cycle 16x16x4 that
+        // also forms the 6 lower blocks).  accD: the diagonal blocks (b, b); accO1: (b, b+1 mod 4); accO2: (0,2), (1,3)
+        // of two row quads.  Operand lane 16k + 4b + c supplies row k, column 4I_b + c (A) / 4J_b + c (B); block b's
+        // entry (i, j) lands at lane 16i + 4b + j (tools/micro/mfma_f64_4x4_layout.hip).
+        double accD = 0.0, accO1 = 0.0, accO2 = 0.0;
+#endif
         const int o0 = fv.x, o1 = fv.y;
         const bool stv = (wave == 0 || wave == N - 1) && it == 2;  // diagnostic stamps: one steady-state frame
         const int sto = wave == 0 ? 130 : 160;
@@ -1631,7 +1640,11 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
           // issued (k-step ks = rows 4ks .. 4ks + 3, even ks into acc0, odd into acc1), the next group's operands in
           // flight during the current group's MFMAs (one LDS round trip per group, not per MFMA).  Row = lane: the
           // lanes of a write hit distinct LDS bank pairs at the 17-double row stride.
+#ifdef KB_SYRK16
           const int ng = (min(64, o1 - base) + 15) >> 4;
+#else
+          const int np = (min(64, o1 - base) + 7) >> 3;  // pairs of row quads holding valid rows (the rest are zero)
+#endif
 #pragma unroll
           for (int r = 0; r < 2; ++r) {
 #ifdef KB_CORNER_NOZERO
@@ -1648,6 +1661,54 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
             for (int q = 0; q < 16; ++q) Xw[lane * XS + q] = r ? xv[q] : xu[q];
 #endif
             KB_WAVE_SYNC();
+#ifndef KB_SYRK16
+            {
+              // per pair of row quads (rows 8p .. 8p + 7): the diagonal-block operand of each quad (row mrow, column
+              // mcol: the 16x16x4 operand), the (b, b+1) operand of each (column (mcol + 4) & 15), and the A / B
+              // operands of the paired (0,2), (1,3) instruction (lanes b < 2: quad 0, columns mcol | mcol + 8; b >= 2:
+              // quad 1, columns mcol - 8 | mcol); the next pair's six loads issued before this pair's five MFMAs
+              const int bq = (lane >> 2) & 3;
+              const int oD = mrow * XS + mcol, oE = mrow * XS + ((mcol + 4) & 15);
+              const int oA = bq < 2 ? oD : (4 + mrow) * XS + mcol - 8, oB = bq < 2 ? oD + 8 : (4 + mrow) * XS + mcol;
+              double xr[3][6];  // the operands of two pairs (the next pair's loads in flight during this pair's MFMAs)
+              auto ld = [&](double* x, int pp) {
+                const double* xp = Xw + 8 * pp * XS;
+                x[0] = xp[oD];
+                x[1] = xp[oE];
+                x[2] = xp[4 * XS + oD];
+                x[3] = xp[4 * XS + oE];
+                x[4] = xp[oA];
+                x[5] = xp[oB];
+                __builtin_amdgcn_sched_barrier(0);
+              };
+              auto mf = [&](const double* x) {
+                accD = __builtin_amdgcn_mfma_f64_4x4x4f64(x[0], x[0], accD, 0, 0, 0);
+                accO1 = __builtin_amdgcn_mfma_f64_4x4x4f64(x[0], x[1], accO1, 0, 0, 0);
+                accD = __builtin_amdgcn_mfma_f64_4x4x4f64(x[2], x[2], accD, 0, 0, 0);
+                accO1 = __builtin_amdgcn_mfma_f64_4x4x4f64(x[2], x[3], accO1, 0, 0, 0);
+                accO2 = __builtin_amdgcn_mfma_f64_4x4x4f64(x[4], x[5], accO2, 0, 0, 0);
+                __builtin_amdgcn_sched_barrier(0);
+              };
+#ifndef KB_SYRK44_RING3  // (a ring of three pairs spills more to AGPRs and measured 0.4 % slower)
+              ld(xr[0], 0);
+#pragma unroll
+              for (int pp = 0; pp < 8; ++pp) {
+                if (pp >= np) break;  // wave-uniform
+                if (pp + 1 < np) ld(xr[(pp + 1) & 1], pp + 1);
+                mf(xr[pp & 1]);
+              }
+#else
+              ld(xr[0], 0);
+              if (np > 1) ld(xr[1], 1);
+#pragma unroll
+              for (int pp = 0; pp < 8; ++pp) {
+                if (pp >= np) break;  // wave-uniform
+                if (pp + 2 < np) ld(xr[(pp + 2) % 3], pp + 2);
+                mf(xr[pp % 3]);
+              }
+#endif
+            }
+#else
             // groups g = 0..3 ping-pong between xa and xb: group g + 1's loads are issued before group g's MFMAs
             double xa[4], xb[4];
             auto ld = [&](double* x, int g) {
@@ -1674,6 +1735,7 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
                 if (ng > 3) mf(xb);
               }
             }
+#endif
             if (stv && pass < 2) KB_TSB(d, sto + 4 * pass + 2 + r);
             if (r == 0 && pass == 0) make_g();
             KB_WAVE_SYNC();
@@ -1690,11 +1752,35 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
         if (it == 3 && wave < 8) KB_TSB(d, 144 + wave);
         // f64 MFMA C/D layout: lane l, reg r -> row (l>>4) + 4r, col l&15
         v4d hv;
+#ifdef KB_SYRK16
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           hv[q] = acc0[q] + acc1[q];
           creg[q] = creg[q] + hv[q];
         }
+#else
+        {
+          // the upper blocks to the 16 x 16 C layout (hv[q] = H[mrow + 4q][mcol]) through the view's tile (free after
+          // the SYRK): each block and its mirror written, the two quads' (0,2), (1,3) parts added first (lane + 8)
+          const int bq = (lane >> 2) & 3, ii = lane >> 4, jj = lane & 3;
+          const double o2 = accO2 + dpp_d<0x128>(accO2);
+          const int rb = 4 * bq + ii, c1 = 4 * ((bq + 1) & 3) + jj;
+          Xw[rb * XS + 4 * bq + jj] = accD;
+          Xw[rb * XS + c1] = accO1;
+          Xw[c1 * XS + rb] = accO1;
+          if (bq < 2) {
+            const int c2 = 4 * (bq + 2) + jj;
+            Xw[rb * XS + c2] = o2;
+            Xw[c2 * XS + rb] = o2;
+          }
+          KB_WAVE_SYNC();
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            hv[q] = Xw[(mrow + 4 * q) * XS + mcol];
+            creg[q] = creg[q] + hv[q];
+          }
+        }
+#endif
         // expansion of view (f, cam) through the 6-D chain G on MFMA steps whose operands stay in registers:
         //   D = H[:, d] G  (A = the lane's own H registers: H is symmetric, so C-layout row r of a lane is A's k-step r;
         //   B = G from LDS), i.e. D[i][a] = P_v[a][i] with P_v = G^T H[d, :]: G^T H_dd, G^T H_dI, G^T g_d;
@@ -3553,6 +3639,29 @@ __device__ __forceinline__ void panel2_steps(double (&dr)[16], double (&br)[16],
   }
 }
 
+// panel2_steps with a one-step lookahead: step K's column K + 1 first, then step K + 1's pivot (D_{K+1} by DPP, the
+// reciprocal, its multipliers), then step K's columns K + 2 .. 15, so that the pivot's broadcast -> v_rcp -> Newton
+// chain issues while the bulk of step K's FMAs is still in the wave's stream (in-order issue: without the lookahead
+// every pivot waits behind the previous step's 2 (15 - K) FMAs).  Same operations and operands per entry as
+// panel2_steps: bitwise the same factor.  nfd / nfb: step K's multipliers (computed by the caller / the previous step).
+template <int K>
+__device__ __forceinline__ void panel3_steps(double (&dr)[16], double (&br)[16], int r, int q, int C, bool& ok,
+                                             double& rd, double nfd, double nfb) {
+  if constexpr (K < 16) {
+    if constexpr (K + 1 < 16) {
+      fmac_bc<K>(br[K + 1], dr[K + 1], nfb);
+      fmac_bc_self<K>(dr[K + 1], nfd);
+      const double Dn = bcast16_dep<K + 1>(dr[K + 1]);
+      const double rdn = Dn > 0.0 ? recip_d1(Dn) : 0.0;
+      const double nfdn = -(dr[K + 1] * rdn), nfbn = -(br[K + 1] * rdn);
+      panel2_cols<K, K + 2>(dr, br, nfd, nfb);
+      ok = ok & ((Dn > 0.0) | (16 * q + K + 1 >= C));
+      rd = (r == K + 1) ? rdn : rd;
+      panel3_steps<K + 1>(dr, br, r, q, C, ok, rd, nfdn, nfbn);
+    }
+  }
+}
+
 // panel q by factor wave fw: lane (t = lane >> 4, r = lane & 15) holds row r of the diagonal tile (every 16-lane row
 // the same copy) and row r of tile q + 1 + 4 fw + t.  The tiles of column q are complete (every earlier panel applied).
 // The below rows' W go back in place; the factored diagonal tile (W strictly below, D on the diagonal) to Dfac and 1/D
@@ -3574,7 +3683,17 @@ __device__ __forceinline__ bool panel_factor2(const KbDev& d, double* S, double*
   bool ok = true;
   double rd = 1.0;
   if (q == 2 && fw == 0) KB_TS(d, 41);
+#ifdef KB_PANEL_NOLOOK
   panel2_steps<0>(dr, br, r, q, C, ok, rd);
+#else
+  {
+    const double D0 = bcast16_dep<0>(dr[0]);
+    const double rd0 = D0 > 0.0 ? recip_d1(D0) : 0.0;
+    ok = ok & ((D0 > 0.0) | (16 * q >= C));
+    rd = (r == 0) ? rd0 : rd;
+    panel3_steps<0>(dr, br, r, q, C, ok, rd, -(dr[0] * rd0), -(br[0] * rd0));
+  }
+#endif
 #ifdef KB_STAMPS
 #pragma unroll
   for (int c = 0; c < 16; ++c) KB_KEEP(br[c]);
