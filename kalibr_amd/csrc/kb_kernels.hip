@@ -1254,6 +1254,7 @@ __global__ void __launch_bounds__(512) k_build(KbDev d, int gate, int fuse) {
 // the baseline columns (per-camera products summed over cameras).
 // ---------------------------------------------------------------------------------------------
 constexpr int kBuildpMaxCams = 8;
+
 // frame waves of k_buildp: the Schur tiles per frame wave TT picks them (<= 5 tiles: 2 waves, else 4: one frame wave
 // per SIMD beside its two view waves)
 template <int TT>
@@ -1587,16 +1588,23 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
           // flips of J_delta = -Jp [I | [p]x] and of the intrinsic rows -Jp, -Jd (CameraDesignVariable.hpp(impl):38-54)
           // are not spent.  Lanes past the view's last corner leave xu / xv undefined and store zero rows instead (no
           // 32-register zero initialisation per pass).
+          // (KB_CORNER_CLAMP: every lane projects a real corner -- lanes past the view's end hold the clamped last
+          // corner -- without the exec-mask branch and the zero initialisation, those lanes storing zero rows: more
+          // VGPRs spilled to AGPRs, k_buildp 93.1 -> 96.9 us; not the default)
           const bool valid = k < o1;
           double xu[16], xv[16];
-#ifndef KB_CORNER_NOZERO
+#if !defined(KB_CORNER_NOZERO) && !defined(KB_CORNER_CLAMP)
 #pragma unroll
           for (int q = 0; q < 16; ++q) {
             xu[q] = 0.0;
             xv[q] = 0.0;
           }
 #endif
+#ifdef KB_CORNER_CLAMP
+          {
+#else
           if (valid) {
+#endif
             double X0, X1, X2;
 #ifdef KB_CORNER_TGB
             if (tg_lds) {  // the staged corners through ds_read (a select of the two pointers compiles to flat loads)
@@ -1617,7 +1625,16 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
             const double p1 = R[3] * X0 + R[4] * X1 + R[5] * X2 + t[1];
             const double p2 = R[6] * X0 + R[7] * X1 + R[8] * X2 + t[2];
             double u, w, Jp[6], Ji[2 * KB_MAX_INTR];
+#ifdef KB_DIAG_NOPROJ  // diagnostic timing variant only (wrong results): the projection and its Jacobian skipped
+            u = p0;
+            w = p1;
+#pragma unroll
+            for (int q = 0; q < 6; ++q) Jp[q] = p2 * q;
+#pragma unroll
+            for (int q = 0; q < 2 * KB_MAX_INTR; ++q) Ji[q] = p0 + q;
+#else
             project_jac<MM>(model, intr, p0, p1, p2, u, w, Jp, Ji);
+#endif
 #pragma unroll
             for (int r = 0; r < 2; ++r) {
               double* xr = r ? xv : xu;
@@ -1647,7 +1664,7 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
 #endif
 #pragma unroll
           for (int r = 0; r < 2; ++r) {
-#ifdef KB_CORNER_NOZERO
+#if defined(KB_CORNER_NOZERO) || defined(KB_CORNER_CLAMP)
             if (valid) {
 #pragma unroll
               for (int q = 0; q < 16; ++q) Xw[lane * XS + q] = r ? xv[q] : xu[q];
@@ -1690,6 +1707,11 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
                 __builtin_amdgcn_sched_barrier(0);
               };
 #ifndef KB_SYRK44_RING3  // (a ring of three pairs spills more to AGPRs and measured 0.4 % slower)
+#ifdef KB_DIAG_NOSYRK  // diagnostic timing variant only (wrong results): the SYRK MFMAs and their loads skipped
+              (void)ld;
+              (void)mf;
+              (void)np;
+#else
               ld(xr[0], 0);
 #pragma unroll
               for (int pp = 0; pp < 8; ++pp) {
@@ -1697,6 +1719,7 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
                 if (pp + 1 < np) ld(xr[(pp + 1) & 1], pp + 1);
                 mf(xr[pp & 1]);
               }
+#endif
 #else
               ld(xr[0], 0);
               if (np > 1) ld(xr[1], 1);
@@ -1981,7 +2004,11 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
         double* P = VBp + N * 44;  // [H_fc | g_f]: the views wrote the intrinsic columns in place
         // the views' P_v (their MFMA A operands, entry (a, k) at register k >> 2, lane 16 (k & 3) + a)
         const double* pab = PvL + ((it - 1) & 1) * N * 128;
+#ifdef KB_DIAG_NOFW  // diagnostic timing variant only (wrong results): the frame waves' sums skipped
+        for (int q = nsum; q < nsum; q += 64 * NF) {
+#else
         for (int q = fw * 64 + lane; q < nsum; q += 64 * NF) {
+#endif
           double sacc = 0.0;
           if (q < nbl) {
             // H_f,B_j = sum_{i > j} P_i K_{i,j}: each camera's product (6 FMAs on the VALU: the MFMA pipes are busy with
@@ -2057,7 +2084,11 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
         asm volatile("" : "+v"(lane));
         if (fw == 0 && it <= 8) KB_TSB(d, 20 + 4 * (it - 1));
         double* P = (((it - 1) & 1) ? VB1 : VB) + N * 44;
+#ifdef KB_DIAG_NOFW
+        const bool ok = true;
+#else
         const bool ok = frame_ldl_cols(d, f, Fh, lam2, P, Q, CZ, lane, qc0, qc1, fw == 0 && it == 3);
+#endif
         if (!ok && lane == 0 && fw == 0) okl = 0;
         // the frame waves meet again before the Schur tiles read every column of Q (the next frame's elimination
         // writes Q only after the next frame's sums meeting, which every wave reaches after its Schur tiles)
@@ -2066,7 +2097,9 @@ __global__ void __launch_bounds__(64 * MW) k_buildp(KbDev d, int gate, int fuse)
         if (lane == 0) atomicAdd(&fcnt, 1);
         while (__hip_atomic_load(&fcnt, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < mt) __builtin_amdgcn_s_sleep(1);
         if (fw == 0 && it <= 8) KB_TSB(d, 22 + 4 * (it - 1));
+#ifndef KB_DIAG_NOFW
         schur_tiles_accumulate6<TT>(P, Q, CZ, tii, tjj, acc, lane);
+#endif
         if (fw == 0 && it <= 8) KB_TSB(d, 23 + 4 * (it - 1));
       }
       if (it < G) __syncthreads();  // the view waves' frame it is in VB[it & 1]
@@ -3662,6 +3695,67 @@ __device__ __forceinline__ void panel3_steps(double (&dr)[16], double (&br)[16],
   }
 }
 
+// the same after 2 wait states (its DPP source was written by the previous VALU instruction)
+template <int L>
+__device__ __forceinline__ void fmac_bc_self_dep(double& x, double f) {
+  asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf"
+               : "+v"(x) : "v"(f), "i"(L));
+}
+
+// columns J .. 15 of a 2 x 2 pivot step (panel4_steps): per column the below row from the ORIGINAL pivot rows K, K + 1
+// (DPP reads before the diagonal rows change), then the diagonal row's step-K part; its step-(K + 1) part is issued
+// after the next column's below-row updates, so that its DPP read of the register the step-K part just wrote has its
+// two wait states without an s_nop (the pivot lanes' own values move by rounding only: their multipliers are 1 / 0 up
+// to rounding, and they are never read again as pivot rows)
+template <int K, int J>
+__device__ __forceinline__ void panel4_cols(double (&dr)[16], double (&br)[16], double nd1, double nd2, double nb1,
+                                            double nb2) {
+  if constexpr (J < 16) {
+    fmac_bc<K>(br[J], dr[J], nb1);
+    fmac_bc<K + 1>(br[J], dr[J], nb2);
+    if constexpr (J > K + 2) fmac_bc_self<K + 1>(dr[J - 1], nd2);
+    fmac_bc_self<K>(dr[J], nd1);
+    if constexpr (J == 15) fmac_bc_self_dep<K + 1>(dr[15], nd2);
+    panel4_cols<K, J + 1>(dr, br, nd1, nd2, nb1, nb2);
+  }
+}
+
+// (KB_PANEL_2X2, not the default: the factor wave is issue-bound, ~7 cycles per f64 FMA of one wave, on the 240 column
+// FMAs per lane of a panel (2 rows x 120), and the block form's three reciprocal chains and multiplier selects add ~40 VALU per pivot
+// pair: 16 pivots 1.0 -> 1.5 us.)  The panel factorisation two pivots at a time: pivots K, K + 1 eliminated together
+// through the 2 x 2 block
+// [[a, b], [b, c]] (rows K, K + 1 from lanes K, K + 1 by DPP): one reciprocal chain per two pivots (1/a, 1/det and 1/c
+// are independent), so the pivot chain of a panel is 8 steps instead of 16.  A lane's multipliers are its two entries
+// times the block inverse, [f1 f2] = [x_K x_K+1] B^-1, and column K + 1 takes the step-K part only, so the factor is
+// the sequential one's (the W = L D form, D on the diagonal, 1/D in rd) up to rounding; when a pivot fails the
+// multipliers follow the sequential semantics (a <= 0: step K skipped, c alone; det <= 0: step K + 1 skipped).
+template <int K>
+__device__ __forceinline__ void panel4_steps(double (&dr)[16], double (&br)[16], int r, int q, int C, bool& ok,
+                                             double& rd) {
+  if constexpr (K < 16) {
+    const double a = bcast16_dep<K>(dr[K]);
+    const double b = bcast16_dep<K>(dr[K + 1]);
+    const double c = bcast16_dep<K + 1>(dr[K + 1]);
+    const double det = fma(a, c, -(b * b));
+    const bool pa = a > 0.0, pd = pa && det > 0.0, pc = c > 0.0;
+    const double rda = pa ? recip_d1(a) : 0.0;
+    const double rdt = pd ? recip_d1(det) : 0.0;
+    const double rc = pc ? recip_d1(c) : 0.0;
+    // B^-1 with the sequential semantics of failed pivots
+    const double i11 = pd ? c * rdt : rda, i12 = pd ? -(b * rdt) : 0.0, i22 = pd ? a * rdt : (pa ? 0.0 : rc);
+    const double xd0 = dr[K], xd1 = dr[K + 1], xb0 = br[K], xb1 = br[K + 1];
+    const double nd1 = -fma(xd0, i11, xd1 * i12), nd2 = -fma(xd0, i12, xd1 * i22);
+    const double nb1 = -fma(xb0, i11, xb1 * i12), nb2 = -fma(xb0, i12, xb1 * i22);
+    // column K + 1: the step-K update only (W form: W[j][K + 1] = S[j][K + 1] - S[j][K] b / a, D_{K+1} on lane K + 1)
+    br[K + 1] = fma(-(xb0 * rda), b, xb1);
+    dr[K + 1] = fma(-(xd0 * rda), b, xd1);
+    panel4_cols<K, K + 2>(dr, br, nd1, nd2, nb1, nb2);
+    ok = ok & (pa | (16 * q + K >= C)) & ((pa ? pd : pc) | (16 * q + K + 1 >= C));  // bitwise: no branch per pivot
+    rd = (r == K) ? rda : ((r == K + 1) ? (pa ? a * rdt : rc) : rd);
+    panel4_steps<K + 2>(dr, br, r, q, C, ok, rd);
+  }
+}
+
 // panel q by factor wave fw: lane (t = lane >> 4, r = lane & 15) holds row r of the diagonal tile (every 16-lane row
 // the same copy) and row r of tile q + 1 + 4 fw + t.  The tiles of column q are complete (every earlier panel applied).
 // The below rows' W go back in place; the factored diagonal tile (W strictly below, D on the diagonal) to Dfac and 1/D
@@ -3685,6 +3779,8 @@ __device__ __forceinline__ bool panel_factor2(const KbDev& d, double* S, double*
   if (q == 2 && fw == 0) KB_TS(d, 41);
 #ifdef KB_PANEL_NOLOOK
   panel2_steps<0>(dr, br, r, q, C, ok, rd);
+#elif defined(KB_PANEL_2X2)  // measured slower (configs[3] pass 0.1237 -> 0.1300 ms): see DESIGN.md 9
+  panel4_steps<0>(dr, br, r, q, C, ok, rd);
 #else
   {
     const double D0 = bcast16_dep<0>(dr[0]);

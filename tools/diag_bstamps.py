@@ -8,7 +8,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from kalibr_amd import capi, synth  # noqa: E402
 
-capi.LIB_PATH = os.path.join(ROOT, "kalibr_amd", "libkalibr_hip_stamps.so")
+capi.LIB_PATH = os.path.join(ROOT, "kalibr_amd", os.environ.get("KB_STAMPS_LIB", "libkalibr_hip_stamps.so"))
 L = capi.lib()
 L.kb_diag_read_ts.argtypes = [C.c_void_p, C.POINTER(C.c_longlong), C.c_int]
 cfg = int(sys.argv[1]) if len(sys.argv) > 1 else 4
@@ -46,7 +46,10 @@ names[142] = "    [fw0] f2 column slot 0 solved+stored"
 names[143] = "    [fw0] f2 column slot 1 solved+stored"
 for rep in range(2):
     g.set_state(p.state_init)
-    g.run_gn(16)
+    try:
+        g.run_gn(16)
+    except capi.KbError as e:  # diagnostic timing variants (wrong results) may fail the solves; the stamps stay
+        print("(run_gn:", e, ")")
     assert L.kb_diag_read_ts(g.h, buf, 256) == 0
     t0 = buf[64]
     order = sorted((buf[64 + i] - t0, i) for i in names if buf[64 + i] >= t0 and buf[64 + i] - t0 < 10_000_000)
