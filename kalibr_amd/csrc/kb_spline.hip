@@ -130,6 +130,12 @@ struct SpDev {
   long long* dbg_ts;      // diagnostics only: [256] KSP_TS stamps
   int dbg_stop;           // diagnostics only (KSP_DBG_STOP): 0, or the phase after which the timed kernels return
   int zero_lam;           // GN pass: k_sp_imu_cc sets lambda^2 = 0 (no separate launch)
+  // round 6: the Schur complement from the forward reduction alone (S = H_tt - sum_i Z_R,i^T Z_R,i over every node's
+  // eliminated right-hand side, the top node's included) and the back substitution with ONE right-hand side
+  // v = [-dtheta | 1] after the camera solve (k_sp_bvec*), instead of X = D^-1 [H_st | g_s] for all C + 1 columns
+  int zs;
+  double* xs;             // [n][18] the nodes' spline steps x_j = X_j v (zs)
+  double* bm;             // [n][18][37] L_j^-T [Z_Uin,j | Z_U,j | Z_R,j v] (zs, k_sp_bprep)
 };
 
 typedef double v4d_t __attribute__((ext_vector_type(4)));
@@ -1559,7 +1565,11 @@ __device__ __forceinline__ void level_step(const SpDev& d, int s, int i, bool ac
   }
   KSP_STOP(3);
   if (!LEAN) KSP_TSB(tsb, tsl + 3);
-  if (fin && top) {  // X_0 = L^-T L^-1 R' (forward in place in W, then backward into X_0)
+  if (fin && top && d.zs) {  // Z_R,0 = L^-1 R' and the factor: the back substitution solves x_0 with one column later
+    node_forward(L, id, W + 2 * NB, wc, m, d.Z + 2 * NB, wc, tid, nth);
+    for (int q = tid; q < NB * NB; q += nth) d.Lf[q] = L[q];
+    if (tid < NB) d.Lid[tid] = id[tid];
+  } else if (fin && top) {  // X_0 = L^-T L^-1 R' (forward in place in W, then backward into X_0)
     if (LEAN) {
       node_forward_lean(L, id, W + 2 * NB, wc, m, W + 2 * NB, wc, tid, nth);
       node_backsolve_lean(L, id, W + 2 * NB, wc, m, d.X, tid, nth);
@@ -1600,6 +1610,12 @@ __global__ void __launch_bounds__(256) k_sp_top(SpDev d) {
     if (!ok && tid == 0) d.sc[SC_OK] = 0.0;
   }
   __syncthreads();
+  if (d.zs) {  // Z_R,0 and the factor (see level_step)
+    node_forward(L, id, T, m, m, d.Z + 2 * NB, 36 + m, tid);
+    for (int q = tid; q < NB * NB; q += blockDim.x) d.Lf[q] = L[q];
+    if (tid < NB) d.Lid[tid] = id[tid];
+    return;
+  }
   node_forward(L, id, T, m, m, T, m, tid);
   node_backsolve(L, id, T, m, m, d.X, tid);
 }
@@ -2161,6 +2177,146 @@ __global__ void __launch_bounds__(256) k_sp_schur(SpDev d) {
   for (int q = tid; q < d.Ws; q += blockDim.x) d.spart[(size_t)blockIdx.x * d.Ws + q] = acc[q];
 }
 
+// zs: the camera-block partial sums of sum_i Z_R,i^T Z_R,i (Z_R,i = L_i^-1 R_i', the right-hand-side part of node i's
+// elimination at any level, the top node's included) = R0^T D^-1 R0 of k_sp_schur's sum_i R0_i^T X_i, from the forward
+// reduction alone; same blocks of NPB nodes, same entry table and k_sp_schur_red
+__global__ void __launch_bounds__(256) k_sp_zschur(SpDev d) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];  // Z_R [18][m] | acc [Ws] | tab
+  const int tid = threadIdx.x, m = d.m, wc = 36 + m;
+  double* Zl = sm;
+  double* acc = sm + 2 * NB * m;  // (k_sp_schur's layout: the LDS size is the host's lds_schur)
+  short2* tab = (short2*)(acc + d.Ws);
+  for (int q = tid; q < d.Ws; q += blockDim.x) {
+    acc[q] = 0.0;
+    tab[q] = d.uab[q];
+  }
+  const int i0 = blockIdx.x * NPB, i1 = min(d.n, i0 + NPB);
+  constexpr int ZS_U = (NB * (MAXC + 1) + 255) / 256;
+  const int nq = NB * m;
+  const float rinv = 1.0f / (float)m;
+  double v[ZS_U];
+  auto load = [&](int i) {
+    const double* Z = d.Z + (size_t)i * NB * wc + 2 * NB;
+#pragma unroll
+    for (int u = 0; u < ZS_U; ++u) {
+      const int q = min(tid + u * 256, nq - 1), r = div_small(q, rinv);
+      v[u] = Z[r * wc + (q - r * m)];
+    }
+  };
+  if (i0 < i1) load(i0);
+  for (int i = i0; i < i1; ++i) {
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < ZS_U; ++u) {
+      const int q = tid + u * 256;
+      if (q < nq) Zl[q] = v[u];
+    }
+    __syncthreads();
+    if (i + 1 < i1) load(i + 1);
+    for (int q = tid; q < d.Ws; q += blockDim.x) {
+      const short2 ab = tab[q];
+      const int a = ab.x, b = ab.y;
+      double s = 0.0;
+#pragma unroll
+      for (int k = 0; k < NB; ++k) s += Zl[k * m + a] * Zl[k * m + b];
+      acc[q] += s;
+    }
+  }
+  __syncthreads();
+  for (int q = tid; q < d.Ws; q += blockDim.x) d.spart[(size_t)blockIdx.x * d.Ws + q] = acc[q];
+}
+
+// zs, step 1 (every node at once, after the camera solve): with v = [-dtheta | 1], node j's operands of the
+// one-column back substitution, [M_l | M_r | u] = L_j^-T [Z_Uin,j | Z_U,j | Z_R,j v] (18 x 37, row-major into bm):
+// the chain of strides then needs no triangular solve, x_j = u_j - M_l x_{j-s} - M_r x_{j+s}
+__global__ void __launch_bounds__(256) k_sp_bprep(SpDev d) {
+  // one wave per node (4 per block), wave-local LDS: L | 1/diag | T = [Z_Uin | Z_U | y] (18 x 37) | y partials | v
+  __shared__ double Ls[4][NB * NB];
+  __shared__ double ids[4][NB];
+  __shared__ double Ts[4][NB * 37];
+  __shared__ double yp[4][3 * NB];
+  __shared__ double vs[4][MAXC + 1];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, m = d.m, wc = 36 + m, C = d.C;
+  const int j = 4 * blockIdx.x + wave;
+  if (j >= d.n) return;  // wave-uniform
+  double* L = Ls[wave];
+  double* id = ids[wave];
+  double* T = Ts[wave];
+  const double* Z = d.Z + (size_t)j * NB * wc;
+  for (int q = lane; q < NB * NB; q += 64) L[q] = d.Lf[(size_t)j * NB * NB + q];
+  if (lane < NB) id[lane] = d.Lid[(size_t)j * NB + lane];
+  for (int c = lane; c < m; c += 64) vs[wave][c] = c < C ? -d.dx[c] : 1.0;
+  for (int q = lane; q < NB * 36; q += 64) {
+    const int r = q / 36, c = q - 36 * r;
+    T[r * 37 + c] = Z[r * wc + c];
+  }
+  KSP_WAVE_SYNC();
+  if (lane < 3 * NB) {  // y = Z_R v: three lanes per row over interleaved columns, summed in a fixed order
+    const int r = lane % NB, pp = lane / NB;
+    double t = 0.0;
+    for (int c = pp; c < m; c += 3) t = fma(Z[r * wc + 36 + c], vs[wave][c], t);
+    yp[wave][pp * NB + r] = t;
+  }
+  KSP_WAVE_SYNC();
+  if (lane < NB) T[lane * 37 + 36] = (yp[wave][lane] + yp[wave][NB + lane]) + yp[wave][2 * NB + lane];
+  KSP_WAVE_SYNC();
+  node_backsolve_lean(L, id, T, 37, 37, d.bm + (size_t)j * NB * 37, lane, 64);
+}
+
+// zs, step 2: node j of stride s on one wave (s = 0: the top node, x_0 = u_0): lane r < 18 forms row r of
+// x_j = u_j - M_l x_{j-s} - M_r x_{j+s} (every load in one round), written to xs and as the node's coefficient steps
+// into dx
+__device__ __forceinline__ void bvec_node(const SpDev& d, int j, int s, int lane) {
+  const int C = d.C;
+  const int l = j - s, r = j + s;
+  const bool hl = s > 0, hr = s > 0 && r < d.n;
+  const int row = lane < NB ? lane : 0;
+  const double* M = d.bm + (size_t)j * NB * 37 + row * 37;
+  double mr[37], xl[NB], xr[NB];
+#pragma unroll
+  for (int k = 0; k < 37; ++k) mr[k] = M[k];
+#pragma unroll
+  for (int k = 0; k < NB; ++k) {
+    xl[k] = d.xs[(size_t)(hl ? l : j) * NB + k];
+    xr[k] = d.xs[(size_t)(hr ? r : j) * NB + k];
+  }
+  double t = mr[36];
+#pragma unroll
+  for (int k = 0; k < NB; ++k) t = fma(-mr[k], hl ? xl[k] : 0.0, t);
+#pragma unroll
+  for (int k = 0; k < NB; ++k) t = fma(-mr[NB + k], hr ? xr[k] : 0.0, t);
+  if (lane < NB) {
+    d.xs[(size_t)j * NB + lane] = t;
+    const int k = SB * j + lane / 6;
+    if (k < d.K) d.dx[C + 6 * k + lane % 6] = t;
+  }
+}
+
+// zs, step 2 for the deep strides in one block of 8 waves: the top node, then strides s_hi .. s_lo (at most 16 nodes
+// each, one or two per wave), a block barrier between strides (the xs stores are block-visible after it)
+constexpr int kBvecDeepWaves = 8;
+__global__ void __launch_bounds__(64 * kBvecDeepWaves) k_sp_bvec_deep(SpDev d, int s_hi, int s_lo) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  int nst = 1;
+  for (int s = s_hi; s >= s_lo && s >= 1; s >>= 1) ++nst;
+  for (int t = 0; t < nst; ++t) {
+    const int s = t == 0 ? 0 : (s_hi >> (t - 1));
+    for (int b = wave; b < (t == 0 ? 1 : 16); b += kBvecDeepWaves) {
+      const int j = t == 0 ? 0 : s + 2 * s * b;
+      if (j < d.n) bvec_node(d, j, s, lane);
+    }
+    __syncthreads();
+  }
+}
+
+// zs, step 2 for one wider stride s: one node per wave (4 per block)
+__global__ void __launch_bounds__(256) k_sp_bvec(SpDev d, int s) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int j = s + 2 * s * (4 * blockIdx.x + wave);
+  if (j >= d.n) return;  // wave-uniform
+  bvec_node(d, j, s, lane);
+}
+
 // S = H_cc + lam2 I - sum_i R0_i^T X_i, b = g_c - sum (4-wave interleaved partial sums), written full
 __global__ void __launch_bounds__(64 * RW) k_sp_schur_red(SpDev d) {
   __shared__ double red[RW][64];
@@ -2234,11 +2390,16 @@ __global__ void __launch_bounds__(64) k_sp_update(SpDev d, int apply) {
   if (tid < NB) {
     const int k = SB * i + tid / 6;
     if (k < d.K) {
-      const double* x = d.X + (size_t)i * NB * m + tid * m;
-      double v = x[C];
+      double v;
+      if (d.zs) {  // written by the one-column back substitution (k_sp_bvec*)
+        v = d.dx[C + 6 * k + tid % 6];
+      } else {
+        const double* x = d.X + (size_t)i * NB * m + tid * m;
+        v = x[C];
 #pragma unroll 16
-      for (int c = 0; c < C; ++c) v -= x[c] * d.dx[c];
-      d.dx[C + 6 * k + tid % 6] = v;
+        for (int c = 0; c < C; ++c) v -= x[c] * d.dx[c];
+        d.dx[C + 6 * k + tid % 6] = v;
+      }
       mx = fabs(v);
       const int o = d.off_coef + 6 * k + tid % 6;
       if (go) {
@@ -2617,6 +2778,7 @@ struct kb_sp_handle {
   std::vector<SpLvl> lv;  // partitioned band solve: lv[0 .. nl) chunk levels, lv[nl] the top system
   bool use_cr = true;     // block cyclic reduction; KSP_PARTITION=1: the partitioned band solve
   int s_deep = 0;         // first stride run by k_sp_deep (0: one launch per level)
+  int s_top = 0;          // zs: the stride the forward reduction ended at (the top node solved there)
   int deep_groups = 0;    // k_sp_deep's node groups (kSpDeepGT threads each)
   size_t lds_deep = 0;
   std::vector<double> trace;
@@ -2678,6 +2840,7 @@ int launch_reduction(kb_sp_handle* h) {
   }
   if (d.n == 1) {
     hipLaunchKernelGGL(k_sp_top, dim3(1), dim3(256), sizeof(double) * NB * d.m, h->stream, d);
+    h->s_top = 1;
     return 0;
   }
   hipLaunchKernelGGL(k_sp_elim1, dim3(d.n / 2), dim3(256), h->lds_elim, h->stream, d);
@@ -2685,6 +2848,10 @@ int launch_reduction(kb_sp_handle* h) {
   const int sd = h->s_deep;
   for (; s < d.n && !(sd && s >= sd); s *= 2)
     hipLaunchKernelGGL(k_sp_level, dim3((d.n + 2 * s - 1) / (2 * s)), dim3(256), h->lds_level, h->stream, d, s);
+  if (d.zs) {  // the back substitution runs after the camera solve, with one column (launch_bvec)
+    h->s_top = s;
+    return 0;
+  }
   if (sd && s < d.n) {  // the remaining levels down and back up to stride sd in one block
     hipLaunchKernelGGL(k_sp_deep, dim3(1), dim3(kSpDeepGT * h->deep_groups), h->lds_deep, h->stream, d, sd);
     s = sd;
@@ -2708,13 +2875,28 @@ int launch_reduction(kb_sp_handle* h) {
   return 0;
 }
 
+// zs: the back substitution with v = [-dtheta | 1]: the top node and the strides with at most 16 nodes in one block
+// (k_sp_bvec_deep), the wider strides one launch each (a wave per node)
+int launch_bvec(kb_sp_handle* h) {
+  SpDev& d = h->d;
+  auto count = [&](int s) { return d.n > s ? (d.n - s + 2 * s - 1) / (2 * s) : 0; };
+  int s = h->s_top / 2, s_lo = s;
+  while (s_lo > 1 && count(s_lo / 2) <= 16) s_lo /= 2;
+  hipLaunchKernelGGL(k_sp_bprep, dim3((d.n + 3) / 4), dim3(256), 0, h->stream, d);
+  hipLaunchKernelGGL(k_sp_bvec_deep, dim3(1), dim3(64 * kBvecDeepWaves), 0, h->stream, d, s, s >= 1 ? s_lo : 1 << 30);
+  for (s = s_lo / 2; s >= 1; s /= 2) hipLaunchKernelGGL(k_sp_bvec, dim3((count(s) + 3) / 4), dim3(256), 0, h->stream, d, s);
+  KSP_HIP(hipGetLastError());
+  return 0;
+}
+
 int launch_solve(kb_sp_handle* h) {
   SpDev& d = h->d;
   void* args[] = {&d};
   launch_reduction(h);
-  hipLaunchKernelGGL(k_sp_schur, dim3(d.nblk_s), dim3(256), h->lds_schur, h->stream, d);
+  hipLaunchKernelGGL(d.zs ? k_sp_zschur : k_sp_schur, dim3(d.nblk_s), dim3(256), h->lds_schur, h->stream, d);
   hipLaunchKernelGGL(k_sp_schur_red, dim3((d.Ws + 63) / 64), dim3(64 * RW), 0, h->stream, d);
   KSP_HIP(hipLaunchKernel(h->fn_camsolve, dim3(1), dim3(64), args, 0, h->stream));
+  if (d.zs) return launch_bvec(h);
   return 0;
 }
 
@@ -2984,6 +3166,17 @@ kb_sp_handle* kb_sp_create(const kb_sp_layout* L) {
     }
   }
   hipFuncSetAttribute((const void*)k_sp_schur, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_schur);
+  hipFuncSetAttribute((const void*)k_sp_zschur, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_schur);
+  {
+    // the Schur complement from the forward reduction and the one-column back substitution (default with the cyclic
+    // reduction; KSP_ZS=0 keeps the C + 1 column back substitution and X)
+    const char* ev = std::getenv("KSP_ZS");
+    d.zs = (h->use_cr && h->s_deep == 0 && !(ev && std::atoi(ev) == 0)) ? 1 : 0;
+    if (d.zs && (h->alloc(&d.xs, (size_t)h->n * NB) || h->alloc(&d.bm, (size_t)h->n * NB * 37))) {
+      kb_sp_destroy(h);
+      return nullptr;
+    }
+  }
   if (hipStreamSynchronize(h->stream) != hipSuccess) {
     fail("kb_sp_create: stream sync failed");
     kb_sp_destroy(h);
@@ -3637,21 +3830,28 @@ int kb_sp_kernel_stats(kb_sp_handle* h, int32_t n, double* ms_out6, double* fram
     hipLaunchKernelGGL(k_sp_reduce_cc, dim3((d.Wc + 63) / 64), dim3(64 * RW), 0, h->stream, d);
     if (d.cq) hipLaunchKernelGGL(k_sp_mcost_build, dim3(1), dim3(256), 0, h->stream, d);
     KSP_HIP(hipEventRecord(ev[2], h->stream));
-    launch_reduction(h);
+    launch_reduction(h);  // (zs: the forward half; the one-column back substitution follows the camera solve)
     KSP_HIP(hipEventRecord(ev[3], h->stream));
-    hipLaunchKernelGGL(k_sp_schur, dim3(d.nblk_s), dim3(256), h->lds_schur, h->stream, d);
+    hipLaunchKernelGGL(d.zs ? k_sp_zschur : k_sp_schur, dim3(d.nblk_s), dim3(256), h->lds_schur, h->stream, d);
     hipLaunchKernelGGL(k_sp_schur_red, dim3((d.Ws + 63) / 64), dim3(64 * RW), 0, h->stream, d);
     KSP_HIP(hipLaunchKernel(h->fn_camsolve, dim3(1), dim3(64), args, 0, h->stream));
     KSP_HIP(hipEventRecord(ev[4], h->stream));
+    if (d.zs && launch_bvec(h)) return -1;
+    KSP_HIP(hipEventRecord(ev[5], h->stream));
     hipLaunchKernelGGL(k_sp_update, dim3(d.n), dim3(64), 0, h->stream, d, 1);
     if (launch_cost(h, 1)) return -1;
-    KSP_HIP(hipEventRecord(ev[5], h->stream));
+    KSP_HIP(hipEventRecord(ev[6], h->stream));
     KSP_HIP(hipStreamSynchronize(h->stream));
-    float t[5];
-    for (int q = 0; q < 5; ++q) KSP_HIP(hipEventElapsedTime(&t[q], ev[q], ev[q + 1]));
-    for (int q = 0; q < 5; ++q) acc[q] += t[q];
+    float t[6];
+    for (int q = 0; q < 6; ++q) KSP_HIP(hipEventElapsedTime(&t[q], ev[q], ev[q + 1]));
+    // frames | assemble | reduction (forward + back substitution) | Schur + camera solve | update + cost | pass
+    acc[0] += t[0];
+    acc[1] += t[1];
+    acc[2] += t[2] + t[4];
+    acc[3] += t[3];
+    acc[4] += t[5];
     float tt;
-    KSP_HIP(hipEventElapsedTime(&tt, ev[0], ev[5]));
+    KSP_HIP(hipEventElapsedTime(&tt, ev[0], ev[6]));
     acc[5] += tt;
   }
   for (auto& e : ev) hipEventDestroy(e);

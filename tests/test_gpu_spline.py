@@ -305,9 +305,12 @@ def test_position_prior_removed_and_bad_input(prior_case):
 
 def test_deep_level_kernel_parity(case, monkeypatch):
     """KSP_DEEP=1 (the cyclic reduction's deep levels in one block, measured slower and kept opt-in): the same GN run
-    as the per-level kernels (the same arithmetic in the same order: state and J bitwise) and as the oracle"""
-    p, o, g = case
+    as the per-level kernels with the C + 1 column back substitution (KSP_ZS=0: the same arithmetic in the same order,
+    state and J bitwise) and as the oracle"""
+    p, o, _ = case
     kw = dict(policy="gn", lambda0=10.0, max_iterations=20, eps_x=1e-3, eps_j=1e-3)
+    monkeypatch.setenv("KSP_ZS", "0")
+    g = capi.SplineSolver(p)
     g.set_state(p.state_init)
     res = g.optimize(**kw)
     st = g.get_state()
@@ -321,3 +324,31 @@ def test_deep_level_kernel_parity(case, monkeypatch):
     assert res_d["iterations"] == res_o["iterations"]
     assert abs(res_d["J_final"] - res_o["J_final"]) <= 1e-9 * res_o["J_final"]
     assert np.abs(gd.get_state() - st_o).max() < 1e-6
+
+
+def test_one_column_back_substitution_matches_full(case, monkeypatch):
+    """The default solve (Schur complement from the forward reduction, sum_i Z_R,i^T Z_R,i, and the back substitution
+    with the one column [-dtheta | 1]) against the C + 1 column back substitution (KSP_ZS=0): the same dx to 1e-10
+    at lambda 0 and 10, and the same GN run (iteration count, J to 1e-12, state to 1e-9)"""
+    p, o, g = case
+    monkeypatch.setenv("KSP_ZS", "0")
+    gf = capi.SplineSolver(p)
+    for sv in (g, gf):
+        sv.set_state(p.state_init)
+        sv.build()
+    for lam in (0.0, 10.0):
+        dxs = []
+        for sv in (g, gf):
+            sv.set_constant_conditioner(lam)
+            ok, dx = sv.solve()
+            assert ok
+            dxs.append(dx)
+        assert np.abs(dxs[0] - dxs[1]).max() <= 1e-10 * np.abs(dxs[1]).max(), lam
+    kw = dict(policy="gn", lambda0=10.0, max_iterations=20, eps_x=1e-3, eps_j=1e-3)
+    res = []
+    for sv in (g, gf):
+        sv.set_state(p.state_init)
+        res.append((sv.optimize(**kw), sv.get_state()))
+    assert res[0][0]["iterations"] == res[1][0]["iterations"]
+    assert abs(res[0][0]["J_final"] - res[1][0]["J_final"]) <= 1e-12 * res[1][0]["J_final"]
+    assert np.abs(res[0][1] - res[1][1]).max() < 1e-9
