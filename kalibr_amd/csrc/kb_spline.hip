@@ -72,7 +72,10 @@ constexpr int WI = 55;      // IMU theta partial row: 9x9 upper (45) | g (9) | c
 constexpr int NPB = 4;      // nodes per k_sp_schur block
 constexpr int TCH = 32;     // IMU samples staged per k_sp_assemble chunk
 constexpr int TCF = 8;      // frames staged per k_sp_assemble chunk
-constexpr int IST = 144 + 15;  // LDS stride of a staged IMU sample: J [6][24] | e [6] | C^T [9]
+constexpr int IRQ = 42;     // IMU record: T1 [9] | T2 [9] | T3 [9] | C^T [9] | e [6] (imu_sample)
+constexpr int IRS = IRQ + 13;  // LDS stride of a staged IMU record: record | w0 w1 w2 [12] | pad
+constexpr int PNS = 8;      // IMU samples per k_sp_assemble operand panel (48 residual rows = 12 MFMA k-steps)
+constexpr int PST = 49;     // LDS row stride of the panel (48 columns: Jw [36] | J_theta [9] | -e | 0 0)
 enum { SC_COST_BUILD = 0, SC_OK = 1, SC_DX = 2, SC_COST = 3, SC_LAM2 = 4, SC_NSC = 8 };
 
 struct SpDev {
@@ -136,6 +139,7 @@ struct SpDev {
   int zs;
   double* xs;             // [n][18] the nodes' spline steps x_j = X_j v (zs)
   double* bm;             // [n][18][37] L_j^-T [Z_Uin,j | Z_U,j | Z_R,j v] (zs, k_sp_bprep)
+  double* irec;           // [IRQ][M] per-sample IMU records (k_sp_imu_cc -> k_sp_assemble): T1 | T2 | T3 | C^T | e
 };
 
 typedef double v4d_t __attribute__((ext_vector_type(4)));
@@ -592,9 +596,10 @@ __global__ void __launch_bounds__(512) k_sp_frames(SpDev d) {
 }
 
 // ---------------------------------------------------------------- IMU sample (defined in DESIGN.md 10)
-// Whitened residual e[6] and the Jacobian blocks J[6][24] (4 coefficients x [p | theta]) of sample m;
-// Ct (C_wb^T) for the gravity columns.  Mirrors oracle/kb_oracle_spline.c:sp_imu (independently written).
-__device__ void imu_sample(const SpDev& d, int m, double* e, double* J, double* Ct) {
+// Whitened residual e[6] of sample m, Ct (C_wb^T) for the gravity columns and, when T is given, the three 3 x 3 factors
+// T1 | T2 | T3 of its Jacobian blocks (J[6][24], 4 coefficients x [p | theta]; expanded in k_sp_assemble's panels).  Mirrors
+// oracle/kb_oracle_spline.c:sp_imu (independently written).
+__device__ void imu_sample(const SpDev& d, int m, double* e, double* T, double* Ct) {
   const int b = d.ib[m];
   const double* w = d.iw + 12 * m;  // w0[4] | w1[4] | w2[4]
   const double* cf = d.state + d.off_coef + 6 * b;
@@ -638,12 +643,14 @@ __device__ void imu_sample(const SpDev& d, int m, double* e, double* J, double* 
     e[r] = (mm[r] - om[r] - ib[r]) * ig;
     e[3 + r] = (mm[3 + r] - fb[r] - ib[3 + r]) * ia;
   }
-  if (!J) return;
+  if (!T) return;
   double Dm[9];
   rv_dSv(v0 + 3, v1 + 3, Dm);
   const double wx[9] = {0, -wv[2], wv[1], wv[2], 0, -wv[0], -wv[1], wv[0], 0};
   const double vx[9] = {0, -vv[2], vv[1], vv[2], 0, -vv[0], -vv[1], vv[0], 0};
-  double T1[9], T2[9], T3[9];  // T1 = -C^T D + C^T [w]x S ; T2 = C^T S ; T3 = C^T [v]x S
+  double* T1 = T;  // T1 = -C^T D + C^T [w]x S ; T2 = C^T S ; T3 = C^T [v]x S
+  double* T2 = T + 9;
+  double* T3 = T + 18;
   {
     double wxS[9], vxS[9];
 #pragma unroll
@@ -670,27 +677,9 @@ __device__ void imu_sample(const SpDev& d, int m, double* e, double* J, double* 
         T3[r * 3 + c] = a4;
       }
   }
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int r = 0; r < 3; ++r)
-#pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        const int rc = r * 3 + c;
-        J[r * 24 + 6 * j + c] = 0.0;
-        J[r * 24 + 6 * j + 3 + c] = -(w[j] * T1[rc] - w[4 + j] * T2[rc]) * ig;
-        J[(3 + r) * 24 + 6 * j + c] = -(w[8 + j] * Ct[rc]) * ia;
-        J[(3 + r) * 24 + 6 * j + 3 + c] = (w[j] * T3[rc]) * ia;
-      }
 }
 
-// IMU Jacobian w.r.t. the 9 IMU columns (b_g | b_a | g_w), row r, column c
-__device__ __forceinline__ double imu_jth(const SpDev& d, const double* Ct, int r, int c) {
-  if (r < 3) return (c == r) ? -d.ig : 0.0;
-  if (c < 3) return 0.0;
-  if (c < 6) return (c - 3 == r - 3) ? -d.ia : 0.0;
-  return Ct[(r - 3) * 3 + (c - 6)] * d.ia;
-}
+
 
 // ---------------------------------------------------------------- k_sp_assemble
 // One block per cyclic-reduction node i (coefficients 3i..3i+2): D_i (18 x 18), U_i (coupling to node
@@ -701,12 +690,13 @@ __global__ void __launch_bounds__(256) k_sp_assemble(SpDev d) {
   const int i = blockIdx.x, tid = threadIdx.x, nth = blockDim.x, C = d.C, m = d.m;
   const int nout = 2 * NB * NB + NB * m;
   double* out = sm;                       // [nout]
-  // frame chunk [TCF][FHS] (FH rows) | IMU chunk [TCH][IST] (J 6 x 24 | e | C^T) share one region: a node has
-  // ~3 frames and ~25 IMU samples, so a 32-term region of FHS rows would cut the blocks per CU to one
+  // frame chunk [TCF][FHS] (FH rows) | IMU records [TCH][IRS] + operand panel [6 PNS][PST] share one region: a node
+  // has ~3 frames and ~25 IMU samples, so a 32-term region of FHS rows would cut the blocks per CU
   double* tj = out + nout;
   const int stride = d.FHS;
   __shared__ int tb[TCH];
   __shared__ double tw[TCH][4];
+  KSP_TSB(500, 241);  // diagnostics: block 500's timeline in slots 241..252 (tools/diag_sp_asm.py)
   for (int q = tid; q < nout; q += nth) out[q] = 0.0;
   const int k0 = SB * i;
   // ---- frames
@@ -731,101 +721,172 @@ __global__ void __launch_bounds__(256) k_sp_assemble(SpDev d) {
             tw[(e - nt) / 4][(e - nt) % 4] = v;
         });
     __syncthreads();
-    for (int q = tid; q < nout; q += nth) {
-      double s = 0.0;
+    // the chunk's frames outer, this thread's UQ entries inner (independent LDS reads in flight); each entry sums its
+    // frames in order.  Entry constants: D | U: coefficient rows kr, columns kc; R: kc = -1 (weight of the row only)
+    constexpr int UQ = (2 * NB * NB + NB * (MAXC + 1) + 255) / 256;
+    int ekr[UQ], ekc[UQ], eoff[UQ];
+    double eacc[UQ];
+#pragma unroll
+    for (int u = 0; u < UQ; ++u) {
+      const int q = min(tid + 256 * u, nout - 1);
+      eacc[u] = 0.0;
       if (q < 2 * NB * NB) {
         const int blk = q / (NB * NB), e = q % (NB * NB), r = e / NB, c = e % NB;
-        const int kr = k0 + r / 6, kc = k0 + SB * blk + c / 6;
-        for (int t = 0; t < nt; ++t) {
-          const int jr = kr - tb[t], jc = kc - tb[t];
-          if (jr < 0 || jr > 3 || jc < 0 || jc > 3) continue;
-          s += tw[t][jr] * tw[t][jc] * tj[t * stride + (r % 6) * 6 + (c % 6)];
-        }
+        ekr[u] = k0 + r / 6;
+        ekc[u] = k0 + SB * blk + c / 6;
+        eoff[u] = (r % 6) * 6 + (c % 6);
       } else {
         const int e = q - 2 * NB * NB, r = e / m, a = e % m;
-        const int kr = k0 + r / 6;
-        for (int t = 0; t < nt; ++t) {
-          const int jr = kr - tb[t];
-          if (jr < 0 || jr > 3) continue;
-          const double h = (a < C) ? tj[t * stride + 36 + (r % 6) * C + a] : tj[t * stride + 36 + 6 * C + (r % 6)];
-          s += tw[t][jr] * h;
-        }
+        ekr[u] = k0 + r / 6;
+        ekc[u] = -1;
+        eoff[u] = (a < C) ? 36 + (r % 6) * C + a : 36 + 6 * C + (r % 6);
       }
-      out[q] += s;
     }
+    for (int t = 0; t < nt; ++t) {
+      const int b = tb[t];
+      const double* W = tw[t];
+      const double* T = tj + t * stride;
+#pragma unroll
+      for (int u = 0; u < UQ; ++u) {
+        const int jr = ekr[u] - b, jc = ekc[u] - b;
+        const bool okr = jr >= 0 && jr <= 3, okc = jc >= 0 && jc <= 3;
+        const double wr = W[min(max(jr, 0), 3)], wc = W[min(max(jc, 0), 3)], h = T[eoff[u]];
+        if (ekc[u] >= 0)
+          eacc[u] += (okr && okc) ? wr * wc * h : 0.0;
+        else
+          eacc[u] += okr ? wr * h : 0.0;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < UQ; ++u)
+      if (tid + 256 * u < nout) out[tid + 256 * u] += eacc[u];
   }
   KSP_STOP(1);
-  // ---- IMU samples
+  KSP_TSB(500, 242);
+  // ---- IMU samples: per chunk of TCH, the records k_sp_imu_cc wrote (T1 | T2 | T3 | C^T | e) and the basis weights staged
+  // in LDS; then per PNS samples an operand panel of 6 PNS residual rows x [Jw (nodes i, i + 1) | J_theta | -e | 0 0] built
+  // by every thread, followed by its MFMA steps: Jn^T [Jw | J_theta | -e] with Jn = the panel's first 18 columns (this
+  // node's rows), k = 4 st + (lane >> 4) = 6 t + z.  Waves 0..2: rows 0..15 x columns 16 w .. 16 w + 15 on
+  // v_mfma_f64_16x16x4f64; wave 3: rows 16, 17 (padded to 4) x the 48 columns as three v_mfma_f64_4x4x4f64 per step
+  // (4 blocks of 4 x 4: operand lane 16 k + 4 b + i, result (row 16 + (lane >> 4), column 16 g + (lane & 15)))
   const int ma = d.node_im[2 * i], mz = d.node_im[2 * i + 1];
   const int wave = tid >> 6, lane = tid & 63;
-  v4d_t iacc[2] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
+  v4d_t iacc = {0.0, 0.0, 0.0, 0.0};
+  double iac4[3] = {0.0, 0.0, 0.0};
+  double* rec = tj;              // [TCH][IRS]
+  double* P = tj + TCH * IRS;    // [6 PNS][PST]
   for (int c0 = ma; c0 < mz; c0 += TCH) {
     const int nt = min(TCH, mz - c0);
     __syncthreads();
-    if (tid < nt) {
-      double* J = tj + tid * IST;
-      imu_sample(d, c0 + tid, J + 144, J, J + 150);  // e at +144, Ct at +150
-      tb[tid] = d.ib[c0 + tid];
-    }
-    __syncthreads();
-    KSP_STOP(2);
-    // Jn^T [Jw | J_theta | -e] over the chunk's 6 nt residual rows: Jn = the samples' Jacobian columns of this
-    // node's 18 rows, Jw those of nodes i and i + 1 (D_i | U_i), J_theta the 9 IMU columns, e the whitened
-    // residual.  A 2 x 3 grid of 16 x 16 tiles (rows 0..17, columns 0..35 D | U, 36..44 IMU, 45 g), tiles wave and
-    // wave + 4, k = 4 st + (lane >> 4) = 6 t + z
-    const int ks = (6 * nt + 3) / 4;
+    {  // every load in flight before the stores: the IRQ field segments of nt samples, then the chunk's 12 nt weights
+      constexpr int U = (TCH * (IRQ + 12) + 255) / 256;
+      const int nr = IRQ * nt, nall = (IRQ + 12) * nt;
+      double v[U];
+      int dst[U];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int tile = wave + 4 * u;
-      if (tile < 6) {  // wave-uniform
-        const int ir = 16 * (tile / 3) + (lane & 15), jc = 16 * (tile % 3) + (lane & 15);
-        auto operands = [&](int st, double& av, double& bv) {
-          const int k = 4 * st + (lane >> 4), t = k / 6, z = k % 6;
-          av = 0.0;
-          bv = 0.0;
-          if (t < nt) {
-            const double* J = tj + t * IST;
-            const int jr = k0 + ir / 6 - tb[t];
-            if (ir < NB && jr >= 0 && jr <= 3) av = J[z * 24 + 6 * jr + ir % 6];
-            if (jc < 2 * NB) {
-              const int jj = k0 + jc / 6 - tb[t];
-              if (jj >= 0 && jj <= 3) bv = J[z * 24 + 6 * jj + jc % 6];
-            } else if (jc < 2 * NB + 9) {
-              bv = imu_jth(d, J + 150, z, jc - 2 * NB);
-            } else if (jc == 2 * NB + 9) {
-              bv = -J[144 + z];
-            }
-          }
-        };
-        for (int st = 0; st < ks; st += 2) {  // two steps' operands loaded before their MFMAs (t >= nt: zeros)
-          double a0, b0, a1, b1;
-          operands(st, a0, b0);
-          operands(st + 1, a1, b1);
-          iacc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, iacc[u], 0, 0, 0);
-          iacc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, iacc[u], 0, 0, 0);
+      for (int u = 0; u < U; ++u) {
+        const int q = min(tid + u * 256, nall - 1);
+        if (q < nr) {
+          const int a = q / nt, t = q - a * nt;
+          v[u] = d.irec[(size_t)a * d.M + c0 + t];
+          dst[u] = t * IRS + a;
+        } else {
+          const int e = q - nr, t = e / 12;
+          v[u] = d.iw[(size_t)12 * c0 + e];
+          dst[u] = t * IRS + IRQ + (e - 12 * t);
         }
       }
+      const int tbv = tid < nt ? d.ib[c0 + tid] : 0;
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (tid + u * 256 < nall) rec[dst[u]] = v[u];
+      if (tid < nt) tb[tid] = tbv;
+    }
+    KSP_STOP(2);
+    KSP_TSB(500, 243);
+    for (int s0 = 0; s0 < nt; s0 += PNS) {
+      const int ns = min(PNS, nt - s0);
+      __syncthreads();  // records staged / the previous panel consumed
+      // one (column c, sample tt) item per thread and pass (48 x PNS = 384 items), its 6 residual rows unrolled: every
+      // candidate operand read at a clamped in-record index, the entry chosen by selects
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int item = tid + 256 * u;
+        if (item < 48 * PNS) {
+          const int tt = item / 48, c = item - 48 * tt;
+          const int t = min(s0 + tt, nt - 1);
+          const double* R = rec + t * IRS;
+          const double* w = R + IRQ;
+          const int cb = c / 6, cc = c - 6 * cb, jj = k0 + cb - tb[t], j = min(max(jj, 0), 3);
+          const bool lo = cc < 3, inj = c < 2 * NB && jj >= 0 && jj <= 3, live = tt < ns;
+          const int cr = lo ? cc : cc - 3, ci = min(max(c - 2 * NB, 0), 8), cg = min(max(ci - 6, 0), 2);
+          const double wj = w[j], w4 = w[4 + j], w8 = w[8 + j];
+#pragma unroll
+          for (int z = 0; z < 6; ++z) {
+            const int zr = z % 3;
+            double vj, vt;
+            if (z < 3) {
+              const double p1 = wj * R[3 * zr + cr], p2 = w4 * R[9 + 3 * zr + cr];
+              vj = lo ? 0.0 : -(p1 - p2) * d.ig;
+              vt = ci == z ? -d.ig : 0.0;
+            } else {
+              const double p1 = (lo ? w8 : wj) * R[(lo ? 27 : 18) + 3 * zr + cr];
+              vj = lo ? -p1 * d.ia : p1 * d.ia;
+              vt = ci < 3 ? 0.0 : ci < 6 ? (ci - 3 == zr ? -d.ia : 0.0) : R[27 + 3 * zr + cg] * d.ia;
+            }
+            const double v = c < 2 * NB ? (inj ? vj : 0.0) : c < 2 * NB + 9 ? vt : c == 2 * NB + 9 ? -R[36 + z] : 0.0;
+            P[(6 * tt + z) * PST + c] = live ? v : 0.0;
+          }
+        }
+      }
+      __syncthreads();
+      if (s0 / PNS < 4) KSP_TSB(500, 244 + 2 * (s0 / PNS));
+      const int ks = (6 * ns + 3) / 4;  // rows k >= 6 ns of the panel are zeros
+      if (wave < 3) {
+        const double* pa = P + (lane >> 4) * PST + (lane & 15);
+        const double* pb = pa + 16 * wave;
+        for (int st = 0; st < ks; st += 2) {
+          const double a0 = pa[4 * st * PST], b0 = pb[4 * st * PST];
+          const double a1 = pa[4 * (st + 1) * PST], b1 = pb[4 * (st + 1) * PST];
+          iacc = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, iacc, 0, 0, 0);
+          iacc = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, iacc, 0, 0, 0);
+        }
+      } else {
+        const int i4 = lane & 3;
+        const double* pk = P + (lane >> 4) * PST;
+        const int cb4 = 4 * ((lane >> 2) & 3) + i4;
+        for (int st = 0; st < ks; ++st) {
+          const double* row = pk + 4 * st * PST;
+          const double a = i4 < 2 ? row[16 + i4] : 0.0;
+          const double b0 = row[cb4], b1 = row[16 + cb4], b2 = row[32 + cb4];
+          iac4[0] = __builtin_amdgcn_mfma_f64_4x4x4f64(a, b0, iac4[0], 0, 0, 0);
+          iac4[1] = __builtin_amdgcn_mfma_f64_4x4x4f64(a, b1, iac4[1], 0, 0, 0);
+          iac4[2] = __builtin_amdgcn_mfma_f64_4x4x4f64(a, b2, iac4[2], 0, 0, 0);
+        }
+      }
+      if (s0 / PNS < 4 && wave == 0) KSP_TSB(500, 245 + 2 * (s0 / PNS));
     }
   }
+  KSP_STOP(3);
   __syncthreads();  // frame sums complete (they are owned per entry q, the tiles per lane)
-  // f64 MFMA C/D layout: lane l, reg r -> row (l >> 4) + 4 r, column l & 15
+  // f64 MFMA C/D layout: lane l, reg r -> row (l >> 4) + 4 r, column l & 15 (waves 0..2, columns 16 w ..);
+  // wave 3: row 16 + (l >> 4), column 16 g + (l & 15) of its 4x4x4 accumulator g
+  if (ma < mz) {
+    auto put = [&](int row, int jc, double v) {
+      if (row >= NB) return;
+      if (jc < 2 * NB)
+        out[(jc < NB ? 0 : NB * NB) + row * NB + jc % NB] += v;
+      else if (jc < 2 * NB + 9)
+        out[2 * NB * NB + row * m + d.col_imu + jc - 2 * NB] += v;
+      else if (jc == 2 * NB + 9)
+        out[2 * NB * NB + row * m + C] += v;
+    };
+    if (wave < 3) {
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int tile = wave + 4 * u;
-    if (tile < 6 && ma < mz) {
-      const int jc = 16 * (tile % 3) + (lane & 15);
+      for (int r = 0; r < 4; ++r) put((lane >> 4) + 4 * r, 16 * wave + (lane & 15), iacc[r]);
+    } else {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = 16 * (tile / 3) + (lane >> 4) + 4 * r;
-        if (row < NB) {
-          if (jc < 2 * NB)
-            out[(jc < NB ? 0 : NB * NB) + row * NB + jc % NB] += iacc[u][r];
-          else if (jc < 2 * NB + 9)
-            out[2 * NB * NB + row * m + d.col_imu + jc - 2 * NB] += iacc[u][r];
-          else if (jc == 2 * NB + 9)
-            out[2 * NB * NB + row * m + C] += iacc[u][r];
-        }
-      }
+      for (int g = 0; g < 3; ++g) put(16 + (lane >> 4), 16 * g + (lane & 15), iac4[g]);
     }
   }
   __syncthreads();
@@ -932,6 +993,7 @@ __global__ void __launch_bounds__(256) k_sp_assemble(SpDev d) {
     __syncthreads();
   }
   if (d.cq && tid == 0) d.mcost[i] = node_cost;
+  KSP_TSB(500, 252);
   // padded rows (coefficients >= K): identity diagonal, no coupling
   for (int q = tid; q < nout; q += nth) {
     double v = out[q];
@@ -966,7 +1028,16 @@ __global__ void __launch_bounds__(64) k_sp_imu_cc(SpDev d) {
     d.sc[SC_LAM2] = 0.0;
     d.sc[SC_OK] = 1.0;
   }
-  if (has) imu_sample(d, m, e, nullptr, Ct);
+  double T[27];
+  if (has) {
+    imu_sample(d, m, e, T, Ct);
+#pragma unroll
+    for (int q = 0; q < 27; ++q) d.irec[(size_t)q * d.M + m] = T[q];  // field-major: coalesced over the wave
+#pragma unroll
+    for (int q = 0; q < 9; ++q) d.irec[(size_t)(27 + q) * d.M + m] = Ct[q];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) d.irec[(size_t)(36 + q) * d.M + m] = e[q];
+  }
   // J_theta = [-ig I, 0, 0; 0, -ia I, ia C^T] (rows gyro | accel; columns b_g | b_a | g_w)
   const double ig2 = d.ig * d.ig, ia2 = d.ia * d.ia;
   int q = 0;
@@ -3132,7 +3203,7 @@ kb_sp_handle* kb_sp_create(const kb_sp_layout* L) {
     h->back2 = !(ev && std::atoi(ev) == 0);
   }
   h->lds_schur = sizeof(double) * (2 * NB * d.m + d.Ws) + sizeof(short2) * d.Ws;
-  h->lds_asm = sizeof(double) * (2 * NB * NB + NB * d.m + std::max(TCH * IST, TCF * d.FHS));
+  h->lds_asm = sizeof(double) * (2 * NB * NB + NB * d.m + std::max(TCH * IRS + 6 * PNS * PST, TCF * d.FHS));
   h->lds_frames = sizeof(double) * (h->N * 64 * XS + h->N * 256 + 2 * h->N * 36 + 2 * h->N * h->N * 36 + d.Wc +
                                     3 * L->n_target) +
                   sizeof(short2) * d.Wc + sizeof(int) * 3 * d.C;
@@ -3282,6 +3353,7 @@ int kb_sp_upload(kb_sp_handle* h, int32_t n_frames, const double* frame_time, in
   rc |= h->alloc(&d.cpart, (size_t)(d.nblk_f + d.nblk_ci + d.nblk_q));
   rc |= h->alloc(&d.mcost, (size_t)h->n);
   rc |= h->alloc(&d.ipart, (size_t)d.nblk_ic * WI);
+  rc |= h->alloc(&d.irec, (size_t)IRQ * std::max(M, 1));
   if (rc) return -1;
   if (n_corners) {
     KSP_HIP(hipMemcpyAsync(dy, y, sizeof(double) * 2 * n_corners, hipMemcpyHostToDevice, h->stream));

@@ -1,0 +1,27 @@
+"""Diagnostic: k_sp_assemble timeline of block 500 (KSP_TSB slots 241..252, s_memrealtime 100 MHz) over one GN pass
+at configs[4], diagnostic library only: python tools/diag_sp_asm.py"""
+import ctypes as C
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from kalibr_amd import capi, synth  # noqa: E402
+
+capi.LIB_PATH = os.path.join(ROOT, "kalibr_amd", "libkalibr_hip_stamps.so")
+L = capi.lib()
+L.kb_sp_diag_read_ts.argtypes = [C.c_void_p, C.POINTER(C.c_longlong), C.c_int]
+p = synth.make_spline_config()
+g = capi.SplineSolver(p)
+g.set_state(p.state_init)
+buf = (C.c_longlong * 256)()
+names = ["entry", "frames done", "records staged"] + [f"panel {j} {w}" for j in range(4) for w in ("built", "MFMA done")] + ["end"]
+for rep in range(3):
+    g.run_gn(2)
+    assert L.kb_sp_diag_read_ts(g.h, buf, 256) == 0
+    t0 = buf[241]
+    print(f"rep {rep} k_sp_assemble block 500:")
+    for k, nm in enumerate(names):
+        v = (buf[241 + k] - t0) / 100
+        if 0 <= v < 1e4:
+            print(f"  {nm:20s} {v:8.2f} us")
