@@ -35,12 +35,12 @@
 // timeline stamp (100 MHz s_memrealtime) of thread 0 of block 0 at slot i (tools/diag_sp_ts.py)
 #define KSP_TS(i)                                                                                          \
   do {                                                                                                     \
-    if (blockIdx.x == 0 && threadIdx.x == 0 && d.dbg_ts && (i) < 256) d.dbg_ts[i] = __builtin_amdgcn_s_memrealtime(); \
+    if (blockIdx.x == 0 && threadIdx.x == 0 && d.dbg_ts && (i) < 320) d.dbg_ts[i] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
 // the same for thread 0 of block b
 #define KSP_TSB(b, i)                                                                                      \
   do {                                                                                                     \
-    if (blockIdx.x == (b) && threadIdx.x == 0 && d.dbg_ts && (i) < 256) d.dbg_ts[i] = __builtin_amdgcn_s_memrealtime(); \
+    if (blockIdx.x == (b) && threadIdx.x == 0 && d.dbg_ts && (i) < 320) d.dbg_ts[i] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
 #else
 #define KSP_TSB(b, i) \
@@ -130,7 +130,7 @@ struct SpDev {
   const double* pp;       // [npos][3] prior
   const double* pW;       // [npos][9] invR
   const int* node_pp;     // [n][4] priors touching node i (b in [3i-3, 3i+2]) | owned by it (b in [3i, 3i+2])
-  long long* dbg_ts;      // diagnostics only: [256] KSP_TS stamps
+  long long* dbg_ts;      // diagnostics only: [320] KSP_TS stamps
   int dbg_stop;           // diagnostics only (KSP_DBG_STOP): 0, or the phase after which the timed kernels return
   int zero_lam;           // GN pass: k_sp_imu_cc sets lambda^2 = 0 (no separate launch)
   // round 6: the Schur complement from the forward reduction alone (S = H_tt - sum_i Z_R,i^T Z_R,i over every node's
@@ -313,8 +313,7 @@ __global__ void __launch_bounds__(512) k_sp_frames(SpDev d) {
   double* Pv = Gv + N * 36;        // [N][36]
   double* Gp = Pv + N * 36;        // [N][N][36]
   double* Qp = Gp + N * N * 36;    // [N][N][36]
-  double* acc = Qp + N * N * 36;   // [Wc] theta-theta accumulators
-  double* tg = acc + d.Wc;         // [n_target][3]
+  double* tg = Qp + N * N * 36;    // [n_target][3]
   // frame-independent column tables, read per entry of every frame: (a, b) of the theta-theta entries and
   // column -> (kind, index, sub) (a load per entry and frame otherwise puts a dependent round trip in each
   // iteration of the per-frame loops)
@@ -322,13 +321,13 @@ __global__ void __launch_bounds__(512) k_sp_frames(SpDev d) {
   int* tck = (int*)(tuab + d.Wc);                 // [C] kind | [C] index | [C] sub
   int* tci = tck + C;
   int* tcs = tci + C;
+  __shared__ double tz[12];  // zeros | unit vector e1
   const int cam = wave;
   const double* st = d.state;
+  KSP_TSB(300, 256);  // diagnostics: block 300's timeline in slots 256..271 (tools/diag_sp_asm.py)
   for (int q = tid; q < 3 * d.n_target; q += nth) tg[q] = d.target[q];
-  for (int q = tid; q < d.Wc; q += nth) {
-    acc[q] = 0.0;
-    tuab[q] = d.uab[q];
-  }
+  for (int q = tid; q < d.Wc; q += nth) tuab[q] = d.uab[q];
+  if (tid < 12) tz[tid] = tid == 6 ? 1.0 : 0.0;
   for (int q = tid; q < C; q += nth) {
     tck[q] = d.ckind[q];
     tci[q] = d.cidx[q];
@@ -376,10 +375,29 @@ __global__ void __launch_bounds__(512) k_sp_frames(SpDev d) {
     tA[2] = t2[2];
   }
   __syncthreads();  // target, accumulators and Gp staged
+  KSP_TSB(300, 257);
   const int model = sp_cam_arg(d.model, cam), nin = sp_cam_arg(d.nin, cam);
   const double* intr = st + cam * KB_MAX_INTR;
   const int mrow = lane >> 4, mcol = lane & 15;
   const int f0 = blockIdx.x * FPB, f1 = min(d.F, f0 + FPB);
+  // The entries of the frame's spline side and of the block's camera side are sums over the views i of 6-term products
+  // x[r xs] y[r ys] (the 12 reads issued before one fma chain), with the operands of each (entry, view) picked by selects
+  // rather than branches: a single H entry is x = H[.] (stride 0) against the unit vector e1, a term the view does not
+  // have is x = the zero vector
+  const double* Z0 = tz;      // [6] zeros
+  const double* E1 = tz + 6;  // [6] 1, 0, 0, 0, 0, 0
+  auto dot6 = [&](const double* x, int xs, const double* y, int ys, double s) {
+    double xv[6], yv[6];
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+      xv[r] = x[r * xs];
+      yv[r] = y[r * ys];
+    }
+#pragma unroll
+    for (int r = 0; r < 6; ++r) s += xv[r] * yv[r];
+    return s;
+  };
+  v4d_t hs = {0.0, 0.0, 0.0, 0.0};  // this lane's entries of its view's H summed over the block's frames
   for (int f = f0; f < f1; ++f) {
     // spline pose at t_f (uniform across the block)
     const int b = d.fb[f];
@@ -441,6 +459,7 @@ __global__ void __launch_bounds__(512) k_sp_frames(SpDev d) {
           Gv[cam * 36 + r * 6 + c] = -s;
         }
     }
+    KSP_TSB(300, 258 + 6 * (f - f0));
     // corners of view (f, cam): [J_delta | J_intr | -e] rows, SYRK on MFMA
     const int2 fv = d.fview[(size_t)f * N + cam];
     v4d_t acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
@@ -499,8 +518,14 @@ __global__ void __launch_bounds__(512) k_sp_frames(SpDev d) {
     }
     // f64 MFMA C/D layout: lane l, reg r -> row (l >> 4) + 4 r, col l & 15
 #pragma unroll
-    for (int r = 0; r < 4; ++r) Hv[cam * 256 + (mrow + 4 * r) * 16 + mcol] = acc0[r] + acc1[r];
+    for (int r = 0; r < 4; ++r) {
+      const double h = acc0[r] + acc1[r];
+      Hv[cam * 256 + (mrow + 4 * r) * 16 + mcol] = h;
+      hs[r] += h;
+    }
+    KSP_TSB(300, 259 + 6 * (f - f0));
     __syncthreads();
+    KSP_TSB(300, 260 + 6 * (f - f0));
     // P_i = H_dd,i G_v,i ; Q_i[q] = H_dd,i Gp[i][q]
     for (int q = tid; q < N * 36 + N * N * 36; q += nth) {
       const bool isP = q < N * 36;
@@ -518,81 +543,85 @@ __global__ void __launch_bounds__(512) k_sp_frames(SpDev d) {
         Qp[qq] = s;
     }
     __syncthreads();
+    KSP_TSB(300, 261 + 6 * (f - f0));
     // spline side of the frame: [H_vv | H_vtheta | g_v]
     double* out = d.FH + (size_t)f * d.FHS;
     for (int q = tid; q < d.FHS; q += nth) {
       double s = 0.0;
-      if (q < 36) {
-        const int a = q / 6, bb = q % 6;
-        for (int i = 0; i < N; ++i)
-#pragma unroll
-          for (int r = 0; r < 6; ++r) s += Gv[i * 36 + r * 6 + a] * Pv[i * 36 + r * 6 + bb];
-      } else if (q < 36 + 6 * C) {
-        const int a = (q - 36) / C, col = (q - 36) % C;
-        const int kind = tck[col], idx = tci[col], sub = tcs[col];
-        for (int i = 0; i < N; ++i) {
-          if (kind == 0 && idx == i) {
-#pragma unroll
-            for (int r = 0; r < 6; ++r) s += Gv[i * 36 + r * 6 + a] * Hv[i * 256 + r * 16 + 6 + sub];
-          } else if (kind == 1 && (idx == N - 1 || idx < i)) {
-#pragma unroll
-            for (int r = 0; r < 6; ++r) s += Gv[i * 36 + r * 6 + a] * Qp[(i * N + idx) * 36 + r * 6 + sub];
-          }
-        }
-      } else {
-        const int a = q - 36 - 6 * C;
-        for (int i = 0; i < N; ++i)
-#pragma unroll
-          for (int r = 0; r < 6; ++r) s += Gv[i * 36 + r * 6 + a] * Hv[i * 256 + r * 16 + 15];
+      const bool vv = q < 36, vt = !vv && q < 36 + 6 * C;
+      const int a = vv ? q / 6 : vt ? (q - 36) / C : q - 36 - 6 * C;
+      const int col = vt ? (q - 36) % C : 0, bb = q % 6;
+      const int kind = tck[col], idx = tci[col], sub = tcs[col];
+      for (int i = 0; i < N; ++i) {
+        const double* G = Gv + i * 36 + a;
+        const double* H = Hv + i * 256;
+        const bool in0 = kind == 0 && idx == i, in1 = kind == 1 && (idx == N - 1 || idx < i);
+        const double* y = vv ? Pv + i * 36 + bb
+                             : !vt ? H + 15 : in0 ? H + 6 + sub : in1 ? Qp + (i * N + idx) * 36 + sub : Z0;
+        const int ys = vv ? 6 : (!vt || in0) ? 16 : in1 ? 6 : 1;
+        s = dot6(G, 6, y, ys, s);
       }
       out[q] = s;
     }
-    // camera side: theta-theta upper | g_theta | cost
-    const int nup = C * (C + 1) / 2;
-    for (int q = tid; q < d.Wc; q += nth) {
-      double s = 0.0;
-      if (q < nup) {
-        const short2 ab = tuab[q];
-        const int a = ab.x, bcol = ab.y;
-        const int ka = tck[a], ia = tci[a], sa = tcs[a];
-        const int kb2 = tck[bcol], ib2 = tci[bcol], sb = tcs[bcol];
-        for (int i = 0; i < N; ++i) {
-          const bool okA = (ka == 0 && ia == i) || (ka == 1 && (ia == N - 1 || ia < i));
-          const bool okB = (kb2 == 0 && ib2 == i) || (kb2 == 1 && (ib2 == N - 1 || ib2 < i));
-          if (!okA || !okB) continue;
-          const double* H = Hv + i * 256;
-          if (ka == 0 && kb2 == 0) {
-            s += H[(6 + sa) * 16 + 6 + sb];
-          } else if (ka == 1 && kb2 == 1) {
-#pragma unroll
-            for (int r = 0; r < 6; ++r) s += Gp[(i * N + ia) * 36 + r * 6 + sa] * Qp[(i * N + ib2) * 36 + r * 6 + sb];
-          } else if (ka == 1) {  // pose a, intr b
-#pragma unroll
-            for (int r = 0; r < 6; ++r) s += Gp[(i * N + ia) * 36 + r * 6 + sa] * H[r * 16 + 6 + sb];
-          } else {  // intr a, pose b
-#pragma unroll
-            for (int r = 0; r < 6; ++r) s += H[r * 16 + 6 + sa] * Gp[(i * N + ib2) * 36 + r * 6 + sb];
-          }
-        }
-      } else if (q < nup + C) {
-        const int a = q - nup, ka = tck[a], ia = tci[a], sa = tcs[a];
-        for (int i = 0; i < N; ++i) {
-          const double* H = Hv + i * 256;
-          if (ka == 0 && ia == i) {
-            s += H[(6 + sa) * 16 + 15];
-          } else if (ka == 1 && (ia == N - 1 || ia < i)) {
-#pragma unroll
-            for (int r = 0; r < 6; ++r) s += Gp[(i * N + ia) * 36 + r * 6 + sa] * H[r * 16 + 15];
-          }
-        }
-      } else {
-        for (int i = 0; i < N; ++i) s += Hv[i * 256 + 255];
-      }
-      acc[q] += s;
-    }
-    __syncthreads();
+    KSP_TSB(300, 262 + 6 * (f - f0));
+    __syncthreads();  // the frame's Gv, Hv, Pv, Qp consumed
+    KSP_TSB(300, 263 + 6 * (f - f0));
   }
-  for (int q = tid; q < d.Wc; q += nth) d.part[(size_t)blockIdx.x * d.Wc + q] = acc[q];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) Hv[cam * 256 + (mrow + 4 * r) * 16 + mcol] = hs[r];
+  __syncthreads();
+  for (int qq = tid; qq < N * N * 36; qq += nth) {  // Q_i[q] = H_dd,i Gp[i][q] of the summed H
+    const int i = qq / (N * 36), e = qq % 36, r = e / 6, c = e % 6;
+    const double* G = Gp + (qq / 36) * 36;
+    const double* H = Hv + i * 256;
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) s += H[r * 16 + k] * G[k * 6 + c];
+    Qp[qq] = s;
+  }
+  __syncthreads();
+  KSP_TSB(300, 271);
+  // camera side of the block: theta-theta upper | g_theta | cost.  Linear in each view's H (the maps Gp are frame
+  // independent), so it is formed once from the views' H summed over the block's frames (per frame it cost ~5-9 us of
+  // LDS round trips)
+  const int nup = C * (C + 1) / 2;
+  for (int q = tid; q < d.Wc; q += nth) {
+    double s = 0.0;
+    const bool up = q < nup, gt = !up && q < nup + C;
+    const short2 ab = tuab[up ? q : 0];
+    const int a = up ? ab.x : q - nup, bcol = up ? ab.y : 0;
+    const int ka = tck[a], ia = tci[a], sa = tcs[a];
+    const int kb2 = tck[bcol], ib2 = tci[bcol], sb = tcs[bcol];
+    for (int i = 0; i < N; ++i) {
+      const double* H = Hv + i * 256;
+      const bool okA = (ka == 0 && ia == i) || (ka == 1 && (ia == N - 1 || ia < i));
+      const bool okB = (kb2 == 0 && ib2 == i) || (kb2 == 1 && (ib2 == N - 1 || ib2 < i));
+      const double* GA = Gp + (i * N + ia) * 36 + sa;
+      const double* x;
+      const double* y;
+      int xs, ys;
+      if (up) {  // (pose | intr) x (pose | intr)
+        const bool pa = ka == 1, pb = kb2 == 1;
+        x = !(okA && okB) ? Z0 : pa ? GA : (pb ? H + 6 + sa : H + (6 + sa) * 16 + 6 + sb);
+        xs = !(okA && okB) ? 1 : pa ? 6 : (pb ? 16 : 0);
+        y = pa ? (pb ? Qp + (i * N + ib2) * 36 + sb : H + 6 + sb) : (pb ? Gp + (i * N + ib2) * 36 + sb : E1);
+        ys = pa ? (pb ? 6 : 16) : (pb ? 6 : 1);
+      } else if (gt) {  // g_theta: intr a -> H[6 + sa][15]; pose a -> Gp^T H[.][15]
+        x = !okA ? Z0 : ka == 1 ? GA : H + (6 + sa) * 16 + 15;
+        xs = !okA ? 1 : ka == 1 ? 6 : 0;
+        y = ka == 1 ? H + 15 : E1;
+        ys = ka == 1 ? 16 : 1;
+      } else {  // cost
+        x = H + 255;
+        xs = 0;
+        y = E1;
+        ys = 1;
+      }
+      s = dot6(x, xs, y, ys, s);
+    }
+    d.part[(size_t)blockIdx.x * d.Wc + q] = s;
+  }
+  KSP_TSB(300, 270);
 }
 
 // ---------------------------------------------------------------- IMU sample (defined in DESIGN.md 10)
@@ -3204,7 +3233,7 @@ kb_sp_handle* kb_sp_create(const kb_sp_layout* L) {
   }
   h->lds_schur = sizeof(double) * (2 * NB * d.m + d.Ws) + sizeof(short2) * d.Ws;
   h->lds_asm = sizeof(double) * (2 * NB * NB + NB * d.m + std::max(TCH * IRS + 6 * PNS * PST, TCF * d.FHS));
-  h->lds_frames = sizeof(double) * (h->N * 64 * XS + h->N * 256 + 2 * h->N * 36 + 2 * h->N * h->N * 36 + d.Wc +
+  h->lds_frames = sizeof(double) * (h->N * 64 * XS + h->N * 256 + 2 * h->N * 36 + 2 * h->N * h->N * 36 +
                                     3 * L->n_target) +
                   sizeof(short2) * d.Wc + sizeof(int) * 3 * d.C;
   if (h->lds_frames > 160 * 1024 || h->lds_asm > 160 * 1024 || h->lds_schur > 160 * 1024) {
@@ -3348,7 +3377,7 @@ int kb_sp_upload(kb_sp_handle* h, int32_t n_frames, const double* frame_time, in
   d.nblk_q = (h->n + 63) / 64;
 #ifdef KB_STAMPS
   if (const char* e = std::getenv("KSP_DBG_STOP")) d.dbg_stop = std::atoi(e);  // diagnostic build only
-  if (!d.dbg_ts) rc |= h->alloc(&d.dbg_ts, 256);
+  if (!d.dbg_ts) rc |= h->alloc(&d.dbg_ts, 320);
 #endif
   rc |= h->alloc(&d.cpart, (size_t)(d.nblk_f + d.nblk_ci + d.nblk_q));
   rc |= h->alloc(&d.mcost, (size_t)h->n);
@@ -3946,7 +3975,7 @@ int kb_sp_kernel_stats(kb_sp_handle* h, int32_t n, double* ms_out6, double* fram
 extern "C" int kb_sp_diag_read_ts(kb_sp_handle* h, long long* out, int n) {
   if (!h->d.dbg_ts) return fail("kb_sp_diag_read_ts: no stamp buffer");
   KSP_HIP(hipStreamSynchronize(h->stream));
-  KSP_HIP(hipMemcpy(out, h->d.dbg_ts, sizeof(long long) * std::min(n, 256), hipMemcpyDeviceToHost));
+  KSP_HIP(hipMemcpy(out, h->d.dbg_ts, sizeof(long long) * std::min(n, 320), hipMemcpyDeviceToHost));
   return 0;
 }
 #endif
