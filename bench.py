@@ -158,7 +158,11 @@ def main_spline(args):
                      "traffic": (pmc[0] / (asm_ms * 1e-3) / 1e9) if pmc else None,
                      "traffic_bytes_per_launch": pmc[0] if pmc else None, "traffic_source": pmc[1] if pmc else None,
                      "avg_ms": asm_ms, "algorithmic_bytes": asm_bytes,
-                     "frames_kernel": {"avg_ms": ks["frames_ms"], "algorithmic_bytes": ks["frames_bytes"]}},
+                     "frames_kernel": {"avg_ms": ks["frames_ms"], "algorithmic_bytes": ks["frames_bytes"]},
+                     # what bounds the pass: the block cyclic reduction (forward levels, Schur sums, the one-column
+                     # back substitution) is a chain of dependent small launches, latency- not byte-bound
+                     "reduction_chain": {"avg_ms": ks["reduction_ms"], "share_of_pass": ks["reduction_ms"] / ks["pass_ms"],
+                                         "bound": "dependent launch chain (per-level latency)"}},
         "pass_breakdown_ms": {k: v for k, v in ks.items() if k.endswith("_ms")},
     }
     if not args.no_cpu_baseline:

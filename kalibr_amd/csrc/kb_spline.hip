@@ -3904,9 +3904,9 @@ int kb_sp_assemble_stats(kb_sp_handle* h, int32_t n, double* ms, double* bytes) 
   hipEventDestroy(e1);
   *ms = acc / n;
   // algorithmic bytes, each once: the frames' spline blocks (FHS doubles) with their basis (4 weights + index), the
-  // IMU samples (12 weights, 6 measurements, index), the coefficients and camera / IMU state, the node tables, the
-  // node blocks D0, U0, R0 written (+ the motion-error blocks when active)
-  *bytes = 8.0 * h->F * (d.FHS + 4) + 4.0 * h->F + h->M * (8.0 * 18 + 4.0) + 8.0 * d.S + 16.0 * h->n +
+  // IMU samples (k_sp_imu_cc's record of IRQ doubles, 12 weights, index), the coefficients and camera / IMU state, the
+  // node tables, the node blocks D0, U0, R0 written (+ the motion-error blocks when active)
+  *bytes = 8.0 * h->F * (d.FHS + 4) + 4.0 * h->F + h->M * (8.0 * (IRQ + 12) + 4.0) + 8.0 * d.S + 16.0 * h->n +
            8.0 * h->n * (2 * NB * NB + NB * d.m) + (d.mot ? 8.0 * h->n * 2 * NB * NB : 0.0);
   h->built = h->solved = false;
   return 0;
