@@ -36,6 +36,7 @@ GN_FUSED = os.environ.get("KB_GN_FUSED", "1") != "0"  # the library's pass varia
 def is_build_kernel(name):
     """The pass's build kernel as rocprofv3 names it: k_build<TW, GNF, MM> or the pipelined k_buildp<TT, GNF, MM>
     (rigs with one wave per camera), with GNF = the GN fused variant (MM = the rig's camera-model set)."""
+    name = name.replace("(anonymous namespace)::", "")  # the per-model-set build TUs (kb_build_tu.hip)
     for pre in ("void kb::k_build<", "void kb::k_buildp<"):
         if name.startswith(pre) and name.endswith(">(kb::KbDev, int, int)"):
             args = name[len(pre):-len(">(kb::KbDev, int, int)")].split(", ")

@@ -601,16 +601,18 @@ __global__ void __launch_bounds__(512) k_sp_frames(SpDev d) {
       const double* y;
       int xs, ys;
       if (up) {  // (pose | intr) x (pose | intr)
-        const bool pa = ka == 1, pb = kb2 == 1;
-        x = !(okA && okB) ? Z0 : pa ? GA : (pb ? H + 6 + sa : H + (6 + sa) * 16 + 6 + sb);
-        xs = !(okA && okB) ? 1 : pa ? 6 : (pb ? 16 : 0);
-        y = pa ? (pb ? Qp + (i * N + ib2) * 36 + sb : H + 6 + sb) : (pb ? Gp + (i * N + ib2) * 36 + sb : E1);
-        ys = pa ? (pb ? 6 : 16) : (pb ? 6 : 1);
+        // an absent term reads zeros on both sides: Gp holds only the pairs (cam, q < cam | N - 1), the rest of its
+        // LDS is whatever the last kernel left there (0 x NaN would poison the sum)
+        const bool pa = ka == 1, pb = kb2 == 1, live = okA && okB;
+        x = !live ? Z0 : pa ? GA : (pb ? H + 6 + sa : H + (6 + sa) * 16 + 6 + sb);
+        xs = !live ? 1 : pa ? 6 : (pb ? 16 : 0);
+        y = !live ? Z0 : pa ? (pb ? Qp + (i * N + ib2) * 36 + sb : H + 6 + sb) : (pb ? Gp + (i * N + ib2) * 36 + sb : E1);
+        ys = !live ? 1 : pa ? (pb ? 6 : 16) : (pb ? 6 : 1);
       } else if (gt) {  // g_theta: intr a -> H[6 + sa][15]; pose a -> Gp^T H[.][15]
         x = !okA ? Z0 : ka == 1 ? GA : H + (6 + sa) * 16 + 15;
         xs = !okA ? 1 : ka == 1 ? 6 : 0;
-        y = ka == 1 ? H + 15 : E1;
-        ys = ka == 1 ? 16 : 1;
+        y = !okA ? Z0 : ka == 1 ? H + 15 : E1;
+        ys = !okA || ka != 1 ? 1 : 16;
       } else {  // cost
         x = H + 255;
         xs = 0;
@@ -716,7 +718,12 @@ __device__ void imu_sample(const SpDev& d, int m, double* e, double* T, double* 
 // node.
 __global__ void __launch_bounds__(256) k_sp_assemble(SpDev d) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
-  const int i = blockIdx.x, tid = threadIdx.x, nth = blockDim.x, C = d.C, m = d.m;
+  // XCD-aware node order: blocks are dealt to the 8 XCDs round-robin (block b on XCD b % 8), and a frame or an IMU sample
+  // is read by the two neighbouring nodes, so each XCD takes a contiguous run of nodes (node i + 1 on the same L2 as
+  // node i, one block later) instead of neighbours on different XCDs fetching the same rows twice from HBM
+  const int nn = gridDim.x, xcd = blockIdx.x & 7, q8 = nn >> 3, r8 = nn & 7;
+  const int i = xcd * q8 + min(xcd, r8) + (blockIdx.x >> 3);
+  const int tid = threadIdx.x, nth = blockDim.x, C = d.C, m = d.m;
   const int nout = 2 * NB * NB + NB * m;
   double* out = sm;                       // [nout]
   // frame chunk [TCF][FHS] (FH rows) | IMU records [TCH][IRS] + operand panel [6 PNS][PST] share one region: a node

@@ -13,8 +13,8 @@ from collections import defaultdict
 def per_kernel(path, counter):
     acc = defaultdict(list)
     for r in csv.DictReader(open(path)):
-        if r["Counter_Name"] == counter:
-            acc[r["Kernel_Name"]].append(float(r["Counter_Value"]))
+        if r["Counter_Name"] == counter:  # the build TUs' kernels sit in an anonymous namespace
+            acc[r["Kernel_Name"].replace("(anonymous namespace)::", "")].append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in acc.items()}, {k: len(v) for k, v in acc.items()}
 
 

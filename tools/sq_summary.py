@@ -13,8 +13,9 @@ for sub in ("pmc_sq1", "pmc_sq2", "pmc_sq3"):
     except OSError:
         continue
     for r in rows:
-        if r["Kernel_Name"].startswith(("kb::", "void kb::")):
-            acc[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        name = r["Kernel_Name"].replace("(anonymous namespace)::", "")  # the build TUs' kernels
+        if name.startswith(("kb::", "void kb::")):
+            acc[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
 res = {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in acc.items()}
 json.dump({"workload": wl, "note": "per-dispatch averages; SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_* in quad-cycles, "
            "SQ_VALU_MFMA_BUSY_CYCLES in cycles", "kernels": res}, open(out, "w"), indent=1)
