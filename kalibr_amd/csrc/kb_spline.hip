@@ -102,7 +102,7 @@ struct SpDev {
   double* backup;
   double* FH;             // [F][FHS]: H_vv (36) | H_vtheta (6 C) | g_v (6)
   double* part;           // [nblk_f][Wc] theta-theta partial rows of the frames
-  double* ipart;          // [nblk_ci][WI]
+  double* ipart;          // [nblk_ic][WI]
   double* Hcc;            // [C][C] | gc [C] | cost
   double *D0, *U0, *R0;   // built node blocks [n][324], [n][324], [n][18 m]
   double *D, *U, *R;      // working copies (cyclic reduction in place)
@@ -302,12 +302,19 @@ __device__ __forceinline__ double bt_basic(const double* R, const double* t, con
 // 16 x 16 local Hessian of [J_delta | J_intr | -e] by f64 MFMA SYRK through an LDS tile; then the frame's
 // spline-side blocks (H_vv, H_vtheta, g_v in the curve-value coordinates v, JT folded in) to HBM and the
 // camera-side (theta-theta) sums into the block's partial row.
+__device__ __forceinline__ void imu_cc_wave(const SpDev& d, int blk, int lane, double* X);
+
 template <unsigned MM>
 __global__ void __launch_bounds__(512) k_sp_frames(SpDev d) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const int N = d.N, C = d.C, nth = blockDim.x, tid = threadIdx.x;
   const int wave = tid >> 6, lane = tid & 63;
   double* Xw = sm + wave * 64 * XS;
+  if ((int)blockIdx.x >= d.nblk_f) {  // the extra blocks: k_sp_imu_cc's work, one of its 64-sample blocks per wave
+    const int blk = ((int)blockIdx.x - d.nblk_f) * N + wave;
+    if (blk < d.nblk_ic) imu_cc_wave(d, blk, lane, Xw);
+    return;
+  }
   double* Hv = sm + N * 64 * XS;   // [N][256]
   double* Gv = Hv + N * 256;       // [N][36]
   double* Pv = Gv + N * 36;        // [N][36]
@@ -1055,9 +1062,11 @@ __global__ void __launch_bounds__(256) k_sp_assemble(SpDev d) {
 // ---------------------------------------------------------------- IMU theta-theta (b_g | b_a | g_w)
 // 64 samples per block (one wave): each lane's J_theta^T J_theta upper (45), -J_theta^T e (9), e^T e staged in
 // LDS, summed per entry in sample order -> one partial row [WI].
-__global__ void __launch_bounds__(64) k_sp_imu_cc(SpDev d) {
-  __shared__ double v[64][WI + 1];
-  const int lane = threadIdx.x, m = blockIdx.x * 64 + lane;
+// k_sp_imu_cc's work for its block blk (64 samples) on one wave: the samples' records for k_sp_assemble and the partial
+// row [WI] of their theta-theta terms, each entry summed over the 64 samples in order through the wave's 64 x XS LDS
+// tile X, 16 entries at a time.  Run by k_sp_imu_cc and by the extra blocks of k_sp_frames (one launch less per pass).
+__device__ __forceinline__ void imu_cc_wave(const SpDev& d, int blk, int lane, double* X) {
+  const int m = blk * 64 + lane;
   double e[6] = {0, 0, 0, 0, 0, 0}, Ct[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
   const bool has = m < d.M;
   if (d.zero_lam && m == 0) {  // k_sp_set_lam(0) of a GN pass, before the reduction reads it (same stream)
@@ -1074,6 +1083,7 @@ __global__ void __launch_bounds__(64) k_sp_imu_cc(SpDev d) {
 #pragma unroll
     for (int q = 0; q < 6; ++q) d.irec[(size_t)(36 + q) * d.M + m] = e[q];
   }
+  double v[WI];
   // J_theta = [-ig I, 0, 0; 0, -ia I, ia C^T] (rows gyro | accel; columns b_g | b_a | g_w)
   const double ig2 = d.ig * d.ig, ia2 = d.ia * d.ia;
   int q = 0;
@@ -1088,7 +1098,7 @@ __global__ void __launch_bounds__(64) k_sp_imu_cc(SpDev d) {
         t = (b == a) ? ia2 : (b >= 6 ? -ia2 * Ct[(a - 3) * 3 + (b - 6)] : 0.0);
       else
         t = (b == a) ? ia2 : 0.0;  // (C^T)^T C^T = I
-      v[lane][q] = has ? t : 0.0;
+      v[q] = has ? t : 0.0;
     }
 #pragma unroll
   for (int a = 0; a < 9; ++a) {
@@ -1100,15 +1110,27 @@ __global__ void __launch_bounds__(64) k_sp_imu_cc(SpDev d) {
     } else {
       t = -d.ia * (Ct[0 * 3 + (a - 6)] * e[3] + Ct[1 * 3 + (a - 6)] * e[4] + Ct[2 * 3 + (a - 6)] * e[5]);
     }
-    v[lane][45 + a] = has ? t : 0.0;
+    v[45 + a] = has ? t : 0.0;
   }
-  v[lane][54] = has ? ((e[0] * e[0] + e[1] * e[1]) + (e[2] * e[2] + e[3] * e[3])) + (e[4] * e[4] + e[5] * e[5]) : 0.0;
-  __syncthreads();
-  if (lane < WI) {
-    double s = 0.0;
-    for (int k = 0; k < 64; ++k) s += v[k][lane];
-    d.ipart[(size_t)blockIdx.x * WI + lane] = s;
+  v[54] = has ? ((e[0] * e[0] + e[1] * e[1]) + (e[2] * e[2] + e[3] * e[3])) + (e[4] * e[4] + e[5] * e[5]) : 0.0;
+#pragma unroll
+  for (int q0 = 0; q0 < WI; q0 += 16) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      if (q0 + j < WI) X[lane * XS + j] = v[q0 + j];
+    KSP_WAVE_SYNC();
+    if (lane < 16 && q0 + lane < WI) {
+      double s = 0.0;
+      for (int k = 0; k < 64; ++k) s += X[k * XS + lane];
+      d.ipart[(size_t)blk * WI + q0 + lane] = s;
+    }
+    KSP_WAVE_SYNC();  // the tile is rewritten by the next 16 entries
   }
+}
+
+__global__ void __launch_bounds__(64) k_sp_imu_cc(SpDev d) {
+  __shared__ double X[64 * XS];
+  imu_cc_wave(d, blockIdx.x, threadIdx.x, X);
 }
 
 // ---------------------------------------------------------------- k_sp_reduce_cc: H_cc, g_c, cost
@@ -2546,6 +2568,26 @@ template <unsigned MM>
 __global__ void __launch_bounds__(512) k_sp_cost_frames(SpDev d) {
   __shared__ double red[8];
   const int N = d.N, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, cam = wave;
+  if ((int)blockIdx.x >= d.nblk_f) {  // the extra blocks: the IMU samples' chi^2, 64 N samples per block
+    const int m = ((int)blockIdx.x - d.nblk_f) * 64 * N + tid;
+    double s = 0.0;
+    if (m < d.M) {
+      double e[6], Ct[9];
+      imu_sample(d, m, e, nullptr, Ct);
+#pragma unroll
+      for (int r = 0; r < 6; ++r) s += e[r] * e[r];
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    if (lane == 0) red[wave] = s;
+    __syncthreads();
+    if (tid == 0) {
+      double t = 0.0;
+      for (int q = 0; q < N; ++q) t += red[q];
+      d.cpart[blockIdx.x] = t;  // cpart[nblk_f + IMU block]
+    }
+    return;
+  }
   const double* st = d.state;
   double RA[9], tA[3];
   kb::quat2r(st + d.off_cb, RA);
@@ -2612,23 +2654,6 @@ __global__ void __launch_bounds__(512) k_sp_cost_frames(SpDev d) {
     for (int q = 0; q < N; ++q) t += red[q];
     d.cpart[blockIdx.x] = t;
   }
-}
-
-__global__ void __launch_bounds__(256) k_sp_cost_imu(SpDev d) {
-  __shared__ double red[4];
-  const int tid = threadIdx.x, m = blockIdx.x * 256 + tid;
-  double s = 0.0;
-  if (m < d.M) {
-    double e[6], Ct[9];
-    imu_sample(d, m, e, nullptr, Ct);
-#pragma unroll
-    for (int r = 0; r < 6; ++r) s += e[r] * e[r];
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-  if ((tid & 63) == 0) red[tid >> 6] = s;
-  __syncthreads();
-  if (tid == 0) d.cpart[d.nblk_f + blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
 // BSplineMotionError::evaluateErrorImplementation (BSplineMotionError.hpp:62-78): c^T Q c of the current state,
@@ -2919,11 +2944,16 @@ void pick_mm(kb_sp_handle* h) {
   h->fn_cost = (const void*)k_sp_cost_frames<MM>;
 }
 
+// k_sp_frames' grid: the frame blocks, then ceil(nblk_ic / N) blocks whose N waves each take one of k_sp_imu_cc's
+// 64-sample blocks
+int frames_grid(const kb_sp_handle* h) { return h->d.nblk_f + (h->d.nblk_ic + h->N - 1) / h->N; }
+
 int launch_build(kb_sp_handle* h) {
   SpDev& d = h->d;
   void* args[] = {&d};
-  KSP_HIP(hipLaunchKernel(h->fn_frames, dim3(d.nblk_f), dim3(64 * h->N), args, h->lds_frames, h->stream));
-  hipLaunchKernelGGL(k_sp_imu_cc, dim3(d.nblk_ic), dim3(64), 0, h->stream, d);  // sets lambda^2 = 0 in a GN pass
+  // the frames and, in its extra blocks, the IMU samples (k_sp_imu_cc's work: records, partial rows, lambda^2 = 0 of a
+  // GN pass)
+  KSP_HIP(hipLaunchKernel(h->fn_frames, dim3(frames_grid(h)), dim3(64 * h->N), args, h->lds_frames, h->stream));
   KSP_HIP(hipLaunchKernel((const void*)k_sp_assemble, dim3(d.n), dim3(256), args, h->lds_asm, h->stream));
   hipLaunchKernelGGL(k_sp_reduce_cc, dim3((d.Wc + 63) / 64), dim3(64 * RW), 0, h->stream, d);
   if (d.cq) hipLaunchKernelGGL(k_sp_mcost_build, dim3(1), dim3(256), 0, h->stream, d);
@@ -3010,8 +3040,8 @@ int launch_solve(kb_sp_handle* h) {
 int launch_cost(kb_sp_handle* h, int with_dx) {
   SpDev& d = h->d;
   void* args[] = {&d};
-  KSP_HIP(hipLaunchKernel(h->fn_cost, dim3(d.nblk_f), dim3(64 * h->N), args, 0, h->stream));
-  hipLaunchKernelGGL(k_sp_cost_imu, dim3(d.nblk_ci), dim3(256), 0, h->stream, d);
+  // the frames' cost and, in its extra nblk_ci blocks, the IMU samples'
+  KSP_HIP(hipLaunchKernel(h->fn_cost, dim3(d.nblk_f + d.nblk_ci), dim3(64 * h->N), args, 0, h->stream));
   if (d.cq) hipLaunchKernelGGL(k_sp_cost_motion, dim3(d.nblk_q), dim3(64), 0, h->stream, d);
   hipLaunchKernelGGL(k_sp_cost_reduce, dim3(1), dim3(64), 0, h->stream, d, with_dx);
   return 0;
@@ -3361,7 +3391,7 @@ int kb_sp_upload(kb_sp_handle* h, int32_t n_frames, const double* frame_time, in
   h->M = d.M = M;
   h->NCo = n_corners;
   d.nblk_f = (F + FPB - 1) / FPB;
-  d.nblk_ci = std::max(1, (M + 255) / 256);
+  d.nblk_ci = std::max(1, (M + 64 * N - 1) / (64 * N));  // k_sp_cost_frames' IMU blocks (64 N samples each)
   d.nblk_ic = std::max(1, (M + 63) / 64);
   int rc = 0;
   double2* dy = nullptr;
@@ -3897,8 +3927,7 @@ int kb_sp_assemble_stats(kb_sp_handle* h, int32_t n, double* ms, double* bytes) 
   double acc = 0.0;
   for (int it = -1; it < n; ++it) {  // it = -1: warm-up
     hipLaunchKernelGGL(k_sp_set_lam, dim3(1), dim3(64), 0, h->stream, d, 0.0);
-    KSP_HIP(hipLaunchKernel(h->fn_frames, dim3(d.nblk_f), dim3(64 * h->N), args, h->lds_frames, h->stream));
-    hipLaunchKernelGGL(k_sp_imu_cc, dim3(d.nblk_ic), dim3(64), 0, h->stream, d);
+    KSP_HIP(hipLaunchKernel(h->fn_frames, dim3(frames_grid(h)), dim3(64 * h->N), args, h->lds_frames, h->stream));
     KSP_HIP(hipEventRecord(e0, h->stream));
     KSP_HIP(hipLaunchKernel((const void*)k_sp_assemble, dim3(d.n), dim3(256), args, h->lds_asm, h->stream));
     KSP_HIP(hipEventRecord(e1, h->stream));
@@ -3931,9 +3960,8 @@ int kb_sp_kernel_stats(kb_sp_handle* h, int32_t n, double* ms_out6, double* fram
   for (int it = 0; it < n; ++it) {
     hipLaunchKernelGGL(k_sp_set_lam, dim3(1), dim3(64), 0, h->stream, d, 0.0);
     KSP_HIP(hipEventRecord(ev[0], h->stream));
-    KSP_HIP(hipLaunchKernel(h->fn_frames, dim3(d.nblk_f), dim3(64 * h->N), args, h->lds_frames, h->stream));
+    KSP_HIP(hipLaunchKernel(h->fn_frames, dim3(frames_grid(h)), dim3(64 * h->N), args, h->lds_frames, h->stream));
     KSP_HIP(hipEventRecord(ev[1], h->stream));
-    hipLaunchKernelGGL(k_sp_imu_cc, dim3(d.nblk_ic), dim3(64), 0, h->stream, d);
     KSP_HIP(hipLaunchKernel((const void*)k_sp_assemble, dim3(d.n), dim3(256), args, h->lds_asm, h->stream));
     hipLaunchKernelGGL(k_sp_reduce_cc, dim3((d.Wc + 63) / 64), dim3(64 * RW), 0, h->stream, d);
     if (d.cq) hipLaunchKernelGGL(k_sp_mcost_build, dim3(1), dim3(256), 0, h->stream, d);
