@@ -133,6 +133,7 @@ struct SpDev {
   long long* dbg_ts;      // diagnostics only: [320] KSP_TS stamps
   int dbg_stop;           // diagnostics only (KSP_DBG_STOP): 0, or the phase after which the timed kernels return
   int zero_lam;           // GN pass: k_sp_imu_cc sets lambda^2 = 0 (no separate launch)
+  int cc_fused;           // GN pass: k_sp_reduce_cc's column sums run as extra blocks of k_sp_elim1 (one launch less)
   // round 6: the Schur complement from the forward reduction alone (S = H_tt - sum_i Z_R,i^T Z_R,i over every node's
   // eliminated right-hand side, the top node's included) and the back substitution with ONE right-hand side
   // v = [-dtheta | 1] after the camera solve (k_sp_bvec*), instead of X = D^-1 [H_st | g_s] for all C + 1 columns
@@ -1476,10 +1477,65 @@ __device__ __forceinline__ void node_backsolve_lean(const double* L, const doubl
 }
 
 // first level (stride 1): odd nodes j eliminated, Z_j = L_j^-1 [U_{j-1}^T | U_j | R_j]
+// k_sp_reduce_cc's column sums for columns 4 e .. 4 e + 3 of the theta partial rows on a 256-thread block (the extra
+// blocks of k_sp_elim1 in a GN pass: H_cc is first read by the Schur sums, after the levels): thread (phase ph, column
+// c) sums rows ph, ph + 64, .. of the frame and IMU partials, then the 64 phases in a fixed tree through red [320]
+__device__ __forceinline__ void cc_sums_block(const SpDev& d, int e, double* red) {
+  const int C = d.C, nup = C * (C + 1) / 2, tid = threadIdx.x, c = tid & 3, ph = tid >> 2;
+  const int q = 4 * e + c;
+  const bool act = q < d.Wc;
+  int ii = -1, a = 0, bcol = 0;
+  if (act) {
+    if (q < nup) {
+      const short2 ab = d.uab[q];
+      a = ab.x;
+      bcol = ab.y;
+      const int ia = a - d.col_imu, ib = bcol - d.col_imu;
+      if (ia >= 0 && ia < 9 && ib >= 0 && ib < 9) ii = ia * 9 - ia * (ia - 1) / 2 + (ib - ia);
+    } else if (q < nup + C) {
+      const int ia = q - nup - d.col_imu;
+      if (ia >= 0 && ia < 9) ii = 45 + ia;
+    } else {
+      ii = 54;
+    }
+  }
+  double s = act ? col_sum(d.part, d.nblk_f, d.Wc, q, ph, 64) : 0.0;
+  if (ii >= 0) s += col_sum(d.ipart, d.nblk_ic, WI, ii, ph, 64);
+  red[ph * 4 + c] = s;
+  __syncthreads();
+  if (tid < 64) {
+    const int g = tid >> 2;
+    red[256 + tid] = (red[16 * g + c] + red[16 * g + 4 + c]) + (red[16 * g + 8 + c] + red[16 * g + 12 + c]);
+  }
+  __syncthreads();
+  if (tid >= 4 || !act) return;
+  double t[16];
+#pragma unroll
+  for (int g = 0; g < 16; ++g) t[g] = red[256 + 4 * g + c];
+#pragma unroll
+  for (int h = 8; h > 0; h >>= 1)
+#pragma unroll
+    for (int g = 0; g < h; ++g) t[g] += t[g + h];
+  s = t[0];
+  if (q < nup) {
+    d.Hcc[a * C + bcol] = s;
+    d.Hcc[bcol * C + a] = s;
+  } else if (q < nup + C) {
+    d.Hcc[C * C + (q - nup)] = s;
+  } else {
+    d.Hcc[C * C + C] = s;
+    d.sc[SC_COST_BUILD] = s;
+  }
+}
+
 __global__ void __launch_bounds__(256) k_sp_elim1(SpDev d) {
   __shared__ double L[NB * NB];
   __shared__ double id[NB];
   extern __shared__ __attribute__((aligned(16))) double W[];  // [18][36 + m]
+  if ((int)blockIdx.x >= d.n / 2) {  // GN pass (cc_fused): the camera block's column sums
+    cc_sums_block(d, (int)blockIdx.x - d.n / 2, L);
+    return;
+  }
   const int j = 1 + 2 * blockIdx.x, tid = threadIdx.x, m = d.m, wc = 36 + m;
   if (j >= d.n) return;
   KSP_TSB(1, 112);
@@ -1513,7 +1569,9 @@ __global__ void __launch_bounds__(256) k_sp_elim1(SpDev d) {
   }
   __syncthreads();
   KSP_TSB(1, 114);
-  node_forward(L, id, W, wc, wc, d.Z + (size_t)j * NB * wc, wc, tid);
+  // the L loads kept per row: the hoisted form held all 171 entries (256 VGPRs + 188 AGPRs, one block per CU, the
+  // 500 blocks in two rounds); lean: 114 VGPRs, every block resident at once.  Same arithmetic, same bits.
+  node_forward_lean(L, id, W, wc, wc, d.Z + (size_t)j * NB * wc, wc, tid);
   for (int q = tid; q < NB * NB; q += blockDim.x) d.Lf[(size_t)j * NB * NB + q] = L[q];
   if (tid < NB) d.Lid[(size_t)j * NB + tid] = id[tid];
   KSP_TSB(1, 115);
@@ -2955,7 +3013,7 @@ int launch_build(kb_sp_handle* h) {
   // GN pass)
   KSP_HIP(hipLaunchKernel(h->fn_frames, dim3(frames_grid(h)), dim3(64 * h->N), args, h->lds_frames, h->stream));
   KSP_HIP(hipLaunchKernel((const void*)k_sp_assemble, dim3(d.n), dim3(256), args, h->lds_asm, h->stream));
-  hipLaunchKernelGGL(k_sp_reduce_cc, dim3((d.Wc + 63) / 64), dim3(64 * RW), 0, h->stream, d);
+  if (!d.cc_fused) hipLaunchKernelGGL(k_sp_reduce_cc, dim3((d.Wc + 63) / 64), dim3(64 * RW), 0, h->stream, d);
   if (d.cq) hipLaunchKernelGGL(k_sp_mcost_build, dim3(1), dim3(256), 0, h->stream, d);
   return 0;
 }
@@ -2980,7 +3038,7 @@ int launch_reduction(kb_sp_handle* h) {
     h->s_top = 1;
     return 0;
   }
-  hipLaunchKernelGGL(k_sp_elim1, dim3(d.n / 2), dim3(256), h->lds_elim, h->stream, d);
+  hipLaunchKernelGGL(k_sp_elim1, dim3(d.n / 2 + (d.cc_fused ? (d.Wc + 3) / 4 : 0)), dim3(256), h->lds_elim, h->stream, d);
   int s = 1;
   const int sd = h->s_deep;
   for (; s < d.n && !(sd && s >= sd); s *= 2)
@@ -3051,10 +3109,13 @@ int launch_cost(kb_sp_handle* h, int with_dx) {
 int enqueue_gn_pass(kb_sp_handle* h) {
   SpDev& d = h->d;
   d.zero_lam = 1;  // lambda = 0 written by the build's k_sp_imu_cc
+  // H_cc's column sums inside k_sp_elim1 (the cyclic reduction, no motion-error build cost to add after them)
+  d.cc_fused = (h->use_cr && d.n > 1 && !d.cq && !std::getenv("KSP_CC_SEPARATE")) ? 1 : 0;
   const int rb = launch_build(h);
   d.zero_lam = 0;
-  if (rb) return -1;
-  if (launch_solve(h)) return -1;
+  const int rs = rb ? 0 : launch_solve(h);
+  d.cc_fused = 0;
+  if (rb || rs) return -1;
   hipLaunchKernelGGL(k_sp_update, dim3(d.n), dim3(64), 0, h->stream, d, 1);
   return launch_cost(h, 1);
 }
