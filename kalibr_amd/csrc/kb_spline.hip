@@ -1689,7 +1689,10 @@ __device__ __forceinline__ void level_products(const SpDev& d, const double* Zl,
 // thread of the block calls it (act: the group has a node at this level), with the same three block barriers on every
 // path, so that k_sp_deep can run several groups (and several levels) in one block.  L, id and sm (Zl | Zr | W,
 // [18][wc] each) are the group's LDS (the couplings Ui, Uo are formed in W, the forward solve's operand).
-template <bool LEAN>  // LEAN: k_sp_deep's 1024-thread block (128 VGPRs): fewer loads in flight, per-row forward solve
+// LEAN: k_sp_deep's 1024-thread block (128 VGPRs): fewer loads in flight, per-row forward solve.  LF: only the solves
+// with per-row L loads (the first level's 501 blocks: 132 VGPRs, all resident at once, 22.7 -> 16.5 us; the hoisted
+// solves are ~2 us faster on the narrower levels, whose blocks fit in one round anyway).  Same arithmetic, same bits.
+template <bool LEAN, bool LF = LEAN>
 __device__ __forceinline__ void level_step(const SpDev& d, int s, int i, bool act, int tid, int nth, double* L,
                                            double* id, double* sm) {
   const int m = d.m, wc = 36 + m;
@@ -1753,11 +1756,12 @@ __device__ __forceinline__ void level_step(const SpDev& d, int s, int i, bool ac
   KSP_STOP(3);
   if (!LEAN) KSP_TSB(tsb, tsl + 3);
   if (fin && top && d.zs) {  // Z_R,0 = L^-1 R' and the factor: the back substitution solves x_0 with one column later
-    node_forward(L, id, W + 2 * NB, wc, m, d.Z + 2 * NB, wc, tid, nth);
+    if (LF) node_forward_lean(L, id, W + 2 * NB, wc, m, d.Z + 2 * NB, wc, tid, nth);
+    else node_forward(L, id, W + 2 * NB, wc, m, d.Z + 2 * NB, wc, tid, nth);
     for (int q = tid; q < NB * NB; q += nth) d.Lf[q] = L[q];
     if (tid < NB) d.Lid[tid] = id[tid];
   } else if (fin && top) {  // X_0 = L^-T L^-1 R' (forward in place in W, then backward into X_0)
-    if (LEAN) {
+    if (LF) {
       node_forward_lean(L, id, W + 2 * NB, wc, m, W + 2 * NB, wc, tid, nth);
       node_backsolve_lean(L, id, W + 2 * NB, wc, m, d.X, tid, nth);
     } else {
@@ -1765,7 +1769,7 @@ __device__ __forceinline__ void level_step(const SpDev& d, int s, int i, bool ac
       node_backsolve(L, id, W + 2 * NB, wc, m, d.X, tid, nth);
     }
   } else if (fin) {
-    if (LEAN) node_forward_lean(L, id, W, wc, wc, d.Z + (size_t)i * NB * wc, wc, tid, nth);
+    if (LF) node_forward_lean(L, id, W, wc, wc, d.Z + (size_t)i * NB * wc, wc, tid, nth);
     else node_forward(L, id, W, wc, wc, d.Z + (size_t)i * NB * wc, wc, tid, nth);
     KSP_STOP(4);
     for (int q = tid; q < NB * NB; q += nth) d.Lf[(size_t)i * NB * NB + q] = L[q];
@@ -1774,13 +1778,14 @@ __device__ __forceinline__ void level_step(const SpDev& d, int s, int i, bool ac
   if (!LEAN) KSP_TSB(tsb, tsl + 4);
 }
 
+template <bool LF>
 __global__ void __launch_bounds__(256) k_sp_level(SpDev d, int s) {
   __shared__ double L[NB * NB];
   __shared__ double id[NB];
   extern __shared__ __attribute__((aligned(16))) double sm[];  // Zl [18][wc] | Zr [18][wc] | W [18][wc]
   const int i = 2 * s * blockIdx.x;
   if (i >= d.n) return;  // block-uniform
-  level_step<false>(d, s, i, true, threadIdx.x, blockDim.x, L, id, sm);
+  level_step<false, LF>(d, s, i, true, threadIdx.x, blockDim.x, L, id, sm);
 }
 
 __global__ void __launch_bounds__(256) k_sp_top(SpDev d) {
@@ -3042,7 +3047,8 @@ int launch_reduction(kb_sp_handle* h) {
   int s = 1;
   const int sd = h->s_deep;
   for (; s < d.n && !(sd && s >= sd); s *= 2)
-    hipLaunchKernelGGL(k_sp_level, dim3((d.n + 2 * s - 1) / (2 * s)), dim3(256), h->lds_level, h->stream, d, s);
+    hipLaunchKernelGGL(s == 1 ? k_sp_level<true> : k_sp_level<false>, dim3((d.n + 2 * s - 1) / (2 * s)), dim3(256),
+                       h->lds_level, h->stream, d, s);
   if (d.zs) {  // the back substitution runs after the camera solve, with one column (launch_bvec)
     h->s_top = s;
     return 0;
@@ -3341,7 +3347,8 @@ kb_sp_handle* kb_sp_create(const kb_sp_layout* L) {
   }
   hipFuncSetAttribute(h->fn_frames, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_frames);
   hipFuncSetAttribute((const void*)k_sp_assemble, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_asm);
-  hipFuncSetAttribute((const void*)k_sp_level, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_level);
+  hipFuncSetAttribute((const void*)k_sp_level<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_level);
+  hipFuncSetAttribute((const void*)k_sp_level<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_level);
   hipFuncSetAttribute((const void*)k_sp_elim1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_elim);
   hipFuncSetAttribute((const void*)k_sp_back, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_back);
   hipFuncSetAttribute((const void*)k_sp_back2, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_back2);
