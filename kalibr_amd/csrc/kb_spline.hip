@@ -4063,9 +4063,12 @@ int kb_sp_kernel_stats(kb_sp_handle* h, int32_t n, double* ms_out6, double* fram
   if (frames_bytes) {
     // algorithmic bytes of one k_sp_frames launch: corners (y 16 B + id 2 B), view ranges (8 B per (frame,
     // camera)), frame basis (4 weights + index), the 4 active coefficients per frame, the camera-side state,
-    // the per-frame spline blocks written (FHS doubles) and one theta partial row per block
+    // the per-frame spline blocks written (FHS doubles) and one theta partial row per block; the extra blocks' IMU
+    // samples (index, 12 weights, 6 measurements, 4 coefficients read; the IRQ-double record and the partial rows
+    // written)
     *frames_bytes = 18.0 * h->NCo + 8.0 * h->F * h->N + 36.0 * h->F + 8.0 * 24 * h->F + 8.0 * d.off_coef +
-                    8.0 * d.FHS * h->F + 8.0 * d.Wc * d.nblk_f;
+                    8.0 * d.FHS * h->F + 8.0 * d.Wc * d.nblk_f +
+                    h->M * (4.0 + 8.0 * (12 + 6 + 24 + IRQ)) + 8.0 * WI * d.nblk_ic;
   }
   h->built = h->solved = false;
   return 0;
