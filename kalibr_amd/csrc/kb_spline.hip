@@ -134,6 +134,8 @@ struct SpDev {
   int dbg_stop;           // diagnostics only (KSP_DBG_STOP): 0, or the phase after which the timed kernels return
   int zero_lam;           // GN pass: k_sp_imu_cc sets lambda^2 = 0 (no separate launch)
   int cc_fused;           // GN pass: k_sp_reduce_cc's column sums run as extra blocks of k_sp_elim1 (one launch less)
+  int zsf;                // zs: the Schur sums of nodes 1.. run as extra blocks of the top level's launch (beside its
+                          // one block), the top node's own term added by k_sp_schur_red
   // round 6: the Schur complement from the forward reduction alone (S = H_tt - sum_i Z_R,i^T Z_R,i over every node's
   // eliminated right-hand side, the top node's included) and the back substitution with ONE right-hand side
   // v = [-dtheta | 1] after the camera solve (k_sp_bvec*), instead of X = D^-1 [H_st | g_s] for all C + 1 columns
@@ -1778,11 +1780,18 @@ __device__ __forceinline__ void level_step(const SpDev& d, int s, int i, bool ac
   if (!LEAN) KSP_TSB(tsb, tsl + 4);
 }
 
+__device__ __forceinline__ void zschur_block(const SpDev& d, int blk, double* sm);
+
 template <bool LF>
 __global__ void __launch_bounds__(256) k_sp_level(SpDev d, int s) {
   __shared__ double L[NB * NB];
   __shared__ double id[NB];
   extern __shared__ __attribute__((aligned(16))) double sm[];  // Zl [18][wc] | Zr [18][wc] | W [18][wc]
+  const int nlb = (d.n + 2 * s - 1) / (2 * s);
+  if ((int)blockIdx.x >= nlb) {  // zsf, top level: the Schur sums of nodes 1.. (all final by now) beside the top node
+    zschur_block(d, (int)blockIdx.x - nlb, sm);
+    return;
+  }
   const int i = 2 * s * blockIdx.x;
   if (i >= d.n) return;  // block-uniform
   level_step<false, LF>(d, s, i, true, threadIdx.x, blockDim.x, L, id, sm);
@@ -2372,8 +2381,8 @@ __global__ void __launch_bounds__(256) k_sp_schur(SpDev d) {
 // zs: the camera-block partial sums of sum_i Z_R,i^T Z_R,i (Z_R,i = L_i^-1 R_i', the right-hand-side part of node i's
 // elimination at any level, the top node's included) = R0^T D^-1 R0 of k_sp_schur's sum_i R0_i^T X_i, from the forward
 // reduction alone; same blocks of NPB nodes, same entry table and k_sp_schur_red
-__global__ void __launch_bounds__(256) k_sp_zschur(SpDev d) {
-  extern __shared__ __attribute__((aligned(16))) double sm[];  // Z_R [18][m] | acc [Ws] | tab
+__device__ __forceinline__ void zschur_block(const SpDev& d, int blk, double* sm) {
+  // sm: Z_R [18][m] | acc [Ws] | tab
   const int tid = threadIdx.x, m = d.m, wc = 36 + m;
   double* Zl = sm;
   double* acc = sm + 2 * NB * m;  // (k_sp_schur's layout: the LDS size is the host's lds_schur)
@@ -2382,7 +2391,7 @@ __global__ void __launch_bounds__(256) k_sp_zschur(SpDev d) {
     acc[q] = 0.0;
     tab[q] = d.uab[q];
   }
-  const int i0 = blockIdx.x * NPB, i1 = min(d.n, i0 + NPB);
+  const int i0 = max(blk * NPB, d.zsf ? 1 : 0), i1 = min(d.n, blk * NPB + NPB);  // zsf: node 0 by k_sp_schur_red
   constexpr int ZS_U = (NB * (MAXC + 1) + 255) / 256;
   const int nq = NB * m;
   const float rinv = 1.0f / (float)m;
@@ -2415,7 +2424,12 @@ __global__ void __launch_bounds__(256) k_sp_zschur(SpDev d) {
     }
   }
   __syncthreads();
-  for (int q = tid; q < d.Ws; q += blockDim.x) d.spart[(size_t)blockIdx.x * d.Ws + q] = acc[q];
+  for (int q = tid; q < d.Ws; q += blockDim.x) d.spart[(size_t)blk * d.Ws + q] = acc[q];
+}
+
+__global__ void __launch_bounds__(256) k_sp_zschur(SpDev d) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  zschur_block(d, blockIdx.x, sm);
 }
 
 // zs, step 1 (every node at once, after the camera solve): with v = [-dtheta | 1], node j's operands of the
@@ -2518,9 +2532,17 @@ __global__ void __launch_bounds__(64 * RW) k_sp_schur_red(SpDev d) {
   red[wave][lane] = act ? col_sum(d.spart, d.nblk_s, d.Ws, q, wave, RW) : 0.0;
   __syncthreads();
   if (wave != 0 || !act) return;
-  const double t = red_waves(red, lane);
+  double t = red_waves(red, lane);
   const short2 ab = d.uab[q];
   const int a = ab.x, b = ab.y;
+  if (d.zsf) {  // the top node's Z_R,0^T Z_R,0 (its Schur sums were not in the top level's extra blocks)
+    const int wc = 36 + d.m;
+    const double* Z0 = d.Z + 2 * NB;
+    double z = 0.0;
+#pragma unroll
+    for (int k = 0; k < NB; ++k) z += Z0[k * wc + a] * Z0[k * wc + b];
+    t += z;
+  }
   if (q < nup) {
     const double v = d.Hcc[a * C + b] + (a == b ? d.sc[SC_LAM2] : 0.0) - t;
     d.Sf[a * C + b] = v;
@@ -3046,9 +3068,12 @@ int launch_reduction(kb_sp_handle* h) {
   hipLaunchKernelGGL(k_sp_elim1, dim3(d.n / 2 + (d.cc_fused ? (d.Wc + 3) / 4 : 0)), dim3(256), h->lds_elim, h->stream, d);
   int s = 1;
   const int sd = h->s_deep;
-  for (; s < d.n && !(sd && s >= sd); s *= 2)
-    hipLaunchKernelGGL(s == 1 ? k_sp_level<true> : k_sp_level<false>, dim3((d.n + 2 * s - 1) / (2 * s)), dim3(256),
-                       h->lds_level, h->stream, d, s);
+  for (; s < d.n && !(sd && s >= sd); s *= 2) {
+    const bool last = d.zsf && 2 * s >= d.n;  // the top level: one block, the Schur sums beside it
+    hipLaunchKernelGGL(s == 1 ? k_sp_level<true> : k_sp_level<false>,
+                       dim3((d.n + 2 * s - 1) / (2 * s) + (last ? d.nblk_s : 0)), dim3(256),
+                       last ? std::max(h->lds_level, h->lds_schur) : h->lds_level, h->stream, d, s);
+  }
   if (d.zs) {  // the back substitution runs after the camera solve, with one column (launch_bvec)
     h->s_top = s;
     return 0;
@@ -3094,7 +3119,7 @@ int launch_solve(kb_sp_handle* h) {
   SpDev& d = h->d;
   void* args[] = {&d};
   launch_reduction(h);
-  hipLaunchKernelGGL(d.zs ? k_sp_zschur : k_sp_schur, dim3(d.nblk_s), dim3(256), h->lds_schur, h->stream, d);
+  if (!d.zsf) hipLaunchKernelGGL(d.zs ? k_sp_zschur : k_sp_schur, dim3(d.nblk_s), dim3(256), h->lds_schur, h->stream, d);
   hipLaunchKernelGGL(k_sp_schur_red, dim3((d.Ws + 63) / 64), dim3(64 * RW), 0, h->stream, d);
   KSP_HIP(hipLaunchKernel(h->fn_camsolve, dim3(1), dim3(64), args, 0, h->stream));
   if (d.zs) return launch_bvec(h);
@@ -3347,8 +3372,11 @@ kb_sp_handle* kb_sp_create(const kb_sp_layout* L) {
   }
   hipFuncSetAttribute(h->fn_frames, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_frames);
   hipFuncSetAttribute((const void*)k_sp_assemble, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_asm);
-  hipFuncSetAttribute((const void*)k_sp_level<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_level);
-  hipFuncSetAttribute((const void*)k_sp_level<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_level);
+  // (the top level's launch may carry the Schur sums' blocks: zsf)
+  hipFuncSetAttribute((const void*)k_sp_level<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                      (int)std::max(h->lds_level, h->lds_schur));
+  hipFuncSetAttribute((const void*)k_sp_level<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                      (int)std::max(h->lds_level, h->lds_schur));
   hipFuncSetAttribute((const void*)k_sp_elim1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_elim);
   hipFuncSetAttribute((const void*)k_sp_back, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_back);
   hipFuncSetAttribute((const void*)k_sp_back2, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds_back2);
@@ -3377,6 +3405,9 @@ kb_sp_handle* kb_sp_create(const kb_sp_layout* L) {
     // reduction; KSP_ZS=0 keeps the C + 1 column back substitution and X)
     const char* ev = std::getenv("KSP_ZS");
     d.zs = (h->use_cr && h->s_deep == 0 && !(ev && std::atoi(ev) == 0)) ? 1 : 0;
+    // the Schur sums beside the top level's block (one launch less; KSP_ZSF=0 keeps k_sp_zschur)
+    const char* ef = std::getenv("KSP_ZSF");
+    d.zsf = (d.zs && h->n > 1 && !(ef && std::atoi(ef) == 0)) ? 1 : 0;
     if (d.zs && (h->alloc(&d.xs, (size_t)h->n * NB) || h->alloc(&d.bm, (size_t)h->n * NB * 37))) {
       kb_sp_destroy(h);
       return nullptr;
@@ -4036,7 +4067,7 @@ int kb_sp_kernel_stats(kb_sp_handle* h, int32_t n, double* ms_out6, double* fram
     KSP_HIP(hipEventRecord(ev[2], h->stream));
     launch_reduction(h);  // (zs: the forward half; the one-column back substitution follows the camera solve)
     KSP_HIP(hipEventRecord(ev[3], h->stream));
-    hipLaunchKernelGGL(d.zs ? k_sp_zschur : k_sp_schur, dim3(d.nblk_s), dim3(256), h->lds_schur, h->stream, d);
+    if (!d.zsf) hipLaunchKernelGGL(d.zs ? k_sp_zschur : k_sp_schur, dim3(d.nblk_s), dim3(256), h->lds_schur, h->stream, d);
     hipLaunchKernelGGL(k_sp_schur_red, dim3((d.Ws + 63) / 64), dim3(64 * RW), 0, h->stream, d);
     KSP_HIP(hipLaunchKernel(h->fn_camsolve, dim3(1), dim3(64), args, 0, h->stream));
     KSP_HIP(hipEventRecord(ev[4], h->stream));
