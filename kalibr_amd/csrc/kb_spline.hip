@@ -2457,10 +2457,17 @@ __global__ void __launch_bounds__(256) k_sp_bprep(SpDev d) {
     T[r * 37 + c] = Z[r * wc + c];
   }
   KSP_WAVE_SYNC();
-  if (lane < 3 * NB) {  // y = Z_R v: three lanes per row over interleaved columns, summed in a fixed order
+  if (lane < 3 * NB) {  // y = Z_R v: three lanes per row over interleaved columns, summed in a fixed order; the
+                        // row's loads all issued before the chain (a run-time trip count serialised them)
     const int r = lane % NB, pp = lane / NB;
+    constexpr int UY = (MAXC + 1 + 2) / 3;
+    double zv[UY];
+#pragma unroll
+    for (int u = 0; u < UY; ++u) zv[u] = Z[r * wc + 36 + min(pp + 3 * u, m - 1)];
     double t = 0.0;
-    for (int c = pp; c < m; c += 3) t = fma(Z[r * wc + 36 + c], vs[wave][c], t);
+#pragma unroll
+    for (int u = 0; u < UY; ++u)
+      if (pp + 3 * u < m) t = fma(zv[u], vs[wave][pp + 3 * u], t);
     yp[wave][pp * NB + r] = t;
   }
   KSP_WAVE_SYNC();
