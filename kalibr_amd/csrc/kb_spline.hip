@@ -300,6 +300,20 @@ __device__ __forceinline__ double bt_basic(const double* R, const double* t, con
   return s;
 }
 
+// LDS staging of n consecutive elements with U loads in flight per thread before their stores (a plain strided loop
+// waits on every load: ~1 us per iteration when one wave per SIMD runs)
+template <int U, class T>
+__device__ __forceinline__ void stage_lds(T* dst, const T* src, int n, int tid, int nth) {
+  for (int q0 = tid; q0 < n; q0 += U * nth) {
+    T v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = src[min(q0 + u * nth, n - 1)];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (q0 + u * nth < n) dst[q0 + u * nth] = v[u];
+  }
+}
+
 // ---------------------------------------------------------------- k_sp_frames: camera terms
 // One block = FPB frames, one wave per camera.  Per frame: spline pose T_wb(t_f) and JT; per view the
 // 16 x 16 local Hessian of [J_delta | J_intr | -e] by f64 MFMA SYRK through an LDS tile; then the frame's
@@ -335,8 +349,8 @@ __global__ void __launch_bounds__(512) k_sp_frames(SpDev d) {
   const int cam = wave;
   const double* st = d.state;
   KSP_TSB(300, 256);  // diagnostics: block 300's timeline in slots 256..271 (tools/diag_sp_asm.py)
-  for (int q = tid; q < 3 * d.n_target; q += nth) tg[q] = d.target[q];
-  for (int q = tid; q < d.Wc; q += nth) tuab[q] = d.uab[q];
+  stage_lds<8>(tg, d.target, 3 * d.n_target, tid, nth);
+  stage_lds<8>(tuab, d.uab, d.Wc, tid, nth);
   if (tid < 12) tz[tid] = tid == 6 ? 1.0 : 0.0;
   for (int q = tid; q < C; q += nth) {
     tck[q] = d.ckind[q];
@@ -2445,18 +2459,38 @@ __global__ void __launch_bounds__(256) k_sp_bprep(SpDev d) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, m = d.m, wc = 36 + m, C = d.C;
   const int j = 4 * blockIdx.x + wave;
   if (j >= d.n) return;  // wave-uniform
+  KSP_TSB(100, 272);  // diagnostics: block 100's (wave 0's) timeline in slots 272..276 (tools/diag_sp_asm.py)
   double* L = Ls[wave];
   double* id = ids[wave];
   double* T = Ts[wave];
   const double* Z = d.Z + (size_t)j * NB * wc;
-  for (int q = lane; q < NB * NB; q += 64) L[q] = d.Lf[(size_t)j * NB * NB + q];
-  if (lane < NB) id[lane] = d.Lid[(size_t)j * NB + lane];
-  for (int c = lane; c < m; c += 64) vs[wave][c] = c < C ? -d.dx[c] : 1.0;
-  for (int q = lane; q < NB * 36; q += 64) {
-    const int r = q / 36, c = q - 36 * r;
-    T[r * 37 + c] = Z[r * wc + c];
+  {  // every load in flight before the LDS stores (the loops' per-iteration waits took ~5 us)
+    constexpr int UL = (NB * NB + 63) / 64, UT = (NB * 36 + 63) / 64;
+    double lv[UL], tv[UT];
+    const double* Lj = d.Lf + (size_t)j * NB * NB;
+#pragma unroll
+    for (int u = 0; u < UL; ++u) lv[u] = Lj[min(lane + 64 * u, NB * NB - 1)];
+#pragma unroll
+    for (int u = 0; u < UT; ++u) {
+      const int q = min(lane + 64 * u, NB * 36 - 1), r = q / 36;
+      tv[u] = Z[r * wc + q - 36 * r];
+    }
+    const double iv = d.Lid[(size_t)j * NB + min(lane, NB - 1)];
+    const double xv = d.dx[min(lane, C - 1)];
+#pragma unroll
+    for (int u = 0; u < UL; ++u)
+      if (lane + 64 * u < NB * NB) L[lane + 64 * u] = lv[u];
+#pragma unroll
+    for (int u = 0; u < UT; ++u) {
+      const int q = lane + 64 * u, r = q / 36;
+      if (q < NB * 36) T[r * 37 + q - 36 * r] = tv[u];
+    }
+    if (lane < NB) id[lane] = iv;
+    if (lane < m) vs[wave][lane] = lane < C ? -xv : 1.0;  // m = C + 1 <= MAXC + 1 = 65: lanes 0..63 and
+    if (lane == 0 && m > 64) vs[wave][64] = 1.0;            // (C = 64) the rhs slot
   }
   KSP_WAVE_SYNC();
+  KSP_TSB(100, 273);
   if (lane < 3 * NB) {  // y = Z_R v: three lanes per row over interleaved columns, summed in a fixed order; the
                         // row's loads all issued before the chain (a run-time trip count serialised them)
     const int r = lane % NB, pp = lane / NB;
@@ -2473,7 +2507,9 @@ __global__ void __launch_bounds__(256) k_sp_bprep(SpDev d) {
   KSP_WAVE_SYNC();
   if (lane < NB) T[lane * 37 + 36] = (yp[wave][lane] + yp[wave][NB + lane]) + yp[wave][2 * NB + lane];
   KSP_WAVE_SYNC();
+  KSP_TSB(100, 274);
   node_backsolve_lean(L, id, T, 37, 37, d.bm + (size_t)j * NB * 37, lane, 64);
+  KSP_TSB(100, 275);
 }
 
 // zs, step 2: node j of stride s on one wave (s = 0: the top node, x_0 = u_0): lane r < 18 forms row r of

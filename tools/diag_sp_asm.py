@@ -36,3 +36,10 @@ for rep in range(3):
         v = (buf[sl] - t0) / 100
         if 0 <= v < 1e4:
             print(f"  {nm:20s} {v:8.2f} us")
+    t0 = buf[272]
+    print(f"rep {rep} k_sp_bprep block 100 wave 0:")
+    for nm, sl in (("entry", 272), ("L, T staged", 273), ("y formed", 274), ("37 columns solved", 275)):
+        v = (buf[sl] - t0) / 100
+        if 0 <= v < 1e4:
+            print(f"  {nm:20s} {v:8.2f} us")
+    print(f"  (block 100 entry {(buf[272] - buf[241]) / 100:.2f} us after k_sp_assemble block 500's entry)")
